@@ -1,0 +1,191 @@
+/*
+ * vvcr.h — C-ABI of libvvcr, the MI355X (gfx950) VVC decode-reconstruction path.
+ *
+ * Drop-in boundary for VTM 7.3 (ultrawide/vvc). The reference reconstructs per block through C
+ * function-pointer tables (InterpolationFilter::m_filterHor/m_filterVer/m_filterCopy
+ * source/Lib/CommonLib/InterpolationFilter.h:100-107, PelBufferOps g_pelBufOP Buffer.h:54-88,
+ * fastInvTrans TrQuant.cpp:69-81, AdaptiveLoopFilter::m_filter5x5Blk/m_filter7x7Blk
+ * AdaptiveLoopFilter.h:101-133) called from DecCu::decompressCtu (DecoderLib/DecCu.cpp:102), once per
+ * CTU from DecSlice::decompressSlice (DecSlice.cpp:204), and through the picture-level loop filters in
+ * DecLib::executeLoopFilters (DecLib.cpp:560-623). libvvcr replaces both at PICTURE granularity:
+ *
+ *   DecSlice::decompressSlice (last slice of a picture)  ->  vvcr_begin_picture + vvcr_submit
+ *   DecLib::executeLoopFilters                           ->  vvcr_end_picture (recon + DBK + SAO + ALF)
+ *   CS::setRefinedMotionField (UnitTools.cpp:68)          <-  vvcr_get_dmvr_deltas
+ *   DecApp::xWriteOutput / DecLib::finishPicture MD5      <-  vvcr_read_picture
+ *
+ * Descriptor rows (vvcr_cu / vvcr_pu / vvcr_tu) are the parsed, MV-derived coding units of one
+ * picture in decode order, i.e. the contents of CodingStructure::cus/pus/tus (CodingStructure.h:194-196)
+ * after DecCu::xDeriveCUMV (DecCu.cpp:878); field meaning follows CodingUnit / PredictionUnit /
+ * TransformUnit (Unit.h:288-456). All fields are int32 so a row is a plain array.
+ *
+ * Conventions: every entry point returns 0 on success or a negative VVCR_E_* code; no C++
+ * exception crosses the ABI; vvcr_last_error() gives the message. The library owns all device
+ * memory (DPB slots, scratch); the caller owns host arrays until the call returns (deep copy).
+ * Samples are 10-bit in uint16/int16 ("Pel", TypeDef.h:313), 4:2:0.
+ */
+#ifndef VVCR_H
+#define VVCR_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VVCR_OK 0
+#define VVCR_E_ARG -1
+#define VVCR_E_HIP -2
+#define VVCR_E_STATE -3
+#define VVCR_E_UNSUPPORTED -4
+#define VVCR_MAX_REF 16
+
+typedef struct vvcr_ctx vvcr_ctx;
+
+/* Sequence-level parameters (SPS subset, Slice.h SPS): replaces Picture::create / PelStorage::create
+ * (Picture.cpp:195-214, Buffer.cpp:687) — the DPB lives in HBM, without border margins (MC clamps
+ * coordinates instead of Picture::extendPicBorder, Picture.cpp:737). */
+typedef struct vvcr_seq_params {
+  int32_t width, height;       /* luma samples */
+  int32_t chroma_format;       /* 1 = 4:2:0 (only supported format) */
+  int32_t bit_depth;           /* luma = chroma bit depth (8..10) */
+  int32_t ctu_log2;            /* 5..7 */
+  int32_t dpb_slots;           /* number of picture buffers to allocate */
+  int32_t device;              /* HIP device ordinal */
+} vvcr_seq_params;
+
+/* CodingUnit (Unit.h:288-372). x,y,w,h = luma area (CU::lumaPos/lumaSize); cx..ch = Cb area. */
+typedef struct vvcr_cu {
+  int32_t x, y, w, h, cx, cy, cw, ch;
+  int32_t chtype, predmode, qp, treetype, modetype, skip, mmvdskip, affine, affinetype, geo;
+  int32_t bdpcm, bdpcmc, imv, rootcbf, sbtinfo, mtsflag, lfnst, bcw, mip, isp;
+  int32_t smvd, act, cqpadj, depth, qtdepth, firstpu, npu, firsttu, ntu, slice;
+  int32_t yvalid, cvalid;
+} vvcr_cu;
+
+/* PredictionUnit (Unit.h:378-456). mv in 1/16 luma sample (MV_FRACTIONAL_BITS_INTERNAL=4,
+ * CommonDef.h:281), already derived (merge / AMVP / MMVD / SMVD resolved). ref0/ref1 = refIdx.
+ * aff[l*6 + k*2 + {0,1}] = mvAffi[l][k]. fidir_l / fidir_c = PU::getFinalIntraMode.
+ * bdof / dmvr = the producer's evaluation of the reference conditions
+ * (InterPrediction.cpp:1584-1635, UnitTools.cpp:1249 PU::checkDMVRCondition). */
+typedef struct vvcr_pu {
+  int32_t cu, x, y, w, h, cx, cy, cw, ch, chtype;
+  int32_t idir_l, idir_c, fidir_l, fidir_c, mipt, mrl;
+  int32_t merge, regmerge, mergeidx, geodir, geoi0, geoi1, mmvd, interdir;
+  int32_t mv0x, mv0y, mv1x, mv1y, ref0, ref1, mrgtype, mvrefine, ciip;
+  int32_t aff[12];
+  int32_t dmvr_off, bdof, dmvr;
+} vvcr_pu;
+
+/* TransformUnit (Unit.h:458+). Per component c: b[c] = {x, y, w, h, cbf, mts, coef_off, qp, qp_ts}.
+ * coef_off indexes the coefficient pool (TCoeff levels, w*h row-major, as parsed:
+ * TransformUnit::getCoeffs); qp / qp_ts = QpParam::Qp(false/true) (Quant.h:68-102). */
+typedef struct vvcr_tu {
+  int32_t cu, chtype, depth, noresi, jccr, cadj;
+  int32_t b[3][9];
+} vvcr_tu;
+
+/* Per-4x4 motion field (MotionInfo, MotionInfo.h:101), before DMVR write-back: what deblocking
+ * boundary strength and sub-block (SbTMVP) motion compensation read. */
+typedef struct vvcr_motion {
+  int32_t is_inter, inter_dir, ref0, ref1, mv0x, mv0y, mv1x, mv1y, bcw, alt_hpel;
+} vvcr_motion;
+
+/* GEO candidate pair captured at InterPrediction::motionCompensationGeo (InterPrediction.cpp:1749). */
+typedef struct vvcr_geo {
+  int32_t cu;
+  int32_t cand[2][6];          /* inter_dir, list, ref_idx, mvx, mvy, alt_hpel */
+} vvcr_geo;
+
+/* SAO per CTB and component (SAOOffset, TypeDef.h:938), merge already resolved. */
+typedef struct vvcr_sao {
+  int32_t mode, type, band, offset[4];
+} vvcr_sao;
+
+/* Picture-level parameters (slice / picture header subset). */
+typedef struct vvcr_pic_params {
+  int32_t poc, slot, slice_type, slice_qp;
+  int32_t num_ref[2];
+  int32_t ref_slot[2][VVCR_MAX_REF];
+  int32_t ref_poc[2][VVCR_MAX_REF];
+  int32_t ref_lt[2][VVCR_MAX_REF];
+  int32_t dual_tree, dep_quant, sign_hiding, joint_cbcr;
+  int32_t bdof_enabled, dmvr_enabled, prof_enabled, lfnst_enabled, mts_intra, mts_inter, sbt;
+  int32_t wp_p, wp_b;
+  int32_t wp[2][VVCR_MAX_REF][3][7];  /* present, log2denom, weight, offset, w, o, offset(scaled) */
+  int32_t dbk_disable, dbk_beta_offset_div2, dbk_tc_offset_div2;
+  int32_t lf_across_slices, lf_across_tiles;
+  int32_t chroma_qp_off[3];          /* per component (pps + slice), index 1,2 */
+  int32_t chroma_qp_map[3][128];     /* mapped chroma QP for qp in [-64,63] at [c][qp+64] */
+  int32_t sao_luma, sao_chroma;
+  int32_t alf_en[3], ccalf_en[2], alf_vb_luma, alf_vb_chroma;
+  int32_t lmcs_enabled, lmcs_chroma_scale, lmcs_min_bin, lmcs_max_bin;
+  int16_t lmcs_fwd[1024], lmcs_inv[1024], lmcs_pivot[17];
+  int32_t lmcs_cadj[16];
+  int32_t max_tb_log2, log2_max_ts;
+} vvcr_pic_params;
+
+/* ALF / CC-ALF filters of the picture (AdaptiveLoopFilter::reconstructCoeffAPSs result,
+ * AdaptiveLoopFilter.cpp:620) and per-CTB control (Picture.h:265-297). */
+typedef struct vvcr_alf {
+  int32_t num_luma_sets;                 /* 16 fixed + slice APS sets */
+  const int16_t *luma_coef;              /* [num_luma_sets][25][13] */
+  const int16_t *luma_clip;              /* [num_luma_sets][25][13] clipping values */
+  const int16_t *chroma_coef;            /* [8][7] */
+  const int16_t *chroma_clip;            /* [8][7] */
+  const int16_t *cc_coef;                /* [2][4][8] */
+  const uint8_t *ctb_en;                 /* [3][n_ctb] */
+  const uint8_t *ctb_alt;                /* [3][n_ctb] chroma alternative */
+  const int16_t *ctb_filter_set;         /* [n_ctb] luma filter set index */
+  const uint8_t *cc_ctl;                 /* [2][n_ctb] CC-ALF filter idx + 1, 0 = off */
+} vvcr_alf;
+
+int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out);
+int vvcr_destroy(vvcr_ctx *ctx);
+const char *vvcr_last_error(vvcr_ctx *ctx);
+
+int vvcr_begin_picture(vvcr_ctx *ctx, const vvcr_pic_params *pp);
+/* Copies one picture's descriptors into pinned staging and uploads them asynchronously. */
+int vvcr_submit(vvcr_ctx *ctx,
+                const vvcr_cu *cu, int32_t ncu,
+                const vvcr_pu *pu, int32_t npu,
+                const vvcr_tu *tu, int32_t ntu,
+                const int32_t *coef, int64_t ncoef,
+                const vvcr_motion *motion,          /* (height/4) x (width/4) */
+                const vvcr_geo *geo, int32_t ngeo,
+                const int32_t *dmvr_delta_unused, int32_t nd);
+int vvcr_set_loop_filter_params(vvcr_ctx *ctx, const vvcr_sao *sao /* [n_ctb][3] */, const vvcr_alf *alf);
+
+/* Stage mask for vvcr_end_picture_stages (tests isolate stages; vvcr_end_picture runs all). */
+#define VVCR_STAGE_RESID 0x01   /* dequant + inverse transform of every TU -> residual planes */
+#define VVCR_STAGE_INTER 0x02   /* motion compensation (+ BDOF/DMVR/affine/GEO/CIIP) + inter recon */
+#define VVCR_STAGE_INTRA 0x04   /* intra prediction dependency waves + recon */
+#define VVCR_STAGE_LMCS_INV 0x08
+#define VVCR_STAGE_DBK 0x10
+#define VVCR_STAGE_SAO 0x20
+#define VVCR_STAGE_ALF 0x40
+#define VVCR_STAGE_ALL 0x7f
+int vvcr_end_picture(vvcr_ctx *ctx);
+int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t stage_mask);
+int vvcr_sync(vvcr_ctx *ctx);
+
+/* Buffers addressable by vvcr_read_plane / vvcr_write_plane (tests and output). */
+#define VVCR_BUF_RECO 0   /* picture slot (the DPB) */
+#define VVCR_BUF_PRED 1   /* prediction plane of the current picture (MC output, before LMCS) */
+#define VVCR_BUF_RESI 2   /* residual plane of the current picture */
+int vvcr_read_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, int16_t *dst, int32_t dst_stride);
+int vvcr_write_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, const int16_t *src, int32_t src_stride);
+int vvcr_read_picture(vvcr_ctx *ctx, int32_t slot, uint16_t *planes[3], const int32_t strides[3]);
+/* DMVR refined deltas per PU sub-block, [npu][64][2] (PredictionUnit::mvdL0SubPu). Blocks. */
+int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n);
+
+/* Timing of the last vvcr_end_picture*, in ms, per stage (HIP events on the library stream). */
+int vvcr_last_stage_times(vvcr_ctx *ctx, float *ms, int32_t n);
+/* Raw HIP stream handle (hipStream_t) of the context, for callers that time or overlap work. */
+void *vvcr_stream(vvcr_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VVCR_H */

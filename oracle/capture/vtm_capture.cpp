@@ -347,8 +347,24 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
       o[PU_DMVR_OFF] = (int32_t)(dmvrPool.size() / 2);
       for (int k = 0; k < MAX_NUM_SUBCU_DMVR; k++) { dmvrPool.push_back(pu.mvdL0SubPu[k].hor); dmvrPool.push_back(pu.mvdL0SubPu[k].ver); }
     }
-    o[PU_DMVR] = (isInterPU && pu.mvRefine && PU::checkDMVRCondition(pu)) ? 1 : 0;
-    o[PU_BDOF] = 0;  // derived on the host (vvc_amd/descriptors.py) from the reference conditions
+    // reference decisions (InterPrediction.cpp:1584-1638): motionCompensation(cu) sets mvRefine=true around MC
+    if (isInterPU && pu.interDir == 3 && !pu.cu->geoFlag) {
+      PredictionUnit &mp = const_cast<PredictionUnit &>(pu);
+      bool saved = mp.mvRefine; mp.mvRefine = true;
+      o[PU_DMVR] = PU::checkDMVRCondition(pu) ? 1 : 0;
+      mp.mvRefine = saved;
+      WPScalingParam *wp0, *wp1;
+      sl.getWpScaling(REF_PIC_LIST_0, pu.refIdx[0], wp0);
+      sl.getWpScaling(REF_PIC_LIST_1, pu.refIdx[1], wp1);
+      bool bio = false;
+      if (sps.getBDOFEnabledFlag() && !ph.getDisBdofFlag() && !pu.cu->affine && pu.mergeType == MRG_TYPE_DEFAULT_N) {
+        bool c0 = !((wp0[0].bPresentFlag || wp0[1].bPresentFlag || wp0[2].bPresentFlag || wp1[0].bPresentFlag || wp1[1].bPresentFlag || wp1[2].bPresentFlag) && sl.getSliceType() == B_SLICE);
+        bool c1 = !(pps.getUseWP() && sl.getSliceType() == P_SLICE);
+        bio = c0 && c1 && PU::isBiPredFromDifferentDirEqDistPoc(pu) && pu.Y().height >= 8 && pu.Y().width >= 8 && pu.Y().height * pu.Y().width >= 128;
+        if (pu.ciipFlag || pu.cu->smvdMode || (sps.getUseBcw() && pu.cu->BcwIdx != BCW_DEFAULT)) bio = false;
+      }
+      o[PU_BDOF] = bio ? 1 : 0;
+    }
   }
   TR("pu table");
   F.i32("pu", put, {cs.pus.size(), (uint64_t)PU_NF});

@@ -1,0 +1,17 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libvvcr's HIP kernels)")
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN

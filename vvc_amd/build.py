@@ -1,0 +1,65 @@
+"""Builds libvvcr (HIP, gfx950) and the oracle's C restatement. No JIT caches: everything is built
+in-tree so the shared objects travel with the repository snapshot to the GPU box."""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "vvc_amd", "csrc")
+OBJ = os.path.join(ROOT, "build", "obj")
+LIB = os.path.join(ROOT, "vvc_amd", "libvvcr.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + os.path.join(ROOT, "include"),
+         "-Wno-unused-result", "-munsafe-fp-atomics"]
+
+
+def _compile(src):
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + \
+        [os.path.join(ROOT, "include", "vvcr.h")]
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
+        return obj
+    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [HIPCC] + FLAGS + ["-x", "hip", "-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("compile failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
+    return obj
+
+
+def build_lib(jobs=8):
+    os.makedirs(OBJ, exist_ok=True)
+    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(_compile, srcs))
+    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("link failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
+    return LIB
+
+
+def build_oracle():
+    """oracle/ C restatement -> oracle/_build/liboracle.so (test infrastructure)."""
+    src_dir = os.path.join(ROOT, "oracle")
+    out_dir = os.path.join(src_dir, "_build")
+    os.makedirs(out_dir, exist_ok=True)
+    srcs = sorted(os.path.join(src_dir, f) for f in os.listdir(src_dir) if f.endswith(".c"))
+    out = os.path.join(out_dir, "liboracle.so")
+    if not srcs:
+        return None
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(s) for s in srcs + [os.path.join(src_dir, "oracle.h")]):
+        cmd = ["gcc", "-O2", "-std=c11", "-fPIC", "-shared", "-Wall", "-o", out] + srcs + ["-lm"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("oracle build failed:\n%s%s" % (r.stdout, r.stderr))
+    return out
+
+
+if __name__ == "__main__":
+    print(build_lib())
+    print(build_oracle())

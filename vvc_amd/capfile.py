@@ -51,3 +51,60 @@ def load(path: str) -> dict:
     if path.endswith(".z"):
         buf = zlib.decompress(buf)
     return parse(buf)
+
+
+# ------------------------------------------------------------------------------------------------
+# compact fixture form (committed under tests/golden/): golden planes are delta-coded along the
+# decode pipeline (pred -> residual -> pre-LF recon -> DBK -> SAO -> ALF) and the whole picture is
+# an lzma-compressed .npz (loaded with allow_pickle=False).
+# ------------------------------------------------------------------------------------------------
+import io
+import lzma
+
+_CHAIN = [("pmc", "pfin"), ("dbkin", "prelf"), ("dbk", "dbkin"), ("sao", "dbk"), ("alf", "sao")]
+
+
+def _recon_guess(pic, c, bd=10):
+    pf = pic["pfin_" + c].astype(np.int32)
+    pf = np.where(pf == -32768, 0, pf)
+    return np.clip(pf + pic["resi_" + c], 0, (1 << bd) - 1)
+
+
+def pack(pic: dict) -> bytes:
+    arrs = {}
+    for k, v in pic.items():
+        if k == "hdr":
+            continue
+        arrs[k] = v
+    for c in "yuv":
+        if "prelf_" + c in pic:
+            arrs["prelf_" + c] = (pic["prelf_" + c].astype(np.int32) - _recon_guess(pic, c)).astype(np.int16)
+        for dst, src in _CHAIN:
+            if dst + "_" + c in pic and src + "_" + c in pic:
+                arrs[dst + "_" + c] = (pic[dst + "_" + c].astype(np.int32) - pic[src + "_" + c]).astype(np.int16)
+    arrs["hdr_keys"] = np.frombuffer(",".join(pic["hdr"].keys()).encode(), np.uint8)
+    arrs["hdr_vals"] = np.array(list(pic["hdr"].values()), np.int64)
+    bio = io.BytesIO()
+    np.savez(bio, **arrs)
+    return lzma.compress(bio.getvalue(), preset=9)
+
+
+def unpack(blob: bytes) -> dict:
+    z = np.load(io.BytesIO(lzma.decompress(blob)), allow_pickle=False)
+    pic = {k: z[k] for k in z.files}
+    keys = bytes(pic.pop("hdr_keys")).decode().split(",")
+    pic["hdr"] = dict(zip(keys, (int(v) for v in pic.pop("hdr_vals"))))
+    for c in "yuv":
+        if "prelf_" + c in pic:
+            pic["prelf_" + c] = (pic["prelf_" + c].astype(np.int32) + _recon_guess(pic, c)).astype(np.int16)
+        for dst, src in _CHAIN:
+            if dst + "_" + c in pic and src + "_" + c in pic:
+                pic[dst + "_" + c] = (pic[dst + "_" + c].astype(np.int32) + pic[src + "_" + c]).astype(np.int16)
+    return pic
+
+
+def load_any(path: str) -> dict:
+    if path.endswith(".xz"):
+        with open(path, "rb") as f:
+            return unpack(f.read())
+    return load(path)

@@ -1,0 +1,65 @@
+// vvcr_internal.h — shared host/device definitions of libvvcr (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+#include <vector>
+#include "../../include/vvcr.h"
+
+#define VVCR_CHECK_HIP(expr)                                                        \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess) throw VvcrError(VVCR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+struct VvcrError {
+  int code;
+  std::string msg;
+  VvcrError(int c, std::string m) : code(c), msg(std::move(m)) {}
+};
+
+// One sample plane in HBM: int16 samples ("Pel"), row pitch in samples (multiple of 64 -> 128 B rows).
+struct DPlane {
+  int16_t *p = nullptr;
+  int32_t stride = 0, w = 0, h = 0;
+};
+
+// ------------------------------------------------------------------------------------------------
+// Motion-compensation work item: one block of <= 16x16 luma (+ its 4:2:0 chroma) with constant
+// motion. PUs are tiled into such blocks on the host (MC is position-invariant per sample, so a
+// PU's prediction equals the union of its tiles' predictions — InterPrediction::xPredInterBlk,
+// InterPrediction.cpp:698). 32 bytes, one wave per job.
+// ------------------------------------------------------------------------------------------------
+enum : uint16_t {
+  MC_L0 = 1 << 0,        // list 0 used
+  MC_L1 = 1 << 1,        // list 1 used (both set = bi)
+  MC_LUMA = 1 << 2,      // predict luma
+  MC_CHROMA = 1 << 3,    // predict both chroma components
+  MC_ALT_HPEL = 1 << 4,  // 6-tap-smoothed half-pel luma filter (cu.imv == IMV_HPEL, InterpolationFilter.cpp:778)
+  MC_BDOF = 1 << 5,      // bi-directional optical flow on luma (InterPrediction.cpp:1274)
+  MC_DMVR = 1 << 6,      // decoder-side MV refinement of this 16x16 sub-block (InterPrediction.cpp:2133)
+  MC_KEEP14 = 1 << 7,    // write 14-bit intermediate (GEO parts) instead of final samples
+};
+
+struct McJob {
+  int16_t x, y;          // luma position (picture coordinates)
+  uint8_t w, h;          // luma size (4..16)
+  uint16_t flags;
+  int16_t mv[2][2];      // [list][hor/ver], 1/16 luma sample
+  int8_t slot[2];        // DPB slot per list
+  int8_t bcw;            // BcwIdx (2 = default average)
+  int8_t pad0;
+  int32_t aux;           // DMVR: index of this sub-block in the delta output buffer
+  int32_t pad1[2];
+};
+static_assert(sizeof(McJob) == 32, "McJob layout");
+
+struct McParams {
+  DPlane ref[32][3];     // DPB planes by slot (only used slots valid)
+  DPlane out[3];         // destination (prediction planes of the current picture)
+  int32_t pic_w, pic_h;  // luma picture size
+  int32_t bd;            // bit depth
+};
+
+// launchers (vvcr_mc.hip)
+void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);

@@ -1,0 +1,193 @@
+// vvcr_mc.hip — motion-compensated prediction for gfx950.
+//
+// One 64-lane wave per McJob (<= 16x16 luma block + 8x8 Cb/Cr). Per component and list the wave
+// stages the (w+N-1)x(h+N-1) reference window in LDS with coordinates clamped to the picture
+// (equivalent to VTM's edge-replicated 288-sample margin, Picture::extendPicBorder Picture.cpp:737,
+// plus clipMv Mv.cpp:54 — every filter phase sums to 64 so a clamped run of equal samples filters to
+// the same value whatever the phase), runs the separable FIR exactly as
+// InterpolationFilter::filter<N,isVertical,isFirst,isLast> (InterpolationFilter.cpp:548-650) with the
+// copy / H-only / V-only / H-then-V split of InterPrediction::xPredInterBlk (InterPrediction.cpp:784-803),
+// keeps per-list results in registers and combines them like AreaBuf::addAvg (Buffer.cpp:447),
+// addWeightedAvg (BCW, Buffer.cpp:350) or the uni-prediction rounding (rndRes = !bi).
+#include "vvcr_internal.h"
+#include "vvcr_tables.h"
+
+namespace {
+
+__constant__ int8_t c_luma[16][8] = VVCR_LUMA_FILTER_TABLE;
+__constant__ int8_t c_luma4x4[16][8] = VVCR_LUMA4x4_FILTER_TABLE;
+__constant__ int8_t c_alt_hpel[8] = VVCR_LUMA_ALT_HPEL;
+__constant__ int8_t c_chroma[32][4] = VVCR_CHROMA_FILTER_TABLE;
+__constant__ int8_t c_bcw_w1[5] = VVCR_BCW_W1;
+
+constexpr int IF_INTERNAL_PREC = 14;
+constexpr int IF_FILTER_PREC = 6;
+constexpr int IF_INTERNAL_OFFS = 1 << (IF_INTERNAL_PREC - 1);
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// LDS budget per wave (one job per 64-thread workgroup)
+constexpr int WIN_STRIDE = 24;              // up to 16+7 = 23 columns
+constexpr int WIN_ROWS = 23;
+constexpr int TMP_STRIDE = 16;
+
+// Predict one component of one list into per-lane registers out[k] (k-th sample of lane).
+// N = taps (8 luma / 4 chroma). Output either final Pel (rnd) or 14-bit intermediate.
+template <int N>
+__device__ void predict_list(const DPlane &ref, int bx, int by, int bw, int bh, int mvx, int mvy,
+                             int fracBits, bool altHpel, bool rnd, int bd, int16_t *win, int16_t *tmp,
+                             int lane, int (&out)[4]) {
+  const int mask = (1 << fracBits) - 1;
+  const int fx = mvx & mask, fy = mvy & mask;
+  const int ix = bx + (mvx >> fracBits), iy = by + (mvy >> fracBits);
+  const int half = N / 2 - 1;
+  const int ww = bw + N - 1, wh = bh + N - 1;
+  const int pw = ref.w, ph = ref.h;
+  // stage window (clamped coordinates)
+  for (int i = lane; i < ww * wh; i += 64) {
+    int r = i / ww, c = i - r * ww;
+    int sx = clampi(ix - half + c, 0, pw - 1), sy = clampi(iy - half + r, 0, ph - 1);
+    win[r * WIN_STRIDE + c] = ref.p[(size_t)sy * ref.stride + sx];
+  }
+  __syncthreads();
+  // coefficient rows
+  int8_t ch[8], cv[8];
+  if (N == 8) {
+    const bool is4x4 = (bw == 4 && bh == 4);
+    const int8_t *th = (fx == 8 && altHpel) ? c_alt_hpel : (is4x4 ? c_luma4x4[fx] : c_luma[fx]);
+    const int8_t *tv = (fy == 8 && altHpel) ? c_alt_hpel : (is4x4 ? c_luma4x4[fy] : c_luma[fy]);
+#pragma unroll
+    for (int t = 0; t < 8; t++) { ch[t] = th[t]; cv[t] = tv[t]; }
+  } else {
+#pragma unroll
+    for (int t = 0; t < 4; t++) { ch[t] = c_chroma[fx][t]; cv[t] = c_chroma[fy][t]; }
+  }
+  const int headRoom = max(2, IF_INTERNAL_PREC - bd);
+  const int n = bw * bh;
+  if (fx == 0 && fy == 0) {
+    // filterCopy<true, isLast> (InterpolationFilter.cpp:403)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int i = lane + 64 * k;
+      if (i < n) {
+        int y = i / bw, x = i - y * bw;
+        int v = win[(y + half) * WIN_STRIDE + x + half];
+        out[k] = rnd ? v : (int)(int16_t)((v << headRoom) - IF_INTERNAL_OFFS);
+      }
+    }
+  } else if (fy == 0 || fx == 0) {
+    // single pass, isFirst = true, isLast = rnd
+    const bool vert = (fx == 0);
+    const int shift = rnd ? IF_FILTER_PREC : IF_FILTER_PREC - headRoom;
+    const int offset = rnd ? (1 << (shift - 1)) : -(IF_INTERNAL_OFFS << shift);
+    const int maxv = (1 << bd) - 1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int i = lane + 64 * k;
+      if (i < n) {
+        int y = i / bw, x = i - y * bw;
+        int sum = 0;
+        if (vert) {
+#pragma unroll
+          for (int t = 0; t < N; t++) sum += win[(y + t) * WIN_STRIDE + x + half] * cv[t];
+        } else {
+#pragma unroll
+          for (int t = 0; t < N; t++) sum += win[(y + half) * WIN_STRIDE + x + t] * ch[t];
+        }
+        int v = (int)(int16_t)((sum + offset) >> shift);
+        out[k] = rnd ? clampi(v, 0, maxv) : v;
+      }
+    }
+  } else {
+    // H pass (isFirst, !isLast) over bh+N-1 rows into tmp, then V pass (!isFirst, isLast = rnd)
+    const int sh1 = IF_FILTER_PREC - headRoom;
+    const int off1 = -(IF_INTERNAL_OFFS << sh1);
+    for (int i = lane; i < bw * wh; i += 64) {
+      int r = i / bw, c = i - r * bw;
+      int sum = 0;
+#pragma unroll
+      for (int t = 0; t < N; t++) sum += win[r * WIN_STRIDE + c + t] * ch[t];
+      tmp[r * TMP_STRIDE + c] = (int16_t)((sum + off1) >> sh1);
+    }
+    __syncthreads();
+    const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
+    const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
+    const int maxv = (1 << bd) - 1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int i = lane + 64 * k;
+      if (i < n) {
+        int y = i / bw, x = i - y * bw;
+        int sum = 0;
+#pragma unroll
+        for (int t = 0; t < N; t++) sum += tmp[(y + t) * TMP_STRIDE + x] * cv[t];
+        int v = (int)(int16_t)((sum + off2) >> sh2);
+        out[k] = rnd ? clampi(v, 0, maxv) : v;
+      }
+    }
+  }
+  __syncthreads();   // window / tmp reused by the next list or component
+}
+
+template <int N>
+__device__ void mc_component(const McParams &P, const McJob &J, int comp, int16_t *win, int16_t *tmp, int lane) {
+  const int cs = comp ? 1 : 0;                 // 4:2:0 scale
+  const int bx = J.x >> cs, by = J.y >> cs, bw = J.w >> cs, bh = J.h >> cs;
+  const int fracBits = 4 + cs;
+  const bool l0 = J.flags & MC_L0, l1 = J.flags & MC_L1;
+  const bool bi = l0 && l1;
+  const bool keep14 = (J.flags & MC_KEEP14) != 0;
+  const bool alt = (J.flags & MC_ALT_HPEL) && comp == 0;
+  const int bd = P.bd;
+  int r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
+  const bool rnd = !bi && !keep14;
+  if (l0) predict_list<N>(P.ref[J.slot[0]][comp], bx, by, bw, bh, J.mv[0][0], J.mv[0][1], fracBits, alt, rnd, bd, win, tmp, lane, r0);
+  if (l1) predict_list<N>(P.ref[J.slot[1]][comp], bx, by, bw, bh, J.mv[1][0], J.mv[1][1], fracBits, alt, rnd, bd, win, tmp, lane, bi ? r1 : r0);
+  const DPlane &o = P.out[comp];
+  const int n = bw * bh;
+  const int maxv = (1 << bd) - 1;
+  const int headRoom = max(2, IF_INTERNAL_PREC - bd);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    int i = lane + 64 * k;
+    if (i >= n) continue;
+    int y = i / bw, x = i - y * bw;
+    int v;
+    if (!bi) {
+      v = r0[k];
+    } else if (J.bcw != 2) {
+      // AreaBuf<Pel>::addWeightedAvg (Buffer.cpp:350)
+      const int w1 = c_bcw_w1[J.bcw], w0 = 8 - w1;
+      const int shiftNum = headRoom + 3;
+      const int offset = (1 << (shiftNum - 1)) + (IF_INTERNAL_OFFS << 3);
+      v = clampi((r0[k] * w0 + r1[k] * w1 + offset) >> shiftNum, 0, maxv);
+    } else {
+      // AreaBuf<Pel>::addAvg (Buffer.cpp:447)
+      const int shiftNum = headRoom + 1;
+      const int offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
+      v = clampi((r0[k] + r1[k] + offset) >> shiftNum, 0, maxv);
+    }
+    o.p[(size_t)(by + y) * o.stride + bx + x] = (int16_t)v;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__restrict__ jobs, int njobs) {
+  __shared__ int16_t win[WIN_ROWS * WIN_STRIDE];
+  __shared__ int16_t tmp[WIN_ROWS * TMP_STRIDE];
+  const int j = blockIdx.x;
+  if (j >= njobs) return;
+  const McJob J = jobs[j];
+  const int lane = threadIdx.x;
+  if (J.flags & MC_LUMA) mc_component<8>(P, J, 0, win, tmp, lane);
+  if (J.flags & MC_CHROMA) {
+    mc_component<4>(P, J, 1, win, tmp, lane);
+    mc_component<4>(P, J, 2, win, tmp, lane);
+  }
+}
+
+}  // namespace
+
+void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(k_mc_basic, dim3(njobs), dim3(64), 0, s, p, jobs, njobs);
+}

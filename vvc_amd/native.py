@@ -1,0 +1,159 @@
+"""ctypes binding of libvvcr's C-ABI (include/vvcr.h). The product path: if the HIP library is not
+built or cannot be loaded this module raises — there is no CPU fallback."""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvvcr.so")
+
+MAX_REF = 16
+STAGE_RESID, STAGE_INTER, STAGE_INTRA, STAGE_LMCS_INV = 0x01, 0x02, 0x04, 0x08
+STAGE_DBK, STAGE_SAO, STAGE_ALF, STAGE_ALL = 0x10, 0x20, 0x40, 0x7F
+BUF_RECO, BUF_PRED, BUF_RESI = 0, 1, 2
+
+I32 = C.c_int32
+
+
+class SeqParams(C.Structure):
+    _fields_ = [(n, I32) for n in ("width", "height", "chroma_format", "bit_depth", "ctu_log2", "dpb_slots", "device")]
+
+
+class PicParams(C.Structure):
+    _fields_ = [
+        ("poc", I32), ("slot", I32), ("slice_type", I32), ("slice_qp", I32),
+        ("num_ref", I32 * 2),
+        ("ref_slot", (I32 * MAX_REF) * 2), ("ref_poc", (I32 * MAX_REF) * 2), ("ref_lt", (I32 * MAX_REF) * 2),
+        ("dual_tree", I32), ("dep_quant", I32), ("sign_hiding", I32), ("joint_cbcr", I32),
+        ("bdof_enabled", I32), ("dmvr_enabled", I32), ("prof_enabled", I32), ("lfnst_enabled", I32),
+        ("mts_intra", I32), ("mts_inter", I32), ("sbt", I32),
+        ("wp_p", I32), ("wp_b", I32),
+        ("wp", (((I32 * 7) * 3) * MAX_REF) * 2),
+        ("dbk_disable", I32), ("dbk_beta_offset_div2", I32), ("dbk_tc_offset_div2", I32),
+        ("lf_across_slices", I32), ("lf_across_tiles", I32),
+        ("chroma_qp_off", I32 * 3),
+        ("chroma_qp_map", (I32 * 128) * 3),
+        ("sao_luma", I32), ("sao_chroma", I32),
+        ("alf_en", I32 * 3), ("ccalf_en", I32 * 2), ("alf_vb_luma", I32), ("alf_vb_chroma", I32),
+        ("lmcs_enabled", I32), ("lmcs_chroma_scale", I32), ("lmcs_min_bin", I32), ("lmcs_max_bin", I32),
+        ("lmcs_fwd", C.c_int16 * 1024), ("lmcs_inv", C.c_int16 * 1024), ("lmcs_pivot", C.c_int16 * 17),
+        ("lmcs_cadj", I32 * 16),
+        ("max_tb_log2", I32), ("log2_max_ts", I32),
+    ]
+
+
+class Alf(C.Structure):
+    _fields_ = [("num_luma_sets", I32),
+                ("luma_coef", C.c_void_p), ("luma_clip", C.c_void_p),
+                ("chroma_coef", C.c_void_p), ("chroma_clip", C.c_void_p), ("cc_coef", C.c_void_p),
+                ("ctb_en", C.c_void_p), ("ctb_alt", C.c_void_p), ("ctb_filter_set", C.c_void_p), ("cc_ctl", C.c_void_p)]
+
+
+class VvcrError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise VvcrError("libvvcr.so is not built (run __graft_entry__.build()); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.vvcr_create.argtypes = [C.POINTER(SeqParams), C.POINTER(P)]
+        L.vvcr_destroy.argtypes = [P]
+        L.vvcr_last_error.argtypes = [P]
+        L.vvcr_last_error.restype = C.c_char_p
+        L.vvcr_begin_picture.argtypes = [P, C.POINTER(PicParams)]
+        L.vvcr_submit.argtypes = [P, P, I32, P, I32, P, I32, P, C.c_int64, P, P, I32, P, I32]
+        L.vvcr_set_loop_filter_params.argtypes = [P, P, C.POINTER(Alf)]
+        L.vvcr_end_picture.argtypes = [P]
+        L.vvcr_end_picture_stages.argtypes = [P, C.c_uint32]
+        L.vvcr_sync.argtypes = [P]
+        L.vvcr_read_plane.argtypes = [P, I32, I32, I32, P, I32]
+        L.vvcr_write_plane.argtypes = [P, I32, I32, I32, P, I32]
+        L.vvcr_last_stage_times.argtypes = [P, C.POINTER(C.c_float), I32]
+        L.vvcr_stream.argtypes = [P]
+        L.vvcr_stream.restype = P
+        _lib = L
+    return _lib
+
+
+EXPORTS = ["vvcr_create", "vvcr_destroy", "vvcr_last_error", "vvcr_begin_picture", "vvcr_submit",
+           "vvcr_set_loop_filter_params", "vvcr_end_picture", "vvcr_end_picture_stages", "vvcr_sync",
+           "vvcr_read_plane", "vvcr_write_plane", "vvcr_read_picture", "vvcr_get_dmvr_deltas",
+           "vvcr_last_stage_times", "vvcr_stream"]
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None and a.size else None
+
+
+class Context:
+    """One libvvcr context = one device-resident DPB and stream."""
+
+    def __init__(self, width, height, bit_depth=10, ctu_log2=7, dpb_slots=16, device=0):
+        self.L = lib()
+        sp = SeqParams(width, height, 1, bit_depth, ctu_log2, dpb_slots, device)
+        h = C.c_void_p()
+        r = self.L.vvcr_create(C.byref(sp), C.byref(h))
+        if r != 0:
+            raise VvcrError("vvcr_create failed (%d): %s" % (r, self.L.vvcr_last_error(None).decode()))
+        self.h = h
+        self.width, self.height = width, height
+        self._keep = []
+
+    def _chk(self, r, what):
+        if r != 0:
+            raise VvcrError("%s failed (%d): %s" % (what, r, self.L.vvcr_last_error(self.h).decode()))
+
+    def close(self):
+        if self.h:
+            self.L.vvcr_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def begin_picture(self, pp: PicParams):
+        self._chk(self.L.vvcr_begin_picture(self.h, C.byref(pp)), "vvcr_begin_picture")
+
+    def submit(self, cu, pu, tu, coef, motion, geo):
+        arrs = [np.ascontiguousarray(a, np.int32) for a in (cu, pu, tu, coef, motion, geo)]
+        cu, pu, tu, coef, motion, geo = arrs
+        self._chk(self.L.vvcr_submit(self.h, _ptr(cu), len(cu), _ptr(pu), len(pu), _ptr(tu), len(tu),
+                                     _ptr(coef), coef.size, _ptr(motion), _ptr(geo), len(geo), None, 0),
+                  "vvcr_submit")
+
+    def set_loop_filter_params(self, sao, alf_struct, keep):
+        self._keep = keep
+        self._chk(self.L.vvcr_set_loop_filter_params(self.h, _ptr(sao), C.byref(alf_struct) if alf_struct else None),
+                  "vvcr_set_loop_filter_params")
+
+    def end_picture(self, stages=STAGE_ALL):
+        self._chk(self.L.vvcr_end_picture_stages(self.h, stages), "vvcr_end_picture_stages")
+
+    def sync(self):
+        self._chk(self.L.vvcr_sync(self.h), "vvcr_sync")
+
+    def read_plane(self, buf, slot, comp):
+        w, h = (self.width, self.height) if comp == 0 else (self.width // 2, self.height // 2)
+        out = np.empty((h, w), np.int16)
+        self._chk(self.L.vvcr_read_plane(self.h, buf, slot, comp, _ptr(out), w), "vvcr_read_plane")
+        return out
+
+    def write_plane(self, buf, slot, comp, data):
+        data = np.ascontiguousarray(data, np.int16)
+        self._chk(self.L.vvcr_write_plane(self.h, buf, slot, comp, _ptr(data), data.shape[1]), "vvcr_write_plane")
+
+    def stage_ms(self):
+        t = (C.c_float * 8)()
+        self._chk(self.L.vvcr_last_stage_times(self.h, t, 8), "vvcr_last_stage_times")
+        return list(t)

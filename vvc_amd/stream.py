@@ -1,0 +1,96 @@
+"""Host driver of the reconstruction path: replays parsed pictures (descriptor captures) through
+libvvcr in decode order, manages DPB slots, and mirrors DecApp/DecLib's per-picture sequencing
+(DecApp::decode DecApp.cpp:118-200: decode NALs -> DecLib::executeLoopFilters -> finishPicture).
+"""
+import glob
+import hashlib
+import json
+import os
+
+import numpy as np
+
+from . import capfile
+from . import native as N
+
+
+def load_sequence(path, max_pics=0):
+    files = sorted(glob.glob(os.path.join(path, "pic_*.xz"))) or sorted(glob.glob(os.path.join(path, "pic_*.cap")))
+    if max_pics:
+        files = files[:max_pics]
+    return [capfile.load_any(f) for f in files]
+
+
+def load_meta(path):
+    with open(os.path.join(path, "md5.json")) as f:
+        return json.load(f)
+
+
+def plane_md5(plane):
+    return hashlib.md5(np.ascontiguousarray(plane).astype("<u2").tobytes()).hexdigest()
+
+
+class SlotAllocator:
+    """Assigns DPB slots so that a picture keeps its slot until its last use as a reference."""
+
+    def __init__(self, pics, nslots):
+        self.last_use = {}
+        for i, p in enumerate(pics):
+            self.last_use.setdefault(p["hdr"]["poc"], i)
+            for l in range(2):
+                for r in range(p["hdr"]["num_ref_l%d" % l]):
+                    self.last_use[int(p["ref_poc"][l][r])] = i
+        self.nslots = nslots
+        self.slot_of = {}
+        self.free = list(range(nslots))
+
+    def assign(self, i, poc):
+        # release pictures no longer referenced at or after decode index i
+        for q, s in list(self.slot_of.items()):
+            if self.last_use.get(q, -1) < i and q != poc:
+                del self.slot_of[q]
+                self.free.append(s)
+        if not self.free:
+            raise RuntimeError("DPB exhausted")
+        s = self.free.pop(0)
+        self.slot_of[poc] = s
+        return s
+
+
+def pic_params(p, slot, slot_of):
+    h = p["hdr"]
+    pp = N.PicParams()
+    pp.poc, pp.slot, pp.slice_type, pp.slice_qp = h["poc"], slot, h["slice_type"], h["slice_qp"]
+    for l in range(2):
+        n = h["num_ref_l%d" % l]
+        pp.num_ref[l] = n
+        for r in range(n):
+            poc = int(p["ref_poc"][l][r])
+            pp.ref_poc[l][r] = poc
+            pp.ref_slot[l][r] = slot_of.get(poc, 0)
+            pp.ref_lt[l][r] = int(p["ref_lt"][l][r])
+    for k in ("dual_tree", "dep_quant", "sign_hiding", "joint_cbcr", "bdof_enabled", "dmvr_enabled", "prof_enabled",
+              "lfnst_enabled", "mts_intra", "mts_inter", "sbt", "wp_p", "wp_b", "dbk_disable", "dbk_beta_offset_div2",
+              "dbk_tc_offset_div2", "lf_across_slices", "lf_across_tiles", "sao_luma", "sao_chroma", "alf_vb_luma",
+              "alf_vb_chroma", "lmcs_chroma_scale", "lmcs_min_bin", "lmcs_max_bin", "log2_max_ts"):
+        setattr(pp, k, h[k])
+    pp.lmcs_enabled = h["lmcs_enabled"] and h["lmcs_slice_flag"]
+    pp.max_tb_log2 = int(h["max_tb_size"]).bit_length() - 1
+    pp.chroma_qp_off[1], pp.chroma_qp_off[2] = h["chroma_qp_off_cb"], h["chroma_qp_off_cr"]
+    wp = np.ascontiguousarray(p["wp"], np.int32)
+    np.copyto(np.ctypeslib.as_array(pp.wp).reshape(wp.shape), wp)
+    cqm = np.ascontiguousarray(p["chroma_qp_map"], np.int32)
+    np.copyto(np.ctypeslib.as_array(pp.chroma_qp_map).reshape(cqm.shape), cqm)
+    for c in range(3):
+        pp.alf_en[c] = h["alf_slice_en%d" % c]
+    pp.ccalf_en[0], pp.ccalf_en[1] = h["ccalf_en_cb"], h["ccalf_en_cr"]
+    for name, n in (("lmcs_fwd", 1024), ("lmcs_inv", 1024), ("lmcs_pivot", 17)):
+        src = np.asarray(p[name], np.int16)[:n]
+        np.copyto(np.ctypeslib.as_array(getattr(pp, name))[:len(src)], src)
+    cadj = np.asarray(p["lmcs_cadj"], np.int32)[:16]
+    np.copyto(np.ctypeslib.as_array(pp.lmcs_cadj)[:len(cadj)], cadj)
+    return pp
+
+
+def submit(ctx, p):
+    geo = p["geo"] if p["geo"].size else np.zeros((0, 13), np.int32)
+    ctx.submit(p["cu"], p["pu"], p["tu"], p["coef"], p["motion"].reshape(-1, 10), geo)
