@@ -46,6 +46,9 @@
 #include "CommonLib/AdaptiveLoopFilter.h"
 #include "CommonLib/Reshape.h"
 #include "CommonLib/dtrace_next.h"
+namespace vtm_mip {
+#include "CommonLib/MipData.h"
+}
 #undef private
 #undef protected
 
@@ -102,6 +105,7 @@ static int g_picCounter = 0;
 static PicCapture g_cap;
 
 static void initPlanes(const CodingStructure &cs) {
+  if (g_dir.empty()) return;   // not capturing: wrappers only forward
   g_cap = PicCapture();
   g_cap.cs = &cs;
   g_cap.active = true;
@@ -114,15 +118,23 @@ static void initPlanes(const CodingStructure &cs) {
   }
 }
 
-// locate a buffer that views the picture-sized CodingStructure pred / resi storage
+// locate a buffer that views the CodingStructure pred / resi storage. Without KEEP_PRED_AND_RESI_SIGNALS
+// those buffers are CTU-sized and indexed with CTU-local coordinates (Picture::getBuf Picture.cpp:841-850),
+// so the absolute position is the current CTU origin (set by every wrapper that knows its unit) + offset.
+static int g_ctuX = 0, g_ctuY = 0;
+static void setCtu(const CodingStructure &cs, int lumaX, int lumaY) {
+  const int m = ~(int)(cs.pcv->maxCUWidth - 1);
+  g_ctuX = lumaX & m; g_ctuY = lumaY & m;
+}
 static bool locate(const CodingStructure &cs, PictureType type, int comp, const Pel *p, int &x, int &y) {
   const PelStorage *st = type == PIC_PREDICTION ? &cs.m_pred : &cs.m_resi;
   if (st->bufs.size() <= (size_t)comp) return false;
   const PelBuf &b = st->bufs[comp];
   ptrdiff_t off = p - b.buf;
   if (off < 0 || off >= (ptrdiff_t)b.stride * (ptrdiff_t)b.height) return false;
-  y = (int)(off / b.stride);
-  x = (int)(off % b.stride);
+  const int sc = comp ? 1 : 0;
+  y = (int)(off / b.stride) + (g_ctuY >> sc);
+  x = (int)(off % b.stride) + (g_ctuX >> sc);
   return true;
 }
 
@@ -221,6 +233,16 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
   H.add("max_tb_size", sps.getMaxTbSize());
   H.add("log2_max_ts", pps.getLog2MaxTransformSkipBlockSize());
   H.add("joint_cbcr", sps.getJointCbCrEnabledFlag() ? 1 : 0);
+  H.add("joint_cbcr_sign", ph.getJointCbCrSignFlag() ? 1 : 0);
+  H.add("use_mts", sps.getUseMTS() ? 1 : 0);
+  H.add("implicit_mts", sps.getUseImplicitMTS() ? 1 : 0);
+  H.add("bdpcm_enabled", sps.m_BDPCMEnabled);
+  H.add("isp_enabled", sps.getUseISP() ? 1 : 0);
+  H.add("mip_enabled", sps.getUseMIP() ? 1 : 0);
+  H.add("lm_chroma", sps.getUseLMChroma() ? 1 : 0);
+  H.add("ciip_enabled", sps.getUseCiip() ? 1 : 0);
+  H.add("bcw_enabled", sps.getUseBcw() ? 1 : 0);
+  H.add("min_qp_ts", 4 + sps.getMinQpPrimeTsMinus4(CHANNEL_TYPE_LUMA));
   H.add("chroma_qp_off_cb", pps.getQpOffset(COMPONENT_Cb) + sl.getSliceChromaQpDelta(COMPONENT_Cb));
   H.add("chroma_qp_off_cr", pps.getQpOffset(COMPONENT_Cr) + sl.getSliceChromaQpDelta(COMPONENT_Cr));
   H.add("pps_cb_qp_offset", pps.getQpOffset(COMPONENT_Cb));
@@ -510,6 +532,38 @@ static void dumpAlf(CapFile &F, DecLib &dec, const CodingStructure &cs) {
   F.i32("ccalf_info", ccn, {2, (uint64_t)(1 + MAX_NUM_CC_ALF_FILTERS)});
 }
 
+// ---------------------------------------------------------------------------------------------
+// constant tables of the reference (transform / LFNST / MIP / deblocking / GEO), dumped once from the
+// running reference so the kernels' generated tables can be pinned against them (tests/golden/tables.cap)
+// ---------------------------------------------------------------------------------------------
+static void dumpTables(const char *path) {
+  CapFile T;
+  T.open(path);
+  auto m = [&](const char *n, const TMatrixCoeff *p, int N) { std::vector<int16_t> v(p, p + N * N); T.i16(n, v, {(uint64_t)N, (uint64_t)N}); };
+  m("dct2_2", &g_trCoreDCT2P2[0][0][0], 2); m("dct2_4", &g_trCoreDCT2P4[0][0][0], 4); m("dct2_8", &g_trCoreDCT2P8[0][0][0], 8);
+  m("dct2_16", &g_trCoreDCT2P16[0][0][0], 16); m("dct2_32", &g_trCoreDCT2P32[0][0][0], 32); m("dct2_64", &g_trCoreDCT2P64[0][0][0], 64);
+  m("dst7_4", &g_trCoreDST7P4[0][0][0], 4); m("dst7_8", &g_trCoreDST7P8[0][0][0], 8); m("dst7_16", &g_trCoreDST7P16[0][0][0], 16); m("dst7_32", &g_trCoreDST7P32[0][0][0], 32);
+  m("dct8_4", &g_trCoreDCT8P4[0][0][0], 4); m("dct8_8", &g_trCoreDCT8P8[0][0][0], 8); m("dct8_16", &g_trCoreDCT8P16[0][0][0], 16); m("dct8_32", &g_trCoreDCT8P32[0][0][0], 32);
+  { std::vector<int16_t> v(&g_lfnst8x8[0][0][0][0], &g_lfnst8x8[0][0][0][0] + 4 * 2 * 16 * 48); T.i16("lfnst8x8", v, {4, 2, 16, 48}); }
+  { std::vector<int16_t> v(&g_lfnst4x4[0][0][0][0], &g_lfnst4x4[0][0][0][0] + 4 * 2 * 16 * 16); T.i16("lfnst4x4", v, {4, 2, 16, 16}); }
+  { std::vector<int16_t> v(g_lfnstLut, g_lfnstLut + NUM_INTRA_MODE + NUM_EXT_LUMA_MODE - 1); T.i16("lfnst_lut", v, {v.size()}); }
+  { std::vector<int16_t> v(&vtm_mip::mipMatrix4x4[0][0][0], &vtm_mip::mipMatrix4x4[0][0][0] + 16 * 16 * 4); T.i16("mip4x4", v, {16, 16, 4}); }
+  { std::vector<int16_t> v(&vtm_mip::mipMatrix8x8[0][0][0], &vtm_mip::mipMatrix8x8[0][0][0] + 8 * 16 * 8); T.i16("mip8x8", v, {8, 16, 8}); }
+  { std::vector<int16_t> v(&vtm_mip::mipMatrix16x16[0][0][0], &vtm_mip::mipMatrix16x16[0][0][0] + 6 * 64 * 7); T.i16("mip16x16", v, {6, 64, 7}); }
+  { std::vector<int16_t> v(LoopFilter::sm_tcTable, LoopFilter::sm_tcTable + MAX_QP + 1 + 2); T.i16("dbk_tc", v, {v.size()}); }
+  { std::vector<int16_t> v(LoopFilter::sm_betaTable, LoopFilter::sm_betaTable + MAX_QP + 1); T.i16("dbk_beta", v, {v.size()}); }
+  { std::vector<int16_t> v(&g_invQuantScales[0][0], &g_invQuantScales[0][0] + 2 * SCALING_LIST_REM_NUM); T.i16("inv_quant_scales", v, {2, (uint64_t)SCALING_LIST_REM_NUM}); }
+  { std::vector<int16_t> v; for (int i = 0; i < GEO_NUM_PARTITION_MODE; i++) { v.push_back(g_GeoParams[i][0]); v.push_back(g_GeoParams[i][1]); } T.i16("geo_params", v, {(uint64_t)GEO_NUM_PARTITION_MODE, 2}); }
+  { std::vector<int16_t> v(g_angle2mask, g_angle2mask + GEO_NUM_ANGLES); T.i16("geo_angle2mask", v, {v.size()}); }
+  { std::vector<int16_t> v(g_Dis, g_Dis + GEO_NUM_ANGLES); T.i16("geo_dis", v, {v.size()}); }
+  { std::vector<int16_t> v(g_angle2mirror, g_angle2mirror + GEO_NUM_ANGLES); T.i16("geo_angle2mirror", v, {v.size()}); }
+  { std::vector<int16_t> v(&g_weightOffset[0][0][0][0], &g_weightOffset[0][0][0][0] + GEO_NUM_PARTITION_MODE * GEO_NUM_CU_SIZE * GEO_NUM_CU_SIZE * 2);
+    T.i16("geo_weight_offset", v, {(uint64_t)GEO_NUM_PARTITION_MODE, (uint64_t)GEO_NUM_CU_SIZE, (uint64_t)GEO_NUM_CU_SIZE, 2}); }
+  { std::vector<int16_t> v; for (int i = 0; i < GEO_NUM_PRESTORED_MASK; i++) v.insert(v.end(), g_globalGeoWeights[i], g_globalGeoWeights[i] + GEO_WEIGHT_MASK_SIZE * GEO_WEIGHT_MASK_SIZE);
+    T.i16("geo_weights", v, {(uint64_t)GEO_NUM_PRESTORED_MASK, (uint64_t)GEO_WEIGHT_MASK_SIZE, (uint64_t)GEO_WEIGHT_MASK_SIZE}); }
+  T.close();
+}
+
 static DecLib *g_dec = nullptr;
 static CapFile g_file;
 
@@ -541,6 +595,8 @@ extern "C" {
 void __real__ZN6DecLib18executeLoopFiltersEv(DecLib *self);
 void __wrap__ZN6DecLib18executeLoopFiltersEv(DecLib *self) {
   g_dec = self;
+  static bool tablesDumped = false;
+  if (!tablesDumped && getenv("VVCR_DUMP_TABLES")) { dumpTables(getenv("VVCR_DUMP_TABLES")); tablesDumped = true; }
   if (!self->m_pcPic || g_dir.empty()) { __real__ZN6DecLib18executeLoopFiltersEv(self); return; }
   CodingStructure &cs = *self->m_pcPic->cs;
   char path[512];
@@ -578,6 +634,7 @@ void __real__ZN15InterPrediction18motionCompensationER10CodingUnitRK10RefPicList
 void __wrap__ZN15InterPrediction18motionCompensationER10CodingUnitRK10RefPicListbb(InterPrediction *self, CodingUnit &cu, const RefPicList &l, bool luma, bool chroma) {
   __real__ZN15InterPrediction18motionCompensationER10CodingUnitRK10RefPicListbb(self, cu, l, luma, chroma);
   if (!g_cap.active || g_cap.cs != cu.cs) { if (!g_cap.active) initPlanes(*cu.cs); }
+  setCtu(*cu.cs, cu.lumaPos().x, cu.lumaPos().y);
   PelUnitBuf pb = cu.cs->getPredBuf(cu);
   for (int c = 0; c < 3; c++) {
     if ((c == 0 && !luma) || (c > 0 && !chroma) || !cu.blocks[c].valid()) continue;
@@ -603,6 +660,7 @@ void __wrap__ZN15InterPrediction21motionCompensationGeoER10CodingUnitR8MergeCtx(
   }
   g_cap.geo[&cu] = g;
   __real__ZN15InterPrediction21motionCompensationGeoER10CodingUnitR8MergeCtx(self, cu, m);
+  setCtu(*cu.cs, cu.lumaPos().x, cu.lumaPos().y);
   PelUnitBuf pb = cu.cs->getPredBuf(cu);
   for (int c = 0; c < 3; c++) {
     if (!cu.blocks[c].valid()) continue;
@@ -616,12 +674,14 @@ void __real__ZN15IntraPrediction16geneWeightedPredE11ComponentIDR7AreaBufIsERK14
 void __wrap__ZN15IntraPrediction16geneWeightedPredE11ComponentIDR7AreaBufIsERK14PredictionUnitPs(IntraPrediction *self, ComponentID c, PelBuf &pred, const PredictionUnit &pu, Pel *src) {
   __real__ZN15IntraPrediction16geneWeightedPredE11ComponentIDR7AreaBufIsERK14PredictionUnitPs(self, c, pred, pu, src);
   if (!g_cap.active) return;
+  setCtu(*pu.cs, pu.lumaPos().x, pu.lumaPos().y);
   int x, y;
   if (locate(*pu.cs, PIC_PREDICTION, c, pred.buf, x, y)) copyBlock(g_cap.pfin[c], pred, x, y);
 }
 
 static void recordIntra(const PredictionUnit &pu, ComponentID c, const PelBuf &pred) {
   if (!g_cap.active) initPlanes(*pu.cs);
+  { const CompArea &a = pu.blocks[pu.chType]; setCtu(*pu.cs, a.x << (pu.chType ? 1 : 0), a.y << (pu.chType ? 1 : 0)); }
   int x, y;
   if (locate(*pu.cs, PIC_PREDICTION, c, pred.buf, x, y)) copyBlock(g_cap.pfin[c], pred, x, y);
 }
@@ -650,6 +710,7 @@ void __real__ZN7TrQuant15invTransformNxNER13TransformUnitRK11ComponentIDR7AreaBu
 void __wrap__ZN7TrQuant15invTransformNxNER13TransformUnitRK11ComponentIDR7AreaBufIsERK7QpParam(TrQuant *self, TransformUnit &tu, const ComponentID &c, PelBuf &resi, const QpParam &q) {
   __real__ZN7TrQuant15invTransformNxNER13TransformUnitRK11ComponentIDR7AreaBufIsERK7QpParam(self, tu, c, resi, q);
   if (!g_cap.active) initPlanes(*tu.cs);
+  { const CompArea &a = tu.blocks[c]; setCtu(*tu.cs, a.x << (c ? 1 : 0), a.y << (c ? 1 : 0)); }
   auto &e = g_cap.tuqp[&tu];
   static bool init = false; (void)init;
   e[c * 2] = q.Qps[0]; e[c * 2 + 1] = q.Qps[1];
@@ -662,6 +723,7 @@ void __real__ZN7TrQuant15invTransformICTERK13TransformUnitR7AreaBufIsES5_(TrQuan
 void __wrap__ZN7TrQuant15invTransformICTERK13TransformUnitR7AreaBufIsES5_(TrQuant *self, const TransformUnit &tu, PelBuf &cb, PelBuf &cr) {
   __real__ZN7TrQuant15invTransformICTERK13TransformUnitR7AreaBufIsES5_(self, tu, cb, cr);
   if (!g_cap.active) return;
+  { const CompArea &a = tu.blocks[1]; setCtu(*tu.cs, a.x << 1, a.y << 1); }
   int x, y;
   if (locate(*tu.cs, PIC_RESIDUAL, 1, cb.buf, x, y)) copyBlock(g_cap.resi[1], cb, x, y);
   if (locate(*tu.cs, PIC_RESIDUAL, 2, cr.buf, x, y)) copyBlock(g_cap.resi[2], cr, x, y);

@@ -1,0 +1,76 @@
+"""Loader for the C oracle (oracle/_build/liboracle.so) — the CPU checker. Tables are the reference's
+own constants (tests/golden/tables.cap, dumped from the running reference by oracle/capture)."""
+import ctypes as C
+import os
+
+import numpy as np
+
+from vvc_amd import capfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_lib = None
+_keep = []
+
+
+class OrTables(C.Structure):
+    _fields_ = [("dct2", C.c_void_p * 7), ("dst7", C.c_void_p * 6), ("dct8", C.c_void_p * 6),
+                ("lfnst8x8", C.c_void_p), ("lfnst4x4", C.c_void_p), ("lfnst_lut", C.c_void_p),
+                ("inv_quant_scales", C.c_void_p)]
+
+
+class OrPic(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("width", "height", "bit_depth", "dep_quant", "joint_cbcr_sign", "use_mts",
+                                       "implicit_mts", "mts_intra", "mts_inter", "lfnst_enabled", "dual_tree")]
+
+
+def tables():
+    return capfile.load(os.path.join(ROOT, "tests", "golden", "tables.cap"))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        from vvc_amd import build
+        path = build.build_oracle()
+        L = C.CDLL(path)
+        t = tables()
+        ot = OrTables()
+
+        def keep(a):
+            a = np.ascontiguousarray(a, np.int16)
+            _keep.append(a)
+            return a.ctypes.data
+
+        for l in range(1, 7):
+            ot.dct2[l] = keep(t["dct2_%d" % (1 << l)])
+        for l in range(2, 6):
+            ot.dst7[l] = keep(t["dst7_%d" % (1 << l)])
+            ot.dct8[l] = keep(t["dct8_%d" % (1 << l)])
+        ot.lfnst8x8 = keep(t["lfnst8x8"])
+        ot.lfnst4x4 = keep(t["lfnst4x4"])
+        ot.lfnst_lut = keep(t["lfnst_lut"])
+        ot.inv_quant_scales = keep(t["inv_quant_scales"])
+        _keep.append(ot)
+        L.or_set_tables(C.byref(ot))
+        _lib = L
+    return _lib
+
+
+def pic_struct(p):
+    h = p["hdr"]
+    return OrPic(h["width"], h["height"], h["bitdepth_y"], h["dep_quant"], h.get("joint_cbcr_sign", 0), h.get("use_mts", 1),
+                 h.get("implicit_mts", 0), h["mts_intra"], h["mts_inter"], h["lfnst_enabled"], h["dual_tree"])
+
+
+def residual_picture(p):
+    L = lib()
+    h = p["hdr"]
+    W, H = h["width"], h["height"]
+    planes = [np.zeros((H, W), np.int16), np.zeros((H // 2, W // 2), np.int16), np.zeros((H // 2, W // 2), np.int16)]
+    cu, pu, tu, coef = (np.ascontiguousarray(p[k], np.int32) for k in ("cu", "pu", "tu", "coef"))
+    ps = pic_struct(p)
+    P = C.c_void_p
+    r = L.or_residual_picture(C.byref(ps), P(cu.ctypes.data), len(cu), P(pu.ctypes.data), len(pu), P(tu.ctypes.data), len(tu),
+                              P(coef.ctypes.data), C.c_int64(coef.size), *(P(x.ctypes.data) for x in planes))
+    assert r == 0, r
+    return planes

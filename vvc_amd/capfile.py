@@ -40,8 +40,9 @@ def parse(buf: bytes) -> dict:
         p += 8
         out[name] = np.frombuffer(buf, _DT[int(dt)], nb // np.dtype(_DT[int(dt)]).itemsize, p).reshape(dims).copy()
         off = p + nb
-    keys = bytes(out.pop("hdr_keys")).decode().split(",")
-    out["hdr"] = dict(zip(keys, (int(v) for v in out.pop("hdr_vals"))))
+    if "hdr_keys" in out:
+        keys = bytes(out.pop("hdr_keys")).decode().split(",")
+        out["hdr"] = dict(zip(keys, (int(v) for v in out.pop("hdr_vals"))))
     return out
 
 
