@@ -124,6 +124,7 @@ typedef struct vvcr_pic_params {
   int16_t lmcs_fwd[1024], lmcs_inv[1024], lmcs_pivot[17];
   int32_t lmcs_cadj[16];
   int32_t max_tb_log2, log2_max_ts;
+  int32_t use_mts, implicit_mts, joint_cbcr_sign;
 } vvcr_pic_params;
 
 /* ALF / CC-ALF filters of the picture (AdaptiveLoopFilter::reconstructCoeffAPSs result,

@@ -54,6 +54,10 @@ struct vvcr_ctx {
   PictureDescriptors desc;          // host copy of the submitted descriptors (vvcr_host.h)
   WorkLists wl;                     // host-built work lists
   DevVec<McJob> d_mc_basic;
+  DevVec<TbJob> d_tb;
+  DevVec<int32_t> d_coef;
+  DevVec<uint16_t> d_scans;
+  ScanTables scans;
   hipEvent_t ev[8] = {};
   float stage_ms[8] = {};
 };
@@ -93,6 +97,8 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       ctx->tmp[c] = alloc_plane(w, h);
     }
     for (auto &e : ctx->ev) VVCR_CHECK_HIP(hipEventCreate(&e));
+    build_scan_tables(ctx->scans);
+    ctx->d_scans.upload(ctx->scans.data, ctx->stream);
   } catch (const VvcrError &e) {
     g_create_error = e.msg;
     return e.code;
@@ -179,6 +185,19 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
   build_work_lists(ctx->sp, ctx->pp, ctx->desc, ctx->wl);
   hipStream_t s = ctx->stream;
   VVCR_CHECK_HIP(hipEventRecord(ctx->ev[0], s));
+  if (mask & VVCR_STAGE_RESID) {
+    for (int c = 0; c < 3; c++)
+      VVCR_CHECK_HIP(hipMemsetAsync(ctx->resi[c].p, 0, (size_t)ctx->resi[c].stride * ctx->resi[c].h * 2, s));
+    ctx->d_coef.upload(ctx->desc.coef, s);
+    ctx->d_tb.upload(ctx->wl.tb, s);
+    TbParams tp{};
+    for (int c = 0; c < 3; c++) tp.out[c] = ctx->resi[c];
+    tp.bd = ctx->sp.bit_depth;
+    memcpy(tp.scan_off, ctx->scans.off, sizeof(tp.scan_off));
+    memcpy(tp.lfnst_scan_off, ctx->scans.lfnst_off, sizeof(tp.lfnst_scan_off));
+    launch_resid(tp, ctx->d_tb.p, (int)ctx->wl.tb.size(), ctx->d_coef.p, ctx->d_scans.p, s);
+    VVCR_CHECK_HIP(hipGetLastError());
+  }
   if (mask & VVCR_STAGE_INTER) {
     ctx->d_mc_basic.upload(ctx->wl.mc_basic, s);
     launch_mc_basic(make_mc_params(ctx), ctx->d_mc_basic.p, (int)ctx->wl.mc_basic.size(), s);

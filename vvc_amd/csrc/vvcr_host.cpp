@@ -3,6 +3,8 @@
 // (InterPrediction.cpp:1517-1660) so that every PU reaches the kernel that reproduces its prediction.
 #include "vvcr_host.h"
 #include <string>
+#include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -81,8 +83,11 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
   if (!d.motion.empty() && d.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4)) fail("motion field size");
 }
 
+void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, std::vector<TbJob> &out);
+
 void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl) {
   wl.clear();
+  build_tb_jobs(sp, pp, d, wl.tb);
   const int W4 = sp.width / 4;
   for (const vvcr_cu &c : d.cu) {
     if (c.predmode != MODE_INTER || !c.yvalid) continue;
@@ -104,6 +109,189 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       if (p.dmvr || p.bdof) { wl.n_unsupported_inter++; continue; }
       McJob j = make_job(pp, p.interdir, p.ref0, p.ref1, p.mv0x, p.mv0y, p.mv1x, p.mv1y, bcw, alt);
       push_tiles(wl.mc_basic, p.x, p.y, p.w, p.h, j);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// scans
+// ------------------------------------------------------------------------------------------------
+namespace {
+// g_log2SbbSize (Rom.cpp:252)
+const uint8_t kSbb[8][8][2] = {
+  { {0,0},{0,1},{0,2},{0,3},{0,4},{0,4},{0,4},{0,4} },
+  { {1,0},{1,1},{1,1},{1,3},{1,3},{1,3},{1,3},{1,3} },
+  { {2,0},{1,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
+  { {3,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
+  { {4,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
+  { {4,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
+  { {4,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
+  { {4,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} } };
+
+void diag(int bw, int bh, std::vector<int> &xs, std::vector<int> &ys) {
+  xs.resize(bw * bh); ys.resize(bw * bh);
+  int line = 0, col = 0;
+  for (int i = 0; i < bw * bh; i++) {
+    xs[i] = col; ys[i] = line;
+    if (col == bw - 1 || line == 0) {
+      line += col + 1; col = 0;
+      if (line >= bh) { col += line - (bh - 1); line = bh - 1; }
+    } else { col++; line--; }
+  }
+}
+int ilog2(int v) { int r = 0; while ((1 << (r + 1)) <= v) r++; return r; }
+}  // namespace
+
+void build_scan_tables(ScanTables &st) {
+  st.data.clear();
+  std::vector<int> gx, gy, cx, cy;
+  for (int lw = 0; lw < 7; lw++)
+    for (int lh = 0; lh < 7; lh++) {
+      const int w = 1 << lw, h = 1 << lh;
+      const int gw = 1 << kSbb[lw][lh][0], gh = 1 << kSbb[lw][lh][1];
+      const int wg = std::min(w, 32) / gw, hg = std::min(h, 32) / gh;
+      st.off[lw][lh] = (int32_t)st.data.size();
+      diag(wg, hg, gx, gy);
+      diag(gw, gh, cx, cy);
+      for (size_t g = 0; g < gx.size(); g++)
+        for (size_t c = 0; c < cx.size(); c++) st.data.push_back((uint16_t)((gy[g] * gh + cy[c]) * w + gx[g] * gw + cx[c]));
+    }
+  diag(2, 2, gx, gy);
+  diag(4, 4, cx, cy);
+  for (int lw = 0; lw < 7; lw++) {
+    st.lfnst_off[lw] = (int32_t)st.data.size();
+    const int w = 1 << lw;
+    for (int g = 0; g < 4; g++)
+      for (int e = 0; e < 16; e++) st.data.push_back((uint16_t)((gy[g] * 4 + cy[e]) * w + gx[g] * 4 + cx[e]));
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// transform blocks: the decisions of TrQuant::invTransformNxN's callers (DecCu.cpp:161-265, 775-850)
+// ------------------------------------------------------------------------------------------------
+namespace {
+constexpr int NUM_LUMA_MODE = 67, NUM_EXT_LUMA_MODE = 28, VDIA_IDX = 66, DIA_IDX = 34;
+
+int wide_angle(int mode, int w, int h) {        // PU::getWideAngIntraMode (UnitTools.cpp:651)
+  if (mode < 2) return mode;
+  static const int modeShift[] = {0, 6, 10, 12, 14, 15};
+  const int d = std::abs(ilog2(w) - ilog2(h));
+  int m = mode;
+  if (w > h && mode < 2 + modeShift[d]) m += VDIA_IDX - 1;
+  else if (h > w && m > VDIA_IDX - modeShift[d]) m -= VDIA_IDX + 1;
+  return m;
+}
+int lfnst_mode_of(int wam) {                    // TrQuant::getLFNSTIntraMode (TrQuant.cpp:283)
+  if (wam < 0) return wam + (NUM_EXT_LUMA_MODE >> 1) + NUM_LUMA_MODE;
+  if (wam >= NUM_LUMA_MODE) return wam + (NUM_EXT_LUMA_MODE >> 1);
+  return wam;
+}
+bool lfnst_transpose(int m) {                   // TrQuant::getTransposeFlag (TrQuant.cpp:300)
+  return (m >= NUM_LUMA_MODE && m >= NUM_LUMA_MODE + (NUM_EXT_LUMA_MODE >> 1)) || (m < NUM_LUMA_MODE && m > DIA_IDX);
+}
+// TrQuant::getTrTypes (TrQuant.cpp:668)
+void tr_types(const vvcr_pic_params &pp, const vvcr_cu &cu, int comp, int w, int h, int mts, int tuLumaW, int tuLumaH, int &trh, int &trv) {
+  const bool isIntra = cu.predmode == 1, isInter = cu.predmode == 0, luma = comp == 0;
+  const bool explicitMTS = (isIntra ? pp.mts_intra : (pp.mts_inter && isInter)) && luma;
+  const bool implicitMTS = isIntra && pp.implicit_mts && luma && cu.lfnst == 0 && cu.mip == 0;
+  const bool isISP = isIntra && cu.isp && luma;
+  const bool isSBT = isInter && cu.sbtinfo && luma;
+  trh = trv = TR_DCT2;
+  if (isISP && cu.lfnst) return;
+  if (!pp.use_mts) return;
+  if (implicitMTS || isISP) {
+    if (w >= 4 && w <= 16) trh = TR_DST7;
+    if (h >= 4 && h <= 16) trv = TR_DST7;
+    return;
+  }
+  if (isSBT) {
+    const int idx = cu.sbtinfo & 0xf, pos = (cu.sbtinfo >> 4) & 3;
+    if (idx == 1 || idx == 3) {
+      if (tuLumaH > 32) return;
+      if (pos == 0) { trh = TR_DCT8; trv = TR_DST7; } else { trh = TR_DST7; trv = TR_DST7; }
+    } else {
+      if (tuLumaW > 32) return;
+      if (pos == 0) { trh = TR_DST7; trv = TR_DCT8; } else { trh = TR_DST7; trv = TR_DST7; }
+    }
+    return;
+  }
+  if (explicitMTS && mts > 1) {
+    trh = ((mts - 2) & 1) ? TR_DCT8 : TR_DST7;
+    trv = ((mts - 2) >> 1) ? TR_DCT8 : TR_DST7;
+  }
+}
+}  // namespace
+
+void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, std::vector<TbJob> &out) {
+  out.clear();
+  const int W4 = sp.width / 4, H4 = sp.height / 4;
+  std::vector<int> lmap;   // luma PU per 4x4, for co-located luma modes (PU::getCoLocatedIntraLumaMode)
+  bool haveMap = false;
+  static const int kIct[2][4] = {{0, 3, 1, 2}, {0, -3, -1, -2}};
+  for (const vvcr_tu &t : d.tu) {
+    const vvcr_cu &cu = d.cu[t.cu];
+    const bool sepTree = cu.treetype != 0 || pp.dual_tree;
+    for (int comp = 0; comp < 3; comp++) {
+      const int32_t *b = t.b[comp];
+      if (b[2] <= 0) continue;
+      if (comp == 2 && t.jccr) continue;
+      int src = comp;
+      if (comp == 1 && t.jccr) src = (t.jccr >> 1) ? 1 : 2;
+      const int32_t *bs = t.b[src];
+      const bool coded = (comp == 1 && t.jccr) ? true : b[4] != 0;
+      if (!coded || bs[6] < 0) continue;      // residual planes are cleared per picture
+      const int w = bs[2], h = bs[3];
+      TbJob j{};
+      j.x = (int16_t)bs[0]; j.y = (int16_t)bs[1]; j.w = (uint8_t)w; j.h = (uint8_t)h;
+      j.comp = (uint8_t)src;
+      const bool ts = bs[5] == 1;
+      j.qp = (uint8_t)(ts ? bs[8] : bs[7]);
+      j.coef = bs[6];
+      int trh, trv;
+      tr_types(pp, cu, src, w, h, bs[5], t.b[0][2], t.b[0][3], trh, trv);
+      j.trh = (uint8_t)trh; j.trv = (uint8_t)trv;
+      if (ts) j.flags |= TB_TS;
+      if (pp.dep_quant && !ts) j.flags |= TB_DQ;
+      const int bdpcm = src == 0 ? cu.bdpcm : cu.bdpcmc;
+      j.flags |= (uint8_t)((bdpcm & 3) << TB_BDPCM_SHIFT);
+      int skipW = (trh != TR_DCT2 && w == 32) ? 16 : (w > 32 ? w - 32 : 0);
+      int skipH = (trv != TR_DCT2 && h == 32) ? 16 : (h > 32 ? h - 32 : 0);
+      if (pp.lfnst_enabled && cu.lfnst) {
+        if ((w == 4 && h > 4) || (w > 4 && h == 4)) { skipW = w - 4; skipH = h - 4; }
+        else if (w >= 8 && h >= 8) { skipW = w - 8; skipH = h - 8; }
+        if (!ts && (sepTree || src == 0) && cu.lfnst < 3) {
+          const vvcr_pu &p = d.pu[cu.firstpu];
+          int mode = src == 0 ? p.fidir_l : p.fidir_c;
+          if (src > 0 && p.idir_c >= 67 && p.idir_c <= 69) {
+            if (!haveMap) {
+              lmap.assign((size_t)W4 * H4, -1);
+              for (size_t i = 0; i < d.pu.size(); i++) {
+                const vvcr_pu &q = d.pu[i];
+                if (q.w <= 0 || q.chtype != 0) continue;
+                for (int y = q.y >> 2; y < (q.y + q.h) >> 2 && y < H4; y++)
+                  for (int x = q.x >> 2; x < (q.x + q.w) >> 2 && x < W4; x++) lmap[(size_t)y * W4 + x] = (int)i;
+              }
+              haveMap = true;
+            }
+            const int lx = cu.cx * 2, ly = cu.cy * 2, lww = cu.cw * 2, lhh = cu.ch * 2;
+            const int rx = sepTree ? lx + (lww >> 1) : lx, ry = sepTree ? ly + (lhh >> 1) : ly;
+            const int li = lmap[(size_t)(ry >> 2) * W4 + (rx >> 2)];
+            if (li < 0) throw VvcrError(VVCR_E_ARG, "no co-located luma PU for CCLM chroma TU");
+            const vvcr_pu &lp = d.pu[li];
+            mode = d.cu[lp.cu].mip ? 0 : lp.idir_l;
+          }
+          if (src == 0 && cu.mip) mode = 0;
+          const int m = lfnst_mode_of(wide_angle(mode, w, h));
+          if (m < 0 || m >= 95) throw VvcrError(VVCR_E_ARG, "LFNST mode out of range");
+          j.lfnst_idx = (uint8_t)cu.lfnst;
+          j.lfnst_mode = (uint8_t)m;   // intra mode; the kernel maps it through g_lfnstLut
+          j.flags |= TB_LFNST_APPLY;
+          if (lfnst_transpose(m)) j.flags |= TB_LFNST_TRANSPOSE;
+        }
+      }
+      j.skip_w = (uint8_t)skipW; j.skip_h = (uint8_t)skipH;
+      if (comp == 1 && t.jccr) j.ict = (int8_t)kIct[pp.joint_cbcr_sign ? 1 : 0][t.jccr];
+      out.push_back(j);
     }
   }
 }

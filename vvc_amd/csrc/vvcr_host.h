@@ -15,9 +15,19 @@ struct PictureDescriptors {
 
 struct WorkLists {
   std::vector<McJob> mc_basic;     // plain uni/bi/BCW blocks (incl. SbTMVP sub-blocks, CIIP inter part)
+  std::vector<TbJob> tb;           // coded transform blocks
   int n_unsupported_inter = 0;     // PUs needing kernels not built yet (reported, never silently skipped)
-  void clear() { mc_basic.clear(); n_unsupported_inter = 0; }
+  void clear() { mc_basic.clear(); tb.clear(); n_unsupported_inter = 0; }
 };
+
+// Grouped diagonal scans (Rom.cpp:321-370) and the LFNST top-left 8x8 scan (Rom.cpp:385-403) as
+// raster indices, for every power-of-two block size; uploaded once per context.
+struct ScanTables {
+  std::vector<uint16_t> data;
+  int32_t off[7][7];
+  int32_t lfnst_off[7];
+};
+void build_scan_tables(ScanTables &st);
 
 // Throws VvcrError on inconsistent descriptors (indices out of range, blocks outside the picture).
 void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d);

@@ -61,5 +61,37 @@ struct McParams {
   int32_t bd;            // bit depth
 };
 
-// launchers (vvcr_mc.hip)
+// ------------------------------------------------------------------------------------------------
+// Residual work item: one transform block (after joint Cb-Cr resolution). 32 bytes.
+// ------------------------------------------------------------------------------------------------
+enum { TR_DCT2 = 0, TR_DST7 = 1, TR_DCT8 = 2 };
+enum : uint8_t {
+  TB_TS = 1 << 0,              // transform skip (mtsIdx == MTS_SKIP)
+  TB_DQ = 1 << 1,              // dependent quantisation (picture header flag, non-TS)
+  TB_LFNST_APPLY = 1 << 2,     // inverse LFNST on this component
+  TB_LFNST_TRANSPOSE = 1 << 3,
+  TB_BDPCM_SHIFT = 4,          // bits 4..5: 0 off, 1 horizontal, 2 vertical
+};
+struct TbJob {
+  int16_t x, y;                // component-plane position
+  uint8_t w, h;                // 1..64
+  uint8_t comp, flags;
+  uint8_t trh, trv, lfnst_idx, lfnst_mode;
+  int8_t ict;                  // joint Cb-Cr mode producing the other chroma plane (TrQuant.cpp:141), 0 = none
+  uint8_t qp;                  // QpParam::Qp(ts)
+  uint8_t skip_w, skip_h;      // zero-out lines of xIT (TrQuant.cpp:841-852)
+  int32_t coef;                // level offset in the coefficient pool
+  int32_t pad[3];
+};
+static_assert(sizeof(TbJob) == 32, "TbJob layout");
+
+struct TbParams {
+  DPlane out[3];               // residual planes
+  int32_t bd;
+  int32_t scan_off[7][7];      // grouped diagonal scan (raster index per scan position) by log2 w / h
+  int32_t lfnst_scan_off[7];   // top-left 8x8 LFNST scan by log2 width
+};
+
+// launchers (vvcr_mc.hip, vvcr_resid.hip)
+void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, const int32_t *coef, const uint16_t *scans, hipStream_t s);
 void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);

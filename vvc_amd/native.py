@@ -40,6 +40,7 @@ class PicParams(C.Structure):
         ("lmcs_fwd", C.c_int16 * 1024), ("lmcs_inv", C.c_int16 * 1024), ("lmcs_pivot", C.c_int16 * 17),
         ("lmcs_cadj", I32 * 16),
         ("max_tb_log2", I32), ("log2_max_ts", I32),
+        ("use_mts", I32), ("implicit_mts", I32), ("joint_cbcr_sign", I32),
     ]
 
 

@@ -74,6 +74,7 @@ def pic_params(p, slot, slot_of):
               "alf_vb_chroma", "lmcs_chroma_scale", "lmcs_min_bin", "lmcs_max_bin", "log2_max_ts"):
         setattr(pp, k, h[k])
     pp.lmcs_enabled = h["lmcs_enabled"] and h["lmcs_slice_flag"]
+    pp.use_mts, pp.implicit_mts, pp.joint_cbcr_sign = h["use_mts"], h["implicit_mts"], h["joint_cbcr_sign"]
     pp.max_tb_log2 = int(h["max_tb_size"]).bit_length() - 1
     pp.chroma_qp_off[1], pp.chroma_qp_off[2] = h["chroma_qp_off_cb"], h["chroma_qp_off_cr"]
     wp = np.ascontiguousarray(p["wp"], np.int32)
