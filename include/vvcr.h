@@ -98,9 +98,12 @@ typedef struct vvcr_geo {
   int32_t cand[2][6];          /* inter_dir, list, ref_idx, mvx, mvy, alt_hpel */
 } vvcr_geo;
 
-/* SAO per CTB and component (SAOOffset, TypeDef.h:938), merge already resolved. */
+/* SAO per CTB and component (SAOOffset, TypeDef.h:938) after SampleAdaptiveOffset::
+ * reconstructBlkSAOParam (SampleAdaptiveOffset.cpp:231): merges resolved, offsets de-quantised.
+ * mode: 0 off / 1 new / 2 merge(resolved); type: 0..3 EO_0/90/135/45, 4 BO; offset[32] indexed by
+ * band (BO) or edge class 0..4 (EO). */
 typedef struct vvcr_sao {
-  int32_t mode, type, band, offset[4];
+  int32_t mode, type, band, offset[32];
 } vvcr_sao;
 
 /* Picture-level parameters (slice / picture header subset). */

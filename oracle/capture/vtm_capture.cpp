@@ -465,16 +465,16 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
 
 static void dumpSao(CapFile &F, const CodingStructure &cs) {
   const int n = cs.pcv->sizeInCtus;
-  std::vector<int32_t> s((size_t)n * 3 * 7, 0);
+  std::vector<int32_t> s((size_t)n * 3 * 35, 0);
   SAOBlkParam *p = cs.picture->getSAO();
   for (int i = 0; i < n; i++)
     for (int c = 0; c < 3; c++) {
       const SAOOffset &o = p[i][c];
-      int32_t *d = &s[((size_t)i * 3 + c) * 7];
+      int32_t *d = &s[((size_t)i * 3 + c) * 35];
       d[0] = o.modeIdc; d[1] = o.typeIdc; d[2] = o.typeAuxInfo;
-      for (int k = 0; k < 4; k++) d[3 + k] = o.offset[k];
+      for (int k = 0; k < 32; k++) d[3 + k] = o.offset[k];
     }
-  F.i32("sao", s, {(uint64_t)n, 3, 7});
+  F.i32("sao", s, {(uint64_t)n, 3, 35});
 }
 
 static void dumpAlf(CapFile &F, DecLib &dec, const CodingStructure &cs) {

@@ -74,3 +74,45 @@ def residual_picture(p):
                               P(coef.ctypes.data), C.c_int64(coef.size), *(P(x.ctypes.data) for x in planes))
     assert r == 0, r
     return planes
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+def alf_luma_sets(p):
+    """luma filter sets of the picture: 16 fixed sets then the slice's APS sets (reconstructCoeffAPSs)."""
+    n = len(p["alf_aps_ids"])
+    coef = np.concatenate([p["alf_fixed"], p["alf_coef_aps"][:n]]).astype(np.int16)
+    clip = np.concatenate([np.broadcast_to(p["alf_clip_default"], p["alf_fixed"].shape), p["alf_clip_aps"][:n]]).astype(np.int16)
+    return np.ascontiguousarray(coef), np.ascontiguousarray(clip)
+
+
+def sao_picture(p, planes):
+    L = lib()
+    h = p["hdr"]
+    out = [np.empty_like(x) for x in planes]
+    src = [np.ascontiguousarray(x, np.int16) for x in planes]
+    sao = np.ascontiguousarray(p["sao"], np.int32)
+    L.or_sao_picture(h["width"], h["height"], h["bitdepth_y"], h["ctu_log2"], _p(sao), *(_p(x) for x in src), *(_p(x) for x in out))
+    return out
+
+
+def alf_picture(p, planes):
+    L = lib()
+    h = p["hdr"]
+    out = [np.empty_like(x) for x in planes]
+    src = [np.ascontiguousarray(x, np.int16) for x in planes]
+    coef, clip = alf_luma_sets(p)
+    cc = np.ascontiguousarray(p["alf_chroma_coef"], np.int16)
+    ccl = np.ascontiguousarray(p["alf_chroma_clip"], np.int16)
+    ccf = np.ascontiguousarray(p["ccalf_coef"], np.int16)
+    en = np.array([h["alf_slice_en0"], h["alf_slice_en1"], h["alf_slice_en2"], h["ccalf_en_cb"], h["ccalf_en_cr"]], np.int32)
+    cte = np.ascontiguousarray(p["alf_ctb_en"], np.uint8)
+    cta = np.ascontiguousarray(p["alf_ctb_alt"], np.uint8)
+    cts = np.ascontiguousarray(p["alf_ctb_fidx"], np.int16)
+    ccc = np.ascontiguousarray(p["ccalf_ctl"], np.uint8)
+    L.or_alf_picture(h["width"], h["height"], h["bitdepth_y"], h["ctu_log2"], h["alf_vb_luma"], h["alf_vb_chroma"],
+                     _p(coef), _p(clip), _p(cc), _p(ccl), _p(ccf), _p(en), _p(cte), _p(cta), _p(cts), _p(ccc),
+                     *(_p(x) for x in src), *(_p(x) for x in out))
+    return out
