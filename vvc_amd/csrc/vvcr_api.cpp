@@ -58,6 +58,12 @@ struct vvcr_ctx {
   DevVec<int32_t> d_coef;
   DevVec<uint16_t> d_scans;
   ScanTables scans;
+  // loop-filter parameters of the current picture
+  DevVec<int32_t> d_sao;
+  DevVec<int16_t> d_alf_luma_coef, d_alf_luma_clip, d_alf_chroma, d_alf_cc;
+  DevVec<uint8_t> d_alf_ctb;      // ctb_en[3n] | ctb_alt[3n] | cc_ctl[2n]
+  DevVec<int16_t> d_alf_set;
+  bool have_sao = false, have_alf = false;
   hipEvent_t ev[8] = {};
   float stage_ms[8] = {};
 };
@@ -159,10 +165,42 @@ int vvcr_submit(vvcr_ctx *ctx, const vvcr_cu *cu, int32_t ncu, const vvcr_pu *pu
   API_END
 }
 
+static int n_ctb(const vvcr_seq_params &sp) {
+  const int ctu = 1 << sp.ctu_log2;
+  return ((sp.width + ctu - 1) / ctu) * ((sp.height + ctu - 1) / ctu);
+}
+
 int vvcr_set_loop_filter_params(vvcr_ctx *ctx, const vvcr_sao *sao, const vvcr_alf *alf) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
-  (void)sao; (void)alf;
+  if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_set_loop_filter_params outside begin/end picture");
+  const int n = n_ctb(ctx->sp);
+  hipStream_t s = ctx->stream;
+  ctx->have_sao = sao != nullptr;
+  if (sao) {
+    std::vector<int32_t> v((const int32_t *)sao, (const int32_t *)sao + (size_t)n * 3 * 35);
+    ctx->d_sao.upload(v, s);
+  }
+  ctx->have_alf = alf != nullptr;
+  if (alf) {
+    if (alf->num_luma_sets < 16 || alf->num_luma_sets > 24) throw VvcrError(VVCR_E_ARG, "bad ALF luma set count");
+    const size_t L = (size_t)alf->num_luma_sets * 25 * 13;
+    ctx->d_alf_luma_coef.upload(std::vector<int16_t>(alf->luma_coef, alf->luma_coef + L), s);
+    ctx->d_alf_luma_clip.upload(std::vector<int16_t>(alf->luma_clip, alf->luma_clip + L), s);
+    std::vector<int16_t> ch(alf->chroma_coef, alf->chroma_coef + 56);
+    ch.insert(ch.end(), alf->chroma_clip, alf->chroma_clip + 56);
+    ctx->d_alf_chroma.upload(ch, s);
+    ctx->d_alf_cc.upload(std::vector<int16_t>(alf->cc_coef, alf->cc_coef + 64), s);
+    std::vector<uint8_t> ctb(alf->ctb_en, alf->ctb_en + 3 * n);
+    ctb.insert(ctb.end(), alf->ctb_alt, alf->ctb_alt + 3 * n);
+    ctb.insert(ctb.end(), alf->cc_ctl, alf->cc_ctl + 2 * n);
+    for (int i = 0; i < 3 * n; i++) if (ctb[3 * n + i] > 7) throw VvcrError(VVCR_E_ARG, "bad ALF chroma alternative");
+    for (int i = 0; i < 2 * n; i++) if (ctb[6 * n + i] > 4) throw VvcrError(VVCR_E_ARG, "bad CC-ALF filter index");
+    std::vector<int16_t> set(alf->ctb_filter_set, alf->ctb_filter_set + n);
+    for (int v : set) if (v < 0 || v >= alf->num_luma_sets) throw VvcrError(VVCR_E_ARG, "bad ALF filter set index");
+    ctx->d_alf_ctb.upload(ctb, s);
+    ctx->d_alf_set.upload(set, s);
+  }
   return VVCR_OK;
   API_END
 }
@@ -202,6 +240,42 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
     ctx->d_mc_basic.upload(ctx->wl.mc_basic, s);
     launch_mc_basic(make_mc_params(ctx), ctx->d_mc_basic.p, (int)ctx->wl.mc_basic.size(), s);
     VVCR_CHECK_HIP(hipGetLastError());
+  }
+  // ---- SAO (DBK picture in the slot -> tmp) and ALF (-> slot)
+  {
+    const vvcr_pic_params &pp = ctx->pp;
+    auto &A = ctx->dpb[pp.slot];
+    const int ctu = 1 << ctx->sp.ctu_log2;
+    const int wc = (ctx->sp.width + ctu - 1) / ctu, n = n_ctb(ctx->sp);
+    bool inTmp = false;
+    if ((mask & VVCR_STAGE_SAO) && ctx->have_sao && (pp.sao_luma || pp.sao_chroma)) {
+      SaoParams sp{};
+      for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ctx->tmp[c]; }
+      sp.sao = ctx->d_sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
+      launch_sao(sp, s);
+      VVCR_CHECK_HIP(hipGetLastError());
+      inTmp = true;
+    }
+    const bool alfOn = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
+    if ((mask & VVCR_STAGE_ALF) && ctx->have_alf && alfOn) {
+      AlfParams ap{};
+      for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ctx->tmp[c] : A[c]; ap.dst[c] = inTmp ? A[c] : ctx->tmp[c]; }
+      ap.bd = ctx->sp.bit_depth; ap.ctu_log2 = ctx->sp.ctu_log2; ap.wc = wc; ap.nctb = n;
+      ap.vb_luma = pp.alf_vb_luma; ap.vb_chroma = pp.alf_vb_chroma;
+      for (int c = 0; c < 3; c++) ap.en[c] = pp.alf_en[c];
+      ap.en[3] = pp.ccalf_en[0]; ap.en[4] = pp.ccalf_en[1];
+      ap.luma_coef = ctx->d_alf_luma_coef.p; ap.luma_clip = ctx->d_alf_luma_clip.p;
+      ap.chroma_coef = ctx->d_alf_chroma.p; ap.chroma_clip = ctx->d_alf_chroma.p + 56; ap.cc_coef = ctx->d_alf_cc.p;
+      ap.ctb_en = ctx->d_alf_ctb.p; ap.ctb_alt = ctx->d_alf_ctb.p + 3 * n; ap.cc_ctl = ctx->d_alf_ctb.p + 6 * n;
+      ap.ctb_set = ctx->d_alf_set.p;
+      launch_alf(ap, s);
+      VVCR_CHECK_HIP(hipGetLastError());
+      inTmp = !inTmp;
+    }
+    if (inTmp)
+      for (int c = 0; c < 3; c++)
+        VVCR_CHECK_HIP(hipMemcpy2DAsync(A[c].p, A[c].stride * 2, ctx->tmp[c].p, ctx->tmp[c].stride * 2, A[c].w * 2, A[c].h,
+                                        hipMemcpyDeviceToDevice, s));
   }
   VVCR_CHECK_HIP(hipEventRecord(ctx->ev[1], s));
   ctx->in_picture = false;

@@ -92,6 +92,25 @@ struct TbParams {
   int32_t lfnst_scan_off[7];   // top-left 8x8 LFNST scan by log2 width
 };
 
-// launchers (vvcr_mc.hip, vvcr_resid.hip)
+struct SaoParams {
+  DPlane src[3], dst[3];
+  const int32_t *sao;          // [nctb][3][35] vvcr_sao rows
+  int32_t bd, ctu, wc;
+};
+
+struct AlfParams {
+  DPlane src[3], dst[3];
+  int32_t bd, ctu_log2, wc, nctb, vb_luma, vb_chroma;
+  int32_t en[5];               // alf Y, Cb, Cr, cc-alf Cb, Cr
+  const int16_t *luma_coef, *luma_clip;     // [nsets][25][13]
+  const int16_t *chroma_coef, *chroma_clip; // [8][7]
+  const int16_t *cc_coef;                   // [2][4][8]
+  const uint8_t *ctb_en, *ctb_alt, *cc_ctl;
+  const int16_t *ctb_set;
+};
+
+// launchers (vvcr_mc.hip, vvcr_resid.hip, vvcr_lf.hip)
+void launch_sao(const SaoParams &p, hipStream_t s);
+void launch_alf(const AlfParams &p, hipStream_t s);
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, const int32_t *coef, const uint16_t *scans, hipStream_t s);
 void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);

@@ -1,0 +1,239 @@
+// vvcr_lf.hip — in-loop filters for gfx950: SAO and ALF / CC-ALF (deblocking: vvcr_dbk.hip).
+//
+// SAO (SampleAdaptiveOffset::offsetBlock, SampleAdaptiveOffset.cpp:293): one lane per 4 horizontally
+// adjacent samples of one component; every sample of the picture is written (copy where SAO is off),
+// reading the deblocked picture and writing the SAO picture (ping-pong, so neighbours are pre-SAO).
+//
+// ALF (AdaptiveLoopFilter::deriveClassificationBlk :873, filterBlk<7x7/5x5> :1085, filterBlkCcAlf :1328):
+// luma: one lane per 4x4 block = one classification + 16 filtered samples (the 8x8 Laplacian window
+// and the 7x7 diamond footprint overlap, so one lane reads a 10x10 / 10x10 neighbourhood through L1);
+// chroma: one lane per chroma sample, 5x5 diamond and the CC-ALF luma->chroma correction fused.
+// Reads the SAO picture, writes the final picture. Coordinates are clamped to the picture
+// (equivalent to PelUnitBuf::extendBorderPel(3) on the ALF input, AdaptiveLoopFilter.cpp:411).
+#include "vvcr_internal.h"
+
+namespace {
+
+__device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
+
+__global__ void k_sao(SaoParams P, int comp) {
+  const DPlane &S = P.src[comp];
+  const DPlane &D = P.dst[comp];
+  const int W = S.w, H = S.h;
+  const int qx = blockIdx.x * blockDim.x + threadIdx.x;     // quad index
+  const int y = blockIdx.y;
+  const int x0 = qx * 4;
+  if (x0 >= W || y >= H) return;
+  const int cs = comp ? P.ctu >> 1 : P.ctu;
+  const int ctbRow = y / cs;
+  const int maxv = (1 << P.bd) - 1;
+  const int16_t *row = S.p + (size_t)y * S.stride;
+  int16_t *out = D.p + (size_t)y * D.stride;
+  for (int k = 0; k < 4; k++) {
+    const int x = x0 + k;
+    if (x >= W) break;
+    const int s = row[x];
+    const int ctb = ctbRow * P.wc + x / cs;
+    const int32_t *prm = P.sao + ((size_t)ctb * 3 + comp) * 35;
+    int v = s;
+    if (prm[0] != 0) {
+      const int type = prm[1];
+      if (type == 4) {
+        v = clip3(0, maxv, s + prm[3 + (s >> (P.bd - 5))]);
+      } else {
+        // neighbours per EO class: 0 horizontal, 1 vertical, 2 135 degrees, 3 45 degrees
+        const int ax = x + (type == 1 ? 0 : (type == 3 ? 1 : -1)), ay = y + (type == 0 ? 0 : -1);
+        const int bx = x + (type == 1 ? 0 : (type == 3 ? -1 : 1)), by = y + (type == 0 ? 0 : 1);
+        if (ax >= 0 && ay >= 0 && ax < W && ay < H && bx >= 0 && by >= 0 && bx < W && by < H) {
+          const int a = S.p[(size_t)ay * S.stride + ax], b = S.p[(size_t)by * S.stride + bx];
+          v = clip3(0, maxv, s + prm[3 + 2 + sgn(s - a) + sgn(s - b)]);
+        }
+      }
+    }
+    out[x] = (int16_t)v;
+  }
+}
+
+__device__ __forceinline__ int at(const DPlane &p, int x, int y) {
+  x = x < 0 ? 0 : (x >= p.w ? p.w - 1 : x);
+  y = y < 0 ? 0 : (y >= p.h ? p.h - 1 : y);
+  return p.p[(size_t)y * p.stride + x];
+}
+__device__ __forceinline__ int clip_alf(int c, int ref, int v0, int v1) { return clip3(-c, c, v0 - ref) + clip3(-c, c, v1 - ref); }
+
+__device__ void alf_rows(int y, int vbH, int vbPos, bool luma, int &r1, int &r2, int &r3, int &r4, int &r5, int &r6) {
+  r1 = y + 1; r2 = y - 1; r3 = y + 2; r4 = y - 2; r5 = y + 3; r6 = y - 3;
+  const int yVb = y & (vbH - 1);
+  if (yVb < vbPos && yVb >= vbPos - (luma ? 4 : 2)) {
+    if (yVb == vbPos - 1) r1 = y;
+    if (yVb >= vbPos - 2) r3 = r1;
+    if (yVb >= vbPos - 3) r5 = r3;
+    if (yVb == vbPos - 1) r2 = y;
+    if (yVb >= vbPos - 2) r4 = r2;
+    if (yVb >= vbPos - 3) r6 = r4;
+  } else if (yVb >= vbPos && yVb <= vbPos + (luma ? 3 : 1)) {
+    if (yVb == vbPos) r2 = y;
+    if (yVb <= vbPos + 1) r4 = r2;
+    if (yVb <= vbPos + 2) r6 = r4;
+    if (yVb == vbPos) r1 = y;
+    if (yVb <= vbPos + 1) r3 = r1;
+    if (yVb <= vbPos + 2) r5 = r3;
+  }
+}
+
+__constant__ int8_t c_perm7[4][13] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12},
+                                      {9, 4, 10, 8, 1, 5, 11, 7, 3, 0, 2, 6, 12},
+                                      {0, 3, 2, 1, 8, 7, 6, 5, 4, 9, 10, 11, 12},
+                                      {9, 8, 10, 4, 3, 7, 11, 5, 1, 0, 2, 6, 12}};
+__constant__ int8_t c_th[16] = {0, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 4};
+__constant__ int8_t c_transpose[8] = {0, 1, 0, 2, 2, 3, 1, 3};
+
+__global__ void k_alf_luma(AlfParams P) {
+  const DPlane &S = P.src[0];
+  const DPlane &D = P.dst[0];
+  const int bx = (blockIdx.x * blockDim.x + threadIdx.x) * 4, by = blockIdx.y * 4;
+  if (bx >= S.w || by >= S.h) return;
+  const int ctb = (by >> P.ctu_log2) * P.wc + (bx >> P.ctu_log2);
+  const int vbH = 1 << P.ctu_log2, vbPos = P.vb_luma;
+  if (!P.en[0] || !P.ctb_en[ctb]) {
+    for (int y = by; y < by + 4 && y < S.h; y++)
+      for (int x = bx; x < bx + 4 && x < S.w; x++) D.p[(size_t)y * D.stride + x] = S.p[(size_t)y * S.stride + x];
+    return;
+  }
+  // --- classification (4x4 block)
+  int sumV = 0, sumH = 0, sumD0 = 0, sumD1 = 0;
+  const int yv = by & (vbH - 1);
+  const int i0 = (yv == vbPos) ? 1 : 0, i1 = (yv == vbPos - 4) ? 3 : 4;
+  for (int ii = i0; ii < i1; ii++) {
+    const int ay = by - 2 + ii * 2;
+    int rA = ay - 1, rB = ay + 1, rB2 = ay + 2;
+    if (ay > 0 && (ay & (vbH - 1)) == vbPos - 2) rB2 = ay + 1;
+    else if (ay > 0 && (ay & (vbH - 1)) == vbPos) rA = ay;
+    for (int jj = 0; jj < 4; jj++) {
+      const int ax = bx - 2 + jj * 2;
+      const int a = at(S, ax, ay) << 1, b = at(S, ax + 1, ay + 1) << 1;
+      sumV += abs(a - at(S, ax, rA) - at(S, ax, rB)) + abs(b - at(S, ax + 1, ay) - at(S, ax + 1, rB2));
+      sumH += abs(a - at(S, ax + 1, ay) - at(S, ax - 1, ay)) + abs(b - at(S, ax + 2, rB) - at(S, ax, rB));
+      sumD0 += abs(a - at(S, ax - 1, rA) - at(S, ax + 1, rB)) + abs(b - at(S, ax, ay) - at(S, ax + 2, rB2));
+      sumD1 += abs(a - at(S, ax - 1, rB) - at(S, ax + 1, rA)) + abs(b - at(S, ax, rB2) - at(S, ax + 2, ay));
+    }
+  }
+  const int shift = P.bd + 4;
+  const int act = clip3(0, 15, ((sumV + sumH) * ((yv == vbPos - 4 || yv == vbPos) ? 96 : 64)) >> shift);
+  int classIdx = c_th[act];
+  int hv1, hv0, d1, d0, dirHV, dirD, mainDir, secDir;
+  if (sumV > sumH) { hv1 = sumV; hv0 = sumH; dirHV = 1; } else { hv1 = sumH; hv0 = sumV; dirHV = 3; }
+  if (sumD0 > sumD1) { d1 = sumD0; d0 = sumD1; dirD = 0; } else { d1 = sumD1; d0 = sumD0; dirD = 2; }
+  int hvd1, hvd0;
+  if ((uint32_t)d1 * (uint32_t)hv0 > (uint32_t)hv1 * (uint32_t)d0) { hvd1 = d1; hvd0 = d0; mainDir = dirD; secDir = dirHV; }
+  else { hvd1 = hv1; hvd0 = hv0; mainDir = dirHV; secDir = dirD; }
+  int strength = 0;
+  if (hvd1 > 2 * hvd0) strength = 1;
+  if (hvd1 * 2 > 9 * hvd0) strength = 2;
+  if (strength) classIdx += (((mainDir & 1) << 1) + strength) * 5;
+  const int tr = c_transpose[mainDir * 2 + (secDir >> 1)];
+  // --- 7x7 diamond filter
+  const int set = P.ctb_set[ctb];
+  const int16_t *coef = P.luma_coef + (set * 25 + classIdx) * 13, *clip = P.luma_clip + (set * 25 + classIdx) * 13;
+  int fc[12], fl[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) { fc[k] = coef[c_perm7[tr][k]]; fl[k] = clip[c_perm7[tr][k]]; }
+  const int maxv = (1 << P.bd) - 1;
+  for (int y = by; y < by + 4 && y < S.h; y++) {
+    int r1, r2, r3, r4, r5, r6;
+    alf_rows(y, vbH, vbPos, true, r1, r2, r3, r4, r5, r6);
+    const int yVb = y & (vbH - 1);
+    const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
+    for (int x = bx; x < bx + 4 && x < S.w; x++) {
+      const int cur = at(S, x, y);
+      int sum = fc[0] * clip_alf(fl[0], cur, at(S, x, r5), at(S, x, r6));
+      sum += fc[1] * clip_alf(fl[1], cur, at(S, x + 1, r3), at(S, x - 1, r4));
+      sum += fc[2] * clip_alf(fl[2], cur, at(S, x, r3), at(S, x, r4));
+      sum += fc[3] * clip_alf(fl[3], cur, at(S, x - 1, r3), at(S, x + 1, r4));
+      sum += fc[4] * clip_alf(fl[4], cur, at(S, x + 2, r1), at(S, x - 2, r2));
+      sum += fc[5] * clip_alf(fl[5], cur, at(S, x + 1, r1), at(S, x - 1, r2));
+      sum += fc[6] * clip_alf(fl[6], cur, at(S, x, r1), at(S, x, r2));
+      sum += fc[7] * clip_alf(fl[7], cur, at(S, x - 1, r1), at(S, x + 1, r2));
+      sum += fc[8] * clip_alf(fl[8], cur, at(S, x - 2, r1), at(S, x + 2, r2));
+      sum += fc[9] * clip_alf(fl[9], cur, at(S, x + 3, y), at(S, x - 3, y));
+      sum += fc[10] * clip_alf(fl[10], cur, at(S, x + 2, y), at(S, x - 2, y));
+      sum += fc[11] * clip_alf(fl[11], cur, at(S, x + 1, y), at(S, x - 1, y));
+      sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
+      D.p[(size_t)y * D.stride + x] = (int16_t)clip3(0, maxv, sum + cur);
+    }
+  }
+}
+
+__global__ void k_alf_chroma(AlfParams P) {
+  const int comp = 1 + blockIdx.z;
+  const DPlane &S = P.src[comp];
+  const DPlane &D = P.dst[comp];
+  const DPlane &Y = P.src[0];
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= S.w || y >= S.h) return;
+  const int cl2 = P.ctu_log2 - 1;
+  const int ctb = (y >> cl2) * P.wc + (x >> cl2);
+  const int n = P.nctb;
+  const int maxv = (1 << P.bd) - 1;
+  const int cur = S.p[(size_t)y * S.stride + x];
+  int v = cur;
+  if (P.en[comp] && P.ctb_en[comp * n + ctb]) {
+    const int alt = P.ctb_alt[comp * n + ctb];
+    const int16_t *fc = P.chroma_coef + alt * 7, *fl = P.chroma_clip + alt * 7;
+    const int vbH = 1 << cl2, vbPos = P.vb_chroma;
+    int r1, r2, r3, r4, r5, r6;
+    alf_rows(y, vbH, vbPos, false, r1, r2, r3, r4, r5, r6);
+    int sum = fc[0] * clip_alf(fl[0], cur, at(S, x, r3), at(S, x, r4));
+    sum += fc[1] * clip_alf(fl[1], cur, at(S, x + 1, r1), at(S, x - 1, r2));
+    sum += fc[2] * clip_alf(fl[2], cur, at(S, x, r1), at(S, x, r2));
+    sum += fc[3] * clip_alf(fl[3], cur, at(S, x - 1, r1), at(S, x + 1, r2));
+    sum += fc[4] * clip_alf(fl[4], cur, at(S, x + 2, y), at(S, x - 2, y));
+    sum += fc[5] * clip_alf(fl[5], cur, at(S, x + 1, y), at(S, x - 1, y));
+    const int yVb = y & (vbH - 1);
+    const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
+    sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
+    v = clip3(0, maxv, sum + cur);
+  }
+  const int ccf = P.en[2 + comp] ? P.cc_ctl[(comp - 1) * n + ctb] : 0;
+  if (ccf) {
+    const int16_t *f = P.cc_coef + ((comp - 1) * 4 + ccf - 1) * 8;
+    const int lx = x * 2, ly = y * 2;
+    const int pos = ly & ((1 << P.ctu_log2) - 1);
+    int o1 = 1, o2 = -1, o3 = 2;
+    if (pos == P.vb_luma - 2 || pos == P.vb_luma + 1) o3 = o1;
+    else if (pos == P.vb_luma - 1 || pos == P.vb_luma) { o1 = 0; o2 = 0; o3 = 0; }
+    const int c0 = at(Y, lx, ly);
+    int sum = f[0] * (at(Y, lx, ly + o2) - c0) + f[1] * (at(Y, lx - 1, ly) - c0) + f[2] * (at(Y, lx + 1, ly) - c0) +
+              f[3] * (at(Y, lx - 1, ly + o1) - c0) + f[4] * (at(Y, lx, ly + o1) - c0) + f[5] * (at(Y, lx + 1, ly + o1) - c0) +
+              f[6] * (at(Y, lx, ly + o3) - c0);
+    sum = (sum + 64) >> 7;
+    const int off = (1 << P.bd) >> 1;
+    sum = clip3(0, maxv, sum + off) - off;
+    v = clip3(0, maxv, sum + v);
+  }
+  D.p[(size_t)y * D.stride + x] = (int16_t)v;
+}
+
+}  // namespace
+
+void launch_sao(const SaoParams &p, hipStream_t s) {
+  for (int c = 0; c < 3; c++) {
+    const int W = p.src[c].w, H = p.src[c].h;
+    dim3 grid(((W + 3) / 4 + 63) / 64, H);
+    hipLaunchKernelGGL(k_sao, grid, dim3(64), 0, s, p, c);
+  }
+}
+
+void launch_alf(const AlfParams &p, hipStream_t s) {
+  {
+    const int W = p.src[0].w, H = p.src[0].h;
+    dim3 grid(((W + 3) / 4 + 63) / 64, (H + 3) / 4);
+    hipLaunchKernelGGL(k_alf_luma, grid, dim3(64), 0, s, p);
+  }
+  {
+    const int W = p.src[1].w, H = p.src[1].h;
+    dim3 grid((W + 63) / 64, H, 2);
+    hipLaunchKernelGGL(k_alf_chroma, grid, dim3(64), 0, s, p);
+  }
+}

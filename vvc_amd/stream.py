@@ -95,3 +95,29 @@ def pic_params(p, slot, slot_of):
 def submit(ctx, p):
     geo = p["geo"] if p["geo"].size else np.zeros((0, 13), np.int32)
     ctx.submit(p["cu"], p["pu"], p["tu"], p["coef"], p["motion"].reshape(-1, 10), geo)
+
+
+def set_loop_filter_params(ctx, p):
+    """SAO / ALF parameters of the picture (as reconstructed by the reference's parameter-set
+    handling: SampleAdaptiveOffset::reconstructBlkSAOParams, AdaptiveLoopFilter::reconstructCoeffAPSs)."""
+    h = p["hdr"]
+    sao = np.ascontiguousarray(p["sao"], np.int32) if "sao" in p else None
+    alf = None
+    keep = [sao]
+    if "alf_ctb_en" in p and h["alf_enabled"]:
+        n = len(p["alf_aps_ids"])
+        coef = np.ascontiguousarray(np.concatenate([p["alf_fixed"], p["alf_coef_aps"][:n]]), np.int16)
+        clip = np.ascontiguousarray(np.concatenate([np.broadcast_to(p["alf_clip_default"], p["alf_fixed"].shape),
+                                                    p["alf_clip_aps"][:n]]), np.int16)
+        cc_ctl = np.array(p["ccalf_ctl"], np.uint8)
+        cc_ctl[0] *= np.uint8(h["ccalf_en_cb"] != 0)     # control words of a disabled component are not coded
+        cc_ctl[1] *= np.uint8(h["ccalf_en_cr"] != 0)
+        alt = np.array(p["alf_ctb_alt"], np.uint8)
+        alt[0] = 0
+        arrs = [coef, clip] + [np.ascontiguousarray(p[k], t) for k, t in (
+            ("alf_chroma_coef", np.int16), ("alf_chroma_clip", np.int16), ("ccalf_coef", np.int16),
+            ("alf_ctb_en", np.uint8))] + [np.ascontiguousarray(alt), np.ascontiguousarray(p["alf_ctb_fidx"], np.int16),
+                                         np.ascontiguousarray(cc_ctl)]
+        keep += arrs
+        alf = N.Alf(16 + n, *(a.ctypes.data for a in arrs))
+    ctx.set_loop_filter_params(sao, alf, keep)
