@@ -245,6 +245,10 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
   H.add("min_qp_ts", 4 + sps.getMinQpPrimeTsMinus4(CHANNEL_TYPE_LUMA));
   H.add("chroma_qp_off_cb", pps.getQpOffset(COMPONENT_Cb) + sl.getSliceChromaQpDelta(COMPONENT_Cb));
   H.add("chroma_qp_off_cr", pps.getQpOffset(COMPONENT_Cr) + sl.getSliceChromaQpDelta(COMPONENT_Cr));
+  H.add("chroma_qp_off_jc", pps.getQpOffset(JOINT_CbCr) + sl.getSliceChromaQpDelta(JOINT_CbCr));
+  H.add("ladf_enabled", sps.getLadfEnabled() ? 1 : 0);
+  H.add("plt_enabled", sps.getPLTMode() ? 1 : 0);
+  H.add("cu_chroma_qp_adj", sl.getUseChromaQpAdj() ? 1 : 0);
   H.add("pps_cb_qp_offset", pps.getQpOffset(COMPONENT_Cb));
   H.add("pps_cr_qp_offset", pps.getQpOffset(COMPONENT_Cr));
   H.add("picture_output", ph.getPicOutputFlag() ? 1 : 0);
@@ -291,6 +295,9 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
     for (int c = 1; c < 3; c++)
       for (int q = -sps.getQpBDOffset(CHANNEL_TYPE_CHROMA); q < 64; q++) m[c * 128 + q + 64] = sps.getMappedChromaQpValue((ComponentID)c, q);
     F.i32("chroma_qp_map", m, {3, 128});
+    std::vector<int32_t> j(128, 0);   // JOINT_CbCr mapping (QpParam with useJQP, Quant.cpp:121)
+    for (int q = -sps.getQpBDOffset(CHANNEL_TYPE_CHROMA); q < 64; q++) j[q + 64] = sps.getMappedChromaQpValue(JOINT_CbCr, q);
+    F.i32("chroma_qp_map_jc", j, {128});
   }
 
   TR("hdr+ref+qp done");

@@ -116,3 +116,37 @@ def alf_picture(p, planes):
                      _p(coef), _p(clip), _p(cc), _p(ccl), _p(ccf), _p(en), _p(cte), _p(cta), _p(cts), _p(ccc),
                      *(_p(x) for x in src), *(_p(x) for x in out))
     return out
+
+
+class OrDbkIn(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("width", "height", "bd", "ctu_log2", "dual_tree", "slice_type", "disable",
+                                       "beta_offset_div2", "tc_offset_div2")] + [
+        ("chroma_qp_off", C.c_int * 3), ("chroma_qp_map", C.c_void_p), ("chroma_qp_map_jc", C.c_void_p),
+        ("ref_poc", C.c_void_p), ("tc_table", C.c_void_p), ("beta_table", C.c_void_p),
+        ("cu", C.c_void_p), ("ncu", C.c_int), ("pu", C.c_void_p), ("npu", C.c_int), ("tu", C.c_void_p), ("ntu", C.c_int),
+        ("motion", C.c_void_p)]
+
+
+def deblock_picture(p, planes):
+    """LoopFilter::loopFilterPic restated (oracle_dbk.c); returns new planes."""
+    L = lib()
+    h = p["hdr"]
+    t = tables()
+    out = [np.ascontiguousarray(x, np.int16).copy() for x in planes]
+    arrs = dict(cqm=np.ascontiguousarray(p["chroma_qp_map"], np.int32), jc=np.ascontiguousarray(p["chroma_qp_map_jc"], np.int32),
+                ref=np.ascontiguousarray(p["ref_poc"], np.int32), tc=np.ascontiguousarray(t["dbk_tc"], np.int16),
+                beta=np.ascontiguousarray(t["dbk_beta"], np.int16), cu=np.ascontiguousarray(p["cu"], np.int32),
+                pu=np.ascontiguousarray(p["pu"], np.int32), tu=np.ascontiguousarray(p["tu"], np.int32),
+                mf=np.ascontiguousarray(p["motion"], np.int32))
+    d = OrDbkIn(h["width"], h["height"], h["bitdepth_y"], h["ctu_log2"], h["dual_tree"], h["slice_type"], h["dbk_disable"],
+                h["dbk_beta_offset_div2"], h["dbk_tc_offset_div2"])
+    d.chroma_qp_off[0], d.chroma_qp_off[1], d.chroma_qp_off[2] = h["chroma_qp_off_cb"], h["chroma_qp_off_cr"], h["chroma_qp_off_jc"]
+    d.chroma_qp_map, d.chroma_qp_map_jc = arrs["cqm"].ctypes.data, arrs["jc"].ctypes.data
+    d.ref_poc, d.tc_table, d.beta_table = arrs["ref"].ctypes.data, arrs["tc"].ctypes.data, arrs["beta"].ctypes.data
+    d.cu, d.ncu = arrs["cu"].ctypes.data, len(arrs["cu"])
+    d.pu, d.npu = arrs["pu"].ctypes.data, len(arrs["pu"])
+    d.tu, d.ntu = arrs["tu"].ctypes.data, len(arrs["tu"])
+    d.motion = arrs["mf"].ctypes.data
+    r = L.or_deblock_picture(C.byref(d), *(_p(x) for x in out))
+    assert r == 0, r
+    return out

@@ -23,3 +23,13 @@ def test_oracle_sao_alf_match_reference(golden_dir, name):
         for c, pl in enumerate("yuv"):
             bad = alf[c] != p["alf_" + pl]
             assert not bad.any(), "ALF POC %d %s: %d differ, first %s" % (poc, pl, bad.sum(), np.argwhere(bad)[0])
+
+
+@pytest.mark.parametrize("name", ["ai416_q37", "ra416_q32"])
+def test_oracle_deblocking_matches_reference(golden_dir, name):
+    for p in S.load_sequence(os.path.join(golden_dir, name)):
+        poc = p["hdr"]["poc"]
+        out = O.deblock_picture(p, [p["dbkin_" + c] for c in "yuv"])
+        for c, pl in enumerate("yuv"):
+            bad = out[c] != p["dbk_" + pl]
+            assert not bad.any(), "DBK POC %d %s: %d differ, first %s" % (poc, pl, bad.sum(), np.argwhere(bad)[0])
