@@ -119,8 +119,9 @@ typedef struct vvcr_pic_params {
   int32_t wp[2][VVCR_MAX_REF][3][7];  /* present, log2denom, weight, offset, w, o, offset(scaled) */
   int32_t dbk_disable, dbk_beta_offset_div2, dbk_tc_offset_div2;
   int32_t lf_across_slices, lf_across_tiles;
-  int32_t chroma_qp_off[3];          /* per component (pps + slice), index 1,2 */
-  int32_t chroma_qp_map[3][128];     /* mapped chroma QP for qp in [-64,63] at [c][qp+64] */
+  int32_t chroma_qp_off[3];          /* pps + slice chroma QP offsets: [1] Cb, [2] Cr, [0] joint Cb-Cr */
+  int32_t chroma_qp_map[3][128];     /* SPS::getMappedChromaQpValue for qp in [-64,63] at [c][qp+64];
+                                        [0] = JOINT_CbCr table (QpParam, Quant.cpp:121) */
   int32_t sao_luma, sao_chroma;
   int32_t alf_en[3], ccalf_en[2], alf_vb_luma, alf_vb_chroma;
   int32_t lmcs_enabled, lmcs_chroma_scale, lmcs_min_bin, lmcs_max_bin;
@@ -184,7 +185,9 @@ int vvcr_read_picture(vvcr_ctx *ctx, int32_t slot, uint16_t *planes[3], const in
 /* DMVR refined deltas per PU sub-block, [npu][64][2] (PredictionUnit::mvdL0SubPu). Blocks. */
 int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n);
 
-/* Timing of the last vvcr_end_picture*, in ms, per stage (HIP events on the library stream). */
+/* Timing of the last vvcr_end_picture*, in ms (HIP events on the library stream): ms[0] = whole call,
+ * ms[1 + k] = stage k in VVCR_STAGE_* bit order (RESID, INTER, INTRA, LMCS_INV, DBK, SAO, ALF), 0 if
+ * the stage did not run. n = number of entries wanted (<= 8). */
 int vvcr_last_stage_times(vvcr_ctx *ctx, float *ms, int32_t n);
 /* Raw HIP stream handle (hipStream_t) of the context, for callers that time or overlap work. */
 void *vvcr_stream(vvcr_ctx *ctx);

@@ -9,6 +9,7 @@
 
 #include "vvcr_internal.h"
 #include "vvcr_host.h"
+#include "vvcr_dbk.h"
 
 namespace {
 
@@ -63,9 +64,13 @@ struct vvcr_ctx {
   DevVec<int16_t> d_alf_luma_coef, d_alf_luma_clip, d_alf_chroma, d_alf_cc;
   DevVec<uint8_t> d_alf_ctb;      // ctb_en[3n] | ctb_alt[3n] | cc_ctl[2n]
   DevVec<int16_t> d_alf_set;
+  DbkLists dbk;
+  std::vector<DbkSeg> dbk_all;
+  DevVec<DbkSeg> d_dbk;
   bool have_sao = false, have_alf = false;
-  hipEvent_t ev[8] = {};
-  float stage_ms[8] = {};
+  hipEvent_t ev[2] = {};            // whole end_picture call
+  hipEvent_t sev[7][2] = {};        // per stage begin / end
+  bool stage_ran[7] = {};
 };
 
 #define API_BEGIN try {
@@ -103,6 +108,8 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       ctx->tmp[c] = alloc_plane(w, h);
     }
     for (auto &e : ctx->ev) VVCR_CHECK_HIP(hipEventCreate(&e));
+    for (auto &se : ctx->sev)
+      for (auto &e : se) VVCR_CHECK_HIP(hipEventCreate(&e));
     build_scan_tables(ctx->scans);
     ctx->d_scans.upload(ctx->scans.data, ctx->stream);
   } catch (const VvcrError &e) {
@@ -120,6 +127,8 @@ int vvcr_destroy(vvcr_ctx *ctx) {
     for (auto &p : s) hipFree(p.p);
   for (int c = 0; c < 3; c++) { hipFree(ctx->pred[c].p); hipFree(ctx->resi[c].p); hipFree(ctx->tmp[c].p); }
   for (auto &e : ctx->ev) if (e) hipEventDestroy(e);
+  for (auto &se : ctx->sev)
+    for (auto &e : se) if (e) hipEventDestroy(e);
   hipStreamDestroy(ctx->stream);
   delete ctx;
   return VVCR_OK;
@@ -216,14 +225,30 @@ static McParams make_mc_params(vvcr_ctx *ctx) {
   return P;
 }
 
+namespace {
+enum { ST_RESID, ST_INTER, ST_INTRA, ST_LMCS, ST_DBK, ST_SAO, ST_ALF };
+struct StageTimer {
+  vvcr_ctx *c;
+  int k;
+  StageTimer(vvcr_ctx *cc, int kk) : c(cc), k(kk) {
+    c->stage_ran[k] = true;
+    VVCR_CHECK_HIP(hipEventRecord(c->sev[k][0], c->stream));
+  }
+  ~StageTimer() { (void)hipEventRecord(c->sev[k][1], c->stream); }
+};
+}  // namespace
+
 int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_end_picture without begin");
   build_work_lists(ctx->sp, ctx->pp, ctx->desc, ctx->wl);
+  if (mask & VVCR_STAGE_DBK) plan_deblocking(ctx->sp, ctx->pp, ctx->desc, ctx->dbk);
+  for (bool &r : ctx->stage_ran) r = false;
   hipStream_t s = ctx->stream;
   VVCR_CHECK_HIP(hipEventRecord(ctx->ev[0], s));
   if (mask & VVCR_STAGE_RESID) {
+    StageTimer t(ctx, ST_RESID);
     for (int c = 0; c < 3; c++)
       VVCR_CHECK_HIP(hipMemsetAsync(ctx->resi[c].p, 0, (size_t)ctx->resi[c].stride * ctx->resi[c].h * 2, s));
     ctx->d_coef.upload(ctx->desc.coef, s);
@@ -237,9 +262,29 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
     VVCR_CHECK_HIP(hipGetLastError());
   }
   if (mask & VVCR_STAGE_INTER) {
+    StageTimer t(ctx, ST_INTER);
     ctx->d_mc_basic.upload(ctx->wl.mc_basic, s);
     launch_mc_basic(make_mc_params(ctx), ctx->d_mc_basic.p, (int)ctx->wl.mc_basic.size(), s);
     VVCR_CHECK_HIP(hipGetLastError());
+  }
+  // ---- deblocking, in place on the picture slot: all vertical edges, then all horizontal edges
+  if ((mask & VVCR_STAGE_DBK) && ctx->dbk.total()) {
+    StageTimer t(ctx, ST_DBK);
+    auto &all = ctx->dbk_all;
+    all.clear();
+    int counts[4];
+    const std::vector<DbkSeg> *parts[4] = {&ctx->dbk.luma[0], &ctx->dbk.chroma[0], &ctx->dbk.luma[1], &ctx->dbk.chroma[1]};
+    for (int k = 0; k < 4; k++) {
+      counts[k] = (int)parts[k]->size();
+      all.insert(all.end(), parts[k]->begin(), parts[k]->end());
+    }
+    ctx->d_dbk.upload(all, s);
+    DbkParams dp{};
+    for (int c = 0; c < 3; c++) dp.pl[c] = ctx->dpb[ctx->pp.slot][c];
+    dp.bd = ctx->sp.bit_depth;
+    dp.beta_offset_div2 = ctx->pp.dbk_beta_offset_div2;
+    dp.tc_offset_div2 = ctx->pp.dbk_tc_offset_div2;
+    launch_dbk(dp, ctx->d_dbk.p, counts, s);
   }
   // ---- SAO (DBK picture in the slot -> tmp) and ALF (-> slot)
   {
@@ -249,6 +294,7 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
     const int wc = (ctx->sp.width + ctu - 1) / ctu, n = n_ctb(ctx->sp);
     bool inTmp = false;
     if ((mask & VVCR_STAGE_SAO) && ctx->have_sao && (pp.sao_luma || pp.sao_chroma)) {
+      StageTimer t(ctx, ST_SAO);
       SaoParams sp{};
       for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ctx->tmp[c]; }
       sp.sao = ctx->d_sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
@@ -258,6 +304,7 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
     }
     const bool alfOn = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
     if ((mask & VVCR_STAGE_ALF) && ctx->have_alf && alfOn) {
+      StageTimer t(ctx, ST_ALF);
       AlfParams ap{};
       for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ctx->tmp[c] : A[c]; ap.dst[c] = inTmp ? A[c] : ctx->tmp[c]; }
       ap.bd = ctx->sp.bit_depth; ap.ctu_log2 = ctx->sp.ctu_log2; ap.wc = wc; ap.nctb = n;
@@ -300,6 +347,11 @@ int vvcr_last_stage_times(vvcr_ctx *ctx, float *ms, int32_t n) {
   float t = 0;
   VVCR_CHECK_HIP(hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]));
   if (n > 0) ms[0] = t;
+  for (int k = 0; k < 7 && k + 1 < n; k++) {
+    float v = 0;
+    if (ctx->stage_ran[k]) VVCR_CHECK_HIP(hipEventElapsedTime(&v, ctx->sev[k][0], ctx->sev[k][1]));
+    ms[k + 1] = v;
+  }
   return VVCR_OK;
   API_END
 }

@@ -1,0 +1,243 @@
+// vvcr_dbk.hip — deblocking filter for gfx950 (LoopFilter.cpp:844-1667 sample decisions + filters).
+//
+// The host plans every 4-sample edge segment (vvcr_dbk_host.cpp); here one lane decides and filters
+// one segment: 4 luma lines (xEdgeFilterLuma :981-1081) or 2 lines of Cb and of Cr
+// (xEdgeFilterChroma :1163-1283). All vertical edges of the picture are filtered before any horizontal
+// edge, as loopFilterPic (:165-240) does. Segments of one direction never overlap: each side modifies
+// at most maxFilterLength samples and reads at most one more, and the reference's length rules
+// (transform size <= 4 -> 1, sub-block edges 8 apart -> <= 3, 32-sample transforms for 7) keep the
+// read window of one edge clear of the writes of the next, so the in-place parallel pass equals the
+// reference's sequential CU order.
+#include "vvcr_dbk.h"
+#include "vvcr_gen_tables.h"
+
+namespace {
+
+__device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__device__ __forceinline__ int calc_dp(const int16_t *s, int o, bool ctbh) {
+  return ctbh ? abs(s[-o * 2] - 2 * s[-o * 2] + s[-o]) : abs(s[-o * 3] - 2 * s[-o * 2] + s[-o]);
+}
+__device__ __forceinline__ int calc_dq(const int16_t *s, int o) { return abs(s[0] - 2 * s[o] + s[o * 2]); }
+
+// xUseStrongFiltering (:1566), JVET_Q0054 variant for long-tap sides
+__device__ bool use_strong(const int16_t *s, int o, int d, int beta, int tc, bool pl, bool ql, int lenP, int lenQ, bool ctbh) {
+  const int m4 = s[0], m3 = s[-o], m7 = s[o * 3], m0 = s[-o * 4], m2 = s[-o * 2];
+  int sp3 = ctbh ? abs(m2 - m3) : abs(m0 - m3);
+  int sq3 = abs(m7 - m4);
+  const int dstrong = sp3 + sq3;
+  if (pl || ql) {
+    if (pl) {
+      int mP4;
+      if (lenP == 7) { sp3 += abs(s[-o * 5] - s[-o * 6] - s[-o * 7] + s[-o * 8]); mP4 = s[-o * 8]; }
+      else mP4 = s[-o * 6];
+      sp3 = (sp3 + abs(m0 - mP4) + 1) >> 1;
+    }
+    if (ql) {
+      int m11;
+      if (lenQ == 7) { sq3 += abs(s[o * 4] - s[o * 5] - s[o * 6] + s[o * 7]); m11 = s[o * 7]; }
+      else m11 = s[o * 5];
+      sq3 = (sq3 + abs(m11 - m7) + 1) >> 1;
+    }
+    return (sp3 + sq3) < (beta * 3 >> 5) && d < (beta >> 4) && abs(m3 - m4) < ((tc * 5 + 1) >> 1);
+  }
+  return dstrong < (beta >> 3) && d < (beta >> 2) && abs(m3 - m4) < ((tc * 5 + 1) >> 1);
+}
+
+// xFilteringPandQ (:1323) + xBilinearFilter (:1302)
+__device__ void filter_long(int16_t *src, int o, int nP, int nQ, int tc) {
+  int16_t *sP = src - o, *sQ = src;
+  const int c7[7] = {59, 50, 41, 32, 23, 14, 5}, c3[3] = {53, 32, 11}, c5[5] = {58, 45, 32, 19, 6};
+  const int *cP = nP == 7 ? c7 : (nP == 5 ? c5 : c3), *cQ = nQ == 7 ? c7 : (nQ == 5 ? c5 : c3);
+  const int refP = nP == 7 ? (sP[-6 * o] + sP[-7 * o] + 1) >> 1 : nP == 3 ? (sP[-2 * o] + sP[-3 * o] + 1) >> 1 : (sP[-4 * o] + sP[-5 * o] + 1) >> 1;
+  const int refQ = nQ == 7 ? (sQ[6 * o] + sQ[7 * o] + 1) >> 1 : nQ == 3 ? (sQ[2 * o] + sQ[3 * o] + 1) >> 1 : (sQ[4 * o] + sQ[5 * o] + 1) >> 1;
+  int mid;
+  if (nP == nQ) {
+    if (nP == 5)
+      mid = (2 * (sP[0] + sQ[0] + sP[-o] + sQ[o] + sP[-2 * o] + sQ[2 * o]) + sP[-3 * o] + sQ[3 * o] + sP[-4 * o] + sQ[4 * o] + 8) >> 4;
+    else
+      mid = (2 * (sP[0] + sQ[0]) + sP[-o] + sQ[o] + sP[-2 * o] + sQ[2 * o] + sP[-3 * o] + sQ[3 * o] + sP[-4 * o] + sQ[4 * o] +
+             sP[-5 * o] + sQ[5 * o] + sP[-6 * o] + sQ[6 * o] + 8) >> 4;
+  } else {
+    const bool swp = nQ > nP;
+    const int16_t *pt = swp ? sQ : sP, *qt = swp ? sP : sQ;
+    const int oP = swp ? o : -o, oQ = -oP;
+    const int big = swp ? nQ : nP, small = swp ? nP : nQ;
+    if (big == 7 && small == 5)
+      mid = (2 * (sP[0] + sQ[0] + sP[-o] + sQ[o]) + sP[-2 * o] + sQ[2 * o] + sP[-3 * o] + sQ[3 * o] + sP[-4 * o] + sQ[4 * o] +
+             sP[-5 * o] + sQ[5 * o] + 8) >> 4;
+    else if (big == 7 && small == 3)
+      mid = (2 * (pt[0] + qt[0]) + qt[0] + 2 * (qt[oQ] + qt[2 * oQ]) + pt[oP] + qt[oQ] + pt[2 * oP] + pt[3 * oP] + pt[4 * oP] +
+             pt[5 * oP] + pt[6 * oP] + 8) >> 4;
+    else
+      mid = (sP[0] + sQ[0] + sP[-o] + sQ[o] + sP[-2 * o] + sQ[2 * o] + sP[-3 * o] + sQ[3 * o] + 4) >> 3;
+  }
+  const int t7[7] = {6, 5, 4, 3, 2, 1, 1}, t3[3] = {6, 4, 2};
+  const int *tP = nP == 3 ? t3 : t7, *tQ = nQ == 3 ? t3 : t7;
+  int vp[7], vq[7];
+  for (int i = 0; i < nP; i++) {
+    const int s = sP[-o * i], cv = (tc * tP[i]) >> 1;
+    vp[i] = clip3(s - cv, s + cv, (mid * cP[i] + refP * (64 - cP[i]) + 32) >> 6);
+  }
+  for (int i = 0; i < nQ; i++) {
+    const int s = sQ[o * i], cv = (tc * tQ[i]) >> 1;
+    vq[i] = clip3(s - cv, s + cv, (mid * cQ[i] + refQ * (64 - cQ[i]) + 32) >> 6);
+  }
+  for (int i = 0; i < nP; i++) sP[-o * i] = (int16_t)vp[i];
+  for (int i = 0; i < nQ; i++) sQ[o * i] = (int16_t)vq[i];
+}
+
+// xPelFilterLuma (:1397)
+__device__ void filter_luma_line(int16_t *s, int o, int tc, bool sw, int thrCut, bool fP, bool fQ, int maxv, bool pl, bool ql,
+                                 int lenP, int lenQ) {
+  const int m4 = s[0], m3 = s[-o], m5 = s[o], m2 = s[-o * 2], m6 = s[o * 2], m1 = s[-o * 3], m7 = s[o * 3], m0 = s[-o * 4];
+  if (sw) {
+    if (pl || ql) {
+      filter_long(s, o, pl ? lenP : 3, ql ? lenQ : 3, tc);
+    } else {
+      s[-o] = (int16_t)clip3(m3 - 3 * tc, m3 + 3 * tc, (m1 + 2 * m2 + 2 * m3 + 2 * m4 + m5 + 4) >> 3);
+      s[0] = (int16_t)clip3(m4 - 3 * tc, m4 + 3 * tc, (m2 + 2 * m3 + 2 * m4 + 2 * m5 + m6 + 4) >> 3);
+      s[-o * 2] = (int16_t)clip3(m2 - 2 * tc, m2 + 2 * tc, (m1 + m2 + m3 + m4 + 2) >> 2);
+      s[o] = (int16_t)clip3(m5 - 2 * tc, m5 + 2 * tc, (m3 + m4 + m5 + m6 + 2) >> 2);
+      s[-o * 3] = (int16_t)clip3(m1 - tc, m1 + tc, (2 * m0 + 3 * m1 + m2 + m3 + m4 + 4) >> 3);
+      s[o * 2] = (int16_t)clip3(m6 - tc, m6 + tc, (m3 + m4 + m5 + 3 * m6 + 2 * m7 + 4) >> 3);
+    }
+    return;
+  }
+  int delta = (9 * (m4 - m3) - 3 * (m5 - m2) + 8) >> 4;
+  if (abs(delta) < thrCut) {
+    delta = clip3(-tc, tc, delta);
+    s[-o] = (int16_t)clip3(0, maxv, m3 + delta);
+    s[0] = (int16_t)clip3(0, maxv, m4 - delta);
+    const int tc2 = tc >> 1;
+    if (fP) s[-o * 2] = (int16_t)clip3(0, maxv, m2 + clip3(-tc2, tc2, (((m1 + m3 + 1) >> 1) - m2 + delta) >> 1));
+    if (fQ) s[o] = (int16_t)clip3(0, maxv, m5 + clip3(-tc2, tc2, (((m6 + m4 + 1) >> 1) - m5 - delta) >> 1));
+  }
+}
+
+// xPelFilterChroma (:1497)
+__device__ void filter_chroma_line(int16_t *s, int o, int tc, bool sw, int maxv, bool ctbh) {
+  const int m0 = s[-o * 4], m1 = s[-o * 3], m2 = s[-o * 2], m3 = s[-o], m4 = s[0], m5 = s[o], m6 = s[o * 2], m7 = s[o * 3];
+  if (sw) {
+    if (ctbh) {
+      s[-o] = (int16_t)clip3(m3 - tc, m3 + tc, (3 * m2 + 2 * m3 + m4 + m5 + m6 + 4) >> 3);
+      s[0] = (int16_t)clip3(m4 - tc, m4 + tc, (2 * m2 + m3 + 2 * m4 + m5 + m6 + m7 + 4) >> 3);
+      s[o] = (int16_t)clip3(m5 - tc, m5 + tc, (m2 + m3 + m4 + 2 * m5 + m6 + 2 * m7 + 4) >> 3);
+      s[o * 2] = (int16_t)clip3(m6 - tc, m6 + tc, (m3 + m4 + m5 + 2 * m6 + 3 * m7 + 4) >> 3);
+    } else {
+      s[-o * 3] = (int16_t)clip3(m1 - tc, m1 + tc, (3 * m0 + 2 * m1 + m2 + m3 + m4 + 4) >> 3);
+      s[-o * 2] = (int16_t)clip3(m2 - tc, m2 + tc, (2 * m0 + m1 + 2 * m2 + m3 + m4 + m5 + 4) >> 3);
+      s[-o] = (int16_t)clip3(m3 - tc, m3 + tc, (m0 + m1 + m2 + 2 * m3 + m4 + m5 + m6 + 4) >> 3);
+      s[0] = (int16_t)clip3(m4 - tc, m4 + tc, (m1 + m2 + m3 + 2 * m4 + m5 + m6 + m7 + 4) >> 3);
+      s[o] = (int16_t)clip3(m5 - tc, m5 + tc, (m2 + m3 + m4 + 2 * m5 + m6 + 2 * m7 + 4) >> 3);
+      s[o * 2] = (int16_t)clip3(m6 - tc, m6 + tc, (m3 + m4 + m5 + 2 * m6 + 3 * m7 + 4) >> 3);
+    }
+    return;
+  }
+  const int delta = clip3(-tc, tc, ((((m4 - m3) << 2) + m2 - m5 + 4) >> 3));
+  s[-o] = (int16_t)clip3(0, maxv, m3 + delta);
+  s[0] = (int16_t)clip3(0, maxv, m4 - delta);
+}
+
+__device__ __forceinline__ int tc_of(int idx, int bd) {
+  const int t = vvcr_tab::dbk_tc[idx];
+  return bd < 10 ? (t + 2) >> (10 - bd) : t << (bd - 10);
+}
+
+template <int DIR>
+__global__ void k_dbk_luma(DbkParams P, const DbkSeg *segs, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DbkSeg sg = segs[i];
+  const uint32_t w = sg.w;
+  const int bs = w & 3, lenP = (w >> 2) & 7, lenQ = (w >> 5) & 7, qp = (w >> 8) & 63;
+  const bool pl = (w >> 14) & 1, ql = (w >> 15) & 1;
+  const DPlane &Y = P.pl[0];
+  const int bd = P.bd, maxv = (1 << bd) - 1;
+  const int o = DIR == 0 ? 1 : Y.stride;
+  const int step = DIR == 0 ? Y.stride : 1;
+  const int tc = tc_of(clip3(0, 65, qp + 2 * (bs - 1) + 2 * P.tc_offset_div2), bd);
+  const int beta = vvcr_tab::dbk_beta[clip3(0, 63, qp + 2 * P.beta_offset_div2)] * (1 << (bd - 8));
+  const int sideThr = (beta + (beta >> 1)) >> 3;
+  const int thrCut = tc * 10;
+  int16_t *base = Y.p + (size_t)(sg.y4 * 4) * Y.stride + sg.x4 * 4;
+  int16_t *s0 = base, *s3 = base + 3 * step;
+  const int dp0 = calc_dp(s0, o, false), dq0 = calc_dq(s0, o), dp3 = calc_dp(s3, o, false), dq3 = calc_dq(s3, o);
+  if (pl || ql) {
+    int dp0L = dp0, dq0L = dq0, dp3L = dp3, dq3L = dq3;
+    if (pl) {
+      dp0L = (dp0L + calc_dp(s0 - 3 * o, o, false) + 1) >> 1;
+      dp3L = (dp3L + calc_dp(s3 - 3 * o, o, false) + 1) >> 1;
+    }
+    if (ql) {
+      dq0L = (dq0L + calc_dq(s0 + 3 * o, o) + 1) >> 1;
+      dq3L = (dq3L + calc_dq(s3 + 3 * o, o) + 1) >> 1;
+    }
+    const int d0L = dp0L + dq0L, d3L = dp3L + dq3L;
+    if (d0L + d3L < beta) {
+      const bool fP = dp0L + dp3L < sideThr, fQ = dq0L + dq3L < sideThr;
+      if (use_strong(s0, o, 2 * d0L, beta, tc, pl, ql, lenP, lenQ, false) && use_strong(s3, o, 2 * d3L, beta, tc, pl, ql, lenP, lenQ, false)) {
+        for (int k = 0; k < 4; k++) filter_luma_line(base + k * step, o, tc, true, thrCut, fP, fQ, maxv, pl, ql, lenP, lenQ);
+        return;
+      }
+    }
+  }
+  const int d0 = dp0 + dq0, d3 = dp3 + dq3;
+  if (d0 + d3 >= beta) return;
+  bool fP = false, fQ = false, sw = false;
+  if (lenP > 1 && lenQ > 1) { fP = dp0 + dp3 < sideThr; fQ = dq0 + dq3 < sideThr; }
+  if (lenP > 2 && lenQ > 2)
+    sw = use_strong(s0, o, 2 * d0, beta, tc, false, false, 7, 7, false) && use_strong(s3, o, 2 * d3, beta, tc, false, false, 7, 7, false);
+  for (int k = 0; k < 4; k++) filter_luma_line(base + k * step, o, tc, sw, thrCut, fP, fQ, maxv, false, false, 7, 7);
+}
+
+template <int DIR>
+__global__ void k_dbk_chroma(DbkParams P, const DbkSeg *segs, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DbkSeg sg = segs[i];
+  const uint32_t w = sg.w;
+  const bool large = (w >> 4) & 1, ctbh = (w >> 19) & 1;
+  const int bd = P.bd, maxv = (1 << bd) - 1;
+  for (int k = 0; k < 2; k++) {
+    const int bs = (w >> (2 * k)) & 3;
+    if (!(bs == 2 || (large && bs == 1))) continue;
+    const int qp = (int)((w >> (5 + 7 * k)) & 127) - 64;
+    const DPlane &C = P.pl[1 + k];
+    const int o = DIR == 0 ? 1 : C.stride;
+    const int step = DIR == 0 ? C.stride : 1;
+    const int tc = tc_of(clip3(0, 65, qp + 2 * (bs - 1) + 2 * P.tc_offset_div2), bd);
+    int16_t *base = C.p + (size_t)(sg.y4 * 2) * C.stride + sg.x4 * 2;
+    bool sw = false;
+    if (large) {
+      const int beta = vvcr_tab::dbk_beta[clip3(0, 63, qp + 2 * P.beta_offset_div2)] * (1 << (bd - 8));
+      int16_t *s0 = base, *s1 = base + step;
+      const int d0 = calc_dp(s0, o, ctbh) + calc_dq(s0, o), d3 = calc_dp(s1, o, ctbh) + calc_dq(s1, o);
+      if (d0 + d3 < beta)
+        sw = use_strong(s0, o, 2 * d0, beta, tc, false, false, 7, 7, ctbh) && use_strong(s1, o, 2 * d3, beta, tc, false, false, 7, 7, ctbh);
+    }
+    for (int l = 0; l < 2; l++) filter_chroma_line(base + l * step, o, tc, sw, maxv, ctbh);
+  }
+}
+
+}  // namespace
+
+void launch_dbk(const DbkParams &p, const DbkSeg *segs, const int counts[4], hipStream_t s) {
+  const int T = 256;
+  int off = 0;
+  for (int k = 0; k < 4; k++) {
+    const int n = counts[k];
+    if (n > 0) {
+      const dim3 g((n + T - 1) / T);
+      const DbkSeg *sg = segs + off;
+      switch (k) {
+        case 0: hipLaunchKernelGGL(k_dbk_luma<0>, g, dim3(T), 0, s, p, sg, n); break;
+        case 1: hipLaunchKernelGGL(k_dbk_chroma<0>, g, dim3(T), 0, s, p, sg, n); break;
+        case 2: hipLaunchKernelGGL(k_dbk_luma<1>, g, dim3(T), 0, s, p, sg, n); break;
+        case 3: hipLaunchKernelGGL(k_dbk_chroma<1>, g, dim3(T), 0, s, p, sg, n); break;
+      }
+      VVCR_CHECK_HIP(hipGetLastError());
+    }
+    off += n;
+  }
+}

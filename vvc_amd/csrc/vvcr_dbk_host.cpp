@@ -1,0 +1,403 @@
+// vvcr_dbk_host.cpp — deblocking edge planning (host producer side).
+//
+// Derives, for every 4-sample edge segment of the picture, the parameters the deblocking decision
+// needs: boundary strength per component, maximum filter lengths, and the P/Q average QPs. This is
+// the control part of LoopFilter::xDeblockCU (source/Lib/CommonLib/LoopFilter.cpp:261-408):
+// edge flags and TU/PU markers (xSetEdgefilterMultiple :627), filter lengths from transform sizes
+// (:454) and for SbTMVP/affine sub-blocks (:550), xGetBoundaryStrengthSingle (:674), and the QP / length
+// bookkeeping of xEdgeFilterLuma (:844-979) and xEdgeFilterChroma (:1087-1244). The sample decisions
+// and filtering run on the GPU (vvcr_dbk.hip). Each CU writes only edge positions inside its own area,
+// so the per-CTU state of the reference reduces to per-CU work over picture-wide maps.
+#include "vvcr_dbk.h"
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+namespace {
+
+enum { VER = 0, HOR = 1 };
+enum { BX = 0, BY, BW, BH, BCBF };
+constexpr int MODE_INTRA = 1;
+constexpr int MRG_TYPE_SUBPU_ATMVP = 1;
+
+struct Planner {
+  const vvcr_seq_params &sp;
+  const vvcr_pic_params &pp;
+  const PictureDescriptors &d;
+  DbkLists &out;
+  int W4, H4, ctu, parts;
+  std::vector<int> cu_map[2], tu_map[2];
+  // per-CU scratch in CTU-relative coordinates (the reference's per-CTU arrays, LoopFilter.h:66-79)
+  int ctu_x = 0, ctu_y = 0;
+  uint8_t bs[2][32 * 32];
+  uint8_t edge[2][32 * 32];
+  uint8_t lenP[3][128][128], lenQ[3][128][128], tedge[128][128];
+  bool left = false, top = false, internal = false;
+
+  Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, DbkLists &o)
+      : sp(s), pp(p), d(dd), out(o) {
+    W4 = sp.width / 4;
+    H4 = sp.height / 4;
+    ctu = 1 << sp.ctu_log2;
+    parts = ctu / 4;
+  }
+
+  int get_cu(int x, int y, int ch) const {
+    const int s = ch ? 1 : 2;
+    const int i = cu_map[ch][(size_t)(y >> s) * W4 + (x >> s)];
+    if (i < 0) throw VvcrError(VVCR_E_ARG, "deblocking: no CU covers a neighbouring position");
+    return i;
+  }
+  int get_tu(int x, int y, int ch) const {
+    const int s = ch ? 1 : 2;
+    const int t = tu_map[ch][(size_t)(y >> s) * W4 + (x >> s)];
+    if (t < 0) throw VvcrError(VVCR_E_ARG, "deblocking: no TU covers a neighbouring position");
+    if (ch) return t;
+    const vvcr_cu &cu = d.cu[d.tu[t].cu];
+    if (cu.isp) {   // CodingStructure::getTU (CodingStructure.cpp:379): search the ISP sub-partitions
+      for (int k = 0; k < 4 && t + k < (int)d.tu.size(); k++) {
+        const int32_t *b = d.tu[t + k].b[0];
+        if (x >= b[BX] && x < b[BX] + b[BW] && y >= b[BY] && y < b[BY] + b[BH]) return t + k;
+      }
+    }
+    return t;
+  }
+  void fill(std::vector<int> &m, int x, int y, int w, int h, int s, int v) {
+    for (int j = y >> s; j < (y + h + (1 << s) - 1) >> s; j++)
+      for (int i = x >> s; i < (x + w + (1 << s) - 1) >> s; i++) m[(size_t)j * W4 + i] = v;
+  }
+  int raster(int x, int y) const { return ((x & (ctu - 1)) >> 2) + ((y & (ctu - 1)) >> 2) * parts; }
+
+  static void cu_area(const vvcr_cu &c, int *a) {
+    if (c.yvalid) { a[0] = c.x; a[1] = c.y; a[2] = c.w; a[3] = c.h; }
+    else { a[0] = c.cx * 2; a[1] = c.cy * 2; a[2] = c.cw * 2; a[3] = c.ch * 2; }
+  }
+
+  void build_maps() {
+    const size_t n = (size_t)W4 * H4;
+    for (int k = 0; k < 2; k++) { cu_map[k].assign(n, -1); tu_map[k].assign(n, -1); }
+    for (size_t i = 0; i < d.cu.size(); i++) {
+      const vvcr_cu &c = d.cu[i];
+      if (c.yvalid) fill(cu_map[0], c.x, c.y, c.w, c.h, 2, (int)i);
+      if (c.cvalid) fill(cu_map[1], c.cx, c.cy, c.cw, c.ch, 1, (int)i);
+    }
+    for (size_t t = 0; t < d.tu.size(); t++) {
+      const vvcr_cu &c = d.cu[d.tu[t].cu];
+      const int32_t *b0 = d.tu[t].b[0], *b1 = d.tu[t].b[1];
+      if (b0[BW] > 0 && b0[BH] > 0) {
+        if (c.isp) {   // the first ISP TU owns the CU area in the index map (CodingStructure::addTU :624)
+          if ((int)t == c.firsttu) fill(tu_map[0], c.x, c.y, c.w, c.h, 2, (int)t);
+        } else {
+          fill(tu_map[0], b0[BX], b0[BY], b0[BW], b0[BH], 2, (int)t);
+        }
+      }
+      if (b1[BW] > 0 && b1[BH] > 0) fill(tu_map[1], b1[BX], b1[BY], b1[BW], b1[BH], 1, (int)t);
+    }
+  }
+
+  void set_edges(int dir, int x, int y, int w, int h, bool val, bool edgeIdx) {
+    const int add = dir == VER ? parts : 1, n = dir == VER ? h / 4 : w / 4;
+    int idx = raster(x, y);
+    for (int i = 0; i < n; i++, idx += add) {
+      edge[dir][idx] = val;
+      if (bs[dir][idx] && val) bs[dir][idx] = 3;
+      else if (!edgeIdx) bs[dir][idx] = val;
+    }
+  }
+
+  void len_from_tu(int dir, const vvcr_cu &cu, int t) {
+    const vvcr_tu &tu = d.tu[t];
+    for (int comp = 0; comp < 3; comp++) {
+      const int ch = comp ? 1 : 0;
+      const int32_t *b = tu.b[comp], *bch = tu.b[ch];
+      if (b[BW] <= 0 || b[BH] <= 0) continue;
+      const int cux = comp ? cu.cx : cu.x, cuy = comp ? cu.cy : cu.y;
+      const int xo = b[BX] - (ctu_x >> ch), yo = b[BY] - (ctu_y >> ch);
+      const int step = 4 >> ch;
+      const bool horz = dir == HOR;
+      if (!(horz ? (b[BY] == cuy ? top : internal) : (b[BX] == cux ? left : internal))) continue;
+      const int n = horz ? b[BW] : b[BH];
+      for (int k = 0; k < n; k += step) {
+        const int qx = horz ? bch[BX] + k : bch[BX], qy = horz ? bch[BY] : bch[BY] + k;
+        const int sizeQ = horz ? b[BH] : b[BW];
+        const int tp = horz ? get_tu(qx, qy - 1, ch) : get_tu(qx - 1, qy, ch);
+        const int sizeP = horz ? d.tu[tp].b[comp][BH] : d.tu[tp].b[comp][BW];
+        const int X = horz ? xo + k : xo, Y = horz ? yo : yo + k;
+        if (comp == 0) {
+          tedge[X][Y] = 1;
+          const bool small = sizeP <= 4 || sizeQ <= 4;
+          lenQ[0][X][Y] = small ? 1 : (sizeQ >= 32 ? 7 : 3);
+          lenP[0][X][Y] = small ? 1 : (sizeP >= 32 ? 7 : 3);
+        } else {
+          lenQ[comp][X][Y] = lenP[comp][X][Y] = (sizeQ >= 8 && sizeP >= 8) ? 3 : 1;
+        }
+      }
+    }
+  }
+
+  void len_subblocks(int dir, const vvcr_pu &pu, int w, int h) {
+    const int xo = pu.x - ctu_x, yo = pu.y - ctu_y;
+    auto &Q = lenQ[0];
+    auto &P = lenP[0];
+    const bool horz = dir == HOR;
+    const int outer = horz ? h : w, inner = horz ? w : h;
+    for (int a = 0; a < outer; a += 8)
+      for (int b = 0; b < inner; b += 4) {
+        const int X = horz ? xo + b : xo + a, Y = horz ? yo + a : yo + b;
+        auto T = [&](int delta) { return horz ? tedge[X][Y + delta] : tedge[X + delta][Y]; };
+        if (T(0)) {
+          if (Q[X][Y] > 5) Q[X][Y] = 5;
+          if (a > 0 && P[X][Y] > 5) P[X][Y] = 5;
+        } else if (a > 0 && (T(-4) || a + 4 >= outer || T(4))) {
+          Q[X][Y] = P[X][Y] = 1;
+        } else if (a > 0 && (T(-8) || a + 8 >= outer || T(8))) {
+          Q[X][Y] = P[X][Y] = 2;
+        } else {
+          Q[X][Y] = P[X][Y] = 3;
+        }
+      }
+  }
+
+  static int bs_set(int v, int comp) { return v << (comp * 2); }
+
+  int boundary_strength(int cui, int dir, int lx, int ly) const {
+    const vvcr_cu &cuQ = d.cu[cui];
+    const int ch = cuQ.chtype;
+    const int sh = cuQ.yvalid ? 0 : 1;
+    const int qx = lx >> sh, qy = ly >> sh;
+    const int px = dir == VER ? qx - 1 : qx, py = dir == VER ? qy : qy - 1;
+    const vvcr_cu &cuP = d.cu[get_cu(px, py, ch)];
+    if (cuP.predmode == MODE_INTRA || cuQ.predmode == MODE_INTRA) {
+      const int bsY = (cuP.predmode == MODE_INTRA && cuP.bdpcm) && (cuQ.predmode == MODE_INTRA && cuQ.bdpcm) ? 0 : 2;
+      const int bsC = (cuP.predmode == MODE_INTRA && cuP.bdpcmc) && (cuQ.predmode == MODE_INTRA && cuQ.bdpcmc) ? 0 : 2;
+      return bs_set(bsY, 0) + bs_set(bsC, 1) + bs_set(bsC, 2);
+    }
+    const vvcr_tu &tq = d.tu[get_tu(qx, qy, ch)], &tp = d.tu[get_tu(px, py, ch)];
+    const int marker = bs[dir][raster(lx, ly)];
+    const bool ciip = d.pu[cuP.firstpu].ciip || d.pu[cuQ.firstpu].ciip;
+    if (marker && ciip) return bs_set(2, 0) + bs_set(2, 1) + bs_set(2, 2);
+    int tmp = 0;
+    if (marker && (tq.b[0][BCBF] || tp.b[0][BCBF])) tmp += bs_set(1, 0);
+    if (marker && (tq.b[1][BCBF] || tp.b[1][BCBF] || tq.jccr || tp.jccr)) tmp += bs_set(1, 1);
+    if (marker && (tq.b[2][BCBF] || tp.b[2][BCBF] || tq.jccr || tp.jccr)) tmp += bs_set(1, 2);
+    if ((tmp & 3) == 1) return tmp;
+    if (ciip) return 1;
+    if (!cuQ.yvalid) return tmp;
+    if (marker != 0 && marker != 3) return tmp;
+    const int lpx = dir == VER ? lx - 1 : lx, lpy = dir == VER ? ly : ly - 1;
+    const vvcr_motion &mq = d.motion[(size_t)(ly >> 2) * W4 + (lx >> 2)];
+    const vvcr_motion &mp = d.motion[(size_t)(lpy >> 2) * W4 + (lpx >> 2)];
+    const int th = 8;
+    if (pp.slice_type == 0) {
+      // Picture identity: entries of the lists with equal POC are the same decoded picture.
+      const int NONE = INT32_MIN;
+      const int rP0 = mp.ref0 >= 0 ? pp.ref_poc[0][mp.ref0] : NONE, rP1 = mp.ref1 >= 0 ? pp.ref_poc[1][mp.ref1] : NONE;
+      const int rQ0 = mq.ref0 >= 0 ? pp.ref_poc[0][mq.ref0] : NONE, rQ1 = mq.ref1 >= 0 ? pp.ref_poc[1][mq.ref1] : NONE;
+      const int p0x = mp.ref0 >= 0 ? mp.mv0x : 0, p0y = mp.ref0 >= 0 ? mp.mv0y : 0;
+      const int p1x = mp.ref1 >= 0 ? mp.mv1x : 0, p1y = mp.ref1 >= 0 ? mp.mv1y : 0;
+      const int q0x = mq.ref0 >= 0 ? mq.mv0x : 0, q0y = mq.ref0 >= 0 ? mq.mv0y : 0;
+      const int q1x = mq.ref1 >= 0 ? mq.mv1x : 0, q1y = mq.ref1 >= 0 ? mq.mv1y : 0;
+      int b;
+      if ((rP0 == rQ0 && rP1 == rQ1) || (rP0 == rQ1 && rP1 == rQ0)) {
+        const bool s00 = std::abs(q0x - p0x) >= th || std::abs(q0y - p0y) >= th || std::abs(q1x - p1x) >= th || std::abs(q1y - p1y) >= th;
+        const bool s01 = std::abs(q1x - p0x) >= th || std::abs(q1y - p0y) >= th || std::abs(q0x - p1x) >= th || std::abs(q0y - p1y) >= th;
+        b = rP0 != rP1 ? (rP0 == rQ0 ? s00 : s01) : (s00 && s01);
+      } else {
+        b = 1;
+      }
+      return b + tmp;
+    }
+    if (mp.ref0 < 0 || mq.ref0 < 0) throw VvcrError(VVCR_E_ARG, "deblocking: P-slice inter block without list-0 reference");
+    if (pp.ref_poc[0][mp.ref0] != pp.ref_poc[0][mq.ref0]) return tmp + 1;
+    return (std::abs(mq.mv0x - mp.mv0x) >= th || std::abs(mq.mv0y - mp.mv0y) >= th) ? tmp + 1 : tmp;
+  }
+
+  // QpParam(tu, comp).Qp(0) - qpBdOffset (Quant.cpp:65-138); joint Cb-Cr mode 3 uses the JOINT_CbCr tables
+  int chroma_qp(int t, int comp) const {
+    const int qpy = d.cu[d.tu[t].cu].qp;
+    const bool jqp = d.tu[t].jccr == 3;
+    const int off = jqp ? pp.chroma_qp_off[0] : pp.chroma_qp_off[comp];
+    const int32_t *map = pp.chroma_qp_map[jqp ? 0 : comp];
+    const int qbd = 6 * (sp.bit_depth - 8);
+    int q = map[std::clamp(qpy, -qbd, 63) + 64];
+    q = std::clamp(q + off, -qbd, 63) + qbd;
+    q = std::clamp(q, 0, 63 + qbd);
+    return q - qbd;
+  }
+
+  void emit_luma(int cui, int dir, int e) {
+    const vvcr_cu &cu = d.cu[cui];
+    const int n = dir == VER ? cu.h / 4 : cu.w / 4;
+    for (int i = 0; i < n; i++) {
+      const int px = dir == VER ? cu.x + e * 4 : cu.x + i * 4;
+      const int py = dir == VER ? cu.y + i * 4 : cu.y + e * 4;
+      const int b = bs[dir][raster(px, py)] & 3;
+      if (!b) continue;
+      const vvcr_cu &cuP = d.cu[get_cu(dir == VER ? px - 1 : px, dir == VER ? py : py - 1, cu.chtype)];
+      const int qp = (cuP.qp + cu.qp + 1) >> 1;
+      int lp = lenP[0][px - ctu_x][py - ctu_y], lq = lenQ[0][px - ctu_x][py - ctu_y];
+      bool pl = false, ql = false;
+      if (lp > 3) {
+        pl = true;
+        if (lp > 5 && cuP.affine) lp = 5;
+      }
+      if (lq > 3) ql = true;
+      if (dir == HOR && py % ctu == 0) pl = false;
+      DbkSeg s;
+      s.x4 = (uint16_t)(px >> 2);
+      s.y4 = (uint16_t)(py >> 2);
+      s.w = (uint32_t)b | (uint32_t)lp << 2 | (uint32_t)lq << 5 | (uint32_t)(qp & 63) << 8 | (uint32_t)pl << 14 | (uint32_t)ql << 15;
+      out.luma[dir].push_back(s);
+    }
+  }
+
+  void emit_chroma(int cui, int dir, int e) {
+    const vvcr_cu &cu = d.cu[cui];
+    int a[4];
+    cu_area(cu, a);
+    const int r = raster(a[0], a[1]);
+    if ((dir == VER && (r % parts + e) % 4) || (dir == HOR && (r / parts + e) % 4)) return;
+    const int n = dir == VER ? a[3] / 4 : a[2] / 4;
+    for (int i = 0; i < n; i++) {
+      const int px = dir == VER ? a[0] + e * 4 : a[0] + i * 4;
+      const int py = dir == VER ? a[1] + i * 4 : a[1] + e * 4;
+      const int v = bs[dir][raster(px, py)];
+      const int bS[2] = {(v >> 2) & 3, (v >> 4) & 3};
+      if (!bS[0] && !bS[1]) continue;
+      const int nlx = dir == VER ? px - 4 : px, nly = dir == VER ? py : py - 4;
+      int cpi = cu.chtype ? get_cu(nlx >> 1, nly >> 1, 1) : get_cu(nlx, nly, 0);
+      if (d.cu[cpi].treetype != 0 || pp.dual_tree) cpi = get_cu(nlx >> 1, nly >> 1, 1);
+      const vvcr_cu &cuP = d.cu[cpi];
+      const int cx = (px - ctu_x) >> 1, cy = (py - ctu_y) >> 1;
+      const bool large = lenP[1][cx][cy] >= 3 && lenQ[1][cx][cy] >= 3;
+      const bool ctbh = dir == HOR && py % ctu == 0;
+      uint32_t w = (uint32_t)large << 4 | (uint32_t)ctbh << 19;
+      bool any = false;
+      for (int k = 0; k < 2; k++) {
+        if (!(bS[k] == 2 || (large && bS[k] == 1))) continue;
+        const int comp = k + 1;
+        const int shP = cuP.yvalid ? 0 : 1, shQ = cu.yvalid ? 0 : 1;
+        const int tq = get_tu(px >> shQ, py >> shQ, cu.chtype);
+        const int p1x = px >> shP, p1y = py >> shP;
+        const int tp = get_tu(dir == VER ? p1x - 1 : p1x, dir == VER ? p1y : p1y - 1, cuP.chtype);
+        const int qp = (chroma_qp(tq, comp) + chroma_qp(tp, comp) + 1) >> 1;
+        w |= (uint32_t)bS[k] << (2 * k) | (uint32_t)((qp + 64) & 127) << (5 + 7 * k);
+        any = true;
+      }
+      if (!any) continue;
+      DbkSeg s;
+      s.x4 = (uint16_t)(px >> 2);
+      s.y4 = (uint16_t)(py >> 2);
+      s.w = w;
+      out.chroma[dir].push_back(s);
+    }
+  }
+
+  void deblock_cu(int cui, int dir) {
+    const vvcr_cu &cu = d.cu[cui];
+    int a[4];
+    cu_area(cu, a);
+    const int ch = cu.chtype;
+    const int cpx = ch ? cu.cx : cu.x, cpy = ch ? cu.cy : cu.y;
+    if (pp.dbk_disable) { left = top = internal = false; }
+    else { internal = true; left = cpx > 0; top = cpy > 0; }
+    int edges[2 * 128 + 16], ne = 0;
+    for (int t = cu.firsttu; t < cu.firsttu + cu.ntu; t++) {
+      int ta[4];
+      if (cu.yvalid) { const int32_t *b = d.tu[t].b[0]; ta[0] = b[BX]; ta[1] = b[BY]; ta[2] = b[BW]; ta[3] = b[BH]; }
+      else std::memcpy(ta, a, sizeof ta);
+      set_edges(VER, ta[0], ta[1], ta[2], ta[3], internal, false);
+      set_edges(HOR, ta[0], ta[1], ta[2], ta[3], internal, false);
+      len_from_tu(dir, cu, t);
+      const int32_t *tb = d.tu[t].b[ch];
+      edges[ne++] = dir == HOR ? (tb[BY] - cpy) / 4 : (tb[BX] - cpx) / 4;
+    }
+    for (int pi = cu.firstpu; pi < cu.firstpu + cu.npu; pi++) {
+      const vvcr_pu &pu = d.pu[pi];
+      int pa[4];
+      if (cu.yvalid) { pa[0] = pu.x; pa[1] = pu.y; pa[2] = pu.w; pa[3] = pu.h; }
+      else std::memcpy(pa, a, sizeof pa);
+      const int pux = ch ? pu.cx : pu.x, puy = ch ? pu.cy : pu.y;
+      const bool xoff = pux != cpx, yoff = puy != cpy;
+      set_edges(VER, pa[0], pa[1], pa[2], pa[3], xoff ? internal : left, xoff);
+      set_edges(HOR, pa[0], pa[1], pa[2], pa[3], yoff ? internal : top, yoff);
+      edges[ne++] = dir == HOR ? (puy - cpy) / 4 : (pux - cpx) / 4;
+      if ((pu.merge && pu.mrgtype == MRG_TYPE_SUBPU_ATMVP) || cu.affine) {
+        if (dir == HOR) {
+          for (int off = 8; off < pa[3]; off += 8) {
+            set_edges(HOR, cu.x, cu.y + off, cu.w, 4, internal, true);
+            edges[ne++] = (puy + off - cpy) / 4;
+          }
+        } else {
+          for (int off = 8; off < pa[2]; off += 8) {
+            set_edges(VER, cu.x + off, cu.y, 4, cu.h, internal, true);
+            edges[ne++] = (pux + off - cpx) / 4;
+          }
+        }
+        if (pu.w > 0) len_subblocks(dir, pu, pa[2], pa[3]);
+      }
+    }
+    for (int y = 0; y < a[3]; y += 4)
+      for (int x = 0; x < a[2]; x += 4) {
+        const int r = raster(a[0] + x, a[1] + y);
+        if (edge[dir][r]) bs[dir][r] = (uint8_t)boundary_strength(cui, dir, a[0] + x, a[1] + y);
+      }
+    std::sort(edges, edges + ne);
+    int prev = -1;
+    for (int k = 0; k < ne; k++) {
+      if (edges[k] == prev) continue;
+      prev = edges[k];
+      if (cu.yvalid) emit_luma(cui, dir, edges[k]);
+      if (cu.cvalid && (!cu.isp || edges[k] == 0)) emit_chroma(cui, dir, edges[k]);
+    }
+  }
+
+  void reset(int dir) {
+    std::memset(bs[dir], 0, sizeof bs[dir]);
+    std::memset(edge[dir], 0, sizeof edge[dir]);
+    std::memset(lenP, 0, sizeof lenP);
+    std::memset(lenQ, 0, sizeof lenQ);
+    std::memset(tedge, 0, sizeof tedge);
+  }
+
+  void run() {
+    build_maps();
+    const int wc = (sp.width + ctu - 1) / ctu, hc = (sp.height + ctu - 1) / ctu;
+    const int ncu = (int)d.cu.size();
+    std::vector<int> start((size_t)wc * hc + 1, 0), order(ncu), ctu_of(ncu);
+    for (int i = 0; i < ncu; i++) {
+      int a[4];
+      cu_area(d.cu[i], a);
+      ctu_of[i] = (a[1] >> sp.ctu_log2) * wc + (a[0] >> sp.ctu_log2);
+      start[ctu_of[i] + 1]++;
+    }
+    for (int k = 0; k < wc * hc; k++) start[k + 1] += start[k];
+    {
+      std::vector<int> pos(start);
+      for (int i = 0; i < ncu; i++) order[pos[ctu_of[i]]++] = i;
+    }
+    for (int dir = 0; dir < 2; dir++)
+      for (int k = 0; k < wc * hc; k++) {
+        ctu_x = (k % wc) * ctu;
+        ctu_y = (k / wc) * ctu;
+        for (int pass = 0; pass < (pp.dual_tree ? 2 : 1); pass++) {
+          reset(dir);
+          for (int j = start[k]; j < start[k + 1]; j++) {
+            const int i = order[j];
+            if (pp.dual_tree && d.cu[i].chtype != pass) continue;
+            deblock_cu(i, dir);
+          }
+        }
+      }
+  }
+};
+
+}  // namespace
+
+void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkLists &out) {
+  out.clear();
+  if (pp.dbk_disable) return;
+  if (sp.width % 8 || sp.height % 8) throw VvcrError(VVCR_E_UNSUPPORTED, "deblocking: picture size not a multiple of 8");
+  auto P = std::make_unique<Planner>(sp, pp, d, out);   // ~200 KB of per-CTU state: keep it off the stack
+  P->run();
+}

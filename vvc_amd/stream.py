@@ -77,9 +77,11 @@ def pic_params(p, slot, slot_of):
     pp.use_mts, pp.implicit_mts, pp.joint_cbcr_sign = h["use_mts"], h["implicit_mts"], h["joint_cbcr_sign"]
     pp.max_tb_log2 = int(h["max_tb_size"]).bit_length() - 1
     pp.chroma_qp_off[1], pp.chroma_qp_off[2] = h["chroma_qp_off_cb"], h["chroma_qp_off_cr"]
+    pp.chroma_qp_off[0] = h["chroma_qp_off_jc"]
     wp = np.ascontiguousarray(p["wp"], np.int32)
     np.copyto(np.ctypeslib.as_array(pp.wp).reshape(wp.shape), wp)
-    cqm = np.ascontiguousarray(p["chroma_qp_map"], np.int32)
+    cqm = np.array(p["chroma_qp_map"], np.int32)
+    cqm[0] = p["chroma_qp_map_jc"]          # row 0 carries the joint Cb-Cr table (vvcr.h)
     np.copyto(np.ctypeslib.as_array(pp.chroma_qp_map).reshape(cqm.shape), cqm)
     for c in range(3):
         pp.alf_en[c] = h["alf_slice_en%d" % c]
