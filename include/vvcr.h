@@ -182,7 +182,10 @@ int vvcr_sync(vvcr_ctx *ctx);
 int vvcr_read_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, int16_t *dst, int32_t dst_stride);
 int vvcr_write_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, const int16_t *src, int32_t src_stride);
 int vvcr_read_picture(vvcr_ctx *ctx, int32_t slot, uint16_t *planes[3], const int32_t strides[3]);
-/* DMVR refined deltas per PU sub-block, [npu][64][2] (PredictionUnit::mvdL0SubPu). Blocks. */
+/* DMVR refinement deltas of the last picture (PredictionUnit::mvdL0SubPu, 1/16 luma sample): one
+ * {dx, dy} per 16x16 DMVR sub-block, PUs in descriptor order, sub-blocks in raster order inside each PU
+ * (xProcessDMVR InterPrediction.cpp:2162-2296). Copies min(n, count) pairs into out and returns the
+ * count (>= 0) or a negative error. Blocks until the picture's motion compensation has run. */
 int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n);
 
 /* Timing of the last vvcr_end_picture*, in ms (HIP events on the library stream): ms[0] = whole call,

@@ -372,10 +372,6 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
       for (int k = 0; k < 3; k++) { o[PU_AFF0 + (l * 3 + k) * 2] = pu.mvAffi[l][k].hor; o[PU_AFF0 + (l * 3 + k) * 2 + 1] = pu.mvAffi[l][k].ver; }
     o[PU_DMVR_OFF] = -1;
     bool isInterPU = CU::isInter(*pu.cu);
-    if (isInterPU && pu.mvRefine) {
-      o[PU_DMVR_OFF] = (int32_t)(dmvrPool.size() / 2);
-      for (int k = 0; k < MAX_NUM_SUBCU_DMVR; k++) { dmvrPool.push_back(pu.mvdL0SubPu[k].hor); dmvrPool.push_back(pu.mvdL0SubPu[k].ver); }
-    }
     // reference decisions (InterPrediction.cpp:1584-1638): motionCompensation(cu) sets mvRefine=true around MC
     if (isInterPU && pu.interDir == 3 && !pu.cu->geoFlag) {
       PredictionUnit &mp = const_cast<PredictionUnit &>(pu);
@@ -393,6 +389,14 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
         if (pu.ciipFlag || pu.cu->smvdMode || (sps.getUseBcw() && pu.cu->BcwIdx != BCW_DEFAULT)) bio = false;
       }
       o[PU_BDOF] = bio ? 1 : 0;
+    }
+    // DMVR refinement deltas per 16x16 sub-block (still held in mvdL0SubPu until CS::setRefinedMotionField,
+    // which runs after deblocking: DecLib.cpp:579-580), in xProcessDMVR raster order
+    if (o[PU_DMVR]) {
+      o[PU_DMVR_OFF] = (int32_t)(dmvrPool.size() / 2);
+      const int dy = std::min<int>(pu.lumaSize().height, DMVR_SUBCU_HEIGHT), dx = std::min<int>(pu.lumaSize().width, DMVR_SUBCU_WIDTH);
+      const int n = (pu.lumaSize().height / dy) * (pu.lumaSize().width / dx);
+      for (int k = 0; k < n; k++) { dmvrPool.push_back(pu.mvdL0SubPu[k].hor); dmvrPool.push_back(pu.mvdL0SubPu[k].ver); }
     }
   }
   TR("pu table");

@@ -33,3 +33,7 @@ def is_basic_mc(c, pus):
         if p[PU["dmvr"]] or p[PU["bdof"]]:
             return False
     return True
+
+
+def is_inter(c, pus):
+    return c[CU["predmode"]] == 0

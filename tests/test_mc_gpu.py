@@ -9,13 +9,14 @@ import pytest
 
 from vvc_amd import native as N
 from vvc_amd import stream as S
-from helpers import cu_mask, is_basic_mc
+from helpers import cu_mask, is_inter
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("name", ["ra416_q32"])
-def test_mc_basic_matches_reference(golden_dir, name):
+def test_mc_matches_reference(golden_dir, name):
+    """Every inter CU (uni/bi/BCW, SbTMVP, GEO, affine+PROF, DMVR, BDOF) and the DMVR deltas."""
     d = os.path.join(golden_dir, name)
     pics = S.load_sequence(d)
     by_poc = {p["hdr"]["poc"]: p for p in pics}
@@ -37,9 +38,12 @@ def test_mc_basic_matches_reference(golden_dir, name):
         ctx.begin_picture(S.pic_params(p, 0, slot_of))
         S.submit(ctx, p)
         ctx.end_picture(N.STAGE_INTER)
+        exp_d = p["dmvr_delta"].reshape(-1, 2)
+        got_d = ctx.dmvr_deltas()
+        assert got_d.shape == exp_d.shape and (got_d == exp_d).all(), "POC %d DMVR deltas differ" % p["hdr"]["poc"]
         for c, pl in enumerate("yuv"):
             got = ctx.read_plane(N.BUF_PRED, 0, c)
-            m = cu_mask(p, is_basic_mc, c)
+            m = cu_mask(p, is_inter, c)
             exp = p["pmc_" + pl]
             bad = (got != exp) & m
             assert not bad.any(), "POC %d comp %s: %d/%d samples differ, first at %s" % (

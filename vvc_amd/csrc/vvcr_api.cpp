@@ -54,7 +54,11 @@ struct vvcr_ctx {
   bool in_picture = false;
   PictureDescriptors desc;          // host copy of the submitted descriptors (vvcr_host.h)
   WorkLists wl;                     // host-built work lists
-  DevVec<McJob> d_mc_basic;
+  DevVec<McJob> d_mc_basic, d_mc_bidir;
+  DevVec<AffPu> d_aff_pu;
+  DevVec<AffJob> d_aff_jobs;
+  DevVec<int32_t> d_dmvr;           // DMVR deltas of the last picture, [n][2]
+  int n_dmvr = 0;
   DevVec<TbJob> d_tb;
   DevVec<int32_t> d_coef;
   DevVec<uint16_t> d_scans;
@@ -222,6 +226,7 @@ static McParams make_mc_params(vvcr_ctx *ctx) {
   P.pic_w = ctx->sp.width;
   P.pic_h = ctx->sp.height;
   P.bd = ctx->sp.bit_depth;
+  P.ctu = 1 << ctx->sp.ctu_log2;
   return P;
 }
 
@@ -263,8 +268,20 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
   }
   if (mask & VVCR_STAGE_INTER) {
     StageTimer t(ctx, ST_INTER);
+    if (ctx->wl.n_unsupported_inter)
+      throw VvcrError(VVCR_E_UNSUPPORTED, std::to_string(ctx->wl.n_unsupported_inter) + " inter CUs use tools not supported yet");
+    const McParams mp = make_mc_params(ctx);
     ctx->d_mc_basic.upload(ctx->wl.mc_basic, s);
-    launch_mc_basic(make_mc_params(ctx), ctx->d_mc_basic.p, (int)ctx->wl.mc_basic.size(), s);
+    launch_mc_basic(mp, ctx->d_mc_basic.p, (int)ctx->wl.mc_basic.size(), s);
+    VVCR_CHECK_HIP(hipGetLastError());
+    ctx->n_dmvr = ctx->wl.n_dmvr;
+    ctx->d_dmvr.ensure(2 * (size_t)ctx->n_dmvr + 2);
+    ctx->d_mc_bidir.upload(ctx->wl.mc_bidir, s);
+    launch_mc_bidir(mp, ctx->d_mc_bidir.p, (int)ctx->wl.mc_bidir.size(), ctx->d_dmvr.p, s);
+    VVCR_CHECK_HIP(hipGetLastError());
+    ctx->d_aff_pu.upload(ctx->wl.aff_pu, s);
+    ctx->d_aff_jobs.upload(ctx->wl.aff_jobs, s);
+    launch_mc_affine(mp, ctx->d_aff_jobs.p, (int)ctx->wl.aff_jobs.size(), ctx->d_aff_pu.p, s);
     VVCR_CHECK_HIP(hipGetLastError());
   }
   // ---- deblocking, in place on the picture slot: all vertical edges, then all horizontal edges
@@ -399,8 +416,15 @@ int vvcr_read_picture(vvcr_ctx *ctx, int32_t slot, uint16_t *planes[3], const in
 
 int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n) {
   if (!ctx || (!out && n)) return VVCR_E_ARG;
-  ctx->err = "DMVR delta readback not implemented yet";
-  return VVCR_E_UNSUPPORTED;
+  API_BEGIN
+  if (n < 0) throw VvcrError(VVCR_E_ARG, "negative count");
+  const int64_t m = std::min<int64_t>(n, ctx->n_dmvr);
+  if (m > 0) {
+    VVCR_CHECK_HIP(hipMemcpyAsync(out, ctx->d_dmvr.p, (size_t)m * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  return (int)ctx->n_dmvr;
+  API_END
 }
 
 }  // extern "C"

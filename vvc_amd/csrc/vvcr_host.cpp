@@ -14,6 +14,7 @@ constexpr int MRG_TYPE_DEFAULT_N = 0, MRG_TYPE_SUBPU_ATMVP = 1;
 constexpr int B_SLICE = 0;       // SliceType (TypeDef.h): B_SLICE=0, P_SLICE=1, I_SLICE=2
 
 void fail(const std::string &m) { throw VvcrError(VVCR_E_ARG, m); }
+int ilog2i(int v) { int r = 0; while ((1 << (r + 1)) <= v) r++; return r; }
 
 // InterPrediction::xCheckIdenticalMotion (InterPrediction.cpp:248): bi-prediction from the same
 // picture with the same MV is predicted as uni-prediction from list 0.
@@ -85,28 +86,174 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
 
 void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, std::vector<TbJob> &out);
 
+namespace {
+
+// initGeoTemplate (Rom.cpp:760-777): split mode -> (angle, distance)
+struct GeoModes {
+  int16_t angle[64], dist[64];
+  GeoModes() {
+    static const int8_t a2m[32] = {0, -1, 1, 2, 3, 4, -1, -1, 5, -1, -1, 4, 3, 2, 1, -1, 0, -1, 1, 2, 3, 4, -1, -1, 5, -1, -1, 4, 3, 2, 1, -1};
+    int m = 0;
+    for (int a = 0; a < 32; a++)
+      for (int d = 0; d < 4; d++) {
+        if ((d == 0 && a >= 16) || ((d == 2 || d == 0) && (a2m[a] == 0 || a2m[a] == 5)) || a2m[a] == -1) continue;
+        if (m < 64) { angle[m] = (int16_t)a; dist[m] = (int16_t)d; }
+        m++;
+      }
+  }
+};
+const GeoModes &geo_modes() {
+  static const GeoModes g;
+  return g;
+}
+
+// InterPrediction::isSubblockVectorSpreadOverLimit (InterPrediction.cpp:850)
+bool spread_over_limit(int a, int b, int c, int d, int predType) {
+  const int s4 = 4 << 11, tap = 6;
+  if (predType == 3) {
+    int W = std::max(std::max(0, 4 * a + s4), std::max(4 * c, 4 * a + 4 * c + s4)) - std::min(std::min(0, 4 * a + s4), std::min(4 * c, 4 * a + 4 * c + s4));
+    int H = std::max(std::max(0, 4 * b), std::max(4 * d + s4, 4 * b + 4 * d + s4)) - std::min(std::min(0, 4 * b), std::min(4 * d + s4, 4 * b + 4 * d + s4));
+    W = (W >> 11) + tap + 3;
+    H = (H >> 11) + tap + 3;
+    return W * H > (tap + 9) * (tap + 9);
+  }
+  int W = std::max(0, 4 * a + s4) - std::min(0, 4 * a + s4), H = std::max(0, 4 * b) - std::min(0, 4 * b);
+  W = (W >> 11) + tap + 3;
+  H = (H >> 11) + tap + 3;
+  if (W * H > (tap + 9) * (tap + 5)) return true;
+  W = std::max(0, 4 * c) - std::min(0, 4 * c);
+  H = std::max(0, 4 * d + s4) - std::min(0, 4 * d + s4);
+  W = (W >> 11) + tap + 3;
+  H = (H >> 11) + tap + 3;
+  return W * H > (tap + 5) * (tap + 9);
+}
+
+// affine model of one list (xPredAffineBlk :917-960)
+AffList affine_list(const vvcr_pic_params &pp, const vvcr_cu &c, const vvcr_pu &p, int l) {
+  AffList A{};
+  const int ref = l ? p.ref1 : p.ref0;
+  A.present = 1;
+  A.slot = pp.ref_slot[l][ref];
+  const int *mv = &p.aff[l * 6];   // LT, RT, LB
+  const int iBit = 7;
+  const int lw = ilog2i(p.w), lh = ilog2i(p.h);
+  A.dhx = (mv[2] - mv[0]) << (iBit - lw);
+  A.dhy = (mv[3] - mv[1]) << (iBit - lw);
+  if (c.affinetype == 1) {   // AFFINEMODEL_6PARAM
+    A.dvx = (mv[4] - mv[0]) << (iBit - lh);
+    A.dvy = (mv[5] - mv[1]) << (iBit - lh);
+  } else {
+    A.dvx = -A.dhy;
+    A.dvy = A.dhx;
+  }
+  A.mvx = mv[0] * (1 << iBit);
+  A.mvy = mv[1] * (1 << iBit);
+  A.spread = spread_over_limit(A.dhx, A.dhy, A.dvx, A.dvy, p.interdir);
+  const bool same = c.affinetype == 1 ? (mv[0] == mv[2] && mv[1] == mv[3] && mv[0] == mv[4] && mv[1] == mv[5])
+                                      : (mv[0] == mv[2] && mv[1] == mv[3]);
+  A.prof = pp.prof_enabled && !same && !A.spread;
+  return A;
+}
+
+}  // namespace
+
 void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl) {
   wl.clear();
   build_tb_jobs(sp, pp, d, wl.tb);
   const int W4 = sp.width / 4;
-  for (const vvcr_cu &c : d.cu) {
+  std::vector<int> geo_of(d.cu.size(), -1);
+  for (size_t g = 0; g < d.geo.size(); g++)
+    if (d.geo[g].cu >= 0 && d.geo[g].cu < (int)d.cu.size()) geo_of[d.geo[g].cu] = (int)g;
+  if ((pp.slice_type == 1 && pp.wp_p) || (pp.slice_type == B_SLICE && pp.wp_b)) {
+    for (const vvcr_cu &c : d.cu) if (c.predmode == MODE_INTER && c.yvalid) wl.n_unsupported_inter++;
+    return;   // explicit weighted prediction: not built yet
+  }
+  for (size_t ci = 0; ci < d.cu.size(); ci++) {
+    const vvcr_cu &c = d.cu[ci];
     if (c.predmode != MODE_INTER || !c.yvalid) continue;
-    if (c.geo || c.affine) { wl.n_unsupported_inter++; continue; }
+    if (c.geo) {
+      // motionCompensationGeo (InterPrediction.cpp:1749): two uni candidates at 14 bits, blended
+      const vvcr_pu &p = d.pu[c.firstpu];
+      if (geo_of[ci] < 0 || p.geodir < 0 || p.geodir >= 64) { wl.n_unsupported_inter++; continue; }
+      const vvcr_geo &g = d.geo[geo_of[ci]];
+      McJob j{};
+      j.flags = MC_L0 | MC_L1 | MC_LUMA | MC_CHROMA | MC_GEO;
+      for (int k = 0; k < 2; k++) {
+        const int l = g.cand[k][1], r = g.cand[k][2];
+        if (l < 0 || l > 1 || r < 0 || r >= pp.num_ref[l]) fail("GEO candidate reference");
+        j.slot[k] = (int8_t)pp.ref_slot[l][r];
+        j.mv[k][0] = (int16_t)g.cand[k][3];
+        j.mv[k][1] = (int16_t)g.cand[k][4];
+      }
+      const GeoModes &gm = geo_modes();
+      const int angle = gm.angle[p.geodir], dist = gm.dist[p.geodir];
+      int offX = (224 - p.w) >> 1, offY = (224 - p.h) >> 1;   // InitGeoTemplate weight offsets (Rom.cpp:807-826)
+      if (dist > 0) {
+        if (angle % 16 == 8 || (angle % 16 != 0 && p.h >= p.w)) offY += angle < 16 ? ((dist * p.h) >> 3) : -((dist * p.h) >> 3);
+        else offX += angle < 16 ? ((dist * p.w) >> 3) : -((dist * p.w) >> 3);
+      }
+      j.aux = angle | offX << 8 | offY << 16;
+      j.pu_x = (int16_t)p.x;
+      j.pu_y = (int16_t)p.y;
+      j.bcw = 2;
+      push_tiles(wl.mc_basic, p.x, p.y, p.w, p.h, j);
+      continue;
+    }
     for (int k = 0; k < c.npu; k++) {
       const vvcr_pu &p = d.pu[c.firstpu + k];
       const bool alt = c.imv == IMV_HPEL;
       const int bcw = p.ciip ? 2 : c.bcw;   // BCW is not applied to CIIP (InterPrediction.cpp:1397)
       if (p.mrgtype == MRG_TYPE_SUBPU_ATMVP) {
         // xSubPuMC (InterPrediction.cpp:289): 8x8 sub-blocks with their own motion, no BDOF / DMVR
+        // (SbTMVP candidates of the sub-block merge list also carry cu.affine; the merge type decides)
         for (int y = 0; y < p.h; y += 8)
           for (int x = 0; x < p.w; x += 8) {
             const vvcr_motion &m = d.motion[(size_t)((p.y + y) >> 2) * W4 + ((p.x + x) >> 2)];
-            McJob j = make_job(pp, m.inter_dir, m.ref0, m.ref1, m.mv0x, m.mv0y, m.mv1x, m.mv1y, m.bcw, alt);
+            McJob j = make_job(pp, m.inter_dir, m.ref0, m.ref1, m.mv0x, m.mv0y, m.mv1x, m.mv1y, bcw, alt);   // BCW of the CU (xWeightedAverage reads pu.cu->BcwIdx)
             push_tiles(wl.mc_basic, p.x + x, p.y + y, std::min(8, p.w - x), std::min(8, p.h - y), j);
           }
         continue;
       }
-      if (p.dmvr || p.bdof) { wl.n_unsupported_inter++; continue; }
+      if (c.affine) {
+        AffPu U{};
+        U.x = (int16_t)p.x; U.y = (int16_t)p.y; U.w = (int16_t)p.w; U.h = (int16_t)p.h;
+        U.bcw = bcw;
+        if (p.interdir & 1) U.l[0] = affine_list(pp, c, p, 0);
+        if (p.interdir & 2) U.l[1] = affine_list(pp, c, p, 1);
+        const int idx = (int)wl.aff_pu.size();
+        wl.aff_pu.push_back(U);
+        for (int y = 0; y < p.h; y += 16)
+          for (int x = 0; x < p.w; x += 16) {
+            AffJob j{};
+            j.x = (int16_t)(p.x + x); j.y = (int16_t)(p.y + y);
+            j.w = (uint8_t)std::min(16, p.w - x); j.h = (uint8_t)std::min(16, p.h - y);
+            j.pu = idx;
+            wl.aff_jobs.push_back(j);
+          }
+        continue;
+      }
+      if (p.dmvr || p.bdof) {
+        McJob j = make_job(pp, p.interdir, p.ref0, p.ref1, p.mv0x, p.mv0y, p.mv1x, p.mv1y, bcw, alt);
+        if ((j.flags & (MC_L0 | MC_L1)) != (MC_L0 | MC_L1)) fail("DMVR/BDOF PU is not bi-predicted");
+        if (p.bdof) j.flags |= MC_BDOF;
+        if (p.dmvr) {
+          // xProcessDMVR sub-blocks (InterPrediction.cpp:2162-2166), raster order = delta order
+          j.flags |= MC_DMVR;
+          const int dx = std::min(16, p.w), dy = std::min(16, p.h);
+          for (int y = 0; y < p.h; y += dy)
+            for (int x = 0; x < p.w; x += dx) {
+              McJob t = j;
+              t.x = (int16_t)(p.x + x); t.y = (int16_t)(p.y + y);
+              t.w = (uint8_t)dx; t.h = (uint8_t)dy;
+              t.aux = wl.n_dmvr++;
+              wl.mc_bidir.push_back(t);
+            }
+        } else {
+          j.aux = -1;
+          push_tiles(wl.mc_bidir, p.x, p.y, p.w, p.h, j);   // xSubPuBio 16x16 split (InterPrediction.cpp:420)
+        }
+        continue;
+      }
       McJob j = make_job(pp, p.interdir, p.ref0, p.ref1, p.mv0x, p.mv0y, p.mv1x, p.mv1y, bcw, alt);
       push_tiles(wl.mc_basic, p.x, p.y, p.w, p.h, j);
     }

@@ -14,10 +14,17 @@ struct PictureDescriptors {
 };
 
 struct WorkLists {
-  std::vector<McJob> mc_basic;     // plain uni/bi/BCW blocks (incl. SbTMVP sub-blocks, CIIP inter part)
+  std::vector<McJob> mc_basic;     // plain uni/bi/BCW blocks (incl. SbTMVP sub-blocks, CIIP inter part, GEO)
+  std::vector<McJob> mc_bidir;     // DMVR sub-blocks and BDOF tiles
+  std::vector<AffPu> aff_pu;       // affine PUs
+  std::vector<AffJob> aff_jobs;    // affine tiles
   std::vector<TbJob> tb;           // coded transform blocks
+  int n_dmvr = 0;                  // DMVR sub-blocks (delta outputs), in PU order
   int n_unsupported_inter = 0;     // PUs needing kernels not built yet (reported, never silently skipped)
-  void clear() { mc_basic.clear(); tb.clear(); n_unsupported_inter = 0; }
+  void clear() {
+    mc_basic.clear(); mc_bidir.clear(); aff_pu.clear(); aff_jobs.clear(); tb.clear();
+    n_dmvr = 0; n_unsupported_inter = 0;
+  }
 };
 
 // Grouped diagonal scans (Rom.cpp:321-370) and the LFNST top-left 8x8 scan (Rom.cpp:385-403) as

@@ -38,7 +38,8 @@ enum : uint16_t {
   MC_ALT_HPEL = 1 << 4,  // 6-tap-smoothed half-pel luma filter (cu.imv == IMV_HPEL, InterpolationFilter.cpp:778)
   MC_BDOF = 1 << 5,      // bi-directional optical flow on luma (InterPrediction.cpp:1274)
   MC_DMVR = 1 << 6,      // decoder-side MV refinement of this 16x16 sub-block (InterPrediction.cpp:2133)
-  MC_KEEP14 = 1 << 7,    // write 14-bit intermediate (GEO parts) instead of final samples
+  MC_KEEP14 = 1 << 7,    // write 14-bit intermediate instead of final samples
+  MC_GEO = 1 << 8,       // two uni-predicted GEO parts blended by split weights (InterpolationFilter.cpp:997)
 };
 
 struct McJob {
@@ -49,16 +50,42 @@ struct McJob {
   int8_t slot[2];        // DPB slot per list
   int8_t bcw;            // BcwIdx (2 = default average)
   int8_t pad0;
-  int32_t aux;           // DMVR: index of this sub-block in the delta output buffer
-  int32_t pad1[2];
+  int32_t aux;           // DMVR: index of this sub-block in the delta output buffer;
+                         // GEO: angle | offsetX << 8 | offsetY << 16 (weight-mask coordinates)
+  int16_t pu_x, pu_y;    // GEO: PU origin (weights are PU-relative)
+  int32_t pad1;
 };
 static_assert(sizeof(McJob) == 32, "McJob layout");
+
+// Affine PU, per reference list: the sub-block MV field parameters of InterPrediction::xPredAffineBlk
+// (InterPrediction.cpp:890-960) precomputed on the host; sub-block MVs are derived on the device.
+struct AffList {
+  int32_t present, slot;
+  int32_t mvx, mvy;                    // mvLT << 7
+  int32_t dhx, dhy, dvx, dvy;          // iDMvHorX/Y, iDMvVerX/Y
+  int32_t spread;                      // isSubblockVectorSpreadOverLimit
+  int32_t prof;                        // PROF applies to luma
+};
+struct AffPu {
+  int16_t x, y, w, h;                  // luma PU area
+  int32_t bcw;                         // BcwIdx (2 = default)
+  AffList l[2];
+};
+// Affine work item: one <= 16x16 luma tile (8x8-aligned inside the PU) and its chroma.
+struct AffJob {
+  int16_t x, y;
+  uint8_t w, h;
+  uint16_t pad;
+  int32_t pu;                          // index into the AffPu table
+};
+static_assert(sizeof(AffJob) == 12, "AffJob layout");
 
 struct McParams {
   DPlane ref[32][3];     // DPB planes by slot (only used slots valid)
   DPlane out[3];         // destination (prediction planes of the current picture)
   int32_t pic_w, pic_h;  // luma picture size
   int32_t bd;            // bit depth
+  int32_t ctu;           // CTU size (affine MV clamp, InterPrediction.cpp:937)
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -109,7 +136,9 @@ struct AlfParams {
   const int16_t *ctb_set;
 };
 
-// launchers (vvcr_mc.hip, vvcr_resid.hip, vvcr_lf.hip)
+// launchers (vvcr_mc.hip, vvcr_mc_ext.hip, vvcr_resid.hip, vvcr_lf.hip)
+void launch_mc_bidir(const McParams &p, const McJob *jobs, int njobs, int32_t *dmvr_out, hipStream_t s);
+void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const AffPu *pus, hipStream_t s);
 void launch_sao(const SaoParams &p, hipStream_t s);
 void launch_alf(const AlfParams &p, hipStream_t s);
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, const int32_t *coef, const uint16_t *scans, hipStream_t s);

@@ -14,17 +14,37 @@
 
 namespace {
 
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
 __constant__ int8_t c_luma[16][8] = VVCR_LUMA_FILTER_TABLE;
 __constant__ int8_t c_luma4x4[16][8] = VVCR_LUMA4x4_FILTER_TABLE;
 __constant__ int8_t c_alt_hpel[8] = VVCR_LUMA_ALT_HPEL;
 __constant__ int8_t c_chroma[32][4] = VVCR_CHROMA_FILTER_TABLE;
 __constant__ int8_t c_bcw_w1[5] = VVCR_BCW_W1;
+// GEO split geometry (Rom.cpp g_angle2mask / g_Dis / g_angle2mirror, CommonDef.h GEO_* sizes)
+__constant__ int8_t c_geo_angle2mask[32] = {0, -1, 1, 2, 3, 4, -1, -1, 5, -1, -1, 4, 3, 2, 1, -1, 0, -1, 1, 2, 3, 4, -1, -1, 5, -1, -1, 4, 3, 2, 1, -1};
+__constant__ int8_t c_geo_dis[32] = {8, 8, 8, 8, 4, 4, 2, 1, 0, -1, -2, -4, -4, -8, -8, -8, -8, -8, -8, -8, -4, -4, -2, -1, 0, 1, 2, 4, 4, 8, 8, 8};
+__constant__ int8_t c_geo_angle2mirror[32] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 2, 2, 2, 2};
+__constant__ int8_t c_geo_mask_angle[6] = {0, 2, 3, 4, 5, 8};   // the angle in 0..8 that generated each stored mask
+constexpr int GEO_WEIGHT_MASK_SIZE = 224, GEO_MASK_OFFSET = 16;
+
+// Blending weight of one sample: the g_globalGeoWeights entry (Rom.cpp:778-801) that
+// InterpolationFilter::xWeightedGeoBlk (InterpolationFilter.cpp:1014-1046) walks to, computed in place.
+__device__ __forceinline__ int geo_weight(int angle, int offX, int offY, int lx, int ly) {
+  const int mir = c_geo_angle2mirror[angle];
+  const int X = mir == 1 ? GEO_WEIGHT_MASK_SIZE - 1 - offX - lx : offX + lx;
+  const int Y = mir == 2 ? GEO_WEIGHT_MASK_SIZE - 1 - offY - ly : offY + ly;
+  const int b = c_geo_mask_angle[c_geo_angle2mask[angle]];
+  const int dX = c_geo_dis[b], dY = c_geo_dis[(b + 8) & 31];
+  const int rho = (dX << 8) + (dY << 8);
+  const int wIdx = (((X + GEO_MASK_OFFSET) << 1) + 1) * dX + (((Y + GEO_MASK_OFFSET) << 1) + 1) * dY - rho;
+  return clampi((32 + wIdx + 4) >> 3, 0, 8);
+}
 
 constexpr int IF_INTERNAL_PREC = 14;
 constexpr int IF_FILTER_PREC = 6;
 constexpr int IF_INTERNAL_OFFS = 1 << (IF_INTERNAL_PREC - 1);
 
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // LDS budget per wave (one job per 64-thread workgroup)
 constexpr int WIN_STRIDE = 24;              // up to 16+7 = 23 columns
@@ -155,6 +175,13 @@ __device__ void mc_component(const McParams &P, const McJob &J, int comp, int16_
     int v;
     if (!bi) {
       v = r0[k];
+    } else if (J.flags & MC_GEO) {
+      // xWeightedGeoBlk: (w*p0 + (8-w)*p1 + offset) >> (headRoom + 3)
+      const int w = geo_weight(J.aux & 31, (J.aux >> 8) & 255, (J.aux >> 16) & 255, (bx + x - (J.pu_x >> cs)) << cs,
+                               (by + y - (J.pu_y >> cs)) << cs);
+      const int shiftW = headRoom + 3;
+      const int offset = (1 << (shiftW - 1)) + (IF_INTERNAL_OFFS << 3);
+      v = clampi((w * r0[k] + (8 - w) * r1[k] + offset) >> shiftW, 0, maxv);
     } else if (J.bcw != 2) {
       // AreaBuf<Pel>::addWeightedAvg (Buffer.cpp:350)
       const int w1 = c_bcw_w1[J.bcw], w0 = 8 - w1;

@@ -78,6 +78,7 @@ def lib():
         L.vvcr_read_plane.argtypes = [P, I32, I32, I32, P, I32]
         L.vvcr_write_plane.argtypes = [P, I32, I32, I32, P, I32]
         L.vvcr_last_stage_times.argtypes = [P, C.POINTER(C.c_float), I32]
+        L.vvcr_get_dmvr_deltas.argtypes = [P, P, C.c_int64]
         L.vvcr_stream.argtypes = [P]
         L.vvcr_stream.restype = P
         _lib = L
@@ -153,6 +154,16 @@ class Context:
     def write_plane(self, buf, slot, comp, data):
         data = np.ascontiguousarray(data, np.int16)
         self._chk(self.L.vvcr_write_plane(self.h, buf, slot, comp, _ptr(data), data.shape[1]), "vvcr_write_plane")
+
+    def dmvr_deltas(self):
+        """DMVR refinement deltas of the last picture, [n][2] (vvcr_get_dmvr_deltas)."""
+        n = self.L.vvcr_get_dmvr_deltas(self.h, None, 0)
+        if n < 0:
+            self._chk(n, "vvcr_get_dmvr_deltas")
+        out = np.zeros((n, 2), np.int32)
+        if n:
+            self._chk(min(0, self.L.vvcr_get_dmvr_deltas(self.h, out.ctypes.data, n)), "vvcr_get_dmvr_deltas")
+        return out
 
     def stage_ms(self):
         t = (C.c_float * 8)()
