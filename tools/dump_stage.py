@@ -40,6 +40,10 @@ def main():
             for c, pl in enumerate("yuv"):
                 out["%d_%s" % (poc, pl)] = ctx.read_plane(N.BUF_PRED, 0, c)
             out["%d_dmvr" % poc] = ctx.dmvr_deltas()
+        elif stage == "recon":
+            ctx.end_picture(N.STAGE_RESID | N.STAGE_INTER | N.STAGE_INTRA)
+            for c, pl in enumerate("yuv"):
+                out["%d_%s" % (poc, pl)] = ctx.read_plane(N.BUF_RECO, 0, c)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.savez_compressed(os.path.join(ROOT, "gpurun_out", "dump_%s_%s.npz" % (name, stage)), **out)
     ctx.close()

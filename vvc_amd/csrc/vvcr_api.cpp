@@ -10,6 +10,7 @@
 #include "vvcr_internal.h"
 #include "vvcr_host.h"
 #include "vvcr_dbk.h"
+#include "vvcr_intra.h"
 
 namespace {
 
@@ -68,6 +69,10 @@ struct vvcr_ctx {
   DevVec<int16_t> d_alf_luma_coef, d_alf_luma_clip, d_alf_chroma, d_alf_cc;
   DevVec<uint8_t> d_alf_ctb;      // ctb_en[3n] | ctb_alt[3n] | cc_ctl[2n]
   DevVec<int16_t> d_alf_set;
+  IntraPlan intra;
+  DevVec<int32_t> d_order;          // luma | chroma order maps
+  DevVec<ReconTile> d_tiles;
+  DevVec<IntraJob> d_ijobs;
   DbkLists dbk;
   std::vector<DbkSeg> dbk_all;
   DevVec<DbkSeg> d_dbk;
@@ -249,6 +254,7 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_end_picture without begin");
   build_work_lists(ctx->sp, ctx->pp, ctx->desc, ctx->wl);
   if (mask & VVCR_STAGE_DBK) plan_deblocking(ctx->sp, ctx->pp, ctx->desc, ctx->dbk);
+  if (mask & VVCR_STAGE_INTRA) plan_intra(ctx->sp, ctx->pp, ctx->desc, ctx->intra);
   for (bool &r : ctx->stage_ran) r = false;
   hipStream_t s = ctx->stream;
   VVCR_CHECK_HIP(hipEventRecord(ctx->ev[0], s));
@@ -282,6 +288,31 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
     ctx->d_aff_pu.upload(ctx->wl.aff_pu, s);
     ctx->d_aff_jobs.upload(ctx->wl.aff_jobs, s);
     launch_mc_affine(mp, ctx->d_aff_jobs.p, (int)ctx->wl.aff_jobs.size(), ctx->d_aff_pu.p, s);
+    VVCR_CHECK_HIP(hipGetLastError());
+  }
+  // ---- reconstruction: inter CUs, then intra / CIIP steps level by level (vvcr_intra.h)
+  if (mask & VVCR_STAGE_INTRA) {
+    StageTimer t(ctx, ST_INTRA);
+    IntraPlan &ip = ctx->intra;
+    const size_t nu = ip.order[0].size();
+    std::vector<int32_t> ord(ip.order[0]);
+    ord.insert(ord.end(), ip.order[1].begin(), ip.order[1].end());
+    ctx->d_order.upload(ord, s);
+    ctx->d_tiles.upload(ip.inter_tiles, s);
+    ctx->d_ijobs.upload(ip.jobs, s);
+    IntraParams P{};
+    for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[ctx->pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
+    P.order[0] = ctx->d_order.p;
+    P.order[1] = ctx->d_order.p + nu;
+    P.W4 = ctx->sp.width / 4;
+    P.bd = ctx->sp.bit_depth;
+    P.ctu = 1 << ctx->sp.ctu_log2;
+    launch_recon_inter(P, ctx->d_tiles.p, (int)ip.inter_tiles.size(), s);
+    VVCR_CHECK_HIP(hipGetLastError());
+    for (size_t L = 1; L + 1 < ip.level_start.size(); L++) {
+      const int a = ip.level_start[L], b = ip.level_start[L + 1];
+      launch_intra_level(P, ctx->d_ijobs.p + a, b - a, s);
+    }
     VVCR_CHECK_HIP(hipGetLastError());
   }
   // ---- deblocking, in place on the picture slot: all vertical edges, then all horizontal edges

@@ -1,0 +1,70 @@
+// vvcr_intra.h — intra prediction + reconstruction in dependency waves (host planning in
+// vvcr_intra_host.cpp, kernels in vvcr_intra.hip).
+//
+// The reference reconstructs block after block in decoding order (DecCu::decompressCtu DecCu.cpp:102):
+// an intra transform block is predicted from the reconstructed samples of the blocks decoded before it
+// (IntraPrediction::xFillReferenceSamples IntraPrediction.cpp:913, availability = "already decompressed",
+// CodingStructure::isDecomp / getCURestricted). libvvcr keeps that semantic exactly: every
+// reconstruction step gets its decoding sequence number `seq` and writes it into a per-4x4-unit order
+// map; a reference unit is available to step s iff order[unit] < s. The host derives a dependency level
+// per step (1 + the highest level among the units it reads); all steps of one level are independent and
+// run as one launch, levels in increasing order. Inter CUs (no intra neighbours) are level 0.
+#pragma once
+#include "vvcr_host.h"
+
+enum : uint8_t {
+  IJ_MIP = 1 << 0,        // matrix intra prediction (mode = MIP mode index)
+  IJ_MIP_T = 1 << 1,      // MIP transposed
+  IJ_BDPCM = 1 << 2,      // BDPCM prediction (direction in mode: 18 HOR, 50 VER)
+  IJ_CIIP = 1 << 3,       // combined inter/intra: planar blended with the inter prediction plane
+  IJ_ISP_HOR = 1 << 4,    // intra sub-partitions, horizontal split
+  IJ_ISP_VER = 1 << 5,    // intra sub-partitions, vertical split
+  IJ_DUAL = 1 << 6,       // CU of a separate chroma tree (CCLM availability on the chroma map)
+};
+
+// One reconstruction step: predict a region, add the residual plane, clip, store into the picture.
+struct IntraJob {
+  int16_t x, y;           // region position (component samples)
+  uint8_t w, h;           // region size (<= 64)
+  uint8_t comp;           // 0 Y, 1 Cb, 2 Cr
+  uint8_t mode;           // final intra mode 0..66, 67/68/69 = LM / MDLM_L / MDLM_T, MIP mode index
+  uint8_t flags;          // IJ_*
+  uint8_t mrl;            // multiRefIdx
+  uint8_t isp_k;          // ISP: index of the region along the split (0 = first)
+  uint8_t ciip_w;         // CIIP intra weight (1..3)
+  int16_t cx, cy;         // CU position (component samples)
+  uint8_t cw, ch;         // CU size (component samples, 128 fits)
+  int32_t seq;            // decoding sequence number (availability: order[unit] < seq)
+};
+static_assert(sizeof(IntraJob) == 24, "IntraJob layout");
+
+// Inter CU reconstruction tile: reco = clip(pred + resi), one <= 16x16 luma tile plus its chroma.
+struct ReconTile {
+  int16_t x, y;
+  uint8_t w, h;
+  uint8_t comps;          // bit 0 luma, bit 1 chroma
+  uint8_t pad;
+};
+
+struct IntraPlan {
+  std::vector<ReconTile> inter_tiles;
+  std::vector<IntraJob> jobs;        // sorted by level
+  std::vector<int32_t> level_start;  // jobs of level L: [level_start[L], level_start[L+1])
+  std::vector<int32_t> order[2];     // per 4x4 luma unit / 2x2 chroma unit: seq of the step that decodes it
+  void clear() {
+    inter_tiles.clear(); jobs.clear(); level_start.clear(); order[0].clear(); order[1].clear();
+  }
+};
+
+struct IntraParams {
+  DPlane reco[3];                    // picture being reconstructed (in place)
+  DPlane pred[3];                    // inter prediction planes (CIIP)
+  DPlane resi[3];                    // residual planes
+  const int32_t *order[2];
+  int32_t W4;                        // order map row pitch (units)
+  int32_t bd, ctu;
+};
+
+void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out);
+void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s);
+void launch_intra_level(const IntraParams &p, const IntraJob *jobs, int n, hipStream_t s);

@@ -1,0 +1,643 @@
+// vvcr_intra.hip — intra prediction and reconstruction for gfx950, one 64-lane workgroup per step.
+//
+// Per step: reference samples from the reconstructed picture with the reference's availability and
+// substitution rules (IntraPrediction::xFillReferenceSamples IntraPrediction.cpp:913-1149; ISP:
+// initIntraPatternChTypeISP :798), [1 2 1] smoothing (:1152), the mode parameters of
+// initPredIntraParams (:351-443), then planar / DC (:289-350), angular with 4-tap cubic / Gaussian or
+// 2-tap chroma interpolation and PDPC (:458-642, predIntraAng :213-261), BDPCM (:644), MIP
+// (MatrixIntraPrediction.cpp:62-374) or CCLM (xGetLumaRecPixels :1316, xGetLMParameters :1654), the
+// CIIP blend (geneWeightedPred :681), and reconstruction clip(pred + resi) into the picture.
+#include "vvcr_intra.h"
+#include "vvcr_gen_tables.h"
+#include "vvcr_tables.h"
+
+namespace {
+
+__constant__ int8_t i_chroma[32][4] = VVCR_CHROMA_FILTER_TABLE;
+__constant__ int16_t i_angTable[32] = {0, 1, 2, 3, 4, 6, 8, 10, 12, 14, 16, 18, 20, 23, 26, 29, 32, 35, 39, 45, 51, 57, 64, 73, 86, 102, 128, 171, 256, 341, 512, 1024};
+__constant__ int16_t i_invAngTable[32] = {0, 16384, 8192, 5461, 4096, 2731, 2048, 1638, 1365, 1170, 1024, 910, 819, 712, 630, 565,
+                                          512, 468, 420, 364, 321, 287, 256, 224, 191, 161, 128, 96, 64, 48, 32, 16};
+__constant__ uint8_t i_intraFilter[8] = {24, 24, 24, 14, 2, 0, 0, 0};
+
+constexpr int PLANAR = 0, DC = 1, HOR = 18, DIA = 34, VER = 50, VDIA = 66, LM = 67, MDLM_L = 68, MDLM_T = 69;
+constexpr int RB = 160;                      // reference buffer length (2*64 + mrl + 1, rounded)
+constexpr int EXT = 64;                      // negative-index room of the angular main reference
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+__device__ __forceinline__ int ilog2(int v) { return v <= 0 ? -1 : 31 - __clz(v); }
+
+struct Ctx {
+  const IntraParams *P;
+  int ch;        // 0 luma map, 1 chroma map
+  int seq;
+};
+
+// "already decompressed" test of the unit containing (x, y) of channel ch (CodingStructure::isDecomp +
+// getCURestricted: same slice/tile, earlier in decoding order)
+__device__ __forceinline__ bool avail(const IntraParams &P, int ch, int x, int y, int seq) {
+  const int pw = ch ? P.reco[1].w : P.reco[0].w, ph = ch ? P.reco[1].h : P.reco[0].h;
+  if (x < 0 || y < 0 || x >= pw || y >= ph) return false;
+  const int s = ch ? 1 : 2;
+  return P.order[ch][(y >> s) * P.W4 + (x >> s)] < seq;
+}
+
+__device__ __forceinline__ int pel(const DPlane &D, int x, int y) { return D.p[(size_t)y * D.stride + x]; }
+
+// xFillReferenceSamples for area (fx, fy, fw, fh) of component plane D; top[0..predSize+mrl],
+// left[0..predHSize+mrl]; index 0 = corner line. Run by one lane.
+__device__ void fill_refs(const IntraParams &P, const DPlane &D, int ch, int seq, int fx, int fy, int fw, int fh, int predSize,
+                          int predHSize, int mrl, int bd, int16_t *top, int16_t *left) {
+  const int uw = ch ? 2 : 4, uh = uw;
+  const int totalAbove = (predSize + uw - 1) / uw, totalLeft = (predHSize + uh - 1) / uh;
+  const int totalUnits = totalAbove + totalLeft + 1;
+  const int numAbove = max(fw / uw, 1), numLeft = max(fh / uh, 1);
+  const int numAR = totalAbove - numAbove, numBL = totalLeft - numLeft;
+  bool F[2 * 64 + 1];
+  for (int i = 0; i < totalUnits; i++) F[i] = false;
+  int cnt = 0;
+  F[totalLeft] = avail(P, ch, fx - 1, fy - 1, seq);
+  cnt += F[totalLeft];
+  for (int i = 0; i < numAbove; i++) {
+    if (!avail(P, ch, fx + i * uw, fy - 1, seq)) break;
+    F[totalLeft + 1 + i] = true; cnt++;
+  }
+  for (int i = 0; i < numAR; i++) {
+    if (!avail(P, ch, fx + fw - 1 + uw + i * uw, fy - 1, seq)) break;
+    F[totalLeft + 1 + numAbove + i] = true; cnt++;
+  }
+  for (int i = 0; i < numLeft; i++) {
+    if (!avail(P, ch, fx - 1, fy + i * uh, seq)) break;
+    F[totalLeft - 1 - i] = true; cnt++;
+  }
+  for (int i = 0; i < numBL; i++) {
+    if (!avail(P, ch, fx - 1, fy + fh - 1 + uh + i * uh, seq)) break;
+    F[totalLeft - 1 - numLeft - i] = true; cnt++;
+  }
+  const int ox = fx - 1 - mrl, oy = fy - 1 - mrl;   // corner sample of the reference line
+  if (cnt == 0) {
+    const int dc = 1 << (bd - 1);
+    for (int j = 0; j <= predSize + mrl; j++) top[j] = (int16_t)dc;
+    for (int i = 0; i <= predHSize + mrl; i++) left[i] = (int16_t)dc;
+    return;
+  }
+  if (cnt == totalUnits) {
+    for (int j = 0; j <= predSize + mrl; j++) top[j] = (int16_t)pel(D, ox + j, oy);
+    for (int i = 0; i <= predHSize + mrl; i++) left[i] = (int16_t)pel(D, ox, oy + i);
+    return;
+  }
+  // partially available: copy available units, then substitute (IntraPrediction.cpp:987-1148)
+  if (F[totalLeft]) {
+    top[0] = left[0] = (int16_t)pel(D, ox, oy);
+    for (int i = 1; i <= mrl; i++) { top[i] = (int16_t)pel(D, ox + i, oy); left[i] = (int16_t)pel(D, ox, oy + i); }
+  }
+  {
+    int di = 1 + mrl;
+    for (int u = totalLeft - 1; u > 0; u--, di += uh)
+      if (F[u]) for (int i = 0; i < uh; i++) left[di + i] = (int16_t)pel(D, ox, oy + di + i);
+    if (F[0]) {
+      const int last = (predHSize % uh == 0) ? uh : predHSize % uh;
+      for (int i = 0; i < last; i++) left[di + i] = (int16_t)pel(D, ox, oy + di + i);
+    }
+  }
+  {
+    int dj = 1 + mrl;
+    for (int u = totalLeft + 1; u < totalUnits - 1; u++, dj += uw)
+      if (F[u]) for (int j = 0; j < uw; j++) top[dj + j] = (int16_t)pel(D, ox + dj + j, fy - 1 - mrl);
+    if (F[totalUnits - 1]) {
+      const int last = (predSize % uw == 0) ? uw : predSize % uw;
+      for (int j = 0; j < last; j++) top[dj + j] = (int16_t)pel(D, ox + dj + j, fy - 1 - mrl);
+    }
+  }
+  int lastAvail = 0;
+  if (!F[0]) {
+    int first = 1;
+    while (first < totalUnits && !F[first]) first++;
+    int row = -1, col = 0;
+    if (first < totalLeft) row = (totalLeft - first) * uh + mrl;
+    else if (first == totalLeft) row = mrl;
+    else col = (first - totalLeft - 1) * uw + 1 + mrl;
+    const int16_t v = row < 0 ? top[col] : left[row];
+    for (int i = predHSize + mrl; i > row; i--) left[i] = v;
+    for (int j = 0; j < col; j++) top[j] = v;
+    lastAvail = first;
+  }
+  for (int u = lastAvail + 1; u < totalUnits; u++) {
+    if (!F[u]) {
+      int row = -1, col = 0;
+      if (lastAvail < totalLeft) row = (totalLeft - lastAvail - 1) * uh + mrl + 1;
+      else if (lastAvail == totalLeft) col = mrl;
+      else col = (lastAvail - totalLeft) * uw + mrl;
+      const int16_t v = row < 0 ? top[col] : left[row];
+      if (u < totalLeft) {
+        for (int i = row - 1; i >= row - uh; i--) left[i] = v;
+      } else if (u == totalLeft) {
+        for (int i = 0; i < mrl + 1; i++) { left[i] = v; top[i] = v; }
+      } else {
+        const int n = (u == totalUnits - 1) ? ((predSize % uw == 0) ? uw : predSize % uw) : uw;
+        for (int j = col + 1; j <= col + n; j++) top[j] = v;
+      }
+    }
+    lastAvail = u;
+  }
+}
+
+// IntraPrediction::getWideAngle (:184)
+__device__ int wide_angle(int w, int h, int mode) {
+  if (mode > DC && mode <= VDIA) {
+    const int modeShift[6] = {0, 6, 10, 12, 14, 15};
+    const int d = abs(ilog2(w) - ilog2(h));
+    if (w > h && mode < 2 + modeShift[d]) mode += VDIA - 1;
+    else if (h > w && mode > VDIA - modeShift[d]) mode -= VDIA - 1;
+  }
+  return mode;
+}
+
+// isAbove/Left/AboveRight/BelowLeftAvailable counts for CCLM (availability with early break)
+struct NbAvail {
+  bool above, left;
+  int ar, bl;          // available above-right / below-left units
+};
+__device__ NbAvail nb_avail(const IntraParams &P, int ch, int seq, int x, int y, int w, int h, int unit) {
+  NbAvail r{};
+  const int na = w / unit, nl = h / unit;
+  int c = 0;
+  for (int i = 0; i < nl; i++) { if (!avail(P, ch, x - 1, y + i * unit, seq)) break; c++; }
+  r.left = c == nl;
+  c = 0;
+  for (int i = 0; i < na; i++) { if (!avail(P, ch, x + i * unit, y - 1, seq)) break; c++; }
+  r.above = c == na;
+  r.bl = r.ar = 0;
+  const int totalA = (2 * (ch ? w : w / 2) + 1) / 2;   // unused placeholder to keep symmetry
+  (void)totalA;
+  if (r.left)
+    for (int i = 0; i < nl; i++) { if (!avail(P, ch, x - 1, y + h - 1 + unit + i * unit, seq)) break; r.bl++; }
+  if (r.above)
+    for (int i = 0; i < na; i++) { if (!avail(P, ch, x + w - 1 + unit + i * unit, y - 1, seq)) break; r.ar++; }
+  return r;
+}
+
+__global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__restrict__ jobs, int njobs) {
+  __shared__ int16_t refU[2][RB];          // unfiltered top / left (index 0 = corner)
+  __shared__ int16_t refF[2][RB];          // filtered
+  __shared__ int16_t mainA[EXT + RB + 64];  // angular main reference (with negative indices)
+  __shared__ int16_t sideA[EXT + RB + 64];
+  __shared__ int32_t aux[64 * 64 / 4];     // MIP reduced pred / CCLM template scratch
+  __shared__ int16_t tmpl[2][132];         // CCLM down-sampled luma: top row / left column
+  __shared__ int32_t lmp[3];
+  const int j = blockIdx.x;
+  if (j >= njobs) return;
+  const IntraJob J = jobs[j];
+  const int lane = threadIdx.x;
+  const int comp = J.comp, ch = comp ? 1 : 0;
+  const int bd = P.bd, maxv = (1 << bd) - 1;
+  const DPlane &D = P.reco[comp];
+  const int w = J.w, h = J.h, x0 = J.x, y0 = J.y;
+  const bool isp = (J.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0;
+  const bool ispVer = (J.flags & IJ_ISP_VER) != 0;
+  const bool mip = (J.flags & IJ_MIP) != 0;
+  const bool bdpcm = (J.flags & IJ_BDPCM) != 0;
+  const bool ciip = (J.flags & IJ_CIIP) != 0;
+  const bool lmMode = comp > 0 && J.mode >= LM && !bdpcm;
+  const int mrl = comp ? 0 : J.mrl;
+
+  // ---- reference lengths (setReferenceArrayLengths / ISP variants)
+  int topLen = 2 * w, leftLen = 2 * h;
+  if (isp) { topLen = J.cw + w; leftLen = J.ch + h; }
+
+  // ---- reference samples
+  if (lane == 0) {
+    int16_t *top = refU[0], *left = refU[1];
+    if (!isp) {
+      fill_refs(P, D, ch, J.seq, x0, y0, w, h, topLen, leftLen, mrl, bd, top, left);
+    } else {
+      // CU-level fill of the first sub-partition (predSize per split direction), then the shift of
+      // initIntraPatternChTypeISP for later sub-partitions
+      const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
+      fill_refs(P, D, 0, J.seq, J.cx, J.cy, J.cw, J.ch, fTop, fLeft, 0, bd, top, left);
+      if (J.isp_k > 0) {
+        if (!ispVer) {   // horizontal split: left column shifted, top row from the sub-partition above
+          const bool la = avail(P, 0, x0 - 1, y0, J.seq);
+          const int sh = J.isp_k * h;
+          const int src0 = pel(D, x0, y0 - 1);
+          for (int i = 0; i <= leftLen; i++) left[i] = la ? left[i + sh] : (int16_t)src0;
+          top[0] = left[0];
+          for (int i = 0; i < w; i++) top[1 + i] = (int16_t)pel(D, x0 + i, y0 - 1);
+          const int16_t last = (int16_t)pel(D, x0 + w - 1, y0 - 1);
+          for (int i = w + 1; i <= topLen; i++) top[i] = last;
+        } else {         // vertical split: top row shifted, left column from the sub-partition to the left
+          const bool aa = avail(P, 0, x0, y0 - 1, J.seq);
+          const int sh = J.isp_k * w;
+          const int src0 = pel(D, x0 - 1, y0);
+          for (int i = 0; i <= topLen; i++) top[i] = aa ? top[i + sh] : (int16_t)src0;
+          left[0] = top[0];
+          for (int i = 0; i < h; i++) left[1 + i] = (int16_t)pel(D, x0 - 1, y0 + i);
+          const int16_t last = (int16_t)pel(D, x0 - 1, y0 + h - 1);
+          for (int i = h + 1; i <= leftLen; i++) left[i] = last;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- prediction parameters (initPredIntraParams)
+  const int dirMode = ciip ? PLANAR : (int)J.mode;
+  const int bw = isp ? J.cw : w, bh = isp ? J.ch : h;
+  const int predMode = (lmMode || mip || bdpcm) ? dirMode : wide_angle(bw, bh, dirMode);
+  const bool isModeVer = predMode >= DIA;
+  bool applyPDPC = w >= 4 && h >= 4 && mrl == 0;
+  const int angMode = isModeVer ? predMode - VER : -(predMode - HOR);
+  int absAng = 0, invAngle = 0, angle = 0, angScale = 0;
+  if (!lmMode && !mip && !bdpcm && dirMode > DC && dirMode < 67) {
+    const int a = abs(angMode);
+    absAng = i_angTable[a];
+    invAngle = i_invAngTable[a];
+    angle = angMode < 0 ? -absAng : absAng;
+    if (angMode < 0) {
+      applyPDPC = false;
+    } else if (angMode > 0) {
+      const int side = isModeVer ? h : w;
+      angScale = min(2, ilog2(side) - (ilog2(3 * invAngle - 2) - 8));
+      applyPDPC = applyPDPC && angScale >= 0;
+    }
+  }
+  bool refFilter = false, interp = false;
+  if (comp == 0 && !isp && !mip && mrl == 0 && dirMode != DC && !bdpcm && !lmMode) {
+    if (dirMode == PLANAR) {
+      refFilter = w * h > 32;
+    } else {
+      const int diff = min(abs(predMode - HOR), abs(predMode - VER));
+      const int log2Size = (ilog2(w) + ilog2(h)) >> 1;
+      if (diff > i_intraFilter[log2Size]) {
+        refFilter = (absAng & 31) == 0;
+        interp = !refFilter;
+      }
+    }
+  }
+  if (refFilter) {
+    const int pS = topLen, pH = leftLen;
+    for (int i = lane; i <= pS; i += 64) {
+      int v;
+      if (i == 0) v = (refU[0][0] + refU[0][1] + refU[1][0] + refU[1][1] + 2) >> 2;
+      else if (i == pS) v = refU[0][pS];
+      else v = (refU[0][i - 1] + 2 * refU[0][i] + refU[0][i + 1] + 2) >> 2;
+      refF[0][i] = (int16_t)v;
+    }
+    for (int i = lane; i <= pH; i += 64) {
+      int v;
+      if (i == 0) v = (refU[0][0] + refU[0][1] + refU[1][0] + refU[1][1] + 2) >> 2;
+      else if (i == pH) v = refU[1][pH];
+      else v = (refU[1][i - 1] + 2 * refU[1][i] + refU[1][i + 1] + 2) >> 2;
+      refF[1][i] = (int16_t)v;
+    }
+    __syncthreads();
+  }
+  const int16_t *top = refFilter ? refF[0] : refU[0];
+  const int16_t *left = refFilter ? refF[1] : refU[1];
+  const int n = w * h;
+  int predv[64];   // up to 64 samples per lane (64x64 block)
+
+  if (lmMode) {
+    // ---------------- CCLM (xGetLumaRecPixels + xGetLMParameters)
+    const DPlane &Y = P.reco[0];
+    const int lx = 2 * x0, ly = 2 * y0;
+    const bool dual = (J.flags & IJ_DUAL) != 0;
+    // luma-template availability: luma map in a single tree, chroma map in a separate chroma tree
+    const NbAvail lr = dual ? nb_avail(P, 1, J.seq, x0, y0, w, h, 2) : nb_avail(P, 0, J.seq, lx, ly, 2 * w, 2 * h, 4);
+    const NbAvail lm = nb_avail(P, 1, J.seq, x0, y0, w, h, 2);
+    const int mode = J.mode;
+    const int addAR = (mode == MDLM_L || mode == MDLM_T) ? lr.ar * 2 : 0;
+    const int addBL = (mode == MDLM_L || mode == MDLM_T) ? lr.bl * 2 : 0;
+    const bool firstRowCtu = (ly & (P.ctu - 1)) == 0;
+    if (lr.above) {
+      for (int i = lane; i < w + addAR; i += 64) {
+        const bool pad = i == 0 && !lr.left;
+        int v;
+        if (firstRowCtu) {
+          const int c = lx + 2 * i;
+          const int l = pad ? pel(Y, c, ly - 1) : pel(Y, c - 1, ly - 1);
+          v = (pel(Y, c, ly - 1) * 2 + l + pel(Y, c + 1, ly - 1) + 2) >> 2;
+        } else {
+          const int c = lx + 2 * i;
+          const int l0 = pad ? pel(Y, c, ly - 2) : pel(Y, c - 1, ly - 2);
+          const int l1 = pad ? pel(Y, c, ly - 1) : pel(Y, c - 1, ly - 1);
+          v = ((pel(Y, c, ly - 2) * 2 + l0 + pel(Y, c + 1, ly - 2)) + (pel(Y, c, ly - 1) * 2 + l1 + pel(Y, c + 1, ly - 1)) + 4) >> 3;
+        }
+        tmpl[0][i] = (int16_t)v;
+      }
+    }
+    if (lr.left) {
+      for (int jj = lane; jj < h + addBL; jj += 64) {
+        const int r = ly + 2 * jj;
+        const int v = ((pel(Y, lx - 2, r) * 2 + pel(Y, lx - 3, r) + pel(Y, lx - 1, r)) +
+                       (pel(Y, lx - 2, r + 1) * 2 + pel(Y, lx - 3, r + 1) + pel(Y, lx - 1, r + 1)) + 4) >> 3;
+        tmpl[1][jj] = (int16_t)v;
+      }
+    }
+    for (int k = lane; k < n; k += 64) {
+      const int yy = k / w, xx = k - yy * w;
+      const int c = lx + 2 * xx, r = ly + 2 * yy;
+      const bool pad = xx == 0 && !lr.left;
+      const int l0 = pad ? pel(Y, c, r) : pel(Y, c - 1, r);
+      const int l1 = pad ? pel(Y, c, r + 1) : pel(Y, c - 1, r + 1);
+      aux[k] = ((pel(Y, c, r) * 2 + pel(Y, c + 1, r) + l0) + (pel(Y, c, r + 1) * 2 + pel(Y, c + 1, r + 1) + l1) + 4) >> 3;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      bool aboveAv = lm.above, leftAv = lm.left;
+      int avAR = lm.ar, avBL = lm.bl;
+      const int avA = aboveAv ? w / 2 : 0, avL = leftAv ? h / 2 : 0;   // units of 2 chroma samples
+      int topN = 0, leftN = 0;
+      if (mode == MDLM_T) {
+        leftAv = false;
+        avAR = avAR > (h / 2) ? h / 2 : avAR;
+        topN = 2 * (avA + avAR);
+      } else if (mode == MDLM_L) {
+        aboveAv = false;
+        avBL = avBL > (w / 2) ? w / 2 : avBL;
+        leftN = 2 * (avL + avBL);
+      } else {
+        topN = w;
+        leftN = h;
+      }
+      const int aboveIs4 = leftAv ? 0 : 1, leftIs4 = aboveAv ? 0 : 1;
+      const int sp0 = topN >> (2 + aboveIs4), st0 = max(1, topN >> (1 + aboveIs4));
+      const int sp1 = leftN >> (2 + leftIs4), st1 = max(1, leftN >> (1 + leftIs4));
+      int sl[4] = {0, 0, 0, 0}, sc[4] = {0, 0, 0, 0};
+      int cntT = 0, cntL = 0;
+      if (aboveAv) {
+        cntT = min(topN, (1 + aboveIs4) << 1);
+        for (int pos = sp0, c = 0; c < cntT; pos += st0, c++) { sl[c] = tmpl[0][pos]; sc[c] = refU[0][1 + pos]; }
+      }
+      if (leftAv) {
+        cntL = min(leftN, (1 + leftIs4) << 1);
+        for (int pos = sp1, c = 0; c < cntL; pos += st1, c++) { sl[c + cntT] = tmpl[1][pos]; sc[c + cntT] = refU[1][1 + pos]; }
+      }
+      if (cntT + cntL == 2) {
+        sl[3] = sl[0]; sc[3] = sc[0];
+        sl[2] = sl[1]; sc[2] = sc[1];
+        sl[0] = sl[1]; sc[0] = sc[1];
+        sl[1] = sl[3]; sc[1] = sc[3];
+      }
+      int mn[2] = {0, 2}, mx[2] = {1, 3};
+      int *a0 = mn, *a1 = mx;
+      if (sl[a0[0]] > sl[a0[1]]) { int t = a0[0]; a0[0] = a0[1]; a0[1] = t; }
+      if (sl[a1[0]] > sl[a1[1]]) { int t = a1[0]; a1[0] = a1[1]; a1[1] = t; }
+      if (sl[a0[0]] > sl[a1[1]]) { int *t = a0; a0 = a1; a1 = t; }
+      if (sl[a0[1]] > sl[a1[0]]) { int t = a0[1]; a0[1] = a1[0]; a1[0] = t; }
+      const int minL = (sl[a0[0]] + sl[a0[1]] + 1) >> 1, minC = (sc[a0[0]] + sc[a0[1]] + 1) >> 1;
+      const int maxL = (sl[a1[0]] + sl[a1[1]] + 1) >> 1, maxC = (sc[a1[0]] + sc[a1[1]] + 1) >> 1;
+      int a = 0, b = 1 << (bd - 1), shift = 0;
+      if (leftAv || aboveAv) {
+        const int diff = maxL - minL;
+        if (diff > 0) {
+          const int diffC = maxC - minC;
+          int x = ilog2(diff);
+          const uint8_t divSig[16] = {0, 7, 6, 5, 5, 4, 4, 3, 3, 2, 2, 1, 1, 1, 1, 0};
+          const int normDiff = (diff << 4 >> x) & 15;
+          const int v = divSig[normDiff] | 8;
+          x += normDiff != 0;
+          const int y = ilog2(abs(diffC)) + 1;
+          const int add = 1 << y >> 1;
+          a = (diffC * v + add) >> y;
+          shift = 3 + x - y;
+          if (shift < 1) {
+            shift = 1;
+            a = (a == 0) ? 0 : (a < 0) ? -15 : 15;
+          }
+          b = minC - ((a * minL) >> shift);
+        } else {
+          a = 0; b = minC; shift = 0;
+        }
+      }
+      lmp[0] = a; lmp[1] = b; lmp[2] = shift;
+    }
+    __syncthreads();
+    for (int k = lane, q = 0; k < n; k += 64, q++) predv[q] = clampi(((lmp[0] * aux[k]) >> lmp[2]) + lmp[1], 0, maxv);
+  } else if (mip) {
+    // ---------------- MIP
+    const int sizeId = (w == 4 && h == 4) ? 0 : ((w == 4 || h == 4 || (w == 8 && h == 8)) ? 1 : 2);
+    const int bdry = sizeId == 0 ? 2 : 4, rp = sizeId < 2 ? 4 : 8;
+    const bool tr = (J.flags & IJ_MIP_T) != 0;
+    __shared__ int inb[8];
+    __shared__ int inOff;
+    if (lane == 0) {
+      int red[8];
+      // boundaryDownsampling1D of top (w) and left (h)
+      for (int side = 0; side < 2; side++) {
+        const int len = side ? h : w;
+        const int16_t *src = side ? refU[1] : refU[0];
+        int *dst = red + side * bdry;
+        if (bdry < len) {
+          const int f = len / bdry, lf = ilog2(f);
+          for (int d = 0, s = 0; d < bdry; d++) {
+            int sum = 0;
+            for (int k = 0; k < f; k++) sum += src[1 + s++];
+            dst[d] = (sum + (1 << (lf - 1))) >> lf;
+          }
+        } else {
+          for (int d = 0; d < bdry; d++) dst[d] = src[1 + d];
+        }
+      }
+      int in[8];
+      const int inputSize = 2 * bdry;
+      if (!tr) for (int i = 0; i < inputSize; i++) in[i] = red[i];
+      else {
+        for (int i = 0; i < bdry; i++) { in[i] = red[bdry + i]; in[bdry + i] = red[i]; }
+      }
+      const int off = in[0];
+      in[0] = sizeId < 2 ? ((1 << (bd - 1)) - off) : 0;
+      for (int i = 1; i < inputSize; i++) in[i] -= off;
+      for (int i = 0; i < inputSize; i++) inb[i] = in[i];
+      inOff = off;
+    }
+    __syncthreads();
+    const int inputSize = 2 * bdry;
+    int sum = 0;
+    for (int i = 0; i < inputSize; i++) sum += inb[i];
+    const int offset = 32 - 32 * sum;   // (1 << (MIP_SHIFT_MATRIX - 1)) - MIP_OFFSET_MATRIX * sum
+    const int mode = J.mode;
+    for (int o = lane; o < rp * rp; o += 64) {
+      int acc = 0;
+      for (int i = 0; i < inputSize; i++) {
+        int wgt;
+        if (sizeId == 0) wgt = vvcr_tab::mip4x4[mode][o][i];
+        else if (sizeId == 1) wgt = vvcr_tab::mip8x8[mode][o][i];
+        else wgt = i == 0 ? 0 : vvcr_tab::mip16x16[mode][o][i - 1];
+        acc += inb[i] * wgt;
+      }
+      const int v = clampi(((acc + offset) >> 6) + inOff, 0, maxv);
+      // transposed matrices produce the transposed block
+      const int oy = o / rp, ox = o - oy * rp;
+      aux[tr ? ox * rp + oy : o] = v;
+    }
+    __syncthreads();
+    const int upH = w / rp, upV = h / rp;
+    // horizontal upsampling into rows (r+1)*upV-1 (predictionUpsampling :252-277), kept in aux2 region
+    int *full = aux + 64;   // w*h <= 64*64? MIP blocks <= 64x64: use registers per sample instead
+    (void)full;
+    for (int k = lane, q = 0; k < n; k += 64, q++) {
+      const int yy = k / w, xx = k - yy * w;
+      // value of the horizontally upsampled row grid at (rowIdx, xx) where rowIdx in [0, rp)
+      auto hval = [&](int rr, int cx) -> int {
+        if (upH <= 1) return aux[rr * rp + cx];
+        const int lf = ilog2(upH);
+        const int c = cx / upH, pos = cx - c * upH + 1;
+        const int before = c == 0 ? (int)refU[1][1 + (rr + 1) * upV - 1] : aux[rr * rp + c - 1];
+        const int behind = aux[rr * rp + c];
+        return (before * (upH - pos) + behind * pos + (1 << (lf - 1))) >> lf;
+      };
+      int v;
+      if (upV <= 1) {
+        v = hval(yy, xx);
+      } else {
+        const int lf = ilog2(upV);
+        const int r = yy / upV, pos = yy - r * upV + 1;
+        const int before = r == 0 ? (int)refU[0][1 + xx] : hval(r - 1, xx);
+        const int behind = hval(r, xx);
+        v = (before * (upV - pos) + behind * pos + (1 << (lf - 1))) >> lf;
+      }
+      predv[q] = v;
+    }
+  } else {
+    // ---------------- planar / DC / angular / BDPCM
+    const int lw = ilog2(w), lh = ilog2(h);
+    if (bdpcm) {
+      for (int k = lane, q = 0; k < n; k += 64, q++) {
+        const int yy = k / w, xx = k - yy * w;
+        predv[q] = J.mode == 1 ? left[yy + 1] : top[xx + 1];
+      }
+    } else if (dirMode == PLANAR) {
+      const int tr = top[w + 1], bl = left[h + 1];
+      for (int k = lane, q = 0; k < n; k += 64, q++) {
+        const int yy = k / w, xx = k - yy * w;
+        const int hor = (left[yy + 1] << lw) + (xx + 1) * (tr - left[yy + 1]);
+        const int ver = (top[xx + 1] << lh) + (yy + 1) * (bl - top[xx + 1]);
+        predv[q] = ((hor << lh) + (ver << lw) + (1 << (lw + lh))) >> (1 + lw + lh);
+      }
+    } else if (dirMode == DC) {
+      int sum = 0;
+      if (w >= h) for (int i = 0; i < w; i++) sum += top[mrl + 1 + i];
+      if (w <= h) for (int i = 0; i < h; i++) sum += left[mrl + 1 + i];
+      const int denom = (w == h) ? (w << 1) : max(w, h);
+      const int dc = (sum + (denom >> 1)) >> ilog2(denom);
+      for (int k = lane, q = 0; k < n; k += 64, q++) predv[q] = dc;
+    } else {
+      // angular: build main / side references exactly as xPredIntraAng does
+      const int W = isModeVer ? w : h, H = isModeVer ? h : w;   // in the (possibly transposed) frame
+      int16_t *refMain = mainA + EXT, *refSide = sideA + EXT;
+      if (lane == 0) {
+        const int16_t *srcMain = isModeVer ? top : left, *srcSide = isModeVer ? left : top;
+        if (angle < 0) {
+          for (int k = 0; k <= W + 1 + mrl; k++) refMain[k] = srcMain[k];
+          for (int k = 0; k <= H + 1 + mrl; k++) refSide[k] = srcSide[k];
+          for (int k = -H; k <= -1; k++) refMain[k] = refSide[min((-k * invAngle + 256) >> 9, H)];
+        } else {
+          const int mainLen = isModeVer ? topLen : leftLen, sideLen = isModeVer ? leftLen : topLen;
+          for (int k = 0; k <= mainLen + mrl; k++) refMain[k] = srcMain[k];
+          for (int k = 0; k <= sideLen + mrl; k++) refSide[k] = srcSide[k];
+          const int log2Ratio = lw - lh;
+          const int s = max(0, isModeVer ? log2Ratio : -log2Ratio);
+          const int maxIndex = (mrl << s) + 2;
+          const int16_t v = refMain[mainLen + mrl];
+          for (int z = 1; z <= maxIndex; z++) refMain[mainLen + mrl + z] = v;
+        }
+      }
+      __syncthreads();
+      const int16_t *rM = refMain + mrl, *rS = refSide + mrl;
+      const bool integerSlope = (absAng & 31) == 0;
+      for (int k = lane, q = 0; k < n; k += 64, q++) {
+        const int oy = k / w, ox = k - oy * w;
+        const int xx = isModeVer ? ox : oy, yy = isModeVer ? oy : ox;   // transposed-frame coordinates
+        int v;
+        if (angle == 0) {
+          v = rM[xx + 1];
+          if (applyPDPC) {
+            const int scale = (ilog2(W) + ilog2(H) - 2) >> 2;
+            if (xx < min(3 << scale, W)) {
+              const int wL = 32 >> (2 * xx >> scale);
+              v = clampi(v + ((wL * (rS[1 + yy] - rM[0]) + 32) >> 6), 0, maxv);
+            }
+          }
+        } else {
+          const int deltaPos = angle * (1 + mrl) + yy * angle;
+          const int di = deltaPos >> 5, df = deltaPos & 31;
+          if (!integerSlope) {
+            if (comp == 0) {
+              int f[4];
+              if (!interp) {
+                for (int t = 0; t < 4; t++) f[t] = i_chroma[df][t];
+              } else {
+                f[0] = 16 - (df >> 1); f[1] = 32 - (df >> 1); f[2] = 16 + (df >> 1); f[3] = df >> 1;
+              }
+              const int s = f[0] * rM[di + xx] + f[1] * rM[di + xx + 1] + f[2] * rM[di + xx + 2] + f[3] * rM[di + xx + 3];
+              v = clampi((s + 32) >> 6, 0, maxv);
+            } else {
+              const int p0 = rM[di + xx + 1], p1 = rM[di + xx + 2];
+              v = p0 + ((df * (p1 - p0) + 16) >> 5);
+            }
+          } else {
+            v = rM[xx + di + 1];
+          }
+          if (applyPDPC && xx < min(3 << angScale, W)) {
+            const int invSum = 256 + (xx + 1) * invAngle;
+            const int wL = 32 >> (2 * xx >> angScale);
+            const int l = rS[yy + (invSum >> 9) + 1];
+            v = (int16_t)(v + ((wL * (l - v) + 32) >> 6));
+          }
+        }
+        predv[q] = v;
+      }
+    }
+    if (applyPDPC && !bdpcm && (dirMode == PLANAR || dirMode == DC)) {
+      const int scale = (lw - 2 + lh - 2 + 2) >> 2;
+      for (int k = lane, q = 0; k < n; k += 64, q++) {
+        const int yy = k / w, xx = k - yy * w;
+        const int wT = 32 >> min(31, (yy << 1) >> scale);
+        const int wL = 32 >> min(31, (xx << 1) >> scale);
+        const int v = predv[q];
+        predv[q] = (int16_t)(v + ((wL * (left[yy + 1] - v) + wT * (top[xx + 1] - v) + 32) >> 6));
+      }
+    }
+  }
+
+  // ---- CIIP blend (geneWeightedPred) and reconstruction
+  const DPlane &R = P.resi[comp];
+  const DPlane &PP = P.pred[comp];
+  for (int k = lane, q = 0; k < n; k += 64, q++) {
+    const int yy = k / w, xx = k - yy * w;
+    int pv = predv[q];
+    if (ciip) pv = ((4 - J.ciip_w) * pel(PP, x0 + xx, y0 + yy) + J.ciip_w * pv + 2) >> 2;
+    const int v = clampi(pv + pel(R, x0 + xx, y0 + yy), 0, maxv);
+    D.p[(size_t)(y0 + yy) * D.stride + x0 + xx] = (int16_t)v;
+  }
+}
+
+__global__ void k_recon_inter(IntraParams P, const ReconTile *__restrict__ tiles, int n) {
+  const int t = blockIdx.x;
+  if (t >= n) return;
+  const ReconTile T = tiles[t];
+  const int maxv = (1 << P.bd) - 1;
+  for (int comp = 0; comp < 3; comp++) {
+    if (!(T.comps & (comp ? 2 : 1))) continue;
+    const int s = comp ? 1 : 0;
+    const int bx = T.x >> s, by = T.y >> s, bw = T.w >> s, bh = T.h >> s;
+    const DPlane &D = P.reco[comp], &Pr = P.pred[comp], &Re = P.resi[comp];
+    for (int k = threadIdx.x; k < bw * bh; k += blockDim.x) {
+      const int yy = k / bw, xx = k - yy * bw;
+      const int v = pel(Pr, bx + xx, by + yy) + pel(Re, bx + xx, by + yy);
+      D.p[(size_t)(by + yy) * D.stride + bx + xx] = (int16_t)clampi(v, 0, maxv);
+    }
+  }
+}
+
+}  // namespace
+
+void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_recon_inter, dim3(n), dim3(64), 0, s, p, tiles, n);
+}
+
+void launch_intra_level(const IntraParams &p, const IntraJob *jobs, int n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_intra, dim3(n), dim3(64), 0, s, p, jobs, n);
+}

@@ -1,0 +1,262 @@
+// vvcr_intra_host.cpp — reconstruction planning: decoding order, availability order maps and
+// dependency levels for the intra / CIIP steps (see vvcr_intra.h).
+//
+// Decoding order follows DecCu::decompressCtu (DecCu.cpp:102-155): CTUs in raster order; inside a CTU
+// the CUs in coding order (separate luma / chroma passes for a dual tree); an intra CU reconstructs all
+// its luma transform blocks, then Cb and Cr per transform unit (xReconIntraQT / xIntraRecQT :489-612);
+// ISP sub-partitions in order, with the prediction regions of CU::isPredRegDiffFromTB (UnitTools.cpp:3692);
+// an inter CU is one step (xReconInter :664-772, setDecomp of the whole CU), CIIP predicting its planar
+// part from the reconstructed neighbours first (IntraPrediction::geneIntrainterPred :735).
+#include "vvcr_intra.h"
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <memory>
+#include <string>
+
+namespace {
+
+constexpr int MODE_INTER = 0, MODE_INTRA = 1;
+
+struct Planner {
+  const vvcr_seq_params &sp;
+  const vvcr_pic_params &pp;
+  const PictureDescriptors &d;
+  IntraPlan &out;
+  int W4, H4, ctu;
+  std::vector<int32_t> level[2];
+  std::vector<int32_t> cu_map;      // luma 4x4 unit -> CU index (for CIIP neighbour tests)
+  std::vector<std::pair<int32_t, IntraJob>> jobs;   // (level, job)
+  int seq = 0;
+
+  Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, IntraPlan &o)
+      : sp(s), pp(p), d(dd), out(o) {
+    W4 = sp.width / 4;
+    H4 = sp.height / 4;
+    ctu = 1 << sp.ctu_log2;
+  }
+
+  // component-sample rectangle -> unit rectangle of map ch (4x4 luma units / 2x2 chroma units)
+  int max_level(int ch, int x0, int y0, int x1, int y1) const {   // inclusive sample bounds
+    const int s = ch ? 1 : 2;
+    const int pw = ch ? sp.width / 2 : sp.width, ph = ch ? sp.height / 2 : sp.height;
+    x0 = std::max(x0, 0); y0 = std::max(y0, 0);
+    x1 = std::min(x1, pw - 1); y1 = std::min(y1, ph - 1);
+    int m = 0;
+    if (x0 > x1 || y0 > y1) return 0;
+    for (int uy = y0 >> s; uy <= (y1 >> s); uy++)
+      for (int ux = x0 >> s; ux <= (x1 >> s); ux++) {
+        const size_t i = (size_t)uy * W4 + ux;
+        if (out.order[ch][i] < seq) m = std::max(m, level[ch][i]);
+      }
+    return m;
+  }
+  void mark(int ch, int x, int y, int w, int h, int lev, bool set_order) {
+    const int s = ch ? 1 : 2;
+    for (int uy = y >> s; uy < (y + h + (1 << s) - 1) >> s; uy++)
+      for (int ux = x >> s; ux < (x + w + (1 << s) - 1) >> s; ux++) {
+        const size_t i = (size_t)uy * W4 + ux;
+        level[ch][i] = lev;
+        if (set_order) out.order[ch][i] = seq;
+      }
+  }
+  // level of a prediction from the reference lines of region (x, y, w, h) with lengths topLen/leftLen
+  int ref_level(int ch, int x, int y, int topLen, int leftLen, int mrl) const {
+    int m = max_level(ch, x - 1 - mrl, y - 1 - mrl, x + topLen - 1, y - 1);
+    m = std::max(m, max_level(ch, x - 1 - mrl, y - 1 - mrl, x - 1, y + leftLen - 1));
+    return m;
+  }
+
+  void push(int lev, const IntraJob &j) { jobs.emplace_back(lev, j); }
+
+  IntraJob base(const vvcr_cu &c, int comp) const {
+    IntraJob j{};
+    j.comp = (uint8_t)comp;
+    j.seq = seq;
+    if (comp == 0) { j.cx = (int16_t)c.x; j.cy = (int16_t)c.y; j.cw = (uint8_t)c.w; j.ch = (uint8_t)c.h; }
+    else { j.cx = (int16_t)c.cx; j.cy = (int16_t)c.cy; j.cw = (uint8_t)c.cw; j.ch = (uint8_t)c.ch; }
+    return j;
+  }
+
+  void inter_cu(int ci) {
+    const vvcr_cu &c = d.cu[ci];
+    const vvcr_pu &p = d.pu[c.firstpu];
+    seq++;
+    if (p.ciip) {
+      // CIIP: planar from the neighbours, blended with the inter prediction (geneWeightedPred :681)
+      auto intraAt = [&](int x, int y) {
+        if (x < 0 || y < 0 || x >= sp.width || y >= sp.height) return false;
+        const int n = cu_map[(size_t)(y >> 2) * W4 + (x >> 2)];
+        return n >= 0 && n <= ci && d.cu[n].predmode == MODE_INTRA;
+      };
+      const bool n0 = intraAt(c.x - 1, c.y + c.h - 1), n1 = intraAt(c.x + c.w - 1, c.y - 1);
+      const int wIntra = (n0 && n1) ? 3 : ((!n0 && !n1) ? 1 : 2);
+      for (int comp = 0; comp < 3; comp++) {
+        const int ch = comp ? 1 : 0;
+        IntraJob j = base(c, comp);
+        j.x = j.cx; j.y = j.cy; j.w = j.cw; j.h = j.ch;
+        j.flags = IJ_CIIP;
+        j.mode = 0;
+        j.ciip_w = (uint8_t)wIntra;
+        const int lev = 1 + ref_level(ch, j.x, j.y, 2 * j.w, 2 * j.h, 0);
+        push(lev, j);
+      }
+      int lev = 0;
+      for (auto it = jobs.end() - 3; it != jobs.end(); ++it) lev = std::max(lev, it->first);
+      mark(0, c.x, c.y, c.w, c.h, lev, true);
+      mark(1, c.cx, c.cy, c.cw, c.ch, lev, true);
+      return;
+    }
+    // plain inter: level 0, reconstructed before the intra waves
+    for (int y = 0; y < c.h; y += 16)
+      for (int x = 0; x < c.w; x += 16) {
+        ReconTile t{};
+        t.x = (int16_t)(c.x + x); t.y = (int16_t)(c.y + y);
+        t.w = (uint8_t)std::min(16, c.w - x); t.h = (uint8_t)std::min(16, c.h - y);
+        t.comps = (uint8_t)((c.yvalid ? 1 : 0) | (c.cvalid ? 2 : 0));
+        out.inter_tiles.push_back(t);
+      }
+    if (c.yvalid) mark(0, c.x, c.y, c.w, c.h, 0, true);
+    if (c.cvalid) mark(1, c.cx, c.cy, c.cw, c.ch, 0, true);
+  }
+
+  void intra_luma(int ci) {
+    const vvcr_cu &c = d.cu[ci];
+    const vvcr_pu &p = d.pu[c.firstpu];
+    if (c.isp) {
+      const bool ver = c.isp == 2;   // ISPType: 1 HOR_INTRA_SUBPARTITIONS, 2 VER_INTRA_SUBPARTITIONS
+      const bool regDiff = ver && ((c.w == 8 && c.h > 4) || c.w == 4);
+      // prediction regions in order (TBs, or 4-wide regions covering several 1/2-wide TBs)
+      std::vector<std::array<int, 4>> regs;
+      for (int t = c.firsttu; t < c.firsttu + c.ntu; t++) {
+        const int32_t *b = d.tu[t].b[0];
+        if (b[2] <= 0) continue;
+        if (regDiff) {
+          if ((b[0] - c.x) % 4 == 0) regs.push_back({b[0], b[1], 4, b[3]});
+        } else {
+          regs.push_back({b[0], b[1], b[2], b[3]});
+        }
+      }
+      int prevLev = 0;
+      for (size_t k = 0; k < regs.size(); k++) {
+        seq++;
+        IntraJob j = base(c, 0);
+        j.x = (int16_t)regs[k][0]; j.y = (int16_t)regs[k][1]; j.w = (uint8_t)regs[k][2]; j.h = (uint8_t)regs[k][3];
+        j.flags = ver ? IJ_ISP_VER : IJ_ISP_HOR;
+        j.mode = (uint8_t)p.fidir_l;
+        j.isp_k = (uint8_t)k;
+        // CU-level reference lines (first sub-partition fill) + the previous sub-partition
+        const int fTop = ver ? 2 * c.w : c.w + j.w, fLeft = ver ? c.h + j.h : 2 * c.h;
+        int lev = ref_level(0, c.x, c.y, fTop, fLeft, 0);
+        lev = std::max(lev, prevLev);
+        lev += 1;
+        if (k == 0) mark(0, c.x, c.y, c.w, c.h, lev, true);   // setDecomp of the whole CU (DecCu.cpp:288-291)
+        else mark(0, j.x, j.y, j.w, j.h, lev, false);
+        prevLev = lev;
+        push(lev, j);
+      }
+      return;
+    }
+    for (int t = c.firsttu; t < c.firsttu + c.ntu; t++) {
+      const int32_t *b = d.tu[t].b[0];
+      if (b[2] <= 0) continue;
+      seq++;
+      IntraJob j = base(c, 0);
+      j.x = (int16_t)b[0]; j.y = (int16_t)b[1]; j.w = (uint8_t)b[2]; j.h = (uint8_t)b[3];
+      j.mrl = (uint8_t)p.mrl;
+      if (c.bdpcm) { j.flags = IJ_BDPCM; j.mode = (uint8_t)c.bdpcm; }
+      else if (c.mip) { j.flags = IJ_MIP | (p.mipt ? IJ_MIP_T : 0); j.mode = (uint8_t)p.idir_l; }
+      else j.mode = (uint8_t)p.fidir_l;
+      const int lev = 1 + ref_level(0, j.x, j.y, 2 * j.w, 2 * j.h, j.mrl);
+      mark(0, j.x, j.y, j.w, j.h, lev, true);
+      push(lev, j);
+    }
+  }
+
+  void intra_chroma(int ci) {
+    const vvcr_cu &c = d.cu[ci];
+    const vvcr_pu &p = d.pu[c.firstpu];
+    const bool dual = c.chtype == 1;
+    for (int t = c.firsttu; t < c.firsttu + c.ntu; t++) {
+      for (int comp = 1; comp < 3; comp++) {
+        const int32_t *b = d.tu[t].b[comp];
+        if (b[2] <= 0) continue;
+        seq++;
+        IntraJob j = base(c, comp);
+        j.x = (int16_t)b[0]; j.y = (int16_t)b[1]; j.w = (uint8_t)b[2]; j.h = (uint8_t)b[3];
+        if (c.bdpcmc) { j.flags = IJ_BDPCM; j.mode = (uint8_t)c.bdpcmc; }
+        else j.mode = (uint8_t)p.fidir_c;
+        if (dual) j.flags |= IJ_DUAL;
+        int lev = ref_level(1, j.x, j.y, 2 * j.w, 2 * j.h, 0);
+        if (!c.bdpcmc && p.fidir_c >= 67) {   // CCLM: co-located luma and its template rows / columns
+          const int lx = 2 * j.x, ly = 2 * j.y;
+          lev = std::max(lev, max_level(0, lx - 4, ly - 4, lx + 4 * j.w - 1, ly + 4 * j.h - 1));
+        }
+        lev += 1;
+        mark(1, j.x, j.y, j.w, j.h, lev, true);
+        push(lev, j);
+      }
+    }
+  }
+
+  void run() {
+    const size_t nu = (size_t)W4 * H4;
+    for (int k = 0; k < 2; k++) { out.order[k].assign(nu, 1 << 30); level[k].assign(nu, 0); }
+    cu_map.assign(nu, -1);
+    for (size_t i = 0; i < d.cu.size(); i++) {
+      const vvcr_cu &c = d.cu[i];
+      if (!c.yvalid) continue;
+      for (int uy = c.y >> 2; uy < (c.y + c.h) >> 2; uy++)
+        for (int ux = c.x >> 2; ux < (c.x + c.w) >> 2; ux++) cu_map[(size_t)uy * W4 + ux] = (int)i;
+    }
+    const int wc = (sp.width + ctu - 1) / ctu, hc = (sp.height + ctu - 1) / ctu;
+    const int ncu = (int)d.cu.size();
+    std::vector<int> start((size_t)wc * hc + 1, 0), order(ncu), ctu_of(ncu);
+    for (int i = 0; i < ncu; i++) {
+      const vvcr_cu &c = d.cu[i];
+      const int x = c.yvalid ? c.x : 2 * c.cx, y = c.yvalid ? c.y : 2 * c.cy;
+      ctu_of[i] = (y >> sp.ctu_log2) * wc + (x >> sp.ctu_log2);
+      start[ctu_of[i] + 1]++;
+    }
+    for (int k = 0; k < wc * hc; k++) start[k + 1] += start[k];
+    {
+      std::vector<int> pos(start);
+      for (int i = 0; i < ncu; i++) order[pos[ctu_of[i]]++] = i;
+    }
+    for (int k = 0; k < wc * hc; k++)
+      for (int pass = 0; pass < (pp.dual_tree ? 2 : 1); pass++)
+        for (int jx = start[k]; jx < start[k + 1]; jx++) {
+          const int i = order[jx];
+          const vvcr_cu &c = d.cu[i];
+          if (pp.dual_tree && c.chtype != pass) continue;
+          if (c.predmode == MODE_INTER) {
+            inter_cu(i);
+          } else if (c.predmode == MODE_INTRA) {
+            if (c.yvalid) intra_luma(i);
+            if (c.cvalid) intra_chroma(i);
+          } else {
+            throw VvcrError(VVCR_E_UNSUPPORTED, "IBC / palette CUs are not supported");
+          }
+        }
+    std::stable_sort(jobs.begin(), jobs.end(), [](const std::pair<int32_t, IntraJob> &a, const std::pair<int32_t, IntraJob> &b) {
+      return a.first < b.first;
+    });
+    int maxLev = jobs.empty() ? 0 : jobs.back().first;
+    out.level_start.assign(maxLev + 2, 0);
+    out.jobs.resize(jobs.size());
+    for (size_t i = 0; i < jobs.size(); i++) {
+      out.jobs[i] = jobs[i].second;
+      out.level_start[jobs[i].first + 1] = (int32_t)(i + 1);
+    }
+    for (int L = 1; L <= maxLev + 1; L++) out.level_start[L] = std::max(out.level_start[L], out.level_start[L - 1]);
+  }
+};
+
+}  // namespace
+
+void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out) {
+  out.clear();
+  if (pp.lmcs_enabled) throw VvcrError(VVCR_E_UNSUPPORTED, "LMCS reconstruction is not supported yet");
+  auto P = std::make_unique<Planner>(sp, pp, d, out);
+  P->run();
+}
