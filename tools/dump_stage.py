@@ -16,7 +16,8 @@ from vvc_amd import stream as S  # noqa: E402
 
 def main():
     name, stage = sys.argv[1], sys.argv[2]
-    pics = S.load_sequence(os.path.join(ROOT, "tests", "golden", name))
+    maxp = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    pics = S.load_sequence(os.path.join(ROOT, "tests", "golden", name), maxp)
     by_poc = {p["hdr"]["poc"]: p for p in pics}
     h0 = pics[0]["hdr"]
     ctx = N.Context(h0["width"], h0["height"], dpb_slots=20)
@@ -40,6 +41,10 @@ def main():
             for c, pl in enumerate("yuv"):
                 out["%d_%s" % (poc, pl)] = ctx.read_plane(N.BUF_PRED, 0, c)
             out["%d_dmvr" % poc] = ctx.dmvr_deltas()
+        elif stage == "resid":
+            ctx.end_picture(N.STAGE_RESID)
+            for c, pl in enumerate("yuv"):
+                out["%d_%s" % (poc, pl)] = ctx.read_plane(N.BUF_RESI, 0, c)
         elif stage == "recon":
             ctx.end_picture(N.STAGE_RESID | N.STAGE_INTER | N.STAGE_INTRA)
             for c, pl in enumerate("yuv"):

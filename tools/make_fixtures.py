@@ -54,7 +54,8 @@ def main():
             continue
         if a.descriptors_only:
             for k in list(p):
-                if k.split("_")[0] in GOLDEN_PLANES:
+                parts = k.split("_")
+                if len(parts) == 2 and parts[0] in GOLDEN_PLANES and parts[1] in ("y", "u", "v"):
                     del p[k]
             if h["slice_type"] != 2:      # reference pictures are re-created by the decoder itself
                 for c in "yuv":

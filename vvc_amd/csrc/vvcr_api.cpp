@@ -158,6 +158,7 @@ int vvcr_begin_picture(vvcr_ctx *ctx, const vvcr_pic_params *pp) {
   }
   ctx->pp = *pp;
   ctx->desc.clear();
+  ctx->have_sao = ctx->have_alf = false;   // loop-filter parameters are per picture
   ctx->in_picture = true;
   return VVCR_OK;
   API_END
@@ -341,6 +342,11 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
     const int ctu = 1 << ctx->sp.ctu_log2;
     const int wc = (ctx->sp.width + ctu - 1) / ctu, n = n_ctb(ctx->sp);
     bool inTmp = false;
+    const bool alfOn = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
+    if ((mask & VVCR_STAGE_SAO) && (pp.sao_luma || pp.sao_chroma) && !ctx->have_sao)
+      throw VvcrError(VVCR_E_STATE, "SAO is enabled for the picture but no SAO parameters were set");
+    if ((mask & VVCR_STAGE_ALF) && alfOn && !ctx->have_alf)
+      throw VvcrError(VVCR_E_STATE, "ALF is enabled for the picture but no ALF parameters were set");
     if ((mask & VVCR_STAGE_SAO) && ctx->have_sao && (pp.sao_luma || pp.sao_chroma)) {
       StageTimer t(ctx, ST_SAO);
       SaoParams sp{};
@@ -350,7 +356,6 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
       VVCR_CHECK_HIP(hipGetLastError());
       inTmp = true;
     }
-    const bool alfOn = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
     if ((mask & VVCR_STAGE_ALF) && ctx->have_alf && alfOn) {
       StageTimer t(ctx, ST_ALF);
       AlfParams ap{};
