@@ -1,0 +1,198 @@
+"""Decode throughput of the MI355X reconstruction path (BASELINE.json configs[1]: 1080p random-access
+QP32, 1 GPU): all pictures of the stream reconstructed by libvvcr in decoding order — residuals, motion
+compensation (DMVR/BDOF/affine-PROF/GEO/CIIP), intra waves, deblocking, SAO, ALF/CC-ALF — with every
+input (parsed descriptors, work lists, loop-filter parameters) resident in HBM when the timed region
+starts (vvcr_prepare_picture once, vvcr_launch_picture per step). One step = one decode of the whole
+sequence. The output of the first pass is checked bit-exact against the reference decoder's MD5s.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--stream ra1080_q32] [--no-cpu]
+
+Multi-GPU (torch.distributed.run, one process per GPU): the path has no intra-picture work split in
+this round, so N ranks decode N independent replicas (weak scaling, no data-path collective); the
+timing barrier and max-over-ranks use torch.distributed.
+"""
+import argparse
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from vvc_amd import native as N  # noqa: E402
+from vvc_amd import stream as S  # noqa: E402
+from vvc_amd import decode as D  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (guides/MI355X_MICROARCH.md)
+
+
+def cpu_baseline(stream_bin, pixels_per_run, min_seconds=10.0, max_runs=40):
+    """VTM DecoderApp (the reference, built here from /root/reference by oracle/ref.mk) on the same
+    bitstream, single-threaded, no output file; repeated until ~min_seconds of CPU work."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "DecoderApp")
+    if not os.path.exists(exe):
+        return None
+    runs, total = 0, 0.0
+    while total < min_seconds and runs < max_runs:
+        t0 = time.perf_counter()
+        r = subprocess.run([exe, "-b", stream_bin], capture_output=True, text=True)
+        dt = time.perf_counter() - t0
+        if r.returncode != 0:
+            return None
+        runs += 1
+        total += dt
+    return {"value": round(pixels_per_run * runs / total / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "reference",
+            "sample": "VTM-7.3 DecoderApp (x86 SIMD, 1 thread) decoding %s.bin %d times (%.1f s), parse + reconstruction"
+                      % (os.path.basename(stream_bin)[:-4], runs, total)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--stream", default="ra1080_q32")
+    ap.add_argument("--no-cpu", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend)
+
+    d = os.path.join(ROOT, "tests", "golden", a.stream)
+    pics = S.load_sequence(d)
+    meta = S.load_meta(d)
+    h0 = pics[0]["hdr"]
+    W, H = h0["width"], h0["height"]
+    px_seq = W * H * len(pics)
+
+    # ---- prepare every picture once (host planning + upload), decoding order, own DPB slots
+    dec = D.Decoder(pics, dpb_slots=12, device=local)
+    ctx = dec.ctx
+    handles, slots = [], []
+    t_prep = time.perf_counter()
+    for i, p in enumerate(pics):
+        slot = dec.alloc.assign(i, p["hdr"]["poc"])
+        ctx.begin_picture(S.pic_params(p, slot, dec.alloc.slot_of))
+        S.submit(ctx, p)
+        S.set_loop_filter_params(ctx, p)
+        handles.append(ctx.prepare(N.STAGE_ALL))
+        slots.append((p["hdr"]["poc"], slot))
+    t_prep = time.perf_counter() - t_prep
+
+    # ---- first pass: bit-exactness against the reference decoder (untimed)
+    yuv = hashlib.md5()
+    outs = {}
+    for hnd, (poc, slot) in zip(handles, slots):
+        ctx.launch(hnd)
+        outs[poc] = D.plane_md5s(dec.read(slot)), dec.read(slot)
+    bitexact = all(outs[int(k)][0] == v for k, v in meta["poc_plane_md5"].items())
+    for poc in sorted(outs):
+        for pl in outs[poc][1]:
+            yuv.update(np.ascontiguousarray(pl).astype("<u2").tobytes())
+    bitexact = bitexact and yuv.hexdigest() == meta["yuv_md5"]
+    outs = None
+
+    def run_step():
+        for hnd in handles:
+            ctx.launch(hnd)
+
+    for _ in range(a.warmup):
+        run_step()
+    ctx.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        run_step()
+    ctx.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- per-kernel timing of the last step (HIP events on the library stream)
+    kern = {}
+    for hnd in handles:
+        for name, launches, ms, alg in ctx.kernel_stats(hnd):
+            k = kern.setdefault(name, [0, 0.0, 0.0])
+            k[0] += launches
+            k[1] += ms
+            k[2] += alg
+    dom = max(kern, key=lambda k: kern[k][1])
+    dl, dms, dalg = kern[dom]
+    per_launch_bytes = dalg / max(dl, 1)
+    per_launch_s = dms / 1e3 / max(dl, 1)
+    achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+    mc = kern.get("mc", [0, 0.0, 0.0])
+    mc_gbs = mc[2] / (mc[1] / 1e3) / 1e9 if mc[1] > 0 else 0.0
+
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    if os.path.exists(tf):
+        with open(tf) as f:
+            traffic = json.load(f).get("per_launch_bytes", {}).get(dom)
+
+    ms_step = elapsed / a.steps * 1e3
+    value = world * px_seq * a.steps / elapsed / 1e6
+    line = {
+        "metric": "decode Mpixels/sec (CABAC on host), bit-exact YUV vs DecoderApp, 1/2/4/8 GPU",
+        "value": round(value, 2),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int16",
+        "data": "synthetic (VTM-7.3-encoded synthetic 1080p RA QP32 stream, parsed descriptors resident in HBM)",
+        "config": {"workload": "%s: %dx%d random access QP32, %d pictures, reconstruction + DBK/SAO/ALF" % (a.stream, W, H, len(pics)),
+                   "parallelism": "replicas%d" % world, "bitexact_vs_reference": bool(bitexact)},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic},
+        "kernels": {k: {"ms_per_step": round(v[1], 4), "launches_per_step": v[0],
+                        "alg_GBps": round(v[2] / (v[1] / 1e3) / 1e9, 2) if v[1] > 0 else 0.0} for k, v in kern.items()},
+        "mc_kernel_GBps": round(mc_gbs, 2),
+        "host_prepare_s": round(t_prep, 3),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, "tests", "golden", "streams", a.stream + ".bin"), px_seq)
+    else:
+        line["cpu_baseline"] = None
+    for hnd in handles:
+        ctx.release(hnd)
+    dec.close()
+    if rank == 0:
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+    if not bitexact:
+        sys.exit("bench: output is not bit-exact to the reference decoder")
+
+
+if __name__ == "__main__":
+    main()

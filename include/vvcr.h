@@ -173,6 +173,25 @@ int vvcr_set_loop_filter_params(vvcr_ctx *ctx, const vvcr_sao *sao /* [n_ctb][3]
 #define VVCR_STAGE_ALL 0x7f
 int vvcr_end_picture(vvcr_ctx *ctx);
 int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t stage_mask);
+
+/* Two-phase form of vvcr_end_picture: prepare plans the picture on the host and uploads every input
+ * (descriptors, work lists, loop-filter parameters) into device memory owned by the returned handle;
+ * launch enqueues the picture's kernels (reading device-resident data only) and may be repeated, e.g.
+ * to replay a resident sequence; release frees the handle after its last launch completed. */
+int vvcr_prepare_picture(vvcr_ctx *ctx, uint32_t stage_mask, int32_t *handle);
+int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle);
+int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle);
+
+/* Per-kernel-group statistics of the last launch of a picture (handle 0 = the last launched picture):
+ * HIP-event time on the library stream, number of kernel launches in the group and the algorithmic
+ * bytes (each logical input and output counted once, 2 bytes per sample). Returns the number of groups. */
+typedef struct vvcr_kernel_stat {
+  char name[16];
+  int32_t launches;
+  float ms;
+  double alg_bytes;
+} vvcr_kernel_stat;
+int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int32_t n);
 int vvcr_sync(vvcr_ctx *ctx);
 
 /* Buffers addressable by vvcr_read_plane / vvcr_write_plane (tests and output). */

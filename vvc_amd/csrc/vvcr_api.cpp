@@ -1,7 +1,15 @@
-// vvcr_api.cpp — C-ABI implementation of libvvcr: device DPB, descriptor staging, per-picture work-list
-// construction on the host (C++), kernel launches on one ordered HIP stream.
+// vvcr_api.cpp — C-ABI implementation of libvvcr: device DPB, descriptor staging, per-picture work
+// planning on the host (C++) and kernel launches on one ordered HIP stream.
+//
+// A picture goes through two phases: prepare (host planning of every work list + upload of the
+// descriptors / lists / loop-filter parameters into device buffers owned by a Prepared record) and
+// launch (enqueue the kernels that read only device-resident data). vvcr_end_picture does both;
+// vvcr_prepare_picture / vvcr_launch_picture expose them separately so that a caller (or bench.py) can
+// keep pictures resident and replay them, and so that host planning of picture N+1 can overlap the GPU
+// work of picture N.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -22,16 +30,21 @@ struct DevVec {
   size_t cap = 0;
   void ensure(size_t n) {
     if (n <= cap) return;
-    if (p) hipFree(p);
+    if (p) VVCR_CHECK_HIP(hipFree(p));
     size_t c = std::max<size_t>(n, cap * 3 / 2 + 64);
     VVCR_CHECK_HIP(hipMalloc(&p, c * sizeof(T)));
     cap = c;
   }
-  void upload(const std::vector<T> &v, hipStream_t s) {
-    ensure(v.size() + 1);
-    if (!v.empty()) VVCR_CHECK_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  // synchronous upload: the caller guarantees no kernel is reading this buffer (Prepared::wait)
+  void upload(const T *src, size_t n) {
+    ensure(n + 1);
+    if (n) VVCR_CHECK_HIP(hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
   }
-  ~DevVec() { if (p) hipFree(p); }
+  void upload(const std::vector<T> &v) { upload(v.data(), v.size()); }
+  DevVec() = default;
+  DevVec(const DevVec &) = delete;
+  DevVec &operator=(const DevVec &) = delete;
+  ~DevVec() { if (p) (void)hipFree(p); }
 };
 
 DPlane alloc_plane(int w, int h) {
@@ -42,6 +55,62 @@ DPlane alloc_plane(int w, int h) {
   VVCR_CHECK_HIP(hipMemset(d.p, 0, (size_t)d.stride * h * sizeof(int16_t)));
   return d;
 }
+
+// kernel groups timed with HIP events (vvcr_kernel_stats)
+enum { K_RESID, K_MC, K_MC_BIDIR, K_MC_AFFINE, K_RECON, K_INTRA, K_DBK, K_SAO, K_ALF, NK };
+const char *const kKernelNames[NK] = {"resid", "mc", "mc_bidir", "mc_affine", "recon_inter", "intra", "deblock", "sao", "alf"};
+// stage of each kernel group (bit index in VVCR_STAGE_*)
+const int kKernelStage[NK] = {0, 1, 1, 1, 2, 2, 4, 5, 6};
+
+struct Prepared {
+  vvcr_pic_params pp{};
+  uint32_t mask = 0;
+  DevVec<int32_t> coef;
+  DevVec<TbJob> tb;
+  DevVec<McJob> mc_basic, mc_bidir;
+  DevVec<AffPu> aff_pu;
+  DevVec<AffJob> aff_jobs;
+  DevVec<int32_t> order;
+  DevVec<ReconTile> tiles;
+  DevVec<IntraJob> ijobs;
+  std::vector<int32_t> level_start;
+  DevVec<DbkSeg> dbk;
+  int dbk_counts[4] = {0, 0, 0, 0};
+  DevVec<int32_t> sao;
+  DevVec<int16_t> alf_luma_coef, alf_luma_clip, alf_chroma, alf_cc, alf_set;
+  DevVec<uint8_t> alf_ctb;
+  DevVec<int32_t> dmvr;
+  bool have_sao = false, have_alf = false;
+  int n_tb = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
+  size_t n_order = 0;
+  hipEvent_t ev[NK][2] = {};
+  hipEvent_t done = nullptr;
+  bool ran[NK] = {};
+  bool launched = false;
+  double alg_bytes[NK] = {};
+  int launches[NK] = {};
+
+  Prepared() {
+    for (auto &e : ev) { VVCR_CHECK_HIP(hipEventCreate(&e[0])); VVCR_CHECK_HIP(hipEventCreate(&e[1])); }
+    VVCR_CHECK_HIP(hipEventCreate(&done));
+  }
+  ~Prepared() {
+    for (auto &e : ev) { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); }
+    (void)hipEventDestroy(done);
+  }
+  void wait() { if (launched) VVCR_CHECK_HIP(hipEventSynchronize(done)); }
+};
+
+struct KernelTimer {
+  Prepared &r;
+  int k;
+  hipStream_t s;
+  KernelTimer(Prepared &rr, int kk, hipStream_t ss) : r(rr), k(kk), s(ss) {
+    r.ran[k] = true;
+    VVCR_CHECK_HIP(hipEventRecord(r.ev[k][0], s));
+  }
+  ~KernelTimer() { (void)hipEventRecord(r.ev[k][1], s); }
+};
 
 }  // namespace
 
@@ -54,32 +123,21 @@ struct vvcr_ctx {
   vvcr_pic_params pp{};
   bool in_picture = false;
   PictureDescriptors desc;          // host copy of the submitted descriptors (vvcr_host.h)
-  WorkLists wl;                     // host-built work lists
-  DevVec<McJob> d_mc_basic, d_mc_bidir;
-  DevVec<AffPu> d_aff_pu;
-  DevVec<AffJob> d_aff_jobs;
-  DevVec<int32_t> d_dmvr;           // DMVR deltas of the last picture, [n][2]
-  int n_dmvr = 0;
-  DevVec<TbJob> d_tb;
-  DevVec<int32_t> d_coef;
+  // loop-filter parameters of the current picture (host copies until prepare)
+  bool have_sao = false, have_alf = false;
+  std::vector<int32_t> h_sao;
+  std::vector<int16_t> h_alf_luma_coef, h_alf_luma_clip, h_alf_chroma, h_alf_cc, h_alf_set;
+  std::vector<uint8_t> h_alf_ctb;
+  // planning scratch
+  WorkLists wl;
+  IntraPlan intra;
+  DbkLists dbk;
   DevVec<uint16_t> d_scans;
   ScanTables scans;
-  // loop-filter parameters of the current picture
-  DevVec<int32_t> d_sao;
-  DevVec<int16_t> d_alf_luma_coef, d_alf_luma_clip, d_alf_chroma, d_alf_cc;
-  DevVec<uint8_t> d_alf_ctb;      // ctb_en[3n] | ctb_alt[3n] | cc_ctl[2n]
-  DevVec<int16_t> d_alf_set;
-  IntraPlan intra;
-  DevVec<int32_t> d_order;          // luma | chroma order maps
-  DevVec<ReconTile> d_tiles;
-  DevVec<IntraJob> d_ijobs;
-  DbkLists dbk;
-  std::vector<DbkSeg> dbk_all;
-  DevVec<DbkSeg> d_dbk;
-  bool have_sao = false, have_alf = false;
-  hipEvent_t ev[2] = {};            // whole end_picture call
-  hipEvent_t sev[7][2] = {};        // per stage begin / end
-  bool stage_ran[7] = {};
+  // prepared pictures: index 0 is the scratch record of vvcr_end_picture
+  std::vector<std::unique_ptr<Prepared>> prepared;
+  Prepared *last = nullptr;          // last launched (stage times, DMVR deltas)
+  hipEvent_t ev[2] = {};             // whole last launch
 };
 
 #define API_BEGIN try {
@@ -88,14 +146,253 @@ struct vvcr_ctx {
   catch (const VvcrError &e) { ctx->err = e.msg; return e.code; } \
   catch (const std::exception &e) { ctx->err = e.what(); return VVCR_E_STATE; }
 
+static int n_ctb(const vvcr_seq_params &sp) {
+  const int ctu = 1 << sp.ctu_log2;
+  return ((sp.width + ctu - 1) / ctu) * ((sp.height + ctu - 1) / ctu);
+}
+
+static McParams make_mc_params(vvcr_ctx *ctx) {
+  McParams P{};
+  for (size_t s = 0; s < ctx->dpb.size() && s < 32; s++)
+    for (int c = 0; c < 3; c++) P.ref[s][c] = ctx->dpb[s][c];
+  for (int c = 0; c < 3; c++) P.out[c] = ctx->pred[c];
+  P.pic_w = ctx->sp.width;
+  P.pic_h = ctx->sp.height;
+  P.bd = ctx->sp.bit_depth;
+  P.ctu = 1 << ctx->sp.ctu_log2;
+  return P;
+}
+
+// ---- algorithmic bytes: each logical input once, each output once, 2 B / sample
+static double mc_bytes(const McJob &j) {
+  const int lists = ((j.flags & MC_L0) ? 1 : 0) + ((j.flags & MC_L1) ? 1 : 0);
+  const double in = (double)(j.w + 7) * (j.h + 7) + 2.0 * (j.w / 2 + 3) * (j.h / 2 + 3);
+  return 2.0 * (lists * in + 1.5 * j.w * j.h);
+}
+
+// Host phase: every work list of the current picture, uploaded into r.
+static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
+  r.wait();
+  r.pp = ctx->pp;
+  r.mask = mask;
+  r.launched = false;
+  for (int k = 0; k < NK; k++) { r.alg_bytes[k] = 0; r.launches[k] = 0; r.ran[k] = false; }
+  const vvcr_seq_params &sp = ctx->sp;
+  const vvcr_pic_params &pp = ctx->pp;
+  const double pix = (double)sp.width * sp.height * 1.5;   // samples of the three planes
+  if (mask & (VVCR_STAGE_RESID | VVCR_STAGE_INTER)) build_work_lists(sp, pp, ctx->desc, ctx->wl);
+  if (mask & VVCR_STAGE_RESID) {
+    r.coef.upload(ctx->desc.coef);
+    r.tb.upload(ctx->wl.tb);
+    r.n_tb = (int)ctx->wl.tb.size();
+    double b = 0;
+    for (const TbJob &t : ctx->wl.tb) b += (double)t.w * t.h * (4 + 2);   // int32 levels in, int16 residual out
+    r.alg_bytes[K_RESID] = b;
+  }
+  if (mask & VVCR_STAGE_INTER) {
+    if (ctx->wl.n_unsupported_inter)
+      throw VvcrError(VVCR_E_UNSUPPORTED, std::to_string(ctx->wl.n_unsupported_inter) + " inter CUs use tools not supported yet");
+    r.mc_basic.upload(ctx->wl.mc_basic);
+    r.mc_bidir.upload(ctx->wl.mc_bidir);
+    r.aff_pu.upload(ctx->wl.aff_pu);
+    r.aff_jobs.upload(ctx->wl.aff_jobs);
+    r.n_basic = (int)ctx->wl.mc_basic.size();
+    r.n_bidir = (int)ctx->wl.mc_bidir.size();
+    r.n_aff = (int)ctx->wl.aff_jobs.size();
+    r.n_dmvr = ctx->wl.n_dmvr;
+    r.dmvr.ensure(2 * (size_t)r.n_dmvr + 2);
+    double b = 0;
+    for (const McJob &j : ctx->wl.mc_basic) b += mc_bytes(j);
+    r.alg_bytes[K_MC] = b;
+    b = 0;
+    for (const McJob &j : ctx->wl.mc_bidir) b += mc_bytes(j);
+    r.alg_bytes[K_MC_BIDIR] = b;
+    b = 0;
+    for (const AffJob &j : ctx->wl.aff_jobs) {
+      const AffPu &U = ctx->wl.aff_pu[j.pu];
+      const int lists = U.l[0].present + U.l[1].present;
+      const double nsb = (j.w / 4.0) * (j.h / 4.0);
+      b += 2.0 * (lists * nsb * (81 + 2 * 0.25 * 49) + 1.5 * j.w * j.h);   // 6-tap (4+5)^2 luma, 4-tap chroma
+    }
+    r.alg_bytes[K_MC_AFFINE] = b;
+  }
+  if (mask & VVCR_STAGE_INTRA) {
+    plan_intra(sp, pp, ctx->desc, ctx->intra);
+    IntraPlan &ip = ctx->intra;
+    r.n_order = ip.order[0].size();
+    std::vector<int32_t> ord(ip.order[0]);
+    ord.insert(ord.end(), ip.order[1].begin(), ip.order[1].end());
+    r.order.upload(ord);
+    r.tiles.upload(ip.inter_tiles);
+    r.ijobs.upload(ip.jobs);
+    r.level_start = ip.level_start;
+    r.n_tiles = (int)ip.inter_tiles.size();
+    double b = 0;
+    for (const ReconTile &t : ip.inter_tiles) b += (double)t.w * t.h * 1.5 * 2 * 3;   // pred + resi in, reco out
+    r.alg_bytes[K_RECON] = b;
+    b = 0;
+    for (const IntraJob &j : ip.jobs) b += (double)j.w * j.h * 2 * 2 + 2.0 * 2 * (2 * j.w + 2 * j.h);   // resi in, reco out, refs
+    r.alg_bytes[K_INTRA] = b;
+  }
+  if (mask & VVCR_STAGE_DBK) {
+    plan_deblocking(sp, pp, ctx->desc, ctx->dbk);
+    std::vector<DbkSeg> all;
+    const std::vector<DbkSeg> *parts[4] = {&ctx->dbk.luma[0], &ctx->dbk.chroma[0], &ctx->dbk.luma[1], &ctx->dbk.chroma[1]};
+    for (int k = 0; k < 4; k++) {
+      r.dbk_counts[k] = (int)parts[k]->size();
+      all.insert(all.end(), parts[k]->begin(), parts[k]->end());
+    }
+    r.dbk.upload(all);
+    r.alg_bytes[K_DBK] = pix * 2 * 2;
+  }
+  const bool saoOn = pp.sao_luma || pp.sao_chroma;
+  const bool alfOn = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
+  if ((mask & VVCR_STAGE_SAO) && saoOn && !ctx->have_sao)
+    throw VvcrError(VVCR_E_STATE, "SAO is enabled for the picture but no SAO parameters were set");
+  if ((mask & VVCR_STAGE_ALF) && alfOn && !ctx->have_alf)
+    throw VvcrError(VVCR_E_STATE, "ALF is enabled for the picture but no ALF parameters were set");
+  r.have_sao = (mask & VVCR_STAGE_SAO) && saoOn;
+  r.have_alf = (mask & VVCR_STAGE_ALF) && alfOn;
+  if (r.have_sao) {
+    r.sao.upload(ctx->h_sao);
+    r.alg_bytes[K_SAO] = pix * 2 * 2;
+  }
+  if (r.have_alf) {
+    r.alf_luma_coef.upload(ctx->h_alf_luma_coef);
+    r.alf_luma_clip.upload(ctx->h_alf_luma_clip);
+    r.alf_chroma.upload(ctx->h_alf_chroma);
+    r.alf_cc.upload(ctx->h_alf_cc);
+    r.alf_ctb.upload(ctx->h_alf_ctb);
+    r.alf_set.upload(ctx->h_alf_set);
+    r.alg_bytes[K_ALF] = pix * 2 * 2;
+  }
+}
+
+// Device phase: enqueue the kernels of a prepared picture on the context stream.
+static void launch(vvcr_ctx *ctx, Prepared &r) {
+  hipStream_t s = ctx->stream;
+  const vvcr_pic_params &pp = r.pp;
+  const uint32_t mask = r.mask;
+  VVCR_CHECK_HIP(hipEventRecord(ctx->ev[0], s));
+  if (mask & VVCR_STAGE_RESID) {
+    KernelTimer t(r, K_RESID, s);
+    for (int c = 0; c < 3; c++)
+      VVCR_CHECK_HIP(hipMemsetAsync(ctx->resi[c].p, 0, (size_t)ctx->resi[c].stride * ctx->resi[c].h * 2, s));
+    TbParams tp{};
+    for (int c = 0; c < 3; c++) tp.out[c] = ctx->resi[c];
+    tp.bd = ctx->sp.bit_depth;
+    memcpy(tp.scan_off, ctx->scans.off, sizeof(tp.scan_off));
+    memcpy(tp.lfnst_scan_off, ctx->scans.lfnst_off, sizeof(tp.lfnst_scan_off));
+    launch_resid(tp, r.tb.p, r.n_tb, r.coef.p, ctx->d_scans.p, s);
+    VVCR_CHECK_HIP(hipGetLastError());
+    r.launches[K_RESID] = r.n_tb ? 1 : 0;
+  }
+  if (mask & VVCR_STAGE_INTER) {
+    const McParams mp = make_mc_params(ctx);
+    {
+      KernelTimer t(r, K_MC, s);
+      launch_mc_basic(mp, r.mc_basic.p, r.n_basic, s);
+      VVCR_CHECK_HIP(hipGetLastError());
+      r.launches[K_MC] = r.n_basic ? 1 : 0;
+    }
+    {
+      KernelTimer t(r, K_MC_BIDIR, s);
+      launch_mc_bidir(mp, r.mc_bidir.p, r.n_bidir, r.dmvr.p, s);
+      VVCR_CHECK_HIP(hipGetLastError());
+      r.launches[K_MC_BIDIR] = r.n_bidir ? 1 : 0;
+    }
+    {
+      KernelTimer t(r, K_MC_AFFINE, s);
+      launch_mc_affine(mp, r.aff_jobs.p, r.n_aff, r.aff_pu.p, s);
+      VVCR_CHECK_HIP(hipGetLastError());
+      r.launches[K_MC_AFFINE] = r.n_aff ? 1 : 0;
+    }
+  }
+  if (mask & VVCR_STAGE_INTRA) {
+    IntraParams P{};
+    for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
+    P.order[0] = r.order.p;
+    P.order[1] = r.order.p + r.n_order;
+    P.W4 = ctx->sp.width / 4;
+    P.bd = ctx->sp.bit_depth;
+    P.ctu = 1 << ctx->sp.ctu_log2;
+    {
+      KernelTimer t(r, K_RECON, s);
+      launch_recon_inter(P, r.tiles.p, r.n_tiles, s);
+      VVCR_CHECK_HIP(hipGetLastError());
+      r.launches[K_RECON] = r.n_tiles ? 1 : 0;
+    }
+    {
+      KernelTimer t(r, K_INTRA, s);
+      int n = 0;
+      for (size_t L = 1; L + 1 < r.level_start.size(); L++) {
+        const int a = r.level_start[L], b = r.level_start[L + 1];
+        if (b > a) { launch_intra_level(P, r.ijobs.p + a, b - a, s); n++; }
+      }
+      VVCR_CHECK_HIP(hipGetLastError());
+      r.launches[K_INTRA] = n;
+    }
+  }
+  auto &A = ctx->dpb[pp.slot];
+  if ((mask & VVCR_STAGE_DBK) && (r.dbk_counts[0] + r.dbk_counts[1] + r.dbk_counts[2] + r.dbk_counts[3])) {
+    KernelTimer t(r, K_DBK, s);
+    DbkParams dp{};
+    for (int c = 0; c < 3; c++) dp.pl[c] = A[c];
+    dp.bd = ctx->sp.bit_depth;
+    dp.beta_offset_div2 = pp.dbk_beta_offset_div2;
+    dp.tc_offset_div2 = pp.dbk_tc_offset_div2;
+    launch_dbk(dp, r.dbk.p, r.dbk_counts, s);
+    r.launches[K_DBK] = (r.dbk_counts[0] > 0) + (r.dbk_counts[1] > 0) + (r.dbk_counts[2] > 0) + (r.dbk_counts[3] > 0);
+  }
+  // SAO (slot -> tmp) and ALF (ping-pong back); the final picture always ends in the slot
+  const int ctu = 1 << ctx->sp.ctu_log2;
+  const int wc = (ctx->sp.width + ctu - 1) / ctu, n = n_ctb(ctx->sp);
+  bool inTmp = false;
+  if (r.have_sao) {
+    KernelTimer t(r, K_SAO, s);
+    SaoParams sp{};
+    for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ctx->tmp[c]; }
+    sp.sao = r.sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
+    launch_sao(sp, s);
+    VVCR_CHECK_HIP(hipGetLastError());
+    inTmp = true;
+    r.launches[K_SAO] = 3;
+  }
+  if (r.have_alf) {
+    KernelTimer t(r, K_ALF, s);
+    AlfParams ap{};
+    for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ctx->tmp[c] : A[c]; ap.dst[c] = inTmp ? A[c] : ctx->tmp[c]; }
+    ap.bd = ctx->sp.bit_depth; ap.ctu_log2 = ctx->sp.ctu_log2; ap.wc = wc; ap.nctb = n;
+    ap.vb_luma = pp.alf_vb_luma; ap.vb_chroma = pp.alf_vb_chroma;
+    for (int c = 0; c < 3; c++) ap.en[c] = pp.alf_en[c];
+    ap.en[3] = pp.ccalf_en[0]; ap.en[4] = pp.ccalf_en[1];
+    ap.luma_coef = r.alf_luma_coef.p; ap.luma_clip = r.alf_luma_clip.p;
+    ap.chroma_coef = r.alf_chroma.p; ap.chroma_clip = r.alf_chroma.p + 56; ap.cc_coef = r.alf_cc.p;
+    ap.ctb_en = r.alf_ctb.p; ap.ctb_alt = r.alf_ctb.p + 3 * n; ap.cc_ctl = r.alf_ctb.p + 6 * n;
+    ap.ctb_set = r.alf_set.p;
+    launch_alf(ap, s);
+    VVCR_CHECK_HIP(hipGetLastError());
+    inTmp = !inTmp;
+    r.launches[K_ALF] = 2;
+  }
+  if (inTmp)
+    for (int c = 0; c < 3; c++)
+      VVCR_CHECK_HIP(hipMemcpy2DAsync(A[c].p, A[c].stride * 2, ctx->tmp[c].p, ctx->tmp[c].stride * 2, A[c].w * 2, A[c].h,
+                                      hipMemcpyDeviceToDevice, s));
+  VVCR_CHECK_HIP(hipEventRecord(ctx->ev[1], s));
+  VVCR_CHECK_HIP(hipEventRecord(r.done, s));
+  r.launched = true;
+  ctx->last = &r;
+}
+
 extern "C" {
 
 int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
   if (!sp || !out) return VVCR_E_ARG;
   *out = nullptr;
   if (sp->chroma_format != 1 || sp->bit_depth < 8 || sp->bit_depth > 10 || sp->width <= 0 || sp->height <= 0 ||
-      sp->dpb_slots <= 0 || sp->dpb_slots > 32) {
-    g_create_error = "unsupported sequence parameters (4:2:0, 8..10 bit, <= 32 DPB slots)";
+      sp->dpb_slots <= 0 || sp->dpb_slots > 32 || sp->width % 8 || sp->height % 8 || sp->ctu_log2 < 5 || sp->ctu_log2 > 7) {
+    g_create_error = "unsupported sequence parameters (4:2:0, 8..10 bit, size multiple of 8, CTU 32..128, <= 32 DPB slots)";
     return VVCR_E_UNSUPPORTED;
   }
   auto ctx = std::make_unique<vvcr_ctx>();
@@ -117,10 +414,9 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       ctx->tmp[c] = alloc_plane(w, h);
     }
     for (auto &e : ctx->ev) VVCR_CHECK_HIP(hipEventCreate(&e));
-    for (auto &se : ctx->sev)
-      for (auto &e : se) VVCR_CHECK_HIP(hipEventCreate(&e));
     build_scan_tables(ctx->scans);
-    ctx->d_scans.upload(ctx->scans.data, ctx->stream);
+    ctx->d_scans.upload(ctx->scans.data);
+    ctx->prepared.emplace_back(new Prepared());   // scratch record of vvcr_end_picture
   } catch (const VvcrError &e) {
     g_create_error = e.msg;
     return e.code;
@@ -131,14 +427,13 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
 
 int vvcr_destroy(vvcr_ctx *ctx) {
   if (!ctx) return VVCR_E_ARG;
-  hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->stream);
+  ctx->prepared.clear();
   for (auto &s : ctx->dpb)
-    for (auto &p : s) hipFree(p.p);
-  for (int c = 0; c < 3; c++) { hipFree(ctx->pred[c].p); hipFree(ctx->resi[c].p); hipFree(ctx->tmp[c].p); }
-  for (auto &e : ctx->ev) if (e) hipEventDestroy(e);
-  for (auto &se : ctx->sev)
-    for (auto &e : se) if (e) hipEventDestroy(e);
-  hipStreamDestroy(ctx->stream);
+    for (auto &p : s) (void)hipFree(p.p);
+  for (int c = 0; c < 3; c++) { (void)hipFree(ctx->pred[c].p); (void)hipFree(ctx->resi[c].p); (void)hipFree(ctx->tmp[c].p); }
+  for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return VVCR_OK;
 }
@@ -184,206 +479,108 @@ int vvcr_submit(vvcr_ctx *ctx, const vvcr_cu *cu, int32_t ncu, const vvcr_pu *pu
   API_END
 }
 
-static int n_ctb(const vvcr_seq_params &sp) {
-  const int ctu = 1 << sp.ctu_log2;
-  return ((sp.width + ctu - 1) / ctu) * ((sp.height + ctu - 1) / ctu);
-}
-
 int vvcr_set_loop_filter_params(vvcr_ctx *ctx, const vvcr_sao *sao, const vvcr_alf *alf) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_set_loop_filter_params outside begin/end picture");
   const int n = n_ctb(ctx->sp);
-  hipStream_t s = ctx->stream;
   ctx->have_sao = sao != nullptr;
-  if (sao) {
-    std::vector<int32_t> v((const int32_t *)sao, (const int32_t *)sao + (size_t)n * 3 * 35);
-    ctx->d_sao.upload(v, s);
-  }
+  if (sao) ctx->h_sao.assign((const int32_t *)sao, (const int32_t *)sao + (size_t)n * 3 * 35);
   ctx->have_alf = alf != nullptr;
   if (alf) {
     if (alf->num_luma_sets < 16 || alf->num_luma_sets > 24) throw VvcrError(VVCR_E_ARG, "bad ALF luma set count");
     const size_t L = (size_t)alf->num_luma_sets * 25 * 13;
-    ctx->d_alf_luma_coef.upload(std::vector<int16_t>(alf->luma_coef, alf->luma_coef + L), s);
-    ctx->d_alf_luma_clip.upload(std::vector<int16_t>(alf->luma_clip, alf->luma_clip + L), s);
-    std::vector<int16_t> ch(alf->chroma_coef, alf->chroma_coef + 56);
-    ch.insert(ch.end(), alf->chroma_clip, alf->chroma_clip + 56);
-    ctx->d_alf_chroma.upload(ch, s);
-    ctx->d_alf_cc.upload(std::vector<int16_t>(alf->cc_coef, alf->cc_coef + 64), s);
-    std::vector<uint8_t> ctb(alf->ctb_en, alf->ctb_en + 3 * n);
+    ctx->h_alf_luma_coef.assign(alf->luma_coef, alf->luma_coef + L);
+    ctx->h_alf_luma_clip.assign(alf->luma_clip, alf->luma_clip + L);
+    ctx->h_alf_chroma.assign(alf->chroma_coef, alf->chroma_coef + 56);
+    ctx->h_alf_chroma.insert(ctx->h_alf_chroma.end(), alf->chroma_clip, alf->chroma_clip + 56);
+    ctx->h_alf_cc.assign(alf->cc_coef, alf->cc_coef + 64);
+    auto &ctb = ctx->h_alf_ctb;
+    ctb.assign(alf->ctb_en, alf->ctb_en + 3 * n);
     ctb.insert(ctb.end(), alf->ctb_alt, alf->ctb_alt + 3 * n);
     ctb.insert(ctb.end(), alf->cc_ctl, alf->cc_ctl + 2 * n);
     for (int i = 0; i < 3 * n; i++) if (ctb[3 * n + i] > 7) throw VvcrError(VVCR_E_ARG, "bad ALF chroma alternative");
     for (int i = 0; i < 2 * n; i++) if (ctb[6 * n + i] > 4) throw VvcrError(VVCR_E_ARG, "bad CC-ALF filter index");
-    std::vector<int16_t> set(alf->ctb_filter_set, alf->ctb_filter_set + n);
-    for (int v : set) if (v < 0 || v >= alf->num_luma_sets) throw VvcrError(VVCR_E_ARG, "bad ALF filter set index");
-    ctx->d_alf_ctb.upload(ctb, s);
-    ctx->d_alf_set.upload(set, s);
+    ctx->h_alf_set.assign(alf->ctb_filter_set, alf->ctb_filter_set + n);
+    for (int v : ctx->h_alf_set) if (v < 0 || v >= alf->num_luma_sets) throw VvcrError(VVCR_E_ARG, "bad ALF filter set index");
   }
   return VVCR_OK;
   API_END
 }
 
-static McParams make_mc_params(vvcr_ctx *ctx) {
-  McParams P{};
-  for (size_t s = 0; s < ctx->dpb.size() && s < 32; s++)
-    for (int c = 0; c < 3; c++) P.ref[s][c] = ctx->dpb[s][c];
-  for (int c = 0; c < 3; c++) P.out[c] = ctx->pred[c];
-  P.pic_w = ctx->sp.width;
-  P.pic_h = ctx->sp.height;
-  P.bd = ctx->sp.bit_depth;
-  P.ctu = 1 << ctx->sp.ctu_log2;
-  return P;
-}
-
-namespace {
-enum { ST_RESID, ST_INTER, ST_INTRA, ST_LMCS, ST_DBK, ST_SAO, ST_ALF };
-struct StageTimer {
-  vvcr_ctx *c;
-  int k;
-  StageTimer(vvcr_ctx *cc, int kk) : c(cc), k(kk) {
-    c->stage_ran[k] = true;
-    VVCR_CHECK_HIP(hipEventRecord(c->sev[k][0], c->stream));
-  }
-  ~StageTimer() { (void)hipEventRecord(c->sev[k][1], c->stream); }
-};
-}  // namespace
-
 int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_end_picture without begin");
-  build_work_lists(ctx->sp, ctx->pp, ctx->desc, ctx->wl);
-  if (mask & VVCR_STAGE_DBK) plan_deblocking(ctx->sp, ctx->pp, ctx->desc, ctx->dbk);
-  if (mask & VVCR_STAGE_INTRA) plan_intra(ctx->sp, ctx->pp, ctx->desc, ctx->intra);
-  for (bool &r : ctx->stage_ran) r = false;
-  hipStream_t s = ctx->stream;
-  VVCR_CHECK_HIP(hipEventRecord(ctx->ev[0], s));
-  if (mask & VVCR_STAGE_RESID) {
-    StageTimer t(ctx, ST_RESID);
-    for (int c = 0; c < 3; c++)
-      VVCR_CHECK_HIP(hipMemsetAsync(ctx->resi[c].p, 0, (size_t)ctx->resi[c].stride * ctx->resi[c].h * 2, s));
-    ctx->d_coef.upload(ctx->desc.coef, s);
-    ctx->d_tb.upload(ctx->wl.tb, s);
-    TbParams tp{};
-    for (int c = 0; c < 3; c++) tp.out[c] = ctx->resi[c];
-    tp.bd = ctx->sp.bit_depth;
-    memcpy(tp.scan_off, ctx->scans.off, sizeof(tp.scan_off));
-    memcpy(tp.lfnst_scan_off, ctx->scans.lfnst_off, sizeof(tp.lfnst_scan_off));
-    launch_resid(tp, ctx->d_tb.p, (int)ctx->wl.tb.size(), ctx->d_coef.p, ctx->d_scans.p, s);
-    VVCR_CHECK_HIP(hipGetLastError());
-  }
-  if (mask & VVCR_STAGE_INTER) {
-    StageTimer t(ctx, ST_INTER);
-    if (ctx->wl.n_unsupported_inter)
-      throw VvcrError(VVCR_E_UNSUPPORTED, std::to_string(ctx->wl.n_unsupported_inter) + " inter CUs use tools not supported yet");
-    const McParams mp = make_mc_params(ctx);
-    ctx->d_mc_basic.upload(ctx->wl.mc_basic, s);
-    launch_mc_basic(mp, ctx->d_mc_basic.p, (int)ctx->wl.mc_basic.size(), s);
-    VVCR_CHECK_HIP(hipGetLastError());
-    ctx->n_dmvr = ctx->wl.n_dmvr;
-    ctx->d_dmvr.ensure(2 * (size_t)ctx->n_dmvr + 2);
-    ctx->d_mc_bidir.upload(ctx->wl.mc_bidir, s);
-    launch_mc_bidir(mp, ctx->d_mc_bidir.p, (int)ctx->wl.mc_bidir.size(), ctx->d_dmvr.p, s);
-    VVCR_CHECK_HIP(hipGetLastError());
-    ctx->d_aff_pu.upload(ctx->wl.aff_pu, s);
-    ctx->d_aff_jobs.upload(ctx->wl.aff_jobs, s);
-    launch_mc_affine(mp, ctx->d_aff_jobs.p, (int)ctx->wl.aff_jobs.size(), ctx->d_aff_pu.p, s);
-    VVCR_CHECK_HIP(hipGetLastError());
-  }
-  // ---- reconstruction: inter CUs, then intra / CIIP steps level by level (vvcr_intra.h)
-  if (mask & VVCR_STAGE_INTRA) {
-    StageTimer t(ctx, ST_INTRA);
-    IntraPlan &ip = ctx->intra;
-    const size_t nu = ip.order[0].size();
-    std::vector<int32_t> ord(ip.order[0]);
-    ord.insert(ord.end(), ip.order[1].begin(), ip.order[1].end());
-    ctx->d_order.upload(ord, s);
-    ctx->d_tiles.upload(ip.inter_tiles, s);
-    ctx->d_ijobs.upload(ip.jobs, s);
-    IntraParams P{};
-    for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[ctx->pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
-    P.order[0] = ctx->d_order.p;
-    P.order[1] = ctx->d_order.p + nu;
-    P.W4 = ctx->sp.width / 4;
-    P.bd = ctx->sp.bit_depth;
-    P.ctu = 1 << ctx->sp.ctu_log2;
-    launch_recon_inter(P, ctx->d_tiles.p, (int)ip.inter_tiles.size(), s);
-    VVCR_CHECK_HIP(hipGetLastError());
-    for (size_t L = 1; L + 1 < ip.level_start.size(); L++) {
-      const int a = ip.level_start[L], b = ip.level_start[L + 1];
-      launch_intra_level(P, ctx->d_ijobs.p + a, b - a, s);
-    }
-    VVCR_CHECK_HIP(hipGetLastError());
-  }
-  // ---- deblocking, in place on the picture slot: all vertical edges, then all horizontal edges
-  if ((mask & VVCR_STAGE_DBK) && ctx->dbk.total()) {
-    StageTimer t(ctx, ST_DBK);
-    auto &all = ctx->dbk_all;
-    all.clear();
-    int counts[4];
-    const std::vector<DbkSeg> *parts[4] = {&ctx->dbk.luma[0], &ctx->dbk.chroma[0], &ctx->dbk.luma[1], &ctx->dbk.chroma[1]};
-    for (int k = 0; k < 4; k++) {
-      counts[k] = (int)parts[k]->size();
-      all.insert(all.end(), parts[k]->begin(), parts[k]->end());
-    }
-    ctx->d_dbk.upload(all, s);
-    DbkParams dp{};
-    for (int c = 0; c < 3; c++) dp.pl[c] = ctx->dpb[ctx->pp.slot][c];
-    dp.bd = ctx->sp.bit_depth;
-    dp.beta_offset_div2 = ctx->pp.dbk_beta_offset_div2;
-    dp.tc_offset_div2 = ctx->pp.dbk_tc_offset_div2;
-    launch_dbk(dp, ctx->d_dbk.p, counts, s);
-  }
-  // ---- SAO (DBK picture in the slot -> tmp) and ALF (-> slot)
-  {
-    const vvcr_pic_params &pp = ctx->pp;
-    auto &A = ctx->dpb[pp.slot];
-    const int ctu = 1 << ctx->sp.ctu_log2;
-    const int wc = (ctx->sp.width + ctu - 1) / ctu, n = n_ctb(ctx->sp);
-    bool inTmp = false;
-    const bool alfOn = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
-    if ((mask & VVCR_STAGE_SAO) && (pp.sao_luma || pp.sao_chroma) && !ctx->have_sao)
-      throw VvcrError(VVCR_E_STATE, "SAO is enabled for the picture but no SAO parameters were set");
-    if ((mask & VVCR_STAGE_ALF) && alfOn && !ctx->have_alf)
-      throw VvcrError(VVCR_E_STATE, "ALF is enabled for the picture but no ALF parameters were set");
-    if ((mask & VVCR_STAGE_SAO) && ctx->have_sao && (pp.sao_luma || pp.sao_chroma)) {
-      StageTimer t(ctx, ST_SAO);
-      SaoParams sp{};
-      for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ctx->tmp[c]; }
-      sp.sao = ctx->d_sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
-      launch_sao(sp, s);
-      VVCR_CHECK_HIP(hipGetLastError());
-      inTmp = true;
-    }
-    if ((mask & VVCR_STAGE_ALF) && ctx->have_alf && alfOn) {
-      StageTimer t(ctx, ST_ALF);
-      AlfParams ap{};
-      for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ctx->tmp[c] : A[c]; ap.dst[c] = inTmp ? A[c] : ctx->tmp[c]; }
-      ap.bd = ctx->sp.bit_depth; ap.ctu_log2 = ctx->sp.ctu_log2; ap.wc = wc; ap.nctb = n;
-      ap.vb_luma = pp.alf_vb_luma; ap.vb_chroma = pp.alf_vb_chroma;
-      for (int c = 0; c < 3; c++) ap.en[c] = pp.alf_en[c];
-      ap.en[3] = pp.ccalf_en[0]; ap.en[4] = pp.ccalf_en[1];
-      ap.luma_coef = ctx->d_alf_luma_coef.p; ap.luma_clip = ctx->d_alf_luma_clip.p;
-      ap.chroma_coef = ctx->d_alf_chroma.p; ap.chroma_clip = ctx->d_alf_chroma.p + 56; ap.cc_coef = ctx->d_alf_cc.p;
-      ap.ctb_en = ctx->d_alf_ctb.p; ap.ctb_alt = ctx->d_alf_ctb.p + 3 * n; ap.cc_ctl = ctx->d_alf_ctb.p + 6 * n;
-      ap.ctb_set = ctx->d_alf_set.p;
-      launch_alf(ap, s);
-      VVCR_CHECK_HIP(hipGetLastError());
-      inTmp = !inTmp;
-    }
-    if (inTmp)
-      for (int c = 0; c < 3; c++)
-        VVCR_CHECK_HIP(hipMemcpy2DAsync(A[c].p, A[c].stride * 2, ctx->tmp[c].p, ctx->tmp[c].stride * 2, A[c].w * 2, A[c].h,
-                                        hipMemcpyDeviceToDevice, s));
-  }
-  VVCR_CHECK_HIP(hipEventRecord(ctx->ev[1], s));
+  Prepared &r = *ctx->prepared[0];
+  prepare(ctx, r, mask);
+  launch(ctx, r);
   ctx->in_picture = false;
   return VVCR_OK;
   API_END
 }
 
 int vvcr_end_picture(vvcr_ctx *ctx) { return vvcr_end_picture_stages(ctx, VVCR_STAGE_ALL); }
+
+int vvcr_prepare_picture(vvcr_ctx *ctx, uint32_t mask, int32_t *handle) {
+  if (!ctx || !handle) return VVCR_E_ARG;
+  API_BEGIN
+  if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_prepare_picture without begin");
+  int h = -1;
+  for (size_t i = 1; i < ctx->prepared.size(); i++)
+    if (!ctx->prepared[i]) { h = (int)i; break; }
+  if (h < 0) { h = (int)ctx->prepared.size(); ctx->prepared.emplace_back(); }
+  ctx->prepared[h].reset(new Prepared());
+  prepare(ctx, *ctx->prepared[h], mask);
+  ctx->in_picture = false;
+  *handle = h;
+  return VVCR_OK;
+  API_END
+}
+
+static Prepared &get_prepared(vvcr_ctx *ctx, int32_t h) {
+  if (h <= 0 || h >= (int)ctx->prepared.size() || !ctx->prepared[h]) throw VvcrError(VVCR_E_ARG, "bad prepared-picture handle");
+  return *ctx->prepared[h];
+}
+
+int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle) {
+  if (!ctx) return VVCR_E_ARG;
+  API_BEGIN
+  launch(ctx, get_prepared(ctx, handle));
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle) {
+  if (!ctx) return VVCR_E_ARG;
+  API_BEGIN
+  Prepared &r = get_prepared(ctx, handle);
+  r.wait();
+  if (ctx->last == &r) ctx->last = nullptr;
+  ctx->prepared[handle].reset();
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int32_t n) {
+  if (!ctx || (!out && n)) return VVCR_E_ARG;
+  API_BEGIN
+  Prepared *r = handle == 0 ? ctx->last : &get_prepared(ctx, handle);
+  if (!r) throw VvcrError(VVCR_E_STATE, "no launched picture");
+  r->wait();
+  for (int k = 0; k < NK && k < n; k++) {
+    vvcr_kernel_stat &s = out[k];
+    memset(&s, 0, sizeof s);
+    strncpy(s.name, kKernelNames[k], sizeof(s.name) - 1);
+    s.launches = r->ran[k] ? r->launches[k] : 0;
+    s.alg_bytes = r->ran[k] ? r->alg_bytes[k] : 0.0;
+    float ms = 0;
+    if (r->ran[k]) VVCR_CHECK_HIP(hipEventElapsedTime(&ms, r->ev[k][0], r->ev[k][1]));
+    s.ms = ms;
+  }
+  return NK;
+  API_END
+}
 
 int vvcr_sync(vvcr_ctx *ctx) {
   if (!ctx) return VVCR_E_ARG;
@@ -400,10 +597,16 @@ int vvcr_last_stage_times(vvcr_ctx *ctx, float *ms, int32_t n) {
   float t = 0;
   VVCR_CHECK_HIP(hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]));
   if (n > 0) ms[0] = t;
-  for (int k = 0; k < 7 && k + 1 < n; k++) {
-    float v = 0;
-    if (ctx->stage_ran[k]) VVCR_CHECK_HIP(hipEventElapsedTime(&v, ctx->sev[k][0], ctx->sev[k][1]));
-    ms[k + 1] = v;
+  for (int k = 1; k < n && k < 8; k++) ms[k] = 0;
+  if (ctx->last) {
+    Prepared &r = *ctx->last;
+    for (int k = 0; k < NK; k++) {
+      if (!r.ran[k]) continue;
+      float v = 0;
+      VVCR_CHECK_HIP(hipEventElapsedTime(&v, r.ev[k][0], r.ev[k][1]));
+      const int st = kKernelStage[k] + 1;
+      if (st < n) ms[st] += v;
+    }
   }
   return VVCR_OK;
   API_END
@@ -454,12 +657,14 @@ int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n) {
   if (!ctx || (!out && n)) return VVCR_E_ARG;
   API_BEGIN
   if (n < 0) throw VvcrError(VVCR_E_ARG, "negative count");
-  const int64_t m = std::min<int64_t>(n, ctx->n_dmvr);
+  Prepared *r = ctx->last;
+  const int cnt = r ? r->n_dmvr : 0;
+  const int64_t m = std::min<int64_t>(n, cnt);
   if (m > 0) {
-    VVCR_CHECK_HIP(hipMemcpyAsync(out, ctx->d_dmvr.p, (size_t)m * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    VVCR_CHECK_HIP(hipMemcpyAsync(out, r->dmvr.p, (size_t)m * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   }
-  return (int)ctx->n_dmvr;
+  return cnt;
   API_END
 }
 

@@ -79,13 +79,21 @@ def lib():
         L.vvcr_write_plane.argtypes = [P, I32, I32, I32, P, I32]
         L.vvcr_last_stage_times.argtypes = [P, C.POINTER(C.c_float), I32]
         L.vvcr_get_dmvr_deltas.argtypes = [P, P, C.c_int64]
+        L.vvcr_prepare_picture.argtypes = [P, C.c_uint32, C.POINTER(I32)]
+        L.vvcr_launch_picture.argtypes = [P, I32]
+        L.vvcr_release_picture.argtypes = [P, I32]
+        L.vvcr_kernel_stats.argtypes = [P, I32, C.POINTER(KernelStat), I32]
         L.vvcr_stream.argtypes = [P]
         L.vvcr_stream.restype = P
         _lib = L
     return _lib
 
 
-EXPORTS = ["vvcr_create", "vvcr_destroy", "vvcr_last_error", "vvcr_begin_picture", "vvcr_submit",
+class KernelStat(C.Structure):
+    _fields_ = [("name", C.c_char * 16), ("launches", C.c_int32), ("ms", C.c_float), ("alg_bytes", C.c_double)]
+
+
+EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_release_picture", "vvcr_kernel_stats", "vvcr_create", "vvcr_destroy", "vvcr_last_error", "vvcr_begin_picture", "vvcr_submit",
            "vvcr_set_loop_filter_params", "vvcr_end_picture", "vvcr_end_picture_stages", "vvcr_sync",
            "vvcr_read_plane", "vvcr_write_plane", "vvcr_read_picture", "vvcr_get_dmvr_deltas",
            "vvcr_last_stage_times", "vvcr_stream"]
@@ -154,6 +162,26 @@ class Context:
     def write_plane(self, buf, slot, comp, data):
         data = np.ascontiguousarray(data, np.int16)
         self._chk(self.L.vvcr_write_plane(self.h, buf, slot, comp, _ptr(data), data.shape[1]), "vvcr_write_plane")
+
+    def prepare(self, stages=STAGE_ALL):
+        """vvcr_prepare_picture: plan + upload the current picture; returns a handle."""
+        h = C.c_int32(0)
+        self._chk(self.L.vvcr_prepare_picture(self.h, stages, C.byref(h)), "vvcr_prepare_picture")
+        return h.value
+
+    def launch(self, handle):
+        self._chk(self.L.vvcr_launch_picture(self.h, handle), "vvcr_launch_picture")
+
+    def release(self, handle):
+        self._chk(self.L.vvcr_release_picture(self.h, handle), "vvcr_release_picture")
+
+    def kernel_stats(self, handle=0):
+        """[(name, launches, ms, alg_bytes)] of the last launch of a prepared picture (0 = last launched)."""
+        arr = (KernelStat * 16)()
+        n = self.L.vvcr_kernel_stats(self.h, handle, arr, 16)
+        if n < 0:
+            self._chk(n, "vvcr_kernel_stats")
+        return [(arr[i].name.decode(), arr[i].launches, arr[i].ms, arr[i].alg_bytes) for i in range(n)]
 
     def dmvr_deltas(self):
         """DMVR refinement deltas of the last picture, [n][2] (vvcr_get_dmvr_deltas)."""
