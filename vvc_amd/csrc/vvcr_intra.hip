@@ -43,102 +43,99 @@ __device__ __forceinline__ bool avail(const IntraParams &P, int ch, int x, int y
 
 __device__ __forceinline__ int pel(const DPlane &D, int x, int y) { return D.p[(size_t)y * D.stride + x]; }
 
+// Leading run of "already decompressed" units along a line of `count` (<= 64) units starting at (x, y),
+// step (dx, dy): the availability scans of the reference stop at the first unit not yet decoded
+// (isAboveAvailable / isLeftAvailable / ... IntraPrediction.cpp:1208-1310). One wave ballot.
+__device__ __forceinline__ int avail_run(const IntraParams &P, int ch, int seq, int x, int y, int dx, int dy, int count, int lane) {
+  const bool ok = lane < count && avail(P, ch, x + lane * dx, y + lane * dy, seq);
+  const uint64_t m = __ballot(ok);
+  const int lead = __builtin_ctzll(~m);   // m has at most 64 set bits; ~m == 0 only when all 64 lanes are in and available
+  return min(lead, count);
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
 // xFillReferenceSamples for area (fx, fy, fw, fh) of component plane D; top[0..predSize+mrl],
-// left[0..predHSize+mrl]; index 0 = corner line. Run by one lane.
+// left[0..predHSize+mrl]; index 0 = corner line.
+//
+// The reference walks the reference units sequentially (IntraPrediction.cpp:913-1149): units are
+// numbered in scan order 0 = bottom-most below-left ... totalLeft = corner ... top-right; missing units
+// get the last sample (in scan order) of the nearest earlier available unit, and the units before the
+// first available one get its first sample. That result depends only on the availability mask, so here
+// every lane derives its own unit's samples from two ballots and the raw reference line in LDS.
 __device__ void fill_refs(const IntraParams &P, const DPlane &D, int ch, int seq, int fx, int fy, int fw, int fh, int predSize,
-                          int predHSize, int mrl, int bd, int16_t *top, int16_t *left) {
+                          int predHSize, int mrl, int bd, int16_t *top, int16_t *left, int16_t *rawT, int16_t *rawL, int lane) {
   const int uw = ch ? 2 : 4, uh = uw;
   const int totalAbove = (predSize + uw - 1) / uw, totalLeft = (predHSize + uh - 1) / uh;
   const int totalUnits = totalAbove + totalLeft + 1;
   const int numAbove = max(fw / uw, 1), numLeft = max(fh / uh, 1);
   const int numAR = totalAbove - numAbove, numBL = totalLeft - numLeft;
-  bool F[2 * 64 + 1];
-  for (int i = 0; i < totalUnits; i++) F[i] = false;
-  int cnt = 0;
-  F[totalLeft] = avail(P, ch, fx - 1, fy - 1, seq);
-  cnt += F[totalLeft];
-  for (int i = 0; i < numAbove; i++) {
-    if (!avail(P, ch, fx + i * uw, fy - 1, seq)) break;
-    F[totalLeft + 1 + i] = true; cnt++;
-  }
-  for (int i = 0; i < numAR; i++) {
-    if (!avail(P, ch, fx + fw - 1 + uw + i * uw, fy - 1, seq)) break;
-    F[totalLeft + 1 + numAbove + i] = true; cnt++;
-  }
-  for (int i = 0; i < numLeft; i++) {
-    if (!avail(P, ch, fx - 1, fy + i * uh, seq)) break;
-    F[totalLeft - 1 - i] = true; cnt++;
-  }
-  for (int i = 0; i < numBL; i++) {
-    if (!avail(P, ch, fx - 1, fy + fh - 1 + uh + i * uh, seq)) break;
-    F[totalLeft - 1 - numLeft - i] = true; cnt++;
-  }
   const int ox = fx - 1 - mrl, oy = fy - 1 - mrl;   // corner sample of the reference line
+  const int pw = D.w, ph = D.h;
+  // raw reference line (clamped coordinates; samples of missing units are never used)
+  for (int j = lane; j <= predSize + mrl; j += 64) rawT[j] = (int16_t)pel(D, clampi(ox + j, 0, pw - 1), clampi(oy, 0, ph - 1));
+  for (int i = lane; i <= predHSize + mrl; i += 64) rawL[i] = (int16_t)pel(D, clampi(ox, 0, pw - 1), clampi(oy + i, 0, ph - 1));
+  // availability runs of the four segments and the corner
+  // (the above-right / below-left scans do not depend on the above / left ones)
+  const int nA = avail_run(P, ch, seq, fx, fy - 1, uw, 0, numAbove, lane);
+  const int nAR2 = avail_run(P, ch, seq, fx + fw - 1 + uw, fy - 1, uw, 0, numAR, lane);
+  const int nL = avail_run(P, ch, seq, fx - 1, fy, 0, uh, numLeft, lane);
+  const int nBL2 = avail_run(P, ch, seq, fx - 1, fy + fh - 1 + uh, 0, uh, numBL, lane);
+  const bool cAv = avail(P, ch, fx - 1, fy - 1, seq);
+  auto unitAv = [&](int u) -> bool {
+    if (u == totalLeft) return cAv;
+    if (u > totalLeft) {
+      const int i = u - totalLeft - 1;
+      return i < numAbove ? i < nA : (i - numAbove) < nAR2;
+    }
+    const int i = totalLeft - 1 - u;   // distance below the top of the left column, in units
+    return i < numLeft ? i < nL : (i - numLeft) < nBL2;
+  };
+  const uint64_t m0 = __ballot(lane < totalUnits && unitAv(lane));
+  const bool av64 = totalUnits > 64 && unitAv(64);
+  const int cnt = __popcll(m0) + (av64 ? 1 : 0);
+  __syncthreads();   // raw line in LDS
   if (cnt == 0) {
-    const int dc = 1 << (bd - 1);
-    for (int j = 0; j <= predSize + mrl; j++) top[j] = (int16_t)dc;
-    for (int i = 0; i <= predHSize + mrl; i++) left[i] = (int16_t)dc;
+    const int16_t dc = (int16_t)(1 << (bd - 1));
+    for (int j = lane; j <= predSize + mrl; j += 64) top[j] = dc;
+    for (int i = lane; i <= predHSize + mrl; i += 64) left[i] = dc;
+    __syncthreads();
     return;
   }
-  if (cnt == totalUnits) {
-    for (int j = 0; j <= predSize + mrl; j++) top[j] = (int16_t)pel(D, ox + j, oy);
-    for (int i = 0; i <= predHSize + mrl; i++) left[i] = (int16_t)pel(D, ox, oy + i);
-    return;
-  }
-  // partially available: copy available units, then substitute (IntraPrediction.cpp:987-1148)
-  if (F[totalLeft]) {
-    top[0] = left[0] = (int16_t)pel(D, ox, oy);
-    for (int i = 1; i <= mrl; i++) { top[i] = (int16_t)pel(D, ox + i, oy); left[i] = (int16_t)pel(D, ox, oy + i); }
-  }
-  {
-    int di = 1 + mrl;
-    for (int u = totalLeft - 1; u > 0; u--, di += uh)
-      if (F[u]) for (int i = 0; i < uh; i++) left[di + i] = (int16_t)pel(D, ox, oy + di + i);
-    if (F[0]) {
-      const int last = (predHSize % uh == 0) ? uh : predHSize % uh;
-      for (int i = 0; i < last; i++) left[di + i] = (int16_t)pel(D, ox, oy + di + i);
+  const int firstAv = m0 ? __builtin_ctzll(m0) : 64;
+  auto scanFirst = [&](int q) -> int16_t {
+    if (q < totalLeft) return rawL[(totalLeft - q) * uh + mrl];
+    if (q == totalLeft) return rawL[mrl];
+    return rawT[(q - totalLeft - 1) * uw + 1 + mrl];
+  };
+  auto scanLast = [&](int q) -> int16_t {
+    if (q < totalLeft) return rawL[(totalLeft - q - 1) * uh + mrl + 1];
+    if (q == totalLeft) return rawT[mrl];
+    return rawT[(q - totalLeft) * uw + mrl];
+  };
+  for (int u = lane; u < totalUnits; u += 64) {
+    const bool a = u < 64 ? ((m0 >> u) & 1) != 0 : av64;
+    int16_t v = 0;
+    if (!a) {
+      const uint64_t below = u < 64 ? (m0 & ((1ull << u) - 1)) : m0;
+      v = below ? scanLast(63 - __builtin_clzll(below)) : scanFirst(firstAv);
+    }
+    if (u == totalLeft) {
+      for (int i = 0; i <= mrl; i++) { top[i] = a ? rawT[i] : v; left[i] = a ? rawL[i] : v; }
+    } else if (u < totalLeft) {
+      const int i0 = (totalLeft - 1 - u) * uh + 1 + mrl;
+      const int n = u == 0 ? ((predHSize % uh == 0) ? uh : predHSize % uh) : uh;
+      for (int i = i0; i < i0 + n; i++) left[i] = a ? rawL[i] : v;
+    } else {
+      const int j0 = (u - totalLeft - 1) * uw + 1 + mrl;
+      const int n = u == totalUnits - 1 ? ((predSize % uw == 0) ? uw : predSize % uw) : uw;
+      for (int j = j0; j < j0 + n; j++) top[j] = a ? rawT[j] : v;
     }
   }
-  {
-    int dj = 1 + mrl;
-    for (int u = totalLeft + 1; u < totalUnits - 1; u++, dj += uw)
-      if (F[u]) for (int j = 0; j < uw; j++) top[dj + j] = (int16_t)pel(D, ox + dj + j, fy - 1 - mrl);
-    if (F[totalUnits - 1]) {
-      const int last = (predSize % uw == 0) ? uw : predSize % uw;
-      for (int j = 0; j < last; j++) top[dj + j] = (int16_t)pel(D, ox + dj + j, fy - 1 - mrl);
-    }
-  }
-  int lastAvail = 0;
-  if (!F[0]) {
-    int first = 1;
-    while (first < totalUnits && !F[first]) first++;
-    int row = -1, col = 0;
-    if (first < totalLeft) row = (totalLeft - first) * uh + mrl;
-    else if (first == totalLeft) row = mrl;
-    else col = (first - totalLeft - 1) * uw + 1 + mrl;
-    const int16_t v = row < 0 ? top[col] : left[row];
-    for (int i = predHSize + mrl; i > row; i--) left[i] = v;
-    for (int j = 0; j < col; j++) top[j] = v;
-    lastAvail = first;
-  }
-  for (int u = lastAvail + 1; u < totalUnits; u++) {
-    if (!F[u]) {
-      int row = -1, col = 0;
-      if (lastAvail < totalLeft) row = (totalLeft - lastAvail - 1) * uh + mrl + 1;
-      else if (lastAvail == totalLeft) col = mrl;
-      else col = (lastAvail - totalLeft) * uw + mrl;
-      const int16_t v = row < 0 ? top[col] : left[row];
-      if (u < totalLeft) {
-        for (int i = row - 1; i >= row - uh; i--) left[i] = v;
-      } else if (u == totalLeft) {
-        for (int i = 0; i < mrl + 1; i++) { left[i] = v; top[i] = v; }
-      } else {
-        const int n = (u == totalUnits - 1) ? ((predSize % uw == 0) ? uw : predSize % uw) : uw;
-        for (int j = col + 1; j <= col + n; j++) top[j] = v;
-      }
-    }
-    lastAvail = u;
-  }
+  __syncthreads();
 }
 
 // IntraPrediction::getWideAngle (:184)
@@ -157,22 +154,13 @@ struct NbAvail {
   bool above, left;
   int ar, bl;          // available above-right / below-left units
 };
-__device__ NbAvail nb_avail(const IntraParams &P, int ch, int seq, int x, int y, int w, int h, int unit) {
+__device__ NbAvail nb_avail(const IntraParams &P, int ch, int seq, int x, int y, int w, int h, int unit, int lane) {
   NbAvail r{};
   const int na = w / unit, nl = h / unit;
-  int c = 0;
-  for (int i = 0; i < nl; i++) { if (!avail(P, ch, x - 1, y + i * unit, seq)) break; c++; }
-  r.left = c == nl;
-  c = 0;
-  for (int i = 0; i < na; i++) { if (!avail(P, ch, x + i * unit, y - 1, seq)) break; c++; }
-  r.above = c == na;
-  r.bl = r.ar = 0;
-  const int totalA = (2 * (ch ? w : w / 2) + 1) / 2;   // unused placeholder to keep symmetry
-  (void)totalA;
-  if (r.left)
-    for (int i = 0; i < nl; i++) { if (!avail(P, ch, x - 1, y + h - 1 + unit + i * unit, seq)) break; r.bl++; }
-  if (r.above)
-    for (int i = 0; i < na; i++) { if (!avail(P, ch, x + w - 1 + unit + i * unit, y - 1, seq)) break; r.ar++; }
+  r.left = avail_run(P, ch, seq, x - 1, y, 0, unit, nl, lane) == nl;
+  r.above = avail_run(P, ch, seq, x, y - 1, unit, 0, na, lane) == na;
+  r.bl = r.left ? avail_run(P, ch, seq, x - 1, y + h - 1 + unit, 0, unit, nl, lane) : 0;
+  r.ar = r.above ? avail_run(P, ch, seq, x + w - 1 + unit, y - 1, unit, 0, na, lane) : 0;
   return r;
 }
 
@@ -184,6 +172,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   __shared__ int32_t aux[64 * 64 / 4];     // MIP reduced pred / CCLM template scratch
   __shared__ int16_t tmpl[2][132];         // CCLM down-sampled luma: top row / left column
   __shared__ int32_t lmp[3];
+  __shared__ int16_t pred[64 * 64];
   const int j = blockIdx.x;
   if (j >= njobs) return;
   const IntraJob J = jobs[j];
@@ -205,34 +194,37 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   if (isp) { topLen = J.cw + w; leftLen = J.ch + h; }
 
   // ---- reference samples
-  if (lane == 0) {
+  {
     int16_t *top = refU[0], *left = refU[1];
     if (!isp) {
-      fill_refs(P, D, ch, J.seq, x0, y0, w, h, topLen, leftLen, mrl, bd, top, left);
+      fill_refs(P, D, ch, J.seq, x0, y0, w, h, topLen, leftLen, mrl, bd, top, left, mainA, sideA, lane);
     } else {
       // CU-level fill of the first sub-partition (predSize per split direction), then the shift of
-      // initIntraPatternChTypeISP for later sub-partitions
+      // initIntraPatternChTypeISP (:798-897) for later sub-partitions
       const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
-      fill_refs(P, D, 0, J.seq, J.cx, J.cy, J.cw, J.ch, fTop, fLeft, 0, bd, top, left);
+      fill_refs(P, D, 0, J.seq, J.cx, J.cy, J.cw, J.ch, fTop, fLeft, 0, bd, top, left, mainA, sideA, lane);
       if (J.isp_k > 0) {
+        // keep the CU-level lines, then rebuild from them and the reconstructed previous sub-partition
+        for (int i = lane; i < RB; i += 64) { refF[0][i] = top[i]; refF[1][i] = left[i]; }
+        __syncthreads();
         if (!ispVer) {   // horizontal split: left column shifted, top row from the sub-partition above
           const bool la = avail(P, 0, x0 - 1, y0, J.seq);
           const int sh = J.isp_k * h;
-          const int src0 = pel(D, x0, y0 - 1);
-          for (int i = 0; i <= leftLen; i++) left[i] = la ? left[i + sh] : (int16_t)src0;
-          top[0] = left[0];
-          for (int i = 0; i < w; i++) top[1 + i] = (int16_t)pel(D, x0 + i, y0 - 1);
+          const int16_t src0 = (int16_t)pel(D, x0, y0 - 1);
+          for (int i = lane; i <= leftLen; i += 64) left[i] = la ? refF[1][i + sh] : src0;
+          const int16_t corner = la ? refF[1][sh] : src0;
           const int16_t last = (int16_t)pel(D, x0 + w - 1, y0 - 1);
-          for (int i = w + 1; i <= topLen; i++) top[i] = last;
+          for (int i = lane; i <= topLen; i += 64)
+            top[i] = i == 0 ? corner : (i <= w ? (int16_t)pel(D, x0 + i - 1, y0 - 1) : last);
         } else {         // vertical split: top row shifted, left column from the sub-partition to the left
           const bool aa = avail(P, 0, x0, y0 - 1, J.seq);
           const int sh = J.isp_k * w;
-          const int src0 = pel(D, x0 - 1, y0);
-          for (int i = 0; i <= topLen; i++) top[i] = aa ? top[i + sh] : (int16_t)src0;
-          left[0] = top[0];
-          for (int i = 0; i < h; i++) left[1 + i] = (int16_t)pel(D, x0 - 1, y0 + i);
+          const int16_t src0 = (int16_t)pel(D, x0 - 1, y0);
+          for (int i = lane; i <= topLen; i += 64) top[i] = aa ? refF[0][i + sh] : src0;
+          const int16_t corner = aa ? refF[0][sh] : src0;
           const int16_t last = (int16_t)pel(D, x0 - 1, y0 + h - 1);
-          for (int i = h + 1; i <= leftLen; i++) left[i] = last;
+          for (int i = lane; i <= leftLen; i += 64)
+            left[i] = i == 0 ? corner : (i <= h ? (int16_t)pel(D, x0 - 1, y0 + i - 1) : last);
         }
       }
     }
@@ -294,7 +286,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   const int16_t *top = refFilter ? refF[0] : refU[0];
   const int16_t *left = refFilter ? refF[1] : refU[1];
   const int n = w * h;
-  int predv[64];   // up to 64 samples per lane (64x64 block)
+#define predv(q) pred[lane + 64 * (q)]
 
   if (lmMode) {
     // ---------------- CCLM (xGetLumaRecPixels + xGetLMParameters)
@@ -302,8 +294,8 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
     const int lx = 2 * x0, ly = 2 * y0;
     const bool dual = (J.flags & IJ_DUAL) != 0;
     // luma-template availability: luma map in a single tree, chroma map in a separate chroma tree
-    const NbAvail lr = dual ? nb_avail(P, 1, J.seq, x0, y0, w, h, 2) : nb_avail(P, 0, J.seq, lx, ly, 2 * w, 2 * h, 4);
-    const NbAvail lm = nb_avail(P, 1, J.seq, x0, y0, w, h, 2);
+    const NbAvail lr = dual ? nb_avail(P, 1, J.seq, x0, y0, w, h, 2, lane) : nb_avail(P, 0, J.seq, lx, ly, 2 * w, 2 * h, 4, lane);
+    const NbAvail lm = nb_avail(P, 1, J.seq, x0, y0, w, h, 2, lane);
     const int mode = J.mode;
     const int addAR = (mode == MDLM_L || mode == MDLM_T) ? lr.ar * 2 : 0;
     const int addBL = (mode == MDLM_L || mode == MDLM_T) ? lr.bl * 2 : 0;
@@ -412,53 +404,47 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
       lmp[0] = a; lmp[1] = b; lmp[2] = shift;
     }
     __syncthreads();
-    for (int k = lane, q = 0; k < n; k += 64, q++) predv[q] = clampi(((lmp[0] * aux[k]) >> lmp[2]) + lmp[1], 0, maxv);
+    for (int k = lane, q = 0; k < n; k += 64, q++) predv(q) = clampi(((lmp[0] * aux[k]) >> lmp[2]) + lmp[1], 0, maxv);
   } else if (mip) {
     // ---------------- MIP
     const int sizeId = (w == 4 && h == 4) ? 0 : ((w == 4 || h == 4 || (w == 8 && h == 8)) ? 1 : 2);
     const int bdry = sizeId == 0 ? 2 : 4, rp = sizeId < 2 ? 4 : 8;
     const bool tr = (J.flags & IJ_MIP_T) != 0;
-    __shared__ int inb[8];
-    __shared__ int inOff;
-    if (lane == 0) {
-      int red[8];
-      // boundaryDownsampling1D of top (w) and left (h)
-      for (int side = 0; side < 2; side++) {
-        const int len = side ? h : w;
-        const int16_t *src = side ? refU[1] : refU[0];
-        int *dst = red + side * bdry;
-        if (bdry < len) {
-          const int f = len / bdry, lf = ilog2(f);
-          for (int d = 0, s = 0; d < bdry; d++) {
-            int sum = 0;
-            for (int k = 0; k < f; k++) sum += src[1 + s++];
-            dst[d] = (sum + (1 << (lf - 1))) >> lf;
-          }
-        } else {
-          for (int d = 0; d < bdry; d++) dst[d] = src[1 + d];
-        }
+    __shared__ int red[8];
+    // boundaryDownsampling1D of top (w) and left (h): one lane per reduced sample
+    if (lane < 2 * bdry) {
+      const int side = lane >= bdry, d = lane - side * bdry;
+      const int len = side ? h : w;
+      const int16_t *src = side ? refU[1] : refU[0];
+      if (bdry < len) {
+        const int f = len / bdry, lf = ilog2(f);
+        int sum = 0;
+        for (int k = 0; k < f; k++) sum += src[1 + d * f + k];
+        red[lane] = (sum + (1 << (lf - 1))) >> lf;
+      } else {
+        red[lane] = src[1 + d];
       }
-      int in[8];
-      const int inputSize = 2 * bdry;
-      if (!tr) for (int i = 0; i < inputSize; i++) in[i] = red[i];
-      else {
-        for (int i = 0; i < bdry; i++) { in[i] = red[bdry + i]; in[bdry + i] = red[i]; }
-      }
-      const int off = in[0];
-      in[0] = sizeId < 2 ? ((1 << (bd - 1)) - off) : 0;
-      for (int i = 1; i < inputSize; i++) in[i] -= off;
-      for (int i = 0; i < inputSize; i++) inb[i] = in[i];
-      inOff = off;
     }
     __syncthreads();
     const int inputSize = 2 * bdry;
-    int sum = 0;
-    for (int i = 0; i < inputSize; i++) sum += inb[i];
+    int inb[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) inb[i] = i < inputSize ? (tr ? red[i < bdry ? bdry + i : i - bdry] : red[i]) : 0;
+    const int inOff = inb[0];
+    inb[0] = sizeId < 2 ? ((1 << (bd - 1)) - inOff) : 0;
+    int sum = inb[0];
+#pragma unroll
+    for (int i = 1; i < 8; i++) {
+      if (i < inputSize) inb[i] -= inOff;
+      sum += inb[i];
+    }
     const int offset = 32 - 32 * sum;   // (1 << (MIP_SHIFT_MATRIX - 1)) - MIP_OFFSET_MATRIX * sum
     const int mode = J.mode;
     for (int o = lane; o < rp * rp; o += 64) {
       int acc = 0;
-      for (int i = 0; i < inputSize; i++) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        if (i >= inputSize) break;
         int wgt;
         if (sizeId == 0) wgt = vvcr_tab::mip4x4[mode][o][i];
         else if (sizeId == 1) wgt = vvcr_tab::mip8x8[mode][o][i];
@@ -496,7 +482,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
         const int behind = hval(r, xx);
         v = (before * (upV - pos) + behind * pos + (1 << (lf - 1))) >> lf;
       }
-      predv[q] = v;
+      predv(q) = v;
     }
   } else {
     // ---------------- planar / DC / angular / BDPCM
@@ -504,7 +490,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
     if (bdpcm) {
       for (int k = lane, q = 0; k < n; k += 64, q++) {
         const int yy = k / w, xx = k - yy * w;
-        predv[q] = J.mode == 1 ? left[yy + 1] : top[xx + 1];
+        predv(q) = J.mode == 1 ? left[yy + 1] : top[xx + 1];
       }
     } else if (dirMode == PLANAR) {
       const int tr = top[w + 1], bl = left[h + 1];
@@ -512,34 +498,34 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
         const int yy = k / w, xx = k - yy * w;
         const int hor = (left[yy + 1] << lw) + (xx + 1) * (tr - left[yy + 1]);
         const int ver = (top[xx + 1] << lh) + (yy + 1) * (bl - top[xx + 1]);
-        predv[q] = ((hor << lh) + (ver << lw) + (1 << (lw + lh))) >> (1 + lw + lh);
+        predv(q) = ((hor << lh) + (ver << lw) + (1 << (lw + lh))) >> (1 + lw + lh);
       }
     } else if (dirMode == DC) {
-      int sum = 0;
-      if (w >= h) for (int i = 0; i < w; i++) sum += top[mrl + 1 + i];
-      if (w <= h) for (int i = 0; i < h; i++) sum += left[mrl + 1 + i];
+      int part = 0;
+      if (w >= h) part += lane < w ? top[mrl + 1 + lane] : 0;
+      if (w <= h) part += lane < h ? left[mrl + 1 + lane] : 0;
+      const int sum = wave_sum(part);
       const int denom = (w == h) ? (w << 1) : max(w, h);
       const int dc = (sum + (denom >> 1)) >> ilog2(denom);
-      for (int k = lane, q = 0; k < n; k += 64, q++) predv[q] = dc;
+      for (int k = lane, q = 0; k < n; k += 64, q++) predv(q) = dc;
     } else {
       // angular: build main / side references exactly as xPredIntraAng does
       const int W = isModeVer ? w : h, H = isModeVer ? h : w;   // in the (possibly transposed) frame
       int16_t *refMain = mainA + EXT, *refSide = sideA + EXT;
-      if (lane == 0) {
+      {
         const int16_t *srcMain = isModeVer ? top : left, *srcSide = isModeVer ? left : top;
         if (angle < 0) {
-          for (int k = 0; k <= W + 1 + mrl; k++) refMain[k] = srcMain[k];
-          for (int k = 0; k <= H + 1 + mrl; k++) refSide[k] = srcSide[k];
-          for (int k = -H; k <= -1; k++) refMain[k] = refSide[min((-k * invAngle + 256) >> 9, H)];
+          for (int k = lane; k <= W + 1 + mrl; k += 64) refMain[k] = srcMain[k];
+          for (int k = lane; k <= H + 1 + mrl; k += 64) refSide[k] = srcSide[k];
+          for (int k = -H + lane; k <= -1; k += 64) refMain[k] = srcSide[min((-k * invAngle + 256) >> 9, H)];
         } else {
           const int mainLen = isModeVer ? topLen : leftLen, sideLen = isModeVer ? leftLen : topLen;
-          for (int k = 0; k <= mainLen + mrl; k++) refMain[k] = srcMain[k];
-          for (int k = 0; k <= sideLen + mrl; k++) refSide[k] = srcSide[k];
           const int log2Ratio = lw - lh;
           const int s = max(0, isModeVer ? log2Ratio : -log2Ratio);
           const int maxIndex = (mrl << s) + 2;
-          const int16_t v = refMain[mainLen + mrl];
-          for (int z = 1; z <= maxIndex; z++) refMain[mainLen + mrl + z] = v;
+          const int16_t v = srcMain[mainLen + mrl];
+          for (int k = lane; k <= mainLen + mrl + maxIndex; k += 64) refMain[k] = k <= mainLen + mrl ? srcMain[k] : v;
+          for (int k = lane; k <= sideLen + mrl; k += 64) refSide[k] = srcSide[k];
         }
       }
       __syncthreads();
@@ -585,7 +571,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
             v = (int16_t)(v + ((wL * (l - v) + 32) >> 6));
           }
         }
-        predv[q] = v;
+        predv(q) = v;
       }
     }
     if (applyPDPC && !bdpcm && (dirMode == PLANAR || dirMode == DC)) {
@@ -594,8 +580,8 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
         const int yy = k / w, xx = k - yy * w;
         const int wT = 32 >> min(31, (yy << 1) >> scale);
         const int wL = 32 >> min(31, (xx << 1) >> scale);
-        const int v = predv[q];
-        predv[q] = (int16_t)(v + ((wL * (left[yy + 1] - v) + wT * (top[xx + 1] - v) + 32) >> 6));
+        const int v = predv(q);
+        predv(q) = (int16_t)(v + ((wL * (left[yy + 1] - v) + wT * (top[xx + 1] - v) + 32) >> 6));
       }
     }
   }
@@ -605,7 +591,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   const DPlane &PP = P.pred[comp];
   for (int k = lane, q = 0; k < n; k += 64, q++) {
     const int yy = k / w, xx = k - yy * w;
-    int pv = predv[q];
+    int pv = predv(q);
     if (ciip) pv = ((4 - J.ciip_w) * pel(PP, x0 + xx, y0 + yy) + J.ciip_w * pv + 2) >> 2;
     const int v = clampi(pv + pel(R, x0 + xx, y0 + yy), 0, maxv);
     D.p[(size_t)(y0 + yy) * D.stride + x0 + xx] = (int16_t)v;
