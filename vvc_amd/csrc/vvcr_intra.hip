@@ -36,9 +36,11 @@ struct Ctx {
 // getCURestricted: same slice/tile, earlier in decoding order)
 __device__ __forceinline__ bool avail(const IntraParams &P, int ch, int x, int y, int seq) {
   const int pw = ch ? P.reco[1].w : P.reco[0].w, ph = ch ? P.reco[1].h : P.reco[0].h;
-  if (x < 0 || y < 0 || x >= pw || y >= ph) return false;
+  const bool in = x >= 0 && y >= 0 && x < pw && y < ph;
   const int s = ch ? 1 : 2;
-  return P.order[ch][(y >> s) * P.W4 + (x >> s)] < seq;
+  // the load is unconditional (clamped) so that the loads of several scans issue together
+  const int32_t o = P.order[ch][(clampi(y, 0, ph - 1) >> s) * P.W4 + (clampi(x, 0, pw - 1) >> s)];
+  return in & (o < seq);
 }
 
 __device__ __forceinline__ int pel(const DPlane &D, int x, int y) { return D.p[(size_t)y * D.stride + x]; }
@@ -47,10 +49,20 @@ __device__ __forceinline__ int pel(const DPlane &D, int x, int y) { return D.p[(
 // step (dx, dy): the availability scans of the reference stop at the first unit not yet decoded
 // (isAboveAvailable / isLeftAvailable / ... IntraPrediction.cpp:1208-1310). One wave ballot.
 __device__ __forceinline__ int avail_run(const IntraParams &P, int ch, int seq, int x, int y, int dx, int dy, int count, int lane) {
-  const bool ok = lane < count && avail(P, ch, x + lane * dx, y + lane * dy, seq);
+  const bool ok = (lane < count) & avail(P, ch, x + lane * dx, y + lane * dy, seq);
   const uint64_t m = __ballot(ok);
   const int lead = __builtin_ctzll(~m);   // m has at most 64 set bits; ~m == 0 only when all 64 lanes are in and available
   return min(lead, count);
+}
+
+// Run of consecutive set bits of m starting at bit p (0 <= p < 64), going up / going down.
+__device__ __forceinline__ int run_up(uint64_t m, int p) {
+  const uint64_t z = ~(m >> p);   // top p bits are ones, so z == 0 only when p == 0 and m is all ones
+  return z ? (int)__builtin_ctzll(z) : 64;
+}
+__device__ __forceinline__ int run_down(uint64_t m, int p) {
+  const uint64_t z = ~(m << (63 - p));
+  return z ? (int)__builtin_clzll(z) : 64;
 }
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -78,13 +90,34 @@ __device__ void fill_refs(const IntraParams &P, const DPlane &D, int ch, int seq
   // raw reference line (clamped coordinates; samples of missing units are never used)
   for (int j = lane; j <= predSize + mrl; j += 64) rawT[j] = (int16_t)pel(D, clampi(ox + j, 0, pw - 1), clampi(oy, 0, ph - 1));
   for (int i = lane; i <= predHSize + mrl; i += 64) rawL[i] = (int16_t)pel(D, clampi(ox, 0, pw - 1), clampi(oy + i, 0, ph - 1));
-  // availability runs of the four segments and the corner
-  // (the above-right / below-left scans do not depend on the above / left ones)
-  const int nA = avail_run(P, ch, seq, fx, fy - 1, uw, 0, numAbove, lane);
-  const int nAR2 = avail_run(P, ch, seq, fx + fw - 1 + uw, fy - 1, uw, 0, numAR, lane);
-  const int nL = avail_run(P, ch, seq, fx - 1, fy, 0, uh, numLeft, lane);
-  const int nBL2 = avail_run(P, ch, seq, fx - 1, fy + fh - 1 + uh, 0, uh, numBL, lane);
-  const bool cAv = avail(P, ch, fx - 1, fy - 1, seq);
+  // raw availability of every unit (unit u = lane, plus unit 64 on every lane), one load phase
+  auto unitPos = [&](int u, int &x, int &y) {
+    if (u == totalLeft) { x = fx - 1; y = fy - 1; }
+    else if (u > totalLeft && u <= totalLeft + numAbove) { x = fx + (u - totalLeft - 1) * uw; y = fy - 1; }
+    else if (u > totalLeft + numAbove) { x = fx + fw - 1 + uw + (u - totalLeft - 1 - numAbove) * uw; y = fy - 1; }
+    else if (u >= totalLeft - numLeft) { x = fx - 1; y = fy + (totalLeft - 1 - u) * uh; }
+    else { x = fx - 1; y = fy + fh - 1 + uh + (totalLeft - 1 - numLeft - u) * uh; }
+  };
+  int ux, uy, vx, vy;
+  unitPos(lane, ux, uy);
+  unitPos(64, vx, vy);
+  const uint64_t raw = __ballot((lane < totalUnits) & avail(P, ch, ux, uy, seq));
+  const bool raw64 = (totalUnits > 64) & avail(P, ch, vx, vy, seq);
+  // the scans stop at the first unit not yet decoded; the above-right / below-left scans do not
+  // depend on the above / left ones. Segments: below-left [0, tl-numLeft), left [tl-numLeft, tl),
+  // corner tl, above (tl, tl+numAbove], above-right (tl+numAbove, totalUnits).
+  const int tl = totalLeft;
+  const int nA = min(run_up(raw, tl + 1), numAbove);
+  const int pAR = tl + 1 + numAbove;
+  int nAR2 = 0;
+  if (numAR > 0) {
+    nAR2 = pAR < 64 ? run_up(raw, pAR) : 0;
+    if (pAR + nAR2 == 64 && raw64) nAR2++;
+    nAR2 = min(nAR2, numAR);
+  }
+  const int nL = min(run_down(raw, tl - 1), numLeft);
+  const int nBL2 = numBL == 0 ? 0 : min(run_down(raw, tl - 1 - numLeft), numBL);
+  const bool cAv = ((raw >> tl) & 1) != 0;
   auto unitAv = [&](int u) -> bool {
     if (u == totalLeft) return cAv;
     if (u > totalLeft) {
@@ -157,10 +190,14 @@ struct NbAvail {
 __device__ NbAvail nb_avail(const IntraParams &P, int ch, int seq, int x, int y, int w, int h, int unit, int lane) {
   NbAvail r{};
   const int na = w / unit, nl = h / unit;
-  r.left = avail_run(P, ch, seq, x - 1, y, 0, unit, nl, lane) == nl;
-  r.above = avail_run(P, ch, seq, x, y - 1, unit, 0, na, lane) == na;
-  r.bl = r.left ? avail_run(P, ch, seq, x - 1, y + h - 1 + unit, 0, unit, nl, lane) : 0;
-  r.ar = r.above ? avail_run(P, ch, seq, x + w - 1 + unit, y - 1, unit, 0, na, lane) : 0;
+  const int l = avail_run(P, ch, seq, x - 1, y, 0, unit, nl, lane);
+  const int a = avail_run(P, ch, seq, x, y - 1, unit, 0, na, lane);
+  const int bl = avail_run(P, ch, seq, x - 1, y + h - 1 + unit, 0, unit, nl, lane);
+  const int ar = avail_run(P, ch, seq, x + w - 1 + unit, y - 1, unit, 0, na, lane);
+  r.left = l == nl;
+  r.above = a == na;
+  r.bl = r.left ? bl : 0;
+  r.ar = r.above ? ar : 0;
   return r;
 }
 
@@ -173,6 +210,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   __shared__ int16_t tmpl[2][132];         // CCLM down-sampled luma: top row / left column
   __shared__ int32_t lmp[3];
   __shared__ int16_t pred[64 * 64];
+  __shared__ int16_t resL[64 * 64];        // residual of the step, prefetched at entry
   const int j = blockIdx.x;
   if (j >= njobs) return;
   const IntraJob J = jobs[j];
@@ -188,6 +226,22 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   const bool ciip = (J.flags & IJ_CIIP) != 0;
   const bool lmMode = comp > 0 && J.mode >= LM && !bdpcm;
   const int mrl = comp ? 0 : J.mrl;
+  const int n = w * h;
+  {
+    // the residual does not depend on earlier steps: its loads issue with the reference loads
+    const DPlane &R = P.resi[comp];
+    if (((w | x0) & 3) == 0) {   // plane strides are multiples of 64 samples
+      for (int k = lane * 4; k < n; k += 256) {
+        const int yy = k / w, xx = k - yy * w;
+        *(uint2 *)&resL[k] = *(const uint2 *)&R.p[(size_t)(y0 + yy) * R.stride + x0 + xx];
+      }
+    } else {
+      for (int k = lane; k < n; k += 64) {
+        const int yy = k / w, xx = k - yy * w;
+        resL[k] = R.p[(size_t)(y0 + yy) * R.stride + x0 + xx];
+      }
+    }
+  }
 
   // ---- reference lengths (setReferenceArrayLengths / ISP variants)
   int topLen = 2 * w, leftLen = 2 * h;
@@ -285,7 +339,6 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   }
   const int16_t *top = refFilter ? refF[0] : refU[0];
   const int16_t *left = refFilter ? refF[1] : refU[1];
-  const int n = w * h;
 #define predv(q) pred[lane + 64 * (q)]
 
   if (lmMode) {
@@ -587,13 +640,12 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   }
 
   // ---- CIIP blend (geneWeightedPred) and reconstruction
-  const DPlane &R = P.resi[comp];
   const DPlane &PP = P.pred[comp];
   for (int k = lane, q = 0; k < n; k += 64, q++) {
     const int yy = k / w, xx = k - yy * w;
     int pv = predv(q);
     if (ciip) pv = ((4 - J.ciip_w) * pel(PP, x0 + xx, y0 + yy) + J.ciip_w * pv + 2) >> 2;
-    const int v = clampi(pv + pel(R, x0 + xx, y0 + yy), 0, maxv);
+    const int v = clampi(pv + resL[k], 0, maxv);
     D.p[(size_t)(y0 + yy) * D.stride + x0 + xx] = (int16_t)v;
   }
 }
