@@ -15,32 +15,33 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + os.path.
          "-Wno-unused-result", "-munsafe-fp-atomics"]
 
 
-def _compile(src):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+def _compile(src, extra=(), obj_dir=OBJ):
+    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + \
         [os.path.join(ROOT, "include", "vvcr.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + list(extra) + ["-c", src, "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC] + FLAGS + ["-x", "hip", "-c", src, "-o", obj]
+        cmd = [HIPCC] + FLAGS + list(extra) + ["-x", "hip", "-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError("compile failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
     return obj
 
 
-def build_lib(jobs=8):
-    os.makedirs(OBJ, exist_ok=True)
+def build_lib(jobs=8, extra=(), obj_dir=OBJ, lib=LIB):
+    """extra/obj_dir/lib: diagnostics variants (e.g. tools/intra_prof.py's -DVVCR_INTRA_PROF build)."""
+    os.makedirs(obj_dir, exist_ok=True)
     srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(_compile, srcs))
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", LIB] + objs
+        objs = list(ex.map(lambda s: _compile(s, extra, obj_dir), srcs))
+    if not os.path.exists(lib) or os.path.getmtime(lib) < max(os.path.getmtime(o) for o in objs):
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", lib] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
-    return LIB
+    return lib
 
 
 def build_oracle():

@@ -231,7 +231,10 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     for (const ReconTile &t : ip.inter_tiles) b += (double)t.w * t.h * 1.5 * 2 * 3;   // pred + resi in, reco out
     r.alg_bytes[K_RECON] = b;
     b = 0;
-    for (const IntraJob &j : ip.jobs) b += (double)j.w * j.h * 2 * 2 + 2.0 * 2 * (2 * j.w + 2 * j.h);   // resi in, reco out, refs
+    for (const IntraJob &j : ip.jobs) {   // resi in, reco out, refs (an ISP job covers isp_k regions)
+      const int nreg = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) ? j.isp_k : 1;
+      b += nreg * ((double)j.w * j.h * 2 * 2 + 2.0 * 2 * (2 * j.w + 2 * j.h));
+    }
     r.alg_bytes[K_INTRA] = b;
   }
   if (mask & VVCR_STAGE_DBK) {

@@ -24,13 +24,13 @@ enum : uint8_t {
 
 // One reconstruction step: predict a region, add the residual plane, clip, store into the picture.
 struct IntraJob {
-  int16_t x, y;           // region position (component samples)
-  uint8_t w, h;           // region size (<= 64)
+  int16_t x, y;           // region position (component samples); ISP: the first region
+  uint8_t w, h;           // region size (<= 64); ISP: every region has this size
   uint8_t comp;           // 0 Y, 1 Cb, 2 Cr
   uint8_t mode;           // final intra mode 0..66, 67/68/69 = LM / MDLM_L / MDLM_T, MIP mode index
   uint8_t flags;          // IJ_*
   uint8_t mrl;            // multiRefIdx
-  uint8_t isp_k;          // ISP: index of the region along the split (0 = first)
+  uint8_t isp_k;          // ISP: number of prediction regions along the split (one step covers the CU)
   uint8_t ciip_w;         // CIIP intra weight (1..3)
   int16_t cx, cy;         // CU position (component samples)
   uint8_t cw, ch;         // CU size (component samples, 128 fits)

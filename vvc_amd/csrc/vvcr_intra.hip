@@ -11,6 +11,24 @@
 #include "vvcr_gen_tables.h"
 #include "vvcr_tables.h"
 
+#ifdef VVCR_INTRA_PROF
+// Diagnostics build only (tools/intra_prof.py): per-step phase timestamps (s_memtime) of k_intra.
+__device__ unsigned long long g_iprof[1 << 17][6];
+__device__ unsigned int g_iprof_n;
+extern "C" int vvcr_intra_prof_read(unsigned long long *dst, int max) {
+  unsigned int n = 0;
+  (void)hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_iprof_n), sizeof(n));
+  n = n < (unsigned)max ? n : (unsigned)max;
+  (void)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_iprof), (size_t)n * 6 * 8);
+  unsigned int z = 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_iprof_n), &z, sizeof(z));
+  return (int)n;
+}
+#define IPROF(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); tstamp[i] = __builtin_readcyclecounter(); } while (0)
+#else
+#define IPROF(i) do { } while (0)
+#endif
+
 namespace {
 
 __constant__ int8_t i_chroma[32][4] = VVCR_CHROMA_FILTER_TABLE;
@@ -87,9 +105,17 @@ __device__ void fill_refs(const IntraParams &P, const DPlane &D, int ch, int seq
   const int numAR = totalAbove - numAbove, numBL = totalLeft - numLeft;
   const int ox = fx - 1 - mrl, oy = fy - 1 - mrl;   // corner sample of the reference line
   const int pw = D.w, ph = D.h;
-  // raw reference line (clamped coordinates; samples of missing units are never used)
-  for (int j = lane; j <= predSize + mrl; j += 64) rawT[j] = (int16_t)pel(D, clampi(ox + j, 0, pw - 1), clampi(oy, 0, ph - 1));
-  for (int i = lane; i <= predHSize + mrl; i += 64) rawL[i] = (int16_t)pel(D, clampi(ox, 0, pw - 1), clampi(oy + i, 0, ph - 1));
+  // raw reference line (clamped coordinates; samples of missing units are never used). All loads of
+  // the fill (3 + 3 samples and 2 order-map entries per lane) are issued before the first wait.
+  int16_t tv[3], lv[3];
+  {
+    const int cy = clampi(oy, 0, ph - 1), cx = clampi(ox, 0, pw - 1);
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      tv[r] = (int16_t)pel(D, clampi(ox + lane + 64 * r, 0, pw - 1), cy);
+      lv[r] = (int16_t)pel(D, cx, clampi(oy + lane + 64 * r, 0, ph - 1));
+    }
+  }
   // raw availability of every unit (unit u = lane, plus unit 64 on every lane), one load phase
   auto unitPos = [&](int u, int &x, int &y) {
     if (u == totalLeft) { x = fx - 1; y = fy - 1; }
@@ -98,11 +124,15 @@ __device__ void fill_refs(const IntraParams &P, const DPlane &D, int ch, int seq
     else if (u >= totalLeft - numLeft) { x = fx - 1; y = fy + (totalLeft - 1 - u) * uh; }
     else { x = fx - 1; y = fy + fh - 1 + uh + (totalLeft - 1 - numLeft - u) * uh; }
   };
-  int ux, uy, vx, vy;
+  int ux, uy;
   unitPos(lane, ux, uy);
-  unitPos(64, vx, vy);
   const uint64_t raw = __ballot((lane < totalUnits) & avail(P, ch, ux, uy, seq));
-  const bool raw64 = (totalUnits > 64) & avail(P, ch, vx, vy, seq);
+  bool raw64 = false;
+  if (totalUnits > 64) {   // only a 64-wide luma block with its 64 above-right samples
+    int vx, vy;
+    unitPos(64, vx, vy);
+    raw64 = avail(P, ch, vx, vy, seq);
+  }
   // the scans stop at the first unit not yet decoded; the above-right / below-left scans do not
   // depend on the above / left ones. Segments: below-left [0, tl-numLeft), left [tl-numLeft, tl),
   // corner tl, above (tl, tl+numAbove], above-right (tl+numAbove, totalUnits).
@@ -130,6 +160,11 @@ __device__ void fill_refs(const IntraParams &P, const DPlane &D, int ch, int seq
   const uint64_t m0 = __ballot(lane < totalUnits && unitAv(lane));
   const bool av64 = totalUnits > 64 && unitAv(64);
   const int cnt = __popcll(m0) + (av64 ? 1 : 0);
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    if (lane + 64 * r <= predSize + mrl) rawT[lane + 64 * r] = tv[r];
+    if (lane + 64 * r <= predHSize + mrl) rawL[lane + 64 * r] = lv[r];
+  }
   __syncthreads();   // raw line in LDS
   if (cnt == 0) {
     const int16_t dc = (int16_t)(1 << (bd - 1));
@@ -211,14 +246,19 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   __shared__ int32_t lmp[3];
   __shared__ int16_t pred[64 * 64];
   __shared__ int16_t resL[64 * 64];        // residual of the step, prefetched at entry
+  __shared__ int16_t ispPrev[64];          // ISP: last row / column of the previous region
   const int j = blockIdx.x;
   if (j >= njobs) return;
+#ifdef VVCR_INTRA_PROF
+  unsigned long long tstamp[5];
+#endif
+  IPROF(0);
   const IntraJob J = jobs[j];
   const int lane = threadIdx.x;
   const int comp = J.comp, ch = comp ? 1 : 0;
   const int bd = P.bd, maxv = (1 << bd) - 1;
   const DPlane &D = P.reco[comp];
-  const int w = J.w, h = J.h, x0 = J.x, y0 = J.y;
+  const int w = J.w, h = J.h;
   const bool isp = (J.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0;
   const bool ispVer = (J.flags & IJ_ISP_VER) != 0;
   const bool mip = (J.flags & IJ_MIP) != 0;
@@ -227,63 +267,94 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   const bool lmMode = comp > 0 && J.mode >= LM && !bdpcm;
   const int mrl = comp ? 0 : J.mrl;
   const int n = w * h;
-  {
-    // the residual does not depend on earlier steps: its loads issue with the reference loads
-    const DPlane &R = P.resi[comp];
-    if (((w | x0) & 3) == 0) {   // plane strides are multiples of 64 samples
-      for (int k = lane * 4; k < n; k += 256) {
-        const int yy = k / w, xx = k - yy * w;
-        *(uint2 *)&resL[k] = *(const uint2 *)&R.p[(size_t)(y0 + yy) * R.stride + x0 + xx];
-      }
-    } else {
-      for (int k = lane; k < n; k += 64) {
-        const int yy = k / w, xx = k - yy * w;
-        resL[k] = R.p[(size_t)(y0 + yy) * R.stride + x0 + xx];
-      }
+  const int nreg = isp ? J.isp_k : 1;
+  // residual rectangle: the block, or the whole CU for ISP
+  const int rx = isp ? J.cx : J.x, ry = isp ? J.cy : J.y, rw = isp ? J.cw : w, rh = isp ? J.ch : h;
+  // The residual does not depend on earlier steps: the first 2048 samples are loaded into registers
+  // here, so that their loads are in flight together with the reference-fill loads, and stored to LDS
+  // after the fill; larger blocks load the rest afterwards.
+  const DPlane &R = P.resi[comp];
+  const int rn = rw * rh;
+  const bool rvec = ((rw | rx) & 3) == 0;   // plane strides are multiples of 64 samples
+  uint2 rv[8];
+  int16_t rs[8];
+  if (rvec) {
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const int k = min((lane + 64 * b) * 4, rn - 4);
+      const int yy = k / rw, xx = k - yy * rw;
+      rv[b] = *(const uint2 *)&R.p[(size_t)(ry + yy) * R.stride + rx + xx];
+    }
+  } else {
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const int k = min(lane + 64 * b, rn - 1);
+      const int yy = k / rw, xx = k - yy * rw;
+      rs[b] = R.p[(size_t)(ry + yy) * R.stride + rx + xx];
     }
   }
+  auto store_resid = [&]() {
+    if (rvec) {
+#pragma unroll
+      for (int b = 0; b < 8; b++)
+        if ((lane + 64 * b) * 4 < rn) *(uint2 *)&resL[(lane + 64 * b) * 4] = rv[b];
+    } else {
+#pragma unroll
+      for (int b = 0; b < 8; b++)
+        if (lane + 64 * b < rn) resL[lane + 64 * b] = rs[b];
+    }
+    for (int k = (lane + 512) * (rvec ? 4 : 1); k < rn; k += 64 * (rvec ? 4 : 1)) {
+      const int yy = k / rw, xx = k - yy * rw;
+      const int16_t *src = &R.p[(size_t)(ry + yy) * R.stride + rx + xx];
+      if (rvec) *(uint2 *)&resL[k] = *(const uint2 *)src;
+      else resL[k] = *src;
+    }
+  };
 
   // ---- reference lengths (setReferenceArrayLengths / ISP variants)
   int topLen = 2 * w, leftLen = 2 * h;
   if (isp) { topLen = J.cw + w; leftLen = J.ch + h; }
+
+  // ISP: the regions of the CU in order; region k reads the CU-level lines and region k-1
+#pragma nounroll
+  for (int kreg = 0; kreg < nreg; kreg++) {
+  const int x0 = J.x + (ispVer ? kreg * w : 0), y0 = J.y + (isp && !ispVer ? kreg * h : 0);
 
   // ---- reference samples
   {
     int16_t *top = refU[0], *left = refU[1];
     if (!isp) {
       fill_refs(P, D, ch, J.seq, x0, y0, w, h, topLen, leftLen, mrl, bd, top, left, mainA, sideA, lane);
-    } else {
-      // CU-level fill of the first sub-partition (predSize per split direction), then the shift of
-      // initIntraPatternChTypeISP (:798-897) for later sub-partitions
+    } else if (kreg == 0) {
+      // CU-level fill of the first region (predSize per split direction), kept in refF for the others
       const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
       fill_refs(P, D, 0, J.seq, J.cx, J.cy, J.cw, J.ch, fTop, fLeft, 0, bd, top, left, mainA, sideA, lane);
-      if (J.isp_k > 0) {
-        // keep the CU-level lines, then rebuild from them and the reconstructed previous sub-partition
+      if (nreg > 1)
         for (int i = lane; i < RB; i += 64) { refF[0][i] = top[i]; refF[1][i] = left[i]; }
-        __syncthreads();
-        if (!ispVer) {   // horizontal split: left column shifted, top row from the sub-partition above
-          const bool la = avail(P, 0, x0 - 1, y0, J.seq);
-          const int sh = J.isp_k * h;
-          const int16_t src0 = (int16_t)pel(D, x0, y0 - 1);
-          for (int i = lane; i <= leftLen; i += 64) left[i] = la ? refF[1][i + sh] : src0;
-          const int16_t corner = la ? refF[1][sh] : src0;
-          const int16_t last = (int16_t)pel(D, x0 + w - 1, y0 - 1);
-          for (int i = lane; i <= topLen; i += 64)
-            top[i] = i == 0 ? corner : (i <= w ? (int16_t)pel(D, x0 + i - 1, y0 - 1) : last);
-        } else {         // vertical split: top row shifted, left column from the sub-partition to the left
-          const bool aa = avail(P, 0, x0, y0 - 1, J.seq);
-          const int sh = J.isp_k * w;
-          const int16_t src0 = (int16_t)pel(D, x0 - 1, y0);
-          for (int i = lane; i <= topLen; i += 64) top[i] = aa ? refF[0][i + sh] : src0;
-          const int16_t corner = aa ? refF[0][sh] : src0;
-          const int16_t last = (int16_t)pel(D, x0 - 1, y0 + h - 1);
-          for (int i = lane; i <= leftLen; i += 64)
-            left[i] = i == 0 ? corner : (i <= h ? (int16_t)pel(D, x0 - 1, y0 + i - 1) : last);
-        }
+    } else {
+      // the shift of initIntraPatternChTypeISP (:798-897); ispPrev = last row / column of region k-1
+      if (!ispVer) {   // horizontal split: left column shifted, top row from the region above
+        const bool la = avail(P, 0, x0 - 1, y0, J.seq);
+        const int sh = kreg * h;
+        const int16_t src0 = ispPrev[0];
+        for (int i = lane; i <= leftLen; i += 64) left[i] = la ? refF[1][i + sh] : src0;
+        const int16_t corner = la ? refF[1][sh] : src0;
+        const int16_t last = ispPrev[w - 1];
+        for (int i = lane; i <= topLen; i += 64) top[i] = i == 0 ? corner : (i <= w ? ispPrev[i - 1] : last);
+      } else {         // vertical split: top row shifted, left column from the region to the left
+        const bool aa = avail(P, 0, x0, y0 - 1, J.seq);
+        const int sh = kreg * w;
+        const int16_t src0 = ispPrev[0];
+        for (int i = lane; i <= topLen; i += 64) top[i] = aa ? refF[0][i + sh] : src0;
+        const int16_t corner = aa ? refF[0][sh] : src0;
+        const int16_t last = ispPrev[h - 1];
+        for (int i = lane; i <= leftLen; i += 64) left[i] = i == 0 ? corner : (i <= h ? ispPrev[i - 1] : last);
       }
     }
   }
+  if (kreg == 0) store_resid();   // read after the barriers that follow
   __syncthreads();
+  IPROF(1);
 
   // ---- prediction parameters (initPredIntraParams)
   const int dirMode = ciip ? PLANAR : (int)J.mode;
@@ -337,6 +408,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
     }
     __syncthreads();
   }
+  IPROF(2);
   const int16_t *top = refFilter ? refF[0] : refU[0];
   const int16_t *left = refFilter ? refF[1] : refU[1];
 #define predv(q) pred[lane + 64 * (q)]
@@ -353,39 +425,45 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
     const int addAR = (mode == MDLM_L || mode == MDLM_T) ? lr.ar * 2 : 0;
     const int addBL = (mode == MDLM_L || mode == MDLM_T) ? lr.bl * 2 : 0;
     const bool firstRowCtu = (ly & (P.ctu - 1)) == 0;
-    if (lr.above) {
-      for (int i = lane; i < w + addAR; i += 64) {
-        const bool pad = i == 0 && !lr.left;
-        int v;
-        if (firstRowCtu) {
-          const int c = lx + 2 * i;
-          const int l = pad ? pel(Y, c, ly - 1) : pel(Y, c - 1, ly - 1);
-          v = (pel(Y, c, ly - 1) * 2 + l + pel(Y, c + 1, ly - 1) + 2) >> 2;
-        } else {
-          const int c = lx + 2 * i;
-          const int l0 = pad ? pel(Y, c, ly - 2) : pel(Y, c - 1, ly - 2);
-          const int l1 = pad ? pel(Y, c, ly - 1) : pel(Y, c - 1, ly - 1);
-          v = ((pel(Y, c, ly - 2) * 2 + l0 + pel(Y, c + 1, ly - 2)) + (pel(Y, c, ly - 1) * 2 + l1 + pel(Y, c + 1, ly - 1)) + 4) >> 3;
-        }
-        tmpl[0][i] = (int16_t)v;
+    // luma loads in batches (templates + 256 down-sampled samples first): every load of a batch is
+    // issued before the first wait
+    auto Yc = [&](int x, int y) { return pel(Y, clampi(x, 0, Y.w - 1), clampi(y, 0, Y.h - 1)); };
+    const int nT = lr.above ? w + addAR : 0, nLt = lr.left ? h + addBL : 0;
+    int ta[6], tl[6];
+    {
+      const int i = min(lane, max(nT - 1, 0));
+      const int c = lx + 2 * i;
+      const int cl = (i == 0 && !lr.left) ? c : c - 1;
+      ta[0] = Yc(cl, ly - 2); ta[1] = Yc(c, ly - 2); ta[2] = Yc(c + 1, ly - 2);
+      ta[3] = Yc(cl, ly - 1); ta[4] = Yc(c, ly - 1); ta[5] = Yc(c + 1, ly - 1);
+      const int r = ly + 2 * min(lane, max(nLt - 1, 0));
+      tl[0] = Yc(lx - 3, r); tl[1] = Yc(lx - 2, r); tl[2] = Yc(lx - 1, r);
+      tl[3] = Yc(lx - 3, r + 1); tl[4] = Yc(lx - 2, r + 1); tl[5] = Yc(lx - 1, r + 1);
+    }
+    auto aux_batch = [&](int k0, bool stores_tmpl) {
+      int v[4][6];
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int k = min(k0 + 64 * b, n - 1);
+        const int yy = k / w, xx = k - yy * w;
+        const int c = lx + 2 * xx, r = ly + 2 * yy;
+        const int cl = (xx == 0 && !lr.left) ? c : c - 1;
+        v[b][0] = pel(Y, cl, r); v[b][1] = pel(Y, c, r); v[b][2] = pel(Y, c + 1, r);
+        v[b][3] = pel(Y, cl, r + 1); v[b][4] = pel(Y, c, r + 1); v[b][5] = pel(Y, c + 1, r + 1);
       }
-    }
-    if (lr.left) {
-      for (int jj = lane; jj < h + addBL; jj += 64) {
-        const int r = ly + 2 * jj;
-        const int v = ((pel(Y, lx - 2, r) * 2 + pel(Y, lx - 3, r) + pel(Y, lx - 1, r)) +
-                       (pel(Y, lx - 2, r + 1) * 2 + pel(Y, lx - 3, r + 1) + pel(Y, lx - 1, r + 1)) + 4) >> 3;
-        tmpl[1][jj] = (int16_t)v;
+      if (stores_tmpl) {
+        if (lane < nT)
+          tmpl[0][lane] = (int16_t)(firstRowCtu ? (ta[4] * 2 + ta[3] + ta[5] + 2) >> 2
+                                                : ((ta[1] * 2 + ta[0] + ta[2]) + (ta[4] * 2 + ta[3] + ta[5]) + 4) >> 3);
+        if (lane < nLt) tmpl[1][lane] = (int16_t)(((tl[1] * 2 + tl[0] + tl[2]) + (tl[4] * 2 + tl[3] + tl[5]) + 4) >> 3);
       }
-    }
-    for (int k = lane; k < n; k += 64) {
-      const int yy = k / w, xx = k - yy * w;
-      const int c = lx + 2 * xx, r = ly + 2 * yy;
-      const bool pad = xx == 0 && !lr.left;
-      const int l0 = pad ? pel(Y, c, r) : pel(Y, c - 1, r);
-      const int l1 = pad ? pel(Y, c, r + 1) : pel(Y, c - 1, r + 1);
-      aux[k] = ((pel(Y, c, r) * 2 + pel(Y, c + 1, r) + l0) + (pel(Y, c, r + 1) * 2 + pel(Y, c + 1, r + 1) + l1) + 4) >> 3;
-    }
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if (k0 + 64 * b < n)
+          aux[k0 + 64 * b] = ((v[b][1] * 2 + v[b][2] + v[b][0]) + (v[b][4] * 2 + v[b][5] + v[b][3]) + 4) >> 3;
+    };
+    aux_batch(lane, true);
+    for (int k0 = lane + 256; k0 < n; k0 += 256) aux_batch(k0, false);
     __syncthreads();
     if (lane == 0) {
       bool aboveAv = lm.above, leftAv = lm.left;
@@ -639,15 +717,34 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
     }
   }
 
+  IPROF(3);
   // ---- CIIP blend (geneWeightedPred) and reconstruction
   const DPlane &PP = P.pred[comp];
   for (int k = lane, q = 0; k < n; k += 64, q++) {
     const int yy = k / w, xx = k - yy * w;
     int pv = predv(q);
     if (ciip) pv = ((4 - J.ciip_w) * pel(PP, x0 + xx, y0 + yy) + J.ciip_w * pv + 2) >> 2;
-    const int v = clampi(pv + resL[k], 0, maxv);
+    const int v = clampi(pv + resL[(y0 - ry + yy) * rw + x0 - rx + xx], 0, maxv);
     D.p[(size_t)(y0 + yy) * D.stride + x0 + xx] = (int16_t)v;
+    if (isp && (ispVer ? xx == w - 1 : yy == h - 1)) ispPrev[ispVer ? yy : xx] = (int16_t)v;
   }
+  __syncthreads();
+  }   // regions
+#ifdef VVCR_INTRA_PROF
+  IPROF(4);
+  if (lane == 0) {
+    const unsigned int slot = atomicAdd(&g_iprof_n, 1u);
+    if (slot < (1u << 17)) {
+      unsigned int xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      g_iprof[slot][0] = tstamp[0];
+      for (int i = 1; i < 5; i++) g_iprof[slot][i] = tstamp[i] - tstamp[0];
+      g_iprof[slot][5] = (unsigned long long)J.comp | (unsigned long long)J.w << 8 | (unsigned long long)J.h << 16 |
+                         (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40 |
+                         (unsigned long long)(njobs & 0xffff) << 44;
+    }
+  }
+#endif
 }
 
 __global__ void k_recon_inter(IntraParams P, const ReconTile *__restrict__ tiles, int n) {

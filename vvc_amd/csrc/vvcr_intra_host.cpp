@@ -137,24 +137,20 @@ struct Planner {
           regs.push_back({b[0], b[1], b[2], b[3]});
         }
       }
-      int prevLev = 0;
-      for (size_t k = 0; k < regs.size(); k++) {
-        seq++;
-        IntraJob j = base(c, 0);
-        j.x = (int16_t)regs[k][0]; j.y = (int16_t)regs[k][1]; j.w = (uint8_t)regs[k][2]; j.h = (uint8_t)regs[k][3];
-        j.flags = ver ? IJ_ISP_VER : IJ_ISP_HOR;
-        j.mode = (uint8_t)p.fidir_l;
-        j.isp_k = (uint8_t)k;
-        // CU-level reference lines (first sub-partition fill) + the previous sub-partition
-        const int fTop = ver ? 2 * c.w : c.w + j.w, fLeft = ver ? c.h + j.h : 2 * c.h;
-        int lev = ref_level(0, c.x, c.y, fTop, fLeft, 0);
-        lev = std::max(lev, prevLev);
-        lev += 1;
-        if (k == 0) mark(0, c.x, c.y, c.w, c.h, lev, true);   // setDecomp of the whole CU (DecCu.cpp:288-291)
-        else mark(0, j.x, j.y, j.w, j.h, lev, false);
-        prevLev = lev;
-        push(lev, j);
-      }
+      // one step runs all regions in order: region k > 0 reads only the CU-level reference lines
+      // and region k-1 (initIntraPatternChTypeISP), both available to the step itself
+      if (regs.empty()) return;
+      seq++;
+      IntraJob j = base(c, 0);
+      j.x = (int16_t)regs[0][0]; j.y = (int16_t)regs[0][1]; j.w = (uint8_t)regs[0][2]; j.h = (uint8_t)regs[0][3];
+      j.flags = ver ? IJ_ISP_VER : IJ_ISP_HOR;
+      j.mode = (uint8_t)p.fidir_l;
+      j.isp_k = (uint8_t)regs.size();
+      const int fTop = ver ? 2 * c.w : c.w + j.w, fLeft = ver ? c.h + j.h : 2 * c.h;
+      const int lev = 1 + ref_level(0, c.x, c.y, fTop, fLeft, 0);
+      mark(0, c.x, c.y, c.w, c.h, lev, true);   // setDecomp of the whole CU (DecCu.cpp:288-291)
+      push(lev, j);
+      seq += (int)regs.size() - 1;
       return;
     }
     for (int t = c.firsttu; t < c.firsttu + c.ntu; t++) {

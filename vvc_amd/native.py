@@ -6,7 +6,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvvcr.so")
+LIB_PATH = os.environ.get("VVCR_LIB") or os.path.join(_HERE, "libvvcr.so")   # VVCR_LIB: diagnostics builds
 
 MAX_REF = 16
 STAGE_RESID, STAGE_INTER, STAGE_INTRA, STAGE_LMCS_INV = 0x01, 0x02, 0x04, 0x08
