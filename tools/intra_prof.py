@@ -35,7 +35,7 @@ def run(stream):
         S.submit(ctx, p)
         S.set_loop_filter_params(ctx, p)
         hs.append(ctx.prepare(N.STAGE_ALL))
-    buf = np.zeros((1 << 17, 6), np.uint64)
+    buf = np.zeros((1 << 17, 8), np.uint64)
     out = []
     for rep in range(3):
         for i, h in enumerate(hs):

@@ -1,13 +1,24 @@
-"""Summarise gpurun_out/iprof_<stream>.npz (tools/intra_prof.py): phase cycles per step type."""
+"""Summarise gpurun_out/iprof_<stream>.npz (tools/intra_prof.py).
+
+Record per step: [0..2] s_memrealtime (100 MHz) at take / dependencies met / done, [3],[4] phase
+cycles (refs | params << 32, predict | total << 32), [5] comp,w,h,flags,mode,xcc, [6] step | block << 32,
+[7] number of dependencies, [8] picture, [9] repetition."""
 import sys
 import numpy as np
 a = np.load(sys.argv[1])['prof']
-a = a[a[:, 7] == a[:, 7].max()]
+a = a[a[:, 9] == a[:, 9].max()]
 info = a[:, 5]
 comp = info & 0xff; w = (info >> 8) & 0xff; h = (info >> 16) & 0xff; flags = (info >> 24) & 0xff; mode = (info >> 32) & 0xff
-ph = a[:, 1:5].astype(np.int64)
+m32 = np.uint64(0xffffffff)
+ph = np.stack([a[:, 3] & m32, a[:, 3] >> np.uint64(32), a[:, 4] & m32, a[:, 4] >> np.uint64(32)], 1).astype(np.int64)
 d = np.diff(np.concatenate([np.zeros((len(a), 1), np.int64), ph], 1), axis=1)
+t0, t1, t2 = (a[:, k].astype(np.int64) for k in range(3))
 print("steps", len(a), "phase cycles [refs, params, predict, recon]", d.mean(0).round(0), "total", ph[:, 3].mean().round(0))
+print("wait (us) mean %.2f  run (us) mean %.2f  median run %.2f" % (((t1 - t0) * 0.01).mean(), ((t2 - t1) * 0.01).mean(), np.median((t2 - t1) * 0.01)))
+for pic in np.unique(a[:, 8]):
+    m = a[:, 8] == pic
+    span = (t2[m].max() - t0[m].min()) * 0.01
+    print("picture %d: %d steps, span %.1f us, mean run %.2f us" % (pic, m.sum(), span, ((t2[m] - t1[m]) * 0.01).mean()))
 for c in range(3):
     m = comp == c
     print("comp", c, m.sum(), d[m].mean(0).round(0), ph[m, 3].mean().round(0))

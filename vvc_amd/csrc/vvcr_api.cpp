@@ -73,6 +73,8 @@ struct Prepared {
   DevVec<int32_t> order;
   DevVec<ReconTile> tiles;
   DevVec<IntraJob> ijobs;
+  DevVec<int32_t> idep_start, ideps, istate;
+  int n_ijobs = 0;
   std::vector<int32_t> level_start;
   DevVec<DbkSeg> dbk;
   int dbk_counts[4] = {0, 0, 0, 0};
@@ -137,6 +139,8 @@ struct vvcr_ctx {
   // prepared pictures: index 0 is the scratch record of vvcr_end_picture
   std::vector<std::unique_ptr<Prepared>> prepared;
   Prepared *last = nullptr;          // last launched (stage times, DMVR deltas)
+  int n_cu = 256;                    // compute units (persistent intra launch width)
+  int32_t *d_err = nullptr;          // device error flag of the persistent intra kernel (checked by vvcr_sync)
   hipEvent_t ev[2] = {};             // whole last launch
 };
 
@@ -225,6 +229,10 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     r.order.upload(ord);
     r.tiles.upload(ip.inter_tiles);
     r.ijobs.upload(ip.jobs);
+    r.idep_start.upload(ip.dep_start);
+    r.ideps.upload(ip.deps);
+    r.istate.ensure(16 + ip.jobs.size());
+    r.n_ijobs = (int)ip.jobs.size();
     r.level_start = ip.level_start;
     r.n_tiles = (int)ip.inter_tiles.size();
     double b = 0;
@@ -327,13 +335,9 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     }
     {
       KernelTimer t(r, K_INTRA, s);
-      int n = 0;
-      for (size_t L = 1; L + 1 < r.level_start.size(); L++) {
-        const int a = r.level_start[L], b = r.level_start[L + 1];
-        if (b > a) { launch_intra_level(P, r.ijobs.p + a, b - a, s); n++; }
-      }
+      launch_intra(P, r.ijobs.p, r.n_ijobs, r.idep_start.p, r.ideps.p, r.istate.p, ctx->d_err, ctx->n_cu, s);
       VVCR_CHECK_HIP(hipGetLastError());
-      r.launches[K_INTRA] = n;
+      r.launches[K_INTRA] = r.n_ijobs ? 1 : 0;
     }
   }
   auto &A = ctx->dpb[pp.slot];
@@ -417,6 +421,9 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       ctx->tmp[c] = alloc_plane(w, h);
     }
     for (auto &e : ctx->ev) VVCR_CHECK_HIP(hipEventCreate(&e));
+    VVCR_CHECK_HIP(hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, sp->device));
+    VVCR_CHECK_HIP(hipMalloc(&ctx->d_err, sizeof(int32_t)));
+    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof(int32_t)));
     build_scan_tables(ctx->scans);
     ctx->d_scans.upload(ctx->scans.data);
     ctx->prepared.emplace_back(new Prepared());   // scratch record of vvcr_end_picture
@@ -436,6 +443,7 @@ int vvcr_destroy(vvcr_ctx *ctx) {
     for (auto &p : s) (void)hipFree(p.p);
   for (int c = 0; c < 3; c++) { (void)hipFree(ctx->pred[c].p); (void)hipFree(ctx->resi[c].p); (void)hipFree(ctx->tmp[c].p); }
   for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
+  if (ctx->d_err) (void)hipFree(ctx->d_err);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return VVCR_OK;
@@ -589,6 +597,12 @@ int vvcr_sync(vvcr_ctx *ctx) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
   VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  int32_t e = 0;
+  VVCR_CHECK_HIP(hipMemcpy(&e, ctx->d_err, sizeof e, hipMemcpyDeviceToHost));
+  if (e) {
+    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof e));
+    throw VvcrError(VVCR_E_STATE, "intra reconstruction: a step's dependency wait timed out (output invalid)");
+  }
   return VVCR_OK;
   API_END
 }
@@ -633,6 +647,12 @@ int vvcr_read_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, int1
   DPlane *p = select_plane(ctx, buf, slot, comp);
   VVCR_CHECK_HIP(hipMemcpy2DAsync(dst, dst_stride * 2, p->p, p->stride * 2, p->w * 2, p->h, hipMemcpyDeviceToHost, ctx->stream));
   VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  int32_t e = 0;
+  VVCR_CHECK_HIP(hipMemcpy(&e, ctx->d_err, sizeof e, hipMemcpyDeviceToHost));
+  if (e) {
+    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof e));
+    throw VvcrError(VVCR_E_STATE, "intra reconstruction: a step's dependency wait timed out (output invalid)");
+  }
   return VVCR_OK;
   API_END
 }
@@ -643,6 +663,12 @@ int vvcr_write_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, con
   DPlane *p = select_plane(ctx, buf, slot, comp);
   VVCR_CHECK_HIP(hipMemcpy2DAsync(p->p, p->stride * 2, src, src_stride * 2, p->w * 2, p->h, hipMemcpyHostToDevice, ctx->stream));
   VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  int32_t e = 0;
+  VVCR_CHECK_HIP(hipMemcpy(&e, ctx->d_err, sizeof e, hipMemcpyDeviceToHost));
+  if (e) {
+    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof e));
+    throw VvcrError(VVCR_E_STATE, "intra reconstruction: a step's dependency wait timed out (output invalid)");
+  }
   return VVCR_OK;
   API_END
 }

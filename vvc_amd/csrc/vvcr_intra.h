@@ -50,9 +50,11 @@ struct IntraPlan {
   std::vector<ReconTile> inter_tiles;
   std::vector<IntraJob> jobs;        // sorted by level
   std::vector<int32_t> level_start;  // jobs of level L: [level_start[L], level_start[L+1])
+  std::vector<int32_t> dep_start;    // step i waits for steps deps[dep_start[i] .. dep_start[i+1]) (all < i)
+  std::vector<int32_t> deps;
   std::vector<int32_t> order[2];     // per 4x4 luma unit / 2x2 chroma unit: seq of the step that decodes it
   void clear() {
-    inter_tiles.clear(); jobs.clear(); level_start.clear(); order[0].clear(); order[1].clear();
+    inter_tiles.clear(); jobs.clear(); level_start.clear(); dep_start.clear(); deps.clear(); order[0].clear(); order[1].clear();
   }
 };
 
@@ -67,4 +69,6 @@ struct IntraParams {
 
 void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out);
 void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s);
-void launch_intra_level(const IntraParams &p, const IntraJob *jobs, int n, hipStream_t s);
+// all steps of a picture in one persistent launch; state: 16 + n int32 (reset here); *err set on a wait timeout
+void launch_intra(const IntraParams &p, const IntraJob *jobs, int n, const int32_t *dep_start, const int32_t *deps,
+                  int32_t *state, int32_t *err, int n_cu, hipStream_t s);

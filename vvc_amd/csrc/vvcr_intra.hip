@@ -13,20 +13,22 @@
 
 #ifdef VVCR_INTRA_PROF
 // Diagnostics build only (tools/intra_prof.py): per-step phase timestamps (s_memtime) of k_intra.
-__device__ unsigned long long g_iprof[1 << 17][6];
+__device__ unsigned long long g_iprof[1 << 17][8];
 __device__ unsigned int g_iprof_n;
 extern "C" int vvcr_intra_prof_read(unsigned long long *dst, int max) {
   unsigned int n = 0;
   (void)hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_iprof_n), sizeof(n));
   n = n < (unsigned)max ? n : (unsigned)max;
-  (void)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_iprof), (size_t)n * 6 * 8);
+  (void)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_iprof), (size_t)n * 8 * 8);
   unsigned int z = 0;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_iprof_n), &z, sizeof(z));
   return (int)n;
 }
 #define IPROF(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); tstamp[i] = __builtin_readcyclecounter(); } while (0)
+#define IPROF_RT(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); rstamp[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define IPROF(i) do { } while (0)
+#define IPROF_RT(i) do { } while (0)
 #endif
 
 namespace {
@@ -62,6 +64,25 @@ __device__ __forceinline__ bool avail(const IntraParams &P, int ch, int x, int y
 }
 
 __device__ __forceinline__ int pel(const DPlane &D, int x, int y) { return D.p[(size_t)y * D.stride + x]; }
+
+// Reconstructed samples are handed between steps of one launch (k_intra is persistent): every store of
+// them is a 4-byte sc1 store and every load of them a 4-byte sc1 load (bypasses the CU's L1), the
+// producing wave drains its stores (s_waitcnt vmcnt(0)) before its one-lane sc1 flag store, and the
+// consumer loads only after its sc1 polls of those flags matched (MI355X_MICROARCH.md, inter-workgroup
+// visibility, first row of the sc1 hand-off table; one workgroup per CU).
+typedef __attribute__((address_space(1))) uint32_t gu32;
+__device__ __forceinline__ uint32_t ld_sc1(const int16_t *p) {   // p 4-byte aligned
+  return __hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(int16_t *p, uint32_t v) {   // p 4-byte aligned
+  __hip_atomic_store((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one reconstructed sample (x any) / the sample pair (x even, x + 1)
+__device__ __forceinline__ int pel_rc(const DPlane &D, int x, int y) {
+  const uint32_t v = ld_sc1(D.p + (size_t)y * D.stride + (x & ~1));
+  return (int)(int16_t)((x & 1) ? (v >> 16) : (v & 0xffff));
+}
+__device__ __forceinline__ uint32_t pair_rc(const DPlane &D, int x, int y) { return ld_sc1(D.p + (size_t)y * D.stride + x); }
 
 // Leading run of "already decompressed" units along a line of `count` (<= 64) units starting at (x, y),
 // step (dx, dy): the availability scans of the reference stop at the first unit not yet decoded
@@ -112,8 +133,8 @@ __device__ void fill_refs(const IntraParams &P, const DPlane &D, int ch, int seq
     const int cy = clampi(oy, 0, ph - 1), cx = clampi(ox, 0, pw - 1);
 #pragma unroll
     for (int r = 0; r < 3; r++) {
-      tv[r] = (int16_t)pel(D, clampi(ox + lane + 64 * r, 0, pw - 1), cy);
-      lv[r] = (int16_t)pel(D, cx, clampi(oy + lane + 64 * r, 0, ph - 1));
+      tv[r] = (int16_t)pel_rc(D, clampi(ox + lane + 64 * r, 0, pw - 1), cy);
+      lv[r] = (int16_t)pel_rc(D, cx, clampi(oy + lane + 64 * r, 0, ph - 1));
     }
   }
   // raw availability of every unit (unit u = lane, plus unit 64 on every lane), one load phase
@@ -236,7 +257,12 @@ __device__ NbAvail nb_avail(const IntraParams &P, int ch, int seq, int x, int y,
   return r;
 }
 
-__global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__restrict__ jobs, int njobs) {
+// Persistent: one workgroup (one wave) per CU takes steps from an atomic counter in topological order
+// and waits, per step, for the steps it reads from (dependency lists built by plan_intra).
+// state[0] = step counter, state[16 + i] = step i done; *err set if a wait times out.
+__global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__restrict__ jobs, int njobs,
+                                              const int32_t *__restrict__ dep_start, const int32_t *__restrict__ deps,
+                                              int32_t *state, int32_t *err) {
   __shared__ int16_t refU[2][RB];          // unfiltered top / left (index 0 = corner)
   __shared__ int16_t refF[2][RB];          // filtered
   __shared__ int16_t mainA[EXT + RB + 64];  // angular main reference (with negative indices)
@@ -247,14 +273,34 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   __shared__ int16_t pred[64 * 64];
   __shared__ int16_t resL[64 * 64];        // residual of the step, prefetched at entry
   __shared__ int16_t ispPrev[64];          // ISP: last row / column of the previous region
-  const int j = blockIdx.x;
-  if (j >= njobs) return;
+  __shared__ int s_job;
+  const int lane = threadIdx.x;
+  int32_t *done = state + 16;
+  for (;;) {
+  // next step in topological order; it waits only for steps taken before it, so every wave makes
+  // progress and every wave leaves once the list is exhausted
+  if (lane == 0) s_job = atomicAdd(&state[0], 1);
+  __syncthreads();
+  const int j = s_job;
+  __syncthreads();
+  if (j >= njobs) break;
 #ifdef VVCR_INTRA_PROF
-  unsigned long long tstamp[5];
+  unsigned long long tstamp[5], rstamp[3];
 #endif
+  IPROF_RT(0);
+  for (int k = dep_start[j] + lane; k < dep_start[j + 1]; k += 64) {
+    const int32_t *f = done + deps[k];
+    for (int it = 1; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; it++) {
+      __builtin_amdgcn_s_sleep(1);
+      // never expected: report instead of hanging, and let every other wait end as well
+      if ((it & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+      if (it > (1 << 23)) { atomicOr(err, 1); break; }
+    }
+  }
+  __syncthreads();
+  IPROF_RT(1);
   IPROF(0);
   const IntraJob J = jobs[j];
-  const int lane = threadIdx.x;
   const int comp = J.comp, ch = comp ? 1 : 0;
   const int bd = P.bd, maxv = (1 << bd) - 1;
   const DPlane &D = P.reco[comp];
@@ -427,7 +473,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
     const bool firstRowCtu = (ly & (P.ctu - 1)) == 0;
     // luma loads in batches (templates + 256 down-sampled samples first): every load of a batch is
     // issued before the first wait
-    auto Yc = [&](int x, int y) { return pel(Y, clampi(x, 0, Y.w - 1), clampi(y, 0, Y.h - 1)); };
+    auto Yc = [&](int x, int y) { return pel_rc(Y, clampi(x, 0, Y.w - 1), clampi(y, 0, Y.h - 1)); };
     const int nT = lr.above ? w + addAR : 0, nLt = lr.left ? h + addBL : 0;
     int ta[6], tl[6];
     {
@@ -448,8 +494,9 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
         const int yy = k / w, xx = k - yy * w;
         const int c = lx + 2 * xx, r = ly + 2 * yy;
         const int cl = (xx == 0 && !lr.left) ? c : c - 1;
-        v[b][0] = pel(Y, cl, r); v[b][1] = pel(Y, c, r); v[b][2] = pel(Y, c + 1, r);
-        v[b][3] = pel(Y, cl, r + 1); v[b][4] = pel(Y, c, r + 1); v[b][5] = pel(Y, c + 1, r + 1);
+        const uint32_t p0 = pair_rc(Y, c, r), p1 = pair_rc(Y, c, r + 1);   // c even
+        v[b][0] = pel_rc(Y, cl, r); v[b][1] = (int16_t)(p0 & 0xffff); v[b][2] = (int16_t)(p0 >> 16);
+        v[b][3] = pel_rc(Y, cl, r + 1); v[b][4] = (int16_t)(p1 & 0xffff); v[b][5] = (int16_t)(p1 >> 16);
       }
       if (stores_tmpl) {
         if (lane < nT)
@@ -720,31 +767,46 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   IPROF(3);
   // ---- CIIP blend (geneWeightedPred) and reconstruction
   const DPlane &PP = P.pred[comp];
-  for (int k = lane, q = 0; k < n; k += 64, q++) {
+  __syncthreads();   // pred[] of other lanes
+  for (int k = 2 * lane; k < n; k += 128) {   // sample pairs (w and x0 are even)
     const int yy = k / w, xx = k - yy * w;
-    int pv = predv(q);
-    if (ciip) pv = ((4 - J.ciip_w) * pel(PP, x0 + xx, y0 + yy) + J.ciip_w * pv + 2) >> 2;
-    const int v = clampi(pv + resL[(y0 - ry + yy) * rw + x0 - rx + xx], 0, maxv);
-    D.p[(size_t)(y0 + yy) * D.stride + x0 + xx] = (int16_t)v;
-    if (isp && (ispVer ? xx == w - 1 : yy == h - 1)) ispPrev[ispVer ? yy : xx] = (int16_t)v;
+    int v2[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) {
+      int pv = pred[k + e];
+      if (ciip) pv = ((4 - J.ciip_w) * pel(PP, x0 + xx + e, y0 + yy) + J.ciip_w * pv + 2) >> 2;
+      v2[e] = clampi(pv + resL[(y0 - ry + yy) * rw + x0 - rx + xx + e], 0, maxv);
+      if (isp && (ispVer ? xx + e == w - 1 : yy == h - 1)) ispPrev[ispVer ? yy : xx + e] = (int16_t)v2[e];
+    }
+    st_sc1(D.p + (size_t)(y0 + yy) * D.stride + x0 + xx, (uint32_t)(uint16_t)v2[0] | ((uint32_t)v2[1] << 16));
   }
   __syncthreads();
   }   // regions
+  // publish: this wave's stores are complete before the flag (one wave per workgroup)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (lane == 0) __hip_atomic_store(&done[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef VVCR_INTRA_PROF
   IPROF(4);
+  IPROF_RT(2);
   if (lane == 0) {
     const unsigned int slot = atomicAdd(&g_iprof_n, 1u);
     if (slot < (1u << 17)) {
       unsigned int xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      g_iprof[slot][0] = tstamp[0];
-      for (int i = 1; i < 5; i++) g_iprof[slot][i] = tstamp[i] - tstamp[0];
+      g_iprof[slot][0] = rstamp[0];
+      g_iprof[slot][1] = rstamp[1];
+      g_iprof[slot][2] = rstamp[2];
+      g_iprof[slot][3] = (tstamp[1] - tstamp[0]) | (tstamp[2] - tstamp[0]) << 32;
+      g_iprof[slot][4] = (tstamp[3] - tstamp[0]) | (tstamp[4] - tstamp[0]) << 32;
       g_iprof[slot][5] = (unsigned long long)J.comp | (unsigned long long)J.w << 8 | (unsigned long long)J.h << 16 |
-                         (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40 |
-                         (unsigned long long)(njobs & 0xffff) << 44;
+                         (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40;
+      g_iprof[slot][6] = (unsigned long long)j | (unsigned long long)blockIdx.x << 32;
+      g_iprof[slot][7] = (unsigned long long)(dep_start[j + 1] - dep_start[j]);
     }
   }
 #endif
+  }   // steps
 }
 
 __global__ void k_recon_inter(IntraParams P, const ReconTile *__restrict__ tiles, int n) {
@@ -772,7 +834,10 @@ void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hip
   hipLaunchKernelGGL(k_recon_inter, dim3(n), dim3(64), 0, s, p, tiles, n);
 }
 
-void launch_intra_level(const IntraParams &p, const IntraJob *jobs, int n, hipStream_t s) {
+void launch_intra(const IntraParams &p, const IntraJob *jobs, int n, const int32_t *dep_start, const int32_t *deps,
+                  int32_t *state, int32_t *err, int n_cu, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_intra, dim3(n), dim3(64), 0, s, p, jobs, n);
+  VVCR_CHECK_HIP(hipMemsetAsync(state, 0, (16 + (size_t)n) * sizeof(int32_t), s));
+  // 64 KiB of dynamic LDS on top of the kernel's own keeps one workgroup per CU
+  hipLaunchKernelGGL(k_intra, dim3(std::min(n, n_cu)), dim3(64), 65536, s, p, jobs, n, dep_start, deps, state, err);
 }

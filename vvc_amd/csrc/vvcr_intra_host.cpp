@@ -25,8 +25,11 @@ struct Planner {
   IntraPlan &out;
   int W4, H4, ctu;
   std::vector<int32_t> level[2];
+  std::vector<int32_t> prod[3];     // per unit of each component: the step (index into jobs) that reconstructs it, -1 = inter
   std::vector<int32_t> cu_map;      // luma 4x4 unit -> CU index (for CIIP neighbour tests)
   std::vector<std::pair<int32_t, IntraJob>> jobs;   // (level, job)
+  std::vector<std::vector<int32_t>> deps;           // per job: the steps it reads from (indices into jobs)
+  std::vector<int32_t> cur;                         // dependencies of the step being planned
   int seq = 0;
 
   Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, IntraPlan &o)
@@ -36,8 +39,10 @@ struct Planner {
     ctu = 1 << sp.ctu_log2;
   }
 
-  // component-sample rectangle -> unit rectangle of map ch (4x4 luma units / 2x2 chroma units)
-  int max_level(int ch, int x0, int y0, int x1, int y1) const {   // inclusive sample bounds
+  // component-sample rectangle -> unit rectangle of map ch (4x4 luma units / 2x2 chroma units); the
+  // highest level among the decoded units read, whose producing steps of component comp are collected
+  // in `cur` (the step's dependencies)
+  int max_level(int ch, int comp, int x0, int y0, int x1, int y1) {   // inclusive sample bounds
     const int s = ch ? 1 : 2;
     const int pw = ch ? sp.width / 2 : sp.width, ph = ch ? sp.height / 2 : sp.height;
     x0 = std::max(x0, 0); y0 = std::max(y0, 0);
@@ -47,27 +52,39 @@ struct Planner {
     for (int uy = y0 >> s; uy <= (y1 >> s); uy++)
       for (int ux = x0 >> s; ux <= (x1 >> s); ux++) {
         const size_t i = (size_t)uy * W4 + ux;
-        if (out.order[ch][i] < seq) m = std::max(m, level[ch][i]);
+        if (out.order[ch][i] < seq) {
+          m = std::max(m, level[ch][i]);
+          if (prod[comp][i] >= 0) cur.push_back(prod[comp][i]);
+        }
       }
     return m;
   }
-  void mark(int ch, int x, int y, int w, int h, int lev, bool set_order) {
+  void mark(int ch, int x, int y, int w, int h, int lev, bool set_order, int comp = -1, int job = -1) {
     const int s = ch ? 1 : 2;
     for (int uy = y >> s; uy < (y + h + (1 << s) - 1) >> s; uy++)
       for (int ux = x >> s; ux < (x + w + (1 << s) - 1) >> s; ux++) {
         const size_t i = (size_t)uy * W4 + ux;
         level[ch][i] = lev;
         if (set_order) out.order[ch][i] = seq;
+        if (comp >= 0) prod[comp][i] = job;
       }
   }
   // level of a prediction from the reference lines of region (x, y, w, h) with lengths topLen/leftLen
-  int ref_level(int ch, int x, int y, int topLen, int leftLen, int mrl) const {
-    int m = max_level(ch, x - 1 - mrl, y - 1 - mrl, x + topLen - 1, y - 1);
-    m = std::max(m, max_level(ch, x - 1 - mrl, y - 1 - mrl, x - 1, y + leftLen - 1));
+  int ref_level(int ch, int comp, int x, int y, int topLen, int leftLen, int mrl) {
+    int m = max_level(ch, comp, x - 1 - mrl, y - 1 - mrl, x + topLen - 1, y - 1);
+    m = std::max(m, max_level(ch, comp, x - 1 - mrl, y - 1 - mrl, x - 1, y + leftLen - 1));
     return m;
   }
 
-  void push(int lev, const IntraJob &j) { jobs.emplace_back(lev, j); }
+  // appends a step with the dependencies collected in `cur`; returns its index
+  int push(int lev, const IntraJob &j) {
+    std::sort(cur.begin(), cur.end());
+    cur.erase(std::unique(cur.begin(), cur.end()), cur.end());
+    jobs.emplace_back(lev, j);
+    deps.push_back(cur);
+    cur.clear();
+    return (int)jobs.size() - 1;
+  }
 
   IntraJob base(const vvcr_cu &c, int comp) const {
     IntraJob j{};
@@ -91,6 +108,7 @@ struct Planner {
       };
       const bool n0 = intraAt(c.x - 1, c.y + c.h - 1), n1 = intraAt(c.x + c.w - 1, c.y - 1);
       const int wIntra = (n0 && n1) ? 3 : ((!n0 && !n1) ? 1 : 2);
+      int id[3];
       for (int comp = 0; comp < 3; comp++) {
         const int ch = comp ? 1 : 0;
         IntraJob j = base(c, comp);
@@ -98,13 +116,14 @@ struct Planner {
         j.flags = IJ_CIIP;
         j.mode = 0;
         j.ciip_w = (uint8_t)wIntra;
-        const int lev = 1 + ref_level(ch, j.x, j.y, 2 * j.w, 2 * j.h, 0);
-        push(lev, j);
+        const int lev = 1 + ref_level(ch, comp, j.x, j.y, 2 * j.w, 2 * j.h, 0);
+        id[comp] = push(lev, j);
       }
       int lev = 0;
       for (auto it = jobs.end() - 3; it != jobs.end(); ++it) lev = std::max(lev, it->first);
-      mark(0, c.x, c.y, c.w, c.h, lev, true);
-      mark(1, c.cx, c.cy, c.cw, c.ch, lev, true);
+      mark(0, c.x, c.y, c.w, c.h, lev, true, 0, id[0]);
+      mark(1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
+      mark(1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
       return;
     }
     // plain inter: level 0, reconstructed before the intra waves
@@ -147,9 +166,9 @@ struct Planner {
       j.mode = (uint8_t)p.fidir_l;
       j.isp_k = (uint8_t)regs.size();
       const int fTop = ver ? 2 * c.w : c.w + j.w, fLeft = ver ? c.h + j.h : 2 * c.h;
-      const int lev = 1 + ref_level(0, c.x, c.y, fTop, fLeft, 0);
-      mark(0, c.x, c.y, c.w, c.h, lev, true);   // setDecomp of the whole CU (DecCu.cpp:288-291)
-      push(lev, j);
+      const int lev = 1 + ref_level(0, 0, c.x, c.y, fTop, fLeft, 0);
+      const int id = push(lev, j);
+      mark(0, c.x, c.y, c.w, c.h, lev, true, 0, id);   // setDecomp of the whole CU (DecCu.cpp:288-291)
       seq += (int)regs.size() - 1;
       return;
     }
@@ -163,9 +182,9 @@ struct Planner {
       if (c.bdpcm) { j.flags = IJ_BDPCM; j.mode = (uint8_t)c.bdpcm; }
       else if (c.mip) { j.flags = IJ_MIP | (p.mipt ? IJ_MIP_T : 0); j.mode = (uint8_t)p.idir_l; }
       else j.mode = (uint8_t)p.fidir_l;
-      const int lev = 1 + ref_level(0, j.x, j.y, 2 * j.w, 2 * j.h, j.mrl);
-      mark(0, j.x, j.y, j.w, j.h, lev, true);
-      push(lev, j);
+      const int lev = 1 + ref_level(0, 0, j.x, j.y, 2 * j.w, 2 * j.h, j.mrl);
+      const int id = push(lev, j);
+      mark(0, j.x, j.y, j.w, j.h, lev, true, 0, id);
     }
   }
 
@@ -183,14 +202,14 @@ struct Planner {
         if (c.bdpcmc) { j.flags = IJ_BDPCM; j.mode = (uint8_t)c.bdpcmc; }
         else j.mode = (uint8_t)p.fidir_c;
         if (dual) j.flags |= IJ_DUAL;
-        int lev = ref_level(1, j.x, j.y, 2 * j.w, 2 * j.h, 0);
+        int lev = ref_level(1, comp, j.x, j.y, 2 * j.w, 2 * j.h, 0);
         if (!c.bdpcmc && p.fidir_c >= 67) {   // CCLM: co-located luma and its template rows / columns
           const int lx = 2 * j.x, ly = 2 * j.y;
-          lev = std::max(lev, max_level(0, lx - 4, ly - 4, lx + 4 * j.w - 1, ly + 4 * j.h - 1));
+          lev = std::max(lev, max_level(0, 0, lx - 4, ly - 4, lx + 4 * j.w - 1, ly + 4 * j.h - 1));
         }
         lev += 1;
-        mark(1, j.x, j.y, j.w, j.h, lev, true);
-        push(lev, j);
+        const int id = push(lev, j);
+        mark(1, j.x, j.y, j.w, j.h, lev, true, comp, id);
       }
     }
   }
@@ -198,6 +217,7 @@ struct Planner {
   void run() {
     const size_t nu = (size_t)W4 * H4;
     for (int k = 0; k < 2; k++) { out.order[k].assign(nu, 1 << 30); level[k].assign(nu, 0); }
+    for (int k = 0; k < 3; k++) prod[k].assign(nu, -1);
     cu_map.assign(nu, -1);
     for (size_t i = 0; i < d.cu.size(); i++) {
       const vvcr_cu &c = d.cu[i];
@@ -234,15 +254,26 @@ struct Planner {
             throw VvcrError(VVCR_E_UNSUPPORTED, "IBC / palette CUs are not supported");
           }
         }
-    std::stable_sort(jobs.begin(), jobs.end(), [](const std::pair<int32_t, IntraJob> &a, const std::pair<int32_t, IntraJob> &b) {
-      return a.first < b.first;
-    });
-    int maxLev = jobs.empty() ? 0 : jobs.back().first;
+    // steps in level order (a topological order of the dependency graph), dependencies renumbered
+    std::vector<int32_t> perm(jobs.size());
+    for (size_t i = 0; i < perm.size(); i++) perm[i] = (int32_t)i;
+    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return jobs[a].first < jobs[b].first; });
+    std::vector<int32_t> rank(jobs.size());
+    for (size_t i = 0; i < perm.size(); i++) rank[perm[i]] = (int32_t)i;
+    int maxLev = jobs.empty() ? 0 : jobs[perm.back()].first;
     out.level_start.assign(maxLev + 2, 0);
     out.jobs.resize(jobs.size());
-    for (size_t i = 0; i < jobs.size(); i++) {
-      out.jobs[i] = jobs[i].second;
-      out.level_start[jobs[i].first + 1] = (int32_t)(i + 1);
+    out.dep_start.assign(jobs.size() + 1, 0);
+    out.deps.clear();
+    for (size_t i = 0; i < perm.size(); i++) {
+      const int32_t o = perm[i];
+      out.jobs[i] = jobs[o].second;
+      out.level_start[jobs[o].first + 1] = (int32_t)(i + 1);
+      for (int32_t d : deps[o]) {
+        if (rank[d] >= (int32_t)i) throw VvcrError(VVCR_E_STATE, "intra plan: dependency is not earlier in step order");
+        out.deps.push_back(rank[d]);
+      }
+      out.dep_start[i + 1] = (int32_t)out.deps.size();
     }
     for (int L = 1; L <= maxLev + 1; L++) out.level_start[L] = std::max(out.level_start[L], out.level_start[L - 1]);
   }
