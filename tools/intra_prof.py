@@ -1,6 +1,6 @@
 """Diagnostics: phase timestamps of every k_intra step (VVCR_INTRA_PROF build).
 
-  python tools/intra_prof.py build           # here: builds build/prof/libvvcr_prof.so
+  python tools/intra_prof.py build [-Dxx]     # here: builds build/prof/libvvcr_prof.so (extra defines)
   python tools/intra_prof.py run [stream]    # GPU box: decodes the stream, writes gpurun_out/iprof_<stream>.npz
 """
 import os
@@ -10,10 +10,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF_LIB = os.path.join(ROOT, "build", "prof", "libvvcr_prof.so")
 
 
-def build():
+def build(extra=()):
     sys.path.insert(0, ROOT)
     from vvc_amd import build as B
-    B.build_lib(extra=["-DVVCR_INTRA_PROF"], obj_dir=os.path.join(ROOT, "build", "prof", "obj"), lib=PROF_LIB)
+    B.build_lib(extra=["-DVVCR_INTRA_PROF"] + list(extra), obj_dir=os.path.join(ROOT, "build", "prof", "obj"), lib=PROF_LIB)
 
 
 def run(stream):
@@ -51,6 +51,6 @@ def run(stream):
 
 if __name__ == "__main__":
     if sys.argv[1] == "build":
-        build()
+        build(sys.argv[2:])
     else:
         run(sys.argv[2] if len(sys.argv) > 2 else "ra1080_q32")

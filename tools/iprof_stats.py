@@ -1,7 +1,7 @@
 """Summarise gpurun_out/iprof_<stream>.npz (tools/intra_prof.py).
 
-Record per step: [0..2] s_memrealtime (100 MHz) at take / dependencies met / done, [3],[4] phase
-cycles (refs | params << 32, predict | total << 32), [5] comp,w,h,flags,mode,xcc, [6] step | block << 32,
+Record per step: [0..2] s_memrealtime (100 MHz) at take / dependencies met / done, [3],[4] eight 16-bit
+phase stamps, [5] comp,w,h,flags,mode,xcc, [6] step | block << 32,
 [7] number of dependencies, [8] picture, [9] repetition."""
 import sys
 import numpy as np
@@ -9,8 +9,11 @@ a = np.load(sys.argv[1])['prof']
 a = a[a[:, 9] == a[:, 9].max()]
 info = a[:, 5]
 comp = info & 0xff; w = (info >> 8) & 0xff; h = (info >> 16) & 0xff; flags = (info >> 24) & 0xff; mode = (info >> 32) & 0xff
-m32 = np.uint64(0xffffffff)
-ph = np.stack([a[:, 3] & m32, a[:, 3] >> np.uint64(32), a[:, 4] & m32, a[:, 4] >> np.uint64(32)], 1).astype(np.int64)
+m16 = np.uint64(0xffff)
+st = np.stack([(a[:, 3 + q // 4] >> np.uint64(16 * (q % 4))) & m16 for q in range(8)], 1).astype(np.int64)
+print("stamps (cycles from start, 16-bit): job, resid, fill-loads, fill, refs, params, predict, end")
+print("  mean", st.mean(0).round(0), " median", np.median(st, 0))
+ph = st[:, [4, 5, 6, 7]]
 d = np.diff(np.concatenate([np.zeros((len(a), 1), np.int64), ph], 1), axis=1)
 t0, t1, t2 = (a[:, k].astype(np.int64) for k in range(3))
 print("steps", len(a), "phase cycles [refs, params, predict, recon]", d.mean(0).round(0), "total", ph[:, 3].mean().round(0))

@@ -70,10 +70,10 @@ struct Prepared {
   DevVec<McJob> mc_basic, mc_bidir;
   DevVec<AffPu> aff_pu;
   DevVec<AffJob> aff_jobs;
-  DevVec<int32_t> order;
   DevVec<ReconTile> tiles;
   DevVec<IntraJob> ijobs;
   DevVec<int32_t> idep_start, ideps, istate;
+  DevVec<IntraParams> iparams;       // device copy of the intra kernel's parameters
   int n_ijobs = 0;
   std::vector<int32_t> level_start;
   DevVec<DbkSeg> dbk;
@@ -84,7 +84,6 @@ struct Prepared {
   DevVec<int32_t> dmvr;
   bool have_sao = false, have_alf = false;
   int n_tb = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
-  size_t n_order = 0;
   hipEvent_t ev[NK][2] = {};
   hipEvent_t done = nullptr;
   bool ran[NK] = {};
@@ -223,15 +222,16 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
   if (mask & VVCR_STAGE_INTRA) {
     plan_intra(sp, pp, ctx->desc, ctx->intra);
     IntraPlan &ip = ctx->intra;
-    r.n_order = ip.order[0].size();
-    std::vector<int32_t> ord(ip.order[0]);
-    ord.insert(ord.end(), ip.order[1].begin(), ip.order[1].end());
-    r.order.upload(ord);
     r.tiles.upload(ip.inter_tiles);
     r.ijobs.upload(ip.jobs);
     r.idep_start.upload(ip.dep_start);
     r.ideps.upload(ip.deps);
     r.istate.ensure(16 + ip.jobs.size());
+    IntraParams P{};
+    for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
+    P.bd = ctx->sp.bit_depth;
+    P.ctu = 1 << ctx->sp.ctu_log2;
+    r.iparams.upload(&P, 1);
     r.n_ijobs = (int)ip.jobs.size();
     r.level_start = ip.level_start;
     r.n_tiles = (int)ip.inter_tiles.size();
@@ -322,9 +322,6 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   if (mask & VVCR_STAGE_INTRA) {
     IntraParams P{};
     for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
-    P.order[0] = r.order.p;
-    P.order[1] = r.order.p + r.n_order;
-    P.W4 = ctx->sp.width / 4;
     P.bd = ctx->sp.bit_depth;
     P.ctu = 1 << ctx->sp.ctu_log2;
     {
@@ -335,7 +332,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     }
     {
       KernelTimer t(r, K_INTRA, s);
-      launch_intra(P, r.ijobs.p, r.n_ijobs, r.idep_start.p, r.ideps.p, r.istate.p, ctx->d_err, ctx->n_cu, s);
+      launch_intra(r.iparams.p, r.ijobs.p, r.n_ijobs, r.idep_start.p, r.ideps.p, r.istate.p, ctx->d_err, ctx->n_cu, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_INTRA] = r.n_ijobs ? 1 : 0;
     }

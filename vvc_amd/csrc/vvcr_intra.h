@@ -35,8 +35,14 @@ struct IntraJob {
   int16_t cx, cy;         // CU position (component samples)
   uint8_t cw, ch;         // CU size (component samples, 128 fits)
   int32_t seq;            // decoding sequence number (availability: order[unit] < seq)
+  // Availability of the reference units, resolved on the host (it depends only on the decoding order):
+  // bit u of av[0..1] / bit 0 of av[2] = unit u (0 = bottom-most below-left ... top-right, the scan of
+  // xFillReferenceSamples) after the scans' early stops; av[2] bit 8 + k: ISP region k (1..3) has its
+  // left (horizontal split) / above (vertical split) neighbour; av[2] bits 16..27 / av[3]: CCLM
+  // neighbourhoods (see nb_bits in vvcr_intra_host.cpp).
+  uint32_t av[4];
 };
-static_assert(sizeof(IntraJob) == 24, "IntraJob layout");
+static_assert(sizeof(IntraJob) == 40, "IntraJob layout");
 
 // Inter CU reconstruction tile: reco = clip(pred + resi), one <= 16x16 luma tile plus its chroma.
 struct ReconTile {
@@ -62,13 +68,11 @@ struct IntraParams {
   DPlane reco[3];                    // picture being reconstructed (in place)
   DPlane pred[3];                    // inter prediction planes (CIIP)
   DPlane resi[3];                    // residual planes
-  const int32_t *order[2];
-  int32_t W4;                        // order map row pitch (units)
   int32_t bd, ctu;
 };
 
 void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out);
 void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s);
 // all steps of a picture in one persistent launch; state: 16 + n int32 (reset here); *err set on a wait timeout
-void launch_intra(const IntraParams &p, const IntraJob *jobs, int n, const int32_t *dep_start, const int32_t *deps,
+void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *dep_start, const int32_t *deps,
                   int32_t *state, int32_t *err, int n_cu, hipStream_t s);

@@ -24,7 +24,8 @@ extern "C" int vvcr_intra_prof_read(unsigned long long *dst, int max) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_iprof_n), &z, sizeof(z));
   return (int)n;
 }
-#define IPROF(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); tstamp[i] = __builtin_readcyclecounter(); } while (0)
+__shared__ unsigned long long tstamp[10];
+#define IPROF(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); if (threadIdx.x == 0) tstamp[i] = __builtin_readcyclecounter(); } while (0)
 #define IPROF_RT(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); rstamp[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define IPROF(i) do { } while (0)
@@ -52,17 +53,6 @@ struct Ctx {
   int seq;
 };
 
-// "already decompressed" test of the unit containing (x, y) of channel ch (CodingStructure::isDecomp +
-// getCURestricted: same slice/tile, earlier in decoding order)
-__device__ __forceinline__ bool avail(const IntraParams &P, int ch, int x, int y, int seq) {
-  const int pw = ch ? P.reco[1].w : P.reco[0].w, ph = ch ? P.reco[1].h : P.reco[0].h;
-  const bool in = x >= 0 && y >= 0 && x < pw && y < ph;
-  const int s = ch ? 1 : 2;
-  // the load is unconditional (clamped) so that the loads of several scans issue together
-  const int32_t o = P.order[ch][(clampi(y, 0, ph - 1) >> s) * P.W4 + (clampi(x, 0, pw - 1) >> s)];
-  return in & (o < seq);
-}
-
 __device__ __forceinline__ int pel(const DPlane &D, int x, int y) { return D.p[(size_t)y * D.stride + x]; }
 
 // Reconstructed samples are handed between steps of one launch (k_intra is persistent): every store of
@@ -72,7 +62,11 @@ __device__ __forceinline__ int pel(const DPlane &D, int x, int y) { return D.p[(
 // visibility, first row of the sc1 hand-off table; one workgroup per CU).
 typedef __attribute__((address_space(1))) uint32_t gu32;
 __device__ __forceinline__ uint32_t ld_sc1(const int16_t *p) {   // p 4-byte aligned
+#ifdef VVCR_PROF_PLAIN_LOADS   // diagnostics only: latency of plain loads (not a valid hand-off)
+  return *(const uint32_t *)p;
+#else
   return __hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 __device__ __forceinline__ void st_sc1(int16_t *p, uint32_t v) {   // p 4-byte aligned
   __hip_atomic_store((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -84,26 +78,6 @@ __device__ __forceinline__ int pel_rc(const DPlane &D, int x, int y) {
 }
 __device__ __forceinline__ uint32_t pair_rc(const DPlane &D, int x, int y) { return ld_sc1(D.p + (size_t)y * D.stride + x); }
 
-// Leading run of "already decompressed" units along a line of `count` (<= 64) units starting at (x, y),
-// step (dx, dy): the availability scans of the reference stop at the first unit not yet decoded
-// (isAboveAvailable / isLeftAvailable / ... IntraPrediction.cpp:1208-1310). One wave ballot.
-__device__ __forceinline__ int avail_run(const IntraParams &P, int ch, int seq, int x, int y, int dx, int dy, int count, int lane) {
-  const bool ok = (lane < count) & avail(P, ch, x + lane * dx, y + lane * dy, seq);
-  const uint64_t m = __ballot(ok);
-  const int lead = __builtin_ctzll(~m);   // m has at most 64 set bits; ~m == 0 only when all 64 lanes are in and available
-  return min(lead, count);
-}
-
-// Run of consecutive set bits of m starting at bit p (0 <= p < 64), going up / going down.
-__device__ __forceinline__ int run_up(uint64_t m, int p) {
-  const uint64_t z = ~(m >> p);   // top p bits are ones, so z == 0 only when p == 0 and m is all ones
-  return z ? (int)__builtin_ctzll(z) : 64;
-}
-__device__ __forceinline__ int run_down(uint64_t m, int p) {
-  const uint64_t z = ~(m << (63 - p));
-  return z ? (int)__builtin_clzll(z) : 64;
-}
-
 __device__ __forceinline__ int wave_sum(int v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
@@ -113,116 +87,76 @@ __device__ __forceinline__ int wave_sum(int v) {
 // left[0..predHSize+mrl]; index 0 = corner line.
 //
 // The reference walks the reference units sequentially (IntraPrediction.cpp:913-1149): units are
-// numbered in scan order 0 = bottom-most below-left ... totalLeft = corner ... top-right; missing units
-// get the last sample (in scan order) of the nearest earlier available unit, and the units before the
-// first available one get its first sample. That result depends only on the availability mask, so here
-// every lane derives its own unit's samples from two ballots and the raw reference line in LDS.
-__device__ void fill_refs(const IntraParams &P, const DPlane &D, int ch, int seq, int fx, int fy, int fw, int fh, int predSize,
-                          int predHSize, int mrl, int bd, int16_t *top, int16_t *left, int16_t *rawT, int16_t *rawL, int lane) {
-  const int uw = ch ? 2 : 4, uh = uw;
-  const int totalAbove = (predSize + uw - 1) / uw, totalLeft = (predHSize + uh - 1) / uh;
-  const int totalUnits = totalAbove + totalLeft + 1;
-  const int numAbove = max(fw / uw, 1), numLeft = max(fh / uh, 1);
-  const int numAR = totalAbove - numAbove, numBL = totalLeft - numLeft;
+// numbered in scan order 0 = bottom-most below-left ... totalLeft = corner ... top-right; a missing unit
+// gets the last sample (in scan order) of the nearest earlier available unit, the units before the first
+// available one get its first sample, and with no unit available every sample is 1 << (bd - 1). The
+// availability mask (lo: units 0..63, hi: unit 64) comes resolved from the host, so every lane handles
+// its own samples: available ones are copied, then missing ones read their source from the lines.
+__device__ void fill_refs(const DPlane &D, int ch, int fx, int fy, int predSize, int predHSize, int mrl, int bd,
+                          uint64_t lo, bool hi, int16_t *top, int16_t *left, int lane) {
+  const int lu = ch ? 1 : 2;   // log2 of the unit size
+  const int totalLeft = (predHSize + (1 << lu) - 1) >> lu;
   const int ox = fx - 1 - mrl, oy = fy - 1 - mrl;   // corner sample of the reference line
-  const int pw = D.w, ph = D.h;
-  // raw reference line (clamped coordinates; samples of missing units are never used). All loads of
-  // the fill (3 + 3 samples and 2 order-map entries per lane) are issued before the first wait.
-  int16_t tv[3], lv[3];
-  {
-    const int cy = clampi(oy, 0, ph - 1), cx = clampi(ox, 0, pw - 1);
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-      tv[r] = (int16_t)pel_rc(D, clampi(ox + lane + 64 * r, 0, pw - 1), cy);
-      lv[r] = (int16_t)pel_rc(D, cx, clampi(oy + lane + 64 * r, 0, ph - 1));
-    }
-  }
-  // raw availability of every unit (unit u = lane, plus unit 64 on every lane), one load phase
-  auto unitPos = [&](int u, int &x, int &y) {
-    if (u == totalLeft) { x = fx - 1; y = fy - 1; }
-    else if (u > totalLeft && u <= totalLeft + numAbove) { x = fx + (u - totalLeft - 1) * uw; y = fy - 1; }
-    else if (u > totalLeft + numAbove) { x = fx + fw - 1 + uw + (u - totalLeft - 1 - numAbove) * uw; y = fy - 1; }
-    else if (u >= totalLeft - numLeft) { x = fx - 1; y = fy + (totalLeft - 1 - u) * uh; }
-    else { x = fx - 1; y = fy + fh - 1 + uh + (totalLeft - 1 - numLeft - u) * uh; }
-  };
-  int ux, uy;
-  unitPos(lane, ux, uy);
-  const uint64_t raw = __ballot((lane < totalUnits) & avail(P, ch, ux, uy, seq));
-  bool raw64 = false;
-  if (totalUnits > 64) {   // only a 64-wide luma block with its 64 above-right samples
-    int vx, vy;
-    unitPos(64, vx, vy);
-    raw64 = avail(P, ch, vx, vy, seq);
-  }
-  // the scans stop at the first unit not yet decoded; the above-right / below-left scans do not
-  // depend on the above / left ones. Segments: below-left [0, tl-numLeft), left [tl-numLeft, tl),
-  // corner tl, above (tl, tl+numAbove], above-right (tl+numAbove, totalUnits).
-  const int tl = totalLeft;
-  const int nA = min(run_up(raw, tl + 1), numAbove);
-  const int pAR = tl + 1 + numAbove;
-  int nAR2 = 0;
-  if (numAR > 0) {
-    nAR2 = pAR < 64 ? run_up(raw, pAR) : 0;
-    if (pAR + nAR2 == 64 && raw64) nAR2++;
-    nAR2 = min(nAR2, numAR);
-  }
-  const int nL = min(run_down(raw, tl - 1), numLeft);
-  const int nBL2 = numBL == 0 ? 0 : min(run_down(raw, tl - 1 - numLeft), numBL);
-  const bool cAv = ((raw >> tl) & 1) != 0;
-  auto unitAv = [&](int u) -> bool {
-    if (u == totalLeft) return cAv;
-    if (u > totalLeft) {
-      const int i = u - totalLeft - 1;
-      return i < numAbove ? i < nA : (i - numAbove) < nAR2;
-    }
-    const int i = totalLeft - 1 - u;   // distance below the top of the left column, in units
-    return i < numLeft ? i < nL : (i - numLeft) < nBL2;
-  };
-  const uint64_t m0 = __ballot(lane < totalUnits && unitAv(lane));
-  const bool av64 = totalUnits > 64 && unitAv(64);
-  const int cnt = __popcll(m0) + (av64 ? 1 : 0);
-#pragma unroll
-  for (int r = 0; r < 3; r++) {
-    if (lane + 64 * r <= predSize + mrl) rawT[lane + 64 * r] = tv[r];
-    if (lane + 64 * r <= predHSize + mrl) rawL[lane + 64 * r] = lv[r];
-  }
-  __syncthreads();   // raw line in LDS
-  if (cnt == 0) {
+  const int nT = predSize + mrl, nL = predHSize + mrl;   // last index of each line
+  if (lo == 0 && !hi) {
     const int16_t dc = (int16_t)(1 << (bd - 1));
-    for (int j = lane; j <= predSize + mrl; j += 64) top[j] = dc;
-    for (int i = lane; i <= predHSize + mrl; i += 64) left[i] = dc;
+    for (int j = lane; j <= nT; j += 64) top[j] = dc;
+    for (int i = lane; i <= nL; i += 64) left[i] = dc;
     __syncthreads();
     return;
   }
-  const int firstAv = m0 ? __builtin_ctzll(m0) : 64;
-  auto scanFirst = [&](int q) -> int16_t {
-    if (q < totalLeft) return rawL[(totalLeft - q) * uh + mrl];
-    if (q == totalLeft) return rawL[mrl];
-    return rawT[(q - totalLeft - 1) * uw + 1 + mrl];
-  };
-  auto scanLast = [&](int q) -> int16_t {
-    if (q < totalLeft) return rawL[(totalLeft - q - 1) * uh + mrl + 1];
-    if (q == totalLeft) return rawT[mrl];
-    return rawT[(q - totalLeft) * uw + mrl];
-  };
-  for (int u = lane; u < totalUnits; u += 64) {
-    const bool a = u < 64 ? ((m0 >> u) & 1) != 0 : av64;
-    int16_t v = 0;
-    if (!a) {
-      const uint64_t below = u < 64 ? (m0 & ((1ull << u) - 1)) : m0;
-      v = below ? scanLast(63 - __builtin_clzll(below)) : scanFirst(firstAv);
+  // unit of top sample j / left sample i
+  auto unitT = [&](int j) { return j <= mrl ? totalLeft : totalLeft + 1 + ((j - 1 - mrl) >> lu); };
+  auto unitL = [&](int i) { return i <= mrl ? totalLeft : totalLeft - 1 - ((i - 1 - mrl) >> lu); };
+  auto unitAv = [&](int u) { return u < 64 ? ((lo >> u) & 1) != 0 : hi; };
+  int16_t tv[3], lv[3];
+  {
+    const int cy = max(oy, 0), cx = max(ox, 0);   // missing samples are loaded from clamped positions, never used
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      tv[r] = (int16_t)pel_rc(D, min(max(ox + min(lane + 64 * r, nT), 0), D.w - 1), cy);
+      lv[r] = (int16_t)pel_rc(D, cx, min(max(oy + min(lane + 64 * r, nL), 0), D.h - 1));
     }
-    if (u == totalLeft) {
-      for (int i = 0; i <= mrl; i++) { top[i] = a ? rawT[i] : v; left[i] = a ? rawL[i] : v; }
-    } else if (u < totalLeft) {
-      const int i0 = (totalLeft - 1 - u) * uh + 1 + mrl;
-      const int n = u == 0 ? ((predHSize % uh == 0) ? uh : predHSize % uh) : uh;
-      for (int i = i0; i < i0 + n; i++) left[i] = a ? rawL[i] : v;
-    } else {
-      const int j0 = (u - totalLeft - 1) * uw + 1 + mrl;
-      const int n = u == totalUnits - 1 ? ((predSize % uw == 0) ? uw : predSize % uw) : uw;
-      for (int j = j0; j < j0 + n; j++) top[j] = a ? rawT[j] : v;
+  }
+  IPROF(3);
+  bool missing = false;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int j = lane + 64 * r;
+    if (j <= nT) { if (unitAv(unitT(j))) top[j] = tv[r]; else missing = true; }
+    if (j <= nL) { if (unitAv(unitL(j))) left[j] = lv[r]; else missing = true; }
+  }
+  if (__ballot(missing) == 0) { __syncthreads(); return; }
+  __syncthreads();
+  // missing units: the scan-order last sample of the nearest earlier available unit, else the first
+  // sample of the first available unit (both are copied samples)
+  const int firstAv = lo ? __builtin_ctzll(lo) : 64;
+  auto source = [&](int u) -> int16_t {
+    const uint64_t below = u < 64 ? (lo & ((1ull << u) - 1)) : lo;
+    if (below) {
+      const int q = 63 - __builtin_clzll(below);   // scan-last sample of unit q
+      if (q < totalLeft) return left[((totalLeft - q - 1) << lu) + mrl + 1];
+      if (q == totalLeft) return top[mrl];
+      return top[((q - totalLeft) << lu) + mrl];
     }
+    const int q = firstAv;                          // scan-first sample of unit q
+    if (q < totalLeft) return left[((totalLeft - q) << lu) + mrl];
+    if (q == totalLeft) return left[mrl];
+    return top[((q - totalLeft - 1) << lu) + 1 + mrl];
+  };
+  int16_t sv[6];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int j = lane + 64 * r;
+    sv[r] = (j <= nT && !unitAv(unitT(j))) ? source(unitT(j)) : 0;
+    sv[3 + r] = (j <= nL && !unitAv(unitL(j))) ? source(unitL(j)) : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int j = lane + 64 * r;
+    if (j <= nT && !unitAv(unitT(j))) top[j] = sv[r];
+    if (j <= nL && !unitAv(unitL(j))) left[j] = sv[3 + r];
   }
   __syncthreads();
 }
@@ -238,29 +172,24 @@ __device__ int wide_angle(int w, int h, int mode) {
   return mode;
 }
 
-// isAbove/Left/AboveRight/BelowLeftAvailable counts for CCLM (availability with early break)
+// isAbove/Left/AboveRight/BelowLeftAvailable counts for CCLM (resolved on the host: nb_bits)
 struct NbAvail {
   bool above, left;
   int ar, bl;          // available above-right / below-left units
 };
-__device__ NbAvail nb_avail(const IntraParams &P, int ch, int seq, int x, int y, int w, int h, int unit, int lane) {
-  NbAvail r{};
-  const int na = w / unit, nl = h / unit;
-  const int l = avail_run(P, ch, seq, x - 1, y, 0, unit, nl, lane);
-  const int a = avail_run(P, ch, seq, x, y - 1, unit, 0, na, lane);
-  const int bl = avail_run(P, ch, seq, x - 1, y + h - 1 + unit, 0, unit, nl, lane);
-  const int ar = avail_run(P, ch, seq, x + w - 1 + unit, y - 1, unit, 0, na, lane);
-  r.left = l == nl;
-  r.above = a == na;
-  r.bl = r.left ? bl : 0;
-  r.ar = r.above ? ar : 0;
+__device__ __forceinline__ NbAvail nb_decode(uint32_t b) {
+  NbAvail r;
+  r.above = (b & 1) != 0;
+  r.left = (b & 2) != 0;
+  r.ar = (b >> 2) & 31;
+  r.bl = (b >> 7) & 31;
   return r;
 }
 
 // Persistent: one workgroup (one wave) per CU takes steps from an atomic counter in topological order
 // and waits, per step, for the steps it reads from (dependency lists built by plan_intra).
 // state[0] = step counter, state[16 + i] = step i done; *err set if a wait times out.
-__global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__restrict__ jobs, int njobs,
+__global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg, const IntraJob *__restrict__ jobs, int njobs,
                                               const int32_t *__restrict__ dep_start, const int32_t *__restrict__ deps,
                                               int32_t *state, int32_t *err) {
   __shared__ int16_t refU[2][RB];          // unfiltered top / left (index 0 = corner)
@@ -285,7 +214,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   __syncthreads();
   if (j >= njobs) break;
 #ifdef VVCR_INTRA_PROF
-  unsigned long long tstamp[5], rstamp[3];
+  unsigned long long rstamp[3];
 #endif
   IPROF_RT(0);
   for (int k = dep_start[j] + lane; k < dep_start[j + 1]; k += 64) {
@@ -300,6 +229,10 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   __syncthreads();
   IPROF_RT(1);
   IPROF(0);
+  // parameters are re-read per step (scalar cache) rather than held in registers across the loop
+  const IntraParams *Pq = Pg;
+  asm volatile("" : "+s"(Pq));
+  const IntraParams &P = *Pq;
   const IntraJob J = jobs[j];
   const int comp = J.comp, ch = comp ? 1 : 0;
   const int bd = P.bd, maxv = (1 << bd) - 1;
@@ -314,6 +247,9 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   const int mrl = comp ? 0 : J.mrl;
   const int n = w * h;
   const int nreg = isp ? J.isp_k : 1;
+  const uint64_t avlo = (uint64_t)J.av[0] | (uint64_t)J.av[1] << 32;
+  const bool avhi = (J.av[2] & 1) != 0;
+  IPROF(1);
   // residual rectangle: the block, or the whole CU for ISP
   const int rx = isp ? J.cx : J.x, ry = isp ? J.cy : J.y, rw = isp ? J.cw : w, rh = isp ? J.ch : h;
   // The residual does not depend on earlier steps: the first 2048 samples are loaded into registers
@@ -339,6 +275,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
       rs[b] = R.p[(size_t)(ry + yy) * R.stride + rx + xx];
     }
   }
+  IPROF(2);
   auto store_resid = [&]() {
     if (rvec) {
 #pragma unroll
@@ -370,17 +307,17 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   {
     int16_t *top = refU[0], *left = refU[1];
     if (!isp) {
-      fill_refs(P, D, ch, J.seq, x0, y0, w, h, topLen, leftLen, mrl, bd, top, left, mainA, sideA, lane);
+      fill_refs(D, ch, x0, y0, topLen, leftLen, mrl, bd, avlo, avhi, top, left, lane);
     } else if (kreg == 0) {
       // CU-level fill of the first region (predSize per split direction), kept in refF for the others
       const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
-      fill_refs(P, D, 0, J.seq, J.cx, J.cy, J.cw, J.ch, fTop, fLeft, 0, bd, top, left, mainA, sideA, lane);
+      fill_refs(D, 0, J.cx, J.cy, fTop, fLeft, 0, bd, avlo, avhi, top, left, lane);
       if (nreg > 1)
         for (int i = lane; i < RB; i += 64) { refF[0][i] = top[i]; refF[1][i] = left[i]; }
     } else {
       // the shift of initIntraPatternChTypeISP (:798-897); ispPrev = last row / column of region k-1
       if (!ispVer) {   // horizontal split: left column shifted, top row from the region above
-        const bool la = avail(P, 0, x0 - 1, y0, J.seq);
+        const bool la = (J.av[2] >> (8 + kreg)) & 1;
         const int sh = kreg * h;
         const int16_t src0 = ispPrev[0];
         for (int i = lane; i <= leftLen; i += 64) left[i] = la ? refF[1][i + sh] : src0;
@@ -388,7 +325,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
         const int16_t last = ispPrev[w - 1];
         for (int i = lane; i <= topLen; i += 64) top[i] = i == 0 ? corner : (i <= w ? ispPrev[i - 1] : last);
       } else {         // vertical split: top row shifted, left column from the region to the left
-        const bool aa = avail(P, 0, x0, y0 - 1, J.seq);
+        const bool aa = (J.av[2] >> (8 + kreg)) & 1;
         const int sh = kreg * w;
         const int16_t src0 = ispPrev[0];
         for (int i = lane; i <= topLen; i += 64) top[i] = aa ? refF[0][i + sh] : src0;
@@ -398,9 +335,10 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
       }
     }
   }
+  IPROF(4);
   if (kreg == 0) store_resid();   // read after the barriers that follow
   __syncthreads();
-  IPROF(1);
+  IPROF(5);
 
   // ---- prediction parameters (initPredIntraParams)
   const int dirMode = ciip ? PLANAR : (int)J.mode;
@@ -454,7 +392,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
     }
     __syncthreads();
   }
-  IPROF(2);
+  IPROF(6);
   const int16_t *top = refFilter ? refF[0] : refU[0];
   const int16_t *left = refFilter ? refF[1] : refU[1];
 #define predv(q) pred[lane + 64 * (q)]
@@ -465,8 +403,8 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
     const int lx = 2 * x0, ly = 2 * y0;
     const bool dual = (J.flags & IJ_DUAL) != 0;
     // luma-template availability: luma map in a single tree, chroma map in a separate chroma tree
-    const NbAvail lr = dual ? nb_avail(P, 1, J.seq, x0, y0, w, h, 2, lane) : nb_avail(P, 0, J.seq, lx, ly, 2 * w, 2 * h, 4, lane);
-    const NbAvail lm = nb_avail(P, 1, J.seq, x0, y0, w, h, 2, lane);
+    const NbAvail lr = nb_decode(J.av[2] >> 16), lm = nb_decode(J.av[3]);
+    (void)dual;
     const int mode = J.mode;
     const int addAR = (mode == MDLM_L || mode == MDLM_T) ? lr.ar * 2 : 0;
     const int addBL = (mode == MDLM_L || mode == MDLM_T) ? lr.bl * 2 : 0;
@@ -764,7 +702,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
     }
   }
 
-  IPROF(3);
+  IPROF(7);
   // ---- CIIP blend (geneWeightedPred) and reconstruction
   const DPlane &PP = P.pred[comp];
   __syncthreads();   // pred[] of other lanes
@@ -787,7 +725,7 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
   __syncthreads();
   if (lane == 0) __hip_atomic_store(&done[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #ifdef VVCR_INTRA_PROF
-  IPROF(4);
+  IPROF(8);
   IPROF_RT(2);
   if (lane == 0) {
     const unsigned int slot = atomicAdd(&g_iprof_n, 1u);
@@ -797,8 +735,8 @@ __global__ __launch_bounds__(64) void k_intra(IntraParams P, const IntraJob *__r
       g_iprof[slot][0] = rstamp[0];
       g_iprof[slot][1] = rstamp[1];
       g_iprof[slot][2] = rstamp[2];
-      g_iprof[slot][3] = (tstamp[1] - tstamp[0]) | (tstamp[2] - tstamp[0]) << 32;
-      g_iprof[slot][4] = (tstamp[3] - tstamp[0]) | (tstamp[4] - tstamp[0]) << 32;
+      g_iprof[slot][3] = (tstamp[1] - tstamp[0]) | (tstamp[2] - tstamp[0]) << 16 | (tstamp[3] - tstamp[0]) << 32 | (tstamp[4] - tstamp[0]) << 48;
+      g_iprof[slot][4] = (tstamp[5] - tstamp[0]) | (tstamp[6] - tstamp[0]) << 16 | (tstamp[7] - tstamp[0]) << 32 | (tstamp[8] - tstamp[0]) << 48;
       g_iprof[slot][5] = (unsigned long long)J.comp | (unsigned long long)J.w << 8 | (unsigned long long)J.h << 16 |
                          (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40;
       g_iprof[slot][6] = (unsigned long long)j | (unsigned long long)blockIdx.x << 32;
@@ -834,10 +772,10 @@ void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hip
   hipLaunchKernelGGL(k_recon_inter, dim3(n), dim3(64), 0, s, p, tiles, n);
 }
 
-void launch_intra(const IntraParams &p, const IntraJob *jobs, int n, const int32_t *dep_start, const int32_t *deps,
+void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *dep_start, const int32_t *deps,
                   int32_t *state, int32_t *err, int n_cu, hipStream_t s) {
   if (n <= 0) return;
   VVCR_CHECK_HIP(hipMemsetAsync(state, 0, (16 + (size_t)n) * sizeof(int32_t), s));
   // 64 KiB of dynamic LDS on top of the kernel's own keeps one workgroup per CU
-  hipLaunchKernelGGL(k_intra, dim3(std::min(n, n_cu)), dim3(64), 65536, s, p, jobs, n, dep_start, deps, state, err);
+  hipLaunchKernelGGL(k_intra, dim3(std::min(n, n_cu)), dim3(64), 65536, s, p_dev, jobs, n, dep_start, deps, state, err);
 }

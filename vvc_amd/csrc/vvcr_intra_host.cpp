@@ -214,6 +214,74 @@ struct Planner {
     }
   }
 
+  // ---- availability, as the reference evaluates it when the step runs (final order map: a unit is
+  // decoded before step s iff order < s)
+  bool av(int ch, int x, int y, int sq) const {
+    const int pw = ch ? sp.width / 2 : sp.width, ph = ch ? sp.height / 2 : sp.height;
+    if (x < 0 || y < 0 || x >= pw || y >= ph) return false;
+    const int s = ch ? 1 : 2;
+    return out.order[ch][(size_t)(y >> s) * W4 + (x >> s)] < sq;
+  }
+  // xFillReferenceSamples unit scan (IntraPrediction.cpp:913-986, isAboveAvailable etc. :1208-1310):
+  // returns the 65-bit availability mask in (lo, hi)
+  void fill_mask(int ch, int sq, int fx, int fy, int fw, int fh, int predSize, int predHSize, uint64_t &lo, uint32_t &hi) const {
+    const int uw = ch ? 2 : 4, uh = uw;
+    const int totalAbove = (predSize + uw - 1) / uw, totalLeft = (predHSize + uh - 1) / uh;
+    const int numAbove = std::max(fw / uw, 1), numLeft = std::max(fh / uh, 1);
+    const int numAR = totalAbove - numAbove, numBL = totalLeft - numLeft;
+    bool F[2 * 64 + 1] = {};
+    F[totalLeft] = av(ch, fx - 1, fy - 1, sq);
+    for (int i = 0; i < numAbove && av(ch, fx + i * uw, fy - 1, sq); i++) F[totalLeft + 1 + i] = true;
+    for (int i = 0; i < numAR && av(ch, fx + fw - 1 + uw + i * uw, fy - 1, sq); i++) F[totalLeft + 1 + numAbove + i] = true;
+    for (int i = 0; i < numLeft && av(ch, fx - 1, fy + i * uh, sq); i++) F[totalLeft - 1 - i] = true;
+    for (int i = 0; i < numBL && av(ch, fx - 1, fy + fh - 1 + uh + i * uh, sq); i++) F[totalLeft - 1 - numLeft - i] = true;
+    lo = 0; hi = 0;
+    const int total = totalAbove + totalLeft + 1;
+    if (total > 65) throw VvcrError(VVCR_E_STATE, "intra plan: more than 65 reference units");
+    for (int u = 0; u < total; u++)
+      if (F[u]) { if (u < 64) lo |= 1ull << u; else hi |= 1u << (u - 64); }
+  }
+  // CCLM neighbourhood (above / left complete, above-right / below-left unit counts): 12 bits
+  uint32_t nb_bits(int ch, int sq, int x, int y, int w, int h, int unit) const {
+    const int na = w / unit, nl = h / unit;
+    int l = 0, a = 0, bl = 0, ar = 0;
+    while (l < nl && av(ch, x - 1, y + l * unit, sq)) l++;
+    while (a < na && av(ch, x + a * unit, y - 1, sq)) a++;
+    const bool left = l == nl, above = a == na;
+    if (left) while (bl < nl && av(ch, x - 1, y + h - 1 + unit + bl * unit, sq)) bl++;
+    if (above) while (ar < na && av(ch, x + w - 1 + unit + ar * unit, y - 1, sq)) ar++;
+    if (ar > 31 || bl > 31) throw VvcrError(VVCR_E_STATE, "intra plan: CCLM neighbourhood too large");
+    return (above ? 1u : 0u) | (left ? 2u : 0u) | (uint32_t)ar << 2 | (uint32_t)bl << 7;
+  }
+  void resolve_availability(IntraJob &j) const {
+    const int comp = j.comp, ch = comp ? 1 : 0;
+    const bool isp = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0, ver = (j.flags & IJ_ISP_VER) != 0;
+    uint64_t lo;
+    uint32_t hi;
+    if (!isp) {
+      fill_mask(ch, j.seq, j.x, j.y, j.w, j.h, 2 * j.w, 2 * j.h, lo, hi);
+    } else {
+      const int fTop = ver ? 2 * j.cw : j.cw + j.w, fLeft = ver ? j.ch + j.h : 2 * j.ch;
+      fill_mask(0, j.seq, j.cx, j.cy, j.cw, j.ch, fTop, fLeft, lo, hi);
+    }
+    j.av[0] = (uint32_t)lo;
+    j.av[1] = (uint32_t)(lo >> 32);
+    j.av[2] = hi;
+    j.av[3] = 0;
+    if (isp)
+      for (int k = 1; k < j.isp_k && k < 4; k++) {
+        const bool a = ver ? av(0, j.x + k * j.w, j.y - 1, j.seq) : av(0, j.x - 1, j.y + k * j.h, j.seq);
+        if (a) j.av[2] |= 1u << (8 + k);
+      }
+    if (comp > 0 && j.mode >= 67 && !(j.flags & IJ_BDPCM)) {
+      const bool dual = (j.flags & IJ_DUAL) != 0;
+      const uint32_t lr = dual ? nb_bits(1, j.seq, j.x, j.y, j.w, j.h, 2) : nb_bits(0, j.seq, 2 * j.x, 2 * j.y, 2 * j.w, 2 * j.h, 4);
+      const uint32_t lm = nb_bits(1, j.seq, j.x, j.y, j.w, j.h, 2);
+      j.av[2] |= lr << 16;
+      j.av[3] = lm;
+    }
+  }
+
   void run() {
     const size_t nu = (size_t)W4 * H4;
     for (int k = 0; k < 2; k++) { out.order[k].assign(nu, 1 << 30); level[k].assign(nu, 0); }
@@ -276,6 +344,7 @@ struct Planner {
       out.dep_start[i + 1] = (int32_t)out.deps.size();
     }
     for (int L = 1; L <= maxLev + 1; L++) out.level_start[L] = std::max(out.level_start[L], out.level_start[L - 1]);
+    for (IntraJob &j : out.jobs) resolve_availability(j);
   }
 };
 
