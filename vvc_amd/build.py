@@ -61,6 +61,19 @@ def build_oracle():
     return out
 
 
+def build_reference(jobs=8):
+    """oracle/_ref: the reference (VTM 7.3) built from /root/reference's own sources by oracle/ref.mk —
+    DecoderApp (CPU baseline), EncoderApp (test streams), vtm_capture (golden fixtures). Test
+    infrastructure; skipped where the reference is absent (the GPU box uses the prebuilt files)."""
+    if not os.path.isdir("/root/reference/source"):
+        return None
+    r = subprocess.run(["make", "-f", os.path.join(ROOT, "oracle", "ref.mk"), "-j%d" % jobs, "all"],
+                       cwd=ROOT, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("reference build failed:\n%s%s" % (r.stdout[-4000:], r.stderr[-4000:]))
+    return os.path.join(ROOT, "oracle", "_ref")
+
+
 if __name__ == "__main__":
     print(build_lib())
     print(build_oracle())
