@@ -7,7 +7,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROF_LIB = os.path.join(ROOT, "build", "prof", "libvvcr_prof.so")
+PROF_LIB = os.environ.get("VVCR_PROF_LIB") or os.path.join(ROOT, "build", "prof", "libvvcr_prof.so")
 
 
 def build(extra=()):

@@ -72,10 +72,9 @@ struct Prepared {
   DevVec<AffJob> aff_jobs;
   DevVec<ReconTile> tiles;
   DevVec<IntraJob> ijobs;
-  DevVec<int32_t> idep_start, ideps, istate;
+  DevVec<int32_t> idep_start, ideps, istate, ictu_list, ictu_start;
   DevVec<IntraParams> iparams;       // device copy of the intra kernel's parameters
-  int n_ijobs = 0;
-  std::vector<int32_t> level_start;
+  int n_ijobs = 0, n_ictu = 0;
   DevVec<DbkSeg> dbk;
   int dbk_counts[4] = {0, 0, 0, 0};
   DevVec<int32_t> sao;
@@ -231,9 +230,12 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
     P.bd = ctx->sp.bit_depth;
     P.ctu = 1 << ctx->sp.ctu_log2;
+    P.ctu_log2 = ctx->sp.ctu_log2;
     r.iparams.upload(&P, 1);
     r.n_ijobs = (int)ip.jobs.size();
-    r.level_start = ip.level_start;
+    r.ictu_list.upload(ip.ctu_list);
+    r.ictu_start.upload(ip.ctu_start);
+    r.n_ictu = (int)ip.ctu_list.size();
     r.n_tiles = (int)ip.inter_tiles.size();
     double b = 0;
     for (const ReconTile &t : ip.inter_tiles) b += (double)t.w * t.h * 1.5 * 2 * 3;   // pred + resi in, reco out
@@ -324,6 +326,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
     P.bd = ctx->sp.bit_depth;
     P.ctu = 1 << ctx->sp.ctu_log2;
+    P.ctu_log2 = ctx->sp.ctu_log2;
     {
       KernelTimer t(r, K_RECON, s);
       launch_recon_inter(P, r.tiles.p, r.n_tiles, s);
@@ -332,7 +335,8 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     }
     {
       KernelTimer t(r, K_INTRA, s);
-      launch_intra(r.iparams.p, r.ijobs.p, r.n_ijobs, r.idep_start.p, r.ideps.p, r.istate.p, ctx->d_err, ctx->n_cu, s);
+      launch_intra(r.iparams.p, r.ijobs.p, r.n_ijobs, r.ictu_list.p, r.ictu_start.p, r.n_ictu, r.idep_start.p, r.ideps.p,
+                   r.istate.p, ctx->d_err, ctx->n_cu, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_INTRA] = r.n_ijobs ? 1 : 0;
     }

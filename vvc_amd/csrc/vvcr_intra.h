@@ -20,7 +20,10 @@ enum : uint8_t {
   IJ_ISP_HOR = 1 << 4,    // intra sub-partitions, horizontal split
   IJ_ISP_VER = 1 << 5,    // intra sub-partitions, vertical split
   IJ_DUAL = 1 << 6,       // CU of a separate chroma tree (CCLM availability on the chroma map)
+  IJ_PUBLISH = 1 << 7,    // a step of another CTU reads this one: drain its stores, raise its global flag
 };
+
+constexpr int kIntraMaxStepsPerCtu = 4096;   // LDS done-flag bytes of k_intra
 
 // One reconstruction step: predict a region, add the residual plane, clip, store into the picture.
 struct IntraJob {
@@ -54,13 +57,14 @@ struct ReconTile {
 
 struct IntraPlan {
   std::vector<ReconTile> inter_tiles;
-  std::vector<IntraJob> jobs;        // sorted by level
-  std::vector<int32_t> level_start;  // jobs of level L: [level_start[L], level_start[L+1])
-  std::vector<int32_t> dep_start;    // step i waits for steps deps[dep_start[i] .. dep_start[i+1]) (all < i)
-  std::vector<int32_t> deps;
+  std::vector<IntraJob> jobs;        // grouped by CTU (raster order), by level inside a CTU
+  std::vector<int32_t> ctu_list;     // raster index of every CTU that has steps
+  std::vector<int32_t> ctu_start;    // steps of ctu_list[c]: [ctu_start[c], ctu_start[c+1])
+  std::vector<int32_t> dep_start;    // step i waits for deps[dep_start[i] .. dep_start[i+1]):
+  std::vector<int32_t> deps;         //   v >= 0: step ctu_start[c] + v of its own CTU; v < 0: global step ~v
   std::vector<int32_t> order[2];     // per 4x4 luma unit / 2x2 chroma unit: seq of the step that decodes it
   void clear() {
-    inter_tiles.clear(); jobs.clear(); level_start.clear(); dep_start.clear(); deps.clear(); order[0].clear(); order[1].clear();
+    inter_tiles.clear(); jobs.clear(); ctu_list.clear(); ctu_start.clear(); dep_start.clear(); deps.clear(); order[0].clear(); order[1].clear();
   }
 };
 
@@ -68,11 +72,13 @@ struct IntraParams {
   DPlane reco[3];                    // picture being reconstructed (in place)
   DPlane pred[3];                    // inter prediction planes (CIIP)
   DPlane resi[3];                    // residual planes
-  int32_t bd, ctu;
+  int32_t bd, ctu, ctu_log2;
 };
 
 void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out);
 void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s);
-// all steps of a picture in one persistent launch; state: 16 + n int32 (reset here); *err set on a wait timeout
-void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *dep_start, const int32_t *deps,
-                  int32_t *state, int32_t *err, int n_cu, hipStream_t s);
+// all steps of a picture in one persistent launch, one CTU per workgroup at a time; state: 16 + n int32
+// (reset here); *err set on a wait timeout
+void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *ctu_list, const int32_t *ctu_start,
+                  int nctu, const int32_t *dep_start, const int32_t *deps, int32_t *state, int32_t *err, int n_cu,
+                  hipStream_t s);

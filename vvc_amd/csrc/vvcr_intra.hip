@@ -24,14 +24,16 @@ extern "C" int vvcr_intra_prof_read(unsigned long long *dst, int max) {
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_iprof_n), &z, sizeof(z));
   return (int)n;
 }
-__shared__ unsigned long long tstamp[10];
-#define IPROF(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); if (threadIdx.x == 0) tstamp[i] = __builtin_readcyclecounter(); } while (0)
-#define IPROF_RT(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); rstamp[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// phase stamps of run_step (shader cycles), kept in registers: ps[i] after waiting for the phase's memory
+#define IPROF(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); ps[i] = __builtin_readcyclecounter(); } while (0)
 #else
 #define IPROF(i) do { } while (0)
-#define IPROF_RT(i) do { } while (0)
 #endif
 
+#ifdef VVCR_DIAG_DUMP
+__device__ int32_t g_dbg[1024];
+extern "C" int vvcr_diag_dump(int32_t *dst) { return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_dbg), sizeof(g_dbg)); }
+#endif
 namespace {
 
 __constant__ int8_t i_chroma[32][4] = VVCR_CHROMA_FILTER_TABLE;
@@ -53,7 +55,16 @@ struct Ctx {
   int seq;
 };
 
-__device__ __forceinline__ int pel(const DPlane &D, int x, int y) { return D.p[(size_t)y * D.stride + x]; }
+// Plane pointers reach the kernels through LDS / structs as generic pointers; loads and stores through
+// them would be FLAT instructions, which count on lgkmcnt too, so every LDS wait would also wait for
+// them. Accesses go through these global-address-space casts instead.
+template <class T> __device__ __forceinline__ const __attribute__((address_space(1))) T *gp(const T *p) {
+  return (const __attribute__((address_space(1))) T *)p;
+}
+template <class T> __device__ __forceinline__ __attribute__((address_space(1))) T *gpw(T *p) {
+  return (__attribute__((address_space(1))) T *)p;
+}
+__device__ __forceinline__ int pel(const DPlane &D, int x, int y) { return *gp(&D.p[(size_t)y * D.stride + x]); }
 
 // Reconstructed samples are handed between steps of one launch (k_intra is persistent): every store of
 // them is a 4-byte sc1 store and every load of them a 4-byte sc1 load (bypasses the CU's L1), the
@@ -83,6 +94,117 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
+// ------------------------------------------------------------------------------------------------
+// CTU-resident reconstruction. A workgroup of NW waves owns one CTU at a time: the CTU's samples (luma
+// and both chroma planes) live in an LDS tile, each wave runs one step at a time, and steps of the
+// same CTU hand over through LDS (a done byte per step). Only samples outside the CTU — the left /
+// above / above-right neighbours' borders — are read from HBM, through the sc1 hand-off below, and
+// only steps that such a read depends on (IJ_PUBLISH) drain their HBM stores and raise a global flag.
+// ------------------------------------------------------------------------------------------------
+#ifndef VVCR_DIAG_NW
+constexpr int NW = 4; 
+#else
+constexpr int NW = VVCR_DIAG_NW;
+#endif
+//                       // waves per workgroup
+constexpr int TPL = 130, TPC = 66;           // LDS tile pitches (odd dword count: column walks hit distinct banks)
+constexpr int TILE_Y = 0, TILE_CB = 128 * TPL, TILE_CR = TILE_CB + 64 * TPC, TILE_N = TILE_CR + 64 * TPC;
+
+struct WaveScratch {
+  int16_t refU[2][RB];          // unfiltered top / left (index 0 = corner)
+  int16_t refF[2][RB];          // filtered
+  int16_t mainA[EXT + RB + 64]; // angular main reference (with negative indices)
+  int16_t sideA[EXT + RB + 64];
+  int32_t aux[64 * 64 / 4];     // MIP reduced pred / CCLM down-sampled luma
+  int16_t tmpl[2][132];         // CCLM down-sampled luma: top row / left column
+  int32_t lmp[4];
+  int32_t red[8];               // MIP reduced boundary
+  int16_t pred[64 * 64];
+  int16_t resL[64 * 64];        // residual of the step, prefetched at entry
+  int16_t ispPrev[64];          // ISP: last row / column of the previous region
+};
+
+__shared__ int16_t s_tile[TILE_N];
+__shared__ WaveScratch s_ws[NW];
+__shared__ uint8_t s_ldone[kIntraMaxStepsPerCtu];
+
+// Wave-level ordering of LDS traffic between the lanes of one wave (the steps of one workgroup run on
+// different waves, so the step body never uses a workgroup barrier). A wavefront-scope fence is not
+// enough: it is dropped before instruction scheduling, which may then hoist a lane's LDS read above
+// another lane's write of the same word when the two do not alias within one thread. An asm statement
+// with a memory clobber is a scheduling barrier for memory operations; the LDS itself executes one
+// wave's DS instructions in order, so no wait is needed.
+__device__ __forceinline__ void wsync() {
+#ifdef VVCR_DIAG_WSYNC_BARRIER
+  __syncthreads();
+#else
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
+
+// Area of the current CTU in luma samples (chroma: halved); scalars only, so that nothing of it is
+// indexed dynamically (a private array would be promoted to per-lane LDS or scratch).
+struct TileGeo {
+  int x0, y0, w, h;
+  __device__ __forceinline__ int cx0(int comp) const { return comp ? x0 >> 1 : x0; }
+  __device__ __forceinline__ int cy0(int comp) const { return comp ? y0 >> 1 : y0; }
+  __device__ __forceinline__ int cw(int comp) const { return comp ? w >> 1 : w; }
+  __device__ __forceinline__ int ch(int comp) const { return comp ? h >> 1 : h; }
+};
+__device__ __forceinline__ int tile_base(int comp) { return comp == 0 ? TILE_Y : (comp == 1 ? TILE_CB : TILE_CR); }
+__device__ __forceinline__ int tile_pitch(int comp) { return comp ? TPC : TPL; }
+
+// Reconstructed samples of one component: inside the current CTU from the LDS tile, elsewhere from HBM.
+struct Src {
+  const int16_t *g;
+  int gs, base, ts, x0, y0, w, h;
+  __device__ __forceinline__ bool inside(int x, int y) const {
+    return (unsigned)(x - x0) < (unsigned)w && (unsigned)(y - y0) < (unsigned)h;
+  }
+  __device__ __forceinline__ uint32_t pair(int x, int y) const {   // x even
+    if (inside(x, y)) return *(const uint32_t *)&s_tile[base + (y - y0) * ts + x - x0];
+    return ld_sc1(g + (size_t)y * gs + x);
+  }  __device__ __forceinline__ int pel(int x, int y) const {
+    const uint32_t v = pair(x & ~1, y);
+    return (int)(int16_t)((x & 1) ? (v >> 16) : (v & 0xffff));
+  }
+};
+__device__ __forceinline__ Src src_of(const IntraParams &P, int comp, const TileGeo &G) {
+  Src s;
+  s.g = P.reco[comp].p; s.gs = P.reco[comp].stride;
+  s.base = tile_base(comp); s.ts = tile_pitch(comp);
+  s.x0 = G.cx0(comp); s.y0 = G.cy0(comp); s.w = G.cw(comp); s.h = G.ch(comp);
+  return s;
+}
+
+// Batched sample reads: every HBM load of the batch is issued before the first wait. (Reading through
+// Src::pel one sample at a time makes each LDS read wait for the previous sample's HBM load, because
+// both results would share a destination register.) Samples with need[k] false read nothing (0).
+template <int N>
+__device__ __forceinline__ void gather(const Src &s, const int (&x)[N], const int (&y)[N], const bool (&need)[N], int (&out)[N]) {
+  bool in[N];
+  uint32_t gv[N], lv[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) in[k] = s.inside(x[k], y[k]);
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+#ifdef VVCR_DIAG_NO_GLOBAL_REFS
+    gv[k] = 0u;
+#else
+    gv[k] = (need[k] && !in[k]) ? ld_sc1(s.g + (size_t)y[k] * s.gs + (x[k] & ~1)) : 0u;
+#endif
+  }
+#pragma unroll
+  for (int k = 0; k < N; k++)
+    lv[k] = (need[k] && in[k]) ? *(const uint32_t *)&s_tile[s.base + (y[k] - s.y0) * s.ts + ((x[k] & ~1) - s.x0)] : 0u;
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    const uint32_t v = in[k] ? lv[k] : gv[k];
+    out[k] = (int)(int16_t)((x[k] & 1) ? (v >> 16) : (v & 0xffff));
+  }
+}
+
 // xFillReferenceSamples for area (fx, fy, fw, fh) of component plane D; top[0..predSize+mrl],
 // left[0..predHSize+mrl]; index 0 = corner line.
 //
@@ -92,8 +214,10 @@ __device__ __forceinline__ int wave_sum(int v) {
 // available one get its first sample, and with no unit available every sample is 1 << (bd - 1). The
 // availability mask (lo: units 0..63, hi: unit 64) comes resolved from the host, so every lane handles
 // its own samples: available ones are copied, then missing ones read their source from the lines.
-__device__ void fill_refs(const DPlane &D, int ch, int fx, int fy, int predSize, int predHSize, int mrl, int bd,
-                          uint64_t lo, bool hi, int16_t *top, int16_t *left, int lane) {
+__device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int ch, int fx, int fy, int predSize, int predHSize,
+                                          int mrl, int bd, uint64_t lo, bool hi, int16_t *top, int16_t *left, int lane,
+                                          unsigned long long *ps) {
+  (void)ps;
   const int lu = ch ? 1 : 2;   // log2 of the unit size
   const int totalLeft = (predHSize + (1 << lu) - 1) >> lu;
   const int ox = fx - 1 - mrl, oy = fy - 1 - mrl;   // corner sample of the reference line
@@ -102,7 +226,7 @@ __device__ void fill_refs(const DPlane &D, int ch, int fx, int fy, int predSize,
     const int16_t dc = (int16_t)(1 << (bd - 1));
     for (int j = lane; j <= nT; j += 64) top[j] = dc;
     for (int i = lane; i <= nL; i += 64) left[i] = dc;
-    __syncthreads();
+    wsync();
     return;
   }
   // unit of top sample j / left sample i
@@ -111,14 +235,22 @@ __device__ void fill_refs(const DPlane &D, int ch, int fx, int fy, int predSize,
   auto unitAv = [&](int u) { return u < 64 ? ((lo >> u) & 1) != 0 : hi; };
   int16_t tv[3], lv[3];
   {
-    const int cy = max(oy, 0), cx = max(ox, 0);   // missing samples are loaded from clamped positions, never used
+    // only available samples are loaded: a sample outside the CTU costs an HBM round trip (sc1), and
+    // the unavailable ones (above-right / below-left beyond the decoded area) are mostly outside it
+    const int cy = max(oy, 0), cx = max(ox, 0);
+    int gx[6], gy[6], gvv[6];
+    bool need[6];
 #pragma unroll
     for (int r = 0; r < 3; r++) {
-      tv[r] = (int16_t)pel_rc(D, min(max(ox + min(lane + 64 * r, nT), 0), D.w - 1), cy);
-      lv[r] = (int16_t)pel_rc(D, cx, min(max(oy + min(lane + 64 * r, nL), 0), D.h - 1));
+      const int j = lane + 64 * r;
+      gx[r] = min(max(ox + j, 0), D.w - 1); gy[r] = cy; need[r] = j <= nT && unitAv(unitT(j));
+      gx[3 + r] = cx; gy[3 + r] = min(max(oy + j, 0), D.h - 1); need[3 + r] = j <= nL && unitAv(unitL(j));
     }
+    IPROF(7);
+    gather(src, gx, gy, need, gvv);
+#pragma unroll
+    for (int r = 0; r < 3; r++) { tv[r] = (int16_t)gvv[r]; lv[r] = (int16_t)gvv[3 + r]; }
   }
-  IPROF(3);
   bool missing = false;
 #pragma unroll
   for (int r = 0; r < 3; r++) {
@@ -126,8 +258,8 @@ __device__ void fill_refs(const DPlane &D, int ch, int fx, int fy, int predSize,
     if (j <= nT) { if (unitAv(unitT(j))) top[j] = tv[r]; else missing = true; }
     if (j <= nL) { if (unitAv(unitL(j))) left[j] = lv[r]; else missing = true; }
   }
-  if (__ballot(missing) == 0) { __syncthreads(); return; }
-  __syncthreads();
+  if (__ballot(missing) == 0) { wsync(); return; }
+  wsync();
   // missing units: the scan-order last sample of the nearest earlier available unit, else the first
   // sample of the first available unit (both are copied samples)
   const int firstAv = lo ? __builtin_ctzll(lo) : 64;
@@ -151,14 +283,14 @@ __device__ void fill_refs(const DPlane &D, int ch, int fx, int fy, int predSize,
     sv[r] = (j <= nT && !unitAv(unitT(j))) ? source(unitT(j)) : 0;
     sv[3 + r] = (j <= nL && !unitAv(unitL(j))) ? source(unitL(j)) : 0;
   }
-  __syncthreads();
+  wsync();
 #pragma unroll
   for (int r = 0; r < 3; r++) {
     const int j = lane + 64 * r;
     if (j <= nT && !unitAv(unitT(j))) top[j] = sv[r];
     if (j <= nL && !unitAv(unitL(j))) left[j] = sv[3 + r];
   }
-  __syncthreads();
+  wsync();
 }
 
 // IntraPrediction::getWideAngle (:184)
@@ -186,57 +318,35 @@ __device__ __forceinline__ NbAvail nb_decode(uint32_t b) {
   return r;
 }
 
-// Persistent: one workgroup (one wave) per CU takes steps from an atomic counter in topological order
-// and waits, per step, for the steps it reads from (dependency lists built by plan_intra).
-// state[0] = step counter, state[16 + i] = step i done; *err set if a wait times out.
-__global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg, const IntraJob *__restrict__ jobs, int njobs,
-                                              const int32_t *__restrict__ dep_start, const int32_t *__restrict__ deps,
-                                              int32_t *state, int32_t *err) {
-  __shared__ int16_t refU[2][RB];          // unfiltered top / left (index 0 = corner)
-  __shared__ int16_t refF[2][RB];          // filtered
-  __shared__ int16_t mainA[EXT + RB + 64];  // angular main reference (with negative indices)
-  __shared__ int16_t sideA[EXT + RB + 64];
-  __shared__ int32_t aux[64 * 64 / 4];     // MIP reduced pred / CCLM template scratch
-  __shared__ int16_t tmpl[2][132];         // CCLM down-sampled luma: top row / left column
-  __shared__ int32_t lmp[3];
-  __shared__ int16_t pred[64 * 64];
-  __shared__ int16_t resL[64 * 64];        // residual of the step, prefetched at entry
-  __shared__ int16_t ispPrev[64];          // ISP: last row / column of the previous region
-  __shared__ int s_job;
-  const int lane = threadIdx.x;
-  int32_t *done = state + 16;
-  for (;;) {
-  // next step in topological order; it waits only for steps taken before it, so every wave makes
-  // progress and every wave leaves once the list is exhausted
-  if (lane == 0) s_job = atomicAdd(&state[0], 1);
-  __syncthreads();
-  const int j = s_job;
-  __syncthreads();
-  if (j >= njobs) break;
-#ifdef VVCR_INTRA_PROF
-  unsigned long long rstamp[3];
+// bounded spin on a flag; sets *err and gives up after ~seconds (never expected)
+__device__ __forceinline__ void wait_global(const int32_t *f, int32_t *err) {
+  for (int it = 1; __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0; it++) {
+#ifdef VVCR_DIAG_SLEEP
+    __builtin_amdgcn_s_sleep(VVCR_DIAG_SLEEP);
+#else
+    __builtin_amdgcn_s_sleep(2);
 #endif
-  IPROF_RT(0);
-  for (int k = dep_start[j] + lane; k < dep_start[j + 1]; k += 64) {
-    const int32_t *f = done + deps[k];
-    for (int it = 1; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; it++) {
-      __builtin_amdgcn_s_sleep(1);
-      // never expected: report instead of hanging, and let every other wait end as well
-      if ((it & 1023) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-      if (it > (1 << 23)) { atomicOr(err, 1); break; }
-    }
+    if ((it & 1023) == 0 && __builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
+    if (it > (1 << 22)) { atomicOr(err, 1); break; }
   }
-  __syncthreads();
-  IPROF_RT(1);
+}
+__device__ __forceinline__ void wait_local(int v, int32_t *err) {
+  for (int it = 1; __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_ldone[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0; it++) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((it & 1023) == 0 && __builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
+    if (it > (1 << 24)) { atomicOr(err, 1); break; }
+  }
+}
+
+// One reconstruction step, run by one wave.
+__device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J, const TileGeo &G, WaveScratch &S,
+                                         const int32_t *dep_start, const int32_t *deps, int gj, int32_t *done,
+                                         int32_t *err, int lane, unsigned long long &t_ready, unsigned long long *ps) {
   IPROF(0);
-  // parameters are re-read per step (scalar cache) rather than held in registers across the loop
-  const IntraParams *Pq = Pg;
-  asm volatile("" : "+s"(Pq));
-  const IntraParams &P = *Pq;
-  const IntraJob J = jobs[j];
   const int comp = J.comp, ch = comp ? 1 : 0;
   const int bd = P.bd, maxv = (1 << bd) - 1;
   const DPlane &D = P.reco[comp];
+  const Src SD = src_of(P, comp, G);
   const int w = J.w, h = J.h;
   const bool isp = (J.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0;
   const bool ispVer = (J.flags & IJ_ISP_VER) != 0;
@@ -246,51 +356,71 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
   const bool lmMode = comp > 0 && J.mode >= LM && !bdpcm;
   const int mrl = comp ? 0 : J.mrl;
   const int n = w * h;
+  const int lw_ = ilog2(w);   // block sizes are powers of two: shifts instead of divisions
   const int nreg = isp ? J.isp_k : 1;
   const uint64_t avlo = (uint64_t)J.av[0] | (uint64_t)J.av[1] << 32;
   const bool avhi = (J.av[2] & 1) != 0;
-  IPROF(1);
   // residual rectangle: the block, or the whole CU for ISP
   const int rx = isp ? J.cx : J.x, ry = isp ? J.cy : J.y, rw = isp ? J.cw : w, rh = isp ? J.ch : h;
   // The residual does not depend on earlier steps: the first 2048 samples are loaded into registers
-  // here, so that their loads are in flight together with the reference-fill loads, and stored to LDS
-  // after the fill; larger blocks load the rest afterwards.
+  // before the dependency wait, and stored to LDS after the reference fill; larger blocks load the
+  // rest afterwards.
   const DPlane &R = P.resi[comp];
   const int rn = rw * rh;
+  const int lrw = ilog2(rw);
   const bool rvec = ((rw | rx) & 3) == 0;   // plane strides are multiples of 64 samples
-  uint2 rv[8];
+  uint64_t rv[8];
   int16_t rs[8];
   if (rvec) {
 #pragma unroll
     for (int b = 0; b < 8; b++) {
       const int k = min((lane + 64 * b) * 4, rn - 4);
-      const int yy = k / rw, xx = k - yy * rw;
-      rv[b] = *(const uint2 *)&R.p[(size_t)(ry + yy) * R.stride + rx + xx];
+      const int yy = k >> lrw, xx = k & (rw - 1);
+      rv[b] = *gp((const uint64_t *)&R.p[(size_t)(ry + yy) * R.stride + rx + xx]);
     }
   } else {
 #pragma unroll
     for (int b = 0; b < 8; b++) {
       const int k = min(lane + 64 * b, rn - 1);
-      const int yy = k / rw, xx = k - yy * rw;
-      rs[b] = R.p[(size_t)(ry + yy) * R.stride + rx + xx];
+      const int yy = k >> lrw, xx = k & (rw - 1);
+      rs[b] = *gp(&R.p[(size_t)(ry + yy) * R.stride + rx + xx]);
     }
   }
-  IPROF(2);
+  // Wait for the steps this one reads from, newest dependency first (the likeliest to be still
+  // running); same-CTU steps through LDS, steps of other CTUs through their global flag. Every lane
+  // runs the (uniform) loop and polls the same word — one request per poll — so that no lane-divergent
+  // region precedes the step body: the step body's wave syncs do not force reconvergence, and code
+  // sunk into a lane-0-only region would run after the other lanes' reads of its results.
+  {
+    const int k0 = __builtin_amdgcn_readfirstlane(dep_start[gj]), k1 = __builtin_amdgcn_readfirstlane(dep_start[gj + 1]);
+    for (int k = k1 - 1; k >= k0; k--) {
+      const int v = __builtin_amdgcn_readfirstlane(deps[k]);
+      if (v >= 0) wait_local(v, err);
+      else wait_global(done + ~v, err);
+    }
+  }
+  wsync();
+#ifdef VVCR_INTRA_PROF
+  t_ready = __builtin_amdgcn_s_memrealtime();
+#else
+  (void)t_ready; (void)ps;
+#endif
+  IPROF(1);
   auto store_resid = [&]() {
     if (rvec) {
 #pragma unroll
       for (int b = 0; b < 8; b++)
-        if ((lane + 64 * b) * 4 < rn) *(uint2 *)&resL[(lane + 64 * b) * 4] = rv[b];
+        if ((lane + 64 * b) * 4 < rn) *(uint64_t *)&S.resL[(lane + 64 * b) * 4] = rv[b];
     } else {
 #pragma unroll
       for (int b = 0; b < 8; b++)
-        if (lane + 64 * b < rn) resL[lane + 64 * b] = rs[b];
+        if (lane + 64 * b < rn) S.resL[lane + 64 * b] = rs[b];
     }
     for (int k = (lane + 512) * (rvec ? 4 : 1); k < rn; k += 64 * (rvec ? 4 : 1)) {
-      const int yy = k / rw, xx = k - yy * rw;
+      const int yy = k >> lrw, xx = k & (rw - 1);
       const int16_t *src = &R.p[(size_t)(ry + yy) * R.stride + rx + xx];
-      if (rvec) *(uint2 *)&resL[k] = *(const uint2 *)src;
-      else resL[k] = *src;
+      if (rvec) *(uint64_t *)&S.resL[k] = *gp((const uint64_t *)src);
+      else S.resL[k] = *gp(src);
     }
   };
 
@@ -305,40 +435,40 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
 
   // ---- reference samples
   {
-    int16_t *top = refU[0], *left = refU[1];
+    int16_t *top = S.refU[0], *left = S.refU[1];
     if (!isp) {
-      fill_refs(D, ch, x0, y0, topLen, leftLen, mrl, bd, avlo, avhi, top, left, lane);
+      fill_refs(SD, D, ch, x0, y0, topLen, leftLen, mrl, bd, avlo, avhi, top, left, lane, ps);
     } else if (kreg == 0) {
       // CU-level fill of the first region (predSize per split direction), kept in refF for the others
       const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
-      fill_refs(D, 0, J.cx, J.cy, fTop, fLeft, 0, bd, avlo, avhi, top, left, lane);
+      fill_refs(SD, D, 0, J.cx, J.cy, fTop, fLeft, 0, bd, avlo, avhi, top, left, lane, ps);
       if (nreg > 1)
-        for (int i = lane; i < RB; i += 64) { refF[0][i] = top[i]; refF[1][i] = left[i]; }
+        for (int i = lane; i < RB; i += 64) { S.refF[0][i] = top[i]; S.refF[1][i] = left[i]; }
     } else {
       // the shift of initIntraPatternChTypeISP (:798-897); ispPrev = last row / column of region k-1
       if (!ispVer) {   // horizontal split: left column shifted, top row from the region above
         const bool la = (J.av[2] >> (8 + kreg)) & 1;
         const int sh = kreg * h;
-        const int16_t src0 = ispPrev[0];
-        for (int i = lane; i <= leftLen; i += 64) left[i] = la ? refF[1][i + sh] : src0;
-        const int16_t corner = la ? refF[1][sh] : src0;
-        const int16_t last = ispPrev[w - 1];
-        for (int i = lane; i <= topLen; i += 64) top[i] = i == 0 ? corner : (i <= w ? ispPrev[i - 1] : last);
+        const int16_t src0 = S.ispPrev[0];
+        for (int i = lane; i <= leftLen; i += 64) left[i] = la ? S.refF[1][i + sh] : src0;
+        const int16_t corner = la ? S.refF[1][sh] : src0;
+        const int16_t last = S.ispPrev[w - 1];
+        for (int i = lane; i <= topLen; i += 64) top[i] = i == 0 ? corner : (i <= w ? S.ispPrev[i - 1] : last);
       } else {         // vertical split: top row shifted, left column from the region to the left
         const bool aa = (J.av[2] >> (8 + kreg)) & 1;
         const int sh = kreg * w;
-        const int16_t src0 = ispPrev[0];
-        for (int i = lane; i <= topLen; i += 64) top[i] = aa ? refF[0][i + sh] : src0;
-        const int16_t corner = aa ? refF[0][sh] : src0;
-        const int16_t last = ispPrev[h - 1];
-        for (int i = lane; i <= leftLen; i += 64) left[i] = i == 0 ? corner : (i <= h ? ispPrev[i - 1] : last);
+        const int16_t src0 = S.ispPrev[0];
+        for (int i = lane; i <= topLen; i += 64) top[i] = aa ? S.refF[0][i + sh] : src0;
+        const int16_t corner = aa ? S.refF[0][sh] : src0;
+        const int16_t last = S.ispPrev[h - 1];
+        for (int i = lane; i <= leftLen; i += 64) left[i] = i == 0 ? corner : (i <= h ? S.ispPrev[i - 1] : last);
       }
     }
   }
-  IPROF(4);
-  if (kreg == 0) store_resid();   // read after the barriers that follow
-  __syncthreads();
-  IPROF(5);
+  if (kreg == 0) IPROF(2);
+  if (kreg == 0) store_resid();   // read after the wave syncs that follow
+  wsync();
+  if (kreg == 0) IPROF(3);
 
   // ---- prediction parameters (initPredIntraParams)
   const int dirMode = ciip ? PLANAR : (int)J.mode;
@@ -378,27 +508,37 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
     const int pS = topLen, pH = leftLen;
     for (int i = lane; i <= pS; i += 64) {
       int v;
-      if (i == 0) v = (refU[0][0] + refU[0][1] + refU[1][0] + refU[1][1] + 2) >> 2;
-      else if (i == pS) v = refU[0][pS];
-      else v = (refU[0][i - 1] + 2 * refU[0][i] + refU[0][i + 1] + 2) >> 2;
-      refF[0][i] = (int16_t)v;
+      if (i == 0) v = (S.refU[0][0] + S.refU[0][1] + S.refU[1][0] + S.refU[1][1] + 2) >> 2;
+      else if (i == pS) v = S.refU[0][pS];
+      else v = (S.refU[0][i - 1] + 2 * S.refU[0][i] + S.refU[0][i + 1] + 2) >> 2;
+      S.refF[0][i] = (int16_t)v;
     }
     for (int i = lane; i <= pH; i += 64) {
       int v;
-      if (i == 0) v = (refU[0][0] + refU[0][1] + refU[1][0] + refU[1][1] + 2) >> 2;
-      else if (i == pH) v = refU[1][pH];
-      else v = (refU[1][i - 1] + 2 * refU[1][i] + refU[1][i + 1] + 2) >> 2;
-      refF[1][i] = (int16_t)v;
+      if (i == 0) v = (S.refU[0][0] + S.refU[0][1] + S.refU[1][0] + S.refU[1][1] + 2) >> 2;
+      else if (i == pH) v = S.refU[1][pH];
+      else v = (S.refU[1][i - 1] + 2 * S.refU[1][i] + S.refU[1][i + 1] + 2) >> 2;
+      S.refF[1][i] = (int16_t)v;
     }
-    __syncthreads();
+    wsync();
   }
-  IPROF(6);
-  const int16_t *top = refFilter ? refF[0] : refU[0];
-  const int16_t *left = refFilter ? refF[1] : refU[1];
-#define predv(q) pred[lane + 64 * (q)]
+  if (kreg == 0) IPROF(4);
+#ifdef VVCR_DIAG_DUMP
+  if (gj == 0 && kreg == 0) {
+    if (lane < 16) { g_dbg[lane] = S.refU[0][lane]; g_dbg[16 + lane] = S.refU[1][lane]; g_dbg[32 + lane] = S.refF[0][lane]; }
+    for (int i = lane; i < RB; i += 64) { g_dbg[256 + i] = S.refU[0][i]; g_dbg[512 + i] = S.refF[0][i]; g_dbg[768 + i] = S.refF[1][i]; }
+    if (lane == 0) { g_dbg[56] = topLen; g_dbg[57] = leftLen; }
+    if (lane == 0) { g_dbg[48] = (int)J.av[0]; g_dbg[49] = (int)J.av[1]; g_dbg[50] = (int)J.av[2]; g_dbg[51] = J.mode;
+                     g_dbg[52] = refFilter; g_dbg[53] = predMode; g_dbg[54] = applyPDPC; g_dbg[55] = J.flags; }
+  }
+#endif
+  const int16_t *top = refFilter ? S.refF[0] : S.refU[0];
+  const int16_t *left = refFilter ? S.refF[1] : S.refU[1];
+#define predv(q) S.pred[lane + 64 * (q)]
 
   if (lmMode) {
     // ---------------- CCLM (xGetLumaRecPixels + xGetLMParameters)
+    const Src SY = src_of(P, 0, G);
     const DPlane &Y = P.reco[0];
     const int lx = 2 * x0, ly = 2 * y0;
     const bool dual = (J.flags & IJ_DUAL) != 0;
@@ -411,46 +551,53 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
     const bool firstRowCtu = (ly & (P.ctu - 1)) == 0;
     // luma loads in batches (templates + 256 down-sampled samples first): every load of a batch is
     // issued before the first wait
-    auto Yc = [&](int x, int y) { return pel_rc(Y, clampi(x, 0, Y.w - 1), clampi(y, 0, Y.h - 1)); };
     const int nT = lr.above ? w + addAR : 0, nLt = lr.left ? h + addBL : 0;
-    int ta[6], tl[6];
+    int ta[6] = {0, 0, 0, 0, 0, 0}, tl[6] = {0, 0, 0, 0, 0, 0};
+    // template rows / columns only where they are used (outside the CTU they cost an HBM round trip)
     {
-      const int i = min(lane, max(nT - 1, 0));
-      const int c = lx + 2 * i;
-      const int cl = (i == 0 && !lr.left) ? c : c - 1;
-      ta[0] = Yc(cl, ly - 2); ta[1] = Yc(c, ly - 2); ta[2] = Yc(c + 1, ly - 2);
-      ta[3] = Yc(cl, ly - 1); ta[4] = Yc(c, ly - 1); ta[5] = Yc(c + 1, ly - 1);
-      const int r = ly + 2 * min(lane, max(nLt - 1, 0));
-      tl[0] = Yc(lx - 3, r); tl[1] = Yc(lx - 2, r); tl[2] = Yc(lx - 1, r);
-      tl[3] = Yc(lx - 3, r + 1); tl[4] = Yc(lx - 2, r + 1); tl[5] = Yc(lx - 1, r + 1);
+      const int c = lx + 2 * lane;
+      const int cl = (lane == 0 && !lr.left) ? c : c - 1;
+      const int r = ly + 2 * lane;
+      const int Xs[12] = {cl, c, c + 1, cl, c, c + 1, lx - 3, lx - 2, lx - 1, lx - 3, lx - 2, lx - 1};
+      const int Ys[12] = {ly - 2, ly - 2, ly - 2, ly - 1, ly - 1, ly - 1, r, r, r, r + 1, r + 1, r + 1};
+      int cx[12], cy[12], tv12[12];
+      bool need[12];
+#pragma unroll
+      for (int k = 0; k < 12; k++) {
+        cx[k] = clampi(Xs[k], 0, Y.w - 1); cy[k] = clampi(Ys[k], 0, Y.h - 1);
+        need[k] = k < 6 ? (lane < nT && (k >= 3 || !firstRowCtu)) : lane < nLt;
+      }
+      gather(SY, cx, cy, need, tv12);
+#pragma unroll
+      for (int k = 0; k < 6; k++) { ta[k] = tv12[k]; tl[k] = tv12[6 + k]; }
     }
     auto aux_batch = [&](int k0, bool stores_tmpl) {
       int v[4][6];
 #pragma unroll
       for (int b = 0; b < 4; b++) {
         const int k = min(k0 + 64 * b, n - 1);
-        const int yy = k / w, xx = k - yy * w;
+        const int yy = k >> lw_, xx = k & (w - 1);
         const int c = lx + 2 * xx, r = ly + 2 * yy;
         const int cl = (xx == 0 && !lr.left) ? c : c - 1;
-        const uint32_t p0 = pair_rc(Y, c, r), p1 = pair_rc(Y, c, r + 1);   // c even
-        v[b][0] = pel_rc(Y, cl, r); v[b][1] = (int16_t)(p0 & 0xffff); v[b][2] = (int16_t)(p0 >> 16);
-        v[b][3] = pel_rc(Y, cl, r + 1); v[b][4] = (int16_t)(p1 & 0xffff); v[b][5] = (int16_t)(p1 >> 16);
+        const int Xs[6] = {cl, c, c + 1, cl, c, c + 1}, Ys[6] = {r, r, r, r + 1, r + 1, r + 1};
+        const bool need[6] = {true, true, true, true, true, true};
+        gather(SY, Xs, Ys, need, v[b]);
       }
       if (stores_tmpl) {
         if (lane < nT)
-          tmpl[0][lane] = (int16_t)(firstRowCtu ? (ta[4] * 2 + ta[3] + ta[5] + 2) >> 2
+          S.tmpl[0][lane] = (int16_t)(firstRowCtu ? (ta[4] * 2 + ta[3] + ta[5] + 2) >> 2
                                                 : ((ta[1] * 2 + ta[0] + ta[2]) + (ta[4] * 2 + ta[3] + ta[5]) + 4) >> 3);
-        if (lane < nLt) tmpl[1][lane] = (int16_t)(((tl[1] * 2 + tl[0] + tl[2]) + (tl[4] * 2 + tl[3] + tl[5]) + 4) >> 3);
+        if (lane < nLt) S.tmpl[1][lane] = (int16_t)(((tl[1] * 2 + tl[0] + tl[2]) + (tl[4] * 2 + tl[3] + tl[5]) + 4) >> 3);
       }
 #pragma unroll
       for (int b = 0; b < 4; b++)
         if (k0 + 64 * b < n)
-          aux[k0 + 64 * b] = ((v[b][1] * 2 + v[b][2] + v[b][0]) + (v[b][4] * 2 + v[b][5] + v[b][3]) + 4) >> 3;
+          S.aux[k0 + 64 * b] = ((v[b][1] * 2 + v[b][2] + v[b][0]) + (v[b][4] * 2 + v[b][5] + v[b][3]) + 4) >> 3;
     };
     aux_batch(lane, true);
     for (int k0 = lane + 256; k0 < n; k0 += 256) aux_batch(k0, false);
-    __syncthreads();
-    if (lane == 0) {
+    wsync();
+    {   // every lane derives the (uniform) model; no lane-divergent region (see the dependency wait)
       bool aboveAv = lm.above, leftAv = lm.left;
       int avAR = lm.ar, avBL = lm.bl;
       const int avA = aboveAv ? w / 2 : 0, avL = leftAv ? h / 2 : 0;   // units of 2 chroma samples
@@ -474,11 +621,11 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
       int cntT = 0, cntL = 0;
       if (aboveAv) {
         cntT = min(topN, (1 + aboveIs4) << 1);
-        for (int pos = sp0, c = 0; c < cntT; pos += st0, c++) { sl[c] = tmpl[0][pos]; sc[c] = refU[0][1 + pos]; }
+        for (int pos = sp0, c = 0; c < cntT; pos += st0, c++) { sl[c] = S.tmpl[0][pos]; sc[c] = S.refU[0][1 + pos]; }
       }
       if (leftAv) {
         cntL = min(leftN, (1 + leftIs4) << 1);
-        for (int pos = sp1, c = 0; c < cntL; pos += st1, c++) { sl[c + cntT] = tmpl[1][pos]; sc[c + cntT] = refU[1][1 + pos]; }
+        for (int pos = sp1, c = 0; c < cntL; pos += st1, c++) { sl[c + cntT] = S.tmpl[1][pos]; sc[c + cntT] = S.refU[1][1 + pos]; }
       }
       if (cntT + cntL == 2) {
         sl[3] = sl[0]; sc[3] = sc[0];
@@ -517,35 +664,34 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
           a = 0; b = minC; shift = 0;
         }
       }
-      lmp[0] = a; lmp[1] = b; lmp[2] = shift;
+      S.lmp[0] = a; S.lmp[1] = b; S.lmp[2] = shift;
     }
-    __syncthreads();
-    for (int k = lane, q = 0; k < n; k += 64, q++) predv(q) = clampi(((lmp[0] * aux[k]) >> lmp[2]) + lmp[1], 0, maxv);
+    wsync();
+    for (int k = lane, q = 0; k < n; k += 64, q++) predv(q) = clampi(((S.lmp[0] * S.aux[k]) >> S.lmp[2]) + S.lmp[1], 0, maxv);
   } else if (mip) {
     // ---------------- MIP
     const int sizeId = (w == 4 && h == 4) ? 0 : ((w == 4 || h == 4 || (w == 8 && h == 8)) ? 1 : 2);
     const int bdry = sizeId == 0 ? 2 : 4, rp = sizeId < 2 ? 4 : 8;
     const bool tr = (J.flags & IJ_MIP_T) != 0;
-    __shared__ int red[8];
     // boundaryDownsampling1D of top (w) and left (h): one lane per reduced sample
     if (lane < 2 * bdry) {
       const int side = lane >= bdry, d = lane - side * bdry;
       const int len = side ? h : w;
-      const int16_t *src = side ? refU[1] : refU[0];
+      const int16_t *src = side ? S.refU[1] : S.refU[0];
       if (bdry < len) {
         const int f = len / bdry, lf = ilog2(f);
         int sum = 0;
         for (int k = 0; k < f; k++) sum += src[1 + d * f + k];
-        red[lane] = (sum + (1 << (lf - 1))) >> lf;
+        S.red[lane] = (sum + (1 << (lf - 1))) >> lf;
       } else {
-        red[lane] = src[1 + d];
+        S.red[lane] = src[1 + d];
       }
     }
-    __syncthreads();
+    wsync();
     const int inputSize = 2 * bdry;
     int inb[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) inb[i] = i < inputSize ? (tr ? red[i < bdry ? bdry + i : i - bdry] : red[i]) : 0;
+    for (int i = 0; i < 8; i++) inb[i] = i < inputSize ? (tr ? S.red[i < bdry ? bdry + i : i - bdry] : S.red[i]) : 0;
     const int inOff = inb[0];
     inb[0] = sizeId < 2 ? ((1 << (bd - 1)) - inOff) : 0;
     int sum = inb[0];
@@ -569,23 +715,23 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
       }
       const int v = clampi(((acc + offset) >> 6) + inOff, 0, maxv);
       // transposed matrices produce the transposed block
-      const int oy = o / rp, ox = o - oy * rp;
-      aux[tr ? ox * rp + oy : o] = v;
+      const int oy = o >> (rp == 8 ? 3 : 2), ox = o & (rp - 1);
+      S.aux[tr ? ox * rp + oy : o] = v;
     }
-    __syncthreads();
+    wsync();
     const int upH = w / rp, upV = h / rp;
     // horizontal upsampling into rows (r+1)*upV-1 (predictionUpsampling :252-277), kept in aux2 region
-    int *full = aux + 64;   // w*h <= 64*64? MIP blocks <= 64x64: use registers per sample instead
+    int *full = S.aux + 64;   // w*h <= 64*64? MIP blocks <= 64x64: use registers per sample instead
     (void)full;
     for (int k = lane, q = 0; k < n; k += 64, q++) {
-      const int yy = k / w, xx = k - yy * w;
+      const int yy = k >> lw_, xx = k & (w - 1);
       // value of the horizontally upsampled row grid at (rowIdx, xx) where rowIdx in [0, rp)
       auto hval = [&](int rr, int cx) -> int {
-        if (upH <= 1) return aux[rr * rp + cx];
+        if (upH <= 1) return S.aux[rr * rp + cx];
         const int lf = ilog2(upH);
-        const int c = cx / upH, pos = cx - c * upH + 1;
-        const int before = c == 0 ? (int)refU[1][1 + (rr + 1) * upV - 1] : aux[rr * rp + c - 1];
-        const int behind = aux[rr * rp + c];
+        const int c = cx >> ilog2(upH), pos = cx - c * upH + 1;
+        const int before = c == 0 ? (int)S.refU[1][1 + (rr + 1) * upV - 1] : S.aux[rr * rp + c - 1];
+        const int behind = S.aux[rr * rp + c];
         return (before * (upH - pos) + behind * pos + (1 << (lf - 1))) >> lf;
       };
       int v;
@@ -593,8 +739,8 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
         v = hval(yy, xx);
       } else {
         const int lf = ilog2(upV);
-        const int r = yy / upV, pos = yy - r * upV + 1;
-        const int before = r == 0 ? (int)refU[0][1 + xx] : hval(r - 1, xx);
+        const int r = yy >> ilog2(upV), pos = yy - r * upV + 1;
+        const int before = r == 0 ? (int)S.refU[0][1 + xx] : hval(r - 1, xx);
         const int behind = hval(r, xx);
         v = (before * (upV - pos) + behind * pos + (1 << (lf - 1))) >> lf;
       }
@@ -605,13 +751,13 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
     const int lw = ilog2(w), lh = ilog2(h);
     if (bdpcm) {
       for (int k = lane, q = 0; k < n; k += 64, q++) {
-        const int yy = k / w, xx = k - yy * w;
+        const int yy = k >> lw_, xx = k & (w - 1);
         predv(q) = J.mode == 1 ? left[yy + 1] : top[xx + 1];
       }
     } else if (dirMode == PLANAR) {
       const int tr = top[w + 1], bl = left[h + 1];
       for (int k = lane, q = 0; k < n; k += 64, q++) {
-        const int yy = k / w, xx = k - yy * w;
+        const int yy = k >> lw_, xx = k & (w - 1);
         const int hor = (left[yy + 1] << lw) + (xx + 1) * (tr - left[yy + 1]);
         const int ver = (top[xx + 1] << lh) + (yy + 1) * (bl - top[xx + 1]);
         predv(q) = ((hor << lh) + (ver << lw) + (1 << (lw + lh))) >> (1 + lw + lh);
@@ -627,7 +773,7 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
     } else {
       // angular: build main / side references exactly as xPredIntraAng does
       const int W = isModeVer ? w : h, H = isModeVer ? h : w;   // in the (possibly transposed) frame
-      int16_t *refMain = mainA + EXT, *refSide = sideA + EXT;
+      int16_t *refMain = S.mainA + EXT, *refSide = S.sideA + EXT;
       {
         const int16_t *srcMain = isModeVer ? top : left, *srcSide = isModeVer ? left : top;
         if (angle < 0) {
@@ -644,11 +790,11 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
           for (int k = lane; k <= sideLen + mrl; k += 64) refSide[k] = srcSide[k];
         }
       }
-      __syncthreads();
+      wsync();
       const int16_t *rM = refMain + mrl, *rS = refSide + mrl;
       const bool integerSlope = (absAng & 31) == 0;
       for (int k = lane, q = 0; k < n; k += 64, q++) {
-        const int oy = k / w, ox = k - oy * w;
+        const int oy = k >> lw_, ox = k & (w - 1);
         const int xx = isModeVer ? ox : oy, yy = isModeVer ? oy : ox;   // transposed-frame coordinates
         int v;
         if (angle == 0) {
@@ -693,7 +839,7 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
     if (applyPDPC && !bdpcm && (dirMode == PLANAR || dirMode == DC)) {
       const int scale = (lw - 2 + lh - 2 + 2) >> 2;
       for (int k = lane, q = 0; k < n; k += 64, q++) {
-        const int yy = k / w, xx = k - yy * w;
+        const int yy = k >> lw_, xx = k & (w - 1);
         const int wT = 32 >> min(31, (yy << 1) >> scale);
         const int wL = 32 >> min(31, (xx << 1) >> scale);
         const int v = predv(q);
@@ -702,49 +848,137 @@ __global__ __launch_bounds__(64) void k_intra(const IntraParams *__restrict__ Pg
     }
   }
 
-  IPROF(7);
-  // ---- CIIP blend (geneWeightedPred) and reconstruction
+#ifdef VVCR_DIAG_DUMP
+  wsync();
+  if (gj == 0 && kreg == 0 && lane < 64) g_dbg[64 + lane] = S.pred[lane];
+#endif
+  if (kreg == 0) IPROF(5);
+  // ---- CIIP blend (geneWeightedPred) and reconstruction into the LDS tile and the picture
   const DPlane &PP = P.pred[comp];
-  __syncthreads();   // pred[] of other lanes
+  const int tb = tile_base(comp), tp = tile_pitch(comp);
+  const bool publish = (J.flags & IJ_PUBLISH) != 0;
+  wsync();   // pred[] of other lanes
   for (int k = 2 * lane; k < n; k += 128) {   // sample pairs (w and x0 are even)
-    const int yy = k / w, xx = k - yy * w;
+    const int yy = k >> lw_, xx = k & (w - 1);
     int v2[2];
 #pragma unroll
     for (int e = 0; e < 2; e++) {
-      int pv = pred[k + e];
+      int pv = S.pred[k + e];
       if (ciip) pv = ((4 - J.ciip_w) * pel(PP, x0 + xx + e, y0 + yy) + J.ciip_w * pv + 2) >> 2;
-      v2[e] = clampi(pv + resL[(y0 - ry + yy) * rw + x0 - rx + xx + e], 0, maxv);
-      if (isp && (ispVer ? xx + e == w - 1 : yy == h - 1)) ispPrev[ispVer ? yy : xx + e] = (int16_t)v2[e];
+      v2[e] = clampi(pv + S.resL[(y0 - ry + yy) * rw + x0 - rx + xx + e], 0, maxv);
+      if (isp && (ispVer ? xx + e == w - 1 : yy == h - 1)) S.ispPrev[ispVer ? yy : xx + e] = (int16_t)v2[e];
     }
-    st_sc1(D.p + (size_t)(y0 + yy) * D.stride + x0 + xx, (uint32_t)(uint16_t)v2[0] | ((uint32_t)v2[1] << 16));
+    const uint32_t pk = (uint32_t)(uint16_t)v2[0] | ((uint32_t)v2[1] << 16);
+    *(uint32_t *)&s_tile[tb + (y0 + yy - G.cy0(comp)) * tp + x0 + xx - G.cx0(comp)] = pk;
+    // Only a step that another CTU reads writes HBM here (sc1, drained before its flag); the CTU's
+    // picture area is written back from the tile once the CTU is done. Every HBM store of a wave
+    // delays that wave's later loads (vmcnt counts loads and stores in issue order), so interior steps
+    // issue none.
+    if (publish) st_sc1(D.p + (size_t)(y0 + yy) * D.stride + x0 + xx, pk);
   }
-  __syncthreads();
+  wsync();
   }   // regions
-  // publish: this wave's stores are complete before the flag (one wave per workgroup)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (lane == 0) __hip_atomic_store(&done[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef VVCR_INTRA_PROF
-  IPROF(8);
-  IPROF_RT(2);
-  if (lane == 0) {
-    const unsigned int slot = atomicAdd(&g_iprof_n, 1u);
-    if (slot < (1u << 17)) {
-      unsigned int xcc;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      g_iprof[slot][0] = rstamp[0];
-      g_iprof[slot][1] = rstamp[1];
-      g_iprof[slot][2] = rstamp[2];
-      g_iprof[slot][3] = (tstamp[1] - tstamp[0]) | (tstamp[2] - tstamp[0]) << 16 | (tstamp[3] - tstamp[0]) << 32 | (tstamp[4] - tstamp[0]) << 48;
-      g_iprof[slot][4] = (tstamp[5] - tstamp[0]) | (tstamp[6] - tstamp[0]) << 16 | (tstamp[7] - tstamp[0]) << 32 | (tstamp[8] - tstamp[0]) << 48;
-      g_iprof[slot][5] = (unsigned long long)J.comp | (unsigned long long)J.w << 8 | (unsigned long long)J.h << 16 |
-                         (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40;
-      g_iprof[slot][6] = (unsigned long long)j | (unsigned long long)blockIdx.x << 32;
-      g_iprof[slot][7] = (unsigned long long)(dep_start[j + 1] - dep_start[j]);
+  IPROF(6);
+}
+
+// Persistent: each workgroup takes CTUs (that have steps) in raster order from an atomic counter; its
+// waves take the CTU's steps in topological order from an LDS counter. A CTU only waits for CTUs taken
+// before it (left / above neighbours), and a step only for earlier steps, so every wave progresses.
+// state[0] = CTU counter, state[16 + i] = global flag of published step i; *err set if a wait times out.
+__global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict__ Pg, const IntraJob *__restrict__ jobs,
+                                                   const int32_t *__restrict__ ctu_list, const int32_t *__restrict__ ctu_start,
+                                                   int nctu, const int32_t *__restrict__ dep_start,
+                                                   const int32_t *__restrict__ deps, int32_t *state, int32_t *err) {
+  __shared__ int s_ctu, s_next;
+  __shared__ __attribute__((aligned(16))) uint32_t s_Praw[sizeof(IntraParams) / 4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int32_t *done = state + 16;
+  WaveScratch &S = s_ws[wid];
+  // The parameters live in LDS for the whole launch: every plane pointer / size the step body reads is
+  // an LDS read, never a vector-memory load queued behind the wave's HBM traffic.
+  static_assert(sizeof(IntraParams) % 4 == 0, "IntraParams copy");
+  for (int i = tid; i < (int)(sizeof(IntraParams) / 4); i += 64 * NW) s_Praw[i] = ((const uint32_t *)Pg)[i];
+  const IntraParams &P = *reinterpret_cast<const IntraParams *>(s_Praw);
+  for (;;) {
+    if (tid == 0) { s_ctu = atomicAdd(&state[0], 1); s_next = 0; }
+    __syncthreads();
+    const int c = s_ctu;
+    if (c >= nctu) break;
+    const int cl = P.ctu_log2, ctu = 1 << cl;
+    const int wc = (P.reco[0].w + ctu - 1) >> cl;
+    const int cy = ctu_list[c] / wc, cx = ctu_list[c] - cy * wc;
+    TileGeo G;
+    G.x0 = cx << cl; G.y0 = cy << cl;
+    G.w = min(ctu, P.reco[0].w - G.x0); G.h = min(ctu, P.reco[0].h - G.y0);
+    const int j0 = ctu_start[c], nj = ctu_start[c + 1] - j0;
+    // tile <- picture (inter CUs were reconstructed by k_recon_inter; intra areas are overwritten
+    // before any step reads them), 4 samples per load
+    for (int k = 0; k < 3; k++) {
+      const DPlane &D = P.reco[k];
+      const int q = G.cw(k) >> 2, tb = tile_base(k), tp = tile_pitch(k), lq = ilog2(q);
+      for (int i = tid; i < q * G.ch(k); i += 64 * NW) {
+        const int yy = i >> lq, xx = (i & (q - 1)) * 4;
+        const uint64_t v = *gp((const uint64_t *)&D.p[(size_t)(G.cy0(k) + yy) * D.stride + G.cx0(k) + xx]);
+        *(uint32_t *)&s_tile[tb + yy * tp + xx] = (uint32_t)v;
+        *(uint32_t *)&s_tile[tb + yy * tp + xx + 2] = (uint32_t)(v >> 32);
+      }
     }
-  }
+    for (int i = tid; i < nj; i += 64 * NW) s_ldone[i] = 0;
+    __syncthreads();
+    for (;;) {
+      // uniform control flow only (no lane-0 regions anywhere around the step body): every lane adds,
+      // lane 0 adds 1, and lane 0's result is the step
+      const int lj = __builtin_amdgcn_readfirstlane(atomicAdd(&s_next, lane == 0 ? 1 : 0));
+      if (lj >= nj) break;
+      const int gj = j0 + lj;
+      const IntraJob J = jobs[gj];
+      unsigned long long t_ready = 0, ps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef VVCR_INTRA_PROF
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  }   // steps
+      run_step(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps);
+      // hand-off: LDS stores of this wave complete before its done byte; a step read by another CTU
+      // also drains its HBM stores (sc1) before its global flag
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __hip_atomic_store(&s_ldone[lj], (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (J.flags & IJ_PUBLISH) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&done[gj], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#ifdef VVCR_INTRA_PROF
+      if (lane == 0) {
+        const unsigned int slot = atomicAdd(&g_iprof_n, 1u);
+        if (slot < (1u << 17)) {
+          unsigned int xcc;
+          asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+          g_iprof[slot][0] = t0;
+          g_iprof[slot][1] = t_ready;
+          g_iprof[slot][2] = __builtin_amdgcn_s_memrealtime();
+          g_iprof[slot][3] = (ps[1] - ps[0]) | (ps[2] - ps[0]) << 16 | (ps[3] - ps[0]) << 32 | (ps[4] - ps[0]) << 48;
+          g_iprof[slot][4] = (ps[5] - ps[0]) | (ps[6] - ps[0]) << 16 | (ps[7] - ps[0]) << 32;
+          g_iprof[slot][5] = (unsigned long long)J.comp | (unsigned long long)J.w << 8 | (unsigned long long)J.h << 16 |
+                             (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40;
+          g_iprof[slot][6] = (unsigned long long)gj | (unsigned long long)blockIdx.x << 32;
+          g_iprof[slot][7] = (unsigned long long)(dep_start[gj + 1] - dep_start[gj]);
+        }
+      }
+#endif
+    }
+    __syncthreads();   // every step of the CTU finished
+    // tile -> picture (the final reconstruction of the CTU; published samples are rewritten with the
+    // same values), 4 samples per store, before the tile is reused
+    for (int k = 0; k < 3; k++) {
+      const DPlane &D = P.reco[k];
+      const int q = G.cw(k) >> 2, tb = tile_base(k), tp = tile_pitch(k), lq = ilog2(q);
+      for (int i = tid; i < q * G.ch(k); i += 64 * NW) {
+        const int yy = i >> lq, xx = (i & (q - 1)) * 4;
+        const uint64_t v = (uint64_t)*(const uint32_t *)&s_tile[tb + yy * tp + xx] |
+                           (uint64_t)*(const uint32_t *)&s_tile[tb + yy * tp + xx + 2] << 32;
+        *gpw((uint64_t *)&D.p[(size_t)(G.cy0(k) + yy) * D.stride + G.cx0(k) + xx]) = v;
+      }
+    }
+    __syncthreads();
+  }
 }
 
 __global__ void k_recon_inter(IntraParams P, const ReconTile *__restrict__ tiles, int n) {
@@ -772,10 +1006,12 @@ void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hip
   hipLaunchKernelGGL(k_recon_inter, dim3(n), dim3(64), 0, s, p, tiles, n);
 }
 
-void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *dep_start, const int32_t *deps,
-                  int32_t *state, int32_t *err, int n_cu, hipStream_t s) {
-  if (n <= 0) return;
+void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *ctu_list, const int32_t *ctu_start,
+                  int nctu, const int32_t *dep_start, const int32_t *deps, int32_t *state, int32_t *err, int n_cu,
+                  hipStream_t s) {
+  if (n <= 0 || nctu <= 0) return;
   VVCR_CHECK_HIP(hipMemsetAsync(state, 0, (16 + (size_t)n) * sizeof(int32_t), s));
-  // 64 KiB of dynamic LDS on top of the kernel's own keeps one workgroup per CU
-  hipLaunchKernelGGL(k_intra, dim3(std::min(n, n_cu)), dim3(64), 65536, s, p_dev, jobs, n, dep_start, deps, state, err);
+  // one workgroup per CU (the LDS tile + wave scratch take ~145 KiB), never more than the CTUs
+  hipLaunchKernelGGL(k_intra, dim3(std::min(nctu, n_cu)), dim3(64 * NW), 0, s, p_dev, jobs, ctu_list, ctu_start, nctu,
+                     dep_start, deps, state, err);
 }

@@ -322,28 +322,60 @@ struct Planner {
             throw VvcrError(VVCR_E_UNSUPPORTED, "IBC / palette CUs are not supported");
           }
         }
-    // steps in level order (a topological order of the dependency graph), dependencies renumbered
-    std::vector<int32_t> perm(jobs.size());
-    for (size_t i = 0; i < perm.size(); i++) perm[i] = (int32_t)i;
-    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) { return jobs[a].first < jobs[b].first; });
-    std::vector<int32_t> rank(jobs.size());
-    for (size_t i = 0; i < perm.size(); i++) rank[perm[i]] = (int32_t)i;
-    int maxLev = jobs.empty() ? 0 : jobs[perm.back()].first;
-    out.level_start.assign(maxLev + 2, 0);
-    out.jobs.resize(jobs.size());
-    out.dep_start.assign(jobs.size() + 1, 0);
+    // Steps grouped by CTU (raster order), inside a CTU by level: a topological order of the dependency
+    // graph (every dependency is in the same CTU at a lower level, or in an earlier CTU — the left /
+    // above neighbours). k_intra runs one CTU per workgroup with the CTU's samples in LDS; a dependency
+    // inside the CTU is encoded as its local index (>= 0), one in another CTU as ~(global index), and
+    // the producing step is flagged IJ_PUBLISH (drains its global stores and raises a global flag).
+    const int nj = (int)jobs.size();
+    std::vector<int32_t> ctu_of_job(nj);
+    for (int i = 0; i < nj; i++) {
+      const IntraJob &j = jobs[i].second;
+      const int s = j.comp ? 1 : 0;
+      const int lx = j.cx << s, ly = j.cy << s;   // CU position in luma samples (a CU never crosses a CTU)
+      ctu_of_job[i] = (ly >> sp.ctu_log2) * wc + (lx >> sp.ctu_log2);
+    }
+    std::vector<int32_t> perm(nj);
+    for (int i = 0; i < nj; i++) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) {
+      if (ctu_of_job[a] != ctu_of_job[b]) return ctu_of_job[a] < ctu_of_job[b];
+      return jobs[a].first < jobs[b].first;
+    });
+    std::vector<int32_t> rank(nj);
+    for (int i = 0; i < nj; i++) rank[perm[i]] = i;
+    out.jobs.resize(nj);
+    out.dep_start.assign(nj + 1, 0);
     out.deps.clear();
-    for (size_t i = 0; i < perm.size(); i++) {
+    out.ctu_list.clear();
+    out.ctu_start.clear();
+    for (int i = 0; i < nj; i++) {
       const int32_t o = perm[i];
+      if (out.ctu_list.empty() || out.ctu_list.back() != ctu_of_job[o]) {
+        out.ctu_list.push_back(ctu_of_job[o]);
+        out.ctu_start.push_back(i);
+      }
       out.jobs[i] = jobs[o].second;
-      out.level_start[jobs[o].first + 1] = (int32_t)(i + 1);
+    }
+    out.ctu_start.push_back(nj);
+    for (size_t c = 0; c + 1 < out.ctu_start.size(); c++)
+      if (out.ctu_start[c + 1] - out.ctu_start[c] > kIntraMaxStepsPerCtu)
+        throw VvcrError(VVCR_E_UNSUPPORTED, "intra plan: more steps in one CTU than the kernel's LDS flag array holds");
+    int c = 0;
+    for (int i = 0; i < nj; i++) {
+      while (out.ctu_start[c + 1] <= i) c++;
+      const int32_t o = perm[i];
       for (int32_t d : deps[o]) {
-        if (rank[d] >= (int32_t)i) throw VvcrError(VVCR_E_STATE, "intra plan: dependency is not earlier in step order");
-        out.deps.push_back(rank[d]);
+        const int32_t rd = rank[d];
+        if (rd >= i) throw VvcrError(VVCR_E_STATE, "intra plan: dependency is not earlier in step order");
+        if (rd >= out.ctu_start[c]) {
+          out.deps.push_back(rd - out.ctu_start[c]);
+        } else {
+          out.deps.push_back(~rd);
+          out.jobs[rd].flags |= IJ_PUBLISH;
+        }
       }
       out.dep_start[i + 1] = (int32_t)out.deps.size();
     }
-    for (int L = 1; L <= maxLev + 1; L++) out.level_start[L] = std::max(out.level_start[L], out.level_start[L - 1]);
     for (IntraJob &j : out.jobs) resolve_availability(j);
   }
 };
@@ -355,4 +387,34 @@ void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const Pict
   if (pp.lmcs_enabled) throw VvcrError(VVCR_E_UNSUPPORTED, "LMCS reconstruction is not supported yet");
   auto P = std::make_unique<Planner>(sp, pp, d, out);
   P->run();
+}
+
+// Diagnostics (host only, no device): the intra plan of one picture's descriptors. Per step
+// out[k*8 + {0..7}] = x, y, comp, w, h, flags, isp_k, seq; deps in CSR form (dep_start[n+1], deps).
+// Returns the number of steps (or a negative error); counts[0] = steps, counts[1] = dependencies.
+extern "C" int vvcr_debug_plan_intra(const vvcr_seq_params *sp, const vvcr_pic_params *pp, const vvcr_cu *cu, int32_t ncu,
+                                     const vvcr_pu *pu, int32_t npu, const vvcr_tu *tu, int32_t ntu, int32_t *out,
+                                     int32_t cap, int32_t *dep_start, int32_t *deps, int32_t dcap, int32_t *counts) {
+  try {
+    PictureDescriptors d;
+    d.cu.assign(cu, cu + ncu);
+    d.pu.assign(pu, pu + npu);
+    d.tu.assign(tu, tu + ntu);
+    IntraPlan ip;
+    plan_intra(*sp, *pp, d, ip);
+    const int n = (int)ip.jobs.size();
+    counts[0] = n;
+    counts[1] = (int)ip.deps.size();
+    if (n > cap || (int)ip.deps.size() > dcap) return n;
+    for (int k = 0; k < n; k++) {
+      const IntraJob &j = ip.jobs[k];
+      const int32_t r[8] = {j.x, j.y, j.comp, j.w, j.h, j.flags, j.isp_k, j.seq};
+      memcpy(out + 8 * k, r, sizeof r);
+    }
+    memcpy(dep_start, ip.dep_start.data(), (n + 1) * sizeof(int32_t));
+    memcpy(deps, ip.deps.data(), ip.deps.size() * sizeof(int32_t));
+    return n;
+  } catch (const VvcrError &e) {
+    return e.code;
+  }
 }
