@@ -82,7 +82,7 @@ struct Prepared {
   DevVec<uint8_t> alf_ctb;
   DevVec<int32_t> dmvr;
   bool have_sao = false, have_alf = false;
-  int n_tb = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
+  int n_tb = 0, n_tb_small = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
   hipEvent_t ev[NK][2] = {};
   hipEvent_t done = nullptr;
   bool ran[NK] = {};
@@ -187,6 +187,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     r.coef.upload(ctx->desc.coef);
     r.tb.upload(ctx->wl.tb);
     r.n_tb = (int)ctx->wl.tb.size();
+    r.n_tb_small = ctx->wl.tb_small;
     double b = 0;
     for (const TbJob &t : ctx->wl.tb) b += (double)t.w * t.h * (4 + 2);   // int32 levels in, int16 residual out
     r.alg_bytes[K_RESID] = b;
@@ -296,9 +297,9 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     tp.bd = ctx->sp.bit_depth;
     memcpy(tp.scan_off, ctx->scans.off, sizeof(tp.scan_off));
     memcpy(tp.lfnst_scan_off, ctx->scans.lfnst_off, sizeof(tp.lfnst_scan_off));
-    launch_resid(tp, r.tb.p, r.n_tb, r.coef.p, ctx->d_scans.p, s);
+    launch_resid(tp, r.tb.p, r.n_tb, r.n_tb_small, r.coef.p, ctx->d_scans.p, s);
     VVCR_CHECK_HIP(hipGetLastError());
-    r.launches[K_RESID] = r.n_tb ? 1 : 0;
+    r.launches[K_RESID] = (r.n_tb_small > 0) + (r.n_tb > r.n_tb_small);
   }
   if (mask & VVCR_STAGE_INTER) {
     const McParams mp = make_mc_params(ctx);

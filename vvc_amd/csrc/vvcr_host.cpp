@@ -160,6 +160,8 @@ AffList affine_list(const vvcr_pic_params &pp, const vvcr_cu &c, const vvcr_pu &
 void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl) {
   wl.clear();
   build_tb_jobs(sp, pp, d, wl.tb);
+  // small blocks first (64-lane workgroups), then the large ones (256 lanes)
+  wl.tb_small = (int)(std::stable_partition(wl.tb.begin(), wl.tb.end(), [](const TbJob &j) { return j.w * j.h <= 256; }) - wl.tb.begin());
   const int W4 = sp.width / 4;
   std::vector<int> geo_of(d.cu.size(), -1);
   for (size_t g = 0; g < d.geo.size(); g++)
@@ -438,6 +440,25 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
       }
       j.skip_w = (uint8_t)skipW; j.skip_h = (uint8_t)skipH;
       if (comp == 1 && t.jccr) j.ict = (int8_t)kIct[pp.joint_cbcr_sign ? 1 : 0][t.jccr];
+      // bounding box of the non-zero levels: the kernel's passes skip the all-zero rows / columns
+      // (dequantisation maps 0 to 0; LFNST widens it to its output area; TS / BDPCM use the whole block)
+      {
+        int R = 0, C = 0;
+        if (ts) {
+          R = h; C = w;
+        } else {
+          if ((size_t)j.coef + (size_t)w * h > d.coef.size()) throw VvcrError(VVCR_E_ARG, "coefficient offset out of range");
+          const int32_t *lv = d.coef.data() + j.coef;
+          for (int yy = 0; yy < h; yy++)
+            for (int xx = 0; xx < w; xx++)
+              if (lv[yy * w + xx]) { R = std::max(R, yy + 1); C = std::max(C, xx + 1); }
+          if (j.flags & TB_LFNST_APPLY) {
+            const int r = (w >= 8 && h >= 8) ? 8 : 4;
+            R = std::max(R, std::min(r, h)); C = std::max(C, std::min(r, w));
+          }
+        }
+        j.nz_rows = (uint8_t)R; j.nz_cols = (uint8_t)C;
+      }
       out.push_back(j);
     }
   }

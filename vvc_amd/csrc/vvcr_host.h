@@ -18,12 +18,13 @@ struct WorkLists {
   std::vector<McJob> mc_bidir;     // DMVR sub-blocks and BDOF tiles
   std::vector<AffPu> aff_pu;       // affine PUs
   std::vector<AffJob> aff_jobs;    // affine tiles
-  std::vector<TbJob> tb;           // coded transform blocks
+  std::vector<TbJob> tb;           // coded transform blocks (the tb_small blocks of <= 256 samples first)
+  int tb_small = 0;
   int n_dmvr = 0;                  // DMVR sub-blocks (delta outputs), in PU order
   int n_unsupported_inter = 0;     // PUs needing kernels not built yet (reported, never silently skipped)
   void clear() {
     mc_basic.clear(); mc_bidir.clear(); aff_pu.clear(); aff_jobs.clear(); tb.clear();
-    n_dmvr = 0; n_unsupported_inter = 0;
+    n_dmvr = 0; n_unsupported_inter = 0; tb_small = 0;
   }
 };
 

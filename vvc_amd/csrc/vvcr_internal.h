@@ -108,7 +108,9 @@ struct TbJob {
   uint8_t qp;                  // QpParam::Qp(ts)
   uint8_t skip_w, skip_h;      // zero-out lines of xIT (TrQuant.cpp:841-852)
   int32_t coef;                // level offset in the coefficient pool
-  int32_t pad[3];
+  uint8_t nz_rows, nz_cols;    // bounding box of the non-zero levels (host-computed; TS/BDPCM: whole block)
+  uint8_t pad8[2];
+  int32_t pad[2];
 };
 static_assert(sizeof(TbJob) == 32, "TbJob layout");
 
@@ -141,5 +143,6 @@ void launch_mc_bidir(const McParams &p, const McJob *jobs, int njobs, int32_t *d
 void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const AffPu *pus, hipStream_t s);
 void launch_sao(const SaoParams &p, hipStream_t s);
 void launch_alf(const AlfParams &p, hipStream_t s);
-void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, const int32_t *coef, const uint16_t *scans, hipStream_t s);
+// jobs[0, nsmall): blocks of <= 256 samples (64-lane workgroups); jobs[nsmall, njobs): larger (256 lanes)
+void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, int nsmall, const int32_t *coef, const uint16_t *scans, hipStream_t s);
 void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);
