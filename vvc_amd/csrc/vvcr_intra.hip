@@ -339,6 +339,19 @@ __device__ __forceinline__ void wait_local(int v, int32_t *err) {
 }
 
 // One reconstruction step, run by one wave.
+// Step kinds: each gets its own instantiation of run_step, so that a step executes only its own
+// path (one generic body made the compiler evaluate and spill the set-up of every path per step).
+enum { K_REG = 0, K_ISP = 1, K_MIP = 2, K_LM = 3, K_CIIP = 4, K_BDPCM = 5 };
+__device__ __forceinline__ int step_kind(const IntraJob &J) {
+  if (J.flags & IJ_BDPCM) return K_BDPCM;
+  if (J.flags & IJ_CIIP) return K_CIIP;
+  if (J.flags & (IJ_ISP_HOR | IJ_ISP_VER)) return K_ISP;
+  if (J.flags & IJ_MIP) return K_MIP;
+  if (J.comp > 0 && J.mode >= LM) return K_LM;
+  return K_REG;
+}
+
+template <int KIND>
 __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J, const TileGeo &G, WaveScratch &S,
                                          const int32_t *dep_start, const int32_t *deps, int gj, int32_t *done,
                                          int32_t *err, int lane, unsigned long long &t_ready, unsigned long long *ps) {
@@ -348,12 +361,12 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   const DPlane &D = P.reco[comp];
   const Src SD = src_of(P, comp, G);
   const int w = J.w, h = J.h;
-  const bool isp = (J.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0;
-  const bool ispVer = (J.flags & IJ_ISP_VER) != 0;
-  const bool mip = (J.flags & IJ_MIP) != 0;
-  const bool bdpcm = (J.flags & IJ_BDPCM) != 0;
-  const bool ciip = (J.flags & IJ_CIIP) != 0;
-  const bool lmMode = comp > 0 && J.mode >= LM && !bdpcm;
+  constexpr bool isp = KIND == K_ISP;
+  const bool ispVer = isp && (J.flags & IJ_ISP_VER) != 0;
+  constexpr bool mip = KIND == K_MIP;
+  constexpr bool bdpcm = KIND == K_BDPCM;
+  constexpr bool ciip = KIND == K_CIIP;
+  constexpr bool lmMode = KIND == K_LM;
   const int mrl = comp ? 0 : J.mrl;
   const int n = w * h;
   const int lw_ = ilog2(w);   // block sizes are powers of two: shifts instead of divisions
@@ -924,6 +937,18 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
       }
     }
     for (int i = tid; i < nj; i += 64 * NW) s_ldone[i] = 0;
+    // Warm the XCD's L2 with the CTU's residual (written by k_resid long before): a step's residual
+    // load then hits L2 instead of paying an HBM round trip on the dependency chain. The loaded values
+    // only feed an opaque register move, so nothing waits for them here.
+    for (int k = 0; k < 3; k++) {
+      const DPlane &R = P.resi[k];
+      const int q = G.cw(k) >> 3, lq = ilog2(q);   // 8 samples (16 B) per load
+      for (int i = tid; i < q * G.ch(k); i += 64 * NW) {
+        const int yy = i >> lq, xx = (i & (q - 1)) * 8;
+        const uint64_t v = *gp((const uint64_t *)&R.p[(size_t)(G.cy0(k) + yy) * R.stride + G.cx0(k) + xx]);
+        asm volatile("" :: "v"(v));
+      }
+    }
     __syncthreads();
     for (;;) {
       // uniform control flow only (no lane-0 regions anywhere around the step body): every lane adds,
@@ -936,7 +961,14 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
 #ifdef VVCR_INTRA_PROF
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-      run_step(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps);
+      switch (step_kind(J)) {
+        case K_REG: run_step<K_REG>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
+        case K_ISP: run_step<K_ISP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
+        case K_MIP: run_step<K_MIP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
+        case K_LM: run_step<K_LM>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
+        case K_CIIP: run_step<K_CIIP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
+        default: run_step<K_BDPCM>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
+      }
       // hand-off: LDS stores of this wave complete before its done byte; a step read by another CTU
       // also drains its HBM stores (sc1) before its global flag
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
