@@ -153,7 +153,8 @@ def main():
     tf = os.path.join(ROOT, "profiles", "r01_traffic.json")
     if os.path.exists(tf):
         with open(tf) as f:
-            traffic = json.load(f).get("per_launch_bytes", {}).get(dom)
+            tj = json.load(f)
+        traffic = tj.get("per_group_launch_bytes", {}).get(dom)   # profiles/: tools/pmc.sh + tools/pmc_summary.py
 
     ms_step = elapsed / a.steps * 1e3
     value = world * px_seq * a.steps / elapsed / 1e6

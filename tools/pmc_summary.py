@@ -1,0 +1,52 @@
+"""Per-kernel HBM traffic from the rocprofv3 PMC passes of tools/pmc.sh, per launch, corrected as
+MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads, so it is doubled (our kernels mix
+access widths: the doubled figure is an upper estimate of the read bytes, the raw one a lower one).
+
+  python tools/pmc_summary.py gpurun_out/pmc_r01 > profiles/r01_traffic.json
+"""
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+
+def per_kernel(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            k = re.sub(r"^void ", "", r["Kernel_Name"].replace("(anonymous namespace)::", "")).split("(")[0]
+            agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[k].add(r["Dispatch_Id"])
+    return {k: {c: v / len(disp[k]) for c, v in cs.items()} for k, cs in agg.items()}, {k: len(v) for k, v in disp.items()}
+
+
+def main(d):
+    fetch, nf = per_kernel(os.path.join(d, "fetch", "run_counter_collection.csv"))
+    write, nw = per_kernel(os.path.join(d, "write", "run_counter_collection.csv"))
+    out = {"source": d, "unit": "bytes per launch",
+           "note": "read = 2 x FETCH_SIZE (gfx950 wide-read correction), write = WRITE_SIZE; KiB -> bytes",
+           "per_launch_bytes": {}, "detail": {}}
+    for k in sorted(set(fetch) | set(write)):
+        if k.startswith("__amd"):
+            continue
+        f = fetch.get(k, {}).get("FETCH_SIZE", 0.0) * 1024
+        w = write.get(k, {}).get("WRITE_SIZE", 0.0) * 1024
+        out["per_launch_bytes"][k] = round(2 * f + w)
+        out["detail"][k] = {"fetch_raw": round(f), "read_corrected": round(2 * f), "write": round(w),
+                            "launches_sampled": nf.get(k, 0)}
+    # kernel-group names used by bench.py (vvcr_kernel_stats groups)
+    groups = {"resid": ["k_resid<256, 64>", "k_resid<4096, 256>"], "intra": ["k_intra"], "mc": ["k_mc_basic"],
+              "mc_bidir": ["k_mc_bidir"], "mc_affine": ["k_mc_affine"], "recon_inter": ["k_recon_inter"],
+              "sao": ["k_sao"], "alf": ["k_alf_luma", "k_alf_chroma"],
+              "deblock": ["k_dbk_luma<0>", "k_dbk_chroma<0>", "k_dbk_luma<1>", "k_dbk_chroma<1>"]}
+    out["per_group_launch_bytes"] = {g: round(sum(out["per_launch_bytes"].get(k, 0) for k in ks))
+                                     for g, ks in groups.items()}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
