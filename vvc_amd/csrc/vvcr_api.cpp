@@ -74,6 +74,7 @@ struct Prepared {
   DevVec<IntraJob> ijobs;
   DevVec<int32_t> idep_start, ideps, istate, ictu_list, ictu_start;
   DevVec<IntraParams> iparams;       // device copy of the intra kernel's parameters
+  DevVec<int16_t> lmcs_lut;          // LMCS forward [0, 1024) and inverse [1024, 2048) luma LUTs
   int n_ijobs = 0, n_ictu = 0;
   DevVec<DbkSeg> dbk;
   int dbk_counts[4] = {0, 0, 0, 0};
@@ -165,6 +166,27 @@ static McParams make_mc_params(vvcr_ctx *ctx) {
   return P;
 }
 
+// parameters of the intra / inter-reconstruction kernels for a prepared picture
+static IntraParams make_intra_params(vvcr_ctx *ctx, const Prepared &r) {
+  const vvcr_pic_params &pp = r.pp;
+  IntraParams P{};
+  for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
+  P.bd = ctx->sp.bit_depth;
+  P.ctu = 1 << ctx->sp.ctu_log2;
+  P.ctu_log2 = ctx->sp.ctu_log2;
+  if (pp.lmcs_enabled) {
+    // forward mapping of inter predictions: slices other than I with the slice reshaper on (the CTU
+    // flag of DecLib.cpp:1726-1742); chroma residual scaling: picture-header flag
+    P.lmcs = (pp.slice_type != 2 ? 1 : 0) | (pp.lmcs_chroma_scale ? 2 : 0);
+    P.lmcs_min_bin = pp.lmcs_min_bin;
+    P.lmcs_max_bin = pp.lmcs_max_bin;
+    for (int i = 0; i < 17; i++) P.lmcs_pivot[i] = pp.lmcs_pivot[i];
+    for (int i = 0; i < 16; i++) P.lmcs_cadj[i] = pp.lmcs_cadj[i];
+    P.lmcs_fwd = r.lmcs_lut.p;
+  }
+  return P;
+}
+
 // ---- algorithmic bytes: each logical input once, each output once, 2 B / sample
 static double mc_bytes(const McJob &j) {
   const int lists = ((j.flags & MC_L0) ? 1 : 0) + ((j.flags & MC_L1) ? 1 : 0);
@@ -219,6 +241,12 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     }
     r.alg_bytes[K_MC_AFFINE] = b;
   }
+  if (pp.lmcs_enabled) {
+    if (sp.bit_depth != 10) throw VvcrError(VVCR_E_UNSUPPORTED, "LMCS tables are captured for 10-bit luma");
+    std::vector<int16_t> lut(pp.lmcs_fwd, pp.lmcs_fwd + 1024);
+    lut.insert(lut.end(), pp.lmcs_inv, pp.lmcs_inv + 1024);
+    r.lmcs_lut.upload(lut);
+  }
   if (mask & VVCR_STAGE_INTRA) {
     plan_intra(sp, pp, ctx->desc, ctx->intra);
     IntraPlan &ip = ctx->intra;
@@ -227,11 +255,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     r.idep_start.upload(ip.dep_start);
     r.ideps.upload(ip.deps);
     r.istate.ensure(16 + ip.jobs.size());
-    IntraParams P{};
-    for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
-    P.bd = ctx->sp.bit_depth;
-    P.ctu = 1 << ctx->sp.ctu_log2;
-    P.ctu_log2 = ctx->sp.ctu_log2;
+    const IntraParams P = make_intra_params(ctx, r);
     r.iparams.upload(&P, 1);
     r.n_ijobs = (int)ip.jobs.size();
     r.ictu_list.upload(ip.ctu_list);
@@ -323,11 +347,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     }
   }
   if (mask & VVCR_STAGE_INTRA) {
-    IntraParams P{};
-    for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
-    P.bd = ctx->sp.bit_depth;
-    P.ctu = 1 << ctx->sp.ctu_log2;
-    P.ctu_log2 = ctx->sp.ctu_log2;
+    const IntraParams P = make_intra_params(ctx, r);
     {
       KernelTimer t(r, K_RECON, s);
       launch_recon_inter(P, r.tiles.p, r.n_tiles, s);
@@ -343,6 +363,10 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     }
   }
   auto &A = ctx->dpb[pp.slot];
+  if ((mask & VVCR_STAGE_LMCS_INV) && pp.lmcs_enabled) {
+    launch_lmcs_inverse(A[0], r.lmcs_lut.p + 1024, s);   // back to the original domain before the loop filters
+    VVCR_CHECK_HIP(hipGetLastError());
+  }
   if ((mask & VVCR_STAGE_DBK) && (r.dbk_counts[0] + r.dbk_counts[1] + r.dbk_counts[2] + r.dbk_counts[3])) {
     KernelTimer t(r, K_DBK, s);
     DbkParams dp{};

@@ -44,8 +44,25 @@ struct IntraJob {
   // left (horizontal split) / above (vertical split) neighbour; av[2] bits 16..27 / av[3]: CCLM
   // neighbourhoods (see nb_bits in vvcr_intra_host.cpp).
   uint32_t av[4];
+  // LMCS chroma residual scaling (Reshape::calculateChromaAdjVpduNei, Reshape.cpp:107): luma position of
+  // the CU at the top-left of the block's 64x64 VPDU, whose left column / above row (64 samples each,
+  // reconstructed, mapped domain) give the scale; vnb = CS_* bits
+  int16_t vx, vy;
+  uint8_t vnb;
+  uint8_t xkind;          // XK_*: step kinds beyond the intra prediction modes
+  uint8_t pad[2];
 };
-static_assert(sizeof(IntraJob) == 40, "IntraJob layout");
+static_assert(sizeof(IntraJob) == 48, "IntraJob layout");
+
+enum : uint8_t {
+  CS_LEFT = 1 << 0,       // left neighbour CU exists (getCURestricted)
+  CS_ABOVE = 1 << 1,      // above neighbour CU exists
+  CS_SCALE = 1 << 2,      // scale this chroma block's residual
+};
+enum : uint8_t {
+  XK_NONE = 0,
+  XK_INTER_CHROMA = 1,    // chroma of an inter CU in a picture with chroma residual scaling: pred + scaled resi
+};
 
 // Inter CU reconstruction tile: reco = clip(pred + resi), one <= 16x16 luma tile plus its chroma.
 struct ReconTile {
@@ -73,10 +90,18 @@ struct IntraParams {
   DPlane pred[3];                    // inter prediction planes (CIIP)
   DPlane resi[3];                    // residual planes
   int32_t bd, ctu, ctu_log2;
+  // LMCS (Reshape.h): lmcs bit 0 = forward-map inter luma predictions (DecCu.cpp:696,742,765), bit 1 =
+  // chroma residual scaling (DecCu.cpp:274,839)
+  int32_t lmcs, lmcs_min_bin, lmcs_max_bin;
+  int16_t lmcs_pivot[18];            // m_reshapePivot (mapped-domain bin starts), 17 used
+  int32_t lmcs_cadj[16];             // m_chromaAdjHelpLUT
+  const int16_t *lmcs_fwd;           // forward LUT, 1 << bd entries (device)
 };
 
 void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out);
 void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s);
+// LMCS inverse luma mapping of the reconstructed picture before deblocking (DecLib.cpp:574)
+void launch_lmcs_inverse(const DPlane &luma, const int16_t *inv_lut, hipStream_t s);
 // all steps of a picture in one persistent launch, one CTU per workgroup at a time; state: 16 + n int32
 // (reset here); *err set on a wait timeout
 void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *ctu_list, const int32_t *ctu_start,

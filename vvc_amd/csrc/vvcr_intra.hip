@@ -339,10 +339,44 @@ __device__ __forceinline__ void wait_local(int v, int32_t *err) {
 }
 
 // One reconstruction step, run by one wave.
+// LMCS chroma residual scale of a block (Reshape::calculateChromaAdjVpduNei, Reshape.cpp:107-198): the
+// average of the reconstructed (mapped) luma left of / above the CU at the block's VPDU corner, clipped,
+// located among the mapped-domain pivots (getPWLIdxInv :204) and looked up in m_chromaAdjHelpLUT.
+__device__ __forceinline__ int chroma_scale(const IntraParams &P, const TileGeo &G, int vx, int vy, int vnb, int lane) {
+  const Src SY = src_of(P, 0, G);
+  const int W = P.reco[0].w, H = P.reco[0].h;
+  const int nn = min(64, P.ctu), lnn = nn == 64 ? 6 : 5;
+  int xs[2], ys[2], v[2];
+  bool need[2];
+  xs[0] = vx - 1; ys[0] = vy + min(lane, H - vy - 1); need[0] = (vnb & CS_LEFT) && lane < nn;
+  xs[1] = vx + min(lane, W - vx - 1); ys[1] = vy - 1; need[1] = (vnb & CS_ABOVE) && lane < nn;
+  gather(SY, xs, ys, need, v);
+  const int sum = wave_sum((need[0] ? v[0] : 0) + (need[1] ? v[1] : 0));
+  const int maxv = (1 << P.bd) - 1;
+  const int cnt = ((vnb & CS_LEFT) ? 1 : 0) + ((vnb & CS_ABOVE) ? 1 : 0);
+  int luma;
+  if (cnt == 1) luma = clampi((sum + (1 << (lnn - 1))) >> lnn, 0, maxv);
+  else if (cnt == 2) luma = clampi((sum + (1 << lnn)) >> (lnn + 1), 0, maxv);
+  else luma = 1 << (P.bd - 1);
+  int idx = P.lmcs_min_bin;
+  for (; idx <= P.lmcs_max_bin; idx++)
+    if (luma < P.lmcs_pivot[idx + 1]) break;
+  return P.lmcs_cadj[min(idx, 15)];
+}
+// AreaBuf::scaleSignal inverse (Buffer.cpp:424-441), CSCALE_FP_PREC = 11
+__device__ __forceinline__ int scale_resi(int r, int scale, int bd) {
+  const int maxAbs = (1 << bd) - 1;
+  r = clampi(r, -maxAbs - 1, maxAbs);
+  const int a = r < 0 ? -r : r;
+  const int v = (a * scale + (1 << 10)) >> 11;
+  return clampi(r < 0 ? -v : v, -32768, 32767);
+}
+
 // Step kinds: each gets its own instantiation of run_step, so that a step executes only its own
 // path (one generic body made the compiler evaluate and spill the set-up of every path per step).
-enum { K_REG = 0, K_ISP = 1, K_MIP = 2, K_LM = 3, K_CIIP = 4, K_BDPCM = 5 };
+enum { K_REG = 0, K_ISP = 1, K_MIP = 2, K_LM = 3, K_CIIP = 4, K_BDPCM = 5, K_INTERC = 6 };
 __device__ __forceinline__ int step_kind(const IntraJob &J) {
+  if (J.xkind == XK_INTER_CHROMA) return K_INTERC;
   if (J.flags & IJ_BDPCM) return K_BDPCM;
   if (J.flags & IJ_CIIP) return K_CIIP;
   if (J.flags & (IJ_ISP_HOR | IJ_ISP_VER)) return K_ISP;
@@ -367,6 +401,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   constexpr bool bdpcm = KIND == K_BDPCM;
   constexpr bool ciip = KIND == K_CIIP;
   constexpr bool lmMode = KIND == K_LM;
+  constexpr bool interc = KIND == K_INTERC;
   const int mrl = comp ? 0 : J.mrl;
   const int n = w * h;
   const int lw_ = ilog2(w);   // block sizes are powers of two: shifts instead of divisions
@@ -419,6 +454,8 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   (void)t_ready; (void)ps;
 #endif
   IPROF(1);
+  // LMCS chroma residual scale (uniform), after the wait: it reads reconstructed luma of other steps
+  const int cscale = (comp > 0 && (J.vnb & CS_SCALE)) ? chroma_scale(P, G, J.vx, J.vy, J.vnb, lane) : 0;
   auto store_resid = [&]() {
     if (rvec) {
 #pragma unroll
@@ -450,7 +487,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   {
     int16_t *top = S.refU[0], *left = S.refU[1];
     if (!isp) {
-      fill_refs(SD, D, ch, x0, y0, topLen, leftLen, mrl, bd, avlo, avhi, top, left, lane, ps);
+      if (!interc) fill_refs(SD, D, ch, x0, y0, topLen, leftLen, mrl, bd, avlo, avhi, top, left, lane, ps);
     } else if (kreg == 0) {
       // CU-level fill of the first region (predSize per split direction), kept in refF for the others
       const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
@@ -549,7 +586,11 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   const int16_t *left = refFilter ? S.refF[1] : S.refU[1];
 #define predv(q) S.pred[lane + 64 * (q)]
 
-  if (lmMode) {
+  if (interc) {
+    // ---------------- chroma of an inter CU (LMCS chroma residual scaling): the MC prediction
+    const DPlane &PI = P.pred[comp];
+    for (int k = lane, q = 0; k < n; k += 64, q++) predv(q) = pel(PI, x0 + (k & (w - 1)), y0 + (k >> lw_));
+  } else if (lmMode) {
     // ---------------- CCLM (xGetLumaRecPixels + xGetLMParameters)
     const Src SY = src_of(P, 0, G);
     const DPlane &Y = P.reco[0];
@@ -877,8 +918,14 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
 #pragma unroll
     for (int e = 0; e < 2; e++) {
       int pv = S.pred[k + e];
-      if (ciip) pv = ((4 - J.ciip_w) * pel(PP, x0 + xx + e, y0 + yy) + J.ciip_w * pv + 2) >> 2;
-      v2[e] = clampi(pv + S.resL[(y0 - ry + yy) * rw + x0 - rx + xx + e], 0, maxv);
+      if (ciip) {
+        int ip = pel(PP, x0 + xx + e, y0 + yy);
+        if (comp == 0 && (P.lmcs & 1)) ip = P.lmcs_fwd[ip];   // LMCS: mapped inter prediction (DecCu.cpp:696)
+        pv = ((4 - J.ciip_w) * ip + J.ciip_w * pv + 2) >> 2;
+      }
+      int rv = S.resL[(y0 - ry + yy) * rw + x0 - rx + xx + e];
+      if (cscale) rv = scale_resi(rv, cscale, bd);
+      v2[e] = clampi(pv + rv, 0, maxv);
       if (isp && (ispVer ? xx + e == w - 1 : yy == h - 1)) S.ispPrev[ispVer ? yy : xx + e] = (int16_t)v2[e];
     }
     const uint32_t pk = (uint32_t)(uint16_t)v2[0] | ((uint32_t)v2[1] << 16);
@@ -967,7 +1014,8 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
         case K_MIP: run_step<K_MIP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
         case K_LM: run_step<K_LM>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
         case K_CIIP: run_step<K_CIIP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
-        default: run_step<K_BDPCM>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
+        case K_BDPCM: run_step<K_BDPCM>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
+        default: run_step<K_INTERC>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
       }
       // hand-off: LDS stores of this wave complete before its done byte; a step read by another CTU
       // also drains its HBM stores (sc1) before its global flag
@@ -1025,13 +1073,29 @@ __global__ void k_recon_inter(IntraParams P, const ReconTile *__restrict__ tiles
     const DPlane &D = P.reco[comp], &Pr = P.pred[comp], &Re = P.resi[comp];
     for (int k = threadIdx.x; k < bw * bh; k += blockDim.x) {
       const int yy = k / bw, xx = k - yy * bw;
-      const int v = pel(Pr, bx + xx, by + yy) + pel(Re, bx + xx, by + yy);
+      int pv = pel(Pr, bx + xx, by + yy);
+      if (comp == 0 && (P.lmcs & 1)) pv = P.lmcs_fwd[pv];   // LMCS forward map of the prediction (DecCu.cpp:742,765)
+      const int v = pv + pel(Re, bx + xx, by + yy);
       D.p[(size_t)(by + yy) * D.stride + bx + xx] = (int16_t)clampi(v, 0, maxv);
     }
   }
 }
 
+// LMCS inverse luma mapping of the whole reconstructed picture (DecLib.cpp:574 rspSignal(invLUT)), in place,
+// 8 samples per lane
+__global__ void k_lmcs_inverse(DPlane L, const int16_t *__restrict__ inv) {
+  const int q = L.w >> 3, y = blockIdx.y, qx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qx >= q) return;
+  int16_t *row = L.p + (size_t)y * L.stride + qx * 8;
+#pragma unroll
+  for (int k = 0; k < 8; k++) row[k] = inv[row[k]];
+}
 }  // namespace
+
+void launch_lmcs_inverse(const DPlane &luma, const int16_t *inv_lut, hipStream_t s) {
+  const int q = luma.w >> 3;
+  hipLaunchKernelGGL(k_lmcs_inverse, dim3((q + 63) / 64, luma.h), dim3(64), 0, s, luma, inv_lut);
+}
 
 void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s) {
   if (n <= 0) return;

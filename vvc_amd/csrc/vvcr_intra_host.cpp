@@ -31,6 +31,7 @@ struct Planner {
   std::vector<std::vector<int32_t>> deps;           // per job: the steps it reads from (indices into jobs)
   std::vector<int32_t> cur;                         // dependencies of the step being planned
   int seq = 0;
+  bool cscale = false;                              // LMCS chroma residual scaling active in this picture
 
   Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, IntraPlan &o)
       : sp(s), pp(p), d(dd), out(o) {
@@ -95,6 +96,23 @@ struct Planner {
     return j;
   }
 
+  // LMCS chroma residual scaling of a chroma block whose luma-equivalent top-left is (lx, ly): the CU
+  // covering the top-left of its 64x64 VPDU gives the neighbour samples (Reshape::calculateChromaAdjVpduNei,
+  // Reshape.cpp:107-198); the step reads them, so their producers become dependencies. Returns the level.
+  int set_cscale(IntraJob &j, int lx, int ly) {
+    const int n64 = std::min(64, ctu);
+    const int vx0 = (lx / n64) * n64, vy0 = (ly / n64) * n64;
+    const int ci = cu_map[(size_t)(vy0 >> 2) * W4 + (vx0 >> 2)];
+    if (ci < 0) throw VvcrError(VVCR_E_STATE, "LMCS: no luma CU at a VPDU corner");
+    const vvcr_cu &t = d.cu[ci];
+    j.vx = (int16_t)t.x; j.vy = (int16_t)t.y;
+    j.vnb = CS_SCALE | (t.x > 0 ? CS_LEFT : 0) | (t.y > 0 ? CS_ABOVE : 0);   // one slice, one tile
+    int lev = 0;
+    if (t.x > 0) lev = std::max(lev, max_level(0, 0, t.x - 1, t.y, t.x - 1, t.y + n64 - 1));
+    if (t.y > 0) lev = std::max(lev, max_level(0, 0, t.x, t.y - 1, t.x + n64 - 1, t.y - 1));
+    return lev;
+  }
+
   void inter_cu(int ci) {
     const vvcr_cu &c = d.cu[ci];
     const vvcr_pu &p = d.pu[c.firstpu];
@@ -116,8 +134,9 @@ struct Planner {
         j.flags = IJ_CIIP;
         j.mode = 0;
         j.ciip_w = (uint8_t)wIntra;
-        const int lev = 1 + ref_level(ch, comp, j.x, j.y, 2 * j.w, 2 * j.h, 0);
-        id[comp] = push(lev, j);
+        int lev = ref_level(ch, comp, j.x, j.y, 2 * j.w, 2 * j.h, 0);
+        if (comp > 0 && cscale && j.w * j.h > 4) lev = std::max(lev, set_cscale(j, c.x, c.y));
+        id[comp] = push(lev + 1, j);
       }
       int lev = 0;
       for (auto it = jobs.end() - 3; it != jobs.end(); ++it) lev = std::max(lev, it->first);
@@ -126,17 +145,32 @@ struct Planner {
       mark(1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
       return;
     }
-    // plain inter: level 0, reconstructed before the intra waves
+    // plain inter: level 0, reconstructed before the intra waves; with LMCS chroma residual scaling the
+    // chroma scale depends on reconstructed luma next to the VPDU, so the chroma becomes a step
+    const bool chromaStep = cscale && c.cvalid;
     for (int y = 0; y < c.h; y += 16)
       for (int x = 0; x < c.w; x += 16) {
         ReconTile t{};
         t.x = (int16_t)(c.x + x); t.y = (int16_t)(c.y + y);
         t.w = (uint8_t)std::min(16, c.w - x); t.h = (uint8_t)std::min(16, c.h - y);
-        t.comps = (uint8_t)((c.yvalid ? 1 : 0) | (c.cvalid ? 2 : 0));
-        out.inter_tiles.push_back(t);
+        t.comps = (uint8_t)((c.yvalid ? 1 : 0) | (c.cvalid && !chromaStep ? 2 : 0));
+        if (t.comps) out.inter_tiles.push_back(t);
       }
     if (c.yvalid) mark(0, c.x, c.y, c.w, c.h, 0, true);
-    if (c.cvalid) mark(1, c.cx, c.cy, c.cw, c.ch, 0, true);
+    if (c.cvalid && !chromaStep) mark(1, c.cx, c.cy, c.cw, c.ch, 0, true);
+    if (chromaStep) {
+      int id[3] = {-1, -1, -1}, lev = 0;
+      for (int comp = 1; comp < 3; comp++) {
+        IntraJob j = base(c, comp);
+        j.x = j.cx; j.y = j.cy; j.w = j.cw; j.h = j.ch;
+        j.xkind = XK_INTER_CHROMA;
+        const int l = 1 + set_cscale(j, c.x, c.y);
+        id[comp] = push(l, j);
+        lev = std::max(lev, l);
+      }
+      mark(1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
+      mark(1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
+    }
   }
 
   void intra_luma(int ci) {
@@ -207,6 +241,7 @@ struct Planner {
           const int lx = 2 * j.x, ly = 2 * j.y;
           lev = std::max(lev, max_level(0, 0, lx - 4, ly - 4, lx + 4 * j.w - 1, ly + 4 * j.h - 1));
         }
+        if (cscale && j.w * j.h > 4) lev = std::max(lev, set_cscale(j, 2 * j.x, 2 * j.y));
         lev += 1;
         const int id = push(lev, j);
         mark(1, j.x, j.y, j.w, j.h, lev, true, comp, id);
@@ -376,7 +411,8 @@ struct Planner {
       }
       out.dep_start[i + 1] = (int32_t)out.deps.size();
     }
-    for (IntraJob &j : out.jobs) resolve_availability(j);
+    for (IntraJob &j : out.jobs)
+      if (j.xkind != XK_INTER_CHROMA) resolve_availability(j);   // inter chroma steps read no reference samples
   }
 };
 
@@ -384,8 +420,8 @@ struct Planner {
 
 void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out) {
   out.clear();
-  if (pp.lmcs_enabled) throw VvcrError(VVCR_E_UNSUPPORTED, "LMCS reconstruction is not supported yet");
   auto P = std::make_unique<Planner>(sp, pp, d, out);
+  P->cscale = pp.lmcs_enabled && pp.lmcs_chroma_scale;
   P->run();
 }
 
