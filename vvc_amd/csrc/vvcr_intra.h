@@ -48,9 +48,9 @@ struct IntraJob {
   // the CU at the top-left of the block's 64x64 VPDU, whose left column / above row (64 samples each,
   // reconstructed, mapped domain) give the scale; vnb = CS_* bits
   int16_t vx, vy;
-  uint8_t vnb;
+  uint8_t vnb;            // CS_* bits (chroma scaling; reference-fill fast path)
   uint8_t xkind;          // XK_*: step kinds beyond the intra prediction modes
-  uint8_t pad[2];
+  uint8_t nul, nut;       // CS_PREFIX: available left / top reference units, counted from the corner
 };
 static_assert(sizeof(IntraJob) == 48, "IntraJob layout");
 
@@ -58,6 +58,9 @@ enum : uint8_t {
   CS_LEFT = 1 << 0,       // left neighbour CU exists (getCURestricted)
   CS_ABOVE = 1 << 1,      // above neighbour CU exists
   CS_SCALE = 1 << 2,      // scale this chroma block's residual
+  CS_PREFIX = 1 << 3,     // availability = corner + a prefix of each line (nul / nut units): fast fill
+  CS_CORNER = 1 << 4,     // CS_PREFIX: the corner unit is available
+  CS_INTILE = 1 << 5,     // every available reference sample lies inside the step's CTU (LDS only)
 };
 enum : uint8_t {
   XK_NONE = 0,

@@ -216,7 +216,7 @@ __device__ __forceinline__ void gather(const Src &s, const int (&x)[N], const in
 // its own samples: available ones are copied, then missing ones read their source from the lines.
 __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int ch, int fx, int fy, int predSize, int predHSize,
                                           int mrl, int bd, uint64_t lo, bool hi, int16_t *top, int16_t *left, int lane,
-                                          unsigned long long *ps) {
+                                          unsigned long long *ps, int vnb = 0, int nul = 0, int nut = 0) {
   (void)ps;
   const int lu = ch ? 1 : 2;   // log2 of the unit size
   const int totalLeft = (predHSize + (1 << lu) - 1) >> lu;
@@ -227,6 +227,58 @@ __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int c
     for (int j = lane; j <= nT; j += 64) top[j] = dc;
     for (int i = lane; i <= nL; i += 64) left[i] = dc;
     wsync();
+    return;
+  }
+  if (vnb & CS_PREFIX) {
+    // Availability is the corner plus a run of units from the corner along each line (the usual case):
+    // copy the available samples, then every missing run takes one sample (the scan rule below reduces to
+    // three sources: the left tail, the corner unit, the top tail).
+    const bool cAv = (vnb & CS_CORNER) != 0;
+    const int aT = mrl + (nut << lu), aL = mrl + (nul << lu);   // last available index of each line
+    auto avT = [&](int j) { return j <= mrl ? cAv : j <= aT; };
+    auto avL = [&](int i) { return i <= mrl ? cAv : i <= aL; };
+    if (vnb & CS_INTILE) {   // all available samples in the LDS tile: plain LDS reads
+      const int b = src.base + (oy - src.y0) * src.ts + (ox - src.x0);
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const int j = lane + 64 * r;
+        if (j <= nT && avT(j)) top[j] = s_tile[b + j];
+        if (j <= nL && avL(j)) left[j] = s_tile[b + j * src.ts];
+      }
+    } else {
+      int gx[6], gy[6], gvv[6];
+      bool need[6];
+      const int cy = max(oy, 0), cx = max(ox, 0);
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const int j = lane + 64 * r;
+        gx[r] = min(max(ox + j, 0), D.w - 1); gy[r] = cy; need[r] = j <= nT && avT(j);
+        gx[3 + r] = cx; gy[3 + r] = min(max(oy + j, 0), D.h - 1); need[3 + r] = j <= nL && avL(j);
+      }
+      gather(src, gx, gy, need, gvv);
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const int j = lane + 64 * r;
+        if (need[r]) top[j] = (int16_t)gvv[r];
+        if (need[3 + r]) left[j] = (int16_t)gvv[3 + r];
+      }
+    }
+    wsync();
+    if (!cAv || aT < nT || aL < nL) {
+      // sources (IntraPrediction.cpp:913-1149 scan: bottom-left -> corner -> top-right): a missing unit
+      // takes the last available sample before it in scan order, else the first available one
+      const int16_t firstAv = nul ? left[aL] : (cAv ? left[mrl] : top[mrl + 1]);
+      const int16_t sCorner = nul ? left[mrl + 1] : top[mrl + 1];
+      const int16_t sTop = nut ? top[aT] : (cAv ? top[mrl] : left[mrl + 1]);
+      wsync();
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const int j = lane + 64 * r;
+        if (j <= nT && !avT(j)) top[j] = j <= mrl ? sCorner : sTop;
+        if (j <= nL && !avL(j)) left[j] = j <= mrl ? sCorner : firstAv;
+      }
+      wsync();
+    }
     return;
   }
   // unit of top sample j / left sample i
@@ -251,6 +303,7 @@ __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int c
 #pragma unroll
     for (int r = 0; r < 3; r++) { tv[r] = (int16_t)gvv[r]; lv[r] = (int16_t)gvv[3 + r]; }
   }
+  IPROF(8);
   bool missing = false;
 #pragma unroll
   for (int r = 0; r < 3; r++) {
@@ -260,6 +313,7 @@ __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int c
   }
   if (__ballot(missing) == 0) { wsync(); return; }
   wsync();
+  IPROF(9);
   // missing units: the scan-order last sample of the nearest earlier available unit, else the first
   // sample of the first available unit (both are copied samples)
   const int firstAv = lo ? __builtin_ctzll(lo) : 64;
@@ -487,11 +541,11 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   {
     int16_t *top = S.refU[0], *left = S.refU[1];
     if (!isp) {
-      if (!interc) fill_refs(SD, D, ch, x0, y0, topLen, leftLen, mrl, bd, avlo, avhi, top, left, lane, ps);
+      if (!interc) fill_refs(SD, D, ch, x0, y0, topLen, leftLen, mrl, bd, avlo, avhi, top, left, lane, ps, J.vnb, J.nul, J.nut);
     } else if (kreg == 0) {
       // CU-level fill of the first region (predSize per split direction), kept in refF for the others
       const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
-      fill_refs(SD, D, 0, J.cx, J.cy, fTop, fLeft, 0, bd, avlo, avhi, top, left, lane, ps);
+      fill_refs(SD, D, 0, J.cx, J.cy, fTop, fLeft, 0, bd, avlo, avhi, top, left, lane, ps, J.vnb, J.nul, J.nut);
       if (nreg > 1)
         for (int i = lane; i < RB; i += 64) { S.refF[0][i] = top[i]; S.refF[1][i] = left[i]; }
     } else {
@@ -1004,7 +1058,7 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
       if (lj >= nj) break;
       const int gj = j0 + lj;
       const IntraJob J = jobs[gj];
-      unsigned long long t_ready = 0, ps[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      unsigned long long t_ready = 0, ps[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef VVCR_INTRA_PROF
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1035,11 +1089,11 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
           g_iprof[slot][1] = t_ready;
           g_iprof[slot][2] = __builtin_amdgcn_s_memrealtime();
           g_iprof[slot][3] = (ps[1] - ps[0]) | (ps[2] - ps[0]) << 16 | (ps[3] - ps[0]) << 32 | (ps[4] - ps[0]) << 48;
-          g_iprof[slot][4] = (ps[5] - ps[0]) | (ps[6] - ps[0]) << 16 | (ps[7] - ps[0]) << 32;
+          g_iprof[slot][4] = (ps[5] - ps[0]) | (ps[6] - ps[0]) << 16 | (ps[7] - ps[0]) << 32 | (ps[8] - ps[0]) << 48;
           g_iprof[slot][5] = (unsigned long long)J.comp | (unsigned long long)J.w << 8 | (unsigned long long)J.h << 16 |
                              (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40;
           g_iprof[slot][6] = (unsigned long long)gj | (unsigned long long)blockIdx.x << 32;
-          g_iprof[slot][7] = (unsigned long long)(dep_start[gj + 1] - dep_start[gj]);
+          g_iprof[slot][7] = ps[9] - ps[0];
         }
       }
 #endif

@@ -259,7 +259,12 @@ struct Planner {
   }
   // xFillReferenceSamples unit scan (IntraPrediction.cpp:913-986, isAboveAvailable etc. :1208-1310):
   // returns the 65-bit availability mask in (lo, hi)
-  void fill_mask(int ch, int sq, int fx, int fy, int fw, int fh, int predSize, int predHSize, uint64_t &lo, uint32_t &hi) const {
+  struct FillShape {
+    bool prefix, corner;
+    int nul, nut;
+  };
+  void fill_mask(int ch, int sq, int fx, int fy, int fw, int fh, int predSize, int predHSize, uint64_t &lo, uint32_t &hi,
+                 FillShape *shape = nullptr) const {
     const int uw = ch ? 2 : 4, uh = uw;
     const int totalAbove = (predSize + uw - 1) / uw, totalLeft = (predHSize + uh - 1) / uh;
     const int numAbove = std::max(fw / uw, 1), numLeft = std::max(fh / uh, 1);
@@ -275,6 +280,16 @@ struct Planner {
     if (total > 65) throw VvcrError(VVCR_E_STATE, "intra plan: more than 65 reference units");
     for (int u = 0; u < total; u++)
       if (F[u]) { if (u < 64) lo |= 1ull << u; else hi |= 1u << (u - 64); }
+    if (shape) {   // corner + leading runs of each line; prefix if nothing is available after a gap
+      FillShape &S = *shape;
+      S.corner = F[totalLeft];
+      S.nut = 0; S.nul = 0;
+      while (S.nut < totalAbove && F[totalLeft + 1 + S.nut]) S.nut++;
+      while (S.nul < totalLeft && F[totalLeft - 1 - S.nul]) S.nul++;
+      S.prefix = true;
+      for (int i = S.nut; i < totalAbove; i++) if (F[totalLeft + 1 + i]) S.prefix = false;
+      for (int i = S.nul; i < totalLeft; i++) if (F[totalLeft - 1 - i]) S.prefix = false;
+    }
   }
   // CCLM neighbourhood (above / left complete, above-right / below-left unit counts): 12 bits
   uint32_t nb_bits(int ch, int sq, int x, int y, int w, int h, int unit) const {
@@ -293,11 +308,26 @@ struct Planner {
     const bool isp = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0, ver = (j.flags & IJ_ISP_VER) != 0;
     uint64_t lo;
     uint32_t hi;
+    FillShape fs;
+    int fx, fy, mrl = comp ? 0 : j.mrl;
     if (!isp) {
-      fill_mask(ch, j.seq, j.x, j.y, j.w, j.h, 2 * j.w, 2 * j.h, lo, hi);
+      fill_mask(ch, j.seq, j.x, j.y, j.w, j.h, 2 * j.w, 2 * j.h, lo, hi, &fs);
+      fx = j.x; fy = j.y;
     } else {
       const int fTop = ver ? 2 * j.cw : j.cw + j.w, fLeft = ver ? j.ch + j.h : 2 * j.ch;
-      fill_mask(0, j.seq, j.cx, j.cy, j.cw, j.ch, fTop, fLeft, lo, hi);
+      fill_mask(0, j.seq, j.cx, j.cy, j.cw, j.ch, fTop, fLeft, lo, hi, &fs);
+      fx = j.cx; fy = j.cy; mrl = 0;
+    }
+    if (fs.prefix && fs.nul < 256 && fs.nut < 256) {
+      j.vnb |= CS_PREFIX | (fs.corner ? CS_CORNER : 0);
+      j.nul = (uint8_t)fs.nul; j.nut = (uint8_t)fs.nut;
+      // the available samples: top row x in [ox, ox + mrl + nut * unit], left column y in [oy, oy + mrl + nul * unit]
+      const int us = ch ? 2 : 4, ox = fx - 1 - mrl, oy = fy - 1 - mrl;
+      const int s = ch ? 1 : 0, t0x = (j.cx << s) >> sp.ctu_log2 << sp.ctu_log2 >> s, t0y = (j.cy << s) >> sp.ctu_log2 << sp.ctu_log2 >> s;
+      const int tw = ctu >> s;
+      const int xe = ox + mrl + fs.nut * us, ye = oy + mrl + fs.nul * us;
+      const bool any = fs.corner || fs.nut || fs.nul;
+      if (!any || (ox >= t0x && oy >= t0y && xe < t0x + tw && ye < t0y + tw)) j.vnb |= CS_INTILE;
     }
     j.av[0] = (uint32_t)lo;
     j.av[1] = (uint32_t)(lo >> 32);
