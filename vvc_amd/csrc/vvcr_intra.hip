@@ -218,6 +218,9 @@ __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int c
                                           int mrl, int bd, uint64_t lo, bool hi, int16_t *top, int16_t *left, int lane,
                                           unsigned long long *ps, int vnb = 0, int nul = 0, int nut = 0) {
   (void)ps;
+#ifdef VVCR_ABL_FILL
+  return;
+#endif
   const int lu = ch ? 1 : 2;   // log2 of the unit size
   const int totalLeft = (predHSize + (1 << lu) - 1) >> lu;
   const int ox = fx - 1 - mrl, oy = fy - 1 - mrl;   // corner sample of the reference line
@@ -372,21 +375,25 @@ __device__ __forceinline__ NbAvail nb_decode(uint32_t b) {
   return r;
 }
 
+// Polling interval (s_sleep units of 64 cycles). A polling wave competes with the working waves of its CU
+// for instruction issue, so the waits sleep between polls.
+#ifndef VVCR_LSLEEP
+#define VVCR_LSLEEP 1
+#endif
+#ifndef VVCR_GSLEEP
+#define VVCR_GSLEEP 2
+#endif
 // bounded spin on a flag; sets *err and gives up after ~seconds (never expected)
 __device__ __forceinline__ void wait_global(const int32_t *f, int32_t *err) {
   for (int it = 1; __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0; it++) {
-#ifdef VVCR_DIAG_SLEEP
-    __builtin_amdgcn_s_sleep(VVCR_DIAG_SLEEP);
-#else
-    __builtin_amdgcn_s_sleep(2);
-#endif
+    __builtin_amdgcn_s_sleep(VVCR_GSLEEP);
     if ((it & 1023) == 0 && __builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
     if (it > (1 << 22)) { atomicOr(err, 1); break; }
   }
 }
 __device__ __forceinline__ void wait_local(int v, int32_t *err) {
   for (int it = 1; __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_ldone[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0; it++) {
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(VVCR_LSLEEP);
     if ((it & 1023) == 0 && __builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
     if (it > (1 << 24)) { atomicOr(err, 1); break; }
   }
@@ -640,6 +647,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   const int16_t *left = refFilter ? S.refF[1] : S.refU[1];
 #define predv(q) S.pred[lane + 64 * (q)]
 
+#ifndef VVCR_ABL_PRED
   if (interc) {
     // ---------------- chroma of an inter CU (LMCS chroma residual scaling): the MC prediction
     const DPlane &PI = P.pred[comp];
@@ -960,12 +968,14 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   wsync();
   if (gj == 0 && kreg == 0 && lane < 64) g_dbg[64 + lane] = S.pred[lane];
 #endif
+#endif
   if (kreg == 0) IPROF(5);
   // ---- CIIP blend (geneWeightedPred) and reconstruction into the LDS tile and the picture
   const DPlane &PP = P.pred[comp];
   const int tb = tile_base(comp), tp = tile_pitch(comp);
   const bool publish = (J.flags & IJ_PUBLISH) != 0;
   wsync();   // pred[] of other lanes
+#ifndef VVCR_ABL_RECON
   for (int k = 2 * lane; k < n; k += 128) {   // sample pairs (w and x0 are even)
     const int yy = k >> lw_, xx = k & (w - 1);
     int v2[2];
@@ -990,6 +1000,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
     // issue none.
     if (publish) st_sc1(D.p + (size_t)(y0 + yy) * D.stride + x0 + xx, pk);
   }
+#endif
   wsync();
   }   // regions
   IPROF(6);

@@ -12,6 +12,7 @@
 #include <array>
 #include <cstring>
 #include <memory>
+#include <queue>
 #include <string>
 
 namespace {
@@ -400,12 +401,52 @@ struct Planner {
       const int lx = j.cx << s, ly = j.cy << s;   // CU position in luma samples (a CU never crosses a CTU)
       ctu_of_job[i] = (ly >> sp.ctu_log2) * wc + (lx >> sp.ctu_log2);
     }
-    std::vector<int32_t> perm(nj);
-    for (int i = 0; i < nj; i++) perm[i] = i;
-    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) {
-      if (ctu_of_job[a] != ctu_of_job[b]) return ctu_of_job[a] < ctu_of_job[b];
-      return jobs[a].first < jobs[b].first;
-    });
+    // Take order inside a CTU: a topological order that prefers the steps with the longest chain of
+    // dependent work behind them (list scheduling by bottom level). The kernel's waves take steps in this
+    // order, so the critical chain is started as early as its dependencies allow. Step costs are rough
+    // estimates in microseconds (measured per step kind on MI355X, tools/iprof_ctu.py).
+    std::vector<double> bl(nj, 0.0);
+    {
+      std::vector<std::vector<int32_t>> succ(nj);
+      for (int i = 0; i < nj; i++)
+        for (int32_t dd : deps[i]) succ[dd].push_back(i);
+      for (int i = nj - 1; i >= 0; i--) {   // creation order is topological (dependencies are earlier)
+        const IntraJob &j = jobs[i].second;
+        const bool isp = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0;
+        double c = 3.0 + 0.002 * j.w * j.h * (isp ? j.isp_k : 1) + (isp ? 1.6 * (j.isp_k - 1) : 0.0) +
+                   ((j.flags & IJ_MIP) ? 2.5 : 0.0) + ((j.comp && j.mode >= 67) ? 3.0 : 0.0);
+        double m = 0.0;
+        for (int32_t t : succ[i]) m = std::max(m, bl[t]);
+        bl[i] = c + m;
+      }
+    }
+    std::vector<int32_t> perm;
+    perm.reserve(nj);
+    {
+      std::vector<int32_t> byCtu(nj);
+      for (int i = 0; i < nj; i++) byCtu[i] = i;
+      std::stable_sort(byCtu.begin(), byCtu.end(), [&](int32_t a, int32_t b) { return ctu_of_job[a] < ctu_of_job[b]; });
+      std::vector<int32_t> indeg(nj, 0);
+      std::vector<std::vector<int32_t>> succLocal(nj);
+      for (int i = 0; i < nj; i++)
+        for (int32_t dd : deps[i])
+          if (ctu_of_job[dd] == ctu_of_job[i]) { indeg[i]++; succLocal[dd].push_back(i); }
+      for (size_t a = 0; a < byCtu.size();) {
+        size_t b = a;
+        while (b < byCtu.size() && ctu_of_job[byCtu[b]] == ctu_of_job[byCtu[a]]) b++;
+        auto cmp = [&](int32_t x, int32_t y) { return bl[x] < bl[y] || (bl[x] == bl[y] && x > y); };
+        std::priority_queue<int32_t, std::vector<int32_t>, decltype(cmp)> ready(cmp);
+        for (size_t k = a; k < b; k++) if (indeg[byCtu[k]] == 0) ready.push(byCtu[k]);
+        while (!ready.empty()) {
+          const int32_t x = ready.top();
+          ready.pop();
+          perm.push_back(x);
+          for (int32_t t : succLocal[x]) if (--indeg[t] == 0) ready.push(t);
+        }
+        a = b;
+      }
+      if ((int)perm.size() != nj) throw VvcrError(VVCR_E_STATE, "intra plan: dependency cycle inside a CTU");
+    }
     std::vector<int32_t> rank(nj);
     for (int i = 0; i < nj; i++) rank[perm[i]] = i;
     out.jobs.resize(nj);
