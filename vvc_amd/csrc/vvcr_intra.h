@@ -23,7 +23,7 @@ enum : uint8_t {
   IJ_PUBLISH = 1 << 7,    // a step of another CTU reads this one: drain its stores, raise its global flag
 };
 
-constexpr int kIntraMaxStepsPerCtu = 4096;   // LDS done-flag bytes of k_intra
+constexpr int kIntraMaxStepsPerCtu = 2048;   // LDS done-flag bytes of k_intra (a 128x128 CTU has at most ~1600 steps)
 
 // One reconstruction step: predict a region, add the residual plane, clip, store into the picture.
 struct IntraJob {

@@ -102,7 +102,7 @@ __device__ __forceinline__ int wave_sum(int v) {
 // only steps that such a read depends on (IJ_PUBLISH) drain their HBM stores and raise a global flag.
 // ------------------------------------------------------------------------------------------------
 #ifndef VVCR_DIAG_NW
-constexpr int NW = 4; 
+constexpr int NW = 6; 
 #else
 constexpr int NW = VVCR_DIAG_NW;
 #endif
@@ -115,11 +115,10 @@ struct WaveScratch {
   int16_t refF[2][RB];          // filtered
   int16_t mainA[EXT + RB + 64]; // angular main reference (with negative indices)
   int16_t sideA[EXT + RB + 64];
-  int32_t aux[64 * 64 / 4];     // MIP reduced pred / CCLM down-sampled luma
+  int16_t aux[64 * 64 / 4];     // MIP reduced pred / CCLM down-sampled luma
   int16_t tmpl[2][132];         // CCLM down-sampled luma: top row / left column
   int32_t lmp[4];
   int32_t red[8];               // MIP reduced boundary
-  int16_t pred[64 * 64];
   int16_t resL[64 * 64];        // residual of the step, prefetched at entry
   int16_t ispPrev[64];          // ISP: last row / column of the previous region
 };
@@ -645,7 +644,10 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
 #endif
   const int16_t *top = refFilter ? S.refF[0] : S.refU[0];
   const int16_t *left = refFilter ? S.refF[1] : S.refU[1];
-#define predv(q) S.pred[lane + 64 * (q)]
+  // The prediction is written straight into the block's area of the LDS tile (nobody reads that area
+  // before this step is done) and the reconstruction then adds the residual in place.
+  const int ptb = tile_base(comp) + (y0 - G.cy0(comp)) * tile_pitch(comp) + (x0 - G.cx0(comp)), ptp = tile_pitch(comp);
+#define predv(q) s_tile[ptb + ((lane + 64 * (q)) >> lw_) * ptp + ((lane + 64 * (q)) & (w - 1))]
 
 #ifndef VVCR_ABL_PRED
   if (interc) {
@@ -837,8 +839,6 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
     wsync();
     const int upH = w / rp, upV = h / rp;
     // horizontal upsampling into rows (r+1)*upV-1 (predictionUpsampling :252-277), kept in aux2 region
-    int *full = S.aux + 64;   // w*h <= 64*64? MIP blocks <= 64x64: use registers per sample instead
-    (void)full;
     for (int k = lane, q = 0; k < n; k += 64, q++) {
       const int yy = k >> lw_, xx = k & (w - 1);
       // value of the horizontally upsampled row grid at (rowIdx, xx) where rowIdx in [0, rp)
@@ -966,7 +966,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
 
 #ifdef VVCR_DIAG_DUMP
   wsync();
-  if (gj == 0 && kreg == 0 && lane < 64) g_dbg[64 + lane] = S.pred[lane];
+  if (gj == 0 && kreg == 0 && lane < 64) g_dbg[64 + lane] = s_tile[ptb + (lane >> lw_) * ptp + (lane & (w - 1))];
 #endif
 #endif
   if (kreg == 0) IPROF(5);
@@ -981,7 +981,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
     int v2[2];
 #pragma unroll
     for (int e = 0; e < 2; e++) {
-      int pv = S.pred[k + e];
+      int pv = s_tile[ptb + yy * ptp + xx + e];
       if (ciip) {
         int ip = pel(PP, x0 + xx + e, y0 + yy);
         if (comp == 0 && (P.lmcs & 1)) ip = P.lmcs_fwd[ip];   // LMCS: mapped inter prediction (DecCu.cpp:696)
