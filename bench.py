@@ -157,6 +157,8 @@ def main():
         traffic = tj.get("per_group_launch_bytes", {}).get(dom)   # profiles/: tools/pmc.sh + tools/pmc_summary.py
 
     ms_step = elapsed / a.steps * 1e3
+    kind, qp = a.stream.split("_")[0], a.stream.split("_")[-1]
+    desc = "%s %s" % ("random access" if kind.startswith("ra") else "all intra", qp.replace("q", "QP"))
     value = world * px_seq * a.steps / elapsed / 1e6
     line = {
         "metric": "decode Mpixels/sec (CABAC on host), bit-exact YUV vs DecoderApp, 1/2/4/8 GPU",
@@ -170,8 +172,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int16",
-        "data": "synthetic (VTM-7.3-encoded synthetic 1080p RA QP32 stream, parsed descriptors resident in HBM)",
-        "config": {"workload": "%s: %dx%d random access QP32, %d pictures, reconstruction + DBK/SAO/ALF" % (a.stream, W, H, len(pics)),
+        "data": "synthetic (VTM-7.3-encoded synthetic %dx%d %s stream, parsed descriptors resident in HBM)" % (W, H, desc),
+        "config": {"workload": "%s: %dx%d %s, %d pictures, reconstruction + DBK/SAO/ALF" % (a.stream, W, H, desc, len(pics)),
                    "parallelism": "replicas%d" % world, "bitexact_vs_reference": bool(bitexact)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic},
