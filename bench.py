@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 from vvc_amd import native as N  # noqa: E402
 from vvc_amd import stream as S  # noqa: E402
 from vvc_amd import decode as D  # noqa: E402
+from vvc_amd import dist as V  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (guides/MI355X_MICROARCH.md)
 
@@ -60,17 +61,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend)
+    R = V.Ranks()
+    world, rank, local = R.world, R.rank, R.local
 
     d = os.path.join(ROOT, "tests", "golden", a.stream)
     pics = S.load_sequence(d)
@@ -80,7 +72,7 @@ def main():
     px_seq = W * H * len(pics)
 
     # ---- prepare every picture once (host planning + upload), decoding order, own DPB slots
-    dec = D.Decoder(pics, dpb_slots=12, device=local)
+    dec = D.Decoder(pics, dpb_slots=12, device=int(os.environ.get("VVCR_DEVICE", local)))   # VVCR_DEVICE: rehearsal of N ranks on one GPU
     ctx = dec.ctx
     handles, slots = [], []
     t_prep = time.perf_counter()
@@ -114,24 +106,15 @@ def main():
         run_step()
     ctx.sync()
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
+    R.barrier()
     ctx.sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         run_step()
     ctx.sync()
     t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    R.barrier()
+    elapsed = R.max_over_ranks(t1 - t0)
 
     # ---- per-kernel timing of the last step (HIP events on the library stream)
     kern = {}
@@ -159,7 +142,7 @@ def main():
     ms_step = elapsed / a.steps * 1e3
     kind, qp = a.stream.split("_")[0], a.stream.split("_")[-1]
     desc = "%s %s" % ("random access" if kind.startswith("ra") else "all intra", qp.replace("q", "QP"))
-    value = world * px_seq * a.steps / elapsed / 1e6
+    value = V.job_throughput(px_seq * a.steps, elapsed, R) / 1e6
     line = {
         "metric": "decode Mpixels/sec (CABAC on host), bit-exact YUV vs DecoderApp, 1/2/4/8 GPU",
         "value": round(value, 2),
@@ -191,8 +174,7 @@ def main():
     dec.close()
     if rank == 0:
         print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
+    R.close()
     if not bitexact:
         sys.exit("bench: output is not bit-exact to the reference decoder")
 
