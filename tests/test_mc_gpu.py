@@ -14,9 +14,10 @@ from helpers import cu_mask, is_inter
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["ra416_q32"])
+@pytest.mark.parametrize("name", ["ra416_q32", "rawp416_q32"])
 def test_mc_matches_reference(golden_dir, name):
-    """Every inter CU (uni/bi/BCW, SbTMVP, GEO, affine+PROF, DMVR, BDOF) and the DMVR deltas."""
+    """Every inter CU (uni/bi/BCW, SbTMVP, GEO, affine+PROF, DMVR, BDOF; explicit weighted prediction in
+    rawp416_q32) and the DMVR deltas."""
     d = os.path.join(golden_dir, name)
     pics = S.load_sequence(d)
     by_poc = {p["hdr"]["poc"]: p for p in pics}

@@ -12,7 +12,7 @@ from vvc_amd import stream as S
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["ai416_q37", "ra416_q32", "ailm416_q37", "ralm416_q32"])
+@pytest.mark.parametrize("name", ["ai416_q37", "ra416_q32", "ailm416_q37", "ralm416_q32", "rawp416_q32"])
 def test_reconstruction_matches_reference(golden_dir, name):
     pics = S.load_sequence(os.path.join(golden_dir, name))
     by_poc = {p["hdr"]["poc"]: p for p in pics}

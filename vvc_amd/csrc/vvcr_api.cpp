@@ -154,7 +154,7 @@ static int n_ctb(const vvcr_seq_params &sp) {
   return ((sp.width + ctu - 1) / ctu) * ((sp.height + ctu - 1) / ctu);
 }
 
-static McParams make_mc_params(vvcr_ctx *ctx) {
+static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp) {
   McParams P{};
   for (size_t s = 0; s < ctx->dpb.size() && s < 32; s++)
     for (int c = 0; c < 3; c++) P.ref[s][c] = ctx->dpb[s][c];
@@ -163,6 +163,16 @@ static McParams make_mc_params(vvcr_ctx *ctx) {
   P.pic_h = ctx->sp.height;
   P.bd = ctx->sp.bit_depth;
   P.ctu = 1 << ctx->sp.ctu_log2;
+  // WeightPrediction::getWpScaling (WeightPrediction.cpp:125-152): offsets scaled to the bit depth
+  const int osc = 1 << (ctx->sp.bit_depth - 8);
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < VVCR_MAX_REF; i++)
+      for (int c = 0; c < 3; c++) {
+        const int32_t *e = pp.wp[l][i][c];
+        P.wp.d[l][i][c] = (int8_t)e[1];
+        P.wp.w[l][i][c] = (int16_t)e[2];
+        P.wp.o[l][i][c] = (int16_t)(e[3] * osc);
+      }
   return P;
 }
 
@@ -326,7 +336,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     r.launches[K_RESID] = (r.n_tb_small > 0) + (r.n_tb > r.n_tb_small);
   }
   if (mask & VVCR_STAGE_INTER) {
-    const McParams mp = make_mc_params(ctx);
+    const McParams mp = make_mc_params(ctx, r.pp);
     {
       KernelTimer t(r, K_MC, s);
       launch_mc_basic(mp, r.mc_basic.p, r.n_basic, s);

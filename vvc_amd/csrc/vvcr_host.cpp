@@ -48,6 +48,22 @@ McJob make_job(const vvcr_pic_params &pp, int interDir, int r0, int r1, int mv0x
   return j;
 }
 
+// Explicit weighted prediction replaces the default combine (InterPrediction::xPredInterBi,
+// InterPrediction.cpp:633-678): P slices with the PPS weighted_pred flag (uni), B slices with
+// weighted_bipred (uni, and bi unless DMVR / BDOF / a non-default BcwIdx of the CU take over; GEO never).
+bool wp_applies(const vvcr_pic_params &pp, bool bi, int cu_bcw) {
+  if (pp.slice_type == 1) return pp.wp_p != 0;
+  if (pp.slice_type == B_SLICE && pp.wp_b) return !bi || cu_bcw == 2;
+  return false;
+}
+
+void set_wp(const vvcr_pic_params &pp, McJob &j, int r0, int r1, int cu_bcw) {
+  const bool bi = (j.flags & (MC_L0 | MC_L1)) == (MC_L0 | MC_L1);
+  if (!wp_applies(pp, bi, cu_bcw)) return;
+  j.flags |= MC_WP;
+  j.ridx = (uint8_t)(((j.flags & MC_L0) ? r0 : 0) | ((j.flags & MC_L1) ? r1 : 0) << 4);
+}
+
 }  // namespace
 
 void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d) {
@@ -134,6 +150,7 @@ AffList affine_list(const vvcr_pic_params &pp, const vvcr_cu &c, const vvcr_pu &
   const int ref = l ? p.ref1 : p.ref0;
   A.present = 1;
   A.slot = pp.ref_slot[l][ref];
+  A.ridx = ref;
   const int *mv = &p.aff[l * 6];   // LT, RT, LB
   const int iBit = 7;
   const int lw = ilog2i(p.w), lh = ilog2i(p.h);
@@ -166,10 +183,6 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   std::vector<int> geo_of(d.cu.size(), -1);
   for (size_t g = 0; g < d.geo.size(); g++)
     if (d.geo[g].cu >= 0 && d.geo[g].cu < (int)d.cu.size()) geo_of[d.geo[g].cu] = (int)g;
-  if ((pp.slice_type == 1 && pp.wp_p) || (pp.slice_type == B_SLICE && pp.wp_b)) {
-    for (const vvcr_cu &c : d.cu) if (c.predmode == MODE_INTER && c.yvalid) wl.n_unsupported_inter++;
-    return;   // explicit weighted prediction: not built yet
-  }
   for (size_t ci = 0; ci < d.cu.size(); ci++) {
     const vvcr_cu &c = d.cu[ci];
     if (c.predmode != MODE_INTER || !c.yvalid) continue;
@@ -212,6 +225,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
           for (int x = 0; x < p.w; x += 8) {
             const vvcr_motion &m = d.motion[(size_t)((p.y + y) >> 2) * W4 + ((p.x + x) >> 2)];
             McJob j = make_job(pp, m.inter_dir, m.ref0, m.ref1, m.mv0x, m.mv0y, m.mv1x, m.mv1y, bcw, alt);   // BCW of the CU (xWeightedAverage reads pu.cu->BcwIdx)
+            set_wp(pp, j, m.ref0, m.ref1, c.bcw);
             push_tiles(wl.mc_basic, p.x + x, p.y + y, std::min(8, p.w - x), std::min(8, p.h - y), j);
           }
         continue;
@@ -222,6 +236,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
         U.bcw = bcw;
         if (p.interdir & 1) U.l[0] = affine_list(pp, c, p, 0);
         if (p.interdir & 2) U.l[1] = affine_list(pp, c, p, 1);
+        U.wp = wp_applies(pp, p.interdir == 3, c.bcw) ? 1 : 0;
         const int idx = (int)wl.aff_pu.size();
         wl.aff_pu.push_back(U);
         for (int y = 0; y < p.h; y += 16)
@@ -257,6 +272,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
         continue;
       }
       McJob j = make_job(pp, p.interdir, p.ref0, p.ref1, p.mv0x, p.mv0y, p.mv1x, p.mv1y, bcw, alt);
+      set_wp(pp, j, p.ref0, p.ref1, c.bcw);   // the CU's BcwIdx, not the CIIP-cleared one (:664 reads pu.cu->BcwIdx)
       push_tiles(wl.mc_basic, p.x, p.y, p.w, p.h, j);
     }
   }

@@ -40,6 +40,7 @@ enum : uint16_t {
   MC_DMVR = 1 << 6,      // decoder-side MV refinement of this 16x16 sub-block (InterPrediction.cpp:2133)
   MC_KEEP14 = 1 << 7,    // write 14-bit intermediate instead of final samples
   MC_GEO = 1 << 8,       // two uni-predicted GEO parts blended by split weights (InterpolationFilter.cpp:997)
+  MC_WP = 1 << 9,        // explicit weighted prediction epilogue (WeightPrediction::addWeightUni / addWeightBi)
 };
 
 struct McJob {
@@ -49,7 +50,7 @@ struct McJob {
   int16_t mv[2][2];      // [list][hor/ver], 1/16 luma sample
   int8_t slot[2];        // DPB slot per list
   int8_t bcw;            // BcwIdx (2 = default average)
-  int8_t pad0;
+  uint8_t ridx;          // MC_WP: refIdx of list 0 | refIdx of list 1 << 4 (selects the weight table rows)
   int32_t aux;           // DMVR: index of this sub-block in the delta output buffer;
                          // GEO: angle | offsetX << 8 | offsetY << 16 (weight-mask coordinates)
   int16_t pu_x, pu_y;    // GEO: PU origin (weights are PU-relative)
@@ -65,10 +66,12 @@ struct AffList {
   int32_t dhx, dhy, dvx, dvy;          // iDMvHorX/Y, iDMvVerX/Y
   int32_t spread;                      // isSubblockVectorSpreadOverLimit
   int32_t prof;                        // PROF applies to luma
+  int32_t ridx;                        // reference index (weighted-prediction table row)
 };
 struct AffPu {
   int16_t x, y, w, h;                  // luma PU area
   int32_t bcw;                         // BcwIdx (2 = default)
+  int32_t wp;                          // explicit weighted prediction applies (uni: 14-bit kept, then addWeightUni)
   AffList l[2];
 };
 // Affine work item: one <= 16x16 luma tile (8x8-aligned inside the PU) and its chroma.
@@ -80,13 +83,39 @@ struct AffJob {
 };
 static_assert(sizeof(AffJob) == 12, "AffJob layout");
 
+// Explicit weighted-prediction table of the slice (pred_weight_table after HLSyntaxReader::
+// parsePredWeightTable: absent entries hold weight 1 << denom, offset 0): weight, offset already scaled
+// by 1 << (bitDepth - 8) (WeightPrediction::getWpScaling, WeightPrediction.cpp:125-152), log2 denominator.
+struct WpTable {
+  int16_t w[2][VVCR_MAX_REF][3];
+  int16_t o[2][VVCR_MAX_REF][3];
+  int8_t d[2][VVCR_MAX_REF][3];
+};
+
 struct McParams {
   DPlane ref[32][3];     // DPB planes by slot (only used slots valid)
   DPlane out[3];         // destination (prediction planes of the current picture)
   int32_t pic_w, pic_h;  // luma picture size
   int32_t bd;            // bit depth
   int32_t ctu;           // CTU size (affine MV clamp, InterPrediction.cpp:937)
+  WpTable wp;
 };
+
+// Weighted-prediction epilogues on 14-bit intermediates p (IF_INTERNAL_OFFS = 8192 removed), for one
+// component c and the reference indices r0 / r1; shiftNum = max(2, 14 - bd).
+// addWeightUni (WeightPrediction.cpp:280-378): weightUnidir and noWeightUnidir agree when w == 1 << d.
+__device__ __forceinline__ int wp_uni(const WpTable &T, int l, int r, int c, int p, int shiftNum, int maxv) {
+  const int w = T.w[l][r][c], o = T.o[l][r][c], shift = T.d[l][r][c] + shiftNum;
+  const int v = ((w * (p + 8192) + (1 << (shift - 1))) >> shift) + o;
+  return v < 0 ? 0 : (v > maxv ? maxv : v);
+}
+// addWeightBi (WeightPrediction.cpp:157-222) with weightBidir (:46): shift = denom + 1 + shiftNum.
+__device__ __forceinline__ int wp_bi(const WpTable &T, int r0, int r1, int c, int p0, int p1, int shiftNum, int maxv) {
+  const int shift = T.d[0][r0][c] + 1 + shiftNum;
+  const int offset = T.o[0][r0][c] + T.o[1][r1][c];
+  const int v = (T.w[0][r0][c] * (p0 + 8192) + T.w[1][r1][c] * (p1 + 8192) + (1 << (shift - 1)) + offset * (1 << (shift - 1))) >> shift;
+  return v < 0 ? 0 : (v > maxv ? maxv : v);
+}
 
 // ------------------------------------------------------------------------------------------------
 // Residual work item: one transform block (after joint Cb-Cr resolution). 32 bytes.

@@ -514,6 +514,9 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   (void)t_ready; (void)ps;
 #endif
   IPROF(1);
+#ifdef VVCR_ABL_ALL
+  return;
+#endif
   // LMCS chroma residual scale (uniform), after the wait: it reads reconstructed luma of other steps
   const int cscale = (comp > 0 && (J.vnb & CS_SCALE)) ? chroma_scale(P, G, J.vx, J.vy, J.vnb, lane) : 0;
   auto store_resid = [&]() {

@@ -160,7 +160,8 @@ __device__ void mc_component(const McParams &P, const McJob &J, int comp, int16_
   const bool alt = (J.flags & MC_ALT_HPEL) && comp == 0;
   const int bd = P.bd;
   int r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
-  const bool rnd = !bi && !keep14;
+  const bool wp = (J.flags & MC_WP) != 0;
+  const bool rnd = !bi && !keep14 && !wp;
   if (l0) predict_list<N>(P.ref[J.slot[0]][comp], bx, by, bw, bh, J.mv[0][0], J.mv[0][1], fracBits, alt, rnd, bd, win, tmp, lane, r0);
   if (l1) predict_list<N>(P.ref[J.slot[1]][comp], bx, by, bw, bh, J.mv[1][0], J.mv[1][1], fracBits, alt, rnd, bd, win, tmp, lane, bi ? r1 : r0);
   const DPlane &o = P.out[comp];
@@ -174,7 +175,9 @@ __device__ void mc_component(const McParams &P, const McJob &J, int comp, int16_
     int y = i / bw, x = i - y * bw;
     int v;
     if (!bi) {
-      v = r0[k];
+      v = wp ? wp_uni(P.wp, l0 ? 0 : 1, l0 ? (J.ridx & 15) : (J.ridx >> 4), comp, r0[k], headRoom, maxv) : r0[k];
+    } else if (wp) {
+      v = wp_bi(P.wp, J.ridx & 15, J.ridx >> 4, comp, r0[k], r1[k], headRoom, maxv);
     } else if (J.flags & MC_GEO) {
       // xWeightedGeoBlk: (w*p0 + (8-w)*p1 + offset) >> (headRoom + 3)
       const int w = geo_weight(J.aux & 31, (J.aux >> 8) & 255, (J.aux >> 16) & 255, (bx + x - (J.pu_x >> cs)) << cs,

@@ -405,7 +405,7 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
     }
     __syncthreads();
     const bool prof = A.prof;
-    const bool rnd = !prof && !bi;
+    const bool rnd = !prof && !bi && !U.wp;
     for (int k = 0; k < 4; k++) {
       const int i = lane + 64 * k;
       if (i >= w * h) break;
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
         dmy = clampi(dmy, -31, 31);
         const int dI = clampi(dmx * gX + dmy * gY, -dILimit, dILimit - 1);
         int v = (int16_t)(c14[y * 16 + x] + dI);
-        if (!bi) v = clampi((v + offset) >> shiftNum, 0, maxv);
+        if (!bi && !U.wp) v = clampi((v + offset) >> shiftNum, 0, maxv);
         res[0][l][k] = v;
       }
     }
@@ -473,12 +473,12 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
         const int y = lane / cw, x = lane - y * cw;
         const int sb = (y >> 2) * ncx + (x >> 2);
         const int fx = sbmv[sb][0] & 31, fy = sbmv[sb][1] & 31;
-        res[comp][l][0] = filt<4>(win[sb], 7, x & 3, y & 3, fx, fy, x_chroma[fx], x_chroma[fy], !bi, bd);
+        res[comp][l][0] = filt<4>(win[sb], 7, x & 3, y & 3, fx, fy, x_chroma[fx], x_chroma[fy], !bi && !U.wp, bd);
       }
       __syncthreads();
     }
   }
-  // ---- combine (xWeightedAverage: addAvg / addWeightedAvg; uni already final)
+  // ---- combine (xWeightedAverage: addAvg / addWeightedAvg; weighted prediction; uni already final without WP)
   for (int comp = 0; comp < 3; comp++) {
     const int cs = comp ? 1 : 0;
     const int bw = w >> cs, bh = h >> cs, bx = J.x >> cs, by = J.y >> cs;
@@ -489,7 +489,11 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
       const int y = i / bw, x = i - y * bw;
       int v;
       if (!bi) {
-        v = U.l[0].present ? res[comp][0][k] : res[comp][1][k];
+        const int l = U.l[0].present ? 0 : 1;
+        v = res[comp][l][k];
+        if (U.wp) v = wp_uni(P.wp, l, U.l[l].ridx, comp, v, headRoom, maxv);
+      } else if (U.wp) {
+        v = wp_bi(P.wp, U.l[0].ridx, U.l[1].ridx, comp, res[comp][0][k], res[comp][1][k], headRoom, maxv);
       } else if (U.bcw != 2) {
         const int w1 = x_bcw_w1[U.bcw], w0 = 8 - w1;
         const int shiftNum = headRoom + 3;
