@@ -420,6 +420,40 @@ struct Planner {
         bl[i] = c + m;
       }
     }
+    // Wait lists: a same-CTU dependency that another dependency of the step already reaches through
+    // same-CTU dependencies is implied (that one could only finish after it: flags are raised after the
+    // step's stores complete, LDS is coherent inside the CU), so the kernel need not poll it. Bitsets of
+    // same-CTU ancestors, in creation order (topological). Cross-CTU dependencies are all kept: they
+    // also decide which steps publish their samples to HBM.
+    std::vector<std::vector<int32_t>> wdeps(nj);
+    {
+      std::vector<int32_t> lidx(nj);   // index among the CTU's steps
+      {
+        std::vector<int32_t> cnt_of((size_t)wc * ((sp.height + (1 << sp.ctu_log2) - 1) >> sp.ctu_log2), 0);
+        for (int i = 0; i < nj; i++) lidx[i] = cnt_of[ctu_of_job[i]]++;
+      }
+      std::vector<std::vector<uint64_t>> anc(nj);
+      for (int i = 0; i < nj; i++) {
+        std::vector<uint64_t> &a = anc[i];
+        std::vector<uint64_t> implied;
+        for (int32_t dd : deps[i]) {
+          if (ctu_of_job[dd] != ctu_of_job[i]) continue;
+          const std::vector<uint64_t> &ad = anc[dd];
+          const size_t need = std::max(ad.size(), (size_t)(lidx[dd] >> 6) + 1);
+          if (a.size() < need) a.resize(need, 0);
+          if (implied.size() < ad.size()) implied.resize(ad.size(), 0);
+          for (size_t w = 0; w < ad.size(); w++) { a[w] |= ad[w]; implied[w] |= ad[w]; }
+          a[lidx[dd] >> 6] |= 1ull << (lidx[dd] & 63);
+        }
+        for (int32_t dd : deps[i]) {
+          if (ctu_of_job[dd] == ctu_of_job[i]) {
+            const int b = lidx[dd];
+            if ((size_t)(b >> 6) < implied.size() && (implied[b >> 6] >> (b & 63) & 1)) continue;
+          }
+          wdeps[i].push_back(dd);
+        }
+      }
+    }
     std::vector<int32_t> perm;
     perm.reserve(nj);
     {
@@ -473,12 +507,11 @@ struct Planner {
       for (int32_t d : deps[o]) {
         const int32_t rd = rank[d];
         if (rd >= i) throw VvcrError(VVCR_E_STATE, "intra plan: dependency is not earlier in step order");
-        if (rd >= out.ctu_start[c]) {
-          out.deps.push_back(rd - out.ctu_start[c]);
-        } else {
-          out.deps.push_back(~rd);
-          out.jobs[rd].flags |= IJ_PUBLISH;
-        }
+        if (rd < out.ctu_start[c]) out.jobs[rd].flags |= IJ_PUBLISH;
+      }
+      for (int32_t d : wdeps[o]) {
+        const int32_t rd = rank[d];
+        out.deps.push_back(rd >= out.ctu_start[c] ? rd - out.ctu_start[c] : ~rd);
       }
       out.dep_start[i + 1] = (int32_t)out.deps.size();
     }
