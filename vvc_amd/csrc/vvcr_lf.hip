@@ -5,8 +5,7 @@
 // reading the deblocked picture and writing the SAO picture (ping-pong, so neighbours are pre-SAO).
 //
 // ALF (AdaptiveLoopFilter::deriveClassificationBlk :873, filterBlk<7x7/5x5> :1085, filterBlkCcAlf :1328):
-// luma: one lane per 4x4 block = one classification + 16 filtered samples (the 8x8 Laplacian window
-// and the 7x7 diamond footprint overlap, so one lane reads a 10x10 / 10x10 neighbourhood through L1);
+// luma: one workgroup per 64x16 tile staged in LDS with its 3-sample halo (classification + filter);
 // chroma: one lane per chroma sample, 5x5 diamond and the CC-ALF luma->chroma correction fused.
 // Reads the SAO picture, writes the final picture. Coordinates are clamped to the picture
 // (equivalent to PelUnitBuf::extendBorderPel(3) on the ALF input, AdaptiveLoopFilter.cpp:411).
@@ -89,80 +88,120 @@ __constant__ int8_t c_perm7[4][13] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12}
 __constant__ int8_t c_th[16] = {0, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 4};
 __constant__ int8_t c_transpose[8] = {0, 1, 0, 2, 2, 3, 1, 3};
 
-__global__ void k_alf_luma(AlfParams P) {
+// Luma ALF, LDS-tiled: one 256-lane workgroup per 64x16 output tile. The tile plus its 3-sample halo
+// (the reach of both the 8x8 Laplacian window of a 4x4 block and the 7x7 diamond) is staged once with
+// coalesced row loads and picture-clamped coordinates; four lanes classify each 4x4 block (one
+// subsampled row pair each, reduced by shuffles), then each lane filters one column of one 4x4 block.
+constexpr int ALF_TW = 64, ALF_TH = 16, ALF_HALO = 3;
+constexpr int ALF_SW = ALF_TW + 2 * ALF_HALO + 2;   // LDS row pitch (72)
+constexpr int ALF_SH = ALF_TH + 2 * ALF_HALO;       // 22 rows
+
+__global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
   const DPlane &S = P.src[0];
   const DPlane &D = P.dst[0];
-  const int bx = (blockIdx.x * blockDim.x + threadIdx.x) * 4, by = blockIdx.y * 4;
-  if (bx >= S.w || by >= S.h) return;
-  const int ctb = (by >> P.ctu_log2) * P.wc + (bx >> P.ctu_log2);
-  const int vbH = 1 << P.ctu_log2, vbPos = P.vb_luma;
-  if (!P.en[0] || !P.ctb_en[ctb]) {
-    for (int y = by; y < by + 4 && y < S.h; y++)
-      for (int x = bx; x < bx + 4 && x < S.w; x++) D.p[(size_t)y * D.stride + x] = S.p[(size_t)y * S.stride + x];
-    return;
+  __shared__ int16_t t[ALF_SH * ALF_SW];
+  __shared__ int32_t blk[(ALF_TW / 4) * (ALF_TH / 4)];   // class | transpose << 8 | enabled << 16
+  const int X0 = blockIdx.x * ALF_TW, Y0 = blockIdx.y * ALF_TH;
+  const int tid = threadIdx.x;
+  const int W = S.w, H = S.h;
+  for (int i = tid; i < ALF_SH * (ALF_TW + 2 * ALF_HALO); i += 256) {
+    const int r = i / (ALF_TW + 2 * ALF_HALO), c = i - r * (ALF_TW + 2 * ALF_HALO);
+    const int sx = clip3(0, W - 1, X0 - ALF_HALO + c), sy = clip3(0, H - 1, Y0 - ALF_HALO + r);
+    t[r * ALF_SW + c] = S.p[(size_t)sy * S.stride + sx];
   }
-  // --- classification (4x4 block)
-  int sumV = 0, sumH = 0, sumD0 = 0, sumD1 = 0;
-  const int yv = by & (vbH - 1);
-  const int i0 = (yv == vbPos) ? 1 : 0, i1 = (yv == vbPos - 4) ? 3 : 4;
-  for (int ii = i0; ii < i1; ii++) {
-    const int ay = by - 2 + ii * 2;
-    int rA = ay - 1, rB = ay + 1, rB2 = ay + 2;
-    if (ay > 0 && (ay & (vbH - 1)) == vbPos - 2) rB2 = ay + 1;
-    else if (ay > 0 && (ay & (vbH - 1)) == vbPos) rA = ay;
-    for (int jj = 0; jj < 4; jj++) {
-      const int ax = bx - 2 + jj * 2;
-      const int a = at(S, ax, ay) << 1, b = at(S, ax + 1, ay + 1) << 1;
-      sumV += abs(a - at(S, ax, rA) - at(S, ax, rB)) + abs(b - at(S, ax + 1, ay) - at(S, ax + 1, rB2));
-      sumH += abs(a - at(S, ax + 1, ay) - at(S, ax - 1, ay)) + abs(b - at(S, ax + 2, rB) - at(S, ax, rB));
-      sumD0 += abs(a - at(S, ax - 1, rA) - at(S, ax + 1, rB)) + abs(b - at(S, ax, ay) - at(S, ax + 2, rB2));
-      sumD1 += abs(a - at(S, ax - 1, rB) - at(S, ax + 1, rA)) + abs(b - at(S, ax, rB2) - at(S, ax + 2, ay));
+  __syncthreads();
+  // sample (x, y) in picture coordinates -> LDS (valid for |x - tile| <= 3 and |y - tile| <= 3)
+#define T(x, y) ((int)t[((y) - Y0 + ALF_HALO) * ALF_SW + (x) - X0 + ALF_HALO])
+  const int vbH = 1 << P.ctu_log2, vbPos = P.vb_luma;
+  {
+    // --- classification (deriveClassificationBlk): block b, subsampled row pair ii
+    const int b = tid >> 2, ii = tid & 3;
+    const int bx = X0 + (b & 15) * 4, by = Y0 + (b >> 4) * 4;
+    const int ctb = (by >> P.ctu_log2) * P.wc + (bx >> P.ctu_log2);
+    const bool on = bx < W && by < H && P.en[0] && P.ctb_en[ctb];
+    int sumV = 0, sumH = 0, sumD0 = 0, sumD1 = 0;
+    const int yv = by & (vbH - 1);
+    const int i0 = (yv == vbPos) ? 1 : 0, i1 = (yv == vbPos - 4) ? 3 : 4;
+    if (on && ii >= i0 && ii < i1) {
+      const int ay = by - 2 + ii * 2;
+      int rA = ay - 1, rB = ay + 1, rB2 = ay + 2;
+      if (ay > 0 && (ay & (vbH - 1)) == vbPos - 2) rB2 = ay + 1;
+      else if (ay > 0 && (ay & (vbH - 1)) == vbPos) rA = ay;
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) {
+        const int ax = bx - 2 + jj * 2;
+        const int a = T(ax, ay) << 1, bb = T(ax + 1, ay + 1) << 1;
+        sumV += abs(a - T(ax, rA) - T(ax, rB)) + abs(bb - T(ax + 1, ay) - T(ax + 1, rB2));
+        sumH += abs(a - T(ax + 1, ay) - T(ax - 1, ay)) + abs(bb - T(ax + 2, rB) - T(ax, rB));
+        sumD0 += abs(a - T(ax - 1, rA) - T(ax + 1, rB)) + abs(bb - T(ax, ay) - T(ax + 2, rB2));
+        sumD1 += abs(a - T(ax - 1, rB) - T(ax + 1, rA)) + abs(bb - T(ax, rB2) - T(ax + 2, ay));
+      }
+    }
+#pragma unroll
+    for (int m = 1; m < 4; m <<= 1) {
+      sumV += __shfl_xor(sumV, m);
+      sumH += __shfl_xor(sumH, m);
+      sumD0 += __shfl_xor(sumD0, m);
+      sumD1 += __shfl_xor(sumD1, m);
+    }
+    if (ii == 0) {
+      const int shift = P.bd + 4;
+      const int act = clip3(0, 15, ((sumV + sumH) * ((yv == vbPos - 4 || yv == vbPos) ? 96 : 64)) >> shift);
+      int classIdx = c_th[act];
+      int hv1, hv0, d1, d0, dirHV, dirD, mainDir, secDir;
+      if (sumV > sumH) { hv1 = sumV; hv0 = sumH; dirHV = 1; } else { hv1 = sumH; hv0 = sumV; dirHV = 3; }
+      if (sumD0 > sumD1) { d1 = sumD0; d0 = sumD1; dirD = 0; } else { d1 = sumD1; d0 = sumD0; dirD = 2; }
+      int hvd1, hvd0;
+      if ((uint32_t)d1 * (uint32_t)hv0 > (uint32_t)hv1 * (uint32_t)d0) { hvd1 = d1; hvd0 = d0; mainDir = dirD; secDir = dirHV; }
+      else { hvd1 = hv1; hvd0 = hv0; mainDir = dirHV; secDir = dirD; }
+      int strength = 0;
+      if (hvd1 > 2 * hvd0) strength = 1;
+      if (hvd1 * 2 > 9 * hvd0) strength = 2;
+      if (strength) classIdx += (((mainDir & 1) << 1) + strength) * 5;
+      const int tr = c_transpose[mainDir * 2 + (secDir >> 1)];
+      blk[b] = classIdx | (tr << 8) | ((on ? 1 : 0) << 16);
     }
   }
-  const int shift = P.bd + 4;
-  const int act = clip3(0, 15, ((sumV + sumH) * ((yv == vbPos - 4 || yv == vbPos) ? 96 : 64)) >> shift);
-  int classIdx = c_th[act];
-  int hv1, hv0, d1, d0, dirHV, dirD, mainDir, secDir;
-  if (sumV > sumH) { hv1 = sumV; hv0 = sumH; dirHV = 1; } else { hv1 = sumH; hv0 = sumV; dirHV = 3; }
-  if (sumD0 > sumD1) { d1 = sumD0; d0 = sumD1; dirD = 0; } else { d1 = sumD1; d0 = sumD0; dirD = 2; }
-  int hvd1, hvd0;
-  if ((uint32_t)d1 * (uint32_t)hv0 > (uint32_t)hv1 * (uint32_t)d0) { hvd1 = d1; hvd0 = d0; mainDir = dirD; secDir = dirHV; }
-  else { hvd1 = hv1; hvd0 = hv0; mainDir = dirHV; secDir = dirD; }
-  int strength = 0;
-  if (hvd1 > 2 * hvd0) strength = 1;
-  if (hvd1 * 2 > 9 * hvd0) strength = 2;
-  if (strength) classIdx += (((mainDir & 1) << 1) + strength) * 5;
-  const int tr = c_transpose[mainDir * 2 + (secDir >> 1)];
-  // --- 7x7 diamond filter
+  __syncthreads();
+  // --- 7x7 diamond filter (filterBlk<ALF_FILTER_7>): lane = one column of one 4x4 block
+  const int x = X0 + (tid & 63), by = Y0 + (tid >> 6) * 4;
+  if (x >= W || by >= H) return;
+  const int bi = blk[((tid >> 6) << 4) + ((tid & 63) >> 2)];
+  int16_t *dst = D.p + x;
+  if (!(bi >> 16)) {
+    for (int y = by; y < by + 4 && y < H; y++) dst[(size_t)y * D.stride] = (int16_t)T(x, y);
+    return;
+  }
+  const int classIdx = bi & 255, tr = (bi >> 8) & 255;
+  const int ctb = (by >> P.ctu_log2) * P.wc + (x >> P.ctu_log2);
   const int set = P.ctb_set[ctb];
   const int16_t *coef = P.luma_coef + (set * 25 + classIdx) * 13, *clip = P.luma_clip + (set * 25 + classIdx) * 13;
   int fc[12], fl[12];
 #pragma unroll
   for (int k = 0; k < 12; k++) { fc[k] = coef[c_perm7[tr][k]]; fl[k] = clip[c_perm7[tr][k]]; }
   const int maxv = (1 << P.bd) - 1;
-  for (int y = by; y < by + 4 && y < S.h; y++) {
+  for (int y = by; y < by + 4 && y < H; y++) {
     int r1, r2, r3, r4, r5, r6;
     alf_rows(y, vbH, vbPos, true, r1, r2, r3, r4, r5, r6);
     const int yVb = y & (vbH - 1);
     const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
-    for (int x = bx; x < bx + 4 && x < S.w; x++) {
-      const int cur = at(S, x, y);
-      int sum = fc[0] * clip_alf(fl[0], cur, at(S, x, r5), at(S, x, r6));
-      sum += fc[1] * clip_alf(fl[1], cur, at(S, x + 1, r3), at(S, x - 1, r4));
-      sum += fc[2] * clip_alf(fl[2], cur, at(S, x, r3), at(S, x, r4));
-      sum += fc[3] * clip_alf(fl[3], cur, at(S, x - 1, r3), at(S, x + 1, r4));
-      sum += fc[4] * clip_alf(fl[4], cur, at(S, x + 2, r1), at(S, x - 2, r2));
-      sum += fc[5] * clip_alf(fl[5], cur, at(S, x + 1, r1), at(S, x - 1, r2));
-      sum += fc[6] * clip_alf(fl[6], cur, at(S, x, r1), at(S, x, r2));
-      sum += fc[7] * clip_alf(fl[7], cur, at(S, x - 1, r1), at(S, x + 1, r2));
-      sum += fc[8] * clip_alf(fl[8], cur, at(S, x - 2, r1), at(S, x + 2, r2));
-      sum += fc[9] * clip_alf(fl[9], cur, at(S, x + 3, y), at(S, x - 3, y));
-      sum += fc[10] * clip_alf(fl[10], cur, at(S, x + 2, y), at(S, x - 2, y));
-      sum += fc[11] * clip_alf(fl[11], cur, at(S, x + 1, y), at(S, x - 1, y));
-      sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
-      D.p[(size_t)y * D.stride + x] = (int16_t)clip3(0, maxv, sum + cur);
-    }
+    const int cur = T(x, y);
+    int sum = fc[0] * clip_alf(fl[0], cur, T(x, r5), T(x, r6));
+    sum += fc[1] * clip_alf(fl[1], cur, T(x + 1, r3), T(x - 1, r4));
+    sum += fc[2] * clip_alf(fl[2], cur, T(x, r3), T(x, r4));
+    sum += fc[3] * clip_alf(fl[3], cur, T(x - 1, r3), T(x + 1, r4));
+    sum += fc[4] * clip_alf(fl[4], cur, T(x + 2, r1), T(x - 2, r2));
+    sum += fc[5] * clip_alf(fl[5], cur, T(x + 1, r1), T(x - 1, r2));
+    sum += fc[6] * clip_alf(fl[6], cur, T(x, r1), T(x, r2));
+    sum += fc[7] * clip_alf(fl[7], cur, T(x - 1, r1), T(x + 1, r2));
+    sum += fc[8] * clip_alf(fl[8], cur, T(x - 2, r1), T(x + 2, r2));
+    sum += fc[9] * clip_alf(fl[9], cur, T(x + 3, y), T(x - 3, y));
+    sum += fc[10] * clip_alf(fl[10], cur, T(x + 2, y), T(x - 2, y));
+    sum += fc[11] * clip_alf(fl[11], cur, T(x + 1, y), T(x - 1, y));
+    sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
+    dst[(size_t)y * D.stride] = (int16_t)clip3(0, maxv, sum + cur);
   }
+#undef T
 }
 
 __global__ void k_alf_chroma(AlfParams P) {
@@ -228,8 +267,8 @@ void launch_sao(const SaoParams &p, hipStream_t s) {
 void launch_alf(const AlfParams &p, hipStream_t s) {
   {
     const int W = p.src[0].w, H = p.src[0].h;
-    dim3 grid(((W + 3) / 4 + 63) / 64, (H + 3) / 4);
-    hipLaunchKernelGGL(k_alf_luma, grid, dim3(64), 0, s, p);
+    dim3 grid((W + ALF_TW - 1) / ALF_TW, (H + ALF_TH - 1) / ALF_TH);
+    hipLaunchKernelGGL(k_alf_luma, grid, dim3(256), 0, s, p);
   }
   {
     const int W = p.src[1].w, H = p.src[1].h;
