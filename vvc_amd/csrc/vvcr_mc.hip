@@ -46,31 +46,44 @@ constexpr int IF_FILTER_PREC = 6;
 constexpr int IF_INTERNAL_OFFS = 1 << (IF_INTERNAL_PREC - 1);
 
 
-// LDS budget per wave (one job per 64-thread workgroup)
-constexpr int WIN_STRIDE = 24;              // up to 16+7 = 23 columns
-constexpr int WIN_ROWS = 23;
+// LDS layout per wave (one job per 64-thread workgroup): the six reference windows of a job (luma and
+// Cb/Cr for lists 0 and 1) are staged in ONE gather phase — every lane issues all of its loads before the
+// first LDS write, so the job pays one memory round trip instead of one per window row chunk — and then
+// filtered from LDS.
+constexpr int LW_PITCH = 24, LW_ROWS = 23;   // luma window: up to 16+7 = 23 columns / rows
+constexpr int CW_PITCH = 12, CW_ROWS = 11;   // chroma window: up to 8+3 = 11
+constexpr int LW_SIZE = LW_PITCH * LW_ROWS, CW_SIZE = CW_PITCH * CW_ROWS;
+constexpr int STAGE_SPAN = 2 * LW_SIZE + 4 * CW_SIZE;       // all six windows
 constexpr int TMP_STRIDE = 16;
 
-// Predict one component of one list into per-lane registers out[k] (k-th sample of lane).
-// N = taps (8 luma / 4 chroma). Output either final Pel (rnd) or 14-bit intermediate.
+// Window geometry of one (component, list): top-left tap in picture coordinates and the window size.
+struct Win {
+  int ox, oy, ww, wh, fx, fy;
+  const int16_t *p;
+  int stride, pw, ph;
+  bool on;
+};
+
+__device__ __forceinline__ Win make_win(const McParams &P, const McJob &J, int comp, int l) {
+  Win w;
+  const int cs = comp ? 1 : 0, N = comp ? 4 : 8, half = N / 2 - 1, fb = 4 + cs;
+  w.on = ((J.flags & (l ? MC_L1 : MC_L0)) != 0) && ((J.flags & (comp ? MC_CHROMA : MC_LUMA)) != 0);
+  const DPlane &R = P.ref[J.slot[l] < 0 ? 0 : J.slot[l]][comp];
+  const int mvx = J.mv[l][0], mvy = J.mv[l][1], mask = (1 << fb) - 1;
+  w.fx = mvx & mask; w.fy = mvy & mask;
+  w.ox = (J.x >> cs) + (mvx >> fb) - half; w.oy = (J.y >> cs) + (mvy >> fb) - half;
+  w.ww = (J.w >> cs) + N - 1; w.wh = (J.h >> cs) + N - 1;
+  w.p = R.p; w.stride = R.stride; w.pw = R.w; w.ph = R.h;
+  return w;
+}
+
+// Separable FIR of one list from its staged window into per-lane registers out[k] (k-th sample of the
+// lane): InterpolationFilter::filter<N,isVertical,isFirst,isLast> with xPredInterBlk's split.
 template <int N>
-__device__ void predict_list(const DPlane &ref, int bx, int by, int bw, int bh, int mvx, int mvy,
-                             int fracBits, bool altHpel, bool rnd, int bd, int16_t *win, int16_t *tmp,
-                             int lane, int (&out)[4]) {
-  const int mask = (1 << fracBits) - 1;
-  const int fx = mvx & mask, fy = mvy & mask;
-  const int ix = bx + (mvx >> fracBits), iy = by + (mvy >> fracBits);
+__device__ void filter_list(const int16_t *win, int pitch, int bw, int bh, int fx, int fy, bool altHpel, bool rnd,
+                            int bd, int16_t *tmp, int lane, int (&out)[4]) {
   const int half = N / 2 - 1;
-  const int ww = bw + N - 1, wh = bh + N - 1;
-  const int pw = ref.w, ph = ref.h;
-  // stage window (clamped coordinates)
-  for (int i = lane; i < ww * wh; i += 64) {
-    int r = i / ww, c = i - r * ww;
-    int sx = clampi(ix - half + c, 0, pw - 1), sy = clampi(iy - half + r, 0, ph - 1);
-    win[r * WIN_STRIDE + c] = ref.p[(size_t)sy * ref.stride + sx];
-  }
-  __syncthreads();
-  // coefficient rows
+  const int wh = bh + N - 1;
   int8_t ch[8], cv[8];
   if (N == 8) {
     const bool is4x4 = (bw == 4 && bh == 4);
@@ -84,14 +97,15 @@ __device__ void predict_list(const DPlane &ref, int bx, int by, int bw, int bh, 
   }
   const int headRoom = max(2, IF_INTERNAL_PREC - bd);
   const int n = bw * bh;
+  const int lw = __ffs(bw) - 1;      // bw is a power of two (4, 8, 16; chroma 2..8)
   if (fx == 0 && fy == 0) {
     // filterCopy<true, isLast> (InterpolationFilter.cpp:403)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       int i = lane + 64 * k;
       if (i < n) {
-        int y = i / bw, x = i - y * bw;
-        int v = win[(y + half) * WIN_STRIDE + x + half];
+        int y = i >> lw, x = i & (bw - 1);
+        int v = win[(y + half) * pitch + x + half];
         out[k] = rnd ? v : (int)(int16_t)((v << headRoom) - IF_INTERNAL_OFFS);
       }
     }
@@ -105,14 +119,14 @@ __device__ void predict_list(const DPlane &ref, int bx, int by, int bw, int bh, 
     for (int k = 0; k < 4; k++) {
       int i = lane + 64 * k;
       if (i < n) {
-        int y = i / bw, x = i - y * bw;
+        int y = i >> lw, x = i & (bw - 1);
         int sum = 0;
         if (vert) {
 #pragma unroll
-          for (int t = 0; t < N; t++) sum += win[(y + t) * WIN_STRIDE + x + half] * cv[t];
+          for (int t = 0; t < N; t++) sum += win[(y + t) * pitch + x + half] * cv[t];
         } else {
 #pragma unroll
-          for (int t = 0; t < N; t++) sum += win[(y + half) * WIN_STRIDE + x + t] * ch[t];
+          for (int t = 0; t < N; t++) sum += win[(y + half) * pitch + x + t] * ch[t];
         }
         int v = (int)(int16_t)((sum + offset) >> shift);
         out[k] = rnd ? clampi(v, 0, maxv) : v;
@@ -122,12 +136,16 @@ __device__ void predict_list(const DPlane &ref, int bx, int by, int bw, int bh, 
     // H pass (isFirst, !isLast) over bh+N-1 rows into tmp, then V pass (!isFirst, isLast = rnd)
     const int sh1 = IF_FILTER_PREC - headRoom;
     const int off1 = -(IF_INTERNAL_OFFS << sh1);
-    for (int i = lane; i < bw * wh; i += 64) {
-      int r = i / bw, c = i - r * bw;
-      int sum = 0;
 #pragma unroll
-      for (int t = 0; t < N; t++) sum += win[r * WIN_STRIDE + c + t] * ch[t];
-      tmp[r * TMP_STRIDE + c] = (int16_t)((sum + off1) >> sh1);
+    for (int k = 0; k < (N == 8 ? 6 : 2); k++) {     // <= 23x16 (luma) / 11x8 (chroma) samples
+      const int i = lane + 64 * k;
+      if (i < bw * wh) {
+        int r = i >> lw, c = i & (bw - 1);
+        int sum = 0;
+#pragma unroll
+        for (int t = 0; t < N; t++) sum += win[r * pitch + c + t] * ch[t];
+        tmp[r * TMP_STRIDE + c] = (int16_t)((sum + off1) >> sh1);
+      }
     }
     __syncthreads();
     const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
@@ -137,7 +155,7 @@ __device__ void predict_list(const DPlane &ref, int bx, int by, int bw, int bh, 
     for (int k = 0; k < 4; k++) {
       int i = lane + 64 * k;
       if (i < n) {
-        int y = i / bw, x = i - y * bw;
+        int y = i >> lw, x = i & (bw - 1);
         int sum = 0;
 #pragma unroll
         for (int t = 0; t < N; t++) sum += tmp[(y + t) * TMP_STRIDE + x] * cv[t];
@@ -145,34 +163,28 @@ __device__ void predict_list(const DPlane &ref, int bx, int by, int bw, int bh, 
         out[k] = rnd ? clampi(v, 0, maxv) : v;
       }
     }
+    __syncthreads();   // tmp reused by the next list / component
   }
-  __syncthreads();   // window / tmp reused by the next list or component
 }
 
-template <int N>
-__device__ void mc_component(const McParams &P, const McJob &J, int comp, int16_t *win, int16_t *tmp, int lane) {
-  const int cs = comp ? 1 : 0;                 // 4:2:0 scale
+// Combine the per-list results of one component and store: uni rounding, WP, GEO blend, BCW, addAvg.
+__device__ void mc_store(const McParams &P, const McJob &J, int comp, const int (&r0)[4], const int (&r1)[4], int lane) {
+  const int cs = comp ? 1 : 0;
   const int bx = J.x >> cs, by = J.y >> cs, bw = J.w >> cs, bh = J.h >> cs;
-  const int fracBits = 4 + cs;
   const bool l0 = J.flags & MC_L0, l1 = J.flags & MC_L1;
   const bool bi = l0 && l1;
-  const bool keep14 = (J.flags & MC_KEEP14) != 0;
-  const bool alt = (J.flags & MC_ALT_HPEL) && comp == 0;
-  const int bd = P.bd;
-  int r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
   const bool wp = (J.flags & MC_WP) != 0;
-  const bool rnd = !bi && !keep14 && !wp;
-  if (l0) predict_list<N>(P.ref[J.slot[0]][comp], bx, by, bw, bh, J.mv[0][0], J.mv[0][1], fracBits, alt, rnd, bd, win, tmp, lane, r0);
-  if (l1) predict_list<N>(P.ref[J.slot[1]][comp], bx, by, bw, bh, J.mv[1][0], J.mv[1][1], fracBits, alt, rnd, bd, win, tmp, lane, bi ? r1 : r0);
   const DPlane &o = P.out[comp];
   const int n = bw * bh;
+  const int lw = __ffs(bw) - 1;
+  const int bd = P.bd;
   const int maxv = (1 << bd) - 1;
   const int headRoom = max(2, IF_INTERNAL_PREC - bd);
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     int i = lane + 64 * k;
     if (i >= n) continue;
-    int y = i / bw, x = i - y * bw;
+    int y = i >> lw, x = i & (bw - 1);
     int v;
     if (!bi) {
       v = wp ? wp_uni(P.wp, l0 ? 0 : 1, l0 ? (J.ridx & 15) : (J.ridx >> 4), comp, r0[k], headRoom, maxv) : r0[k];
@@ -202,16 +214,68 @@ __device__ void mc_component(const McParams &P, const McJob &J, int comp, int16_
 }
 
 __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__restrict__ jobs, int njobs) {
-  __shared__ int16_t win[WIN_ROWS * WIN_STRIDE];
-  __shared__ int16_t tmp[WIN_ROWS * TMP_STRIDE];
+  // windows: [0] luma L0, [1] luma L1 (LW_SIZE each), then Cb L0, Cb L1, Cr L0, Cr L1 (CW_SIZE each)
+  __shared__ int16_t win[STAGE_SPAN];
+  __shared__ int16_t tmp[LW_ROWS * TMP_STRIDE];
   const int j = blockIdx.x;
   if (j >= njobs) return;
   const McJob J = jobs[j];
   const int lane = threadIdx.x;
-  if (J.flags & MC_LUMA) mc_component<8>(P, J, 0, win, tmp, lane);
+  Win w[6];
+#pragma unroll
+  for (int c = 0; c < 3; c++)
+#pragma unroll
+    for (int l = 0; l < 2; l++) w[c * 2 + l] = make_win(P, J, c, l);
+  // ---- gather: all loads of the job in flight together, coordinates clamped to the picture.
+  // Windows are walked with compile-time indices (a dynamically indexed Win[] would live in scratch).
+  constexpr int LIT = (LW_SIZE + 63) / 64, CIT = (CW_SIZE + 63) / 64;
+  int16_t v[6][LIT] = {};
+#pragma unroll
+  for (int wi = 0; wi < 6; wi++) {
+    const Win &W = w[wi];
+    const int pitch = wi < 2 ? LW_PITCH : CW_PITCH, size = wi < 2 ? LW_SIZE : CW_SIZE;
+#pragma unroll
+    for (int k = 0; k < (wi < 2 ? LIT : CIT); k++) {
+      const int i = lane + 64 * k;
+      const int r = i / pitch, c = i - r * pitch;
+      if (W.on && i < size && c < W.ww && r < W.wh) {
+        const int sx = clampi(W.ox + c, 0, W.pw - 1), sy = clampi(W.oy + r, 0, W.ph - 1);
+        v[wi][k] = W.p[(size_t)sy * W.stride + sx];
+      }
+    }
+  }
+#pragma unroll
+  for (int wi = 0; wi < 6; wi++) {
+    int16_t *dst = win + (wi < 2 ? wi * LW_SIZE : 2 * LW_SIZE + (wi - 2) * CW_SIZE);
+    const int size = wi < 2 ? LW_SIZE : CW_SIZE;
+#pragma unroll
+    for (int k = 0; k < (wi < 2 ? LIT : CIT); k++) {
+      const int i = lane + 64 * k;
+      if (i < size) dst[i] = v[wi][k];
+    }
+  }
+  __syncthreads();
+  // ---- filter and combine
+  const bool bi = (J.flags & MC_L0) && (J.flags & MC_L1);
+  const bool keep14 = (J.flags & MC_KEEP14) != 0, wp = (J.flags & MC_WP) != 0;
+  const bool rnd = !bi && !keep14 && !wp;
+  const int bd = P.bd;
+  if (J.flags & MC_LUMA) {
+    int r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
+    const bool alt = (J.flags & MC_ALT_HPEL) != 0;
+    if (w[0].on) filter_list<8>(win, LW_PITCH, J.w, J.h, w[0].fx, w[0].fy, alt, rnd, bd, tmp, lane, r0);
+    if (w[1].on) filter_list<8>(win + LW_SIZE, LW_PITCH, J.w, J.h, w[1].fx, w[1].fy, alt, rnd, bd, tmp, lane, bi ? r1 : r0);
+    mc_store(P, J, 0, r0, r1, lane);
+  }
   if (J.flags & MC_CHROMA) {
-    mc_component<4>(P, J, 1, win, tmp, lane);
-    mc_component<4>(P, J, 2, win, tmp, lane);
+#pragma unroll
+    for (int c = 1; c < 3; c++) {
+      int r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
+      const int16_t *cw = win + 2 * LW_SIZE + (c - 1) * 2 * CW_SIZE;
+      if (w[c * 2].on) filter_list<4>(cw, CW_PITCH, J.w >> 1, J.h >> 1, w[c * 2].fx, w[c * 2].fy, false, rnd, bd, tmp, lane, r0);
+      if (w[c * 2 + 1].on) filter_list<4>(cw + CW_SIZE, CW_PITCH, J.w >> 1, J.h >> 1, w[c * 2 + 1].fx, w[c * 2 + 1].fy, false, rnd, bd, tmp, lane, bi ? r1 : r0);
+      mc_store(P, J, c, r0, r1, lane);
+    }
   }
 }
 

@@ -43,13 +43,6 @@ __device__ __forceinline__ int sample(const DPlane &P, int x, int y, const Clamp
   return P.p[(size_t)y * P.stride + x];
 }
 
-__device__ void load_window(const DPlane &P, int ox, int oy, int ww, int wh, const Clamp &c, int16_t *win, int ws, int lane) {
-  for (int i = lane; i < ww * wh; i += 64) {
-    const int r = i / ww, col = i - r * ww;
-    win[r * ws + col] = (int16_t)sample(P, ox + col, oy + r, c);
-  }
-}
-
 // One output sample of InterpolationFilter::filter<N,...> applied as xPredInterBlk does (copy / H / V /
 // H-then-V), from a window whose (0,0) is the top-left tap of output (0,0). rnd: final Pel (isLast).
 template <int N>
@@ -125,9 +118,31 @@ __device__ void subpel_surface(const unsigned long long *s, int *d) {   // xSubP
 constexpr int WS = 24;        // LDS window stride (<= 16 + 7 columns)
 constexpr int BS = 20;        // bilinear buffer stride (16 + 4)
 constexpr int PS = 18;        // BDOF buffers: (16 + 2) with the 1-sample ring
+constexpr int CWS = 12;       // chroma window stride (<= 8 + 3 columns)
+
+// Gather of one window (clamped like sample()) into per-lane registers: ITS loads per lane, pitch PITCH.
+template <int ITS, int PITCH>
+__device__ __forceinline__ void gather_regs(const DPlane &P, int ox, int oy, int ww, int wh, const Clamp &c, int lane, int16_t (&v)[ITS]) {
+#pragma unroll
+  for (int k = 0; k < ITS; k++) {
+    const int i = lane + 64 * k;
+    const int r = i / PITCH, col = i - r * PITCH;
+    if (col < ww && r < wh) v[k] = (int16_t)sample(P, ox + col, oy + r, c);
+  }
+}
+template <int ITS>
+__device__ __forceinline__ void regs_to_lds(int16_t *dst, int size, int lane, const int16_t (&v)[ITS]) {
+#pragma unroll
+  for (int k = 0; k < ITS; k++) {
+    const int i = lane + 64 * k;
+    if (i < size) dst[i] = v[k];
+  }
+}
 
 __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__restrict__ jobs, int njobs, int32_t *dmvr_out) {
-  __shared__ int16_t win[23 * WS];
+  // staged reference windows: luma L0/L1 (23 x WS each), then Cb L0/L1, Cr L0/L1 (11 x CWS each); the two
+  // DMVR search windows reuse the luma part first
+  __shared__ int16_t fwin[2 * 23 * WS + 4 * 11 * CWS];
   __shared__ int16_t bl[2][BS * BS];
   __shared__ unsigned long long sad[25];
   __shared__ int16_t pr[2][PS * PS];
@@ -150,12 +165,21 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
   bool bdof = (J.flags & MC_BDOF) != 0;
   if (dmvr) {
     const int shB = bd - 6, offB = 1 << (shB - 1);   // IF_FILTER_PREC_BILINEAR - (IF_INTERNAL_PREC_BILINEAR - bd)
+    {
+      // both (w+5)x(h+5) search windows in one gather (21 rows of pitch WS at most)
+      constexpr int DIT = (21 * WS + 63) / 64;
+      int16_t v0[DIT] = {}, v1[DIT] = {};
+      gather_regs<DIT, WS>(*R[0], J.x + (J.mv[0][0] >> 4) - 2, J.y + (J.mv[0][1] >> 4) - 2, w + 5, h + 5, none, lane, v0);
+      gather_regs<DIT, WS>(*R[1], J.x + (J.mv[1][0] >> 4) - 2, J.y + (J.mv[1][1] >> 4) - 2, w + 5, h + 5, none, lane, v1);
+      regs_to_lds(fwin, 21 * WS, lane, v0);
+      regs_to_lds(fwin + 23 * WS, 21 * WS, lane, v1);
+    }
+    __syncthreads();
+#pragma unroll
     for (int l = 0; l < 2; l++) {
       const int mvx = J.mv[l][0], mvy = J.mv[l][1];
       const int fx = mvx & 15, fy = mvy & 15;
-      const int ox = J.x + (mvx >> 4) - 2, oy = J.y + (mvy >> 4) - 2;
-      load_window(*R[l], ox, oy, w + 5, h + 5, none, win, WS, lane);
-      __syncthreads();
+      const int16_t *win = fwin + l * 23 * WS;
       for (int i = lane; i < (w + 4) * (h + 4); i += 64) {
         const int r = i / (w + 4), c = i - r * (w + 4);
         const int16_t *s = win + r * WS + c;
@@ -173,8 +197,8 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
         }
         bl[l][r * BS + c] = (int16_t)v;
       }
-      __syncthreads();
     }
+    __syncthreads();
     if (lane < 25) {
       const int ox = x_search[lane][0], oy = x_search[lane][1];
       unsigned long long acc = 0;
@@ -214,43 +238,74 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
     dx = sh_delta[0]; dy = sh_delta[1]; bdof = sh_bdof;
   }
 
-  // ---- final MC (xFinalPaddedMCForDMVR / xPredInterBlk with bioApplied) per list
+  // ---- final MC (xFinalPaddedMCForDMVR / xPredInterBlk with bioApplied) per list: geometry of the six
+  // (component, list) windows, then ONE gather of all of them, then the filters from LDS
   const int MVLIM = (1 << 17) - 1;
+  int gfx[3][2], gfy[3][2], gix[3][2], giy[3][2];
+  {
+    constexpr int LIT = (23 * WS + 63) / 64, CIT = (11 * CWS + 63) / 64;
+    int16_t vl[2][LIT] = {}, vc[2][2][CIT] = {};
+#pragma unroll
+    for (int comp = 0; comp < 3; comp++) {
+      const int cs = comp ? 1 : 0;
+      const int bx = J.x >> cs, by = J.y >> cs, bw = w >> cs, bh = h >> cs;
+#pragma unroll
+      for (int l = 0; l < 2; l++) {
+        const int sgn = l ? -1 : 1;
+        const int mvx = clampi(J.mv[l][0] + sgn * dx, -MVLIM - 1, MVLIM), mvy = clampi(J.mv[l][1] + sgn * dy, -MVLIM - 1, MVLIM);
+        const DPlane &ref = P.ref[J.slot[l]][comp];
+        Clamp cl = none;
+        if (dmvr) {
+          // xPrefetch window of the unrefined MV ((w+N-1)x(h+N-1) from the N/2-1 left/top taps), beyond which
+          // xPad replicates its edge samples
+          const int t = comp ? 1 : 3, ext = comp ? 3 : 7;
+          const int X0 = bx + (J.mv[l][0] >> (4 + cs)) - t, Y0 = by + (J.mv[l][1] >> (4 + cs)) - t;
+          cl = Clamp{X0, X0 + bw + ext - 1, Y0, Y0 + bh + ext - 1};
+        }
+        const int fb = 4 + cs, mask = (1 << fb) - 1;
+        gfx[comp][l] = mvx & mask; gfy[comp][l] = mvy & mask;
+        gix[comp][l] = bx + (mvx >> fb); giy[comp][l] = by + (mvy >> fb);
+        const int N = comp ? 4 : 8, half = N / 2 - 1;
+        if (comp == 0)
+          gather_regs<LIT, WS>(ref, gix[0][l] - half, giy[0][l] - half, bw + N - 1, bh + N - 1, cl, lane, vl[l]);
+        else
+          gather_regs<CIT, CWS>(ref, gix[comp][l] - half, giy[comp][l] - half, bw + N - 1, bh + N - 1, cl, lane, vc[comp - 1][l]);
+      }
+    }
+    __syncthreads();   // the DMVR search windows (same LDS) are no longer read
+#pragma unroll
+    for (int l = 0; l < 2; l++) regs_to_lds(fwin + l * 23 * WS, 23 * WS, lane, vl[l]);
+#pragma unroll
+    for (int c = 0; c < 2; c++)
+#pragma unroll
+      for (int l = 0; l < 2; l++) regs_to_lds(fwin + 2 * 23 * WS + (c * 2 + l) * 11 * CWS, 11 * CWS, lane, vc[c][l]);
+  }
+  __syncthreads();
+#pragma unroll
   for (int comp = 0; comp < 3; comp++) {
     const int cs = comp ? 1 : 0;
     const int bx = J.x >> cs, by = J.y >> cs, bw = w >> cs, bh = h >> cs;
     int r[2][4];
+#pragma unroll
     for (int l = 0; l < 2; l++) {
-      const int sgn = l ? -1 : 1;
-      const int mvx = clampi(J.mv[l][0] + sgn * dx, -MVLIM - 1, MVLIM), mvy = clampi(J.mv[l][1] + sgn * dy, -MVLIM - 1, MVLIM);
-      const DPlane &ref = P.ref[J.slot[l]][comp];
-      Clamp cl = none;
-      if (dmvr) {
-        // xPrefetch window of the unrefined MV ((w+N-1)x(h+N-1) from the N/2-1 left/top taps), beyond which
-        // xPad replicates its edge samples
-        const int t = comp ? 1 : 3, ext = comp ? 3 : 7;
-        const int X0 = bx + (J.mv[l][0] >> (4 + cs)) - t, Y0 = by + (J.mv[l][1] >> (4 + cs)) - t;
-        cl = Clamp{X0, X0 + bw + ext - 1, Y0, Y0 + bh + ext - 1};
-      }
-      const int fb = 4 + cs, mask = (1 << fb) - 1;
-      const int fx = mvx & mask, fy = mvy & mask;
-      const int ix = bx + (mvx >> fb), iy = by + (mvy >> fb);
-      const int N = comp ? 4 : 8, half = N / 2 - 1;
-      load_window(ref, ix - half, iy - half, bw + N - 1, bh + N - 1, cl, win, WS, lane);
-      __syncthreads();
+      const int fx = gfx[comp][l], fy = gfy[comp][l];
+      const int16_t *win = comp == 0 ? fwin + l * 23 * WS : fwin + 2 * 23 * WS + ((comp - 1) * 2 + l) * 11 * CWS;
+      const int ws = comp == 0 ? WS : CWS;
+#pragma unroll
       for (int k = 0; k < 4; k++) {
         const int i = lane + 64 * k;
-        if (i >= bw * bh) break;
+        if (i >= bw * bh) continue;
         const int y = i / bw, x = i - y * bw;
         int v;
-        if (comp == 0) v = filt<8>(win, WS, x, y, fx, fy, (alt && fx == 8) ? x_alt_hpel : x_luma[fx],
+        if (comp == 0) v = filt<8>(win, ws, x, y, fx, fy, (alt && fx == 8) ? x_alt_hpel : x_luma[fx],
                                    (alt && fy == 8) ? x_alt_hpel : x_luma[fy], false, bd);
-        else v = filt<4>(win, WS, x, y, fx, fy, x_chroma[fx], x_chroma[fy], false, bd);
+        else v = filt<4>(win, ws, x, y, fx, fy, x_chroma[fx], x_chroma[fy], false, bd);
         r[l][k] = v;
         if (comp == 0) pr[l][(y + 1) * PS + x + 1] = (int16_t)v;
       }
       if (comp == 0 && bdof) {
-        // integer-sample ring (xPredInterBlk :812-846): nearest integer position, << headRoom, - offset
+        // integer-sample ring (xPredInterBlk :812-846): nearest integer position, << headRoom, - offset; the
+        // ring lies inside the staged 8-tap window (same clamps), 3 samples in from its top-left
         const int xo = fx >= 8 ? 1 : 0, yo = fy >= 8 ? 1 : 0;
         const int n = 2 * (bw + 2) + 2 * bh;
         for (int i = lane; i < n; i += 64) {
@@ -258,12 +313,12 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
           if (i < bw + 2) { x = i - 1; y = -1; }
           else if (i < 2 * (bw + 2)) { x = i - (bw + 2) - 1; y = bh; }
           else { const int k2 = i - 2 * (bw + 2); y = k2 >> 1; x = (k2 & 1) ? bw : -1; }
-          const int s = sample(ref, ix + x + xo, iy + y + yo, cl);
+          const int s = win[(y + yo + 3) * WS + x + xo + 3];
           pr[l][(y + 1) * PS + x + 1] = (int16_t)((s << max(2, IF_INTERNAL_PREC - bd)) - IF_INTERNAL_OFFS);
         }
       }
-      __syncthreads();
     }
+    __syncthreads();
     const DPlane &o = P.out[comp];
     if (comp == 0 && bdof) {
       // gradients of both lists (gradFilterCore, shift 6), replicated to the ring
@@ -331,9 +386,10 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
     } else {
       const int headRoom = max(2, IF_INTERNAL_PREC - bd);
       const int shiftNum = headRoom + 1, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
+#pragma unroll
       for (int k = 0; k < 4; k++) {
         const int i = lane + 64 * k;
-        if (i >= bw * bh) break;
+        if (i >= bw * bh) continue;
         const int y = i / bw, x = i - y * bw;
         o.p[(size_t)(by + y) * o.stride + bx + x] = (int16_t)clampi((r[0][k] + r[1][k] + offset) >> shiftNum, 0, maxv);
       }
@@ -351,11 +407,16 @@ __device__ __forceinline__ void round_affine(int &x, int &y, int s) {   // round
 }
 
 constexpr int AWS = 11;   // 4 + 7 luma window per sub-block
+constexpr int ALW = 16 * AWS * AWS;                  // luma windows of one list (16 sub-blocks)
+constexpr int ACW = 4 * 49;                          // chroma windows of one list and component (4 sub-blocks of 7x7)
+constexpr int A_SPAN = 2 * ALW + 2 * 2 * ACW;        // all windows of a tile
 
 __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__restrict__ jobs, int njobs, const AffPu *__restrict__ pus) {
-  __shared__ int16_t win[16][AWS * AWS];
-  __shared__ int sbmv[16][2];          // MC MV of each luma sub-block (clamped)
-  __shared__ int stmv[16][2];          // stored MV (before the picture clamp) for chroma
+  // all windows of the tile: luma [list][sub-block][11x11], then chroma [list][Cb/Cr][sub-block][7x7]
+  __shared__ int16_t win[A_SPAN];
+  __shared__ int sbmv[2][16][2];       // MC MV of each luma sub-block (clamped)
+  __shared__ int stmv[2][16][2];       // stored MV (before the picture clamp) for chroma
+  __shared__ int csmv[2][4][2];        // chroma sub-block MVs
   __shared__ int16_t c14[16 * 16];     // PROF: 14-bit prediction of the tile
   const int j = blockIdx.x;
   if (j >= njobs) return;
@@ -365,20 +426,19 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
   const int bd = P.bd, maxv = (1 << bd) - 1;
   const int headRoom = max(2, IF_INTERNAL_PREC - bd);
   const bool bi = U.l[0].present && U.l[1].present;
-  const int w = J.w, h = J.h;
-  const int nsx = w >> 2, nsb = (w >> 2) * (h >> 2);
-  const Clamp none{-(1 << 30), 1 << 30, -(1 << 30), 1 << 30};
+  const int w = J.w, h = J.h;           // 8 or 16 (affine PUs are >= 8x8, tiled by 16)
+  const int lnsx = w == 16 ? 2 : 1, nsx = 1 << lnsx, nsb = (w >> 2) * (h >> 2);
+  const int cw = w >> 1, chh = h >> 1, ncx = cw >> 2, ncb = (cw >> 2) * (chh >> 2);
   // MV clamp of xPredAffineBlk (:936-939), relative to the PU
   const int iHorMax = (P.pic_w + 8 - U.x - 1) << 4, iHorMin = (-P.ctu - 8 - U.x + 1) << 4;
   const int iVerMax = (P.pic_h + 8 - U.y - 1) << 4, iVerMin = (-P.ctu - 8 - U.y + 1) << 4;
   const int MVLIM = (1 << 17) - 1;
-  int res[3][2][4];
-  for (int l = 0; l < 2; l++) {
-    const AffList &A = U.l[l];
-    if (!A.present) continue;
-    // sub-block MVs (:1102-1140)
-    if (lane < nsb) {
-      const int sw = (J.x - U.x) + (lane % nsx) * 4, sh = (J.y - U.y) + (lane / nsx) * 4;
+  // ---- sub-block MVs of both lists (:1102-1140)
+  if (lane < 32) {
+    const int l = lane >> 4, sb = lane & 15;
+    const AffList &A = pus[J.pu].l[l];      // lane-dependent list: read from global (a local copy would go to scratch)
+    if (A.present && sb < nsb) {
+      const int sw = (J.x - U.x) + (sb & (nsx - 1)) * 4, sh = (J.y - U.y) + (sb >> lnsx) * 4;
       int mx, my;
       if (!A.spread) {
         mx = A.mvx + A.dhx * (2 + sw) + A.dvx * (2 + sh);
@@ -390,29 +450,96 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
       round_affine(mx, my, 7);
       mx = clampi(mx, -MVLIM - 1, MVLIM);
       my = clampi(my, -MVLIM - 1, MVLIM);
-      stmv[lane][0] = mx; stmv[lane][1] = my;
-      sbmv[lane][0] = clampi(mx, iHorMin, iHorMax);
-      sbmv[lane][1] = clampi(my, iVerMin, iVerMax);
+      stmv[l][sb][0] = mx; stmv[l][sb][1] = my;
+      sbmv[l][sb][0] = clampi(mx, iHorMin, iHorMax);
+      sbmv[l][sb][1] = clampi(my, iVerMin, iVerMax);
     }
-    __syncthreads();
+  }
+  __syncthreads();
+  // ---- chroma: 4x4 sub-blocks, MV = mean of two luma sub-block MVs (:1142-1160)
+  if (lane < 8) {
+    const int l = lane >> 2, cb = lane & 3;
+    if (pus[J.pu].l[l].present && cb < ncb) {
+      const int cxs = (cb % ncx) * 2, cys = (cb / ncx) * 2;   // luma sub-block indices in the tile
+      const int a = cys * nsx + cxs, b = (cys + 1) * nsx + cxs + 1;
+      int mx = stmv[l][a][0] + stmv[l][b][0], my = stmv[l][a][1] + stmv[l][b][1];
+      round_affine(mx, my, 1);
+      csmv[l][cb][0] = clampi(mx, iHorMin, iHorMax);
+      csmv[l][cb][1] = clampi(my, iVerMin, iVerMax);
+    }
+  }
+  __syncthreads();
+  // ---- gather every window of the tile in one phase (all loads in flight before the first LDS write);
+  // lists and components are walked with compile-time indices so nothing lands in scratch
+  {
+    constexpr int ALIT = (ALW + 63) / 64, ACIT = (ACW + 63) / 64;
+    int16_t vl[2][ALIT] = {}, vc[2][2][ACIT] = {};
+#pragma unroll
+    for (int l = 0; l < 2; l++) {
+      if (!U.l[l].present) continue;
+      const DPlane &R = P.ref[U.l[l].slot][0];
+#pragma unroll
+      for (int k = 0; k < ALIT; k++) {
+        const int e = lane + 64 * k;
+        const int sb = e / (AWS * AWS), e2 = e - sb * (AWS * AWS);
+        const int r = e2 / AWS, c = e2 - r * AWS;
+        if (e < ALW && sb < nsb) {
+          const int sx = J.x + (sb & (nsx - 1)) * 4 + (sbmv[l][sb][0] >> 4) - 3 + c;
+          const int sy = J.y + (sb >> lnsx) * 4 + (sbmv[l][sb][1] >> 4) - 3 + r;
+          vl[l][k] = R.p[(size_t)clampi(sy, 0, R.h - 1) * R.stride + clampi(sx, 0, R.w - 1)];
+        }
+      }
+#pragma unroll
+      for (int comp = 1; comp < 3; comp++) {
+        const DPlane &RC = P.ref[U.l[l].slot][comp];
+#pragma unroll
+        for (int k = 0; k < ACIT; k++) {
+          const int e = lane + 64 * k;
+          const int cb = e / 49, e3 = e - cb * 49;
+          const int r = e3 / 7, c = e3 - r * 7;
+          if (e < ACW && cb < ncb) {
+            const int sx = (J.x >> 1) + (cb % ncx) * 4 + (csmv[l][cb][0] >> 5) - 1 + c;
+            const int sy = (J.y >> 1) + (cb / ncx) * 4 + (csmv[l][cb][1] >> 5) - 1 + r;
+            vc[l][comp - 1][k] = RC.p[(size_t)clampi(sy, 0, RC.h - 1) * RC.stride + clampi(sx, 0, RC.w - 1)];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < 2; l++) {
+      if (!U.l[l].present) continue;
+#pragma unroll
+      for (int k = 0; k < ALIT; k++) {
+        const int e = lane + 64 * k;
+        if (e < ALW) win[l * ALW + e] = vl[l][k];
+      }
+#pragma unroll
+      for (int comp = 1; comp < 3; comp++)
+#pragma unroll
+        for (int k = 0; k < ACIT; k++) {
+          const int e = lane + 64 * k;
+          if (e < ACW) win[2 * ALW + l * 2 * ACW + (comp - 1) * ACW + e] = vc[l][comp - 1][k];
+        }
+    }
+  }
+  __syncthreads();
+  int res[3][2][4];
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    const AffList &A = U.l[l];
+    if (!A.present) continue;
+    const int16_t *lwin = win + l * ALW;
     // ---- luma: per sub-block 11x11 windows
-    const DPlane &RY = P.ref[A.slot][0];
-    for (int i = lane; i < nsb * AWS * AWS; i += 64) {
-      const int sb = i / (AWS * AWS), e = i - sb * (AWS * AWS);
-      const int r = e / AWS, c = e - r * AWS;
-      const int sx = J.x + (sb % nsx) * 4 + (sbmv[sb][0] >> 4) - 3, sy = J.y + (sb / nsx) * 4 + (sbmv[sb][1] >> 4) - 3;
-      win[sb][e] = (int16_t)sample(RY, sx + c, sy + r, none);
-    }
-    __syncthreads();
     const bool prof = A.prof;
     const bool rnd = !prof && !bi && !U.wp;
+#pragma unroll
     for (int k = 0; k < 4; k++) {
       const int i = lane + 64 * k;
-      if (i >= w * h) break;
+      if (i >= w * h) continue;
       const int y = i / w, x = i - y * w;
       const int sb = (y >> 2) * nsx + (x >> 2);
-      const int fx = sbmv[sb][0] & 15, fy = sbmv[sb][1] & 15;
-      const int v = filt<8>(win[sb], AWS, x & 3, y & 3, fx, fy, x_luma4x4[fx], x_luma4x4[fy], rnd, bd);
+      const int fx = sbmv[l][sb][0] & 15, fy = sbmv[l][sb][1] & 15;
+      const int v = filt<8>(lwin + sb * AWS * AWS, AWS, x & 3, y & 3, fx, fy, x_luma4x4[fx], x_luma4x4[fy], rnd, bd);
       res[0][l][k] = v;
       if (prof) c14[y * 16 + x] = (int16_t)v;
     }
@@ -421,17 +548,19 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
       // PROF (:1209-1251): ring of integer samples, gradients (shift 6), dMv per position, applyPROFCore
       const int dILimit = 1 << max(bd + 1, 13);
       const int shiftNum = headRoom, offset = (1 << (shiftNum - 1)) + IF_INTERNAL_OFFS;
+#pragma unroll
       for (int k = 0; k < 4; k++) {
         const int i = lane + 64 * k;
-        if (i >= w * h) break;
+        if (i >= w * h) continue;
         const int y = i / w, x = i - y * w;
         const int sb = (y >> 2) * nsx + (x >> 2);
-        const int fx = sbmv[sb][0] & 15, fy = sbmv[sb][1] & 15;
+        const int fx = sbmv[l][sb][0] & 15, fy = sbmv[l][sb][1] & 15;
         const int xo = fx >> 3, yo = fy >> 3;
         const int px = x & 3, py = y & 3;
+        const int16_t *sw = lwin + sb * AWS * AWS;
         auto ext = [&](int ex, int ey) -> int {   // dstExt value at sub-block position (ex, ey) in [-1,4]
           if (ex >= 0 && ex < 4 && ey >= 0 && ey < 4) return c14[(y - py + ey) * 16 + (x - px + ex)];
-          const int s = win[sb][(3 + ey + yo) * AWS + 3 + ex + xo];
+          const int s = sw[(3 + ey + yo) * AWS + 3 + ex + xo];
           return (int16_t)((s << headRoom) - IF_INTERNAL_OFFS);
         };
         const int gX = (ext(px + 1, py) >> 6) - (ext(px - 1, py) >> 6);
@@ -446,46 +575,30 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
         if (!bi && !U.wp) v = clampi((v + offset) >> shiftNum, 0, maxv);
         res[0][l][k] = v;
       }
+      __syncthreads();   // c14 is reused by the other list
     }
-    __syncthreads();
-    // ---- chroma: 4x4 sub-blocks, MV = mean of two luma sub-block MVs (:1142-1160)
-    const int cw = w >> 1, chh = h >> 1, ncx = cw >> 2, ncb = (cw >> 2) * (chh >> 2);
-    if (lane < ncb) {
-      const int cxs = (lane % ncx) * 2, cys = (lane / ncx) * 2;   // luma sub-block indices in the tile
-      const int a = cys * nsx + cxs, b = (cys + 1) * nsx + cxs + 1;
-      int mx = stmv[a][0] + stmv[b][0], my = stmv[a][1] + stmv[b][1];
-      round_affine(mx, my, 1);
-      sbmv[lane][0] = clampi(mx, iHorMin, iHorMax);
-      sbmv[lane][1] = clampi(my, iVerMin, iVerMax);
-    }
-    __syncthreads();
+    // ---- chroma
+#pragma unroll
     for (int comp = 1; comp < 3; comp++) {
-      const DPlane &RC = P.ref[A.slot][comp];
-      const int bx = J.x >> 1, by = J.y >> 1;
-      for (int i = lane; i < ncb * 49; i += 64) {
-        const int sb = i / 49, e = i - sb * 49;
-        const int r = e / 7, c = e - r * 7;
-        const int sx = bx + (sb % ncx) * 4 + (sbmv[sb][0] >> 5) - 1, sy = by + (sb / ncx) * 4 + (sbmv[sb][1] >> 5) - 1;
-        win[sb][e] = (int16_t)sample(RC, sx + c, sy + r, none);
-      }
-      __syncthreads();
       if (lane < cw * chh) {
+        const int16_t *cwin = win + 2 * ALW + l * 2 * ACW + (comp - 1) * ACW;
         const int y = lane / cw, x = lane - y * cw;
         const int sb = (y >> 2) * ncx + (x >> 2);
-        const int fx = sbmv[sb][0] & 31, fy = sbmv[sb][1] & 31;
-        res[comp][l][0] = filt<4>(win[sb], 7, x & 3, y & 3, fx, fy, x_chroma[fx], x_chroma[fy], !bi && !U.wp, bd);
+        const int fx = csmv[l][sb][0] & 31, fy = csmv[l][sb][1] & 31;
+        res[comp][l][0] = filt<4>(cwin + sb * 49, 7, x & 3, y & 3, fx, fy, x_chroma[fx], x_chroma[fy], !bi && !U.wp, bd);
       }
-      __syncthreads();
     }
   }
   // ---- combine (xWeightedAverage: addAvg / addWeightedAvg; weighted prediction; uni already final without WP)
+#pragma unroll
   for (int comp = 0; comp < 3; comp++) {
     const int cs = comp ? 1 : 0;
     const int bw = w >> cs, bh = h >> cs, bx = J.x >> cs, by = J.y >> cs;
     const DPlane &o = P.out[comp];
+#pragma unroll
     for (int k = 0; k < (comp ? 1 : 4); k++) {
       const int i = lane + 64 * k;
-      if (i >= bw * bh) break;
+      if (i >= bw * bh) continue;
       const int y = i / bw, x = i - y * bw;
       int v;
       if (!bi) {
