@@ -4,8 +4,11 @@ compensation (DMVR/BDOF/affine-PROF/GEO/CIIP), intra waves, deblocking, SAO, ALF
 input (parsed descriptors, work lists, loop-filter parameters) resident in HBM when the timed region
 starts (vvcr_prepare_picture once, vvcr_launch_picture per step). One step = one decode of the whole
 sequence. The output of the first pass is checked bit-exact against the reference decoder's MD5s.
+Steps cycle through --segments (default 2) copies of the sequence on disjoint DPB slots, as consecutive
+intra-started segments of one long stream: the library runs each picture once its reference / slot
+dependencies are met, so a segment's intra picture may overlap the previous segment's B pictures.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--stream ra1080_q32] [--no-cpu]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--stream ra1080_q32] [--segments 2] [--no-cpu]
 
 Multi-GPU (torch.distributed.run, one process per GPU): the path has no intra-picture work split in
 this round, so N ranks decode N independent replicas (weak scaling, no data-path collective); the
@@ -59,6 +62,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--stream", default="ra1080_q32")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--segments", type=int, default=2, help="copies of the sequence the steps cycle through")
     a = ap.parse_args()
 
     R = V.Ranks()
@@ -71,36 +75,50 @@ def main():
     W, H = h0["width"], h0["height"]
     px_seq = W * H * len(pics)
 
-    # ---- prepare every picture once (host planning + upload), decoding order, own DPB slots
-    dec = D.Decoder(pics, dpb_slots=12, device=int(os.environ.get("VVCR_DEVICE", local)))   # VVCR_DEVICE: rehearsal of N ranks on one GPU
+    # ---- prepare every picture once (host planning + upload), decoding order. The sequence is prepared
+    # --segments times over disjoint DPB slot ranges and the steps cycle through these copies: step k+1
+    # then decodes its segment like the next intra-started segment of a longer stream would be decoded
+    # (its intra picture references nothing, so it may start while step k's B pictures still run —
+    # the library orders pictures only by their DPB-slot dependencies). --segments 1 serialises steps.
+    per = 12
+    dec = D.Decoder(pics, dpb_slots=per * a.segments,
+                    device=int(os.environ.get("VVCR_DEVICE", local)))   # VVCR_DEVICE: rehearsal of N ranks on one GPU
     ctx = dec.ctx
-    handles, slots = [], []
+    copies = []
     t_prep = time.perf_counter()
-    for i, p in enumerate(pics):
-        slot = dec.alloc.assign(i, p["hdr"]["poc"])
-        ctx.begin_picture(S.pic_params(p, slot, dec.alloc.slot_of))
-        S.submit(ctx, p)
-        S.set_loop_filter_params(ctx, p)
-        handles.append(ctx.prepare(N.STAGE_ALL))
-        slots.append((p["hdr"]["poc"], slot))
-    t_prep = time.perf_counter() - t_prep
+    for c in range(a.segments):
+        alloc = S.SlotAllocator(pics, per, base=per * c)
+        handles, slots = [], []
+        for i, p in enumerate(pics):
+            slot = alloc.assign(i, p["hdr"]["poc"])
+            ctx.begin_picture(S.pic_params(p, slot, alloc.slot_of))
+            S.submit(ctx, p)
+            S.set_loop_filter_params(ctx, p)
+            handles.append(ctx.prepare(N.STAGE_ALL))
+            slots.append((p["hdr"]["poc"], slot))
+        copies.append((handles, slots))
+    t_prep = (time.perf_counter() - t_prep) / a.segments
 
-    # ---- first pass: bit-exactness against the reference decoder (untimed)
-    yuv = hashlib.md5()
-    outs = {}
-    for hnd, (poc, slot) in zip(handles, slots):
-        ctx.launch(hnd)
-        outs[poc] = D.plane_md5s(dec.read(slot)), dec.read(slot)
-    bitexact = all(outs[int(k)][0] == v for k, v in meta["poc_plane_md5"].items())
-    for poc in sorted(outs):
-        for pl in outs[poc][1]:
-            yuv.update(np.ascontiguousarray(pl).astype("<u2").tobytes())
-    bitexact = bitexact and yuv.hexdigest() == meta["yuv_md5"]
-    outs = None
+    # ---- first pass: bit-exactness of every copy against the reference decoder (untimed)
+    bitexact = True
+    for handles, slots in copies:
+        yuv = hashlib.md5()
+        outs = {}
+        for hnd, (poc, slot) in zip(handles, slots):
+            ctx.launch(hnd)
+            outs[poc] = D.plane_md5s(dec.read(slot)), dec.read(slot)
+        bitexact = bitexact and all(outs[int(k)][0] == v for k, v in meta["poc_plane_md5"].items())
+        for poc in sorted(outs):
+            for pl in outs[poc][1]:
+                yuv.update(np.ascontiguousarray(pl).astype("<u2").tobytes())
+        bitexact = bitexact and yuv.hexdigest() == meta["yuv_md5"]
+        outs = None
+    nstep = [0]
 
     def run_step():
-        for hnd in handles:
+        for hnd in copies[nstep[0] % a.segments][0]:
             ctx.launch(hnd)
+        nstep[0] += 1
 
     for _ in range(a.warmup):
         run_step()
@@ -116,9 +134,22 @@ def main():
     R.barrier()
     elapsed = R.max_over_ranks(t1 - t0)
 
+    # ---- the same steps one segment at a time (each step synchronised before the next starts): the
+    # latency-bound view, reported beside value
+    ctx.sync()
+    R.barrier()
+    t2 = time.perf_counter()
+    for _ in range(a.steps):
+        run_step()
+        ctx.sync()
+    t3 = time.perf_counter()
+    R.barrier()
+    elapsed_serial = R.max_over_ranks(t3 - t2)
+
     # ---- per-kernel timing of the last step (HIP events on the library stream)
     kern = {}
-    for hnd in handles:
+    last = copies[(nstep[0] - 1) % a.segments][0]
+    for hnd in last:
         for name, launches, ms, alg in ctx.kernel_stats(hnd):
             k = kern.setdefault(name, [0, 0.0, 0.0])
             k[0] += launches
@@ -157,11 +188,14 @@ def main():
         "dtype": "int16",
         "data": "synthetic (VTM-7.3-encoded synthetic %dx%d %s stream, parsed descriptors resident in HBM)" % (W, H, desc),
         "config": {"workload": "%s: %dx%d %s, %d pictures, reconstruction + DBK/SAO/ALF" % (a.stream, W, H, desc, len(pics)),
-                   "parallelism": "replicas%d" % world, "bitexact_vs_reference": bool(bitexact)},
+                   "parallelism": "replicas%d" % world, "segments_in_flight": a.segments, "bitexact_vs_reference": bool(bitexact)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic},
         "kernels": {k: {"ms_per_step": round(v[1], 4), "launches_per_step": v[0],
                         "alg_GBps": round(v[2] / (v[1] / 1e3) / 1e9, 2) if v[1] > 0 else 0.0} for k, v in kern.items()},
+        "serial": {"value": round(V.job_throughput(px_seq * a.steps, elapsed_serial, R) / 1e6, 2),
+                   "ms_per_step": round(elapsed_serial / a.steps * 1e3, 3),
+                   "note": "one segment in flight (sync after every step)"},
         "mc_kernel_GBps": round(mc_gbs, 2),
         "host_prepare_s": round(t_prep, 3),
     }
@@ -169,8 +203,9 @@ def main():
         line["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, "tests", "golden", "streams", a.stream + ".bin"), px_seq)
     else:
         line["cpu_baseline"] = None
-    for hnd in handles:
-        ctx.release(hnd)
+    for handles, _ in copies:
+        for hnd in handles:
+            ctx.release(hnd)
     dec.close()
     if rank == 0:
         print(json.dumps(line))

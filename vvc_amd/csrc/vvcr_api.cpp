@@ -88,6 +88,7 @@ struct Prepared {
   hipEvent_t done = nullptr;
   bool ran[NK] = {};
   bool launched = false;
+  int lane = 0;                      // execution lane of the last launch (its stream and scratch planes)
   double alg_bytes[NK] = {};
   int launches[NK] = {};
 
@@ -115,12 +116,33 @@ struct KernelTimer {
 
 }  // namespace
 
+// Execution lanes: pictures are launched on NLANE HIP streams, each with its own scratch planes
+// (prediction, residual, loop-filter ping-pong). A picture waits only for the pictures it depends on —
+// the last writer of each reference slot (RAW), and the last writer and every reader since of its own
+// slot (WAW / WAR) — so pictures that do not reference each other (the pictures of one temporal layer of
+// an RA GOP, an intra picture and the B pictures decoded before it) reconstruct concurrently.
+constexpr int NLANE = 4;              // = the process's hardware queues (GPU_MAX_HW_QUEUES default)
+constexpr int NINTRA = 2;             // lanes reserved for pictures without references
+constexpr int NEV = 128;             // event ring (dependency markers)
+struct Lane {
+  hipStream_t s = nullptr;
+  DPlane pred[3], resi[3], tmp[3];
+  int tail_slot = -1;                // DPB slot written by the lane's last picture
+  uint64_t tail_seq = 0;             // launch sequence number of that picture
+};
+
 struct vvcr_ctx {
   vvcr_seq_params sp{};
   std::string err;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // lane 0's stream (host copies, vvcr_stream)
   std::vector<std::array<DPlane, 3>> dpb;
-  DPlane pred[3], resi[3], tmp[3];
+  Lane lanes[NLANE];
+  uint64_t seq = 0;
+  std::vector<hipEvent_t> slot_w;                 // per DPB slot: completion of its last writer
+  std::vector<std::vector<hipEvent_t>> slot_r;    // per DPB slot: completions of its readers since
+  std::vector<uint64_t> slot_seq;                 // per DPB slot: launch sequence number of its last writer
+  hipEvent_t ev_ring[NEV] = {};
+  int ev_next = 0;
   vvcr_pic_params pp{};
   bool in_picture = false;
   PictureDescriptors desc;          // host copy of the submitted descriptors (vvcr_host.h)
@@ -143,6 +165,11 @@ struct vvcr_ctx {
   hipEvent_t ev[2] = {};             // whole last launch
 };
 
+// every lane idle (host reads / writes of planes, vvcr_sync)
+static void sync_lanes(vvcr_ctx *ctx) {
+  for (Lane &ln : ctx->lanes) VVCR_CHECK_HIP(hipStreamSynchronize(ln.s));
+}
+
 #define API_BEGIN try {
 #define API_END                                                  \
   }                                                              \
@@ -154,11 +181,11 @@ static int n_ctb(const vvcr_seq_params &sp) {
   return ((sp.width + ctu - 1) / ctu) * ((sp.height + ctu - 1) / ctu);
 }
 
-static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp) {
+static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lane) {
   McParams P{};
   for (size_t s = 0; s < ctx->dpb.size() && s < 32; s++)
     for (int c = 0; c < 3; c++) P.ref[s][c] = ctx->dpb[s][c];
-  for (int c = 0; c < 3; c++) P.out[c] = ctx->pred[c];
+  for (int c = 0; c < 3; c++) P.out[c] = ctx->lanes[lane].pred[c];
   P.pic_w = ctx->sp.width;
   P.pic_h = ctx->sp.height;
   P.bd = ctx->sp.bit_depth;
@@ -177,10 +204,14 @@ static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp) {
 }
 
 // parameters of the intra / inter-reconstruction kernels for a prepared picture
-static IntraParams make_intra_params(vvcr_ctx *ctx, const Prepared &r) {
+static IntraParams make_intra_params(vvcr_ctx *ctx, const Prepared &r, int lane) {
   const vvcr_pic_params &pp = r.pp;
   IntraParams P{};
-  for (int c = 0; c < 3; c++) { P.reco[c] = ctx->dpb[pp.slot][c]; P.pred[c] = ctx->pred[c]; P.resi[c] = ctx->resi[c]; }
+  for (int c = 0; c < 3; c++) {
+    P.reco[c] = ctx->dpb[pp.slot][c];
+    P.pred[c] = ctx->lanes[lane].pred[c];
+    P.resi[c] = ctx->lanes[lane].resi[c];
+  }
   P.bd = ctx->sp.bit_depth;
   P.ctu = 1 << ctx->sp.ctu_log2;
   P.ctu_log2 = ctx->sp.ctu_log2;
@@ -265,8 +296,9 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     r.idep_start.upload(ip.dep_start);
     r.ideps.upload(ip.deps);
     r.istate.ensure(16 + ip.jobs.size());
-    const IntraParams P = make_intra_params(ctx, r);
-    r.iparams.upload(&P, 1);
+    IntraParams P[NLANE];   // one device copy per lane (scratch plane pointers differ)
+    for (int l = 0; l < NLANE; l++) P[l] = make_intra_params(ctx, r, l);
+    r.iparams.upload(P, NLANE);
     r.n_ijobs = (int)ip.jobs.size();
     r.ictu_list.upload(ip.ctu_list);
     r.ictu_start.upload(ip.ctu_start);
@@ -318,16 +350,45 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
 
 // Device phase: enqueue the kernels of a prepared picture on the context stream.
 static void launch(vvcr_ctx *ctx, Prepared &r) {
-  hipStream_t s = ctx->stream;
   const vvcr_pic_params &pp = r.pp;
   const uint32_t mask = r.mask;
+  std::vector<int> refs;
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < pp.num_ref[l]; i++)
+      if (std::find(refs.begin(), refs.end(), pp.ref_slot[l][i]) == refs.end()) refs.push_back(pp.ref_slot[l][i]);
+  // Lane choice: pictures without references (intra) take lanes [0, NINTRA), which only intra pictures
+  // use, so an intra picture never queues behind B pictures and two intra-started segments may overlap;
+  // the others take the lane of [NINTRA, NLANE) whose last picture is one of their references (stream
+  // order then costs nothing), else the least recently used of those lanes.
+  const int lo = refs.empty() ? 0 : NINTRA, hi = refs.empty() ? NINTRA : NLANE;
+  int L = -1;
+  if (!refs.empty())
+    for (int l = lo; l < hi && L < 0; l++) {
+      const int ts = ctx->lanes[l].tail_slot;
+      if (ts >= 0 && std::find(refs.begin(), refs.end(), ts) != refs.end() && ctx->lanes[l].tail_seq == ctx->slot_seq[ts]) L = l;
+    }
+  if (L < 0) {
+    uint64_t best = ~0ull;
+    for (int l = lo; l < hi; l++)
+      if (ctx->lanes[l].tail_seq < best) { best = ctx->lanes[l].tail_seq; L = l; }
+  }
+  Lane &ln = ctx->lanes[L];
+  hipStream_t s = ln.s;
+  r.lane = L;
+  ln.tail_slot = pp.slot;
+  ln.tail_seq = ++ctx->seq;
+  // dependencies on pictures of other lanes (same-lane work is ordered by the stream anyway)
+  for (int rs : refs)
+    if (ctx->slot_w[rs]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[rs], 0));
+  if (ctx->slot_w[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[pp.slot], 0));
+  for (hipEvent_t e : ctx->slot_r[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, e, 0));
   VVCR_CHECK_HIP(hipEventRecord(ctx->ev[0], s));
   if (mask & VVCR_STAGE_RESID) {
     KernelTimer t(r, K_RESID, s);
     for (int c = 0; c < 3; c++)
-      VVCR_CHECK_HIP(hipMemsetAsync(ctx->resi[c].p, 0, (size_t)ctx->resi[c].stride * ctx->resi[c].h * 2, s));
+      VVCR_CHECK_HIP(hipMemsetAsync(ln.resi[c].p, 0, (size_t)ln.resi[c].stride * ln.resi[c].h * 2, s));
     TbParams tp{};
-    for (int c = 0; c < 3; c++) tp.out[c] = ctx->resi[c];
+    for (int c = 0; c < 3; c++) tp.out[c] = ln.resi[c];
     tp.bd = ctx->sp.bit_depth;
     memcpy(tp.scan_off, ctx->scans.off, sizeof(tp.scan_off));
     memcpy(tp.lfnst_scan_off, ctx->scans.lfnst_off, sizeof(tp.lfnst_scan_off));
@@ -336,7 +397,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     r.launches[K_RESID] = (r.n_tb_small > 0) + (r.n_tb > r.n_tb_small);
   }
   if (mask & VVCR_STAGE_INTER) {
-    const McParams mp = make_mc_params(ctx, r.pp);
+    const McParams mp = make_mc_params(ctx, r.pp, L);
     {
       KernelTimer t(r, K_MC, s);
       launch_mc_basic(mp, r.mc_basic.p, r.n_basic, s);
@@ -357,7 +418,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     }
   }
   if (mask & VVCR_STAGE_INTRA) {
-    const IntraParams P = make_intra_params(ctx, r);
+    const IntraParams P = make_intra_params(ctx, r, L);
     {
       KernelTimer t(r, K_RECON, s);
       launch_recon_inter(P, r.tiles.p, r.n_tiles, s);
@@ -366,7 +427,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     }
     {
       KernelTimer t(r, K_INTRA, s);
-      launch_intra(r.iparams.p, r.ijobs.p, r.n_ijobs, r.ictu_list.p, r.ictu_start.p, r.n_ictu, r.idep_start.p, r.ideps.p,
+      launch_intra(r.iparams.p + L, r.ijobs.p, r.n_ijobs, r.ictu_list.p, r.ictu_start.p, r.n_ictu, r.idep_start.p, r.ideps.p,
                    r.istate.p, ctx->d_err, ctx->n_cu, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_INTRA] = r.n_ijobs ? 1 : 0;
@@ -394,7 +455,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   if (r.have_sao) {
     KernelTimer t(r, K_SAO, s);
     SaoParams sp{};
-    for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ctx->tmp[c]; }
+    for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ln.tmp[c]; }
     sp.sao = r.sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
     launch_sao(sp, s);
     VVCR_CHECK_HIP(hipGetLastError());
@@ -404,7 +465,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   if (r.have_alf) {
     KernelTimer t(r, K_ALF, s);
     AlfParams ap{};
-    for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ctx->tmp[c] : A[c]; ap.dst[c] = inTmp ? A[c] : ctx->tmp[c]; }
+    for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ln.tmp[c] : A[c]; ap.dst[c] = inTmp ? A[c] : ln.tmp[c]; }
     ap.bd = ctx->sp.bit_depth; ap.ctu_log2 = ctx->sp.ctu_log2; ap.wc = wc; ap.nctb = n;
     ap.vb_luma = pp.alf_vb_luma; ap.vb_chroma = pp.alf_vb_chroma;
     for (int c = 0; c < 3; c++) ap.en[c] = pp.alf_en[c];
@@ -420,10 +481,18 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   }
   if (inTmp)
     for (int c = 0; c < 3; c++)
-      VVCR_CHECK_HIP(hipMemcpy2DAsync(A[c].p, A[c].stride * 2, ctx->tmp[c].p, ctx->tmp[c].stride * 2, A[c].w * 2, A[c].h,
+      VVCR_CHECK_HIP(hipMemcpy2DAsync(A[c].p, A[c].stride * 2, ln.tmp[c].p, ln.tmp[c].stride * 2, A[c].w * 2, A[c].h,
                                       hipMemcpyDeviceToDevice, s));
   VVCR_CHECK_HIP(hipEventRecord(ctx->ev[1], s));
   VVCR_CHECK_HIP(hipEventRecord(r.done, s));
+  hipEvent_t e = ctx->ev_ring[ctx->ev_next];
+  ctx->ev_next = (ctx->ev_next + 1) % NEV;
+  VVCR_CHECK_HIP(hipEventRecord(e, s));
+  ctx->slot_w[pp.slot] = e;
+  ctx->slot_seq[pp.slot] = ln.tail_seq;
+  ctx->slot_r[pp.slot].clear();
+  for (int rs : refs)
+    if (rs != pp.slot) ctx->slot_r[rs].push_back(e);
   r.launched = true;
   ctx->last = &r;
 }
@@ -442,7 +511,9 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
   ctx->sp = *sp;
   try {
     VVCR_CHECK_HIP(hipSetDevice(sp->device));
-    VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    for (Lane &ln : ctx->lanes) VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ln.s, hipStreamNonBlocking));
+    ctx->stream = ctx->lanes[0].s;
+    for (auto &e : ctx->ev_ring) VVCR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const int W = sp->width, H = sp->height;
     ctx->dpb.resize(sp->dpb_slots);
     for (auto &s : ctx->dpb) {
@@ -450,12 +521,16 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       s[1] = alloc_plane(W / 2, H / 2);
       s[2] = alloc_plane(W / 2, H / 2);
     }
-    for (int c = 0; c < 3; c++) {
-      int w = c ? W / 2 : W, h = c ? H / 2 : H;
-      ctx->pred[c] = alloc_plane(w, h);
-      ctx->resi[c] = alloc_plane(w, h);
-      ctx->tmp[c] = alloc_plane(w, h);
-    }
+    ctx->slot_w.assign(sp->dpb_slots, nullptr);
+    ctx->slot_r.assign(sp->dpb_slots, {});
+    ctx->slot_seq.assign(sp->dpb_slots, 0);
+    for (Lane &ln : ctx->lanes)
+      for (int c = 0; c < 3; c++) {
+        int w = c ? W / 2 : W, h = c ? H / 2 : H;
+        ln.pred[c] = alloc_plane(w, h);
+        ln.resi[c] = alloc_plane(w, h);
+        ln.tmp[c] = alloc_plane(w, h);
+      }
     for (auto &e : ctx->ev) VVCR_CHECK_HIP(hipEventCreate(&e));
     VVCR_CHECK_HIP(hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, sp->device));
     VVCR_CHECK_HIP(hipMalloc(&ctx->d_err, sizeof(int32_t)));
@@ -473,14 +548,16 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
 
 int vvcr_destroy(vvcr_ctx *ctx) {
   if (!ctx) return VVCR_E_ARG;
-  (void)hipStreamSynchronize(ctx->stream);
+  for (Lane &ln : ctx->lanes) (void)hipStreamSynchronize(ln.s);
   ctx->prepared.clear();
   for (auto &s : ctx->dpb)
     for (auto &p : s) (void)hipFree(p.p);
-  for (int c = 0; c < 3; c++) { (void)hipFree(ctx->pred[c].p); (void)hipFree(ctx->resi[c].p); (void)hipFree(ctx->tmp[c].p); }
+  for (Lane &ln : ctx->lanes)
+    for (int c = 0; c < 3; c++) { (void)hipFree(ln.pred[c].p); (void)hipFree(ln.resi[c].p); (void)hipFree(ln.tmp[c].p); }
   for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
+  for (auto &e : ctx->ev_ring) if (e) (void)hipEventDestroy(e);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
-  (void)hipStreamDestroy(ctx->stream);
+  for (Lane &ln : ctx->lanes) (void)hipStreamDestroy(ln.s);
   delete ctx;
   return VVCR_OK;
 }
@@ -632,7 +709,7 @@ int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int3
 int vvcr_sync(vvcr_ctx *ctx) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
-  VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  sync_lanes(ctx);
   int32_t e = 0;
   VVCR_CHECK_HIP(hipMemcpy(&e, ctx->d_err, sizeof e, hipMemcpyDeviceToHost));
   if (e) {
@@ -671,8 +748,8 @@ static DPlane *select_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t co
     case VVCR_BUF_RECO:
       if (slot < 0 || slot >= (int)ctx->dpb.size()) throw VvcrError(VVCR_E_ARG, "bad slot");
       return &ctx->dpb[slot][comp];
-    case VVCR_BUF_PRED: return &ctx->pred[comp];
-    case VVCR_BUF_RESI: return &ctx->resi[comp];
+    case VVCR_BUF_PRED: return &ctx->lanes[ctx->last ? ctx->last->lane : 0].pred[comp];   // of the last launched picture
+    case VVCR_BUF_RESI: return &ctx->lanes[ctx->last ? ctx->last->lane : 0].resi[comp];
     default: throw VvcrError(VVCR_E_ARG, "bad buffer id");
   }
 }
@@ -681,6 +758,7 @@ int vvcr_read_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, int1
   if (!ctx || !dst) return VVCR_E_ARG;
   API_BEGIN
   DPlane *p = select_plane(ctx, buf, slot, comp);
+  sync_lanes(ctx);
   VVCR_CHECK_HIP(hipMemcpy2DAsync(dst, dst_stride * 2, p->p, p->stride * 2, p->w * 2, p->h, hipMemcpyDeviceToHost, ctx->stream));
   VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   int32_t e = 0;
@@ -697,6 +775,7 @@ int vvcr_write_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, con
   if (!ctx || !src) return VVCR_E_ARG;
   API_BEGIN
   DPlane *p = select_plane(ctx, buf, slot, comp);
+  sync_lanes(ctx);
   VVCR_CHECK_HIP(hipMemcpy2DAsync(p->p, p->stride * 2, src, src_stride * 2, p->w * 2, p->h, hipMemcpyHostToDevice, ctx->stream));
   VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
   int32_t e = 0;
@@ -726,8 +805,9 @@ int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n) {
   const int cnt = r ? r->n_dmvr : 0;
   const int64_t m = std::min<int64_t>(n, cnt);
   if (m > 0) {
-    VVCR_CHECK_HIP(hipMemcpyAsync(out, r->dmvr.p, (size_t)m * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    hipStream_t s = ctx->lanes[r->lane].s;
+    VVCR_CHECK_HIP(hipMemcpyAsync(out, r->dmvr.p, (size_t)m * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    VVCR_CHECK_HIP(hipStreamSynchronize(s));
   }
   return cnt;
   API_END

@@ -32,7 +32,7 @@ def plane_md5(plane):
 class SlotAllocator:
     """Assigns DPB slots so that a picture keeps its slot until its last use as a reference."""
 
-    def __init__(self, pics, nslots):
+    def __init__(self, pics, nslots, base=0):
         self.last_use = {}
         for i, p in enumerate(pics):
             self.last_use.setdefault(p["hdr"]["poc"], i)
@@ -41,7 +41,7 @@ class SlotAllocator:
                     self.last_use[int(p["ref_poc"][l][r])] = i
         self.nslots = nslots
         self.slot_of = {}
-        self.free = list(range(nslots))
+        self.free = list(range(base, base + nslots))   # base: a disjoint slot range per segment copy (bench.py)
 
     def assign(self, i, poc):
         # release pictures no longer referenced at or after decode index i
