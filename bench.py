@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--stream", default="ra1080_q32")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--segments", type=int, default=2, help="copies of the sequence the steps cycle through")
+    ap.add_argument("--sync-pictures", action="store_true",
+                    help="host sync after every picture (profiling: kernel durations without overlap)")
     a = ap.parse_args()
 
     R = V.Ranks()
@@ -118,6 +120,8 @@ def main():
     def run_step():
         for hnd in copies[nstep[0] % a.segments][0]:
             ctx.launch(hnd)
+            if a.sync_pictures:
+                ctx.sync()
         nstep[0] += 1
 
     for _ in range(a.warmup):

@@ -418,6 +418,7 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
   __shared__ int stmv[2][16][2];       // stored MV (before the picture clamp) for chroma
   __shared__ int csmv[2][4][2];        // chroma sub-block MVs
   __shared__ int16_t c14[16 * 16];     // PROF: 14-bit prediction of the tile
+  __shared__ int16_t hmid[16 * 44];    // separable luma: H-pass output, 11 rows x 4 columns per sub-block
   const int j = blockIdx.x;
   if (j >= njobs) return;
   const AffJob J = jobs[j];
@@ -529,9 +530,29 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
     const AffList &A = U.l[l];
     if (!A.present) continue;
     const int16_t *lwin = win + l * ALW;
-    // ---- luma: per sub-block 11x11 windows
+    // ---- luma: per sub-block 11x11 windows. Sub-blocks with both fractions non-zero run separably
+    // (filter<8,false,true,false> H pass over 11 rows into hmid, then the V pass), using the 6 non-zero
+    // taps of m_lumaFilter4x4 (InterpolationFilter.cpp:57: taps 0 and 7 are 0); the others take filt.
     const bool prof = A.prof;
     const bool rnd = !prof && !bi && !U.wp;
+    {
+      const int sh1 = IF_FILTER_PREC - headRoom, off1 = -(IF_INTERNAL_OFFS << sh1);
+#pragma unroll
+      for (int k = 0; k < 11; k++) {                 // <= 16 sub-blocks x 11 rows x 4 columns
+        const int i = lane + 64 * k;
+        const int sb = i / 44, e = i - sb * 44;
+        if (sb >= nsb) continue;
+        const int fx = sbmv[l][sb][0] & 15, fy = sbmv[l][sb][1] & 15;
+        if (fx == 0 || fy == 0) continue;
+        const int r = e >> 2, c = e & 3;
+        const int16_t *src = lwin + sb * AWS * AWS + r * AWS + c;
+        int sum = 0;
+#pragma unroll
+        for (int u = 1; u < 7; u++) sum += src[u] * x_luma4x4[fx][u];
+        hmid[i] = (int16_t)((sum + off1) >> sh1);
+      }
+    }
+    __syncthreads();
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const int i = lane + 64 * k;
@@ -539,10 +560,23 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
       const int y = i / w, x = i - y * w;
       const int sb = (y >> 2) * nsx + (x >> 2);
       const int fx = sbmv[l][sb][0] & 15, fy = sbmv[l][sb][1] & 15;
-      const int v = filt<8>(lwin + sb * AWS * AWS, AWS, x & 3, y & 3, fx, fy, x_luma4x4[fx], x_luma4x4[fy], rnd, bd);
+      int v;
+      if (fx != 0 && fy != 0) {
+        const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
+        const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
+        const int16_t *col = hmid + sb * 44 + (y & 3) * 4 + (x & 3);
+        int sum = 0;
+#pragma unroll
+        for (int t = 1; t < 7; t++) sum += col[t * 4] * x_luma4x4[fy][t];
+        v = (int)(int16_t)((sum + off2) >> sh2);
+        if (rnd) v = clampi(v, 0, maxv);
+      } else {
+        v = filt<8>(lwin + sb * AWS * AWS, AWS, x & 3, y & 3, fx, fy, x_luma4x4[fx], x_luma4x4[fy], rnd, bd);
+      }
       res[0][l][k] = v;
       if (prof) c14[y * 16 + x] = (int16_t)v;
     }
+    __syncthreads();   // hmid is reused by the other list
     if (prof) {
       __syncthreads();
       // PROF (:1209-1251): ring of integer samples, gradients (shift 6), dMv per position, applyPROFCore
