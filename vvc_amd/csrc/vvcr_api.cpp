@@ -85,7 +85,8 @@ struct Prepared {
   bool have_sao = false, have_alf = false;
   int n_tb = 0, n_tb_small = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
   hipEvent_t ev[NK][2] = {};
-  hipEvent_t done = nullptr;
+  hipEvent_t start = nullptr, done = nullptr;   // whole launch (events of this picture only: an event
+                                                // shared by pictures of several lanes would serialise them)
   bool ran[NK] = {};
   bool launched = false;
   int lane = 0;                      // execution lane of the last launch (its stream and scratch planes)
@@ -95,10 +96,12 @@ struct Prepared {
   Prepared() {
     for (auto &e : ev) { VVCR_CHECK_HIP(hipEventCreate(&e[0])); VVCR_CHECK_HIP(hipEventCreate(&e[1])); }
     VVCR_CHECK_HIP(hipEventCreate(&done));
+    VVCR_CHECK_HIP(hipEventCreate(&start));
   }
   ~Prepared() {
     for (auto &e : ev) { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); }
     (void)hipEventDestroy(done);
+    (void)hipEventDestroy(start);
   }
   void wait() { if (launched) VVCR_CHECK_HIP(hipEventSynchronize(done)); }
 };
@@ -162,7 +165,6 @@ struct vvcr_ctx {
   Prepared *last = nullptr;          // last launched (stage times, DMVR deltas)
   int n_cu = 256;                    // compute units (persistent intra launch width)
   int32_t *d_err = nullptr;          // device error flag of the persistent intra kernel (checked by vvcr_sync)
-  hipEvent_t ev[2] = {};             // whole last launch
 };
 
 // every lane idle (host reads / writes of planes, vvcr_sync)
@@ -382,7 +384,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     if (ctx->slot_w[rs]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[rs], 0));
   if (ctx->slot_w[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[pp.slot], 0));
   for (hipEvent_t e : ctx->slot_r[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, e, 0));
-  VVCR_CHECK_HIP(hipEventRecord(ctx->ev[0], s));
+  VVCR_CHECK_HIP(hipEventRecord(r.start, s));
   if (mask & VVCR_STAGE_RESID) {
     KernelTimer t(r, K_RESID, s);
     for (int c = 0; c < 3; c++)
@@ -483,7 +485,6 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     for (int c = 0; c < 3; c++)
       VVCR_CHECK_HIP(hipMemcpy2DAsync(A[c].p, A[c].stride * 2, ln.tmp[c].p, ln.tmp[c].stride * 2, A[c].w * 2, A[c].h,
                                       hipMemcpyDeviceToDevice, s));
-  VVCR_CHECK_HIP(hipEventRecord(ctx->ev[1], s));
   VVCR_CHECK_HIP(hipEventRecord(r.done, s));
   hipEvent_t e = ctx->ev_ring[ctx->ev_next];
   ctx->ev_next = (ctx->ev_next + 1) % NEV;
@@ -531,7 +532,6 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
         ln.resi[c] = alloc_plane(w, h);
         ln.tmp[c] = alloc_plane(w, h);
       }
-    for (auto &e : ctx->ev) VVCR_CHECK_HIP(hipEventCreate(&e));
     VVCR_CHECK_HIP(hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, sp->device));
     VVCR_CHECK_HIP(hipMalloc(&ctx->d_err, sizeof(int32_t)));
     VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof(int32_t)));
@@ -554,7 +554,6 @@ int vvcr_destroy(vvcr_ctx *ctx) {
     for (auto &p : s) (void)hipFree(p.p);
   for (Lane &ln : ctx->lanes)
     for (int c = 0; c < 3; c++) { (void)hipFree(ln.pred[c].p); (void)hipFree(ln.resi[c].p); (void)hipFree(ln.tmp[c].p); }
-  for (auto &e : ctx->ev) if (e) (void)hipEventDestroy(e);
   for (auto &e : ctx->ev_ring) if (e) (void)hipEventDestroy(e);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   for (Lane &ln : ctx->lanes) (void)hipStreamDestroy(ln.s);
@@ -723,9 +722,11 @@ int vvcr_sync(vvcr_ctx *ctx) {
 int vvcr_last_stage_times(vvcr_ctx *ctx, float *ms, int32_t n) {
   if (!ctx || !ms) return VVCR_E_ARG;
   API_BEGIN
-  VVCR_CHECK_HIP(hipEventSynchronize(ctx->ev[1]));
   float t = 0;
-  VVCR_CHECK_HIP(hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]));
+  if (ctx->last) {
+    VVCR_CHECK_HIP(hipEventSynchronize(ctx->last->done));
+    VVCR_CHECK_HIP(hipEventElapsedTime(&t, ctx->last->start, ctx->last->done));
+  }
   if (n > 0) ms[0] = t;
   for (int k = 1; k < n && k < 8; k++) ms[k] = 0;
   if (ctx->last) {
