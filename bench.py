@@ -172,7 +172,8 @@ def main():
     if os.path.exists(tf):
         with open(tf) as f:
             tj = json.load(f)
-        traffic = tj.get("per_group_launch_bytes", {}).get(dom)   # profiles/: tools/pmc.sh + tools/pmc_summary.py
+        if tj.get("stream", "ra1080_q32") == a.stream:   # the PMC passes were taken on this workload
+            traffic = tj.get("per_group_launch_bytes", {}).get(dom)   # profiles/: tools/pmc.sh + tools/pmc_summary.py
 
     ms_step = elapsed / a.steps * 1e3
     kind, qp = a.stream.split("_")[0], a.stream.split("_")[-1]

@@ -3,7 +3,7 @@ MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE and WRITE_SIZE are in K
 FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads, so it is doubled (our kernels mix
 access widths: the doubled figure is an upper estimate of the read bytes, the raw one a lower one).
 
-  python tools/pmc_summary.py gpurun_out/pmc_r01 > profiles/r01_traffic.json
+  python tools/pmc_summary.py gpurun_out/pmc_r01 [stream] > profiles/r01_traffic.json
 """
 import collections
 import csv
@@ -24,10 +24,10 @@ def per_kernel(path):
     return {k: {c: v / len(disp[k]) for c, v in cs.items()} for k, cs in agg.items()}, {k: len(v) for k, v in disp.items()}
 
 
-def main(d):
+def main(d, stream="ra1080_q32"):
     fetch, nf = per_kernel(os.path.join(d, "fetch", "run_counter_collection.csv"))
     write, nw = per_kernel(os.path.join(d, "write", "run_counter_collection.csv"))
-    out = {"source": d, "unit": "bytes per launch",
+    out = {"source": d, "stream": stream, "unit": "bytes per launch",
            "note": "read = 2 x FETCH_SIZE (gfx950 wide-read correction), write = WRITE_SIZE; KiB -> bytes",
            "per_launch_bytes": {}, "detail": {}}
     for k in sorted(set(fetch) | set(write)):
@@ -49,4 +49,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:3])
