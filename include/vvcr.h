@@ -177,7 +177,14 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t stage_mask);
 /* Two-phase form of vvcr_end_picture: prepare plans the picture on the host and uploads every input
  * (descriptors, work lists, loop-filter parameters) into device memory owned by the returned handle;
  * launch enqueues the picture's kernels (reading device-resident data only) and may be repeated, e.g.
- * to replay a resident sequence; release frees the handle after its last launch completed. */
+ * to replay a resident sequence; release frees the handle after its last launch completed.
+ *
+ * Ordering: launches are asynchronous and run on one of the context's execution lanes (HIP streams with
+ * their own scratch planes). A picture starts once the pictures it depends on through the DPB are done:
+ * the last writer of each of its reference slots, and the last writer and all readers since of its own
+ * slot. Pictures without such a dependency (e.g. the pictures of one temporal layer, or the intra
+ * picture of the next segment) may run concurrently. Host reads/writes of planes, vvcr_sync and
+ * vvcr_get_dmvr_deltas wait for the work they depend on. */
 int vvcr_prepare_picture(vvcr_ctx *ctx, uint32_t stage_mask, int32_t *handle);
 int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle);
 int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle);
@@ -211,7 +218,7 @@ int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n);
  * ms[1 + k] = stage k in VVCR_STAGE_* bit order (RESID, INTER, INTRA, LMCS_INV, DBK, SAO, ALF), 0 if
  * the stage did not run. n = number of entries wanted (<= 8). */
 int vvcr_last_stage_times(vvcr_ctx *ctx, float *ms, int32_t n);
-/* Raw HIP stream handle (hipStream_t) of the context, for callers that time or overlap work. */
+/* Raw HIP stream handle (hipStream_t) of the context's first execution lane (host copies use it). */
 void *vvcr_stream(vvcr_ctx *ctx);
 
 #ifdef __cplusplus
