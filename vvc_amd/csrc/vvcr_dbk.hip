@@ -1,8 +1,8 @@
 // vvcr_dbk.hip — deblocking filter for gfx950 (LoopFilter.cpp:844-1667 sample decisions + filters).
 //
-// The host plans every 4-sample edge segment (vvcr_dbk_host.cpp); here one lane decides and filters
-// one segment: 4 luma lines (xEdgeFilterLuma :981-1081) or 2 lines of Cb and of Cr
-// (xEdgeFilterChroma :1163-1283). All vertical edges of the picture are filtered before any horizontal
+// The host plans every 4-sample edge segment (vvcr_dbk_host.cpp); here four lanes decide and filter
+// one segment: one luma line each (xEdgeFilterLuma :981-1081), or one line of Cb or Cr each
+// (xEdgeFilterChroma :1163-1283), with the segment decisions exchanged by shuffles. All vertical edges of the picture are filtered before any horizontal
 // edge, as loopFilterPic (:165-240) does. Segments of one direction never overlap: each side modifies
 // at most maxFilterLength samples and reads at most one more, and the reference's length rules
 // (transform size <= 4 -> 1, sub-block edges 8 apart -> <= 3, 32-sample transforms for 7) keep the
@@ -144,11 +144,14 @@ __device__ __forceinline__ int tc_of(int idx, int bd) {
   return bd < 10 ? (t + 2) >> (10 - bd) : t << (bd - 10);
 }
 
+// Four lanes per 4-line luma segment, one line each: the segment decisions (xEdgeFilterLuma :981-1050)
+// need lines 0 and 3, whose terms the lanes exchange by shuffles; each lane then filters its own line.
 template <int DIR>
-__global__ void k_dbk_luma(DbkParams P, const DbkSeg *segs, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const DbkSeg sg = segs[i];
+__global__ __launch_bounds__(256) void k_dbk_luma(DbkParams P, const DbkSeg *segs, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = t >> 2, line = t & 3, l0 = (threadIdx.x & 63) & ~3;   // lane of line 0 of this segment
+  const bool valid = i < n;
+  const DbkSeg sg = valid ? segs[i] : DbkSeg{0, 0, 0};
   const uint32_t w = sg.w;
   const int bs = w & 3, lenP = (w >> 2) & 7, lenQ = (w >> 5) & 7, qp = (w >> 8) & 63;
   const bool pl = (w >> 14) & 1, ql = (w >> 15) & 1;
@@ -160,64 +163,73 @@ __global__ void k_dbk_luma(DbkParams P, const DbkSeg *segs, int n) {
   const int beta = vvcr_tab::dbk_beta[clip3(0, 63, qp + 2 * P.beta_offset_div2)] * (1 << (bd - 8));
   const int sideThr = (beta + (beta >> 1)) >> 3;
   const int thrCut = tc * 10;
-  int16_t *base = Y.p + (size_t)(sg.y4 * 4) * Y.stride + sg.x4 * 4;
-  int16_t *s0 = base, *s3 = base + 3 * step;
-  const int dp0 = calc_dp(s0, o, false), dq0 = calc_dq(s0, o), dp3 = calc_dp(s3, o, false), dq3 = calc_dq(s3, o);
+  int16_t *s = Y.p + (size_t)(sg.y4 * 4) * Y.stride + sg.x4 * 4 + line * step;
+  // this line's terms (all lanes compute, lines 0 and 3 are used)
+  int dp = 0, dq = 0, dpL = 0, dqL = 0;
+  if (valid) {
+    dp = calc_dp(s, o, false);
+    dq = calc_dq(s, o);
+    dpL = dp; dqL = dq;
+    if (pl) dpL = (dpL + calc_dp(s - 3 * o, o, false) + 1) >> 1;
+    if (ql) dqL = (dqL + calc_dq(s + 3 * o, o) + 1) >> 1;
+  }
+  const int dp0 = __shfl(dp, l0), dq0 = __shfl(dq, l0), dp3 = __shfl(dp, l0 + 3), dq3 = __shfl(dq, l0 + 3);
+  const int dp0L = __shfl(dpL, l0), dq0L = __shfl(dqL, l0), dp3L = __shfl(dpL, l0 + 3), dq3L = __shfl(dqL, l0 + 3);
+  // long-filter decision
+  bool longStrong = false, fPL = false, fQL = false;
   if (pl || ql) {
-    int dp0L = dp0, dq0L = dq0, dp3L = dp3, dq3L = dq3;
-    if (pl) {
-      dp0L = (dp0L + calc_dp(s0 - 3 * o, o, false) + 1) >> 1;
-      dp3L = (dp3L + calc_dp(s3 - 3 * o, o, false) + 1) >> 1;
-    }
-    if (ql) {
-      dq0L = (dq0L + calc_dq(s0 + 3 * o, o) + 1) >> 1;
-      dq3L = (dq3L + calc_dq(s3 + 3 * o, o) + 1) >> 1;
-    }
     const int d0L = dp0L + dq0L, d3L = dp3L + dq3L;
     if (d0L + d3L < beta) {
-      const bool fP = dp0L + dp3L < sideThr, fQ = dq0L + dq3L < sideThr;
-      if (use_strong(s0, o, 2 * d0L, beta, tc, pl, ql, lenP, lenQ, false) && use_strong(s3, o, 2 * d3L, beta, tc, pl, ql, lenP, lenQ, false)) {
-        for (int k = 0; k < 4; k++) filter_luma_line(base + k * step, o, tc, true, thrCut, fP, fQ, maxv, pl, ql, lenP, lenQ);
-        return;
-      }
+      fPL = dp0L + dp3L < sideThr;
+      fQL = dq0L + dq3L < sideThr;
+      const int myd = line == 0 ? d0L : d3L;
+      const bool st = valid && (line == 0 || line == 3) && use_strong(s, o, 2 * myd, beta, tc, pl, ql, lenP, lenQ, false);
+      longStrong = __shfl((int)st, l0) && __shfl((int)st, l0 + 3);
     }
   }
+  // normal / strong short-filter decision
   const int d0 = dp0 + dq0, d3 = dp3 + dq3;
-  if (d0 + d3 >= beta) return;
   bool fP = false, fQ = false, sw = false;
-  if (lenP > 1 && lenQ > 1) { fP = dp0 + dp3 < sideThr; fQ = dq0 + dq3 < sideThr; }
-  if (lenP > 2 && lenQ > 2)
-    sw = use_strong(s0, o, 2 * d0, beta, tc, false, false, 7, 7, false) && use_strong(s3, o, 2 * d3, beta, tc, false, false, 7, 7, false);
-  for (int k = 0; k < 4; k++) filter_luma_line(base + k * step, o, tc, sw, thrCut, fP, fQ, maxv, false, false, 7, 7);
+  const bool on = !longStrong && d0 + d3 < beta;
+  if (!longStrong) {
+    if (lenP > 1 && lenQ > 1) { fP = dp0 + dp3 < sideThr; fQ = dq0 + dq3 < sideThr; }
+    bool st = false;
+    if (on && lenP > 2 && lenQ > 2 && valid && (line == 0 || line == 3))
+      st = use_strong(s, o, 2 * (line == 0 ? d0 : d3), beta, tc, false, false, 7, 7, false);
+    sw = __shfl((int)st, l0) && __shfl((int)st, l0 + 3);
+  }
+  if (!valid) return;
+  if (longStrong) filter_luma_line(s, o, tc, true, thrCut, fPL, fQL, maxv, pl, ql, lenP, lenQ);
+  else if (on) filter_luma_line(s, o, tc, sw, thrCut, fP, fQ, maxv, false, false, 7, 7);
 }
 
+// Four lanes per chroma segment: (component, line) = (lane >> 1, lane & 1); the strong-filter decision
+// of a component uses both of its lines (xEdgeFilterChroma :1163-1283), exchanged by shuffles.
 template <int DIR>
-__global__ void k_dbk_chroma(DbkParams P, const DbkSeg *segs, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const DbkSeg sg = segs[i];
+__global__ __launch_bounds__(256) void k_dbk_chroma(DbkParams P, const DbkSeg *segs, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = t >> 2, k = (t >> 1) & 1, l = t & 1, lp = (threadIdx.x & 63) & ~1;   // lp: line 0 of this component
+  const bool valid = i < n;
+  const DbkSeg sg = valid ? segs[i] : DbkSeg{0, 0, 0};
   const uint32_t w = sg.w;
   const bool large = (w >> 4) & 1, ctbh = (w >> 19) & 1;
   const int bd = P.bd, maxv = (1 << bd) - 1;
-  for (int k = 0; k < 2; k++) {
-    const int bs = (w >> (2 * k)) & 3;
-    if (!(bs == 2 || (large && bs == 1))) continue;
-    const int qp = (int)((w >> (5 + 7 * k)) & 127) - 64;
-    const DPlane &C = P.pl[1 + k];
-    const int o = DIR == 0 ? 1 : C.stride;
-    const int step = DIR == 0 ? C.stride : 1;
-    const int tc = tc_of(clip3(0, 65, qp + 2 * (bs - 1) + 2 * P.tc_offset_div2), bd);
-    int16_t *base = C.p + (size_t)(sg.y4 * 2) * C.stride + sg.x4 * 2;
-    bool sw = false;
-    if (large) {
-      const int beta = vvcr_tab::dbk_beta[clip3(0, 63, qp + 2 * P.beta_offset_div2)] * (1 << (bd - 8));
-      int16_t *s0 = base, *s1 = base + step;
-      const int d0 = calc_dp(s0, o, ctbh) + calc_dq(s0, o), d3 = calc_dp(s1, o, ctbh) + calc_dq(s1, o);
-      if (d0 + d3 < beta)
-        sw = use_strong(s0, o, 2 * d0, beta, tc, false, false, 7, 7, ctbh) && use_strong(s1, o, 2 * d3, beta, tc, false, false, 7, 7, ctbh);
-    }
-    for (int l = 0; l < 2; l++) filter_chroma_line(base + l * step, o, tc, sw, maxv, ctbh);
-  }
+  const int bs = (w >> (2 * k)) & 3;
+  const bool act = valid && (bs == 2 || (large && bs == 1));
+  const int qp = (int)((w >> (5 + 7 * k)) & 127) - 64;
+  const DPlane &C = P.pl[1 + k];
+  const int o = DIR == 0 ? 1 : C.stride;
+  const int step = DIR == 0 ? C.stride : 1;
+  const int tc = tc_of(clip3(0, 65, qp + 2 * (bs - 1) + 2 * P.tc_offset_div2), bd);
+  int16_t *s = C.p + (size_t)(sg.y4 * 2) * C.stride + sg.x4 * 2 + l * step;
+  int d = 0;
+  const int beta = vvcr_tab::dbk_beta[clip3(0, 63, qp + 2 * P.beta_offset_div2)] * (1 << (bd - 8));
+  if (act && large) d = calc_dp(s, o, ctbh) + calc_dq(s, o);
+  const int dsum = __shfl(d, lp) + __shfl(d, lp + 1);
+  bool st = false;
+  if (act && large && dsum < beta) st = use_strong(s, o, 2 * d, beta, tc, false, false, 7, 7, ctbh);
+  const bool sw = __shfl((int)st, lp) && __shfl((int)st, lp + 1);
+  if (act) filter_chroma_line(s, o, tc, sw, maxv, ctbh);
 }
 
 }  // namespace
@@ -228,7 +240,7 @@ void launch_dbk(const DbkParams &p, const DbkSeg *segs, const int counts[4], hip
   for (int k = 0; k < 4; k++) {
     const int n = counts[k];
     if (n > 0) {
-      const dim3 g((n + T - 1) / T);
+      const dim3 g((4 * n + T - 1) / T);   // four lanes per segment
       const DbkSeg *sg = segs + off;
       switch (k) {
         case 0: hipLaunchKernelGGL(k_dbk_luma<0>, g, dim3(T), 0, s, p, sg, n); break;
