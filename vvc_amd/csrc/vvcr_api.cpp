@@ -387,8 +387,9 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   VVCR_CHECK_HIP(hipEventRecord(r.start, s));
   if (mask & VVCR_STAGE_RESID) {
     KernelTimer t(r, K_RESID, s);
-    for (int c = 0; c < 3; c++)
-      VVCR_CHECK_HIP(hipMemsetAsync(ln.resi[c].p, 0, (size_t)ln.resi[c].stride * ln.resi[c].h * 2, s));
+    Planes3 clr{};
+    for (int c = 0; c < 3; c++) clr.dst[c] = ln.resi[c];
+    launch_planes3(clr, s);
     TbParams tp{};
     for (int c = 0; c < 3; c++) tp.out[c] = ln.resi[c];
     tp.bd = ctx->sp.bit_depth;
@@ -481,10 +482,12 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     inTmp = !inTmp;
     r.launches[K_ALF] = 2;
   }
-  if (inTmp)
-    for (int c = 0; c < 3; c++)
-      VVCR_CHECK_HIP(hipMemcpy2DAsync(A[c].p, A[c].stride * 2, ln.tmp[c].p, ln.tmp[c].stride * 2, A[c].w * 2, A[c].h,
-                                      hipMemcpyDeviceToDevice, s));
+  if (inTmp) {
+    Planes3 cp{};
+    for (int c = 0; c < 3; c++) { cp.dst[c] = A[c]; cp.src[c] = ln.tmp[c]; }
+    cp.copy = 1;
+    launch_planes3(cp, s);
+  }
   VVCR_CHECK_HIP(hipEventRecord(r.done, s));
   hipEvent_t e = ctx->ev_ring[ctx->ev_next];
   ctx->ev_next = (ctx->ev_next + 1) % NEV;

@@ -167,11 +167,17 @@ struct AlfParams {
   const int16_t *ctb_set;
 };
 
+struct Planes3 {
+  DPlane dst[3], src[3];
+  int32_t copy;                // 0: clear dst, 1: dst <- src (same sizes)
+};
+
 // launchers (vvcr_mc.hip, vvcr_mc_ext.hip, vvcr_resid.hip, vvcr_lf.hip)
 void launch_mc_bidir(const McParams &p, const McJob *jobs, int njobs, int32_t *dmvr_out, hipStream_t s);
 void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const AffPu *pus, hipStream_t s);
 void launch_sao(const SaoParams &p, hipStream_t s);
 void launch_alf(const AlfParams &p, hipStream_t s);
+void launch_planes3(const Planes3 &p, hipStream_t s);
 // jobs[0, nsmall): blocks of <= 256 samples (64-lane workgroups); jobs[nsmall, njobs): larger (256 lanes)
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, int nsmall, const int32_t *coef, const uint16_t *scans, hipStream_t s);
 void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);

@@ -16,7 +16,8 @@ namespace {
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
 
-__global__ void k_sao(SaoParams P, int comp) {
+__global__ void k_sao(SaoParams P) {
+  const int comp = blockIdx.z;               // one launch for the three planes
   const DPlane &S = P.src[comp];
   const DPlane &D = P.dst[comp];
   const int W = S.w, H = S.h;
@@ -257,11 +258,27 @@ __global__ void k_alf_chroma(AlfParams P) {
 }  // namespace
 
 void launch_sao(const SaoParams &p, hipStream_t s) {
-  for (int c = 0; c < 3; c++) {
-    const int W = p.src[c].w, H = p.src[c].h;
-    dim3 grid(((W + 3) / 4 + 63) / 64, H);
-    hipLaunchKernelGGL(k_sao, grid, dim3(64), 0, s, p, c);
-  }
+  const int W = p.src[0].w, H = p.src[0].h;   // luma bounds; chroma blocks beyond their plane exit
+  dim3 grid(((W + 3) / 4 + 63) / 64, H, 3);
+  hipLaunchKernelGGL(k_sao, grid, dim3(64), 0, s, p);
+}
+
+// Clear (copy == 0) or copy the three planes of a picture in one launch (the per-picture residual
+// clear and the SAO-only copy-back would otherwise be three runtime fill / copy dispatches each).
+__global__ __launch_bounds__(256) void k_planes3(Planes3 P) {
+  const int c = blockIdx.z;
+  const DPlane &D = P.dst[c];
+  const int y = blockIdx.y, x = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (y >= D.h || x >= D.w) return;
+  // 8 samples (16 B) per lane: planes are 128-B pitched, so the vector stays inside the row
+  uint4 *d = (uint4 *)(D.p + (size_t)y * D.stride + x);
+  *d = P.copy ? *(const uint4 *)(P.src[c].p + (size_t)y * P.src[c].stride + x) : make_uint4(0, 0, 0, 0);
+}
+
+void launch_planes3(const Planes3 &p, hipStream_t s) {
+  const int W = p.dst[0].w, H = p.dst[0].h;
+  dim3 grid(((W + 7) / 8 + 255) / 256, H, 3);
+  hipLaunchKernelGGL(k_planes3, grid, dim3(256), 0, s, p);
 }
 
 void launch_alf(const AlfParams &p, hipStream_t s) {
