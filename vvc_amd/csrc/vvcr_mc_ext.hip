@@ -470,39 +470,37 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
     }
   }
   __syncthreads();
-  // ---- gather every window of the tile in one phase (all loads in flight before the first LDS write);
-  // lists and components are walked with compile-time indices so nothing lands in scratch
+  // ---- gather every window of the tile in one phase (all loads in flight before the first LDS write).
+  // A lane owns fixed window positions — luma e = lane, lane + 64 of the 11x11 window, chroma e = lane of
+  // the 7x7 — and walks the sub-blocks, whose window origins are wave-uniform (scalar), so a load costs
+  // a few VALU ops; lists / components / sub-blocks have compile-time indices (nothing in scratch).
   {
-    constexpr int ALIT = (ALW + 63) / 64, ACIT = (ACW + 63) / 64;
-    int16_t vl[2][ALIT] = {}, vc[2][2][ACIT] = {};
+    const int r0 = lane / AWS, c0 = lane - r0 * AWS, e1 = lane + 64, r1 = e1 / AWS, c1 = e1 - r1 * AWS;
+    const bool has1 = e1 < AWS * AWS;
+    const int rc = lane / 7, cc = lane - rc * 7;
+    const bool hasc = lane < 49;
+    int16_t vl[2][16][2] = {}, vc[2][2][4] = {};
 #pragma unroll
     for (int l = 0; l < 2; l++) {
       if (!U.l[l].present) continue;
       const DPlane &R = P.ref[U.l[l].slot][0];
 #pragma unroll
-      for (int k = 0; k < ALIT; k++) {
-        const int e = lane + 64 * k;
-        const int sb = e / (AWS * AWS), e2 = e - sb * (AWS * AWS);
-        const int r = e2 / AWS, c = e2 - r * AWS;
-        if (e < ALW && sb < nsb) {
-          const int sx = J.x + (sb & (nsx - 1)) * 4 + (sbmv[l][sb][0] >> 4) - 3 + c;
-          const int sy = J.y + (sb >> lnsx) * 4 + (sbmv[l][sb][1] >> 4) - 3 + r;
-          vl[l][k] = R.p[(size_t)clampi(sy, 0, R.h - 1) * R.stride + clampi(sx, 0, R.w - 1)];
-        }
+      for (int sb = 0; sb < 16; sb++) {
+        if (sb >= nsb) continue;
+        const int ox = __builtin_amdgcn_readfirstlane(J.x + (sb & (nsx - 1)) * 4 + (sbmv[l][sb][0] >> 4) - 3);
+        const int oy = __builtin_amdgcn_readfirstlane(J.y + (sb >> lnsx) * 4 + (sbmv[l][sb][1] >> 4) - 3);
+        vl[l][sb][0] = R.p[clampi(oy + r0, 0, R.h - 1) * R.stride + clampi(ox + c0, 0, R.w - 1)];
+        if (has1) vl[l][sb][1] = R.p[clampi(oy + r1, 0, R.h - 1) * R.stride + clampi(ox + c1, 0, R.w - 1)];
       }
 #pragma unroll
       for (int comp = 1; comp < 3; comp++) {
         const DPlane &RC = P.ref[U.l[l].slot][comp];
 #pragma unroll
-        for (int k = 0; k < ACIT; k++) {
-          const int e = lane + 64 * k;
-          const int cb = e / 49, e3 = e - cb * 49;
-          const int r = e3 / 7, c = e3 - r * 7;
-          if (e < ACW && cb < ncb) {
-            const int sx = (J.x >> 1) + (cb % ncx) * 4 + (csmv[l][cb][0] >> 5) - 1 + c;
-            const int sy = (J.y >> 1) + (cb / ncx) * 4 + (csmv[l][cb][1] >> 5) - 1 + r;
-            vc[l][comp - 1][k] = RC.p[(size_t)clampi(sy, 0, RC.h - 1) * RC.stride + clampi(sx, 0, RC.w - 1)];
-          }
+        for (int cb = 0; cb < 4; cb++) {
+          if (cb >= ncb) continue;
+          const int ox = __builtin_amdgcn_readfirstlane((J.x >> 1) + (cb % ncx) * 4 + (csmv[l][cb][0] >> 5) - 1);
+          const int oy = __builtin_amdgcn_readfirstlane((J.y >> 1) + (cb / ncx) * 4 + (csmv[l][cb][1] >> 5) - 1);
+          if (hasc) vc[l][comp - 1][cb] = RC.p[clampi(oy + rc, 0, RC.h - 1) * RC.stride + clampi(ox + cc, 0, RC.w - 1)];
         }
       }
     }
@@ -510,17 +508,16 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
     for (int l = 0; l < 2; l++) {
       if (!U.l[l].present) continue;
 #pragma unroll
-      for (int k = 0; k < ALIT; k++) {
-        const int e = lane + 64 * k;
-        if (e < ALW) win[l * ALW + e] = vl[l][k];
+      for (int sb = 0; sb < 16; sb++) {
+        if (sb >= nsb) continue;
+        win[l * ALW + sb * AWS * AWS + lane] = vl[l][sb][0];
+        if (has1) win[l * ALW + sb * AWS * AWS + e1] = vl[l][sb][1];
       }
 #pragma unroll
       for (int comp = 1; comp < 3; comp++)
 #pragma unroll
-        for (int k = 0; k < ACIT; k++) {
-          const int e = lane + 64 * k;
-          if (e < ACW) win[2 * ALW + l * 2 * ACW + (comp - 1) * ACW + e] = vc[l][comp - 1][k];
-        }
+        for (int cb = 0; cb < 4; cb++)
+          if (cb < ncb && hasc) win[2 * ALW + l * 2 * ACW + (comp - 1) * ACW + cb * 49 + lane] = vc[l][comp - 1][cb];
     }
   }
   __syncthreads();
