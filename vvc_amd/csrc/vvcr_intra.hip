@@ -379,6 +379,9 @@ __device__ __forceinline__ NbAvail nb_decode(uint32_t b) {
 #ifndef VVCR_LSLEEP
 #define VVCR_LSLEEP 1
 #endif
+#ifndef VVCR_INTRA_PRIO
+#define VVCR_INTRA_PRIO 3
+#endif
 #ifndef VVCR_GSLEEP
 #define VVCR_GSLEEP 2
 #endif
@@ -1020,6 +1023,9 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
   __shared__ int s_ctu, s_next;
   __shared__ __attribute__((aligned(16))) uint32_t s_Praw[sizeof(IntraParams) / 4];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // The intra chain is latency bound and shares its CUs with the B pictures' kernels of other lanes:
+  // its waves take issue priority over them.
+  __builtin_amdgcn_s_setprio(VVCR_INTRA_PRIO);
   int32_t *done = state + 16;
   WaveScratch &S = s_ws[wid];
   // The parameters live in LDS for the whole launch: every plane pointer / size the step body reads is
