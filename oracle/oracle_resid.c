@@ -357,3 +357,47 @@ int or_residual_picture(const or_pic *P, const int32_t *cu, int ncu, const int32
   free(lmap);
   return 0;
 }
+
+/* ---------------------------------------------------------------------------------------------------
+ * Forward transform of the encoder's RDO loop: TrQuant::xT (TrQuant.cpp:749-824) with
+ * maxLog2TrDynamicRange 15. Each 1-D pass restates the partial butterflies fastForwardDCT2_B* /
+ * DST7 / DCT8 (TrQuant_EMT.cpp; _fastForwardMM for the larger DST7 / DCT8) as the integer matrix
+ * product they compute: dst[k * line + j] = (sum_n M[k][n] src[j][n] + rnd) >> shift for the first
+ * line - skipLine lines, zero elsewhere (no clipping in the forward path). The output cut-off
+ * N - skipLine2 is honoured by DST7 / DCT8 (_fastForwardMM :237-276, B16/B32) and by DCT2_B64 (:689-690)
+ * only: fastForwardDCT2_B2..B32 compute all N outputs whatever skipLine2 (:131-175, :287-343, :527-607).
+ * trh / trv: 0 DCT2, 1 DST7, 2 DCT8; lfnst != 0 selects the LFNST zero-out of xT (:766-777).
+ * ------------------------------------------------------------------------------------------------- */
+static void fwd_1d(const int32_t *src, int32_t *dst, int N, int line, int skipLine, int skipLine2, int shift, const int16_t *M,
+                   int type) {
+  const int rnd = shift > 0 ? 1 << (shift - 1) : 0, reduced = line - skipLine;
+  const int cutoff = (type == DCT2 && N <= 32) ? N : N - skipLine2;
+  for (int k = 0; k < N; k++)
+    for (int j = 0; j < line; j++) {
+      int32_t v = 0;
+      if (k < cutoff && j < reduced) {
+        int64_t s = 0;
+        for (int n = 0; n < N; n++) s += (int64_t)M[k * N + n] * src[j * N + n];
+        v = (int32_t)((s + rnd) >> shift);
+      }
+      dst[k * line + j] = v;
+    }
+}
+
+int or_fwd_transform(const int16_t *resi, int w, int h, int trh, int trv, int lfnst, int bd, int32_t *coef) {
+  int skipW = (trh != DCT2 && w == 32) ? 16 : (w > 32 ? w - 32 : 0);
+  int skipH = (trv != DCT2 && h == 32) ? 16 : (h > 32 ? h - 32 : 0);
+  if (lfnst) {
+    if ((w == 4 && h > 4) || (w > 4 && h == 4)) { skipW = w - 4; skipH = h - 4; }
+    else if (w >= 8 && h >= 8) { skipW = w - 8; skipH = h - 8; }
+  }
+  if (w < 4 || h < 4) return -1;
+  int32_t *blk = (int32_t *)malloc(sizeof(int32_t) * w * h), *tmp = (int32_t *)malloc(sizeof(int32_t) * w * h);
+  for (int i = 0; i < w * h; i++) blk[i] = resi[i];
+  const int s1 = ilog2(w) + bd + 6 - 15, s2 = ilog2(h) + 6;   /* g_transformMatrixShift[FORWARD] = 6 */
+  fwd_1d(blk, tmp, w, h, 0, skipW, s1, tr_matrix(trh, w), trh);
+  fwd_1d(tmp, coef, h, w, skipW, skipH, s2, tr_matrix(trv, h), trv);
+  free(blk);
+  free(tmp);
+  return 0;
+}

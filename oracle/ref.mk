@@ -43,7 +43,7 @@ ENCAPP_OBJ = $(call obj,$(ENCAPP_SRC))
 WRAPS = $(shell cat $(CURDIR)/oracle/capture/wraps.txt 2>/dev/null)
 WRAPFLAGS = $(foreach s,$(WRAPS),-Wl,--wrap=$(s))
 
-all: apps capture
+all: apps capture rdo_kat
 apps: $(OUT)/DecoderApp $(OUT)/EncoderApp
 capture: $(OUT)/vtm_capture
 
@@ -69,6 +69,13 @@ $(OUT)/obj/capture/vtm_capture.o: $(CAP_SRC) $(CURDIR)/oracle/capture/wraps.txt
 CAPAPP_OBJ = $(call obj,$(SRC)/App/DecoderApp/DecApp.cpp $(SRC)/App/DecoderApp/DecAppCfg.cpp)
 $(OUT)/vtm_capture: $(OUT)/obj/capture/vtm_capture.o $(CAPAPP_OBJ) $(DEC_OBJ) $(COMMON_OBJ) $(UTIL_OBJ) $(CURDIR)/oracle/capture/wraps.txt
 	$(CXX) -pthread -o $@ $(OUT)/obj/capture/vtm_capture.o $(CAPAPP_OBJ) $(DEC_OBJ) $(UTIL_OBJ) $(COMMON_OBJ) $(WRAPFLAGS)
+
+# RDO known-answer harness (RdCost distortion + forward transforms of the reference, oracle/capture/rdo_kat.cpp)
+rdo_kat: $(OUT)/rdo_kat
+$(OUT)/obj/capture/rdo_kat.o: $(CURDIR)/oracle/capture/rdo_kat.cpp
+	@mkdir -p $(@D); $(CXX) $(CXXFLAGS) -c $< -o $@
+$(OUT)/rdo_kat: $(OUT)/obj/capture/rdo_kat.o $(OUT)/libCommonLib.a
+	$(CXX) -pthread -o $@ $(OUT)/obj/capture/rdo_kat.o $(OUT)/libCommonLib.a
 
 $(OUT)/obj/Lib/CommonLib/x86/sse41/%.o: $(SRC)/Lib/CommonLib/x86/sse41/%.cpp
 	@mkdir -p $(@D); $(CXX) $(CXXFLAGS) -msse4.1 -DUSE_SSE41 -c $< -o $@
