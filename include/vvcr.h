@@ -221,6 +221,41 @@ int vvcr_last_stage_times(vvcr_ctx *ctx, float *ms, int32_t n);
 /* Raw HIP stream handle (hipStream_t) of the context's first execution lane (host copies use it). */
 void *vvcr_stream(vvcr_ctx *ctx);
 
+
+/* ============================================================================================== *
+ * Encoder RDO inner loop (BASELINE config 5): batched distortion and forward
+ * transforms. They replace, for a batch of blocks at once, the per-block calls the encoder makes:
+ *   vvcr_rd_*   <- RdCost::setDistParam + DistParam::distFunc (RdCost.h:181, RdCost.cpp:503 xGetSAD,
+ *                  :2800 xGetHADs — the Hadamard SATD with its 2x2 .. 16x8 tiles), bit depth 10;
+ *   vvcr_fwd_*  <- TrQuant::xT (TrQuant.cpp:749-824) over fastFwdTrans (TrQuant.cpp:69-74).
+ * plan uploads the block list (host pointers) and returns a handle; run reads DEVICE pointers (inputs
+ * resident in HBM) and is asynchronous on the context stream (vvcr_sync waits); the vvcr_rd_dist /
+ * vvcr_fwd_transform forms take host pointers and block until the results are copied back.
+ * ============================================================================================== */
+typedef struct vvcr_rd_block {
+  int64_t org_off, cur_off;        /* sample offsets of the block in the original / prediction pools */
+  int32_t org_stride, cur_stride;  /* row pitch in samples */
+  int32_t width, height;           /* even sizes (xGetHADs rejects odd ones) */
+} vvcr_rd_block;
+typedef struct vvcr_fwd_block {
+  int64_t src_off;                 /* residual sample offset */
+  int64_t dst_off;                 /* coefficient offset: width*height int32, row-major */
+  int32_t src_stride;
+  int32_t width, height;           /* 4..64 (DCT2), 4..32 (DST7 / DCT8) */
+  int32_t tr_hor, tr_ver;          /* 0 DCT2, 1 DST7, 2 DCT8 */
+  int32_t lfnst;                   /* non-zero: the zero-out xT applies when lfnstIdx != 0 */
+} vvcr_fwd_block;
+int vvcr_rd_plan(vvcr_ctx *ctx, const vvcr_rd_block *blocks, int32_t n, int32_t *plan);
+int vvcr_rd_run(vvcr_ctx *ctx, int32_t plan, const int16_t *org_dev, const int16_t *cur_dev, uint32_t *sad_dev,
+                uint32_t *satd_dev);
+int vvcr_fwd_plan(vvcr_ctx *ctx, const vvcr_fwd_block *blocks, int32_t n, int32_t bit_depth, int32_t *plan);
+int vvcr_fwd_run(vvcr_ctx *ctx, int32_t plan, const int16_t *resi_dev, int32_t *coef_dev);
+int vvcr_rdo_release(vvcr_ctx *ctx, int32_t plan);
+int vvcr_rd_dist(vvcr_ctx *ctx, const vvcr_rd_block *blocks, int32_t n, const int16_t *org, int64_t norg,
+                 const int16_t *cur, int64_t ncur, uint32_t *sad, uint32_t *satd);
+int vvcr_fwd_transform(vvcr_ctx *ctx, const vvcr_fwd_block *blocks, int32_t n, int32_t bit_depth, const int16_t *resi,
+                       int64_t nresi, int32_t *coef, int64_t ncoef);
+
 #ifdef __cplusplus
 }
 #endif

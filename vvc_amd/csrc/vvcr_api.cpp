@@ -119,6 +119,30 @@ struct KernelTimer {
 
 }  // namespace
 
+// A planned batch of the encoder RDO inner loop: Hadamard tiles sorted by kind (distortion) or the
+// transform blocks (forward transform), resident on the device.
+struct RdoPlan {
+  bool fwd = false;
+  int nblocks = 0, bd = 10;
+  DevVec<RdBlockDev> blocks;
+  DevVec<RdTile> tiles[RD_KINDS];
+  int ntiles[RD_KINDS] = {};
+  DevVec<FwdBlockDev> fblocks;
+  int64_t coef_total = 0;
+};
+
+// Hadamard tile of RdCost::xGetHADs for a w x h block (RdCost.cpp:2818-2911), or -1 for odd sizes
+static int rd_kind(int w, int h, int &tw, int &th) {
+  if (w > h && (h & 7) == 0 && (w & 15) == 0) { tw = 16; th = 8; return RD_16x8; }
+  if (w < h && (w & 7) == 0 && (h & 15) == 0) { tw = 8; th = 16; return RD_8x16; }
+  if (w > h && (h & 3) == 0 && (w & 7) == 0) { tw = 8; th = 4; return RD_8x4; }
+  if (w < h && (w & 3) == 0 && (h & 7) == 0) { tw = 4; th = 8; return RD_4x8; }
+  if (h % 8 == 0 && w % 8 == 0) { tw = 8; th = 8; return RD_8x8; }
+  if (h % 4 == 0 && w % 4 == 0) { tw = 4; th = 4; return RD_4x4; }
+  if (h % 2 == 0 && w % 2 == 0) { tw = 2; th = 2; return RD_2x2; }
+  return -1;
+}
+
 // Execution lanes: pictures are launched on NLANE HIP streams, each with its own scratch planes
 // (prediction, residual, loop-filter ping-pong). A picture waits only for the pictures it depends on —
 // the last writer of each reference slot (RAW), and the last writer and every reader since of its own
@@ -164,6 +188,7 @@ struct vvcr_ctx {
   std::vector<std::unique_ptr<Prepared>> prepared;
   Prepared *last = nullptr;          // last launched (stage times, DMVR deltas)
   int n_cu = 256;                    // compute units (persistent intra launch width)
+  std::vector<std::unique_ptr<struct RdoPlan>> rdo;   // encoder RDO plans (vvcr_rd_plan / vvcr_fwd_plan)
   int32_t *d_err = nullptr;          // device error flag of the persistent intra kernel (checked by vvcr_sync)
 };
 
@@ -817,4 +842,163 @@ int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n) {
   API_END
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Encoder RDO inner loop (include/vvcr.h): plans, runs on device pointers, host-pointer conveniences
+// ---------------------------------------------------------------------------------------------------
+static RdoPlan &get_rdo(vvcr_ctx *ctx, int32_t h) {
+  if (h < 0 || h >= (int)ctx->rdo.size() || !ctx->rdo[h]) throw VvcrError(VVCR_E_ARG, "bad RDO plan handle");
+  return *ctx->rdo[h];
+}
+static int32_t new_rdo(vvcr_ctx *ctx) {
+  for (size_t i = 0; i < ctx->rdo.size(); i++)
+    if (!ctx->rdo[i]) { ctx->rdo[i].reset(new RdoPlan()); return (int32_t)i; }
+  ctx->rdo.emplace_back(new RdoPlan());
+  return (int32_t)ctx->rdo.size() - 1;
+}
+
+int vvcr_rd_plan(vvcr_ctx *ctx, const vvcr_rd_block *blocks, int32_t n, int32_t *plan) {
+  if (!ctx || !plan || n < 0 || (n && !blocks)) return VVCR_E_ARG;
+  API_BEGIN
+  std::vector<RdBlockDev> bd(n);
+  std::vector<RdTile> tl[RD_KINDS];
+  for (int i = 0; i < n; i++) {
+    const vvcr_rd_block &b = blocks[i];
+    int tw, th;
+    const int k = rd_kind(b.width, b.height, tw, th);
+    if (k < 0 || b.width <= 0 || b.height <= 0 || b.width > 128 || b.height > 128)
+      throw VvcrError(VVCR_E_ARG, "RDO block size not supported by xGetHADs (even sizes up to 128)");
+    bd[i] = RdBlockDev{b.org_off, b.cur_off, b.org_stride, b.cur_stride};
+    for (int y = 0; y < b.height; y += th)
+      for (int x = 0; x < b.width; x += tw) tl[k].push_back(RdTile{i, (int16_t)x, (int16_t)y});
+  }
+  const int32_t h = new_rdo(ctx);
+  RdoPlan &P = *ctx->rdo[h];
+  P.nblocks = n;
+  P.blocks.upload(bd);
+  for (int k = 0; k < RD_KINDS; k++) { P.tiles[k].upload(tl[k]); P.ntiles[k] = (int)tl[k].size(); }
+  *plan = h;
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_rd_run(vvcr_ctx *ctx, int32_t plan, const int16_t *org_dev, const int16_t *cur_dev, uint32_t *sad_dev,
+                uint32_t *satd_dev) {
+  if (!ctx || !org_dev || !cur_dev || !sad_dev || !satd_dev) return VVCR_E_ARG;
+  API_BEGIN
+  RdoPlan &P = get_rdo(ctx, plan);
+  if (P.fwd) throw VvcrError(VVCR_E_ARG, "plan is a forward-transform plan");
+  hipStream_t s = ctx->stream;
+  VVCR_CHECK_HIP(hipMemsetAsync(sad_dev, 0, (size_t)P.nblocks * 4, s));
+  VVCR_CHECK_HIP(hipMemsetAsync(satd_dev, 0, (size_t)P.nblocks * 4, s));
+  for (int k = 0; k < RD_KINDS; k++)
+    launch_rd_tiles(k, org_dev, cur_dev, P.tiles[k].p, P.ntiles[k], P.blocks.p, sad_dev, satd_dev, s);
+  VVCR_CHECK_HIP(hipGetLastError());
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_fwd_plan(vvcr_ctx *ctx, const vvcr_fwd_block *blocks, int32_t n, int32_t bit_depth, int32_t *plan) {
+  if (!ctx || !plan || n < 0 || (n && !blocks)) return VVCR_E_ARG;
+  API_BEGIN
+  if (bit_depth < 8 || bit_depth > 10) throw VvcrError(VVCR_E_UNSUPPORTED, "bit depth 8..10");
+  std::vector<FwdBlockDev> fb(n);
+  int64_t total = 0;
+  for (int i = 0; i < n; i++) {
+    const vvcr_fwd_block &b = blocks[i];
+    const bool pow2 = b.width >= 4 && b.height >= 4 && !(b.width & (b.width - 1)) && !(b.height & (b.height - 1));
+    const int maxH = b.tr_hor == 0 ? 64 : 32, maxV = b.tr_ver == 0 ? 64 : 32;
+    if (!pow2 || b.width > maxH || b.height > maxV || b.tr_hor < 0 || b.tr_hor > 2 || b.tr_ver < 0 || b.tr_ver > 2)
+      throw VvcrError(VVCR_E_ARG, "forward transform block: power-of-two 4..64 (DCT2) / 4..32 (DST7, DCT8)");
+    fb[i] = FwdBlockDev{b.src_off, b.dst_off, b.src_stride, (uint8_t)b.width, (uint8_t)b.height, (uint8_t)b.tr_hor,
+                        (uint8_t)b.tr_ver, b.lfnst ? 1 : 0};
+    total = std::max<int64_t>(total, b.dst_off + (int64_t)b.width * b.height);
+  }
+  const int32_t h = new_rdo(ctx);
+  RdoPlan &P = *ctx->rdo[h];
+  P.fwd = true;
+  P.nblocks = n;
+  P.bd = bit_depth;
+  P.coef_total = total;
+  P.fblocks.upload(fb);
+  *plan = h;
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_fwd_run(vvcr_ctx *ctx, int32_t plan, const int16_t *resi_dev, int32_t *coef_dev) {
+  if (!ctx || !resi_dev || !coef_dev) return VVCR_E_ARG;
+  API_BEGIN
+  RdoPlan &P = get_rdo(ctx, plan);
+  if (!P.fwd) throw VvcrError(VVCR_E_ARG, "plan is a distortion plan");
+  launch_fwd_tr(resi_dev, coef_dev, P.fblocks.p, P.nblocks, P.bd, ctx->stream);
+  VVCR_CHECK_HIP(hipGetLastError());
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_rdo_release(vvcr_ctx *ctx, int32_t plan) {
+  if (!ctx) return VVCR_E_ARG;
+  API_BEGIN
+  get_rdo(ctx, plan);
+  VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->rdo[plan].reset();
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_rd_dist(vvcr_ctx *ctx, const vvcr_rd_block *blocks, int32_t n, const int16_t *org, int64_t norg,
+                 const int16_t *cur, int64_t ncur, uint32_t *sad, uint32_t *satd) {
+  if (!ctx || !org || !cur || !sad || !satd || norg <= 0 || ncur <= 0) return VVCR_E_ARG;
+  int32_t plan = -1;
+  int r = vvcr_rd_plan(ctx, blocks, n, &plan);
+  if (r) return r;
+  API_BEGIN
+  for (int i = 0; i < n; i++) {   // every block must lie inside its pool
+    const vvcr_rd_block &b = blocks[i];
+    const int64_t eo = b.org_off + (int64_t)(b.height - 1) * b.org_stride + b.width, ec = b.cur_off + (int64_t)(b.height - 1) * b.cur_stride + b.width;
+    if (b.org_off < 0 || b.cur_off < 0 || eo > norg || ec > ncur) throw VvcrError(VVCR_E_ARG, "RDO block outside its sample pool");
+  }
+  DevVec<int16_t> o, c;
+  DevVec<uint32_t> ds, dh;
+  o.upload(org, norg);
+  c.upload(cur, ncur);
+  ds.ensure(n + 1);
+  dh.ensure(n + 1);
+  const int rr = vvcr_rd_run(ctx, plan, o.p, c.p, ds.p, dh.p);
+  if (rr) { vvcr_rdo_release(ctx, plan); return rr; }
+  VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  VVCR_CHECK_HIP(hipMemcpy(sad, ds.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  VVCR_CHECK_HIP(hipMemcpy(satd, dh.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+  vvcr_rdo_release(ctx, plan);
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_fwd_transform(vvcr_ctx *ctx, const vvcr_fwd_block *blocks, int32_t n, int32_t bit_depth, const int16_t *resi,
+                       int64_t nresi, int32_t *coef, int64_t ncoef) {
+  if (!ctx || !resi || !coef || nresi <= 0 || ncoef <= 0) return VVCR_E_ARG;
+  int32_t plan = -1;
+  int r = vvcr_fwd_plan(ctx, blocks, n, bit_depth, &plan);
+  if (r) return r;
+  API_BEGIN
+  for (int i = 0; i < n; i++) {
+    const vvcr_fwd_block &b = blocks[i];
+    const int64_t er = b.src_off + (int64_t)(b.height - 1) * b.src_stride + b.width;
+    if (b.src_off < 0 || b.dst_off < 0 || er > nresi || b.dst_off + (int64_t)b.width * b.height > ncoef)
+      throw VvcrError(VVCR_E_ARG, "transform block outside its buffer");
+  }
+  DevVec<int16_t> rd;
+  DevVec<int32_t> cd;
+  rd.upload(resi, nresi);
+  cd.ensure(ncoef + 1);
+  const int rr = vvcr_fwd_run(ctx, plan, rd.p, cd.p);
+  if (rr) { vvcr_rdo_release(ctx, plan); return rr; }
+  VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+  VVCR_CHECK_HIP(hipMemcpy(coef, cd.p, (size_t)ncoef * 4, hipMemcpyDeviceToHost));
+  vvcr_rdo_release(ctx, plan);
+  return VVCR_OK;
+  API_END
+}
+
 }  // extern "C"
+

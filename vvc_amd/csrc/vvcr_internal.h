@@ -172,6 +172,28 @@ struct Planes3 {
   int32_t copy;                // 0: clear dst, 1: dst <- src (same sizes)
 };
 
+// ------------------------------------------------------------------------------------------------
+// Encoder RDO inner loop (vvcr_rdo.hip): Hadamard tile kinds of RdCost::xGetHADs (RdCost.cpp:2818-2911)
+// ------------------------------------------------------------------------------------------------
+enum { RD_16x8 = 0, RD_8x16, RD_8x4, RD_4x8, RD_8x8, RD_4x4, RD_2x2, RD_KINDS };
+struct RdBlockDev {
+  int64_t org_off, cur_off;    // sample offsets into the original / prediction pools
+  int32_t org_stride, cur_stride;
+};
+struct RdTile {
+  int32_t block;
+  int16_t x, y;                // tile origin inside the block
+};
+struct FwdBlockDev {
+  int64_t src_off, dst_off;    // residual sample offset, coefficient offset (w*h int32, row-major)
+  int32_t src_stride;
+  uint8_t w, h, tr_hor, tr_ver; // tr: 0 DCT2, 1 DST7, 2 DCT8
+  int32_t lfnst;
+};
+void launch_rd_tiles(int kind, const int16_t *org, const int16_t *cur, const RdTile *tiles, int n, const RdBlockDev *blocks,
+                     uint32_t *sad, uint32_t *satd, hipStream_t s);
+void launch_fwd_tr(const int16_t *resi, int32_t *coef, const FwdBlockDev *blocks, int n, int bd, hipStream_t s);
+
 // launchers (vvcr_mc.hip, vvcr_mc_ext.hip, vvcr_resid.hip, vvcr_lf.hip)
 void launch_mc_bidir(const McParams &p, const McJob *jobs, int njobs, int32_t *dmvr_out, hipStream_t s);
 void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const AffPu *pus, hipStream_t s);

@@ -85,6 +85,13 @@ def lib():
         L.vvcr_kernel_stats.argtypes = [P, I32, C.POINTER(KernelStat), I32]
         L.vvcr_stream.argtypes = [P]
         L.vvcr_stream.restype = P
+        L.vvcr_rd_plan.argtypes = [P, P, I32, C.POINTER(I32)]
+        L.vvcr_rd_run.argtypes = [P, I32, P, P, P, P]
+        L.vvcr_fwd_plan.argtypes = [P, P, I32, I32, C.POINTER(I32)]
+        L.vvcr_fwd_run.argtypes = [P, I32, P, P]
+        L.vvcr_rdo_release.argtypes = [P, I32]
+        L.vvcr_rd_dist.argtypes = [P, P, I32, P, C.c_int64, P, C.c_int64, P, P]
+        L.vvcr_fwd_transform.argtypes = [P, P, I32, I32, P, C.c_int64, P, C.c_int64]
         _lib = L
     return _lib
 
@@ -96,7 +103,14 @@ class KernelStat(C.Structure):
 EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_release_picture", "vvcr_kernel_stats", "vvcr_create", "vvcr_destroy", "vvcr_last_error", "vvcr_begin_picture", "vvcr_submit",
            "vvcr_set_loop_filter_params", "vvcr_end_picture", "vvcr_end_picture_stages", "vvcr_sync",
            "vvcr_read_plane", "vvcr_write_plane", "vvcr_read_picture", "vvcr_get_dmvr_deltas",
-           "vvcr_last_stage_times", "vvcr_stream"]
+           "vvcr_last_stage_times", "vvcr_stream", "vvcr_rd_plan", "vvcr_rd_run", "vvcr_fwd_plan", "vvcr_fwd_run",
+           "vvcr_rdo_release", "vvcr_rd_dist", "vvcr_fwd_transform"]
+
+# encoder RDO block descriptors (include/vvcr.h vvcr_rd_block / vvcr_fwd_block) as numpy record types
+RD_BLOCK = [("org_off", "<i8"), ("cur_off", "<i8"), ("org_stride", "<i4"), ("cur_stride", "<i4"), ("width", "<i4"),
+            ("height", "<i4")]
+FWD_BLOCK = [("src_off", "<i8"), ("dst_off", "<i8"), ("src_stride", "<i4"), ("width", "<i4"), ("height", "<i4"),
+             ("tr_hor", "<i4"), ("tr_ver", "<i4"), ("lfnst", "<i4")]
 
 
 def _ptr(a):
@@ -174,6 +188,48 @@ class Context:
 
     def release(self, handle):
         self._chk(self.L.vvcr_release_picture(self.h, handle), "vvcr_release_picture")
+
+    # ---- encoder RDO inner loop (vvcr_rd_* / vvcr_fwd_*)
+    def rd_dist(self, blocks, org, cur):
+        """SAD and Hadamard SATD per block (RdCost xGetSAD / xGetHADs); host arrays in and out."""
+        blocks = np.ascontiguousarray(blocks)
+        org, cur = np.ascontiguousarray(org, np.int16), np.ascontiguousarray(cur, np.int16)
+        n = len(blocks)
+        sad, satd = np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+        self._chk(self.L.vvcr_rd_dist(self.h, blocks.ctypes.data, n, org.ctypes.data, org.size, cur.ctypes.data, cur.size,
+                                      sad.ctypes.data, satd.ctypes.data), "vvcr_rd_dist")
+        return sad, satd
+
+    def fwd_transform(self, blocks, resi, ncoef, bit_depth=10):
+        """Forward transforms (TrQuant::xT) of the blocks; returns the int32 coefficient pool."""
+        blocks = np.ascontiguousarray(blocks)
+        resi = np.ascontiguousarray(resi, np.int16)
+        coef = np.zeros(ncoef, np.int32)
+        self._chk(self.L.vvcr_fwd_transform(self.h, blocks.ctypes.data, len(blocks), bit_depth, resi.ctypes.data, resi.size,
+                                            coef.ctypes.data, coef.size), "vvcr_fwd_transform")
+        return coef
+
+    def rd_plan(self, blocks):
+        blocks = np.ascontiguousarray(blocks)
+        h = C.c_int32(0)
+        self._chk(self.L.vvcr_rd_plan(self.h, blocks.ctypes.data, len(blocks), C.byref(h)), "vvcr_rd_plan")
+        return h.value
+
+    def rd_run(self, plan, org_ptr, cur_ptr, sad_ptr, satd_ptr):
+        """device pointers (e.g. torch tensor data_ptr()); asynchronous on the context stream"""
+        self._chk(self.L.vvcr_rd_run(self.h, plan, org_ptr, cur_ptr, sad_ptr, satd_ptr), "vvcr_rd_run")
+
+    def fwd_plan(self, blocks, bit_depth=10):
+        blocks = np.ascontiguousarray(blocks)
+        h = C.c_int32(0)
+        self._chk(self.L.vvcr_fwd_plan(self.h, blocks.ctypes.data, len(blocks), bit_depth, C.byref(h)), "vvcr_fwd_plan")
+        return h.value
+
+    def fwd_run(self, plan, resi_ptr, coef_ptr):
+        self._chk(self.L.vvcr_fwd_run(self.h, plan, resi_ptr, coef_ptr), "vvcr_fwd_run")
+
+    def rdo_release(self, plan):
+        self._chk(self.L.vvcr_rdo_release(self.h, plan), "vvcr_rdo_release")
 
     def kernel_stats(self, handle=0):
         """[(name, launches, ms, alg_bytes)] of the last launch of a prepared picture (0 = last launched)."""
