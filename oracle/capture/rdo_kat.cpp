@@ -8,11 +8,15 @@
 //   * forward transform: the fastFwdTrans[trType][size] partial butterflies (TrQuant.cpp:69-74,
 //     TrQuant_EMT.cpp) driven with the shifts and zero-out of TrQuant::xT (TrQuant.cpp:749-824).
 // Usage: rdo_kat <seed> <dist.bin> <tr.bin>
+//        rdo_kat --bench <width> <height> <seconds>   (CPU baseline of bench_rdo.py: the same block set —
+//        every rectangle w x h, w, h in {8..128}, on its own size grid inside each 128x128 CTU, clipped to
+//        the picture — SAD + SATD + DCT2 forward transform (w, h <= 64) per block, one thread)
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
 #include <vector>
 #include <random>
+#include <string>
 #include "RdCost.h"
 #include "TrQuant_EMT.h"
 #include "Rom.h"
@@ -21,7 +25,59 @@ extern FwdTrans *fastFwdTrans[NUM_TRANS_TYPE][g_numTransformMatrixSizes];   // T
 
 static const int kSizes[6] = {4, 8, 16, 32, 64, 128};
 
+#include <chrono>
+static int bench(int W, int H, double seconds) {
+  RdCost rc;
+  std::mt19937 rng(5);
+  std::vector<int16_t> org((size_t)W * H), cur((size_t)W * H);
+  for (size_t i = 0; i < org.size(); i++) {
+    org[i] = (int16_t)(rng() % 1024);
+    cur[i] = (int16_t)std::min(1023, std::max(0, org[i] + (int)(rng() % 81) - 40));
+  }
+  struct B { int x, y, w, h; };
+  std::vector<B> bl;
+  for (int cy = 0; cy < H; cy += 128)
+    for (int cx = 0; cx < W; cx += 128)
+      for (int w = 8; w <= 128; w <<= 1)
+        for (int h = 8; h <= 128; h <<= 1)
+          for (int y = cy; y < cy + 128; y += h)
+            for (int x = cx; x < cx + 128; x += w)
+              if (x + w <= W && y + h <= H) bl.push_back({x, y, w, h});
+  const int maxLog2 = 15, mshift = g_transformMatrixShift[TRANSFORM_FORWARD], bd = 10;
+  std::vector<TCoeff> blk(128 * 128), tmp(128 * 128), coef(128 * 128);
+  double samples = 0;
+  uint64_t acc = 0;
+  int passes = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  double el = 0;
+  do {
+    for (const B &b : bl) {
+      const CPelBuf ob(&org[(size_t)b.y * W + b.x], W, b.w, b.h), cb(&cur[(size_t)b.y * W + b.x], W, b.w, b.h);
+      DistParam dp;
+      rc.setDistParam(dp, ob, cb, bd, COMPONENT_Y, false);
+      acc += dp.distFunc(dp);
+      rc.setDistParam(dp, ob, cb, bd, COMPONENT_Y, true);
+      acc += dp.distFunc(dp);
+      if (b.w <= 64 && b.h <= 64) {
+        for (int y = 0; y < b.h; y++)
+          for (int x = 0; x < b.w; x++) blk[y * b.w + x] = org[(size_t)(b.y + y) * W + b.x + x] - cur[(size_t)(b.y + y) * W + b.x + x];
+        const int skipW = b.w > 32 ? b.w - 32 : 0, skipH = b.h > 32 ? b.h - 32 : 0;
+        fastFwdTrans[DCT2][floorLog2(b.w) - 1](blk.data(), tmp.data(), (floorLog2(b.w) + bd + mshift) - maxLog2, b.h, 0, skipW);
+        fastFwdTrans[DCT2][floorLog2(b.h) - 1](tmp.data(), coef.data(), floorLog2(b.h) + mshift, b.w, skipW, skipH);
+        acc += coef[0];
+      }
+      samples += (double)b.w * b.h;
+    }
+    passes++;
+    el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  } while (el < seconds);
+  printf("{\"blocks\": %zu, \"passes\": %d, \"seconds\": %.3f, \"msamples_per_s\": %.3f, \"check\": %llu}\n", bl.size(), passes, el,
+         samples / el / 1e6, (unsigned long long)acc);
+  return 0;
+}
+
 int main(int argc, char **argv) {
+  if (argc >= 5 && std::string(argv[1]) == "--bench") return bench(atoi(argv[2]), atoi(argv[3]), atof(argv[4]));
   if (argc < 4) { fprintf(stderr, "usage: rdo_kat seed dist.bin tr.bin\n"); return 2; }
   std::mt19937 rng((unsigned)atoi(argv[1]));
   RdCost rc;   // RdCost::init() fills m_afpDistortFunc (with the x86 SIMD variants when enabled)

@@ -127,7 +127,9 @@ struct RdoPlan {
   DevVec<RdBlockDev> blocks;
   DevVec<RdTile> tiles[RD_KINDS];
   int ntiles[RD_KINDS] = {};
-  DevVec<FwdBlockDev> fblocks;
+  DevVec<FwdBlockDev> fblocks;      // sorted by class (w, h, tr_hor, tr_ver, lfnst)
+  struct Cls { int start, n, w, h, trh, trv, lfnst; };
+  std::vector<Cls> classes;
   int64_t coef_total = 0;
 };
 
@@ -913,12 +915,21 @@ int vvcr_fwd_plan(vvcr_ctx *ctx, const vvcr_fwd_block *blocks, int32_t n, int32_
                         (uint8_t)b.tr_ver, b.lfnst ? 1 : 0};
     total = std::max<int64_t>(total, b.dst_off + (int64_t)b.width * b.height);
   }
+  // group by class: one launch per class (vvcr_rdo.hip launch_fwd_tr)
+  auto key = [](const FwdBlockDev &b) { return (b.w << 24) | (b.h << 16) | (b.tr_hor << 8) | (b.tr_ver << 4) | b.lfnst; };
+  std::stable_sort(fb.begin(), fb.end(), [&](const FwdBlockDev &a, const FwdBlockDev &b) { return key(a) < key(b); });
   const int32_t h = new_rdo(ctx);
   RdoPlan &P = *ctx->rdo[h];
   P.fwd = true;
   P.nblocks = n;
   P.bd = bit_depth;
   P.coef_total = total;
+  for (int i = 0; i < n;) {
+    int j = i;
+    while (j < n && key(fb[j]) == key(fb[i])) j++;
+    P.classes.push_back({i, j - i, fb[i].w, fb[i].h, fb[i].tr_hor, fb[i].tr_ver, fb[i].lfnst});
+    i = j;
+  }
   P.fblocks.upload(fb);
   *plan = h;
   return VVCR_OK;
@@ -930,7 +941,8 @@ int vvcr_fwd_run(vvcr_ctx *ctx, int32_t plan, const int16_t *resi_dev, int32_t *
   API_BEGIN
   RdoPlan &P = get_rdo(ctx, plan);
   if (!P.fwd) throw VvcrError(VVCR_E_ARG, "plan is a distortion plan");
-  launch_fwd_tr(resi_dev, coef_dev, P.fblocks.p, P.nblocks, P.bd, ctx->stream);
+  for (const RdoPlan::Cls &c : P.classes)
+    launch_fwd_tr(resi_dev, coef_dev, P.fblocks.p + c.start, c.n, P.bd, c.w, c.h, c.trh, c.trv, c.lfnst, ctx->stream);
   VVCR_CHECK_HIP(hipGetLastError());
   return VVCR_OK;
   API_END

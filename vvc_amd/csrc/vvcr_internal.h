@@ -192,7 +192,8 @@ struct FwdBlockDev {
 };
 void launch_rd_tiles(int kind, const int16_t *org, const int16_t *cur, const RdTile *tiles, int n, const RdBlockDev *blocks,
                      uint32_t *sad, uint32_t *satd, hipStream_t s);
-void launch_fwd_tr(const int16_t *resi, int32_t *coef, const FwdBlockDev *blocks, int n, int bd, hipStream_t s);
+void launch_fwd_tr(const int16_t *resi, int32_t *coef, const FwdBlockDev *blocks, int n, int bd, int w, int h, int trh,
+                   int trv, int lfnst, hipStream_t s);
 
 // launchers (vvcr_mc.hip, vvcr_mc_ext.hip, vvcr_resid.hip, vvcr_lf.hip)
 void launch_mc_bidir(const McParams &p, const McJob *jobs, int njobs, int32_t *dmvr_out, hipStream_t s);

@@ -11,8 +11,8 @@
 // SATD and SAD to its block with one integer atomic each (order-independent, so deterministic).
 // Tiles are sorted by kind on the host and each kind is one launch of its template instantiation.
 //
-// Forward transform (TrQuant::xT TrQuant.cpp:749-824): one 256-lane workgroup per block, the residual
-// and the first-pass output staged in LDS; each 1-D pass is the integer matrix product the partial
+// Forward transform (TrQuant::xT TrQuant.cpp:749-824): blocks grouped by size and transform types on
+// the host, one launch per group, the matrices, residuals and first-pass outputs staged in LDS; each 1-D pass is the integer matrix product the partial
 // butterflies compute (fastForwardDCT2_B* / DST7 / DCT8, TrQuant_EMT.cpp), with xT's shifts and
 // zero-out; DCT2 up to 32 points ignores the output cut-off exactly as the reference does (:131-607).
 #include "vvcr_internal.h"
@@ -102,47 +102,63 @@ __device__ __forceinline__ int tr_coef(int type, int N, int k, int n) {
   }
 }
 
-// one forward 1-D pass of fastFwdTrans: dst[k * line + j] = (sum_n M[k][n] src[j * N + n] + rnd) >> shift
-__device__ void fwd_pass(const int32_t *src, int32_t *dst, int N, int line, int skipLine, int cutoff, int shift, int type,
-                         int16_t *mat, int tid) {
-  for (int i = tid; i < N * N; i += 256) mat[i] = (int16_t)tr_coef(type, N, i / N, i % N);
-  __syncthreads();
-  const int rnd = 1 << (shift - 1), reduced = line - skipLine;
-  for (int i = tid; i < N * line; i += 256) {
-    const int k = i / line, j = i - k * line;
-    int32_t v = 0;
-    if (k < cutoff && j < reduced) {
-      int64_t s = 0;
-      const int32_t *x = src + j * N;
-      const int16_t *m = mat + k * N;
-      for (int n = 0; n < N; n++) s += (int64_t)m[n] * x[n];
-      v = (int32_t)((s + rnd) >> shift);
+// Forward transform of one size class: a workgroup stages the class's two matrices in LDS once and then
+// transforms NB blocks at a time (NB * W * H >= 256 samples per pass keeps the 256 lanes busy). The
+// products (residual <= 11 bits or first-pass outputs <= 17 bits, times matrix entries <= 8 bits) and
+// sums fit the 32-bit integer path the reference's TCoeff butterflies use, so v_mad_i32_i24 + int32
+// accumulation reproduces them exactly.
+template <int W, int H>
+__global__ __launch_bounds__(256) void k_fwd_sz(const int16_t *__restrict__ resi, int32_t *__restrict__ coef,
+                                                const FwdBlockDev *__restrict__ blocks, int n, int bd, int trh, int trv,
+                                                int skipW, int cut1, int cut2) {
+  constexpr int NB = (W * H >= 256) ? 1 : 256 / (W * H);
+  __shared__ int16_t mh[W * W], mv[H * H];
+  __shared__ int32_t x[NB * W * H], t[NB * W * H];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < W * W; i += 256) mh[i] = (int16_t)tr_coef(trh, W, i / W, i % W);
+  for (int i = tid; i < H * H; i += 256) mv[i] = (int16_t)tr_coef(trv, H, i / H, i % H);
+  constexpr int lw = W == 4 ? 2 : W == 8 ? 3 : W == 16 ? 4 : W == 32 ? 5 : 6;
+  constexpr int lh = H == 4 ? 2 : H == 8 ? 3 : H == 16 ? 4 : H == 32 ? 5 : 6;
+  const int s1 = lw + bd + 6 - 15, s2 = lh + 6;
+  const int r1 = 1 << (s1 - 1), r2 = 1 << (s2 - 1);
+  for (int b0 = blockIdx.x * NB; b0 < n; b0 += gridDim.x * NB) {
+    __syncthreads();   // matrices staged / previous blocks' LDS consumed
+    for (int i = tid; i < NB * W * H; i += 256) {
+      const int b = i / (W * H), e = i % (W * H);
+      x[i] = b0 + b < n ? (int)resi[blocks[b0 + b].src_off + (int64_t)(e / W) * blocks[b0 + b].src_stride + (e % W)] : 0;
     }
-    dst[i] = v;
+    __syncthreads();
+    // pass 1 (rows, fastFwdTrans[trh][W]): t[b][k * H + j] = (sum_m mh[k][m] x[b][j][m] + r1) >> s1
+    for (int i = tid; i < NB * W * H; i += 256) {
+      const int b = i / (W * H), e = i % (W * H), k = e / H, j = e % H;
+      int v = 0;
+      if (k < cut1) {
+        const int32_t *xr = x + b * W * H + j * W;
+        const int16_t *m = mh + k * W;
+        int s = 0;
+#pragma unroll
+        for (int q = 0; q < W; q++) s += m[q] * xr[q];
+        v = (s + r1) >> s1;
+      }
+      t[i] = v;
+    }
+    __syncthreads();
+    // pass 2 (columns, fastFwdTrans[trv][H], line = W, skipLine = skipW): out[b][kv * W + i2]
+    for (int i = tid; i < NB * W * H; i += 256) {
+      const int b = i / (W * H), e = i % (W * H), kv = e / W, i2 = e % W;
+      if (b0 + b >= n) continue;
+      int v = 0;
+      if (kv < cut2 && i2 < W - skipW) {
+        const int32_t *tr = t + b * W * H + i2 * H;
+        const int16_t *m = mv + kv * H;
+        int s = 0;
+#pragma unroll
+        for (int q = 0; q < H; q++) s += m[q] * tr[q];
+        v = (s + r2) >> s2;
+      }
+      coef[blocks[b0 + b].dst_off + e] = v;
+    }
   }
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(256) void k_fwd_tr(const int16_t *__restrict__ resi, int32_t *__restrict__ coef,
-                                                const FwdBlockDev *__restrict__ blocks, int bd) {
-  __shared__ int32_t a[64 * 64], b[64 * 64];
-  __shared__ int16_t mat[64 * 64];
-  const FwdBlockDev B = blocks[blockIdx.x];
-  const int w = B.w, h = B.h, tid = threadIdx.x;
-  const int th = B.tr_hor, tv = B.tr_ver;
-  int skipW = (th != 0 && w == 32) ? 16 : (w > 32 ? w - 32 : 0);
-  int skipH = (tv != 0 && h == 32) ? 16 : (h > 32 ? h - 32 : 0);
-  if (B.lfnst) {   // xT's LFNST zero-out (TrQuant.cpp:766-777)
-    if ((w == 4 && h > 4) || (w > 4 && h == 4)) { skipW = w - 4; skipH = h - 4; }
-    else if (w >= 8 && h >= 8) { skipW = w - 8; skipH = h - 8; }
-  }
-  for (int i = tid; i < w * h; i += 256) a[i] = resi[B.src_off + (int64_t)(i / w) * B.src_stride + (i % w)];
-  __syncthreads();
-  const int lw = 31 - __clz(w), lh = 31 - __clz(h);
-  const int s1 = lw + bd + 6 - 15, s2 = lh + 6;   // g_transformMatrixShift[FORWARD] = 6, maxLog2TrDynamicRange 15
-  fwd_pass(a, b, w, h, 0, (th == 0 && w <= 32) ? w : w - skipW, s1, th, mat, tid);
-  fwd_pass(b, a, h, w, skipW, (tv == 0 && h <= 32) ? h : h - skipH, s2, tv, mat, tid);
-  for (int i = tid; i < w * h; i += 256) coef[B.dst_off + i] = a[i];
 }
 
 }  // namespace
@@ -163,7 +179,42 @@ void launch_rd_tiles(int kind, const int16_t *org, const int16_t *cur, const RdT
   }
 }
 
-void launch_fwd_tr(const int16_t *resi, int32_t *coef, const FwdBlockDev *blocks, int n, int bd, hipStream_t s) {
+template <int W, int H>
+static void launch_sz(const int16_t *resi, int32_t *coef, const FwdBlockDev *blocks, int n, int bd, int trh, int trv, int skipW,
+                      int cut1, int cut2, hipStream_t s) {
+  constexpr int NB = (W * H >= 256) ? 1 : 256 / (W * H);
+  const int g = std::min((n + NB - 1) / NB, 4096);
+  hipLaunchKernelGGL((k_fwd_sz<W, H>), dim3(g), dim3(256), 0, s, resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2);
+}
+template <int W>
+static void launch_w(int h, const int16_t *resi, int32_t *coef, const FwdBlockDev *blocks, int n, int bd, int trh, int trv,
+                     int skipW, int cut1, int cut2, hipStream_t s) {
+  switch (h) {
+    case 4: launch_sz<W, 4>(resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+    case 8: launch_sz<W, 8>(resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+    case 16: launch_sz<W, 16>(resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+    case 32: launch_sz<W, 32>(resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+    default: launch_sz<W, 64>(resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+  }
+}
+
+// One launch per class of blocks sharing (w, h, trh, trv, lfnst), blocks[0, n) of the class; the
+// zero-out of TrQuant::xT (:762-777) and the per-type output cut-off are uniform per class.
+void launch_fwd_tr(const int16_t *resi, int32_t *coef, const FwdBlockDev *blocks, int n, int bd, int w, int h, int trh,
+                   int trv, int lfnst, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_fwd_tr, dim3(n), dim3(256), 0, s, resi, coef, blocks, bd);
+  int skipW = (trh != 0 && w == 32) ? 16 : (w > 32 ? w - 32 : 0);
+  int skipH = (trv != 0 && h == 32) ? 16 : (h > 32 ? h - 32 : 0);
+  if (lfnst) {
+    if ((w == 4 && h > 4) || (w > 4 && h == 4)) { skipW = w - 4; skipH = h - 4; }
+    else if (w >= 8 && h >= 8) { skipW = w - 8; skipH = h - 8; }
+  }
+  const int cut1 = (trh == 0 && w <= 32) ? w : w - skipW, cut2 = (trv == 0 && h <= 32) ? h : h - skipH;
+  switch (w) {
+    case 4: launch_w<4>(h, resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+    case 8: launch_w<8>(h, resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+    case 16: launch_w<16>(h, resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+    case 32: launch_w<32>(h, resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+    default: launch_w<64>(h, resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2, s); break;
+  }
 }
