@@ -17,6 +17,7 @@
 // zero-out; DCT2 up to 32 points ignores the output cut-off exactly as the reference does (:131-607).
 #include "vvcr_internal.h"
 #include "vvcr_gen_tables.h"
+#include <cstdlib>
 
 namespace {
 
@@ -161,7 +162,109 @@ __global__ __launch_bounds__(256) void k_fwd_sz(const int16_t *__restrict__ resi
   }
 }
 
+
+// MFMA form of a size class with W, H >= 16 (the forward transform is the one dense contraction of the
+// path). Both passes are 16x16x32 f16 MFMAs with f32 accumulation, and stay exact:
+//  * pass 1: residuals (|x| <= 1023) and matrix entries (|m| <= 90) are exact f16 integers; every
+//    partial sum is an integer below 64 * 90 * 1023 < 2^24, so f32 accumulation is exact in any order;
+//  * pass 2: first-pass outputs v (|v| < 2^16) are split v = 256 * hi + lo, lo in [0, 255], |hi| <= 256,
+//    both exact f16; each of the two MFMA sums stays below 64 * 90 * 256 < 2^24 and the int32
+//    recombination 256 * S_hi + S_lo is exact.
+// The first pass writes its output transposed (T1T[k][j]) so that the second pass reads its B fragments
+// as contiguous 16-byte rows, like the first. Fragment maps (mfma_f32_16x16x32_f16): lane l holds
+// A[l & 15][8 (l >> 4) + e] and B[8 (l >> 4) + e][l & 15], e = 0..7; C/D col = l & 15,
+// row = 4 (l >> 4) + r.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int W, int H>
+__global__ __launch_bounds__(256) void k_fwd_mfma(const int16_t *__restrict__ resi, int32_t *__restrict__ coef,
+                                                  const FwdBlockDev *__restrict__ blocks, int n, int bd, int trh, int trv,
+                                                  int skipW, int cut1, int cut2) {
+  constexpr int TPB = (W / 16) * (H / 16);             // 16x16 output tiles per block and pass
+  constexpr int NB = TPB >= 4 ? 1 : 4 / TPB;           // blocks per iteration: >= 4 tiles for the 4 waves
+  constexpr int PW = W + 8, PH = H + 8;                // f16 row pitches (16-byte aligned, spread banks)
+  __shared__ __attribute__((aligned(16))) _Float16 mh[W * PW], mv[H * PH];
+  __shared__ __attribute__((aligned(16))) _Float16 xs[NB * H * PW];
+  __shared__ __attribute__((aligned(16))) _Float16 thi[NB * W * PH], tlo[NB * W * PH];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < W * W; i += 256) mh[(i / W) * PW + i % W] = (_Float16)tr_coef(trh, W, i / W, i % W);
+  for (int i = tid; i < H * H; i += 256) mv[(i / H) * PH + i % H] = (_Float16)tr_coef(trv, H, i / H, i % H);
+  constexpr int lw = W == 16 ? 4 : W == 32 ? 5 : 6;
+  constexpr int lh = H == 16 ? 4 : H == 32 ? 5 : 6;
+  const int s1 = lw + bd + 6 - 15, s2 = lh + 6;
+  const int r1 = 1 << (s1 - 1), r2 = 1 << (s2 - 1);
+  const int fr = lane & 15, fk = 8 * (lane >> 4);      // fragment row / first k of this lane
+  for (int b0 = blockIdx.x * NB; b0 < n; b0 += gridDim.x * NB) {
+    __syncthreads();
+    for (int i = tid; i < NB * W * H; i += 256) {
+      const int b = i / (W * H), e = i % (W * H), y = e / W, x = e % W;
+      xs[(b * H + y) * PW + x] = (_Float16)(b0 + b < n ? (int)resi[blocks[b0 + b].src_off + (int64_t)y * blocks[b0 + b].src_stride + x] : 0);
+    }
+    __syncthreads();
+    // ---- pass 1: T1[j][k] = sum_n X[j][n] Mh[k][n]  (A = X rows, B = Mh rows as columns)
+    for (int t = wv; t < NB * TPB; t += 4) {
+      const int b = t / TPB, tt = t % TPB, tr = tt / (W / 16), tc = tt % (W / 16);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < W; kk += 32) {
+        f16x8 a, bb;
+        if (kk + fk < W) {
+          a = *(const f16x8 *)&xs[(b * H + 16 * tr + fr) * PW + kk + fk];
+          bb = *(const f16x8 *)&mh[(16 * tc + fr) * PW + kk + fk];
+        } else {
+          a = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+          bb = a;
+        }
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bb, acc, 0, 0, 0);
+      }
+      const int k = 16 * tc + fr;                       // output column (frequency) of this lane
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int j = 16 * tr + 4 * (lane >> 4) + r;    // output row
+        const int v = k < cut1 ? (((int)acc[r]) + r1) >> s1 : 0;
+        thi[(b * W + k) * PH + j] = (_Float16)(v >> 8);
+        tlo[(b * W + k) * PH + j] = (_Float16)(v & 255);
+      }
+    }
+    __syncthreads();
+    // ---- pass 2: out[kv][i2] = sum_q Mv[kv][q] T1[q][i2]  (A = Mv rows, B = T1T rows as columns)
+    for (int t = wv; t < NB * TPB; t += 4) {
+      const int b = t / TPB, tt = t % TPB, tr = tt / (W / 16), tc = tt % (W / 16);
+      f32x4 ah = {0.f, 0.f, 0.f, 0.f}, al = ah;
+#pragma unroll
+      for (int kk = 0; kk < H; kk += 32) {
+        f16x8 a, bh, bl;
+        if (kk + fk < H) {
+          a = *(const f16x8 *)&mv[(16 * tr + fr) * PH + kk + fk];
+          bh = *(const f16x8 *)&thi[(b * W + 16 * tc + fr) * PH + kk + fk];
+          bl = *(const f16x8 *)&tlo[(b * W + 16 * tc + fr) * PH + kk + fk];
+        } else {
+          a = (f16x8){0, 0, 0, 0, 0, 0, 0, 0};
+          bh = a;
+          bl = a;
+        }
+        ah = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bh, ah, 0, 0, 0);
+        al = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bl, al, 0, 0, 0);
+      }
+      if (b0 + b < n) {
+        const int i2 = 16 * tc + fr;
+        int32_t *dst = coef + blocks[b0 + b].dst_off;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int kv = 16 * tr + 4 * (lane >> 4) + r;
+          const int sum = (int)ah[r] * 256 + (int)al[r];
+          dst[kv * W + i2] = (kv < cut2 && i2 < W - skipW) ? (sum + r2) >> s2 : 0;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
+
+// VVCR_FWD_MFMA=0 selects the int32 VALU kernels for every class (A/B and fallback)
+static const bool g_fwd_mfma = [] { const char *e = getenv("VVCR_FWD_MFMA"); return !(e && e[0] == '0'); }();
 
 void launch_rd_tiles(int kind, const int16_t *org, const int16_t *cur, const RdTile *tiles, int n, const RdBlockDev *blocks,
                      uint32_t *sad, uint32_t *satd, hipStream_t s) {
@@ -182,6 +285,14 @@ void launch_rd_tiles(int kind, const int16_t *org, const int16_t *cur, const RdT
 template <int W, int H>
 static void launch_sz(const int16_t *resi, int32_t *coef, const FwdBlockDev *blocks, int n, int bd, int trh, int trv, int skipW,
                       int cut1, int cut2, hipStream_t s) {
+  if constexpr (W >= 16 && H >= 16) {
+    if (g_fwd_mfma) {
+      constexpr int TPB = (W / 16) * (H / 16), NB = TPB >= 4 ? 1 : 4 / TPB;
+      const int g = std::min((n + NB - 1) / NB, 4096);
+      hipLaunchKernelGGL((k_fwd_mfma<W, H>), dim3(g), dim3(256), 0, s, resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2);
+      return;
+    }
+  }
   constexpr int NB = (W * H >= 256) ? 1 : 256 / (W * H);
   const int g = std::min((n + NB - 1) / NB, 4096);
   hipLaunchKernelGGL((k_fwd_sz<W, H>), dim3(g), dim3(256), 0, s, resi, coef, blocks, n, bd, trh, trv, skipW, cut1, cut2);
