@@ -199,6 +199,9 @@ typedef struct vvcr_kernel_stat {
   double alg_bytes;
 } vvcr_kernel_stat;
 int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int32_t n);
+/* Per-kernel-group event timing of later launches on (default) or off; with it off, vvcr_kernel_stats
+ * reports ms = 0 (each event record is a marker packet in the execution lane's queue). */
+int vvcr_set_timing(vvcr_ctx *ctx, int32_t on);
 int vvcr_sync(vvcr_ctx *ctx);
 
 /* Buffers addressable by vvcr_read_plane / vvcr_write_plane (tests and output). */

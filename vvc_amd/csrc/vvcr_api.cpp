@@ -88,6 +88,7 @@ struct Prepared {
   hipEvent_t start = nullptr, done = nullptr;   // whole launch (events of this picture only: an event
                                                 // shared by pictures of several lanes would serialise them)
   bool ran[NK] = {};
+  bool timed[NK] = {};              // the group's events were recorded by the last launch
   bool launched = false;
   int lane = 0;                      // execution lane of the last launch (its stream and scratch planes)
   double alg_bytes[NK] = {};
@@ -106,15 +107,19 @@ struct Prepared {
   void wait() { if (launched) VVCR_CHECK_HIP(hipEventSynchronize(done)); }
 };
 
+// Per-kernel-group HIP events (vvcr_kernel_stats). Every event record is a marker packet in the lane's
+// queue, so the events are only recorded while timing is on (vvcr_set_timing; on by default).
 struct KernelTimer {
   Prepared &r;
   int k;
   hipStream_t s;
-  KernelTimer(Prepared &rr, int kk, hipStream_t ss) : r(rr), k(kk), s(ss) {
+  bool on;
+  KernelTimer(Prepared &rr, int kk, hipStream_t ss, bool timing) : r(rr), k(kk), s(ss), on(timing) {
     r.ran[k] = true;
-    VVCR_CHECK_HIP(hipEventRecord(r.ev[k][0], s));
+    r.timed[k] = on;
+    if (on) VVCR_CHECK_HIP(hipEventRecord(r.ev[k][0], s));
   }
-  ~KernelTimer() { (void)hipEventRecord(r.ev[k][1], s); }
+  ~KernelTimer() { if (on) (void)hipEventRecord(r.ev[k][1], s); }
 };
 
 }  // namespace
@@ -167,6 +172,7 @@ struct vvcr_ctx {
   std::vector<std::array<DPlane, 3>> dpb;
   Lane lanes[NLANE];
   uint64_t seq = 0;
+  bool timing = true;                // record per-kernel-group events (vvcr_set_timing)
   std::vector<hipEvent_t> slot_w;                 // per DPB slot: completion of its last writer
   std::vector<std::vector<hipEvent_t>> slot_r;    // per DPB slot: completions of its readers since
   std::vector<uint64_t> slot_seq;                 // per DPB slot: launch sequence number of its last writer
@@ -413,7 +419,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   for (hipEvent_t e : ctx->slot_r[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, e, 0));
   VVCR_CHECK_HIP(hipEventRecord(r.start, s));
   if (mask & VVCR_STAGE_RESID) {
-    KernelTimer t(r, K_RESID, s);
+    KernelTimer t(r, K_RESID, s, ctx->timing);
     Planes3 clr{};
     for (int c = 0; c < 3; c++) clr.dst[c] = ln.resi[c];
     launch_planes3(clr, s);
@@ -429,19 +435,19 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   if (mask & VVCR_STAGE_INTER) {
     const McParams mp = make_mc_params(ctx, r.pp, L);
     {
-      KernelTimer t(r, K_MC, s);
+      KernelTimer t(r, K_MC, s, ctx->timing);
       launch_mc_basic(mp, r.mc_basic.p, r.n_basic, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_MC] = r.n_basic ? 1 : 0;
     }
     {
-      KernelTimer t(r, K_MC_BIDIR, s);
+      KernelTimer t(r, K_MC_BIDIR, s, ctx->timing);
       launch_mc_bidir(mp, r.mc_bidir.p, r.n_bidir, r.dmvr.p, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_MC_BIDIR] = r.n_bidir ? 1 : 0;
     }
     {
-      KernelTimer t(r, K_MC_AFFINE, s);
+      KernelTimer t(r, K_MC_AFFINE, s, ctx->timing);
       launch_mc_affine(mp, r.aff_jobs.p, r.n_aff, r.aff_pu.p, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_MC_AFFINE] = r.n_aff ? 1 : 0;
@@ -450,13 +456,13 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   if (mask & VVCR_STAGE_INTRA) {
     const IntraParams P = make_intra_params(ctx, r, L);
     {
-      KernelTimer t(r, K_RECON, s);
+      KernelTimer t(r, K_RECON, s, ctx->timing);
       launch_recon_inter(P, r.tiles.p, r.n_tiles, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_RECON] = r.n_tiles ? 1 : 0;
     }
     {
-      KernelTimer t(r, K_INTRA, s);
+      KernelTimer t(r, K_INTRA, s, ctx->timing);
       launch_intra(r.iparams.p + L, r.ijobs.p, r.n_ijobs, r.ictu_list.p, r.ictu_start.p, r.n_ictu, r.idep_start.p, r.ideps.p,
                    r.istate.p, ctx->d_err, ctx->n_cu, s);
       VVCR_CHECK_HIP(hipGetLastError());
@@ -469,7 +475,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     VVCR_CHECK_HIP(hipGetLastError());
   }
   if ((mask & VVCR_STAGE_DBK) && (r.dbk_counts[0] + r.dbk_counts[1] + r.dbk_counts[2] + r.dbk_counts[3])) {
-    KernelTimer t(r, K_DBK, s);
+    KernelTimer t(r, K_DBK, s, ctx->timing);
     DbkParams dp{};
     for (int c = 0; c < 3; c++) dp.pl[c] = A[c];
     dp.bd = ctx->sp.bit_depth;
@@ -483,7 +489,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   const int wc = (ctx->sp.width + ctu - 1) / ctu, n = n_ctb(ctx->sp);
   bool inTmp = false;
   if (r.have_sao) {
-    KernelTimer t(r, K_SAO, s);
+    KernelTimer t(r, K_SAO, s, ctx->timing);
     SaoParams sp{};
     for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ln.tmp[c]; }
     sp.sao = r.sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
@@ -493,7 +499,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     r.launches[K_SAO] = 3;
   }
   if (r.have_alf) {
-    KernelTimer t(r, K_ALF, s);
+    KernelTimer t(r, K_ALF, s, ctx->timing);
     AlfParams ap{};
     for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ln.tmp[c] : A[c]; ap.dst[c] = inTmp ? A[c] : ln.tmp[c]; }
     ap.bd = ctx->sp.bit_depth; ap.ctu_log2 = ctx->sp.ctu_log2; ap.wc = wc; ap.nctb = n;
@@ -728,11 +734,17 @@ int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int3
     s.launches = r->ran[k] ? r->launches[k] : 0;
     s.alg_bytes = r->ran[k] ? r->alg_bytes[k] : 0.0;
     float ms = 0;
-    if (r->ran[k]) VVCR_CHECK_HIP(hipEventElapsedTime(&ms, r->ev[k][0], r->ev[k][1]));
+    if (r->ran[k] && r->timed[k]) VVCR_CHECK_HIP(hipEventElapsedTime(&ms, r->ev[k][0], r->ev[k][1]));
     s.ms = ms;
   }
   return NK;
   API_END
+}
+
+int vvcr_set_timing(vvcr_ctx *ctx, int32_t on) {
+  if (!ctx) return VVCR_E_ARG;
+  ctx->timing = on != 0;
+  return VVCR_OK;
 }
 
 int vvcr_sync(vvcr_ctx *ctx) {
@@ -762,7 +774,7 @@ int vvcr_last_stage_times(vvcr_ctx *ctx, float *ms, int32_t n) {
   if (ctx->last) {
     Prepared &r = *ctx->last;
     for (int k = 0; k < NK; k++) {
-      if (!r.ran[k]) continue;
+      if (!r.ran[k] || !r.timed[k]) continue;
       float v = 0;
       VVCR_CHECK_HIP(hipEventElapsedTime(&v, r.ev[k][0], r.ev[k][1]));
       const int st = kKernelStage[k] + 1;

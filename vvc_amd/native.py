@@ -85,6 +85,7 @@ def lib():
         L.vvcr_kernel_stats.argtypes = [P, I32, C.POINTER(KernelStat), I32]
         L.vvcr_stream.argtypes = [P]
         L.vvcr_stream.restype = P
+        L.vvcr_set_timing.argtypes = [P, I32]
         L.vvcr_rd_plan.argtypes = [P, P, I32, C.POINTER(I32)]
         L.vvcr_rd_run.argtypes = [P, I32, P, P, P, P]
         L.vvcr_fwd_plan.argtypes = [P, P, I32, I32, C.POINTER(I32)]
@@ -104,7 +105,7 @@ EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_release_picture"
            "vvcr_set_loop_filter_params", "vvcr_end_picture", "vvcr_end_picture_stages", "vvcr_sync",
            "vvcr_read_plane", "vvcr_write_plane", "vvcr_read_picture", "vvcr_get_dmvr_deltas",
            "vvcr_last_stage_times", "vvcr_stream", "vvcr_rd_plan", "vvcr_rd_run", "vvcr_fwd_plan", "vvcr_fwd_run",
-           "vvcr_rdo_release", "vvcr_rd_dist", "vvcr_fwd_transform"]
+           "vvcr_rdo_release", "vvcr_rd_dist", "vvcr_fwd_transform", "vvcr_set_timing"]
 
 # encoder RDO block descriptors (include/vvcr.h vvcr_rd_block / vvcr_fwd_block) as numpy record types
 RD_BLOCK = [("org_off", "<i8"), ("cur_off", "<i8"), ("org_stride", "<i4"), ("cur_stride", "<i4"), ("width", "<i4"),
@@ -188,6 +189,9 @@ class Context:
 
     def release(self, handle):
         self._chk(self.L.vvcr_release_picture(self.h, handle), "vvcr_release_picture")
+
+    def set_timing(self, on):
+        self._chk(self.L.vvcr_set_timing(self.h, 1 if on else 0), "vvcr_set_timing")
 
     # ---- encoder RDO inner loop (vvcr_rd_* / vvcr_fwd_*)
     def rd_dist(self, blocks, org, cur):
