@@ -4,16 +4,24 @@ compensation (DMVR/BDOF/affine-PROF/GEO/CIIP), intra waves, deblocking, SAO, ALF
 input (parsed descriptors, work lists, loop-filter parameters) resident in HBM when the timed region
 starts (vvcr_prepare_picture once, vvcr_launch_picture per step). One step = one decode of the whole
 sequence. The output of the first pass is checked bit-exact against the reference decoder's MD5s.
-Steps cycle through --segments (default 2) copies of the sequence on disjoint DPB slots, as consecutive
+Steps cycle through --segments (default 4) copies of the sequence on disjoint DPB slots, as consecutive
 intra-started segments of one long stream: the library runs each picture once its reference / slot
 dependencies are met, so a segment's intra picture may overlap the previous segment's B pictures.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--stream ra1080_q32] [--segments 2] [--no-cpu]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--stream ra1080_q32] [--segments 4] [--no-cpu]
 
 Multi-GPU (torch.distributed.run, one process per GPU): the path has no intra-picture work split in
 this round, so N ranks decode N independent replicas (weak scaling, no data-path collective); the
 timing barrier and max-over-ranks use torch.distributed.
 """
+import os
+
+# Execution lanes (libvvcr reads VVCR_LANES at vvcr_create): 3 intra lanes + 4 B lanes, each on its own
+# hardware queue, so that three intra-started segments and the B pictures of a fourth overlap; HIP's
+# default is 4 hardware queues per process, so the bench asks for 8 before the runtime starts.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+os.environ.setdefault("VVCR_LANES", "7")
+
 import argparse
 import hashlib
 import json
@@ -62,7 +70,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--stream", default="ra1080_q32")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--segments", type=int, default=2, help="copies of the sequence the steps cycle through")
+    ap.add_argument("--segments", type=int, default=4, help="copies of the sequence the steps cycle through (<= 6)")
     ap.add_argument("--sync-pictures", action="store_true",
                     help="host sync after every picture (profiling: kernel durations without overlap)")
     a = ap.parse_args()
@@ -82,7 +90,7 @@ def main():
     # then decodes its segment like the next intra-started segment of a longer stream would be decoded
     # (its intra picture references nothing, so it may start while step k's B pictures still run —
     # the library orders pictures only by their DPB-slot dependencies). --segments 1 serialises steps.
-    per = 12
+    per = min(12, 32 // a.segments)   # DPB slots per copy (32 in all)
     dec = D.Decoder(pics, dpb_slots=per * a.segments,
                     device=int(os.environ.get("VVCR_DEVICE", local)))   # VVCR_DEVICE: rehearsal of N ranks on one GPU
     ctx = dec.ctx

@@ -22,12 +22,14 @@ def test_decode_matches_reference_md5(golden_dir, name):
     assert yuv == meta["yuv_md5"]
 
 
+@pytest.mark.parametrize("lanes", ["4", "7"])
 @pytest.mark.parametrize("name", ["ra416_q32", "ra1080_q32"])
-def test_concurrent_segments_match_reference_md5(golden_dir, name):
+def test_concurrent_segments_match_reference_md5(golden_dir, name, lanes, monkeypatch):
     """Two copies of the stream on disjoint DPB slots, every picture launched back to back with no host
     synchronisation in between: the execution lanes run pictures concurrently, ordered only by their
     slot dependencies (vvcr_api.cpp launch), and every picture of both copies must still be bit-exact."""
     from vvc_amd import native as N
+    monkeypatch.setenv("VVCR_LANES", lanes)   # read by vvcr_create
     d = os.path.join(golden_dir, name)
     pics = S.load_sequence(d)
     meta = S.load_meta(d)

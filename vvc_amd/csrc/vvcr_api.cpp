@@ -150,13 +150,13 @@ static int rd_kind(int w, int h, int &tw, int &th) {
   return -1;
 }
 
-// Execution lanes: pictures are launched on NLANE HIP streams, each with its own scratch planes
+// Execution lanes: pictures are launched on nlane HIP streams (VVCR_LANES, default 4 = HIP's default
+// hardware queues per process; up to MAXLANE when GPU_MAX_HW_QUEUES allows), each with its own scratch planes
 // (prediction, residual, loop-filter ping-pong). A picture waits only for the pictures it depends on —
 // the last writer of each reference slot (RAW), and the last writer and every reader since of its own
 // slot (WAW / WAR) — so pictures that do not reference each other (the pictures of one temporal layer of
 // an RA GOP, an intra picture and the B pictures decoded before it) reconstruct concurrently.
-constexpr int NLANE = 4;              // = the process's hardware queues (GPU_MAX_HW_QUEUES default)
-constexpr int NINTRA = 2;             // lanes reserved for pictures without references
+constexpr int MAXLANE = 8;
 constexpr int NEV = 128;             // event ring (dependency markers)
 struct Lane {
   hipStream_t s = nullptr;
@@ -170,7 +170,8 @@ struct vvcr_ctx {
   std::string err;
   hipStream_t stream = nullptr;      // lane 0's stream (host copies, vvcr_stream)
   std::vector<std::array<DPlane, 3>> dpb;
-  Lane lanes[NLANE];
+  Lane lanes[MAXLANE];
+  int nlane = 4, nintra = 2;         // lanes; the first nintra take pictures without references
   uint64_t seq = 0;
   bool timing = true;                // record per-kernel-group events (vvcr_set_timing)
   std::vector<hipEvent_t> slot_w;                 // per DPB slot: completion of its last writer
@@ -202,7 +203,7 @@ struct vvcr_ctx {
 
 // every lane idle (host reads / writes of planes, vvcr_sync)
 static void sync_lanes(vvcr_ctx *ctx) {
-  for (Lane &ln : ctx->lanes) VVCR_CHECK_HIP(hipStreamSynchronize(ln.s));
+  for (int l = 0; l < ctx->nlane; l++) VVCR_CHECK_HIP(hipStreamSynchronize(ctx->lanes[l].s));
 }
 
 #define API_BEGIN try {
@@ -331,9 +332,9 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     r.idep_start.upload(ip.dep_start);
     r.ideps.upload(ip.deps);
     r.istate.ensure(16 + ip.jobs.size());
-    IntraParams P[NLANE];   // one device copy per lane (scratch plane pointers differ)
-    for (int l = 0; l < NLANE; l++) P[l] = make_intra_params(ctx, r, l);
-    r.iparams.upload(P, NLANE);
+    IntraParams P[MAXLANE];   // one device copy per lane (scratch plane pointers differ)
+    for (int l = 0; l < MAXLANE; l++) P[l] = make_intra_params(ctx, r, l);
+    r.iparams.upload(P, MAXLANE);
     r.n_ijobs = (int)ip.jobs.size();
     r.ictu_list.upload(ip.ctu_list);
     r.ictu_start.upload(ip.ctu_start);
@@ -391,11 +392,11 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   for (int l = 0; l < 2; l++)
     for (int i = 0; i < pp.num_ref[l]; i++)
       if (std::find(refs.begin(), refs.end(), pp.ref_slot[l][i]) == refs.end()) refs.push_back(pp.ref_slot[l][i]);
-  // Lane choice: pictures without references (intra) take lanes [0, NINTRA), which only intra pictures
+  // Lane choice: pictures without references (intra) take lanes [0, nintra), which only intra pictures
   // use, so an intra picture never queues behind B pictures and two intra-started segments may overlap;
-  // the others take the lane of [NINTRA, NLANE) whose last picture is one of their references (stream
+  // the others take the lane of [nintra, nlane) whose last picture is one of their references (stream
   // order then costs nothing), else the least recently used of those lanes.
-  const int lo = refs.empty() ? 0 : NINTRA, hi = refs.empty() ? NINTRA : NLANE;
+  const int lo = refs.empty() ? 0 : ctx->nintra, hi = refs.empty() ? ctx->nintra : ctx->nlane;
   int L = -1;
   if (!refs.empty())
     for (int l = lo; l < hi && L < 0; l++) {
@@ -548,7 +549,9 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
   ctx->sp = *sp;
   try {
     VVCR_CHECK_HIP(hipSetDevice(sp->device));
-    for (Lane &ln : ctx->lanes) VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ln.s, hipStreamNonBlocking));
+    if (const char *e = getenv("VVCR_LANES")) ctx->nlane = std::max(2, std::min(MAXLANE, atoi(e)));
+    ctx->nintra = ctx->nlane / 2;
+    for (int l = 0; l < ctx->nlane; l++) VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->lanes[l].s, hipStreamNonBlocking));
     ctx->stream = ctx->lanes[0].s;
     for (auto &e : ctx->ev_ring) VVCR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const int W = sp->width, H = sp->height;
@@ -561,8 +564,9 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     ctx->slot_w.assign(sp->dpb_slots, nullptr);
     ctx->slot_r.assign(sp->dpb_slots, {});
     ctx->slot_seq.assign(sp->dpb_slots, 0);
-    for (Lane &ln : ctx->lanes)
+    for (int l = 0; l < ctx->nlane; l++)
       for (int c = 0; c < 3; c++) {
+        Lane &ln = ctx->lanes[l];
         int w = c ? W / 2 : W, h = c ? H / 2 : H;
         ln.pred[c] = alloc_plane(w, h);
         ln.resi[c] = alloc_plane(w, h);
@@ -584,15 +588,18 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
 
 int vvcr_destroy(vvcr_ctx *ctx) {
   if (!ctx) return VVCR_E_ARG;
-  for (Lane &ln : ctx->lanes) (void)hipStreamSynchronize(ln.s);
+  for (int l = 0; l < ctx->nlane; l++) (void)hipStreamSynchronize(ctx->lanes[l].s);
   ctx->prepared.clear();
   for (auto &s : ctx->dpb)
     for (auto &p : s) (void)hipFree(p.p);
-  for (Lane &ln : ctx->lanes)
-    for (int c = 0; c < 3; c++) { (void)hipFree(ln.pred[c].p); (void)hipFree(ln.resi[c].p); (void)hipFree(ln.tmp[c].p); }
+  for (int l = 0; l < ctx->nlane; l++)
+    for (int c = 0; c < 3; c++) {
+      Lane &ln = ctx->lanes[l];
+      (void)hipFree(ln.pred[c].p); (void)hipFree(ln.resi[c].p); (void)hipFree(ln.tmp[c].p);
+    }
   for (auto &e : ctx->ev_ring) if (e) (void)hipEventDestroy(e);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
-  for (Lane &ln : ctx->lanes) (void)hipStreamDestroy(ln.s);
+  for (int l = 0; l < ctx->nlane; l++) (void)hipStreamDestroy(ctx->lanes[l].s);
   delete ctx;
   return VVCR_OK;
 }

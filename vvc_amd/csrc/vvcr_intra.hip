@@ -45,6 +45,11 @@ __constant__ uint8_t i_intraFilter[8] = {24, 24, 24, 14, 2, 0, 0, 0};
 constexpr int PLANAR = 0, DC = 1, HOR = 18, DIA = 34, VER = 50, VDIA = 66, LM = 67, MDLM_L = 68, MDLM_T = 69;
 constexpr int RB = 160;                      // reference buffer length (2*64 + mrl + 1, rounded)
 constexpr int EXT = 64;                      // negative-index room of the angular main reference
+// Residual rectangles of up to RESL samples (32x32, and every ISP CU up to 32x32) are staged in LDS;
+// larger ones (64-sample sides, rare in intra pictures) are read from HBM (L2-warm) by the
+// reconstruction. This keeps a 4-wave workgroup within half of the CU's 160 KB of LDS, so two CTU
+// workgroups — e.g. of two concurrently decoded intra pictures — share a CU.
+constexpr int RESL = 1024;
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ int ilog2(int v) { return v <= 0 ? -1 : 31 - __clz(v); }
@@ -102,7 +107,7 @@ __device__ __forceinline__ int wave_sum(int v) {
 // only steps that such a read depends on (IJ_PUBLISH) drain their HBM stores and raise a global flag.
 // ------------------------------------------------------------------------------------------------
 #ifndef VVCR_DIAG_NW
-constexpr int NW = 6; 
+constexpr int NW = 4; 
 #else
 constexpr int NW = VVCR_DIAG_NW;
 #endif
@@ -119,7 +124,7 @@ struct WaveScratch {
   int16_t tmpl[2][132];         // CCLM down-sampled luma: top row / left column
   int32_t lmp[4];
   int32_t red[8];               // MIP reduced boundary
-  int16_t resL[64 * 64];        // residual of the step, prefetched at entry
+  int16_t resL[RESL];           // residual of the step (rectangles of <= RESL samples), prefetched at entry
   int16_t ispPrev[64];          // ISP: last row / column of the previous region
 };
 
@@ -473,18 +478,19 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   const bool avhi = (J.av[2] & 1) != 0;
   // residual rectangle: the block, or the whole CU for ISP
   const int rx = isp ? J.cx : J.x, ry = isp ? J.cy : J.y, rw = isp ? J.cw : w, rh = isp ? J.ch : h;
-  // The residual does not depend on earlier steps: the first 2048 samples are loaded into registers
-  // before the dependency wait, and stored to LDS after the reference fill; larger blocks load the
-  // rest afterwards.
+  // The residual does not depend on earlier steps: up to RESL samples are loaded into registers before
+  // the dependency wait, and stored to LDS after the reference fill; larger rectangles are read from
+  // HBM by the reconstruction.
   const DPlane &R = P.resi[comp];
   const int rn = rw * rh;
   const int lrw = ilog2(rw);
   const bool rvec = ((rw | rx) & 3) == 0;   // plane strides are multiples of 64 samples
-  uint64_t rv[8];
+  const bool rlds = rn <= RESL;
+  uint64_t rv[4];
   int16_t rs[8];
   if (rvec) {
 #pragma unroll
-    for (int b = 0; b < 8; b++) {
+    for (int b = 0; b < 4; b++) {
       const int k = min((lane + 64 * b) * 4, rn - 4);
       const int yy = k >> lrw, xx = k & (rw - 1);
       rv[b] = *gp((const uint64_t *)&R.p[(size_t)(ry + yy) * R.stride + rx + xx]);
@@ -523,16 +529,17 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   // LMCS chroma residual scale (uniform), after the wait: it reads reconstructed luma of other steps
   const int cscale = (comp > 0 && (J.vnb & CS_SCALE)) ? chroma_scale(P, G, J.vx, J.vy, J.vnb, lane) : 0;
   auto store_resid = [&]() {
+    if (!rlds) return;
     if (rvec) {
 #pragma unroll
-      for (int b = 0; b < 8; b++)
+      for (int b = 0; b < 4; b++)
         if ((lane + 64 * b) * 4 < rn) *(uint64_t *)&S.resL[(lane + 64 * b) * 4] = rv[b];
     } else {
 #pragma unroll
       for (int b = 0; b < 8; b++)
         if (lane + 64 * b < rn) S.resL[lane + 64 * b] = rs[b];
     }
-    for (int k = (lane + 512) * (rvec ? 4 : 1); k < rn; k += 64 * (rvec ? 4 : 1)) {
+    for (int k = rvec ? RESL : (lane + 512); k < rn; k += 64) {   // non-vector rectangles above 512 samples
       const int yy = k >> lrw, xx = k & (rw - 1);
       const int16_t *src = &R.p[(size_t)(ry + yy) * R.stride + rx + xx];
       if (rvec) *(uint64_t *)&S.resL[k] = *gp((const uint64_t *)src);
@@ -993,7 +1000,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
         if (comp == 0 && (P.lmcs & 1)) ip = P.lmcs_fwd[ip];   // LMCS: mapped inter prediction (DecCu.cpp:696)
         pv = ((4 - J.ciip_w) * ip + J.ciip_w * pv + 2) >> 2;
       }
-      int rv = S.resL[(y0 - ry + yy) * rw + x0 - rx + xx + e];
+      int rv = rlds ? S.resL[(y0 - ry + yy) * rw + x0 - rx + xx + e] : *gp(&R.p[(size_t)(y0 + yy) * R.stride + x0 + xx + e]);
       if (cscale) rv = scale_resi(rv, cscale, bd);
       v2[e] = clampi(pv + rv, 0, maxv);
       if (isp && (ispVer ? xx + e == w - 1 : yy == h - 1)) S.ispPrev[ispVer ? yy : xx + e] = (int16_t)v2[e];
