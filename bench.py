@@ -19,7 +19,8 @@ import os
 # Execution lanes (libvvcr reads VVCR_LANES at vvcr_create): 3 intra lanes + 4 B lanes, each on its own
 # hardware queue, so that three intra-started segments and the B pictures of a fourth overlap; HIP's
 # default is 4 hardware queues per process, so the bench asks for 8 before the runtime starts.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:   # the box exports HIP's default of 4
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 os.environ.setdefault("VVCR_LANES", "7")
 
 import argparse
