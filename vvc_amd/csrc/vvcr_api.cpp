@@ -551,6 +551,7 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     VVCR_CHECK_HIP(hipSetDevice(sp->device));
     if (const char *e = getenv("VVCR_LANES")) ctx->nlane = std::max(2, std::min(MAXLANE, atoi(e)));
     ctx->nintra = ctx->nlane / 2;
+    if (const char *e = getenv("VVCR_INTRA_LANES")) ctx->nintra = std::max(1, std::min(ctx->nlane - 1, atoi(e)));
     for (int l = 0; l < ctx->nlane; l++) VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->lanes[l].s, hipStreamNonBlocking));
     ctx->stream = ctx->lanes[0].s;
     for (auto &e : ctx->ev_ring) VVCR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
