@@ -84,6 +84,28 @@ __device__ int filt(const int16_t *win, int ws, int x, int y, int fx, int fy, co
   return rnd ? clampi(v, 0, maxv) : v;
 }
 
+// The H-then-V branch of filt for every fraction (identity rows for zero fractions give the same
+// results as the copy / 1-D branches, see k_mc_affine), so lanes with different fractions do not diverge.
+template <int N>
+__device__ int filt2d(const int16_t *win, int ws, int x, int y, const int8_t *ch, const int8_t *cv, bool rnd, int bd) {
+  const int headRoom = max(2, IF_INTERNAL_PREC - bd);
+  const int maxv = (1 << bd) - 1;
+  const int sh1 = IF_FILTER_PREC - headRoom;
+  const int off1 = -(IF_INTERNAL_OFFS << sh1);
+  const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
+  const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
+  int sum = 0;
+#pragma unroll
+  for (int t = 0; t < N; t++) {
+    int s = 0;
+#pragma unroll
+    for (int u = 0; u < N; u++) s += win[(y + t) * ws + x + u] * ch[u];
+    sum += (int)(int16_t)((s + off1) >> sh1) * cv[t];
+  }
+  const int v = (int)(int16_t)((sum + off2) >> sh2);
+  return rnd ? clampi(v, 0, maxv) : v;
+}
+
 // ---------------------------------------------------------------------------------------------
 // DMVR helpers
 // ---------------------------------------------------------------------------------------------
@@ -527,9 +549,12 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
     const AffList &A = U.l[l];
     if (!A.present) continue;
     const int16_t *lwin = win + l * ALW;
-    // ---- luma: per sub-block 11x11 windows. Sub-blocks with both fractions non-zero run separably
-    // (filter<8,false,true,false> H pass over 11 rows into hmid, then the V pass), using the 6 non-zero
-    // taps of m_lumaFilter4x4 (InterpolationFilter.cpp:57: taps 0 and 7 are 0); the others take filt.
+    // ---- luma: per sub-block 11x11 windows, every sub-block through the same separable path (H pass over
+    // 11 rows into hmid, then the V pass; the 6 non-zero taps of m_lumaFilter4x4, InterpolationFilter.cpp:57),
+    // so the lanes of a tile whose sub-blocks have different fractions do not diverge. A zero fraction
+    // takes the identity row {.., 64, ..}: its intermediate is exact (16 s - 8192 fits int16) and the
+    // 2-D roundings then equal the copy / 1-D paths of xPredInterBlk (InterPrediction.cpp:784-803):
+    // ((64 t + off2) >> sh2 == t, and (((S - 8192 * 4) >> 2) * 64 + 2^9 + 2^19) >> 10 == (S + 32) >> 6).
     const bool prof = A.prof;
     const bool rnd = !prof && !bi && !U.wp;
     {
@@ -539,8 +564,7 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
         const int i = lane + 64 * k;
         const int sb = i / 44, e = i - sb * 44;
         if (sb >= nsb) continue;
-        const int fx = sbmv[l][sb][0] & 15, fy = sbmv[l][sb][1] & 15;
-        if (fx == 0 || fy == 0) continue;
+        const int fx = sbmv[l][sb][0] & 15;
         const int r = e >> 2, c = e & 3;
         const int16_t *src = lwin + sb * AWS * AWS + r * AWS + c;
         int sum = 0;
@@ -558,7 +582,7 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
       const int sb = (y >> 2) * nsx + (x >> 2);
       const int fx = sbmv[l][sb][0] & 15, fy = sbmv[l][sb][1] & 15;
       int v;
-      if (fx != 0 && fy != 0) {
+      {
         const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
         const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
         const int16_t *col = hmid + sb * 44 + (y & 3) * 4 + (x & 3);
@@ -567,8 +591,6 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
         for (int t = 1; t < 7; t++) sum += col[t * 4] * x_luma4x4[fy][t];
         v = (int)(int16_t)((sum + off2) >> sh2);
         if (rnd) v = clampi(v, 0, maxv);
-      } else {
-        v = filt<8>(lwin + sb * AWS * AWS, AWS, x & 3, y & 3, fx, fy, x_luma4x4[fx], x_luma4x4[fy], rnd, bd);
       }
       res[0][l][k] = v;
       if (prof) c14[y * 16 + x] = (int16_t)v;
@@ -616,7 +638,7 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
         const int y = lane / cw, x = lane - y * cw;
         const int sb = (y >> 2) * ncx + (x >> 2);
         const int fx = csmv[l][sb][0] & 31, fy = csmv[l][sb][1] & 31;
-        res[comp][l][0] = filt<4>(cwin + sb * 49, 7, x & 3, y & 3, fx, fy, x_chroma[fx], x_chroma[fy], !bi && !U.wp, bd);
+        res[comp][l][0] = filt2d<4>(cwin + sb * 49, 7, x & 3, y & 3, x_chroma[fx], x_chroma[fy], !bi && !U.wp, bd);
       }
     }
   }
