@@ -105,10 +105,23 @@ __global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
   const int X0 = blockIdx.x * ALF_TW, Y0 = blockIdx.y * ALF_TH;
   const int tid = threadIdx.x;
   const int W = S.w, H = S.h;
-  for (int i = tid; i < ALF_SH * (ALF_TW + 2 * ALF_HALO); i += 256) {
-    const int r = i / (ALF_TW + 2 * ALF_HALO), c = i - r * (ALF_TW + 2 * ALF_HALO);
-    const int sx = clip3(0, W - 1, X0 - ALF_HALO + c), sy = clip3(0, H - 1, Y0 - ALF_HALO + r);
-    t[r * ALF_SW + c] = S.p[(size_t)sy * S.stride + sx];
+  {
+    // all of a lane's tile loads in flight before its first LDS store (one memory round trip)
+    constexpr int TWH = ALF_TW + 2 * ALF_HALO, NIT = (ALF_SH * TWH + 255) / 256;
+    int16_t v[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; k++) {
+      const int i = tid + 256 * k;
+      const int r = i / TWH, c = i - r * TWH;
+      const int sx = clip3(0, W - 1, X0 - ALF_HALO + c), sy = clip3(0, H - 1, Y0 - ALF_HALO + min(r, ALF_SH - 1));
+      v[k] = S.p[sy * S.stride + sx];
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; k++) {
+      const int i = tid + 256 * k;
+      const int r = i / TWH, c = i - r * TWH;
+      if (i < ALF_SH * TWH) t[r * ALF_SW + c] = v[k];
+    }
   }
   __syncthreads();
   // sample (x, y) in picture coordinates -> LDS (valid for |x - tile| <= 3 and |y - tile| <= 3)
