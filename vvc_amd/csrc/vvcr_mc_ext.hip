@@ -221,13 +221,18 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
       }
     }
     __syncthreads();
-    if (lane < 25) {
-      const int ox = x_search[lane][0], oy = x_search[lane][1];
-      unsigned long long acc = 0;
-      for (int r = 0; r < h; r += 2)
-        for (int c = 0; c < w; c++)
-          acc += (unsigned long long)abs(bl[0][(2 + oy + r) * BS + 2 + ox + c] - bl[1][(2 - oy + r) * BS + 2 - ox + c]);
-      sad[lane] = acc;   // xGetSAD with subShift 1: (sum << 1) >> 1 in xDMVRCost
+    {
+      // 25 search positions x 2 lanes (every other sampled row each); the partial SADs (< 2^18) are
+      // added by a shuffle, so the sum is the reference's whatever the order
+      const int pos = lane < 50 ? lane % 25 : 0, half = lane < 50 ? lane / 25 : 0;
+      const int ox = x_search[pos][0], oy = x_search[pos][1];
+      uint32_t acc = 0;
+      if (lane < 50)
+        for (int r = 2 * half; r < h; r += 4)
+          for (int c = 0; c < w; c++)
+            acc += (uint32_t)abs(bl[0][(2 + oy + r) * BS + 2 + ox + c] - bl[1][(2 - oy + r) * BS + 2 - ox + c]);
+      const uint32_t other = __shfl(acc, (lane + 25) & 63);
+      if (lane < 25) sad[lane] = (unsigned long long)(acc + other);   // xGetSAD with subShift 1: (sum << 1) >> 1 in xDMVRCost
     }
     __syncthreads();
     if (lane == 0) {
@@ -370,21 +375,34 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
       __syncthreads();
       // per 4x4: 6x6 window sums -> (vx, vy)  (calcBIOSumsCore + applyBiOptFlow :1338-1351)
       const int nu = (bw >> 2) * (bh >> 2);
-      if (lane < nu) {
-        const int xu = lane % (bw >> 2), yu = lane / (bw >> 2);
+      {
+        // 4 lanes per 4x4 unit, window rows {p, p + 4} of the 6 for lane part p; the five integer sums
+        // are reduced by shuffles (exact, order-independent)
+        const int u = lane >> 2, part = lane & 3;
+        const int xu = u % (bw >> 2), yu = u / (bw >> 2);
         int sGX = 0, sGY = 0, sDIX = 0, sDIY = 0, sSGG = 0;
-        for (int yy = 0; yy < 6; yy++)
-          for (int xx = 0; xx < 6; xx++) {
-            const int idx = (4 * yu + yy) * PS + 4 * xu + xx;
-            const int tGX = (gx[0][idx] + gx[1][idx]) >> 1;
-            const int tGY = (gy[0][idx] + gy[1][idx]) >> 1;
-            const int tDI = (pr[1][idx] >> 4) - (pr[0][idx] >> 4);
-            sGX += abs(tGX);
-            sGY += abs(tGY);
-            sDIX += tGX < 0 ? -tDI : (tGX == 0 ? 0 : tDI);
-            sDIY += tGY < 0 ? -tDI : (tGY == 0 ? 0 : tDI);
-            sSGG += tGY < 0 ? -tGX : (tGY == 0 ? 0 : tGX);
-          }
+        if (u < nu)
+          for (int yy = part; yy < 6; yy += 4)
+            for (int xx = 0; xx < 6; xx++) {
+              const int idx = (4 * yu + yy) * PS + 4 * xu + xx;
+              const int tGX = (gx[0][idx] + gx[1][idx]) >> 1;
+              const int tGY = (gy[0][idx] + gy[1][idx]) >> 1;
+              const int tDI = (pr[1][idx] >> 4) - (pr[0][idx] >> 4);
+              sGX += abs(tGX);
+              sGY += abs(tGY);
+              sDIX += tGX < 0 ? -tDI : (tGX == 0 ? 0 : tDI);
+              sDIY += tGY < 0 ? -tDI : (tGY == 0 ? 0 : tDI);
+              sSGG += tGY < 0 ? -tGX : (tGY == 0 ? 0 : tGX);
+            }
+#pragma unroll
+        for (int m = 1; m < 4; m <<= 1) {
+          sGX += __shfl_xor(sGX, m);
+          sGY += __shfl_xor(sGY, m);
+          sDIX += __shfl_xor(sDIX, m);
+          sDIY += __shfl_xor(sDIY, m);
+          sSGG += __shfl_xor(sSGG, m);
+        }
+        if (u < nu && part == 0) {
         const int limit = 15;
         int vx = sGX == 0 ? 0 : (sDIX << 2) >> (31 - __clz(sGX));
         vx = clampi(vx, -limit, limit);
@@ -392,7 +410,8 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
         const int tmpData = ((vx * mains) * (1 << 12) + vx * secs) >> 1;
         int vy = sGY == 0 ? 0 : ((sDIY << 2) - tmpData) >> (31 - __clz(sGY));
         vy = clampi(vy, -limit, limit);
-        sh_v[lane][0] = vx; sh_v[lane][1] = vy;
+        sh_v[u][0] = vx; sh_v[u][1] = vy;
+        }
       }
       __syncthreads();
       const int shiftNum = IF_INTERNAL_PREC + 1 - bd, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
