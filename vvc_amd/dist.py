@@ -17,7 +17,7 @@ class Ranks:
             import torch.distributed as dist
             backend = os.environ.get("VVCR_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
             if backend == "nccl":
-                torch.cuda.set_device(self.local)
+                torch.cuda.set_device(int(os.environ.get("VVCR_DEVICE", self.local)))   # VVCR_DEVICE: one-GPU rehearsal
                 self.device = "cuda"
             dist.init_process_group(backend)
             self.dist = dist
