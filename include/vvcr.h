@@ -40,6 +40,7 @@ extern "C" {
 #define VVCR_E_STATE -3
 #define VVCR_E_UNSUPPORTED -4
 #define VVCR_MAX_REF 16
+#define VVCR_MAX_TILE_LINES 64   /* tile columns / rows per picture */
 
 typedef struct vvcr_ctx vvcr_ctx;
 
@@ -129,6 +130,12 @@ typedef struct vvcr_pic_params {
   int32_t lmcs_cadj[16];
   int32_t max_tb_log2, log2_max_ts;
   int32_t use_mts, implicit_mts, joint_cbcr_sign;
+  /* Tiles (PPS::getTileColumnBd / getTileRowBd, in CTUs; bd[n] = picture size in CTUs). num_tile_* = 0
+   * means one tile. Intra prediction, CCLM, CIIP and LMCS chroma scaling read neighbours of the same
+   * slice (vvcr_cu.slice) and tile only (CodingStructure::getCURestricted, CodingStructure.cpp:1519). */
+  int32_t num_tile_cols, num_tile_rows;
+  int32_t tile_col_bd[VVCR_MAX_TILE_LINES + 1], tile_row_bd[VVCR_MAX_TILE_LINES + 1];
+  int32_t entropy_sync;        /* WPP (pps entropy_coding_sync): not supported, rejected */
 } vvcr_pic_params;
 
 /* ALF / CC-ALF filters of the picture (AdaptiveLoopFilter::reconstructCoeffAPSs result,
@@ -188,6 +195,30 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t stage_mask);
 int vvcr_prepare_picture(vvcr_ctx *ctx, uint32_t stage_mask, int32_t *handle);
 int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle);
 int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle);
+
+/* Host-only picture builder: the same begin / submit / loop-filter / plan sequence on a standalone
+ * object that needs no context and no device, so a parallel host producer (one thread per picture —
+ * the reference decodes a picture's slices in DecLib::decode / DecSlice::decompressSlice, DecLib.cpp:1753)
+ * can validate and plan several pictures at once. vvcr_prepare_planned then only uploads the planned
+ * work lists into a prepared-picture handle of ctx; it may be called from several threads at once
+ * (each with its own picture). pp->slot / ref_slot are checked against sp->dpb_slots.
+ *   vvcr_picture_work_counts: counts[0..7] = transform blocks, MC blocks, DMVR/BDOF blocks, affine tiles,
+ *   inter recon tiles, intra steps, deblocking segments, DMVR sub-blocks (diagnostics); returns 8. */
+typedef struct vvcr_picture vvcr_picture;
+int vvcr_picture_create(const vvcr_seq_params *sp, const vvcr_pic_params *pp, vvcr_picture **out);
+int vvcr_picture_submit(vvcr_picture *pic,
+                        const vvcr_cu *cu, int32_t ncu,
+                        const vvcr_pu *pu, int32_t npu,
+                        const vvcr_tu *tu, int32_t ntu,
+                        const int32_t *coef, int64_t ncoef,
+                        const vvcr_motion *motion,
+                        const vvcr_geo *geo, int32_t ngeo);
+int vvcr_picture_set_loop_filter_params(vvcr_picture *pic, const vvcr_sao *sao, const vvcr_alf *alf);
+int vvcr_picture_plan(vvcr_picture *pic, uint32_t stage_mask);
+int vvcr_picture_work_counts(const vvcr_picture *pic, int64_t *counts, int32_t n);
+const char *vvcr_picture_last_error(const vvcr_picture *pic);
+int vvcr_picture_destroy(vvcr_picture *pic);
+int vvcr_prepare_planned(vvcr_ctx *ctx, const vvcr_picture *pic, int32_t *handle);
 
 /* Per-kernel-group statistics of the last launch of a picture (handle 0 = the last launched picture):
  * HIP-event time on the library stream, number of kernel launches in the group and the algorithmic

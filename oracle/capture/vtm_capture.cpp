@@ -204,6 +204,7 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
   H.add("lf_across_slices", pps.getLoopFilterAcrossSlicesEnabledFlag() ? 1 : 0);
   H.add("lf_across_tiles", pps.getLoopFilterAcrossTilesEnabledFlag() ? 1 : 0);
   H.add("num_tiles", pps.getNumTiles());
+  H.add("entropy_sync", pps.getEntropyCodingSyncEnabledFlag() ? 1 : 0);
   H.add("sao_enabled", sps.getSAOEnabledFlag() ? 1 : 0);
   H.add("sao_luma", sl.getSaoEnabledFlag(CHANNEL_TYPE_LUMA) ? 1 : 0);
   H.add("sao_chroma", sl.getSaoEnabledFlag(CHANNEL_TYPE_CHROMA) ? 1 : 0);
@@ -287,6 +288,17 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
         }
       }
     F.i32("wp", wp, {2, (uint64_t)MAX_NUM_REF, 3, 7});
+  }
+
+  // tile layout in CTUs (PPS::getTileColumnBd / getTileRowBd); bd[n] = picture size in CTUs
+  {
+    std::vector<int32_t> cb, rb;
+    for (uint32_t i = 0; i < pps.getNumTileColumns(); i++) cb.push_back((int32_t)pps.getTileColumnBd(i));
+    cb.push_back((int32_t)pcv.widthInCtus);
+    for (uint32_t i = 0; i < pps.getNumTileRows(); i++) rb.push_back((int32_t)pps.getTileRowBd(i));
+    rb.push_back((int32_t)pcv.heightInCtus);
+    F.i32("tile_col_bd", cb, {(uint64_t)cb.size()});
+    F.i32("tile_row_bd", rb, {(uint64_t)rb.size()});
   }
 
   // chroma QP mapping: mapped[c][qp + 64] for qp in [-64, 63]

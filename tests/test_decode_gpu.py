@@ -11,7 +11,8 @@ from vvc_amd import stream as S
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["ai416_q37", "ra416_q32", "ra1080_q32", "ailm416_q37", "ralm416_q32", "rawp416_q32", "ra2160_q27", "ra2160_q32"])
+@pytest.mark.parametrize("name", ["ai416_q37", "ra416_q32", "ra1080_q32", "ailm416_q37", "ralm416_q32", "rawp416_q32", "ratile416_q32",
+                                  "ra2160_q27", "ra2160_q32"])
 def test_decode_matches_reference_md5(golden_dir, name):
     d = os.path.join(golden_dir, name)
     pics = S.load_sequence(d)
@@ -64,3 +65,81 @@ def test_concurrent_segments_match_reference_md5(golden_dir, name, lanes, monkey
                 ctx.release(h)
     finally:
         dec.close()
+
+
+def test_many_launches_without_sync_keep_reference_ordering(golden_dir):
+    """Dependency markers are per DPB slot (vvcr_api.cpp launch): 300 launches with no host sync, one
+    reference slot kept alive across all of them and rewritten in the middle (write after read of ~100
+    readers on several lanes) — every slot ends with the right picture."""
+    from vvc_amd import native as N
+    d = os.path.join(golden_dir, "ra416_q32")
+    pics = S.load_sequence(d, max_pics=2)         # POC 0 (I) and POC 16 (B, references POC 0 only)
+    meta = S.load_meta(d)
+    I, B = pics
+    assert {int(v) for l in range(2) for v in B["ref_poc"][l][:B["hdr"]["num_ref_l%d" % l]]} == {0}
+    dec = D.Decoder(pics, dpb_slots=6)
+    ctx = dec.ctx
+    try:
+        def prep(p, slot):
+            ctx.begin_picture(S.pic_params(p, slot, {0: 0}))
+            S.submit(ctx, p)
+            S.set_loop_filter_params(ctx, p)
+            return ctx.prepare(N.STAGE_ALL)
+        hi = prep(I, 0)
+        hb = [prep(B, s) for s in range(1, 6)]
+        ctx.launch(hi)
+        for k in range(300):
+            ctx.launch(hb[k % 5])
+            if k == 150:
+                ctx.launch(hi)                        # rewrites the reference slot while its readers run
+        ctx.sync()
+        assert D.plane_md5s(dec.read(0)) == meta["poc_plane_md5"]["0"]
+        for s in range(1, 6):
+            assert D.plane_md5s(dec.read(s)) == meta["poc_plane_md5"]["16"], "slot %d" % s
+        for h in [hi] + hb:
+            ctx.release(h)
+    finally:
+        dec.close()
+
+
+def test_bench_configuration_in_flight_matches_reference_md5(golden_dir, tmp_path):
+    """bench.py's timed configuration: 4 segment copies in flight, 7 lanes (3 intra) on 8 hardware queues
+    (set before the HIP runtime starts, hence a fresh process), no host sync between pictures."""
+    import subprocess
+    import sys
+    script = tmp_path / "inflight.py"
+    script.write_text(r'''
+import os, sys
+sys.path.insert(0, %r)
+from vvc_amd import native as N, stream as S, decode as D
+d = os.path.join(%r, "ra1080_q32")
+pics, meta = S.load_sequence(d), S.load_meta(d)
+per = 8
+dec = D.Decoder(pics, dpb_slots=4 * per)
+ctx = dec.ctx
+copies = []
+for c in range(4):
+    alloc = S.SlotAllocator(pics, per, base=per * c)
+    hs = []
+    for i, p in enumerate(pics):
+        slot = alloc.assign(i, p["hdr"]["poc"])
+        ctx.begin_picture(S.pic_params(p, slot, alloc.slot_of)); S.submit(ctx, p); S.set_loop_filter_params(ctx, p)
+        hs.append((ctx.prepare(N.STAGE_ALL), p["hdr"]["poc"], slot))
+    copies.append(hs)
+ctx.set_timing(False)
+for rnd in range(3):
+    for hs in copies:
+        for h, _, _ in hs:
+            ctx.launch(h)
+ctx.sync()
+bad = 0
+for hs in copies:
+    owner = {slot: poc for _, poc, slot in hs}
+    for slot, poc in owner.items():
+        bad += D.plane_md5s(dec.read(slot)) != meta["poc_plane_md5"][str(poc)]
+print("MISMATCHES", bad)
+''' % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), golden_dir))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="8", VVCR_LANES="7", VVCR_INTRA_LANES="3")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "MISMATCHES 0" in r.stdout, r.stdout[-2000:]

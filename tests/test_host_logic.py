@@ -37,3 +37,89 @@ def test_slot_allocator_reports_exhaustion():
         a = S.SlotAllocator(pics, 2)
         for i, p in enumerate(pics):
             a.assign(i, p["hdr"]["poc"])
+
+
+# ---- host-only picture builder (vvcr_picture_*): validation and planning without a device
+
+def _first_pic(name, idx=0):
+    pics = S.load_sequence(os.path.join(GOLD, name), max_pics=idx + 1)
+    alloc = S.SlotAllocator(pics, 16)
+    for i, p in enumerate(pics):
+        slot = alloc.assign(i, p["hdr"]["poc"])
+    return p, slot, dict(alloc.slot_of)
+
+
+def _picture(p, slot, slot_of):
+    from vvc_amd import native as N
+    h = p["hdr"]
+    return N.Picture(h["width"], h["height"], S.pic_params(p, slot, slot_of), bit_depth=h["bitdepth_y"],
+                     ctu_log2=h["ctu_log2"], dpb_slots=16)
+
+
+def test_builder_rejects_tu_crossing_the_bottom_edge():
+    import numpy as np
+    from vvc_amd import native as N
+    p, slot, slot_of = _first_pic("ai416_q37")
+    H = p["hdr"]["height"]
+    tu = np.array(p["tu"], np.int32)
+    k = int(np.nonzero(tu[:, 6 + 2] > 0)[0][-1])     # a TU with a luma block (b[0][2] = width > 0)
+    tu[k, 6 + 1] = H - tu[k, 6 + 3] + 4               # b[0][1] = y: 4 rows past the bottom edge
+    pic = _picture(p, slot, slot_of)
+    geo = np.zeros((0, 13), np.int32)
+    with pytest.raises(N.VvcrError) as e:
+        pic.submit(p["cu"], p["pu"], tu, p["coef"], p["motion"].reshape(-1, 10), geo)
+    assert "(-1)" in str(e.value) and "area" in str(e.value)      # VVCR_E_ARG
+    pic.close()
+
+
+def test_builder_rejects_cu_outside_the_picture():
+    import numpy as np
+    from vvc_amd import native as N
+    p, slot, slot_of = _first_pic("ra416_q32", 1)
+    cu = np.array(p["cu"], np.int32)
+    cu[0, 0] = p["hdr"]["width"] - cu[0, 2] + 8         # x: past the right edge
+    pic = _picture(p, slot, slot_of)
+    with pytest.raises(N.VvcrError):
+        pic.submit(cu, p["pu"], p["tu"], p["coef"], p["motion"].reshape(-1, 10), np.zeros((0, 13), np.int32))
+    pic.close()
+
+
+def test_pic_params_refuses_missing_reference():
+    p, slot, slot_of = _first_pic("ra416_q32", 1)
+    with pytest.raises(KeyError):
+        S.pic_params(p, slot, {})
+
+
+@pytest.mark.parametrize("name", ["ai416_q37", "ra416_q32", "ralm416_q32", "rawp416_q32", "ratile416_q32"])
+def test_builder_plans_every_picture(name):
+    pics = S.load_sequence(os.path.join(GOLD, name))
+    alloc = S.SlotAllocator(pics, 16)
+    for i, p in enumerate(pics):
+        slot = alloc.assign(i, p["hdr"]["poc"])
+        pic = S.plan_picture(p, slot, alloc.slot_of, dpb_slots=16)
+        c = pic.work_counts()
+        if p["hdr"]["slice_type"] == 2:
+            assert c["intra_steps"] > 0 and c["mc"] == 0
+        pic.close()
+
+
+def test_threaded_planning_is_deterministic():
+    """Several pictures planned at once on several threads (the library drops the GIL) give the same
+    work lists as one at a time."""
+    import concurrent.futures as cf
+    pics = S.load_sequence(os.path.join(GOLD, "ra416_q32"))
+    alloc = S.SlotAllocator(pics, 16)
+    jobs = []
+    for i, p in enumerate(pics):
+        slot = alloc.assign(i, p["hdr"]["poc"])
+        jobs.append((p, slot, dict(alloc.slot_of)))
+
+    def counts(j):
+        pic = S.plan_picture(*j, dpb_slots=16)
+        c = pic.work_counts()
+        pic.close()
+        return c
+    serial = [counts(j) for j in jobs]
+    with cf.ThreadPoolExecutor(6) as ex:
+        par = list(ex.map(counts, jobs))
+    assert par == serial

@@ -2,11 +2,13 @@
 # Re-creates the committed test bitstreams with the REFERENCE encoder built by oracle/ref.mk
 # (VTM 7.3 EncoderApp, CTC configs from /root/reference/cfg). Test-infrastructure only; runs in the
 # build container (needs /root/reference). Every stream carries MD5 decoded-picture-hash SEI.
-#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32
+#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32
 set -e
 R=/root/reference/cfg; E=${E:-$(dirname $0)/../oracle/_ref/EncoderApp}; T=${T:-/tmp/enc}; O=${O:-$(dirname $0)/../tests/golden/streams}
 mkdir -p $T $O
 G="python3 $(dirname $0)/gen_synth.py"
+TILES="--EnablePicPartitioning=1 --RasterScanSlices=1 --RasterSliceSizes=1000 --DisableLoopFilterAcrossTiles=0 --DisableLoopFilterAcrossSlices=0"
+FAST="--SearchRange=32 --MaxMTTHierarchyDepth=1 --MaxMTTHierarchyDepthISliceL=1 --MaxMTTHierarchyDepthISliceC=1 --LCTUFast=1 --FastMrg=1 --PBIntraFast=1 --FastMIP=1 --FastLFNST=1 --ISPFast=1 --BcwFast=1 --TransformSkipFast=1"
 enc() { # name cfg W H frames qp yuv extra...
   local n=$1 cfg=$2 w=$3 h=$4 f=$5 q=$6 y=$7; shift 7
   $E -c $R/$cfg -i $y -wdt $w -hgt $h -fr 50 -f $f -q $q --InputBitDepth=8 --SEIDecodedPictureHash=1 \
@@ -26,5 +28,11 @@ for n in "$@"; do case $n in
   # brightness fade with explicit weighted prediction on (WeightPrediction::xWeightedPredictionBi/Uni)
   rawp416_q32) [ -f $T/syn416f.yuv ] || $G 416 240 17 $T/syn416f.yuv 0.002 0 0.03; enc $n encoder_randomaccess_vtm.cfg 416 240 17 32 $T/syn416f.yuv --WeightedPredP=1 --WeightedPredB=1 ;;
   ailm416_q37) [ -f $T/syn416v.yuv ] || $G 416 240 17 $T/syn416v.yuv 0.002 1; enc $n encoder_intra_vtm.cfg 416 240 8 37 $T/syn416v.yuv --TemporalSubsampleRatio=1 ;;
+  # tile rows (one raster-scan slice holding every tile; loop filters cross tile edges): the spatial
+  # shards of the multi-GPU path -- intra / CABAC stop at tile rows, DBK/SAO/ALF do not
+  ratile416_q32) [ -f $T/syn416.yuv ] || $G 416 240 17 $T/syn416.yuv; enc $n encoder_randomaccess_vtm.cfg 416 240 17 32 $T/syn416.yuv $TILES --TileColumnWidthArray=4 --TileRowHeightArray=1 ;;
+  ratile1080_q32) [ -f $T/syn1080.yuv ] || $G 1920 1080 9 $T/syn1080.yuv; enc $n encoder_randomaccess_vtm.cfg 1920 1080 9 32 $T/syn1080.yuv --SearchRange=64 $TILES --TileColumnWidthArray=15 --TileRowHeightArray=1 ;;
+  # 8K, 8 tile rows (4,4,4,4,4,4,5,5 CTU rows); encoder fast-search settings only (the coded tools are the CTC set)
+  ra4320t_q32) [ -f $T/syn4320.yuv ] || $G 7680 4320 3 $T/syn4320.yuv; enc $n encoder_randomaccess_vtm.cfg 7680 4320 3 32 $T/syn4320.yuv $TILES $FAST --TileColumnWidthArray=60 --TileRowHeightArray="4 4 4 4 4 4 5" ;;
   *) echo "unknown stream $n"; exit 1 ;;
 esac; done

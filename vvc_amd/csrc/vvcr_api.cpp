@@ -12,6 +12,8 @@
 #include <array>
 #include <cstring>
 #include <memory>
+#include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -138,6 +140,27 @@ struct RdoPlan {
   int64_t coef_total = 0;
 };
 
+// A picture under construction on the host (vvcr_picture_*): its parameters, descriptors and loop-filter
+// parameters, and after vvcr_picture_plan its work lists. Host memory only, no device or context: a
+// producer may build and plan several pictures on several threads at once (one thread per picture) and
+// hand them to vvcr_prepare_planned, which only uploads.
+struct vvcr_picture {
+  vvcr_seq_params sp{};
+  vvcr_pic_params pp{};
+  std::string err;
+  PictureDescriptors desc;
+  bool submitted = false;
+  bool have_sao = false, have_alf = false;
+  std::vector<int32_t> h_sao;
+  std::vector<int16_t> h_alf_luma_coef, h_alf_luma_clip, h_alf_chroma, h_alf_cc, h_alf_set;
+  std::vector<uint8_t> h_alf_ctb;
+  uint32_t mask = 0;
+  bool planned = false;
+  WorkLists wl;
+  IntraPlan intra;
+  DbkLists dbk;
+};
+
 // Hadamard tile of RdCost::xGetHADs for a w x h block (RdCost.cpp:2818-2911), or -1 for odd sizes
 static int rd_kind(int w, int h, int &tw, int &th) {
   if (w > h && (h & 7) == 0 && (w & 15) == 0) { tw = 16; th = 8; return RD_16x8; }
@@ -157,7 +180,6 @@ static int rd_kind(int w, int h, int &tw, int &th) {
 // slot (WAW / WAR) — so pictures that do not reference each other (the pictures of one temporal layer of
 // an RA GOP, an intra picture and the B pictures decoded before it) reconstruct concurrently.
 constexpr int MAXLANE = 8;
-constexpr int NEV = 128;             // event ring (dependency markers)
 struct Lane {
   hipStream_t s = nullptr;
   DPlane pred[3], resi[3], tmp[3];
@@ -174,27 +196,26 @@ struct vvcr_ctx {
   int nlane = 4, nintra = 2;         // lanes; the first nintra take pictures without references
   uint64_t seq = 0;
   bool timing = true;                // record per-kernel-group events (vvcr_set_timing)
-  std::vector<hipEvent_t> slot_w;                 // per DPB slot: completion of its last writer
-  std::vector<std::vector<hipEvent_t>> slot_r;    // per DPB slot: completions of its readers since
-  std::vector<uint64_t> slot_seq;                 // per DPB slot: launch sequence number of its last writer
-  hipEvent_t ev_ring[NEV] = {};
-  int ev_next = 0;
-  vvcr_pic_params pp{};
+  // Dependency markers, owned per DPB slot so that no event is ever shared between slots: slot_w[s] is
+  // re-recorded by every writer of slot s, slot_r[s][l] by every reader of s on lane l. A stream wait
+  // captures the event's most recent record, so a later picture waits on exactly the last writer (RAW)
+  // and, when it overwrites s, on the last reader of every lane (WAR) — a lane's stream is in order, so
+  // its last reader follows all its earlier ones. Readers of s from before its previous writer are
+  // covered by that writer (it waited on them). No launch count or host sync bounds this.
+  std::vector<hipEvent_t> slot_w;                   // per DPB slot: its last writer
+  std::vector<uint8_t> slot_w_set;                  // slot_w recorded at least once
+  std::vector<std::array<hipEvent_t, MAXLANE>> slot_r;   // per DPB slot and lane: last reader
+  std::vector<uint32_t> slot_r_set;                 // per DPB slot: lanes with a reader since the last write
+  std::vector<uint64_t> slot_seq;                   // per DPB slot: launch sequence number of its last writer
   bool in_picture = false;
-  PictureDescriptors desc;          // host copy of the submitted descriptors (vvcr_host.h)
-  // loop-filter parameters of the current picture (host copies until prepare)
-  bool have_sao = false, have_alf = false;
-  std::vector<int32_t> h_sao;
-  std::vector<int16_t> h_alf_luma_coef, h_alf_luma_clip, h_alf_chroma, h_alf_cc, h_alf_set;
-  std::vector<uint8_t> h_alf_ctb;
-  // planning scratch
-  WorkLists wl;
-  IntraPlan intra;
-  DbkLists dbk;
+  vvcr_picture cur;                  // the picture of vvcr_begin_picture .. vvcr_end_picture / vvcr_prepare_picture
   DevVec<uint16_t> d_scans;
   ScanTables scans;
-  // prepared pictures: index 0 is the scratch record of vvcr_end_picture
+  // prepared pictures: index 0 is the scratch record of vvcr_end_picture. The table is shared by the
+  // threads calling vvcr_prepare_planned and the launching thread: `prepared_mu` guards it (a record
+  // itself is only touched by the thread that prepares it, then by launch / release).
   std::vector<std::unique_ptr<Prepared>> prepared;
+  std::mutex prepared_mu;
   Prepared *last = nullptr;          // last launched (stage times, DMVR deltas)
   int n_cu = 256;                    // compute units (persistent intra launch width)
   std::vector<std::unique_ptr<struct RdoPlan>> rdo;   // encoder RDO plans (vvcr_rd_plan / vvcr_fwd_plan)
@@ -271,47 +292,92 @@ static double mc_bytes(const McJob &j) {
   return 2.0 * (lists * in + 1.5 * j.w * j.h);
 }
 
-// Host phase: every work list of the current picture, uploaded into r.
-static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
+// Host phase, part 1 (no device): every work list of the picture.
+static void plan_picture(vvcr_picture &b, uint32_t mask) {
+  if (!b.submitted) throw VvcrError(VVCR_E_STATE, "picture planned before its descriptors were submitted");
+  const vvcr_seq_params &sp = b.sp;
+  const vvcr_pic_params &pp = b.pp;
+  b.wl.clear();
+  b.intra.clear();
+  b.dbk.clear();
+  if (pp.lmcs_enabled && sp.bit_depth != 10) throw VvcrError(VVCR_E_UNSUPPORTED, "LMCS tables are captured for 10-bit luma");
+  // The three planners read the descriptors only and write disjoint outputs: deblocking runs on a
+  // second thread beside the work lists and the intra plan (a 4K intra picture plans in ~100 ms each).
+  std::exception_ptr dbk_err;
+  std::thread dbk_thread;
+  if (mask & VVCR_STAGE_DBK)
+    dbk_thread = std::thread([&] {
+      try {
+        plan_deblocking(sp, pp, b.desc, b.dbk);
+      } catch (...) {
+        dbk_err = std::current_exception();
+      }
+    });
+  try {
+    if (mask & (VVCR_STAGE_RESID | VVCR_STAGE_INTER)) build_work_lists(sp, pp, b.desc, b.wl);
+    if ((mask & VVCR_STAGE_INTER) && b.wl.n_unsupported_inter)
+      throw VvcrError(VVCR_E_UNSUPPORTED, std::to_string(b.wl.n_unsupported_inter) + " inter CUs use tools not supported yet");
+    if (mask & VVCR_STAGE_INTRA) plan_intra(sp, pp, b.desc, b.intra);
+  } catch (...) {
+    if (dbk_thread.joinable()) dbk_thread.join();
+    throw;
+  }
+  if (dbk_thread.joinable()) dbk_thread.join();
+  if (dbk_err) std::rethrow_exception(dbk_err);
+  const bool saoOn = pp.sao_luma || pp.sao_chroma;
+  const bool alfOn = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
+  if ((mask & VVCR_STAGE_SAO) && saoOn && !b.have_sao)
+    throw VvcrError(VVCR_E_STATE, "SAO is enabled for the picture but no SAO parameters were set");
+  if ((mask & VVCR_STAGE_ALF) && alfOn && !b.have_alf)
+    throw VvcrError(VVCR_E_STATE, "ALF is enabled for the picture but no ALF parameters were set");
+  b.mask = mask;
+  b.planned = true;
+}
+
+// Host phase, part 2: upload the planned lists of b into the device buffers of r.
+static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
+  if (!bp.planned) throw VvcrError(VVCR_E_STATE, "picture not planned");
+  if (bp.sp.width != ctx->sp.width || bp.sp.height != ctx->sp.height || bp.sp.ctu_log2 != ctx->sp.ctu_log2 ||
+      bp.sp.bit_depth != ctx->sp.bit_depth || bp.sp.dpb_slots > ctx->sp.dpb_slots)
+    throw VvcrError(VVCR_E_ARG, "picture built for other sequence parameters than the context's");
   r.wait();
-  r.pp = ctx->pp;
+  r.pp = bp.pp;
+  const uint32_t mask = bp.mask;
   r.mask = mask;
   r.launched = false;
   for (int k = 0; k < NK; k++) { r.alg_bytes[k] = 0; r.launches[k] = 0; r.ran[k] = false; }
   const vvcr_seq_params &sp = ctx->sp;
-  const vvcr_pic_params &pp = ctx->pp;
+  const vvcr_pic_params &pp = bp.pp;
+  const WorkLists &wl = bp.wl;
   const double pix = (double)sp.width * sp.height * 1.5;   // samples of the three planes
-  if (mask & (VVCR_STAGE_RESID | VVCR_STAGE_INTER)) build_work_lists(sp, pp, ctx->desc, ctx->wl);
   if (mask & VVCR_STAGE_RESID) {
-    r.coef.upload(ctx->desc.coef);
-    r.tb.upload(ctx->wl.tb);
-    r.n_tb = (int)ctx->wl.tb.size();
-    r.n_tb_small = ctx->wl.tb_small;
+    r.coef.upload(bp.desc.coef);
+    r.tb.upload(wl.tb);
+    r.n_tb = (int)wl.tb.size();
+    r.n_tb_small = wl.tb_small;
     double b = 0;
-    for (const TbJob &t : ctx->wl.tb) b += (double)t.w * t.h * (4 + 2);   // int32 levels in, int16 residual out
+    for (const TbJob &t : wl.tb) b += (double)t.w * t.h * (4 + 2);   // int32 levels in, int16 residual out
     r.alg_bytes[K_RESID] = b;
   }
   if (mask & VVCR_STAGE_INTER) {
-    if (ctx->wl.n_unsupported_inter)
-      throw VvcrError(VVCR_E_UNSUPPORTED, std::to_string(ctx->wl.n_unsupported_inter) + " inter CUs use tools not supported yet");
-    r.mc_basic.upload(ctx->wl.mc_basic);
-    r.mc_bidir.upload(ctx->wl.mc_bidir);
-    r.aff_pu.upload(ctx->wl.aff_pu);
-    r.aff_jobs.upload(ctx->wl.aff_jobs);
-    r.n_basic = (int)ctx->wl.mc_basic.size();
-    r.n_bidir = (int)ctx->wl.mc_bidir.size();
-    r.n_aff = (int)ctx->wl.aff_jobs.size();
-    r.n_dmvr = ctx->wl.n_dmvr;
+    r.mc_basic.upload(wl.mc_basic);
+    r.mc_bidir.upload(wl.mc_bidir);
+    r.aff_pu.upload(wl.aff_pu);
+    r.aff_jobs.upload(wl.aff_jobs);
+    r.n_basic = (int)wl.mc_basic.size();
+    r.n_bidir = (int)wl.mc_bidir.size();
+    r.n_aff = (int)wl.aff_jobs.size();
+    r.n_dmvr = wl.n_dmvr;
     r.dmvr.ensure(2 * (size_t)r.n_dmvr + 2);
     double b = 0;
-    for (const McJob &j : ctx->wl.mc_basic) b += mc_bytes(j);
+    for (const McJob &j : wl.mc_basic) b += mc_bytes(j);
     r.alg_bytes[K_MC] = b;
     b = 0;
-    for (const McJob &j : ctx->wl.mc_bidir) b += mc_bytes(j);
+    for (const McJob &j : wl.mc_bidir) b += mc_bytes(j);
     r.alg_bytes[K_MC_BIDIR] = b;
     b = 0;
-    for (const AffJob &j : ctx->wl.aff_jobs) {
-      const AffPu &U = ctx->wl.aff_pu[j.pu];
+    for (const AffJob &j : wl.aff_jobs) {
+      const AffPu &U = wl.aff_pu[j.pu];
       const int lists = U.l[0].present + U.l[1].present;
       const double nsb = (j.w / 4.0) * (j.h / 4.0);
       b += 2.0 * (lists * nsb * (81 + 2 * 0.25 * 49) + 1.5 * j.w * j.h);   // 6-tap (4+5)^2 luma, 4-tap chroma
@@ -319,14 +385,12 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     r.alg_bytes[K_MC_AFFINE] = b;
   }
   if (pp.lmcs_enabled) {
-    if (sp.bit_depth != 10) throw VvcrError(VVCR_E_UNSUPPORTED, "LMCS tables are captured for 10-bit luma");
     std::vector<int16_t> lut(pp.lmcs_fwd, pp.lmcs_fwd + 1024);
     lut.insert(lut.end(), pp.lmcs_inv, pp.lmcs_inv + 1024);
     r.lmcs_lut.upload(lut);
   }
   if (mask & VVCR_STAGE_INTRA) {
-    plan_intra(sp, pp, ctx->desc, ctx->intra);
-    IntraPlan &ip = ctx->intra;
+    const IntraPlan &ip = bp.intra;
     r.tiles.upload(ip.inter_tiles);
     r.ijobs.upload(ip.jobs);
     r.idep_start.upload(ip.dep_start);
@@ -351,9 +415,8 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
     r.alg_bytes[K_INTRA] = b;
   }
   if (mask & VVCR_STAGE_DBK) {
-    plan_deblocking(sp, pp, ctx->desc, ctx->dbk);
     std::vector<DbkSeg> all;
-    const std::vector<DbkSeg> *parts[4] = {&ctx->dbk.luma[0], &ctx->dbk.chroma[0], &ctx->dbk.luma[1], &ctx->dbk.chroma[1]};
+    const std::vector<DbkSeg> *parts[4] = {&bp.dbk.luma[0], &bp.dbk.chroma[0], &bp.dbk.luma[1], &bp.dbk.chroma[1]};
     for (int k = 0; k < 4; k++) {
       r.dbk_counts[k] = (int)parts[k]->size();
       all.insert(all.end(), parts[k]->begin(), parts[k]->end());
@@ -363,23 +426,19 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, uint32_t mask) {
   }
   const bool saoOn = pp.sao_luma || pp.sao_chroma;
   const bool alfOn = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
-  if ((mask & VVCR_STAGE_SAO) && saoOn && !ctx->have_sao)
-    throw VvcrError(VVCR_E_STATE, "SAO is enabled for the picture but no SAO parameters were set");
-  if ((mask & VVCR_STAGE_ALF) && alfOn && !ctx->have_alf)
-    throw VvcrError(VVCR_E_STATE, "ALF is enabled for the picture but no ALF parameters were set");
   r.have_sao = (mask & VVCR_STAGE_SAO) && saoOn;
   r.have_alf = (mask & VVCR_STAGE_ALF) && alfOn;
   if (r.have_sao) {
-    r.sao.upload(ctx->h_sao);
+    r.sao.upload(bp.h_sao);
     r.alg_bytes[K_SAO] = pix * 2 * 2;
   }
   if (r.have_alf) {
-    r.alf_luma_coef.upload(ctx->h_alf_luma_coef);
-    r.alf_luma_clip.upload(ctx->h_alf_luma_clip);
-    r.alf_chroma.upload(ctx->h_alf_chroma);
-    r.alf_cc.upload(ctx->h_alf_cc);
-    r.alf_ctb.upload(ctx->h_alf_ctb);
-    r.alf_set.upload(ctx->h_alf_set);
+    r.alf_luma_coef.upload(bp.h_alf_luma_coef);
+    r.alf_luma_clip.upload(bp.h_alf_luma_clip);
+    r.alf_chroma.upload(bp.h_alf_chroma);
+    r.alf_cc.upload(bp.h_alf_cc);
+    r.alf_ctb.upload(bp.h_alf_ctb);
+    r.alf_set.upload(bp.h_alf_set);
     r.alg_bytes[K_ALF] = pix * 2 * 2;
   }
 }
@@ -415,9 +474,10 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   ln.tail_seq = ++ctx->seq;
   // dependencies on pictures of other lanes (same-lane work is ordered by the stream anyway)
   for (int rs : refs)
-    if (ctx->slot_w[rs]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[rs], 0));
-  if (ctx->slot_w[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[pp.slot], 0));
-  for (hipEvent_t e : ctx->slot_r[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, e, 0));
+    if (ctx->slot_w_set[rs]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[rs], 0));
+  if (ctx->slot_w_set[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[pp.slot], 0));
+  for (int l = 0; l < ctx->nlane; l++)
+    if (l != L && (ctx->slot_r_set[pp.slot] >> l & 1)) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_r[pp.slot][l], 0));
   VVCR_CHECK_HIP(hipEventRecord(r.start, s));
   if (mask & VVCR_STAGE_RESID) {
     KernelTimer t(r, K_RESID, s, ctx->timing);
@@ -523,14 +583,15 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     launch_planes3(cp, s);
   }
   VVCR_CHECK_HIP(hipEventRecord(r.done, s));
-  hipEvent_t e = ctx->ev_ring[ctx->ev_next];
-  ctx->ev_next = (ctx->ev_next + 1) % NEV;
-  VVCR_CHECK_HIP(hipEventRecord(e, s));
-  ctx->slot_w[pp.slot] = e;
+  VVCR_CHECK_HIP(hipEventRecord(ctx->slot_w[pp.slot], s));
+  ctx->slot_w_set[pp.slot] = 1;
   ctx->slot_seq[pp.slot] = ln.tail_seq;
-  ctx->slot_r[pp.slot].clear();
+  ctx->slot_r_set[pp.slot] = 0;
   for (int rs : refs)
-    if (rs != pp.slot) ctx->slot_r[rs].push_back(e);
+    if (rs != pp.slot) {
+      VVCR_CHECK_HIP(hipEventRecord(ctx->slot_r[rs][L], s));
+      ctx->slot_r_set[rs] |= 1u << L;
+    }
   r.launched = true;
   ctx->last = &r;
 }
@@ -554,7 +615,6 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     if (const char *e = getenv("VVCR_INTRA_LANES")) ctx->nintra = std::max(1, std::min(ctx->nlane - 1, atoi(e)));
     for (int l = 0; l < ctx->nlane; l++) VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->lanes[l].s, hipStreamNonBlocking));
     ctx->stream = ctx->lanes[0].s;
-    for (auto &e : ctx->ev_ring) VVCR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const int W = sp->width, H = sp->height;
     ctx->dpb.resize(sp->dpb_slots);
     for (auto &s : ctx->dpb) {
@@ -563,8 +623,14 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       s[2] = alloc_plane(W / 2, H / 2);
     }
     ctx->slot_w.assign(sp->dpb_slots, nullptr);
+    ctx->slot_w_set.assign(sp->dpb_slots, 0);
     ctx->slot_r.assign(sp->dpb_slots, {});
+    ctx->slot_r_set.assign(sp->dpb_slots, 0);
     ctx->slot_seq.assign(sp->dpb_slots, 0);
+    for (int k = 0; k < sp->dpb_slots; k++) {
+      VVCR_CHECK_HIP(hipEventCreateWithFlags(&ctx->slot_w[k], hipEventDisableTiming));
+      for (int l = 0; l < MAXLANE; l++) VVCR_CHECK_HIP(hipEventCreateWithFlags(&ctx->slot_r[k][l], hipEventDisableTiming));
+    }
     for (int l = 0; l < ctx->nlane; l++)
       for (int c = 0; c < 3; c++) {
         Lane &ln = ctx->lanes[l];
@@ -598,7 +664,9 @@ int vvcr_destroy(vvcr_ctx *ctx) {
       Lane &ln = ctx->lanes[l];
       (void)hipFree(ln.pred[c].p); (void)hipFree(ln.resi[c].p); (void)hipFree(ln.tmp[c].p);
     }
-  for (auto &e : ctx->ev_ring) if (e) (void)hipEventDestroy(e);
+  for (auto &e : ctx->slot_w) if (e) (void)hipEventDestroy(e);
+  for (auto &a : ctx->slot_r)
+    for (auto &e : a) if (e) (void)hipEventDestroy(e);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   for (int l = 0; l < ctx->nlane; l++) (void)hipStreamDestroy(ctx->lanes[l].s);
   delete ctx;
@@ -609,18 +677,90 @@ const char *vvcr_last_error(vvcr_ctx *ctx) { return ctx ? ctx->err.c_str() : g_c
 
 void *vvcr_stream(vvcr_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
+// ---- picture builder: shared by the context's current picture and the host-only vvcr_picture_* API
+static void pic_begin(vvcr_picture &b, const vvcr_seq_params &sp, const vvcr_pic_params &pp) {
+  if (pp.slot < 0 || pp.slot >= sp.dpb_slots) throw VvcrError(VVCR_E_ARG, "picture slot out of range");
+  for (int l = 0; l < 2; l++) {
+    if (pp.num_ref[l] < 0 || pp.num_ref[l] > VVCR_MAX_REF) throw VvcrError(VVCR_E_ARG, "bad num_ref");
+    for (int i = 0; i < pp.num_ref[l]; i++)
+      if (pp.ref_slot[l][i] < 0 || pp.ref_slot[l][i] >= sp.dpb_slots) throw VvcrError(VVCR_E_ARG, "ref slot out of range");
+  }
+  b.sp = sp;
+  b.pp = pp;
+  b.desc.clear();
+  b.submitted = false;
+  b.have_sao = b.have_alf = false;   // loop-filter parameters are per picture
+  b.planned = false;
+  b.mask = 0;
+}
+
+static void pic_submit(vvcr_picture &b, const vvcr_cu *cu, int32_t ncu, const vvcr_pu *pu, int32_t npu, const vvcr_tu *tu,
+                       int32_t ntu, const int32_t *coef, int64_t ncoef, const vvcr_motion *motion, const vvcr_geo *geo,
+                       int32_t ngeo) {
+  if (ncu < 0 || npu < 0 || ntu < 0 || ncoef < 0 || ngeo < 0 || (ncu && !cu) || (npu && !pu) || (ntu && !tu) ||
+      (ncoef && !coef) || (ngeo && !geo))
+    throw VvcrError(VVCR_E_ARG, "bad descriptor array");
+  auto &d = b.desc;
+  d.cu.assign(cu, cu + ncu);
+  d.pu.assign(pu, pu + npu);
+  d.tu.assign(tu, tu + ntu);
+  d.coef.assign(coef, coef + ncoef);
+  const size_t nm = (size_t)(b.sp.width / 4) * (b.sp.height / 4);
+  if (motion) d.motion.assign(motion, motion + nm); else d.motion.clear();
+  d.geo.assign(geo, geo + ngeo);
+  b.planned = false;
+  validate_descriptors(b.sp, b.pp, d);
+  b.submitted = true;
+}
+
+static void pic_set_lf(vvcr_picture &b, const vvcr_sao *sao, const vvcr_alf *alf) {
+  const int n = n_ctb(b.sp);
+  b.planned = false;
+  b.have_sao = sao != nullptr;
+  if (sao) b.h_sao.assign((const int32_t *)sao, (const int32_t *)sao + (size_t)n * 3 * 35);
+  b.have_alf = false;
+  if (alf) {
+    if (alf->num_luma_sets < 16 || alf->num_luma_sets > 24) throw VvcrError(VVCR_E_ARG, "bad ALF luma set count");
+    const size_t L = (size_t)alf->num_luma_sets * 25 * 13;
+    b.h_alf_luma_coef.assign(alf->luma_coef, alf->luma_coef + L);
+    b.h_alf_luma_clip.assign(alf->luma_clip, alf->luma_clip + L);
+    b.h_alf_chroma.assign(alf->chroma_coef, alf->chroma_coef + 56);
+    b.h_alf_chroma.insert(b.h_alf_chroma.end(), alf->chroma_clip, alf->chroma_clip + 56);
+    b.h_alf_cc.assign(alf->cc_coef, alf->cc_coef + 64);
+    auto &ctb = b.h_alf_ctb;
+    ctb.assign(alf->ctb_en, alf->ctb_en + 3 * n);
+    ctb.insert(ctb.end(), alf->ctb_alt, alf->ctb_alt + 3 * n);
+    ctb.insert(ctb.end(), alf->cc_ctl, alf->cc_ctl + 2 * n);
+    for (int i = 0; i < 3 * n; i++) if (ctb[3 * n + i] > 7) throw VvcrError(VVCR_E_ARG, "bad ALF chroma alternative");
+    for (int i = 0; i < 2 * n; i++) if (ctb[6 * n + i] > 4) throw VvcrError(VVCR_E_ARG, "bad CC-ALF filter index");
+    b.h_alf_set.assign(alf->ctb_filter_set, alf->ctb_filter_set + n);
+    for (int v : b.h_alf_set) if (v < 0 || v >= alf->num_luma_sets) throw VvcrError(VVCR_E_ARG, "bad ALF filter set index");
+    b.have_alf = true;
+  }
+}
+
+// a free prepared-picture handle (> 0) holding a fresh record
+static int32_t new_prepared(vvcr_ctx *ctx) {
+  std::lock_guard<std::mutex> g(ctx->prepared_mu);
+  int h = -1;
+  for (size_t i = 1; i < ctx->prepared.size(); i++)
+    if (!ctx->prepared[i]) { h = (int)i; break; }
+  if (h < 0) { h = (int)ctx->prepared.size(); ctx->prepared.emplace_back(); }
+  ctx->prepared[h].reset(new Prepared());
+  return h;
+}
+
+static Prepared &get_prepared(vvcr_ctx *ctx, int32_t h) {
+  std::lock_guard<std::mutex> g(ctx->prepared_mu);
+  if (h <= 0 || h >= (int)ctx->prepared.size() || !ctx->prepared[h]) throw VvcrError(VVCR_E_ARG, "bad prepared-picture handle");
+  return *ctx->prepared[h];
+}
+
 int vvcr_begin_picture(vvcr_ctx *ctx, const vvcr_pic_params *pp) {
   if (!ctx || !pp) return VVCR_E_ARG;
   API_BEGIN
-  if (pp->slot < 0 || pp->slot >= (int)ctx->dpb.size()) throw VvcrError(VVCR_E_ARG, "picture slot out of range");
-  for (int l = 0; l < 2; l++) {
-    if (pp->num_ref[l] < 0 || pp->num_ref[l] > VVCR_MAX_REF) throw VvcrError(VVCR_E_ARG, "bad num_ref");
-    for (int i = 0; i < pp->num_ref[l]; i++)
-      if (pp->ref_slot[l][i] < 0 || pp->ref_slot[l][i] >= (int)ctx->dpb.size()) throw VvcrError(VVCR_E_ARG, "ref slot out of range");
-  }
-  ctx->pp = *pp;
-  ctx->desc.clear();
-  ctx->have_sao = ctx->have_alf = false;   // loop-filter parameters are per picture
+  vvcr_seq_params sp = ctx->sp;
+  pic_begin(ctx->cur, sp, *pp);
   ctx->in_picture = true;
   return VVCR_OK;
   API_END
@@ -630,18 +770,10 @@ int vvcr_submit(vvcr_ctx *ctx, const vvcr_cu *cu, int32_t ncu, const vvcr_pu *pu
                 int32_t ntu, const int32_t *coef, int64_t ncoef, const vvcr_motion *motion, const vvcr_geo *geo,
                 int32_t ngeo, const int32_t *dmvr_delta_unused, int32_t nd) {
   (void)dmvr_delta_unused; (void)nd;
-  if (!ctx || ncu < 0 || npu < 0 || ntu < 0 || ncoef < 0 || ngeo < 0) return VVCR_E_ARG;
+  if (!ctx) return VVCR_E_ARG;
   API_BEGIN
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_submit outside begin/end picture");
-  auto &d = ctx->desc;
-  d.cu.assign(cu, cu + ncu);
-  d.pu.assign(pu, pu + npu);
-  d.tu.assign(tu, tu + ntu);
-  d.coef.assign(coef, coef + ncoef);
-  const size_t nm = (size_t)(ctx->sp.width / 4) * (ctx->sp.height / 4);
-  if (motion) d.motion.assign(motion, motion + nm); else d.motion.clear();
-  d.geo.assign(geo, geo + ngeo);
-  validate_descriptors(ctx->sp, ctx->pp, d);
+  pic_submit(ctx->cur, cu, ncu, pu, npu, tu, ntu, coef, ncoef, motion, geo, ngeo);
   return VVCR_OK;
   API_END
 }
@@ -650,27 +782,7 @@ int vvcr_set_loop_filter_params(vvcr_ctx *ctx, const vvcr_sao *sao, const vvcr_a
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_set_loop_filter_params outside begin/end picture");
-  const int n = n_ctb(ctx->sp);
-  ctx->have_sao = sao != nullptr;
-  if (sao) ctx->h_sao.assign((const int32_t *)sao, (const int32_t *)sao + (size_t)n * 3 * 35);
-  ctx->have_alf = alf != nullptr;
-  if (alf) {
-    if (alf->num_luma_sets < 16 || alf->num_luma_sets > 24) throw VvcrError(VVCR_E_ARG, "bad ALF luma set count");
-    const size_t L = (size_t)alf->num_luma_sets * 25 * 13;
-    ctx->h_alf_luma_coef.assign(alf->luma_coef, alf->luma_coef + L);
-    ctx->h_alf_luma_clip.assign(alf->luma_clip, alf->luma_clip + L);
-    ctx->h_alf_chroma.assign(alf->chroma_coef, alf->chroma_coef + 56);
-    ctx->h_alf_chroma.insert(ctx->h_alf_chroma.end(), alf->chroma_clip, alf->chroma_clip + 56);
-    ctx->h_alf_cc.assign(alf->cc_coef, alf->cc_coef + 64);
-    auto &ctb = ctx->h_alf_ctb;
-    ctb.assign(alf->ctb_en, alf->ctb_en + 3 * n);
-    ctb.insert(ctb.end(), alf->ctb_alt, alf->ctb_alt + 3 * n);
-    ctb.insert(ctb.end(), alf->cc_ctl, alf->cc_ctl + 2 * n);
-    for (int i = 0; i < 3 * n; i++) if (ctb[3 * n + i] > 7) throw VvcrError(VVCR_E_ARG, "bad ALF chroma alternative");
-    for (int i = 0; i < 2 * n; i++) if (ctb[6 * n + i] > 4) throw VvcrError(VVCR_E_ARG, "bad CC-ALF filter index");
-    ctx->h_alf_set.assign(alf->ctb_filter_set, alf->ctb_filter_set + n);
-    for (int v : ctx->h_alf_set) if (v < 0 || v >= alf->num_luma_sets) throw VvcrError(VVCR_E_ARG, "bad ALF filter set index");
-  }
+  pic_set_lf(ctx->cur, sao, alf);
   return VVCR_OK;
   API_END
 }
@@ -680,7 +792,8 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
   API_BEGIN
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_end_picture without begin");
   Prepared &r = *ctx->prepared[0];
-  prepare(ctx, r, mask);
+  plan_picture(ctx->cur, mask);
+  prepare(ctx, r, ctx->cur);
   launch(ctx, r);
   ctx->in_picture = false;
   return VVCR_OK;
@@ -693,21 +806,35 @@ int vvcr_prepare_picture(vvcr_ctx *ctx, uint32_t mask, int32_t *handle) {
   if (!ctx || !handle) return VVCR_E_ARG;
   API_BEGIN
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_prepare_picture without begin");
-  int h = -1;
-  for (size_t i = 1; i < ctx->prepared.size(); i++)
-    if (!ctx->prepared[i]) { h = (int)i; break; }
-  if (h < 0) { h = (int)ctx->prepared.size(); ctx->prepared.emplace_back(); }
-  ctx->prepared[h].reset(new Prepared());
-  prepare(ctx, *ctx->prepared[h], mask);
+  plan_picture(ctx->cur, mask);
+  const int32_t h = new_prepared(ctx);
+  try {
+    prepare(ctx, get_prepared(ctx, h), ctx->cur);
+  } catch (...) {
+    std::lock_guard<std::mutex> g(ctx->prepared_mu);
+    ctx->prepared[h].reset();
+    throw;
+  }
   ctx->in_picture = false;
   *handle = h;
   return VVCR_OK;
   API_END
 }
 
-static Prepared &get_prepared(vvcr_ctx *ctx, int32_t h) {
-  if (h <= 0 || h >= (int)ctx->prepared.size() || !ctx->prepared[h]) throw VvcrError(VVCR_E_ARG, "bad prepared-picture handle");
-  return *ctx->prepared[h];
+int vvcr_prepare_planned(vvcr_ctx *ctx, const vvcr_picture *pic, int32_t *handle) {
+  if (!ctx || !pic || !handle) return VVCR_E_ARG;
+  API_BEGIN
+  const int32_t h = new_prepared(ctx);
+  try {
+    prepare(ctx, get_prepared(ctx, h), *pic);
+  } catch (...) {
+    std::lock_guard<std::mutex> g(ctx->prepared_mu);
+    ctx->prepared[h].reset();
+    throw;
+  }
+  *handle = h;
+  return VVCR_OK;
+  API_END
 }
 
 int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle) {
@@ -724,9 +851,80 @@ int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle) {
   Prepared &r = get_prepared(ctx, handle);
   r.wait();
   if (ctx->last == &r) ctx->last = nullptr;
+  std::lock_guard<std::mutex> g(ctx->prepared_mu);
   ctx->prepared[handle].reset();
   return VVCR_OK;
   API_END
+}
+
+// ---- host-only picture builder (no device): see include/vvcr.h
+#define PIC_BEGIN try {
+#define PIC_END                                                  \
+  }                                                              \
+  catch (const VvcrError &e) { pic->err = e.msg; return e.code; } \
+  catch (const std::exception &e) { pic->err = e.what(); return VVCR_E_STATE; }
+
+int vvcr_picture_create(const vvcr_seq_params *sp, const vvcr_pic_params *pp, vvcr_picture **out) {
+  if (!sp || !pp || !out) return VVCR_E_ARG;
+  *out = nullptr;
+  if (sp->chroma_format != 1 || sp->width <= 0 || sp->height <= 0 || sp->width % 8 || sp->height % 8 ||
+      sp->ctu_log2 < 5 || sp->ctu_log2 > 7 || sp->dpb_slots <= 0 || sp->dpb_slots > 32) {
+    g_create_error = "unsupported sequence parameters";
+    return VVCR_E_UNSUPPORTED;
+  }
+  auto pic = std::make_unique<vvcr_picture>();
+  try {
+    pic_begin(*pic, *sp, *pp);
+  } catch (const VvcrError &e) {
+    g_create_error = e.msg;
+    return e.code;
+  }
+  *out = pic.release();
+  return VVCR_OK;
+}
+
+int vvcr_picture_submit(vvcr_picture *pic, const vvcr_cu *cu, int32_t ncu, const vvcr_pu *pu, int32_t npu, const vvcr_tu *tu,
+                        int32_t ntu, const int32_t *coef, int64_t ncoef, const vvcr_motion *motion, const vvcr_geo *geo,
+                        int32_t ngeo) {
+  if (!pic) return VVCR_E_ARG;
+  PIC_BEGIN
+  pic_submit(*pic, cu, ncu, pu, npu, tu, ntu, coef, ncoef, motion, geo, ngeo);
+  return VVCR_OK;
+  PIC_END
+}
+
+int vvcr_picture_set_loop_filter_params(vvcr_picture *pic, const vvcr_sao *sao, const vvcr_alf *alf) {
+  if (!pic) return VVCR_E_ARG;
+  PIC_BEGIN
+  pic_set_lf(*pic, sao, alf);
+  return VVCR_OK;
+  PIC_END
+}
+
+int vvcr_picture_plan(vvcr_picture *pic, uint32_t stage_mask) {
+  if (!pic) return VVCR_E_ARG;
+  PIC_BEGIN
+  plan_picture(*pic, stage_mask);
+  return VVCR_OK;
+  PIC_END
+}
+
+int vvcr_picture_work_counts(const vvcr_picture *pic, int64_t *counts, int32_t n) {
+  if (!pic || (!counts && n)) return VVCR_E_ARG;
+  if (!pic->planned) return VVCR_E_STATE;
+  const int64_t v[8] = {(int64_t)pic->wl.tb.size(), (int64_t)pic->wl.mc_basic.size(), (int64_t)pic->wl.mc_bidir.size(),
+                        (int64_t)pic->wl.aff_jobs.size(), (int64_t)pic->intra.inter_tiles.size(), (int64_t)pic->intra.jobs.size(),
+                        (int64_t)pic->dbk.total(), (int64_t)pic->wl.n_dmvr};
+  for (int k = 0; k < n && k < 8; k++) counts[k] = v[k];
+  return 8;
+}
+
+const char *vvcr_picture_last_error(const vvcr_picture *pic) { return pic ? pic->err.c_str() : g_create_error.c_str(); }
+
+int vvcr_picture_destroy(vvcr_picture *pic) {
+  if (!pic) return VVCR_E_ARG;
+  delete pic;
+  return VVCR_OK;
 }
 
 int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int32_t n) {

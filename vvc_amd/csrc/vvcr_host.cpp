@@ -70,8 +70,14 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
   const int ncu = (int)d.cu.size(), npu = (int)d.pu.size(), ntu = (int)d.tu.size();
   for (int i = 0; i < ncu; i++) {
     const vvcr_cu &c = d.cu[i];
-    if (c.yvalid && (c.x < 0 || c.y < 0 || c.w <= 0 || c.h <= 0 || c.w > 128 || c.h > 128)) fail("CU " + std::to_string(i) + " has a bad luma area");
-    if (c.cvalid && (c.cx < 0 || c.cy < 0 || c.cw <= 0 || c.ch <= 0 || c.cw > 64 || c.ch > 64)) fail("CU " + std::to_string(i) + " has a bad chroma area");
+    // CUs lie inside the picture: VVC splits implicitly at the picture boundary (CU::divideSplit /
+    // the implicit QT/BT of UnitPartitioner), and the sizes are multiples of 8 (vvcr_create)
+    if (c.yvalid && (c.x < 0 || c.y < 0 || c.w <= 0 || c.h <= 0 || c.w > 128 || c.h > 128 || c.x + c.w > sp.width ||
+                     c.y + c.h > sp.height))
+      fail("CU " + std::to_string(i) + " has a bad luma area");
+    if (c.cvalid && (c.cx < 0 || c.cy < 0 || c.cw <= 0 || c.ch <= 0 || c.cw > 64 || c.ch > 64 || c.cx + c.cw > sp.width / 2 ||
+                     c.cy + c.ch > sp.height / 2))
+      fail("CU " + std::to_string(i) + " has a bad chroma area");
     if (!c.yvalid && !c.cvalid) fail("CU " + std::to_string(i) + " has no component");
     if (c.npu > 0 && (c.firstpu < 0 || c.firstpu + c.npu > npu)) fail("CU " + std::to_string(i) + " PU range");
     if (c.ntu > 0 && (c.firsttu < 0 || c.firsttu + c.ntu > ntu)) fail("CU " + std::to_string(i) + " TU range");
@@ -80,6 +86,8 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
     const vvcr_pu &p = d.pu[i];
     if (p.cu < 0 || p.cu >= ncu) fail("PU " + std::to_string(i) + " CU index");
     const vvcr_cu &c = d.cu[p.cu];
+    if (p.w > 0 && (p.x < 0 || p.y < 0 || p.x + p.w > sp.width || p.y + p.h > sp.height || p.w > 128 || p.h > 128))
+      fail("PU " + std::to_string(i) + " area");
     if (c.predmode == MODE_INTER) {
       if ((p.interdir & 1) && (p.ref0 < 0 || p.ref0 >= pp.num_ref[0])) fail("PU " + std::to_string(i) + " ref0");
       if ((p.interdir & 2) && (p.ref1 < 0 || p.ref1 >= pp.num_ref[1])) fail("PU " + std::to_string(i) + " ref1");
@@ -93,11 +101,28 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
       if (b[2] <= 0) continue;
       const int pw = c ? sp.width / 2 : sp.width, ph = c ? sp.height / 2 : sp.height;
       const int maxs = b[6] >= 0 ? 64 : 128;   // coded TBs are <= 64 (maxTbSize); residual-free TUs span the CU
-      if (b[0] < 0 || b[1] < 0 || b[0] + b[2] > pw + 128 || b[1] + b[3] > ph + 128 || b[2] > maxs || b[3] > maxs) fail("TU " + std::to_string(i) + " area");
+      // every block lies inside its plane: the kernels store residual / reconstruction rows unclipped
+      if (b[0] < 0 || b[1] < 0 || b[0] + b[2] > pw || b[1] + b[3] > ph || b[2] > maxs || b[3] > maxs) fail("TU " + std::to_string(i) + " area");
       if (b[6] >= 0 && (int64_t)b[6] + (int64_t)b[2] * b[3] > (int64_t)d.coef.size()) fail("TU " + std::to_string(i) + " coefficient range");
     }
   }
   if (!d.motion.empty() && d.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4)) fail("motion field size");
+  // picture partitioning: tiles with loop filtering across their edges, one or more slices with loop
+  // filtering across theirs (the deblocking / SAO / ALF planners do not stop at tile or slice edges)
+  const int ctu = 1 << sp.ctu_log2, wc = (sp.width + ctu - 1) / ctu, hc = (sp.height + ctu - 1) / ctu;
+  for (int k = 0; k < 2; k++) {
+    const int n = k ? pp.num_tile_rows : pp.num_tile_cols, lim = k ? hc : wc;
+    const int32_t *bd = k ? pp.tile_row_bd : pp.tile_col_bd;
+    if (n < 0 || n > VVCR_MAX_TILE_LINES) fail("tile count");
+    if (n > 0 && (bd[0] != 0 || bd[n] != lim)) fail("tile boundaries do not span the picture");
+    for (int t = 0; t < n; t++) if (bd[t + 1] <= bd[t]) fail("tile boundaries not increasing");
+  }
+  if ((pp.num_tile_cols > 1 || pp.num_tile_rows > 1) && !pp.lf_across_tiles)
+    throw VvcrError(VVCR_E_UNSUPPORTED, "tiles without loop filtering across tile boundaries");
+  bool multiSlice = false;
+  for (const vvcr_cu &c : d.cu) multiSlice |= c.slice != (ncu ? d.cu[0].slice : 0);
+  if (multiSlice && !pp.lf_across_slices) throw VvcrError(VVCR_E_UNSUPPORTED, "slices without loop filtering across slice boundaries");
+  if (pp.entropy_sync) throw VvcrError(VVCR_E_UNSUPPORTED, "wavefront parallel processing (entropy coding sync)");
 }
 
 void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, std::vector<TbJob> &out);
@@ -465,9 +490,15 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
         } else {
           if ((size_t)j.coef + (size_t)w * h > d.coef.size()) throw VvcrError(VVCR_E_ARG, "coefficient offset out of range");
           const int32_t *lv = d.coef.data() + j.coef;
-          for (int yy = 0; yy < h; yy++)
-            for (int xx = 0; xx < w; xx++)
-              if (lv[yy * w + xx]) { R = std::max(R, yy + 1); C = std::max(C, xx + 1); }
+          for (int yy = 0; yy < h; yy++) {
+            const int32_t *row = lv + yy * w;
+            int32_t any = 0;
+            for (int xx = 0; xx < w; xx++) any |= row[xx];   // vectorised OR: most rows are all zero
+            if (!any) continue;
+            R = yy + 1;
+            for (int xx = w - 1; xx >= C; xx--)
+              if (row[xx]) { C = xx + 1; break; }
+          }
           if (j.flags & TB_LFNST_APPLY) {
             const int r = (w >= 8 && h >= 8) ? 8 : 4;
             R = std::max(R, std::min(r, h)); C = std::max(C, std::min(r, w));

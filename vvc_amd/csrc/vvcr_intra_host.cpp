@@ -14,6 +14,9 @@
 #include <memory>
 #include <queue>
 #include <string>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 
 namespace {
 
@@ -29,10 +32,16 @@ struct Planner {
   std::vector<int32_t> prod[3];     // per unit of each component: the step (index into jobs) that reconstructs it, -1 = inter
   std::vector<int32_t> cu_map;      // luma 4x4 unit -> CU index (for CIIP neighbour tests)
   std::vector<std::pair<int32_t, IntraJob>> jobs;   // (level, job)
-  std::vector<std::vector<int32_t>> deps;           // per job: the steps it reads from (indices into jobs)
+  std::vector<int32_t> dep_off{0}, dep_flat;        // per job (CSR): the steps it reads from (indices into jobs)
   std::vector<int32_t> cur;                         // dependencies of the step being planned
   int seq = 0;
   bool cscale = false;                              // LMCS chroma residual scaling active in this picture
+  // Slice / tile of every CTU (getCURestricted: a neighbour is usable only inside the same slice and
+  // tile, CodingStructure.cpp:1519-1537, CU::isSameSliceAndTile UnitTools.cpp:170); cur_reg is the
+  // region of the CU being planned / the step being resolved.
+  std::vector<int32_t> ctu_reg;
+  int wc = 1, cur_reg = 0;
+  int region_at(int lx, int ly) const { return ctu_reg[(size_t)(ly >> sp.ctu_log2) * wc + (lx >> sp.ctu_log2)]; }
 
   Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, IntraPlan &o)
       : sp(s), pp(p), d(dd), out(o) {
@@ -51,12 +60,14 @@ struct Planner {
     x1 = std::min(x1, pw - 1); y1 = std::min(y1, ph - 1);
     int m = 0;
     if (x0 > x1 || y0 > y1) return 0;
+    const int cs = ch ? 1 : 0;
     for (int uy = y0 >> s; uy <= (y1 >> s); uy++)
       for (int ux = x0 >> s; ux <= (x1 >> s); ux++) {
         const size_t i = (size_t)uy * W4 + ux;
-        if (out.order[ch][i] < seq) {
+        if (out.order[ch][i] < seq && region_at((ux << s) << cs, (uy << s) << cs) == cur_reg) {
           m = std::max(m, level[ch][i]);
-          if (prod[comp][i] >= 0) cur.push_back(prod[comp][i]);
+          const int32_t pr = prod[comp][i];
+          if (pr >= 0 && (cur.empty() || cur.back() != pr)) cur.push_back(pr);   // runs of one producer: once
         }
       }
     return m;
@@ -83,7 +94,8 @@ struct Planner {
     std::sort(cur.begin(), cur.end());
     cur.erase(std::unique(cur.begin(), cur.end()), cur.end());
     jobs.emplace_back(lev, j);
-    deps.push_back(cur);
+    dep_flat.insert(dep_flat.end(), cur.begin(), cur.end());
+    dep_off.push_back((int32_t)dep_flat.size());
     cur.clear();
     return (int)jobs.size() - 1;
   }
@@ -107,10 +119,11 @@ struct Planner {
     if (ci < 0) throw VvcrError(VVCR_E_STATE, "LMCS: no luma CU at a VPDU corner");
     const vvcr_cu &t = d.cu[ci];
     j.vx = (int16_t)t.x; j.vy = (int16_t)t.y;
-    j.vnb = CS_SCALE | (t.x > 0 ? CS_LEFT : 0) | (t.y > 0 ? CS_ABOVE : 0);   // one slice, one tile
+    const bool left = t.x > 0 && region_at(t.x - 1, t.y) == cur_reg, above = t.y > 0 && region_at(t.x, t.y - 1) == cur_reg;
+    j.vnb = CS_SCALE | (left ? CS_LEFT : 0) | (above ? CS_ABOVE : 0);
     int lev = 0;
-    if (t.x > 0) lev = std::max(lev, max_level(0, 0, t.x - 1, t.y, t.x - 1, t.y + n64 - 1));
-    if (t.y > 0) lev = std::max(lev, max_level(0, 0, t.x, t.y - 1, t.x + n64 - 1, t.y - 1));
+    if (left) lev = std::max(lev, max_level(0, 0, t.x - 1, t.y, t.x - 1, t.y + n64 - 1));
+    if (above) lev = std::max(lev, max_level(0, 0, t.x, t.y - 1, t.x + n64 - 1, t.y - 1));
     return lev;
   }
 
@@ -121,7 +134,7 @@ struct Planner {
     if (p.ciip) {
       // CIIP: planar from the neighbours, blended with the inter prediction (geneWeightedPred :681)
       auto intraAt = [&](int x, int y) {
-        if (x < 0 || y < 0 || x >= sp.width || y >= sp.height) return false;
+        if (x < 0 || y < 0 || x >= sp.width || y >= sp.height || region_at(x, y) != cur_reg) return false;
         const int n = cu_map[(size_t)(y >> 2) * W4 + (x >> 2)];
         return n >= 0 && n <= ci && d.cu[n].predmode == MODE_INTRA;
       };
@@ -238,9 +251,14 @@ struct Planner {
         else j.mode = (uint8_t)p.fidir_c;
         if (dual) j.flags |= IJ_DUAL;
         int lev = ref_level(1, comp, j.x, j.y, 2 * j.w, 2 * j.h, 0);
-        if (!c.bdpcmc && p.fidir_c >= 67) {   // CCLM: co-located luma and its template rows / columns
+        if (!c.bdpcmc && p.fidir_c >= 67) {
+          // CCLM (xGetLumaRecPixels IntraPrediction.cpp:1316-1650): the co-located luma block, the luma
+          // rows above it (with the above-right extension, up to twice the width) and the columns left of
+          // it (with the below-left extension); the strips are taken 4 samples deep
           const int lx = 2 * j.x, ly = 2 * j.y;
-          lev = std::max(lev, max_level(0, 0, lx - 4, ly - 4, lx + 4 * j.w - 1, ly + 4 * j.h - 1));
+          lev = std::max(lev, max_level(0, 0, lx, ly, lx + 2 * j.w - 1, ly + 2 * j.h - 1));
+          lev = std::max(lev, max_level(0, 0, lx - 4, ly - 4, lx + 4 * j.w - 1, ly - 1));
+          lev = std::max(lev, max_level(0, 0, lx - 4, ly, lx - 1, ly + 4 * j.h - 1));
         }
         if (cscale && j.w * j.h > 4) lev = std::max(lev, set_cscale(j, 2 * j.x, 2 * j.y));
         lev += 1;
@@ -255,8 +273,8 @@ struct Planner {
   bool av(int ch, int x, int y, int sq) const {
     const int pw = ch ? sp.width / 2 : sp.width, ph = ch ? sp.height / 2 : sp.height;
     if (x < 0 || y < 0 || x >= pw || y >= ph) return false;
-    const int s = ch ? 1 : 2;
-    return out.order[ch][(size_t)(y >> s) * W4 + (x >> s)] < sq;
+    const int s = ch ? 1 : 2, cs = ch ? 1 : 0;
+    return out.order[ch][(size_t)(y >> s) * W4 + (x >> s)] < sq && region_at(x << cs, y << cs) == cur_reg;
   }
   // xFillReferenceSamples unit scan (IntraPrediction.cpp:913-986, isAboveAvailable etc. :1208-1310):
   // returns the 65-bit availability mask in (lo, hi)
@@ -304,8 +322,9 @@ struct Planner {
     if (ar > 31 || bl > 31) throw VvcrError(VVCR_E_STATE, "intra plan: CCLM neighbourhood too large");
     return (above ? 1u : 0u) | (left ? 2u : 0u) | (uint32_t)ar << 2 | (uint32_t)bl << 7;
   }
-  void resolve_availability(IntraJob &j) const {
+  void resolve_availability(IntraJob &j) {
     const int comp = j.comp, ch = comp ? 1 : 0;
+    cur_reg = region_at(j.cx << ch, j.cy << ch);
     const bool isp = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0, ver = (j.flags & IJ_ISP_VER) != 0;
     uint64_t lo;
     uint32_t hi;
@@ -349,6 +368,14 @@ struct Planner {
   }
 
   void run() {
+    static const bool prof = getenv("VVCR_PLAN_PROF") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+#define PROF_MARK(n)                                                                                             \
+  if (prof) {                                                                                                    \
+    auto t1 = std::chrono::steady_clock::now();                                                                  \
+    fprintf(stderr, "  intra plan %-6s %.2f ms\n", n, std::chrono::duration<double, std::milli>(t1 - t0).count()); \
+    t0 = t1;                                                                                                     \
+  }
     const size_t nu = (size_t)W4 * H4;
     for (int k = 0; k < 2; k++) { out.order[k].assign(nu, 1 << 30); level[k].assign(nu, 0); }
     for (int k = 0; k < 3; k++) prod[k].assign(nu, -1);
@@ -359,8 +386,28 @@ struct Planner {
       for (int uy = c.y >> 2; uy < (c.y + c.h) >> 2; uy++)
         for (int ux = c.x >> 2; ux < (c.x + c.w) >> 2; ux++) cu_map[(size_t)uy * W4 + ux] = (int)i;
     }
-    const int wc = (sp.width + ctu - 1) / ctu, hc = (sp.height + ctu - 1) / ctu;
+    wc = (sp.width + ctu - 1) / ctu;
+    const int hc = (sp.height + ctu - 1) / ctu;
     const int ncu = (int)d.cu.size();
+    {
+      // tile of every CTU from the column / row boundaries, slice from the CUs it holds
+      std::vector<int32_t> tcol(wc, 0), trow(hc, 0);
+      const int ntc = std::max(1, pp.num_tile_cols), ntr = std::max(1, pp.num_tile_rows);
+      if (pp.num_tile_cols > 0)
+        for (int t = 0; t < ntc; t++)
+          for (int x = pp.tile_col_bd[t]; x < pp.tile_col_bd[t + 1] && x < wc; x++) tcol[x] = t;
+      if (pp.num_tile_rows > 0)
+        for (int t = 0; t < ntr; t++)
+          for (int y = pp.tile_row_bd[t]; y < pp.tile_row_bd[t + 1] && y < hc; y++) trow[y] = t;
+      ctu_reg.assign((size_t)wc * hc, 0);
+      for (int y = 0; y < hc; y++)
+        for (int x = 0; x < wc; x++) ctu_reg[(size_t)y * wc + x] = (trow[y] * ntc + tcol[x]) << 16;
+      for (const vvcr_cu &c : d.cu) {
+        const int x = c.yvalid ? c.x : 2 * c.cx, y = c.yvalid ? c.y : 2 * c.cy;
+        int32_t &r = ctu_reg[(size_t)(y >> sp.ctu_log2) * wc + (x >> sp.ctu_log2)];
+        r = (r & ~0xffff) | (c.slice & 0xffff);
+      }
+    }
     std::vector<int> start((size_t)wc * hc + 1, 0), order(ncu), ctu_of(ncu);
     for (int i = 0; i < ncu; i++) {
       const vvcr_cu &c = d.cu[i];
@@ -379,6 +426,7 @@ struct Planner {
           const int i = order[jx];
           const vvcr_cu &c = d.cu[i];
           if (pp.dual_tree && c.chtype != pass) continue;
+          cur_reg = ctu_reg[k];
           if (c.predmode == MODE_INTER) {
             inter_cu(i);
           } else if (c.predmode == MODE_INTRA) {
@@ -388,6 +436,7 @@ struct Planner {
             throw VvcrError(VVCR_E_UNSUPPORTED, "IBC / palette CUs are not supported");
           }
         }
+    PROF_MARK("jobs");
     // Steps grouped by CTU (raster order), inside a CTU by level: a topological order of the dependency
     // graph (every dependency is in the same CTU at a lower level, or in an earlier CTU — the left /
     // above neighbours). k_intra runs one CTU per workgroup with the CTU's samples in LDS; a dependency
@@ -400,92 +449,103 @@ struct Planner {
       const int s = j.comp ? 1 : 0;
       const int lx = j.cx << s, ly = j.cy << s;   // CU position in luma samples (a CU never crosses a CTU)
       ctu_of_job[i] = (ly >> sp.ctu_log2) * wc + (lx >> sp.ctu_log2);
+      if (i && ctu_of_job[i] < ctu_of_job[i - 1]) throw VvcrError(VVCR_E_STATE, "intra plan: steps not created in CTU order");
     }
+    // the steps of one CTU are contiguous in creation order: blocks [cb[k], cb[k+1])
+    std::vector<int32_t> cb;
+    for (int i = 0; i < nj; i++)
+      if (i == 0 || ctu_of_job[i] != ctu_of_job[i - 1]) cb.push_back(i);
+    cb.push_back(nj);
+    auto D = [&](int i) { return std::make_pair(dep_flat.data() + dep_off[i], dep_flat.data() + dep_off[i + 1]); };
     // Take order inside a CTU: a topological order that prefers the steps with the longest chain of
     // dependent work behind them (list scheduling by bottom level). The kernel's waves take steps in this
     // order, so the critical chain is started as early as its dependencies allow. Step costs are rough
     // estimates in microseconds (measured per step kind on MI355X, tools/iprof_ctu.py).
-    std::vector<double> bl(nj, 0.0);
-    {
-      std::vector<std::vector<int32_t>> succ(nj);
-      for (int i = 0; i < nj; i++)
-        for (int32_t dd : deps[i]) succ[dd].push_back(i);
-      for (int i = nj - 1; i >= 0; i--) {   // creation order is topological (dependencies are earlier)
-        const IntraJob &j = jobs[i].second;
-        const bool isp = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0;
-        double c = 3.0 + 0.002 * j.w * j.h * (isp ? j.isp_k : 1) + (isp ? 1.6 * (j.isp_k - 1) : 0.0) +
-                   ((j.flags & IJ_MIP) ? 2.5 : 0.0) + ((j.comp && j.mode >= 67) ? 3.0 : 0.0);
-        double m = 0.0;
-        for (int32_t t : succ[i]) m = std::max(m, bl[t]);
-        bl[i] = c + m;
-      }
+    std::vector<double> bl(nj, 0.0), maxsucc(nj, 0.0);
+    for (int i = nj - 1; i >= 0; i--) {   // creation order is topological (dependencies are earlier)
+      const IntraJob &j = jobs[i].second;
+      const bool isp = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0;
+      const double c = 3.0 + 0.002 * j.w * j.h * (isp ? j.isp_k : 1) + (isp ? 1.6 * (j.isp_k - 1) : 0.0) +
+                       ((j.flags & IJ_MIP) ? 2.5 : 0.0) + ((j.comp && j.mode >= 67) ? 3.0 : 0.0);
+      bl[i] = c + maxsucc[i];
+      for (auto [p, e] = D(i); p != e; ++p) maxsucc[*p] = std::max(maxsucc[*p], bl[i]);
     }
+    PROF_MARK("bl");
     // Wait lists: a same-CTU dependency that another dependency of the step already reaches through
     // same-CTU dependencies is implied (that one could only finish after it: flags are raised after the
     // step's stores complete, LDS is coherent inside the CU), so the kernel need not poll it. Bitsets of
-    // same-CTU ancestors, in creation order (topological). Cross-CTU dependencies are all kept: they
-    // also decide which steps publish their samples to HBM.
-    std::vector<std::vector<int32_t>> wdeps(nj);
-    {
-      std::vector<int32_t> lidx(nj);   // index among the CTU's steps
-      {
-        std::vector<int32_t> cnt_of((size_t)wc * ((sp.height + (1 << sp.ctu_log2) - 1) >> sp.ctu_log2), 0);
-        for (int i = 0; i < nj; i++) lidx[i] = cnt_of[ctu_of_job[i]]++;
-      }
-      std::vector<std::vector<uint64_t>> anc(nj);
-      for (int i = 0; i < nj; i++) {
-        std::vector<uint64_t> &a = anc[i];
-        std::vector<uint64_t> implied;
-        for (int32_t dd : deps[i]) {
-          if (ctu_of_job[dd] != ctu_of_job[i]) continue;
-          const std::vector<uint64_t> &ad = anc[dd];
-          const size_t need = std::max(ad.size(), (size_t)(lidx[dd] >> 6) + 1);
-          if (a.size() < need) a.resize(need, 0);
-          if (implied.size() < ad.size()) implied.resize(ad.size(), 0);
-          for (size_t w = 0; w < ad.size(); w++) { a[w] |= ad[w]; implied[w] |= ad[w]; }
-          a[lidx[dd] >> 6] |= 1ull << (lidx[dd] & 63);
-        }
-        for (int32_t dd : deps[i]) {
-          if (ctu_of_job[dd] == ctu_of_job[i]) {
-            const int b = lidx[dd];
-            if ((size_t)(b >> 6) < implied.size() && (implied[b >> 6] >> (b & 63) & 1)) continue;
-          }
-          wdeps[i].push_back(dd);
-        }
-      }
-    }
+    // same-CTU ancestors per CTU block, in creation order (topological). Cross-CTU dependencies are all
+    // kept: they also decide which steps publish their samples to HBM.
+    std::vector<int32_t> wd_off(nj + 1, 0), wd_flat;
+    wd_flat.reserve(dep_flat.size());
+    // In-CTU take order (list scheduling by bottom level) in the same pass over the CTU blocks.
     std::vector<int32_t> perm;
     perm.reserve(nj);
     {
-      std::vector<int32_t> byCtu(nj);
-      for (int i = 0; i < nj; i++) byCtu[i] = i;
-      std::stable_sort(byCtu.begin(), byCtu.end(), [&](int32_t a, int32_t b) { return ctu_of_job[a] < ctu_of_job[b]; });
-      std::vector<int32_t> indeg(nj, 0);
-      std::vector<std::vector<int32_t>> succLocal(nj);
-      for (int i = 0; i < nj; i++)
-        for (int32_t dd : deps[i])
-          if (ctu_of_job[dd] == ctu_of_job[i]) { indeg[i]++; succLocal[dd].push_back(i); }
-      for (size_t a = 0; a < byCtu.size();) {
-        size_t b = a;
-        while (b < byCtu.size() && ctu_of_job[byCtu[b]] == ctu_of_job[byCtu[a]]) b++;
-        auto cmp = [&](int32_t x, int32_t y) { return bl[x] < bl[y] || (bl[x] == bl[y] && x > y); };
+      std::vector<uint64_t> anc, implied;
+      std::vector<int32_t> indeg, soff, sflat;
+      for (size_t k = 0; k + 1 < cb.size(); k++) {
+        const int b0 = cb[k], n = cb[k + 1] - b0, words = (n + 63) / 64;
+        anc.assign((size_t)n * words, 0);
+        implied.assign(words, 0);
+        for (int i = b0; i < b0 + n; i++) {
+          const int li = i - b0;
+          uint64_t *a = anc.data() + (size_t)li * words;
+          const int lw = (li >> 6) + 1;   // ancestors of step li are < li
+          std::fill(implied.begin(), implied.begin() + lw, 0);
+          for (auto [p, e] = D(i); p != e; ++p) {
+            const int dd = *p;
+            if (dd < b0) continue;
+            const int ld = dd - b0;
+            const uint64_t *ad = anc.data() + (size_t)ld * words;
+            for (int w = 0; w <= (ld >> 6); w++) { a[w] |= ad[w]; implied[w] |= ad[w]; }
+            a[ld >> 6] |= 1ull << (ld & 63);
+          }
+          for (auto [p, e] = D(i); p != e; ++p) {
+            const int dd = *p;
+            if (dd >= b0) {
+              const int ld = dd - b0;
+              if (implied[ld >> 6] >> (ld & 63) & 1) continue;
+            }
+            wd_flat.push_back(dd);
+          }
+          wd_off[i + 1] = (int32_t)wd_flat.size();
+        }
+        // successors inside the CTU (CSR over local indices) and in-degrees
+        indeg.assign(n, 0);
+        soff.assign(n + 1, 0);
+        for (int i = b0; i < b0 + n; i++)
+          for (auto [p, e] = D(i); p != e; ++p)
+            if (*p >= b0) { indeg[i - b0]++; soff[*p - b0 + 1]++; }
+        for (int q = 0; q < n; q++) soff[q + 1] += soff[q];
+        sflat.assign(soff[n], 0);
+        {
+          std::vector<int32_t> pos(soff.begin(), soff.end() - 1);
+          for (int i = b0; i < b0 + n; i++)
+            for (auto [p, e] = D(i); p != e; ++p)
+              if (*p >= b0) sflat[pos[*p - b0]++] = i - b0;
+        }
+        auto cmp = [&](int32_t x, int32_t y) { return bl[b0 + x] < bl[b0 + y] || (bl[b0 + x] == bl[b0 + y] && x > y); };
         std::priority_queue<int32_t, std::vector<int32_t>, decltype(cmp)> ready(cmp);
-        for (size_t k = a; k < b; k++) if (indeg[byCtu[k]] == 0) ready.push(byCtu[k]);
+        for (int q = 0; q < n; q++) if (indeg[q] == 0) ready.push(q);
+        int taken = 0;
         while (!ready.empty()) {
           const int32_t x = ready.top();
           ready.pop();
-          perm.push_back(x);
-          for (int32_t t : succLocal[x]) if (--indeg[t] == 0) ready.push(t);
+          perm.push_back(b0 + x);
+          taken++;
+          for (int t = soff[x]; t < soff[x + 1]; t++) if (--indeg[sflat[t]] == 0) ready.push(sflat[t]);
         }
-        a = b;
+        if (taken != n) throw VvcrError(VVCR_E_STATE, "intra plan: dependency cycle inside a CTU");
       }
-      if ((int)perm.size() != nj) throw VvcrError(VVCR_E_STATE, "intra plan: dependency cycle inside a CTU");
     }
+    PROF_MARK("wdeps");
     std::vector<int32_t> rank(nj);
     for (int i = 0; i < nj; i++) rank[perm[i]] = i;
     out.jobs.resize(nj);
     out.dep_start.assign(nj + 1, 0);
     out.deps.clear();
+    out.deps.reserve(wd_flat.size());
     out.ctu_list.clear();
     out.ctu_start.clear();
     for (int i = 0; i < nj; i++) {
@@ -504,19 +564,21 @@ struct Planner {
     for (int i = 0; i < nj; i++) {
       while (out.ctu_start[c + 1] <= i) c++;
       const int32_t o = perm[i];
-      for (int32_t d : deps[o]) {
-        const int32_t rd = rank[d];
+      for (auto [p, e] = D(o); p != e; ++p) {
+        const int32_t rd = rank[*p];
         if (rd >= i) throw VvcrError(VVCR_E_STATE, "intra plan: dependency is not earlier in step order");
         if (rd < out.ctu_start[c]) out.jobs[rd].flags |= IJ_PUBLISH;
       }
-      for (int32_t d : wdeps[o]) {
-        const int32_t rd = rank[d];
+      for (int t = wd_off[o]; t < wd_off[o + 1]; t++) {
+        const int32_t rd = rank[wd_flat[t]];
         out.deps.push_back(rd >= out.ctu_start[c] ? rd - out.ctu_start[c] : ~rd);
       }
       out.dep_start[i + 1] = (int32_t)out.deps.size();
     }
+    PROF_MARK("final");
     for (IntraJob &j : out.jobs)
       if (j.xkind != XK_INTER_CHROMA) resolve_availability(j);   // inter chroma steps read no reference samples
+    PROF_MARK("avail");
   }
 };
 

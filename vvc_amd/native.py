@@ -9,6 +9,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VVCR_LIB") or os.path.join(_HERE, "libvvcr.so")   # VVCR_LIB: diagnostics builds
 
 MAX_REF = 16
+MAX_TILE_LINES = 64
 STAGE_RESID, STAGE_INTER, STAGE_INTRA, STAGE_LMCS_INV = 0x01, 0x02, 0x04, 0x08
 STAGE_DBK, STAGE_SAO, STAGE_ALF, STAGE_ALL = 0x10, 0x20, 0x40, 0x7F
 BUF_RECO, BUF_PRED, BUF_RESI = 0, 1, 2
@@ -41,6 +42,9 @@ class PicParams(C.Structure):
         ("lmcs_cadj", I32 * 16),
         ("max_tb_log2", I32), ("log2_max_ts", I32),
         ("use_mts", I32), ("implicit_mts", I32), ("joint_cbcr_sign", I32),
+        ("num_tile_cols", I32), ("num_tile_rows", I32),
+        ("tile_col_bd", I32 * (MAX_TILE_LINES + 1)), ("tile_row_bd", I32 * (MAX_TILE_LINES + 1)),
+        ("entropy_sync", I32),
     ]
 
 
@@ -93,6 +97,15 @@ def lib():
         L.vvcr_rdo_release.argtypes = [P, I32]
         L.vvcr_rd_dist.argtypes = [P, P, I32, P, C.c_int64, P, C.c_int64, P, P]
         L.vvcr_fwd_transform.argtypes = [P, P, I32, I32, P, C.c_int64, P, C.c_int64]
+        L.vvcr_picture_create.argtypes = [C.POINTER(SeqParams), C.POINTER(PicParams), C.POINTER(P)]
+        L.vvcr_picture_submit.argtypes = [P, P, I32, P, I32, P, I32, P, C.c_int64, P, P, I32]
+        L.vvcr_picture_set_loop_filter_params.argtypes = [P, P, C.POINTER(Alf)]
+        L.vvcr_picture_plan.argtypes = [P, C.c_uint32]
+        L.vvcr_picture_work_counts.argtypes = [P, C.POINTER(C.c_int64), I32]
+        L.vvcr_picture_last_error.argtypes = [P]
+        L.vvcr_picture_last_error.restype = C.c_char_p
+        L.vvcr_picture_destroy.argtypes = [P]
+        L.vvcr_prepare_planned.argtypes = [P, P, C.POINTER(I32)]
         _lib = L
     return _lib
 
@@ -105,7 +118,9 @@ EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_release_picture"
            "vvcr_set_loop_filter_params", "vvcr_end_picture", "vvcr_end_picture_stages", "vvcr_sync",
            "vvcr_read_plane", "vvcr_write_plane", "vvcr_read_picture", "vvcr_get_dmvr_deltas",
            "vvcr_last_stage_times", "vvcr_stream", "vvcr_rd_plan", "vvcr_rd_run", "vvcr_fwd_plan", "vvcr_fwd_run",
-           "vvcr_rdo_release", "vvcr_rd_dist", "vvcr_fwd_transform", "vvcr_set_timing"]
+           "vvcr_rdo_release", "vvcr_rd_dist", "vvcr_fwd_transform", "vvcr_set_timing",
+           "vvcr_picture_create", "vvcr_picture_submit", "vvcr_picture_set_loop_filter_params", "vvcr_picture_plan",
+           "vvcr_picture_work_counts", "vvcr_picture_last_error", "vvcr_picture_destroy", "vvcr_prepare_planned"]
 
 # encoder RDO block descriptors (include/vvcr.h vvcr_rd_block / vvcr_fwd_block) as numpy record types
 RD_BLOCK = [("org_off", "<i8"), ("cur_off", "<i8"), ("org_stride", "<i4"), ("cur_stride", "<i4"), ("width", "<i4"),
@@ -116,6 +131,59 @@ FWD_BLOCK = [("src_off", "<i8"), ("dst_off", "<i8"), ("src_stride", "<i4"), ("wi
 
 def _ptr(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None and a.size else None
+
+
+class Picture:
+    """Host-only picture builder (vvcr_picture_*): validate and plan one picture without a context or a
+    device. Several Pictures may be planned on several threads at once (ctypes drops the GIL in the
+    library calls); Context.prepare_planned uploads a planned one."""
+
+    def __init__(self, width, height, pp, bit_depth=10, ctu_log2=7, dpb_slots=32):
+        self.L = lib()
+        sp = SeqParams(width, height, 1, bit_depth, ctu_log2, dpb_slots, 0)
+        h = C.c_void_p()
+        r = self.L.vvcr_picture_create(C.byref(sp), C.byref(pp), C.byref(h))
+        if r != 0:
+            raise VvcrError("vvcr_picture_create failed (%d): %s" % (r, self.L.vvcr_picture_last_error(None).decode()))
+        self.h = h
+        self._keep = []
+
+    def _chk(self, r, what):
+        if r != 0:
+            raise VvcrError("%s failed (%d): %s" % (what, r, self.L.vvcr_picture_last_error(self.h).decode()))
+
+    def submit(self, cu, pu, tu, coef, motion, geo):
+        arrs = [np.ascontiguousarray(a, np.int32) for a in (cu, pu, tu, coef, motion, geo)]
+        cu, pu, tu, coef, motion, geo = arrs
+        self._chk(self.L.vvcr_picture_submit(self.h, _ptr(cu), len(cu), _ptr(pu), len(pu), _ptr(tu), len(tu),
+                                             _ptr(coef), coef.size, _ptr(motion), _ptr(geo), len(geo)),
+                  "vvcr_picture_submit")
+
+    def set_loop_filter_params(self, sao, alf_struct, keep):
+        self._keep = keep
+        self._chk(self.L.vvcr_picture_set_loop_filter_params(self.h, _ptr(sao), C.byref(alf_struct) if alf_struct else None),
+                  "vvcr_picture_set_loop_filter_params")
+
+    def plan(self, stages=STAGE_ALL):
+        self._chk(self.L.vvcr_picture_plan(self.h, stages), "vvcr_picture_plan")
+
+    def work_counts(self):
+        c = (C.c_int64 * 8)()
+        n = self.L.vvcr_picture_work_counts(self.h, c, 8)
+        if n < 0:
+            self._chk(n, "vvcr_picture_work_counts")
+        return dict(zip(("tb", "mc", "mc_bidir", "affine", "recon_tiles", "intra_steps", "dbk_segments", "dmvr"), list(c)))
+
+    def close(self):
+        if self.h:
+            self.L.vvcr_picture_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Context:
@@ -182,6 +250,12 @@ class Context:
         """vvcr_prepare_picture: plan + upload the current picture; returns a handle."""
         h = C.c_int32(0)
         self._chk(self.L.vvcr_prepare_picture(self.h, stages, C.byref(h)), "vvcr_prepare_picture")
+        return h.value
+
+    def prepare_planned(self, pic):
+        """vvcr_prepare_planned: upload a planned Picture; returns a handle (thread-safe per picture)."""
+        h = C.c_int32(0)
+        self._chk(self.L.vvcr_prepare_planned(self.h, pic.h, C.byref(h)), "vvcr_prepare_planned")
         return h.value
 
     def launch(self, handle):

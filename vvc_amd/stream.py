@@ -66,7 +66,9 @@ def pic_params(p, slot, slot_of):
         for r in range(n):
             poc = int(p["ref_poc"][l][r])
             pp.ref_poc[l][r] = poc
-            pp.ref_slot[l][r] = slot_of.get(poc, 0)
+            if poc not in slot_of:   # a reference the DPB does not hold: never substitute another picture
+                raise KeyError("POC %d: reference POC %d is not in the DPB" % (h["poc"], poc))
+            pp.ref_slot[l][r] = slot_of[poc]
             pp.ref_lt[l][r] = int(p["ref_lt"][l][r])
     for k in ("dual_tree", "dep_quant", "sign_hiding", "joint_cbcr", "bdof_enabled", "dmvr_enabled", "prof_enabled",
               "lfnst_enabled", "mts_intra", "mts_inter", "sbt", "wp_p", "wp_b", "dbk_disable", "dbk_beta_offset_div2",
@@ -91,7 +93,25 @@ def pic_params(p, slot, slot_of):
         np.copyto(np.ctypeslib.as_array(getattr(pp, name))[:len(src)], src)
     cadj = np.asarray(p["lmcs_cadj"], np.int32)[:16]
     np.copyto(np.ctypeslib.as_array(pp.lmcs_cadj)[:len(cadj)], cadj)
+    if "tile_col_bd" in p:   # captures without these fields hold one tile
+        cb, rb = np.asarray(p["tile_col_bd"], np.int32), np.asarray(p["tile_row_bd"], np.int32)
+        pp.num_tile_cols, pp.num_tile_rows = len(cb) - 1, len(rb) - 1
+        np.copyto(np.ctypeslib.as_array(pp.tile_col_bd)[:len(cb)], cb)
+        np.copyto(np.ctypeslib.as_array(pp.tile_row_bd)[:len(rb)], rb)
+    pp.entropy_sync = h.get("entropy_sync", 0)
     return pp
+
+
+def plan_picture(p, slot, slot_of, dpb_slots=32, stages=N.STAGE_ALL):
+    """Host-only planning of one parsed picture (vvcr_picture_*): returns a planned N.Picture. Runs
+    without a device; safe to call for several pictures on several threads."""
+    h = p["hdr"]
+    pic = N.Picture(h["width"], h["height"], pic_params(p, slot, slot_of), bit_depth=h["bitdepth_y"],
+                    ctu_log2=h["ctu_log2"], dpb_slots=dpb_slots)
+    submit(pic, p)
+    set_loop_filter_params(pic, p)
+    pic.plan(stages)
+    return pic
 
 
 def submit(ctx, p):
