@@ -21,7 +21,7 @@ def test_sao_alf_match_reference(golden_dir, name):
                                  (N.STAGE_ALF, "sao", "alf")):
             for c, pl in enumerate("yuv"):
                 ctx.write_plane(N.BUF_RECO, 0, c, p[src + "_" + pl])
-            ctx.begin_picture(S.pic_params(p, 0, {}))
+            ctx.begin_picture(S.pic_params(p, 0, {}, missing_ref_slot=0))
             S.submit(ctx, p)
             S.set_loop_filter_params(ctx, p)
             ctx.end_picture(stages)
@@ -43,7 +43,7 @@ def test_deblocking_matches_reference(golden_dir, name):
         for stages, dst in ((N.STAGE_DBK, "dbk"), (N.STAGE_DBK | N.STAGE_SAO | N.STAGE_ALF, "alf")):
             for c, pl in enumerate("yuv"):
                 ctx.write_plane(N.BUF_RECO, 0, c, p["dbkin_" + pl])
-            ctx.begin_picture(S.pic_params(p, 0, {}))
+            ctx.begin_picture(S.pic_params(p, 0, {}, missing_ref_slot=0))
             S.submit(ctx, p)
             S.set_loop_filter_params(ctx, p)
             ctx.end_picture(stages)

@@ -19,7 +19,7 @@ def test_residual_matches_reference_and_oracle(golden_dir, name):
     h0 = pics[0]["hdr"]
     ctx = N.Context(h0["width"], h0["height"], dpb_slots=2)
     for p in pics:
-        ctx.begin_picture(S.pic_params(p, 0, {}))
+        ctx.begin_picture(S.pic_params(p, 0, {}, missing_ref_slot=0))
         S.submit(ctx, p)
         ctx.end_picture(N.STAGE_RESID)
         orc = O.residual_picture(p)

@@ -56,7 +56,10 @@ class SlotAllocator:
         return s
 
 
-def pic_params(p, slot, slot_of):
+def pic_params(p, slot, slot_of, missing_ref_slot=None):
+    """Picture parameters with the DPB slots of the references. A reference POC missing from slot_of is
+    an error, unless the caller runs only stages that read no reference picture (residual / loop-filter
+    stage tests) and names a placeholder slot explicitly (missing_ref_slot)."""
     h = p["hdr"]
     pp = N.PicParams()
     pp.poc, pp.slot, pp.slice_type, pp.slice_qp = h["poc"], slot, h["slice_type"], h["slice_qp"]
@@ -66,9 +69,12 @@ def pic_params(p, slot, slot_of):
         for r in range(n):
             poc = int(p["ref_poc"][l][r])
             pp.ref_poc[l][r] = poc
-            if poc not in slot_of:   # a reference the DPB does not hold: never substitute another picture
+            if poc in slot_of:
+                pp.ref_slot[l][r] = slot_of[poc]
+            elif missing_ref_slot is not None:
+                pp.ref_slot[l][r] = missing_ref_slot
+            else:   # a reference the DPB does not hold: never substitute another picture silently
                 raise KeyError("POC %d: reference POC %d is not in the DPB" % (h["poc"], poc))
-            pp.ref_slot[l][r] = slot_of[poc]
             pp.ref_lt[l][r] = int(p["ref_lt"][l][r])
     for k in ("dual_tree", "dep_quant", "sign_hiding", "joint_cbcr", "bdof_enabled", "dmvr_enabled", "prof_enabled",
               "lfnst_enabled", "mts_intra", "mts_inter", "sbt", "wp_p", "wp_b", "dbk_disable", "dbk_beta_offset_div2",
