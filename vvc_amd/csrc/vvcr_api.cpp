@@ -53,8 +53,11 @@ DPlane alloc_plane(int w, int h) {
   DPlane d;
   d.w = w; d.h = h;
   d.stride = (w + 63) & ~63;
-  VVCR_CHECK_HIP(hipMalloc(&d.p, (size_t)d.stride * h * sizeof(int16_t)));
-  VVCR_CHECK_HIP(hipMemset(d.p, 0, (size_t)d.stride * h * sizeof(int16_t)));
+  // + 64 samples: the MC gathers read whole aligned 4-sample chunks, up to 16 samples past the last
+  // window sample (never used, but they must be inside the allocation on the last row)
+  const size_t n = (size_t)d.stride * h + 64;
+  VVCR_CHECK_HIP(hipMalloc(&d.p, n * sizeof(int16_t)));
+  VVCR_CHECK_HIP(hipMemset(d.p, 0, n * sizeof(int16_t)));
   return d;
 }
 

@@ -1,20 +1,34 @@
-// vvcr_mc.hip — motion-compensated prediction for gfx950.
+// vvcr_mc.hip — motion-compensated prediction for gfx950 (k_mc_basic).
 //
-// One 64-lane wave per McJob (<= 16x16 luma block + 8x8 Cb/Cr). Per component and list the wave
-// stages the (w+N-1)x(h+N-1) reference window in LDS with coordinates clamped to the picture
-// (equivalent to VTM's edge-replicated 288-sample margin, Picture::extendPicBorder Picture.cpp:737,
-// plus clipMv Mv.cpp:54 — every filter phase sums to 64 so a clamped run of equal samples filters to
-// the same value whatever the phase), runs the separable FIR exactly as
-// InterpolationFilter::filter<N,isVertical,isFirst,isLast> (InterpolationFilter.cpp:548-650) with the
-// copy / H-only / V-only / H-then-V split of InterPrediction::xPredInterBlk (InterPrediction.cpp:784-803),
-// keeps per-list results in registers and combines them like AreaBuf::addAvg (Buffer.cpp:447),
-// addWeightedAvg (BCW, Buffer.cpp:350) or the uni-prediction rounding (rndRes = !bi).
+// One 64-lane wave per McJob (<= 16x16 luma block + its 4:2:0 chroma, one or two lists). The reference
+// windows are gathered with 8-byte loads of aligned 4-sample chunks (every active window of the job in
+// one phase, all loads in flight before the first LDS write) into LDS; a window that reaches outside the
+// picture is gathered per sample with clamped coordinates instead (equivalent to VTM's edge-replicated
+// 288-sample margin, Picture::extendPicBorder Picture.cpp:737, plus clipMv Mv.cpp:54: every filter phase
+// sums to 64, so a clamped run of equal samples filters to the same value whatever the phase).
+//
+// Filtering is InterpolationFilter::filter<N,isVertical,isFirst,isLast> (InterpolationFilter.cpp:548-650)
+// as the H-then-V pass of xPredInterBlk (InterPrediction.cpp:784-803) for EVERY fraction: a zero fraction
+// takes the identity phase {.., 64, ..}, whose intermediate is exact (16 s - 8192 fits int16), and the
+// 2-D roundings then equal the copy / H-only / V-only branches (((64 t + off2) >> sh2) == t;
+// ((16 X - 2^19) >> 6) == ((X - 2^15) >> 2); (16 X + 2^9) >> 10 == (X + 32) >> 6). One code path, no
+// divergence on fractions.
+//
+// Arithmetic is packed: samples are int16 pairs in LDS dwords and each tap pair is one v_dot2c_i32_i16.
+// An output whose first tap sits on an even sample uses the pair-aligned coefficients A = (c0,c1)(c2,c3)..,
+// one starting on an odd sample the shifted set B = (0,c0)(c1,c2)..(c_{N-1},0) over the same aligned
+// pairs, so every LDS read is an aligned dword. The H pass writes its outputs transposed (column-major,
+// vertical pairs packed), so the V pass reads aligned vertical pairs the same way. Results combine like
+// AreaBuf::addAvg (Buffer.cpp:447), addWeightedAvg (BCW, Buffer.cpp:350), explicit WP
+// (WeightPrediction.cpp:157-378), the GEO blend (InterpolationFilter::xWeightedGeoBlk :997) or the
+// uni-prediction rounding, and leave as 8-byte row stores.
 #include "vvcr_internal.h"
 #include "vvcr_tables.h"
+#include "vvcr_mcdev.h"
 
 namespace {
 
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+using namespace mcdev;
 
 __constant__ int8_t c_luma[16][8] = VVCR_LUMA_FILTER_TABLE;
 __constant__ int8_t c_luma4x4[16][8] = VVCR_LUMA4x4_FILTER_TABLE;
@@ -41,240 +55,301 @@ __device__ __forceinline__ int geo_weight(int angle, int offX, int offY, int lx,
   return clampi((32 + wIdx + 4) >> 3, 0, 8);
 }
 
-constexpr int IF_INTERNAL_PREC = 14;
-constexpr int IF_FILTER_PREC = 6;
-constexpr int IF_INTERNAL_OFFS = 1 << (IF_INTERNAL_PREC - 1);
+// LDS geometry (int16 samples). Windows hold aligned 4-sample chunks: element e of a row is the sample at
+// picture column ax + e, ax = window origin rounded down to a multiple of 4.
+constexpr int LP = 28, LR = 24;     // luma window: 7 chunks per row, 23 rows (+1 pad row for the last pair)
+constexpr int CP = 16, CR = 12;     // chroma window: 4 chunks, 11 rows (+1)
+constexpr int TP = 26, CTP = 14;    // H-pass outputs, column-major: rows per column (even: aligned pairs)
 
+// Combine one sample of the two lists: uni rounding (already final when rnd), WP, GEO blend, BCW, addAvg.
+__device__ __forceinline__ int combine(const McParams &P, const McJob &J, int comp, int x, int y, int a, int b) {
+  const int cs = comp ? 1 : 0;
+  const bool l0 = J.flags & MC_L0, l1 = J.flags & MC_L1, bi = l0 && l1;
+  const int bd = P.bd, maxv = (1 << bd) - 1, headRoom = max(2, IF_INTERNAL_PREC - bd);
+  if (!bi) {
+    if (J.flags & MC_WP) return wp_uni(P.wp, l0 ? 0 : 1, l0 ? (J.ridx & 15) : (J.ridx >> 4), comp, a, headRoom, maxv);
+    return a;
+  }
+  if (J.flags & MC_WP) return wp_bi(P.wp, J.ridx & 15, J.ridx >> 4, comp, a, b, headRoom, maxv);
+  if (J.flags & MC_GEO) {
+    // xWeightedGeoBlk: (w*p0 + (8-w)*p1 + offset) >> (headRoom + 3)
+    const int w = geo_weight(J.aux & 31, (J.aux >> 8) & 255, (J.aux >> 16) & 255, ((J.x >> cs) + x - (J.pu_x >> cs)) << cs,
+                             ((J.y >> cs) + y - (J.pu_y >> cs)) << cs);
+    const int shiftW = headRoom + 3;
+    const int offset = (1 << (shiftW - 1)) + (IF_INTERNAL_OFFS << 3);
+    return clampi((w * a + (8 - w) * b + offset) >> shiftW, 0, maxv);
+  }
+  if (J.bcw != 2) {   // AreaBuf<Pel>::addWeightedAvg (Buffer.cpp:350)
+    const int w1 = c_bcw_w1[J.bcw], w0 = 8 - w1;
+    const int shiftNum = headRoom + 3;
+    const int offset = (1 << (shiftNum - 1)) + (IF_INTERNAL_OFFS << 3);
+    return clampi((a * w0 + b * w1 + offset) >> shiftNum, 0, maxv);
+  }
+  const int shiftNum = headRoom + 1;   // AreaBuf<Pel>::addAvg (Buffer.cpp:447)
+  const int offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
+  return clampi((a + b + offset) >> shiftNum, 0, maxv);
+}
 
-// LDS layout per wave (one job per 64-thread workgroup): the six reference windows of a job (luma and
-// Cb/Cr for lists 0 and 1) are staged in ONE gather phase — every lane issues all of its loads before the
-// first LDS write, so the job pays one memory round trip instead of one per window row chunk — and then
-// filtered from LDS.
-constexpr int LW_PITCH = 24, LW_ROWS = 23;   // luma window: up to 16+7 = 23 columns / rows
-constexpr int CW_PITCH = 12, CW_ROWS = 11;   // chroma window: up to 8+3 = 11
-constexpr int LW_SIZE = LW_PITCH * LW_ROWS, CW_SIZE = CW_PITCH * CW_ROWS;
-constexpr int STAGE_SPAN = 2 * LW_SIZE + 4 * CW_SIZE;       // all six windows
-constexpr int TMP_STRIDE = 16;
-
-// Window geometry of one (component, list): top-left tap in picture coordinates and the window size.
+// window geometry of one (component, list)
 struct Win {
-  int ox, oy, ww, wh, fx, fy;
   const int16_t *p;
-  int stride, pw, ph;
-  bool on;
+  int stride, pw, ph, ax, oy, s, frac_x, frac_y;
+  bool on, inside;
 };
-
 __device__ __forceinline__ Win make_win(const McParams &P, const McJob &J, int comp, int l) {
   Win w;
   const int cs = comp ? 1 : 0, N = comp ? 4 : 8, half = N / 2 - 1, fb = 4 + cs;
   w.on = ((J.flags & (l ? MC_L1 : MC_L0)) != 0) && ((J.flags & (comp ? MC_CHROMA : MC_LUMA)) != 0);
   const DPlane &R = P.ref[J.slot[l] < 0 ? 0 : J.slot[l]][comp];
   const int mvx = J.mv[l][0], mvy = J.mv[l][1], mask = (1 << fb) - 1;
-  w.fx = mvx & mask; w.fy = mvy & mask;
-  w.ox = (J.x >> cs) + (mvx >> fb) - half; w.oy = (J.y >> cs) + (mvy >> fb) - half;
-  w.ww = (J.w >> cs) + N - 1; w.wh = (J.h >> cs) + N - 1;
+  w.frac_x = mvx & mask;
+  w.frac_y = mvy & mask;
+  const int ox = (J.x >> cs) + (mvx >> fb) - half;
+  w.oy = (J.y >> cs) + (mvy >> fb) - half;
+  w.s = ox & 3;
+  w.ax = ox - w.s;
+  const int ww = (J.w >> cs) + N - 1, wh = (J.h >> cs) + N - 1;
   w.p = R.p; w.stride = R.stride; w.pw = R.w; w.ph = R.h;
+  w.inside = w.ax >= 0 && ox + ww <= R.w && w.oy >= 0 && w.oy + wh <= R.h;
   return w;
 }
 
-// Separable FIR of one list from its staged window into per-lane registers out[k] (k-th sample of the
-// lane): InterpolationFilter::filter<N,isVertical,isFirst,isLast> with xPredInterBlk's split.
-template <int N>
-__device__ void filter_list(const int16_t *win, int pitch, int bw, int bh, int fx, int fy, bool altHpel, bool rnd,
-                            int bd, int16_t *tmp, int lane, int (&out)[4]) {
-  const int half = N / 2 - 1;
-  const int wh = bh + N - 1;
-  int8_t ch[8], cv[8];
-  if (N == 8) {
-    const bool is4x4 = (bw == 4 && bh == 4);
-    const int8_t *th = (fx == 8 && altHpel) ? c_alt_hpel : (is4x4 ? c_luma4x4[fx] : c_luma[fx]);
-    const int8_t *tv = (fy == 8 && altHpel) ? c_alt_hpel : (is4x4 ? c_luma4x4[fy] : c_luma[fy]);
-#pragma unroll
-    for (int t = 0; t < 8; t++) { ch[t] = th[t]; cv[t] = tv[t]; }
-  } else {
-#pragma unroll
-    for (int t = 0; t < 4; t++) { ch[t] = c_chroma[fx][t]; cv[t] = c_chroma[fy][t]; }
-  }
-  const int headRoom = max(2, IF_INTERNAL_PREC - bd);
-  const int n = bw * bh;
-  const int lw = __ffs(bw) - 1;      // bw is a power of two (4, 8, 16; chroma 2..8)
-  if (fx == 0 && fy == 0) {
-    // filterCopy<true, isLast> (InterpolationFilter.cpp:403)
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      int i = lane + 64 * k;
-      if (i < n) {
-        int y = i >> lw, x = i & (bw - 1);
-        int v = win[(y + half) * pitch + x + half];
-        out[k] = rnd ? v : (int)(int16_t)((v << headRoom) - IF_INTERNAL_OFFS);
-      }
-    }
-  } else if (fy == 0 || fx == 0) {
-    // single pass, isFirst = true, isLast = rnd
-    const bool vert = (fx == 0);
-    const int shift = rnd ? IF_FILTER_PREC : IF_FILTER_PREC - headRoom;
-    const int offset = rnd ? (1 << (shift - 1)) : -(IF_INTERNAL_OFFS << shift);
-    const int maxv = (1 << bd) - 1;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      int i = lane + 64 * k;
-      if (i < n) {
-        int y = i >> lw, x = i & (bw - 1);
-        int sum = 0;
-        if (vert) {
-#pragma unroll
-          for (int t = 0; t < N; t++) sum += win[(y + t) * pitch + x + half] * cv[t];
-        } else {
-#pragma unroll
-          for (int t = 0; t < N; t++) sum += win[(y + half) * pitch + x + t] * ch[t];
-        }
-        int v = (int)(int16_t)((sum + offset) >> shift);
-        out[k] = rnd ? clampi(v, 0, maxv) : v;
-      }
-    }
-  } else {
-    // H pass (isFirst, !isLast) over bh+N-1 rows into tmp, then V pass (!isFirst, isLast = rnd)
-    const int sh1 = IF_FILTER_PREC - headRoom;
-    const int off1 = -(IF_INTERNAL_OFFS << sh1);
-#pragma unroll
-    for (int k = 0; k < (N == 8 ? 6 : 2); k++) {     // <= 23x16 (luma) / 11x8 (chroma) samples
-      const int i = lane + 64 * k;
-      if (i < bw * wh) {
-        int r = i >> lw, c = i & (bw - 1);
-        int sum = 0;
-#pragma unroll
-        for (int t = 0; t < N; t++) sum += win[r * pitch + c + t] * ch[t];
-        tmp[r * TMP_STRIDE + c] = (int16_t)((sum + off1) >> sh1);
-      }
-    }
-    __syncthreads();
-    const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
-    const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
-    const int maxv = (1 << bd) - 1;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      int i = lane + 64 * k;
-      if (i < n) {
-        int y = i >> lw, x = i & (bw - 1);
-        int sum = 0;
-#pragma unroll
-        for (int t = 0; t < N; t++) sum += tmp[(y + t) * TMP_STRIDE + x] * cv[t];
-        int v = (int)(int16_t)((sum + off2) >> sh2);
-        out[k] = rnd ? clampi(v, 0, maxv) : v;
-      }
-    }
-    __syncthreads();   // tmp reused by the next list / component
-  }
-}
-
-// Combine the per-list results of one component and store: uni rounding, WP, GEO blend, BCW, addAvg.
-__device__ void mc_store(const McParams &P, const McJob &J, int comp, const int (&r0)[4], const int (&r1)[4], int lane) {
-  const int cs = comp ? 1 : 0;
-  const int bx = J.x >> cs, by = J.y >> cs, bw = J.w >> cs, bh = J.h >> cs;
-  const bool l0 = J.flags & MC_L0, l1 = J.flags & MC_L1;
-  const bool bi = l0 && l1;
-  const bool wp = (J.flags & MC_WP) != 0;
-  const DPlane &o = P.out[comp];
-  const int n = bw * bh;
-  const int lw = __ffs(bw) - 1;
-  const int bd = P.bd;
-  const int maxv = (1 << bd) - 1;
-  const int headRoom = max(2, IF_INTERNAL_PREC - bd);
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    int i = lane + 64 * k;
-    if (i >= n) continue;
-    int y = i >> lw, x = i & (bw - 1);
-    int v;
-    if (!bi) {
-      v = wp ? wp_uni(P.wp, l0 ? 0 : 1, l0 ? (J.ridx & 15) : (J.ridx >> 4), comp, r0[k], headRoom, maxv) : r0[k];
-    } else if (wp) {
-      v = wp_bi(P.wp, J.ridx & 15, J.ridx >> 4, comp, r0[k], r1[k], headRoom, maxv);
-    } else if (J.flags & MC_GEO) {
-      // xWeightedGeoBlk: (w*p0 + (8-w)*p1 + offset) >> (headRoom + 3)
-      const int w = geo_weight(J.aux & 31, (J.aux >> 8) & 255, (J.aux >> 16) & 255, (bx + x - (J.pu_x >> cs)) << cs,
-                               (by + y - (J.pu_y >> cs)) << cs);
-      const int shiftW = headRoom + 3;
-      const int offset = (1 << (shiftW - 1)) + (IF_INTERNAL_OFFS << 3);
-      v = clampi((w * r0[k] + (8 - w) * r1[k] + offset) >> shiftW, 0, maxv);
-    } else if (J.bcw != 2) {
-      // AreaBuf<Pel>::addWeightedAvg (Buffer.cpp:350)
-      const int w1 = c_bcw_w1[J.bcw], w0 = 8 - w1;
-      const int shiftNum = headRoom + 3;
-      const int offset = (1 << (shiftNum - 1)) + (IF_INTERNAL_OFFS << 3);
-      v = clampi((r0[k] * w0 + r1[k] * w1 + offset) >> shiftNum, 0, maxv);
-    } else {
-      // AreaBuf<Pel>::addAvg (Buffer.cpp:447)
-      const int shiftNum = headRoom + 1;
-      const int offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
-      v = clampi((r0[k] + r1[k] + offset) >> shiftNum, 0, maxv);
-    }
-    o.p[(size_t)(by + y) * o.stride + bx + x] = (int16_t)v;
-  }
-}
-
 __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__restrict__ jobs, int njobs) {
-  // windows: [0] luma L0, [1] luma L1 (LW_SIZE each), then Cb L0, Cb L1, Cr L0, Cr L1 (CW_SIZE each)
-  __shared__ int16_t win[STAGE_SPAN];
-  __shared__ int16_t tmp[LW_ROWS * TMP_STRIDE];
+  __shared__ __attribute__((aligned(16))) int16_t s_lwin[2][LR * LP];   // luma windows per list
+  __shared__ __attribute__((aligned(16))) int16_t s_cwin[4][CR * CP];   // chroma windows, combo = 2 * (comp - 1) + list
+  __shared__ __attribute__((aligned(16))) int16_t s_lt[2][16 * TP];     // luma H outputs [col][row]
+  __shared__ __attribute__((aligned(16))) int16_t s_ct[4][8 * CTP];     // chroma H outputs [col][row]
+  __shared__ __attribute__((aligned(16))) int16_t s_lo[2][256];         // luma V outputs per list [y * w + x]
+  __shared__ __attribute__((aligned(16))) int16_t s_co[4][64];          // chroma V outputs [y * cw + x]
+  __shared__ uint32_t s_ctap[4][2][5];                                   // chroma taps: [combo][H/V][A0 A1 B0 B1 B2]
   const int j = blockIdx.x;
   if (j >= njobs) return;
   const McJob J = jobs[j];
   const int lane = threadIdx.x;
-  Win w[6];
+  const int w = J.w, h = J.h, lw = __ffs(w) - 1;
+  const int cw = w >> 1, chh = h >> 1, lcw = lw - 1;
+  const bool bi = (J.flags & MC_L0) && (J.flags & MC_L1);
+  const bool rnd = !bi && !(J.flags & MC_KEEP14) && !(J.flags & MC_WP);
+  const int bd = P.bd, maxv = (1 << bd) - 1, headRoom = max(2, IF_INTERNAL_PREC - bd);
+  const int sh1 = IF_FILTER_PREC - headRoom, off1 = -(IF_INTERNAL_OFFS << sh1);
+  const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
+  const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
+
+  Win wl[2], wc[4];
 #pragma unroll
-  for (int c = 0; c < 3; c++)
+  for (int l = 0; l < 2; l++) wl[l] = make_win(P, J, 0, l);
 #pragma unroll
-    for (int l = 0; l < 2; l++) w[c * 2 + l] = make_win(P, J, c, l);
-  // ---- gather: all loads of the job in flight together, coordinates clamped to the picture.
-  // Windows are walked with compile-time indices (a dynamically indexed Win[] would live in scratch).
-  constexpr int LIT = (LW_SIZE + 63) / 64, CIT = (CW_SIZE + 63) / 64;
-  int16_t v[6][LIT] = {};
+  for (int k = 0; k < 4; k++) wc[k] = make_win(P, J, 1 + (k >> 1), k & 1);
+  bool inside = true;
 #pragma unroll
-  for (int wi = 0; wi < 6; wi++) {
-    const Win &W = w[wi];
-    const int pitch = wi < 2 ? LW_PITCH : CW_PITCH, size = wi < 2 ? LW_SIZE : CW_SIZE;
+  for (int l = 0; l < 2; l++) inside = inside && (!wl[l].on || wl[l].inside);
 #pragma unroll
-    for (int k = 0; k < (wi < 2 ? LIT : CIT); k++) {
-      const int i = lane + 64 * k;
-      const int r = i / pitch, c = i - r * pitch;
-      if (W.on && i < size && c < W.ww && r < W.wh) {
-        const int sx = clampi(W.ox + c, 0, W.pw - 1), sy = clampi(W.oy + r, 0, W.ph - 1);
-        v[wi][k] = W.p[(size_t)sy * W.stride + sx];
+  for (int k = 0; k < 4; k++) inside = inside && (!wc[k].on || wc[k].inside);
+
+  // chroma taps per combo (lanes 0..7): H from the horizontal fraction, V from the vertical one
+  if (lane < 8) {
+    const int k = lane >> 1, v = lane & 1;
+    // explicit selects: a lane-indexed J.mv[][] would put the job record in scratch
+    const int m0 = v ? J.mv[0][1] : J.mv[0][0], m1 = v ? J.mv[1][1] : J.mv[1][0];
+    const int mvf = ((k & 1) ? m1 : m0) & 31;
+    const Taps<4> t = make_taps<4>(c_chroma[mvf]);
+    s_ctap[k][v][0] = t.A[0]; s_ctap[k][v][1] = t.A[1];
+    s_ctap[k][v][2] = t.B[0]; s_ctap[k][v][3] = t.B[1]; s_ctap[k][v][4] = t.B[2];
+  }
+
+  // ---- gather
+  if (inside) {
+    uint2 vl[2][3], vc[4];
+#pragma unroll
+    for (int l = 0; l < 2; l++)
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const int i = lane + 64 * k, r = i / 7, c = i - 7 * r;
+        if (wl[l].on && r < h + 7)
+          vl[l][k] = *(const uint2 *)(wl[l].p + (size_t)(wl[l].oy + r) * wl[l].stride + wl[l].ax + 4 * c);
+      }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int r = lane >> 2, c = lane & 3;
+      if (wc[k].on && r < chh + 3) vc[k] = *(const uint2 *)(wc[k].p + (size_t)(wc[k].oy + r) * wc[k].stride + wc[k].ax + 4 * c);
+    }
+#pragma unroll
+    for (int l = 0; l < 2; l++)
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const int i = lane + 64 * k, r = i / 7, c = i - 7 * r;
+        if (wl[l].on && r < h + 7) *(uint2 *)&s_lwin[l][r * LP + 4 * c] = vl[l][k];
+      }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int r = lane >> 2, c = lane & 3;
+      if (wc[k].on && r < chh + 3) *(uint2 *)&s_cwin[k][r * CP + 4 * c] = vc[k];
+    }
+  } else {
+    // a window reaches outside the picture: per-sample gather with clamped coordinates, same layout
+#pragma unroll
+    for (int l = 0; l < 2; l++) {
+      if (!wl[l].on) continue;
+      const Win &W = wl[l];
+      for (int i = lane; i < (h + 7) * LP; i += 64) {
+        const int r = i / LP, e = i - LP * r;
+        s_lwin[l][i] = W.p[(size_t)clampi(W.oy + r, 0, W.ph - 1) * W.stride + clampi(W.ax + e, 0, W.pw - 1)];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (!wc[k].on) continue;
+      const Win &W = wc[k];
+      for (int i = lane; i < (chh + 3) * CP; i += 64) {
+        const int r = i / CP, e = i - CP * r;
+        s_cwin[k][i] = W.p[(size_t)clampi(W.oy + r, 0, W.ph - 1) * W.stride + clampi(W.ax + e, 0, W.pw - 1)];
       }
     }
   }
+  __syncthreads();
+
+  // ---- H pass: luma per list (items: 2 rows x 4 columns), chroma combos together (16 lanes each)
+  const bool is4x4 = (w == 4 && h == 4);
+  const bool alt = (J.flags & MC_ALT_HPEL) != 0;
 #pragma unroll
-  for (int wi = 0; wi < 6; wi++) {
-    int16_t *dst = win + (wi < 2 ? wi * LW_SIZE : 2 * LW_SIZE + (wi - 2) * CW_SIZE);
-    const int size = wi < 2 ? LW_SIZE : CW_SIZE;
+  for (int l = 0; l < 2; l++) {
+    if (!wl[l].on) continue;
+    const int fx = wl[l].frac_x;
+    const Taps<8> th = make_taps<8>((fx == 8 && alt) ? c_alt_hpel : (is4x4 ? c_luma4x4[fx] : c_luma[fx]));
+    const int lnq = lw - 2, nrp = (h + 8) >> 1;
+    const int rp = lane >> lnq, q = lane & ((1 << lnq) - 1);
+    if (rp < nrp) {
+      const uint32_t *r0 = (const uint32_t *)s_lwin[l] + (2 * rp) * (LP / 2) + (wl[l].s >> 1) + 2 * q;
+      uint32_t w0[6], w1[6];
 #pragma unroll
-    for (int k = 0; k < (wi < 2 ? LIT : CIT); k++) {
-      const int i = lane + 64 * k;
-      if (i < size) dst[i] = v[wi][k];
+      for (int k = 0; k < 6; k++) { w0[k] = r0[k]; w1[k] = r0[LP / 2 + k]; }
+      int a[4], b[4];
+      if (wl[l].s & 1) { fir4<8, 1>(w0, th, a); fir4<8, 1>(w1, th, b); }
+      else { fir4<8, 0>(w0, th, a); fir4<8, 0>(w1, th, b); }
+      uint32_t *dst = (uint32_t *)s_lt[l];
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++)
+        dst[((4 * q + jj) * TP + 2 * rp) >> 1] = pk((int16_t)((a[jj] + off1) >> sh1), (int16_t)((b[jj] + off1) >> sh1));
+    }
+  }
+  {
+    const int k = lane >> 4, it = lane & 15;
+    const int lnq = lcw >= 2 ? lcw - 2 : 0, nrp = (chh + 4) >> 1;
+    const int rp = it >> lnq, q = it & ((1 << lnq) - 1);
+    const int s = k == 0 ? wc[0].s : k == 1 ? wc[1].s : k == 2 ? wc[2].s : wc[3].s;
+    const bool on = k == 0 ? wc[0].on : k == 1 ? wc[1].on : k == 2 ? wc[2].on : wc[3].on;
+    if (on && rp < nrp) {
+      Taps<4> t;
+      t.A[0] = s_ctap[k][0][0]; t.A[1] = s_ctap[k][0][1];
+      t.B[0] = s_ctap[k][0][2]; t.B[1] = s_ctap[k][0][3]; t.B[2] = s_ctap[k][0][4];
+      const uint32_t *r0 = (const uint32_t *)s_cwin[k] + (2 * rp) * (CP / 2) + (s >> 1) + 2 * q;
+      uint32_t w0[5], w1[5];
+#pragma unroll
+      for (int m = 0; m < 5; m++) { w0[m] = r0[m]; w1[m] = r0[CP / 2 + m]; }
+      int a[4], b[4];
+      fir4_var<4>(w0, t, s & 1, a);
+      fir4_var<4>(w1, t, s & 1, b);
+      uint32_t *dst = (uint32_t *)s_ct[k];
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++)
+        dst[((4 * q + jj) * CTP + 2 * rp) >> 1] = pk((int16_t)((a[jj] + off1) >> sh1), (int16_t)((b[jj] + off1) >> sh1));
     }
   }
   __syncthreads();
-  // ---- filter and combine
-  const bool bi = (J.flags & MC_L0) && (J.flags & MC_L1);
-  const bool keep14 = (J.flags & MC_KEEP14) != 0, wp = (J.flags & MC_WP) != 0;
-  const bool rnd = !bi && !keep14 && !wp;
-  const int bd = P.bd;
+
+  // ---- V pass: items of one column x 4 rows
+#pragma unroll
+  for (int l = 0; l < 2; l++) {
+    if (!wl[l].on) continue;
+    const int fy = wl[l].frac_y;
+    const Taps<8> tv = make_taps<8>((fy == 8 && alt) ? c_alt_hpel : (is4x4 ? c_luma4x4[fy] : c_luma[fy]));
+    const int x = lane & (w - 1), g = lane >> lw;
+    if (4 * g < h) {
+      const uint32_t *c0 = (const uint32_t *)s_lt[l] + ((x * TP + 4 * g) >> 1);
+      uint32_t wv[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) wv[k] = c0[k];
+      int o[4];
+      fir4<8, 0>(wv, tv, o);
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) {
+        int v = (int16_t)((o[jj] + off2) >> sh2);
+        if (rnd) v = clampi(v, 0, maxv);
+        s_lo[l][(4 * g + jj) * w + x] = (int16_t)v;
+      }
+    }
+  }
+  {
+    const int k = lane >> 4, x = lane & 7, g = (lane >> 3) & 1;
+    const bool on = k == 0 ? wc[0].on : k == 1 ? wc[1].on : k == 2 ? wc[2].on : wc[3].on;
+    if (on && x < cw && 4 * g < chh) {
+      Taps<4> t;
+      t.A[0] = s_ctap[k][1][0]; t.A[1] = s_ctap[k][1][1];
+      t.B[0] = s_ctap[k][1][2]; t.B[1] = s_ctap[k][1][3]; t.B[2] = s_ctap[k][1][4];
+      const uint32_t *c0 = (const uint32_t *)s_ct[k] + ((x * CTP + 4 * g) >> 1);
+      uint32_t wv[4];
+#pragma unroll
+      for (int m = 0; m < 4; m++) wv[m] = c0[m];
+      int o[4];
+      fir4<4, 0>(wv, t, o);
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) {
+        if (4 * g + jj >= chh) break;
+        int v = (int16_t)((o[jj] + off2) >> sh2);
+        if (rnd) v = clampi(v, 0, maxv);
+        s_co[k][(4 * g + jj) * cw + x] = (int16_t)v;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- combine and store: 4 (chroma of 4-wide blocks: 2) consecutive samples of a row per lane
+  const int la = (J.flags & MC_L0) ? 0 : 1;   // the list of a uni-predicted block
   if (J.flags & MC_LUMA) {
-    int r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
-    const bool alt = (J.flags & MC_ALT_HPEL) != 0;
-    if (w[0].on) filter_list<8>(win, LW_PITCH, J.w, J.h, w[0].fx, w[0].fy, alt, rnd, bd, tmp, lane, r0);
-    if (w[1].on) filter_list<8>(win + LW_SIZE, LW_PITCH, J.w, J.h, w[1].fx, w[1].fy, alt, rnd, bd, tmp, lane, bi ? r1 : r0);
-    mc_store(P, J, 0, r0, r1, lane);
+    if (lane * 4 < w * h) {
+      const int i = lane * 4, y = i >> lw, x = i & (w - 1);
+      const uint2 a = *(const uint2 *)&s_lo[la][i];
+      uint2 b = a;
+      if (bi) b = *(const uint2 *)&s_lo[1][i];
+      int v[4] = {(int16_t)(a.x & 0xffff), (int16_t)(a.x >> 16), (int16_t)(a.y & 0xffff), (int16_t)(a.y >> 16)};
+      const int u[4] = {(int16_t)(b.x & 0xffff), (int16_t)(b.x >> 16), (int16_t)(b.y & 0xffff), (int16_t)(b.y >> 16)};
+      if (!rnd)
+#pragma unroll
+        for (int t = 0; t < 4; t++) v[t] = combine(P, J, 0, x + t, y, v[t], u[t]);
+      const DPlane &o = P.out[0];
+      *(uint2 *)(o.p + (size_t)(J.y + y) * o.stride + J.x + x) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+    }
   }
   if (J.flags & MC_CHROMA) {
+    const int comp = 1 + (lane >> 5), k = lane & 31;
+    const int ka = 2 * (comp - 1) + la, kb = 2 * (comp - 1) + 1;
+    const DPlane &o = P.out[comp];
+    if (cw >= 4) {
+      if (k * 4 < cw * chh) {
+        const int i = k * 4, y = i >> lcw, x = i & (cw - 1);
+        const uint2 a = *(const uint2 *)&s_co[ka][i];
+        uint2 b = a;
+        if (bi) b = *(const uint2 *)&s_co[kb][i];
+        int v[4] = {(int16_t)(a.x & 0xffff), (int16_t)(a.x >> 16), (int16_t)(a.y & 0xffff), (int16_t)(a.y >> 16)};
+        const int u[4] = {(int16_t)(b.x & 0xffff), (int16_t)(b.x >> 16), (int16_t)(b.y & 0xffff), (int16_t)(b.y >> 16)};
+        if (!rnd)
 #pragma unroll
-    for (int c = 1; c < 3; c++) {
-      int r0[4] = {0, 0, 0, 0}, r1[4] = {0, 0, 0, 0};
-      const int16_t *cw = win + 2 * LW_SIZE + (c - 1) * 2 * CW_SIZE;
-      if (w[c * 2].on) filter_list<4>(cw, CW_PITCH, J.w >> 1, J.h >> 1, w[c * 2].fx, w[c * 2].fy, false, rnd, bd, tmp, lane, r0);
-      if (w[c * 2 + 1].on) filter_list<4>(cw + CW_SIZE, CW_PITCH, J.w >> 1, J.h >> 1, w[c * 2 + 1].fx, w[c * 2 + 1].fy, false, rnd, bd, tmp, lane, bi ? r1 : r0);
-      mc_store(P, J, c, r0, r1, lane);
+          for (int t = 0; t < 4; t++) v[t] = combine(P, J, comp, x + t, y, v[t], u[t]);
+        *(uint2 *)(o.p + (size_t)((J.y >> 1) + y) * o.stride + (J.x >> 1) + x) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+      }
+    } else {   // 2-wide chroma (4-wide luma blocks)
+      if (k * 2 < cw * chh) {
+        const int i = k * 2, y = i >> lcw, x = i & (cw - 1);
+        const uint32_t a = *(const uint32_t *)&s_co[ka][i];
+        uint32_t b = a;
+        if (bi) b = *(const uint32_t *)&s_co[kb][i];
+        int v[2] = {(int16_t)(a & 0xffff), (int16_t)(a >> 16)};
+        const int u[2] = {(int16_t)(b & 0xffff), (int16_t)(b >> 16)};
+        if (!rnd)
+#pragma unroll
+          for (int t = 0; t < 2; t++) v[t] = combine(P, J, comp, x + t, y, v[t], u[t]);
+        *(uint32_t *)(o.p + (size_t)((J.y >> 1) + y) * o.stride + (J.x >> 1) + x) = pk(v[0], v[1]);
+      }
     }
   }
 }

@@ -6,9 +6,7 @@
 //   prefetch window) and/or bi-directional optical flow (BDOF, applyBiOptFlow :1274-1367 with the
 //   integer-sample extension of xPredInterBlk :812-850 and the gradient / sum / average cores of
 //   Buffer.cpp:88-199). The block is one DMVR sub-block (min(16, PU size)) or one xSubPuBio tile.
-// k_mc_affine: one wave per <= 16x16 luma tile of an affine PU (xPredAffineBlk :890-1272): 4x4 luma
-//   sub-block MVs from the control-point model, 6-tap-in-8 luma filter, PROF gradient correction
-//   (applyPROFCore Buffer.cpp:45), 4x4 chroma sub-blocks with the mean MV of two luma sub-blocks.
+// (k_mc_affine: vvcr_mc_affine.hip)
 // Reference windows are staged in LDS with coordinates clamped to the picture (and, for DMVR, to the
 // prefetched window, reproducing xPad's edge replication).
 #include "vvcr_internal.h"
@@ -438,270 +436,9 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// affine
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void round_affine(int &x, int &y, int s) {   // roundAffineMv (Mv.cpp:47)
-  const int o = 1 << (s - 1);
-  x = (x + o - (x >= 0)) >> s;
-  y = (y + o - (y >= 0)) >> s;
-}
-
-constexpr int AWS = 11;   // 4 + 7 luma window per sub-block
-constexpr int ALW = 16 * AWS * AWS;                  // luma windows of one list (16 sub-blocks)
-constexpr int ACW = 4 * 49;                          // chroma windows of one list and component (4 sub-blocks of 7x7)
-constexpr int A_SPAN = 2 * ALW + 2 * 2 * ACW;        // all windows of a tile
-
-__global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__restrict__ jobs, int njobs, const AffPu *__restrict__ pus) {
-  // all windows of the tile: luma [list][sub-block][11x11], then chroma [list][Cb/Cr][sub-block][7x7]
-  __shared__ int16_t win[A_SPAN];
-  __shared__ int sbmv[2][16][2];       // MC MV of each luma sub-block (clamped)
-  __shared__ int stmv[2][16][2];       // stored MV (before the picture clamp) for chroma
-  __shared__ int csmv[2][4][2];        // chroma sub-block MVs
-  __shared__ int16_t c14[16 * 16];     // PROF: 14-bit prediction of the tile
-  __shared__ int16_t hmid[16 * 44];    // separable luma: H-pass output, 11 rows x 4 columns per sub-block
-  const int j = blockIdx.x;
-  if (j >= njobs) return;
-  const AffJob J = jobs[j];
-  const AffPu U = pus[J.pu];
-  const int lane = threadIdx.x;
-  const int bd = P.bd, maxv = (1 << bd) - 1;
-  const int headRoom = max(2, IF_INTERNAL_PREC - bd);
-  const bool bi = U.l[0].present && U.l[1].present;
-  const int w = J.w, h = J.h;           // 8 or 16 (affine PUs are >= 8x8, tiled by 16)
-  const int lnsx = w == 16 ? 2 : 1, nsx = 1 << lnsx, nsb = (w >> 2) * (h >> 2);
-  const int cw = w >> 1, chh = h >> 1, ncx = cw >> 2, ncb = (cw >> 2) * (chh >> 2);
-  // MV clamp of xPredAffineBlk (:936-939), relative to the PU
-  const int iHorMax = (P.pic_w + 8 - U.x - 1) << 4, iHorMin = (-P.ctu - 8 - U.x + 1) << 4;
-  const int iVerMax = (P.pic_h + 8 - U.y - 1) << 4, iVerMin = (-P.ctu - 8 - U.y + 1) << 4;
-  const int MVLIM = (1 << 17) - 1;
-  // ---- sub-block MVs of both lists (:1102-1140)
-  if (lane < 32) {
-    const int l = lane >> 4, sb = lane & 15;
-    const AffList &A = pus[J.pu].l[l];      // lane-dependent list: read from global (a local copy would go to scratch)
-    if (A.present && sb < nsb) {
-      const int sw = (J.x - U.x) + (sb & (nsx - 1)) * 4, sh = (J.y - U.y) + (sb >> lnsx) * 4;
-      int mx, my;
-      if (!A.spread) {
-        mx = A.mvx + A.dhx * (2 + sw) + A.dvx * (2 + sh);
-        my = A.mvy + A.dhy * (2 + sw) + A.dvy * (2 + sh);
-      } else {
-        mx = A.mvx + A.dhx * (U.w >> 1) + A.dvx * (U.h >> 1);
-        my = A.mvy + A.dhy * (U.w >> 1) + A.dvy * (U.h >> 1);
-      }
-      round_affine(mx, my, 7);
-      mx = clampi(mx, -MVLIM - 1, MVLIM);
-      my = clampi(my, -MVLIM - 1, MVLIM);
-      stmv[l][sb][0] = mx; stmv[l][sb][1] = my;
-      sbmv[l][sb][0] = clampi(mx, iHorMin, iHorMax);
-      sbmv[l][sb][1] = clampi(my, iVerMin, iVerMax);
-    }
-  }
-  __syncthreads();
-  // ---- chroma: 4x4 sub-blocks, MV = mean of two luma sub-block MVs (:1142-1160)
-  if (lane < 8) {
-    const int l = lane >> 2, cb = lane & 3;
-    if (pus[J.pu].l[l].present && cb < ncb) {
-      const int cxs = (cb % ncx) * 2, cys = (cb / ncx) * 2;   // luma sub-block indices in the tile
-      const int a = cys * nsx + cxs, b = (cys + 1) * nsx + cxs + 1;
-      int mx = stmv[l][a][0] + stmv[l][b][0], my = stmv[l][a][1] + stmv[l][b][1];
-      round_affine(mx, my, 1);
-      csmv[l][cb][0] = clampi(mx, iHorMin, iHorMax);
-      csmv[l][cb][1] = clampi(my, iVerMin, iVerMax);
-    }
-  }
-  __syncthreads();
-  // ---- gather every window of the tile in one phase (all loads in flight before the first LDS write).
-  // A lane owns fixed window positions — luma e = lane, lane + 64 of the 11x11 window, chroma e = lane of
-  // the 7x7 — and walks the sub-blocks, whose window origins are wave-uniform (scalar), so a load costs
-  // a few VALU ops; lists / components / sub-blocks have compile-time indices (nothing in scratch).
-  {
-    const int r0 = lane / AWS, c0 = lane - r0 * AWS, e1 = lane + 64, r1 = e1 / AWS, c1 = e1 - r1 * AWS;
-    const bool has1 = e1 < AWS * AWS;
-    const int rc = lane / 7, cc = lane - rc * 7;
-    const bool hasc = lane < 49;
-    int16_t vl[2][16][2] = {}, vc[2][2][4] = {};
-#pragma unroll
-    for (int l = 0; l < 2; l++) {
-      if (!U.l[l].present) continue;
-      const DPlane &R = P.ref[U.l[l].slot][0];
-#pragma unroll
-      for (int sb = 0; sb < 16; sb++) {
-        if (sb >= nsb) continue;
-        const int ox = __builtin_amdgcn_readfirstlane(J.x + (sb & (nsx - 1)) * 4 + (sbmv[l][sb][0] >> 4) - 3);
-        const int oy = __builtin_amdgcn_readfirstlane(J.y + (sb >> lnsx) * 4 + (sbmv[l][sb][1] >> 4) - 3);
-        vl[l][sb][0] = R.p[clampi(oy + r0, 0, R.h - 1) * R.stride + clampi(ox + c0, 0, R.w - 1)];
-        if (has1) vl[l][sb][1] = R.p[clampi(oy + r1, 0, R.h - 1) * R.stride + clampi(ox + c1, 0, R.w - 1)];
-      }
-#pragma unroll
-      for (int comp = 1; comp < 3; comp++) {
-        const DPlane &RC = P.ref[U.l[l].slot][comp];
-#pragma unroll
-        for (int cb = 0; cb < 4; cb++) {
-          if (cb >= ncb) continue;
-          const int ox = __builtin_amdgcn_readfirstlane((J.x >> 1) + (cb % ncx) * 4 + (csmv[l][cb][0] >> 5) - 1);
-          const int oy = __builtin_amdgcn_readfirstlane((J.y >> 1) + (cb / ncx) * 4 + (csmv[l][cb][1] >> 5) - 1);
-          if (hasc) vc[l][comp - 1][cb] = RC.p[clampi(oy + rc, 0, RC.h - 1) * RC.stride + clampi(ox + cc, 0, RC.w - 1)];
-        }
-      }
-    }
-#pragma unroll
-    for (int l = 0; l < 2; l++) {
-      if (!U.l[l].present) continue;
-#pragma unroll
-      for (int sb = 0; sb < 16; sb++) {
-        if (sb >= nsb) continue;
-        win[l * ALW + sb * AWS * AWS + lane] = vl[l][sb][0];
-        if (has1) win[l * ALW + sb * AWS * AWS + e1] = vl[l][sb][1];
-      }
-#pragma unroll
-      for (int comp = 1; comp < 3; comp++)
-#pragma unroll
-        for (int cb = 0; cb < 4; cb++)
-          if (cb < ncb && hasc) win[2 * ALW + l * 2 * ACW + (comp - 1) * ACW + cb * 49 + lane] = vc[l][comp - 1][cb];
-    }
-  }
-  __syncthreads();
-  int res[3][2][4];
-#pragma unroll
-  for (int l = 0; l < 2; l++) {
-    const AffList &A = U.l[l];
-    if (!A.present) continue;
-    const int16_t *lwin = win + l * ALW;
-    // ---- luma: per sub-block 11x11 windows, every sub-block through the same separable path (H pass over
-    // 11 rows into hmid, then the V pass; the 6 non-zero taps of m_lumaFilter4x4, InterpolationFilter.cpp:57),
-    // so the lanes of a tile whose sub-blocks have different fractions do not diverge. A zero fraction
-    // takes the identity row {.., 64, ..}: its intermediate is exact (16 s - 8192 fits int16) and the
-    // 2-D roundings then equal the copy / 1-D paths of xPredInterBlk (InterPrediction.cpp:784-803):
-    // ((64 t + off2) >> sh2 == t, and (((S - 8192 * 4) >> 2) * 64 + 2^9 + 2^19) >> 10 == (S + 32) >> 6).
-    const bool prof = A.prof;
-    const bool rnd = !prof && !bi && !U.wp;
-    {
-      const int sh1 = IF_FILTER_PREC - headRoom, off1 = -(IF_INTERNAL_OFFS << sh1);
-#pragma unroll
-      for (int k = 0; k < 11; k++) {                 // <= 16 sub-blocks x 11 rows x 4 columns
-        const int i = lane + 64 * k;
-        const int sb = i / 44, e = i - sb * 44;
-        if (sb >= nsb) continue;
-        const int fx = sbmv[l][sb][0] & 15;
-        const int r = e >> 2, c = e & 3;
-        const int16_t *src = lwin + sb * AWS * AWS + r * AWS + c;
-        int sum = 0;
-#pragma unroll
-        for (int u = 1; u < 7; u++) sum += src[u] * x_luma4x4[fx][u];
-        hmid[i] = (int16_t)((sum + off1) >> sh1);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int i = lane + 64 * k;
-      if (i >= w * h) continue;
-      const int y = i / w, x = i - y * w;
-      const int sb = (y >> 2) * nsx + (x >> 2);
-      const int fx = sbmv[l][sb][0] & 15, fy = sbmv[l][sb][1] & 15;
-      int v;
-      {
-        const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
-        const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
-        const int16_t *col = hmid + sb * 44 + (y & 3) * 4 + (x & 3);
-        int sum = 0;
-#pragma unroll
-        for (int t = 1; t < 7; t++) sum += col[t * 4] * x_luma4x4[fy][t];
-        v = (int)(int16_t)((sum + off2) >> sh2);
-        if (rnd) v = clampi(v, 0, maxv);
-      }
-      res[0][l][k] = v;
-      if (prof) c14[y * 16 + x] = (int16_t)v;
-    }
-    __syncthreads();   // hmid is reused by the other list
-    if (prof) {
-      __syncthreads();
-      // PROF (:1209-1251): ring of integer samples, gradients (shift 6), dMv per position, applyPROFCore
-      const int dILimit = 1 << max(bd + 1, 13);
-      const int shiftNum = headRoom, offset = (1 << (shiftNum - 1)) + IF_INTERNAL_OFFS;
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int i = lane + 64 * k;
-        if (i >= w * h) continue;
-        const int y = i / w, x = i - y * w;
-        const int sb = (y >> 2) * nsx + (x >> 2);
-        const int fx = sbmv[l][sb][0] & 15, fy = sbmv[l][sb][1] & 15;
-        const int xo = fx >> 3, yo = fy >> 3;
-        const int px = x & 3, py = y & 3;
-        const int16_t *sw = lwin + sb * AWS * AWS;
-        auto ext = [&](int ex, int ey) -> int {   // dstExt value at sub-block position (ex, ey) in [-1,4]
-          if (ex >= 0 && ex < 4 && ey >= 0 && ey < 4) return c14[(y - py + ey) * 16 + (x - px + ex)];
-          const int s = sw[(3 + ey + yo) * AWS + 3 + ex + xo];
-          return (int16_t)((s << headRoom) - IF_INTERNAL_OFFS);
-        };
-        const int gX = (ext(px + 1, py) >> 6) - (ext(px - 1, py) >> 6);
-        const int gY = (ext(px, py + 1) >> 6) - (ext(px, py - 1) >> 6);
-        int dmx = 4 * A.dhx * px + 4 * A.dvx * py - 6 * A.dhx - 6 * A.dvx;
-        int dmy = 4 * A.dhy * px + 4 * A.dvy * py - 6 * A.dhy - 6 * A.dvy;
-        round_affine(dmx, dmy, 8);
-        dmx = clampi(dmx, -31, 31);
-        dmy = clampi(dmy, -31, 31);
-        const int dI = clampi(dmx * gX + dmy * gY, -dILimit, dILimit - 1);
-        int v = (int16_t)(c14[y * 16 + x] + dI);
-        if (!bi && !U.wp) v = clampi((v + offset) >> shiftNum, 0, maxv);
-        res[0][l][k] = v;
-      }
-      __syncthreads();   // c14 is reused by the other list
-    }
-    // ---- chroma
-#pragma unroll
-    for (int comp = 1; comp < 3; comp++) {
-      if (lane < cw * chh) {
-        const int16_t *cwin = win + 2 * ALW + l * 2 * ACW + (comp - 1) * ACW;
-        const int y = lane / cw, x = lane - y * cw;
-        const int sb = (y >> 2) * ncx + (x >> 2);
-        const int fx = csmv[l][sb][0] & 31, fy = csmv[l][sb][1] & 31;
-        res[comp][l][0] = filt2d<4>(cwin + sb * 49, 7, x & 3, y & 3, x_chroma[fx], x_chroma[fy], !bi && !U.wp, bd);
-      }
-    }
-  }
-  // ---- combine (xWeightedAverage: addAvg / addWeightedAvg; weighted prediction; uni already final without WP)
-#pragma unroll
-  for (int comp = 0; comp < 3; comp++) {
-    const int cs = comp ? 1 : 0;
-    const int bw = w >> cs, bh = h >> cs, bx = J.x >> cs, by = J.y >> cs;
-    const DPlane &o = P.out[comp];
-#pragma unroll
-    for (int k = 0; k < (comp ? 1 : 4); k++) {
-      const int i = lane + 64 * k;
-      if (i >= bw * bh) continue;
-      const int y = i / bw, x = i - y * bw;
-      int v;
-      if (!bi) {
-        const int l = U.l[0].present ? 0 : 1;
-        v = res[comp][l][k];
-        if (U.wp) v = wp_uni(P.wp, l, U.l[l].ridx, comp, v, headRoom, maxv);
-      } else if (U.wp) {
-        v = wp_bi(P.wp, U.l[0].ridx, U.l[1].ridx, comp, res[comp][0][k], res[comp][1][k], headRoom, maxv);
-      } else if (U.bcw != 2) {
-        const int w1 = x_bcw_w1[U.bcw], w0 = 8 - w1;
-        const int shiftNum = headRoom + 3;
-        const int offset = (1 << (shiftNum - 1)) + (IF_INTERNAL_OFFS << 3);
-        v = clampi((res[comp][0][k] * w0 + res[comp][1][k] * w1 + offset) >> shiftNum, 0, maxv);
-      } else {
-        const int shiftNum = headRoom + 1;
-        const int offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
-        v = clampi((res[comp][0][k] + res[comp][1][k] + offset) >> shiftNum, 0, maxv);
-      }
-      o.p[(size_t)(by + y) * o.stride + bx + x] = (int16_t)v;
-    }
-  }
-}
-
 }  // namespace
 
 void launch_mc_bidir(const McParams &p, const McJob *jobs, int njobs, int32_t *dmvr_out, hipStream_t s) {
   if (njobs <= 0) return;
   hipLaunchKernelGGL(k_mc_bidir, dim3(njobs), dim3(64), 0, s, p, jobs, njobs, dmvr_out);
-}
-
-void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const AffPu *pus, hipStream_t s) {
-  if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_mc_affine, dim3(njobs), dim3(64), 0, s, p, jobs, njobs, pus);
 }

@@ -1,0 +1,82 @@
+// vvcr_mcdev.h — device helpers shared by the motion-compensation kernels (gfx950): packed integer FIR
+// on int16 sample pairs with v_dot2c_i32_i16, and the constants of InterpolationFilter.h:48-52.
+#pragma once
+#include "vvcr_internal.h"
+
+namespace mcdev {
+
+constexpr int IF_INTERNAL_PREC = 14;
+constexpr int IF_FILTER_PREC = 6;
+constexpr int IF_INTERNAL_OFFS = 1 << (IF_INTERNAL_PREC - 1);
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+typedef short short2_t __attribute__((ext_vector_type(2)));
+// a.lo * b.lo + a.hi * b.hi + c (signed 16-bit halves)
+__device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, a), __builtin_bit_cast(short2_t, b), c, false);
+}
+__host__ __device__ constexpr uint32_t pk(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
+
+// Packed pair coefficients of an N-tap filter c[0..N): A[k] = (c[2k], c[2k+1]) for an output whose first
+// tap sits on an even sample of the pair sequence, B[k] = (c[2k-1], c[2k]) with c[-1] = c[N] = 0 for one
+// whose first tap sits on an odd sample. Either way every operand is an aligned dword of sample pairs.
+template <int N>
+struct Taps {
+  uint32_t A[N / 2], B[N / 2 + 1];
+};
+template <int N, class T>
+__host__ __device__ constexpr Taps<N> make_taps(const T *c) {
+  Taps<N> t{};
+  for (int k = 0; k < N / 2; k++) t.A[k] = pk(c[2 * k], c[2 * k + 1]);
+  t.B[0] = pk(0, c[0]);
+  for (int k = 1; k < N / 2; k++) t.B[k] = pk(c[2 * k - 1], c[2 * k]);
+  t.B[N / 2] = pk(c[N - 1], 0);
+  return t;
+}
+
+// Four consecutive outputs from aligned sample pairs w[]: output j's first tap is element PAR + j.
+template <int N, int PAR>
+__device__ __forceinline__ void fir4(const uint32_t *w, const Taps<N> &t, int (&o)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const int e = PAR + j;
+    int s = 0;
+    if ((e & 1) == 0) {
+#pragma unroll
+      for (int k = 0; k < N / 2; k++) s = dot2(w[e / 2 + k], t.A[k], s);
+    } else {
+#pragma unroll
+      for (int k = 0; k < N / 2 + 1; k++) s = dot2(w[(e - 1) / 2 + k], t.B[k], s);
+    }
+    o[j] = s;
+  }
+}
+// The same with a lane-dependent parity par (0 / 1); reads w[0 .. N/2 + 1].
+template <int N>
+__device__ __forceinline__ void fir4_var(const uint32_t *w, const Taps<N> &t, int par, int (&o)[4]) {
+  uint32_t u[N / 2 + 1];
+#pragma unroll
+  for (int k = 0; k < N / 2 + 1; k++) u[k] = par ? w[k + 1] : w[k];
+  int ea[2], eb[2];      // A over u (outputs with an even first tap), B over w (odd first tap)
+#pragma unroll
+  for (int m = 0; m < 2; m++) {
+    int s = 0;
+#pragma unroll
+    for (int k = 0; k < N / 2; k++) s = dot2(u[m + k], t.A[k], s);
+    ea[m] = s;
+    s = 0;
+#pragma unroll
+    for (int k = 0; k < N / 2 + 1; k++) s = dot2(w[m + k], t.B[k], s);
+    eb[m] = s;
+  }
+  o[0] = par ? eb[0] : ea[0];
+  o[1] = par ? ea[0] : eb[0];
+  o[2] = par ? eb[1] : ea[1];
+  o[3] = par ? ea[1] : eb[1];
+}
+
+__device__ __forceinline__ int lo16(uint32_t v) { return (int16_t)(v & 0xffff); }
+__device__ __forceinline__ int hi16(uint32_t v) { return (int16_t)(v >> 16); }
+
+}  // namespace mcdev
