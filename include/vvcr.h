@@ -136,7 +136,17 @@ typedef struct vvcr_pic_params {
   int32_t num_tile_cols, num_tile_rows;
   int32_t tile_col_bd[VVCR_MAX_TILE_LINES + 1], tile_row_bd[VVCR_MAX_TILE_LINES + 1];
   int32_t entropy_sync;        /* WPP (pps entropy_coding_sync): not supported, rejected */
+  /* Spatial shard (multi-GPU): luma rows [shard_y0, shard_y1) of the picture, on tile-row
+   * boundaries; shard_y1 = 0 means the whole picture. Reconstruction covers the CUs of the shard only.
+   * The loop-filter stages then produce the final samples of the shard's rows and need, in the picture
+   * slot, the reconstructed (pre-deblocking, post-LMCS-inverse) samples of the VVCR_LF_HALO luma rows
+   * above and below the shard (the neighbours' rows: vvcr_import_rows) and the descriptors of the CUs
+   * there (they are part of the submitted picture). Motion compensation reads reference rows within
+   * the picture's reach (vvcr_picture_work_counts counts[8..9]); they must be present in the slots. */
+  int32_t shard_y0, shard_y1;
 } vvcr_pic_params;
+
+#define VVCR_LF_HALO 24   /* luma rows (chroma: 12) of pre-deblocking samples a shard's loop filters read */
 
 /* ALF / CC-ALF filters of the picture (AdaptiveLoopFilter::reconstructCoeffAPSs result,
  * AdaptiveLoopFilter.cpp:620) and per-CTB control (Picture.h:265-297). */
@@ -203,7 +213,9 @@ int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle);
  * work lists into a prepared-picture handle of ctx; it may be called from several threads at once
  * (each with its own picture). pp->slot / ref_slot are checked against sp->dpb_slots.
  *   vvcr_picture_work_counts: counts[0..7] = transform blocks, MC blocks, DMVR/BDOF blocks, affine tiles,
- *   inter recon tiles, intra steps, deblocking segments, DMVR sub-blocks (diagnostics); returns 8. */
+ *   inter recon tiles, intra steps, deblocking segments, DMVR sub-blocks; counts[8..9] = the first and
+ *   one past the last luma row of the reference pictures the motion compensation reads (0, 0 without
+ *   inter blocks); returns 10. */
 typedef struct vvcr_picture vvcr_picture;
 int vvcr_picture_create(const vvcr_seq_params *sp, const vvcr_pic_params *pp, vvcr_picture **out);
 int vvcr_picture_submit(vvcr_picture *pic,
@@ -219,6 +231,16 @@ int vvcr_picture_work_counts(const vvcr_picture *pic, int64_t *counts, int32_t n
 const char *vvcr_picture_last_error(const vvcr_picture *pic);
 int vvcr_picture_destroy(vvcr_picture *pic);
 int vvcr_prepare_planned(vvcr_ctx *ctx, const vvcr_picture *pic, int32_t *handle);
+
+/* Halo exchange of a spatial shard: copy luma rows [y0, y0 + n) of DPB slot and the co-located chroma
+ * rows [y0 / 2, (y0 + n) / 2) of Cb and Cr (y0, n even) to / from a packed DEVICE buffer of
+ * vvcr_rows_bytes(ctx, n) bytes: n luma rows of `width` int16 samples, then the Cb rows, then the Cr
+ * rows. Export waits for the slot's last writer; import waits for its writer and readers; both return
+ * once the copy is complete, so the caller may hand the buffer to a collective (RCCL) right away and
+ * later launches see the imported rows. */
+int64_t vvcr_rows_bytes(const vvcr_ctx *ctx, int32_t n);
+int vvcr_export_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, void *dev_dst);
+int vvcr_import_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, const void *dev_src);
 
 /* Per-kernel-group statistics of the last launch of a picture (handle 0 = the last launched picture):
  * HIP-event time on the library stream, number of kernel launches in the group and the algorithmic

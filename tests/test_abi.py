@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_header_and_library_agree():
     hdr = open(os.path.join(ROOT, "include", "vvcr.h")).read()
-    declared = set(re.findall(r"^(?:int|const char \*|void \*)\s*(vvcr_\w+)\(", hdr, re.M))
+    declared = set(re.findall(r"^(?:int|int64_t|const char \*|void \*)\s*(vvcr_\w+)\(", hdr, re.M))
     assert declared == set(N.EXPORTS)
     out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True, check=True).stdout
     exported = set(re.findall(r" T (vvcr_\w+)", out))

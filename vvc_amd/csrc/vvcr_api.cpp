@@ -194,6 +194,7 @@ struct vvcr_ctx {
   vvcr_seq_params sp{};
   std::string err;
   hipStream_t stream = nullptr;      // lane 0's stream (host copies, vvcr_stream)
+  hipStream_t copy_stream = nullptr; // halo row export / import (vvcr_export_rows / vvcr_import_rows)
   std::vector<std::array<DPlane, 3>> dpb;
   Lane lanes[MAXLANE];
   int nlane = 4, nintra = 2;         // lanes; the first nintra take pictures without references
@@ -473,6 +474,12 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   Lane &ln = ctx->lanes[L];
   hipStream_t s = ln.s;
   r.lane = L;
+  // rows: a spatial shard reconstructs and filters its own rows; its SAO also covers the 8 rows around
+  // them that its ALF reads (their deblocked inputs come from the VVCR_LF_HALO rows the caller imported)
+  const int H = ctx->sp.height;
+  const bool shard = pp.shard_y1 > 0;
+  const int own0 = shard ? pp.shard_y0 : 0, own1 = shard ? pp.shard_y1 : H;
+  const int sao0 = shard ? std::max(0, own0 - 8) : 0, sao1 = shard ? std::min(H, own1 + 8) : H;
   ln.tail_slot = pp.slot;
   ln.tail_seq = ++ctx->seq;
   // dependencies on pictures of other lanes (same-lane work is ordered by the stream anyway)
@@ -486,6 +493,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     KernelTimer t(r, K_RESID, s, ctx->timing);
     Planes3 clr{};
     for (int c = 0; c < 3; c++) clr.dst[c] = ln.resi[c];
+    clr.y0 = own0; clr.y1 = own1;
     launch_planes3(clr, s);
     TbParams tp{};
     for (int c = 0; c < 3; c++) tp.out[c] = ln.resi[c];
@@ -535,7 +543,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   }
   auto &A = ctx->dpb[pp.slot];
   if ((mask & VVCR_STAGE_LMCS_INV) && pp.lmcs_enabled) {
-    launch_lmcs_inverse(A[0], r.lmcs_lut.p + 1024, s);   // back to the original domain before the loop filters
+    launch_lmcs_inverse(A[0], r.lmcs_lut.p + 1024, own0, own1, s);   // back to the original domain before the loop filters
     VVCR_CHECK_HIP(hipGetLastError());
   }
   if ((mask & VVCR_STAGE_DBK) && (r.dbk_counts[0] + r.dbk_counts[1] + r.dbk_counts[2] + r.dbk_counts[3])) {
@@ -557,6 +565,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     SaoParams sp{};
     for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ln.tmp[c]; }
     sp.sao = r.sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
+    sp.y0 = sao0; sp.y1 = sao1;
     launch_sao(sp, s);
     VVCR_CHECK_HIP(hipGetLastError());
     inTmp = true;
@@ -574,6 +583,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     ap.chroma_coef = r.alf_chroma.p; ap.chroma_clip = r.alf_chroma.p + 56; ap.cc_coef = r.alf_cc.p;
     ap.ctb_en = r.alf_ctb.p; ap.ctb_alt = r.alf_ctb.p + 3 * n; ap.cc_ctl = r.alf_ctb.p + 6 * n;
     ap.ctb_set = r.alf_set.p;
+    ap.y0 = own0; ap.y1 = own1;
     launch_alf(ap, s);
     VVCR_CHECK_HIP(hipGetLastError());
     inTmp = !inTmp;
@@ -583,6 +593,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     Planes3 cp{};
     for (int c = 0; c < 3; c++) { cp.dst[c] = A[c]; cp.src[c] = ln.tmp[c]; }
     cp.copy = 1;
+    cp.y0 = own0; cp.y1 = own1;
     launch_planes3(cp, s);
   }
   VVCR_CHECK_HIP(hipEventRecord(r.done, s));
@@ -618,6 +629,7 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     if (const char *e = getenv("VVCR_INTRA_LANES")) ctx->nintra = std::max(1, std::min(ctx->nlane - 1, atoi(e)));
     for (int l = 0; l < ctx->nlane; l++) VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->lanes[l].s, hipStreamNonBlocking));
     ctx->stream = ctx->lanes[0].s;
+    VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
     const int W = sp->width, H = sp->height;
     ctx->dpb.resize(sp->dpb_slots);
     for (auto &s : ctx->dpb) {
@@ -672,6 +684,7 @@ int vvcr_destroy(vvcr_ctx *ctx) {
     for (auto &e : a) if (e) (void)hipEventDestroy(e);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   for (int l = 0; l < ctx->nlane; l++) (void)hipStreamDestroy(ctx->lanes[l].s);
+  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;
   return VVCR_OK;
 }
@@ -915,11 +928,11 @@ int vvcr_picture_plan(vvcr_picture *pic, uint32_t stage_mask) {
 int vvcr_picture_work_counts(const vvcr_picture *pic, int64_t *counts, int32_t n) {
   if (!pic || (!counts && n)) return VVCR_E_ARG;
   if (!pic->planned) return VVCR_E_STATE;
-  const int64_t v[8] = {(int64_t)pic->wl.tb.size(), (int64_t)pic->wl.mc_basic.size(), (int64_t)pic->wl.mc_bidir.size(),
-                        (int64_t)pic->wl.aff_jobs.size(), (int64_t)pic->intra.inter_tiles.size(), (int64_t)pic->intra.jobs.size(),
-                        (int64_t)pic->dbk.total(), (int64_t)pic->wl.n_dmvr};
-  for (int k = 0; k < n && k < 8; k++) counts[k] = v[k];
-  return 8;
+  const int64_t v[10] = {(int64_t)pic->wl.tb.size(), (int64_t)pic->wl.mc_basic.size(), (int64_t)pic->wl.mc_bidir.size(),
+                         (int64_t)pic->wl.aff_jobs.size(), (int64_t)pic->intra.inter_tiles.size(), (int64_t)pic->intra.jobs.size(),
+                         (int64_t)pic->dbk.total(), (int64_t)pic->wl.n_dmvr, pic->wl.ref_y0, pic->wl.ref_y1};
+  for (int k = 0; k < n && k < 10; k++) counts[k] = v[k];
+  return 10;
 }
 
 const char *vvcr_picture_last_error(const vvcr_picture *pic) { return pic ? pic->err.c_str() : g_create_error.c_str(); }
@@ -1062,6 +1075,52 @@ int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n) {
     VVCR_CHECK_HIP(hipStreamSynchronize(s));
   }
   return cnt;
+  API_END
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Halo exchange of spatial shards (include/vvcr.h): rows of a DPB slot <-> packed device buffer
+// ---------------------------------------------------------------------------------------------------
+int64_t vvcr_rows_bytes(const vvcr_ctx *ctx, int32_t n) {
+  if (!ctx || n < 0) return VVCR_E_ARG;
+  const int64_t W = ctx->sp.width;
+  return (int64_t)n * W * 2 + 2 * (int64_t)(n / 2) * (W / 2) * 2;
+}
+
+static void rows_copy(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, char *dev, bool to_slot) {
+  if (slot < 0 || slot >= (int)ctx->dpb.size()) throw VvcrError(VVCR_E_ARG, "bad slot");
+  if (y0 < 0 || n <= 0 || (y0 | n) & 1 || y0 + n > ctx->sp.height) throw VvcrError(VVCR_E_ARG, "rows outside the picture (y0, n even)");
+  if (!dev) throw VvcrError(VVCR_E_ARG, "null buffer");
+  hipStream_t cs = ctx->copy_stream;
+  if (ctx->slot_w_set[slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(cs, ctx->slot_w[slot], 0));
+  if (to_slot)   // write after read: every lane's last reader of the slot
+    for (int l = 0; l < ctx->nlane; l++)
+      if (ctx->slot_r_set[slot] >> l & 1) VVCR_CHECK_HIP(hipStreamWaitEvent(cs, ctx->slot_r[slot][l], 0));
+  for (int c = 0; c < 3; c++) {
+    const DPlane &pl = ctx->dpb[slot][c];
+    const int s = c ? 1 : 0, r0 = y0 >> s, nr = n >> s;
+    int16_t *plane = pl.p + (size_t)r0 * pl.stride;
+    const size_t rowb = (size_t)pl.w * 2;
+    if (to_slot) VVCR_CHECK_HIP(hipMemcpy2DAsync(plane, pl.stride * 2, dev, rowb, rowb, nr, hipMemcpyDeviceToDevice, cs));
+    else VVCR_CHECK_HIP(hipMemcpy2DAsync(dev, rowb, plane, pl.stride * 2, rowb, nr, hipMemcpyDeviceToDevice, cs));
+    dev += rowb * nr;
+  }
+  VVCR_CHECK_HIP(hipStreamSynchronize(cs));
+}
+
+int vvcr_export_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, void *dev_dst) {
+  if (!ctx) return VVCR_E_ARG;
+  API_BEGIN
+  rows_copy(ctx, slot, y0, n, (char *)dev_dst, false);
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_import_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, const void *dev_src) {
+  if (!ctx) return VVCR_E_ARG;
+  API_BEGIN
+  rows_copy(ctx, slot, y0, n, (char *)dev_src, true);
+  return VVCR_OK;
   API_END
 }
 

@@ -376,15 +376,21 @@ struct Planner {
       std::vector<int> pos(start);
       for (int i = 0; i < ncu; i++) order[pos[ctu_of[i]]++] = i;
     }
+    // a shard plans the edges of the CUs within VVCR_LF_HALO rows of its own rows: its loop filters
+    // rebuild the deblocked samples the SAO / ALF of its rows read (see vvcr.h)
+    const bool shard = pp.shard_y1 > 0;
+    const int ly0 = pp.shard_y0 - VVCR_LF_HALO, ly1 = pp.shard_y1 + VVCR_LF_HALO;
     for (int dir = 0; dir < 2; dir++)
       for (int k = 0; k < wc * hc; k++) {
         ctu_x = (k % wc) * ctu;
         ctu_y = (k / wc) * ctu;
+        if (shard && (ctu_y + ctu <= ly0 || ctu_y >= ly1)) continue;
         for (int pass = 0; pass < (pp.dual_tree ? 2 : 1); pass++) {
           reset(dir);
           for (int j = start[k]; j < start[k + 1]; j++) {
             const int i = order[j];
             if (pp.dual_tree && d.cu[i].chtype != pass) continue;
+            if (shard && !cu_in_rows(d.cu[i], ly0, ly1)) continue;
             deblock_cu(i, dir);
           }
         }

@@ -123,6 +123,19 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
   for (const vvcr_cu &c : d.cu) multiSlice |= c.slice != (ncu ? d.cu[0].slice : 0);
   if (multiSlice && !pp.lf_across_slices) throw VvcrError(VVCR_E_UNSUPPORTED, "slices without loop filtering across slice boundaries");
   if (pp.entropy_sync) throw VvcrError(VVCR_E_UNSUPPORTED, "wavefront parallel processing (entropy coding sync)");
+  if (pp.shard_y1 > 0) {
+    // a shard is a run of whole tile rows: intra prediction and CABAC stop at its edges, so its
+    // reconstruction needs nothing from the other shards (the loop filters do: VVCR_LF_HALO)
+    auto on_tile_row = [&](int y) {
+      if (y == 0 || y == sp.height) return true;
+      if (y % ctu) return false;
+      for (int t = 0; t <= pp.num_tile_rows; t++) if (pp.tile_row_bd[t] * ctu == y) return true;
+      return false;
+    };
+    if (pp.shard_y0 < 0 || pp.shard_y0 >= pp.shard_y1 || pp.shard_y1 > sp.height || !on_tile_row(pp.shard_y0) ||
+        !on_tile_row(pp.shard_y1))
+      fail("shard rows must be a run of whole tile rows");
+  }
 }
 
 void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, std::vector<TbJob> &out);
@@ -208,9 +221,14 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   std::vector<int> geo_of(d.cu.size(), -1);
   for (size_t g = 0; g < d.geo.size(); g++)
     if (d.geo[g].cu >= 0 && d.geo[g].cu < (int)d.cu.size()) geo_of[d.geo[g].cu] = (int)g;
+  int ry0 = 1 << 30, ry1 = -(1 << 30);   // reference rows read (luma), with filter / DMVR / BDOF margins
+  auto reach = [&](int y, int h, int mvy) {
+    ry0 = std::min(ry0, y + (mvy >> 4) - 8);
+    ry1 = std::max(ry1, y + h + (mvy >> 4) + 9);
+  };
   for (size_t ci = 0; ci < d.cu.size(); ci++) {
     const vvcr_cu &c = d.cu[ci];
-    if (c.predmode != MODE_INTER || !c.yvalid) continue;
+    if (c.predmode != MODE_INTER || !c.yvalid || !in_shard(pp, c)) continue;
     if (c.geo) {
       // motionCompensationGeo (InterPrediction.cpp:1749): two uni candidates at 14 bits, blended
       const vvcr_pu &p = d.pu[c.firstpu];
@@ -262,6 +280,13 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
         if (p.interdir & 1) U.l[0] = affine_list(pp, c, p, 0);
         if (p.interdir & 2) U.l[1] = affine_list(pp, c, p, 1);
         U.wp = wp_applies(pp, p.interdir == 3, c.bcw) ? 1 : 0;
+        for (int l = 0; l < 2; l++) {   // the sub-block MVs lie within the model's values at the PU corners
+          if (!U.l[l].present) continue;
+          const AffList &A = U.l[l];
+          for (int cy = 0; cy <= 1; cy++)
+            for (int cx = 0; cx <= 1; cx++) reach(p.y + cy * p.h, 0, (A.mvy + A.dhy * cx * p.w + A.dvy * cy * p.h) >> 7);
+          reach(p.y, p.h, A.mvy >> 7);
+        }
         const int idx = (int)wl.aff_pu.size();
         wl.aff_pu.push_back(U);
         for (int y = 0; y < p.h; y += 16)
@@ -300,6 +325,14 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       set_wp(pp, j, p.ref0, p.ref1, c.bcw);   // the CU's BcwIdx, not the CIIP-cleared one (:664 reads pu.cu->BcwIdx)
       push_tiles(wl.mc_basic, p.x, p.y, p.w, p.h, j);
     }
+  }
+  for (const std::vector<McJob> *v : {&wl.mc_basic, &wl.mc_bidir})
+    for (const McJob &j : *v)
+      for (int l = 0; l < 2; l++)
+        if (j.flags & (l ? MC_L1 : MC_L0)) reach(j.y, j.h, j.mv[l][1]);
+  if (ry0 <= ry1) {
+    wl.ref_y0 = std::max(0, ry0);
+    wl.ref_y1 = std::min(sp.height, ry1);
   }
 }
 
@@ -420,6 +453,7 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
   static const int kIct[2][4] = {{0, 3, 1, 2}, {0, -3, -1, -2}};
   for (const vvcr_tu &t : d.tu) {
     const vvcr_cu &cu = d.cu[t.cu];
+    if (!in_shard(pp, cu)) continue;
     const bool sepTree = cu.treetype != 0 || pp.dual_tree;
     for (int comp = 0; comp < 3; comp++) {
       const int32_t *b = t.b[comp];

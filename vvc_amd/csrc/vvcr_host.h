@@ -22,9 +22,10 @@ struct WorkLists {
   int tb_small = 0;
   int n_dmvr = 0;                  // DMVR sub-blocks (delta outputs), in PU order
   int n_unsupported_inter = 0;     // PUs needing kernels not built yet (reported, never silently skipped)
+  int ref_y0 = 0, ref_y1 = 0;      // luma rows of the reference pictures the MC jobs read (with margins)
   void clear() {
     mc_basic.clear(); mc_bidir.clear(); aff_pu.clear(); aff_jobs.clear(); tb.clear();
-    n_dmvr = 0; n_unsupported_inter = 0; tb_small = 0;
+    n_dmvr = 0; n_unsupported_inter = 0; tb_small = 0; ref_y0 = ref_y1 = 0;
   }
 };
 
@@ -40,3 +41,13 @@ void build_scan_tables(ScanTables &st);
 // Throws VvcrError on inconsistent descriptors (indices out of range, blocks outside the picture).
 void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d);
 void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl);
+
+// Spatial shard of a picture (vvcr_pic_params::shard_y0 / shard_y1): whether a CU is reconstructed by
+// this shard (its luma position lies in the shard rows), and the rows whose deblocking edges it plans.
+inline bool cu_in_rows(const vvcr_cu &c, int y0, int y1) {
+  const int y = c.yvalid ? c.y : 2 * c.cy, h = c.yvalid ? c.h : 2 * c.ch;
+  return y + h > y0 && y < y1;
+}
+inline bool in_shard(const vvcr_pic_params &pp, const vvcr_cu &c) {
+  return pp.shard_y1 <= 0 || cu_in_rows(c, pp.shard_y0, pp.shard_y1);
+}

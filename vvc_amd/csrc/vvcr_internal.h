@@ -154,6 +154,7 @@ struct SaoParams {
   DPlane src[3], dst[3];
   const int32_t *sao;          // [nctb][3][35] vvcr_sao rows
   int32_t bd, ctu, wc;
+  int32_t y0, y1;              // luma rows processed (chroma: halves); the picture edges stay the edges
 };
 
 struct AlfParams {
@@ -165,11 +166,13 @@ struct AlfParams {
   const int16_t *cc_coef;                   // [2][4][8]
   const uint8_t *ctb_en, *ctb_alt, *cc_ctl;
   const int16_t *ctb_set;
+  int32_t y0, y1;              // luma rows processed (multiple of 16; chroma: halves)
 };
 
 struct Planes3 {
   DPlane dst[3], src[3];
   int32_t copy;                // 0: clear dst, 1: dst <- src (same sizes)
+  int32_t y0, y1;              // luma rows (chroma: halves)
 };
 
 // ------------------------------------------------------------------------------------------------

@@ -104,7 +104,7 @@ struct IntraParams {
 void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out);
 void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s);
 // LMCS inverse luma mapping of the reconstructed picture before deblocking (DecLib.cpp:574)
-void launch_lmcs_inverse(const DPlane &luma, const int16_t *inv_lut, hipStream_t s);
+void launch_lmcs_inverse(const DPlane &luma, const int16_t *inv_lut, int y0, int y1, hipStream_t s);
 // all steps of a picture in one persistent launch, one CTU per workgroup at a time; state: 16 + n int32
 // (reset here); *err set on a wait timeout
 void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *ctu_list, const int32_t *ctu_start,

@@ -1164,8 +1164,8 @@ __global__ void k_recon_inter(IntraParams P, const ReconTile *__restrict__ tiles
 
 // LMCS inverse luma mapping of the whole reconstructed picture (DecLib.cpp:574 rspSignal(invLUT)), in place,
 // 8 samples per lane
-__global__ void k_lmcs_inverse(DPlane L, const int16_t *__restrict__ inv) {
-  const int q = L.w >> 3, y = blockIdx.y, qx = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void k_lmcs_inverse(DPlane L, const int16_t *__restrict__ inv, int y0) {
+  const int q = L.w >> 3, y = y0 + blockIdx.y, qx = blockIdx.x * blockDim.x + threadIdx.x;
   if (qx >= q) return;
   int16_t *row = L.p + (size_t)y * L.stride + qx * 8;
 #pragma unroll
@@ -1173,9 +1173,10 @@ __global__ void k_lmcs_inverse(DPlane L, const int16_t *__restrict__ inv) {
 }
 }  // namespace
 
-void launch_lmcs_inverse(const DPlane &luma, const int16_t *inv_lut, hipStream_t s) {
+void launch_lmcs_inverse(const DPlane &luma, const int16_t *inv_lut, int y0, int y1, hipStream_t s) {
+  if (y1 <= y0) return;
   const int q = luma.w >> 3;
-  hipLaunchKernelGGL(k_lmcs_inverse, dim3((q + 63) / 64, luma.h), dim3(64), 0, s, luma, inv_lut);
+  hipLaunchKernelGGL(k_lmcs_inverse, dim3((q + 63) / 64, y1 - y0), dim3(64), 0, s, luma, inv_lut, y0);
 }
 
 void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s) {

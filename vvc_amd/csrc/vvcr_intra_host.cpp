@@ -426,6 +426,7 @@ struct Planner {
           const int i = order[jx];
           const vvcr_cu &c = d.cu[i];
           if (pp.dual_tree && c.chtype != pass) continue;
+          if (!in_shard(pp, c)) continue;   // another shard reconstructs it (different tile: never read here)
           cur_reg = ctu_reg[k];
           if (c.predmode == MODE_INTER) {
             inter_cu(i);

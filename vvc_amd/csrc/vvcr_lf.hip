@@ -22,9 +22,9 @@ __global__ void k_sao(SaoParams P) {
   const DPlane &D = P.dst[comp];
   const int W = S.w, H = S.h;
   const int qx = blockIdx.x * blockDim.x + threadIdx.x;     // quad index
-  const int y = blockIdx.y;
+  const int y = (comp ? P.y0 >> 1 : P.y0) + blockIdx.y;
   const int x0 = qx * 4;
-  if (x0 >= W || y >= H) return;
+  if (x0 >= W || y >= H || y >= (comp ? P.y1 >> 1 : P.y1)) return;
   const int cs = comp ? P.ctu >> 1 : P.ctu;
   const int ctbRow = y / cs;
   const int maxv = (1 << P.bd) - 1;
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
   const DPlane &D = P.dst[0];
   __shared__ int16_t t[ALF_SH * ALF_SW];
   __shared__ int32_t blk[(ALF_TW / 4) * (ALF_TH / 4)];   // class | transpose << 8 | enabled << 16
-  const int X0 = blockIdx.x * ALF_TW, Y0 = blockIdx.y * ALF_TH;
+  const int X0 = blockIdx.x * ALF_TW, Y0 = P.y0 + blockIdx.y * ALF_TH;
   const int tid = threadIdx.x;
   const int W = S.w, H = S.h;
   {
@@ -223,8 +223,8 @@ __global__ void k_alf_chroma(AlfParams P) {
   const DPlane &S = P.src[comp];
   const DPlane &D = P.dst[comp];
   const DPlane &Y = P.src[0];
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
-  if (x >= S.w || y >= S.h) return;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = (P.y0 >> 1) + blockIdx.y;
+  if (x >= S.w || y >= S.h || y >= (P.y1 >> 1)) return;
   const int cl2 = P.ctu_log2 - 1;
   const int ctb = (y >> cl2) * P.wc + (x >> cl2);
   const int n = P.nctb;
@@ -271,8 +271,9 @@ __global__ void k_alf_chroma(AlfParams P) {
 }  // namespace
 
 void launch_sao(const SaoParams &p, hipStream_t s) {
-  const int W = p.src[0].w, H = p.src[0].h;   // luma bounds; chroma blocks beyond their plane exit
-  dim3 grid(((W + 3) / 4 + 63) / 64, H, 3);
+  const int W = p.src[0].w;   // luma bounds; chroma blocks beyond their rows exit
+  if (p.y1 <= p.y0) return;
+  dim3 grid(((W + 3) / 4 + 63) / 64, p.y1 - p.y0, 3);
   hipLaunchKernelGGL(k_sao, grid, dim3(64), 0, s, p);
 }
 
@@ -281,28 +282,30 @@ void launch_sao(const SaoParams &p, hipStream_t s) {
 __global__ __launch_bounds__(256) void k_planes3(Planes3 P) {
   const int c = blockIdx.z;
   const DPlane &D = P.dst[c];
-  const int y = blockIdx.y, x = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (y >= D.h || x >= D.w) return;
+  const int y = (c ? P.y0 >> 1 : P.y0) + blockIdx.y, x = (blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (y >= D.h || x >= D.w || y >= (c ? P.y1 >> 1 : P.y1)) return;
   // 8 samples (16 B) per lane: planes are 128-B pitched, so the vector stays inside the row
   uint4 *d = (uint4 *)(D.p + (size_t)y * D.stride + x);
   *d = P.copy ? *(const uint4 *)(P.src[c].p + (size_t)y * P.src[c].stride + x) : make_uint4(0, 0, 0, 0);
 }
 
 void launch_planes3(const Planes3 &p, hipStream_t s) {
-  const int W = p.dst[0].w, H = p.dst[0].h;
-  dim3 grid(((W + 7) / 8 + 255) / 256, H, 3);
+  const int W = p.dst[0].w;
+  if (p.y1 <= p.y0) return;
+  dim3 grid(((W + 7) / 8 + 255) / 256, p.y1 - p.y0, 3);
   hipLaunchKernelGGL(k_planes3, grid, dim3(256), 0, s, p);
 }
 
 void launch_alf(const AlfParams &p, hipStream_t s) {
+  if (p.y1 <= p.y0) return;
   {
-    const int W = p.src[0].w, H = p.src[0].h;
-    dim3 grid((W + ALF_TW - 1) / ALF_TW, (H + ALF_TH - 1) / ALF_TH);
+    const int W = p.src[0].w;
+    dim3 grid((W + ALF_TW - 1) / ALF_TW, (p.y1 - p.y0 + ALF_TH - 1) / ALF_TH);
     hipLaunchKernelGGL(k_alf_luma, grid, dim3(256), 0, s, p);
   }
   {
-    const int W = p.src[1].w, H = p.src[1].h;
-    dim3 grid((W + 63) / 64, H, 2);
+    const int W = p.src[1].w;
+    dim3 grid((W + 63) / 64, (p.y1 - p.y0) >> 1, 2);
     hipLaunchKernelGGL(k_alf_chroma, grid, dim3(64), 0, s, p);
   }
 }

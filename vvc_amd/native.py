@@ -45,6 +45,7 @@ class PicParams(C.Structure):
         ("num_tile_cols", I32), ("num_tile_rows", I32),
         ("tile_col_bd", I32 * (MAX_TILE_LINES + 1)), ("tile_row_bd", I32 * (MAX_TILE_LINES + 1)),
         ("entropy_sync", I32),
+        ("shard_y0", I32), ("shard_y1", I32),
     ]
 
 
@@ -106,6 +107,10 @@ def lib():
         L.vvcr_picture_last_error.restype = C.c_char_p
         L.vvcr_picture_destroy.argtypes = [P]
         L.vvcr_prepare_planned.argtypes = [P, P, C.POINTER(I32)]
+        L.vvcr_rows_bytes.argtypes = [P, I32]
+        L.vvcr_rows_bytes.restype = C.c_int64
+        L.vvcr_export_rows.argtypes = [P, I32, I32, I32, P]
+        L.vvcr_import_rows.argtypes = [P, I32, I32, I32, P]
         _lib = L
     return _lib
 
@@ -120,7 +125,8 @@ EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_release_picture"
            "vvcr_last_stage_times", "vvcr_stream", "vvcr_rd_plan", "vvcr_rd_run", "vvcr_fwd_plan", "vvcr_fwd_run",
            "vvcr_rdo_release", "vvcr_rd_dist", "vvcr_fwd_transform", "vvcr_set_timing",
            "vvcr_picture_create", "vvcr_picture_submit", "vvcr_picture_set_loop_filter_params", "vvcr_picture_plan",
-           "vvcr_picture_work_counts", "vvcr_picture_last_error", "vvcr_picture_destroy", "vvcr_prepare_planned"]
+           "vvcr_picture_work_counts", "vvcr_picture_last_error", "vvcr_picture_destroy", "vvcr_prepare_planned",
+           "vvcr_rows_bytes", "vvcr_export_rows", "vvcr_import_rows"]
 
 # encoder RDO block descriptors (include/vvcr.h vvcr_rd_block / vvcr_fwd_block) as numpy record types
 RD_BLOCK = [("org_off", "<i8"), ("cur_off", "<i8"), ("org_stride", "<i4"), ("cur_stride", "<i4"), ("width", "<i4"),
@@ -168,11 +174,12 @@ class Picture:
         self._chk(self.L.vvcr_picture_plan(self.h, stages), "vvcr_picture_plan")
 
     def work_counts(self):
-        c = (C.c_int64 * 8)()
-        n = self.L.vvcr_picture_work_counts(self.h, c, 8)
+        c = (C.c_int64 * 10)()
+        n = self.L.vvcr_picture_work_counts(self.h, c, 10)
         if n < 0:
             self._chk(n, "vvcr_picture_work_counts")
-        return dict(zip(("tb", "mc", "mc_bidir", "affine", "recon_tiles", "intra_steps", "dbk_segments", "dmvr"), list(c)))
+        return dict(zip(("tb", "mc", "mc_bidir", "affine", "recon_tiles", "intra_steps", "dbk_segments", "dmvr",
+                         "ref_y0", "ref_y1"), list(c)))
 
     def close(self):
         if self.h:
@@ -257,6 +264,16 @@ class Context:
         h = C.c_int32(0)
         self._chk(self.L.vvcr_prepare_planned(self.h, pic.h, C.byref(h)), "vvcr_prepare_planned")
         return h.value
+
+    def rows_bytes(self, n):
+        return self.L.vvcr_rows_bytes(self.h, n)
+
+    def export_rows(self, slot, y0, n, dev_ptr):
+        """luma rows [y0, y0+n) + co-located chroma rows of a DPB slot -> packed device buffer"""
+        self._chk(self.L.vvcr_export_rows(self.h, slot, y0, n, dev_ptr), "vvcr_export_rows")
+
+    def import_rows(self, slot, y0, n, dev_ptr):
+        self._chk(self.L.vvcr_import_rows(self.h, slot, y0, n, dev_ptr), "vvcr_import_rows")
 
     def launch(self, handle):
         self._chk(self.L.vvcr_launch_picture(self.h, handle), "vvcr_launch_picture")

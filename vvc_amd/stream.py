@@ -111,8 +111,13 @@ def pic_params(p, slot, slot_of, missing_ref_slot=None):
 def plan_picture(p, slot, slot_of, dpb_slots=32, stages=N.STAGE_ALL):
     """Host-only planning of one parsed picture (vvcr_picture_*): returns a planned N.Picture. Runs
     without a device; safe to call for several pictures on several threads."""
+    return plan_picture_pp(p, pic_params(p, slot, slot_of), dpb_slots, stages)
+
+
+def plan_picture_pp(p, pp, dpb_slots=32, stages=N.STAGE_ALL):
+    """plan_picture with explicit picture parameters (e.g. a spatial shard's rows)"""
     h = p["hdr"]
-    pic = N.Picture(h["width"], h["height"], pic_params(p, slot, slot_of), bit_depth=h["bitdepth_y"],
+    pic = N.Picture(h["width"], h["height"], pp, bit_depth=h["bitdepth_y"],
                     ctu_log2=h["ctu_log2"], dpb_slots=dpb_slots)
     submit(pic, p)
     set_loop_filter_params(pic, p)
