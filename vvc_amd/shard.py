@@ -19,6 +19,9 @@ point-to-point: nccl = RCCL on ROCm with device buffers, or gloo with host buffe
 emulated inside one process, each with its own context, e.g. on a one-GPU box).
 """
 import numpy as np
+# torch before any libvvcr context: torch's HIP runtime must be the process's first (a HIP runtime loaded
+# after libvvcr initialised the system one sees no GPU)
+import torch  # noqa: F401
 
 from . import native as N
 from . import stream as S
