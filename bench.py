@@ -32,6 +32,7 @@ import sys
 import time
 
 import numpy as np
+import torch  # noqa: F401  (before any libvvcr context: torch's HIP runtime must load first)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -62,6 +63,63 @@ def cpu_baseline(stream_bin, pixels_per_run, min_seconds=10.0, max_runs=40):
     return {"value": round(pixels_per_run * runs / total / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "reference",
             "sample": "VTM-7.3 DecoderApp (x86 SIMD, 1 thread) decoding %s.bin %d times (%.1f s), parse + reconstruction"
                       % (os.path.basename(stream_bin)[:-4], runs, total)}
+
+
+def shard_bench(a, R):
+    """BASELINE config 4: one tile-row stream decoded by all ranks together, each rank reconstructing and
+    filtering its own rows (vvc_amd/shard.py) and exchanging only the loop-filter halo (24 pre-deblocking
+    rows per edge) and the motion-reach rows of reference pictures with its neighbours over RCCL.
+    Strong scaling: the whole job decodes every picture once per step. Checked bit-exact afterwards:
+    rank 0 gathers every rank's rows of each slot's last picture and compares its MD5s."""
+    from vvc_amd import shard as SH
+    d = os.path.join(ROOT, "tests", "golden", a.shard_stream)
+    if not os.path.isdir(d):
+        return None
+    pics = S.load_sequence(d)
+    meta = S.load_meta(d)
+    h0 = pics[0]["hdr"]
+    W, H = h0["width"], h0["height"]
+    slots = 8
+    ctx = N.Context(W, H, bit_depth=h0["bitdepth_y"], ctu_log2=h0["ctu_log2"], dpb_slots=slots,
+                    device=int(os.environ.get("VVCR_DEVICE", R.local)))
+    t0 = time.perf_counter()
+    rk = SH.ShardRank(ctx, pics, R.rank, R.world, slots)
+    t_plan = time.perf_counter() - t0
+    comm = SH.TorchComm(R.device) if R.world > 1 else None
+    M = SH.plan_and_reach([rk], comm)
+    ctx.set_timing(False)
+
+    def step():
+        for i in range(len(pics)):
+            SH.decode_picture(rk, comm, i)
+        ctx.sync()
+    for _ in range(max(1, a.warmup)):
+        step()
+    R.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.shard_steps):
+        step()
+    t1 = time.perf_counter()
+    R.barrier()
+    elapsed = R.max_over_ranks(t1 - t0)
+    owner = {}
+    for i, p in enumerate(pics):
+        owner[rk.slots[i]] = p["hdr"]["poc"]
+    ok = True
+    for slot, poc in sorted(owner.items()):
+        SH.gather_to_root(rk, comm, slot)
+        if R.rank == 0:
+            got = D.plane_md5s([ctx.read_plane(N.BUF_RECO, slot, c) for c in range(3)])
+            ok = ok and got == meta["poc_plane_md5"][str(poc)]
+    rk.release()
+    ctx.close()
+    px = W * H * len(pics) * a.shard_steps
+    heights = [b - y for y, b in rk.rows]
+    return {"value": round(px / elapsed / 1e6, 2), "unit": "Mpixels/s", "n_gpus": R.world, "scaling": "strong",
+            "stream": a.shard_stream, "picture": "%dx%d" % (W, H), "pictures_per_step": len(pics), "steps": a.shard_steps,
+            "ms_per_step": round(elapsed / a.shard_steps * 1e3, 3), "shard_rows": heights, "lf_halo_rows": SH.LF_HALO,
+            "ref_halo_rows": M, "host_plan_s": round(t_plan, 3), "bitexact_vs_reference": bool(ok) if R.rank == 0 else None,
+            "note": "tile-row shards, halo exchange over torch.distributed %s point to point" % (R.dist.get_backend() if R.dist else "-")}
 
 
 def end_to_end(ctx, dec, pics, meta, per, a, copies=4):
@@ -123,6 +181,9 @@ def main():
                     help="host sync after every picture (profiling: kernel durations without overlap)")
     ap.add_argument("--e2e-threads", type=int, default=12,
                     help="host planning threads of the end-to-end pass (0 = skip it)")
+    ap.add_argument("--shard-stream", default="ra4320t_q32",
+                    help="tile-row stream of the spatially sharded pass (BASELINE config 4: 8K, one shard per rank)")
+    ap.add_argument("--shard-steps", type=int, default=3, help="timed steps of the sharded pass (0 = skip it)")
     a = ap.parse_args()
 
     R = V.Ranks()
@@ -299,6 +360,11 @@ def main():
         for hnd in handles:
             ctx.release(hnd)
     dec.close()
+    if a.shard_steps > 0:
+        try:
+            line["shard"] = shard_bench(a, R)
+        except Exception as e:   # reported, never silently dropped: the replica line above stays valid
+            line["shard"] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
     if rank == 0:
         print(json.dumps(line))
     R.close()

@@ -14,7 +14,8 @@ from vvc_amd import stream as S
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name,world", [("ratile416_q32", 2), ("ratile1080_q32", 2), ("ratile1080_q32", 4), ("ratile1080_q32", 9)])
+@pytest.mark.parametrize("name,world", [("ratile416_q32", 2), ("ratile1080_q32", 2), ("ratile1080_q32", 4), ("ratile1080_q32", 9),
+                                        ("ra4320t_q32", 8)])
 def test_sharded_decode_matches_reference_md5(golden_dir, name, world):
     d = os.path.join(golden_dir, name)
     pics = S.load_sequence(d)

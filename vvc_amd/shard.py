@@ -162,10 +162,22 @@ def exchange(rk, comm, lists, slot):
 def decode_picture(rk, comm, i):
     """one picture on one rank (ranks in other processes run the same steps at the same time)"""
     rk.ctx.launch(rk.h_recon[i])
-    exchange(rk, comm, rk.lf_halo(), rk.slots[i])
+    if rk.world > 1:
+        exchange(rk, comm, rk.lf_halo(), rk.slots[i])
     rk.ctx.launch(rk.h_lf[i])
-    if rk.ref_later[i]:
+    if rk.world > 1 and rk.ref_later[i]:
         exchange(rk, comm, rk.ref_halo(), rk.slots[i])
+
+
+def gather_to_root(rk, comm, slot):
+    """every rank's own rows of a DPB slot into rank 0's slot (rank 0 then holds the whole picture)"""
+    if rk.world == 1:
+        return
+    if rk.rank == 0:
+        recvs = [(peer, a, b - a) for peer, (a, b) in enumerate(rk.rows) if peer]
+        exchange(rk, comm, ([], recvs), slot)
+    else:
+        exchange(rk, comm, ([(0, rk.y0, rk.y1 - rk.y0)], []), slot)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -198,7 +210,7 @@ class TorchComm:
         key = id(buf)
         d = self._stage.get(key)
         if d is None or d.numel() != buf.numel():
-            d = t.empty(buf.numel(), dtype=t.uint8, device=self.device)
+            d = t.empty(buf.numel(), dtype=t.uint8, device="cuda")   # the context's rows live on the GPU
             self._stage[key] = d
         if staged:
             d.copy_(buf)
