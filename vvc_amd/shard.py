@@ -41,10 +41,10 @@ def shard_rows(p, world):
         raise ValueError("%d ranks but only %d tile rows" % (world, ntile))
     total = bd[-1]
     cuts = [0]
-    for r in range(1, world):   # first tile-row boundary at or after the ideal cut, leaving a row per later rank
+    for r in range(1, world):   # the tile-row boundary nearest the ideal cut, leaving a tile row per later rank
         ideal = total * r / world
-        k = next(k for k in range(cuts[-1] + 1, ntile + 1) if bd[k] >= ideal or ntile - k <= world - r)
-        cuts.append(min(k, ntile - (world - r)))
+        lo, hi = cuts[-1] + 1, ntile - (world - r)
+        cuts.append(min(range(lo, hi + 1), key=lambda k: (abs(bd[k] - ideal), k)))
     cuts.append(ntile)
     return [(bd[cuts[r]] * ctu, min(H, bd[cuts[r + 1]] * ctu)) for r in range(world)]
 
@@ -142,7 +142,7 @@ def plan_and_reach(ranks, comm=None):
         M = comm.max_int(M)
     for r in ranks:
         r.set_reach(M)
-    return M
+    return ranks[0].M
 
 
 def exchange(rk, comm, lists, slot):
