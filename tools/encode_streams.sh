@@ -2,7 +2,7 @@
 # Re-creates the committed test bitstreams with the REFERENCE encoder built by oracle/ref.mk
 # (VTM 7.3 EncoderApp, CTC configs from /root/reference/cfg). Test-infrastructure only; runs in the
 # build container (needs /root/reference). Every stream carries MD5 decoded-picture-hash SEI.
-#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32
+#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32
 set -e
 R=/root/reference/cfg; E=${E:-$(dirname $0)/../oracle/_ref/EncoderApp}; T=${T:-/tmp/enc}; O=${O:-$(dirname $0)/../tests/golden/streams}
 mkdir -p $T $O
@@ -20,6 +20,8 @@ for n in "$@"; do case $n in
   ai480_q32)  [ -f $T/syn480.yuv ]  || $G 832 480 33 $T/syn480.yuv;   enc $n encoder_intra_vtm.cfg 832 480 8 32 $T/syn480.yuv --TemporalSubsampleRatio=1 ;;
   ra480_q32)  [ -f $T/syn480.yuv ]  || $G 832 480 33 $T/syn480.yuv;   enc $n encoder_randomaccess_vtm.cfg 832 480 33 32 $T/syn480.yuv --SearchRange=64 ;;
   ra1080_q32) [ -f $T/syn1080.yuv ] || $G 1920 1080 9 $T/syn1080.yuv; enc $n encoder_randomaccess_vtm.cfg 1920 1080 9 32 $T/syn1080.yuv --SearchRange=64 ;;
+  # 33 pictures: a whole intra period of the CTC random-access configuration (IntraPeriod 32, GOP 16)
+  ra1080l_q32) [ -f $T/syn1080l.yuv ] || $G 1920 1080 33 $T/syn1080l.yuv; enc $n encoder_randomaccess_vtm.cfg 1920 1080 33 32 $T/syn1080l.yuv --SearchRange=64 ;;
   ra1080t_q32) [ -f $T/syn1080t.yuv ] || $G 1920 1080 9 $T/syn1080t.yuv 0; enc $n encoder_randomaccess_vtm.cfg 1920 1080 9 32 $T/syn1080t.yuv --SearchRange=64 ;;
   ra2160_q27) [ -f $T/syn2160.yuv ] || $G 3840 2160 3 $T/syn2160.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 3 27 $T/syn2160.yuv --SearchRange=64 ;;
   ra2160_q32) [ -f $T/syn2160.yuv ] || $G 3840 2160 3 $T/syn2160.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 3 32 $T/syn2160.yuv --SearchRange=64 ;;
