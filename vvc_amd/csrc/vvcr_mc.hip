@@ -114,7 +114,26 @@ __device__ __forceinline__ Win make_win(const McParams &P, const McJob &J, int c
   return w;
 }
 
-__global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__restrict__ jobs, int njobs) {
+// Field-wise select of one of two windows (keeps both in registers; a selected reference would not).
+__device__ __forceinline__ Win sel_win(bool second, const Win &a, const Win &b) {
+  Win w;
+  w.on = second ? b.on : a.on;
+  w.inside = second ? b.inside : a.inside;
+  w.frac_x = second ? b.frac_x : a.frac_x;
+  w.frac_y = second ? b.frac_y : a.frac_y;
+  w.oy = second ? b.oy : a.oy;
+  w.s = second ? b.s : a.s;
+  w.ax = second ? b.ax : a.ax;
+  w.p = second ? b.p : a.p;
+  w.stride = second ? b.stride : a.stride;
+  w.pw = second ? b.pw : a.pw;
+  w.ph = second ? b.ph : a.ph;
+  return w;
+}
+
+// Two waves per job: with both lists, wave l filters list l (luma, then its chroma); with one list,
+// wave 0 filters the luma and wave 1 the chroma. Wave 0 stores the luma, wave 1 the chroma.
+__global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__restrict__ jobs, int njobs) {
   __shared__ __attribute__((aligned(16))) int16_t s_lwin[2][LR * LP];   // luma windows per list
   __shared__ __attribute__((aligned(16))) int16_t s_cwin[4][CR * CP];   // chroma windows, combo = 2 * (comp - 1) + list
   __shared__ __attribute__((aligned(16))) int16_t s_lt[2][16 * TP];     // luma H outputs [col][row]
@@ -125,15 +144,19 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
   const int j = blockIdx.x;
   if (j >= njobs) return;
   const McJob J = jobs[j];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int w = J.w, h = J.h, lw = __ffs(w) - 1;
   const int cw = w >> 1, chh = h >> 1, lcw = lw - 1;
   const bool bi = (J.flags & MC_L0) && (J.flags & MC_L1);
+  const int la = (J.flags & MC_L0) ? 0 : 1;   // the list of a uni-predicted block
   const bool rnd = !bi && !(J.flags & MC_KEEP14) && !(J.flags & MC_WP);
   const int bd = P.bd, maxv = (1 << bd) - 1, headRoom = max(2, IF_INTERNAL_PREC - bd);
   const int sh1 = IF_FILTER_PREC - headRoom, off1 = -(IF_INTERNAL_OFFS << sh1);
   const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
   const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
+  // this wave's share: the luma of list ll (if dol) and the chroma of list cl (if doc)
+  const int ll = bi ? wave : la, cl = bi ? wave : la;
+  const bool dol = (J.flags & MC_LUMA) && (bi || wave == 0), doc = (J.flags & MC_CHROMA) && (bi || wave == 1);
 
   Win wl[2], wc[4];
 #pragma unroll
@@ -145,10 +168,11 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
   for (int l = 0; l < 2; l++) inside = inside && (!wl[l].on || wl[l].inside);
 #pragma unroll
   for (int k = 0; k < 4; k++) inside = inside && (!wc[k].on || wc[k].inside);
+  const Win WL = sel_win(ll, wl[0], wl[1]), WC1 = sel_win(cl, wc[0], wc[1]), WC2 = sel_win(cl, wc[2], wc[3]);
 
-  // chroma taps per combo (lanes 0..7): H from the horizontal fraction, V from the vertical one
-  if (lane < 8) {
-    const int k = lane >> 1, v = lane & 1;
+  // chroma taps per combo (lanes 0..7 of wave 0): H from the horizontal fraction, V from the vertical one
+  if (tid < 8) {
+    const int k = tid >> 1, v = tid & 1;
     // explicit selects: a lane-indexed J.mv[][] would put the job record in scratch
     const int m0 = v ? J.mv[0][1] : J.mv[0][0], m1 = v ? J.mv[1][1] : J.mv[1][0];
     const int mvf = ((k & 1) ? m1 : m0) & 31;
@@ -157,88 +181,84 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
     s_ctap[k][v][2] = t.B[0]; s_ctap[k][v][3] = t.B[1]; s_ctap[k][v][4] = t.B[2];
   }
 
-  // ---- gather
+  // ---- gather (each wave its share; all of a lane's loads before its LDS writes)
+  int16_t *lwin = s_lwin[ll];
+  int16_t *cwin1 = s_cwin[cl], *cwin2 = s_cwin[2 + cl];
   if (inside) {
-    uint2 vl[2][3], vc[4];
-#pragma unroll
-    for (int l = 0; l < 2; l++)
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const int i = lane + 64 * k, r = i / 7, c = i - 7 * r;
-        if (wl[l].on && r < h + 7)
-          vl[l][k] = *(const uint2 *)(wl[l].p + (size_t)(wl[l].oy + r) * wl[l].stride + wl[l].ax + 4 * c);
-      }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int r = lane >> 2, c = lane & 3;
-      if (wc[k].on && r < chh + 3) vc[k] = *(const uint2 *)(wc[k].p + (size_t)(wc[k].oy + r) * wc[k].stride + wc[k].ax + 4 * c);
-    }
-#pragma unroll
-    for (int l = 0; l < 2; l++)
+    uint2 vl[3], vc[2][2];
+    if (dol)
 #pragma unroll
       for (int k = 0; k < 3; k++) {
         const int i = lane + 64 * k, r = i / 7, c = i - 7 * r;
-        if (wl[l].on && r < h + 7) *(uint2 *)&s_lwin[l][r * LP + 4 * c] = vl[l][k];
+        if (r < h + 7) vl[k] = *(const uint2 *)(WL.p + (size_t)(WL.oy + r) * WL.stride + WL.ax + 4 * c);
       }
+    if (doc)
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int r = lane >> 2, c = lane & 3;
-      if (wc[k].on && r < chh + 3) *(uint2 *)&s_cwin[k][r * CP + 4 * c] = vc[k];
-    }
+      for (int k = 0; k < 2; k++) {
+        const Win &W = k ? WC2 : WC1;
+        const int r = lane >> 2, c = lane & 3;
+        if (r < chh + 3) vc[k][0] = *(const uint2 *)(W.p + (size_t)(W.oy + r) * W.stride + W.ax + 4 * c);
+      }
+    if (dol)
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const int i = lane + 64 * k, r = i / 7, c = i - 7 * r;
+        if (r < h + 7) *(uint2 *)&lwin[r * LP + 4 * c] = vl[k];
+      }
+    if (doc)
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const int r = lane >> 2, c = lane & 3;
+        if (r < chh + 3) *(uint2 *)&(k ? cwin2 : cwin1)[r * CP + 4 * c] = vc[k][0];
+      }
   } else {
     // a window reaches outside the picture: per-sample gather with clamped coordinates, same layout
-#pragma unroll
-    for (int l = 0; l < 2; l++) {
-      if (!wl[l].on) continue;
-      const Win &W = wl[l];
+    if (dol)
       for (int i = lane; i < (h + 7) * LP; i += 64) {
         const int r = i / LP, e = i - LP * r;
-        s_lwin[l][i] = W.p[(size_t)clampi(W.oy + r, 0, W.ph - 1) * W.stride + clampi(W.ax + e, 0, W.pw - 1)];
+        lwin[i] = WL.p[(size_t)clampi(WL.oy + r, 0, WL.ph - 1) * WL.stride + clampi(WL.ax + e, 0, WL.pw - 1)];
       }
-    }
+    if (doc)
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (!wc[k].on) continue;
-      const Win &W = wc[k];
-      for (int i = lane; i < (chh + 3) * CP; i += 64) {
-        const int r = i / CP, e = i - CP * r;
-        s_cwin[k][i] = W.p[(size_t)clampi(W.oy + r, 0, W.ph - 1) * W.stride + clampi(W.ax + e, 0, W.pw - 1)];
+      for (int k = 0; k < 2; k++) {
+        const Win &W = k ? WC2 : WC1;
+        int16_t *dst = k ? cwin2 : cwin1;
+        for (int i = lane; i < (chh + 3) * CP; i += 64) {
+          const int r = i / CP, e = i - CP * r;
+          dst[i] = W.p[(size_t)clampi(W.oy + r, 0, W.ph - 1) * W.stride + clampi(W.ax + e, 0, W.pw - 1)];
+        }
       }
-    }
   }
   __syncthreads();
 
-  // ---- H pass: luma per list (items: 2 rows x 4 columns), chroma combos together (16 lanes each)
+  // ---- H pass: luma (items: 2 rows x 4 columns), then the two chroma combos of the wave's list
   const bool is4x4 = (w == 4 && h == 4);
   const bool alt = (J.flags & MC_ALT_HPEL) != 0;
-#pragma unroll
-  for (int l = 0; l < 2; l++) {
-    if (!wl[l].on) continue;
-    const int fx = wl[l].frac_x;
+  if (dol) {
+    const int fx = WL.frac_x;
     const Taps<8> th = make_taps<8>((fx == 8 && alt) ? c_alt_hpel : (is4x4 ? c_luma4x4[fx] : c_luma[fx]));
     const int lnq = lw - 2, nrp = (h + 8) >> 1;
     const int rp = lane >> lnq, q = lane & ((1 << lnq) - 1);
     if (rp < nrp) {
-      const uint32_t *r0 = (const uint32_t *)s_lwin[l] + (2 * rp) * (LP / 2) + (wl[l].s >> 1) + 2 * q;
+      const uint32_t *r0 = (const uint32_t *)lwin + (2 * rp) * (LP / 2) + (WL.s >> 1) + 2 * q;
       uint32_t w0[6], w1[6];
 #pragma unroll
       for (int k = 0; k < 6; k++) { w0[k] = r0[k]; w1[k] = r0[LP / 2 + k]; }
       int a[4], b[4];
-      if (wl[l].s & 1) { fir4<8, 1>(w0, th, a); fir4<8, 1>(w1, th, b); }
+      if (WL.s & 1) { fir4<8, 1>(w0, th, a); fir4<8, 1>(w1, th, b); }
       else { fir4<8, 0>(w0, th, a); fir4<8, 0>(w1, th, b); }
-      uint32_t *dst = (uint32_t *)s_lt[l];
+      uint32_t *dst = (uint32_t *)s_lt[ll];
 #pragma unroll
       for (int jj = 0; jj < 4; jj++)
         dst[((4 * q + jj) * TP + 2 * rp) >> 1] = pk((int16_t)((a[jj] + off1) >> sh1), (int16_t)((b[jj] + off1) >> sh1));
     }
   }
-  {
-    const int k = lane >> 4, it = lane & 15;
+  if (doc && lane < 32) {
+    const int cc = lane >> 4, it = lane & 15, k = 2 * cc + cl;   // combo: component cc + 1, list cl
     const int lnq = lcw >= 2 ? lcw - 2 : 0, nrp = (chh + 4) >> 1;
     const int rp = it >> lnq, q = it & ((1 << lnq) - 1);
-    const int s = k == 0 ? wc[0].s : k == 1 ? wc[1].s : k == 2 ? wc[2].s : wc[3].s;
-    const bool on = k == 0 ? wc[0].on : k == 1 ? wc[1].on : k == 2 ? wc[2].on : wc[3].on;
-    if (on && rp < nrp) {
+    const int s = cc ? WC2.s : WC1.s;
+    if (rp < nrp) {
       Taps<4> t;
       t.A[0] = s_ctap[k][0][0]; t.A[1] = s_ctap[k][0][1];
       t.B[0] = s_ctap[k][0][2]; t.B[1] = s_ctap[k][0][3]; t.B[2] = s_ctap[k][0][4];
@@ -257,15 +277,13 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
   }
   __syncthreads();
 
-  // ---- V pass: items of one column x 4 rows
-#pragma unroll
-  for (int l = 0; l < 2; l++) {
-    if (!wl[l].on) continue;
-    const int fy = wl[l].frac_y;
+  // ---- V pass: items of one column x 4 rows (luma, then the chroma combos of the wave's list)
+  if (dol) {
+    const int fy = WL.frac_y;
     const Taps<8> tv = make_taps<8>((fy == 8 && alt) ? c_alt_hpel : (is4x4 ? c_luma4x4[fy] : c_luma[fy]));
     const int x = lane & (w - 1), g = lane >> lw;
     if (4 * g < h) {
-      const uint32_t *c0 = (const uint32_t *)s_lt[l] + ((x * TP + 4 * g) >> 1);
+      const uint32_t *c0 = (const uint32_t *)s_lt[ll] + ((x * TP + 4 * g) >> 1);
       uint32_t wv[6];
 #pragma unroll
       for (int k = 0; k < 6; k++) wv[k] = c0[k];
@@ -275,14 +293,13 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
       for (int jj = 0; jj < 4; jj++) {
         int v = (int16_t)((o[jj] + off2) >> sh2);
         if (rnd) v = clampi(v, 0, maxv);
-        s_lo[l][(4 * g + jj) * w + x] = (int16_t)v;
+        s_lo[ll][(4 * g + jj) * w + x] = (int16_t)v;
       }
     }
   }
-  {
-    const int k = lane >> 4, x = lane & 7, g = (lane >> 3) & 1;
-    const bool on = k == 0 ? wc[0].on : k == 1 ? wc[1].on : k == 2 ? wc[2].on : wc[3].on;
-    if (on && x < cw && 4 * g < chh) {
+  if (doc && lane < 32) {
+    const int cc = lane >> 4, k = 2 * cc + cl, x = lane & 7, g = (lane >> 3) & 1;
+    if (x < cw && 4 * g < chh) {
       Taps<4> t;
       t.A[0] = s_ctap[k][1][0]; t.A[1] = s_ctap[k][1][1];
       t.B[0] = s_ctap[k][1][2]; t.B[1] = s_ctap[k][1][3]; t.B[2] = s_ctap[k][1][4];
@@ -303,16 +320,16 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
   }
   __syncthreads();
 
-  // ---- combine and store: 4 (chroma of 4-wide blocks: 2) consecutive samples of a row per lane
-  const int la = (J.flags & MC_L0) ? 0 : 1;   // the list of a uni-predicted block
-  if (J.flags & MC_LUMA) {
+  // ---- combine and store: 4 (chroma of 4-wide blocks: 2) consecutive samples of a row per lane;
+  // wave 0 the luma, wave 1 the chroma
+  if (wave == 0 && (J.flags & MC_LUMA)) {
     if (lane * 4 < w * h) {
       const int i = lane * 4, y = i >> lw, x = i & (w - 1);
       const uint2 a = *(const uint2 *)&s_lo[la][i];
       uint2 b = a;
       if (bi) b = *(const uint2 *)&s_lo[1][i];
-      int v[4] = {(int16_t)(a.x & 0xffff), (int16_t)(a.x >> 16), (int16_t)(a.y & 0xffff), (int16_t)(a.y >> 16)};
-      const int u[4] = {(int16_t)(b.x & 0xffff), (int16_t)(b.x >> 16), (int16_t)(b.y & 0xffff), (int16_t)(b.y >> 16)};
+      int v[4] = {lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y)};
+      const int u[4] = {lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y)};
       if (!rnd)
 #pragma unroll
         for (int t = 0; t < 4; t++) v[t] = combine(P, J, 0, x + t, y, v[t], u[t]);
@@ -320,7 +337,7 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
       *(uint2 *)(o.p + (size_t)(J.y + y) * o.stride + J.x + x) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
     }
   }
-  if (J.flags & MC_CHROMA) {
+  if (wave == 1 && (J.flags & MC_CHROMA)) {
     const int comp = 1 + (lane >> 5), k = lane & 31;
     const int ka = 2 * (comp - 1) + la, kb = 2 * (comp - 1) + 1;
     const DPlane &o = P.out[comp];
@@ -330,8 +347,8 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
         const uint2 a = *(const uint2 *)&s_co[ka][i];
         uint2 b = a;
         if (bi) b = *(const uint2 *)&s_co[kb][i];
-        int v[4] = {(int16_t)(a.x & 0xffff), (int16_t)(a.x >> 16), (int16_t)(a.y & 0xffff), (int16_t)(a.y >> 16)};
-        const int u[4] = {(int16_t)(b.x & 0xffff), (int16_t)(b.x >> 16), (int16_t)(b.y & 0xffff), (int16_t)(b.y >> 16)};
+        int v[4] = {lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y)};
+        const int u[4] = {lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y)};
         if (!rnd)
 #pragma unroll
           for (int t = 0; t < 4; t++) v[t] = combine(P, J, comp, x + t, y, v[t], u[t]);
@@ -343,8 +360,8 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
         const uint32_t a = *(const uint32_t *)&s_co[ka][i];
         uint32_t b = a;
         if (bi) b = *(const uint32_t *)&s_co[kb][i];
-        int v[2] = {(int16_t)(a & 0xffff), (int16_t)(a >> 16)};
-        const int u[2] = {(int16_t)(b & 0xffff), (int16_t)(b >> 16)};
+        int v[2] = {lo16(a), hi16(a)};
+        const int u[2] = {lo16(b), hi16(b)};
         if (!rnd)
 #pragma unroll
           for (int t = 0; t < 2; t++) v[t] = combine(P, J, comp, x + t, y, v[t], u[t]);
@@ -358,5 +375,5 @@ __global__ __launch_bounds__(64) void k_mc_basic(McParams P, const McJob *__rest
 
 void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s) {
   if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_mc_basic, dim3(njobs), dim3(64), 0, s, p, jobs, njobs);
+  hipLaunchKernelGGL(k_mc_basic, dim3(njobs), dim3(128), 0, s, p, jobs, njobs);
 }
