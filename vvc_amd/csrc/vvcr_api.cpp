@@ -88,7 +88,7 @@ struct Prepared {
   DevVec<uint8_t> alf_ctb;
   DevVec<int32_t> dmvr;
   bool have_sao = false, have_alf = false;
-  int n_tb = 0, n_tb_small = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
+  int n_tb = 0, n_tb_small = 0, n_mctile = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
   hipEvent_t ev[NK][2] = {};
   hipEvent_t start = nullptr, done = nullptr;   // whole launch (events of this picture only: an event
                                                 // shared by pictures of several lanes would serialise them)
@@ -364,19 +364,22 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.alg_bytes[K_RESID] = b;
   }
   if (mask & VVCR_STAGE_INTER) {
-    r.mc_basic.upload(wl.mc_basic);
+    {   // 32x32 tiles first, then the small jobs, in one buffer
+      std::vector<McJob> all(wl.mc_tile);
+      all.insert(all.end(), wl.mc_basic.begin(), wl.mc_basic.end());
+      r.mc_basic.upload(all);
+    }
     r.mc_bidir.upload(wl.mc_bidir);
     r.aff_pu.upload(wl.aff_pu);
     r.aff_jobs.upload(wl.aff_jobs);
+    r.n_mctile = (int)wl.mc_tile.size();
     r.n_basic = (int)wl.mc_basic.size();
     r.n_bidir = (int)wl.mc_bidir.size();
     r.n_aff = (int)wl.aff_jobs.size();
     r.n_dmvr = wl.n_dmvr;
     r.dmvr.ensure(2 * (size_t)r.n_dmvr + 2);
+    r.alg_bytes[K_MC] = wl.mc_alg;
     double b = 0;
-    for (const McJob &j : wl.mc_basic) b += mc_bytes(j);
-    r.alg_bytes[K_MC] = b;
-    b = 0;
     for (const McJob &j : wl.mc_bidir) b += mc_bytes(j);
     r.alg_bytes[K_MC_BIDIR] = b;
     b = 0;
@@ -508,9 +511,10 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     const McParams mp = make_mc_params(ctx, r.pp, L);
     {
       KernelTimer t(r, K_MC, s, ctx->timing);
-      launch_mc_basic(mp, r.mc_basic.p, r.n_basic, s);
+      launch_mc_tile(mp, r.mc_basic.p, r.n_mctile, s);
+      launch_mc_basic(mp, r.mc_basic.p + r.n_mctile, r.n_basic, s);
       VVCR_CHECK_HIP(hipGetLastError());
-      r.launches[K_MC] = r.n_basic ? 1 : 0;
+      r.launches[K_MC] = (r.n_mctile ? 1 : 0) + (r.n_basic ? 1 : 0);
     }
     {
       KernelTimer t(r, K_MC_BIDIR, s, ctx->timing);
@@ -928,7 +932,7 @@ int vvcr_picture_plan(vvcr_picture *pic, uint32_t stage_mask) {
 int vvcr_picture_work_counts(const vvcr_picture *pic, int64_t *counts, int32_t n) {
   if (!pic || (!counts && n)) return VVCR_E_ARG;
   if (!pic->planned) return VVCR_E_STATE;
-  const int64_t v[10] = {(int64_t)pic->wl.tb.size(), (int64_t)pic->wl.mc_basic.size(), (int64_t)pic->wl.mc_bidir.size(),
+  const int64_t v[10] = {(int64_t)pic->wl.tb.size(), (int64_t)(pic->wl.mc_tile.size() + pic->wl.mc_basic.size()), (int64_t)pic->wl.mc_bidir.size(),
                          (int64_t)pic->wl.aff_jobs.size(), (int64_t)pic->intra.inter_tiles.size(), (int64_t)pic->intra.jobs.size(),
                          (int64_t)pic->dbk.total(), (int64_t)pic->wl.n_dmvr, pic->wl.ref_y0, pic->wl.ref_y1};
   for (int k = 0; k < n && k < 10; k++) counts[k] = v[k];

@@ -36,6 +36,32 @@ void push_tiles(std::vector<McJob> &out, int x0, int y0, int w, int h, McJob pro
     }
 }
 
+// Algorithmic bytes of one plain MC unit: every reference window once per list (8-tap luma
+// (w+7)(h+7), 4-tap chroma 2 (w/2+3)(h/2+3)) and the 4:2:0 prediction written once, 2 B per sample.
+double mc_alg_bytes(uint16_t flags, int w, int h) {
+  const int lists = ((flags & MC_L0) ? 1 : 0) + ((flags & MC_L1) ? 1 : 0);
+  const double in = (double)(w + 7) * (h + 7) + 2.0 * (w / 2 + 3) * (h / 2 + 3);
+  return 2.0 * (lists * in + 1.5 * w * h);
+}
+
+// One plain MC unit (a PU, or an SbTMVP sub-block): 32x32 tiles for k_mc_tile when the PU is at least
+// 32x32 (all VVC block sizes are powers of two, so the tiles cover it exactly), else <= 16x16 jobs.
+void push_mc(WorkLists &wl, int x0, int y0, int w, int h, const McJob &proto) {
+  wl.mc_alg += mc_alg_bytes(proto.flags, w, h);
+  if (w >= 32 && h >= 32 && (x0 & 7) == 0) {
+    for (int y = 0; y < h; y += 32)
+      for (int x = 0; x < w; x += 32) {
+        McJob j = proto;
+        j.x = (int16_t)(x0 + x);
+        j.y = (int16_t)(y0 + y);
+        j.w = j.h = 32;
+        wl.mc_tile.push_back(j);
+      }
+    return;
+  }
+  push_tiles(wl.mc_basic, x0, y0, w, h, proto);
+}
+
 McJob make_job(const vvcr_pic_params &pp, int interDir, int r0, int r1, int mv0x, int mv0y, int mv1x, int mv1y,
                int bcw, bool altHpel) {
   McJob j{};
@@ -254,7 +280,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       j.pu_x = (int16_t)p.x;
       j.pu_y = (int16_t)p.y;
       j.bcw = 2;
-      push_tiles(wl.mc_basic, p.x, p.y, p.w, p.h, j);
+      push_mc(wl, p.x, p.y, p.w, p.h, j);
       continue;
     }
     for (int k = 0; k < c.npu; k++) {
@@ -269,7 +295,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
             const vvcr_motion &m = d.motion[(size_t)((p.y + y) >> 2) * W4 + ((p.x + x) >> 2)];
             McJob j = make_job(pp, m.inter_dir, m.ref0, m.ref1, m.mv0x, m.mv0y, m.mv1x, m.mv1y, bcw, alt);   // BCW of the CU (xWeightedAverage reads pu.cu->BcwIdx)
             set_wp(pp, j, m.ref0, m.ref1, c.bcw);
-            push_tiles(wl.mc_basic, p.x + x, p.y + y, std::min(8, p.w - x), std::min(8, p.h - y), j);
+            push_mc(wl, p.x + x, p.y + y, std::min(8, p.w - x), std::min(8, p.h - y), j);
           }
         continue;
       }
@@ -323,10 +349,10 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       }
       McJob j = make_job(pp, p.interdir, p.ref0, p.ref1, p.mv0x, p.mv0y, p.mv1x, p.mv1y, bcw, alt);
       set_wp(pp, j, p.ref0, p.ref1, c.bcw);   // the CU's BcwIdx, not the CIIP-cleared one (:664 reads pu.cu->BcwIdx)
-      push_tiles(wl.mc_basic, p.x, p.y, p.w, p.h, j);
+      push_mc(wl, p.x, p.y, p.w, p.h, j);
     }
   }
-  for (const std::vector<McJob> *v : {&wl.mc_basic, &wl.mc_bidir})
+  for (const std::vector<McJob> *v : {&wl.mc_tile, &wl.mc_basic, &wl.mc_bidir})
     for (const McJob &j : *v)
       for (int l = 0; l < 2; l++)
         if (j.flags & (l ? MC_L1 : MC_L0)) reach(j.y, j.h, j.mv[l][1]);

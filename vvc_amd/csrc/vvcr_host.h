@@ -14,7 +14,8 @@ struct PictureDescriptors {
 };
 
 struct WorkLists {
-  std::vector<McJob> mc_basic;     // plain uni/bi/BCW blocks (incl. SbTMVP sub-blocks, CIIP inter part, GEO)
+  std::vector<McJob> mc_tile;      // plain uni/bi/BCW/GEO/CIIP-inter MC of PUs >= 32x32: 32x32 tiles (k_mc_tile)
+  std::vector<McJob> mc_basic;     // the other plain MC blocks (<= 16x16 jobs, incl. SbTMVP sub-blocks)
   std::vector<McJob> mc_bidir;     // DMVR sub-blocks and BDOF tiles
   std::vector<AffPu> aff_pu;       // affine PUs
   std::vector<AffJob> aff_jobs;    // affine tiles
@@ -23,7 +24,9 @@ struct WorkLists {
   int n_dmvr = 0;                  // DMVR sub-blocks (delta outputs), in PU order
   int n_unsupported_inter = 0;     // PUs needing kernels not built yet (reported, never silently skipped)
   int ref_y0 = 0, ref_y1 = 0;      // luma rows of the reference pictures the MC jobs read (with margins)
+  double mc_alg = 0;               // algorithmic bytes of the plain MC (per PU / sub-block)
   void clear() {
+    mc_alg = 0; mc_tile.clear();
     mc_basic.clear(); mc_bidir.clear(); aff_pu.clear(); aff_jobs.clear(); tb.clear();
     n_dmvr = 0; n_unsupported_inter = 0; tb_small = 0; ref_y0 = ref_y1 = 0;
   }

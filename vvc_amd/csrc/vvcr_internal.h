@@ -207,3 +207,4 @@ void launch_planes3(const Planes3 &p, hipStream_t s);
 // jobs[0, nsmall): blocks of <= 256 samples (64-lane workgroups); jobs[nsmall, njobs): larger (256 lanes)
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, int nsmall, const int32_t *coef, const uint16_t *scans, hipStream_t s);
 void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);
+void launch_mc_tile(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);   // 32x32 jobs

@@ -1,11 +1,12 @@
 // vvcr_mc.hip — motion-compensated prediction for gfx950 (k_mc_basic).
 //
-// One 64-lane wave per McJob (<= 16x16 luma block + its 4:2:0 chroma, one or two lists). The reference
-// windows are gathered with 8-byte loads of aligned 4-sample chunks (every active window of the job in
-// one phase, all loads in flight before the first LDS write) into LDS; a window that reaches outside the
-// picture is gathered per sample with clamped coordinates instead (equivalent to VTM's edge-replicated
-// 288-sample margin, Picture::extendPicBorder Picture.cpp:737, plus clipMv Mv.cpp:54: every filter phase
-// sums to 64, so a clamped run of equal samples filters to the same value whatever the phase).
+// k_mc_basic: two waves per McJob (<= 16x16 luma block + its 4:2:0 chroma, one or two lists); k_mc_tile:
+// four waves per 32x32 tile of a PU of at least 32x32. The reference windows are gathered in aligned
+// 4- / 8-sample chunks (every window of a wave in one phase, all loads in flight before the first LDS
+// write) into LDS, rows clamped to the picture and chunks that cross the left / right picture edge
+// loaded per sample with clamped columns (equivalent to VTM's edge-replicated 288-sample margin,
+// Picture::extendPicBorder Picture.cpp:737, plus clipMv Mv.cpp:54: every filter phase sums to 64, so a
+// clamped run of equal samples filters to the same value whatever the phase).
 //
 // Filtering is InterpolationFilter::filter<N,isVertical,isFirst,isLast> (InterpolationFilter.cpp:548-650)
 // as the H-then-V pass of xPredInterBlk (InterPrediction.cpp:784-803) for EVERY fraction: a zero fraction
@@ -30,10 +31,6 @@ namespace {
 
 using namespace mcdev;
 
-__constant__ int8_t c_luma[16][8] = VVCR_LUMA_FILTER_TABLE;
-__constant__ int8_t c_luma4x4[16][8] = VVCR_LUMA4x4_FILTER_TABLE;
-__constant__ int8_t c_alt_hpel[8] = VVCR_LUMA_ALT_HPEL;
-__constant__ int8_t c_chroma[32][4] = VVCR_CHROMA_FILTER_TABLE;
 __constant__ int8_t c_bcw_w1[5] = VVCR_BCW_W1;
 // GEO split geometry (Rom.cpp g_angle2mask / g_Dis / g_angle2mirror, CommonDef.h GEO_* sizes)
 __constant__ int8_t c_geo_angle2mask[32] = {0, -1, 1, 2, 3, 4, -1, -1, 5, -1, -1, 4, 3, 2, 1, -1, 0, -1, 1, 2, 3, 4, -1, -1, 5, -1, -1, 4, 3, 2, 1, -1};
@@ -90,45 +87,91 @@ __device__ __forceinline__ int combine(const McParams &P, const McJob &J, int co
   return clampi((a + b + offset) >> shiftNum, 0, maxv);
 }
 
+// Packed taps (mcdev::make_taps) of every filter phase, built at compile time: a wave's taps are then
+// plain scalar loads, not per-job unpacking of the int8 tables.
+struct McTapTables {
+  Taps<8> l[16], l4[16], alt;
+  Taps<4> c[32];
+};
+constexpr int8_t k_luma[16][8] = VVCR_LUMA_FILTER_TABLE;
+constexpr int8_t k_luma4x4[16][8] = VVCR_LUMA4x4_FILTER_TABLE;
+constexpr int8_t k_alt_hpel[8] = VVCR_LUMA_ALT_HPEL;
+constexpr int8_t k_chroma[32][4] = VVCR_CHROMA_FILTER_TABLE;
+constexpr McTapTables make_mc_taps() {
+  McTapTables t{};
+  for (int f = 0; f < 16; f++) {
+    t.l[f] = make_taps<8>(k_luma[f]);
+    t.l4[f] = make_taps<8>(k_luma4x4[f]);
+  }
+  t.alt = make_taps<8>(k_alt_hpel);
+  for (int f = 0; f < 32; f++) t.c[f] = make_taps<4>(k_chroma[f]);
+  return t;
+}
+__constant__ McTapTables c_mtaps = make_mc_taps();
+// luma taps of a fraction: the 6-tap set of 4x4 blocks (InterpolationFilter::m_lumaFilter4x4), the
+// alternative half-sample filter of IMV_HPEL CUs, else the 8-tap set
+__device__ __forceinline__ const Taps<8> &luma_taps(int frac, bool alt, bool is4x4) {
+  return (frac == 8 && alt) ? c_mtaps.alt : (is4x4 ? c_mtaps.l4[frac] : c_mtaps.l[frac]);
+}
+
 // window geometry of one (component, list)
 struct Win {
   const int16_t *p;
   int stride, pw, ph, ax, oy, s, frac_x, frac_y;
-  bool on, inside;
+  bool on;
 };
+// comp / l may be runtime (wave-uniform) values: the job's per-list fields are picked with selects,
+// never indexed (a runtime index into the job record would copy it to scratch)
 __device__ __forceinline__ Win make_win(const McParams &P, const McJob &J, int comp, int l) {
   Win w;
   const int cs = comp ? 1 : 0, N = comp ? 4 : 8, half = N / 2 - 1, fb = 4 + cs;
   w.on = ((J.flags & (l ? MC_L1 : MC_L0)) != 0) && ((J.flags & (comp ? MC_CHROMA : MC_LUMA)) != 0);
-  const DPlane &R = P.ref[J.slot[l] < 0 ? 0 : J.slot[l]][comp];
-  const int mvx = J.mv[l][0], mvy = J.mv[l][1], mask = (1 << fb) - 1;
+  const int slot = l ? J.slot[1] : J.slot[0];
+  const DPlane &R = P.ref[slot < 0 ? 0 : slot][comp];
+  const int mvx = l ? J.mv[1][0] : J.mv[0][0], mvy = l ? J.mv[1][1] : J.mv[0][1], mask = (1 << fb) - 1;
   w.frac_x = mvx & mask;
   w.frac_y = mvy & mask;
   const int ox = (J.x >> cs) + (mvx >> fb) - half;
   w.oy = (J.y >> cs) + (mvy >> fb) - half;
   w.s = ox & 3;
   w.ax = ox - w.s;
-  const int ww = (J.w >> cs) + N - 1, wh = (J.h >> cs) + N - 1;
   w.p = R.p; w.stride = R.stride; w.pw = R.w; w.ph = R.h;
-  w.inside = w.ax >= 0 && ox + ww <= R.w && w.oy >= 0 && w.oy + wh <= R.h;
   return w;
 }
 
-// Field-wise select of one of two windows (keeps both in registers; a selected reference would not).
-__device__ __forceinline__ Win sel_win(bool second, const Win &a, const Win &b) {
-  Win w;
-  w.on = second ? b.on : a.on;
-  w.inside = second ? b.inside : a.inside;
-  w.frac_x = second ? b.frac_x : a.frac_x;
-  w.frac_y = second ? b.frac_y : a.frac_y;
-  w.oy = second ? b.oy : a.oy;
-  w.s = second ? b.s : a.s;
-  w.ax = second ? b.ax : a.ax;
-  w.p = second ? b.p : a.p;
-  w.stride = second ? b.stride : a.stride;
-  w.pw = second ? b.pw : a.pw;
-  w.ph = second ? b.ph : a.ph;
-  return w;
+// The default bi-prediction average (AreaBuf::addAvg, Buffer.cpp:447) when no other combine applies.
+__device__ __forceinline__ bool plain_avg(const McJob &J) { return !(J.flags & (MC_WP | MC_GEO)) && J.bcw == 2; }
+
+// Combine-and-store of 4 consecutive samples of one row (2 for 2-wide chroma): the uni rounding is
+// already final when rnd; the default average takes the short path; WP / GEO / BCW go through combine().
+template <int NS>
+__device__ __forceinline__ void combine_store(const McParams &P, const McJob &J, int comp, bool bi, bool rnd, int x, int y,
+                                              const int16_t *pa, const int16_t *pb, int16_t *dst) {
+  int v[NS], u[NS];
+  if (NS == 4) {
+    const uint2 a = *(const uint2 *)pa;
+    const uint2 b = bi ? *(const uint2 *)pb : a;
+    v[0] = lo16(a.x); v[1] = hi16(a.x); v[2 % NS] = lo16(a.y); v[3 % NS] = hi16(a.y);
+    u[0] = lo16(b.x); u[1] = hi16(b.x); u[2 % NS] = lo16(b.y); u[3 % NS] = hi16(b.y);
+  } else {
+    const uint32_t a = *(const uint32_t *)pa;
+    const uint32_t b = bi ? *(const uint32_t *)pb : a;
+    v[0] = lo16(a); v[1] = hi16(a);
+    u[0] = lo16(b); u[1] = hi16(b);
+  }
+  if (!rnd) {
+    if (bi && plain_avg(J)) {
+      const int headRoom = max(2, IF_INTERNAL_PREC - P.bd), shiftNum = headRoom + 1;
+      const int offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS, maxv = (1 << P.bd) - 1;
+#pragma unroll
+      for (int t = 0; t < NS; t++) v[t] = clampi((v[t] + u[t] + offset) >> shiftNum, 0, maxv);
+    } else {
+#pragma unroll
+      for (int t = 0; t < NS; t++) v[t] = combine(P, J, comp, x + t, y, v[t], u[t]);
+    }
+  }
+  if (NS == 4) *(uint2 *)dst = make_uint2(pk(v[0], v[1]), pk(v[2 % NS], v[3 % NS]));
+  else *(uint32_t *)dst = pk(v[0], v[1]);
 }
 
 // Two waves per job: with both lists, wave l filters list l (luma, then its chroma); with one list,
@@ -140,11 +183,12 @@ __global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__res
   __shared__ __attribute__((aligned(16))) int16_t s_ct[4][8 * CTP];     // chroma H outputs [col][row]
   __shared__ __attribute__((aligned(16))) int16_t s_lo[2][256];         // luma V outputs per list [y * w + x]
   __shared__ __attribute__((aligned(16))) int16_t s_co[4][64];          // chroma V outputs [y * cw + x]
-  __shared__ uint32_t s_ctap[4][2][5];                                   // chroma taps: [combo][H/V][A0 A1 B0 B1 B2]
   const int j = blockIdx.x;
   if (j >= njobs) return;
-  const McJob J = jobs[j];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const McJob J = load_uniform(jobs + j);
+  // readfirstlane: the wave index is uniform, and everything derived from it (list, component, window,
+  // taps) then stays in SGPRs instead of being computed per lane
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int w = J.w, h = J.h, lw = __ffs(w) - 1;
   const int cw = w >> 1, chh = h >> 1, lcw = lw - 1;
   const bool bi = (J.flags & MC_L0) && (J.flags & MC_L1);
@@ -155,79 +199,39 @@ __global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__res
   const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
   const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
   // this wave's share: the luma of list ll (if dol) and the chroma of list cl (if doc)
-  const int ll = bi ? wave : la, cl = bi ? wave : la;
+  const int ll = bi ? wave : la, cl = ll;
   const bool dol = (J.flags & MC_LUMA) && (bi || wave == 0), doc = (J.flags & MC_CHROMA) && (bi || wave == 1);
+  const Win WL = make_win(P, J, 0, ll), WC1 = make_win(P, J, 1, cl), WC2 = make_win(P, J, 2, cl);
+  // Cb and Cr of one list share the MV, hence the taps
+  const Taps<4> &tcH = c_mtaps.c[WC1.frac_x], &tcV = c_mtaps.c[WC1.frac_y];
 
-  Win wl[2], wc[4];
-#pragma unroll
-  for (int l = 0; l < 2; l++) wl[l] = make_win(P, J, 0, l);
-#pragma unroll
-  for (int k = 0; k < 4; k++) wc[k] = make_win(P, J, 1 + (k >> 1), k & 1);
-  bool inside = true;
-#pragma unroll
-  for (int l = 0; l < 2; l++) inside = inside && (!wl[l].on || wl[l].inside);
-#pragma unroll
-  for (int k = 0; k < 4; k++) inside = inside && (!wc[k].on || wc[k].inside);
-  const Win WL = sel_win(ll, wl[0], wl[1]), WC1 = sel_win(cl, wc[0], wc[1]), WC2 = sel_win(cl, wc[2], wc[3]);
-
-  // chroma taps per combo (lanes 0..7 of wave 0): H from the horizontal fraction, V from the vertical one
-  if (tid < 8) {
-    const int k = tid >> 1, v = tid & 1;
-    // explicit selects: a lane-indexed J.mv[][] would put the job record in scratch
-    const int m0 = v ? J.mv[0][1] : J.mv[0][0], m1 = v ? J.mv[1][1] : J.mv[1][0];
-    const int mvf = ((k & 1) ? m1 : m0) & 31;
-    const Taps<4> t = make_taps<4>(c_chroma[mvf]);
-    s_ctap[k][v][0] = t.A[0]; s_ctap[k][v][1] = t.A[1];
-    s_ctap[k][v][2] = t.B[0]; s_ctap[k][v][3] = t.B[1]; s_ctap[k][v][4] = t.B[2];
-  }
-
-  // ---- gather (each wave its share; all of a lane's loads before its LDS writes)
+  // ---- gather (each wave its share; all of a lane's loads before its LDS writes), 4-sample chunks
   int16_t *lwin = s_lwin[ll];
   int16_t *cwin1 = s_cwin[cl], *cwin2 = s_cwin[2 + cl];
-  if (inside) {
-    uint2 vl[3], vc[2][2];
-    if (dol)
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
+  {
+    uint2 vl0 = {}, vl1 = {}, vl2 = {}, vc0 = {}, vc1 = {};
+    auto lch = [&](int k) {   // luma chunk k of this lane (index clamped: every lane loads)
+      const int i = min(lane + 64 * k, (h + 7) * 7 - 1), r = i / 7, c = i - 7 * r;
+      return chunk4(WL.p, WL.stride, WL.pw, WL.ph, WL.oy + r, WL.ax + 4 * c);
+    };
+    auto cch = [&](const Win &W) {
+      const int i = min(lane, (chh + 3) * 4 - 1), r = i >> 2, c = i & 3;
+      return chunk4(W.p, W.stride, W.pw, W.ph, W.oy + r, W.ax + 4 * c);
+    };
+    if (dol) { vl0 = lch(0); vl1 = lch(1); vl2 = lch(2); }
+    if (doc) { vc0 = cch(WC1); vc1 = cch(WC2); }
+    if (dol) {
+      auto put = [&](int k, uint2 v) {
         const int i = lane + 64 * k, r = i / 7, c = i - 7 * r;
-        if (r < h + 7) vl[k] = *(const uint2 *)(WL.p + (size_t)(WL.oy + r) * WL.stride + WL.ax + 4 * c);
-      }
-    if (doc)
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const Win &W = k ? WC2 : WC1;
-        const int r = lane >> 2, c = lane & 3;
-        if (r < chh + 3) vc[k][0] = *(const uint2 *)(W.p + (size_t)(W.oy + r) * W.stride + W.ax + 4 * c);
-      }
-    if (dol)
-#pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const int i = lane + 64 * k, r = i / 7, c = i - 7 * r;
-        if (r < h + 7) *(uint2 *)&lwin[r * LP + 4 * c] = vl[k];
-      }
-    if (doc)
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const int r = lane >> 2, c = lane & 3;
-        if (r < chh + 3) *(uint2 *)&(k ? cwin2 : cwin1)[r * CP + 4 * c] = vc[k][0];
-      }
-  } else {
-    // a window reaches outside the picture: per-sample gather with clamped coordinates, same layout
-    if (dol)
-      for (int i = lane; i < (h + 7) * LP; i += 64) {
-        const int r = i / LP, e = i - LP * r;
-        lwin[i] = WL.p[(size_t)clampi(WL.oy + r, 0, WL.ph - 1) * WL.stride + clampi(WL.ax + e, 0, WL.pw - 1)];
-      }
-    if (doc)
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        const Win &W = k ? WC2 : WC1;
-        int16_t *dst = k ? cwin2 : cwin1;
-        for (int i = lane; i < (chh + 3) * CP; i += 64) {
-          const int r = i / CP, e = i - CP * r;
-          dst[i] = W.p[(size_t)clampi(W.oy + r, 0, W.ph - 1) * W.stride + clampi(W.ax + e, 0, W.pw - 1)];
-        }
-      }
+        if (r < h + 7) *(uint2 *)&lwin[r * LP + 4 * c] = v;
+      };
+      put(0, vl0); put(1, vl1); put(2, vl2);
+    }
+    if (doc && (lane >> 2) < chh + 3) {
+      const int r = lane >> 2, c = lane & 3;
+      *(uint2 *)&cwin1[r * CP + 4 * c] = vc0;
+      *(uint2 *)&cwin2[r * CP + 4 * c] = vc1;
+    }
   }
   __syncthreads();
 
@@ -235,8 +239,7 @@ __global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__res
   const bool is4x4 = (w == 4 && h == 4);
   const bool alt = (J.flags & MC_ALT_HPEL) != 0;
   if (dol) {
-    const int fx = WL.frac_x;
-    const Taps<8> th = make_taps<8>((fx == 8 && alt) ? c_alt_hpel : (is4x4 ? c_luma4x4[fx] : c_luma[fx]));
+    const Taps<8> &th = luma_taps(WL.frac_x, alt, is4x4);
     const int lnq = lw - 2, nrp = (h + 8) >> 1;
     const int rp = lane >> lnq, q = lane & ((1 << lnq) - 1);
     if (rp < nrp) {
@@ -259,16 +262,13 @@ __global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__res
     const int rp = it >> lnq, q = it & ((1 << lnq) - 1);
     const int s = cc ? WC2.s : WC1.s;
     if (rp < nrp) {
-      Taps<4> t;
-      t.A[0] = s_ctap[k][0][0]; t.A[1] = s_ctap[k][0][1];
-      t.B[0] = s_ctap[k][0][2]; t.B[1] = s_ctap[k][0][3]; t.B[2] = s_ctap[k][0][4];
       const uint32_t *r0 = (const uint32_t *)s_cwin[k] + (2 * rp) * (CP / 2) + (s >> 1) + 2 * q;
       uint32_t w0[5], w1[5];
 #pragma unroll
       for (int m = 0; m < 5; m++) { w0[m] = r0[m]; w1[m] = r0[CP / 2 + m]; }
       int a[4], b[4];
-      fir4_var<4>(w0, t, s & 1, a);
-      fir4_var<4>(w1, t, s & 1, b);
+      fir4_var<4>(w0, tcH, s & 1, a);
+      fir4_var<4>(w1, tcH, s & 1, b);
       uint32_t *dst = (uint32_t *)s_ct[k];
 #pragma unroll
       for (int jj = 0; jj < 4; jj++)
@@ -279,8 +279,7 @@ __global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__res
 
   // ---- V pass: items of one column x 4 rows (luma, then the chroma combos of the wave's list)
   if (dol) {
-    const int fy = WL.frac_y;
-    const Taps<8> tv = make_taps<8>((fy == 8 && alt) ? c_alt_hpel : (is4x4 ? c_luma4x4[fy] : c_luma[fy]));
+    const Taps<8> &tv = luma_taps(WL.frac_y, alt, is4x4);
     const int x = lane & (w - 1), g = lane >> lw;
     if (4 * g < h) {
       const uint32_t *c0 = (const uint32_t *)s_lt[ll] + ((x * TP + 4 * g) >> 1);
@@ -300,15 +299,12 @@ __global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__res
   if (doc && lane < 32) {
     const int cc = lane >> 4, k = 2 * cc + cl, x = lane & 7, g = (lane >> 3) & 1;
     if (x < cw && 4 * g < chh) {
-      Taps<4> t;
-      t.A[0] = s_ctap[k][1][0]; t.A[1] = s_ctap[k][1][1];
-      t.B[0] = s_ctap[k][1][2]; t.B[1] = s_ctap[k][1][3]; t.B[2] = s_ctap[k][1][4];
       const uint32_t *c0 = (const uint32_t *)s_ct[k] + ((x * CTP + 4 * g) >> 1);
       uint32_t wv[4];
 #pragma unroll
       for (int m = 0; m < 4; m++) wv[m] = c0[m];
       int o[4];
-      fir4<4, 0>(wv, t, o);
+      fir4<4, 0>(wv, tcV, o);
 #pragma unroll
       for (int jj = 0; jj < 4; jj++) {
         if (4 * g + jj >= chh) break;
@@ -325,16 +321,8 @@ __global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__res
   if (wave == 0 && (J.flags & MC_LUMA)) {
     if (lane * 4 < w * h) {
       const int i = lane * 4, y = i >> lw, x = i & (w - 1);
-      const uint2 a = *(const uint2 *)&s_lo[la][i];
-      uint2 b = a;
-      if (bi) b = *(const uint2 *)&s_lo[1][i];
-      int v[4] = {lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y)};
-      const int u[4] = {lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y)};
-      if (!rnd)
-#pragma unroll
-        for (int t = 0; t < 4; t++) v[t] = combine(P, J, 0, x + t, y, v[t], u[t]);
       const DPlane &o = P.out[0];
-      *(uint2 *)(o.p + (size_t)(J.y + y) * o.stride + J.x + x) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+      combine_store<4>(P, J, 0, bi, rnd, x, y, &s_lo[la][i], &s_lo[1][i], o.p + (size_t)(J.y + y) * o.stride + J.x + x);
     }
   }
   if (wave == 1 && (J.flags & MC_CHROMA)) {
@@ -344,34 +332,200 @@ __global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__res
     if (cw >= 4) {
       if (k * 4 < cw * chh) {
         const int i = k * 4, y = i >> lcw, x = i & (cw - 1);
-        const uint2 a = *(const uint2 *)&s_co[ka][i];
-        uint2 b = a;
-        if (bi) b = *(const uint2 *)&s_co[kb][i];
-        int v[4] = {lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y)};
-        const int u[4] = {lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y)};
-        if (!rnd)
-#pragma unroll
-          for (int t = 0; t < 4; t++) v[t] = combine(P, J, comp, x + t, y, v[t], u[t]);
-        *(uint2 *)(o.p + (size_t)((J.y >> 1) + y) * o.stride + (J.x >> 1) + x) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+        combine_store<4>(P, J, comp, bi, rnd, x, y, &s_co[ka][i], &s_co[kb][i], o.p + (size_t)((J.y >> 1) + y) * o.stride + (J.x >> 1) + x);
       }
     } else {   // 2-wide chroma (4-wide luma blocks)
       if (k * 2 < cw * chh) {
         const int i = k * 2, y = i >> lcw, x = i & (cw - 1);
-        const uint32_t a = *(const uint32_t *)&s_co[ka][i];
-        uint32_t b = a;
-        if (bi) b = *(const uint32_t *)&s_co[kb][i];
-        int v[2] = {lo16(a), hi16(a)};
-        const int u[2] = {lo16(b), hi16(b)};
-        if (!rnd)
-#pragma unroll
-          for (int t = 0; t < 2; t++) v[t] = combine(P, J, comp, x + t, y, v[t], u[t]);
-        *(uint32_t *)(o.p + (size_t)((J.y >> 1) + y) * o.stride + (J.x >> 1) + x) = pk(v[0], v[1]);
+        combine_store<2>(P, J, comp, bi, rnd, x, y, &s_co[ka][i], &s_co[kb][i], o.p + (size_t)((J.y >> 1) + y) * o.stride + (J.x >> 1) + x);
       }
     }
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// k_mc_tile: 32x32 luma tiles (+ 16x16 chroma) of PUs of at least 32x32, four waves per tile. The same
+// arithmetic as k_mc_basic; a larger tile shares the window halo and the per-job set-up among 4x the
+// samples. Every wave owns one luma window (list) and one chroma window (component, list) for all
+// passes, so its set-up is scalar and computed once:
+//   bi   luma list l on waves {2l, 2l+1}; chroma (comp, list) = (wave >> 1, wave & 1)
+//   uni  luma on all waves (gather / H) and waves 0, 1 (V); chroma Cb / Cr on waves 2 / 3
+//   gather   16-byte chunks of 8 aligned samples
+//   H pass   luma items of 2 rows x 4 columns; chroma items of 2 rows x 4 columns
+//   V pass   luma items of 1 column x 8 rows; chroma 1 column x 4 rows
+//   combine  all 256 lanes, 4 luma samples each; lanes 0..127 4 chroma samples each
+// ------------------------------------------------------------------------------------------------
+constexpr int TL_LP = 48, TL_LR = 40;    // luma window: 6 chunks of 8 per row, 39 rows (+1 pad)
+constexpr int TL_CP = 32, TL_CR = 20;    // chroma window: 4 chunks, 19 rows (+1 pad)
+constexpr int TL_TP = 42, TL_CTP = 22;   // H outputs, column-major: rows per column (odd dword pitch)
+constexpr int TL_LWIN = TL_LR * TL_LP, TL_CWIN = TL_CR * TL_CP;
+
+__global__ __launch_bounds__(256) void k_mc_tile(McParams P, const McJob *__restrict__ jobs, int njobs) {
+  // windows, then (after the H pass has read them) the V outputs in the same space
+  __shared__ __attribute__((aligned(16))) int16_t s_win[2 * TL_LWIN + 4 * TL_CWIN];
+  __shared__ __attribute__((aligned(16))) int16_t s_lt[2][32 * TL_TP];    // luma H outputs [col][row]
+  __shared__ __attribute__((aligned(16))) int16_t s_ct[4][16 * TL_CTP];   // chroma H outputs [col][row]
+  int16_t *const s_lwin = s_win, *const s_cwin = s_win + 2 * TL_LWIN;
+  int16_t *const s_lo = s_win;                    // luma V outputs [list][y * 32 + x]
+  int16_t *const s_co = s_win + 2 * TL_LWIN;      // chroma V outputs [combo][y * 16 + x]
+  const int j = blockIdx.x;
+  if (j >= njobs) return;
+  const McJob J = load_uniform(jobs + j);
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const bool bi = (J.flags & MC_L0) && (J.flags & MC_L1);
+  const int la = (J.flags & MC_L0) ? 0 : 1;
+  const bool rnd = !bi && !(J.flags & MC_KEEP14) && !(J.flags & MC_WP);
+  const int bd = P.bd, maxv = (1 << bd) - 1, headRoom = max(2, IF_INTERNAL_PREC - bd);
+  const int sh1 = IF_FILTER_PREC - headRoom, off1 = -(IF_INTERNAL_OFFS << sh1);
+  const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
+  const int off2 = rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0;
+  const bool alt = (J.flags & MC_ALT_HPEL) != 0;
+  const bool doL = (J.flags & MC_LUMA) != 0, doC = (J.flags & MC_CHROMA) != 0;
+
+  // this wave's luma list and lanes, and its chroma window
+  const int ll = bi ? (wave >> 1) : la;
+  const int lidx = bi ? (tid & 127) : tid, lstep = bi ? 128 : 256;
+  const bool chw = doC && (bi || wave >= 2);
+  const int ccomp = bi ? (wave >> 1) : (wave & 1);   // 0 = Cb, 1 = Cr
+  const int clist = bi ? (wave & 1) : la;
+  const int combo = 2 * ccomp + clist;
+  const Win WL = make_win(P, J, 0, ll);
+  const Win WC = make_win(P, J, 1 + ccomp, clist);
+  // 16-byte chunks: the window origins rounded down to a multiple of 8 samples
+  const int lax = WL.ax & ~7, lsh = WL.ax - lax + WL.s;   // first tap column within the LDS row
+  const int cax = WC.ax & ~7, csh = WC.ax - cax + WC.s;
+  int16_t *lwin = s_lwin + ll * TL_LWIN;
+  int16_t *cwin = s_cwin + combo * TL_CWIN;
+
+  // ---- gather (clamped indices: every lane loads, no branch around the loads)
+  {
+    auto lsrc = [&](int k) {
+      const int i = min(lidx + lstep * k, 39 * 6 - 1), r = i / 6, c = i - 6 * r;
+      return chunk8(WL.p, WL.stride, WL.pw, WL.ph, WL.oy + r, lax + 8 * c);
+    };
+    auto ldst = [&](int k) {
+      const int i = lidx + lstep * k, r = i / 6, c = i - 6 * r;
+      return (uint4 *)&lwin[r * TL_LP + 8 * c];
+    };
+    auto csrc = [&](int k) {
+      const int i = min(lane + 64 * k, 19 * 4 - 1), r = i >> 2, c = i & 3;
+      return chunk8(WC.p, WC.stride, WC.pw, WC.ph, WC.oy + r, cax + 8 * c);
+    };
+    auto cdst = [&](int k) {
+      const int i = lane + 64 * k, r = i >> 2, c = i & 3;
+      return (uint4 *)&cwin[r * TL_CP + 8 * c];
+    };
+    uint4 vl0 = {}, vl1 = {}, vc0 = {}, vc1 = {};
+    if (doL) { vl0 = lsrc(0); vl1 = lsrc(1); }
+    if (chw) { vc0 = csrc(0); vc1 = csrc(1); }
+    if (doL) {
+      if (lidx < 39 * 6) *ldst(0) = vl0;
+      if (lidx + lstep < 39 * 6) *ldst(1) = vl1;
+    }
+    if (chw) {
+      if (lane < 19 * 4) *cdst(0) = vc0;
+      if (lane + 64 < 19 * 4) *cdst(1) = vc1;
+    }
+  }
+  __syncthreads();
+
+  // ---- H pass
+  // luma items: row pair rp (0..19) x 8-column segment g (0..3), 80 per list, spread over the list's waves
+  const int hl_n = bi ? 40 : 20, hl_i = lane + hl_n * (bi ? (wave & 1) : wave);
+  if (doL && lane < hl_n) {
+    const Taps<8> &th = luma_taps(WL.frac_x, alt, false);
+    const int rp = hl_i >> 2, g = hl_i & 3;
+    const uint32_t *r0 = (const uint32_t *)lwin + (2 * rp) * (TL_LP / 2) + (lsh >> 1) + 4 * g;
+    uint32_t w0[8], w1[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) { w0[m] = r0[m]; w1[m] = r0[TL_LP / 2 + m]; }
+    int a[8], b[8];
+    {
+      int a0[4], a1[4], b0[4], b1[4];
+      if (lsh & 1) { fir4<8, 1>(w0, th, a0); fir4<8, 1>(w0 + 2, th, a1); fir4<8, 1>(w1, th, b0); fir4<8, 1>(w1 + 2, th, b1); }
+      else { fir4<8, 0>(w0, th, a0); fir4<8, 0>(w0 + 2, th, a1); fir4<8, 0>(w1, th, b0); fir4<8, 0>(w1 + 2, th, b1); }
+#pragma unroll
+      for (int m = 0; m < 4; m++) { a[m] = a0[m]; a[4 + m] = a1[m]; b[m] = b0[m]; b[4 + m] = b1[m]; }
+    }
+    uint32_t *dst = (uint32_t *)s_lt[ll] + ((8 * g * TL_TP + 2 * rp) >> 1);
+#pragma unroll
+    for (int jj = 0; jj < 8; jj++) dst[jj * (TL_TP / 2)] = pack_h(a[jj], b[jj], sh1);
+  }
+  if (chw && lane < 40) {   // item: row pair rp (0..9) x quad q (0..3)
+    const Taps<4> &t = c_mtaps.c[WC.frac_x];
+    const int rp = lane >> 2, q = lane & 3;
+    const uint32_t *r0 = (const uint32_t *)cwin + (2 * rp) * (TL_CP / 2) + (csh >> 1) + 2 * q;
+    uint32_t w0[5], w1[5];
+#pragma unroll
+    for (int m = 0; m < 5; m++) { w0[m] = r0[m]; w1[m] = r0[TL_CP / 2 + m]; }
+    int a[4], b[4];
+    if (csh & 1) { fir4<4, 1>(w0, t, a); fir4<4, 1>(w1, t, b); }
+    else { fir4<4, 0>(w0, t, a); fir4<4, 0>(w1, t, b); }
+    uint32_t *dst = (uint32_t *)s_ct[combo] + ((4 * q * TL_CTP + 2 * rp) >> 1);
+#pragma unroll
+    for (int jj = 0; jj < 4; jj++) dst[jj * (TL_CTP / 2)] = pack_h(a[jj], b[jj], sh1);
+  }
+  __syncthreads();
+
+  // ---- V pass (outputs over the windows, which nobody reads any more)
+  if (doL && (bi || wave < 2)) {
+    const Taps<8> &tv = luma_taps(WL.frac_y, alt, false);
+    const int i = tid & 127, x = i & 31, g = i >> 5;   // column x, rows 8g .. 8g+7
+    const uint32_t *c0 = (const uint32_t *)s_lt[ll] + ((x * TL_TP + 8 * g) >> 1);
+    uint32_t wv[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) wv[m] = c0[m];
+    int o0[4], o1[4];
+    fir4<8, 0>(wv, tv, o0);
+    fir4<8, 0>(wv + 2, tv, o1);
+    int16_t *dst = s_lo + ll * 1024 + 8 * g * 32 + x;
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+      int v = (int16_t)(((m < 4 ? o0[m & 3] : o1[m & 3]) + off2) >> sh2);
+      if (rnd) v = clampi(v, 0, maxv);
+      dst[m * 32] = (int16_t)v;
+    }
+  }
+  if (chw) {
+    const Taps<4> &t = c_mtaps.c[WC.frac_y];
+    const int x = lane & 15, g = lane >> 4;   // column x, rows 4g .. 4g+3
+    const uint32_t *c0 = (const uint32_t *)s_ct[combo] + ((x * TL_CTP + 4 * g) >> 1);
+    uint32_t wv[4];
+#pragma unroll
+    for (int m = 0; m < 4; m++) wv[m] = c0[m];
+    int o[4];
+    fir4<4, 0>(wv, t, o);
+    int16_t *dst = s_co + combo * 256 + 4 * g * 16 + x;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      int v = (int16_t)((o[m] + off2) >> sh2);
+      if (rnd) v = clampi(v, 0, maxv);
+      dst[m * 16] = (int16_t)v;
+    }
+  }
+  __syncthreads();
+
+  // ---- combine and store (8-byte row stores)
+  if (doL) {
+    const int i = tid * 4, y = i >> 5, x = i & 31;
+    const DPlane &o = P.out[0];
+    combine_store<4>(P, J, 0, bi, rnd, x, y, &s_lo[la * 1024 + i], &s_lo[1024 + i], o.p + (size_t)(J.y + y) * o.stride + J.x + x);
+  }
+  if (doC && wave < 2) {
+    const int comp = 1 + wave, i = lane * 4, y = i >> 4, x = i & 15;
+    const int ka = 2 * (comp - 1) + la, kb = 2 * (comp - 1) + 1;
+    const DPlane &o = P.out[comp];
+    combine_store<4>(P, J, comp, bi, rnd, x, y, &s_co[ka * 256 + i], &s_co[kb * 256 + i],
+                     o.p + (size_t)((J.y >> 1) + y) * o.stride + (J.x >> 1) + x);
+  }
+}
+
 }  // namespace
+
+void launch_mc_tile(const McParams &p, const McJob *jobs, int njobs, hipStream_t s) {
+  if (njobs <= 0) return;
+  hipLaunchKernelGGL(k_mc_tile, dim3(njobs), dim3(256), 0, s, p, jobs, njobs);
+}
 
 void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s) {
   if (njobs <= 0) return;

@@ -188,7 +188,7 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
 
   // ---- window buffers. Per list (luma) and per (component, list) (chroma): the union box of the
   // sub-block windows (reduced above), its aligned origin, and the mode.
-  int lax[2], loy[2], lrows[2], lnch[2], lmode[2];   // mode: 0 union inside, 1 union clamped, 2 per sub-block
+  int lax[2], loy[2], lrows[2], lnch[2], lmode[2];   // mode: 0 union box, 2 per sub-block
   int cax[4], coy[4], crows[4], cnch[4], cmode[4];
 #pragma unroll
   for (int l = 0; l < 2; l++) {
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
     lax[l] = x0 & ~3; loy[l] = y0;
     lnch[l] = (x1 - lax[l] + 3) >> 2; lrows[l] = y1 - y0;
     if (lnch[l] * 4 > LUP || lrows[l] > LUR || lrows[l] * (lnch[l] <= 8 ? 8 : 16) > 8 * 64) lmode[l] = 2;
-    else if (lax[l] < 0 || x1 > R.w || y0 < 0 || y1 > R.h) lmode[l] = 1;
+    (void)R;
   }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -211,10 +211,11 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
     cax[k] = x0 & ~3; coy[k] = y0;
     cnch[k] = (x1 - cax[k] + 3) >> 2; crows[k] = y1 - y0;
     if (cnch[k] > 8 || crows[k] > 16) cmode[k] = 2;
-    else if (cax[k] < 0 || x1 > R.w || y0 < 0 || y1 > R.h) cmode[k] = 1;
+    (void)R;
   }
 
-  // ---- gather: inside unions with 8-byte chunk loads (all in flight before the LDS writes), the rest per sample
+  // ---- gather: union boxes in 4-sample chunks (all in flight before the LDS writes; rows clamped to the
+  // picture, edge chunks per sample: chunk4), per-sub-block windows per sample in batches of 8
   {
     uint2 vl[2][4], vc[4];
 #pragma unroll
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const int i = lane + 128 * k, r = i >> lg, c = i & ((1 << lg) - 1);
-        if (i < n && c < lnch[l]) vl[l][k] = *(const uint2 *)(R.p + (size_t)(loy[l] + r) * R.stride + lax[l] + 4 * c);
+        if (i < n && c < lnch[l]) vl[l][k] = chunk4(R.p, R.stride, R.w, R.h, loy[l] + r, lax[l] + 4 * c);
       }
     }
 #pragma unroll
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
       const int n = crows[k] << 3;   // 8 chunk slots per row
       {
         const int i = lane, r = i >> 3, c = i & 7;
-        if (i < n && c < cnch[k]) vc[k] = *(const uint2 *)(R.p + (size_t)(coy[k] + r) * R.stride + cax[k] + 4 * c);
+        if (i < n && c < cnch[k]) vc[k] = chunk4(R.p, R.stride, R.w, R.h, coy[k] + r, cax[k] + 4 * c);
       }
     }
 #pragma unroll
@@ -257,23 +258,23 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
         if (i < n && c < cnch[k]) *(uint2 *)&s_cw[k][r * CUP + 4 * c] = vc[k];
       }
     }
-    // clamped unions and per-sub-block windows
+    // per-sub-block windows
 #pragma unroll
     for (int l = 0; l < 2; l++) {
       if (!U.l[l].present || lmode[l] == 0) continue;
       const DPlane &R = P.ref[U.l[l].slot][0];
-      if (lmode[l] == 1) {
-        const int W4 = lnch[l] * 4;
-        for (int i = lane; i < W4 * lrows[l]; i += 128) {
-          const int r = i / W4, e = i - r * W4;
-          s_lw[l][r * LUP + e] = R.p[(size_t)clampi(loy[l] + r, 0, R.h - 1) * R.stride + clampi(lax[l] + e, 0, R.w - 1)];
-        }
-      } else {
-        for (int i = lane; i < nsb * LSBS; i += 128) {
+      for (int i0 = lane; i0 < nsb * LSBS; i0 += 8 * 128) {
+        int16_t v[8];
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+          const int i = min(i0 + 128 * b, nsb * LSBS - 1);
           const int sb = i / LSBS, rem = i - sb * LSBS, r = rem / LSBP, e = rem - r * LSBP;
           const int ox = J.x + (sb & (nsx - 1)) * 4 + (s_sbmv[l][sb][0] >> 4) - 3, oy = J.y + (sb >> lnsx) * 4 + (s_sbmv[l][sb][1] >> 4) - 3;
-          s_lw[l][i] = R.p[(size_t)clampi(oy + r, 0, R.h - 1) * R.stride + clampi(ox + e, 0, R.w - 1)];
+          v[b] = R.p[(size_t)clampi(oy + r, 0, R.h - 1) * R.stride + clampi(ox + e, 0, R.w - 1)];
         }
+#pragma unroll
+        for (int b = 0; b < 8; b++)
+          if (i0 + 128 * b < nsb * LSBS) s_lw[l][i0 + 128 * b] = v[b];
       }
     }
 #pragma unroll
@@ -281,18 +282,18 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
       const int l = k & 1;
       if (!U.l[l].present || cmode[k] == 0) continue;
       const DPlane &R = P.ref[U.l[l].slot][1 + (k >> 1)];
-      if (cmode[k] == 1) {
-        const int W4 = cnch[k] * 4;
-        for (int i = lane; i < W4 * crows[k]; i += 128) {
-          const int r = i / W4, e = i - r * W4;
-          s_cw[k][r * CUP + e] = R.p[(size_t)clampi(coy[k] + r, 0, R.h - 1) * R.stride + clampi(cax[k] + e, 0, R.w - 1)];
-        }
-      } else {
-        for (int i = lane; i < ncb * CSBS; i += 128) {
+      for (int i0 = lane; i0 < ncb * CSBS; i0 += 8 * 128) {
+        int16_t v[8];
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+          const int i = min(i0 + 128 * b, ncb * CSBS - 1);
           const int cb = i / CSBS, rem = i - cb * CSBS, r = rem / CSBP, e = rem - r * CSBP;
           const int ox = (J.x >> 1) + (cb % ncx) * 4 + (s_csmv[l][cb][0] >> 5) - 1, oy = (J.y >> 1) + (cb / ncx) * 4 + (s_csmv[l][cb][1] >> 5) - 1;
-          s_cw[k][i] = R.p[(size_t)clampi(oy + r, 0, R.h - 1) * R.stride + clampi(ox + e, 0, R.w - 1)];
+          v[b] = R.p[(size_t)clampi(oy + r, 0, R.h - 1) * R.stride + clampi(ox + e, 0, R.w - 1)];
         }
+#pragma unroll
+        for (int b = 0; b < 8; b++)
+          if (i0 + 128 * b < ncb * CSBS) s_cw[k][i0 + 128 * b] = v[b];
       }
     }
   }

@@ -76,6 +76,50 @@ __device__ __forceinline__ void fir4_var(const uint32_t *w, const Taps<N> &t, in
   o[3] = par ? ea[1] : eb[1];
 }
 
+// N = 4 or 8 samples of a reference row starting at column c0 (a multiple of N), the row index clamped to
+// the picture: one vector load when the chunk lies inside the row, else per-sample loads with clamped
+// columns. Clamping reproduces the edge-replicated margin of the reference picture
+// (Picture::extendPicBorder, Picture.cpp:737), so no window needs a slower path at picture edges; the
+// loads of both branches are plain issues (their wait comes at the LDS write).
+__device__ __forceinline__ uint2 chunk4(const int16_t *p, int stride, int w, int h, int y, int c0) {
+  const int16_t *row = p + (size_t)clampi(y, 0, h - 1) * stride;
+  if (c0 >= 0 && c0 + 4 <= w) return *(const uint2 *)(row + c0);
+  const int a = row[clampi(c0, 0, w - 1)], b = row[clampi(c0 + 1, 0, w - 1)];
+  const int c = row[clampi(c0 + 2, 0, w - 1)], d = row[clampi(c0 + 3, 0, w - 1)];
+  return make_uint2(pk(a, b), pk(c, d));
+}
+__device__ __forceinline__ uint4 chunk8(const int16_t *p, int stride, int w, int h, int y, int c0) {
+  const int16_t *row = p + (size_t)clampi(y, 0, h - 1) * stride;
+  if (c0 >= 0 && c0 + 8 <= w) return *(const uint4 *)(row + c0);
+  int v[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) v[e] = row[clampi(c0 + e, 0, w - 1)];
+  return make_uint4(pk(v[0], v[1]), pk(v[2], v[3]), pk(v[4], v[5]), pk(v[6], v[7]));
+}
+
+// A workgroup-uniform record (job descriptor) through dword loads at a uniform address, so that it lands in
+// SGPRs (s_load): a plain struct copy loads its 16-bit fields with per-lane global loads, and everything
+// derived from them (flags, lists, windows) would then be computed per lane.
+template <class T>
+__device__ __forceinline__ T load_uniform(const T *p) {
+  static_assert(sizeof(T) % 4 == 0, "load_uniform: dword-sized records");
+  uint32_t raw[sizeof(T) / 4];
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) raw[k] = reinterpret_cast<const uint32_t *>(p)[k];
+  T v;
+  __builtin_memcpy(&v, raw, sizeof(T));
+  return v;
+}
+
+// Two H-pass intermediates (a, b: filter sums) as the packed int16 pair ((a + off1) >> sh, (b + off1) >> sh)
+// with off1 = -(IF_INTERNAL_OFFS << sh): shift both, take their low halves with one byte permute, and
+// subtract IF_INTERNAL_OFFS from both halves with one packed 16-bit op (exact: every value fits int16).
+__device__ __forceinline__ uint32_t pack_h(int a, int b, int sh) {
+  const uint32_t p = __builtin_amdgcn_perm((uint32_t)(b >> sh), (uint32_t)(a >> sh), 0x05040100u);
+  const short2_t r = __builtin_bit_cast(short2_t, p) - (short2_t){(short)IF_INTERNAL_OFFS, (short)IF_INTERNAL_OFFS};
+  return __builtin_bit_cast(uint32_t, r);
+}
+
 __device__ __forceinline__ int lo16(uint32_t v) { return (int16_t)(v & 0xffff); }
 __device__ __forceinline__ int hi16(uint32_t v) { return (int16_t)(v >> 16); }
 
