@@ -101,6 +101,27 @@ struct McParams {
   WpTable wp;
 };
 
+// A workgroup-uniform record (job descriptor) through dword loads at a uniform address, so that it lands in
+// SGPRs (s_load): a plain struct copy loads its 16-bit fields with per-lane global loads, and everything
+// derived from them (flags, lists, windows) would then be computed per lane.
+template <class T>
+__device__ __forceinline__ T load_uniform(const T *p) {
+  static_assert(sizeof(T) % 4 == 0, "load_uniform: dword-sized records");
+  uint32_t raw[sizeof(T) / 4];
+  // through the constant address space: always scalar loads (a global-space load that follows stores in
+  // the kernel may be emitted as a per-lane load), whole dwords pinned to SGPRs (no narrowing to the
+  // 16-bit fields that are used: gfx950 has no 16-bit scalar loads)
+  const __attribute__((address_space(4))) uint32_t *cp = (const __attribute__((address_space(4))) uint32_t *)(uintptr_t)p;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 4); k++) {
+    raw[k] = cp[k];
+    asm volatile("" : "+s"(raw[k]));
+  }
+  T v;
+  __builtin_memcpy(&v, raw, sizeof(T));
+  return v;
+}
+
 // Weighted-prediction epilogues on 14-bit intermediates p (IF_INTERNAL_OFFS = 8192 removed), for one
 // component c and the reference indices r0 / r1; shiftNum = max(2, 14 - bd).
 // addWeightUni (WeightPrediction.cpp:280-378): weightUnidir and noWeightUnidir agree when w == 1 << d.

@@ -486,9 +486,16 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   const int lrw = ilog2(rw);
   const bool rvec = ((rw | rx) & 3) == 0;   // plane strides are multiples of 64 samples
   const bool rlds = rn <= RESL;
+  // The reconstruction takes the residual straight from the prefetch registers when their layout is the
+  // block's: one sample per lane (k = lane + 64 b -> rs[b]) for blocks of <= 512 samples, which keeps all
+  // 64 lanes busy on small blocks (the chain is latency bound), four consecutive samples per lane
+  // (k = 4 (lane + 64 b) -> rv[b]) for larger vector-aligned ones.
+  const bool rsreg = !isp && rn <= 512;
+  const bool rreg = !isp && !rsreg && rvec && n <= 4 * 64 * 4;
+  const bool rvload = rvec && !rsreg;
   uint64_t rv[4];
   int16_t rs[8];
-  if (rvec) {
+  if (rvload) {
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       const int k = min((lane + 64 * b) * 4, rn - 4);
@@ -498,9 +505,12 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   } else {
 #pragma unroll
     for (int b = 0; b < 8; b++) {
-      const int k = min(lane + 64 * b, rn - 1);
-      const int yy = k >> lrw, xx = k & (rw - 1);
-      rs[b] = *gp(&R.p[(size_t)(ry + yy) * R.stride + rx + xx]);
+      rs[b] = 0;
+      if (64 * b < rn) {   // uniform: small blocks issue one load per lane
+        const int k = min(lane + 64 * b, rn - 1);
+        const int yy = k >> lrw, xx = k & (rw - 1);
+        rs[b] = *gp(&R.p[(size_t)(ry + yy) * R.stride + rx + xx]);
+      }
     }
   }
   // Wait for the steps this one reads from, newest dependency first (the likeliest to be still
@@ -529,8 +539,8 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   // LMCS chroma residual scale (uniform), after the wait: it reads reconstructed luma of other steps
   const int cscale = (comp > 0 && (J.vnb & CS_SCALE)) ? chroma_scale(P, G, J.vx, J.vy, J.vnb, lane) : 0;
   auto store_resid = [&]() {
-    if (!rlds) return;
-    if (rvec) {
+    if (!rlds || rreg || rsreg) return;
+    if (rvload) {
 #pragma unroll
       for (int b = 0; b < 4; b++)
         if ((lane + 64 * b) * 4 < rn) *(uint64_t *)&S.resL[(lane + 64 * b) * 4] = rv[b];
@@ -539,10 +549,10 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       for (int b = 0; b < 8; b++)
         if (lane + 64 * b < rn) S.resL[lane + 64 * b] = rs[b];
     }
-    for (int k = rvec ? RESL : (lane + 512); k < rn; k += 64) {   // non-vector rectangles above 512 samples
+    for (int k = rvload ? RESL : (lane + 512); k < rn; k += 64) {   // non-vector rectangles above 512 samples
       const int yy = k >> lrw, xx = k & (rw - 1);
       const int16_t *src = &R.p[(size_t)(ry + yy) * R.stride + rx + xx];
-      if (rvec) *(uint64_t *)&S.resL[k] = *gp((const uint64_t *)src);
+      if (rvload) *(uint64_t *)&S.resL[k] = *gp((const uint64_t *)src);
       else S.resL[k] = *gp(src);
     }
   };
@@ -657,25 +667,82 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
 #endif
   const int16_t *top = refFilter ? S.refF[0] : S.refU[0];
   const int16_t *left = refFilter ? S.refF[1] : S.refU[1];
-  // The prediction is written straight into the block's area of the LDS tile (nobody reads that area
-  // before this step is done) and the reconstruction then adds the residual in place.
-  const int ptb = tile_base(comp) + (y0 - G.cy0(comp)) * tile_pitch(comp) + (x0 - G.cx0(comp)), ptp = tile_pitch(comp);
-#define predv(q) s_tile[ptb + ((lane + 64 * (q)) >> lw_) * ptp + ((lane + 64 * (q)) & (w - 1))]
+  // ---- prediction fused with the reconstruction. Each lane takes groups of GS = min(4, w) consecutive
+  // samples of a row: pred(xx, yy) gives a sample's prediction in registers, then the CIIP blend
+  // (geneWeightedPred), the residual (from the registers prefetched at entry when their layout is the
+  // block's, else from LDS / HBM), the LMCS chroma scale and the clip, and the final samples go to the LDS
+  // tile once (and to HBM, sc1, when another CTU reads them).
+  const DPlane &PP = P.pred[comp];
+  const int tb = tile_base(comp), tp = tile_pitch(comp);
+  const int ptb = tb + (y0 - G.cy0(comp)) * tp + (x0 - G.cx0(comp));
+  const bool publish = (J.flags & IJ_PUBLISH) != 0;
+  auto finish = [&](auto pred) {
+#ifndef VVCR_ABL_RECON
+    // one sample: CIIP blend, residual, LMCS chroma scale, clip; ISP keeps the region's last row / column
+    auto recon1 = [&](int xx, int yy, int rr) {
+      int pv = pred(xx, yy);
+      if (ciip) {
+        int ip = pel(PP, x0 + xx, y0 + yy);
+        if (comp == 0 && (P.lmcs & 1)) ip = P.lmcs_fwd[ip];   // LMCS: mapped inter prediction (DecCu.cpp:696)
+        pv = ((4 - J.ciip_w) * ip + J.ciip_w * pv + 2) >> 2;
+      }
+      if (cscale) rr = scale_resi(rr, cscale, bd);
+      const int v = clampi(pv + rr, 0, maxv);
+      if (isp && (ispVer ? xx == w - 1 : yy == h - 1)) S.ispPrev[ispVer ? yy : xx] = (int16_t)v;
+      return v;
+    };
+    // Only a step that another CTU reads writes HBM here (sc1, drained before its flag); the CTU's
+    // picture area is written back from the tile once the CTU is done. Every HBM store of a wave delays
+    // that wave's later loads (vmcnt counts loads and stores in issue order), so interior steps issue none.
+    if (rreg) {
+      for (int g = lane, b = 0; (g << 2) < n; g += 64, b++) {
+        const int k = g << 2, yy = k >> lw_, xx = k & (w - 1);
+        // explicit selects: a runtime index into rv[] would put it in scratch
+        const uint64_t r = b == 0 ? rv[0] : (b == 1 ? rv[1] : (b == 2 ? rv[2] : rv[3]));
+        int v[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = recon1(xx + e, yy, (int16_t)(r >> (16 * e)));
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const uint32_t pk = (uint32_t)(uint16_t)v[e] | ((uint32_t)v[e + 1] << 16);
+          *(uint32_t *)&s_tile[ptb + yy * tp + xx + e] = pk;
+          if (publish) st_sc1(D.p + (size_t)(y0 + yy) * D.stride + x0 + xx + e, pk);
+        }
+      }
+    } else {
+      for (int k = lane, b = 0; k < n; k += 64, b++) {
+        const int yy = k >> lw_, xx = k & (w - 1);
+        int rr;
+        if (rsreg) {
+          rr = b == 0 ? rs[0] : (b == 1 ? rs[1] : (b == 2 ? rs[2] : (b == 3 ? rs[3] : (b == 4 ? rs[4] : (b == 5 ? rs[5] : (b == 6 ? rs[6] : rs[7]))))));
+        } else {
+          rr = rlds ? S.resL[(y0 - ry + yy) * rw + x0 - rx + xx] : *gp(&R.p[(size_t)(y0 + yy) * R.stride + x0 + xx]);
+        }
+        const int v = recon1(xx, yy, rr);
+        s_tile[ptb + yy * tp + xx] = (int16_t)v;
+        if (publish) {   // sample pairs (w and x0 are even): the even lane stores its pair
+          const int o = __shfl_xor(v, 1);
+          if ((k & 1) == 0) st_sc1(D.p + (size_t)(y0 + yy) * D.stride + x0 + xx, (uint32_t)(uint16_t)v | ((uint32_t)o << 16));
+        }
+      }
+    }
+#else
+    (void)pred;
+#endif
+  };
 
 #ifndef VVCR_ABL_PRED
   if (interc) {
     // ---------------- chroma of an inter CU (LMCS chroma residual scaling): the MC prediction
     const DPlane &PI = P.pred[comp];
-    for (int k = lane, q = 0; k < n; k += 64, q++) predv(q) = pel(PI, x0 + (k & (w - 1)), y0 + (k >> lw_));
+    finish([&](int xx, int yy) { return pel(PI, x0 + xx, y0 + yy); });
   } else if (lmMode) {
     // ---------------- CCLM (xGetLumaRecPixels + xGetLMParameters)
     const Src SY = src_of(P, 0, G);
     const DPlane &Y = P.reco[0];
     const int lx = 2 * x0, ly = 2 * y0;
-    const bool dual = (J.flags & IJ_DUAL) != 0;
     // luma-template availability: luma map in a single tree, chroma map in a separate chroma tree
     const NbAvail lr = nb_decode(J.av[2] >> 16), lm = nb_decode(J.av[3]);
-    (void)dual;
     const int mode = J.mode;
     const int addAR = (mode == MDLM_L || mode == MDLM_T) ? lr.ar * 2 : 0;
     const int addBL = (mode == MDLM_L || mode == MDLM_T) ? lr.bl * 2 : 0;
@@ -728,6 +795,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
     aux_batch(lane, true);
     for (int k0 = lane + 256; k0 < n; k0 += 256) aux_batch(k0, false);
     wsync();
+    int la_ = 0, lb_ = 1 << (bd - 1), lshift = 0;
     {   // every lane derives the (uniform) model; no lane-divergent region (see the dependency wait)
       bool aboveAv = lm.above, leftAv = lm.left;
       int avAR = lm.ar, avBL = lm.bl;
@@ -772,7 +840,6 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       if (sl[a0[1]] > sl[a1[0]]) { int t = a0[1]; a0[1] = a1[0]; a1[0] = t; }
       const int minL = (sl[a0[0]] + sl[a0[1]] + 1) >> 1, minC = (sc[a0[0]] + sc[a0[1]] + 1) >> 1;
       const int maxL = (sl[a1[0]] + sl[a1[1]] + 1) >> 1, maxC = (sc[a1[0]] + sc[a1[1]] + 1) >> 1;
-      int a = 0, b = 1 << (bd - 1), shift = 0;
       if (leftAv || aboveAv) {
         const int diff = maxL - minL;
         if (diff > 0) {
@@ -784,21 +851,19 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
           x += normDiff != 0;
           const int y = ilog2(abs(diffC)) + 1;
           const int add = 1 << y >> 1;
-          a = (diffC * v + add) >> y;
-          shift = 3 + x - y;
-          if (shift < 1) {
-            shift = 1;
-            a = (a == 0) ? 0 : (a < 0) ? -15 : 15;
+          la_ = (diffC * v + add) >> y;
+          lshift = 3 + x - y;
+          if (lshift < 1) {
+            lshift = 1;
+            la_ = (la_ == 0) ? 0 : (la_ < 0) ? -15 : 15;
           }
-          b = minC - ((a * minL) >> shift);
+          lb_ = minC - ((la_ * minL) >> lshift);
         } else {
-          a = 0; b = minC; shift = 0;
+          la_ = 0; lb_ = minC; lshift = 0;
         }
       }
-      S.lmp[0] = a; S.lmp[1] = b; S.lmp[2] = shift;
     }
-    wsync();
-    for (int k = lane, q = 0; k < n; k += 64, q++) predv(q) = clampi(((S.lmp[0] * S.aux[k]) >> S.lmp[2]) + S.lmp[1], 0, maxv);
+    finish([&](int xx, int yy) { return clampi(((la_ * S.aux[(yy << lw_) + xx]) >> lshift) + lb_, 0, maxv); });
   } else if (mip) {
     // ---------------- MIP
     const int sizeId = (w == 4 && h == 4) ? 0 : ((w == 4 || h == 4 || (w == 8 && h == 8)) ? 1 : 2);
@@ -851,46 +916,45 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
     }
     wsync();
     const int upH = w / rp, upV = h / rp;
-    // horizontal upsampling into rows (r+1)*upV-1 (predictionUpsampling :252-277), kept in aux2 region
-    for (int k = lane, q = 0; k < n; k += 64, q++) {
-      const int yy = k >> lw_, xx = k & (w - 1);
-      // value of the horizontally upsampled row grid at (rowIdx, xx) where rowIdx in [0, rp)
-      auto hval = [&](int rr, int cx) -> int {
-        if (upH <= 1) return S.aux[rr * rp + cx];
-        const int lf = ilog2(upH);
-        const int c = cx >> ilog2(upH), pos = cx - c * upH + 1;
-        const int before = c == 0 ? (int)S.refU[1][1 + (rr + 1) * upV - 1] : S.aux[rr * rp + c - 1];
-        const int behind = S.aux[rr * rp + c];
-        return (before * (upH - pos) + behind * pos + (1 << (lf - 1))) >> lf;
-      };
-      int v;
-      if (upV <= 1) {
-        v = hval(yy, xx);
-      } else {
-        const int lf = ilog2(upV);
-        const int r = yy >> ilog2(upV), pos = yy - r * upV + 1;
-        const int before = r == 0 ? (int)S.refU[0][1 + xx] : hval(r - 1, xx);
-        const int behind = hval(r, xx);
-        v = (before * (upV - pos) + behind * pos + (1 << (lf - 1))) >> lf;
-      }
-      predv(q) = v;
-    }
+    // predictionUpsampling (:252-277): the horizontally upsampled row grid, then vertically
+    auto hval = [&](int rr, int cx) -> int {
+      if (upH <= 1) return S.aux[rr * rp + cx];
+      const int lf = ilog2(upH);
+      const int c = cx >> ilog2(upH), pos = cx - c * upH + 1;
+      const int before = c == 0 ? (int)S.refU[1][1 + (rr + 1) * upV - 1] : S.aux[rr * rp + c - 1];
+      const int behind = S.aux[rr * rp + c];
+      return (before * (upH - pos) + behind * pos + (1 << (lf - 1))) >> lf;
+    };
+    finish([&](int xx, int yy) {
+      if (upV <= 1) return hval(yy, xx);
+      const int lf = ilog2(upV);
+      const int r = yy >> ilog2(upV), pos = yy - r * upV + 1;
+      const int before = r == 0 ? (int)S.refU[0][1 + xx] : hval(r - 1, xx);
+      const int behind = hval(r, xx);
+      return (before * (upV - pos) + behind * pos + (1 << (lf - 1))) >> lf;
+    });
   } else {
     // ---------------- planar / DC / angular / BDPCM
     const int lw = ilog2(w), lh = ilog2(h);
+    const bool pdpcPD = applyPDPC && !bdpcm && (dirMode == PLANAR || dirMode == DC);
+    const int pdScale = (lw - 2 + lh - 2 + 2) >> 2;
+    // PDPC of planar / DC (xPredIntraPlanar / DC + the PDPC of predIntraAng)
+    auto pdpc = [&](int v, int xx, int yy) {
+      if (!pdpcPD) return v;
+      const int wT = 32 >> min(31, (yy << 1) >> pdScale);
+      const int wL = 32 >> min(31, (xx << 1) >> pdScale);
+      return (int)(int16_t)(v + ((wL * (left[yy + 1] - v) + wT * (top[xx + 1] - v) + 32) >> 6));
+    };
     if (bdpcm) {
-      for (int k = lane, q = 0; k < n; k += 64, q++) {
-        const int yy = k >> lw_, xx = k & (w - 1);
-        predv(q) = J.mode == 1 ? left[yy + 1] : top[xx + 1];
-      }
+      const bool hor = J.mode == 1;
+      finish([&](int xx, int yy) { return hor ? (int)left[yy + 1] : (int)top[xx + 1]; });
     } else if (dirMode == PLANAR) {
       const int tr = top[w + 1], bl = left[h + 1];
-      for (int k = lane, q = 0; k < n; k += 64, q++) {
-        const int yy = k >> lw_, xx = k & (w - 1);
+      finish([&](int xx, int yy) {
         const int hor = (left[yy + 1] << lw) + (xx + 1) * (tr - left[yy + 1]);
         const int ver = (top[xx + 1] << lh) + (yy + 1) * (bl - top[xx + 1]);
-        predv(q) = ((hor << lh) + (ver << lw) + (1 << (lw + lh))) >> (1 + lw + lh);
-      }
+        return pdpc(((hor << lh) + (ver << lw) + (1 << (lw + lh))) >> (1 + lw + lh), xx, yy);
+      });
     } else if (dirMode == DC) {
       int part = 0;
       if (w >= h) part += lane < w ? top[mrl + 1 + lane] : 0;
@@ -898,7 +962,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       const int sum = wave_sum(part);
       const int denom = (w == h) ? (w << 1) : max(w, h);
       const int dc = (sum + (denom >> 1)) >> ilog2(denom);
-      for (int k = lane, q = 0; k < n; k += 64, q++) predv(q) = dc;
+      finish([&](int xx, int yy) { return pdpc(dc, xx, yy); });
     } else {
       // angular: build main / side references exactly as xPredIntraAng does
       const int W = isModeVer ? w : h, H = isModeVer ? h : w;   // in the (possibly transposed) frame
@@ -922,18 +986,15 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       wsync();
       const int16_t *rM = refMain + mrl, *rS = refSide + mrl;
       const bool integerSlope = (absAng & 31) == 0;
-      for (int k = lane, q = 0; k < n; k += 64, q++) {
-        const int oy = k >> lw_, ox = k & (w - 1);
+      const int scale0 = (ilog2(W) + ilog2(H) - 2) >> 2;
+      finish([&](int ox, int oy) {
         const int xx = isModeVer ? ox : oy, yy = isModeVer ? oy : ox;   // transposed-frame coordinates
         int v;
         if (angle == 0) {
           v = rM[xx + 1];
-          if (applyPDPC) {
-            const int scale = (ilog2(W) + ilog2(H) - 2) >> 2;
-            if (xx < min(3 << scale, W)) {
-              const int wL = 32 >> (2 * xx >> scale);
-              v = clampi(v + ((wL * (rS[1 + yy] - rM[0]) + 32) >> 6), 0, maxv);
-            }
+          if (applyPDPC && xx < min(3 << scale0, W)) {
+            const int wL = 32 >> (2 * xx >> scale0);
+            v = clampi(v + ((wL * (rS[1 + yy] - rM[0]) + 32) >> 6), 0, maxv);
           }
         } else {
           const int deltaPos = angle * (1 + mrl) + yy * angle;
@@ -946,8 +1007,8 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
               } else {
                 f[0] = 16 - (df >> 1); f[1] = 32 - (df >> 1); f[2] = 16 + (df >> 1); f[3] = df >> 1;
               }
-              const int s = f[0] * rM[di + xx] + f[1] * rM[di + xx + 1] + f[2] * rM[di + xx + 2] + f[3] * rM[di + xx + 3];
-              v = clampi((s + 32) >> 6, 0, maxv);
+              const int sm = f[0] * rM[di + xx] + f[1] * rM[di + xx + 1] + f[2] * rM[di + xx + 2] + f[3] * rM[di + xx + 3];
+              v = clampi((sm + 32) >> 6, 0, maxv);
             } else {
               const int p0 = rM[di + xx + 1], p1 = rM[di + xx + 2];
               v = p0 + ((df * (p1 - p0) + 16) >> 5);
@@ -962,58 +1023,14 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
             v = (int16_t)(v + ((wL * (l - v) + 32) >> 6));
           }
         }
-        predv(q) = v;
-      }
-    }
-    if (applyPDPC && !bdpcm && (dirMode == PLANAR || dirMode == DC)) {
-      const int scale = (lw - 2 + lh - 2 + 2) >> 2;
-      for (int k = lane, q = 0; k < n; k += 64, q++) {
-        const int yy = k >> lw_, xx = k & (w - 1);
-        const int wT = 32 >> min(31, (yy << 1) >> scale);
-        const int wL = 32 >> min(31, (xx << 1) >> scale);
-        const int v = predv(q);
-        predv(q) = (int16_t)(v + ((wL * (left[yy + 1] - v) + wT * (top[xx + 1] - v) + 32) >> 6));
-      }
+        return v;
+      });
     }
   }
-
-#ifdef VVCR_DIAG_DUMP
-  wsync();
-  if (gj == 0 && kreg == 0 && lane < 64) g_dbg[64 + lane] = s_tile[ptb + (lane >> lw_) * ptp + (lane & (w - 1))];
-#endif
+#else
+  finish([&](int, int) { return 0; });
 #endif
   if (kreg == 0) IPROF(5);
-  // ---- CIIP blend (geneWeightedPred) and reconstruction into the LDS tile and the picture
-  const DPlane &PP = P.pred[comp];
-  const int tb = tile_base(comp), tp = tile_pitch(comp);
-  const bool publish = (J.flags & IJ_PUBLISH) != 0;
-  wsync();   // pred[] of other lanes
-#ifndef VVCR_ABL_RECON
-  for (int k = 2 * lane; k < n; k += 128) {   // sample pairs (w and x0 are even)
-    const int yy = k >> lw_, xx = k & (w - 1);
-    int v2[2];
-#pragma unroll
-    for (int e = 0; e < 2; e++) {
-      int pv = s_tile[ptb + yy * ptp + xx + e];
-      if (ciip) {
-        int ip = pel(PP, x0 + xx + e, y0 + yy);
-        if (comp == 0 && (P.lmcs & 1)) ip = P.lmcs_fwd[ip];   // LMCS: mapped inter prediction (DecCu.cpp:696)
-        pv = ((4 - J.ciip_w) * ip + J.ciip_w * pv + 2) >> 2;
-      }
-      int rv = rlds ? S.resL[(y0 - ry + yy) * rw + x0 - rx + xx + e] : *gp(&R.p[(size_t)(y0 + yy) * R.stride + x0 + xx + e]);
-      if (cscale) rv = scale_resi(rv, cscale, bd);
-      v2[e] = clampi(pv + rv, 0, maxv);
-      if (isp && (ispVer ? xx + e == w - 1 : yy == h - 1)) S.ispPrev[ispVer ? yy : xx + e] = (int16_t)v2[e];
-    }
-    const uint32_t pk = (uint32_t)(uint16_t)v2[0] | ((uint32_t)v2[1] << 16);
-    *(uint32_t *)&s_tile[tb + (y0 + yy - G.cy0(comp)) * tp + x0 + xx - G.cx0(comp)] = pk;
-    // Only a step that another CTU reads writes HBM here (sc1, drained before its flag); the CTU's
-    // picture area is written back from the tile once the CTU is done. Every HBM store of a wave
-    // delays that wave's later loads (vmcnt counts loads and stores in issue order), so interior steps
-    // issue none.
-    if (publish) st_sc1(D.p + (size_t)(y0 + yy) * D.stride + x0 + xx, pk);
-  }
-#endif
   wsync();
   }   // regions
   IPROF(6);

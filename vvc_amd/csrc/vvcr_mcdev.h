@@ -97,20 +97,6 @@ __device__ __forceinline__ uint4 chunk8(const int16_t *p, int stride, int w, int
   return make_uint4(pk(v[0], v[1]), pk(v[2], v[3]), pk(v[4], v[5]), pk(v[6], v[7]));
 }
 
-// A workgroup-uniform record (job descriptor) through dword loads at a uniform address, so that it lands in
-// SGPRs (s_load): a plain struct copy loads its 16-bit fields with per-lane global loads, and everything
-// derived from them (flags, lists, windows) would then be computed per lane.
-template <class T>
-__device__ __forceinline__ T load_uniform(const T *p) {
-  static_assert(sizeof(T) % 4 == 0, "load_uniform: dword-sized records");
-  uint32_t raw[sizeof(T) / 4];
-#pragma unroll
-  for (int k = 0; k < (int)(sizeof(T) / 4); k++) raw[k] = reinterpret_cast<const uint32_t *>(p)[k];
-  T v;
-  __builtin_memcpy(&v, raw, sizeof(T));
-  return v;
-}
-
 // Two H-pass intermediates (a, b: filter sums) as the packed int16 pair ((a + off1) >> sh, (b + off1) >> sh)
 // with off1 = -(IF_INTERNAL_OFFS << sh): shift both, take their low halves with one byte permute, and
 // subtract IF_INTERNAL_OFFS from both halves with one packed 16-bit op (exact: every value fits int16).
