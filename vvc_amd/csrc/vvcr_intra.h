@@ -51,8 +51,22 @@ struct IntraJob {
   uint8_t vnb;            // CS_* bits (chroma scaling; reference-fill fast path)
   uint8_t xkind;          // XK_*: step kinds beyond the intra prediction modes
   uint8_t nul, nut;       // CS_PREFIX: available left / top reference units, counted from the corner
+  // Prediction parameters of IntraPrediction::initPredIntraParams (IntraPrediction.cpp:1030-1100) with the
+  // wide-angle mapping (getWideAngle :184), resolved on the host (set_pred_params in vvcr_intra_host.cpp):
+  // they depend only on the step, and a derivation per step on the device (table lookups in a dependent
+  // chain) sat on the reconstruction chain.
+  int16_t ang;            // intraPredAngle (signed; 0 when the mode is not angular)
+  int16_t inv_ang;        // invAngle
+  int8_t pred_mode;       // predMode after the wide-angle mapping (LM / MIP / BDPCM: the signalled mode)
+  uint8_t pbits;          // PB_* | angScale << 4
+  uint8_t pad_[2];
 };
-static_assert(sizeof(IntraJob) == 48, "IntraJob layout");
+static_assert(sizeof(IntraJob) == 56, "IntraJob layout");
+enum : uint8_t {
+  PB_PDPC = 1 << 0,       // position-dependent prediction combination applies
+  PB_REFFILT = 1 << 1,    // [1 2 1] reference smoothing (luma)
+  PB_INTERP = 1 << 2,     // 4-tap Gaussian interpolation filter (luma, fractional angles) instead of DCT-IF
+};
 
 enum : uint8_t {
   CS_LEFT = 1 << 0,       // left neighbour CU exists (getCURestricted)

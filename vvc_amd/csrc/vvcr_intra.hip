@@ -37,10 +37,6 @@ extern "C" int vvcr_diag_dump(int32_t *dst) { return (int)hipMemcpyFromSymbol(ds
 namespace {
 
 __constant__ int8_t i_chroma[32][4] = VVCR_CHROMA_FILTER_TABLE;
-__constant__ int16_t i_angTable[32] = {0, 1, 2, 3, 4, 6, 8, 10, 12, 14, 16, 18, 20, 23, 26, 29, 32, 35, 39, 45, 51, 57, 64, 73, 86, 102, 128, 171, 256, 341, 512, 1024};
-__constant__ int16_t i_invAngTable[32] = {0, 16384, 8192, 5461, 4096, 2731, 2048, 1638, 1365, 1170, 1024, 910, 819, 712, 630, 565,
-                                          512, 468, 420, 364, 321, 287, 256, 224, 191, 161, 128, 96, 64, 48, 32, 16};
-__constant__ uint8_t i_intraFilter[8] = {24, 24, 24, 14, 2, 0, 0, 0};
 
 constexpr int PLANAR = 0, DC = 1, HOR = 18, DIA = 34, VER = 50, VDIA = 66, LM = 67, MDLM_L = 68, MDLM_T = 69;
 constexpr int RB = 160;                      // reference buffer length (2*64 + mrl + 1, rounded)
@@ -131,6 +127,7 @@ struct WaveScratch {
 __shared__ int16_t s_tile[TILE_N];
 __shared__ WaveScratch s_ws[NW];
 __shared__ uint8_t s_ldone[kIntraMaxStepsPerCtu];
+__shared__ int8_t s_cubic[32][4];   // the 4-tap DCT-IF (chroma) filter the luma angular prediction uses
 
 // Wave-level ordering of LDS traffic between the lanes of one wave (the steps of one workgroup run on
 // different waves, so the step body never uses a workgroup barrier). A wavefront-scope fence is not
@@ -354,16 +351,6 @@ __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int c
   wsync();
 }
 
-// IntraPrediction::getWideAngle (:184)
-__device__ int wide_angle(int w, int h, int mode) {
-  if (mode > DC && mode <= VDIA) {
-    const int modeShift[6] = {0, 6, 10, 12, 14, 15};
-    const int d = abs(ilog2(w) - ilog2(h));
-    if (w > h && mode < 2 + modeShift[d]) mode += VDIA - 1;
-    else if (h > w && mode > VDIA - modeShift[d]) mode -= VDIA - 1;
-  }
-  return mode;
-}
 
 // isAbove/Left/AboveRight/BelowLeftAvailable counts for CCLM (resolved on the host: nb_bits)
 struct NbAvail {
@@ -603,40 +590,12 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   wsync();
   if (kreg == 0) IPROF(3);
 
-  // ---- prediction parameters (initPredIntraParams)
+  // ---- prediction parameters (initPredIntraParams), resolved on the host (IntraJob::pbits ...)
   const int dirMode = ciip ? PLANAR : (int)J.mode;
-  const int bw = isp ? J.cw : w, bh = isp ? J.ch : h;
-  const int predMode = (lmMode || mip || bdpcm) ? dirMode : wide_angle(bw, bh, dirMode);
+  const int predMode = J.pred_mode;
   const bool isModeVer = predMode >= DIA;
-  bool applyPDPC = w >= 4 && h >= 4 && mrl == 0;
-  const int angMode = isModeVer ? predMode - VER : -(predMode - HOR);
-  int absAng = 0, invAngle = 0, angle = 0, angScale = 0;
-  if (!lmMode && !mip && !bdpcm && dirMode > DC && dirMode < 67) {
-    const int a = abs(angMode);
-    absAng = i_angTable[a];
-    invAngle = i_invAngTable[a];
-    angle = angMode < 0 ? -absAng : absAng;
-    if (angMode < 0) {
-      applyPDPC = false;
-    } else if (angMode > 0) {
-      const int side = isModeVer ? h : w;
-      angScale = min(2, ilog2(side) - (ilog2(3 * invAngle - 2) - 8));
-      applyPDPC = applyPDPC && angScale >= 0;
-    }
-  }
-  bool refFilter = false, interp = false;
-  if (comp == 0 && !isp && !mip && mrl == 0 && dirMode != DC && !bdpcm && !lmMode) {
-    if (dirMode == PLANAR) {
-      refFilter = w * h > 32;
-    } else {
-      const int diff = min(abs(predMode - HOR), abs(predMode - VER));
-      const int log2Size = (ilog2(w) + ilog2(h)) >> 1;
-      if (diff > i_intraFilter[log2Size]) {
-        refFilter = (absAng & 31) == 0;
-        interp = !refFilter;
-      }
-    }
-  }
+  const bool applyPDPC = (J.pbits & PB_PDPC) != 0, refFilter = (J.pbits & PB_REFFILT) != 0, interp = (J.pbits & PB_INTERP) != 0;
+  const int angle = J.ang, invAngle = J.inv_ang, absAng = angle < 0 ? -angle : angle, angScale = J.pbits >> 4;
   if (refFilter) {
     const int pS = topLen, pH = leftLen;
     for (int i = lane; i <= pS; i += 64) {
@@ -964,27 +923,22 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       const int dc = (sum + (denom >> 1)) >> ilog2(denom);
       finish([&](int xx, int yy) { return pdpc(dc, xx, yy); });
     } else {
-      // angular: build main / side references exactly as xPredIntraAng does
+      // angular (xPredIntraAng): positive and zero angles read the main / side lines in place, the main
+      // one clamped at its end (the reference extends it with its last sample); negative angles build the
+      // main reference with its projected side part first
       const int W = isModeVer ? w : h, H = isModeVer ? h : w;   // in the (possibly transposed) frame
-      int16_t *refMain = S.mainA + EXT, *refSide = S.sideA + EXT;
-      {
-        const int16_t *srcMain = isModeVer ? top : left, *srcSide = isModeVer ? left : top;
-        if (angle < 0) {
-          for (int k = lane; k <= W + 1 + mrl; k += 64) refMain[k] = srcMain[k];
-          for (int k = lane; k <= H + 1 + mrl; k += 64) refSide[k] = srcSide[k];
-          for (int k = -H + lane; k <= -1; k += 64) refMain[k] = srcSide[min((-k * invAngle + 256) >> 9, H)];
-        } else {
-          const int mainLen = isModeVer ? topLen : leftLen, sideLen = isModeVer ? leftLen : topLen;
-          const int log2Ratio = lw - lh;
-          const int s = max(0, isModeVer ? log2Ratio : -log2Ratio);
-          const int maxIndex = (mrl << s) + 2;
-          const int16_t v = srcMain[mainLen + mrl];
-          for (int k = lane; k <= mainLen + mrl + maxIndex; k += 64) refMain[k] = k <= mainLen + mrl ? srcMain[k] : v;
-          for (int k = lane; k <= sideLen + mrl; k += 64) refSide[k] = srcSide[k];
-        }
+      const int16_t *srcMain = isModeVer ? top : left, *srcSide = isModeVer ? left : top;
+      const int16_t *rM = srcMain + mrl, *rS = srcSide + mrl;
+      int lastM = (isModeVer ? topLen : leftLen);   // last index of rM (= mainLen + mrl of the line)
+      if (angle < 0) {
+        int16_t *refMain = S.mainA + EXT, *refSide = S.sideA + EXT;
+        for (int k = lane; k <= W + 1 + mrl; k += 64) refMain[k] = srcMain[k];
+        for (int k = lane; k <= H + 1 + mrl; k += 64) refSide[k] = srcSide[k];
+        for (int k = -H + lane; k <= -1; k += 64) refMain[k] = srcSide[min((-k * invAngle + 256) >> 9, H)];
+        wsync();
+        rM = refMain + mrl; rS = refSide + mrl;
+        lastM = 1 << 20;
       }
-      wsync();
-      const int16_t *rM = refMain + mrl, *rS = refSide + mrl;
       const bool integerSlope = (absAng & 31) == 0;
       const int scale0 = (ilog2(W) + ilog2(H) - 2) >> 2;
       finish([&](int ox, int oy) {
@@ -1003,18 +957,20 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
             if (comp == 0) {
               int f[4];
               if (!interp) {
-                for (int t = 0; t < 4; t++) f[t] = i_chroma[df][t];
+                for (int t = 0; t < 4; t++) f[t] = s_cubic[df][t];   // LDS copy: df differs per lane
               } else {
                 f[0] = 16 - (df >> 1); f[1] = 32 - (df >> 1); f[2] = 16 + (df >> 1); f[3] = df >> 1;
               }
-              const int sm = f[0] * rM[di + xx] + f[1] * rM[di + xx + 1] + f[2] * rM[di + xx + 2] + f[3] * rM[di + xx + 3];
+              const int j0 = di + xx;
+              const int sm = f[0] * rM[min(j0, lastM)] + f[1] * rM[min(j0 + 1, lastM)] + f[2] * rM[min(j0 + 2, lastM)] +
+                             f[3] * rM[min(j0 + 3, lastM)];
               v = clampi((sm + 32) >> 6, 0, maxv);
             } else {
-              const int p0 = rM[di + xx + 1], p1 = rM[di + xx + 2];
+              const int p0 = rM[min(di + xx + 1, lastM)], p1 = rM[min(di + xx + 2, lastM)];
               v = p0 + ((df * (p1 - p0) + 16) >> 5);
             }
           } else {
-            v = rM[xx + di + 1];
+            v = rM[min(xx + di + 1, lastM)];
           }
           if (applyPDPC && xx < min(3 << angScale, W)) {
             const int invSum = 256 + (xx + 1) * invAngle;
@@ -1056,6 +1012,7 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
   // an LDS read, never a vector-memory load queued behind the wave's HBM traffic.
   static_assert(sizeof(IntraParams) % 4 == 0, "IntraParams copy");
   for (int i = tid; i < (int)(sizeof(IntraParams) / 4); i += 64 * NW) s_Praw[i] = ((const uint32_t *)Pg)[i];
+  if (tid < 128) (&s_cubic[0][0])[tid] = (&i_chroma[0][0])[tid];
   const IntraParams &P = *reinterpret_cast<const IntraParams *>(s_Praw);
   for (;;) {
     if (tid == 0) { s_ctu = atomicAdd(&state[0], 1); s_next = 0; }

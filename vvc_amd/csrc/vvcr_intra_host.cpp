@@ -20,6 +20,70 @@
 
 namespace {
 
+// IntraPrediction::initPredIntraParams (IntraPrediction.cpp:1030-1100) for one step: the wide-angle mode
+// (getWideAngle :184), intraPredAngle / invAngle (g_intraPredAngle-style tables :72-76), PDPC and its
+// angular scale, the reference smoothing and the interpolation-filter choice (m_ipaParam), the same
+// derivation k_intra made per step before. Block sizes: the region (ISP: predSize by the CU).
+constexpr int kPlanar = 0, kDC = 1, kHor = 18, kDia = 34, kVer = 50, kVdia = 66;
+constexpr int16_t kAngTable[32] = {0, 1, 2, 3, 4, 6, 8, 10, 12, 14, 16, 18, 20, 23, 26, 29, 32, 35, 39, 45, 51, 57, 64, 73, 86, 102, 128, 171, 256, 341, 512, 1024};
+constexpr int16_t kInvAngTable[32] = {0, 16384, 8192, 5461, 4096, 2731, 2048, 1638, 1365, 1170, 1024, 910, 819, 712, 630, 565,
+                                      512, 468, 420, 364, 321, 287, 256, 224, 191, 161, 128, 96, 64, 48, 32, 16};
+constexpr uint8_t kIntraFilter[8] = {24, 24, 24, 14, 2, 0, 0, 0};
+int ilog2i(int v) { int r = -1; while (v > 0) { v >>= 1; r++; } return r; }
+int wide_angle_h(int w, int h, int mode) {
+  if (mode > kDC && mode <= kVdia) {
+    const int modeShift[6] = {0, 6, 10, 12, 14, 15};
+    const int d = std::abs(ilog2i(w) - ilog2i(h));
+    if (w > h && mode < 2 + modeShift[d]) mode += kVdia - 1;
+    else if (h > w && mode > kVdia - modeShift[d]) mode -= kVdia - 1;
+  }
+  return mode;
+}
+void set_pred_params(IntraJob &J) {
+  const bool ciip = J.flags & IJ_CIIP, isp = J.flags & (IJ_ISP_HOR | IJ_ISP_VER), mip = J.flags & IJ_MIP;
+  const bool bdpcm = J.flags & IJ_BDPCM, lmMode = J.comp > 0 && J.mode >= 67;
+  const int w = J.w, h = J.h, mrl = J.comp ? 0 : J.mrl;
+  const int dirMode = ciip ? kPlanar : (int)J.mode;
+  const int bw = isp ? J.cw : w, bh = isp ? J.ch : h;
+  const int predMode = (lmMode || mip || bdpcm) ? dirMode : wide_angle_h(bw, bh, dirMode);
+  const bool isModeVer = predMode >= kDia;
+  bool applyPDPC = w >= 4 && h >= 4 && mrl == 0;
+  const int angMode = isModeVer ? predMode - kVer : -(predMode - kHor);
+  int absAng = 0, invAngle = 0, angle = 0, angScale = 0;
+  if (!lmMode && !mip && !bdpcm && dirMode > kDC && dirMode < 67) {
+    const int a = std::abs(angMode);
+    absAng = kAngTable[a];
+    invAngle = kInvAngTable[a];
+    angle = angMode < 0 ? -absAng : absAng;
+    if (angMode < 0) {
+      applyPDPC = false;
+    } else if (angMode > 0) {
+      const int side = isModeVer ? h : w;
+      angScale = std::min(2, ilog2i(side) - (ilog2i(3 * invAngle - 2) - 8));
+      applyPDPC = applyPDPC && angScale >= 0;
+    }
+  }
+  bool refFilter = false, interp = false;
+  if (J.comp == 0 && !isp && !mip && mrl == 0 && dirMode != kDC && !bdpcm && !lmMode) {
+    if (dirMode == kPlanar) {
+      refFilter = w * h > 32;
+    } else {
+      const int diff = std::min(std::abs(predMode - kHor), std::abs(predMode - kVer));
+      const int log2Size = (ilog2i(w) + ilog2i(h)) >> 1;
+      if (diff > kIntraFilter[log2Size]) {
+        refFilter = (absAng & 31) == 0;
+        interp = !refFilter;
+      }
+    }
+  }
+  J.ang = (int16_t)angle;
+  J.inv_ang = (int16_t)invAngle;
+  J.pred_mode = (int8_t)predMode;
+  J.pbits = (uint8_t)((applyPDPC ? PB_PDPC : 0) | (refFilter ? PB_REFFILT : 0) | (interp ? PB_INTERP : 0) |
+                      (std::max(0, angScale) << 4));
+}
+
+
 constexpr int MODE_INTER = 0, MODE_INTRA = 1;
 
 struct Planner {
@@ -578,7 +642,10 @@ struct Planner {
     }
     PROF_MARK("final");
     for (IntraJob &j : out.jobs)
-      if (j.xkind != XK_INTER_CHROMA) resolve_availability(j);   // inter chroma steps read no reference samples
+      if (j.xkind != XK_INTER_CHROMA) {
+        resolve_availability(j);   // inter chroma steps read no reference samples
+        set_pred_params(j);
+      }
     PROF_MARK("avail");
   }
 };
