@@ -548,6 +548,20 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   int topLen = 2 * w, leftLen = 2 * h;
   if (isp) { topLen = J.cw + w; leftLen = J.ch + h; }
 
+  // ---- prediction parameters (initPredIntraParams), resolved on the host (IntraJob::pbits ...)
+  const int dirMode = ciip ? PLANAR : (int)J.mode;
+  const int predMode = J.pred_mode;
+  const bool isModeVer = predMode >= DIA;
+  const bool applyPDPC = (J.pbits & PB_PDPC) != 0, refFilter = (J.pbits & PB_REFFILT) != 0, interp = (J.pbits & PB_INTERP) != 0;
+  const int angle = J.ang, invAngle = J.inv_ang, absAng = angle < 0 ? -angle : angle, angScale = J.pbits >> 4;
+  // Direct reference lines: when every reference sample of the step is in the LDS tile and available as
+  // the corner plus a run from it along each line (CS_PREFIX: the substitution then only repeats a line's
+  // last available sample), the prediction reads the lines in place in the tile (top: a row, left: a
+  // column, index clamped at the last available sample) - no copy into refU, no wave sync. Planar's
+  // [1 2 1] smoothing is then applied on the fly; other filtered modes take the copy.
+  const int lu_ = ch ? 1 : 2;
+  const bool direct = (KIND == K_REG || KIND == K_CIIP || KIND == K_BDPCM) && (J.vnb & CS_PREFIX) && (J.vnb & CS_INTILE) &&
+                      (J.vnb & CS_CORNER) && J.nul > 0 && J.nut > 0 && (!refFilter || dirMode == PLANAR);
   // ISP: the regions of the CU in order; region k reads the CU-level lines and region k-1
 #pragma nounroll
   for (int kreg = 0; kreg < nreg; kreg++) {
@@ -557,7 +571,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   {
     int16_t *top = S.refU[0], *left = S.refU[1];
     if (!isp) {
-      if (!interc) fill_refs(SD, D, ch, x0, y0, topLen, leftLen, mrl, bd, avlo, avhi, top, left, lane, ps, J.vnb, J.nul, J.nut);
+      if (!interc && !direct) fill_refs(SD, D, ch, x0, y0, topLen, leftLen, mrl, bd, avlo, avhi, top, left, lane, ps, J.vnb, J.nul, J.nut);
     } else if (kreg == 0) {
       // CU-level fill of the first region (predSize per split direction), kept in refF for the others
       const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
@@ -590,13 +604,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   wsync();
   if (kreg == 0) IPROF(3);
 
-  // ---- prediction parameters (initPredIntraParams), resolved on the host (IntraJob::pbits ...)
-  const int dirMode = ciip ? PLANAR : (int)J.mode;
-  const int predMode = J.pred_mode;
-  const bool isModeVer = predMode >= DIA;
-  const bool applyPDPC = (J.pbits & PB_PDPC) != 0, refFilter = (J.pbits & PB_REFFILT) != 0, interp = (J.pbits & PB_INTERP) != 0;
-  const int angle = J.ang, invAngle = J.inv_ang, absAng = angle < 0 ? -angle : angle, angScale = J.pbits >> 4;
-  if (refFilter) {
+  if (refFilter && !direct) {
     const int pS = topLen, pH = leftLen;
     for (int i = lane; i <= pS; i += 64) {
       int v;
@@ -626,6 +634,16 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
 #endif
   const int16_t *top = refFilter ? S.refF[0] : S.refU[0];
   const int16_t *left = refFilter ? S.refF[1] : S.refU[1];
+  // line views: element j of the top / left reference line (0 = corner), in place or from the copy
+  const int dcb = SD.base + (y0 - 1 - mrl - SD.y0) * SD.ts + (x0 - 1 - mrl - SD.x0);   // tile index of the corner
+  const int16_t *tp_ = direct ? &s_tile[dcb] : top, *lp_ = direct ? &s_tile[dcb] : left;
+  const int lst_ = direct ? SD.ts : 1;
+  const int tlast_ = direct ? mrl + (J.nut << lu_) : (1 << 20), llast_ = direct ? mrl + (J.nul << lu_) : (1 << 20);
+  const bool ffilt_ = direct && refFilter;   // planar on in-place lines: [1 2 1] on the fly (never at index 0 / the end)
+  auto rawT = [&](int j) { return (int)tp_[min(j, tlast_)]; };
+  auto rawL = [&](int i) { return (int)lp_[min(i, llast_) * lst_]; };
+  auto TOPv = [&](int j) { return ffilt_ ? (rawT(j - 1) + 2 * rawT(j) + rawT(j + 1) + 2) >> 2 : rawT(j); };
+  auto LEFTv = [&](int i) { return ffilt_ ? (rawL(i - 1) + 2 * rawL(i) + rawL(i + 1) + 2) >> 2 : rawL(i); };
   // ---- prediction fused with the reconstruction. Each lane takes groups of GS = min(4, w) consecutive
   // samples of a row: pred(xx, yy) gives a sample's prediction in registers, then the CIIP blend
   // (geneWeightedPred), the residual (from the registers prefetched at entry when their layout is the
@@ -902,22 +920,23 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       if (!pdpcPD) return v;
       const int wT = 32 >> min(31, (yy << 1) >> pdScale);
       const int wL = 32 >> min(31, (xx << 1) >> pdScale);
-      return (int)(int16_t)(v + ((wL * (left[yy + 1] - v) + wT * (top[xx + 1] - v) + 32) >> 6));
+      return (int)(int16_t)(v + ((wL * (LEFTv(yy + 1) - v) + wT * (TOPv(xx + 1) - v) + 32) >> 6));
     };
     if (bdpcm) {
       const bool hor = J.mode == 1;
-      finish([&](int xx, int yy) { return hor ? (int)left[yy + 1] : (int)top[xx + 1]; });
+      finish([&](int xx, int yy) { return hor ? LEFTv(yy + 1) : TOPv(xx + 1); });
     } else if (dirMode == PLANAR) {
-      const int tr = top[w + 1], bl = left[h + 1];
+      const int tr = TOPv(w + 1), bl = LEFTv(h + 1);
       finish([&](int xx, int yy) {
-        const int hor = (left[yy + 1] << lw) + (xx + 1) * (tr - left[yy + 1]);
-        const int ver = (top[xx + 1] << lh) + (yy + 1) * (bl - top[xx + 1]);
+        const int lv = LEFTv(yy + 1), tv = TOPv(xx + 1);
+        const int hor = (lv << lw) + (xx + 1) * (tr - lv);
+        const int ver = (tv << lh) + (yy + 1) * (bl - tv);
         return pdpc(((hor << lh) + (ver << lw) + (1 << (lw + lh))) >> (1 + lw + lh), xx, yy);
       });
     } else if (dirMode == DC) {
       int part = 0;
-      if (w >= h) part += lane < w ? top[mrl + 1 + lane] : 0;
-      if (w <= h) part += lane < h ? left[mrl + 1 + lane] : 0;
+      if (w >= h) part += lane < w ? TOPv(mrl + 1 + lane) : 0;
+      if (w <= h) part += lane < h ? LEFTv(mrl + 1 + lane) : 0;
       const int sum = wave_sum(part);
       const int denom = (w == h) ? (w << 1) : max(w, h);
       const int dc = (sum + (denom >> 1)) >> ilog2(denom);
@@ -927,28 +946,30 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       // one clamped at its end (the reference extends it with its last sample); negative angles build the
       // main reference with its projected side part first
       const int W = isModeVer ? w : h, H = isModeVer ? h : w;   // in the (possibly transposed) frame
-      const int16_t *srcMain = isModeVer ? top : left, *srcSide = isModeVer ? left : top;
-      const int16_t *rM = srcMain + mrl, *rS = srcSide + mrl;
-      int lastM = (isModeVer ? topLen : leftLen);   // last index of rM (= mainLen + mrl of the line)
+      auto MAINv = [&](int k) { return isModeVer ? TOPv(k) : LEFTv(k); };
+      auto SIDEv = [&](int k) { return isModeVer ? LEFTv(k) : TOPv(k); };
+      const int lastM = (isModeVer ? topLen : leftLen);   // last index of the main line past mrl (mainLen)
+      const int16_t *cM = S.mainA + EXT + mrl, *cS = S.sideA + EXT + mrl;
       if (angle < 0) {
         int16_t *refMain = S.mainA + EXT, *refSide = S.sideA + EXT;
-        for (int k = lane; k <= W + 1 + mrl; k += 64) refMain[k] = srcMain[k];
-        for (int k = lane; k <= H + 1 + mrl; k += 64) refSide[k] = srcSide[k];
-        for (int k = -H + lane; k <= -1; k += 64) refMain[k] = srcSide[min((-k * invAngle + 256) >> 9, H)];
+        for (int k = lane; k <= W + 1 + mrl; k += 64) refMain[k] = (int16_t)MAINv(k);
+        for (int k = lane; k <= H + 1 + mrl; k += 64) refSide[k] = (int16_t)SIDEv(k);
+        for (int k = -H + lane; k <= -1; k += 64) refMain[k] = (int16_t)SIDEv(min((-k * invAngle + 256) >> 9, H));
         wsync();
-        rM = refMain + mrl; rS = refSide + mrl;
-        lastM = 1 << 20;
       }
+      // rM / rS of xPredIntraAng (main / side reference from index mrl on)
+      auto rM = [&](int j) { return angle < 0 ? (int)cM[j] : MAINv(min(j, lastM) + mrl); };
+      auto rS = [&](int j) { return angle < 0 ? (int)cS[j] : SIDEv(j + mrl); };
       const bool integerSlope = (absAng & 31) == 0;
       const int scale0 = (ilog2(W) + ilog2(H) - 2) >> 2;
       finish([&](int ox, int oy) {
         const int xx = isModeVer ? ox : oy, yy = isModeVer ? oy : ox;   // transposed-frame coordinates
         int v;
         if (angle == 0) {
-          v = rM[xx + 1];
+          v = rM(xx + 1);
           if (applyPDPC && xx < min(3 << scale0, W)) {
             const int wL = 32 >> (2 * xx >> scale0);
-            v = clampi(v + ((wL * (rS[1 + yy] - rM[0]) + 32) >> 6), 0, maxv);
+            v = clampi(v + ((wL * (rS(1 + yy) - rM(0)) + 32) >> 6), 0, maxv);
           }
         } else {
           const int deltaPos = angle * (1 + mrl) + yy * angle;
@@ -962,20 +983,19 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
                 f[0] = 16 - (df >> 1); f[1] = 32 - (df >> 1); f[2] = 16 + (df >> 1); f[3] = df >> 1;
               }
               const int j0 = di + xx;
-              const int sm = f[0] * rM[min(j0, lastM)] + f[1] * rM[min(j0 + 1, lastM)] + f[2] * rM[min(j0 + 2, lastM)] +
-                             f[3] * rM[min(j0 + 3, lastM)];
+              const int sm = f[0] * rM(j0) + f[1] * rM(j0 + 1) + f[2] * rM(j0 + 2) + f[3] * rM(j0 + 3);
               v = clampi((sm + 32) >> 6, 0, maxv);
             } else {
-              const int p0 = rM[min(di + xx + 1, lastM)], p1 = rM[min(di + xx + 2, lastM)];
+              const int p0 = rM(di + xx + 1), p1 = rM(di + xx + 2);
               v = p0 + ((df * (p1 - p0) + 16) >> 5);
             }
           } else {
-            v = rM[min(xx + di + 1, lastM)];
+            v = rM(xx + di + 1);
           }
           if (applyPDPC && xx < min(3 << angScale, W)) {
             const int invSum = 256 + (xx + 1) * invAngle;
             const int wL = 32 >> (2 * xx >> angScale);
-            const int l = rS[yy + (invSum >> 9) + 1];
+            const int l = rS(yy + (invSum >> 9) + 1);
             v = (int16_t)(v + ((wL * (l - v) + 32) >> 6));
           }
         }
