@@ -25,6 +25,7 @@ os.environ.setdefault("VVCR_LANES", "7")
 
 import argparse
 import hashlib
+import glob
 import json
 import os
 import subprocess
@@ -313,8 +314,9 @@ def main():
     mc_gbs = mc[2] / (mc[1] / 1e3) / 1e9 if mc[1] > 0 else 0.0
 
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "r01_traffic.json")
-    if os.path.exists(tf):
+    tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_traffic.json")))   # the newest round's
+    tf = tfs[-1] if tfs else ""
+    if tf and os.path.exists(tf):
         with open(tf) as f:
             tj = json.load(f)
         if tj.get("stream", "ra1080_q32") == a.stream:   # the PMC passes were taken on this workload
