@@ -36,7 +36,8 @@ def main():
             if name == "intra" and r >= 2:
                 ms.append(t)
     ms.sort()
-    out = {"lib": os.path.basename(os.environ.get("VVCR_LIB", "libvvcr.so")), "stream": a.stream,
+    out = {"lib": os.path.basename(os.environ.get("VVCR_LIB", "libvvcr.so")) + (" " + os.environ["AB_LABEL"] if os.environ.get("AB_LABEL") else ""),
+           "stream": a.stream,
            "intra_ms_median": round(ms[len(ms) // 2], 4), "intra_ms_min": round(ms[0], 4), "reps": len(ms)}
     ctx.release(h)
     ctx.close()

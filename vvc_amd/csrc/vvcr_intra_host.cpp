@@ -526,12 +526,15 @@ struct Planner {
     // dependent work behind them (list scheduling by bottom level). The kernel's waves take steps in this
     // order, so the critical chain is started as early as its dependencies allow. Step costs are rough
     // estimates in microseconds (measured per step kind on MI355X, tools/iprof_ctu.py).
-    std::vector<double> bl(nj, 0.0), maxsucc(nj, 0.0);
+    std::vector<double> bl(nj, 0.0), maxsucc(nj, 0.0), cost(nj, 0.0), fin(nj, 0.0);
+    static const bool take_order_bl = [] { const char *e = getenv("VVCR_TAKE_ORDER"); return e && !strcmp(e, "bl"); }();
+    static const double take_alpha = [] { const char *e = getenv("VVCR_TAKE_ALPHA"); return e ? atof(e) : 2.5; }();
     for (int i = nj - 1; i >= 0; i--) {   // creation order is topological (dependencies are earlier)
       const IntraJob &j = jobs[i].second;
       const bool isp = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0;
       const double c = 3.0 + 0.002 * j.w * j.h * (isp ? j.isp_k : 1) + (isp ? 1.6 * (j.isp_k - 1) : 0.0) +
                        ((j.flags & IJ_MIP) ? 2.5 : 0.0) + ((j.comp && j.mode >= 67) ? 3.0 : 0.0);
+      cost[i] = c;
       bl[i] = c + maxsucc[i];
       for (auto [p, e] = D(i); p != e; ++p) maxsucc[*p] = std::max(maxsucc[*p], bl[i]);
     }
@@ -590,16 +593,66 @@ struct Planner {
             for (auto [p, e] = D(i); p != e; ++p)
               if (*p >= b0) sflat[pos[*p - b0]++] = i - b0;
         }
-        auto cmp = [&](int32_t x, int32_t y) { return bl[b0 + x] < bl[b0 + y] || (bl[b0 + x] == bl[b0 + y] && x > y); };
-        std::priority_queue<int32_t, std::vector<int32_t>, decltype(cmp)> ready(cmp);
-        for (int q = 0; q < n; q++) if (indeg[q] == 0) ready.push(q);
         int taken = 0;
-        while (!ready.empty()) {
-          const int32_t x = ready.top();
-          ready.pop();
-          perm.push_back(b0 + x);
-          taken++;
-          for (int t = soff[x]; t < soff[x + 1]; t++) if (--indeg[sflat[t]] == 0) ready.push(sflat[t]);
+        if (take_order_bl) {
+          auto cmp = [&](int32_t x, int32_t y) { return bl[b0 + x] < bl[b0 + y] || (bl[b0 + x] == bl[b0 + y] && x > y); };
+          std::priority_queue<int32_t, std::vector<int32_t>, decltype(cmp)> ready(cmp);
+          for (int q = 0; q < n; q++) if (indeg[q] == 0) ready.push(q);
+          while (!ready.empty()) {
+            const int32_t x = ready.top();
+            ready.pop();
+            perm.push_back(b0 + x);
+            taken++;
+            for (int t = soff[x]; t < soff[x + 1]; t++) if (--indeg[sflat[t]] == 0) ready.push(sflat[t]);
+          }
+        } else {
+          // Take order from a timing simulation of the kernel: kNW waves take steps in list order, a wave
+          // that takes a step waits for its dependencies, then runs it for its estimated cost. Each time a
+          // wave frees up, the list gets the step (among those whose same-CTU dependencies are already in
+          // the list) with the longest chain behind it, less VVCR_TAKE_ALPHA (2.5) times the idle time it
+          // would cost that wave. Dependencies on other CTUs use the finish times simulated for those CTUs
+          // (raster order: they come first; all CTU workgroups start together). A pure bottom-level order
+          // (VVCR_TAKE_ORDER=bl, r01) lets ready steps queue behind steps that wait on another CTU; pure
+          // earliest-start delays the critical chain. Measured (k_intra, median of 20): 1080p I picture
+          // 5.67 (bl) -> 5.59 ms, 4K 12.25 -> 11.97 ms; earliest-start first 6.67 / 14.8 ms.
+          constexpr int kNW = 4;
+          constexpr double kLocal = 0.3, kGlobal = 1.5;   // hand-off latencies (us)
+          double wfree[kNW] = {0, 0, 0, 0};
+          std::vector<double> rdy(n, 0.0);
+          std::vector<int32_t> known;
+          auto make_known = [&](int q) {
+            double r = 0;
+            for (auto [p, e] = D(b0 + q); p != e; ++p) r = std::max(r, fin[*p] + (*p >= b0 ? kLocal : kGlobal));
+            rdy[q] = r;
+            known.push_back(q);
+          };
+          for (int q = 0; q < n; q++) if (indeg[q] == 0) make_known(q);
+          while (!known.empty()) {
+            int w = 0;
+            for (int k = 1; k < kNW; k++) if (wfree[k] < wfree[w]) w = k;
+            const double t = wfree[w];
+            // priority: the chain behind the step, less the wave idle time it would cost (alpha per us)
+            size_t best = 0;
+            double bs = std::max(t, rdy[known[0]]), bk = bl[b0 + known[0]] - take_alpha * (bs - t);
+            for (size_t k = 1; k < known.size(); k++) {
+              const double st = std::max(t, rdy[known[k]]);
+              const int q = known[k], qb = known[best];
+              const double key = bl[b0 + q] - take_alpha * (st - t);
+              if (key > bk + 1e-9 || (key > bk - 1e-9 && q < qb)) {
+                best = k;
+                bs = st;
+                bk = key;
+              }
+            }
+            const int x = known[best];
+            known[best] = known.back();
+            known.pop_back();
+            fin[b0 + x] = bs + cost[b0 + x];
+            wfree[w] = fin[b0 + x];
+            perm.push_back(b0 + x);
+            taken++;
+            for (int t2 = soff[x]; t2 < soff[x + 1]; t2++) if (--indeg[sflat[t2]] == 0) make_known(sflat[t2]);
+          }
         }
         if (taken != n) throw VvcrError(VVCR_E_STATE, "intra plan: dependency cycle inside a CTU");
       }
