@@ -500,6 +500,19 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       }
     }
   }
+  // MIP: this lane's row of the mode's matrix (output o = lane; <= 64 outputs), loaded before the wait as
+  // well (lane-dependent indices into the constant tables are per-lane memory loads)
+  int mw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr (mip) {
+    const int sizeId = (w == 4 && h == 4) ? 0 : ((w == 4 || h == 4 || (w == 8 && h == 8)) ? 1 : 2);
+    const int rp = sizeId < 2 ? 4 : 8, o = min(lane, rp * rp - 1), md = J.mode;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if (sizeId == 0) mw[i] = i < 4 ? vvcr_tab::mip4x4[md][o][i] : 0;
+      else if (sizeId == 1) mw[i] = vvcr_tab::mip8x8[md][o][i];
+      else mw[i] = i == 0 ? 0 : vvcr_tab::mip16x16[md][o][i - 1];
+    }
+  }
   // Wait for the steps this one reads from, newest dependency first (the likeliest to be still
   // running); same-CTU steps through LDS, steps of other CTUs through their global flag. Every lane
   // runs the (uniform) loop and polls the same word — one request per poll — so that no lane-divergent
@@ -875,16 +888,14 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
     }
     const int offset = 32 - 32 * sum;   // (1 << (MIP_SHIFT_MATRIX - 1)) - MIP_OFFSET_MATRIX * sum
     const int mode = J.mode;
-    for (int o = lane; o < rp * rp; o += 64) {
+    (void)mode;
+    if (lane < rp * rp) {   // rp * rp <= 64: one output per lane, its matrix row prefetched in mw[]
+      const int o = lane;
       int acc = 0;
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         if (i >= inputSize) break;
-        int wgt;
-        if (sizeId == 0) wgt = vvcr_tab::mip4x4[mode][o][i];
-        else if (sizeId == 1) wgt = vvcr_tab::mip8x8[mode][o][i];
-        else wgt = i == 0 ? 0 : vvcr_tab::mip16x16[mode][o][i - 1];
-        acc += inb[i] * wgt;
+        acc += inb[i] * mw[i];
       }
       const int v = clampi(((acc + offset) >> 6) + inOff, 0, maxv);
       // transposed matrices produce the transposed block
