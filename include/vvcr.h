@@ -264,6 +264,24 @@ int vvcr_sync(vvcr_ctx *ctx);
 int vvcr_read_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, int16_t *dst, int32_t dst_stride);
 int vvcr_write_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, const int16_t *src, int32_t src_stride);
 int vvcr_read_picture(vvcr_ctx *ctx, int32_t slot, uint16_t *planes[3], const int32_t strides[3]);
+
+/* Output frame of a DPB slot exactly as DecoderApp writes it to its -o file (VideoIOYuv::write,
+ * Utilities/VideoIOYuv.cpp:964-1047, writePlane :456-700; called from DecApp::xWriteOutput DecApp.cpp:853):
+ * bit-depth change of scalePlane (:69-104; file bit depth = -d, 0 = the internal one; a smaller depth
+ * rounds, (v + 2^(s-1)) >> s, and clips to [0, 2^d - 1], or to the BT.709 range with clip_rec709), samples
+ * as bytes for 8-bit files and 16-bit little-endian otherwise, the conformance window cropped out (offsets
+ * in luma samples: conf_win_*_offset times SubWidthC / SubHeightC) with every row still `width` samples
+ * long and the cropped area at its top-left, zero-filled to the right and below, as VTM 7.3 writes it.
+ * Planes Y, Cb, Cr one after the other; vvcr_output_bytes gives the frame size. dst: host memory
+ * (dst_on_device 0; returns when the copy is complete) or device memory (1; returns when written). The
+ * conversion runs on the GPU after the slot's last writer. */
+typedef struct vvcr_output_params {
+  int32_t file_bit_depth;       /* DecoderApp -d (0: internal bit depth) */
+  int32_t conf_left, conf_right, conf_top, conf_bottom;
+  int32_t clip_rec709;          /* DecoderApp --ClipOutputVideoToRec709Range */
+} vvcr_output_params;
+int64_t vvcr_output_bytes(const vvcr_ctx *ctx, const vvcr_output_params *op);
+int vvcr_write_output(vvcr_ctx *ctx, int32_t slot, const vvcr_output_params *op, void *dst, int32_t dst_on_device);
 /* DMVR refinement deltas of the last picture (PredictionUnit::mvdL0SubPu, 1/16 luma sample): one
  * {dx, dy} per 16x16 DMVR sub-block, PUs in descriptor order, sub-blocks in raster order inside each PU
  * (xProcessDMVR InterPrediction.cpp:2162-2296). Copies min(n, count) pairs into out and returns the

@@ -150,3 +150,16 @@ def deblock_picture(p, planes):
     r = L.or_deblock_picture(C.byref(d), *(_p(x) for x in out))
     assert r == 0, r
     return out
+
+
+def write_output(planes, bd, file_bd=0, conf=(0, 0, 0, 0), clip709=0):
+    """DecoderApp's output frame of one picture (oracle_output.c) as a uint8 array"""
+    L = lib()
+    y, u, v = (np.ascontiguousarray(x, np.int16) for x in planes)
+    h, w = y.shape
+    fbd = file_bd or bd
+    out = np.zeros(((2 if fbd > 8 else 1) * (w * h + 2 * (w // 2) * (h // 2)),), np.uint8)
+    L.or_write_output.restype = C.c_int64
+    n = L.or_write_output(w, h, bd, _p(y), _p(u), _p(v), w, w // 2, file_bd, *conf, clip709, _p(out))
+    assert n == out.size
+    return out

@@ -2,7 +2,7 @@
 # Re-creates the committed test bitstreams with the REFERENCE encoder built by oracle/ref.mk
 # (VTM 7.3 EncoderApp, CTC configs from /root/reference/cfg). Test-infrastructure only; runs in the
 # build container (needs /root/reference). Every stream carries MD5 decoded-picture-hash SEI.
-#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32
+#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32
 set -e
 R=/root/reference/cfg; E=${E:-$(dirname $0)/../oracle/_ref/EncoderApp}; T=${T:-/tmp/enc}; O=${O:-$(dirname $0)/../tests/golden/streams}
 mkdir -p $T $O
@@ -36,5 +36,8 @@ for n in "$@"; do case $n in
   ratile1080_q32) [ -f $T/syn1080.yuv ] || $G 1920 1080 9 $T/syn1080.yuv; enc $n encoder_randomaccess_vtm.cfg 1920 1080 9 32 $T/syn1080.yuv --SearchRange=64 $TILES --TileColumnWidthArray=15 --TileRowHeightArray=1 ;;
   # 8K, 8 tile rows (4,4,4,4,4,4,5,5 CTU rows); encoder fast-search settings only (the coded tools are the CTC set)
   ra4320t_q32) [ -f $T/syn4320.yuv ] || $G 7680 4320 3 $T/syn4320.yuv; enc $n encoder_randomaccess_vtm.cfg 7680 4320 3 32 $T/syn4320.yuv $TILES $FAST --TileColumnWidthArray=60 --TileRowHeightArray="4 4 4 4 4 4 5" ;;
+  # 412x236 coded as 416x240 with a conformance window (the encoder pads right / bottom to the 8-sample
+  # minimum CU size): DecoderApp's output crops it (VideoIOYuv::write), vvcr_write_output must too
+  ra412c_q32) [ -f $T/syn412.yuv ] || $G 412 236 5 $T/syn412.yuv; enc $n encoder_randomaccess_vtm.cfg 412 236 5 32 $T/syn412.yuv --ConformanceWindowMode=1 ;;
   *) echo "unknown stream $n"; exit 1 ;;
 esac; done

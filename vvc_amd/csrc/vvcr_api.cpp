@@ -194,7 +194,8 @@ struct vvcr_ctx {
   vvcr_seq_params sp{};
   std::string err;
   hipStream_t stream = nullptr;      // lane 0's stream (host copies, vvcr_stream)
-  hipStream_t copy_stream = nullptr; // halo row export / import (vvcr_export_rows / vvcr_import_rows)
+  hipStream_t copy_stream = nullptr; // halo row export / import (vvcr_export_rows / vvcr_import_rows), output frames
+  DevVec<uint8_t> out_stage;         // vvcr_write_output to host memory
   std::vector<std::array<DPlane, 3>> dpb;
   Lane lanes[MAXLANE];
   int nlane = 4, nintra = 2;         // lanes; the first nintra take pictures without references
@@ -1110,6 +1111,47 @@ static void rows_copy(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, char *
     dev += rowb * nr;
   }
   VVCR_CHECK_HIP(hipStreamSynchronize(cs));
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Output frames (include/vvcr.h vvcr_write_output)
+// ---------------------------------------------------------------------------------------------------
+static void check_output(const vvcr_ctx *ctx, const vvcr_output_params *op) {
+  if (!op) throw VvcrError(VVCR_E_ARG, "null output parameters");
+  const int W = ctx->sp.width, H = ctx->sp.height;
+  if (op->file_bit_depth < 0 || op->file_bit_depth > 16) throw VvcrError(VVCR_E_ARG, "file bit depth outside 0..16");
+  if (op->conf_left < 0 || op->conf_right < 0 || op->conf_top < 0 || op->conf_bottom < 0 ||
+      ((op->conf_left | op->conf_right | op->conf_top | op->conf_bottom) & 1) || op->conf_left + op->conf_right >= W ||
+      op->conf_top + op->conf_bottom >= H)
+    throw VvcrError(VVCR_E_ARG, "conformance window: even luma offsets (4:2:0) inside the picture");
+}
+
+int64_t vvcr_output_bytes(const vvcr_ctx *ctx, const vvcr_output_params *op) {
+  if (!ctx || !op) return VVCR_E_ARG;
+  const int bd = op->file_bit_depth ? op->file_bit_depth : ctx->sp.bit_depth;
+  const int64_t W = ctx->sp.width, H = ctx->sp.height;
+  return (bd > 8 ? 2 : 1) * (W * H + 2 * (W / 2) * (H / 2));
+}
+
+int vvcr_write_output(vvcr_ctx *ctx, int32_t slot, const vvcr_output_params *op, void *dst, int32_t dst_on_device) {
+  if (!ctx || !dst) return VVCR_E_ARG;
+  API_BEGIN
+  if (slot < 0 || slot >= (int)ctx->dpb.size()) throw VvcrError(VVCR_E_ARG, "bad slot");
+  check_output(ctx, op);
+  const int64_t nb = vvcr_output_bytes(ctx, op);
+  hipStream_t cs = ctx->copy_stream;
+  if (ctx->slot_w_set[slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(cs, ctx->slot_w[slot], 0));
+  uint8_t *out = (uint8_t *)dst;
+  if (!dst_on_device) {
+    ctx->out_stage.ensure((size_t)nb);
+    out = ctx->out_stage.p;
+  }
+  launch_output(ctx->dpb[slot], *op, ctx->sp.bit_depth, out, cs);
+  VVCR_CHECK_HIP(hipGetLastError());
+  if (!dst_on_device) VVCR_CHECK_HIP(hipMemcpyAsync(dst, out, (size_t)nb, hipMemcpyDeviceToHost, cs));
+  VVCR_CHECK_HIP(hipStreamSynchronize(cs));
+  return VVCR_OK;
+  API_END
 }
 
 int vvcr_export_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, void *dev_dst) {

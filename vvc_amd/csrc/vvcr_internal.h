@@ -1,6 +1,7 @@
 // vvcr_internal.h — shared host/device definitions of libvvcr (gfx950 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <array>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -228,4 +229,6 @@ void launch_planes3(const Planes3 &p, hipStream_t s);
 // jobs[0, nsmall): blocks of <= 256 samples (64-lane workgroups); jobs[nsmall, njobs): larger (256 lanes)
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, int nsmall, const int32_t *coef, const uint16_t *scans, hipStream_t s);
 void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);
+// DecoderApp output frame of a picture (vvcr_write_output)
+void launch_output(const std::array<DPlane, 3> &pic, const vvcr_output_params &op, int bd, uint8_t *dst, hipStream_t s);
 void launch_mc_tile(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);   // 32x32 jobs

@@ -17,6 +17,11 @@ BUF_RECO, BUF_PRED, BUF_RESI = 0, 1, 2
 I32 = C.c_int32
 
 
+class OutputParams(C.Structure):
+    """vvcr_output_params: DecoderApp -d, the conformance window (luma samples), --ClipOutputVideoToRec709Range"""
+    _fields_ = [(n, I32) for n in ("file_bit_depth", "conf_left", "conf_right", "conf_top", "conf_bottom", "clip_rec709")]
+
+
 class SeqParams(C.Structure):
     _fields_ = [(n, I32) for n in ("width", "height", "chroma_format", "bit_depth", "ctu_log2", "dpb_slots", "device")]
 
@@ -107,6 +112,9 @@ def lib():
         L.vvcr_picture_last_error.restype = C.c_char_p
         L.vvcr_picture_destroy.argtypes = [P]
         L.vvcr_prepare_planned.argtypes = [P, P, C.POINTER(I32)]
+        L.vvcr_output_bytes.argtypes = [P, C.POINTER(OutputParams)]
+        L.vvcr_output_bytes.restype = C.c_int64
+        L.vvcr_write_output.argtypes = [P, I32, C.POINTER(OutputParams), P, I32]
         L.vvcr_rows_bytes.argtypes = [P, I32]
         L.vvcr_rows_bytes.restype = C.c_int64
         L.vvcr_export_rows.argtypes = [P, I32, I32, I32, P]
@@ -126,7 +134,7 @@ EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_release_picture"
            "vvcr_rdo_release", "vvcr_rd_dist", "vvcr_fwd_transform", "vvcr_set_timing",
            "vvcr_picture_create", "vvcr_picture_submit", "vvcr_picture_set_loop_filter_params", "vvcr_picture_plan",
            "vvcr_picture_work_counts", "vvcr_picture_last_error", "vvcr_picture_destroy", "vvcr_prepare_planned",
-           "vvcr_rows_bytes", "vvcr_export_rows", "vvcr_import_rows"]
+           "vvcr_rows_bytes", "vvcr_export_rows", "vvcr_import_rows", "vvcr_output_bytes", "vvcr_write_output"]
 
 # encoder RDO block descriptors (include/vvcr.h vvcr_rd_block / vvcr_fwd_block) as numpy record types
 RD_BLOCK = [("org_off", "<i8"), ("cur_off", "<i8"), ("org_stride", "<i4"), ("cur_stride", "<i4"), ("width", "<i4"),
@@ -264,6 +272,19 @@ class Context:
         h = C.c_int32(0)
         self._chk(self.L.vvcr_prepare_planned(self.h, pic.h, C.byref(h)), "vvcr_prepare_planned")
         return h.value
+
+    def output_bytes(self, op):
+        return self.L.vvcr_output_bytes(self.h, C.byref(op))
+
+    def write_output(self, slot, op, dev_ptr=None):
+        """the slot's frame as DecoderApp writes it to its -o file (bytes); dev_ptr: write into device
+        memory instead and return None"""
+        if dev_ptr is not None:
+            self._chk(self.L.vvcr_write_output(self.h, slot, C.byref(op), dev_ptr, 1), "vvcr_write_output")
+            return None
+        buf = np.empty(self.output_bytes(op), np.uint8)
+        self._chk(self.L.vvcr_write_output(self.h, slot, C.byref(op), buf.ctypes.data, 0), "vvcr_write_output")
+        return buf
 
     def rows_bytes(self, n):
         return self.L.vvcr_rows_bytes(self.h, n)
