@@ -957,20 +957,24 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       // one clamped at its end (the reference extends it with its last sample); negative angles build the
       // main reference with its projected side part first
       const int W = isModeVer ? w : h, H = isModeVer ? h : w;   // in the (possibly transposed) frame
-      auto MAINv = [&](int k) { return isModeVer ? TOPv(k) : LEFTv(k); };
-      auto SIDEv = [&](int k) { return isModeVer ? LEFTv(k) : TOPv(k); };
+      // main / side lines as (pointer, stride, last index), resolved once: in place (tile, or refU / refF)
+      // for non-negative angles, the built references for negative ones. (Angular steps never use the
+      // on-the-fly smoothing: a smoothed angular step takes the refF copy.)
       const int lastM = (isModeVer ? topLen : leftLen);   // last index of the main line past mrl (mainLen)
-      const int16_t *cM = S.mainA + EXT + mrl, *cS = S.sideA + EXT + mrl;
+      const int16_t *mP = isModeVer ? tp_ : lp_, *sP = isModeVer ? lp_ : tp_;
+      int mSt = isModeVer ? 1 : lst_, sSt = isModeVer ? lst_ : 1;
+      int mLast = min(isModeVer ? tlast_ : llast_, lastM + mrl), sLast = isModeVer ? llast_ : tlast_;
       if (angle < 0) {
         int16_t *refMain = S.mainA + EXT, *refSide = S.sideA + EXT;
-        for (int k = lane; k <= W + 1 + mrl; k += 64) refMain[k] = (int16_t)MAINv(k);
-        for (int k = lane; k <= H + 1 + mrl; k += 64) refSide[k] = (int16_t)SIDEv(k);
-        for (int k = -H + lane; k <= -1; k += 64) refMain[k] = (int16_t)SIDEv(min((-k * invAngle + 256) >> 9, H));
+        for (int k = lane; k <= W + 1 + mrl; k += 64) refMain[k] = mP[min(k, mLast) * mSt];
+        for (int k = lane; k <= H + 1 + mrl; k += 64) refSide[k] = sP[min(k, sLast) * sSt];
+        for (int k = -H + lane; k <= -1; k += 64) refMain[k] = sP[min(min((-k * invAngle + 256) >> 9, H), sLast) * sSt];
         wsync();
+        mP = refMain; sP = refSide; mSt = sSt = 1; mLast = sLast = 1 << 20;
       }
       // rM / rS of xPredIntraAng (main / side reference from index mrl on)
-      auto rM = [&](int j) { return angle < 0 ? (int)cM[j] : MAINv(min(j, lastM) + mrl); };
-      auto rS = [&](int j) { return angle < 0 ? (int)cS[j] : SIDEv(j + mrl); };
+      auto rM = [&](int j) { return (int)mP[min(j + mrl, mLast) * mSt]; };
+      auto rS = [&](int j) { return (int)sP[min(j + mrl, sLast) * sSt]; };
       const bool integerSlope = (absAng & 31) == 0;
       const int scale0 = (ilog2(W) + ilog2(H) - 2) >> 2;
       finish([&](int ox, int oy) {
