@@ -127,7 +127,7 @@ struct WaveScratch {
 __shared__ int16_t s_tile[TILE_N];
 __shared__ WaveScratch s_ws[NW];
 __shared__ uint8_t s_ldone[kIntraMaxStepsPerCtu];
-__shared__ int8_t s_cubic[32][4];   // the 4-tap DCT-IF (chroma) filter the luma angular prediction uses
+__shared__ __attribute__((aligned(4))) int8_t s_cubic[32][4];   // the 4-tap DCT-IF (chroma) filter the luma angular prediction uses
 
 // Wave-level ordering of LDS traffic between the lanes of one wave (the steps of one workgroup run on
 // different waves, so the step body never uses a workgroup barrier). A wavefront-scope fence is not
@@ -993,7 +993,9 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
             if (comp == 0) {
               int f[4];
               if (!interp) {
-                for (int t = 0; t < 4; t++) f[t] = s_cubic[df][t];   // LDS copy: df differs per lane
+                const uint32_t cw = *reinterpret_cast<const uint32_t *>(&s_cubic[df][0]);   // df differs per lane: LDS, one read
+#pragma unroll
+                for (int t = 0; t < 4; t++) f[t] = (int)(int8_t)(cw >> (8 * t));
               } else {
                 f[0] = 16 - (df >> 1); f[1] = 32 - (df >> 1); f[2] = 16 + (df >> 1); f[3] = df >> 1;
               }
