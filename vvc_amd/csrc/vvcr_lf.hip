@@ -62,7 +62,7 @@ __device__ __forceinline__ int at(const DPlane &p, int x, int y) {
 }
 __device__ __forceinline__ int clip_alf(int c, int ref, int v0, int v1) { return clip3(-c, c, v0 - ref) + clip3(-c, c, v1 - ref); }
 
-__device__ void alf_rows(int y, int vbH, int vbPos, bool luma, int &r1, int &r2, int &r3, int &r4, int &r5, int &r6) {
+__device__ __forceinline__ void alf_rows(int y, int vbH, int vbPos, bool luma, int &r1, int &r2, int &r3, int &r4, int &r5, int &r6) {
   r1 = y + 1; r2 = y - 1; r3 = y + 2; r4 = y - 2; r5 = y + 3; r6 = y - 3;
   const int yVb = y & (vbH - 1);
   if (yVb < vbPos && yVb >= vbPos - (luma ? 4 : 2)) {
@@ -102,9 +102,22 @@ __global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
   const DPlane &D = P.dst[0];
   __shared__ int16_t t[ALF_SH * ALF_SW];
   __shared__ int32_t blk[(ALF_TW / 4) * (ALF_TH / 4)];   // class | transpose << 8 | enabled << 16
+  __shared__ int16_t s_cf[25 * 13], s_cl[25 * 13];       // the CTB's filter set: coefficients / clips per class
+  __shared__ int8_t s_perm[4 * 13];
   const int X0 = blockIdx.x * ALF_TW, Y0 = P.y0 + blockIdx.y * ALF_TH;
   const int tid = threadIdx.x;
   const int W = S.w, H = S.h;
+  // A 64x16 tile lies in one CTB: its enable flag and filter set are uniform, read at once (scalar), and
+  // the set's 25 classes of coefficients / clips are staged in LDS together with the samples, so the
+  // per-lane class lookups of the filter read LDS instead of memory after the classification.
+  const int ctbT = (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2);
+  const bool ctbOn = P.en[0] && P.ctb_en[ctbT];
+  if (ctbOn) {
+    const int set = P.ctb_set[ctbT];
+    const int16_t *cf = P.luma_coef + set * 25 * 13, *cl = P.luma_clip + set * 25 * 13;
+    for (int i = tid; i < 25 * 13; i += 256) { s_cf[i] = cf[i]; s_cl[i] = cl[i]; }
+    if (tid < 4 * 13) s_perm[tid] = (&c_perm7[0][0])[tid];
+  }
   {
     // all of a lane's tile loads in flight before its first LDS store (one memory round trip)
     constexpr int TWH = ALF_TW + 2 * ALF_HALO, NIT = (ALF_SH * TWH + 255) / 256;
@@ -131,8 +144,7 @@ __global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
     // --- classification (deriveClassificationBlk): block b, subsampled row pair ii
     const int b = tid >> 2, ii = tid & 3;
     const int bx = X0 + (b & 15) * 4, by = Y0 + (b >> 4) * 4;
-    const int ctb = (by >> P.ctu_log2) * P.wc + (bx >> P.ctu_log2);
-    const bool on = bx < W && by < H && P.en[0] && P.ctb_en[ctb];
+    const bool on = bx < W && by < H && ctbOn;
     int sumV = 0, sumH = 0, sumD0 = 0, sumD1 = 0;
     const int yv = by & (vbH - 1);
     const int i0 = (yv == vbPos) ? 1 : 0, i1 = (yv == vbPos - 4) ? 3 : 4;
@@ -187,12 +199,14 @@ __global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
     return;
   }
   const int classIdx = bi & 255, tr = (bi >> 8) & 255;
-  const int ctb = (by >> P.ctu_log2) * P.wc + (x >> P.ctu_log2);
-  const int set = P.ctb_set[ctb];
-  const int16_t *coef = P.luma_coef + (set * 25 + classIdx) * 13, *clip = P.luma_clip + (set * 25 + classIdx) * 13;
+  const int16_t *coef = s_cf + classIdx * 13, *clip = s_cl + classIdx * 13;
   int fc[12], fl[12];
 #pragma unroll
-  for (int k = 0; k < 12; k++) { fc[k] = coef[c_perm7[tr][k]]; fl[k] = clip[c_perm7[tr][k]]; }
+  for (int k = 0; k < 12; k++) {
+    const int pk = s_perm[tr * 13 + k];
+    fc[k] = coef[pk];
+    fl[k] = clip[pk];
+  }
   const int maxv = (1 << P.bd) - 1;
   for (int y = by; y < by + 4 && y < H; y++) {
     int r1, r2, r3, r4, r5, r6;
