@@ -20,88 +20,173 @@ constexpr int TMIN = -(1 << MAX_TR_DYN), TMAX = (1 << MAX_TR_DYN) - 1;
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ int ilog2d(int v) { return 31 - __clz(v); }
 
-// transform matrix entry M_N[k][j] (k = basis index)
-__device__ __forceinline__ int tmat(int type, int N, int k, int j) {
-  if (type == TR_DCT2) return vvcr_tab::dct2_64[k * (64 / N)][j];
+
+// A transform matrix M_N as rows: entry (k, j) at base[k * rs + j].
+struct TMat {
+  const int8_t *base;
+  int rs;
+};
+__device__ __forceinline__ TMat tmat_rows(int type, int N) {
+  if (type == TR_DCT2) return {&vvcr_tab::dct2_64[0][0], 64 * (64 / N)};
   if (type == TR_DST7) {
     switch (N) {
-      case 4: return vvcr_tab::dst7_4[k][j];
-      case 8: return vvcr_tab::dst7_8[k][j];
-      case 16: return vvcr_tab::dst7_16[k][j];
-      default: return vvcr_tab::dst7_32[k][j];
+      case 4: return {&vvcr_tab::dst7_4[0][0], 4};
+      case 8: return {&vvcr_tab::dst7_8[0][0], 8};
+      case 16: return {&vvcr_tab::dst7_16[0][0], 16};
+      default: return {&vvcr_tab::dst7_32[0][0], 32};
     }
   }
   switch (N) {
-    case 4: return vvcr_tab::dct8_4[k][j];
-    case 8: return vvcr_tab::dct8_8[k][j];
-    case 16: return vvcr_tab::dct8_16[k][j];
-    default: return vvcr_tab::dct8_32[k][j];
+    case 4: return {&vvcr_tab::dct8_4[0][0], 4};
+    case 8: return {&vvcr_tab::dct8_8[0][0], 8};
+    case 16: return {&vvcr_tab::dct8_16[0][0], 16};
+    default: return {&vvcr_tab::dct8_32[0][0], 32};
   }
 }
 
-// state after consuming one level (DepQuant.cpp:768: table 32040)
-__device__ __forceinline__ int dq_next(int s, int level) { return (32040 >> ((s << 2) + ((level & 1) << 1))) & 3; }
+// Staged matrix rows are packed row-major, N int8 per row, four to a dword; a 2-point matrix is one dword.
+__device__ __forceinline__ int mat_dwords(int N, int rows) { return N >= 4 ? rows * N / 4 : (rows > 0 ? 1 : 0); }
+__device__ __forceinline__ int32_t mat_dword(const TMat &m, int N, int d) {
+  if (N >= 4) {
+    const int lq = ilog2d(N) - 2;
+    const int k = d >> lq, j = (d & ((1 << lq) - 1)) << 2;
+    return *(const int32_t *)(m.base + k * m.rs + j);
+  }
+  const int8_t *p0 = m.base, *p1 = m.base + m.rs;
+  return (p0[0] & 255) | ((p0[1] & 255) << 8) | ((p1[0] & 255) << 16) | ((int32_t)(p1[1] & 255) << 24);
+}
+__device__ __forceinline__ int sbyte(int32_t m, int e) { return (m << (24 - 8 * e)) >> 24; }
 
 // One workgroup of NT lanes per transform block (NT = 64 for blocks of <= 256 samples, 256 above),
 // the block in LDS as int32. The passes only visit the bounding box of the non-zero levels
 // (TbJob::nz_rows/nz_cols, host-computed): a row / column of zero levels contributes nothing to the
-// vertical / horizontal sums, so restricting the sums to the box is exact. The transform matrix rows
-// of the two passes are staged in LDS once per block.
+// vertical / horizontal sums, so restricting the sums to the box is exact.
+//
+// The kernel is latency bound (one small block per workgroup, a dependent chain of global loads, LDS
+// round trips and barriers), so every global read of the block — the box of levels, the scan positions
+// of the dependent-quantisation lanes, the matrix rows of both passes — is issued at the start, flat
+// dequantisation is applied in registers, and the transform passes produce four outputs per lane from
+// dword reads of the packed matrix rows.
 template <int MAXN, int NT>
 __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restrict__ jobs, const int32_t *__restrict__ coef,
                                               const uint16_t *__restrict__ scans) {
-  __shared__ int32_t c[MAXN];
-  __shared__ int32_t t[MAXN];
-  __shared__ int8_t mv[32 * 64];           // vertical-pass matrix rows k < 32 (zero-out), columns < h
-  __shared__ int8_t mh[32 * 64];           // horizontal-pass matrix rows k < 32, columns < w
-  __shared__ int32_t lf[48];
+  constexpr int PER = MAXN / NT;             // level slots per lane
+  constexpr int MD = 32 * 64 / 4 / NT;       // matrix dwords per lane and pass
+  __shared__ __attribute__((aligned(16))) int32_t c[MAXN];
+  __shared__ __attribute__((aligned(16))) int32_t t[MAXN];
+  __shared__ int32_t mv[32 * 64 / 4];        // vertical-pass matrix rows k < 32 (zero-out), packed int8
+  __shared__ int32_t mh[32 * 64 / 4];        // horizontal-pass (or 1-D) matrix rows
   const int tid = threadIdx.x, lane = tid & 63;
-  const TbJob J = jobs[blockIdx.x];
+  const TbJob J = load_uniform(jobs + blockIdx.x);
   const int w = J.w, h = J.h, n = w * h;
   const int lw = ilog2d(w), lh = ilog2d(h);
   const bool ts = J.flags & TB_TS;
-  int R = J.nz_rows, C = J.nz_cols;
-  // 1. levels: the box from the pool, zeros elsewhere
+  const bool dq = (J.flags & TB_DQ) && !ts;
+  const int bdpcm = (J.flags >> TB_BDPCM_SHIFT) & 3;
+  const int R = J.nz_rows, C = J.nz_cols;
+  const bool two_d = w > 1 && h > 1;
+  // transform geometry (TrQuant.cpp:841-888): the non-zero rows / columns of the two passes, or the 1-D cut
+  const int N1 = w > 1 ? w : h;
+  const int Rv = min(R, h - J.skip_h), Cv = min(C, w - J.skip_w);
+  const int cut = N1 - (w > 1 ? J.skip_w : J.skip_h);
+  const TMat Mv = tmat_rows(J.trv, h);
+  const TMat Mh = tmat_rows(two_d || w > 1 ? J.trh : J.trv, two_d ? w : N1);
+  const int Nh = two_d ? w : N1;
+  const int nv = (ts || !two_d) ? 0 : mat_dwords(h, Rv), nh = ts ? 0 : mat_dwords(Nh, two_d ? Cv : cut);
+
+  // 1. every global read of the block up front
   const int32_t *lv = coef + J.coef;
-  for (int i = tid; i < n; i += NT) {
-    const int y = i >> lw, x = i & (w - 1);
-    c[i] = (y < R && x < C) ? lv[i] : 0;
+  int lvv[PER];
+#pragma unroll
+  for (int q = 0; q < PER; q++) {
+    const int i = tid + q * NT;
+    lvv[q] = (i < n && (i >> lw) < R && (i & (w - 1)) < C) ? lv[i] : 0;
+  }
+  const int ns = min(w, 32) * min(h, 32);
+  uint32_t sc[16];
+  if (dq && tid < 64) {
+    const uint16_t *scan = scans + P.scan_off[lw][lh];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      const int s = lane * 16 + k;
+      sc[k] = s < ns ? scan[s] : 0;
+    }
+  }
+  int32_t mvr[MD], mhr[MD];
+#pragma unroll
+  for (int q = 0; q < MD; q++) {
+    const int d = tid + q * NT;
+    mvr[q] = d < nv ? mat_dword(Mv, h, d) : 0;
+    mhr[q] = d < nh ? mat_dword(Mh, Nh, d) : 0;
+  }
+  // 2a. flat dequantisation (Quant::dequant, Quant.cpp:369) in registers; zeros stay zero
+  const bool flat = !dq && !bdpcm;
+  const int sqrtAdjF = !ts && ((lw + lh) & 1);
+  const int trShiftF = MAX_TR_DYN - P.bd - ((lw + lh) >> 1) - sqrtAdjF;
+  const int perF = J.qp / 6, remF = J.qp % 6;
+  const int rsF = 6 - ((ts ? 0 : trShiftF) + perF);
+  const int scaleF = vvcr_tab::inv_quant_scales[sqrtAdjF][remF];
+  const int tibF = min(32 + rsF - 7, MAX_TR_DYN + 1);
+  const int cminF = -(1 << (tibF - 1)), cmaxF = (1 << (tibF - 1)) - 1;
+  auto flat_dq = [&](int lvl) {
+    const int q = clip3(cminF, cmaxF, lvl);
+    const int v = rsF > 0 ? (q * scaleF + (1 << (rsF - 1))) >> rsF : (q * scaleF) << -rsF;
+    return clip3(TMIN, TMAX, v);
+  };
+#pragma unroll
+  for (int q = 0; q < PER; q++) {
+    const int i = tid + q * NT;
+    if (i < n) c[i] = flat ? flat_dq(lvv[q]) : lvv[q];
+  }
+#pragma unroll
+  for (int q = 0; q < MD; q++) {
+    const int d = tid + q * NT;
+    if (d < nv) mv[d] = mvr[q];
+    if (d < nh) mh[d] = mhr[q];
   }
   __syncthreads();
-  // 2. dequantisation
-  if ((J.flags & TB_DQ) && !ts) {
-    // 4-state machine along the reverse scan, in parallel on the first wave: each lane owns 16
-    // consecutive scan positions, summarises them as a state->state map, a wave-wide prefix of map
-    // compositions gives every lane its entry state, then lanes dequantise their positions in place.
+
+  // 2b. dependent quantisation: the 4-state machine along the reverse scan, on the first wave. Each lane
+  // owns 16 consecutive scan positions and summarises them as a state map; a wave-wide prefix of map
+  // compositions gives every lane its entry state, then lanes dequantise their positions in place.
+  // The machine (DepQuant.cpp:768, table 32040) is (lo, hi) -> (hi, lo ^ parity) per level, so every
+  // composition of steps has the form (l, h) -> swap ? (h ^ x, l ^ y) : (l ^ x, h ^ y).
+  if (dq) {
     if (tid < 64) {
-      const uint16_t *scan = scans + P.scan_off[lw][lh];
-      const int ns = min(w, 32) * min(h, 32);
+      int lev[16];
       int last = -1;
+#pragma unroll
       for (int k = 0; k < 16; k++) {
         const int s = lane * 16 + k;
-        if (s < ns && c[scan[s]] != 0) last = s;
+        lev[k] = s < ns ? c[sc[k]] : 0;
+        if (lev[k] != 0) last = s;
       }
       for (int o = 32; o > 0; o >>= 1) last = max(last, __shfl_xor(last, o));
       if (last >= 0) {
-        const int lo = lane * 16, hi = min(lo + 15, last);
-        int m = 0;   // packed map: 2 bits per entry state
-        for (int s0 = 0; s0 < 4; s0++) {
-          int st = s0;
-          for (int p = hi; p >= lo; p--) st = dq_next(st, c[scan[p]]);
-          m |= st << (2 * s0);
-        }
-        // inclusive prefix over lanes in DESCENDING lane order: F_l = M_l o M_{l+1} o ... (apply higher first)
-        int f = m;
+        const int cnt = last - lane * 16;   // positions k <= cnt of this lane take part
+        int sw = 0, x = 0, y = 0;
+#pragma unroll
+        for (int k = 15; k >= 0; k--)
+          if (k <= cnt) {
+            const int nx = y;
+            y = x ^ (lev[k] & 1);
+            x = nx;
+            sw ^= 1;
+          }
+        // inclusive prefix over lanes in DESCENDING lane order: F_l = M_l o M_{l+1} o ... (higher first);
+        // packed as bit 0 swap, bit 1 x, bit 2 y
+        int f = sw | (x << 1) | (y << 2);
         for (int o = 1; o < 64; o <<= 1) {
           const int g = __shfl_down(f, o);
           if (lane + o < 64) {
-            int r = 0;
-            for (int s0 = 0; s0 < 4; s0++) r |= ((f >> (2 * ((g >> (2 * s0)) & 3))) & 3) << (2 * s0);
-            f = r;
+            const int sB = f & 1, xB = (f >> 1) & 1, yB = (f >> 2) & 1;
+            const int sA = g & 1, xA = (g >> 1) & 1, yA = (g >> 2) & 1;
+            const int xs = sB ? yA : xA, ys = sB ? xA : yA;
+            f = (sA ^ sB) | ((xs ^ xB) << 1) | ((ys ^ yB) << 2);
           }
         }
         const int fin = __shfl_down(f, 1);
-        const int sIn = (lane == 63) ? 0 : (fin & 3);   // start state 0 at 'last'
+        int st = (lane == 63) ? 0 : ((fin >> 1) & 3);   // start state 0 at 'last'
         const int qpDQ = J.qp + 1, per = qpDQ / 6, rem = qpDQ - 6 * per;
         const int sqrtAdj = (lw + lh) & 1;
         const int trShift = MAX_TR_DYN - P.bd - ((lw + lh) >> 1) - sqrtAdj;
@@ -110,91 +195,78 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
         if (shift < 0) scale <<= -shift;     // applied at the last position and kept (DepQuant.cpp:760-763)
         const int add = shift < 0 ? 0 : ((1 << shift) >> 1);
         const int sh = shift < 0 ? 0 : shift;
-        int st = sIn;
-        for (int p = hi; p >= lo; p--) {   // each position is read then written by its own lane only
-          const int level = c[scan[p]];
-          int v = 0;
-          if (level) {
-            const int q = (level << 1) + (level > 0 ? -(st >> 1) : (st >> 1));
-            const long long nom = ((long long)q * scale + add) >> sh;
-            v = (int)(nom < TMIN ? TMIN : (nom > TMAX ? TMAX : nom));
+#pragma unroll
+        for (int k = 15; k >= 0; k--) {      // each position is read then written by its own lane only
+          if (k <= cnt) {
+            const int level = lev[k];
+            int v = 0;
+            if (level) {
+              const int q = (level << 1) + (level > 0 ? -(st >> 1) : (st >> 1));
+              const long long nom = ((long long)q * scale + add) >> sh;
+              v = (int)(nom < TMIN ? TMIN : (nom > TMAX ? TMAX : nom));
+            }
+            c[sc[k]] = v;
+            st = (st >> 1) | (((st ^ level) & 1) << 1);
           }
-          c[scan[p]] = v;
-          st = dq_next(st, level);
         }
       }
     }
     __syncthreads();
-  } else {
+  } else if (bdpcm) {
     // BDPCM accumulation of levels (invResDPCM Quant.cpp:155), then flat dequant
-    const int bdpcm = (J.flags >> TB_BDPCM_SHIFT) & 3;
     if (bdpcm == 1) {
       for (int y = tid; y < h; y += NT)
         for (int x = 1; x < w; x++) c[y * w + x] = clip3(TMIN, TMAX, c[y * w + x - 1] + c[y * w + x]);
-    } else if (bdpcm == 2) {
+    } else {
       for (int x = tid; x < w; x += NT)
         for (int y = 1; y < h; y++) c[y * w + x] = clip3(TMIN, TMAX, c[(y - 1) * w + x] + c[y * w + x]);
     }
-    if (bdpcm) __syncthreads();
-    const int sqrtAdj = !ts && ((lw + lh) & 1);
-    const int trShift = MAX_TR_DYN - P.bd - ((lw + lh) >> 1) - sqrtAdj;
-    const int per = J.qp / 6, rem = J.qp % 6;
-    const int rs = 6 - ((ts ? 0 : trShift) + per);
-    const int scale = vvcr_tab::inv_quant_scales[sqrtAdj][rem];
-    int tib = 32 + rs - 7;
-    if (tib > MAX_TR_DYN + 1) tib = MAX_TR_DYN + 1;
-    const int cmin = -(1 << (tib - 1)), cmax = (1 << (tib - 1)) - 1;
-    for (int i = tid; i < n; i += NT) {
-      if ((i >> lw) >= R || (i & (w - 1)) >= C) continue;
-      const int q = clip3(cmin, cmax, c[i]);
-      const int v = rs > 0 ? (q * scale + (1 << (rs - 1))) >> rs : (q * scale) << -rs;
-      c[i] = clip3(TMIN, TMAX, v);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      const int i = tid + q * NT;
+      if (i < n && (i >> lw) < R && (i & (w - 1)) < C) c[i] = flat_dq(c[i]);
     }
     __syncthreads();
   }
-  // 3. inverse LFNST (TrQuant::xInvLfnst); its output area is inside the box (host widened it)
+  // 3. inverse LFNST (TrQuant::xInvLfnst); its output area is inside the box (host widened it). Lane tid
+  // computes output tid, then writes it to its position of the top-left 4x4 / 8x8 region.
   if (!ts && J.lfnst_idx > 0 && (J.flags & TB_LFNST_APPLY)) {
     const bool whge3 = w >= 8 && h >= 8;
     const uint16_t *scan = whge3 ? scans + P.lfnst_scan_off[lw] : scans + P.scan_off[lw][lh];
     const int trSize = whge3 ? 48 : 16;
     const int zeroOut = ((w == 4 && h == 4) || (w == 8 && h == 8)) ? 8 : 16;
     const int lm = vvcr_tab::lfnst_lut[J.lfnst_mode];
-    if (tid < trSize) {
+    const bool act = tid < trSize;
+    int v = 0;
+    if (act) {
+      const int8_t *m = whge3 ? &vvcr_tab::lfnst8x8[lm][J.lfnst_idx - 1][0][tid] : &vvcr_tab::lfnst4x4[lm][J.lfnst_idx - 1][0][tid];
+      const int ms = whge3 ? 48 : 16;
       int s = 0;
-      for (int i = 0; i < zeroOut; i++) {
-        const int m = whge3 ? vvcr_tab::lfnst8x8[lm][J.lfnst_idx - 1][i][tid]
-                            : vvcr_tab::lfnst4x4[lm][J.lfnst_idx - 1][i][tid];
-        s += c[scan[i]] * m;
-      }
-      lf[tid] = clip3(TMIN, TMAX, (s + 64) >> 7);
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        if (i < zeroOut) s += c[scan[i]] * m[i * ms];
+      v = clip3(TMIN, TMAX, (s + 64) >> 7);
     }
     __syncthreads();
-    if (tid == 0) {
-      const int *p = lf;
+    if (act) {
+      int y, x;
       if (J.flags & TB_LFNST_TRANSPOSE) {
-        if (!whge3) {
-          for (int y = 0; y < 4; y++, p++) { c[y * w] = p[0]; c[y * w + 1] = p[4]; c[y * w + 2] = p[8]; c[y * w + 3] = p[12]; }
-        } else {
-          for (int y = 0; y < 8; y++, p++) {
-            c[y * w] = p[0]; c[y * w + 1] = p[8]; c[y * w + 2] = p[16]; c[y * w + 3] = p[24];
-            if (y < 4) { c[y * w + 4] = p[32]; c[y * w + 5] = p[36]; c[y * w + 6] = p[40]; c[y * w + 7] = p[44]; }
-          }
-        }
+        if (!whge3) { y = tid & 3; x = tid >> 2; }
+        else if (tid < 32) { y = tid & 7; x = tid >> 3; }
+        else { y = (tid - 32) & 3; x = 4 + ((tid - 32) >> 2); }
       } else {
-        const int sb = whge3 ? 8 : 4;
-        for (int y = 0; y < sb; y++) {
-          const int st = y < 4 ? sb : 4;
-          for (int x = 0; x < st; x++) c[y * w + x] = p[x];
-          p += st;
-        }
+        if (!whge3) { y = tid >> 2; x = tid & 3; }
+        else if (tid < 32) { y = tid >> 3; x = tid & 7; }
+        else { y = 4 + ((tid - 32) >> 2); x = (tid - 32) & 3; }
       }
+      c[y * w + x] = v;
     }
     __syncthreads();
   }
   // 4. inverse transform (or transform skip) -> residual, written straight to the plane(s)
   const DPlane &o = P.out[J.comp];
-  auto store = [&](int i, int v) {   // sample i (row-major) of the block, + joint Cb-Cr second component
-    const int y = i >> lw, x = i & (w - 1);
+  auto store = [&](int y, int x, int v) {   // sample (x, y) of the block, + joint Cb-Cr second component
     o.p[(size_t)(J.y + y) * o.stride + J.x + x] = (int16_t)v;
     if (J.ict) {
       const DPlane &o2 = P.out[J.comp == 1 ? 2 : 1];
@@ -209,39 +281,78 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
     }
   };
   if (ts) {
-    for (int i = tid; i < n; i += NT) store(i, (int16_t)c[i]);
+    for (int i = tid; i < n; i += NT) store(i >> lw, i & (w - 1), (int16_t)c[i]);
     return;
   }
   const int shift2 = 6 + MAX_TR_DYN - 1 - P.bd;
-  if (w > 1 && h > 1) {
-    const int Cv = min(C, w - J.skip_w), Rv = min(R, h - J.skip_h);   // non-zero columns / rows
-    // stage matrix rows: vertical M_h-point rows k < Rv, horizontal M_w-point rows k < Cv
-    for (int i = tid; i < Rv * h; i += NT) { const int k = i >> lh, j = i & (h - 1); mv[i] = (int8_t)tmat(J.trv, h, k, j); }
-    for (int i = tid; i < Cv * w; i += NT) { const int k = i >> lw, j = i & (w - 1); mh[i] = (int8_t)tmat(J.trh, w, k, j); }
-    __syncthreads();
-    // vertical pass: t[i*h + j] for columns i < Cv (TrQuant.cpp:868)
-    for (int idx = tid; idx < Cv * h; idx += NT) {
-      const int i = idx >> lh, j = idx & (h - 1);
-      int s = 0;
-      for (int k = 0; k < Rv; k++) s += c[k * w + i] * mv[k * h + j];
-      t[i * h + j] = clip3(TMIN, TMAX, (s + 64) >> 7);
+  const int8_t *mvb = (const int8_t *)mv, *mhb = (const int8_t *)mh;
+  if (two_d) {
+    // vertical pass (TrQuant.cpp:868): t[i*h + j] for columns i < Cv, four rows j per lane
+    if (h >= 4) {
+      const int lq = lh - 2, qm = (1 << lq) - 1;
+      for (int idx = tid; idx < (Cv << lq); idx += NT) {
+        const int i = idx >> lq, jq = idx & qm;
+        int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll 4
+        for (int k = 0; k < Rv; k++) {
+          const int cv = c[k * w + i];
+          const int32_t m = mv[(k << lq) + jq];
+          s0 += cv * sbyte(m, 0);
+          s1 += cv * sbyte(m, 1);
+          s2 += cv * sbyte(m, 2);
+          s3 += cv * sbyte(m, 3);
+        }
+        *(int4 *)&t[i * h + (jq << 2)] = make_int4(clip3(TMIN, TMAX, (s0 + 64) >> 7), clip3(TMIN, TMAX, (s1 + 64) >> 7),
+                                                   clip3(TMIN, TMAX, (s2 + 64) >> 7), clip3(TMIN, TMAX, (s3 + 64) >> 7));
+      }
+    } else {
+      for (int idx = tid; idx < Cv * h; idx += NT) {
+        const int i = idx >> lh, j = idx & (h - 1);
+        int s = 0;
+        for (int k = 0; k < Rv; k++) s += c[k * w + i] * mvb[k * h + j];
+        t[i * h + j] = clip3(TMIN, TMAX, (s + 64) >> 7);
+      }
     }
     __syncthreads();
-    // horizontal pass over the Cv non-zero columns of t
-    for (int idx = tid; idx < n; idx += NT) {
-      const int r = idx >> lw, j = idx & (w - 1);
-      int s = 0;
-      for (int k = 0; k < Cv; k++) s += t[k * h + r] * mh[k * w + j];
-      store(idx, (int16_t)clip3(TMIN, TMAX, (s + (1 << (shift2 - 1))) >> shift2));
+    // horizontal pass over the Cv non-zero columns of t, four columns j per lane
+    const int rnd = 1 << (shift2 - 1);
+    if (w >= 4) {
+      const int lq = lw - 2, qm = (1 << lq) - 1;
+      for (int idx = tid; idx < (h << lq); idx += NT) {
+        const int r = idx >> lq, jq = idx & qm;
+        int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+#pragma unroll 4
+        for (int k = 0; k < Cv; k++) {
+          const int tv = t[k * h + r];
+          const int32_t m = mh[(k << lq) + jq];
+          s0 += tv * sbyte(m, 0);
+          s1 += tv * sbyte(m, 1);
+          s2 += tv * sbyte(m, 2);
+          s3 += tv * sbyte(m, 3);
+        }
+        const int j0 = jq << 2;
+        store(r, j0, (int16_t)clip3(TMIN, TMAX, (s0 + rnd) >> shift2));
+        store(r, j0 + 1, (int16_t)clip3(TMIN, TMAX, (s1 + rnd) >> shift2));
+        store(r, j0 + 2, (int16_t)clip3(TMIN, TMAX, (s2 + rnd) >> shift2));
+        store(r, j0 + 3, (int16_t)clip3(TMIN, TMAX, (s3 + rnd) >> shift2));
+      }
+    } else {
+      for (int idx = tid; idx < n; idx += NT) {
+        const int r = idx >> lw, j = idx & (w - 1);
+        int s = 0;
+        for (int k = 0; k < Cv; k++) s += t[k * h + r] * mhb[k * w + j];
+        store(r, j, (int16_t)clip3(TMIN, TMAX, (s + rnd) >> shift2));
+      }
     }
   } else {
     // 1-D (ISP 1xN / Nx1): single pass with shift + 1 (TrQuant.cpp:874-888)
-    const int N = w > 1 ? w : h, type = w > 1 ? J.trh : J.trv, cut = N - (w > 1 ? J.skip_w : J.skip_h);
     const int sh = shift2 + 1;
-    for (int j = tid; j < N; j += NT) {
+    for (int j = tid; j < N1; j += NT) {
       int s = 0;
-      for (int k = 0; k < cut; k++) s += c[k] * tmat(type, N, k, j);
-      store(j, (int16_t)clip3(TMIN, TMAX, (s + (1 << (sh - 1))) >> sh));
+#pragma unroll 4
+      for (int k = 0; k < cut; k++) s += c[k] * mhb[k * N1 + j];
+      const int v = (int16_t)clip3(TMIN, TMAX, (s + (1 << (sh - 1))) >> sh);
+      if (w > 1) store(0, j, v); else store(j, 0, v);
     }
   }
 }
