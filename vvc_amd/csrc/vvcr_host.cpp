@@ -328,6 +328,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       if (p.dmvr || p.bdof) {
         McJob j = make_job(pp, p.interdir, p.ref0, p.ref1, p.mv0x, p.mv0y, p.mv1x, p.mv1y, bcw, alt);
         if ((j.flags & (MC_L0 | MC_L1)) != (MC_L0 | MC_L1)) fail("DMVR/BDOF PU is not bi-predicted");
+        if (p.w % 8 || p.h % 8) fail("DMVR/BDOF PU size is not a multiple of 8");   // k_mc_bidir: 8 or 16 per side
         if (p.bdof) j.flags |= MC_BDOF;
         if (p.dmvr) {
           // xProcessDMVR sub-blocks (InterPrediction.cpp:2162-2166), raster order = delta order
