@@ -199,6 +199,7 @@ struct vvcr_ctx {
   std::vector<std::array<DPlane, 3>> dpb;
   Lane lanes[MAXLANE];
   int nlane = 4, nintra = 2;         // lanes; the first nintra take pictures without references
+  int intra_wg = 0;                  // k_intra workgroups (VVCR_INTRA_WG, default set in vvcr_create)
   uint64_t seq = 0;
   bool timing = true;                // record per-kernel-group events (vvcr_set_timing)
   // Dependency markers, owned per DPB slot so that no event is ever shared between slots: slot_w[s] is
@@ -541,7 +542,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     {
       KernelTimer t(r, K_INTRA, s, ctx->timing);
       launch_intra(r.iparams.p + L, r.ijobs.p, r.n_ijobs, r.ictu_list.p, r.ictu_start.p, r.n_ictu, r.idep_start.p, r.ideps.p,
-                   r.istate.p, ctx->d_err, ctx->n_cu, s);
+                   r.istate.p, ctx->d_err, ctx->intra_wg, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_INTRA] = r.n_ijobs ? 1 : 0;
     }
@@ -632,6 +633,7 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     if (const char *e = getenv("VVCR_LANES")) ctx->nlane = std::max(2, std::min(MAXLANE, atoi(e)));
     ctx->nintra = ctx->nlane / 2;
     if (const char *e = getenv("VVCR_INTRA_LANES")) ctx->nintra = std::max(1, std::min(ctx->nlane - 1, atoi(e)));
+    if (const char *e = getenv("VVCR_INTRA_WG")) ctx->intra_wg = std::max(0, atoi(e));
     for (int l = 0; l < ctx->nlane; l++) VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->lanes[l].s, hipStreamNonBlocking));
     ctx->stream = ctx->lanes[0].s;
     VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
@@ -660,6 +662,13 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
         ln.tmp[c] = alloc_plane(w, h);
       }
     VVCR_CHECK_HIP(hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, sp->device));
+    if (ctx->intra_wg <= 0) {
+      // k_intra takes CTUs in wavefront order: the CTUs in flight are those of about two anti-diagonals
+      // (x + 2y), so four diagonals' worth of workgroups keeps the wavefront busy (1080p, CTU 128: 32,
+      // as fast as one per CU, and the other lanes' kernels get the CUs the idle workgroups held)
+      const int ctu = 1 << sp->ctu_log2, wc = (sp->width + ctu - 1) / ctu, hc = (sp->height + ctu - 1) / ctu;
+      ctx->intra_wg = std::min(ctx->n_cu, 4 * std::min(hc, (wc + 1) / 2));
+    }
     VVCR_CHECK_HIP(hipMalloc(&ctx->d_err, sizeof(int32_t)));
     VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof(int32_t)));
     build_scan_tables(ctx->scans);

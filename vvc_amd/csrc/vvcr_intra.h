@@ -122,5 +122,5 @@ void launch_lmcs_inverse(const DPlane &luma, const int16_t *inv_lut, int y0, int
 // all steps of a picture in one persistent launch, one CTU per workgroup at a time; state: 16 + n int32
 // (reset here); *err set on a wait timeout
 void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *ctu_list, const int32_t *ctu_start,
-                  int nctu, const int32_t *dep_start, const int32_t *deps, int32_t *state, int32_t *err, int n_cu,
+                  int nctu, const int32_t *dep_start, const int32_t *deps, int32_t *state, int32_t *err, int n_wg,
                   hipStream_t s);

@@ -1029,9 +1029,10 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   IPROF(6);
 }
 
-// Persistent: each workgroup takes CTUs (that have steps) in raster order from an atomic counter; its
-// waves take the CTU's steps in topological order from an LDS counter. A CTU only waits for CTUs taken
-// before it (left / above neighbours), and a step only for earlier steps, so every wave progresses.
+// Persistent: each workgroup takes CTUs (that have steps) in the plan's order (wavefront) from an
+// atomic counter; its waves take the CTU's steps in topological order from an LDS counter. A CTU only
+// waits for CTUs taken before it (left / above neighbours), and a step only for earlier steps, so every
+// wave progresses.
 // state[0] = CTU counter, state[16 + i] = global flag of published step i; *err set if a wait times out.
 __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict__ Pg, const IntraJob *__restrict__ jobs,
                                                    const int32_t *__restrict__ ctu_list, const int32_t *__restrict__ ctu_start,
@@ -1196,11 +1197,11 @@ void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hip
 }
 
 void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *ctu_list, const int32_t *ctu_start,
-                  int nctu, const int32_t *dep_start, const int32_t *deps, int32_t *state, int32_t *err, int n_cu,
+                  int nctu, const int32_t *dep_start, const int32_t *deps, int32_t *state, int32_t *err, int n_wg,
                   hipStream_t s) {
   if (n <= 0 || nctu <= 0) return;
   VVCR_CHECK_HIP(hipMemsetAsync(state, 0, (16 + (size_t)n) * sizeof(int32_t), s));
-  // one workgroup per CU (the LDS tile + wave scratch take ~145 KiB), never more than the CTUs
-  hipLaunchKernelGGL(k_intra, dim3(std::min(nctu, n_cu)), dim3(64 * NW), 0, s, p_dev, jobs, ctu_list, ctu_start, nctu,
+  // n_wg persistent workgroups (the caller sizes it to the wavefront), never more than the CTUs
+  hipLaunchKernelGGL(k_intra, dim3(std::min(nctu, n_wg)), dim3(64 * NW), 0, s, p_dev, jobs, ctu_list, ctu_start, nctu,
                      dep_start, deps, state, err);
 }

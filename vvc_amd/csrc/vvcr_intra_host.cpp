@@ -658,6 +658,28 @@ struct Planner {
       }
     }
     PROF_MARK("wdeps");
+    // CTU order of the launch: wavefront (anti-diagonals x + 2y, VVCR_CTU_ORDER=raster for the raster
+    // order). Every cross-CTU dependency (left, above-left, above, above-right) is on an earlier CTU in
+    // both orders, so a workgroup only ever waits for CTUs already taken; in wavefront order the CTUs
+    // taken but not finished are the few on the active diagonals, so a launch of a few dozen workgroups
+    // keeps the whole wavefront busy (raster order needs about a row of CTUs per active row).
+    {
+      static const bool raster = [] { const char *e = getenv("VVCR_CTU_ORDER"); return e && !strcmp(e, "raster"); }();
+      const int nb = (int)cb.size() - 1;
+      if (!raster && nb > 1) {
+        std::vector<int32_t> bo(nb);
+        for (int k = 0; k < nb; k++) bo[k] = k;
+        auto key = [&](int k) {
+          const int c = ctu_of_job[cb[k]], x = c % wc, y = c / wc;
+          return std::make_pair(x + 2 * y, y);
+        };
+        std::stable_sort(bo.begin(), bo.end(), [&](int a, int b) { return key(a) < key(b); });
+        std::vector<int32_t> p2;
+        p2.reserve(nj);
+        for (int k : bo) p2.insert(p2.end(), perm.begin() + cb[k], perm.begin() + cb[k + 1]);
+        perm.swap(p2);
+      }
+    }
     std::vector<int32_t> rank(nj);
     for (int i = 0; i < nj; i++) rank[perm[i]] = i;
     out.jobs.resize(nj);
