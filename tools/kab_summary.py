@@ -9,7 +9,8 @@ import sys
 tag = sys.argv[1]
 pats = sys.argv[2:]
 out = "gpurun_out"
-log = open(os.path.join(out, "pytest_%s.log" % tag)).read().strip().splitlines()
+lp = os.path.join(out, "pytest_%s.log" % tag)
+log = open(lp).read().strip().splitlines() if os.path.exists(lp) else []
 print(log[-1] if log else "(no pytest log)")
 stats = {}
 for v in ("new", "old"):

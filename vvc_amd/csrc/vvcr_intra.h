@@ -23,6 +23,13 @@ enum : uint8_t {
   IJ_PUBLISH = 1 << 7,    // a step of another CTU reads this one: drain its stores, raise its global flag
 };
 
+// Waves per k_intra workgroup (one CTU): the host's take-order simulation assumes the same count. Six
+// waves (96 KiB of LDS, one workgroup per CU) since the launch has only a few dozen workgroups.
+#ifndef VVCR_DIAG_NW
+constexpr int kIntraWaves = 6;
+#else
+constexpr int kIntraWaves = VVCR_DIAG_NW;
+#endif
 constexpr int kIntraMaxStepsPerCtu = 2048;   // LDS done-flag bytes of k_intra (a 128x128 CTU has at most ~1600 steps)
 
 // One reconstruction step: predict a region, add the residual plane, clip, store into the picture.

@@ -102,12 +102,7 @@ __device__ __forceinline__ int wave_sum(int v) {
 // above / above-right neighbours' borders — are read from HBM, through the sc1 hand-off below, and
 // only steps that such a read depends on (IJ_PUBLISH) drain their HBM stores and raise a global flag.
 // ------------------------------------------------------------------------------------------------
-#ifndef VVCR_DIAG_NW
-constexpr int NW = 4; 
-#else
-constexpr int NW = VVCR_DIAG_NW;
-#endif
-//                       // waves per workgroup
+constexpr int NW = kIntraWaves;              // waves per workgroup
 constexpr int TPL = 130, TPC = 66;           // LDS tile pitches (odd dword count: column walks hit distinct banks)
 constexpr int TILE_Y = 0, TILE_CB = 128 * TPL, TILE_CR = TILE_CB + 64 * TPC, TILE_N = TILE_CR + 64 * TPC;
 

@@ -615,9 +615,9 @@ struct Planner {
           // (VVCR_TAKE_ORDER=bl, r01) lets ready steps queue behind steps that wait on another CTU; pure
           // earliest-start delays the critical chain. Measured (k_intra, median of 20): 1080p I picture
           // 5.67 (bl) -> 5.59 ms, 4K 12.25 -> 11.97 ms; earliest-start first 6.67 / 14.8 ms.
-          constexpr int kNW = 4;
+          constexpr int kNW = kIntraWaves;
           constexpr double kLocal = 0.3, kGlobal = 1.5;   // hand-off latencies (us)
-          double wfree[kNW] = {0, 0, 0, 0};
+          double wfree[kNW] = {};
           std::vector<double> rdy(n, 0.0);
           std::vector<int32_t> known;
           auto make_known = [&](int q) {
