@@ -62,24 +62,20 @@ __device__ __forceinline__ int at(const DPlane &p, int x, int y) {
 }
 __device__ __forceinline__ int clip_alf(int c, int ref, int v0, int v1) { return clip3(-c, c, v0 - ref) + clip3(-c, c, v1 - ref); }
 
+// Rows of the diamond's taps at distance 1..3 below (r1, r3, r5) / above (r2, r4, r6) row y, padded at
+// the ALF virtual boundary (AdaptiveLoopFilter.cpp filterBlk); all selects (conditional assignments
+// through references were lowered to scratch stores).
 __device__ __forceinline__ void alf_rows(int y, int vbH, int vbPos, bool luma, int &r1, int &r2, int &r3, int &r4, int &r5, int &r6) {
-  r1 = y + 1; r2 = y - 1; r3 = y + 2; r4 = y - 2; r5 = y + 3; r6 = y - 3;
   const int yVb = y & (vbH - 1);
-  if (yVb < vbPos && yVb >= vbPos - (luma ? 4 : 2)) {
-    if (yVb == vbPos - 1) r1 = y;
-    if (yVb >= vbPos - 2) r3 = r1;
-    if (yVb >= vbPos - 3) r5 = r3;
-    if (yVb == vbPos - 1) r2 = y;
-    if (yVb >= vbPos - 2) r4 = r2;
-    if (yVb >= vbPos - 3) r6 = r4;
-  } else if (yVb >= vbPos && yVb <= vbPos + (luma ? 3 : 1)) {
-    if (yVb == vbPos) r2 = y;
-    if (yVb <= vbPos + 1) r4 = r2;
-    if (yVb <= vbPos + 2) r6 = r4;
-    if (yVb == vbPos) r1 = y;
-    if (yVb <= vbPos + 1) r3 = r1;
-    if (yVb <= vbPos + 2) r5 = r3;
-  }
+  const bool up = yVb < vbPos && yVb >= vbPos - (luma ? 4 : 2);     // rows above the boundary
+  const bool dn = yVb >= vbPos && yVb <= vbPos + (luma ? 3 : 1);    // rows below it
+  const bool e1 = up ? yVb == vbPos - 1 : (dn && yVb == vbPos);
+  const bool e2 = up ? yVb >= vbPos - 2 : (dn && yVb <= vbPos + 1);
+  const bool e3 = up ? yVb >= vbPos - 3 : (dn && yVb <= vbPos + 2);
+  const int a1 = e1 ? y : y + 1, b1 = e1 ? y : y - 1;
+  const int a3 = e2 ? a1 : y + 2, b3 = e2 ? b1 : y - 2;
+  const int a5 = e3 ? a3 : y + 3, b5 = e3 ? b3 : y - 3;
+  r1 = a1; r2 = b1; r3 = a3; r4 = b3; r5 = a5; r6 = b5;
 }
 
 __constant__ int8_t c_perm7[4][13] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12},
@@ -107,34 +103,46 @@ __global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
   const int X0 = blockIdx.x * ALF_TW, Y0 = P.y0 + blockIdx.y * ALF_TH;
   const int tid = threadIdx.x;
   const int W = S.w, H = S.h;
-  // A 64x16 tile lies in one CTB: its enable flag and filter set are uniform, read at once (scalar), and
-  // the set's 25 classes of coefficients / clips are staged in LDS together with the samples, so the
-  // per-lane class lookups of the filter read LDS instead of memory after the classification.
-  const int ctbT = (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2);
-  const bool ctbOn = P.en[0] && P.ctb_en[ctbT];
-  if (ctbOn) {
-    const int set = P.ctb_set[ctbT];
-    const int16_t *cf = P.luma_coef + set * 25 * 13, *cl = P.luma_clip + set * 25 * 13;
-    for (int i = tid; i < 25 * 13; i += 256) { s_cf[i] = cf[i]; s_cl[i] = cl[i]; }
-    if (tid < 4 * 13) s_perm[tid] = (&c_perm7[0][0])[tid];
+  // all of a lane's tile loads in flight first (one memory round trip), then the CTB's flag and filter
+  // set: a 64x16 tile lies in one CTB, so both are uniform (scalar loads, read together), and the set's 25
+  // classes of coefficients / clips are staged in LDS with the samples, so the per-lane class lookups of
+  // the filter read LDS instead of memory after the classification
+  constexpr int TWH = ALF_TW + 2 * ALF_HALO, NIT = (ALF_SH * TWH + 255) / 256;
+  int16_t v[NIT];
+#pragma unroll
+  for (int k = 0; k < NIT; k++) {
+    const int i = tid + 256 * k;
+    const int r = i / TWH, c = i - r * TWH;
+    const int sx = clip3(0, W - 1, X0 - ALF_HALO + c), sy = clip3(0, H - 1, Y0 - ALF_HALO + min(r, ALF_SH - 1));
+    v[k] = S.p[sy * S.stride + sx];
   }
-  {
-    // all of a lane's tile loads in flight before its first LDS store (one memory round trip)
-    constexpr int TWH = ALF_TW + 2 * ALF_HALO, NIT = (ALF_SH * TWH + 255) / 256;
-    int16_t v[NIT];
+  const int ctbT = (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2);
+  const int ctbE = P.ctb_en[ctbT], set = P.ctb_set[ctbT];
+  const bool ctbOn = P.en[0] && ctbE;
+  constexpr int NC = (25 * 13 + 255) / 256;
+  int16_t cfv[NC] = {}, clv[NC] = {};
+  if (ctbOn) {
+    const int16_t *cf = P.luma_coef + set * 25 * 13, *cl = P.luma_clip + set * 25 * 13;
 #pragma unroll
-    for (int k = 0; k < NIT; k++) {
-      const int i = tid + 256 * k;
-      const int r = i / TWH, c = i - r * TWH;
-      const int sx = clip3(0, W - 1, X0 - ALF_HALO + c), sy = clip3(0, H - 1, Y0 - ALF_HALO + min(r, ALF_SH - 1));
-      v[k] = S.p[sy * S.stride + sx];
+    for (int q = 0; q < NC; q++) {
+      const int i = min(tid + 256 * q, 25 * 13 - 1);
+      cfv[q] = cf[i];
+      clv[q] = cl[i];
     }
+  }
 #pragma unroll
-    for (int k = 0; k < NIT; k++) {
-      const int i = tid + 256 * k;
-      const int r = i / TWH, c = i - r * TWH;
-      if (i < ALF_SH * TWH) t[r * ALF_SW + c] = v[k];
+  for (int k = 0; k < NIT; k++) {
+    const int i = tid + 256 * k;
+    const int r = i / TWH, c = i - r * TWH;
+    if (i < ALF_SH * TWH) t[r * ALF_SW + c] = v[k];
+  }
+  if (ctbOn) {
+#pragma unroll
+    for (int q = 0; q < NC; q++) {
+      const int i = tid + 256 * q;
+      if (i < 25 * 13) { s_cf[i] = cfv[q]; s_cl[i] = clv[q]; }
     }
+    if (tid < 4 * 13) s_perm[tid] = (&c_perm7[0][0])[tid];
   }
   __syncthreads();
   // sample (x, y) in picture coordinates -> LDS (valid for |x - tile| <= 3 and |y - tile| <= 3)
@@ -208,7 +216,10 @@ __global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
     fl[k] = clip[pk];
   }
   const int maxv = (1 << P.bd) - 1;
-  for (int y = by; y < by + 4 && y < H; y++) {
+#pragma unroll
+  for (int dy = 0; dy < 4; dy++) {
+    const int y = by + dy;
+    if (y >= H) break;
     int r1, r2, r3, r4, r5, r6;
     alf_rows(y, vbH, vbPos, true, r1, r2, r3, r4, r5, r6);
     const int yVb = y & (vbH - 1);
@@ -232,6 +243,9 @@ __global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
 #undef T
 }
 
+// One lane per chroma sample. Every sample load (the 5x5 diamond, and the CC-ALF luma taps when the
+// picture uses CC-ALF) is issued before the CTB controls are known, so that the lane waits for one
+// memory round trip plus the coefficient lookups, not a chain of them.
 __global__ void k_alf_chroma(AlfParams P) {
   const int comp = 1 + blockIdx.z;
   const DPlane &S = P.src[comp];
@@ -243,37 +257,53 @@ __global__ void k_alf_chroma(AlfParams P) {
   const int ctb = (y >> cl2) * P.wc + (x >> cl2);
   const int n = P.nctb;
   const int maxv = (1 << P.bd) - 1;
+  const bool alfPic = P.en[comp] != 0, ccPic = P.en[2 + comp] != 0;
   const int cur = S.p[(size_t)y * S.stride + x];
+  const int vbH = 1 << cl2, vbPos = P.vb_chroma;
+  int r1, r2, r3, r4, r5, r6;
+  alf_rows(y, vbH, vbPos, false, r1, r2, r3, r4, r5, r6);
+  (void)r5; (void)r6;
+  int sa[12] = {};
+  if (alfPic) {
+    sa[0] = at(S, x, r3); sa[1] = at(S, x, r4);
+    sa[2] = at(S, x + 1, r1); sa[3] = at(S, x - 1, r2);
+    sa[4] = at(S, x, r1); sa[5] = at(S, x, r2);
+    sa[6] = at(S, x - 1, r1); sa[7] = at(S, x + 1, r2);
+    sa[8] = at(S, x + 2, y); sa[9] = at(S, x - 2, y);
+    sa[10] = at(S, x + 1, y); sa[11] = at(S, x - 1, y);
+  }
+  const int lx = x * 2, ly = y * 2;
+  const int pos = ly & ((1 << P.ctu_log2) - 1);
+  int o1 = 1, o2 = -1, o3 = 2;
+  if (pos == P.vb_luma - 2 || pos == P.vb_luma + 1) o3 = o1;
+  else if (pos == P.vb_luma - 1 || pos == P.vb_luma) { o1 = 0; o2 = 0; o3 = 0; }
+  int sl[8] = {};
+  if (ccPic) {
+    sl[0] = at(Y, lx, ly);
+    sl[1] = at(Y, lx, ly + o2); sl[2] = at(Y, lx - 1, ly); sl[3] = at(Y, lx + 1, ly);
+    sl[4] = at(Y, lx - 1, ly + o1); sl[5] = at(Y, lx, ly + o1); sl[6] = at(Y, lx + 1, ly + o1);
+    sl[7] = at(Y, lx, ly + o3);
+  }
+  const bool on = alfPic && P.ctb_en[comp * n + ctb];
+  const int alt = P.ctb_alt[comp * n + ctb];
+  const int ccf = ccPic ? P.cc_ctl[(comp - 1) * n + ctb] : 0;
   int v = cur;
-  if (P.en[comp] && P.ctb_en[comp * n + ctb]) {
-    const int alt = P.ctb_alt[comp * n + ctb];
+  if (on) {
     const int16_t *fc = P.chroma_coef + alt * 7, *fl = P.chroma_clip + alt * 7;
-    const int vbH = 1 << cl2, vbPos = P.vb_chroma;
-    int r1, r2, r3, r4, r5, r6;
-    alf_rows(y, vbH, vbPos, false, r1, r2, r3, r4, r5, r6);
-    int sum = fc[0] * clip_alf(fl[0], cur, at(S, x, r3), at(S, x, r4));
-    sum += fc[1] * clip_alf(fl[1], cur, at(S, x + 1, r1), at(S, x - 1, r2));
-    sum += fc[2] * clip_alf(fl[2], cur, at(S, x, r1), at(S, x, r2));
-    sum += fc[3] * clip_alf(fl[3], cur, at(S, x - 1, r1), at(S, x + 1, r2));
-    sum += fc[4] * clip_alf(fl[4], cur, at(S, x + 2, y), at(S, x - 2, y));
-    sum += fc[5] * clip_alf(fl[5], cur, at(S, x + 1, y), at(S, x - 1, y));
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) sum += fc[k] * clip_alf(fl[k], cur, sa[2 * k], sa[2 * k + 1]);
     const int yVb = y & (vbH - 1);
     const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
     sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
     v = clip3(0, maxv, sum + cur);
   }
-  const int ccf = P.en[2 + comp] ? P.cc_ctl[(comp - 1) * n + ctb] : 0;
   if (ccf) {
     const int16_t *f = P.cc_coef + ((comp - 1) * 4 + ccf - 1) * 8;
-    const int lx = x * 2, ly = y * 2;
-    const int pos = ly & ((1 << P.ctu_log2) - 1);
-    int o1 = 1, o2 = -1, o3 = 2;
-    if (pos == P.vb_luma - 2 || pos == P.vb_luma + 1) o3 = o1;
-    else if (pos == P.vb_luma - 1 || pos == P.vb_luma) { o1 = 0; o2 = 0; o3 = 0; }
-    const int c0 = at(Y, lx, ly);
-    int sum = f[0] * (at(Y, lx, ly + o2) - c0) + f[1] * (at(Y, lx - 1, ly) - c0) + f[2] * (at(Y, lx + 1, ly) - c0) +
-              f[3] * (at(Y, lx - 1, ly + o1) - c0) + f[4] * (at(Y, lx, ly + o1) - c0) + f[5] * (at(Y, lx + 1, ly + o1) - c0) +
-              f[6] * (at(Y, lx, ly + o3) - c0);
+    const int c0 = sl[0];
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < 7; k++) sum += f[k] * (sl[1 + k] - c0);
     sum = (sum + 64) >> 7;
     const int off = (1 << P.bd) >> 1;
     sum = clip3(0, maxv, sum + off) - off;
