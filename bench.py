@@ -177,7 +177,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--stream", default="ra1080_q32")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--segments", type=int, default=4, help="copies of the sequence the steps cycle through (<= 6)")
+    ap.add_argument("--segments", type=int, default=6, help="copies of the sequence the steps cycle through (<= 6)")
+    ap.add_argument("--kernels-inflight", action="store_true",
+                    help="diagnostics: take the kernel table from a pass with every segment in flight")
     ap.add_argument("--sync-pictures", action="store_true",
                     help="host sync after every picture (profiling: kernel durations without overlap)")
     ap.add_argument("--e2e-threads", type=int, default=12,
@@ -271,6 +273,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         run_step()
+    t_sub = time.perf_counter()   # host submission done (the library never blocks the host on the GPU)
     ctx.sync()
     t1 = time.perf_counter()
     R.barrier()
@@ -292,13 +295,19 @@ def main():
     bitexact = bitexact and inflight_ok
     # one more (untimed) step with per-kernel HIP events, one segment in flight: the kernel table and roofline
     ctx.set_timing(True)
-    run_step()
+    if a.kernels_inflight:   # every segment in flight (as timed), all steps' kernel tables summed below
+        for _ in range(a.segments):
+            run_step()
+    else:
+        run_step()
     ctx.sync()
     e2e = end_to_end(ctx, dec, pics, meta, per, a) if (world == 1 and a.e2e_threads > 0) else None
 
     # ---- per-kernel timing of the last step (HIP events on the library stream)
     kern = {}
     last = copies[(nstep[0] - 1) % a.segments][0]
+    if a.kernels_inflight:
+        last = [h for c in copies for h in c[0]]
     for hnd in last:
         for name, launches, ms, alg in ctx.kernel_stats(hnd):
             k = kern.setdefault(name, [0, 0.0, 0.0])
@@ -345,6 +354,7 @@ def main():
                      "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic},
         "kernels": {k: {"ms_per_step": round(v[1], 4), "launches_per_step": v[0],
                         "alg_GBps": round(v[2] / (v[1] / 1e3) / 1e9, 2) if v[1] > 0 else 0.0} for k, v in kern.items()},
+        "host_submit_ms_per_step": round((t_sub - t0) / a.steps * 1e3, 3),
         "serial": {"value": round(V.job_throughput(px_seq * a.steps, elapsed_serial, R) / 1e6, 2),
                    "ms_per_step": round(elapsed_serial / a.steps * 1e3, 3),
                    "note": "one segment in flight (sync after every step)"},

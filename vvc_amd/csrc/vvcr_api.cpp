@@ -560,7 +560,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     dp.beta_offset_div2 = pp.dbk_beta_offset_div2;
     dp.tc_offset_div2 = pp.dbk_tc_offset_div2;
     launch_dbk(dp, r.dbk.p, r.dbk_counts, s);
-    r.launches[K_DBK] = (r.dbk_counts[0] > 0) + (r.dbk_counts[1] > 0) + (r.dbk_counts[2] > 0) + (r.dbk_counts[3] > 0);
+    r.launches[K_DBK] = (r.dbk_counts[0] + r.dbk_counts[1] > 0) + (r.dbk_counts[2] + r.dbk_counts[3] > 0);
   }
   // SAO (slot -> tmp) and ALF (ping-pong back); the final picture always ends in the slot
   const int ctu = 1 << ctx->sp.ctu_log2;
@@ -634,7 +634,23 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     ctx->nintra = ctx->nlane / 2;
     if (const char *e = getenv("VVCR_INTRA_LANES")) ctx->nintra = std::max(1, std::min(ctx->nlane - 1, atoi(e)));
     if (const char *e = getenv("VVCR_INTRA_WG")) ctx->intra_wg = std::max(0, atoi(e));
-    for (int l = 0; l < ctx->nlane; l++) VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->lanes[l].s, hipStreamNonBlocking));
+    VVCR_CHECK_HIP(hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, sp->device));
+    // VVCR_CU_INTRA=N: the intra lanes' streams run on N CUs (spread evenly over the device), the B lanes'
+    // on the others, so that the intra chain's waves never share a CU with B-picture kernels
+    int cu_intra = 0;
+    if (const char *e = getenv("VVCR_CU_INTRA")) cu_intra = std::max(0, std::min(ctx->n_cu - 1, atoi(e)));
+    for (int l = 0; l < ctx->nlane; l++) {
+      if (cu_intra > 0) {
+        std::vector<uint32_t> mask((ctx->n_cu + 31) / 32, 0);
+        for (int i = 0; i < ctx->n_cu; i++) {
+          const bool in = (i * cu_intra) / ctx->n_cu != ((i + 1) * cu_intra) / ctx->n_cu;
+          if (in == (l < ctx->nintra)) mask[i >> 5] |= 1u << (i & 31);
+        }
+        VVCR_CHECK_HIP(hipExtStreamCreateWithCUMask(&ctx->lanes[l].s, (uint32_t)mask.size(), mask.data()));
+      } else {
+        VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->lanes[l].s, hipStreamNonBlocking));
+      }
+    }
     ctx->stream = ctx->lanes[0].s;
     VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
     const int W = sp->width, H = sp->height;
@@ -661,7 +677,6 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
         ln.resi[c] = alloc_plane(w, h);
         ln.tmp[c] = alloc_plane(w, h);
       }
-    VVCR_CHECK_HIP(hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, sp->device));
     if (ctx->intra_wg <= 0) {
       // k_intra takes CTUs in wavefront order: the CTUs in flight are those of about two anti-diagonals
       // (x + 2y), so four diagonals' worth of workgroups keeps the wavefront busy (1080p, CTU 128: 32,

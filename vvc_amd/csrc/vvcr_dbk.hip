@@ -44,11 +44,18 @@ __device__ bool use_strong(const int16_t *s, int o, int d, int beta, int tc, boo
   return dstrong < (beta >> 3) && d < (beta >> 2) && abs(m3 - m4) < ((tc * 5 + 1) >> 1);
 }
 
-// xFilteringPandQ (:1323) + xBilinearFilter (:1302)
+// xFilteringPandQ (:1323) + xBilinearFilter (:1302). The per-tap coefficients are selected by the side's
+// length with compile-time indices (an unrolled loop): local arrays indexed at run time live in scratch.
+__device__ __forceinline__ int long_coef(int n, int i) {   // dbCoeffs7/5/3
+  constexpr int c7[7] = {59, 50, 41, 32, 23, 14, 5}, c5[5] = {58, 45, 32, 19, 6}, c3[3] = {53, 32, 11};
+  return n == 7 ? c7[i] : (n == 5 ? (i < 5 ? c5[i] : 0) : (i < 3 ? c3[i] : 0));
+}
+__device__ __forceinline__ int long_taper(int n, int i) {   // tc7 / tc3 (length 5 uses tc7)
+  constexpr int t7[7] = {6, 5, 4, 3, 2, 1, 1}, t3[3] = {6, 4, 2};
+  return n == 3 ? (i < 3 ? t3[i] : 0) : t7[i];
+}
 __device__ void filter_long(int16_t *src, int o, int nP, int nQ, int tc) {
   int16_t *sP = src - o, *sQ = src;
-  const int c7[7] = {59, 50, 41, 32, 23, 14, 5}, c3[3] = {53, 32, 11}, c5[5] = {58, 45, 32, 19, 6};
-  const int *cP = nP == 7 ? c7 : (nP == 5 ? c5 : c3), *cQ = nQ == 7 ? c7 : (nQ == 5 ? c5 : c3);
   const int refP = nP == 7 ? (sP[-6 * o] + sP[-7 * o] + 1) >> 1 : nP == 3 ? (sP[-2 * o] + sP[-3 * o] + 1) >> 1 : (sP[-4 * o] + sP[-5 * o] + 1) >> 1;
   const int refQ = nQ == 7 ? (sQ[6 * o] + sQ[7 * o] + 1) >> 1 : nQ == 3 ? (sQ[2 * o] + sQ[3 * o] + 1) >> 1 : (sQ[4 * o] + sQ[5 * o] + 1) >> 1;
   int mid;
@@ -72,19 +79,20 @@ __device__ void filter_long(int16_t *src, int o, int nP, int nQ, int tc) {
     else
       mid = (sP[0] + sQ[0] + sP[-o] + sQ[o] + sP[-2 * o] + sQ[2 * o] + sP[-3 * o] + sQ[3 * o] + 4) >> 3;
   }
-  const int t7[7] = {6, 5, 4, 3, 2, 1, 1}, t3[3] = {6, 4, 2};
-  const int *tP = nP == 3 ? t3 : t7, *tQ = nQ == 3 ? t3 : t7;
   int vp[7], vq[7];
-  for (int i = 0; i < nP; i++) {
-    const int s = sP[-o * i], cv = (tc * tP[i]) >> 1;
-    vp[i] = clip3(s - cv, s + cv, (mid * cP[i] + refP * (64 - cP[i]) + 32) >> 6);
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    const int sp = i < nP ? sP[-o * i] : 0, sq = i < nQ ? sQ[o * i] : 0;
+    const int cvp = (tc * long_taper(nP, i)) >> 1, cvq = (tc * long_taper(nQ, i)) >> 1;
+    const int kp = long_coef(nP, i), kq = long_coef(nQ, i);
+    vp[i] = clip3(sp - cvp, sp + cvp, (mid * kp + refP * (64 - kp) + 32) >> 6);
+    vq[i] = clip3(sq - cvq, sq + cvq, (mid * kq + refQ * (64 - kq) + 32) >> 6);
   }
-  for (int i = 0; i < nQ; i++) {
-    const int s = sQ[o * i], cv = (tc * tQ[i]) >> 1;
-    vq[i] = clip3(s - cv, s + cv, (mid * cQ[i] + refQ * (64 - cQ[i]) + 32) >> 6);
+#pragma unroll
+  for (int i = 0; i < 7; i++) {
+    if (i < nP) sP[-o * i] = (int16_t)vp[i];
+    if (i < nQ) sQ[o * i] = (int16_t)vq[i];
   }
-  for (int i = 0; i < nP; i++) sP[-o * i] = (int16_t)vp[i];
-  for (int i = 0; i < nQ; i++) sQ[o * i] = (int16_t)vq[i];
 }
 
 // xPelFilterLuma (:1397)
@@ -147,8 +155,8 @@ __device__ __forceinline__ int tc_of(int idx, int bd) {
 // Four lanes per 4-line luma segment, one line each: the segment decisions (xEdgeFilterLuma :981-1050)
 // need lines 0 and 3, whose terms the lanes exchange by shuffles; each lane then filters its own line.
 template <int DIR>
-__global__ __launch_bounds__(256) void k_dbk_luma(DbkParams P, const DbkSeg *segs, int n) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void dbk_luma(const DbkParams &P, const DbkSeg *segs, int n, int blk) {
+  const int t = blk * 256 + threadIdx.x;
   const int i = t >> 2, line = t & 3, l0 = (threadIdx.x & 63) & ~3;   // lane of line 0 of this segment
   const bool valid = i < n;
   const DbkSeg sg = valid ? segs[i] : DbkSeg{0, 0, 0};
@@ -206,8 +214,8 @@ __global__ __launch_bounds__(256) void k_dbk_luma(DbkParams P, const DbkSeg *seg
 // Four lanes per chroma segment: (component, line) = (lane >> 1, lane & 1); the strong-filter decision
 // of a component uses both of its lines (xEdgeFilterChroma :1163-1283), exchanged by shuffles.
 template <int DIR>
-__global__ __launch_bounds__(256) void k_dbk_chroma(DbkParams P, const DbkSeg *segs, int n) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void dbk_chroma(const DbkParams &P, const DbkSeg *segs, int n, int blk) {
+  const int t = blk * 256 + threadIdx.x;
   const int i = t >> 2, k = (t >> 1) & 1, l = t & 1, lp = (threadIdx.x & 63) & ~1;   // lp: line 0 of this component
   const bool valid = i < n;
   const DbkSeg sg = valid ? segs[i] : DbkSeg{0, 0, 0};
@@ -232,24 +240,27 @@ __global__ __launch_bounds__(256) void k_dbk_chroma(DbkParams P, const DbkSeg *s
   if (act) filter_chroma_line(s, o, tc, sw, maxv, ctbh);
 }
 
+// One launch per direction: the first gL workgroups take the luma segments, the others the chroma ones
+// (the planes are independent; the vertical launch precedes the horizontal one).
+template <int DIR>
+__global__ __launch_bounds__(256) void k_dbk(DbkParams P, const DbkSeg *segL, int nL, int gL, const DbkSeg *segC, int nC) {
+  if ((int)blockIdx.x < gL) dbk_luma<DIR>(P, segL, nL, blockIdx.x);
+  else dbk_chroma<DIR>(P, segC, nC, blockIdx.x - gL);
+}
+
 }  // namespace
 
 void launch_dbk(const DbkParams &p, const DbkSeg *segs, const int counts[4], hipStream_t s) {
-  const int T = 256;
+  const int T = 256;   // four lanes per segment
   int off = 0;
-  for (int k = 0; k < 4; k++) {
-    const int n = counts[k];
-    if (n > 0) {
-      const dim3 g((4 * n + T - 1) / T);   // four lanes per segment
-      const DbkSeg *sg = segs + off;
-      switch (k) {
-        case 0: hipLaunchKernelGGL(k_dbk_luma<0>, g, dim3(T), 0, s, p, sg, n); break;
-        case 1: hipLaunchKernelGGL(k_dbk_chroma<0>, g, dim3(T), 0, s, p, sg, n); break;
-        case 2: hipLaunchKernelGGL(k_dbk_luma<1>, g, dim3(T), 0, s, p, sg, n); break;
-        case 3: hipLaunchKernelGGL(k_dbk_chroma<1>, g, dim3(T), 0, s, p, sg, n); break;
-      }
-      VVCR_CHECK_HIP(hipGetLastError());
-    }
-    off += n;
+  for (int dir = 0; dir < 2; dir++) {
+    const int nL = counts[2 * dir], nC = counts[2 * dir + 1];
+    const DbkSeg *sL = segs + off, *sC = segs + off + nL;
+    off += nL + nC;
+    if (nL + nC == 0) continue;
+    const int gL = (4 * nL + T - 1) / T, gC = (4 * nC + T - 1) / T;
+    if (dir == 0) hipLaunchKernelGGL(k_dbk<0>, dim3(gL + gC), dim3(T), 0, s, p, sL, nL, gL, sC, nC);
+    else hipLaunchKernelGGL(k_dbk<1>, dim3(gL + gC), dim3(T), 0, s, p, sL, nL, gL, sC, nC);
+    VVCR_CHECK_HIP(hipGetLastError());
   }
 }
