@@ -507,7 +507,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     memcpy(tp.lfnst_scan_off, ctx->scans.lfnst_off, sizeof(tp.lfnst_scan_off));
     launch_resid(tp, r.tb.p, r.n_tb, r.n_tb_small, r.coef.p, ctx->d_scans.p, s);
     VVCR_CHECK_HIP(hipGetLastError());
-    r.launches[K_RESID] = (r.n_tb_small > 0) + (r.n_tb > r.n_tb_small);
+    r.launches[K_RESID] = r.n_tb > 0 ? 1 : 0;
   }
   if (mask & VVCR_STAGE_INTER) {
     const McParams mp = make_mc_params(ctx, r.pp, L);
@@ -593,7 +593,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     launch_alf(ap, s);
     VVCR_CHECK_HIP(hipGetLastError());
     inTmp = !inTmp;
-    r.launches[K_ALF] = 2;
+    r.launches[K_ALF] = 1;
   }
   if (inTmp) {
     Planes3 cp{};

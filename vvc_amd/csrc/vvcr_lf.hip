@@ -93,14 +93,14 @@ constexpr int ALF_TW = 64, ALF_TH = 16, ALF_HALO = 3;
 constexpr int ALF_SW = ALF_TW + 2 * ALF_HALO + 2;   // LDS row pitch (72)
 constexpr int ALF_SH = ALF_TH + 2 * ALF_HALO;       // 22 rows
 
-__global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
+__device__ __forceinline__ void alf_luma(const AlfParams &P, int tx, int ty) {
   const DPlane &S = P.src[0];
   const DPlane &D = P.dst[0];
   __shared__ int16_t t[ALF_SH * ALF_SW];
   __shared__ int32_t blk[(ALF_TW / 4) * (ALF_TH / 4)];   // class | transpose << 8 | enabled << 16
   __shared__ int16_t s_cf[25 * 13], s_cl[25 * 13];       // the CTB's filter set: coefficients / clips per class
   __shared__ int8_t s_perm[4 * 13];
-  const int X0 = blockIdx.x * ALF_TW, Y0 = P.y0 + blockIdx.y * ALF_TH;
+  const int X0 = tx * ALF_TW, Y0 = P.y0 + ty * ALF_TH;
   const int tid = threadIdx.x;
   const int W = S.w, H = S.h;
   // all of a lane's tile loads in flight first (one memory round trip), then the CTB's flag and filter
@@ -246,12 +246,10 @@ __global__ __launch_bounds__(256) void k_alf_luma(AlfParams P) {
 // One lane per chroma sample. Every sample load (the 5x5 diamond, and the CC-ALF luma taps when the
 // picture uses CC-ALF) is issued before the CTB controls are known, so that the lane waits for one
 // memory round trip plus the coefficient lookups, not a chain of them.
-__global__ void k_alf_chroma(AlfParams P) {
-  const int comp = 1 + blockIdx.z;
+__device__ __forceinline__ void alf_chroma(const AlfParams &P, int comp, int x, int y) {
   const DPlane &S = P.src[comp];
   const DPlane &D = P.dst[comp];
   const DPlane &Y = P.src[0];
-  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = (P.y0 >> 1) + blockIdx.y;
   if (x >= S.w || y >= S.h || y >= (P.y1 >> 1)) return;
   const int cl2 = P.ctu_log2 - 1;
   const int ctb = (y >> cl2) * P.wc + (x >> cl2);
@@ -312,6 +310,19 @@ __global__ void k_alf_chroma(AlfParams P) {
   D.p[(size_t)y * D.stride + x] = (int16_t)v;
 }
 
+// Luma and chroma ALF in one launch: the first gx * gy workgroups are luma tiles, the others take 64
+// chroma columns x 4 rows (a wave per row) of Cb, then Cr.
+__global__ __launch_bounds__(256) void k_alf(AlfParams P, int gx, int gy, int gcx, int gcy) {
+  const int b = blockIdx.x;
+  if (b < gx * gy) {
+    alf_luma(P, b % gx, b / gx);
+    return;
+  }
+  const int c = b - gx * gy, per = gcx * gcy, comp = 1 + c / per, r = c % per;
+  const int x = (r % gcx) * 64 + (threadIdx.x & 63), y = (P.y0 >> 1) + (r / gcx) * 4 + (threadIdx.x >> 6);
+  alf_chroma(P, comp, x, y);
+}
+
 }  // namespace
 
 void launch_sao(const SaoParams &p, hipStream_t s) {
@@ -342,14 +353,7 @@ void launch_planes3(const Planes3 &p, hipStream_t s) {
 
 void launch_alf(const AlfParams &p, hipStream_t s) {
   if (p.y1 <= p.y0) return;
-  {
-    const int W = p.src[0].w;
-    dim3 grid((W + ALF_TW - 1) / ALF_TW, (p.y1 - p.y0 + ALF_TH - 1) / ALF_TH);
-    hipLaunchKernelGGL(k_alf_luma, grid, dim3(256), 0, s, p);
-  }
-  {
-    const int W = p.src[1].w;
-    dim3 grid((W + 63) / 64, (p.y1 - p.y0) >> 1, 2);
-    hipLaunchKernelGGL(k_alf_chroma, grid, dim3(64), 0, s, p);
-  }
+  const int gx = (p.src[0].w + ALF_TW - 1) / ALF_TW, gy = (p.y1 - p.y0 + ALF_TH - 1) / ALF_TH;
+  const int gcx = (p.src[1].w + 63) / 64, gcy = (((p.y1 - p.y0) >> 1) + 3) / 4;
+  hipLaunchKernelGGL(k_alf, dim3(gx * gy + 2 * gcx * gcy), dim3(256), 0, s, p, gx, gy, gcx, gcy);
 }

@@ -1,6 +1,7 @@
 // vvcr_resid.hip — residual reconstruction for gfx950: dequantisation (flat / 4-state dependent
 // quantisation / BDPCM), inverse LFNST, inverse DCT-2 / DST-7 / DCT-8 (2..64 point) or transform
-// skip, joint Cb-Cr. One 64-lane workgroup per transform block; the block lives in LDS as int32.
+// skip, joint Cb-Cr. One workgroup (or, for blocks of <= 256 samples, one wave) per transform block; the block
+// lives in LDS as int16.
 //
 // Reference semantics: Quant::dequant (Quant.cpp:369), DQIntern::Quantizer::dequantBlock
 // (DepQuant.cpp:705), TrQuant::xInvLfnst (TrQuant.cpp:310), TrQuant::xIT + _fastInverseMM
@@ -57,8 +58,8 @@ __device__ __forceinline__ int32_t mat_dword(const TMat &m, int N, int d) {
 }
 __device__ __forceinline__ int sbyte(int32_t m, int e) { return (m << (24 - 8 * e)) >> 24; }
 
-// One workgroup of NT lanes per transform block (NT = 64 for blocks of <= 256 samples, 256 above),
-// the block in LDS as int32. The passes only visit the bounding box of the non-zero levels
+// NT lanes per transform block (NT = 64, one wave, for blocks of <= 256 samples; 256 above), the block in
+// LDS as int16. The passes only visit the bounding box of the non-zero levels
 // (TbJob::nz_rows/nz_cols, host-computed): a row / column of zero levels contributes nothing to the
 // vertical / horizontal sums, so restricting the sums to the box is exact.
 //
@@ -67,17 +68,34 @@ __device__ __forceinline__ int sbyte(int32_t m, int e) { return (m << (24 - 8 * 
 // of the dependent-quantisation lanes, the matrix rows of both passes — is issued at the start, flat
 // dequantisation is applied in registers, and the transform passes produce four outputs per lane from
 // dword reads of the packed matrix rows.
+#ifdef VVCR_RESID_I32   // diagnostics: int32 LDS cells
+typedef int32_t cell_t;
+#else
+typedef int16_t cell_t;
+#endif
+
+template <int NT>
+__device__ __forceinline__ void bar() {
+#ifdef VVCR_RESID_BLOCKBAR   // diagnostics (with VVCR_RESID_ONEWAVE): block barriers everywhere
+  if constexpr (false) {
+#else
+  if constexpr (NT == 64) {   // one wave per block: LDS executes a wave's accesses in order
+#endif
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  } else {
+    __syncthreads();
+  }
+}
+
 template <int MAXN, int NT>
-__global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restrict__ jobs, const int32_t *__restrict__ coef,
-                                              const uint16_t *__restrict__ scans) {
+__device__ __forceinline__ void resid_tb(const TbParams &P, const TbJob *jp, const int32_t *__restrict__ coef,
+                                         const uint16_t *__restrict__ scans, cell_t *c, cell_t *t, int32_t *mv, int32_t *mh,
+                                         int tid) {
   constexpr int PER = MAXN / NT;             // level slots per lane
   constexpr int MD = 32 * 64 / 4 / NT;       // matrix dwords per lane and pass
-  __shared__ __attribute__((aligned(16))) int32_t c[MAXN];
-  __shared__ __attribute__((aligned(16))) int32_t t[MAXN];
-  __shared__ int32_t mv[32 * 64 / 4];        // vertical-pass matrix rows k < 32 (zero-out), packed int8
-  __shared__ int32_t mh[32 * 64 / 4];        // horizontal-pass (or 1-D) matrix rows
-  const int tid = threadIdx.x, lane = tid & 63;
-  const TbJob J = load_uniform(jobs + blockIdx.x);
+  const int lane = tid & 63;
+  const TbJob J = load_uniform(jp);
   const int w = J.w, h = J.h, n = w * h;
   const int lw = ilog2d(w), lh = ilog2d(h);
   const bool ts = J.flags & TB_TS;
@@ -144,7 +162,7 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
     if (d < nv) mv[d] = mvr[q];
     if (d < nh) mh[d] = mhr[q];
   }
-  __syncthreads();
+  bar<NT>();
 
   // 2b. dependent quantisation: the 4-state machine along the reverse scan, on the first wave. Each lane
   // owns 16 consecutive scan positions and summarises them as a state map; a wave-wide prefix of map
@@ -211,7 +229,7 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
         }
       }
     }
-    __syncthreads();
+    bar<NT>();
   } else if (bdpcm) {
     // BDPCM accumulation of levels (invResDPCM Quant.cpp:155), then flat dequant
     if (bdpcm == 1) {
@@ -221,13 +239,13 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
       for (int x = tid; x < w; x += NT)
         for (int y = 1; y < h; y++) c[y * w + x] = clip3(TMIN, TMAX, c[(y - 1) * w + x] + c[y * w + x]);
     }
-    __syncthreads();
+    bar<NT>();
 #pragma unroll
     for (int q = 0; q < PER; q++) {
       const int i = tid + q * NT;
       if (i < n && (i >> lw) < R && (i & (w - 1)) < C) c[i] = flat_dq(c[i]);
     }
-    __syncthreads();
+    bar<NT>();
   }
   // 3. inverse LFNST (TrQuant::xInvLfnst); its output area is inside the box (host widened it). Lane tid
   // computes output tid, then writes it to its position of the top-left 4x4 / 8x8 region.
@@ -248,7 +266,7 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
         if (i < zeroOut) s += c[scan[i]] * m[i * ms];
       v = clip3(TMIN, TMAX, (s + 64) >> 7);
     }
-    __syncthreads();
+    bar<NT>();
     if (act) {
       int y, x;
       if (J.flags & TB_LFNST_TRANSPOSE) {
@@ -262,7 +280,7 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
       }
       c[y * w + x] = v;
     }
-    __syncthreads();
+    bar<NT>();
   }
   // 4. inverse transform (or transform skip) -> residual, written straight to the plane(s)
   const DPlane &o = P.out[J.comp];
@@ -302,8 +320,12 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
           s2 += cv * sbyte(m, 2);
           s3 += cv * sbyte(m, 3);
         }
-        *(int4 *)&t[i * h + (jq << 2)] = make_int4(clip3(TMIN, TMAX, (s0 + 64) >> 7), clip3(TMIN, TMAX, (s1 + 64) >> 7),
-                                                   clip3(TMIN, TMAX, (s2 + 64) >> 7), clip3(TMIN, TMAX, (s3 + 64) >> 7));
+        const int u0 = clip3(TMIN, TMAX, (s0 + 64) >> 7), u1 = clip3(TMIN, TMAX, (s1 + 64) >> 7);
+        const int u2 = clip3(TMIN, TMAX, (s2 + 64) >> 7), u3 = clip3(TMIN, TMAX, (s3 + 64) >> 7);
+        if constexpr (sizeof(cell_t) == 2)
+          *(uint2 *)&t[i * h + (jq << 2)] = make_uint2((uint32_t)(uint16_t)u0 | ((uint32_t)u1 << 16), (uint32_t)(uint16_t)u2 | ((uint32_t)u3 << 16));
+        else
+          *(int4 *)&t[i * h + (jq << 2)] = make_int4(u0, u1, u2, u3);
       }
     } else {
       for (int idx = tid; idx < Cv * h; idx += NT) {
@@ -313,7 +335,7 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
         t[i * h + j] = clip3(TMIN, TMAX, (s + 64) >> 7);
       }
     }
-    __syncthreads();
+    bar<NT>();
     // horizontal pass over the Cv non-zero columns of t, four columns j per lane
     const int rnd = 1 << (shift2 - 1);
     if (w >= 4) {
@@ -357,10 +379,43 @@ __global__ __launch_bounds__(NT) void k_resid(TbParams P, const TbJob *__restric
   }
 }
 
+// One launch for the picture's transform blocks: the first nbig workgroups take one large block each
+// (256 lanes), the others four small blocks (<= 256 samples), one per wave. Levels and the transform
+// intermediates fit int16 (every stage clips to the 16-bit dynamic range), so both layouts share 20 KiB.
+constexpr int RS_CB = (int)sizeof(cell_t);
+constexpr int RS_BIG = 2 * 4096 * RS_CB + 4096, RS_SMALL = 2 * 256 * RS_CB + 4096;   // bytes: c, t, mv, mh
+constexpr int RS_LDS = RS_BIG > 4 * RS_SMALL ? RS_BIG : 4 * RS_SMALL;
+__global__ __launch_bounds__(256) void k_resid(TbParams P, const TbJob *__restrict__ jobs, int nsmall, int nbig,
+                                               const int32_t *__restrict__ coef, const uint16_t *__restrict__ scans) {
+  __shared__ __attribute__((aligned(16))) char raw[RS_LDS];
+  const int b = blockIdx.x;
+  if (b < nbig) {
+    cell_t *c = (cell_t *)raw, *t = c + 4096;
+    int32_t *mv = (int32_t *)(raw + 2 * 4096 * RS_CB), *mh = mv + 512;
+    resid_tb<4096, 256>(P, jobs + nsmall + b, coef, scans, c, t, mv, mh, threadIdx.x);
+  } else {
+#ifdef VVCR_RESID_ONEWAVE   // diagnostics: one small block per workgroup
+    const int w = 0, j = b - nbig;
+    if (threadIdx.x >= 64 || j >= nsmall) return;
+#else
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), j = (b - nbig) * 4 + w;
+    if (j >= nsmall) return;
+#endif
+    char *base = raw + w * RS_SMALL;
+    cell_t *c = (cell_t *)base, *t = c + 256;
+    int32_t *mv = (int32_t *)(base + 2 * 256 * RS_CB), *mh = mv + 512;
+    resid_tb<256, 64>(P, jobs + j, coef, scans, c, t, mv, mh, threadIdx.x & 63);
+  }
+}
+
 }  // namespace
 
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, int nsmall, const int32_t *coef, const uint16_t *scans,
                   hipStream_t s) {
-  if (nsmall > 0) hipLaunchKernelGGL((k_resid<256, 64>), dim3(nsmall), dim3(64), 0, s, p, jobs, coef, scans);
-  if (njobs > nsmall) hipLaunchKernelGGL((k_resid<4096, 256>), dim3(njobs - nsmall), dim3(256), 0, s, p, jobs + nsmall, coef, scans);
+#ifdef VVCR_RESID_ONEWAVE
+  const int nbig = njobs - nsmall, g = nbig + nsmall;
+#else
+  const int nbig = njobs - nsmall, g = nbig + (nsmall + 3) / 4;
+#endif
+  if (g > 0) hipLaunchKernelGGL(k_resid, dim3(g), dim3(256), 0, s, p, jobs, nsmall, nbig, coef, scans);
 }
