@@ -1,4 +1,4 @@
-"""MC kernels in isolation: the inter stage (VVCR_STAGE_INTER: k_mc_basic, k_mc_bidir, k_mc_affine) of
+"""MC kernels in isolation: the inter stage (VVCR_STAGE_INTER: k_mc, k_mc_bidir, k_mc_affine) of
 every B picture of a stream, prepared once and launched --reps times back to back; per-kernel HIP-event
 times and algorithmic bytes (vvcr_kernel_stats) of the last repetition, and the wall time per picture.
 Reference content is irrelevant for timing (the DPB holds whatever the slots contain).

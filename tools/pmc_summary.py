@@ -39,10 +39,9 @@ def main(d, stream="ra1080_q32"):
         out["detail"][k] = {"fetch_raw": round(f), "read_corrected": round(2 * f), "write": round(w),
                             "launches_sampled": nf.get(k, 0)}
     # kernel-group names used by bench.py (vvcr_kernel_stats groups)
-    groups = {"resid": ["k_resid<256, 64>", "k_resid<4096, 256>"], "intra": ["k_intra"], "mc": ["k_mc_basic", "k_mc_tile"],
+    groups = {"resid": ["k_resid"], "intra": ["k_intra"], "mc": ["k_mc"],
               "mc_bidir": ["k_mc_bidir"], "mc_affine": ["k_mc_affine"], "recon_inter": ["k_recon_inter"],
-              "sao": ["k_sao"], "alf": ["k_alf_luma", "k_alf_chroma"],
-              "deblock": ["k_dbk_luma<0>", "k_dbk_chroma<0>", "k_dbk_luma<1>", "k_dbk_chroma<1>"]}
+              "sao": ["k_sao"], "alf": ["k_alf"], "deblock": ["k_dbk<0>", "k_dbk<1>"]}
     out["per_group_launch_bytes"] = {g: round(sum(out["per_launch_bytes"].get(k, 0) for k in ks))
                                      for g, ks in groups.items()}
     print(json.dumps(out, indent=1))

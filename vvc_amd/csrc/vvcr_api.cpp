@@ -513,10 +513,9 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     const McParams mp = make_mc_params(ctx, r.pp, L);
     {
       KernelTimer t(r, K_MC, s, ctx->timing);
-      launch_mc_tile(mp, r.mc_basic.p, r.n_mctile, s);
-      launch_mc_basic(mp, r.mc_basic.p + r.n_mctile, r.n_basic, s);
+      launch_mc(mp, r.mc_basic.p, r.n_mctile, r.n_basic, s);
       VVCR_CHECK_HIP(hipGetLastError());
-      r.launches[K_MC] = (r.n_mctile ? 1 : 0) + (r.n_basic ? 1 : 0);
+      r.launches[K_MC] = (r.n_mctile + r.n_basic) ? 1 : 0;
     }
     {
       KernelTimer t(r, K_MC_BIDIR, s, ctx->timing);

@@ -226,9 +226,8 @@ void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const Af
 void launch_sao(const SaoParams &p, hipStream_t s);
 void launch_alf(const AlfParams &p, hipStream_t s);
 void launch_planes3(const Planes3 &p, hipStream_t s);
-// jobs[0, nsmall): blocks of <= 256 samples (64-lane workgroups); jobs[nsmall, njobs): larger (256 lanes)
+// jobs[0, nsmall): blocks of <= 256 samples (one wave each); jobs[nsmall, njobs): larger (a 256-lane workgroup each)
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, int nsmall, const int32_t *coef, const uint16_t *scans, hipStream_t s);
-void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);
 // DecoderApp output frame of a picture (vvcr_write_output)
 void launch_output(const std::array<DPlane, 3> &pic, const vvcr_output_params &op, int bd, uint8_t *dst, hipStream_t s);
-void launch_mc_tile(const McParams &p, const McJob *jobs, int njobs, hipStream_t s);   // 32x32 jobs
+void launch_mc(const McParams &p, const McJob *jobs, int ntile, int nbasic, hipStream_t s);   // 32x32 tiles, then <= 16x16 jobs

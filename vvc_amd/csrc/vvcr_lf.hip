@@ -1,12 +1,13 @@
 // vvcr_lf.hip — in-loop filters for gfx950: SAO and ALF / CC-ALF (deblocking: vvcr_dbk.hip).
 //
-// SAO (SampleAdaptiveOffset::offsetBlock, SampleAdaptiveOffset.cpp:293): one lane per 4 horizontally
+// SAO (SampleAdaptiveOffset::offsetBlock, SampleAdaptiveOffset.cpp:293): one lane per 8 horizontally
 // adjacent samples of one component; every sample of the picture is written (copy where SAO is off),
 // reading the deblocked picture and writing the SAO picture (ping-pong, so neighbours are pre-SAO).
 //
 // ALF (AdaptiveLoopFilter::deriveClassificationBlk :873, filterBlk<7x7/5x5> :1085, filterBlkCcAlf :1328):
 // luma: one workgroup per 64x16 tile staged in LDS with its 3-sample halo (classification + filter);
-// chroma: one lane per chroma sample, 5x5 diamond and the CC-ALF luma->chroma correction fused.
+// chroma: one lane per chroma sample, 5x5 diamond and the CC-ALF luma->chroma correction fused; both in
+// one launch.
 // Reads the SAO picture, writes the final picture. Coordinates are clamped to the picture
 // (equivalent to PelUnitBuf::extendBorderPel(3) on the ALF input, AdaptiveLoopFilter.cpp:411).
 #include "vvcr_internal.h"
@@ -16,42 +17,70 @@ namespace {
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 __device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
 
-__global__ void k_sao(SaoParams P) {
+// One lane per 8 horizontally adjacent samples (a 16-byte vector) of one component, a wave per row, four
+// rows per workgroup. The lane's row and both neighbour rows are loaded as vectors, with the samples
+// left / right of them, all before the CTB's parameters are known; the 8 samples lie in one CTB (CTB
+// widths are multiples of 8). The edge-offset classes read their neighbours from these registers.
+__global__ __launch_bounds__(256) void k_sao(SaoParams P) {
   const int comp = blockIdx.z;               // one launch for the three planes
   const DPlane &S = P.src[comp];
   const DPlane &D = P.dst[comp];
   const int W = S.w, H = S.h;
-  const int qx = blockIdx.x * blockDim.x + threadIdx.x;     // quad index
-  const int y = (comp ? P.y0 >> 1 : P.y0) + blockIdx.y;
-  const int x0 = qx * 4;
+  const int x0 = (blockIdx.x * 64 + (threadIdx.x & 63)) * 8;
+  const int y = (comp ? P.y0 >> 1 : P.y0) + blockIdx.y * 4 + (threadIdx.x >> 6);
   if (x0 >= W || y >= H || y >= (comp ? P.y1 >> 1 : P.y1)) return;
   const int cs = comp ? P.ctu >> 1 : P.ctu;
-  const int ctbRow = y / cs;
   const int maxv = (1 << P.bd) - 1;
-  const int16_t *row = S.p + (size_t)y * S.stride;
-  int16_t *out = D.p + (size_t)y * D.stride;
-  for (int k = 0; k < 4; k++) {
-    const int x = x0 + k;
-    if (x >= W) break;
-    const int s = row[x];
-    const int ctb = ctbRow * P.wc + x / cs;
-    const int32_t *prm = P.sao + ((size_t)ctb * 3 + comp) * 35;
-    int v = s;
-    if (prm[0] != 0) {
-      const int type = prm[1];
-      if (type == 4) {
-        v = clip3(0, maxv, s + prm[3 + (s >> (P.bd - 5))]);
-      } else {
-        // neighbours per EO class: 0 horizontal, 1 vertical, 2 135 degrees, 3 45 degrees
-        const int ax = x + (type == 1 ? 0 : (type == 3 ? 1 : -1)), ay = y + (type == 0 ? 0 : -1);
-        const int bx = x + (type == 1 ? 0 : (type == 3 ? -1 : 1)), by = y + (type == 0 ? 0 : 1);
-        if (ax >= 0 && ay >= 0 && ax < W && ay < H && bx >= 0 && by >= 0 && bx < W && by < H) {
-          const int a = S.p[(size_t)ay * S.stride + ax], b = S.p[(size_t)by * S.stride + bx];
-          v = clip3(0, maxv, s + prm[3 + 2 + sgn(s - a) + sgn(s - b)]);
-        }
+  const int ya = max(y - 1, 0), yb = min(y + 1, H - 1);
+  const int16_t *rc = S.p + (size_t)y * S.stride, *ra = S.p + (size_t)ya * S.stride, *rb = S.p + (size_t)yb * S.stride;
+  const int xl = max(x0 - 1, 0), xr = min(x0 + 8, W - 1);
+  // rows as [x0 - 1 .. x0 + 8] (plane rows are 64-sample pitched: the vector stays inside the row)
+  const uint4 vc = *(const uint4 *)(rc + x0), va = *(const uint4 *)(ra + x0), vb = *(const uint4 *)(rb + x0);
+  int C[10], A[10], B[10];
+  C[0] = rc[xl]; C[9] = rc[xr]; A[0] = ra[xl]; A[9] = ra[xr]; B[0] = rb[xl]; B[9] = rb[xr];
+  const int32_t *prm = P.sao + ((size_t)((y / cs) * P.wc + x0 / cs) * 3 + comp) * 35;
+  const int on = prm[0], type = prm[1];
+  const int e0 = prm[3], e1 = prm[4], e2 = prm[5], e3 = prm[6], e4 = prm[7];
+  {
+    const uint32_t wc[4] = {vc.x, vc.y, vc.z, vc.w}, wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      C[1 + 2 * k] = (int16_t)(wc[k] & 0xffff); C[2 + 2 * k] = (int16_t)(wc[k] >> 16);
+      A[1 + 2 * k] = (int16_t)(wa[k] & 0xffff); A[2 + 2 * k] = (int16_t)(wa[k] >> 16);
+      B[1 + 2 * k] = (int16_t)(wb[k] & 0xffff); B[2 + 2 * k] = (int16_t)(wb[k] >> 16);
+    }
+  }
+  int v[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = C[1 + k];
+  if (on) {
+    if (type == 4) {   // band offset
+#pragma unroll
+      for (int k = 0; k < 8; k++) v[k] = clip3(0, maxv, v[k] + prm[3 + (v[k] >> (P.bd - 5))]);
+    } else {
+      // neighbours per EO class: 0 horizontal, 1 vertical, 2 135 degrees, 3 45 degrees
+      const int dax = type == 1 ? 0 : (type == 3 ? 1 : -1), day = type == 0 ? 0 : -1;
+      const bool rowsIn = day == 0 || (y - 1 >= 0 && y + 1 < H);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int x = x0 + k;
+        const int a = type == 0 ? C[k] : (type == 1 ? A[1 + k] : (type == 2 ? A[k] : A[2 + k]));
+        const int b = type == 0 ? C[2 + k] : (type == 1 ? B[1 + k] : (type == 2 ? B[2 + k] : B[k]));
+        const bool in = rowsIn && x + dax >= 0 && x + dax < W && x - dax >= 0 && x - dax < W && x < W;
+        const int s0 = v[k], ei = 2 + sgn(s0 - a) + sgn(s0 - b);
+        const int off = ei == 0 ? e0 : (ei == 1 ? e1 : (ei == 2 ? e2 : (ei == 3 ? e3 : e4)));
+        if (in) v[k] = clip3(0, maxv, s0 + off);
       }
     }
-    out[x] = (int16_t)v;
+  }
+  int16_t *out = D.p + (size_t)y * D.stride + x0;
+  if (x0 + 8 <= W) {
+    *(uint4 *)out = make_uint4((uint32_t)(uint16_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)(uint16_t)v[2] | ((uint32_t)v[3] << 16),
+                               (uint32_t)(uint16_t)v[4] | ((uint32_t)v[5] << 16), (uint32_t)(uint16_t)v[6] | ((uint32_t)v[7] << 16));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if (x0 + k < W) out[k] = (int16_t)v[k];
   }
 }
 
@@ -328,8 +357,8 @@ __global__ __launch_bounds__(256) void k_alf(AlfParams P, int gx, int gy, int gc
 void launch_sao(const SaoParams &p, hipStream_t s) {
   const int W = p.src[0].w;   // luma bounds; chroma blocks beyond their rows exit
   if (p.y1 <= p.y0) return;
-  dim3 grid(((W + 3) / 4 + 63) / 64, p.y1 - p.y0, 3);
-  hipLaunchKernelGGL(k_sao, grid, dim3(64), 0, s, p);
+  dim3 grid(((W + 7) / 8 + 63) / 64, (p.y1 - p.y0 + 3) / 4, 3);
+  hipLaunchKernelGGL(k_sao, grid, dim3(256), 0, s, p);
 }
 
 // Clear (copy == 0) or copy the three planes of a picture in one launch (the per-picture residual

@@ -176,19 +176,29 @@ __device__ __forceinline__ void combine_store(const McParams &P, const McJob &J,
 
 // Two waves per job: with both lists, wave l filters list l (luma, then its chroma); with one list,
 // wave 0 filters the luma and wave 1 the chroma. Wave 0 stores the luma, wave 1 the chroma.
-__global__ __launch_bounds__(128) void k_mc_basic(McParams P, const McJob *__restrict__ jobs, int njobs) {
-  __shared__ __attribute__((aligned(16))) int16_t s_lwin[2][LR * LP];   // luma windows per list
-  __shared__ __attribute__((aligned(16))) int16_t s_cwin[4][CR * CP];   // chroma windows, combo = 2 * (comp - 1) + list
-  __shared__ __attribute__((aligned(16))) int16_t s_lt[2][16 * TP];     // luma H outputs [col][row]
-  __shared__ __attribute__((aligned(16))) int16_t s_ct[4][8 * CTP];     // chroma H outputs [col][row]
-  __shared__ __attribute__((aligned(16))) int16_t s_lo[2][256];         // luma V outputs per list [y * w + x]
-  __shared__ __attribute__((aligned(16))) int16_t s_co[4][64];          // chroma V outputs [y * cw + x]
-  const int j = blockIdx.x;
+struct BasicLds {
+  alignas(16) int16_t lwin[2][LR * LP];   // luma windows per list
+  alignas(16) int16_t cwin[4][CR * CP];   // chroma windows, combo = 2 * (comp - 1) + list
+  alignas(16) int16_t lt[2][16 * TP];     // luma H outputs [col][row]
+  alignas(16) int16_t ct[4][8 * CTP];     // chroma H outputs [col][row]
+  alignas(16) int16_t lo[2][256];         // luma V outputs per list [y * w + x]
+  alignas(16) int16_t co[4][64];          // chroma V outputs [y * cw + x]
+};
+
+// One job on 128 lanes (tid 0..127) with LDS L; the caller's workgroup runs two jobs, so every
+// __syncthreads here is reached the same number of times by both (three, unconditionally).
+__device__ __forceinline__ void mc_basic(const McParams &P, const McJob *__restrict__ jobs, int njobs, int j, int tid, BasicLds &L) {
+  auto &s_lwin = L.lwin;
+  auto &s_cwin = L.cwin;
+  auto &s_lt = L.lt;
+  auto &s_ct = L.ct;
+  auto &s_lo = L.lo;
+  auto &s_co = L.co;
   if (j >= njobs) return;
   const McJob J = load_uniform(jobs + j);
   // readfirstlane: the wave index is uniform, and everything derived from it (list, component, window,
   // taps) then stays in SGPRs instead of being computed per lane
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int w = J.w, h = J.h, lw = __ffs(w) - 1;
   const int cw = w >> 1, chh = h >> 1, lcw = lw - 1;
   const bool bi = (J.flags & MC_L0) && (J.flags & MC_L1);
@@ -360,15 +370,19 @@ constexpr int TL_CP = 32, TL_CR = 20;    // chroma window: 4 chunks, 19 rows (+1
 constexpr int TL_TP = 42, TL_CTP = 22;   // H outputs, column-major: rows per column (odd dword pitch)
 constexpr int TL_LWIN = TL_LR * TL_LP, TL_CWIN = TL_CR * TL_CP;
 
-__global__ __launch_bounds__(256) void k_mc_tile(McParams P, const McJob *__restrict__ jobs, int njobs) {
-  // windows, then (after the H pass has read them) the V outputs in the same space
-  __shared__ __attribute__((aligned(16))) int16_t s_win[2 * TL_LWIN + 4 * TL_CWIN];
-  __shared__ __attribute__((aligned(16))) int16_t s_lt[2][32 * TL_TP];    // luma H outputs [col][row]
-  __shared__ __attribute__((aligned(16))) int16_t s_ct[4][16 * TL_CTP];   // chroma H outputs [col][row]
+struct TileLds {
+  alignas(16) int16_t win[2 * TL_LWIN + 4 * TL_CWIN];   // windows, then (after the H pass) the V outputs
+  alignas(16) int16_t lt[2][32 * TL_TP];                // luma H outputs [col][row]
+  alignas(16) int16_t ct[4][16 * TL_CTP];               // chroma H outputs [col][row]
+};
+
+__device__ __forceinline__ void mc_tile(const McParams &P, const McJob *__restrict__ jobs, int njobs, int j, TileLds &L) {
+  auto &s_win = L.win;
+  auto &s_lt = L.lt;
+  auto &s_ct = L.ct;
   int16_t *const s_lwin = s_win, *const s_cwin = s_win + 2 * TL_LWIN;
   int16_t *const s_lo = s_win;                    // luma V outputs [list][y * 32 + x]
   int16_t *const s_co = s_win + 2 * TL_LWIN;      // chroma V outputs [combo][y * 16 + x]
-  const int j = blockIdx.x;
   if (j >= njobs) return;
   const McJob J = load_uniform(jobs + j);
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -520,14 +534,24 @@ __global__ __launch_bounds__(256) void k_mc_tile(McParams P, const McJob *__rest
   }
 }
 
-}  // namespace
-
-void launch_mc_tile(const McParams &p, const McJob *jobs, int njobs, hipStream_t s) {
-  if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_mc_tile, dim3(njobs), dim3(256), 0, s, p, jobs, njobs);
+// One launch for the plain MC of a picture: the first ntile workgroups take a 32x32 tile each, the
+// others two <= 16x16 jobs (128 lanes each); both layouts share one LDS allocation.
+constexpr int MC_LDS = sizeof(TileLds) > 2 * sizeof(BasicLds) ? sizeof(TileLds) : 2 * sizeof(BasicLds);
+__global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict__ jobs, int ntile, int nbasic) {
+  __shared__ __attribute__((aligned(16))) char raw[MC_LDS];
+  const int b = blockIdx.x;
+  if (b < ntile) {
+    mc_tile(P, jobs, ntile, b, *reinterpret_cast<TileLds *>(raw));
+  } else {
+    const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
+    mc_basic(P, jobs + ntile, nbasic, 2 * (b - ntile) + half, threadIdx.x & 127,
+             *reinterpret_cast<BasicLds *>(raw + half * sizeof(BasicLds)));
+  }
 }
 
-void launch_mc_basic(const McParams &p, const McJob *jobs, int njobs, hipStream_t s) {
-  if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_mc_basic, dim3(njobs), dim3(128), 0, s, p, jobs, njobs);
+}  // namespace
+
+void launch_mc(const McParams &p, const McJob *jobs, int ntile, int nbasic, hipStream_t s) {
+  const int g = ntile + (nbasic + 1) / 2;
+  if (g > 0) hipLaunchKernelGGL(k_mc, dim3(g), dim3(256), 0, s, p, jobs, ntile, nbasic);
 }
