@@ -1149,23 +1149,45 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
   }
 }
 
-__global__ void k_recon_inter(IntraParams P, const ReconTile *__restrict__ tiles, int n) {
-  const int t = blockIdx.x;
+// One wave per inter tile (<= 16x16 luma, sides 4 / 8 / 16), four tiles per workgroup: four luma samples per lane (8-byte loads of
+// the prediction and the residual), two chroma samples per lane (Cb on lanes 0..31, Cr on 32..63); all
+// loads are issued before the first use.
+__global__ __launch_bounds__(256) void k_recon_inter(IntraParams P, const ReconTile *__restrict__ tiles, int n) {
+  const int t = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // a tile per wave
   if (t >= n) return;
-  const ReconTile T = tiles[t];
-  const int maxv = (1 << P.bd) - 1;
-  for (int comp = 0; comp < 3; comp++) {
-    if (!(T.comps & (comp ? 2 : 1))) continue;
-    const int s = comp ? 1 : 0;
-    const int bx = T.x >> s, by = T.y >> s, bw = T.w >> s, bh = T.h >> s;
-    const DPlane &D = P.reco[comp], &Pr = P.pred[comp], &Re = P.resi[comp];
-    for (int k = threadIdx.x; k < bw * bh; k += blockDim.x) {
-      const int yy = k / bw, xx = k - yy * bw;
-      int pv = pel(Pr, bx + xx, by + yy);
-      if (comp == 0 && (P.lmcs & 1)) pv = P.lmcs_fwd[pv];   // LMCS forward map of the prediction (DecCu.cpp:742,765)
-      const int v = pv + pel(Re, bx + xx, by + yy);
-      D.p[(size_t)(by + yy) * D.stride + bx + xx] = (int16_t)clampi(v, 0, maxv);
+  const ReconTile T = load_uniform(tiles + t);
+  const int lane = threadIdx.x & 63, maxv = (1 << P.bd) - 1;
+  const int w = T.w, h = T.h, lq = ilog2(w) - 2;
+  const bool doY = (T.comps & 1) && lane < ((w >> 2) * h);
+  const int yy = lane >> lq, xx = (lane & ((1 << lq) - 1)) * 4;
+  const int cw = w >> 1, chh = h >> 1, cq = ilog2(cw) - 1, comp = 1 + (lane >> 5), cl = lane & 31;
+  const bool doC = (T.comps & 2) && cl < ((cw >> 1) * chh);
+  const int cy = cl >> cq, cx = (cl & ((1 << cq) - 1)) * 2;
+  uint2 py = {}, ry = {};
+  uint32_t pc = 0, rc = 0;
+  const DPlane &DY = P.reco[0], &PY = P.pred[0], &RY = P.resi[0];
+  const DPlane &DC = P.reco[comp], &PC = P.pred[comp], &RC = P.resi[comp];
+  const size_t oy = (size_t)(T.y + yy) * PY.stride + T.x + xx;
+  const size_t oc = (size_t)((T.y >> 1) + cy) * PC.stride + (T.x >> 1) + cx;
+  if (doY) { py = *(const uint2 *)&PY.p[oy]; ry = *(const uint2 *)&RY.p[oy]; }
+  if (doC) { pc = *(const uint32_t *)&PC.p[oc]; rc = *(const uint32_t *)&RC.p[oc]; }
+  if (doY) {
+    int pv[4] = {(int16_t)(py.x & 0xffff), (int16_t)(py.x >> 16), (int16_t)(py.y & 0xffff), (int16_t)(py.y >> 16)};
+    const int rv[4] = {(int16_t)(ry.x & 0xffff), (int16_t)(ry.x >> 16), (int16_t)(ry.y & 0xffff), (int16_t)(ry.y >> 16)};
+    if (P.lmcs & 1) {   // LMCS forward map of the prediction (DecCu.cpp:742,765)
+#pragma unroll
+      for (int e = 0; e < 4; e++) pv[e] = P.lmcs_fwd[pv[e]];
     }
+    int v[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) v[e] = clampi(pv[e] + rv[e], 0, maxv);
+    *(uint2 *)(&DY.p[(size_t)(T.y + yy) * DY.stride + T.x + xx]) =
+        make_uint2((uint32_t)(uint16_t)v[0] | ((uint32_t)v[1] << 16), (uint32_t)(uint16_t)v[2] | ((uint32_t)v[3] << 16));
+  }
+  if (doC) {
+    const int v0 = clampi((int)(int16_t)(pc & 0xffff) + (int)(int16_t)(rc & 0xffff), 0, maxv);
+    const int v1 = clampi((int)(int16_t)(pc >> 16) + (int)(int16_t)(rc >> 16), 0, maxv);
+    *(uint32_t *)(&DC.p[(size_t)((T.y >> 1) + cy) * DC.stride + (T.x >> 1) + cx]) = (uint32_t)(uint16_t)v0 | ((uint32_t)v1 << 16);
   }
 }
 
@@ -1188,7 +1210,7 @@ void launch_lmcs_inverse(const DPlane &luma, const int16_t *inv_lut, int y0, int
 
 void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_recon_inter, dim3(n), dim3(64), 0, s, p, tiles, n);
+  hipLaunchKernelGGL(k_recon_inter, dim3((n + 3) / 4), dim3(256), 0, s, p, tiles, n);
 }
 
 void launch_intra(const IntraParams *p_dev, const IntraJob *jobs, int n, const int32_t *ctu_list, const int32_t *ctu_start,
