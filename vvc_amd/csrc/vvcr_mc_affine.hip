@@ -1,6 +1,6 @@
 // vvcr_mc_affine.hip — affine motion compensation with PROF for gfx950 (k_mc_affine).
 //
-// One 64-lane wave per <= 16x16 luma tile of an affine PU (InterPrediction::xPredAffineBlk,
+// Two waves (128 lanes) per <= 16x16 luma tile of an affine PU, two tiles per workgroup (InterPrediction::xPredAffineBlk,
 // InterPrediction.cpp:890-1272): 4x4 luma sub-block MVs from the control-point model, the 6-tap
 // m_lumaFilter4x4 (InterpolationFilter.cpp:57), PROF gradient correction (applyPROFCore Buffer.cpp:45),
 // 4x4 chroma sub-blocks with the mean MV of two luma sub-blocks, then the bi / BCW / WP combine.
@@ -70,27 +70,41 @@ struct Place {
   int base, pitch, ex, ey;
 };
 
-__global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__restrict__ jobs, int njobs, const AffPu *__restrict__ pus) {
-  __shared__ __attribute__((aligned(16))) int16_t s_lw[2][LWS];
-  __shared__ __attribute__((aligned(16))) int16_t s_cw[4][CWS];       // combo k = 2 * (comp - 1) + list
-  __shared__ __attribute__((aligned(16))) int16_t s_ht[2][16 * HTS];
-  __shared__ __attribute__((aligned(16))) int16_t s_ct[4][4 * CTS];
-  __shared__ __attribute__((aligned(16))) uint32_t s_tl[16][8];
-  __shared__ __attribute__((aligned(16))) uint32_t s_tc[32][8];
-  __shared__ int s_sbmv[2][16][2];     // MC MV of each luma sub-block (clamped)
-  __shared__ int s_stmv[2][16][2];     // stored MV (before the picture clamp) for chroma
-  __shared__ int s_csmv[2][4][2];      // chroma sub-block MVs
-  __shared__ int s_box[2][2][4];      // union boxes: [luma / chroma][list][x0 x1 y0 y1]
+struct AffLds {
+  alignas(16) int16_t lw[2][LWS];
+  alignas(16) int16_t cw[4][CWS];       // combo k = 2 * (comp - 1) + list
+  alignas(16) int16_t ht[2][16 * HTS];
+  alignas(16) int16_t ct[4][4 * CTS];
+  alignas(16) uint32_t tl[16][8];
+  alignas(16) uint32_t tc[32][8];
+  int sbmv[2][16][2];     // MC MV of each luma sub-block (clamped)
+  int stmv[2][16][2];     // stored MV (before the picture clamp) for chroma
+  int csmv[2][4][2];      // chroma sub-block MVs
+  int box[2][2][4];       // union boxes: [luma / chroma][list][x0 x1 y0 y1]
+};
+
+// One job on 128 lanes (lane 0..127) with LDS L; the workgroup runs two jobs, so every __syncthreads
+// here is reached unconditionally (the same number of times by both).
+__device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__restrict__ jobs, int njobs, const AffPu *__restrict__ pus,
+                                          int j, int lane, AffLds &L) {
+  auto &s_lw = L.lw;
+  auto &s_cw = L.cw;
+  auto &s_ht = L.ht;
+  auto &s_ct = L.ct;
+  auto &s_tl = L.tl;
+  auto &s_tc = L.tc;
+  auto &s_sbmv = L.sbmv;
+  auto &s_stmv = L.stmv;
+  auto &s_csmv = L.csmv;
+  auto &s_box = L.box;
   // after the H passes the chroma windows are dead: chroma predictions [combo][y * 8 + x] and the luma
   // prediction per list [y * 16 + x] live there
   int16_t(*s_co)[64] = (int16_t(*)[64])s_cw[0];
   int16_t(*s_lo)[256] = (int16_t(*)[256])s_cw[1];
 
-  const int j = blockIdx.x;
   if (j >= njobs) return;
   const AffJob J = jobs[j];
   const AffPu U = pus[J.pu];
-  const int lane = threadIdx.x;
   const int bd = P.bd, maxv = (1 << bd) - 1;
   const int headRoom = max(2, IF_INTERNAL_PREC - bd);
   const bool bi = U.l[0].present && U.l[1].present;
@@ -426,7 +440,8 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
   // samples around each sub-block, gradients (shift 6), dMv per position, applyPROFCore. A lane takes a
   // 4-sample row chunk of one sub-block: its row and the rows above / below come from the prediction
   // (or the ring at the sub-block's top / bottom), the left / right neighbours of the chunk from the ring;
-  // results are written back after every lane has read its neighbours.
+  // results are written back after every lane of the wave has read its neighbours (list l is wave l:
+  // the wave's LDS accesses execute in order, the asm statement keeps the compiler from moving them).
 #pragma unroll
   for (int l = 0; l < 2; l++) {
     const AffList &A = U.l[l];
@@ -467,10 +482,11 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
         res[px] = v;
       }
     }
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
     if (act) *(uint2 *)&s_lo[l][y * 16 + x0] = make_uint2(pk(res[0], res[1]), pk(res[2], res[3]));
-    __syncthreads();
   }
+  __syncthreads();
 
   // ---- combine (xWeightedAverage: addAvg / addWeightedAvg; weighted prediction; uni already final
   // without WP) and store 4 consecutive samples of a row per lane
@@ -514,9 +530,15 @@ __global__ __launch_bounds__(128) void k_mc_affine(McParams P, const AffJob *__r
   }
 }
 
+__global__ __launch_bounds__(256) void k_mc_affine(McParams P, const AffJob *__restrict__ jobs, int njobs, const AffPu *__restrict__ pus) {
+  __shared__ AffLds lds[2];
+  const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
+  mc_affine(P, jobs, njobs, pus, 2 * blockIdx.x + half, threadIdx.x & 127, lds[half]);
+}
+
 }  // namespace
 
 void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const AffPu *pus, hipStream_t s) {
   if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_mc_affine, dim3(njobs), dim3(128), 0, s, p, jobs, njobs, pus);
+  hipLaunchKernelGGL(k_mc_affine, dim3((njobs + 1) / 2), dim3(256), 0, s, p, jobs, njobs, pus);
 }
