@@ -15,6 +15,7 @@
 namespace {
 
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+typedef short short2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int sgn(int v) { return (v > 0) - (v < 0); }
 
 // One lane per 8 horizontally adjacent samples (a 16-byte vector) of one component, a wave per row, four
@@ -237,12 +238,17 @@ __device__ __forceinline__ void alf_luma(const AlfParams &P, int tx, int ty) {
   }
   const int classIdx = bi & 255, tr = (bi >> 8) & 255;
   const int16_t *coef = s_cf + classIdx * 13, *clip = s_cl + classIdx * 13;
-  int fc[12], fl[12];
+  // packed 16-bit arithmetic: the two samples of a tap pair as one int16x2 (differences to the centre
+  // fit 16 bits, clips <= 1 << bd), clipped with packed min / max, then one dot2 with the coefficient
+  // pair (c, c): exactly c * clip(a - cur) + c * clip(b - cur)
+  short2_t fcp[12], clp[12], cln[12];
 #pragma unroll
   for (int k = 0; k < 12; k++) {
     const int pk = s_perm[tr * 13 + k];
-    fc[k] = coef[pk];
-    fl[k] = clip[pk];
+    const int c = coef[pk], l = clip[pk];
+    fcp[k] = (short2_t){(short)c, (short)c};
+    clp[k] = (short2_t){(short)l, (short)l};
+    cln[k] = (short2_t){(short)-l, (short)-l};
   }
   const int maxv = (1 << P.bd) - 1;
 #pragma unroll
@@ -254,18 +260,25 @@ __device__ __forceinline__ void alf_luma(const AlfParams &P, int tx, int ty) {
     const int yVb = y & (vbH - 1);
     const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
     const int cur = T(x, y);
-    int sum = fc[0] * clip_alf(fl[0], cur, T(x, r5), T(x, r6));
-    sum += fc[1] * clip_alf(fl[1], cur, T(x + 1, r3), T(x - 1, r4));
-    sum += fc[2] * clip_alf(fl[2], cur, T(x, r3), T(x, r4));
-    sum += fc[3] * clip_alf(fl[3], cur, T(x - 1, r3), T(x + 1, r4));
-    sum += fc[4] * clip_alf(fl[4], cur, T(x + 2, r1), T(x - 2, r2));
-    sum += fc[5] * clip_alf(fl[5], cur, T(x + 1, r1), T(x - 1, r2));
-    sum += fc[6] * clip_alf(fl[6], cur, T(x, r1), T(x, r2));
-    sum += fc[7] * clip_alf(fl[7], cur, T(x - 1, r1), T(x + 1, r2));
-    sum += fc[8] * clip_alf(fl[8], cur, T(x - 2, r1), T(x + 2, r2));
-    sum += fc[9] * clip_alf(fl[9], cur, T(x + 3, y), T(x - 3, y));
-    sum += fc[10] * clip_alf(fl[10], cur, T(x + 2, y), T(x - 2, y));
-    sum += fc[11] * clip_alf(fl[11], cur, T(x + 1, y), T(x - 1, y));
+    const short2_t cc = {(short)cur, (short)cur};
+    int sum = 0;
+    auto tap = [&](int k, int a, int b) {
+      short2_t d = (short2_t){(short)a, (short)b} - cc;
+      d = __builtin_elementwise_min(__builtin_elementwise_max(d, cln[k]), clp[k]);
+      sum = __builtin_amdgcn_sdot2(d, fcp[k], sum, false);
+    };
+    tap(0, T(x, r5), T(x, r6));
+    tap(1, T(x + 1, r3), T(x - 1, r4));
+    tap(2, T(x, r3), T(x, r4));
+    tap(3, T(x - 1, r3), T(x + 1, r4));
+    tap(4, T(x + 2, r1), T(x - 2, r2));
+    tap(5, T(x + 1, r1), T(x - 1, r2));
+    tap(6, T(x, r1), T(x, r2));
+    tap(7, T(x - 1, r1), T(x + 1, r2));
+    tap(8, T(x - 2, r1), T(x + 2, r2));
+    tap(9, T(x + 3, y), T(x - 3, y));
+    tap(10, T(x + 2, y), T(x - 2, y));
+    tap(11, T(x + 1, y), T(x - 1, y));
     sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
     dst[(size_t)y * D.stride] = (int16_t)clip3(0, maxv, sum + cur);
   }
