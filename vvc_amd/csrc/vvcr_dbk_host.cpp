@@ -31,7 +31,9 @@ struct Planner {
   int ctu_x = 0, ctu_y = 0;
   uint8_t bs[2][32 * 32];
   uint8_t edge[2][32 * 32];
-  uint8_t lenP[3][128][128], lenQ[3][128][128], tedge[128][128];
+  // edge lengths / transform-edge flags on the edge grid of the CTU: 4x4 luma units, 2x2 chroma units
+  // (edges off the grid, ISP sub-partitions 1 or 2 samples wide, are never filtered nor read)
+  uint8_t lenP[3][32][32], lenQ[3][32][32], tedge[32][32];
   bool left = false, top = false, internal = false;
 
   Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, DbkLists &o)
@@ -123,13 +125,16 @@ struct Planner {
         const int tp = horz ? get_tu(qx, qy - 1, ch) : get_tu(qx - 1, qy, ch);
         const int sizeP = horz ? d.tu[tp].b[comp][BH] : d.tu[tp].b[comp][BW];
         const int X = horz ? xo + k : xo, Y = horz ? yo : yo + k;
+        const int g = ch ? 1 : 2;   // log2 of the grid unit in component samples
+        if ((X | Y) & ((1 << g) - 1)) continue;
+        const int U = X >> g, V = Y >> g;
         if (comp == 0) {
-          tedge[X][Y] = 1;
+          tedge[U][V] = 1;
           const bool small = sizeP <= 4 || sizeQ <= 4;
-          lenQ[0][X][Y] = small ? 1 : (sizeQ >= 32 ? 7 : 3);
-          lenP[0][X][Y] = small ? 1 : (sizeP >= 32 ? 7 : 3);
+          lenQ[0][U][V] = small ? 1 : (sizeQ >= 32 ? 7 : 3);
+          lenP[0][U][V] = small ? 1 : (sizeP >= 32 ? 7 : 3);
         } else {
-          lenQ[comp][X][Y] = lenP[comp][X][Y] = (sizeQ >= 8 && sizeP >= 8) ? 3 : 1;
+          lenQ[comp][U][V] = lenP[comp][U][V] = (sizeQ >= 8 && sizeP >= 8) ? 3 : 1;
         }
       }
     }
@@ -143,17 +148,17 @@ struct Planner {
     const int outer = horz ? h : w, inner = horz ? w : h;
     for (int a = 0; a < outer; a += 8)
       for (int b = 0; b < inner; b += 4) {
-        const int X = horz ? xo + b : xo + a, Y = horz ? yo + a : yo + b;
-        auto T = [&](int delta) { return horz ? tedge[X][Y + delta] : tedge[X + delta][Y]; };
+        const int U = (horz ? xo + b : xo + a) >> 2, V = (horz ? yo + a : yo + b) >> 2;   // 4x4 units
+        auto T = [&](int delta) { return horz ? tedge[U][V + (delta >> 2)] : tedge[U + (delta >> 2)][V]; };
         if (T(0)) {
-          if (Q[X][Y] > 5) Q[X][Y] = 5;
-          if (a > 0 && P[X][Y] > 5) P[X][Y] = 5;
+          if (Q[U][V] > 5) Q[U][V] = 5;
+          if (a > 0 && P[U][V] > 5) P[U][V] = 5;
         } else if (a > 0 && (T(-4) || a + 4 >= outer || T(4))) {
-          Q[X][Y] = P[X][Y] = 1;
+          Q[U][V] = P[U][V] = 1;
         } else if (a > 0 && (T(-8) || a + 8 >= outer || T(8))) {
-          Q[X][Y] = P[X][Y] = 2;
+          Q[U][V] = P[U][V] = 2;
         } else {
-          Q[X][Y] = P[X][Y] = 3;
+          Q[U][V] = P[U][V] = 3;
         }
       }
   }
@@ -166,20 +171,26 @@ struct Planner {
     const int sh = cuQ.yvalid ? 0 : 1;
     const int qx = lx >> sh, qy = ly >> sh;
     const int px = dir == VER ? qx - 1 : qx, py = dir == VER ? qy : qy - 1;
-    const vvcr_cu &cuP = d.cu[get_cu(px, py, ch)];
+    // an edge inside the CU (sub-block / TU edges): P is the same CU, without a map lookup
+    const bool same = px >= (cuQ.yvalid ? cuQ.x : cuQ.cx) && py >= (cuQ.yvalid ? cuQ.y : cuQ.cy);
+    const vvcr_cu &cuP = same ? cuQ : d.cu[get_cu(px, py, ch)];
     if (cuP.predmode == MODE_INTRA || cuQ.predmode == MODE_INTRA) {
       const int bsY = (cuP.predmode == MODE_INTRA && cuP.bdpcm) && (cuQ.predmode == MODE_INTRA && cuQ.bdpcm) ? 0 : 2;
       const int bsC = (cuP.predmode == MODE_INTRA && cuP.bdpcmc) && (cuQ.predmode == MODE_INTRA && cuQ.bdpcmc) ? 0 : 2;
       return bs_set(bsY, 0) + bs_set(bsC, 1) + bs_set(bsC, 2);
     }
-    const vvcr_tu &tq = d.tu[get_tu(qx, qy, ch)], &tp = d.tu[get_tu(px, py, ch)];
     const int marker = bs[dir][raster(lx, ly)];
-    const bool ciip = d.pu[cuP.firstpu].ciip || d.pu[cuQ.firstpu].ciip;
+    const bool ciip = d.pu[cuQ.firstpu].ciip || (!same && d.pu[cuP.firstpu].ciip);
     if (marker && ciip) return bs_set(2, 0) + bs_set(2, 1) + bs_set(2, 2);
     int tmp = 0;
-    if (marker && (tq.b[0][BCBF] || tp.b[0][BCBF])) tmp += bs_set(1, 0);
-    if (marker && (tq.b[1][BCBF] || tp.b[1][BCBF] || tq.jccr || tp.jccr)) tmp += bs_set(1, 1);
-    if (marker && (tq.b[2][BCBF] || tp.b[2][BCBF] || tq.jccr || tp.jccr)) tmp += bs_set(1, 2);
+    if (marker) {   // transform edge: the coded-block flags of both sides (a sub-block-only edge has none)
+      const int tqi = get_tu(qx, qy, ch);
+      const int tpi = (same && cuQ.ntu == 1 && !cuQ.isp) ? tqi : get_tu(px, py, ch);   // one TU: both sides
+      const vvcr_tu &tq = d.tu[tqi], &tp = d.tu[tpi];
+      if (tq.b[0][BCBF] || tp.b[0][BCBF]) tmp += bs_set(1, 0);
+      if (tq.b[1][BCBF] || tp.b[1][BCBF] || tq.jccr || tp.jccr) tmp += bs_set(1, 1);
+      if (tq.b[2][BCBF] || tp.b[2][BCBF] || tq.jccr || tp.jccr) tmp += bs_set(1, 2);
+    }
     if ((tmp & 3) == 1) return tmp;
     if (ciip) return 1;
     if (!cuQ.yvalid) return tmp;
@@ -235,7 +246,7 @@ struct Planner {
       if (!b) continue;
       const vvcr_cu &cuP = d.cu[get_cu(dir == VER ? px - 1 : px, dir == VER ? py : py - 1, cu.chtype)];
       const int qp = (cuP.qp + cu.qp + 1) >> 1;
-      int lp = lenP[0][px - ctu_x][py - ctu_y], lq = lenQ[0][px - ctu_x][py - ctu_y];
+      int lp = lenP[0][(px - ctu_x) >> 2][(py - ctu_y) >> 2], lq = lenQ[0][(px - ctu_x) >> 2][(py - ctu_y) >> 2];
       bool pl = false, ql = false;
       if (lp > 3) {
         pl = true;
@@ -268,7 +279,7 @@ struct Planner {
       int cpi = cu.chtype ? get_cu(nlx >> 1, nly >> 1, 1) : get_cu(nlx, nly, 0);
       if (d.cu[cpi].treetype != 0 || pp.dual_tree) cpi = get_cu(nlx >> 1, nly >> 1, 1);
       const vvcr_cu &cuP = d.cu[cpi];
-      const int cx = (px - ctu_x) >> 1, cy = (py - ctu_y) >> 1;
+      const int cx = (px - ctu_x) >> 2, cy = (py - ctu_y) >> 2;   // 2x2 chroma units
       const bool large = lenP[1][cx][cy] >= 3 && lenQ[1][cx][cy] >= 3;
       const bool ctbh = dir == HOR && py % ctu == 0;
       uint32_t w = (uint32_t)large << 4 | (uint32_t)ctbh << 19;
