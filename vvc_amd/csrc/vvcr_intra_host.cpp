@@ -658,20 +658,24 @@ struct Planner {
       }
     }
     PROF_MARK("wdeps");
-    // CTU order of the launch: wavefront (anti-diagonals x + 2y, VVCR_CTU_ORDER=raster for the raster
-    // order). Every cross-CTU dependency (left, above-left, above, above-right) is on an earlier CTU in
+    // CTU order of the launch: wavefront (anti-diagonals x + 2y, the lower CTU of a diagonal first: 4K
+    // I picture -1 %; VVCR_CTU_ORDER=raster for the raster order). Every cross-CTU dependency (left, above-left, above, above-right) is on an earlier CTU in
     // both orders, so a workgroup only ever waits for CTUs already taken; in wavefront order the CTUs
     // taken but not finished are the few on the active diagonals, so a launch of a few dozen workgroups
     // keeps the whole wavefront busy (raster order needs about a row of CTUs per active row).
     {
-      static const bool raster = [] { const char *e = getenv("VVCR_CTU_ORDER"); return e && !strcmp(e, "raster"); }();
+      static const int order_kind = [] {   // 0 wavefront, lower CTU of a diagonal first; 1 raster; 2 upper first
+        const char *e = getenv("VVCR_CTU_ORDER");
+        return !e ? 0 : (!strcmp(e, "raster") ? 1 : (!strcmp(e, "wf_up") ? 2 : 0));
+      }();
+      const bool raster = order_kind == 1;
       const int nb = (int)cb.size() - 1;
       if (!raster && nb > 1) {
         std::vector<int32_t> bo(nb);
         for (int k = 0; k < nb; k++) bo[k] = k;
         auto key = [&](int k) {
           const int c = ctu_of_job[cb[k]], x = c % wc, y = c / wc;
-          return std::make_pair(x + 2 * y, y);
+          return std::make_pair(x + 2 * y, order_kind == 2 ? y : -y);
         };
         std::stable_sort(bo.begin(), bo.end(), [&](int a, int b) { return key(a) < key(b); });
         std::vector<int32_t> p2;
