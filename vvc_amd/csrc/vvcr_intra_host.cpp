@@ -98,6 +98,13 @@ struct Planner {
   std::vector<std::pair<int32_t, IntraJob>> jobs;   // (level, job)
   std::vector<int32_t> dep_off{0}, dep_flat;        // per job (CSR): the steps it reads from (indices into jobs)
   std::vector<int32_t> cur;                         // dependencies of the step being planned
+  std::vector<int32_t> cur_mark;                    // per job: the step count at which it last entered `cur`
+  std::vector<int32_t> cclm_deps;                   // scratch of intra_chroma
+  void add_dep(int32_t pr) {   // O(1) de-duplication (a CCLM block reads hundreds of luma units)
+    if ((size_t)pr >= cur_mark.size()) cur_mark.resize(std::max<size_t>(2 * cur_mark.size(), (size_t)pr + 1024), -1);
+    const int32_t tok = (int32_t)jobs.size();
+    if (cur_mark[pr] != tok) { cur_mark[pr] = tok; cur.push_back(pr); }
+  }
   int seq = 0;
   bool cscale = false;                              // LMCS chroma residual scaling active in this picture
   // Slice / tile of every CTU (getCURestricted: a neighbour is usable only inside the same slice and
@@ -131,7 +138,7 @@ struct Planner {
         if (out.order[ch][i] < seq && region_at((ux << s) << cs, (uy << s) << cs) == cur_reg) {
           m = std::max(m, level[ch][i]);
           const int32_t pr = prod[comp][i];
-          if (pr >= 0 && (cur.empty() || cur.back() != pr)) cur.push_back(pr);   // runs of one producer: once
+          if (pr >= 0) add_dep(pr);
         }
       }
     return m;
@@ -305,6 +312,8 @@ struct Planner {
     const vvcr_pu &p = d.pu[c.firstpu];
     const bool dual = c.chtype == 1;
     for (int t = c.firsttu; t < c.firsttu + c.ntu; t++) {
+      int cclm_lev = -1, cclm_box[4] = {0, 0, 0, 0};   // Cb's CCLM luma dependencies, reused by Cr (same block)
+      cclm_deps.clear();
       for (int comp = 1; comp < 3; comp++) {
         const int32_t *b = d.tu[t].b[comp];
         if (b[2] <= 0) continue;
@@ -320,9 +329,19 @@ struct Planner {
           // rows above it (with the above-right extension, up to twice the width) and the columns left of
           // it (with the below-left extension); the strips are taken 4 samples deep
           const int lx = 2 * j.x, ly = 2 * j.y;
-          lev = std::max(lev, max_level(0, 0, lx, ly, lx + 2 * j.w - 1, ly + 2 * j.h - 1));
-          lev = std::max(lev, max_level(0, 0, lx - 4, ly - 4, lx + 4 * j.w - 1, ly - 1));
-          lev = std::max(lev, max_level(0, 0, lx - 4, ly, lx - 1, ly + 4 * j.h - 1));
+          if (cclm_lev >= 0 && cclm_box[0] == j.x && cclm_box[1] == j.y && cclm_box[2] == j.w && cclm_box[3] == j.h) {
+            lev = std::max(lev, cclm_lev);
+            for (int32_t pr : cclm_deps) add_dep(pr);
+          } else {
+            const size_t c0 = cur.size();   // the luma producers follow the chroma ones (disjoint sets)
+            int cl = max_level(0, 0, lx, ly, lx + 2 * j.w - 1, ly + 2 * j.h - 1);
+            cl = std::max(cl, max_level(0, 0, lx - 4, ly - 4, lx + 4 * j.w - 1, ly - 1));
+            cl = std::max(cl, max_level(0, 0, lx - 4, ly, lx - 1, ly + 4 * j.h - 1));
+            lev = std::max(lev, cl);
+            cclm_lev = cl;
+            cclm_box[0] = j.x; cclm_box[1] = j.y; cclm_box[2] = j.w; cclm_box[3] = j.h;
+            cclm_deps.assign(cur.begin() + c0, cur.end());
+          }
         }
         if (cscale && j.w * j.h > 4) lev = std::max(lev, set_cscale(j, 2 * j.x, 2 * j.y));
         lev += 1;
