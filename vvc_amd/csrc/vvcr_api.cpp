@@ -213,6 +213,8 @@ struct vvcr_ctx {
   std::vector<std::array<hipEvent_t, MAXLANE>> slot_r;   // per DPB slot and lane: last reader
   std::vector<uint32_t> slot_r_set;                 // per DPB slot: lanes with a reader since the last write
   std::vector<uint64_t> slot_seq;                   // per DPB slot: launch sequence number of its last writer
+  std::vector<int> slot_lane;                       // per DPB slot: lane of its last writer (-1 none)
+  int lane_policy = 1;                              // VVCR_LANE_POLICY: 1 lane of the newest reference, 0 tail only
   bool in_picture = false;
   vvcr_picture cur;                  // the picture of vvcr_begin_picture .. vvcr_end_picture / vvcr_prepare_picture
   DevVec<uint16_t> d_scans;
@@ -462,11 +464,22 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
       if (std::find(refs.begin(), refs.end(), pp.ref_slot[l][i]) == refs.end()) refs.push_back(pp.ref_slot[l][i]);
   // Lane choice: pictures without references (intra) take lanes [0, nintra), which only intra pictures
   // use, so an intra picture never queues behind B pictures and two intra-started segments may overlap;
-  // the others take the lane of [nintra, nlane) whose last picture is one of their references (stream
-  // order then costs nothing), else the least recently used of those lanes.
+  // the others take the lane of [nintra, nlane) that wrote their newest reference (stream order then
+  // costs nothing; VVCR_LANE_POLICY=0: only a lane whose last picture is a reference), else the least
+  // recently used of those lanes. Dependencies on pictures of the chosen lane need no event wait.
   const int lo = refs.empty() ? 0 : ctx->nintra, hi = refs.empty() ? ctx->nintra : ctx->nlane;
   int L = -1;
-  if (!refs.empty())
+  if (!refs.empty() && ctx->lane_policy == 1) {
+    // the B lane that wrote the newest of the references (still in its slot): the pictures of one
+    // segment then stay on one lane even when other segments' pictures are interleaved on it, and their
+    // dependencies are stream order instead of cross-lane event waits
+    uint64_t best = 0;
+    for (int rs : refs) {
+      const int wl = ctx->slot_lane[rs];
+      if (wl >= lo && wl < hi && ctx->slot_seq[rs] > best) { best = ctx->slot_seq[rs]; L = wl; }
+    }
+  }
+  if (!refs.empty() && L < 0)
     for (int l = lo; l < hi && L < 0; l++) {
       const int ts = ctx->lanes[l].tail_slot;
       if (ts >= 0 && std::find(refs.begin(), refs.end(), ts) != refs.end() && ctx->lanes[l].tail_seq == ctx->slot_seq[ts]) L = l;
@@ -489,8 +502,8 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   ln.tail_seq = ++ctx->seq;
   // dependencies on pictures of other lanes (same-lane work is ordered by the stream anyway)
   for (int rs : refs)
-    if (ctx->slot_w_set[rs]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[rs], 0));
-  if (ctx->slot_w_set[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[pp.slot], 0));
+    if (ctx->slot_w_set[rs] && ctx->slot_lane[rs] != L) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[rs], 0));
+  if (ctx->slot_w_set[pp.slot] && ctx->slot_lane[pp.slot] != L) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[pp.slot], 0));
   for (int l = 0; l < ctx->nlane; l++)
     if (l != L && (ctx->slot_r_set[pp.slot] >> l & 1)) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_r[pp.slot][l], 0));
   VVCR_CHECK_HIP(hipEventRecord(r.start, s));
@@ -605,6 +618,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   VVCR_CHECK_HIP(hipEventRecord(ctx->slot_w[pp.slot], s));
   ctx->slot_w_set[pp.slot] = 1;
   ctx->slot_seq[pp.slot] = ln.tail_seq;
+  ctx->slot_lane[pp.slot] = L;
   ctx->slot_r_set[pp.slot] = 0;
   for (int rs : refs)
     if (rs != pp.slot) {
@@ -664,6 +678,8 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     ctx->slot_r.assign(sp->dpb_slots, {});
     ctx->slot_r_set.assign(sp->dpb_slots, 0);
     ctx->slot_seq.assign(sp->dpb_slots, 0);
+    ctx->slot_lane.assign(sp->dpb_slots, -1);
+    if (const char *e = getenv("VVCR_LANE_POLICY")) ctx->lane_policy = atoi(e);
     for (int k = 0; k < sp->dpb_slots; k++) {
       VVCR_CHECK_HIP(hipEventCreateWithFlags(&ctx->slot_w[k], hipEventDisableTiming));
       for (int l = 0; l < MAXLANE; l++) VVCR_CHECK_HIP(hipEventCreateWithFlags(&ctx->slot_r[k][l], hipEventDisableTiming));
