@@ -248,8 +248,11 @@ static int n_ctb(const vvcr_seq_params &sp) {
 
 static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lane) {
   McParams P{};
-  for (size_t s = 0; s < ctx->dpb.size() && s < 32; s++)
-    for (int c = 0; c < 3; c++) P.ref[s][c] = ctx->dpb[s][c];
+  for (size_t s = 0; s < ctx->dpb.size() && s < (size_t)VVCR_MAX_SLOTS; s++)
+    for (int c = 0; c < 3; c++) P.ref.p[s][c] = ctx->dpb[s][c].p;
+  for (int c = 0; c < 3; c++) {
+    P.ref.stride[c] = ctx->dpb[0][c].stride; P.ref.w[c] = ctx->dpb[0][c].w; P.ref.h[c] = ctx->dpb[0][c].h;
+  }
   for (int c = 0; c < 3; c++) P.out[c] = ctx->lanes[lane].pred[c];
   P.pic_w = ctx->sp.width;
   P.pic_h = ctx->sp.height;
@@ -635,8 +638,8 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
   if (!sp || !out) return VVCR_E_ARG;
   *out = nullptr;
   if (sp->chroma_format != 1 || sp->bit_depth < 8 || sp->bit_depth > 10 || sp->width <= 0 || sp->height <= 0 ||
-      sp->dpb_slots <= 0 || sp->dpb_slots > 32 || sp->width % 8 || sp->height % 8 || sp->ctu_log2 < 5 || sp->ctu_log2 > 7) {
-    g_create_error = "unsupported sequence parameters (4:2:0, 8..10 bit, size multiple of 8, CTU 32..128, <= 32 DPB slots)";
+      sp->dpb_slots <= 0 || sp->dpb_slots > VVCR_MAX_SLOTS || sp->width % 8 || sp->height % 8 || sp->ctu_log2 < 5 || sp->ctu_log2 > 7) {
+    g_create_error = "unsupported sequence parameters (4:2:0, 8..10 bit, size multiple of 8, CTU 32..128, <= 64 DPB slots)";
     return VVCR_E_UNSUPPORTED;
   }
   auto ctx = std::make_unique<vvcr_ctx>();
@@ -929,7 +932,7 @@ int vvcr_picture_create(const vvcr_seq_params *sp, const vvcr_pic_params *pp, vv
   if (!sp || !pp || !out) return VVCR_E_ARG;
   *out = nullptr;
   if (sp->chroma_format != 1 || sp->width <= 0 || sp->height <= 0 || sp->width % 8 || sp->height % 8 ||
-      sp->ctu_log2 < 5 || sp->ctu_log2 > 7 || sp->dpb_slots <= 0 || sp->dpb_slots > 32) {
+      sp->ctu_log2 < 5 || sp->ctu_log2 > 7 || sp->dpb_slots <= 0 || sp->dpb_slots > VVCR_MAX_SLOTS) {
     g_create_error = "unsupported sequence parameters";
     return VVCR_E_UNSUPPORTED;
   }

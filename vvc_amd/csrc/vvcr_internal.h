@@ -93,8 +93,22 @@ struct WpTable {
   int8_t d[2][VVCR_MAX_REF][3];
 };
 
+constexpr int VVCR_MAX_SLOTS = 64;   // DPB slots of a context (vvcr_seq_params::dpb_slots)
+
+// DPB planes by slot: one pointer per (slot, component); every slot of a component has the same geometry.
+struct RefPlanes {
+  const int16_t *p[VVCR_MAX_SLOTS][3];
+  int32_t stride[3], w[3], h[3];
+  __host__ __device__ DPlane get(int slot, int comp) const {
+    DPlane d;
+    d.p = const_cast<int16_t *>(p[slot][comp]);
+    d.stride = stride[comp]; d.w = w[comp]; d.h = h[comp];
+    return d;
+  }
+};
+
 struct McParams {
-  DPlane ref[32][3];     // DPB planes by slot (only used slots valid)
+  RefPlanes ref;         // DPB planes by slot (only used slots valid)
   DPlane out[3];         // destination (prediction planes of the current picture)
   int32_t pic_w, pic_h;  // luma picture size
   int32_t bd;            // bit depth

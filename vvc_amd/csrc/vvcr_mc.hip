@@ -127,7 +127,7 @@ __device__ __forceinline__ Win make_win(const McParams &P, const McJob &J, int c
   const int cs = comp ? 1 : 0, N = comp ? 4 : 8, half = N / 2 - 1, fb = 4 + cs;
   w.on = ((J.flags & (l ? MC_L1 : MC_L0)) != 0) && ((J.flags & (comp ? MC_CHROMA : MC_LUMA)) != 0);
   const int slot = l ? J.slot[1] : J.slot[0];
-  const DPlane &R = P.ref[slot < 0 ? 0 : slot][comp];
+  const DPlane &R = P.ref.get(slot < 0 ? 0 : slot, comp);
   const int mvx = l ? J.mv[1][0] : J.mv[0][0], mvy = l ? J.mv[1][1] : J.mv[0][1], mask = (1 << fb) - 1;
   w.frac_x = mvx & mask;
   w.frac_y = mvy & mask;

@@ -208,7 +208,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
   for (int l = 0; l < 2; l++) {
     lmode[l] = 0; lax[l] = loy[l] = lrows[l] = lnch[l] = 0;
     if (!U.l[l].present) continue;
-    const DPlane &R = P.ref[U.l[l].slot][0];
+    const DPlane &R = P.ref.get(U.l[l].slot, 0);
     const int x0 = ubox[l][0], x1 = ubox[l][1], y0 = ubox[l][2], y1 = ubox[l][3];
     lax[l] = x0 & ~3; loy[l] = y0;
     lnch[l] = (x1 - lax[l] + 3) >> 2; lrows[l] = y1 - y0;
@@ -220,7 +220,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
     const int l = k & 1, comp = 1 + (k >> 1);
     cmode[k] = 0; cax[k] = coy[k] = crows[k] = cnch[k] = 0;
     if (!U.l[l].present) continue;
-    const DPlane &R = P.ref[U.l[l].slot][comp];
+    const DPlane &R = P.ref.get(U.l[l].slot, comp);
     const int x0 = cbox[l][0], x1 = cbox[l][1], y0 = cbox[l][2], y1 = cbox[l][3];
     cax[k] = x0 & ~3; coy[k] = y0;
     cnch[k] = (x1 - cax[k] + 3) >> 2; crows[k] = y1 - y0;
@@ -235,7 +235,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
 #pragma unroll
     for (int l = 0; l < 2; l++) {
       if (!U.l[l].present || lmode[l] != 0) continue;
-      const DPlane &R = P.ref[U.l[l].slot][0];
+      const DPlane &R = P.ref.get(U.l[l].slot, 0);
       const int lg = lnch[l] <= 8 ? 3 : 4, n = lrows[l] << lg;   // chunk slots per row: 8 or 16
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -246,7 +246,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       if (!U.l[k & 1].present || cmode[k] != 0) continue;
-      const DPlane &R = P.ref[U.l[k & 1].slot][1 + (k >> 1)];
+      const DPlane &R = P.ref.get(U.l[k & 1].slot, 1 + (k >> 1));
       const int n = crows[k] << 3;   // 8 chunk slots per row
       {
         const int i = lane, r = i >> 3, c = i & 7;
@@ -276,7 +276,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
 #pragma unroll
     for (int l = 0; l < 2; l++) {
       if (!U.l[l].present || lmode[l] == 0) continue;
-      const DPlane &R = P.ref[U.l[l].slot][0];
+      const DPlane &R = P.ref.get(U.l[l].slot, 0);
       for (int i0 = lane; i0 < nsb * LSBS; i0 += 8 * 128) {
         int16_t v[8];
 #pragma unroll
@@ -295,7 +295,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
     for (int k = 0; k < 4; k++) {
       const int l = k & 1;
       if (!U.l[l].present || cmode[k] == 0) continue;
-      const DPlane &R = P.ref[U.l[l].slot][1 + (k >> 1)];
+      const DPlane &R = P.ref.get(U.l[l].slot, 1 + (k >> 1));
       for (int i0 = lane; i0 < ncb * CSBS; i0 += 8 * 128) {
         int16_t v[8];
 #pragma unroll

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
       // this list's (w+5)x(h+5) search window (21 rows of pitch WS at most)
       constexpr int DIT = (21 * WS + 127) / 128;
       int16_t v[DIT] = {};
-      gather_regs<DIT, WS, 128>(P.ref[slotof(ll)][0], J.x + (mvof(ll, 0) >> 4) - 2, J.y + (mvof(ll, 1) >> 4) - 2, w + 5, h + 5,
+      gather_regs<DIT, WS, 128>(P.ref.get(slotof(ll), 0), J.x + (mvof(ll, 0) >> 4) - 2, J.y + (mvof(ll, 1) >> 4) - 2, w + 5, h + 5,
                                 none, li, v);
       regs_to_lds<DIT, 128>(fwin + ll * LWIN, 21 * WS, li, v);
     }
@@ -261,8 +261,8 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
     refined(cl, 1 + ccomp, cfx, cfy, cix, ciy, cc);
     constexpr int LIT = (LWIN + 127) / 128, CIT = (CWIN + 63) / 64;
     int16_t vl[LIT] = {}, vc[CIT] = {};
-    gather_regs<LIT, WS, 128>(P.ref[slotof(ll)][0], lix - 3, liy - 3, w + 7, h + 7, lc, li, vl);
-    gather_regs<CIT, CWS, 64>(P.ref[slotof(cl)][1 + ccomp], cix - 1, ciy - 1, (w >> 1) + 3, (h >> 1) + 3, cc, lane, vc);
+    gather_regs<LIT, WS, 128>(P.ref.get(slotof(ll), 0), lix - 3, liy - 3, w + 7, h + 7, lc, li, vl);
+    gather_regs<CIT, CWS, 64>(P.ref.get(slotof(cl), 1 + ccomp), cix - 1, ciy - 1, (w >> 1) + 3, (h >> 1) + 3, cc, lane, vc);
     regs_to_lds<LIT, 128>(fwin + ll * LWIN, LWIN, li, vl);
     regs_to_lds<CIT, 64>(fwin + 2 * LWIN + wave * CWIN, CWIN, lane, vc);
   }
