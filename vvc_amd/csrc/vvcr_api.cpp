@@ -697,11 +697,11 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       }
     if (ctx->intra_wg <= 0) {
       // k_intra takes CTUs in wavefront order: the CTUs in flight are those of a few anti-diagonals
-      // (x + 2y), so six diagonals' worth of workgroups keeps the wavefront busy (1080p, CTU 128: 48, as
-      // fast as one per CU; 4K: 90, 1 % faster than 60), and the other lanes' kernels get the CUs the
-      // idle workgroups held
+      // (x + 2y), so four diagonals' worth of workgroups keeps the wavefront busy (1080p, CTU 128: 32,
+      // as fast in isolation as one per CU), and the other lanes' kernels get the CUs the idle workgroups
+      // held: with five intra lanes in flight, 32 workgroups per launch 12.1 Gpx/s, 48 11.0
       const int ctu = 1 << sp->ctu_log2, wc = (sp->width + ctu - 1) / ctu, hc = (sp->height + ctu - 1) / ctu;
-      ctx->intra_wg = std::min(ctx->n_cu, 6 * std::min(hc, (wc + 1) / 2));
+      ctx->intra_wg = std::min(ctx->n_cu, 4 * std::min(hc, (wc + 1) / 2));
     }
     VVCR_CHECK_HIP(hipMalloc(&ctx->d_err, sizeof(int32_t)));
     VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof(int32_t)));
