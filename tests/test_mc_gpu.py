@@ -3,6 +3,8 @@
 Reference pictures are the reference decoder's own decoded pictures, so every picture is an
 independent check. Bit-exact."""
 import os
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -18,6 +20,23 @@ pytestmark = pytest.mark.gpu
 def test_mc_matches_reference(golden_dir, name):
     """Every inter CU (uni/bi/BCW, SbTMVP, GEO, affine+PROF, DMVR, BDOF; explicit weighted prediction in
     rawp416_q32) and the DMVR deltas."""
+    check_mc(golden_dir, name)
+
+
+@pytest.mark.parametrize("name", ["ra416_q32", "rawp416_q32"])
+def test_affine_global_fallback_matches_reference(golden_dir, name):
+    """k_mc_affine's path for sub-block windows whose union does not fit its LDS buffers (strongly
+    diverging affine MVs: windows read straight from the reference picture), forced on every affine tile
+    with VVCR_AFF_FALLBACK=1 (read once per process, hence the child process)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path[:0] = [%r, %r]; import test_mc_gpu as T; T.check_mc(%r, %r); print('ok')"
+            % (here, os.path.dirname(here), golden_dir, name))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, VVCR_AFF_FALLBACK="1"),
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def check_mc(golden_dir, name):
     d = os.path.join(golden_dir, name)
     pics = S.load_sequence(d)
     by_poc = {p["hdr"]["poc"]: p for p in pics}

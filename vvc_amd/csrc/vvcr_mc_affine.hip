@@ -8,15 +8,20 @@
 // Reference samples: the 11x11 windows of the sub-blocks overlap almost completely (neighbouring affine
 // sub-block MVs differ by a fraction of a sample), so per list the tile gathers the UNION of its
 // sub-block windows once — whole aligned 4-sample chunks, one 8-byte load per lane per chunk — and each
-// sub-block filters from its offset inside that union (a 16x16 tile: ~24x24 samples instead of
-// 16 x 121). A tile whose union does not fit the buffer (strongly diverging MVs) gathers every
-// sub-block window on its own (per-sample); one that reaches outside the picture gathers per sample
-// with clamped coordinates (= the reference's edge-extended margin, Picture::extendPicBorder).
+// sub-block filters from its offset inside that union (a 16x16 tile: ~24x28 samples instead of
+// 16 x 121). The union buffers are sized for the unions of ordinary affine motion (luma <= 32 x 25,
+// chroma <= 16 x 13 per list: every tile of the test streams fits) so that a 256-lane workgroup of two
+// tiles needs < 20 KB of LDS and eight fit a CU (the kernel is latency-bound: its time scales with
+// the workgroups per CU). A list whose union does not fit (strongly diverging MVs) reads its window
+// samples straight from the reference picture instead (per sample, clamped), in the H pass and PROF.
+// Chunks that reach outside the picture are loaded per sample with clamped coordinates (= the
+// reference's edge-extended margin, Picture::extendPicBorder).
 //
 // Filtering is the separable H-then-V form for every fraction (identity phase for zero fractions; see
 // vvcr_mc.hip), with packed int16 pairs and v_dot2c (vvcr_mcdev.h): lanes hold different sub-blocks, so
 // taps come from LDS tables indexed by each lane's fraction and the pair parity is per lane (fir4_var).
 #include "vvcr_internal.h"
+#include <cstdlib>
 #include "vvcr_tables.h"
 #include "vvcr_mcdev.h"
 
@@ -56,52 +61,77 @@ __device__ __forceinline__ void round_affine(int &x, int &y, int s) {   // round
 }
 
 // LDS geometry (int16 samples)
-constexpr int LUP = 48, LUR = 44, LWS = LUP * LUR;   // luma union window per list: 12 chunks x 44 rows
-constexpr int LSBP = 12, LSBS = 11 * LSBP;            // fallback: per sub-block 11 rows x 12
-constexpr int CUP = 32, CUR = 17, CWS = CUP * CUR;    // chroma union per (component, list): 8 chunks x 16 rows (+1 pad row)
-constexpr int CSBP = 8, CSBS = 7 * CSBP;              // fallback: per chroma sub-block 7 rows x 8
+constexpr int LUP = 32, LUR = 25, LWS = LUP * LUR;   // luma union window per list: 8 chunks x 25 rows
+constexpr int CUP = 16, CUR = 14, CWS = CUP * CUR;    // chroma union per (component, list): 4 chunks x 13 rows (+1 pad row)
 constexpr int HTC = 10, HTS = 4 * HTC;                // luma H outputs [sub-block][col][10 rows]
 constexpr int CTC = 8, CTS = 4 * CTC;                 // chroma H outputs [sub-block][col][8 rows]
-static_assert(16 * LSBS <= LWS && 4 * CSBS <= CWS, "fallback windows fit the union buffers");
+// after the H passes the chroma windows hold the chroma predictions [combo][y * 8 + x], then the luma
+// prediction per list [y * 16 + x]
+static_assert(4 * 64 + 2 * 256 <= 4 * CWS, "predictions fit the chroma window buffers");
 
-// Where the window of a sub-block lies in its list's buffer: element (r, e) of the window (row r, column
-// e, relative to the window's top-left tap) is buf[base + (ey + r) * pitch + ex + e].
+// Where the window of a sub-block lies in its list's union buffer: element (r, e) of the window (row r,
+// column e, relative to the window's top-left tap) is buf[(ey + r) * pitch + ex + e]; ox / oy: the window's
+// top-left tap in the reference picture (the global fallback reads there).
 struct Place {
-  int base, pitch, ex, ey;
+  int pitch, ex, ey, ox, oy;
 };
+
+// N sample pairs of row r of a sub-block window, from window element e0 on (pair k = elements e0 + 2k,
+// e0 + 2k + 1): aligned dwords of the union buffer, or (glob) per sample from the reference picture with
+// clamped coordinates
+template <int N>
+__device__ __forceinline__ void win_pairs(bool glob, const int16_t *buf, const Place &pl, const DPlane &R, int r, int e0, uint32_t (&w)[N]) {
+  if (!glob) {
+    const uint32_t *q = (const uint32_t *)(buf + (pl.ey + r) * pl.pitch + pl.ex + e0);
+#pragma unroll
+    for (int k = 0; k < N; k++) w[k] = q[k];
+  } else {
+    const int16_t *row = R.p + (size_t)clampi(pl.oy + r, 0, R.h - 1) * R.stride;
+#pragma unroll
+    for (int k = 0; k < N; k++)
+      w[k] = pk(row[clampi(pl.ox + e0 + 2 * k, 0, R.w - 1)], row[clampi(pl.ox + e0 + 2 * k + 1, 0, R.w - 1)]);
+  }
+}
+
 
 struct AffLds {
   alignas(16) int16_t lw[2][LWS];
   alignas(16) int16_t cw[4][CWS];       // combo k = 2 * (comp - 1) + list
   alignas(16) int16_t ht[2][16 * HTS];
   alignas(16) int16_t ct[4][4 * CTS];
-  alignas(16) uint32_t tl[16][8];
-  alignas(16) uint32_t tc[32][8];
   int sbmv[2][16][2];     // MC MV of each luma sub-block (clamped)
-  int stmv[2][16][2];     // stored MV (before the picture clamp) for chroma
   int csmv[2][4][2];      // chroma sub-block MVs
   int box[2][2][4];       // union boxes: [luma / chroma][list][x0 x1 y0 y1]
+};
+
+// packed tap tables of the workgroup (both jobs)
+struct AffTapLds {
+  alignas(16) uint32_t tl[16][8];
+  alignas(16) uint32_t tc[32][8];
 };
 
 // One job on 128 lanes (lane 0..127) with LDS L; the workgroup runs two jobs, so every __syncthreads
 // here is reached unconditionally (the same number of times by both).
 __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__restrict__ jobs, int njobs, const AffPu *__restrict__ pus,
-                                          int j, int lane, AffLds &L) {
+                                          int j, int lane, AffLds &L, AffTapLds &T, bool force_glob) {
   auto &s_lw = L.lw;
   auto &s_cw = L.cw;
   auto &s_ht = L.ht;
   auto &s_ct = L.ct;
-  auto &s_tl = L.tl;
-  auto &s_tc = L.tc;
+  auto &s_tl = T.tl;
+  auto &s_tc = T.tc;
   auto &s_sbmv = L.sbmv;
-  auto &s_stmv = L.stmv;
   auto &s_csmv = L.csmv;
   auto &s_box = L.box;
   // after the H passes the chroma windows are dead: chroma predictions [combo][y * 8 + x] and the luma
   // prediction per list [y * 16 + x] live there
   int16_t(*s_co)[64] = (int16_t(*)[64])s_cw[0];
-  int16_t(*s_lo)[256] = (int16_t(*)[256])s_cw[1];
+  int16_t(*s_lo)[256] = (int16_t(*)[256])(s_cw[0] + 4 * 64);
 
+  // packed tap tables (global, L2-resident) -> LDS, every lane of both jobs (the same values)
+  (&s_tl[0][0])[lane] = (&a_taps.l[0][0])[lane];
+#pragma unroll
+  for (int k = 0; k < 2; k++) (&s_tc[0][0])[lane + 128 * k] = (&a_taps.c[0][0])[lane + 128 * k];
   if (j >= njobs) return;
   const AffJob J = jobs[j];
   const AffPu U = pus[J.pu];
@@ -111,38 +141,46 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
   // per-list flags as scalars: a lane-indexed U.l[l] would copy the PU record to scratch
   const bool pres[2] = {U.l[0].present != 0, U.l[1].present != 0}, prof[2] = {U.l[0].prof != 0, U.l[1].prof != 0};
   auto PRES = [&](int l) { return l ? pres[1] : pres[0]; };
+  // reference planes of the lists as scalars (a lane-indexed slot would index the kernel arguments per
+  // lane); Cb and Cr share stride and size
+  const int slot0 = pres[0] ? U.l[0].slot : 0, slot1 = pres[1] ? U.l[1].slot : 0;
+  const DPlane RL0 = P.ref.get(slot0, 0), RL1 = P.ref.get(slot1, 0);
+  const DPlane RC00 = P.ref.get(slot0, 1), RC01 = P.ref.get(slot1, 1), RC10 = P.ref.get(slot0, 2), RC11 = P.ref.get(slot1, 2);
+  auto lref = [&](int l) { DPlane d = RL0; d.p = l ? RL1.p : RL0.p; return d; };
+  auto cref = [&](int k) { DPlane d = RC00; d.p = k == 0 ? RC00.p : k == 1 ? RC01.p : k == 2 ? RC10.p : RC11.p; return d; };
   const int w = J.w, h = J.h;           // 8 or 16 (affine PUs are >= 8x8, tiled by 16)
   const int lnsx = w == 16 ? 2 : 1, nsx = 1 << lnsx, nsb = (w >> 2) * (h >> 2);
   const int cw = w >> 1, chh = h >> 1, ncx = cw >> 2, ncb = (cw >> 2) * (chh >> 2);
   const int sh1 = IF_FILTER_PREC - headRoom, off1 = -(IF_INTERNAL_OFFS << sh1);
 
-  // packed tap tables (global, L2-resident) -> LDS
-  (&s_tl[0][0])[lane] = (&a_taps.l[0][0])[lane];
-#pragma unroll
-  for (int k = 0; k < 2; k++) (&s_tc[0][0])[lane + 128 * k] = (&a_taps.c[0][0])[lane + 128 * k];
-
-  // ---- sub-block MVs of both lists (:1102-1140); MV clamp of xPredAffineBlk (:936-939), relative to the PU
+  // ---- sub-block MVs of both lists (:1102-1140); MV clamp of xPredAffineBlk (:936-939), relative to the PU.
+  // One phase: lanes 0..31 the luma sub-blocks (list = lane / 16), lanes 32..39 the chroma sub-blocks
+  // (list = (lane - 32) / 4), each chroma lane deriving the two luma sub-block MVs it averages itself.
   const int iHorMax = (P.pic_w + 8 - U.x - 1) << 4, iHorMin = (-P.ctu - 8 - U.x + 1) << 4;
   const int iVerMax = (P.pic_h + 8 - U.y - 1) << 4, iVerMin = (-P.ctu - 8 - U.y + 1) << 4;
   const int MVLIM = (1 << 17) - 1;
+  // stored (unclamped to the picture) MV of luma sub-block sb
+  auto stored_mv = [&](const AffList &A, int sb, int &mx, int &my) {
+    const int sw = (J.x - U.x) + (sb & (nsx - 1)) * 4, shh = (J.y - U.y) + (sb >> lnsx) * 4;
+    if (!A.spread) {
+      mx = A.mvx + A.dhx * (2 + sw) + A.dvx * (2 + shh);
+      my = A.mvy + A.dhy * (2 + sw) + A.dvy * (2 + shh);
+    } else {
+      mx = A.mvx + A.dhx * (U.w >> 1) + A.dvx * (U.h >> 1);
+      my = A.mvy + A.dhy * (U.w >> 1) + A.dvy * (U.h >> 1);
+    }
+    round_affine(mx, my, 7);
+    mx = clampi(mx, -MVLIM - 1, MVLIM);
+    my = clampi(my, -MVLIM - 1, MVLIM);
+  };
   int bx0 = 1 << 30, bx1 = -(1 << 30), by0 = 1 << 30, by1 = -(1 << 30);   // window box of this lane's sub-block
+  int cx0 = 1 << 30, cx1 = -(1 << 30), cy0 = 1 << 30, cy1 = -(1 << 30);
   if (lane < 32) {
     const int l = lane >> 4, sb = lane & 15;
     const AffList &A = pus[J.pu].l[l];      // lane-dependent list: read from global (a local copy would go to scratch)
     if (A.present && sb < nsb) {
-      const int sw = (J.x - U.x) + (sb & (nsx - 1)) * 4, shh = (J.y - U.y) + (sb >> lnsx) * 4;
       int mx, my;
-      if (!A.spread) {
-        mx = A.mvx + A.dhx * (2 + sw) + A.dvx * (2 + shh);
-        my = A.mvy + A.dhy * (2 + sw) + A.dvy * (2 + shh);
-      } else {
-        mx = A.mvx + A.dhx * (U.w >> 1) + A.dvx * (U.h >> 1);
-        my = A.mvy + A.dhy * (U.w >> 1) + A.dvy * (U.h >> 1);
-      }
-      round_affine(mx, my, 7);
-      mx = clampi(mx, -MVLIM - 1, MVLIM);
-      my = clampi(my, -MVLIM - 1, MVLIM);
-      s_stmv[l][sb][0] = mx; s_stmv[l][sb][1] = my;
+      stored_mv(A, sb, mx, my);
       const int cmx = clampi(mx, iHorMin, iHorMax), cmy = clampi(my, iVerMin, iVerMax);
       s_sbmv[l][sb][0] = cmx;
       s_sbmv[l][sb][1] = cmy;
@@ -151,26 +189,15 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
       bx1 = bx0 + 11;
       by1 = by0 + 11;
     }
-  }
-  // union box per list: min / max over the 16 lanes of the list (xor shuffles stay inside the group)
-#pragma unroll
-  for (int m = 8; m >= 1; m >>= 1) {
-    bx0 = min(bx0, __shfl_xor(bx0, m)); bx1 = max(bx1, __shfl_xor(bx1, m));
-    by0 = min(by0, __shfl_xor(by0, m)); by1 = max(by1, __shfl_xor(by1, m));
-  }
-  if (lane == 0 || lane == 16) {   // wave 0 holds the MV lanes; the box reaches the other wave through LDS
-    s_box[0][lane >> 4][0] = bx0; s_box[0][lane >> 4][1] = bx1;
-    s_box[0][lane >> 4][2] = by0; s_box[0][lane >> 4][3] = by1;
-  }
-  __syncthreads();
-  // chroma: 4x4 sub-blocks, MV = mean of two luma sub-block MVs (:1142-1160)
-  int cx0 = 1 << 30, cx1 = -(1 << 30), cy0 = 1 << 30, cy1 = -(1 << 30);
-  if (lane < 8) {
-    const int l = lane >> 2, cb = lane & 3;
-    if (pus[J.pu].l[l].present && cb < ncb) {
+  } else if (lane < 40) {   // chroma: 4x4 sub-blocks, MV = mean of two luma sub-block MVs (:1142-1160)
+    const int l = (lane >> 2) & 1, cb = lane & 3;
+    const AffList &A = pus[J.pu].l[l];
+    if (A.present && cb < ncb) {
       const int cxs = (cb % ncx) * 2, cys = (cb / ncx) * 2;   // luma sub-block indices in the tile
-      const int a = cys * nsx + cxs, b = (cys + 1) * nsx + cxs + 1;
-      int mx = s_stmv[l][a][0] + s_stmv[l][b][0], my = s_stmv[l][a][1] + s_stmv[l][b][1];
+      int ax, ay, bx, by;
+      stored_mv(A, cys * nsx + cxs, ax, ay);
+      stored_mv(A, (cys + 1) * nsx + cxs + 1, bx, by);
+      int mx = ax + bx, my = ay + by;
       round_affine(mx, my, 1);
       const int cmx = clampi(mx, iHorMin, iHorMax), cmy = clampi(my, iVerMin, iVerMax);
       s_csmv[l][cb][0] = cmx;
@@ -181,14 +208,25 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
       cy1 = cy0 + 7;
     }
   }
+  // union boxes: min / max over the 16 luma lanes / 4 chroma lanes of a list (xor shuffles stay inside
+  // the group; lanes outside a group hold the neutral values)
+#pragma unroll
+  for (int m = 8; m >= 1; m >>= 1) {
+    bx0 = min(bx0, __shfl_xor(bx0, m)); bx1 = max(bx1, __shfl_xor(bx1, m));
+    by0 = min(by0, __shfl_xor(by0, m)); by1 = max(by1, __shfl_xor(by1, m));
+  }
 #pragma unroll
   for (int m = 2; m >= 1; m >>= 1) {
     cx0 = min(cx0, __shfl_xor(cx0, m)); cx1 = max(cx1, __shfl_xor(cx1, m));
     cy0 = min(cy0, __shfl_xor(cy0, m)); cy1 = max(cy1, __shfl_xor(cy1, m));
   }
-  if (lane == 0 || lane == 4) {   // chroma union box per list (Cb and Cr share the MVs and the plane size)
-    s_box[1][lane >> 2][0] = cx0; s_box[1][lane >> 2][1] = cx1;
-    s_box[1][lane >> 2][2] = cy0; s_box[1][lane >> 2][3] = cy1;
+  if (lane == 0 || lane == 16) {   // wave 0 holds the MV lanes; the boxes reach the other wave through LDS
+    s_box[0][lane >> 4][0] = bx0; s_box[0][lane >> 4][1] = bx1;
+    s_box[0][lane >> 4][2] = by0; s_box[0][lane >> 4][3] = by1;
+  }
+  if (lane == 32 || lane == 36) {   // chroma union box per list (Cb and Cr share the MVs and the plane size)
+    s_box[1][(lane >> 2) & 1][0] = cx0; s_box[1][(lane >> 2) & 1][1] = cx1;
+    s_box[1][(lane >> 2) & 1][2] = cy0; s_box[1][(lane >> 2) & 1][3] = cy1;
   }
   __syncthreads();
   int ubox[2][4], cbox[2][4];
@@ -202,7 +240,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
 
   // ---- window buffers. Per list (luma) and per (component, list) (chroma): the union box of the
   // sub-block windows (reduced above), its aligned origin, and the mode.
-  int lax[2], loy[2], lrows[2], lnch[2], lmode[2];   // mode: 0 union box, 2 per sub-block
+  int lax[2], loy[2], lrows[2], lnch[2], lmode[2];   // mode: 0 union box in LDS, 2 global reads
   int cax[4], coy[4], crows[4], cnch[4], cmode[4];
 #pragma unroll
   for (int l = 0; l < 2; l++) {
@@ -212,7 +250,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
     const int x0 = ubox[l][0], x1 = ubox[l][1], y0 = ubox[l][2], y1 = ubox[l][3];
     lax[l] = x0 & ~3; loy[l] = y0;
     lnch[l] = (x1 - lax[l] + 3) >> 2; lrows[l] = y1 - y0;
-    if (lnch[l] * 4 > LUP || lrows[l] > LUR || lrows[l] * (lnch[l] <= 8 ? 8 : 16) > 8 * 64) lmode[l] = 2;
+    if (lnch[l] * 4 > LUP || lrows[l] > LUR || force_glob) lmode[l] = 2;
     (void)R;
   }
 #pragma unroll
@@ -224,22 +262,22 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
     const int x0 = cbox[l][0], x1 = cbox[l][1], y0 = cbox[l][2], y1 = cbox[l][3];
     cax[k] = x0 & ~3; coy[k] = y0;
     cnch[k] = (x1 - cax[k] + 3) >> 2; crows[k] = y1 - y0;
-    if (cnch[k] > 8 || crows[k] > 16) cmode[k] = 2;
+    if (cnch[k] * 4 > CUP || crows[k] > CUR - 1 || force_glob) cmode[k] = 2;
     (void)R;
   }
 
   // ---- gather: union boxes in 4-sample chunks (all in flight before the LDS writes; rows clamped to the
-  // picture, edge chunks per sample: chunk4), per-sub-block windows per sample in batches of 8
+  // picture, edge chunks per sample: chunk4)
   {
-    uint2 vl[2][4], vc[4];
+    uint2 vl[2][2], vc[4];
 #pragma unroll
     for (int l = 0; l < 2; l++) {
       if (!U.l[l].present || lmode[l] != 0) continue;
       const DPlane &R = P.ref.get(U.l[l].slot, 0);
-      const int lg = lnch[l] <= 8 ? 3 : 4, n = lrows[l] << lg;   // chunk slots per row: 8 or 16
+      const int n = lrows[l] << 3;   // 8 chunk slots per row
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int i = lane + 128 * k, r = i >> lg, c = i & ((1 << lg) - 1);
+      for (int k = 0; k < 2; k++) {
+        const int i = lane + 128 * k, r = i >> 3, c = i & 7;
         if (i < n && c < lnch[l]) vl[l][k] = chunk4(R.p, R.stride, R.w, R.h, loy[l] + r, lax[l] + 4 * c);
       }
     }
@@ -247,85 +285,50 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
     for (int k = 0; k < 4; k++) {
       if (!U.l[k & 1].present || cmode[k] != 0) continue;
       const DPlane &R = P.ref.get(U.l[k & 1].slot, 1 + (k >> 1));
-      const int n = crows[k] << 3;   // 8 chunk slots per row
+      const int n = crows[k] << 2;   // 4 chunk slots per row
       {
-        const int i = lane, r = i >> 3, c = i & 7;
+        const int i = lane, r = i >> 2, c = i & 3;
         if (i < n && c < cnch[k]) vc[k] = chunk4(R.p, R.stride, R.w, R.h, coy[k] + r, cax[k] + 4 * c);
       }
     }
 #pragma unroll
     for (int l = 0; l < 2; l++) {
       if (!U.l[l].present || lmode[l] != 0) continue;
-      const int lg = lnch[l] <= 8 ? 3 : 4, n = lrows[l] << lg;
+      const int n = lrows[l] << 3;
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const int i = lane + 128 * k, r = i >> lg, c = i & ((1 << lg) - 1);
+      for (int k = 0; k < 2; k++) {
+        const int i = lane + 128 * k, r = i >> 3, c = i & 7;
         if (i < n && c < lnch[l]) *(uint2 *)&s_lw[l][r * LUP + 4 * c] = vl[l][k];
       }
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       if (!U.l[k & 1].present || cmode[k] != 0) continue;
-      const int n = crows[k] << 3;
+      const int n = crows[k] << 2;
       {
-        const int i = lane, r = i >> 3, c = i & 7;
+        const int i = lane, r = i >> 2, c = i & 3;
         if (i < n && c < cnch[k]) *(uint2 *)&s_cw[k][r * CUP + 4 * c] = vc[k];
-      }
-    }
-    // per-sub-block windows
-#pragma unroll
-    for (int l = 0; l < 2; l++) {
-      if (!U.l[l].present || lmode[l] == 0) continue;
-      const DPlane &R = P.ref.get(U.l[l].slot, 0);
-      for (int i0 = lane; i0 < nsb * LSBS; i0 += 8 * 128) {
-        int16_t v[8];
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-          const int i = min(i0 + 128 * b, nsb * LSBS - 1);
-          const int sb = i / LSBS, rem = i - sb * LSBS, r = rem / LSBP, e = rem - r * LSBP;
-          const int ox = J.x + (sb & (nsx - 1)) * 4 + (s_sbmv[l][sb][0] >> 4) - 3, oy = J.y + (sb >> lnsx) * 4 + (s_sbmv[l][sb][1] >> 4) - 3;
-          v[b] = R.p[(size_t)clampi(oy + r, 0, R.h - 1) * R.stride + clampi(ox + e, 0, R.w - 1)];
-        }
-#pragma unroll
-        for (int b = 0; b < 8; b++)
-          if (i0 + 128 * b < nsb * LSBS) s_lw[l][i0 + 128 * b] = v[b];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int l = k & 1;
-      if (!U.l[l].present || cmode[k] == 0) continue;
-      const DPlane &R = P.ref.get(U.l[l].slot, 1 + (k >> 1));
-      for (int i0 = lane; i0 < ncb * CSBS; i0 += 8 * 128) {
-        int16_t v[8];
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-          const int i = min(i0 + 128 * b, ncb * CSBS - 1);
-          const int cb = i / CSBS, rem = i - cb * CSBS, r = rem / CSBP, e = rem - r * CSBP;
-          const int ox = (J.x >> 1) + (cb % ncx) * 4 + (s_csmv[l][cb][0] >> 5) - 1, oy = (J.y >> 1) + (cb / ncx) * 4 + (s_csmv[l][cb][1] >> 5) - 1;
-          v[b] = R.p[(size_t)clampi(oy + r, 0, R.h - 1) * R.stride + clampi(ox + e, 0, R.w - 1)];
-        }
-#pragma unroll
-        for (int b = 0; b < 8; b++)
-          if (i0 + 128 * b < ncb * CSBS) s_cw[k][i0 + 128 * b] = v[b];
       }
     }
   }
   __syncthreads();
 
   // placement of a luma sub-block window of list l / a chroma sub-block window of combo k
+  // (a list read from the reference picture gets ex = ey = 0: the parity logic below then starts its
+  // dword pairs on the window's own columns)
+  auto lglob = [&](int l) { return (l ? lmode[1] : lmode[0]) == 2; };
   auto lplace = [&](int l, int sb) -> Place {
-    const int lm = l ? lmode[1] : lmode[0];
-    if (lm == 2) return Place{sb * LSBS, LSBP, 0, 0};
     const int ox = J.x + (sb & (nsx - 1)) * 4 + (s_sbmv[l][sb][0] >> 4) - 3, oy = J.y + (sb >> lnsx) * 4 + (s_sbmv[l][sb][1] >> 4) - 3;
-    return Place{0, LUP, ox - (l ? lax[1] : lax[0]), oy - (l ? loy[1] : loy[0])};
+    if (lglob(l)) return Place{0, 0, 0, ox, oy};
+    return Place{LUP, ox - (l ? lax[1] : lax[0]), oy - (l ? loy[1] : loy[0]), ox, oy};
   };
   auto csel = [&](const int (&a)[4], int k) { return k == 0 ? a[0] : k == 1 ? a[1] : k == 2 ? a[2] : a[3]; };
+  auto cglob = [&](int k) { return csel(cmode, k) == 2; };
   auto cplace = [&](int k, int cb) -> Place {
     const int l = k & 1;
-    if (csel(cmode, k) == 2) return Place{cb * CSBS, CSBP, 0, 0};
     const int ox = (J.x >> 1) + (cb % ncx) * 4 + (s_csmv[l][cb][0] >> 5) - 1, oy = (J.y >> 1) + (cb / ncx) * 4 + (s_csmv[l][cb][1] >> 5) - 1;
-    return Place{0, CUP, ox - csel(cax, k), oy - csel(coy, k)};
+    if (cglob(k)) return Place{0, 0, 0, ox, oy};
+    return Place{CUP, ox - csel(cax, k), oy - csel(coy, k), ox, oy};
   };
 
   // ---- H passes. Luma items (list, sub-block, row pair): window rows 1..10 (the V taps read 1..9), the
@@ -340,10 +343,10 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
       const int sb = rem / 5, rp = rem - sb * 5;
       const Place pl = lplace(l, sb);
       const int b = pl.ex + 1, par = b & 1;
-      const uint32_t *r0 = (const uint32_t *)(s_lw[l] + pl.base + (pl.ey + 1 + 2 * rp) * pl.pitch) + ((b - par) >> 1);
+      const DPlane R = lref(l);   // lane-dependent list: only the fallback reads it
       uint32_t w0[5], w1[5];
-#pragma unroll
-      for (int k = 0; k < 5; k++) { w0[k] = r0[k]; w1[k] = r0[pl.pitch / 2 + k]; }
+      win_pairs<5>(lglob(l), s_lw[l], pl, R, 1 + 2 * rp, 1 - par, w0);
+      win_pairs<5>(lglob(l), s_lw[l], pl, R, 2 + 2 * rp, 1 - par, w1);
       const uint32_t *tp = s_tl[s_sbmv[l][sb][0] & 15];
       Taps<6> t;
 #pragma unroll
@@ -363,10 +366,10 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
     if (PRES(l) && cb < ncb) {
       const Place pl = cplace(k, cb);
       const int b = pl.ex, par = b & 1;
-      const uint32_t *r0 = (const uint32_t *)(s_cw[k] + pl.base + (pl.ey + 2 * rp) * pl.pitch) + ((b - par) >> 1);
+      const DPlane R = cref(k);
       uint32_t w0[4], w1[4];
-#pragma unroll
-      for (int m = 0; m < 4; m++) { w0[m] = r0[m]; w1[m] = r0[pl.pitch / 2 + m]; }
+      win_pairs<4>(cglob(k), s_cw[k], pl, R, 2 * rp, -par, w0);
+      win_pairs<4>(cglob(k), s_cw[k], pl, R, 2 * rp + 1, -par, w1);
       const uint32_t *tp = s_tc[s_csmv[l][cb][0] & 31];
       Taps<4> t;
       t.A[0] = tp[0]; t.A[1] = tp[1]; t.B[0] = tp[2]; t.B[1] = tp[3]; t.B[2] = tp[4];
@@ -455,9 +458,15 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
       const int sb = (y >> 2) * nsx + (x0 >> 2);
       const int xo = (s_sbmv[l][sb][0] & 15) >> 3, yo = (s_sbmv[l][sb][1] & 15) >> 3;
       const Place pl = lplace(l, sb);
-      const int16_t *swin = s_lw[l] + pl.base + (pl.ey + 3 + yo) * pl.pitch + pl.ex + 3 + xo;   // ring origin
+      const int16_t *swin = s_lw[l] + (pl.ey + 3 + yo) * pl.pitch + pl.ex + 3 + xo;   // ring origin
+      const DPlane R = lref(l);
+      const bool glob = lglob(l);
       const int py = y & 3;
-      auto ring = [&](int ex, int ey) -> int { return (int16_t)((swin[ey * pl.pitch + ex] << headRoom) - IF_INTERNAL_OFFS); };
+      auto ring = [&](int ex, int ey) -> int {
+        const int v = glob ? R.p[(size_t)clampi(pl.oy + 3 + yo + ey, 0, R.h - 1) * R.stride + clampi(pl.ox + 3 + xo + ex, 0, R.w - 1)]
+                           : swin[ey * pl.pitch + ex];
+        return (int16_t)((v << headRoom) - IF_INTERNAL_OFFS);
+      };
       const uint2 cr = *(const uint2 *)&s_lo[l][y * 16 + x0];
       const uint2 ur = *(const uint2 *)&s_lo[l][max(y - 1, 0) * 16 + x0];
       const uint2 dr = *(const uint2 *)&s_lo[l][min(y + 1, 15) * 16 + x0];
@@ -530,15 +539,19 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
   }
 }
 
-__global__ __launch_bounds__(256) void k_mc_affine(McParams P, const AffJob *__restrict__ jobs, int njobs, const AffPu *__restrict__ pus) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_mc_affine(McParams P, const AffJob *__restrict__ jobs, int njobs, const AffPu *__restrict__ pus, int force_glob) {
   __shared__ AffLds lds[2];
+  __shared__ AffTapLds taps;
   const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
-  mc_affine(P, jobs, njobs, pus, 2 * blockIdx.x + half, threadIdx.x & 127, lds[half]);
+  mc_affine(P, jobs, njobs, pus, 2 * blockIdx.x + half, threadIdx.x & 127, lds[half], taps, force_glob != 0);
 }
 
 }  // namespace
 
 void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const AffPu *pus, hipStream_t s) {
   if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_mc_affine, dim3((njobs + 1) / 2), dim3(256), 0, s, p, jobs, njobs, pus);
+  // VVCR_AFF_FALLBACK=1 (tests): every list reads its windows from the reference picture, the path of
+  // unions that do not fit the LDS buffers
+  static const int force = [] { const char *e = getenv("VVCR_AFF_FALLBACK"); return e && e[0] == '1' ? 1 : 0; }();
+  hipLaunchKernelGGL(k_mc_affine, dim3((njobs + 1) / 2), dim3(256), 0, s, p, jobs, njobs, pus, force);
 }
