@@ -61,7 +61,7 @@ __device__ __forceinline__ void round_affine(int &x, int &y, int s) {   // round
 }
 
 // LDS geometry (int16 samples)
-constexpr int LUP = 32, LUR = 25, LWS = LUP * LUR;   // luma union window per list: 8 chunks x 25 rows
+constexpr int LUP = 36, LUR = 25, LWS = LUP * LUR;   // luma union window per list: 8 chunks x 25 rows, pitch 18 dwords (H-pass reads of neighbouring row pairs and sub-blocks in different banks)
 constexpr int CUP = 16, CUR = 14, CWS = CUP * CUR;    // chroma union per (component, list): 4 chunks x 13 rows (+1 pad row)
 constexpr int HTC = 10, HTS = 4 * HTC;                // luma H outputs [sub-block][col][10 rows]
 constexpr int CTC = 8, CTS = 4 * CTC;                 // chroma H outputs [sub-block][col][8 rows]
@@ -250,7 +250,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
     const int x0 = ubox[l][0], x1 = ubox[l][1], y0 = ubox[l][2], y1 = ubox[l][3];
     lax[l] = x0 & ~3; loy[l] = y0;
     lnch[l] = (x1 - lax[l] + 3) >> 2; lrows[l] = y1 - y0;
-    if (lnch[l] * 4 > LUP || lrows[l] > LUR || force_glob) lmode[l] = 2;
+    if (lnch[l] > 8 || lrows[l] > LUR || force_glob) lmode[l] = 2;   // 8 chunk slots per row
     (void)R;
   }
 #pragma unroll
