@@ -195,6 +195,12 @@ struct Planner {
     if (ciip) return 1;
     if (!cuQ.yvalid) return tmp;
     if (marker != 0 && marker != 3) return tmp;
+    return motion_bs(dir, lx, ly, tmp);
+  }
+
+  // the motion part of xGetBoundaryStrengthSingle (LoopFilter.cpp:748-812) for luma position (lx, ly) of an
+  // inter Q block and its P neighbour, on top of the transform part tmp
+  int motion_bs(int dir, int lx, int ly, int tmp) const {
     const int lpx = dir == VER ? lx - 1 : lx, lpy = dir == VER ? ly : ly - 1;
     const vvcr_motion &mq = d.motion[(size_t)(ly >> 2) * W4 + (lx >> 2)];
     const vvcr_motion &mp = d.motion[(size_t)(lpy >> 2) * W4 + (lpx >> 2)];
@@ -348,10 +354,15 @@ struct Planner {
         if (pu.w > 0) len_subblocks(dir, pu, pa[2], pa[3]);
       }
     }
+    // An edge inside an inter, non-CIIP luma CU that is not a transform edge (sub-block edges of affine /
+    // SbTMVP CUs: most of the edges of a B picture) has only the motion part of the boundary strength.
+    const bool fast = cu.yvalid && cu.predmode != MODE_INTRA && !d.pu[cu.firstpu].ciip;
     for (int y = 0; y < a[3]; y += 4)
       for (int x = 0; x < a[2]; x += 4) {
         const int r = raster(a[0] + x, a[1] + y);
-        if (edge[dir][r]) bs[dir][r] = (uint8_t)boundary_strength(cui, dir, a[0] + x, a[1] + y);
+        if (!edge[dir][r]) continue;
+        if (fast && bs[dir][r] == 0 && (dir == VER ? x : y) > 0) bs[dir][r] = (uint8_t)motion_bs(dir, a[0] + x, a[1] + y, 0);
+        else bs[dir][r] = (uint8_t)boundary_strength(cui, dir, a[0] + x, a[1] + y);
       }
     std::sort(edges, edges + ne);
     int prev = -1;
