@@ -322,8 +322,14 @@ def main():
     per_launch_bytes = dalg / max(dl, 1)
     per_launch_s = dms / 1e3 / max(dl, 1)
     achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-    mc = kern.get("mc", [0, 0.0, 0.0])
-    mc_gbs = mc[2] / (mc[1] / 1e3) / 1e9 if mc[1] > 0 else 0.0
+    # the north-star's MC-interpolation kernels (plain and affine): algorithmic bytes / HIP-event time
+    mc_roof = {"peak": PEAK_HBM_GBS, "unit": "GB/s",
+               "note": "MC interpolation kernels on this workload (one segment in flight); "
+                       "4K figures: profiles/r02_mc_kernels.json"}
+    for k in ("mc", "mc_affine"):
+        v = kern.get(k, [0, 0.0, 0.0])
+        g = v[2] / (v[1] / 1e3) / 1e9 if v[1] > 0 else 0.0
+        mc_roof[k] = {"achieved": round(g, 2), "frac": round(g / PEAK_HBM_GBS, 4), "us_per_launch": round(v[1] / max(v[0], 1) * 1e3, 2)}
 
     traffic = None
     tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_traffic.json")))   # the newest round's
@@ -361,7 +367,7 @@ def main():
         "serial": {"value": round(V.job_throughput(px_seq * a.steps, elapsed_serial, R) / 1e6, 2),
                    "ms_per_step": round(elapsed_serial / a.steps * 1e3, 3),
                    "note": "one segment in flight (sync after every step)"},
-        "mc_kernel_GBps": round(mc_gbs, 2),
+        "mc_roofline": mc_roof,
         "host_prepare_s": round(t_prep, 3),
         "value_scope": "GPU reconstruction + loop filters of pre-planned pictures (descriptors and work lists resident "
                        "in HBM); host planning and CABAC parsing excluded - see end_to_end",
