@@ -323,8 +323,7 @@ struct Planner {
       int ta[4];
       if (cu.yvalid) { const int32_t *b = d.tu[t].b[0]; ta[0] = b[BX]; ta[1] = b[BY]; ta[2] = b[BW]; ta[3] = b[BH]; }
       else std::memcpy(ta, a, sizeof ta);
-      set_edges(VER, ta[0], ta[1], ta[2], ta[3], internal, false);
-      set_edges(HOR, ta[0], ta[1], ta[2], ta[3], internal, false);
+      set_edges(dir, ta[0], ta[1], ta[2], ta[3], internal, false);   // the other direction's pass sets its own
       len_from_tu(dir, cu, t);
       const int32_t *tb = d.tu[t].b[ch];
       edges[ne++] = dir == HOR ? (tb[BY] - cpy) / 4 : (tb[BX] - cpx) / 4;
@@ -336,8 +335,8 @@ struct Planner {
       else std::memcpy(pa, a, sizeof pa);
       const int pux = ch ? pu.cx : pu.x, puy = ch ? pu.cy : pu.y;
       const bool xoff = pux != cpx, yoff = puy != cpy;
-      set_edges(VER, pa[0], pa[1], pa[2], pa[3], xoff ? internal : left, xoff);
-      set_edges(HOR, pa[0], pa[1], pa[2], pa[3], yoff ? internal : top, yoff);
+      if (dir == VER) set_edges(VER, pa[0], pa[1], pa[2], pa[3], xoff ? internal : left, xoff);
+      else set_edges(HOR, pa[0], pa[1], pa[2], pa[3], yoff ? internal : top, yoff);
       edges[ne++] = dir == HOR ? (puy - cpy) / 4 : (pux - cpx) / 4;
       if ((pu.merge && pu.mrgtype == MRG_TYPE_SUBPU_ATMVP) || cu.affine) {
         if (dir == HOR) {
