@@ -16,14 +16,15 @@ timing barrier and max-over-ranks use torch.distributed.
 """
 import os
 
-# Execution lanes (libvvcr reads VVCR_LANES / VVCR_INTRA_LANES at vvcr_create): 5 intra lanes + 5 B lanes,
-# each on its own hardware queue, so that five intra-started segments and the B pictures of five others
-# overlap; HIP's default is 4 hardware queues per process, so the bench asks for 12 (10 lanes + the copy
-# stream) before the runtime starts. Measured on 1080p with 12 segments in flight: 7 lanes (3 intra) 8.8,
-# 8 (4) 11.5, 10 (5) 12.1, 10 (6) 10.0, 12 (6) 9.7 Gpx/s.
+# Execution lanes (libvvcr reads VVCR_LANES / VVCR_INTRA_LANES at vvcr_create): 5 intra lanes + 3 B lanes,
+# each on its own hardware queue, so that five intra-started segments and the B pictures of three others
+# overlap; HIP's default is 4 hardware queues per process, so the bench asks for 12 before the runtime
+# starts. Measured on 1080p with 12 segments in flight (lanes (intra lanes)): 8 (4) 11.5, 8 (5) 12.2,
+# 9 (5) 12.3, 10 (5) 11.5, 10 (4) 10.8, 12 (6) 12.0 Gpx/s. (Until late r02 the library clamped VVCR_LANES
+# to 8: the "10 lanes" of earlier r02 lines were 8.)
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 12:   # the box exports HIP's default of 4
     os.environ["GPU_MAX_HW_QUEUES"] = "12"
-os.environ.setdefault("VVCR_LANES", "10")
+os.environ.setdefault("VVCR_LANES", "8")
 os.environ.setdefault("VVCR_INTRA_LANES", "5")
 
 import argparse

@@ -182,7 +182,7 @@ static int rd_kind(int w, int h, int &tw, int &th) {
 // the last writer of each reference slot (RAW), and the last writer and every reader since of its own
 // slot (WAW / WAR) — so pictures that do not reference each other (the pictures of one temporal layer of
 // an RA GOP, an intra picture and the B pictures decoded before it) reconstruct concurrently.
-constexpr int MAXLANE = 8;
+constexpr int MAXLANE = 16;
 struct Lane {
   hipStream_t s = nullptr;
   DPlane pred[3], resi[3], tmp[3];
