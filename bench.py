@@ -209,8 +209,17 @@ def main():
     # (its intra picture references nothing, so it may start while step k's B pictures still run —
     # the library orders pictures only by their DPB-slot dependencies). --segments 1 serialises steps.
     per = min(12, 64 // a.segments)   # DPB slots per copy (64 in all)
+    # k_intra workgroups of this context (VVCR_INTRA_WG, read at vvcr_create): the library's default sizes
+    # one intra picture at a time (four wavefront diagonals' worth: 32 at 1080p, 60 at 4K); with five intra
+    # pictures in flight 32 each is better (4K 7.6 -> 8.6 Gpx/s, 1080p unchanged). The 8K shard pass, one
+    # picture at a time, keeps the default (32 there: 5.4 -> 4.4 Gpx/s).
+    wg_env = os.environ.get("VVCR_INTRA_WG")
+    if wg_env is None:
+        os.environ["VVCR_INTRA_WG"] = "32"
     dec = D.Decoder(pics, dpb_slots=per * a.segments,
                     device=int(os.environ.get("VVCR_DEVICE", local)))   # VVCR_DEVICE: rehearsal of N ranks on one GPU
+    if wg_env is None:
+        del os.environ["VVCR_INTRA_WG"]
     ctx = dec.ctx
     copies = []
     t_prep = time.perf_counter()
