@@ -1,0 +1,80 @@
+"""Diagnostics: per-workgroup start / end timestamps of k_mc (VVCR_MC_PROF build) on a stream's B pictures.
+
+  python tools/mc_prof.py build               # here: builds vvc_amd/libvvcr_mcprof.so
+  python tools/mc_prof.py run [stream]        # GPU box: one k_mc launch per B picture, prints the duration
+                                              # distribution and the slowest workgroups' first jobs
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF_LIB = os.path.join(ROOT, "vvc_amd", "libvvcr_mcprof.so")   # vvc_amd/ travels to the GPU box, build/ does not
+
+
+def build():
+    sys.path.insert(0, ROOT)
+    from vvc_amd import build as B
+    B.build_lib(extra=["-DVVCR_MC_PROF"], obj_dir=os.path.join(ROOT, "build", "mcprof", "obj"), lib=PROF_LIB)
+
+
+def run(stream):
+    os.environ["VVCR_LIB"] = PROF_LIB
+    sys.path.insert(0, ROOT)
+    import ctypes as C
+    import numpy as np
+    from vvc_amd import native as N, stream as S
+    L = N.lib()
+    L.vvcr_mc_prof_read.argtypes = [C.c_void_p, C.c_int]
+    pics = S.load_sequence(os.path.join(ROOT, "tests", "golden", stream))
+    h0 = pics[0]["hdr"]
+    ctx = N.Context(h0["width"], h0["height"], dpb_slots=16)
+    alloc = S.SlotAllocator(pics, 16)
+    prev_end = 0
+    for i, p in enumerate(pics):
+        slot = alloc.assign(i, p["hdr"]["poc"])
+        if p["hdr"]["slice_type"] == 2:
+            continue
+        ctx.begin_picture(S.pic_params(p, slot, alloc.slot_of))
+        S.submit(ctx, p)
+        h = ctx.prepare(N.STAGE_INTER)
+        buf = np.zeros((1 << 16, 4), np.uint64)
+        for rep in range(3):
+            ctx.launch(h)
+            ctx.sync()
+            if rep < 2:   # only the last launch's stamps count: start after the previous ones
+                L.vvcr_mc_prof_read(buf.ctypes.data, buf.shape[0])
+                m = buf[:, 1].max()
+                prev_end = max(prev_end, int(m))
+        L.vvcr_mc_prof_read(buf.ctypes.data, buf.shape[0])
+        valid = buf[:, 1] > prev_end   # entries of this picture's last launch (older ones are stale)
+        b = buf[valid]
+        if len(b) == 0:
+            print("POC %d: no plain-MC launch" % p["hdr"]["poc"])
+            ctx.release(h)
+            continue
+        prev_end = int(b[:, 1].max())
+        t0 = b[:, 0].astype(np.int64)
+        t1 = b[:, 1].astype(np.int64)
+        base = t0.min()
+        dur = (t1 - t0) / 100.0   # us (100 MHz)
+        start = (t0 - base) / 100.0
+        end = (t1 - base) / 100.0
+        x = (b[:, 2] & 0xffff).astype(np.int64)
+        y = ((b[:, 2] >> 16) & 0xffff).astype(np.int64)
+        w = ((b[:, 2] >> 32) & 0xff).astype(np.int64)
+        fl = b[:, 3].astype(np.int64)
+        order = np.argsort(-dur)
+        print("POC %d: %d workgroups, span %.1f us, start spread %.1f us, duration median %.2f p90 %.2f max %.2f us" % (
+            p["hdr"]["poc"], len(b), end.max(), start.max(), np.median(dur), np.percentile(dur, 90), dur.max()))
+        print("   last end at %.1f us; workgroups ending after 80%% of the span: %d" % (end.max(), int((end > 0.8 * end.max()).sum())))
+        for k in order[:8]:
+            print("   slow: start %.1f dur %.1f  job x %d y %d w %d flags 0x%x" % (start[k], dur[k], x[k], y[k], w[k], fl[k]))
+        ctx.release(h)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build()
+    else:
+        run(sys.argv[2] if len(sys.argv) > 2 else "ra2160_q32")

@@ -27,6 +27,15 @@
 #include "vvcr_tables.h"
 #include "vvcr_mcdev.h"
 
+#ifdef VVCR_MC_PROF
+// Diagnostics build only: per-workgroup start / end timestamps (s_memrealtime, 100 MHz) of k_mc with the
+// workgroup's first job (tools/mc_prof.py).
+__device__ unsigned long long g_mcprof[1 << 16][4];
+extern "C" int vvcr_mc_prof_read(unsigned long long *dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_mcprof), (size_t)n * 4 * 8);
+}
+#endif
+
 namespace {
 
 using namespace mcdev;
@@ -540,6 +549,26 @@ constexpr int MC_LDS = sizeof(TileLds) > 2 * sizeof(BasicLds) ? sizeof(TileLds) 
 __global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict__ jobs, int ntile, int nbasic) {
   __shared__ __attribute__((aligned(16))) char raw[MC_LDS];
   const int b = blockIdx.x;
+#ifdef VVCR_MC_PROF
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  struct Stamp {
+    unsigned long long t0;
+    int b;
+    const McJob *j;
+    __device__ ~Stamp() {
+      __syncthreads();
+      if (threadIdx.x == 0 && b < (1 << 16)) {
+        unsigned int xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_mcprof[b][0] = t0;
+        g_mcprof[b][1] = __builtin_amdgcn_s_memrealtime();
+        g_mcprof[b][2] = (unsigned long long)(uint16_t)j->x | (unsigned long long)(uint16_t)j->y << 16 |
+                         (unsigned long long)j->w << 32 | (unsigned long long)j->h << 40 | (unsigned long long)(xcc & 15) << 48;
+        g_mcprof[b][3] = (unsigned long long)j->flags;
+      }
+    }
+  } stamp{t_start, b, jobs + (b < ntile ? b : ntile + 2 * (b - ntile))};
+#endif
   if (b < ntile) {
     mc_tile(P, jobs, ntile, b, *reinterpret_cast<TileLds *>(raw));
   } else {
