@@ -108,3 +108,35 @@ def test_submit_rejects_out_of_range_references_and_coefficients():
     with pytest.raises(N.VvcrError) as e:
         plan(cu_past_width)
     assert "(-1)" in str(e.value)
+
+
+# ---- the device context (vvcr_*): the same conventions on a GPU
+
+@pytest.mark.gpu
+def test_context_calls_out_of_order_and_bad_arguments():
+    p, pp = _pic0()
+    h = p["hdr"]
+    ctx = N.Context(h["width"], h["height"], dpb_slots=4)
+    try:
+        with pytest.raises(N.VvcrError) as e:
+            ctx.end_picture()                                  # no picture begun
+        assert "(-3)" in str(e.value)
+        with pytest.raises(N.VvcrError) as e:
+            ctx.read_plane(N.BUF_RECO, 4, 0)                   # slot past the DPB
+        assert "(-1)" in str(e.value)
+        with pytest.raises(N.VvcrError) as e:
+            ctx.launch(12345)                                  # no such prepared picture
+        assert "(-1)" in str(e.value) or "(-3)" in str(e.value)
+        bad = S.pic_params(p, 0, {})
+        bad.slot = 7                                           # current picture's slot past the DPB
+        with pytest.raises(N.VvcrError) as e:
+            ctx.begin_picture(bad)
+        assert "(-1)" in str(e.value)
+        # the context stays usable: the picture reconstructs after the failed calls
+        ctx.begin_picture(pp)
+        S.submit(ctx, p)
+        S.set_loop_filter_params(ctx, p)
+        ctx.end_picture()
+        ctx.sync()
+    finally:
+        ctx.close()
