@@ -24,6 +24,7 @@ import os
 # to 8: the "10 lanes" of earlier r02 lines were 8.)
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 12:   # the box exports HIP's default of 4
     os.environ["GPU_MAX_HW_QUEUES"] = "12"
+USER_LANES = "VVCR_LANES" in os.environ or "VVCR_INTRA_LANES" in os.environ
 os.environ.setdefault("VVCR_LANES", "8")
 os.environ.setdefault("VVCR_INTRA_LANES", "5")
 
@@ -213,13 +214,22 @@ def main():
     # one intra picture at a time (four wavefront diagonals' worth: 32 at 1080p, 60 at 4K); with five intra
     # pictures in flight 32 each is better (4K 7.6 -> 8.6 Gpx/s, 1080p unchanged). The 8K shard pass, one
     # picture at a time, keeps the default (32 there: 5.4 -> 4.4 Gpx/s).
-    wg_env = os.environ.get("VVCR_INTRA_WG")
-    if wg_env is None:
+    # At 4K an intra picture takes ~11 ms (5 at 1080p): 12 lanes, 7 of them intra, keep more of them in
+    # flight (interleaved A/B, 4K QP32: 9.0 vs 8.6 Gpx/s; at 1080p 12 / 7 loses: 10.7 vs 12.2).
+    saved = {k: os.environ.get(k) for k in ("VVCR_INTRA_WG", "VVCR_LANES", "VVCR_INTRA_LANES")}
+    if saved["VVCR_INTRA_WG"] is None:
         os.environ["VVCR_INTRA_WG"] = "32"
+    if not USER_LANES and W * H >= 3840 * 2160:
+        os.environ["VVCR_LANES"], os.environ["VVCR_INTRA_LANES"] = "12", "7"
     dec = D.Decoder(pics, dpb_slots=per * a.segments,
                     device=int(os.environ.get("VVCR_DEVICE", local)))   # VVCR_DEVICE: rehearsal of N ranks on one GPU
-    if wg_env is None:
-        del os.environ["VVCR_INTRA_WG"]
+    lanes_cfg = "%s lanes (%s intra), %s k_intra workgroups" % (os.environ["VVCR_LANES"], os.environ["VVCR_INTRA_LANES"],
+                                                              os.environ["VVCR_INTRA_WG"])
+    for k, v in saved.items():   # the shard pass's context takes the library / process defaults
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     ctx = dec.ctx
     copies = []
     t_prep = time.perf_counter()
@@ -368,7 +378,8 @@ def main():
         "dtype": "int16",
         "data": "synthetic (VTM-7.3-encoded synthetic %dx%d %s stream, parsed descriptors resident in HBM)" % (W, H, desc),
         "config": {"workload": "%s: %dx%d %s, %d pictures, reconstruction + DBK/SAO/ALF" % (a.stream, W, H, desc, len(pics)),
-                   "parallelism": "replicas%d" % world, "segments_in_flight": a.segments, "bitexact_vs_reference": bool(bitexact)},
+                   "parallelism": "replicas%d" % world, "segments_in_flight": a.segments, "lanes": lanes_cfg,
+                   "bitexact_vs_reference": bool(bitexact)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic},
         "kernels": {k: {"ms_per_step": round(v[1], 4), "launches_per_step": v[0],
