@@ -16,16 +16,17 @@ timing barrier and max-over-ranks use torch.distributed.
 """
 import os
 
-# Execution lanes (libvvcr reads VVCR_LANES / VVCR_INTRA_LANES at vvcr_create): 5 intra lanes + 3 B lanes,
-# each on its own hardware queue, so that five intra-started segments and the B pictures of three others
+# Execution lanes (libvvcr reads VVCR_LANES / VVCR_INTRA_LANES at vvcr_create): 5 intra lanes + 4 B lanes,
+# each on its own hardware queue, so that five intra-started segments and the B pictures of four others
 # overlap; HIP's default is 4 hardware queues per process, so the bench asks for 12 before the runtime
-# starts. Measured on 1080p with 12 segments in flight (lanes (intra lanes)): 8 (4) 11.5, 8 (5) 12.2,
-# 9 (5) 12.3, 10 (5) 11.5, 10 (4) 10.8, 12 (6) 12.0 Gpx/s. (Until late r02 the library clamped VVCR_LANES
-# to 8: the "10 lanes" of earlier r02 lines were 8.)
+# starts. Measured on 1080p with 12 segments in flight (lanes (intra lanes)): one sweep 8 (4) 11.5,
+# 8 (5) 12.2, 9 (5) 12.3, 10 (5) 11.5, 10 (4) 10.8, 12 (6) 12.0 Gpx/s; interleaved A/B on one box, twice
+# each: 8 (5) 10.5-10.7, 9 (5) 11.2, 10 (5) 10.6 Gpx/s. (Until late r02 the library clamped VVCR_LANES to 8:
+# the "10 lanes" of earlier r02 lines were 8.)
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 12:   # the box exports HIP's default of 4
     os.environ["GPU_MAX_HW_QUEUES"] = "12"
 USER_LANES = "VVCR_LANES" in os.environ or "VVCR_INTRA_LANES" in os.environ
-os.environ.setdefault("VVCR_LANES", "8")
+os.environ.setdefault("VVCR_LANES", "9")
 os.environ.setdefault("VVCR_INTRA_LANES", "5")
 
 import argparse
