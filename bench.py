@@ -1,33 +1,80 @@
-"""Decode throughput of the MI355X reconstruction path (BASELINE.json configs[1]: 1080p random-access
-QP32, 1 GPU): all pictures of the stream reconstructed by libvvcr in decoding order — residuals, motion
-compensation (DMVR/BDOF/affine-PROF/GEO/CIIP), intra waves, deblocking, SAO, ALF/CC-ALF — with every
-input (parsed descriptors, work lists, loop-filter parameters) resident in HBM when the timed region
-starts (vvcr_prepare_picture once, vvcr_launch_picture per step). One step = one decode of the whole
-sequence. The output of the first pass is checked bit-exact against the reference decoder's MD5s.
-Steps cycle through --segments (default 4) copies of the sequence on disjoint DPB slots, as consecutive
-intra-started segments of one long stream: the library runs each picture once its reference / slot
-dependencies are met, so a segment's intra picture may overlap the previous segment's B pictures.
+"""Decode throughput of the MI355X reconstruction path on BASELINE.json configs[2], the largest
+single-GPU configuration: 4K 3840x2160 random access QP27 (the north star's QP32 is --stream ra2160l_q32).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--stream ra1080_q32] [--segments 4] [--no-cpu]
+value (the headline) is END TO END from parsed pictures: each step decodes the whole sequence again,
+and every picture goes through host validation + planning (work lists, intra dependency plan, deblocking
+edges; a pool of --e2e-threads threads, vvcr_picture_*), upload (vvcr_prepare_planned) and the GPU
+(residuals, motion compensation with DMVR/BDOF/affine-PROF/GEO/CIIP, intra, deblocking, SAO, ALF/CC-ALF),
+all inside the timed region. CABAC parsing is not in it yet: the pictures are the reference parser's
+output (tests/golden/<stream>, captured by oracle/_ref/vtm_capture) - value_scope says so.
+The `resident` object is the same reconstruction with every input already planned and resident in HBM
+(vvcr_prepare_picture once, vvcr_launch_picture per step): the GPU-side rate.
+Every pass is checked bit-exact against the reference decoder's MD5s.
 
-Multi-GPU (torch.distributed.run, one process per GPU): the path has no intra-picture work split in
-this round, so N ranks decode N independent replicas (weak scaling, no data-path collective); the
-timing barrier and max-over-ranks use torch.distributed.
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--stream ra2160l_q27] [--no-cpu]
+
+Multi-GPU: one process per GPU (torch.distributed.run; a plain `python bench.py --gpus N` spawns the N
+ranks itself before anything touches the GPU). N ranks decode N independent replicas of the stream
+(weak scaling, no data-path collective); the timing barrier and max-over-ranks use torch.distributed.
 """
 import os
+import sys
 
-# Execution lanes (libvvcr reads VVCR_LANES / VVCR_INTRA_LANES at vvcr_create): 5 intra lanes + 4 B lanes,
-# each on its own hardware queue, so that five intra-started segments and the B pictures of four others
-# overlap; HIP's default is 4 hardware queues per process, so the bench asks for 12 before the runtime
-# starts. Measured on 1080p with 12 segments in flight (lanes (intra lanes)): one sweep 8 (4) 11.5,
-# 8 (5) 12.2, 9 (5) 12.3, 10 (5) 11.5, 10 (4) 10.8, 12 (6) 12.0 Gpx/s; interleaved A/B on one box, twice
-# each: 8 (5) 10.5-10.7, 9 (5) 11.2, 10 (5) 10.6 Gpx/s. (Until late r02 the library clamped VVCR_LANES to 8:
-# the "10 lanes" of earlier r02 lines were 8.)
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 12:   # the box exports HIP's default of 4
-    os.environ["GPU_MAX_HW_QUEUES"] = "12"
 USER_LANES = "VVCR_LANES" in os.environ or "VVCR_INTRA_LANES" in os.environ
-os.environ.setdefault("VVCR_LANES", "9")
-os.environ.setdefault("VVCR_INTRA_LANES", "5")
+
+
+def _spawn_ranks():
+    """`python bench.py --gpus N` outside torch.distributed.run: start the N ranks as child processes
+    (nothing here has touched the GPU yet) and exit with their status."""
+    import argparse
+    import socket
+    import subprocess
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    a, _ = ap.parse_known_args()
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != a.gpus:
+            sys.exit("bench: --gpus %d but WORLD_SIZE=%s" % (a.gpus, world))
+        return
+    if a.gpus <= 1:
+        return
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def _default_stream():
+    root = os.path.dirname(os.path.abspath(__file__))
+    for n in ("ra2160l_q27", "ra2160_q27"):   # 17-picture GOP-16 stream once captured, else the 3-picture one
+        if os.path.isdir(os.path.join(root, "tests", "golden", n)):
+            return n
+    return "ra2160_q27"
+
+
+def _lanes_for(stream):
+    """Execution lanes (libvvcr reads VVCR_LANES / VVCR_INTRA_LANES at vvcr_create) and the HIP hardware
+    queues they need: each lane, the library's copy stream and torch's stream on a queue of its own, so
+    GPU_MAX_HW_QUEUES = lanes + 2 (the box exports HIP's default of 4; the limit here is 32). Measured:
+    4K 12 lanes (7 intra) 9.0 vs 8 (5) 8.6 Gpx/s; 1080p 9 (5) 11.2-12.3 vs 8 (5) 10.5-12.2, 12 (7) 10.7."""
+    small = any(t in stream for t in ("1080", "480", "416", "412"))
+    lanes, intra = (9, 5) if small else (12, 7)
+    if not USER_LANES:
+        os.environ["VVCR_LANES"], os.environ["VVCR_INTRA_LANES"] = str(lanes), str(intra)
+    lanes = int(os.environ.get("VVCR_LANES", lanes))
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < lanes + 2:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, lanes + 2))
+
+
+if __name__ == "__main__":
+    _spawn_ranks()
+    import argparse as _ap
+    _p = _ap.ArgumentParser(add_help=False)
+    _p.add_argument("--stream", default=None)
+    _lanes_for(_p.parse_known_args()[0].stream or _default_stream())
 
 import argparse
 import hashlib
@@ -129,67 +176,84 @@ def shard_bench(a, R):
             "note": "tile-row shards, halo exchange over torch.distributed %s point to point" % (R.dist.get_backend() if R.dist else "-")}
 
 
-def end_to_end(ctx, dec, pics, meta, per, a, copies=4):
-    """Descriptors (host arrays) -> reconstructed pictures, host planning included: a pool of
-    --e2e-threads threads validates and plans pictures (vvcr_picture_*, no GIL inside the library) and
-    uploads them (vvcr_prepare_planned) while this thread launches them in decoding order as soon as each
-    is ready; `copies` consecutive segments of the sequence. Every picture is planned from scratch.
-    CABAC parsing is not included: the descriptors are the capture of the reference's parser."""
-    import concurrent.futures as cf
-    jobs = []
-    for c in range(copies):
-        alloc = S.SlotAllocator(pics, per, base=per * (c % a.segments))
-        for i, p in enumerate(pics):
-            slot = alloc.assign(i, p["hdr"]["poc"])
-            jobs.append((p, slot, dict(alloc.slot_of)))
+class E2E:
+    """Host planning + upload + GPU for every picture, in the timed region (the headline).
 
-    def work(job):
+    Steps decode the whole sequence again and again as consecutive intra-started segments of one long
+    stream, on `segments` disjoint DPB slot ranges. A pool of `threads` threads plans each picture from
+    its host descriptors (vvcr_picture_*: validation, work lists, intra dependency plan, deblocking edges;
+    the library releases the GIL) and uploads it (vvcr_prepare_planned); this thread launches the
+    pictures in decoding order as each becomes ready, and releases a handle once `keep` later pictures
+    were launched (its work is then long done). The pool runs ahead of the launches, so the host work of
+    later pictures overlaps the GPU work of earlier ones, as a decoder's parse of picture n+1 would."""
+
+    def __init__(self, ctx, pics, per, segments, threads, keep=96):
+        import concurrent.futures as cf
+        self.ctx, self.pics, self.per, self.segments = ctx, pics, per, segments
+        self.ex = cf.ThreadPoolExecutor(threads)
+        self.threads, self.keep = threads, keep
+        self.jobs = []
+        for c in range(segments):
+            alloc = S.SlotAllocator(pics, per, base=per * c)
+            seg = []
+            for i, p in enumerate(pics):
+                slot = alloc.assign(i, p["hdr"]["poc"])
+                seg.append((p, slot, dict(alloc.slot_of)))
+            self.jobs.append(seg)
+        self.step_no = 0
+        self.live = []
+
+    def _work(self, job):
         p, slot, slot_of = job
-        pic = S.plan_picture(p, slot, slot_of, dpb_slots=per * a.segments)
-        h = ctx.prepare_planned(pic)
-        pic.close()
-        return h
+        pic = S.plan_picture(p, slot, slot_of, dpb_slots=self.per * self.segments)
+        try:
+            return self.ctx.prepare_planned(pic)
+        finally:
+            pic.close()
 
-    ctx.sync()
-    with cf.ThreadPoolExecutor(a.e2e_threads) as ex:
-        t0 = time.perf_counter()
-        futs = [ex.submit(work, j) for j in jobs]
-        handles = []
+    def run(self, steps):
+        """Enqueue `steps` steps; returns when the last picture is launched (not finished)."""
+        jobs = []
+        for k in range(steps):
+            jobs += self.jobs[(self.step_no + k) % self.segments]
+        self.step_no += steps
+        futs = [self.ex.submit(self._work, j) for j in jobs]
         for f in futs:
             h = f.result()
-            ctx.launch(h)
-            handles.append(h)
-        ctx.sync()
-        t1 = time.perf_counter()
-    ok = True
-    owner = {}
-    for (p, slot, _) in jobs[-len(pics):]:
-        owner[slot] = p["hdr"]["poc"]
-    for slot, poc in owner.items():
-        ok = ok and D.plane_md5s(dec.read(slot)) == meta["poc_plane_md5"][str(poc)]
-    for h in handles:
-        ctx.release(h)
-    px = pics[0]["hdr"]["width"] * pics[0]["hdr"]["height"] * len(jobs)
-    return {"value": round(px / (t1 - t0) / 1e6, 2), "unit": "Mpixels/s", "threads": a.e2e_threads,
-            "pictures": len(jobs), "ms_per_sequence": round((t1 - t0) / copies * 1e3, 2), "bitexact_vs_reference": ok,
-            "note": "host planning (validation, work lists, intra dependency plan, deblocking edges) + upload + GPU, "
-                    "from parsed descriptors; CABAC parsing excluded"}
+            self.ctx.launch(h)
+            self.live.append(h)
+            if len(self.live) > self.keep:
+                self.ctx.release(self.live.pop(0))
+
+    def last_segment_slots(self):
+        seg = self.jobs[(self.step_no - 1) % self.segments]
+        return {slot: p["hdr"]["poc"] for p, slot, _ in seg}
+
+    def close(self):
+        self.ctx.sync()
+        for h in self.live:
+            self.ctx.release(h)
+        self.live = []
+        self.ex.shutdown()
+
+
+def check_slots(dec, owner, meta):
+    return all(D.plane_md5s(dec.read(slot)) == meta["poc_plane_md5"][str(poc)] for slot, poc in owner.items())
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--stream", default="ra1080_q32")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--stream", default=_default_stream())
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--segments", type=int, default=12, help="copies of the sequence the steps cycle through (<= 12)")
-    ap.add_argument("--kernels-inflight", action="store_true",
-                    help="diagnostics: take the kernel table from a pass with every segment in flight")
+    ap.add_argument("--segments", type=int, default=8, help="DPB copies of the sequence the steps cycle through (<= 12)")
+    ap.add_argument("--resident-steps", type=int, default=20, help="timed steps of the resident (pre-planned) pass, 0 = skip")
     ap.add_argument("--sync-pictures", action="store_true",
-                    help="host sync after every picture (profiling: kernel durations without overlap)")
-    ap.add_argument("--e2e-threads", type=int, default=12,
-                    help="host planning threads of the end-to-end pass (0 = skip it)")
+                    help="host sync after every picture of the resident pass (profiling: kernel durations without overlap)")
+    ap.add_argument("--e2e-threads", type=int, default=16,
+                    help="host planning threads (the GPU box's CPU share is 16)")
     ap.add_argument("--shard-stream", default="ra4320t_q32",
                     help="tile-row stream of the spatially sharded pass (BASELINE config 4: 8K, one shard per rank)")
     ap.add_argument("--shard-steps", type=int, default=3, help="timed steps of the sharded pass (0 = skip it)")
@@ -197,6 +261,8 @@ def main():
 
     R = V.Ranks()
     world, rank, local = R.world, R.rank, R.local
+    if world != a.gpus:
+        sys.exit("bench: --gpus %d but %d ranks" % (a.gpus, world))
 
     d = os.path.join(ROOT, "tests", "golden", a.stream)
     pics = S.load_sequence(d)
@@ -204,162 +270,152 @@ def main():
     h0 = pics[0]["hdr"]
     W, H = h0["width"], h0["height"]
     px_seq = W * H * len(pics)
+    nI = sum(1 for p in pics if p["hdr"]["slice_type"] == 2)
 
-    # ---- prepare every picture once (host planning + upload), decoding order. The sequence is prepared
-    # --segments times over disjoint DPB slot ranges and the steps cycle through these copies: step k+1
-    # then decodes its segment like the next intra-started segment of a longer stream would be decoded
-    # (its intra picture references nothing, so it may start while step k's B pictures still run —
-    # the library orders pictures only by their DPB-slot dependencies). --segments 1 serialises steps.
     per = min(12, 64 // a.segments)   # DPB slots per copy (64 in all)
-    # k_intra workgroups of this context (VVCR_INTRA_WG, read at vvcr_create): the library's default sizes
-    # one intra picture at a time (four wavefront diagonals' worth: 32 at 1080p, 60 at 4K); with five intra
-    # pictures in flight 32 each is better (4K 7.6 -> 8.6 Gpx/s, 1080p unchanged). The 8K shard pass, one
-    # picture at a time, keeps the default (32 there: 5.4 -> 4.4 Gpx/s).
-    # At 4K an intra picture takes ~11 ms (5 at 1080p): 12 lanes, 7 of them intra, keep more of them in
-    # flight (interleaved A/B, 4K QP32: 9.0 vs 8.6 Gpx/s; at 1080p 12 / 7 loses: 10.7 vs 12.2).
-    saved = {k: os.environ.get(k) for k in ("VVCR_INTRA_WG", "VVCR_LANES", "VVCR_INTRA_LANES")}
-    if saved["VVCR_INTRA_WG"] is None:
-        os.environ["VVCR_INTRA_WG"] = "32"
-    if not USER_LANES and W * H >= 3840 * 2160:
-        os.environ["VVCR_LANES"], os.environ["VVCR_INTRA_LANES"] = "12", "7"
+    # k_intra workgroups (VVCR_INTRA_WG, read at vvcr_create): the library's default sizes one intra picture at
+    # a time (32 at 1080p, 60 at 4K); with several intra pictures in flight 32 each is better (4K 7.6 -> 8.6
+    # Gpx/s). The 8K shard pass, one picture at a time, keeps the default.
+    saved = os.environ.get("VVCR_INTRA_WG")
+    os.environ.setdefault("VVCR_INTRA_WG", "32")
     dec = D.Decoder(pics, dpb_slots=per * a.segments,
                     device=int(os.environ.get("VVCR_DEVICE", local)))   # VVCR_DEVICE: rehearsal of N ranks on one GPU
-    lanes_cfg = "%s lanes (%s intra), %s k_intra workgroups" % (os.environ["VVCR_LANES"], os.environ["VVCR_INTRA_LANES"],
-                                                              os.environ["VVCR_INTRA_WG"])
-    for k, v in saved.items():   # the shard pass's context takes the library / process defaults
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
+    lanes_cfg = "%s lanes (%s intra) on %s hardware queues, %s k_intra workgroups" % (
+        os.environ["VVCR_LANES"], os.environ["VVCR_INTRA_LANES"], os.environ.get("GPU_MAX_HW_QUEUES", "4"),
+        os.environ["VVCR_INTRA_WG"])
+    if saved is None:
+        os.environ.pop("VVCR_INTRA_WG", None)
     ctx = dec.ctx
-    copies = []
-    t_prep = time.perf_counter()
-    for c in range(a.segments):
-        alloc = S.SlotAllocator(pics, per, base=per * c)
-        handles, slots = [], []
-        for i, p in enumerate(pics):
-            slot = alloc.assign(i, p["hdr"]["poc"])
-            ctx.begin_picture(S.pic_params(p, slot, alloc.slot_of))
-            S.submit(ctx, p)
-            S.set_loop_filter_params(ctx, p)
-            handles.append(ctx.prepare(N.STAGE_ALL))
-            slots.append((p["hdr"]["poc"], slot))
-        copies.append((handles, slots))
-    t_prep = (time.perf_counter() - t_prep) / a.segments
 
-    # ---- first pass: bit-exactness of every copy against the reference decoder (untimed, one picture at
-    # a time: every picture's planes and the YUV file MD5)
-    bitexact = True
-    for handles, slots in copies:
-        yuv = hashlib.md5()
-        outs = {}
-        for hnd, (poc, slot) in zip(handles, slots):
-            ctx.launch(hnd)
-            planes = dec.read(slot)
-            outs[poc] = D.plane_md5s(planes), planes
-        bitexact = bitexact and all(outs[int(k)][0] == v for k, v in meta["poc_plane_md5"].items())
-        for poc in sorted(outs):
-            for pl in outs[poc][1]:
-                yuv.update(np.ascontiguousarray(pl).astype("<u2").tobytes())
-        bitexact = bitexact and yuv.hexdigest() == meta["yuv_md5"]
-        outs = None
-    nstep = [0]
-
-    def check_in_flight():
-        """The timed configuration itself: every segment copy launched back to back with no host sync in
-        between (all segments in flight on the lanes), then the last picture of every DPB slot of every
-        copy checked against the reference MD5s."""
-        for handles, _ in copies:
-            for hnd in handles:
-                ctx.launch(hnd)
-        ctx.sync()
-        ok = True
-        for _, slots in copies:
-            owner = {slot: poc for poc, slot in slots}
-            for slot, poc in owner.items():
-                ok = ok and D.plane_md5s(dec.read(slot)) == meta["poc_plane_md5"][str(poc)]
-        return ok
-
-    def run_step():
-        for hnd in copies[nstep[0] % a.segments][0]:
-            ctx.launch(hnd)
-            if a.sync_pictures:
-                ctx.sync()
-        nstep[0] += 1
-
-    ctx.set_timing(False)   # the throughput passes record no per-kernel events (marker packets)
-    for _ in range(a.warmup):
-        run_step()
+    # ---- headline: end to end (host planning + upload + GPU inside the timed region)
+    ctx.set_timing(False)
+    e2e = E2E(ctx, pics, per, a.segments, a.e2e_threads)
+    e2e.run(1)                      # first pass, one picture at a time is not needed: checked below
     ctx.sync()
-
+    bitexact = check_slots(dec, e2e.last_segment_slots(), meta)
+    if a.warmup > 1:
+        e2e.run(a.warmup - 1)
+        ctx.sync()
     R.barrier()
     ctx.sync()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        run_step()
-    t_sub = time.perf_counter()   # host submission done (the library never blocks the host on the GPU)
+    e2e.run(a.steps)
     ctx.sync()
     t1 = time.perf_counter()
     R.barrier()
     elapsed = R.max_over_ranks(t1 - t0)
+    e2e_ok = check_slots(dec, e2e.last_segment_slots(), meta)
+    bitexact = bitexact and e2e_ok
+    e2e.close()
 
-    # ---- the same steps one segment at a time (each step synchronised before the next starts): the
-    # latency-bound view, reported beside value
-    ctx.sync()
-    R.barrier()
-    t2 = time.perf_counter()
-    for _ in range(a.steps):
+    # ---- resident: every picture planned and uploaded once, the steps only launch (GPU-side rate)
+    resident = None
+    kern = {}
+    if a.resident_steps > 0:
+        copies = []
+        t_prep = time.perf_counter()
+        for c in range(a.segments):
+            alloc = S.SlotAllocator(pics, per, base=per * c)
+            handles, slots = [], []
+            for i, p in enumerate(pics):
+                slot = alloc.assign(i, p["hdr"]["poc"])
+                ctx.begin_picture(S.pic_params(p, slot, alloc.slot_of))
+                S.submit(ctx, p)
+                S.set_loop_filter_params(ctx, p)
+                handles.append(ctx.prepare(N.STAGE_ALL))
+                slots.append((p["hdr"]["poc"], slot))
+            copies.append((handles, slots))
+        t_prep = (time.perf_counter() - t_prep) / a.segments
+        # first pass of the first copy one picture at a time: every plane and the YUV file MD5
+        yuv = hashlib.md5()
+        outs = {}
+        for hnd, (poc, slot) in zip(*copies[0]):
+            ctx.launch(hnd)
+            planes = dec.read(slot)
+            outs[poc] = D.plane_md5s(planes), planes
+        res_ok = all(outs[int(k)][0] == v for k, v in meta["poc_plane_md5"].items())
+        for poc in sorted(outs):
+            for pl in outs[poc][1]:
+                yuv.update(np.ascontiguousarray(pl).astype("<u2").tobytes())
+        res_ok = res_ok and yuv.hexdigest() == meta["yuv_md5"]
+        outs = None
+        nstep = [0]
+
+        def run_step():
+            for hnd in copies[nstep[0] % a.segments][0]:
+                ctx.launch(hnd)
+                if a.sync_pictures:
+                    ctx.sync()
+            nstep[0] += 1
+        for _ in range(a.warmup):
+            run_step()
+        ctx.sync()
+        R.barrier()
+        r0 = time.perf_counter()
+        for _ in range(a.resident_steps):
+            run_step()
+        ctx.sync()
+        r1 = time.perf_counter()
+        R.barrier()
+        r_el = R.max_over_ranks(r1 - r0)
+        # every copy launched back to back (as timed), then each copy's slots checked
+        for handles, _ in copies:
+            for hnd in handles:
+                ctx.launch(hnd)
+        ctx.sync()
+        for _, slots in copies:
+            res_ok = res_ok and check_slots(dec, {slot: poc for poc, slot in slots}, meta)
+        # serial view: one step at a time
+        s0 = time.perf_counter()
+        for _ in range(max(1, a.resident_steps // 2)):
+            run_step()
+            ctx.sync()
+        s_el = (time.perf_counter() - s0) / max(1, a.resident_steps // 2)
+        # one more step with per-kernel HIP events (one segment in flight): the kernel table and roofline
+        ctx.set_timing(True)
         run_step()
         ctx.sync()
-    t3 = time.perf_counter()
-    R.barrier()
-    elapsed_serial = R.max_over_ranks(t3 - t2)
-    # the timed configuration (all segments in flight, no per-kernel events), checked bit-exact
-    inflight_ok = check_in_flight()
-    bitexact = bitexact and inflight_ok
-    # one more (untimed) step with per-kernel HIP events, one segment in flight: the kernel table and roofline
-    ctx.set_timing(True)
-    if a.kernels_inflight:   # every segment in flight (as timed), all steps' kernel tables summed below
-        for _ in range(a.segments):
-            run_step()
-    else:
-        run_step()
-    ctx.sync()
-    e2e = end_to_end(ctx, dec, pics, meta, per, a) if (world == 1 and a.e2e_threads > 0) else None
+        for hnd in copies[(nstep[0] - 1) % a.segments][0]:
+            for name, launches, ms, alg in ctx.kernel_stats(hnd):
+                k = kern.setdefault(name, [0, 0.0, 0.0])
+                k[0] += launches
+                k[1] += ms
+                k[2] += alg
+        for handles, _ in copies:
+            for hnd in handles:
+                ctx.release(hnd)
+        bitexact = bitexact and res_ok
+        resident = {"value": round(V.job_throughput(px_seq * a.resident_steps, r_el, R) / 1e6, 2), "unit": "Mpixels/s",
+                    "steps": a.resident_steps, "ms_per_step": round(r_el / a.resident_steps * 1e3, 3),
+                    "serial_ms_per_step": round(s_el * 1e3, 3),
+                    "serial_value": round(px_seq / s_el / 1e6, 2),
+                    "host_prepare_s_per_sequence": round(t_prep, 3), "bitexact_vs_reference": bool(res_ok),
+                    "note": "GPU reconstruction + loop filters of pictures planned and uploaded beforehand "
+                            "(descriptors and work lists resident in HBM), %d segments in flight; serial = one "
+                            "step at a time" % a.segments}
 
-    # ---- per-kernel timing of the last step (HIP events on the library stream)
-    kern = {}
-    last = copies[(nstep[0] - 1) % a.segments][0]
-    if a.kernels_inflight:
-        last = [h for c in copies for h in c[0]]
-    for hnd in last:
-        for name, launches, ms, alg in ctx.kernel_stats(hnd):
-            k = kern.setdefault(name, [0, 0.0, 0.0])
-            k[0] += launches
-            k[1] += ms
-            k[2] += alg
-    dom = max(kern, key=lambda k: kern[k][1])
-    dl, dms, dalg = kern[dom]
-    per_launch_bytes = dalg / max(dl, 1)
-    per_launch_s = dms / 1e3 / max(dl, 1)
-    achieved = per_launch_bytes / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
-    # the north-star's MC-interpolation kernels (plain and affine): algorithmic bytes / HIP-event time
-    mc_roof = {"peak": PEAK_HBM_GBS, "unit": "GB/s",
-               "note": "MC interpolation kernels on this workload (one segment in flight); "
-                       "4K figures: profiles/r02_mc_kernels.json"}
-    for k in ("mc", "mc_affine"):
+    roof = None
+    if kern:
+        dom = max(kern, key=lambda k: kern[k][1])
+        dl, dms, dalg = kern[dom]
+        per_launch_s = dms / 1e3 / max(dl, 1)
+        achieved = dalg / max(dl, 1) / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
+        traffic = None
+        tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_traffic*.json")))
+        for tf in reversed(tfs):   # the newest PMC summary taken on this workload
+            with open(tf) as f:
+                tj = json.load(f)
+            if tj.get("stream") == a.stream:
+                traffic = tj.get("per_group_launch_bytes", {}).get(dom)
+                break
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
+                "us_per_launch": round(per_launch_s * 1e6, 2)}
+    mc_roof = {"peak": PEAK_HBM_GBS, "unit": "GB/s", "note": "MC interpolation kernels, HIP events, one segment in flight"}
+    for k in ("mc", "mc_affine", "mc_bidir"):
         v = kern.get(k, [0, 0.0, 0.0])
         g = v[2] / (v[1] / 1e3) / 1e9 if v[1] > 0 else 0.0
         mc_roof[k] = {"achieved": round(g, 2), "frac": round(g / PEAK_HBM_GBS, 4), "us_per_launch": round(v[1] / max(v[0], 1) * 1e3, 2)}
-
-    traffic = None
-    tfs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_traffic.json")))   # the newest round's
-    tf = tfs[-1] if tfs else ""
-    if tf and os.path.exists(tf):
-        with open(tf) as f:
-            tj = json.load(f)
-        if tj.get("stream", "ra1080_q32") == a.stream:   # the PMC passes were taken on this workload
-            traffic = tj.get("per_group_launch_bytes", {}).get(dom)   # profiles/: tools/pmc.sh + tools/pmc_summary.py
 
     ms_step = elapsed / a.steps * 1e3
     kind, qp = a.stream.split("_")[0], a.stream.split("_")[-1]
@@ -377,36 +433,28 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int16",
-        "data": "synthetic (VTM-7.3-encoded synthetic %dx%d %s stream, parsed descriptors resident in HBM)" % (W, H, desc),
-        "config": {"workload": "%s: %dx%d %s, %d pictures, reconstruction + DBK/SAO/ALF" % (a.stream, W, H, desc, len(pics)),
-                   "parallelism": "replicas%d" % world, "segments_in_flight": a.segments, "lanes": lanes_cfg,
-                   "bitexact_vs_reference": bool(bitexact)},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic},
+        "data": "synthetic (VTM-7.3-encoded synthetic %dx%d %s stream)" % (W, H, desc),
+        "config": {"workload": "%s: %dx%d %s, %d pictures (%d intra) per step, reconstruction + DBK/SAO/ALF" % (
+                       a.stream, W, H, desc, len(pics), nI),
+                   "parallelism": "replicas%d" % world, "segments": a.segments, "lanes": lanes_cfg,
+                   "host_threads": a.e2e_threads, "bitexact_vs_reference": bool(bitexact)},
+        "value_scope": "end to end from parsed pictures: host validation + planning (work lists, intra dependency plan, "
+                       "deblocking edges) + upload + GPU reconstruction and loop filters, every picture of every step; "
+                       "CABAC parsing excluded (pictures are the reference parser's output) - see README",
+        "roofline": roof,
+        "cpu_baseline": None,
+        "resident": resident,
+        "mc_roofline": mc_roof,
         "kernels": {k: {"ms_per_step": round(v[1], 4), "launches_per_step": v[0],
                         "alg_GBps": round(v[2] / (v[1] / 1e3) / 1e9, 2) if v[1] > 0 else 0.0} for k, v in kern.items()},
-        "host_submit_ms_per_step": round((t_sub - t0) / a.steps * 1e3, 3),
-        "serial": {"value": round(V.job_throughput(px_seq * a.steps, elapsed_serial, R) / 1e6, 2),
-                   "ms_per_step": round(elapsed_serial / a.steps * 1e3, 3),
-                   "note": "one segment in flight (sync after every step)"},
-        "mc_roofline": mc_roof,
-        "host_prepare_s": round(t_prep, 3),
-        "value_scope": "GPU reconstruction + loop filters of pre-planned pictures (descriptors and work lists resident "
-                       "in HBM); host planning and CABAC parsing excluded - see end_to_end",
-        "end_to_end": e2e,
     }
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, "tests", "golden", "streams", a.stream + ".bin"), px_seq)
-    else:
-        line["cpu_baseline"] = None
-    for handles, _ in copies:
-        for hnd in handles:
-            ctx.release(hnd)
     dec.close()
     if a.shard_steps > 0:
         try:
             line["shard"] = shard_bench(a, R)
-        except Exception as e:   # reported, never silently dropped: the replica line above stays valid
+        except Exception as e:   # reported, never silently dropped: the line above stays valid
             line["shard"] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
     if rank == 0:
         print(json.dumps(line))

@@ -175,8 +175,7 @@ int vvcr_submit(vvcr_ctx *ctx,
                 const vvcr_tu *tu, int32_t ntu,
                 const int32_t *coef, int64_t ncoef,
                 const vvcr_motion *motion,          /* (height/4) x (width/4) */
-                const vvcr_geo *geo, int32_t ngeo,
-                const int32_t *dmvr_delta_unused, int32_t nd);
+                const vvcr_geo *geo, int32_t ngeo);
 int vvcr_set_loop_filter_params(vvcr_ctx *ctx, const vvcr_sao *sao /* [n_ctb][3] */, const vvcr_alf *alf);
 
 /* Stage mask for vvcr_end_picture_stages (tests isolate stages; vvcr_end_picture runs all). */

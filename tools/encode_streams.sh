@@ -2,12 +2,13 @@
 # Re-creates the committed test bitstreams with the REFERENCE encoder built by oracle/ref.mk
 # (VTM 7.3 EncoderApp, CTC configs from /root/reference/cfg). Test-infrastructure only; runs in the
 # build container (needs /root/reference). Every stream carries MD5 decoded-picture-hash SEI.
-#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32
+#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32
 set -e
 R=/root/reference/cfg; E=${E:-$(dirname $0)/../oracle/_ref/EncoderApp}; T=${T:-/tmp/enc}; O=${O:-$(dirname $0)/../tests/golden/streams}
 mkdir -p $T $O
 G="python3 $(dirname $0)/gen_synth.py"
 TILES="--EnablePicPartitioning=1 --RasterScanSlices=1 --RasterSliceSizes=1000 --DisableLoopFilterAcrossTiles=0 --DisableLoopFilterAcrossSlices=0"
+EFAST="--SearchRange=64 --LCTUFast=1 --FastMrg=1 --PBIntraFast=1 --FastMIP=1 --FastLFNST=1 --ISPFast=1 --BcwFast=1 --TransformSkipFast=1"
 FAST="--SearchRange=32 --MaxMTTHierarchyDepth=1 --MaxMTTHierarchyDepthISliceL=1 --MaxMTTHierarchyDepthISliceC=1 --LCTUFast=1 --FastMrg=1 --PBIntraFast=1 --FastMIP=1 --FastLFNST=1 --ISPFast=1 --BcwFast=1 --TransformSkipFast=1"
 enc() { # name cfg W H frames qp yuv extra...
   local n=$1 cfg=$2 w=$3 h=$4 f=$5 q=$6 y=$7; shift 7
@@ -39,5 +40,19 @@ for n in "$@"; do case $n in
   # 412x236 coded as 416x240 with a conformance window (the encoder pads right / bottom to the 8-sample
   # minimum CU size): DecoderApp's output crops it (VideoIOYuv::write), vvcr_write_output must too
   ra412c_q32) [ -f $T/syn412.yuv ] || $G 412 236 5 $T/syn412.yuv; enc $n encoder_randomaccess_vtm.cfg 412 236 5 32 $T/syn412.yuv --ConformanceWindowMode=1 ;;
+  # 4K random access, a whole GOP-16 after the intra picture (17 pictures), so the I picture is 1/17 of
+  # the work as in the CTC random-access configuration (BASELINE configs[2] QP27, north star QP32).
+  # Encoder-side speed-ups only (search range, fast decisions); the coded tool set is the CTC one.
+  ra2160l_q27) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 17 27 $T/syn2160l.yuv $EFAST ;;
+  ra2160l_q32) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 17 32 $T/syn2160l.yuv $EFAST ;;
+  # a second independently moving layer cut by polygon edges: GEO (InterPrediction.cpp:1749) and CIIP
+  # (IntraPrediction.cpp:681,735) CUs in quantity
+  rageo480_q32) [ -f $T/syn480g.yuv ] || $G 832 480 17 $T/syn480g.yuv 0.002 0 0 layers; enc $n encoder_randomaccess_vtm.cfg 832 480 17 32 $T/syn480g.yuv ;;
+  # screen-like content, BDPCM (luma; VTM 7.3 allows chroma BDPCM only in 4:4:4, VLCWriter.cpp:965) (IntraPrediction.cpp:644, TrQuant.cpp:533)
+  aibdpcm416_q32) [ -f $T/syn416s.yuv ] || $G 416 240 17 $T/syn416s.yuv 0 0 0 screen; enc $n encoder_intra_vtm.cfg 416 240 8 32 $T/syn416s.yuv --TemporalSubsampleRatio=1 --BDPCM=1 ;;
+  # scalar dequantisation on every block (Quant.cpp:369), sign data hiding, explicit MTS for inter too
+  radq0416_q32) [ -f $T/syn416g.yuv ] || $G 416 240 17 $T/syn416g.yuv 0.002 0 0 layers; enc $n encoder_randomaccess_vtm.cfg 416 240 17 32 $T/syn416g.yuv --DepQuant=0 --SignHideFlag=1 --MTS=3 ;;
+  # explicit weighted prediction at 1080p (WeightPrediction.cpp:382,413)
+  rawp1080_q32) [ -f $T/syn1080f.yuv ] || $G 1920 1080 9 $T/syn1080f.yuv 0.002 0 0.03; enc $n encoder_randomaccess_vtm.cfg 1920 1080 9 32 $T/syn1080f.yuv --SearchRange=64 --WeightedPredP=1 --WeightedPredB=1 ;;
   *) echo "unknown stream $n"; exit 1 ;;
 esac; done

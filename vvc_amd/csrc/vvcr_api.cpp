@@ -25,6 +25,9 @@
 namespace {
 
 thread_local std::string g_create_error;
+// Error text of the last failing context call, per calling thread (like errno): vvcr_prepare_planned may
+// fail on several threads at once, so the message is never a field shared between threads.
+thread_local std::string g_ctx_error;
 
 template <class T>
 struct DevVec {
@@ -192,7 +195,6 @@ struct Lane {
 
 struct vvcr_ctx {
   vvcr_seq_params sp{};
-  std::string err;
   hipStream_t stream = nullptr;      // lane 0's stream (host copies, vvcr_stream)
   hipStream_t copy_stream = nullptr; // halo row export / import (vvcr_export_rows / vvcr_import_rows), output frames
   DevVec<uint8_t> out_stage;         // vvcr_write_output to host memory
@@ -238,8 +240,8 @@ static void sync_lanes(vvcr_ctx *ctx) {
 #define API_BEGIN try {
 #define API_END                                                  \
   }                                                              \
-  catch (const VvcrError &e) { ctx->err = e.msg; return e.code; } \
-  catch (const std::exception &e) { ctx->err = e.what(); return VVCR_E_STATE; }
+  catch (const VvcrError &e) { g_ctx_error = e.msg; return e.code; } \
+  catch (const std::exception &e) { g_ctx_error = e.what(); return VVCR_E_STATE; }
 
 static int n_ctb(const vvcr_seq_params &sp) {
   const int ctu = 1 << sp.ctu_log2;
@@ -737,7 +739,7 @@ int vvcr_destroy(vvcr_ctx *ctx) {
   return VVCR_OK;
 }
 
-const char *vvcr_last_error(vvcr_ctx *ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+const char *vvcr_last_error(vvcr_ctx *ctx) { return ctx ? g_ctx_error.c_str() : g_create_error.c_str(); }
 
 void *vvcr_stream(vvcr_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
@@ -832,8 +834,7 @@ int vvcr_begin_picture(vvcr_ctx *ctx, const vvcr_pic_params *pp) {
 
 int vvcr_submit(vvcr_ctx *ctx, const vvcr_cu *cu, int32_t ncu, const vvcr_pu *pu, int32_t npu, const vvcr_tu *tu,
                 int32_t ntu, const int32_t *coef, int64_t ncoef, const vvcr_motion *motion, const vvcr_geo *geo,
-                int32_t ngeo, const int32_t *dmvr_delta_unused, int32_t nd) {
-  (void)dmvr_delta_unused; (void)nd;
+                int32_t ngeo) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_submit outside begin/end picture");
@@ -855,7 +856,12 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
   if (!ctx->in_picture) throw VvcrError(VVCR_E_STATE, "vvcr_end_picture without begin");
-  Prepared &r = *ctx->prepared[0];
+  Prepared *rp;
+  {   // the table may be reallocated by new_prepared on another thread; the record at index 0 is not
+    std::lock_guard<std::mutex> g(ctx->prepared_mu);
+    rp = ctx->prepared[0].get();
+  }
+  Prepared &r = *rp;
   plan_picture(ctx->cur, mask);
   prepare(ctx, r, ctx->cur);
   launch(ctx, r);
@@ -932,8 +938,9 @@ int vvcr_picture_create(const vvcr_seq_params *sp, const vvcr_pic_params *pp, vv
   if (!sp || !pp || !out) return VVCR_E_ARG;
   *out = nullptr;
   if (sp->chroma_format != 1 || sp->width <= 0 || sp->height <= 0 || sp->width % 8 || sp->height % 8 ||
+      sp->bit_depth < 8 || sp->bit_depth > 10 ||
       sp->ctu_log2 < 5 || sp->ctu_log2 > 7 || sp->dpb_slots <= 0 || sp->dpb_slots > VVCR_MAX_SLOTS) {
-    g_create_error = "unsupported sequence parameters";
+    g_create_error = "unsupported sequence parameters (4:2:0, 8..10 bit, size multiple of 8, CTU 32..128)";
     return VVCR_E_UNSUPPORTED;
   }
   auto pic = std::make_unique<vvcr_picture>();

@@ -80,7 +80,7 @@ def lib():
         L.vvcr_last_error.argtypes = [P]
         L.vvcr_last_error.restype = C.c_char_p
         L.vvcr_begin_picture.argtypes = [P, C.POINTER(PicParams)]
-        L.vvcr_submit.argtypes = [P, P, I32, P, I32, P, I32, P, C.c_int64, P, P, I32, P, I32]
+        L.vvcr_submit.argtypes = [P, P, I32, P, I32, P, I32, P, C.c_int64, P, P, I32]
         L.vvcr_set_loop_filter_params.argtypes = [P, P, C.POINTER(Alf)]
         L.vvcr_end_picture.argtypes = [P]
         L.vvcr_end_picture_stages.argtypes = [P, C.c_uint32]
@@ -237,7 +237,7 @@ class Context:
         arrs = [np.ascontiguousarray(a, np.int32) for a in (cu, pu, tu, coef, motion, geo)]
         cu, pu, tu, coef, motion, geo = arrs
         self._chk(self.L.vvcr_submit(self.h, _ptr(cu), len(cu), _ptr(pu), len(pu), _ptr(tu), len(tu),
-                                     _ptr(coef), coef.size, _ptr(motion), _ptr(geo), len(geo), None, 0),
+                                     _ptr(coef), coef.size, _ptr(motion), _ptr(geo), len(geo)),
                   "vvcr_submit")
 
     def set_loop_filter_params(self, sao, alf_struct, keep):
