@@ -584,6 +584,32 @@ static void dumpTables(const char *path) {
     T.i16("geo_weight_offset", v, {(uint64_t)GEO_NUM_PARTITION_MODE, (uint64_t)GEO_NUM_CU_SIZE, (uint64_t)GEO_NUM_CU_SIZE, 2}); }
   { std::vector<int16_t> v; for (int i = 0; i < GEO_NUM_PRESTORED_MASK; i++) v.insert(v.end(), g_globalGeoWeights[i], g_globalGeoWeights[i] + GEO_WEIGHT_MASK_SIZE * GEO_WEIGHT_MASK_SIZE);
     T.i16("geo_weights", v, {(uint64_t)GEO_NUM_PRESTORED_MASK, (uint64_t)GEO_WEIGHT_MASK_SIZE, (uint64_t)GEO_WEIGHT_MASK_SIZE}); }
+  // CABAC context sets (Contexts.cpp:188-908): offset/size of every set and the four init tables
+  // (B, P, I init values and the log2 window sizes, ContextSetCfg::getInitTable 0..3)
+#define VVCR_CS(n) { const CtxSet &s = ContextSetCfg::n; std::vector<int32_t> v{(int32_t)s.Offset, (int32_t)s.Size}; T.i32("ctx_" #n, v, {2}); }
+#define VVCR_CSA(n, k) { const CtxSet &s = ContextSetCfg::n[k]; std::vector<int32_t> v{(int32_t)s.Offset, (int32_t)s.Size}; T.i32("ctx_" #n #k, v, {2}); }
+  VVCR_CS(SplitFlag) VVCR_CS(SplitQtFlag) VVCR_CS(SplitHvFlag) VVCR_CS(Split12Flag) VVCR_CS(ModeConsFlag) VVCR_CS(SkipFlag)
+  VVCR_CS(MergeFlag) VVCR_CS(RegularMergeFlag) VVCR_CS(MergeIdx) VVCR_CS(PredMode) VVCR_CS(MultiRefLineIdx)
+  VVCR_CS(IntraLumaMpmFlag) VVCR_CS(IntraLumaPlanarFlag) VVCR_CS(CclmModeFlag) VVCR_CS(CclmModeIdx) VVCR_CS(IntraChromaPredMode)
+  VVCR_CS(MipFlag) VVCR_CS(DeltaQP) VVCR_CS(InterDir) VVCR_CS(RefPic) VVCR_CS(MmvdFlag) VVCR_CS(MmvdMergeIdx) VVCR_CS(MmvdStepMvpIdx)
+  VVCR_CS(SubblockMergeFlag) VVCR_CS(AffineFlag) VVCR_CS(AffineType) VVCR_CS(AffMergeIdx) VVCR_CS(Mvd) VVCR_CS(BDPCMMode)
+  VVCR_CS(QtRootCbf) VVCR_CS(ACTFlag) VVCR_CSA(QtCbf, 0) VVCR_CSA(QtCbf, 1) VVCR_CSA(QtCbf, 2)
+  VVCR_CSA(SigCoeffGroup, 0) VVCR_CSA(SigCoeffGroup, 1) VVCR_CSA(LastX, 0) VVCR_CSA(LastX, 1) VVCR_CSA(LastY, 0) VVCR_CSA(LastY, 1)
+  VVCR_CSA(SigFlag, 0) VVCR_CSA(SigFlag, 1) VVCR_CSA(SigFlag, 2) VVCR_CSA(SigFlag, 3) VVCR_CSA(SigFlag, 4) VVCR_CSA(SigFlag, 5)
+  VVCR_CSA(ParFlag, 0) VVCR_CSA(ParFlag, 1) VVCR_CSA(GtxFlag, 0) VVCR_CSA(GtxFlag, 1) VVCR_CSA(GtxFlag, 2) VVCR_CSA(GtxFlag, 3)
+  VVCR_CS(TsSigCoeffGroup) VVCR_CS(TsSigFlag) VVCR_CS(TsParFlag) VVCR_CS(TsGtxFlag) VVCR_CS(TsLrg1Flag) VVCR_CS(TsResidualSign)
+  VVCR_CS(MVPIdx) VVCR_CS(SaoMergeFlag) VVCR_CS(SaoTypeIdx) VVCR_CS(TransformSkipFlag) VVCR_CS(MTSIdx) VVCR_CS(LFNSTIdx)
+  VVCR_CS(PLTFlag) VVCR_CS(RdpcmFlag) VVCR_CS(RdpcmDir) VVCR_CS(SbtFlag) VVCR_CS(SbtQuadFlag) VVCR_CS(SbtHorFlag) VVCR_CS(SbtPosFlag)
+  VVCR_CS(CrossCompPred) VVCR_CS(ChromaQpAdjFlag) VVCR_CS(ChromaQpAdjIdc) VVCR_CS(ImvFlag) VVCR_CS(BcwIdx) VVCR_CS(ctbAlfFlag)
+  VVCR_CS(ctbAlfAlternative) VVCR_CS(AlfUseTemporalFilt) VVCR_CS(CcAlfFilterControlFlag) VVCR_CS(CiipFlag) VVCR_CS(SmvdFlag)
+  VVCR_CS(IBCFlag) VVCR_CS(ISPMode) VVCR_CS(JointCbCrFlag)
+#undef VVCR_CS
+#undef VVCR_CSA
+  for (int k = 0; k < 4; k++) {
+    const std::vector<uint8_t> &t = ContextSetCfg::getInitTable(k);
+    char nm[24]; snprintf(nm, sizeof nm, "ctx_init%d", k);
+    T.u8(nm, t, {t.size()});
+  }
   T.close();
 }
 
