@@ -14,7 +14,7 @@ CXX      ?= g++
 CXXFLAGS  = -O3 -std=c++11 -fPIC -msse4.1 -DNDEBUG -w -pthread \
             -DENABLE_SPLIT_PARALLELISM=0 -DENABLE_WPP_PARALLELISM=0 \
             -I$(SRC)/Lib -I$(SRC)/Lib/CommonLib -I$(SRC)/Lib/CommonLib/x86 -I$(SRC)/Lib/libmd5 \
-            -I$(SRC)/Lib/DecoderLib -I$(SRC)/Lib/EncoderLib -I$(SRC)/Lib/Utilities
+            -I$(SRC)/Lib/DecoderLib -I$(SRC)/Lib/EncoderLib -I$(SRC)/Lib/Utilities $(EXTRA)
 
 COMMON_SRC = $(wildcard $(SRC)/Lib/CommonLib/*.cpp) $(wildcard $(SRC)/Lib/CommonLib/x86/*.cpp) \
              $(wildcard $(SRC)/Lib/libmd5/*.cpp)
@@ -44,6 +44,11 @@ WRAPS = $(shell cat $(CURDIR)/oracle/capture/wraps.txt 2>/dev/null)
 WRAPFLAGS = $(foreach s,$(WRAPS),-Wl,--wrap=$(s))
 
 all: apps capture rdo_kat
+
+# syntax-trace decoder (the reference's own ENABLE_TRACING / DTRACE build, TypeDef.h) for debugging the
+# host parser element by element: make -f oracle/ref.mk trace  ->  oracle/_ref/trace/DecoderApp
+trace:
+	$(MAKE) -f $(CURDIR)/oracle/ref.mk OUT=$(OUT)/trace EXTRA=-DENABLE_TRACING=1 $(OUT)/trace/DecoderApp
 apps: $(OUT)/DecoderApp $(OUT)/EncoderApp
 capture: $(OUT)/vtm_capture
 

@@ -10,6 +10,7 @@
 // collocated picture's motion) so pictures can be parsed on several threads.
 #pragma once
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -131,6 +132,9 @@ struct Cabac {
     value += byte();
     bitsNeeded = -8;
   }
+#ifdef VVCP_TRACE   // bin trace in the format of the reference's D_CABAC channel (BinDecoder.cpp:315)
+  int traceCount = 0;
+#endif
   unsigned bin(unsigned id) {   // TBinDecoder::decodeBin
     CtxModel &m = ctx[id];
     const uint8_t st = m.state();
@@ -138,6 +142,9 @@ struct Cabac {
     uint16_t q = st;
     if (q & 0x80) q ^= 0xff;
     const uint32_t lps = (((q >> 2) * (range >> 5)) >> 1) + 4;
+#ifdef VVCP_TRACE
+    fprintf(stderr, "%d %d %d  [%d:%d]  %2d(MPS=%d)    -  ", traceCount++, id, range, range - lps, lps, st, value < ((range - lps) << 7));
+#endif
     range -= lps;
     const uint32_t sr = range << 7;
     if (value < sr) {
@@ -155,14 +162,21 @@ struct Cabac {
       if (bitsNeeded >= 0) { value += byte() << bitsNeeded; bitsNeeded -= 8; }
     }
     m.update(b);
+#ifdef VVCP_TRACE
+    fprintf(stderr, "%d\n", b);
+#endif
     return b;
   }
   unsigned ep() {   // decodeBinEP
     value += value;
     if (++bitsNeeded >= 0) { value += byte(); bitsNeeded = -8; }
     const uint32_t sr = range << 7;
-    if (value >= sr) { value -= sr; return 1; }
-    return 0;
+    unsigned b = 0;
+    if (value >= sr) { value -= sr; b = 1; }
+#ifdef VVCP_TRACE
+    fprintf(stderr, "%d  %d  EP=%d \n", traceCount++, range, b);
+#endif
+    return b;
   }
   unsigned eps(unsigned n) {   // decodeBinsEP (bit-serial form, same result as the batched one)
     unsigned v = 0;

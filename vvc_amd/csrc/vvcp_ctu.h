@@ -1,0 +1,67 @@
+// vvcp_ctu.h — slice-data parser of the host parser: CABAC decoding of the coding tree units of one
+// picture into vvcr_cu / vvcr_pu / vvcr_tu rows, coefficient levels, SAO and ALF CTB parameters.
+// Restates the reference's CABACReader (DecoderLib/CABACReader.cpp), the partitioner
+// (CommonLib/UnitPartitioner.cpp), the context derivations (CommonLib/ContextModelling.{h,cpp}) and
+// the parse-time unit rules of CommonLib/UnitTools.cpp; motion vectors are not derived here
+// (vvcp_mv.cpp does that in decoding order afterwards).
+#pragma once
+#include "vvcp_ps.h"
+
+namespace vvcp {
+
+// Syntax values kept per PU that the motion derivation needs (PredictionUnit::mvd / mvdAffi / mvpIdx /
+// mmvdMergeIdx, Unit.h:378-456)
+struct PuSyntax {
+  int32_t mvd[2][2] = {{0, 0}, {0, 0}};
+  int32_t mvdAffi[2][3][2] = {{{0}}};
+  int32_t mvpIdx[2] = {255, 255};
+  int32_t mmvdMergeIdx = -1;
+};
+
+// Per-CU state the parser keeps beside the vvcr_cu row
+struct CuAux {
+  uint64_t splitSeries = 0;     // split mode per depth, 5 bits each (Partitioner::getSplitSeries)
+  int mtDepth = 0, btDepth = 0;
+  int tile = 0, slice = 0;      // tile index, independent slice index
+  int ctu = 0;                  // CTU raster address
+  bool hmvpReset = false;       // first CU of a CTU at a tile-column start (DecSlice.cpp:186-191)
+};
+
+struct PictureSyntax {
+  // geometry
+  int W = 0, H = 0, ctuLog2 = 7, ctuSize = 128, wCtu = 0, hCtu = 0, w4 = 0, h4 = 0;
+  // rows in decoding order
+  std::vector<vvcr_cu> cu;
+  std::vector<CuAux> cux;
+  std::vector<vvcr_pu> pu;
+  std::vector<PuSyntax> pux;
+  std::vector<vvcr_tu> tu;
+  std::vector<int32_t> coef;
+  // maps over 4x4 luma units: CU index per channel (-1 = not decoded)
+  std::vector<int32_t> map[2];
+  // loop-filter syntax per CTB
+  std::vector<vvcr_sao> sao;        // [nCtb][3], merges resolved at finish()
+  std::vector<uint8_t> alfEn[3], alfAlt[3], ccCtl[2];
+  std::vector<int16_t> alfFset;
+  void reset(int W, int H, int ctuLog2);
+  int cuAt(int ch, int x, int y) const;   // x, y in samples of channel ch; -1 outside / not decoded
+};
+
+// Slice-level inputs of the CTU parser
+struct SliceCtx {
+  const SPS *sps;
+  const PPS *pps;
+  const PicHeader *ph;
+  const SliceHeader *sh;
+  const ParamSets *ps;
+  int sliceIdx;
+};
+
+// Parses one slice's data into pic. rbsp/n: the slice NAL's RBSP (after the 2-byte header);
+// nal_epb: emulation-prevention positions of the NAL (entry points count them).
+void parse_slice_data(PictureSyntax &pic, const SliceCtx &sc, const uint8_t *rbsp, size_t n,
+                      const std::vector<uint32_t> &nal_epb);
+// After the last slice: SAO merge resolution and de-quantisation (SampleAdaptiveOffset.cpp:148-264)
+void finish_picture_syntax(PictureSyntax &pic, int bitDepth);
+
+}  // namespace vvcp

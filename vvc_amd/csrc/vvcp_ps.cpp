@@ -121,7 +121,7 @@ void parse_sps(Bits &b, SPS &s) {
   s.maxTLayers = (int)b.u(3) + 1;
   VVCP_CHECK(b.u(5) != 0, "sps_reserved_zero_5bits");
   skip_ptl(b, s.maxTLayers - 1);
-  VVCP_CHECK(b.flag(), "GDR is not supported");
+  b.u(1);   // gdr_enabled_flag: GDR pictures themselves are rejected at the picture header
   s.id = (int)b.u(4);
   s.chromaFormat = (int)b.u(2);
   VVCP_CHECK(s.chromaFormat != 1, "only 4:2:0 is supported");
@@ -487,6 +487,7 @@ void parse_ph(Bits &b, PicHeader &h, const ParamSets &ps) {
   h.gdr = b.flag();
   h.noOutputPrior = b.flag();
   VVCP_CHECK(h.gdr, "GDR pictures are not supported");
+  if (h.gdr) b.ue();   // recovery_poc_cnt
   h.ppsId = (int)b.ue();
   const PPS *pps = ps.pps(h.ppsId);
   VVCP_CHECK(!pps, "picture header references a missing PPS");
@@ -845,7 +846,9 @@ void parse_sh(Bits &b, SliceHeader &s, PicHeader &ph, const ParamSets &ps, int p
     const int len = (int)b.ue() + 1;
     for (int i = 0; i < nEntry; i++) s.entryPoints.push_back(b.u(len) + 1);
   }
-  b.align();   // byte_alignment(): the alignment bits are 1 then 0s; the CABAC start is the next byte
+  // byte_alignment(): alignment_bit_equal_to_one, then zero bits up to the byte boundary
+  VVCP_CHECK(b.u(1) != 1, "byte_alignment bit is not 1");
+  while (!b.aligned()) VVCP_CHECK(b.u(1) != 0, "byte_alignment zero bit is not 0");
   s.dataOffset = b.byte_pos();
 }
 

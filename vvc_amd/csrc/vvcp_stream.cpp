@@ -1,0 +1,248 @@
+// vvcp_stream.cpp — see vvcp_stream.h. Picture boundaries, POC and reference lists follow
+// DecLib::decode / xDecodeSlice (DecLib.cpp:1339-1645); the C-ABI of include/vvcp.h is at the end.
+#include "vvcp_stream.h"
+
+#include <algorithm>
+#include <cstring>
+
+#include "vvcp.h"
+
+namespace vvcp {
+
+namespace {
+// DecLib.cpp:1535-1642 (checkLDC, SMVD reference pair) and Slice::constructRefPicList (Slice.cpp:414)
+void derive_refs(SliceHeader &s) {
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < VVCR_MAX_REF; i++) { s.refPoc[l][i] = 0; s.refLT[l][i] = false; }
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < s.numRef[l]; i++) {
+      VVCP_CHECK(i >= s.rpl[l].num, "active reference beyond the list");
+      VVCP_CHECK(s.rpl[l].isLT[i], "long-term references are not supported");
+      s.refPoc[l][i] = s.poc - s.rpl[l].ident[i];
+      s.refLT[l][i] = false;
+    }
+  s.checkLDC = false;
+  s.biDirPred = false;
+  s.symRefIdx[0] = s.symRefIdx[1] = -1;
+  if (s.isIntra()) return;
+  bool low = true;
+  for (int i = 0; i < s.numRef[0] && low; i++)
+    if (s.refPoc[0][i] > s.poc) low = false;
+  if (s.isInterB())
+    for (int i = 0; i < s.numRef[1] && low; i++)
+      if (s.refPoc[1][i] > s.poc) low = false;
+  s.checkLDC = low;
+}
+void derive_smvd(SliceHeader &s, const SPS &sps, const PicHeader &ph) {
+  if (!(sps.smvd && !s.checkLDC && !ph.mvdL1Zero)) return;
+  const int cur = s.poc;
+  int fwd = cur, bwd = cur, r0 = -1, r1 = -1;
+  for (int r = 0; r < s.numRef[0]; r++) {
+    const int poc = s.refPoc[0][r];
+    if (poc < cur && (poc > fwd || r0 == -1) && !s.refLT[0][r]) { fwd = poc; r0 = r; }
+  }
+  for (int r = 0; r < s.numRef[1]; r++) {
+    const int poc = s.refPoc[1][r];
+    if (poc > cur && (poc < bwd || r1 == -1) && !s.refLT[1][r]) { bwd = poc; r1 = r; }
+  }
+  if (!(fwd < cur && bwd > cur)) {
+    fwd = bwd = cur;
+    r0 = r1 = -1;
+    for (int r = 0; r < s.numRef[0]; r++) {
+      const int poc = s.refPoc[0][r];
+      if (poc > cur && (poc < bwd || r0 == -1) && !s.refLT[0][r]) { bwd = poc; r0 = r; }
+    }
+    for (int r = 0; r < s.numRef[1]; r++) {
+      const int poc = s.refPoc[1][r];
+      if (poc < cur && (poc > fwd || r1 == -1) && !s.refLT[1][r]) { fwd = poc; r1 = r; }
+    }
+  }
+  if (fwd < cur && bwd > cur) { s.biDirPred = true; s.symRefIdx[0] = r0; s.symRefIdx[1] = r1; }
+}
+}  // namespace
+
+void Stream::open(const uint8_t *d, size_t n) {
+  data.assign(d, d + n);
+  nals = split_annexb(data.data(), data.size());
+  ParamSets ps;
+  PicHeader ph;
+  int prevTid0Poc = 0;
+  PictureUnit *cur = nullptr;
+  for (size_t k = 0; k < nals.size(); k++) {
+    Nal &nal = nals[k];
+    if (is_vcl(nal.type)) {   // trailing cabac_zero_words (NALread.cpp:89)
+      while (!nal.rbsp.empty() && nal.rbsp.back() == 0) nal.rbsp.pop_back();
+    }
+    Bits b(nal.rbsp.data(), nal.rbsp.size());
+    switch (nal.type) {
+      case NAL_SPS:
+      case NAL_PPS: {
+        if (nal.type == NAL_SPS) { SPS s; parse_sps(b, s); ps.spsMap[s.id] = s; }
+        else { PPS p; parse_pps(b, p); ps.ppsMap[p.id] = p; }
+        for (auto &kv : ps.ppsMap) {   // tile layout needs the CTU size of the referenced SPS
+          const SPS *sps = ps.sps(kv.second.spsId);
+          if (sps) finalize_pps(kv.second, *sps);
+        }
+        break;
+      }
+      case NAL_PREFIX_APS:
+      case NAL_SUFFIX_APS: {
+        APS a;
+        parse_aps(b, a);
+        a.tid = nal.tid;
+        if (a.type == 0) { VVCP_CHECK(a.id > 7, "bad ALF APS id"); ps.alfAps[a.id] = a; ps.alfValid[a.id] = true; }
+        else { VVCP_CHECK(a.id > 3, "bad LMCS APS id"); ps.lmcsAps[a.id] = a; ps.lmcsValid[a.id] = true; }
+        break;
+      }
+      case NAL_PH:
+        parse_ph(b, ph, ps);
+        cur = nullptr;   // next slice starts a new picture
+        break;
+      default:
+        if (nal.type <= NAL_GDR && is_vcl(nal.type)) {
+          SliceHeader sh;
+          sh.nalType = nal.type;
+          sh.tid = nal.tid;
+          const bool phInSh = nal.rbsp.size() > 0 && (nal.rbsp[0] & 0x80);
+          if (phInSh) cur = nullptr;
+          parse_sh(b, sh, ph, ps, prevTid0Poc);
+          const PPS *pps = ps.pps(ph.ppsId);
+          const SPS *sps = ps.sps(pps->spsId);
+          if (!cur) {
+            pics.emplace_back(new PictureUnit());
+            cur = pics.back().get();
+            cur->poc = sh.poc;
+            cur->nalType = nal.type;
+            cur->tid = nal.tid;
+            cur->sps = *sps;
+            cur->pps = *pps;
+            cur->ph = ph;
+            for (int i = 0; i < 8; i++) { cur->alfAps[i] = ps.alfAps[i]; cur->alfValid[i] = ps.alfValid[i]; }
+            for (int i = 0; i < 4; i++) { cur->lmcsAps[i] = ps.lmcsAps[i]; cur->lmcsValid[i] = ps.lmcsValid[i]; }
+          }
+          VVCP_CHECK(sh.poc != cur->poc, "slices of one picture with different POC");
+          derive_refs(sh);
+          derive_smvd(sh, cur->sps, cur->ph);
+          sh.indepSliceIdx = (int)cur->slices.size();
+          cur->slices.push_back(sh);
+          cur->sliceNal.push_back((int)k);
+          if (nal.tid == 0 && nal.type != NAL_RASL && nal.type != NAL_RADL) prevTid0Poc = sh.poc;   // DecLib.h:209
+        }
+        break;
+    }
+  }
+}
+
+void Stream::parse_picture(int idx) {
+  PictureUnit &p = *pics.at(idx);
+  if (p.parsed) {
+    VVCP_CHECK(p.failed, "picture failed to parse");
+    return;
+  }
+  p.syn.reset(p.pps.width, p.pps.height, p.sps.ctuLog2);
+  ParamSets ps;
+  for (int i = 0; i < 8; i++) { ps.alfAps[i] = p.alfAps[i]; ps.alfValid[i] = p.alfValid[i]; }
+  for (int i = 0; i < 4; i++) { ps.lmcsAps[i] = p.lmcsAps[i]; ps.lmcsValid[i] = p.lmcsValid[i]; }
+  try {
+    for (size_t s = 0; s < p.slices.size(); s++) {
+      const Nal &nal = nals[p.sliceNal[s]];
+      SliceCtx sc{&p.sps, &p.pps, &p.ph, &p.slices[s], &ps, (int)s};
+      parse_slice_data(p.syn, sc, nal.rbsp.data(), nal.rbsp.size(), nal.epb);
+    }
+  } catch (...) {
+    p.parsed = true;   // the rows parsed so far stay readable (diagnostics)
+    p.failed = true;
+    throw;
+  }
+  finish_picture_syntax(p.syn, p.sps.bitDepth);
+  p.parsed = true;
+}
+
+}  // namespace vvcp
+
+// ================================================================================================
+// C-ABI (include/vvcp.h)
+// ================================================================================================
+struct vvcp_stream {
+  vvcp::Stream s;
+  std::string err;
+  std::mutex mu;
+};
+
+static thread_local std::string g_vvcp_err;
+
+#define VVCP_API_BEGIN try {
+#define VVCP_API_END                                              \
+  }                                                               \
+  catch (const std::exception &e) {                               \
+    g_vvcp_err = e.what();                                        \
+    return VVCR_E_UNSUPPORTED;                                    \
+  }
+
+extern "C" {
+
+int vvcp_open(const uint8_t *data, size_t n, vvcp_stream **out) {
+  if (!data || !out) return VVCR_E_ARG;
+  *out = nullptr;
+  VVCP_API_BEGIN
+  std::unique_ptr<vvcp_stream> h(new vvcp_stream());
+  h->s.open(data, n);
+  *out = h.release();
+  return VVCR_OK;
+  VVCP_API_END
+}
+
+int vvcp_close(vvcp_stream *h) {
+  delete h;
+  return VVCR_OK;
+}
+
+const char *vvcp_last_error(void) { return g_vvcp_err.c_str(); }
+
+int vvcp_num_pictures(const vvcp_stream *h) { return h ? (int)h->s.pics.size() : VVCR_E_ARG; }
+
+int vvcp_picture_info(const vvcp_stream *h, int32_t idx, int32_t *info, int32_t n) {
+  if (!h || !info || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
+  const vvcp::PictureUnit &p = *h->s.pics[idx];
+  const int32_t v[] = {p.poc, p.slices.empty() ? 2 : p.slices[0].sliceType, p.pps.width, p.pps.height, p.sps.ctuLog2,
+                       p.sps.bitDepth, (int32_t)p.slices.size(), p.tid, p.nalType, p.slices.empty() ? 0 : p.slices[0].qp};
+  const int m = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < n && i < m; i++) info[i] = v[i];
+  return m;
+}
+
+int vvcp_parse_picture(vvcp_stream *h, int32_t idx) {
+  if (!h || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
+  VVCP_API_BEGIN
+  h->s.parse_picture(idx);
+  return VVCR_OK;
+  VVCP_API_END
+}
+
+int64_t vvcp_picture_rows(const vvcp_stream *h, int32_t idx, int32_t what, void *dst, int64_t cap) {
+  if (!h || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
+  const vvcp::PictureUnit &p = *h->s.pics[idx];
+  if (!p.parsed) return VVCR_E_STATE;
+  const vvcp::PictureSyntax &s = p.syn;
+  const void *src = nullptr;
+  int64_t count = 0, esz = 0;
+  switch (what) {
+    case VVCP_ROWS_CU: src = s.cu.data(); count = (int64_t)s.cu.size(); esz = sizeof(vvcr_cu); break;
+    case VVCP_ROWS_PU: src = s.pu.data(); count = (int64_t)s.pu.size(); esz = sizeof(vvcr_pu); break;
+    case VVCP_ROWS_TU: src = s.tu.data(); count = (int64_t)s.tu.size(); esz = sizeof(vvcr_tu); break;
+    case VVCP_ROWS_COEF: src = s.coef.data(); count = (int64_t)s.coef.size(); esz = 4; break;
+    case VVCP_ROWS_SAO: src = s.sao.data(); count = (int64_t)s.sao.size(); esz = sizeof(vvcr_sao); break;
+    case VVCP_ROWS_ALF_EN0: case VVCP_ROWS_ALF_EN0 + 1: case VVCP_ROWS_ALF_EN0 + 2:
+      src = s.alfEn[what - VVCP_ROWS_ALF_EN0].data(); count = (int64_t)s.alfEn[0].size(); esz = 1; break;
+    case VVCP_ROWS_ALF_ALT0: case VVCP_ROWS_ALF_ALT0 + 1: case VVCP_ROWS_ALF_ALT0 + 2:
+      src = s.alfAlt[what - VVCP_ROWS_ALF_ALT0].data(); count = (int64_t)s.alfAlt[0].size(); esz = 1; break;
+    case VVCP_ROWS_ALF_FSET: src = s.alfFset.data(); count = (int64_t)s.alfFset.size(); esz = 2; break;
+    case VVCP_ROWS_CCALF0: case VVCP_ROWS_CCALF0 + 1:
+      src = s.ccCtl[what - VVCP_ROWS_CCALF0].data(); count = (int64_t)s.ccCtl[0].size(); esz = 1; break;
+    default: return VVCR_E_ARG;
+  }
+  if (dst && cap > 0) std::memcpy(dst, src, (size_t)(std::min(cap, count) * esz));
+  return count;
+}
+
+}  // extern "C"

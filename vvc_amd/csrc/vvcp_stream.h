@@ -1,0 +1,34 @@
+// vvcp_stream.h — stream-level state of the host parser: NAL units, parameter sets and the pictures of
+// an Annex-B VVC (VTM-7.3 draft) bitstream in decoding order (DecLib::decode / xActivateParameterSets /
+// xDecodeSlice, DecoderLib/DecLib.cpp). Header parsing is serial; the CABAC pass of each picture
+// (parse_picture) only reads its own slices and may run on any thread.
+#pragma once
+#include <memory>
+#include <mutex>
+
+#include "vvcp_ctu.h"
+
+namespace vvcp {
+
+struct PictureUnit {
+  int poc = 0, nalType = 0, tid = 0;
+  SPS sps;
+  PPS pps;
+  PicHeader ph;
+  std::vector<SliceHeader> slices;
+  std::vector<int> sliceNal;      // index into Stream::nals
+  APS alfAps[8], lmcsAps[4];      // APS content at the time the picture is decoded
+  bool alfValid[8] = {false}, lmcsValid[4] = {false};
+  PictureSyntax syn;
+  bool parsed = false, failed = false;
+};
+
+struct Stream {
+  std::vector<uint8_t> data;
+  std::vector<Nal> nals;
+  std::vector<std::unique_ptr<PictureUnit>> pics;
+  void open(const uint8_t *d, size_t n);   // splits NALs and parses every header
+  void parse_picture(int idx);             // CABAC pass (thread-safe across different idx)
+};
+
+}  // namespace vvcp

@@ -1,0 +1,98 @@
+"""Host bitstream parser of libvvcr (include/vvcp.h) through ctypes.
+
+Stream(data) opens an Annex-B VVC bitstream (all NAL units and headers are read at once); parse(i)
+runs the CABAC pass of picture i (decoding order) and rows(i) returns its descriptor rows as numpy
+arrays shaped like the capture records (vvc_amd/capfile.py): cu (N, 40), pu (N, 48), tu (N, 33) int32,
+coef, sao (n_ctb, 3, 35) and the ALF CTB arrays.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import native as N
+
+ROWS_CU, ROWS_PU, ROWS_TU, ROWS_COEF, ROWS_SAO = 0, 1, 2, 3, 4
+ROWS_ALF_EN0, ROWS_ALF_ALT0, ROWS_ALF_FSET, ROWS_CCALF0 = 5, 8, 11, 12
+
+_P, _I32, _I64 = C.c_void_p, C.c_int32, C.c_int64
+
+
+def _bind(lib):
+    if getattr(lib, "_vvcp_bound", False):
+        return lib
+    lib.vvcp_open.argtypes = [C.c_char_p, C.c_size_t, C.POINTER(_P)]
+    lib.vvcp_open.restype = C.c_int
+    lib.vvcp_close.argtypes = [_P]
+    lib.vvcp_last_error.restype = C.c_char_p
+    lib.vvcp_num_pictures.argtypes = [_P]
+    lib.vvcp_picture_info.argtypes = [_P, _I32, C.POINTER(_I32), _I32]
+    lib.vvcp_parse_picture.argtypes = [_P, _I32]
+    lib.vvcp_picture_rows.argtypes = [_P, _I32, _I32, _P, _I64]
+    lib.vvcp_picture_rows.restype = _I64
+    lib._vvcp_bound = True
+    return lib
+
+
+class ParseError(RuntimeError):
+    pass
+
+
+class Stream:
+    def __init__(self, data, lib=None):
+        self.lib = _bind(lib or N.lib())
+        self._data = bytes(data)
+        h = _P()
+        rc = self.lib.vvcp_open(self._data, len(self._data), C.byref(h))
+        if rc != 0:
+            raise ParseError("vvcp_open: %s" % self.lib.vvcp_last_error().decode())
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.vvcp_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return self.lib.vvcp_num_pictures(self.h)
+
+    def info(self, i):
+        v = (_I32 * 10)()
+        self.lib.vvcp_picture_info(self.h, i, v, 10)
+        keys = ("poc", "slice_type", "width", "height", "ctu_log2", "bit_depth", "num_slices", "tid", "nal_type", "slice_qp")
+        return dict(zip(keys, list(v)))
+
+    def parse(self, i):
+        rc = self.lib.vvcp_parse_picture(self.h, i)
+        if rc != 0:
+            raise ParseError("picture %d: %s" % (i, self.lib.vvcp_last_error().decode()))
+
+    def _rows(self, i, what, dtype, shape_tail):
+        n = self.lib.vvcp_picture_rows(self.h, i, what, None, 0)
+        if n < 0:
+            raise ParseError("rows: %d" % n)
+        esz = int(np.prod(shape_tail)) if shape_tail else 1
+        out = np.zeros((n * esz,), dtype)
+        if n:
+            self.lib.vvcp_picture_rows(self.h, i, what, out.ctypes.data, n)
+        return out.reshape((n,) + tuple(shape_tail)) if shape_tail else out
+
+    def rows(self, i):
+        r = {
+            "cu": self._rows(i, ROWS_CU, np.int32, (40,)),
+            "pu": self._rows(i, ROWS_PU, np.int32, (48,)),
+            "tu": self._rows(i, ROWS_TU, np.int32, (33,)),
+            "coef": self._rows(i, ROWS_COEF, np.int32, ()),
+            "sao": self._rows(i, ROWS_SAO, np.int32, (35,)),
+            "alf_ctb_fidx": self._rows(i, ROWS_ALF_FSET, np.int16, ()),
+        }
+        r["sao"] = r["sao"].reshape(-1, 3, 35)
+        r["alf_ctb_en"] = np.stack([self._rows(i, ROWS_ALF_EN0 + c, np.uint8, ()) for c in range(3)])
+        r["alf_ctb_alt"] = np.stack([self._rows(i, ROWS_ALF_ALT0 + c, np.uint8, ()) for c in range(3)])
+        r["ccalf_ctl"] = np.stack([self._rows(i, ROWS_CCALF0 + c, np.uint8, ()) for c in range(2)])
+        return r
