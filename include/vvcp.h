@@ -34,8 +34,20 @@ int vvcp_num_pictures(const vvcp_stream *s);
 int vvcp_picture_info(const vvcp_stream *s, int32_t idx, int32_t *info, int32_t n);
 int vvcp_parse_picture(vvcp_stream *s, int32_t idx);
 
+/* Motion derivation of a parsed picture (DecCu::xDeriveCUMV, DecCu.cpp:878, with the merge / AMVP /
+ * affine / SbTMVP / GEO / MMVD candidate tools of UnitTools.cpp and the history table): fills the MV
+ * fields of its vvcr_cu / vvcr_pu rows, the 4x4 motion field and the GEO rows. Pictures must be derived
+ * in decoding order, and every earlier picture must have been refined (vvcp_refine_motion) first, since
+ * it may be the collocated reference. */
+int vvcp_derive_motion(vvcp_stream *s, int32_t idx);
+/* CS::setRefinedMotionField (UnitTools.cpp:68): records the motion of a derived picture as later
+ * pictures' temporal candidates see it, with the DMVR deltas of its PUs (vvcr_get_dmvr_deltas layout:
+ * n (dx, dy) pairs, PUs with pu.dmvr in row order, 16x16 sub-blocks in raster order). deltas may be
+ * NULL when no PU of the picture refines. */
+int vvcp_refine_motion(vvcp_stream *s, int32_t idx, const int32_t *deltas, int64_t n);
+
 /* Parsed rows of a picture (after vvcp_parse_picture): copies min(cap, count) entries to dst (dst may be
- * NULL) and returns count. Motion vectors of vvcr_pu are not derived by the parse pass. */
+ * NULL) and returns count. MV fields of vvcr_cu / vvcr_pu hold parsed values until vvcp_derive_motion. */
 #define VVCP_ROWS_CU 0        /* vvcr_cu */
 #define VVCP_ROWS_PU 1        /* vvcr_pu */
 #define VVCP_ROWS_TU 2        /* vvcr_tu */
@@ -45,6 +57,8 @@ int vvcp_parse_picture(vvcp_stream *s, int32_t idx);
 #define VVCP_ROWS_ALF_ALT0 8  /* uint8 [n_ctb], components 0..2 at 8..10 */
 #define VVCP_ROWS_ALF_FSET 11 /* int16 [n_ctb] luma filter set */
 #define VVCP_ROWS_CCALF0 12   /* uint8 [n_ctb], Cb at 12, Cr at 13 */
+#define VVCP_ROWS_MOTION 14   /* vvcr_motion [h/4][w/4] (after vvcp_derive_motion) */
+#define VVCP_ROWS_GEO 15      /* vvcr_geo (after vvcp_derive_motion) */
 int64_t vvcp_picture_rows(const vvcp_stream *s, int32_t idx, int32_t what, void *dst, int64_t cap);
 
 #ifdef __cplusplus

@@ -3,9 +3,12 @@
 Every picture of the golden streams is parsed from the .bin and its rows are compared field by field
 with tests/golden/<stream>/pic_NNN.xz (the reference's CodingStructure after DecLib decoded the
 picture, oracle/capture/vtm_capture.cpp): CU / PU / TU rows, coefficient levels, SAO parameters
-(merges resolved) and ALF / CC-ALF CTB syntax. Fields that depend on motion derivation (DecCu::
-xDeriveCUMV) are excluded until the derivation runs in the parser; the LMCS chroma scale of a TU
-(computed by DecCu) likewise. Bit-exact: integer syntax, no tolerance.
+(merges resolved) and ALF / CC-ALF CTB syntax. Motion is derived in decoding order (vvcp_derive_motion:
+merge / AMVP / affine / SbTMVP / GEO / MMVD / history candidates, TMVP from the refined field of the
+collocated picture) and compared too: the MV fields of the rows, the 4x4 motion field and the GEO
+candidate rows. The DMVR refinements that feed later pictures' temporal candidates are the capture's
+own (dmvr_delta) here; tests/test_decode_gpu.py closes that loop with the GPU's. The LMCS chroma
+scale of a TU (computed by DecCu) is not a parser output. Bit-exact: integer syntax, no tolerance.
 """
 import glob
 import os
@@ -22,20 +25,16 @@ PU_F = ("cu x y w h cx cy cw ch chtype idir_l idir_c fidir_l fidir_c mipt mrl me
         "interdir mv0x mv0y mv1x mv1y ref0 ref1 mrgtype mvrefine ciip").split() + ["aff%d" % i for i in range(12)] + [
         "dmvr_off", "bdof", "dmvr"]
 TU_F = "cu chtype depth noresi jccr cadj".split() + ["%s%d" % (f, c) for c in range(3) for f in "x y w h cbf mts coff qp qpts".split()]
-CU_MV = {"imv", "bcw", "affinetype"}
-PU_MV = {"interdir", "mv0x", "mv0y", "mv1x", "mv1y", "ref0", "ref1", "mrgtype", "mvrefine", "mergeidx", "dmvr_off", "bdof",
-         "dmvr"} | {"aff%d" % k for k in range(12)}
 
 
 def _cols(fields, mask):
     return [i for i, f in enumerate(fields) if f not in mask]
 
 
-def compare_picture(rows, cap, intra):
+def compare_picture(rows, cap):
     """Returns a list of mismatch descriptions (empty = identical)."""
     out = []
-    for name, fields, mask in (("cu", CU_F, set() if intra else CU_MV), ("pu", PU_F, set() if intra else PU_MV),
-                               ("tu", TU_F, {"cadj"})):
+    for name, fields, mask in (("cu", CU_F, set()), ("pu", PU_F, set()), ("tu", TU_F, {"cadj"})):
         a, b = rows[name], cap[name]
         if a.shape != b.shape:
             out.append("%s shape %s vs %s" % (name, a.shape, b.shape))
@@ -56,6 +55,17 @@ def compare_picture(rows, cap, intra):
     for c, key in enumerate(("ccalf_en_cb", "ccalf_en_cr")):   # the capture's array is stale when CC-ALF is off
         if cap["hdr"].get(key) and not np.array_equal(rows["ccalf_ctl"][c], cap["ccalf_ctl"][c]):
             out.append("ccalf_ctl[%d]" % c)
+    if "motion" in rows:
+        if rows["motion"].shape != cap["motion"].shape:
+            out.append("motion shape")
+        else:
+            d = np.argwhere(rows["motion"] != cap["motion"])
+            if len(d):
+                out.append("motion at 4x4 (%d,%d) field %d (%d diffs)" % (d[0][1], d[0][0], d[0][2], len(d)))
+        g = cap["geo"]   # captured in reconstruction order; the parser emits CU order
+        g = g[np.argsort(g[:, 0], kind="stable")] if len(g) else g
+        if not np.array_equal(rows["geo"], g):
+            out.append("geo")
     return out
 
 
@@ -75,8 +85,25 @@ def test_parser_matches_capture(stream):
         assert info["poc"] == cap["hdr"]["poc"]
         assert info["slice_type"] == cap["hdr"]["slice_type"]
         s.parse(i)
-        bad = compare_picture(s.rows(i), cap, info["slice_type"] == 2)
+        s.derive(i)
+        s.refine(i, cap["dmvr_delta"])
+        bad = compare_picture(s.rows(i), cap)
         assert not bad, "%s picture %d (POC %d): %s" % (stream, i, info["poc"], "; ".join(bad))
+
+
+def test_motion_needs_order():
+    """The collocated picture must be refined before a picture that reads it is derived."""
+    data = open(os.path.join(ROOT, "streams", "ra416_q32.bin"), "rb").read()
+    s = parser.Stream(data)
+    s.parse(0)
+    s.parse(1)
+    with pytest.raises(parser.ParseError):
+        s.derive(1)             # POC 16 reads POC 0's motion, which is not refined yet
+    with pytest.raises(parser.ParseError):
+        s.refine(0)             # not derived
+    s.derive(0)
+    s.refine(0)
+    s.derive(1)
 
 
 def test_parser_rejects_garbage():

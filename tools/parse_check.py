@@ -34,6 +34,7 @@ def main():
     ap.add_argument("stream")
     ap.add_argument("--lib")
     ap.add_argument("--pics", type=int, default=0)
+    ap.add_argument("--no-mv", action="store_true", help="skip motion derivation (syntax fields only)")
     args = ap.parse_args()
     lib = C.CDLL(args.lib) if args.lib else None
     root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden")
@@ -66,10 +67,33 @@ def main():
             ok = False
             break
         msgs = []
-        mvmask = {"imv", "bcw", "affinetype"} if info["slice_type"] != 2 else set()
+        mvmask = set()
+        pumask = set()
+        if args.no_mv and info["slice_type"] != 2:
+            mvmask = {"imv", "bcw", "affinetype"}
+            pumask = {"interdir", "mv0x", "mv0y", "mv1x", "mv1y", "ref0", "ref1", "mrgtype", "mvrefine", "mergeidx", "dmvr_off", "bdof", "dmvr"} | {"aff%d" % k for k in range(12)}
+        else:
+            try:
+                s.derive(i)
+                s.refine(i, cap["dmvr_delta"])
+            except parser.ParseError as e:
+                msgs.append(str(e))
+            r = s.rows(i)
+            if "motion" in r:
+                mo, mc = r["motion"], cap["motion"]
+                if mo.shape != mc.shape:
+                    msgs.append("motion shape %s vs %s" % (mo.shape, mc.shape))
+                else:
+                    d = np.argwhere(mo != mc)
+                    if len(d):
+                        y, x, f = d[0]
+                        msgs.append("motion (%d,%d) field %d: ours %s cap %s (%d diffs)" % (x * 4, y * 4, f, mo[y, x].tolist(), mc[y, x].tolist(), len(d)))
+                cg = cap["geo"][np.argsort(cap["geo"][:, 0], kind="stable")] if len(cap["geo"]) else cap["geo"]
+                if not np.array_equal(r["geo"], cg):
+                    g = r["geo"]
+                    msgs.append("geo differs: %d vs %d rows; first ours %s cap %s" % (len(g), len(cg), g[:1].tolist(), cg[:1].tolist()))
         m = first_diff("cu", r["cu"], cap["cu"], CU_F, mvmask)
         if m: msgs.append(m)
-        pumask = {"interdir", "mv0x", "mv0y", "mv1x", "mv1y", "ref0", "ref1", "mrgtype", "mvrefine", "mergeidx", "dmvr_off", "bdof", "dmvr"} | {"aff%d" % k for k in range(12)}
         m = first_diff("pu", r["pu"], cap["pu"], PU_F, pumask)
         if m: msgs.append(m)
         m = first_diff("tu", r["tu"], cap["tu"], TU_F, {"cadj"})

@@ -1,0 +1,52 @@
+// vvcp_mv.h — motion derivation of the host parser: turns the parsed inter syntax of a picture into
+// motion vectors, reference indices and the 4x4 motion field (DecCu::xDeriveCUMV DecCu.cpp:878 and the
+// PU:: candidate-list tools of CommonLib/UnitTools.cpp), in decoding order, CU by CU, with the
+// history-based candidate table (CodingStructure::addMiToLut) and the collocated picture's motion.
+#pragma once
+#include <vector>
+
+#include "vvcp_ctu.h"
+
+namespace vvcp {
+
+// MotionInfo (MotionInfo.h:101) of one 4x4 luma unit
+struct Mi {
+  bool isInter = false;
+  int8_t interDir = 0;
+  bool altHpel = false;
+  uint8_t bcw = 0;
+  uint16_t slice = 0;
+  int16_t ref[2] = {-1, -1};
+  int32_t mv[2][2] = {{0, 0}, {0, 0}};
+  bool same(const Mi &o) const;   // MotionInfo::operator==
+};
+
+// Reference structure of one slice of a picture (what getColocatedMVP reads of the collocated picture)
+struct SliceRefs {
+  int refPoc[2][VVCR_MAX_REF];
+  bool refLT[2][VVCR_MAX_REF];
+};
+
+// Motion of a decoded picture as later pictures' temporal candidates see it: the 4x4 field after
+// CS::setRefinedMotionField (UnitTools.cpp:68), i.e. with the DMVR refinements written back.
+struct MotionPicture {
+  int poc = 0, w4 = 0, h4 = 0;
+  std::vector<Mi> mf;
+  std::vector<SliceRefs> slices;
+};
+
+struct PictureUnit;
+
+// Derives the motion of picture p (all slices), given the already decoded pictures (for the collocated
+// reference, looked up by POC). Fills the MV-dependent fields of p.syn's rows, the 4x4 field (pre-DMVR,
+// as deblocking reads it) and the GEO candidate rows; returns the 4x4 field in `field`.
+void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb, std::vector<Mi> &field,
+                   std::vector<vvcr_motion> &motionRows, std::vector<vvcr_geo> &geoRows);
+
+// CS::setRefinedMotionField: the collocated-reference view of p, given its pre-DMVR field and the
+// DMVR deltas of its PUs (vvcr_get_dmvr_deltas order: PUs with pu.dmvr in row order, 16x16 sub-blocks
+// in raster order). deltas may be null when no PU of the picture uses DMVR.
+void refine_motion(const PictureUnit &p, const std::vector<Mi> &field, const int32_t *deltas, int64_t ndeltas,
+                   MotionPicture &out);
+
+}  // namespace vvcp

@@ -158,6 +158,27 @@ void Stream::parse_picture(int idx) {
   p.parsed = true;
 }
 
+void Stream::derive_motion(int idx) {
+  PictureUnit &p = *pics.at(idx);
+  VVCP_CHECK(!p.parsed || p.failed, "picture not parsed");
+  if (p.derived) return;
+  std::vector<const MotionPicture *> dpb;
+  for (int i = std::max(0, idx - 64); i < idx; i++)
+    if (pics[i]->refined) dpb.push_back(pics[i]->refined.get());
+  vvcp::derive_motion(p, dpb, p.field, p.motion, p.geo);
+  p.derived = true;
+}
+
+void Stream::refine_motion(int idx, const int32_t *deltas, int64_t n) {
+  PictureUnit &p = *pics.at(idx);
+  VVCP_CHECK(!p.derived, "picture motion not derived");
+  std::unique_ptr<MotionPicture> m(new MotionPicture());
+  vvcp::refine_motion(p, p.field, deltas, n, *m);
+  p.refined = std::move(m);
+  // pictures far behind in decoding order are no longer collocated candidates
+  if (idx >= 64 && pics[idx - 64]->refined) pics[idx - 64]->refined.reset();
+}
+
 }  // namespace vvcp
 
 // ================================================================================================
@@ -219,6 +240,22 @@ int vvcp_parse_picture(vvcp_stream *h, int32_t idx) {
   VVCP_API_END
 }
 
+int vvcp_derive_motion(vvcp_stream *h, int32_t idx) {
+  if (!h || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
+  VVCP_API_BEGIN
+  h->s.derive_motion(idx);
+  return VVCR_OK;
+  VVCP_API_END
+}
+
+int vvcp_refine_motion(vvcp_stream *h, int32_t idx, const int32_t *deltas, int64_t n) {
+  if (!h || idx < 0 || idx >= (int)h->s.pics.size() || n < 0) return VVCR_E_ARG;
+  VVCP_API_BEGIN
+  h->s.refine_motion(idx, deltas, n);
+  return VVCR_OK;
+  VVCP_API_END
+}
+
 int64_t vvcp_picture_rows(const vvcp_stream *h, int32_t idx, int32_t what, void *dst, int64_t cap) {
   if (!h || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
   const vvcp::PictureUnit &p = *h->s.pics[idx];
@@ -239,6 +276,12 @@ int64_t vvcp_picture_rows(const vvcp_stream *h, int32_t idx, int32_t what, void 
     case VVCP_ROWS_ALF_FSET: src = s.alfFset.data(); count = (int64_t)s.alfFset.size(); esz = 2; break;
     case VVCP_ROWS_CCALF0: case VVCP_ROWS_CCALF0 + 1:
       src = s.ccCtl[what - VVCP_ROWS_CCALF0].data(); count = (int64_t)s.ccCtl[0].size(); esz = 1; break;
+    case VVCP_ROWS_MOTION:
+      if (!p.derived) return VVCR_E_STATE;
+      src = p.motion.data(); count = (int64_t)p.motion.size(); esz = sizeof(vvcr_motion); break;
+    case VVCP_ROWS_GEO:
+      if (!p.derived) return VVCR_E_STATE;
+      src = p.geo.data(); count = (int64_t)p.geo.size(); esz = sizeof(vvcr_geo); break;
     default: return VVCR_E_ARG;
   }
   if (dst && cap > 0) std::memcpy(dst, src, (size_t)(std::min(cap, count) * esz));

@@ -7,6 +7,7 @@
 #include <mutex>
 
 #include "vvcp_ctu.h"
+#include "vvcp_mv.h"
 
 namespace vvcp {
 
@@ -21,6 +22,12 @@ struct PictureUnit {
   bool alfValid[8] = {false}, lmcsValid[4] = {false};
   PictureSyntax syn;
   bool parsed = false, failed = false;
+  // motion (derive_motion): the 4x4 field before DMVR, its row form and the GEO candidate rows
+  std::vector<Mi> field;
+  std::vector<vvcr_motion> motion;
+  std::vector<vvcr_geo> geo;
+  bool derived = false;
+  std::unique_ptr<MotionPicture> refined;   // set by refine_motion; read as a collocated picture
 };
 
 struct Stream {
@@ -29,6 +36,10 @@ struct Stream {
   std::vector<std::unique_ptr<PictureUnit>> pics;
   void open(const uint8_t *d, size_t n);   // splits NALs and parses every header
   void parse_picture(int idx);             // CABAC pass (thread-safe across different idx)
+  // Motion derivation of picture idx; every picture it may use as collocated reference (any earlier
+  // picture in decoding order) must have been refined already.
+  void derive_motion(int idx);
+  void refine_motion(int idx, const int32_t *deltas, int64_t n);
 };
 
 }  // namespace vvcp

@@ -3,7 +3,9 @@
 Stream(data) opens an Annex-B VVC bitstream (all NAL units and headers are read at once); parse(i)
 runs the CABAC pass of picture i (decoding order) and rows(i) returns its descriptor rows as numpy
 arrays shaped like the capture records (vvc_amd/capfile.py): cu (N, 40), pu (N, 48), tu (N, 33) int32,
-coef, sao (n_ctb, 3, 35) and the ALF CTB arrays.
+coef, sao (n_ctb, 3, 35) and the ALF CTB arrays. derive(i) then resolves the motion of picture i
+(decoding order; every earlier picture refined first) and refine(i, deltas) records its motion after
+DMVR for later pictures' temporal candidates; rows(i) then also holds motion (h/4, w/4, 10) and geo.
 """
 import ctypes as C
 
@@ -13,6 +15,7 @@ from . import native as N
 
 ROWS_CU, ROWS_PU, ROWS_TU, ROWS_COEF, ROWS_SAO = 0, 1, 2, 3, 4
 ROWS_ALF_EN0, ROWS_ALF_ALT0, ROWS_ALF_FSET, ROWS_CCALF0 = 5, 8, 11, 12
+ROWS_MOTION, ROWS_GEO = 14, 15
 
 _P, _I32, _I64 = C.c_void_p, C.c_int32, C.c_int64
 
@@ -29,6 +32,8 @@ def _bind(lib):
     lib.vvcp_parse_picture.argtypes = [_P, _I32]
     lib.vvcp_picture_rows.argtypes = [_P, _I32, _I32, _P, _I64]
     lib.vvcp_picture_rows.restype = _I64
+    lib.vvcp_derive_motion.argtypes = [_P, _I32]
+    lib.vvcp_refine_motion.argtypes = [_P, _I32, _P, _I64]
     lib._vvcp_bound = True
     return lib
 
@@ -72,6 +77,17 @@ class Stream:
         if rc != 0:
             raise ParseError("picture %d: %s" % (i, self.lib.vvcp_last_error().decode()))
 
+    def derive(self, i):
+        rc = self.lib.vvcp_derive_motion(self.h, i)
+        if rc != 0:
+            raise ParseError("picture %d motion: %s" % (i, self.lib.vvcp_last_error().decode()))
+
+    def refine(self, i, deltas=None):
+        d = None if deltas is None or len(deltas) == 0 else np.ascontiguousarray(deltas, np.int32).reshape(-1, 2)
+        rc = self.lib.vvcp_refine_motion(self.h, i, None if d is None else d.ctypes.data, 0 if d is None else len(d))
+        if rc != 0:
+            raise ParseError("picture %d refine: %s" % (i, self.lib.vvcp_last_error().decode()))
+
     def _rows(self, i, what, dtype, shape_tail):
         n = self.lib.vvcp_picture_rows(self.h, i, what, None, 0)
         if n < 0:
@@ -95,4 +111,8 @@ class Stream:
         r["alf_ctb_en"] = np.stack([self._rows(i, ROWS_ALF_EN0 + c, np.uint8, ()) for c in range(3)])
         r["alf_ctb_alt"] = np.stack([self._rows(i, ROWS_ALF_ALT0 + c, np.uint8, ()) for c in range(3)])
         r["ccalf_ctl"] = np.stack([self._rows(i, ROWS_CCALF0 + c, np.uint8, ()) for c in range(2)])
+        if self.lib.vvcp_picture_rows(self.h, i, ROWS_MOTION, None, 0) >= 0:
+            inf = self.info(i)
+            r["motion"] = self._rows(i, ROWS_MOTION, np.int32, (10,)).reshape((inf["height"] + 3) // 4, (inf["width"] + 3) // 4, 10)
+            r["geo"] = self._rows(i, ROWS_GEO, np.int32, (13,))
         return r
