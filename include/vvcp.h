@@ -46,6 +46,17 @@ int vvcp_derive_motion(vvcp_stream *s, int32_t idx);
  * NULL when no PU of the picture refines. */
 int vvcp_refine_motion(vvcp_stream *s, int32_t idx, const int32_t *deltas, int64_t n);
 
+/* Picture parameters of the reconstruction path (include/vvcr.h vvcr_pic_params) from the parsed
+ * headers: everything except pp->slot and pp->ref_slot, which the caller's DPB assigns. Slice-level
+ * fields are the last slice's; slices of one picture must share their reference lists. */
+int vvcp_picture_params(const vvcp_stream *s, int32_t idx, vvcr_pic_params *pp);
+/* ALF / CC-ALF filters of a picture as vvcr_alf takes them (AdaptiveLoopFilter::reconstructCoeffAPSs,
+ * AdaptiveLoopFilter.cpp:620): luma_coef / luma_clip [sets][25][13] for the 16 fixed sets then the
+ * slice's luma APS sets (at most max_sets copied), chroma [8][7], cc_coef [2][4][8]. Any pointer may be
+ * NULL. Returns the number of luma sets (16 + luma APS count). */
+int vvcp_alf_filters(const vvcp_stream *s, int32_t idx, int16_t *luma_coef, int16_t *luma_clip, int32_t max_sets,
+                     int16_t *chroma_coef, int16_t *chroma_clip, int16_t *cc_coef);
+
 /* Parsed rows of a picture (after vvcp_parse_picture): copies min(cap, count) entries to dst (dst may be
  * NULL) and returns count. MV fields of vvcr_cu / vvcr_pu hold parsed values until vvcp_derive_motion. */
 #define VVCP_ROWS_CU 0        /* vvcr_cu */

@@ -276,7 +276,7 @@ struct PPS {
   bool rectSlice = true, singleSlicePerSubPic = false;
   int numSlicesInPic = 1;
   std::vector<std::vector<int>> rectSliceCtus;   // CTU addresses of each rectangular slice
-  bool lfAcrossTiles = true, lfAcrossSlices = true;
+  bool lfAcrossTiles = true, lfAcrossSlices = false;   // PPS constructor defaults (no picture partition)
   bool entropySync = false, cabacInitPresent = false;
   int numRefDefault[2] = {1, 1};
   bool rpl1IdxPresent = false;

@@ -6,6 +6,7 @@
 #include <cstring>
 
 #include "vvcp.h"
+#include "vvcp_params.h"
 
 namespace vvcp {
 
@@ -253,6 +254,31 @@ int vvcp_refine_motion(vvcp_stream *h, int32_t idx, const int32_t *deltas, int64
   VVCP_API_BEGIN
   h->s.refine_motion(idx, deltas, n);
   return VVCR_OK;
+  VVCP_API_END
+}
+
+int vvcp_picture_params(const vvcp_stream *h, int32_t idx, vvcr_pic_params *pp) {
+  if (!h || !pp || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
+  VVCP_API_BEGIN
+  vvcp::build_pic_params(*h->s.pics[idx], *pp);
+  return VVCR_OK;
+  VVCP_API_END
+}
+
+int vvcp_alf_filters(const vvcp_stream *h, int32_t idx, int16_t *luma_coef, int16_t *luma_clip, int32_t max_sets,
+                     int16_t *chroma_coef, int16_t *chroma_clip, int16_t *cc_coef) {
+  if (!h || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
+  VVCP_API_BEGIN
+  vvcp::AlfFilters f;
+  vvcp::build_alf(*h->s.pics[idx], f);
+  const size_t per = 25 * 13;
+  const int n = std::min(max_sets, f.numLumaSets);
+  if (luma_coef && n > 0) std::memcpy(luma_coef, f.lumaCoef.data(), n * per * sizeof(int16_t));
+  if (luma_clip && n > 0) std::memcpy(luma_clip, f.lumaClip.data(), n * per * sizeof(int16_t));
+  if (chroma_coef) std::memcpy(chroma_coef, f.chromaCoef, sizeof(f.chromaCoef));
+  if (chroma_clip) std::memcpy(chroma_clip, f.chromaClip, sizeof(f.chromaClip));
+  if (cc_coef) std::memcpy(cc_coef, f.ccCoef, sizeof(f.ccCoef));
+  return f.numLumaSets;
   VVCP_API_END
 }
 

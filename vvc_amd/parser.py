@@ -32,6 +32,8 @@ def _bind(lib):
     lib.vvcp_parse_picture.argtypes = [_P, _I32]
     lib.vvcp_picture_rows.argtypes = [_P, _I32, _I32, _P, _I64]
     lib.vvcp_picture_rows.restype = _I64
+    lib.vvcp_picture_params.argtypes = [_P, _I32, _P]
+    lib.vvcp_alf_filters.argtypes = [_P, _I32, _P, _P, _I32, _P, _P, _P]
     lib.vvcp_derive_motion.argtypes = [_P, _I32]
     lib.vvcp_refine_motion.argtypes = [_P, _I32, _P, _I64]
     lib._vvcp_bound = True
@@ -87,6 +89,27 @@ class Stream:
         rc = self.lib.vvcp_refine_motion(self.h, i, None if d is None else d.ctypes.data, 0 if d is None else len(d))
         if rc != 0:
             raise ParseError("picture %d refine: %s" % (i, self.lib.vvcp_last_error().decode()))
+
+    def pic_params(self, i):
+        """vvcr_pic_params of picture i (N.PicParams) without the DPB slots"""
+        pp = N.PicParams()
+        rc = self.lib.vvcp_picture_params(self.h, i, C.addressof(pp))
+        if rc != 0:
+            raise ParseError("picture %d params: %s" % (i, self.lib.vvcp_last_error().decode()))
+        return pp
+
+    def alf_filters(self, i):
+        """ALF / CC-ALF filters of picture i: luma_coef / luma_clip (sets, 25, 13), chroma_coef /
+        chroma_clip (8, 7), cc_coef (2, 4, 8)"""
+        n = self.lib.vvcp_alf_filters(self.h, i, None, None, 0, None, None, None)
+        if n < 0:
+            raise ParseError("picture %d ALF: %s" % (i, self.lib.vvcp_last_error().decode()))
+        out = {"luma_coef": np.zeros((n, 25, 13), np.int16), "luma_clip": np.zeros((n, 25, 13), np.int16),
+               "chroma_coef": np.zeros((8, 7), np.int16), "chroma_clip": np.zeros((8, 7), np.int16),
+               "cc_coef": np.zeros((2, 4, 8), np.int16)}
+        self.lib.vvcp_alf_filters(self.h, i, *(out[k].ctypes.data for k in ("luma_coef", "luma_clip")), n,
+                                  *(out[k].ctypes.data for k in ("chroma_coef", "chroma_clip", "cc_coef")))
+        return out
 
     def _rows(self, i, what, dtype, shape_tail):
         n = self.lib.vvcp_picture_rows(self.h, i, what, None, 0)
