@@ -29,8 +29,9 @@ int vvcp_open(const uint8_t *data, size_t n, vvcp_stream **out);
 int vvcp_close(vvcp_stream *s);
 const char *vvcp_last_error(void);
 int vvcp_num_pictures(const vvcp_stream *s);
-/* info[0..9] = poc, slice type of the first slice (0 B, 1 P, 2 I), width, height, ctu_log2, bit depth,
- * number of slices, temporal id, NAL unit type, slice QP. Returns the number of fields (10). */
+/* info[0..15] = poc, slice type of the first slice (0 B, 1 P, 2 I), width, height, ctu_log2, bit depth,
+ * number of slices, temporal id, NAL unit type, slice QP, conformance window left / right / top / bottom
+ * offsets in luma samples, pic_output_flag, non-reference picture flag. Returns the number of fields (16). */
 int vvcp_picture_info(const vvcp_stream *s, int32_t idx, int32_t *info, int32_t n);
 int vvcp_parse_picture(vvcp_stream *s, int32_t idx);
 
@@ -56,6 +57,15 @@ int vvcp_picture_params(const vvcp_stream *s, int32_t idx, vvcr_pic_params *pp);
  * NULL. Returns the number of luma sets (16 + luma APS count). */
 int vvcp_alf_filters(const vvcp_stream *s, int32_t idx, int16_t *luma_coef, int16_t *luma_clip, int32_t max_sets,
                      int16_t *chroma_coef, int16_t *chroma_clip, int16_t *cc_coef);
+
+/* Plans a parsed and motion-derived picture for the reconstruction path: vvcr_picture_create with
+ * vvcp_picture_params plus the caller's DPB slots (slot; ref_slot[l * VVCR_MAX_REF + r] for the active
+ * references), vvcr_picture_submit of the rows, vvcr_picture_set_loop_filter_params (SAO, ALF / CC-ALF)
+ * and vvcr_picture_plan(stage_mask), in native code. On success *out is the planned picture (the
+ * caller uploads it with vvcr_prepare_planned and frees it with vvcr_picture_destroy). Thread-safe for
+ * different pictures. */
+int vvcp_plan_picture(vvcp_stream *s, int32_t idx, const vvcr_seq_params *sp, int32_t slot, const int32_t *ref_slot,
+                      uint32_t stage_mask, vvcr_picture **out);
 
 /* Parsed rows of a picture (after vvcp_parse_picture): copies min(cap, count) entries to dst (dst may be
  * NULL) and returns count. MV fields of vvcr_cu / vvcr_pu hold parsed values until vvcp_derive_motion. */

@@ -286,6 +286,10 @@ int vvcr_write_output(vvcr_ctx *ctx, int32_t slot, const vvcr_output_params *op,
  * (xProcessDMVR InterPrediction.cpp:2162-2296). Copies min(n, count) pairs into out and returns the
  * count (>= 0) or a negative error. Blocks until the picture's motion compensation has run. */
 int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n);
+/* The same for a launched prepared picture (any, not only the last): waits for that picture's inter
+ * stage only, so a host producer can hand a picture's refined motion to the pictures that use it as
+ * collocated reference (vvcp_refine_motion) while its lane goes on with intra and the loop filters. */
+int vvcr_picture_dmvr_deltas(vvcr_ctx *ctx, int32_t handle, int32_t *out, int64_t n);
 
 /* Timing of the last vvcr_end_picture*, in ms (HIP events on the library stream): ms[0] = whole call,
  * ms[1 + k] = stage k in VVCR_STAGE_* bit order (RESID, INTER, INTRA, LMCS_INV, DBK, SAO, ALF), 0 if

@@ -1,0 +1,76 @@
+// vvcp_plan.cpp — hands a parsed, motion-derived picture of the host parser to the reconstruction
+// path's host-only planner (vvcr_picture_*, include/vvcr.h) without leaving native code: the same
+// create / submit / loop-filter / plan sequence a ctypes producer makes (vvc_amd/stream.py), with the
+// rows, picture parameters and ALF filters taken straight from the parser's state.
+#include <cstring>
+
+#include "vvcp.h"
+#include "vvcp_params.h"
+
+namespace {
+int fail(vvcr_picture *pic, int rc, const char *what) {
+  vvcp::set_api_error(std::string(what) + ": " + vvcr_picture_last_error(pic));
+  if (pic) vvcr_picture_destroy(pic);
+  return rc;
+}
+}  // namespace
+
+extern "C" int vvcp_plan_picture(vvcp_stream *h, int32_t idx, const vvcr_seq_params *sp, int32_t slot,
+                                 const int32_t *ref_slot, uint32_t stage_mask, vvcr_picture **out) {
+  if (!h || !sp || !out || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
+  *out = nullptr;
+  const vvcp::PictureUnit &p = *h->s.pics[idx];
+  if (!p.derived) return VVCR_E_STATE;
+  vvcr_pic_params pp;
+  vvcp::AlfFilters alf;
+  try {
+    vvcp::build_pic_params(p, pp);
+    if (p.sps.alf) vvcp::build_alf(p, alf);
+  } catch (const std::exception &e) {
+    vvcp::set_api_error(e.what());
+    return VVCR_E_UNSUPPORTED;
+  }
+  pp.slot = slot;
+  for (int l = 0; l < 2; l++)
+    for (int r = 0; r < pp.num_ref[l]; r++) {
+      if (!ref_slot) return VVCR_E_ARG;
+      pp.ref_slot[l][r] = ref_slot[l * VVCR_MAX_REF + r];
+    }
+  vvcr_picture *pic = nullptr;
+  int rc = vvcr_picture_create(sp, &pp, &pic);
+  if (rc) return fail(nullptr, rc, "vvcr_picture_create");
+  const vvcp::PictureSyntax &S = p.syn;
+  rc = vvcr_picture_submit(pic, S.cu.data(), (int32_t)S.cu.size(), S.pu.data(), (int32_t)S.pu.size(), S.tu.data(),
+                           (int32_t)S.tu.size(), S.coef.data(), (int64_t)S.coef.size(), p.motion.data(), p.geo.data(),
+                           (int32_t)p.geo.size());
+  if (rc) return fail(pic, rc, "vvcr_picture_submit");
+  // loop-filter parameters as vvc_amd/stream.py set_loop_filter_params arranges them
+  const size_t n = S.alfFset.size();
+  std::vector<uint8_t> en(3 * n), alt(3 * n), cc(2 * n);
+  std::vector<int16_t> chroma(2 * 56);
+  vvcr_alf A{};
+  if (p.sps.alf) {
+    for (int c = 0; c < 3; c++) {
+      std::memcpy(&en[c * n], S.alfEn[c].data(), n);
+      if (c) std::memcpy(&alt[c * n], S.alfAlt[c].data(), n);   // luma has no alternatives
+    }
+    for (int c = 0; c < 2; c++)   // control words of a disabled component are not coded
+      if (p.slices.back().ccAlf[c]) std::memcpy(&cc[c * n], S.ccCtl[c].data(), n);
+    A.num_luma_sets = alf.numLumaSets;
+    A.luma_coef = alf.lumaCoef.data();
+    A.luma_clip = alf.lumaClip.data();
+    A.chroma_coef = &alf.chromaCoef[0][0];
+    A.chroma_clip = &alf.chromaClip[0][0];
+    A.cc_coef = &alf.ccCoef[0][0][0];
+    A.ctb_en = en.data();
+    A.ctb_alt = alt.data();
+    A.ctb_filter_set = S.alfFset.data();
+    A.cc_ctl = cc.data();
+  }
+  rc = vvcr_picture_set_loop_filter_params(pic, S.sao.data(), p.sps.alf ? &A : nullptr);
+  if (rc) return fail(pic, rc, "vvcr_picture_set_loop_filter_params");
+  rc = vvcr_picture_plan(pic, stage_mask);
+  if (rc) return fail(pic, rc, "vvcr_picture_plan");
+  *out = pic;
+  return VVCR_OK;
+}

@@ -185,13 +185,8 @@ void Stream::refine_motion(int idx, const int32_t *deltas, int64_t n) {
 // ================================================================================================
 // C-ABI (include/vvcp.h)
 // ================================================================================================
-struct vvcp_stream {
-  vvcp::Stream s;
-  std::string err;
-  std::mutex mu;
-};
-
 static thread_local std::string g_vvcp_err;
+void vvcp::set_api_error(const std::string &msg) { g_vvcp_err = msg; }
 
 #define VVCP_API_BEGIN try {
 #define VVCP_API_END                                              \
@@ -226,8 +221,11 @@ int vvcp_num_pictures(const vvcp_stream *h) { return h ? (int)h->s.pics.size() :
 int vvcp_picture_info(const vvcp_stream *h, int32_t idx, int32_t *info, int32_t n) {
   if (!h || !info || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
   const vvcp::PictureUnit &p = *h->s.pics[idx];
+  const int sw = p.sps.chromaFormat == 1 || p.sps.chromaFormat == 2 ? 2 : 1, shh = p.sps.chromaFormat == 1 ? 2 : 1;
   const int32_t v[] = {p.poc, p.slices.empty() ? 2 : p.slices[0].sliceType, p.pps.width, p.pps.height, p.sps.ctuLog2,
-                       p.sps.bitDepth, (int32_t)p.slices.size(), p.tid, p.nalType, p.slices.empty() ? 0 : p.slices[0].qp};
+                       p.sps.bitDepth, (int32_t)p.slices.size(), p.tid, p.nalType, p.slices.empty() ? 0 : p.slices[0].qp,
+                       p.pps.confLeft * sw, p.pps.confRight * sw, p.pps.confTop * shh, p.pps.confBottom * shh,
+                       p.ph.picOutput ? 1 : 0, p.ph.nonRef ? 1 : 0};
   const int m = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < m; i++) info[i] = v[i];
   return m;

@@ -42,4 +42,11 @@ struct Stream {
   void refine_motion(int idx, const int32_t *deltas, int64_t n);
 };
 
+void set_api_error(const std::string &msg);   // vvcp_last_error() of the calling thread
+
 }  // namespace vvcp
+
+// the C-ABI handle (include/vvcp.h)
+struct vvcp_stream {
+  vvcp::Stream s;
+};

@@ -95,6 +95,10 @@ struct Prepared {
   hipEvent_t ev[NK][2] = {};
   hipEvent_t start = nullptr, done = nullptr;   // whole launch (events of this picture only: an event
                                                 // shared by pictures of several lanes would serialise them)
+  hipEvent_t ev_mc = nullptr;                   // after the inter stage on the lane
+  hipEvent_t mc_done = nullptr;                 // the DMVR deltas of the launch are in h_dmvr
+  int32_t *h_dmvr = nullptr;                    // pinned host copy of the DMVR deltas
+  size_t h_dmvr_cap = 0;
   bool ran[NK] = {};
   bool timed[NK] = {};              // the group's events were recorded by the last launch
   bool launched = false;
@@ -106,11 +110,16 @@ struct Prepared {
     for (auto &e : ev) { VVCR_CHECK_HIP(hipEventCreate(&e[0])); VVCR_CHECK_HIP(hipEventCreate(&e[1])); }
     VVCR_CHECK_HIP(hipEventCreate(&done));
     VVCR_CHECK_HIP(hipEventCreate(&start));
+    VVCR_CHECK_HIP(hipEventCreateWithFlags(&mc_done, hipEventDisableTiming));
+    VVCR_CHECK_HIP(hipEventCreateWithFlags(&ev_mc, hipEventDisableTiming));
   }
   ~Prepared() {
     for (auto &e : ev) { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); }
     (void)hipEventDestroy(done);
     (void)hipEventDestroy(start);
+    (void)hipEventDestroy(mc_done);
+    (void)hipEventDestroy(ev_mc);
+    if (h_dmvr) (void)hipHostFree(h_dmvr);
   }
   void wait() { if (launched) VVCR_CHECK_HIP(hipEventSynchronize(done)); }
 };
@@ -387,6 +396,12 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.n_aff = (int)wl.aff_jobs.size();
     r.n_dmvr = wl.n_dmvr;
     r.dmvr.ensure(2 * (size_t)r.n_dmvr + 2);
+    if (r.h_dmvr_cap < 2 * (size_t)r.n_dmvr + 2) {
+      if (r.h_dmvr) VVCR_CHECK_HIP(hipHostFree(r.h_dmvr));
+      r.h_dmvr = nullptr;
+      r.h_dmvr_cap = 2 * (size_t)r.n_dmvr + 2;
+      VVCR_CHECK_HIP(hipHostMalloc((void **)&r.h_dmvr, r.h_dmvr_cap * sizeof(int32_t), hipHostMallocDefault));
+    }
     r.alg_bytes[K_MC] = wl.mc_alg;
     double b = 0;
     for (const McJob &j : wl.mc_bidir) b += mc_bytes(j);
@@ -547,6 +562,13 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_MC_AFFINE] = r.n_aff ? 1 : 0;
     }
+    // the deltas go to the host on the copy stream, so the lane goes on with intra and the loop filters
+    VVCR_CHECK_HIP(hipEventRecord(r.ev_mc, s));
+    VVCR_CHECK_HIP(hipStreamWaitEvent(ctx->copy_stream, r.ev_mc, 0));
+    if (r.n_dmvr > 0)
+      VVCR_CHECK_HIP(hipMemcpyAsync(r.h_dmvr, r.dmvr.p, (size_t)r.n_dmvr * 2 * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                    ctx->copy_stream));
+    VVCR_CHECK_HIP(hipEventRecord(r.mc_done, ctx->copy_stream));
   }
   if (mask & VVCR_STAGE_INTRA) {
     const IntraParams P = make_intra_params(ctx, r, L);
@@ -1130,6 +1152,22 @@ int vvcr_get_dmvr_deltas(vvcr_ctx *ctx, int32_t *out, int64_t n) {
     VVCR_CHECK_HIP(hipStreamSynchronize(s));
   }
   return cnt;
+  API_END
+}
+
+int vvcr_picture_dmvr_deltas(vvcr_ctx *ctx, int32_t handle, int32_t *out, int64_t n) {
+  if (!ctx || (!out && n)) return VVCR_E_ARG;
+  API_BEGIN
+  if (n < 0) throw VvcrError(VVCR_E_ARG, "negative count");
+  Prepared &r = get_prepared(ctx, handle);
+  if (!r.launched) throw VvcrError(VVCR_E_STATE, "picture not launched");
+  if (!(r.mask & VVCR_STAGE_INTER)) throw VvcrError(VVCR_E_STATE, "picture launched without its inter stage");
+  const int64_t m = std::min<int64_t>(n, r.n_dmvr);
+  // waits for this picture's inter stage and the copy of its deltas only, not for the rest of its lane;
+  // reads only the record of this picture, so several host threads may call it at once
+  VVCR_CHECK_HIP(hipEventSynchronize(r.mc_done));
+  if (m > 0) std::memcpy(out, r.h_dmvr, (size_t)m * 2 * sizeof(int32_t));
+  return r.n_dmvr;
   API_END
 }
 

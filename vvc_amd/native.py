@@ -89,6 +89,7 @@ def lib():
         L.vvcr_write_plane.argtypes = [P, I32, I32, I32, P, I32]
         L.vvcr_last_stage_times.argtypes = [P, C.POINTER(C.c_float), I32]
         L.vvcr_get_dmvr_deltas.argtypes = [P, P, C.c_int64]
+        L.vvcr_picture_dmvr_deltas.argtypes = [P, I32, P, C.c_int64]
         L.vvcr_prepare_picture.argtypes = [P, C.c_uint32, C.POINTER(I32)]
         L.vvcr_launch_picture.argtypes = [P, I32]
         L.vvcr_release_picture.argtypes = [P, I32]
@@ -129,7 +130,7 @@ class KernelStat(C.Structure):
 
 EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_release_picture", "vvcr_kernel_stats", "vvcr_create", "vvcr_destroy", "vvcr_last_error", "vvcr_begin_picture", "vvcr_submit",
            "vvcr_set_loop_filter_params", "vvcr_end_picture", "vvcr_end_picture_stages", "vvcr_sync",
-           "vvcr_read_plane", "vvcr_write_plane", "vvcr_read_picture", "vvcr_get_dmvr_deltas",
+           "vvcr_read_plane", "vvcr_write_plane", "vvcr_read_picture", "vvcr_get_dmvr_deltas", "vvcr_picture_dmvr_deltas",
            "vvcr_last_stage_times", "vvcr_stream", "vvcr_rd_plan", "vvcr_rd_run", "vvcr_fwd_plan", "vvcr_fwd_run",
            "vvcr_rdo_release", "vvcr_rd_dist", "vvcr_fwd_transform", "vvcr_set_timing",
            "vvcr_picture_create", "vvcr_picture_submit", "vvcr_picture_set_loop_filter_params", "vvcr_picture_plan",
@@ -161,6 +162,13 @@ class Picture:
             raise VvcrError("vvcr_picture_create failed (%d): %s" % (r, self.L.vvcr_picture_last_error(None).decode()))
         self.h = h
         self._keep = []
+
+    @classmethod
+    def wrap(cls, handle):
+        """a Picture for a vvcr_picture made elsewhere (e.g. vvcp_plan_picture); takes ownership"""
+        pic = cls.__new__(cls)
+        pic.L, pic.h, pic._keep = lib(), handle, []
+        return pic
 
     def _chk(self, r, what):
         if r != 0:
@@ -213,6 +221,7 @@ class Context:
             raise VvcrError("vvcr_create failed (%d): %s" % (r, self.L.vvcr_last_error(None).decode()))
         self.h = h
         self.width, self.height = width, height
+        self.dpb_slots = dpb_slots
         self._keep = []
 
     def _chk(self, r, what):
@@ -364,6 +373,16 @@ class Context:
         if n:
             self._chk(min(0, self.L.vvcr_get_dmvr_deltas(self.h, out.ctypes.data, n)), "vvcr_get_dmvr_deltas")
         return out
+
+    def picture_dmvr_deltas(self, handle, cap):
+        """DMVR deltas of a launched prepared picture (vvcr_picture_dmvr_deltas); cap = expected count"""
+        out = np.zeros((max(cap, 1), 2), np.int32)
+        n = self.L.vvcr_picture_dmvr_deltas(self.h, handle, out.ctypes.data, cap)
+        if n < 0:
+            self._chk(n, "vvcr_picture_dmvr_deltas")
+        if n > cap:
+            raise VvcrError("DMVR delta count %d > %d" % (n, cap))
+        return out[:n]
 
     def stage_ms(self):
         t = (C.c_float * 8)()

@@ -69,9 +69,10 @@ class Stream:
         return self.lib.vvcp_num_pictures(self.h)
 
     def info(self, i):
-        v = (_I32 * 10)()
-        self.lib.vvcp_picture_info(self.h, i, v, 10)
-        keys = ("poc", "slice_type", "width", "height", "ctu_log2", "bit_depth", "num_slices", "tid", "nal_type", "slice_qp")
+        v = (_I32 * 16)()
+        self.lib.vvcp_picture_info(self.h, i, v, 16)
+        keys = ("poc", "slice_type", "width", "height", "ctu_log2", "bit_depth", "num_slices", "tid", "nal_type", "slice_qp",
+                "conf_left", "conf_right", "conf_top", "conf_bottom", "output", "non_ref")
         return dict(zip(keys, list(v)))
 
     def parse(self, i):
