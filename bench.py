@@ -1,15 +1,15 @@
-"""Decode throughput of the MI355X reconstruction path on BASELINE.json configs[2], the largest
-single-GPU configuration: 4K 3840x2160 random access QP27 (the north star's QP32 is --stream ra2160l_q32).
+"""Decode throughput of the MI355X path on BASELINE.json configs[2], the largest single-GPU
+configuration: 4K 3840x2160 random access QP27 (the north star's QP32 is --stream ra2160l_q32).
 
-value (the headline) is END TO END from parsed pictures: each step decodes the whole sequence again,
-and every picture goes through host validation + planning (work lists, intra dependency plan, deblocking
-edges; a pool of --e2e-threads threads, vvcr_picture_*), upload (vvcr_prepare_planned) and the GPU
-(residuals, motion compensation with DMVR/BDOF/affine-PROF/GEO/CIIP, intra, deblocking, SAO, ALF/CC-ALF),
-all inside the timed region. CABAC parsing is not in it yet: the pictures are the reference parser's
-output (tests/golden/<stream>, captured by oracle/_ref/vtm_capture) - value_scope says so.
-The `resident` object is the same reconstruction with every input already planned and resident in HBM
-(vvcr_prepare_picture once, vvcr_launch_picture per step): the GPU-side rate.
-Every pass is checked bit-exact against the reference decoder's MD5s.
+value (the headline) is END TO END FROM THE BITSTREAM: every step decodes the .bin again from its first
+NAL unit - header parsing, the CABAC pass of every picture (host threads), motion derivation in decoding
+order with each collocated picture's DMVR deltas read back from the GPU, host planning (work lists,
+intra dependency plan, deblocking edges), upload (vvcr_prepare_planned) and the GPU (residuals, motion
+compensation with DMVR/BDOF/affine-PROF/GEO/CIIP, intra, deblocking, SAO, ALF/CC-ALF) - all inside the
+timed region, `--segments` independent decodes in flight (vvc_amd/bitstream.py).
+The `resident` object is the same reconstruction with every picture already planned and resident in
+HBM (launch only): the GPU-side rate. Output is checked bit-exact against DecoderApp: the YUV file MD5
+of one decode, and the plane MD5s of every segment's pictures after the timed steps.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--stream ra2160l_q27] [--no-cpu]
 
@@ -176,69 +176,81 @@ def shard_bench(a, R):
             "note": "tile-row shards, halo exchange over torch.distributed %s point to point" % (R.dist.get_backend() if R.dist else "-")}
 
 
-class E2E:
-    """Host planning + upload + GPU for every picture, in the timed region (the headline).
+class BitstreamE2E:
+    """The headline: bitstream in, pictures out, everything in the timed region.
 
-    Steps decode the whole sequence again and again as consecutive intra-started segments of one long
-    stream, on `segments` disjoint DPB slot ranges. A pool of `threads` threads plans each picture from
-    its host descriptors (vvcr_picture_*: validation, work lists, intra dependency plan, deblocking edges;
-    the library releases the GIL) and uploads it (vvcr_prepare_planned); this thread launches the
-    pictures in decoding order as each becomes ready, and releases a handle once `keep` later pictures
-    were launched (its work is then long done). The pool runs ahead of the launches, so the host work of
-    later pictures overlaps the GPU work of earlier ones, as a decoder's parse of picture n+1 would."""
+    Every step decodes the .bin again from its first NAL: a fresh host parser (vvcp_open: NAL split and
+    every header), the CABAC pass of each picture on a shared pool of `threads` threads, motion
+    derivation in decoding order with each collocated picture's DMVR deltas from the GPU, native
+    planning (vvcp_plan_picture), upload (vvcr_prepare_planned) and the GPU. Steps run as `segments`
+    independent decodes in flight at once, each on its own DPB slot range and host thread (a serving
+    process decoding several streams), launches serialised by one lock."""
 
-    def __init__(self, ctx, pics, per, segments, threads, keep=96):
+    def __init__(self, ctx, data, per, segments, threads):
         import concurrent.futures as cf
-        self.ctx, self.pics, self.per, self.segments = ctx, pics, per, segments
-        self.ex = cf.ThreadPoolExecutor(threads)
-        self.threads, self.keep = threads, keep
-        self.jobs = []
-        for c in range(segments):
-            alloc = S.SlotAllocator(pics, per, base=per * c)
-            seg = []
-            for i, p in enumerate(pics):
-                slot = alloc.assign(i, p["hdr"]["poc"])
-                seg.append((p, slot, dict(alloc.slot_of)))
-            self.jobs.append(seg)
-        self.step_no = 0
-        self.live = []
+        import threading
+        from vvc_amd import bitstream as B
+        self.B, self.ctx, self.data, self.per, self.segments = B, ctx, data, per, segments
+        self.pool = cf.ThreadPoolExecutor(threads)
+        self.seg_ex = cf.ThreadPoolExecutor(segments)
+        self.lock = threading.Lock()
+        self.final = [None] * segments   # per segment: {slot: poc} after its last decode
 
-    def _work(self, job):
-        p, slot, slot_of = job
-        pic = S.plan_picture(p, slot, slot_of, dpb_slots=self.per * self.segments)
-        try:
-            return self.ctx.prepare_planned(pic)
-        finally:
-            pic.close()
+    def _decode(self, c):
+        seq = self.B.SequenceDecode(self.ctx, self.data, self.pool, nslots=self.per, base=self.per * c,
+                                    launch_lock=self.lock)
+        seq.run()
+        owner = {}
+        for i, inf in enumerate(seq.plan.info):
+            owner[seq.plan.slot[i]] = inf["poc"]
+        self.final[c] = owner
+
+    def _segment(self, c, n):
+        for _ in range(n):
+            self._decode(c)
 
     def run(self, steps):
-        """Enqueue `steps` steps; returns when the last picture is launched (not finished)."""
-        jobs = []
-        for k in range(steps):
-            jobs += self.jobs[(self.step_no + k) % self.segments]
-        self.step_no += steps
-        futs = [self.ex.submit(self._work, j) for j in jobs]
+        """Decodes the stream `steps` times; returns when every picture is launched (not finished)."""
+        per_seg = [steps // self.segments + (1 if c < steps % self.segments else 0) for c in range(self.segments)]
+        futs = [self.seg_ex.submit(self._segment, c, n) for c, n in enumerate(per_seg) if n]
         for f in futs:
-            h = f.result()
-            self.ctx.launch(h)
-            self.live.append(h)
-            if len(self.live) > self.keep:
-                self.ctx.release(self.live.pop(0))
-
-    def last_segment_slots(self):
-        seg = self.jobs[(self.step_no - 1) % self.segments]
-        return {slot: p["hdr"]["poc"] for p, slot, _ in seg}
+            f.result()
 
     def close(self):
         self.ctx.sync()
-        for h in self.live:
-            self.ctx.release(h)
-        self.live = []
-        self.ex.shutdown()
+        self.pool.shutdown()
+        self.seg_ex.shutdown()
 
 
-def check_slots(dec, owner, meta):
-    return all(D.plane_md5s(dec.read(slot)) == meta["poc_plane_md5"][str(poc)] for slot, poc in owner.items())
+def output_yuv_md5(ctx, data, meta):
+    """One decode with DecoderApp's output: the YUV file's MD5 (vvcr_write_output, output order) and
+    every output picture's plane MD5s, compared with the reference's."""
+    import concurrent.futures as cf
+    from vvc_amd import bitstream as B
+    from vvc_amd import parser as P
+    s = P.Stream(data)
+    inf = s.info(0)
+    s.close()
+    op = N.OutputParams(0, inf["conf_left"], inf["conf_right"], inf["conf_top"], inf["conf_bottom"], 0)
+    yuv, ok = hashlib.md5(), [True]
+
+    def on_output(poc, slot):
+        yuv.update(ctx.write_output(slot, op).tobytes())
+        exp = meta["poc_plane_md5"].get(str(poc))
+        if exp is not None and D.plane_md5s([ctx.read_plane(N.BUF_RECO, slot, c) for c in range(3)]) != exp:
+            ok[0] = False
+    with cf.ThreadPoolExecutor(8) as pool:
+        B.SequenceDecode(ctx, data, pool, nslots=min(16, ctx.dpb_slots)).run(on_output)
+    ctx.sync()
+    return ok[0] and yuv.hexdigest() == meta["yuv_md5"]
+
+
+def read_slot(ctx, slot):
+    return [ctx.read_plane(N.BUF_RECO, slot, c) for c in range(3)]
+
+
+def check_slots(ctx, owner, meta):
+    return all(D.plane_md5s(read_slot(ctx, slot)) == meta["poc_plane_md5"][str(poc)] for slot, poc in owner.items())
 
 
 def main():
@@ -265,36 +277,37 @@ def main():
         sys.exit("bench: --gpus %d but %d ranks" % (a.gpus, world))
 
     d = os.path.join(ROOT, "tests", "golden", a.stream)
-    pics = S.load_sequence(d)
     meta = S.load_meta(d)
-    h0 = pics[0]["hdr"]
-    W, H = h0["width"], h0["height"]
-    px_seq = W * H * len(pics)
-    nI = sum(1 for p in pics if p["hdr"]["slice_type"] == 2)
+    with open(os.path.join(ROOT, "tests", "golden", "streams", a.stream + ".bin"), "rb") as f:
+        data = f.read()
+    from vvc_amd import parser as P
+    ps = P.Stream(data)
+    infos = [ps.info(i) for i in range(len(ps))]
+    ps.close()
+    W, H = infos[0]["width"], infos[0]["height"]
+    px_seq = W * H * len(infos)
+    nI = sum(1 for inf in infos if inf["slice_type"] == 2)
 
-    per = min(12, 64 // a.segments)   # DPB slots per copy (64 in all)
+    per = min(16, 64 // a.segments)   # DPB slots per copy (64 in all)
     # k_intra workgroups (VVCR_INTRA_WG, read at vvcr_create): the library's default sizes one intra picture at
     # a time (32 at 1080p, 60 at 4K); with several intra pictures in flight 32 each is better (4K 7.6 -> 8.6
     # Gpx/s). The 8K shard pass, one picture at a time, keeps the default.
     saved = os.environ.get("VVCR_INTRA_WG")
     os.environ.setdefault("VVCR_INTRA_WG", "32")
-    dec = D.Decoder(pics, dpb_slots=per * a.segments,
+    ctx = N.Context(W, H, bit_depth=infos[0]["bit_depth"], ctu_log2=infos[0]["ctu_log2"], dpb_slots=per * a.segments,
                     device=int(os.environ.get("VVCR_DEVICE", local)))   # VVCR_DEVICE: rehearsal of N ranks on one GPU
     lanes_cfg = "%s lanes (%s intra) on %s hardware queues, %s k_intra workgroups" % (
         os.environ["VVCR_LANES"], os.environ["VVCR_INTRA_LANES"], os.environ.get("GPU_MAX_HW_QUEUES", "4"),
         os.environ["VVCR_INTRA_WG"])
     if saved is None:
         os.environ.pop("VVCR_INTRA_WG", None)
-    ctx = dec.ctx
 
-    # ---- headline: end to end (host planning + upload + GPU inside the timed region)
+    # ---- headline: end to end from the bitstream (parse + derive + plan + upload + GPU in the timed region)
     ctx.set_timing(False)
-    e2e = E2E(ctx, pics, per, a.segments, a.e2e_threads)
-    e2e.run(1)                      # first pass, one picture at a time is not needed: checked below
-    ctx.sync()
-    bitexact = check_slots(dec, e2e.last_segment_slots(), meta)
-    if a.warmup > 1:
-        e2e.run(a.warmup - 1)
+    bitexact = output_yuv_md5(ctx, data, meta)      # one decode writing DecoderApp's output file: its MD5
+    e2e = BitstreamE2E(ctx, data, per, a.segments, a.e2e_threads)
+    if a.warmup > 0:
+        e2e.run(a.warmup)
         ctx.sync()
     R.barrier()
     ctx.sync()
@@ -304,41 +317,27 @@ def main():
     t1 = time.perf_counter()
     R.barrier()
     elapsed = R.max_over_ranks(t1 - t0)
-    e2e_ok = check_slots(dec, e2e.last_segment_slots(), meta)
-    bitexact = bitexact and e2e_ok
+    for owner in e2e.final:
+        if owner is not None:
+            bitexact = bitexact and check_slots(ctx, owner, meta)
     e2e.close()
 
     # ---- resident: every picture planned and uploaded once, the steps only launch (GPU-side rate)
     resident = None
     kern = {}
     if a.resident_steps > 0:
+        import concurrent.futures as cf
+        from vvc_amd import bitstream as B
         copies = []
         t_prep = time.perf_counter()
-        for c in range(a.segments):
-            alloc = S.SlotAllocator(pics, per, base=per * c)
-            handles, slots = [], []
-            for i, p in enumerate(pics):
-                slot = alloc.assign(i, p["hdr"]["poc"])
-                ctx.begin_picture(S.pic_params(p, slot, alloc.slot_of))
-                S.submit(ctx, p)
-                S.set_loop_filter_params(ctx, p)
-                handles.append(ctx.prepare(N.STAGE_ALL))
-                slots.append((p["hdr"]["poc"], slot))
-            copies.append((handles, slots))
+        with cf.ThreadPoolExecutor(a.e2e_threads) as pool:
+            for c in range(a.segments):
+                seq = B.SequenceDecode(ctx, data, pool, nslots=per, base=per * c)
+                _, handles = seq.run(keep_handles=True)
+                copies.append((handles, [(inf["poc"], seq.plan.slot[i]) for i, inf in enumerate(seq.plan.info)]))
+        ctx.sync()
         t_prep = (time.perf_counter() - t_prep) / a.segments
-        # first pass of the first copy one picture at a time: every plane and the YUV file MD5
-        yuv = hashlib.md5()
-        outs = {}
-        for hnd, (poc, slot) in zip(*copies[0]):
-            ctx.launch(hnd)
-            planes = dec.read(slot)
-            outs[poc] = D.plane_md5s(planes), planes
-        res_ok = all(outs[int(k)][0] == v for k, v in meta["poc_plane_md5"].items())
-        for poc in sorted(outs):
-            for pl in outs[poc][1]:
-                yuv.update(np.ascontiguousarray(pl).astype("<u2").tobytes())
-        res_ok = res_ok and yuv.hexdigest() == meta["yuv_md5"]
-        outs = None
+        res_ok = True
         nstep = [0]
 
         def run_step():
@@ -364,7 +363,7 @@ def main():
                 ctx.launch(hnd)
         ctx.sync()
         for _, slots in copies:
-            res_ok = res_ok and check_slots(dec, {slot: poc for poc, slot in slots}, meta)
+            res_ok = res_ok and check_slots(ctx, {slot: poc for poc, slot in slots}, meta)
         # serial view: one step at a time
         s0 = time.perf_counter()
         for _ in range(max(1, a.resident_steps // 2)):
@@ -435,12 +434,12 @@ def main():
         "dtype": "int16",
         "data": "synthetic (VTM-7.3-encoded synthetic %dx%d %s stream)" % (W, H, desc),
         "config": {"workload": "%s: %dx%d %s, %d pictures (%d intra) per step, reconstruction + DBK/SAO/ALF" % (
-                       a.stream, W, H, desc, len(pics), nI),
+                       a.stream, W, H, desc, len(infos), nI),
                    "parallelism": "replicas%d" % world, "segments": a.segments, "lanes": lanes_cfg,
                    "host_threads": a.e2e_threads, "bitexact_vs_reference": bool(bitexact)},
-        "value_scope": "end to end from parsed pictures: host validation + planning (work lists, intra dependency plan, "
-                       "deblocking edges) + upload + GPU reconstruction and loop filters, every picture of every step; "
-                       "CABAC parsing excluded (pictures are the reference parser's output) - see README",
+        "value_scope": "end to end from the bitstream: NAL/header parsing, CABAC (host threads), motion derivation "
+                       "with the GPU's DMVR feedback, host planning, upload, GPU reconstruction and loop filters, every "
+                       "picture of every step; %d independent decodes in flight" % a.segments,
         "roofline": roof,
         "cpu_baseline": None,
         "resident": resident,
@@ -450,7 +449,7 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, "tests", "golden", "streams", a.stream + ".bin"), px_seq)
-    dec.close()
+    ctx.close()
     if a.shard_steps > 0:
         try:
             line["shard"] = shard_bench(a, R)

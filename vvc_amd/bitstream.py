@@ -127,7 +127,9 @@ class SequenceDecode:
             raise P.ParseError("picture %d plan: %s" % (i, self.L.vvcp_last_error().decode()))
         return N.Picture.wrap(h)
 
-    def run(self, on_output=None):
+    def run(self, on_output=None, keep_handles=False):
+        """Decodes the stream; returns [(poc, slot)] in output order, and with keep_handles also the
+        prepared-picture handles in decoding order (not released: the caller may launch them again)."""
         n = len(self.s)
         parsed = [self.pool.submit(self.s.parse, i) for i in range(n)]
         handles = {}          # decode index -> prepared-picture handle
@@ -166,15 +168,17 @@ class SequenceDecode:
                         on_output(self.plan.info[k]["poc"], self.plan.slot[k])
                     out_pos += 1
                 # release handles of pictures far behind whose deltas are no longer needed
-                while len(live) > self.keep and live[0] in refined:
+                while not keep_handles and len(live) > self.keep and live[0] in refined:
                     self.ctx.release(handles.pop(live.pop(0)))
+            kept = [handles.pop(i) for i in range(n)] if keep_handles else None
         finally:
             for f in parsed:
                 f.cancel()
             for i in live:
                 if i in handles:
                     self.ctx.release(handles.pop(i))
-        return [(self.plan.info[k]["poc"], self.plan.slot[k]) for k in out]
+        order = [(self.plan.info[k]["poc"], self.plan.slot[k]) for k in out]
+        return (order, kept) if keep_handles else order
 
 
 def decode_bitstream(data, ctx=None, threads=8, dpb_slots=16, device=0, on_output=None):

@@ -211,8 +211,10 @@ struct Planner {
       };
       const bool n0 = intraAt(c.x - 1, c.y + c.h - 1), n1 = intraAt(c.x + c.w - 1, c.y - 1);
       const int wIntra = (n0 && n1) ? 3 : ((!n0 && !n1) ? 1 : 2);
+      // chroma blocks 2 samples wide keep the plain inter prediction (DecCu.cpp:701, IntraPrediction.cpp:746)
+      const int ncomp = c.cw > 2 ? 3 : 1;
       int id[3];
-      for (int comp = 0; comp < 3; comp++) {
+      for (int comp = 0; comp < ncomp; comp++) {
         const int ch = comp ? 1 : 0;
         IntraJob j = base(c, comp);
         j.x = j.cx; j.y = j.cy; j.w = j.cw; j.h = j.ch;
@@ -224,10 +226,14 @@ struct Planner {
         id[comp] = push(lev + 1, j);
       }
       int lev = 0;
-      for (auto it = jobs.end() - 3; it != jobs.end(); ++it) lev = std::max(lev, it->first);
+      for (auto it = jobs.end() - ncomp; it != jobs.end(); ++it) lev = std::max(lev, it->first);
       mark(0, c.x, c.y, c.w, c.h, lev, true, 0, id[0]);
-      mark(1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
-      mark(1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
+      if (ncomp == 3) {
+        mark(1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
+        mark(1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
+      } else if (c.cvalid) {
+        inter_chroma(c);
+      }
       return;
     }
     // plain inter: level 0, reconstructed before the intra waves; with LMCS chroma residual scaling the
@@ -243,19 +249,38 @@ struct Planner {
       }
     if (c.yvalid) mark(0, c.x, c.y, c.w, c.h, 0, true);
     if (c.cvalid && !chromaStep) mark(1, c.cx, c.cy, c.cw, c.ch, 0, true);
-    if (chromaStep) {
-      int id[3] = {-1, -1, -1}, lev = 0;
-      for (int comp = 1; comp < 3; comp++) {
-        IntraJob j = base(c, comp);
-        j.x = j.cx; j.y = j.cy; j.w = j.cw; j.h = j.ch;
-        j.xkind = XK_INTER_CHROMA;
-        const int l = 1 + set_cscale(j, c.x, c.y);
-        id[comp] = push(l, j);
-        lev = std::max(lev, l);
-      }
-      mark(1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
-      mark(1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
+    if (chromaStep) inter_chroma_step(c);
+  }
+
+  // the chroma of an inter CU on its own (a CIIP CU whose chroma is not blended)
+  void inter_chroma(const vvcr_cu &c) {
+    if (cscale) {
+      inter_chroma_step(c);
+      return;
     }
+    for (int y = 0; y < c.h; y += 16)
+      for (int x = 0; x < c.w; x += 16) {
+        ReconTile t{};
+        t.x = (int16_t)(c.x + x); t.y = (int16_t)(c.y + y);
+        t.w = (uint8_t)std::min(16, c.w - x); t.h = (uint8_t)std::min(16, c.h - y);
+        t.comps = 2;
+        out.inter_tiles.push_back(t);
+      }
+    mark(1, c.cx, c.cy, c.cw, c.ch, 0, true);
+  }
+
+  void inter_chroma_step(const vvcr_cu &c) {
+    int id[3] = {-1, -1, -1}, lev = 0;
+    for (int comp = 1; comp < 3; comp++) {
+      IntraJob j = base(c, comp);
+      j.x = j.cx; j.y = j.cy; j.w = j.cw; j.h = j.ch;
+      j.xkind = XK_INTER_CHROMA;
+      const int l = 1 + set_cscale(j, c.x, c.y);
+      id[comp] = push(l, j);
+      lev = std::max(lev, l);
+    }
+    mark(1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
+    mark(1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
   }
 
   void intra_luma(int ci) {
