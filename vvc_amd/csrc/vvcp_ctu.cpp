@@ -1556,21 +1556,16 @@ struct Parser {
       if ((c.predmode == MODE_INTRA && mask) || mask == 3) t.jccr = cab.bin(JointCbCrFlag + mask - 1) ? mask : 0;
     }
     (void)isp;
-    std::vector<int32_t> buf[3];
-    if (cbfLuma) residual_coding(ci, ti, 0, cuCtx, buf[0]);
-    if (!lumaOnly) {
-      for (int comp = 1; comp <= 2; comp++)
-        if (t.b[comp][4]) residual_coding(ci, ti, comp, cuCtx, buf[comp]);
-    }
+    // coefficient levels go straight into the picture's pool: a zeroed w*h block per coded component
+    // (and per chroma component of a joint Cb-Cr TU), in component order
     for (int comp = 0; comp < 3; comp++) {
       vvcr_tu &tt = pic.tu[ti];
-      if (!tuValid(tt, comp)) continue;
-      if (tt.b[comp][4] || (comp > 0 && tt.jccr)) {
-        const size_t n = (size_t)tt.b[comp][2] * tt.b[comp][3];
-        tt.b[comp][6] = (int32_t)pic.coef.size();
-        if (buf[comp].empty()) pic.coef.insert(pic.coef.end(), n, 0);
-        else pic.coef.insert(pic.coef.end(), buf[comp].begin(), buf[comp].end());
-      }
+      if (!tuValid(tt, comp) || !(tt.b[comp][4] || (comp > 0 && tt.jccr))) continue;
+      const size_t n = (size_t)tt.b[comp][2] * tt.b[comp][3], off = pic.coef.size();
+      tt.b[comp][6] = (int32_t)off;
+      pic.coef.resize(off + n);
+      const bool coded = comp == 0 ? cbfLuma : (!lumaOnly && tt.b[comp][4]);
+      if (coded) residual_coding(ci, ti, comp, cuCtx, pic.coef.data() + off);
     }
   }
 
@@ -1605,20 +1600,18 @@ struct Parser {
   }
 
   // residual_coding (:2918)
-  void residual_coding(int ci, int ti, int comp, CuCtx &cuCtx, std::vector<int32_t> &buf) {
+  void residual_coding(int ci, int ti, int comp, CuCtx &cuCtx, int32_t *coeff) {   // coeff: zeroed w*h
     const vvcr_cu &c = pic.cu[ci];
     vvcr_tu &t = pic.tu[ti];
     const int w = t.b[comp][2], h = t.b[comp][3];
-    buf.assign((size_t)w * h, 0);
     if (comp == 2 && t.jccr == 3) return;
     // ts_flag (:3007)
     int ts = ((c.bdpcm && comp == 0) || (c.bdpcmc && comp != 0)) ? 1 : (t.b[comp][5] == MTS_SKIP ? 1 : 0);
     if (tsAllowed(c, t, comp)) ts = cab.bin(TransformSkipFlag + (comp == 0 ? 0 : 1));
     t.b[comp][5] = ts ? MTS_SKIP : MTS_DCT2;
-    if (ts) { residual_codingTS(c, comp, w, h, buf.data()); return; }
+    if (ts) { residual_codingTS(c, comp, w, h, coeff); return; }
     const bool signHiding = ph.signHiding;
     CoefCtx cc(comp, w, h, signHiding, false);
-    int32_t *coeff = buf.data();
     cc.scanPosLast = last_sig_coeff(cc, c, comp, w, h);
     if (h >= 4 && w >= 4) {
       const int maxLfnstPos = ((h == 4 && w == 4) || (h == 8 && w == 8)) ? 7 : 15;
@@ -2121,6 +2114,7 @@ void PictureSyntax::reset(int W_, int H_, int ctuLog2_) {
   w4 = (W + 3) >> 2;
   h4 = (H + 3) >> 2;
   cu.clear(); cux.clear(); pu.clear(); pux.clear(); tu.clear(); coef.clear();
+  coef.reserve((size_t)W * H * 3 / 2 + 8192);   // dense blocks: at most every sample of the three planes
   for (int c = 0; c < 2; c++) map[c].assign((size_t)w4 * h4, -1);
   const size_t n = (size_t)wCtu * hCtu;
   sao.assign(n * 3, vvcr_sao());

@@ -5,6 +5,7 @@
 // the parse-time unit rules of CommonLib/UnitTools.cpp; motion vectors are not derived here
 // (vvcp_mv.cpp does that in decoding order afterwards).
 #pragma once
+#include "vvcr_bigbuf.h"
 #include "vvcp_ps.h"
 
 namespace vvcp {
@@ -31,14 +32,14 @@ struct PictureSyntax {
   // geometry
   int W = 0, H = 0, ctuLog2 = 7, ctuSize = 128, wCtu = 0, hCtu = 0, w4 = 0, h4 = 0;
   // rows in decoding order
-  std::vector<vvcr_cu> cu;
-  std::vector<CuAux> cux;
-  std::vector<vvcr_pu> pu;
-  std::vector<PuSyntax> pux;
-  std::vector<vvcr_tu> tu;
-  std::vector<int32_t> coef;
+  bigbuf::vec<vvcr_cu> cu;
+  bigbuf::vec<CuAux> cux;
+  bigbuf::vec<vvcr_pu> pu;
+  bigbuf::vec<PuSyntax> pux;
+  bigbuf::vec<vvcr_tu> tu;
+  bigbuf::vec<int32_t> coef;
   // maps over 4x4 luma units: CU index per channel (-1 = not decoded)
-  std::vector<int32_t> map[2];
+  bigbuf::vec<int32_t> map[2];
   // loop-filter syntax per CTB
   std::vector<vvcr_sao> sao;        // [nCtb][3], merges resolved at finish()
   std::vector<uint8_t> alfEn[3], alfAlt[3], ccCtl[2];

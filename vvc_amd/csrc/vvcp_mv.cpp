@@ -109,7 +109,7 @@ struct Deriver {
   PictureSyntax &S;
   const SPS &sps;
   const PicHeader &ph;
-  std::vector<Mi> &mf;
+  MotionField &mf;
   std::vector<vvcr_geo> &geoRows;
   const std::vector<const MotionPicture *> &dpb;
   const SliceHeader *sh = nullptr;
@@ -124,7 +124,7 @@ struct Deriver {
   std::vector<int> puRef[2], puInterDir, puMrgType;
   std::vector<Mv> puAff[2][3];
 
-  Deriver(PictureUnit &p, std::vector<Mi> &f, std::vector<vvcr_geo> &g, const std::vector<const MotionPicture *> &d)
+  Deriver(PictureUnit &p, MotionField &f, std::vector<vvcr_geo> &g, const std::vector<const MotionPicture *> &d)
       : P(p), S(p.syn), sps(p.sps), ph(p.ph), mf(f), geoRows(g), dpb(d) {}
 
   Mi &at(int x, int y) { return mf[(size_t)(y >> 2) * S.w4 + (x >> 2)]; }
@@ -148,7 +148,7 @@ struct Deriver {
   // Temporal candidates: PU::getColocatedMVP (UnitTools.cpp:1387)
   // ----------------------------------------------------------------------------------------------
   bool colocatedMVP(int l, int px, int py, Mv &out, int refIdx, bool sbFlag) const {
-    if (!col) return false;
+    if (!col || col->intra) return false;
     const int x = px & ~7, y = py & ~7;
     const Mi &mi = col->mf[(size_t)(y >> 2) * col->w4 + (x >> 2)];
     if (!mi.isInter) return false;
@@ -627,7 +627,8 @@ struct Deriver {
     y = std::min(verMax, std::max(verMin, y));
   }
   // PU::getInterMergeSubPuMvpCand (:2872) with the left candidate as the only spatial input
-  bool subPuMvpCand(int ci, const MergeCtx &sp, int count, MvField out[2], int &outDir) {
+  // fill: also build the sub-block motion (only needed when this candidate is the one selected)
+  bool subPuMvpCand(int ci, const MergeCtx &sp, int count, MvField out[2], int &outDir, bool fill) {
     const vvcr_cu &c = S.cu[ci];
     const int colPoc = sh->isInterB() ? refPoc(sh->colFromL0 ? 1 : 0, sh->colRefIdx) : refPoc(0, sh->colRefIdx);
     const int colList = sh->isInterB() ? 1 - (sh->colFromL0 ? 1 : 0) : 0;
@@ -643,7 +644,7 @@ struct Deriver {
     int cx = c.x + (c.w >> 1) + t.h, cy = c.y + (c.h >> 1) + t.v;
     clipColPos(c, cx, cy);
     cx &= ~7; cy &= ~7;
-    if (!col) return false;
+    if (!col || col->intra) return false;
     const Mi &mi = col->mf[(size_t)(cy >> 2) * col->w4 + (cx >> 2)];
     bool found = false;
     outDir = 0;
@@ -660,7 +661,7 @@ struct Deriver {
         }
       }
     }
-    if (!found) return false;
+    if (!found || !fill) return found;
     subW = c.w >> 2;
     subPu.assign((size_t)(c.w >> 2) * (c.h >> 2), Mi());
     const int xOff = (pW >> 1) + t.h, yOff = (pH >> 1) + t.v;
@@ -716,7 +717,7 @@ struct Deriver {
       }
       MvField out[2];
       int dir = 0;
-      if (subPuMvpCand(ci, sp, pos, out, dir)) {
+      if (subPuMvpCand(ci, sp, pos, out, dir, mrgCandIdx == am.numValid)) {
         for (int k = 0; k < 3; k++) { am.mvf[am.numValid << 1][k] = out[0]; am.mvf[(am.numValid << 1) + 1][k] = out[1]; }
         am.interDir[am.numValid] = dir;
         am.affType[am.numValid] = AFF_NUM;
@@ -999,7 +1000,7 @@ struct Deriver {
     const int pi = c.firstpu;
     vvcr_pu &u = S.pu[pi];
     const PuSyntax &s = S.pux[pi];
-    spanParse(ci);
+    if (c.affine || c.geo) spanParse(ci);   // the later spans overwrite every field of other CUs
     if (u.merge) {
       if (u.mmvd) {   // getInterMergeCandidates + getInterMMVDMergeCandidates + setMmvdMergeCandiInfo
         const int base = s.mmvdMergeIdx / 32;
@@ -1183,8 +1184,7 @@ struct Deriver {
         puRef[0][pi] = S.pu[pi].ref0; puRef[1][pi] = S.pu[pi].ref1;
       }
     }
-    mf.assign((size_t)S.w4 * S.h4, Mi());
-    for (Mi &m : mf) { m.ref[0] = m.ref[1] = 0; }   // CodingStructure::initStructData memsets the field
+    mf.alloc((size_t)S.w4 * S.h4, true);   // CodingStructure::initStructData memsets the field
     int curSlice = -1;
     for (size_t i = 0; i < ncu; i++) {
       const vvcr_cu &c = S.cu[i];
@@ -1253,28 +1253,36 @@ struct Deriver {
 
 }  // namespace
 
-void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb, std::vector<Mi> &field,
-                   std::vector<vvcr_motion> &motionRows, std::vector<vvcr_geo> &geoRows) {
+void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb, MotionField &field,
+                   MotionRows &motionRows, std::vector<vvcr_geo> &geoRows) {
   geoRows.clear();
+  bool intra = true;
+  for (const SliceHeader &s : p.slices) intra &= s.isIntra();
+  if (intra) {   // no inter CU: the field stays empty, the rows all-zero (CodingStructure::initStructData)
+    field.reset();
+    motionRows.alloc((size_t)p.syn.w4 * p.syn.h4, true);
+    return;
+  }
   Deriver d(p, field, geoRows, dpb);
   d.run();
-  motionRows.resize(field.size());
+  motionRows.alloc(field.size(), false);
   for (size_t i = 0; i < field.size(); i++) {
     const Mi &m = field[i];
-    vvcr_motion &o = motionRows[i];
+    vvcr_motion &o = motionRows.data()[i];
     o.is_inter = m.isInter; o.inter_dir = m.interDir; o.ref0 = m.ref[0]; o.ref1 = m.ref[1];
     o.mv0x = m.mv[0][0]; o.mv0y = m.mv[0][1]; o.mv1x = m.mv[1][0]; o.mv1y = m.mv[1][1];
     o.bcw = m.bcw; o.alt_hpel = m.altHpel;
   }
 }
 
-void refine_motion(const PictureUnit &p, const std::vector<Mi> &field, const int32_t *deltas, int64_t ndeltas,
+void refine_motion(const PictureUnit &p, MotionField &&field, const int32_t *deltas, int64_t ndeltas,
                    MotionPicture &out) {
   const PictureSyntax &S = p.syn;
   out.poc = p.poc;
   out.w4 = S.w4;
   out.h4 = S.h4;
-  out.mf = field;
+  out.intra = field.empty();
+  out.mf = std::move(field);
   out.slices.resize(p.slices.size());
   for (size_t s = 0; s < p.slices.size(); s++)
     for (int l = 0; l < 2; l++)

@@ -3,6 +3,10 @@
 // PU:: candidate-list tools of CommonLib/UnitTools.cpp), in decoding order, CU by CU, with the
 // history-based candidate table (CodingStructure::addMiToLut) and the collocated picture's motion.
 #pragma once
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <new>
 #include <vector>
 
 #include "vvcp_ctu.h"
@@ -27,11 +31,45 @@ struct SliceRefs {
   bool refLT[2][VVCR_MAX_REF];
 };
 
+// A large uninitialised array from the buffer cache (vvcr_bigbuf.h): the 4x4 motion field and the
+// motion rows handed to the reconstruction path (vvcr_picture_submit's `motion`), whose passes write every
+// entry, or zero them at allocation.
+template <class T>
+struct RawArray {
+  T *p = nullptr;
+  size_t n = 0;
+  RawArray() = default;
+  RawArray(const RawArray &) = delete;
+  RawArray &operator=(const RawArray &) = delete;
+  RawArray(RawArray &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  RawArray &operator=(RawArray &&o) noexcept {
+    if (this != &o) { reset(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+    return *this;
+  }
+  ~RawArray() { reset(); }
+  void reset() { bigbuf::release(p, n * sizeof(T)); p = nullptr; n = 0; }
+  void alloc(size_t count, bool zero) {
+    reset();
+    p = static_cast<T *>(bigbuf::alloc(count * sizeof(T)));
+    n = count;
+    if (zero) std::memset((void *)p, 0, count * sizeof(T));
+  }
+  T *data() { return p; }
+  const T *data() const { return p; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  T &operator[](size_t i) { return p[i]; }
+  const T &operator[](size_t i) const { return p[i]; }
+};
+using MotionRows = RawArray<vvcr_motion>;
+using MotionField = RawArray<Mi>;   // all-zero = CodingStructure::initStructData's memset
+
 // Motion of a decoded picture as later pictures' temporal candidates see it: the 4x4 field after
 // CS::setRefinedMotionField (UnitTools.cpp:68), i.e. with the DMVR refinements written back.
 struct MotionPicture {
   int poc = 0, w4 = 0, h4 = 0;
-  std::vector<Mi> mf;
+  bool intra = false;              // every slice intra: no motion (mf empty), never a temporal candidate
+  MotionField mf;
   std::vector<SliceRefs> slices;
 };
 
@@ -40,13 +78,13 @@ struct PictureUnit;
 // Derives the motion of picture p (all slices), given the already decoded pictures (for the collocated
 // reference, looked up by POC). Fills the MV-dependent fields of p.syn's rows, the 4x4 field (pre-DMVR,
 // as deblocking reads it) and the GEO candidate rows; returns the 4x4 field in `field`.
-void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb, std::vector<Mi> &field,
-                   std::vector<vvcr_motion> &motionRows, std::vector<vvcr_geo> &geoRows);
+void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb, MotionField &field,
+                   MotionRows &motionRows, std::vector<vvcr_geo> &geoRows);
 
-// CS::setRefinedMotionField: the collocated-reference view of p, given its pre-DMVR field and the
-// DMVR deltas of its PUs (vvcr_get_dmvr_deltas order: PUs with pu.dmvr in row order, 16x16 sub-blocks
-// in raster order). deltas may be null when no PU of the picture uses DMVR.
-void refine_motion(const PictureUnit &p, const std::vector<Mi> &field, const int32_t *deltas, int64_t ndeltas,
+// CS::setRefinedMotionField: the collocated-reference view of p, given its pre-DMVR field (taken over,
+// refined in place) and the DMVR deltas of its PUs (vvcr_get_dmvr_deltas order: PUs with pu.dmvr in row
+// order, 16x16 sub-blocks in raster order). deltas may be null when no PU of the picture uses DMVR.
+void refine_motion(const PictureUnit &p, MotionField &&field, const int32_t *deltas, int64_t ndeltas,
                    MotionPicture &out);
 
 }  // namespace vvcp

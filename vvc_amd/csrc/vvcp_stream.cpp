@@ -174,7 +174,7 @@ void Stream::refine_motion(int idx, const int32_t *deltas, int64_t n) {
   PictureUnit &p = *pics.at(idx);
   VVCP_CHECK(!p.derived, "picture motion not derived");
   std::unique_ptr<MotionPicture> m(new MotionPicture());
-  vvcp::refine_motion(p, p.field, deltas, n, *m);
+  vvcp::refine_motion(p, std::move(p.field), deltas, n, *m);
   p.refined = std::move(m);
   // pictures far behind in decoding order are no longer collocated candidates
   if (idx >= 64 && pics[idx - 64]->refined) pics[idx - 64]->refined.reset();

@@ -23,8 +23,8 @@ struct PictureUnit {
   PictureSyntax syn;
   bool parsed = false, failed = false;
   // motion (derive_motion): the 4x4 field before DMVR, its row form and the GEO candidate rows
-  std::vector<Mi> field;
-  std::vector<vvcr_motion> motion;
+  MotionField field;
+  MotionRows motion;
   std::vector<vvcr_geo> geo;
   bool derived = false;
   std::unique_ptr<MotionPicture> refined;   // set by refine_motion; read as a collocated picture
