@@ -16,7 +16,7 @@ from vvc_amd import capfile, parser, stream
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 STREAMS = ["ai416_q37", "ailm416_q37", "ra416_q32", "ralm416_q32", "rawp416_q32", "ratile416_q32", "ra412c_q32",
-           "ra1080_q32", "ratile1080_q32", "aibdpcm416_q32", "radq0416_q32", "rageo480_q32"]
+           "ra1080_q32", "ratile1080_q32", "rawp1080_q32", "aibdpcm416_q32", "radq0416_q32", "rageo480_q32"]
 
 
 def _fields(pp):

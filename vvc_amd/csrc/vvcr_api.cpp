@@ -45,7 +45,7 @@ struct DevVec {
     ensure(n + 1);
     if (n) VVCR_CHECK_HIP(hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
   }
-  void upload(const std::vector<T> &v) { upload(v.data(), v.size()); }
+  template <class A> void upload(const std::vector<T, A> &v) { upload(v.data(), v.size()); }
   DevVec() = default;
   DevVec(const DevVec &) = delete;
   DevVec &operator=(const DevVec &) = delete;
@@ -383,7 +383,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   }
   if (mask & VVCR_STAGE_INTER) {
     {   // 32x32 tiles first, then the small jobs, in one buffer
-      std::vector<McJob> all(wl.mc_tile);
+      bigbuf::vec<McJob> all(wl.mc_tile);
       all.insert(all.end(), wl.mc_basic.begin(), wl.mc_basic.end());
       r.mc_basic.upload(all);
     }
@@ -446,8 +446,8 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.alg_bytes[K_INTRA] = b;
   }
   if (mask & VVCR_STAGE_DBK) {
-    std::vector<DbkSeg> all;
-    const std::vector<DbkSeg> *parts[4] = {&bp.dbk.luma[0], &bp.dbk.chroma[0], &bp.dbk.luma[1], &bp.dbk.chroma[1]};
+    bigbuf::vec<DbkSeg> all;
+    const bigbuf::vec<DbkSeg> *parts[4] = {&bp.dbk.luma[0], &bp.dbk.chroma[0], &bp.dbk.luma[1], &bp.dbk.chroma[1]};
     for (int k = 0; k < 4; k++) {
       r.dbk_counts[k] = (int)parts[k]->size();
       all.insert(all.end(), parts[k]->begin(), parts[k]->end());

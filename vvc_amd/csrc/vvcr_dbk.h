@@ -1,5 +1,6 @@
 // vvcr_dbk.h — deblocking: host edge planning (vvcr_dbk_host.cpp) and GPU filtering (vvcr_dbk.hip).
 #pragma once
+#include "vvcr_bigbuf.h"
 #include <memory>
 #include "vvcr_host.h"
 
@@ -14,7 +15,7 @@ struct DbkSeg {
 static_assert(sizeof(DbkSeg) == 8, "DbkSeg layout");
 
 struct DbkLists {
-  std::vector<DbkSeg> luma[2], chroma[2];   // [VER, HOR]
+  bigbuf::vec<DbkSeg> luma[2], chroma[2];   // [VER, HOR]
   void clear() { for (int d = 0; d < 2; d++) { luma[d].clear(); chroma[d].clear(); } }
   size_t total() const { return luma[0].size() + luma[1].size() + chroma[0].size() + chroma[1].size(); }
 };

@@ -26,7 +26,7 @@ struct Planner {
   const PictureDescriptors &d;
   DbkLists &out;
   int W4, H4, ctu, parts;
-  std::vector<int> cu_map[2], tu_map[2];
+  bigbuf::vec<int> cu_map[2], tu_map[2];
   // per-CU scratch in CTU-relative coordinates (the reference's per-CTU arrays, LoopFilter.h:66-79)
   int ctu_x = 0, ctu_y = 0;
   uint8_t bs[2][32 * 32];
@@ -64,7 +64,7 @@ struct Planner {
     }
     return t;
   }
-  void fill(std::vector<int> &m, int x, int y, int w, int h, int s, int v) {
+  void fill(bigbuf::vec<int> &m, int x, int y, int w, int h, int s, int v) {
     for (int j = y >> s; j < (y + h + (1 << s) - 1) >> s; j++)
       for (int i = x >> s; i < (x + w + (1 << s) - 1) >> s; i++) m[(size_t)j * W4 + i] = v;
   }

@@ -24,7 +24,7 @@ bool identical_motion(const vvcr_pic_params &pp, int interDir, int r0, int r1, i
   return pp.ref_poc[0][r0] == pp.ref_poc[1][r1] && mv0x == mv1x && mv0y == mv1y;
 }
 
-void push_tiles(std::vector<McJob> &out, int x0, int y0, int w, int h, McJob proto) {
+void push_tiles(bigbuf::vec<McJob> &out, int x0, int y0, int w, int h, McJob proto) {
   for (int y = 0; y < h; y += 16)
     for (int x = 0; x < w; x += 16) {
       McJob j = proto;
@@ -164,7 +164,7 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
   }
 }
 
-void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, std::vector<TbJob> &out);
+void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out);
 
 namespace {
 
@@ -244,7 +244,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   // small blocks first (64-lane workgroups), then the large ones (256 lanes)
   wl.tb_small = (int)(std::stable_partition(wl.tb.begin(), wl.tb.end(), [](const TbJob &j) { return j.w * j.h <= 256; }) - wl.tb.begin());
   const int W4 = sp.width / 4;
-  std::vector<int> geo_of(d.cu.size(), -1);
+  bigbuf::vec<int> geo_of(d.cu.size(), -1);
   for (size_t g = 0; g < d.geo.size(); g++)
     if (d.geo[g].cu >= 0 && d.geo[g].cu < (int)d.cu.size()) geo_of[d.geo[g].cu] = (int)g;
   int ry0 = 1 << 30, ry1 = -(1 << 30);   // reference rows read (luma), with filter / DMVR / BDOF margins
@@ -355,7 +355,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   }
   // bi-predicted work first (about twice the work of a uni job): the long jobs start in the first
   // dispatch rounds instead of forming the launch's tail
-  auto bi_first = [](std::vector<McJob> &v) {
+  auto bi_first = [](bigbuf::vec<McJob> &v) {
     std::stable_partition(v.begin(), v.end(), [](const McJob &j) { return (j.flags & (MC_L0 | MC_L1)) == (MC_L0 | MC_L1); });
   };
   bi_first(wl.mc_tile);
@@ -364,7 +364,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
     const AffPu &U = wl.aff_pu[j.pu];
     return U.l[0].present && U.l[1].present;
   });
-  for (const std::vector<McJob> *v : {&wl.mc_tile, &wl.mc_basic, &wl.mc_bidir})
+  for (const bigbuf::vec<McJob> *v : {&wl.mc_tile, &wl.mc_basic, &wl.mc_bidir})
     for (const McJob &j : *v)
       for (int l = 0; l < 2; l++)
         if (j.flags & (l ? MC_L1 : MC_L0)) reach(j.y, j.h, j.mv[l][1]);
@@ -483,10 +483,10 @@ void tr_types(const vvcr_pic_params &pp, const vvcr_cu &cu, int comp, int w, int
 }
 }  // namespace
 
-void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, std::vector<TbJob> &out) {
+void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out) {
   out.clear();
   const int W4 = sp.width / 4, H4 = sp.height / 4;
-  std::vector<int> lmap;   // luma PU per 4x4, for co-located luma modes (PU::getCoLocatedIntraLumaMode)
+  bigbuf::vec<int> lmap;   // luma PU per 4x4, for co-located luma modes (PU::getCoLocatedIntraLumaMode)
   bool haveMap = false;
   static const int kIct[2][4] = {{0, 3, 1, 2}, {0, -3, -1, -2}};
   for (const vvcr_tu &t : d.tu) {

@@ -1,25 +1,26 @@
 // vvcr_host.h — host side of libvvcr: per-picture descriptor store and work-list construction.
 #pragma once
+#include "vvcr_bigbuf.h"
 #include <vector>
 #include "vvcr_internal.h"
 
 struct PictureDescriptors {
-  std::vector<vvcr_cu> cu;
-  std::vector<vvcr_pu> pu;
-  std::vector<vvcr_tu> tu;
-  std::vector<int32_t> coef;
-  std::vector<vvcr_motion> motion;
-  std::vector<vvcr_geo> geo;
+  bigbuf::vec<vvcr_cu> cu;
+  bigbuf::vec<vvcr_pu> pu;
+  bigbuf::vec<vvcr_tu> tu;
+  bigbuf::vec<int32_t> coef;
+  bigbuf::vec<vvcr_motion> motion;
+  bigbuf::vec<vvcr_geo> geo;
   void clear() { cu.clear(); pu.clear(); tu.clear(); coef.clear(); motion.clear(); geo.clear(); }
 };
 
 struct WorkLists {
-  std::vector<McJob> mc_tile;      // plain uni/bi/BCW/GEO/CIIP-inter MC of PUs >= 32x32: 32x32 tiles (k_mc_tile)
-  std::vector<McJob> mc_basic;     // the other plain MC blocks (<= 16x16 jobs, incl. SbTMVP sub-blocks)
-  std::vector<McJob> mc_bidir;     // DMVR sub-blocks and BDOF tiles
-  std::vector<AffPu> aff_pu;       // affine PUs
-  std::vector<AffJob> aff_jobs;    // affine tiles
-  std::vector<TbJob> tb;           // coded transform blocks (the tb_small blocks of <= 256 samples first)
+  bigbuf::vec<McJob> mc_tile;      // plain uni/bi/BCW/GEO/CIIP-inter MC of PUs >= 32x32: 32x32 tiles (k_mc_tile)
+  bigbuf::vec<McJob> mc_basic;     // the other plain MC blocks (<= 16x16 jobs, incl. SbTMVP sub-blocks)
+  bigbuf::vec<McJob> mc_bidir;     // DMVR sub-blocks and BDOF tiles
+  bigbuf::vec<AffPu> aff_pu;       // affine PUs
+  bigbuf::vec<AffJob> aff_jobs;    // affine tiles
+  bigbuf::vec<TbJob> tb;           // coded transform blocks (the tb_small blocks of <= 256 samples first)
   int tb_small = 0;
   int n_dmvr = 0;                  // DMVR sub-blocks (delta outputs), in PU order
   int n_unsupported_inter = 0;     // PUs needing kernels not built yet (reported, never silently skipped)
@@ -35,7 +36,7 @@ struct WorkLists {
 // Grouped diagonal scans (Rom.cpp:321-370) and the LFNST top-left 8x8 scan (Rom.cpp:385-403) as
 // raster indices, for every power-of-two block size; uploaded once per context.
 struct ScanTables {
-  std::vector<uint16_t> data;
+  bigbuf::vec<uint16_t> data;
   int32_t off[7][7];
   int32_t lfnst_off[7];
 };

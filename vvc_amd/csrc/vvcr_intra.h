@@ -10,6 +10,7 @@
 // per step (1 + the highest level among the units it reads); all steps of one level are independent and
 // run as one launch, levels in increasing order. Inter CUs (no intra neighbours) are level 0.
 #pragma once
+#include "vvcr_bigbuf.h"
 #include "vvcr_host.h"
 
 enum : uint8_t {
@@ -97,13 +98,13 @@ struct ReconTile {
 };
 
 struct IntraPlan {
-  std::vector<ReconTile> inter_tiles;
-  std::vector<IntraJob> jobs;        // grouped by CTU (raster order), by level inside a CTU
-  std::vector<int32_t> ctu_list;     // raster index of every CTU that has steps
-  std::vector<int32_t> ctu_start;    // steps of ctu_list[c]: [ctu_start[c], ctu_start[c+1])
-  std::vector<int32_t> dep_start;    // step i waits for deps[dep_start[i] .. dep_start[i+1]):
-  std::vector<int32_t> deps;         //   v >= 0: step ctu_start[c] + v of its own CTU; v < 0: global step ~v
-  std::vector<int32_t> order[2];     // per 4x4 luma unit / 2x2 chroma unit: seq of the step that decodes it
+  bigbuf::vec<ReconTile> inter_tiles;
+  bigbuf::vec<IntraJob> jobs;        // grouped by CTU (raster order), by level inside a CTU
+  bigbuf::vec<int32_t> ctu_list;     // raster index of every CTU that has steps
+  bigbuf::vec<int32_t> ctu_start;    // steps of ctu_list[c]: [ctu_start[c], ctu_start[c+1])
+  bigbuf::vec<int32_t> dep_start;    // step i waits for deps[dep_start[i] .. dep_start[i+1]):
+  bigbuf::vec<int32_t> deps;         //   v >= 0: step ctu_start[c] + v of its own CTU; v < 0: global step ~v
+  bigbuf::vec<int32_t> order[2];     // per 4x4 luma unit / 2x2 chroma unit: seq of the step that decodes it
   void clear() {
     inter_tiles.clear(); jobs.clear(); ctu_list.clear(); ctu_start.clear(); dep_start.clear(); deps.clear(); order[0].clear(); order[1].clear();
   }

@@ -92,14 +92,14 @@ struct Planner {
   const PictureDescriptors &d;
   IntraPlan &out;
   int W4, H4, ctu;
-  std::vector<int32_t> level[2];
-  std::vector<int32_t> prod[3];     // per unit of each component: the step (index into jobs) that reconstructs it, -1 = inter
-  std::vector<int32_t> cu_map;      // luma 4x4 unit -> CU index (for CIIP neighbour tests)
-  std::vector<std::pair<int32_t, IntraJob>> jobs;   // (level, job)
-  std::vector<int32_t> dep_off{0}, dep_flat;        // per job (CSR): the steps it reads from (indices into jobs)
-  std::vector<int32_t> cur;                         // dependencies of the step being planned
-  std::vector<int32_t> cur_mark;                    // per job: the step count at which it last entered `cur`
-  std::vector<int32_t> cclm_deps;                   // scratch of intra_chroma
+  bigbuf::vec<int32_t> level[2];
+  bigbuf::vec<int32_t> prod[3];     // per unit of each component: the step (index into jobs) that reconstructs it, -1 = inter
+  bigbuf::vec<int32_t> cu_map;      // luma 4x4 unit -> CU index (for CIIP neighbour tests)
+  bigbuf::vec<std::pair<int32_t, IntraJob>> jobs;   // (level, job)
+  bigbuf::vec<int32_t> dep_off{0}, dep_flat;        // per job (CSR): the steps it reads from (indices into jobs)
+  bigbuf::vec<int32_t> cur;                         // dependencies of the step being planned
+  bigbuf::vec<int32_t> cur_mark;                    // per job: the step count at which it last entered `cur`
+  bigbuf::vec<int32_t> cclm_deps;                   // scratch of intra_chroma
   void add_dep(int32_t pr) {   // O(1) de-duplication (a CCLM block reads hundreds of luma units)
     if ((size_t)pr >= cur_mark.size()) cur_mark.resize(std::max<size_t>(2 * cur_mark.size(), (size_t)pr + 1024), -1);
     const int32_t tok = (int32_t)jobs.size();
@@ -110,7 +110,7 @@ struct Planner {
   // Slice / tile of every CTU (getCURestricted: a neighbour is usable only inside the same slice and
   // tile, CodingStructure.cpp:1519-1537, CU::isSameSliceAndTile UnitTools.cpp:170); cur_reg is the
   // region of the CU being planned / the step being resolved.
-  std::vector<int32_t> ctu_reg;
+  bigbuf::vec<int32_t> ctu_reg;
   int wc = 1, cur_reg = 0;
   int region_at(int lx, int ly) const { return ctu_reg[(size_t)(ly >> sp.ctu_log2) * wc + (lx >> sp.ctu_log2)]; }
 
