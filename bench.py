@@ -195,11 +195,16 @@ class BitstreamE2E:
         self.seg_ex = cf.ThreadPoolExecutor(segments)
         self.lock = threading.Lock()
         self.final = [None] * segments   # per segment: {slot: poc} after its last decode
+        self.times = {}                  # summed per-phase seconds of the decode threads
+        self.tlock = threading.Lock()
 
     def _decode(self, c):
         seq = self.B.SequenceDecode(self.ctx, self.data, self.pool, nslots=self.per, base=self.per * c,
                                     launch_lock=self.lock)
         seq.run()
+        with self.tlock:
+            for k, v in seq.times.items():
+                self.times[k] = self.times.get(k, 0.0) + v
         owner = {}
         for i, inf in enumerate(seq.plan.info):
             owner[seq.plan.slot[i]] = inf["poc"]
@@ -309,6 +314,7 @@ def main():
     if a.warmup > 0:
         e2e.run(a.warmup)
         ctx.sync()
+    e2e.times = {}
     R.barrier()
     ctx.sync()
     t0 = time.perf_counter()
@@ -440,6 +446,7 @@ def main():
         "value_scope": "end to end from the bitstream: NAL/header parsing, CABAC (host threads), motion derivation "
                        "with the GPU's DMVR feedback, host planning, upload, GPU reconstruction and loop filters, every "
                        "picture of every step; %d independent decodes in flight" % a.segments,
+        "host_ms_per_picture": {k: round(v / (a.steps * len(infos)) * 1e3, 3) for k, v in e2e.times.items()},
         "roofline": roof,
         "cpu_baseline": None,
         "resident": resident,

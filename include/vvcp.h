@@ -63,7 +63,8 @@ int vvcp_alf_filters(const vvcp_stream *s, int32_t idx, int16_t *luma_coef, int1
  * references), vvcr_picture_submit of the rows, vvcr_picture_set_loop_filter_params (SAO, ALF / CC-ALF)
  * and vvcr_picture_plan(stage_mask), in native code. On success *out is the planned picture (the
  * caller uploads it with vvcr_prepare_planned and frees it with vvcr_picture_destroy). Thread-safe for
- * different pictures. */
+ * different pictures. The picture's TU rows, coefficient pool and motion rows are handed over, not
+ * copied: afterwards vvcp_picture_rows returns them empty and the picture cannot be planned again. */
 int vvcp_plan_picture(vvcp_stream *s, int32_t idx, const vvcr_seq_params *sp, int32_t slot, const int32_t *ref_slot,
                       uint32_t stage_mask, vvcr_picture **out);
 

@@ -14,6 +14,7 @@ reference and its output; output is POC order within a coded video sequence (IDR
 import ctypes as C
 import concurrent.futures as cf
 import threading
+import time
 
 import numpy as np
 
@@ -117,6 +118,17 @@ class SequenceDecode:
         self.stages = stages
         self.lock = launch_lock or threading.Lock()
         self.keep = keep
+        # seconds this decode's thread spent per phase (waiting on the parse pool, on the GPU's DMVR
+        # deltas, deriving motion, planning, uploading, launching)
+        self.times = dict.fromkeys(("parse", "parse_wait", "dmvr_wait", "derive", "plan", "prepare", "launch"), 0.0)
+        self._tlock = threading.Lock()
+
+    def _parse(self, i):
+        t0 = time.perf_counter()
+        self.s.parse(i)
+        dt = time.perf_counter() - t0
+        with self._tlock:
+            self.times["parse"] += dt   # on the pool's threads
 
     def _plan_picture(self, i):
         rs = self.plan.ref_slots(i)
@@ -131,7 +143,7 @@ class SequenceDecode:
         """Decodes the stream; returns [(poc, slot)] in output order, and with keep_handles also the
         prepared-picture handles in decoding order (not released: the caller may launch them again)."""
         n = len(self.s)
-        parsed = [self.pool.submit(self.s.parse, i) for i in range(n)]
+        parsed = [self.pool.submit(self._parse, i) for i in range(n)]
         handles = {}          # decode index -> prepared-picture handle
         n_dmvr = {}
         refined = set()
@@ -139,8 +151,12 @@ class SequenceDecode:
         out_pos = 0
         out = self.plan.out_order
         try:
+            T = self.times
+            clk = time.perf_counter
             for i in range(n):
+                t0 = clk()
                 parsed[i].result()
+                t1 = clk()
                 # the collocated picture is one of the references: refine those still pending
                 for l in range(2):
                     for poc in self.plan.refs[i][l]:
@@ -149,15 +165,27 @@ class SequenceDecode:
                             d = self.ctx.picture_dmvr_deltas(handles[j], n_dmvr[j])
                             self.s.refine(j, d)
                             refined.add(j)
+                t2 = clk()
                 self.s.derive(i)
+                t3 = clk()
                 pic = self._plan_picture(i)
+                t4 = clk()
                 try:
                     n_dmvr[i] = pic.work_counts()["dmvr"]
                     h = self.ctx.prepare_planned(pic)
                 finally:
                     pic.close()
+                t5 = clk()
                 with self.lock:
                     self.ctx.launch(h)
+                t6 = clk()
+                with self._tlock:
+                    T["parse_wait"] += t1 - t0
+                T["dmvr_wait"] += t2 - t1
+                T["derive"] += t3 - t2
+                T["plan"] += t4 - t3
+                T["prepare"] += t5 - t4
+                T["launch"] += t6 - t5
                 handles[i] = h
                 live.append(i)
                 if not self.plan.referenced[i]:

@@ -31,36 +31,9 @@ struct SliceRefs {
   bool refLT[2][VVCR_MAX_REF];
 };
 
-// A large uninitialised array from the buffer cache (vvcr_bigbuf.h): the 4x4 motion field and the
-// motion rows handed to the reconstruction path (vvcr_picture_submit's `motion`), whose passes write every
-// entry, or zero them at allocation.
-template <class T>
-struct RawArray {
-  T *p = nullptr;
-  size_t n = 0;
-  RawArray() = default;
-  RawArray(const RawArray &) = delete;
-  RawArray &operator=(const RawArray &) = delete;
-  RawArray(RawArray &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
-  RawArray &operator=(RawArray &&o) noexcept {
-    if (this != &o) { reset(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
-    return *this;
-  }
-  ~RawArray() { reset(); }
-  void reset() { bigbuf::release(p, n * sizeof(T)); p = nullptr; n = 0; }
-  void alloc(size_t count, bool zero) {
-    reset();
-    p = static_cast<T *>(bigbuf::alloc(count * sizeof(T)));
-    n = count;
-    if (zero) std::memset((void *)p, 0, count * sizeof(T));
-  }
-  T *data() { return p; }
-  const T *data() const { return p; }
-  size_t size() const { return n; }
-  bool empty() const { return n == 0; }
-  T &operator[](size_t i) { return p[i]; }
-  const T &operator[](size_t i) const { return p[i]; }
-};
+// the 4x4 motion field and the motion rows handed to the reconstruction path (vvcr_picture_submit's
+// `motion`): uninitialised arrays from the large-buffer cache whose passes write every entry
+template <class T> using RawArray = bigbuf::raw<T>;
 using MotionRows = RawArray<vvcr_motion>;
 using MotionField = RawArray<Mi>;   // all-zero = CodingStructure::initStructData's memset
 

@@ -6,6 +6,7 @@
 
 #include "vvcp.h"
 #include "vvcp_params.h"
+#include "vvcr_host.h"
 
 namespace {
 int fail(vvcr_picture *pic, int rc, const char *what) {
@@ -19,8 +20,8 @@ extern "C" int vvcp_plan_picture(vvcp_stream *h, int32_t idx, const vvcr_seq_par
                                  const int32_t *ref_slot, uint32_t stage_mask, vvcr_picture **out) {
   if (!h || !sp || !out || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
   *out = nullptr;
-  const vvcp::PictureUnit &p = *h->s.pics[idx];
-  if (!p.derived) return VVCR_E_STATE;
+  vvcp::PictureUnit &p = *h->s.pics[idx];
+  if (!p.derived || p.handedOver) return VVCR_E_STATE;
   vvcr_pic_params pp;
   vvcp::AlfFilters alf;
   try {
@@ -39,11 +40,23 @@ extern "C" int vvcp_plan_picture(vvcp_stream *h, int32_t idx, const vvcr_seq_par
   vvcr_picture *pic = nullptr;
   int rc = vvcr_picture_create(sp, &pp, &pic);
   if (rc) return fail(nullptr, rc, "vvcr_picture_create");
-  const vvcp::PictureSyntax &S = p.syn;
-  rc = vvcr_picture_submit(pic, S.cu.data(), (int32_t)S.cu.size(), S.pu.data(), (int32_t)S.pu.size(), S.tu.data(),
-                           (int32_t)S.tu.size(), S.coef.data(), (int64_t)S.coef.size(), p.motion.data(), p.geo.data(),
-                           (int32_t)p.geo.size());
-  if (rc) return fail(pic, rc, "vvcr_picture_submit");
+  vvcp::PictureSyntax &S = p.syn;
+  try {
+    // the transform rows, coefficient pool and motion rows move to the picture (nothing on the host reads
+    // them again); CU / PU rows are copied: refine_motion still reads them
+    PictureDescriptors D;
+    D.cu.assign(S.cu.begin(), S.cu.end());
+    D.pu.assign(S.pu.begin(), S.pu.end());
+    D.tu = std::move(S.tu);
+    D.coef = std::move(S.coef);
+    D.motion = std::move(p.motion);
+    D.geo.assign(p.geo.begin(), p.geo.end());
+    vvcr_picture_adopt(pic, std::move(D));
+  } catch (const std::exception &e) {
+    vvcp::set_api_error(std::string("vvcr_picture_submit: ") + e.what());
+    vvcr_picture_destroy(pic);
+    return VVCR_E_ARG;
+  }
   // loop-filter parameters as vvc_amd/stream.py set_loop_filter_params arranges them
   const size_t n = S.alfFset.size();
   std::vector<uint8_t> en(3 * n), alt(3 * n), cc(2 * n);
@@ -71,6 +84,7 @@ extern "C" int vvcp_plan_picture(vvcp_stream *h, int32_t idx, const vvcr_seq_par
   if (rc) return fail(pic, rc, "vvcr_picture_set_loop_filter_params");
   rc = vvcr_picture_plan(pic, stage_mask);
   if (rc) return fail(pic, rc, "vvcr_picture_plan");
+  p.handedOver = true;
   *out = pic;
   return VVCR_OK;
 }

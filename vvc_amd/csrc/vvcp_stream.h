@@ -27,6 +27,7 @@ struct PictureUnit {
   MotionRows motion;
   std::vector<vvcr_geo> geo;
   bool derived = false;
+  bool handedOver = false;   // vvcp_plan_picture moved the TU rows, coefficients and motion rows out
   std::unique_ptr<MotionPicture> refined;   // set by refine_motion; read as a collocated picture
 };
 

@@ -801,6 +801,15 @@ static void pic_submit(vvcr_picture &b, const vvcr_cu *cu, int32_t ncu, const vv
   b.submitted = true;
 }
 
+// In-library producers (the host parser, vvcp_plan.cpp) hand their arrays over instead of copying them.
+extern "C++" void vvcr_picture_adopt(vvcr_picture *pic, PictureDescriptors &&d) {
+  if (!pic) throw VvcrError(VVCR_E_ARG, "null picture");
+  pic->desc = std::move(d);
+  pic->planned = false;
+  validate_descriptors(pic->sp, pic->pp, pic->desc);
+  pic->submitted = true;
+}
+
 static void pic_set_lf(vvcr_picture &b, const vvcr_sao *sao, const vvcr_alf *alf) {
   const int n = n_ctb(b.sp);
   b.planned = false;

@@ -7,6 +7,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <new>
 #include <unordered_map>
@@ -89,5 +90,39 @@ struct Alloc {
 };
 
 template <class T> using vec = std::vector<T, Alloc<T>>;
+
+// an array of trivially copyable T from the cache, NOT initialised unless asked (alloc(n, true) zeroes)
+template <class T>
+struct raw {
+  T *p = nullptr;
+  size_t n = 0;
+  raw() = default;
+  raw(const raw &) = delete;
+  raw &operator=(const raw &) = delete;
+  raw(raw &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+  raw &operator=(raw &&o) noexcept {
+    if (this != &o) { reset(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+    return *this;
+  }
+  ~raw() { reset(); }
+  void reset() { release(p, n * sizeof(T)); p = nullptr; n = 0; }
+  void clear() { reset(); }
+  void alloc(size_t count, bool zero) {
+    reset();
+    p = static_cast<T *>(bigbuf::alloc(count * sizeof(T)));
+    n = count;
+    if (zero) std::memset((void *)p, 0, count * sizeof(T));
+  }
+  void assign(const T *b, const T *e) {
+    alloc((size_t)(e - b), false);
+    if (n) std::memcpy((void *)p, b, n * sizeof(T));
+  }
+  T *data() { return p; }
+  const T *data() const { return p; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  T &operator[](size_t i) { return p[i]; }
+  const T &operator[](size_t i) const { return p[i]; }
+};
 
 }  // namespace bigbuf

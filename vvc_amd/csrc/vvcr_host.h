@@ -9,10 +9,14 @@ struct PictureDescriptors {
   bigbuf::vec<vvcr_pu> pu;
   bigbuf::vec<vvcr_tu> tu;
   bigbuf::vec<int32_t> coef;
-  bigbuf::vec<vvcr_motion> motion;
+  bigbuf::raw<vvcr_motion> motion;
   bigbuf::vec<vvcr_geo> geo;
   void clear() { cu.clear(); pu.clear(); tu.clear(); coef.clear(); motion.clear(); geo.clear(); }
 };
+
+// Hands a producer's descriptor arrays to a picture (vvcr_picture_submit without the copies; validates
+// them the same way). For producers inside the library (vvcp_plan.cpp); throws VvcrError.
+void vvcr_picture_adopt(vvcr_picture *pic, PictureDescriptors &&d);
 
 struct WorkLists {
   bigbuf::vec<McJob> mc_tile;      // plain uni/bi/BCW/GEO/CIIP-inter MC of PUs >= 32x32: 32x32 tiles (k_mc_tile)
