@@ -180,34 +180,32 @@ class BitstreamE2E:
     """The headline: bitstream in, pictures out, everything in the timed region.
 
     Every step decodes the .bin again from its first NAL: a fresh host parser (vvcp_open: NAL split and
-    every header), the CABAC pass of each picture on a shared pool of `threads` threads, motion
-    derivation in decoding order with each collocated picture's DMVR deltas from the GPU, native
-    planning (vvcp_plan_picture), upload (vvcr_prepare_planned) and the GPU. Steps run as `segments`
-    independent decodes in flight at once, each on its own DPB slot range and host thread (a serving
-    process decoding several streams), launches serialised by one lock."""
+    every header), then one native decode loop (vvcp_decode, GIL released): the CABAC pass of each
+    picture on threads // segments parser threads, motion derivation in decoding order with each
+    collocated picture's DMVR deltas from the GPU, native planning (vvcp_plan_picture), upload
+    (vvcr_prepare_planned) and the GPU. Steps run as `segments` independent decodes in flight at once,
+    each on its own DPB slot range and host thread (a serving process decoding several streams)."""
 
     def __init__(self, ctx, data, per, segments, threads):
         import concurrent.futures as cf
         import threading
         from vvc_amd import bitstream as B
         self.B, self.ctx, self.data, self.per, self.segments = B, ctx, data, per, segments
-        self.pool = cf.ThreadPoolExecutor(threads)
+        self.parse_threads = max(1, threads // segments)   # parser threads per decode (vvcp_decode)
         self.seg_ex = cf.ThreadPoolExecutor(segments)
-        self.lock = threading.Lock()
         self.final = [None] * segments   # per segment: {slot: poc} after its last decode
         self.times = {}                  # summed per-phase seconds of the decode threads
         self.tlock = threading.Lock()
 
     def _decode(self, c):
-        seq = self.B.SequenceDecode(self.ctx, self.data, self.pool, nslots=self.per, base=self.per * c,
-                                    launch_lock=self.lock)
+        seq = self.B.SequenceDecode(self.ctx, self.data, nslots=self.per, base=self.per * c, threads=self.parse_threads)
         seq.run()
         with self.tlock:
             for k, v in seq.times.items():
                 self.times[k] = self.times.get(k, 0.0) + v
         owner = {}
-        for i, inf in enumerate(seq.plan.info):
-            owner[seq.plan.slot[i]] = inf["poc"]
+        for i, inf in enumerate(seq.info):
+            owner[seq.slot[i]] = inf["poc"]
         self.final[c] = owner
 
     def _segment(self, c, n):
@@ -223,14 +221,12 @@ class BitstreamE2E:
 
     def close(self):
         self.ctx.sync()
-        self.pool.shutdown()
         self.seg_ex.shutdown()
 
 
 def output_yuv_md5(ctx, data, meta):
     """One decode with DecoderApp's output: the YUV file's MD5 (vvcr_write_output, output order) and
     every output picture's plane MD5s, compared with the reference's."""
-    import concurrent.futures as cf
     from vvc_amd import bitstream as B
     from vvc_amd import parser as P
     s = P.Stream(data)
@@ -244,8 +240,7 @@ def output_yuv_md5(ctx, data, meta):
         exp = meta["poc_plane_md5"].get(str(poc))
         if exp is not None and D.plane_md5s([ctx.read_plane(N.BUF_RECO, slot, c) for c in range(3)]) != exp:
             ok[0] = False
-    with cf.ThreadPoolExecutor(8) as pool:
-        B.SequenceDecode(ctx, data, pool, nslots=min(16, ctx.dpb_slots)).run(on_output)
+    B.SequenceDecode(ctx, data, nslots=min(16, ctx.dpb_slots), threads=8).run(on_output)
     ctx.sync()
     return ok[0] and yuv.hexdigest() == meta["yuv_md5"]
 
@@ -332,15 +327,13 @@ def main():
     resident = None
     kern = {}
     if a.resident_steps > 0:
-        import concurrent.futures as cf
         from vvc_amd import bitstream as B
         copies = []
         t_prep = time.perf_counter()
-        with cf.ThreadPoolExecutor(a.e2e_threads) as pool:
-            for c in range(a.segments):
-                seq = B.SequenceDecode(ctx, data, pool, nslots=per, base=per * c)
-                _, handles = seq.run(keep_handles=True)
-                copies.append((handles, [(inf["poc"], seq.plan.slot[i]) for i, inf in enumerate(seq.plan.info)]))
+        for c in range(a.segments):
+            seq = B.SequenceDecode(ctx, data, nslots=per, base=per * c, threads=8)
+            _, handles = seq.run(keep_handles=True)
+            copies.append((handles, [(inf["poc"], seq.slot[i]) for i, inf in enumerate(seq.info)]))
         ctx.sync()
         t_prep = (time.perf_counter() - t_prep) / a.segments
         res_ok = True

@@ -34,6 +34,10 @@ int vvcp_num_pictures(const vvcp_stream *s);
  * offsets in luma samples, pic_output_flag, non-reference picture flag. Returns the number of fields (16). */
 int vvcp_picture_info(const vvcp_stream *s, int32_t idx, int32_t *info, int32_t n);
 int vvcp_parse_picture(vvcp_stream *s, int32_t idx);
+/* The decoded picture hash SEI that follows picture idx (SEIReader::xParseSEIDecodedPictureHash,
+ * SEIread.cpp:420): returns its hash_type (0 MD5, 1 CRC, 2 checksum) and copies the per-component
+ * hashes (16 / 2 / 4 bytes each, Y Cb Cr) to out[0..n); -1 when the picture has none. */
+int vvcp_picture_hash(const vvcp_stream *s, int32_t idx, uint8_t *out, int32_t n);
 
 /* Motion derivation of a parsed picture (DecCu::xDeriveCUMV, DecCu.cpp:878, with the merge / AMVP /
  * affine / SbTMVP / GEO / MMVD candidate tools of UnitTools.cpp and the history table): fills the MV
@@ -67,6 +71,46 @@ int vvcp_alf_filters(const vvcp_stream *s, int32_t idx, int16_t *luma_coef, int1
  * copied: afterwards vvcp_picture_rows returns them empty and the picture cannot be planned again. */
 int vvcp_plan_picture(vvcp_stream *s, int32_t idx, const vvcr_seq_params *sp, int32_t slot, const int32_t *ref_slot,
                       uint32_t stage_mask, vvcr_picture **out);
+
+/* The whole decode loop in native code (DecApp::decode, App/DecoderApp/DecApp.cpp:76-200, with this
+ * parser and libvvcr in place of DecLib): CABAC of every picture on `threads` parser threads, then per
+ * picture in decoding order the refined motion of its pending references (their DMVR deltas from the
+ * GPU), motion derivation, vvcp_plan_picture, vvcr_prepare_planned and vvcr_launch_picture on ctx.
+ * DPB slots [slot_base, slot_base + num_slots) of ctx (created with ctx_slots slots) hold the pictures;
+ * a picture keeps its slot until its last use as a reference and its output. on_output(user, idx, poc,
+ * slot) is called in output order (POC order within each coded video sequence) as soon as the picture
+ * may be output, its samples still in the slot (vvcr_write_output / vvcr_read_picture wait for them).
+ * handles_out (optional, [number of pictures]): the prepared pictures are kept and their handles
+ * written there in decoding order (the caller may launch them again and must release them).
+ * phase_seconds (optional, [VVCP_DECODE_PHASES]) accumulates the time spent per phase. Several
+ * decodes may run on several threads at once against one context, on disjoint slot ranges.
+ * Returns 0 or a negative VVCR_E_* code (vvcp_last_error() of the calling thread). */
+typedef void (*vvcp_output_fn)(void *user, int32_t idx, int32_t poc, int32_t slot);
+enum {
+  VVCP_PHASE_PARSE = 0,       /* CABAC on the parser threads (summed) */
+  VVCP_PHASE_PARSE_WAIT,      /* decode loop waiting for the parser threads */
+  VVCP_PHASE_DMVR_WAIT,       /* waiting for reference pictures' DMVR deltas, refining their motion */
+  VVCP_PHASE_DERIVE,          /* motion derivation */
+  VVCP_PHASE_PLAN,            /* picture parameters, ALF filters, work lists, intra plan, deblocking edges */
+  VVCP_PHASE_PREPARE,         /* upload (vvcr_prepare_planned) */
+  VVCP_PHASE_LAUNCH,          /* vvcr_launch_picture */
+  VVCP_PHASE_OUTPUT,          /* on_output callbacks */
+  VVCP_DECODE_PHASES
+};
+typedef struct vvcp_decode_params {
+  int32_t slot_base, num_slots, ctx_slots;
+  int32_t threads;
+  uint32_t stage_mask;
+  vvcp_output_fn on_output;
+  void *user;
+  int32_t *handles_out;
+  double *phase_seconds;
+} vvcp_decode_params;
+int vvcp_decode(vvcp_stream *s, vvcr_ctx *ctx, const vvcp_decode_params *p);
+/* The plan vvcp_decode follows: the DPB slot of every picture (slots[number of pictures]) and the
+ * decode indices in output order (out_order[number of pictures]); either may be NULL. Returns the
+ * number of output pictures. */
+int vvcp_decode_plan(const vvcp_stream *s, int32_t slot_base, int32_t num_slots, int32_t *slots, int32_t *out_order);
 
 /* Parsed rows of a picture (after vvcp_parse_picture): copies min(cap, count) entries to dst (dst may be
  * NULL) and returns count. MV fields of vvcr_cu / vvcr_pu hold parsed values until vvcp_derive_motion. */

@@ -67,6 +67,22 @@ def test_decode_plan_order_and_slots():
         B.Plan(s, 2)     # an RA GOP needs more than two pictures in the DPB
 
 
+@pytest.mark.parametrize("name", ["ra1080l_q32", "ra416_q32", "ai416_q37", "ratile416_q32"])
+def test_native_decode_plan_matches(name):
+    """vvcp_decode_plan (the plan the native loop follows) equals the Python restatement above."""
+    s = parser.Stream(_bin(name))
+    L = B._bind(N.lib())
+    n = len(s)
+    for base, nslots in ((0, 16), (5, 9)):
+        slots, order = (C.c_int32 * n)(), (C.c_int32 * n)()
+        m = L.vvcp_decode_plan(s.h, base, nslots, slots, order)
+        plan = B.Plan(s, nslots, base)
+        assert list(slots) == plan.slot
+        assert list(order)[:m] == plan.out_order
+    if name.startswith("ra"):   # a random-access GOP needs more than one picture in the DPB
+        assert L.vvcp_decode_plan(s.h, 0, 1, None, None) < 0
+
+
 STREAMS = ["ai416_q37", "ailm416_q37", "ra416_q32", "ralm416_q32", "rawp416_q32", "ratile416_q32", "ra412c_q32",
            "ra1080_q32", "ratile1080_q32", "rawp1080_q32", "ra1080l_q32", "aibdpcm416_q32", "radq0416_q32", "rageo480_q32",
            "ra2160_q27", "ra2160_q32"]

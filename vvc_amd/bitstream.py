@@ -1,20 +1,18 @@
 """Bitstream-to-pictures driver: the decode loop of DecoderApp (DecApp::decode, DecApp.cpp:118-200 ->
 DecLib::decode / executeLoopFilters, DecLib.cpp) on the MI355X path, from an Annex-B VVC bitstream.
 
-Per picture, in decoding order:
+The loop runs natively (vvcp_decode, vvc_amd/csrc/vvcp_decode.cpp); per picture, in decoding order:
   1. CABAC parse (vvcp_parse_picture) — independent of every other picture, so all pictures are parsed
-     ahead on a thread pool (the library releases the GIL);
+     ahead on parser threads;
   2. motion derivation (vvcp_derive_motion) — needs the refined motion of the collocated picture, i.e.
      that picture's DMVR deltas from the GPU (vvcr_picture_dmvr_deltas waits for its inter stage only);
   3. native planning from the parser's state (vvcp_plan_picture -> vvcr_picture_*), upload
      (vvcr_prepare_planned) and launch on the context's execution lanes.
 The DPB (slots) and output order follow DecLib: a picture keeps its slot until its last use as a
 reference and its output; output is POC order within a coded video sequence (IDR starts a new one).
+Plan below restates that plan in Python for the tests (vvcp_decode_plan is the one decoding uses).
 """
 import ctypes as C
-import concurrent.futures as cf
-import threading
-import time
 
 import numpy as np
 
@@ -29,6 +27,8 @@ def _bind(L):
     if not _bound:
         L.vvcp_plan_picture.argtypes = [C.c_void_p, C.c_int32, C.POINTER(N.SeqParams), C.c_int32, C.c_void_p, C.c_uint32,
                                         C.POINTER(C.c_void_p)]
+        L.vvcp_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.vvcp_decode_plan.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         _bound = True
     return L
 
@@ -99,114 +99,66 @@ class Plan:
         return rs
 
 
+OUTPUT_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int32, C.c_int32, C.c_int32)
+PHASES = ("parse", "parse_wait", "dmvr_wait", "derive", "plan", "prepare", "launch", "output")
+
+
+class DecodeParams(C.Structure):
+    """vvcp_decode_params (include/vvcp.h)"""
+    _fields_ = [("slot_base", C.c_int32), ("num_slots", C.c_int32), ("ctx_slots", C.c_int32), ("threads", C.c_int32),
+                ("stage_mask", C.c_uint32), ("on_output", OUTPUT_FN), ("user", C.c_void_p),
+                ("handles_out", C.POINTER(C.c_int32)), ("phase_seconds", C.POINTER(C.c_double))]
+
+
 class SequenceDecode:
-    """One decode of a bitstream through a Context, on DPB slots [base, base + nslots).
+    """One decode of a bitstream through a Context, on DPB slots [base, base + nslots): the native
+    decode loop vvcp_decode (vvc_amd/csrc/vvcp_decode.cpp) — parser threads, motion derivation with
+    the GPU's DMVR feedback, planning, upload and launch all in C++, the GIL released for the whole
+    decode. on_output(poc, slot) is called in output order while the slot still holds the picture.
+    Several SequenceDecodes on disjoint slot ranges may run on several threads against one Context."""
 
-    run() parses ahead on `pool`, derives / plans / launches in decoding order on the calling thread and
-    calls on_output(poc, slot) in output order while the slot still holds the picture (e.g. to write the
-    YUV file). Launches go through `launch_lock`, so several SequenceDecodes (on disjoint slot ranges) may
-    run on several threads against one Context."""
-
-    def __init__(self, ctx, data, pool, nslots=16, base=0, stages=N.STAGE_ALL, launch_lock=None, keep=24):
-        self.ctx, self.pool = ctx, pool
+    def __init__(self, ctx, data, pool=None, nslots=16, base=0, stages=N.STAGE_ALL, launch_lock=None, keep=24, threads=4):
+        self.ctx = ctx
         self.L = _bind(N.lib())
         self.s = P.Stream(data, lib=self.L)
-        self.plan = Plan(self.s, nslots, base)
-        inf = self.plan.info[0]
-        self.W, self.H = inf["width"], inf["height"]
-        self.sp = N.SeqParams(self.W, self.H, 1, inf["bit_depth"], inf["ctu_log2"], ctx.dpb_slots, 0)
-        self.stages = stages
-        self.lock = launch_lock or threading.Lock()
-        self.keep = keep
-        # seconds this decode's thread spent per phase (waiting on the parse pool, on the GPU's DMVR
-        # deltas, deriving motion, planning, uploading, launching)
-        self.times = dict.fromkeys(("parse", "parse_wait", "dmvr_wait", "derive", "plan", "prepare", "launch"), 0.0)
-        self._tlock = threading.Lock()
-
-    def _parse(self, i):
-        t0 = time.perf_counter()
-        self.s.parse(i)
-        dt = time.perf_counter() - t0
-        with self._tlock:
-            self.times["parse"] += dt   # on the pool's threads
-
-    def _plan_picture(self, i):
-        rs = self.plan.ref_slots(i)
-        h = C.c_void_p()
-        rc = self.L.vvcp_plan_picture(self.s.h, i, C.byref(self.sp), self.plan.slot[i], rs.ctypes.data, self.stages,
-                                      C.byref(h))
-        if rc != 0:
-            raise P.ParseError("picture %d plan: %s" % (i, self.L.vvcp_last_error().decode()))
-        return N.Picture.wrap(h)
+        self.nslots, self.base, self.stages, self.threads = nslots, base, stages, threads
+        n = len(self.s)
+        slots, order = (C.c_int32 * max(n, 1))(), (C.c_int32 * max(n, 1))()
+        m = self.L.vvcp_decode_plan(self.s.h, base, nslots, slots, order)
+        if m < 0:
+            raise P.ParseError("decode plan: %s" % self.L.vvcp_last_error().decode())
+        self.slot = list(slots)[:n]
+        self.out_order = list(order)[:m]
+        self.info = [self.s.info(i) for i in range(n)]
+        # seconds per phase (include/vvcp.h VVCP_PHASE_*): parse summed over the parser threads
+        self.times = dict.fromkeys(PHASES, 0.0)
 
     def run(self, on_output=None, keep_handles=False):
         """Decodes the stream; returns [(poc, slot)] in output order, and with keep_handles also the
         prepared-picture handles in decoding order (not released: the caller may launch them again)."""
         n = len(self.s)
-        parsed = [self.pool.submit(self._parse, i) for i in range(n)]
-        handles = {}          # decode index -> prepared-picture handle
-        n_dmvr = {}
-        refined = set()
-        live = []
-        out_pos = 0
-        out = self.plan.out_order
-        try:
-            T = self.times
-            clk = time.perf_counter
-            for i in range(n):
-                t0 = clk()
-                parsed[i].result()
-                t1 = clk()
-                # the collocated picture is one of the references: refine those still pending
-                for l in range(2):
-                    for poc in self.plan.refs[i][l]:
-                        j = self.plan._find(i, poc)
-                        if j not in refined:
-                            d = self.ctx.picture_dmvr_deltas(handles[j], n_dmvr[j])
-                            self.s.refine(j, d)
-                            refined.add(j)
-                t2 = clk()
-                self.s.derive(i)
-                t3 = clk()
-                pic = self._plan_picture(i)
-                t4 = clk()
-                try:
-                    n_dmvr[i] = pic.work_counts()["dmvr"]
-                    h = self.ctx.prepare_planned(pic)
-                finally:
-                    pic.close()
-                t5 = clk()
-                with self.lock:
-                    self.ctx.launch(h)
-                t6 = clk()
-                with self._tlock:
-                    T["parse_wait"] += t1 - t0
-                T["dmvr_wait"] += t2 - t1
-                T["derive"] += t3 - t2
-                T["plan"] += t4 - t3
-                T["prepare"] += t5 - t4
-                T["launch"] += t6 - t5
-                handles[i] = h
-                live.append(i)
-                if not self.plan.referenced[i]:
-                    refined.add(i)
-                while out_pos < len(out) and self.plan.out_ready[out[out_pos]] <= i:
-                    k = out[out_pos]
-                    if on_output:
-                        on_output(self.plan.info[k]["poc"], self.plan.slot[k])
-                    out_pos += 1
-                # release handles of pictures far behind whose deltas are no longer needed
-                while not keep_handles and len(live) > self.keep and live[0] in refined:
-                    self.ctx.release(handles.pop(live.pop(0)))
-            kept = [handles.pop(i) for i in range(n)] if keep_handles else None
-        finally:
-            for f in parsed:
-                f.cancel()
-            for i in live:
-                if i in handles:
-                    self.ctx.release(handles.pop(i))
-        order = [(self.plan.info[k]["poc"], self.plan.slot[k]) for k in out]
-        return (order, kept) if keep_handles else order
+        err = []
+
+        def cb(user, idx, poc, slot):
+            try:
+                on_output(poc, slot)
+            except Exception as e:   # never unwind through the C frames: reported after the decode
+                err.append(e)
+        fn = OUTPUT_FN(cb) if on_output else OUTPUT_FN()
+        handles = (C.c_int32 * max(n, 1))() if keep_handles else None
+        phases = (C.c_double * len(PHASES))()
+        prm = DecodeParams(self.base, self.nslots, self.ctx.dpb_slots, self.threads, self.stages, fn, None,
+                           C.cast(handles, C.POINTER(C.c_int32)) if handles is not None else None,
+                           C.cast(phases, C.POINTER(C.c_double)))
+        rc = self.L.vvcp_decode(self.s.h, self.ctx.h, C.byref(prm))
+        for k, name in enumerate(PHASES):
+            self.times[name] += phases[k]
+        if rc != 0:
+            raise P.ParseError("vvcp_decode: %s" % self.L.vvcp_last_error().decode())
+        if err:
+            raise err[0]
+        order = [(self.info[k]["poc"], self.slot[k]) for k in self.out_order]
+        return (order, list(handles)[:n]) if keep_handles else order
 
 
 def decode_bitstream(data, ctx=None, threads=8, dpb_slots=16, device=0, on_output=None):
@@ -219,8 +171,7 @@ def decode_bitstream(data, ctx=None, threads=8, dpb_slots=16, device=0, on_outpu
     if own:
         ctx = N.Context(inf["width"], inf["height"], bit_depth=inf["bit_depth"], ctu_log2=inf["ctu_log2"],
                         dpb_slots=dpb_slots, device=device)
-    with cf.ThreadPoolExecutor(threads) as pool:
-        seq = SequenceDecode(ctx, data, pool, nslots=dpb_slots)
-        order = seq.run(on_output)
+    seq = SequenceDecode(ctx, data, nslots=dpb_slots, threads=threads)
+    order = seq.run(on_output)
     ctx.sync()
     return order, ctx

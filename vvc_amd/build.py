@@ -18,7 +18,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=" + ARCH, "-I" + os.path.
 def _compile(src, extra=(), obj_dir=OBJ):
     obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     deps = [src] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + \
-        [os.path.join(ROOT, "include", "vvcr.h")]
+        [os.path.join(ROOT, "include", h) for h in ("vvcr.h", "vvcp.h")]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
     cmd = [HIPCC] + FLAGS + list(extra) + ["-c", src, "-o", obj]
@@ -42,6 +42,24 @@ def build_lib(jobs=8, extra=(), obj_dir=OBJ, lib=LIB):
         if r.returncode != 0:
             raise RuntimeError("link failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
     return lib
+
+
+APP = os.path.join(ROOT, "vvc_amd", "vvcdec")
+
+
+def build_app(lib=LIB):
+    """vvc_amd/vvcdec: the DecoderApp-compatible command-line decoder (vvc_amd/app/vvcdec.cpp) over the
+    C-ABI of libvvcr.so (found next to it at run time)."""
+    src = os.path.join(ROOT, "vvc_amd", "app", "vvcdec.cpp")
+    deps = [src, lib] + [os.path.join(ROOT, "include", h) for h in ("vvcr.h", "vvcp.h")]
+    if os.path.exists(APP) and os.path.getmtime(APP) >= max(os.path.getmtime(d) for d in deps):
+        return APP
+    cmd = ["g++", "-O2", "-std=c++17", "-Wall", "-pthread", "-I" + os.path.join(ROOT, "include"), "-o", APP, src,
+           lib, "-Wl,-rpath,$ORIGIN"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("vvcdec build failed: %s\n%s%s" % (" ".join(cmd), r.stdout, r.stderr))
+    return APP
 
 
 def build_oracle():
@@ -76,4 +94,5 @@ def build_reference(jobs=8):
 
 if __name__ == "__main__":
     print(build_lib())
+    print(build_app())
     print(build_oracle())

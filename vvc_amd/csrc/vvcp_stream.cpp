@@ -62,6 +62,30 @@ void derive_smvd(SliceHeader &s, const SPS &sps, const PicHeader &ph) {
 }
 }  // namespace
 
+// sei_rbsp (SEIReader::parseSEImessage, SEIread.cpp:117): the decoded picture hash message (type 132)
+static void parse_sei_hash(const std::vector<uint8_t> &r, PictureUnit &p) {
+  size_t pos = 0;
+  while (pos < r.size() && !(pos + 1 == r.size() && r[pos] == 0x80)) {
+    uint32_t type = 0, size = 0;
+    while (pos < r.size() && r[pos] == 0xff) { type += 255; pos++; }
+    if (pos >= r.size()) return;
+    type += r[pos++];
+    while (pos < r.size() && r[pos] == 0xff) { size += 255; pos++; }
+    if (pos >= r.size()) return;
+    size += r[pos++];
+    if (pos + size > r.size()) return;
+    if (type == 132 && size >= 1) {
+      const int t = r[pos];
+      const int per = t == 0 ? 16 : (t == 1 ? 2 : (t == 2 ? 4 : 0));
+      if (per && size >= 1 + 3 * (uint32_t)per) {
+        p.hashType = t;
+        for (int c = 0; c < 3; c++) std::memcpy(p.hash[c], &r[pos + 1 + c * per], per);
+      }
+    }
+    pos += size;
+  }
+}
+
 void Stream::open(const uint8_t *d, size_t n) {
   data.assign(d, d + n);
   nals = split_annexb(data.data(), data.size());
@@ -98,6 +122,9 @@ void Stream::open(const uint8_t *d, size_t n) {
       case NAL_PH:
         parse_ph(b, ph, ps);
         cur = nullptr;   // next slice starts a new picture
+        break;
+      case NAL_SUFFIX_SEI:
+        if (cur) parse_sei_hash(nal.rbsp, *cur);   // the hash of the picture whose slices it follows
         break;
       default:
         if (nal.type <= NAL_GDR && is_vcl(nal.type)) {
@@ -229,6 +256,16 @@ int vvcp_picture_info(const vvcp_stream *h, int32_t idx, int32_t *info, int32_t 
   const int m = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < m; i++) info[i] = v[i];
   return m;
+}
+
+int vvcp_picture_hash(const vvcp_stream *h, int32_t idx, uint8_t *out, int32_t n) {
+  if (!h || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
+  const vvcp::PictureUnit &p = *h->s.pics[idx];
+  if (p.hashType < 0) return -1;
+  const int per = p.hashType == 0 ? 16 : (p.hashType == 1 ? 2 : 4);
+  for (int c = 0; c < 3; c++)
+    for (int k = 0; k < per && c * per + k < n; k++) out[c * per + k] = p.hash[c][k];
+  return p.hashType;
 }
 
 int vvcp_parse_picture(vvcp_stream *h, int32_t idx) {

@@ -22,6 +22,10 @@ struct PictureUnit {
   bool alfValid[8] = {false}, lmcsValid[4] = {false};
   PictureSyntax syn;
   bool parsed = false, failed = false;
+  // decoded picture hash SEI (SEIDecodedPictureHash, SEIread.cpp:420) of the picture: -1 none,
+  // 0 MD5 (16 bytes per component), 1 CRC (2), 2 checksum (4)
+  int hashType = -1;
+  uint8_t hash[3][16] = {{0}};
   // motion (derive_motion): the 4x4 field before DMVR, its row form and the GEO candidate rows
   MotionField field;
   MotionRows motion;

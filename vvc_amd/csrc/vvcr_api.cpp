@@ -235,6 +235,8 @@ struct vvcr_ctx {
   // itself is only touched by the thread that prepares it, then by launch / release).
   std::vector<std::unique_ptr<Prepared>> prepared;
   std::mutex prepared_mu;
+  std::mutex launch_mu;              // launches, releases and host reads / writes of the DPB may come from
+                                     // several host threads (vvcp_decode of several streams at once)
   Prepared *last = nullptr;          // last launched (stage times, DMVR deltas)
   int n_cu = 256;                    // compute units (persistent intra launch width)
   std::vector<std::unique_ptr<struct RdoPlan>> rdo;   // encoder RDO plans (vvcr_rd_plan / vvcr_fwd_plan)
@@ -941,6 +943,7 @@ int vvcr_prepare_planned(vvcr_ctx *ctx, const vvcr_picture *pic, int32_t *handle
 int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
+  std::lock_guard<std::mutex> g(ctx->launch_mu);
   launch(ctx, get_prepared(ctx, handle));
   return VVCR_OK;
   API_END
@@ -951,6 +954,7 @@ int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle) {
   API_BEGIN
   Prepared &r = get_prepared(ctx, handle);
   r.wait();
+  std::lock_guard<std::mutex> lg(ctx->launch_mu);
   if (ctx->last == &r) ctx->last = nullptr;
   std::lock_guard<std::mutex> g(ctx->prepared_mu);
   ctx->prepared[handle].reset();
@@ -1058,6 +1062,7 @@ int vvcr_set_timing(vvcr_ctx *ctx, int32_t on) {
 int vvcr_sync(vvcr_ctx *ctx) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
+  std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
   sync_lanes(ctx);
   int32_t e = 0;
   VVCR_CHECK_HIP(hipMemcpy(&e, ctx->d_err, sizeof e, hipMemcpyDeviceToHost));
@@ -1108,6 +1113,7 @@ static DPlane *select_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t co
 int vvcr_read_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, int16_t *dst, int32_t dst_stride) {
   if (!ctx || !dst) return VVCR_E_ARG;
   API_BEGIN
+  std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
   DPlane *p = select_plane(ctx, buf, slot, comp);
   sync_lanes(ctx);
   VVCR_CHECK_HIP(hipMemcpy2DAsync(dst, dst_stride * 2, p->p, p->stride * 2, p->w * 2, p->h, hipMemcpyDeviceToHost, ctx->stream));
@@ -1125,6 +1131,7 @@ int vvcr_read_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, int1
 int vvcr_write_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, const int16_t *src, int32_t src_stride) {
   if (!ctx || !src) return VVCR_E_ARG;
   API_BEGIN
+  std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
   DPlane *p = select_plane(ctx, buf, slot, comp);
   sync_lanes(ctx);
   VVCR_CHECK_HIP(hipMemcpy2DAsync(p->p, p->stride * 2, src, src_stride * 2, p->w * 2, p->h, hipMemcpyHostToDevice, ctx->stream));
@@ -1233,6 +1240,7 @@ int64_t vvcr_output_bytes(const vvcr_ctx *ctx, const vvcr_output_params *op) {
 int vvcr_write_output(vvcr_ctx *ctx, int32_t slot, const vvcr_output_params *op, void *dst, int32_t dst_on_device) {
   if (!ctx || !dst) return VVCR_E_ARG;
   API_BEGIN
+  std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
   if (slot < 0 || slot >= (int)ctx->dpb.size()) throw VvcrError(VVCR_E_ARG, "bad slot");
   check_output(ctx, op);
   const int64_t nb = vvcr_output_bytes(ctx, op);
@@ -1254,6 +1262,7 @@ int vvcr_write_output(vvcr_ctx *ctx, int32_t slot, const vvcr_output_params *op,
 int vvcr_export_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, void *dev_dst) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
+  std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
   rows_copy(ctx, slot, y0, n, (char *)dev_dst, false);
   return VVCR_OK;
   API_END
@@ -1262,6 +1271,7 @@ int vvcr_export_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, void *d
 int vvcr_import_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, const void *dev_src) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
+  std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
   rows_copy(ctx, slot, y0, n, (char *)dev_src, true);
   return VVCR_OK;
   API_END
