@@ -122,6 +122,17 @@ struct Prepared {
     if (h_dmvr) (void)hipHostFree(h_dmvr);
   }
   void wait() { if (launched) VVCR_CHECK_HIP(hipEventSynchronize(done)); }
+  // back to the state of a new record, keeping its device buffers, events and pinned memory for reuse
+  void recycle() {
+    mask = 0;
+    n_ijobs = n_ictu = 0;
+    for (int &c : dbk_counts) c = 0;
+    have_sao = have_alf = false;
+    n_tb = n_tb_small = n_mctile = n_basic = n_bidir = n_aff = n_tiles = n_dmvr = 0;
+    for (int k = 0; k < NK; k++) { ran[k] = timed[k] = false; alg_bytes[k] = 0; launches[k] = 0; }
+    launched = false;
+    lane = 0;
+  }
 };
 
 // Per-kernel-group HIP events (vvcr_kernel_stats). Every event record is a marker packet in the lane's
@@ -235,6 +246,9 @@ struct vvcr_ctx {
   // itself is only touched by the thread that prepares it, then by launch / release).
   std::vector<std::unique_ptr<Prepared>> prepared;
   std::mutex prepared_mu;
+  // released records, kept with their device buffers: allocating and freeing device memory per picture
+  // would cost a hipMalloc per buffer and a device-wide synchronisation per hipFree
+  std::vector<std::unique_ptr<Prepared>> spare;
   std::mutex launch_mu;              // launches, releases and host reads / writes of the DPB may come from
                                      // several host threads (vvcp_decode of several streams at once)
   Prepared *last = nullptr;          // last launched (stage times, DMVR deltas)
@@ -375,7 +389,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   const WorkLists &wl = bp.wl;
   const double pix = (double)sp.width * sp.height * 1.5;   // samples of the three planes
   if (mask & VVCR_STAGE_RESID) {
-    r.coef.upload(bp.desc.coef);
+    r.coef.upload(bp.wl.coef);   // the packed levels of the transform blocks
     r.tb.upload(wl.tb);
     r.n_tb = (int)wl.tb.size();
     r.n_tb_small = wl.tb_small;
@@ -845,7 +859,13 @@ static int32_t new_prepared(vvcr_ctx *ctx) {
   for (size_t i = 1; i < ctx->prepared.size(); i++)
     if (!ctx->prepared[i]) { h = (int)i; break; }
   if (h < 0) { h = (int)ctx->prepared.size(); ctx->prepared.emplace_back(); }
-  ctx->prepared[h].reset(new Prepared());
+  if (!ctx->spare.empty()) {
+    ctx->prepared[h] = std::move(ctx->spare.back());
+    ctx->spare.pop_back();
+    ctx->prepared[h]->recycle();
+  } else {
+    ctx->prepared[h].reset(new Prepared());
+  }
   return h;
 }
 
@@ -957,7 +977,8 @@ int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle) {
   std::lock_guard<std::mutex> lg(ctx->launch_mu);
   if (ctx->last == &r) ctx->last = nullptr;
   std::lock_guard<std::mutex> g(ctx->prepared_mu);
-  ctx->prepared[handle].reset();
+  if (ctx->spare.size() < 96) ctx->spare.push_back(std::move(ctx->prepared[handle]));
+  else ctx->prepared[handle].reset();
   return VVCR_OK;
   API_END
 }

@@ -3,6 +3,7 @@
 // (InterPrediction.cpp:1517-1660) so that every PU reaches the kernel that reproduces its prediction.
 #include "vvcr_host.h"
 #include <string>
+#include <cstring>
 #include <algorithm>
 #include <cstdlib>
 
@@ -164,7 +165,8 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
   }
 }
 
-void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out);
+void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out,
+                   bigbuf::vec<int32_t> &packed);
 
 namespace {
 
@@ -240,7 +242,7 @@ AffList affine_list(const vvcr_pic_params &pp, const vvcr_cu &c, const vvcr_pu &
 
 void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl) {
   wl.clear();
-  build_tb_jobs(sp, pp, d, wl.tb);
+  build_tb_jobs(sp, pp, d, wl.tb, wl.coef);
   // small blocks first (64-lane workgroups), then the large ones (256 lanes)
   wl.tb_small = (int)(std::stable_partition(wl.tb.begin(), wl.tb.end(), [](const TbJob &j) { return j.w * j.h <= 256; }) - wl.tb.begin());
   const int W4 = sp.width / 4;
@@ -483,8 +485,10 @@ void tr_types(const vvcr_pic_params &pp, const vvcr_cu &cu, int comp, int w, int
 }
 }  // namespace
 
-void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out) {
+void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out,
+                   bigbuf::vec<int32_t> &packed) {
   out.clear();
+  packed.clear();
   const int W4 = sp.width / 4, H4 = sp.height / 4;
   bigbuf::vec<int> lmap;   // luma PU per 4x4, for co-located luma modes (PU::getCoLocatedIntraLumaMode)
   bool haveMap = false;
@@ -557,11 +561,11 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
       // (dequantisation maps 0 to 0; LFNST widens it to its output area; TS / BDPCM use the whole block)
       {
         int R = 0, C = 0;
+        if ((size_t)j.coef + (size_t)w * h > d.coef.size()) throw VvcrError(VVCR_E_ARG, "coefficient offset out of range");
+        const int32_t *lv = d.coef.data() + j.coef;
         if (ts) {
           R = h; C = w;
         } else {
-          if ((size_t)j.coef + (size_t)w * h > d.coef.size()) throw VvcrError(VVCR_E_ARG, "coefficient offset out of range");
-          const int32_t *lv = d.coef.data() + j.coef;
           for (int yy = 0; yy < h; yy++) {
             const int32_t *row = lv + yy * w;
             int32_t any = 0;
@@ -577,6 +581,12 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
           }
         }
         j.nz_rows = (uint8_t)R; j.nz_cols = (uint8_t)C;
+        // only the box travels to the device (most of a large inter TB is zero)
+        const size_t off = packed.size();
+        packed.resize(off + (size_t)R * C);
+        for (int yy = 0; yy < R; yy++) std::memcpy(packed.data() + off + (size_t)yy * C, lv + (size_t)yy * w, (size_t)C * sizeof(int32_t));
+        j.coef = (int32_t)off;
+        j.flags |= TB_PACKED;
       }
       out.push_back(j);
     }

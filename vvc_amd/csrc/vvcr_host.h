@@ -25,6 +25,7 @@ struct WorkLists {
   bigbuf::vec<AffPu> aff_pu;       // affine PUs
   bigbuf::vec<AffJob> aff_jobs;    // affine tiles
   bigbuf::vec<TbJob> tb;           // coded transform blocks (the tb_small blocks of <= 256 samples first)
+  bigbuf::vec<int32_t> coef;       // their levels, packed: each block's non-zero box (TB_PACKED), uploaded
   int tb_small = 0;
   int n_dmvr = 0;                  // DMVR sub-blocks (delta outputs), in PU order
   int n_unsupported_inter = 0;     // PUs needing kernels not built yet (reported, never silently skipped)
@@ -32,7 +33,7 @@ struct WorkLists {
   double mc_alg = 0;               // algorithmic bytes of the plain MC (per PU / sub-block)
   void clear() {
     mc_alg = 0; mc_tile.clear();
-    mc_basic.clear(); mc_bidir.clear(); aff_pu.clear(); aff_jobs.clear(); tb.clear();
+    mc_basic.clear(); mc_bidir.clear(); aff_pu.clear(); aff_jobs.clear(); tb.clear(); coef.clear();
     n_dmvr = 0; n_unsupported_inter = 0; tb_small = 0; ref_y0 = ref_y1 = 0;
   }
 };
