@@ -42,8 +42,8 @@ extern "C" int vvcp_plan_picture(vvcp_stream *h, int32_t idx, const vvcr_seq_par
   if (rc) return fail(nullptr, rc, "vvcr_picture_create");
   vvcp::PictureSyntax &S = p.syn;
   try {
-    // the transform rows, coefficient pool and motion rows move to the picture (nothing on the host reads
-    // them again); CU / PU rows are copied: refine_motion still reads them
+    // the transform rows, coefficient pool, motion rows and CU maps move to the picture (nothing on the
+    // host reads them again); CU / PU rows are copied: refine_motion still reads them
     PictureDescriptors D;
     D.cu.assign(S.cu.begin(), S.cu.end());
     D.pu.assign(S.pu.begin(), S.pu.end());
@@ -51,6 +51,8 @@ extern "C" int vvcp_plan_picture(vvcp_stream *h, int32_t idx, const vvcr_seq_par
     D.coef = std::move(S.coef);
     D.motion = std::move(p.motion);
     D.geo.assign(p.geo.begin(), p.geo.end());
+    D.cu_map[0] = std::move(S.map[0]);
+    D.cu_map[1] = std::move(S.map[1]);
     vvcr_picture_adopt(pic, std::move(D));
   } catch (const std::exception &e) {
     vvcp::set_api_error(std::string("vvcr_picture_submit: ") + e.what());

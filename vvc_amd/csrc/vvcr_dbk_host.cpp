@@ -26,7 +26,8 @@ struct Planner {
   const PictureDescriptors &d;
   DbkLists &out;
   int W4, H4, ctu, parts;
-  bigbuf::vec<int> cu_map[2], tu_map[2];
+  bigbuf::vec<int> own_cu_map[2], tu_map[2];
+  const int32_t *cu_map[2] = {nullptr, nullptr};   // the producer's CU maps when handed over, else own_cu_map
   // per-CU scratch in CTU-relative coordinates (the reference's per-CTU arrays, LoopFilter.h:66-79)
   int ctu_x = 0, ctu_y = 0;
   uint8_t bs[2][32 * 32];
@@ -77,11 +78,16 @@ struct Planner {
 
   void build_maps() {
     const size_t n = (size_t)W4 * H4;
-    for (int k = 0; k < 2; k++) { cu_map[k].assign(n, -1); tu_map[k].assign(n, -1); }
-    for (size_t i = 0; i < d.cu.size(); i++) {
-      const vvcr_cu &c = d.cu[i];
-      if (c.yvalid) fill(cu_map[0], c.x, c.y, c.w, c.h, 2, (int)i);
-      if (c.cvalid) fill(cu_map[1], c.cx, c.cy, c.cw, c.ch, 1, (int)i);
+    for (int k = 0; k < 2; k++) {
+      tu_map[k].assign(n, -1);
+      if (d.cu_map[k].size() == n) { cu_map[k] = d.cu_map[k].data(); continue; }
+      own_cu_map[k].assign(n, -1);
+      for (size_t i = 0; i < d.cu.size(); i++) {
+        const vvcr_cu &c = d.cu[i];
+        if (k == 0 && c.yvalid) fill(own_cu_map[0], c.x, c.y, c.w, c.h, 2, (int)i);
+        if (k == 1 && c.cvalid) fill(own_cu_map[1], c.cx, c.cy, c.cw, c.ch, 1, (int)i);
+      }
+      cu_map[k] = own_cu_map[k].data();
     }
     for (size_t t = 0; t < d.tu.size(); t++) {
       const vvcr_cu &c = d.cu[d.tu[t].cu];
@@ -356,14 +362,25 @@ struct Planner {
     // An edge inside an inter, non-CIIP luma CU that is not a transform edge (sub-block edges of affine /
     // SbTMVP CUs: most of the edges of a B picture) has only the motion part of the boundary strength.
     const bool fast = cu.yvalid && cu.predmode != MODE_INTRA && !d.pu[cu.firstpu].ciip;
-    for (int y = 0; y < a[3]; y += 4)
-      for (int x = 0; x < a[2]; x += 4) {
-        const int r = raster(a[0] + x, a[1] + y);
-        if (!edge[dir][r]) continue;
-        if (fast && bs[dir][r] == 0 && (dir == VER ? x : y) > 0) bs[dir][r] = (uint8_t)motion_bs(dir, a[0] + x, a[1] + y, 0);
-        else bs[dir][r] = (uint8_t)boundary_strength(cui, dir, a[0] + x, a[1] + y);
-      }
     std::sort(edges, edges + ne);
+    auto bs_at = [&](int x, int y) {
+      const int r = raster(a[0] + x, a[1] + y);
+      if (!edge[dir][r]) return;
+      if (fast && bs[dir][r] == 0 && (dir == VER ? x : y) > 0) bs[dir][r] = (uint8_t)motion_bs(dir, a[0] + x, a[1] + y, 0);
+      else bs[dir][r] = (uint8_t)boundary_strength(cui, dir, a[0] + x, a[1] + y);
+    };
+    if (cu.yvalid) {   // edge flags are only ever set on the edge lines listed: visit those, not the whole CU
+      for (int k = 0; k < ne; k++) {
+        if (k && edges[k] == edges[k - 1]) continue;
+        const int o = edges[k] * 4;
+        if (o < 0 || o >= (dir == VER ? a[2] : a[3])) continue;
+        if (dir == VER) for (int y = 0; y < a[3]; y += 4) bs_at(o, y);
+        else for (int x = 0; x < a[2]; x += 4) bs_at(x, o);
+      }
+    } else {
+      for (int y = 0; y < a[3]; y += 4)
+        for (int x = 0; x < a[2]; x += 4) bs_at(x, y);
+    }
     int prev = -1;
     for (int k = 0; k < ne; k++) {
       if (edges[k] == prev) continue;

@@ -11,7 +11,10 @@ struct PictureDescriptors {
   bigbuf::vec<int32_t> coef;
   bigbuf::raw<vvcr_motion> motion;
   bigbuf::vec<vvcr_geo> geo;
-  void clear() { cu.clear(); pu.clear(); tu.clear(); coef.clear(); motion.clear(); geo.clear(); }
+  // optional: CU index per 4x4 luma unit of each channel (chroma: 2x2 chroma units), -1 where none;
+  // the host parser hands its maps over, other producers leave them empty and the planners build them
+  bigbuf::vec<int32_t> cu_map[2];
+  void clear() { cu.clear(); pu.clear(); tu.clear(); coef.clear(); motion.clear(); geo.clear(); cu_map[0].clear(); cu_map[1].clear(); }
 };
 
 // Hands a producer's descriptor arrays to a picture (vvcr_picture_submit without the copies; validates

@@ -92,9 +92,39 @@ struct Planner {
   const PictureDescriptors &d;
   IntraPlan &out;
   int W4, H4, ctu;
+  // Per 4x4 luma unit / 2x2 chroma unit: the CU covering it per channel (umap: the producer's maps when
+  // it hands them over, else own_map). Only the units of CUs whose reconstruction is a step ("written":
+  // intra, CIIP, chroma steps) carry their own order / level / producers in out.order / level / prod,
+  // initialised when the CU is planned; the units of a plain inter CU share its cu_seq, level 0 and no
+  // producer, so a B picture's inter CUs cost no per-unit work.
   bigbuf::vec<int32_t> level[2];
-  bigbuf::vec<int32_t> prod[3];     // per unit of each component: the step (index into jobs) that reconstructs it, -1 = inter
-  bigbuf::vec<int32_t> cu_map;      // luma 4x4 unit -> CU index (for CIIP neighbour tests)
+  bigbuf::vec<int32_t> prod[3];     // per unit of each component: the step (index into jobs) that reconstructs it
+  const int32_t *umap[2] = {nullptr, nullptr};
+  bigbuf::vec<int32_t> own_map[2];
+  bigbuf::vec<int32_t> cu_seq;      // per CU: the seq of a plain inter CU, kInf until planned
+  bigbuf::vec<uint8_t> written[2];  // per CU and channel: its units carry their own order / level / producers
+  static constexpr int32_t kInf = 1 << 30;
+  int32_t order_of(int ch, size_t i) const {
+    const int32_t m = umap[ch][i];
+    if (m < 0) return kInf;
+    return written[ch][m] ? out.order[ch][i] : cu_seq[m];
+  }
+  // first write of CU ci's units of channel ch: their own order / level / producers from here on
+  void touch(int ch, int ci) {
+    if (written[ch][ci]) return;
+    written[ch][ci] = 1;
+    const vvcr_cu &c = d.cu[ci];
+    const int s = ch ? 1 : 2;
+    const int x = ch ? c.cx : c.x, y = ch ? c.cy : c.y, w = ch ? c.cw : c.w, h = ch ? c.ch : c.h;
+    for (int uy = y >> s; uy < (y + h + (1 << s) - 1) >> s; uy++)
+      for (int ux = x >> s; ux < (x + w + (1 << s) - 1) >> s; ux++) {
+        const size_t i = (size_t)uy * W4 + ux;
+        out.order[ch][i] = kInf;
+        level[ch][i] = 0;
+        if (ch) prod[1][i] = prod[2][i] = -1;
+        else prod[0][i] = -1;
+      }
+  }
   bigbuf::vec<std::pair<int32_t, IntraJob>> jobs;   // (level, job)
   bigbuf::vec<int32_t> dep_off{0}, dep_flat;        // per job (CSR): the steps it reads from (indices into jobs)
   bigbuf::vec<int32_t> cur;                         // dependencies of the step being planned
@@ -135,7 +165,10 @@ struct Planner {
     for (int uy = y0 >> s; uy <= (y1 >> s); uy++)
       for (int ux = x0 >> s; ux <= (x1 >> s); ux++) {
         const size_t i = (size_t)uy * W4 + ux;
-        if (out.order[ch][i] < seq && region_at((ux << s) << cs, (uy << s) << cs) == cur_reg) {
+        const int32_t cu = umap[ch][i];
+        if (cu < 0) continue;
+        const bool own = written[ch][cu];
+        if ((own ? out.order[ch][i] : cu_seq[cu]) < seq && region_at((ux << s) << cs, (uy << s) << cs) == cur_reg && own) {
           m = std::max(m, level[ch][i]);
           const int32_t pr = prod[comp][i];
           if (pr >= 0) add_dep(pr);
@@ -143,7 +176,8 @@ struct Planner {
       }
     return m;
   }
-  void mark(int ch, int x, int y, int w, int h, int lev, bool set_order, int comp = -1, int job = -1) {
+  void mark(int ci, int ch, int x, int y, int w, int h, int lev, bool set_order, int comp = -1, int job = -1) {
+    touch(ch, ci);
     const int s = ch ? 1 : 2;
     for (int uy = y >> s; uy < (y + h + (1 << s) - 1) >> s; uy++)
       for (int ux = x >> s; ux < (x + w + (1 << s) - 1) >> s; ux++) {
@@ -186,7 +220,7 @@ struct Planner {
   int set_cscale(IntraJob &j, int lx, int ly) {
     const int n64 = std::min(64, ctu);
     const int vx0 = (lx / n64) * n64, vy0 = (ly / n64) * n64;
-    const int ci = cu_map[(size_t)(vy0 >> 2) * W4 + (vx0 >> 2)];
+    const int ci = umap[0][(size_t)(vy0 >> 2) * W4 + (vx0 >> 2)];
     if (ci < 0) throw VvcrError(VVCR_E_STATE, "LMCS: no luma CU at a VPDU corner");
     const vvcr_cu &t = d.cu[ci];
     j.vx = (int16_t)t.x; j.vy = (int16_t)t.y;
@@ -206,7 +240,7 @@ struct Planner {
       // CIIP: planar from the neighbours, blended with the inter prediction (geneWeightedPred :681)
       auto intraAt = [&](int x, int y) {
         if (x < 0 || y < 0 || x >= sp.width || y >= sp.height || region_at(x, y) != cur_reg) return false;
-        const int n = cu_map[(size_t)(y >> 2) * W4 + (x >> 2)];
+        const int n = umap[0][(size_t)(y >> 2) * W4 + (x >> 2)];
         return n >= 0 && n <= ci && d.cu[n].predmode == MODE_INTRA;
       };
       const bool n0 = intraAt(c.x - 1, c.y + c.h - 1), n1 = intraAt(c.x + c.w - 1, c.y - 1);
@@ -227,12 +261,12 @@ struct Planner {
       }
       int lev = 0;
       for (auto it = jobs.end() - ncomp; it != jobs.end(); ++it) lev = std::max(lev, it->first);
-      mark(0, c.x, c.y, c.w, c.h, lev, true, 0, id[0]);
+      mark(ci, 0, c.x, c.y, c.w, c.h, lev, true, 0, id[0]);
       if (ncomp == 3) {
-        mark(1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
-        mark(1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
+        mark(ci, 1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
+        mark(ci, 1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
       } else if (c.cvalid) {
-        inter_chroma(c);
+        inter_chroma(ci);
       }
       return;
     }
@@ -247,15 +281,15 @@ struct Planner {
         t.comps = (uint8_t)((c.yvalid ? 1 : 0) | (c.cvalid && !chromaStep ? 2 : 0));
         if (t.comps) out.inter_tiles.push_back(t);
       }
-    if (c.yvalid) mark(0, c.x, c.y, c.w, c.h, 0, true);
-    if (c.cvalid && !chromaStep) mark(1, c.cx, c.cy, c.cw, c.ch, 0, true);
-    if (chromaStep) inter_chroma_step(c);
+    cu_seq[ci] = seq;   // its units: level 0, no producer (reconstructed before the intra waves)
+    if (chromaStep) inter_chroma_step(ci);
   }
 
   // the chroma of an inter CU on its own (a CIIP CU whose chroma is not blended)
-  void inter_chroma(const vvcr_cu &c) {
+  void inter_chroma(int ci) {
+    const vvcr_cu &c = d.cu[ci];
     if (cscale) {
-      inter_chroma_step(c);
+      inter_chroma_step(ci);
       return;
     }
     for (int y = 0; y < c.h; y += 16)
@@ -266,10 +300,11 @@ struct Planner {
         t.comps = 2;
         out.inter_tiles.push_back(t);
       }
-    mark(1, c.cx, c.cy, c.cw, c.ch, 0, true);
+    cu_seq[ci] = seq;
   }
 
-  void inter_chroma_step(const vvcr_cu &c) {
+  void inter_chroma_step(int ci) {
+    const vvcr_cu &c = d.cu[ci];
     int id[3] = {-1, -1, -1}, lev = 0;
     for (int comp = 1; comp < 3; comp++) {
       IntraJob j = base(c, comp);
@@ -279,8 +314,8 @@ struct Planner {
       id[comp] = push(l, j);
       lev = std::max(lev, l);
     }
-    mark(1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
-    mark(1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
+    mark(ci, 1, c.cx, c.cy, c.cw, c.ch, lev, true, 1, id[1]);
+    mark(ci, 1, c.cx, c.cy, c.cw, c.ch, lev, false, 2, id[2]);
   }
 
   void intra_luma(int ci) {
@@ -312,7 +347,7 @@ struct Planner {
       const int fTop = ver ? 2 * c.w : c.w + j.w, fLeft = ver ? c.h + j.h : 2 * c.h;
       const int lev = 1 + ref_level(0, 0, c.x, c.y, fTop, fLeft, 0);
       const int id = push(lev, j);
-      mark(0, c.x, c.y, c.w, c.h, lev, true, 0, id);   // setDecomp of the whole CU (DecCu.cpp:288-291)
+      mark(ci, 0, c.x, c.y, c.w, c.h, lev, true, 0, id);   // setDecomp of the whole CU (DecCu.cpp:288-291)
       seq += (int)regs.size() - 1;
       return;
     }
@@ -328,7 +363,7 @@ struct Planner {
       else j.mode = (uint8_t)p.fidir_l;
       const int lev = 1 + ref_level(0, 0, j.x, j.y, 2 * j.w, 2 * j.h, j.mrl);
       const int id = push(lev, j);
-      mark(0, j.x, j.y, j.w, j.h, lev, true, 0, id);
+      mark(ci, 0, j.x, j.y, j.w, j.h, lev, true, 0, id);
     }
   }
 
@@ -371,7 +406,7 @@ struct Planner {
         if (cscale && j.w * j.h > 4) lev = std::max(lev, set_cscale(j, 2 * j.x, 2 * j.y));
         lev += 1;
         const int id = push(lev, j);
-        mark(1, j.x, j.y, j.w, j.h, lev, true, comp, id);
+        mark(ci, 1, j.x, j.y, j.w, j.h, lev, true, comp, id);
       }
     }
   }
@@ -382,7 +417,7 @@ struct Planner {
     const int pw = ch ? sp.width / 2 : sp.width, ph = ch ? sp.height / 2 : sp.height;
     if (x < 0 || y < 0 || x >= pw || y >= ph) return false;
     const int s = ch ? 1 : 2, cs = ch ? 1 : 0;
-    return out.order[ch][(size_t)(y >> s) * W4 + (x >> s)] < sq && region_at(x << cs, y << cs) == cur_reg;
+    return order_of(ch, (size_t)(y >> s) * W4 + (x >> s)) < sq && region_at(x << cs, y << cs) == cur_reg;
   }
   // xFillReferenceSamples unit scan (IntraPrediction.cpp:913-986, isAboveAvailable etc. :1208-1310):
   // returns the 65-bit availability mask in (lo, hi)
@@ -485,14 +520,27 @@ struct Planner {
     t0 = t1;                                                                                                     \
   }
     const size_t nu = (size_t)W4 * H4;
-    for (int k = 0; k < 2; k++) { out.order[k].assign(nu, 1 << 30); level[k].assign(nu, 0); }
-    for (int k = 0; k < 3; k++) prod[k].assign(nu, -1);
-    cu_map.assign(nu, -1);
-    for (size_t i = 0; i < d.cu.size(); i++) {
-      const vvcr_cu &c = d.cu[i];
-      if (!c.yvalid) continue;
-      for (int uy = c.y >> 2; uy < (c.y + c.h) >> 2; uy++)
-        for (int ux = c.x >> 2; ux < (c.x + c.w) >> 2; ux++) cu_map[(size_t)uy * W4 + ux] = (int)i;
+    // per-unit arrays without initialisation: only the units of written CUs are read (touch)
+    for (int k = 0; k < 2; k++) { out.order[k].resize(nu); level[k].resize(nu); }
+    for (int k = 0; k < 3; k++) prod[k].resize(nu);
+    cu_seq.assign(d.cu.size(), kInf);
+    for (int k = 0; k < 2; k++) written[k].assign(d.cu.size(), 0);
+    for (int k = 0; k < 2; k++) {
+      if (d.cu_map[k].size() == nu) {   // the producer's CU maps (the host parser hands them over)
+        umap[k] = d.cu_map[k].data();
+        continue;
+      }
+      own_map[k].assign(nu, -1);
+      for (size_t i = 0; i < d.cu.size(); i++) {
+        const vvcr_cu &c = d.cu[i];
+        if (k == 0 && c.yvalid)
+          for (int uy = c.y >> 2; uy < (c.y + c.h) >> 2; uy++)
+            for (int ux = c.x >> 2; ux < (c.x + c.w) >> 2; ux++) own_map[0][(size_t)uy * W4 + ux] = (int)i;
+        if (k == 1 && c.cvalid)
+          for (int uy = c.cy >> 1; uy < (c.cy + c.ch + 1) >> 1; uy++)
+            for (int ux = c.cx >> 1; ux < (c.cx + c.cw + 1) >> 1; ux++) own_map[1][(size_t)uy * W4 + ux] = (int)i;
+      }
+      umap[k] = own_map[k].data();
     }
     wc = (sp.width + ctu - 1) / ctu;
     const int hc = (sp.height + ctu - 1) / ctu;
