@@ -40,12 +40,42 @@ def _create(sp, pp):
 def test_create_rejects_unsupported_sequences():
     p, pp = _pic0()
     h = p["hdr"]
-    for kw in ({"chroma": 2}, {"width": h["width"] + 4}, {"ctu": 8}, {"slots": 0}, {"slots": 65}, {"height": 0}):
+    for kw in ({"chroma": 2}, {"width": h["width"] + 4}, {"ctu": 8}, {"slots": 0}, {"slots": 65}, {"height": 0},
+               {"bd": 7}, {"bd": 12}):
         r, hd = _create(_seq(h, **kw), pp)
         assert r == E_UNSUPPORTED, kw
         assert not hd.value
     L = N.lib()
     assert L.vvcr_picture_create(None, C.byref(pp), C.byref(C.c_void_p())) == E_ARG
+
+
+def test_create_errors_from_several_threads():
+    """The error text of a failed create is per thread (vvcr_picture_last_error(NULL)): threads failing
+    and succeeding at once each read their own outcome."""
+    import threading
+    p, pp = _pic0()
+    h = p["hdr"]
+    L = N.lib()
+    bad = []
+
+    def run(k):
+        for _ in range(50):
+            r, hd = _create(_seq(h, bd=12) if k % 2 else _seq(h), pp)
+            if k % 2:
+                msg = L.vvcr_picture_last_error(None).decode()
+                if r != E_UNSUPPORTED or hd.value or "8..10 bit" not in msg:
+                    bad.append((k, r, msg))
+            else:
+                if r != 0 or not hd.value:
+                    bad.append((k, r))
+                else:
+                    L.vvcr_picture_destroy(hd)
+    ts = [threading.Thread(target=run, args=(k,)) for k in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not bad, bad[:3]
 
 
 def test_calls_out_of_order_and_null_handles():

@@ -2,7 +2,12 @@
 decoder's own output files (MD5 of the whole file at several output bit depths, tests/golden/<stream>/
 output_md5.json) and, per picture, against the C oracle (oracle/oracle_output.c) for parameters the
 fixtures do not cover (odd bit depths, other conformance windows). Also the plane MD5s (= the stream's SEI)
-of the conformance-window stream ra412c_q32."""
+of the conformance-window stream ra412c_q32.
+
+Parity unpinned: the reference's own output files cover 8/10/12-bit output with the right/bottom crop
+of ra412c_q32 (0, 4, 0, 4) only. 9- and 16-bit output and crops with left/top offsets (`extra` below) are
+checked against the C oracle alone, a restatement of TVideoIOYuv::write (VideoIOYuv.cpp) that no
+reference-produced file confirms."""
 import hashlib
 import json
 import os
