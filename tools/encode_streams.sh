@@ -2,7 +2,7 @@
 # Re-creates the committed test bitstreams with the REFERENCE encoder built by oracle/ref.mk
 # (VTM 7.3 EncoderApp, CTC configs from /root/reference/cfg). Test-infrastructure only; runs in the
 # build container (needs /root/reference). Every stream carries MD5 decoded-picture-hash SEI.
-#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32
+#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 ra2160n_q27 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32
 set -e
 R=/root/reference/cfg; E=${E:-$(dirname $0)/../oracle/_ref/EncoderApp}; T=${T:-/tmp/enc}; O=${O:-$(dirname $0)/../tests/golden/streams}
 mkdir -p $T $O
@@ -42,9 +42,12 @@ for n in "$@"; do case $n in
   ra412c_q32) [ -f $T/syn412.yuv ] || $G 412 236 5 $T/syn412.yuv; enc $n encoder_randomaccess_vtm.cfg 412 236 5 32 $T/syn412.yuv --ConformanceWindowMode=1 ;;
   # 4K random access, a whole GOP-16 after the intra picture (17 pictures), so the I picture is 1/17 of
   # the work as in the CTC random-access configuration (BASELINE configs[2] QP27, north star QP32).
-  # Encoder-side speed-ups only (search range, fast decisions); the coded tool set is the CTC one.
-  ra2160l_q27) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 17 27 $T/syn2160l.yuv $EFAST ;;
-  ra2160l_q32) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 17 32 $T/syn2160l.yuv $EFAST ;;
+  # Encoder-side speed-ups only (search range, fast decisions, multi-type-tree search depth 1 as for 8K:
+  # the CTC-depth search took ~90 min per 4K picture here); the coded tool set is the CTC one.
+  # ra2160n: the first 9 pictures (I + the first 8 of the GOP), a shorter run of the same encode.
+  ra2160l_q27) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 17 27 $T/syn2160l.yuv $FAST ;;
+  ra2160l_q32) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 17 32 $T/syn2160l.yuv $FAST ;;
+  ra2160n_q27) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 9 27 $T/syn2160l.yuv $FAST ;;
   # a second independently moving layer cut by polygon edges: GEO (InterPrediction.cpp:1749) and CIIP
   # (IntraPrediction.cpp:681,735) CUs in quantity
   rageo480_q32) [ -f $T/syn480g.yuv ] || $G 832 480 17 $T/syn480g.yuv 0.002 0 0 layers; enc $n encoder_randomaccess_vtm.cfg 832 480 17 32 $T/syn480g.yuv ;;

@@ -94,7 +94,7 @@ inline int tbMax(uint32_t v) { return floorLog2(v); }   // g_tbMax (Rom.h:195) f
 // Coefficient coding context (ContextModelling.h:51 CoeffCodingContext)
 // ------------------------------------------------------------------------------------------------
 struct CoefCtx {
-  int ch, comp, w, h, log2CGw, log2CGh, log2CG, wg, hg, maxNumCoeff;
+  int ch, comp, w, h, log2w, log2CGw, log2CGh, log2CG, wg, hg, maxNumCoeff;
   bool signHiding, bdpcm;
   const ScanPos *scan, *scanCG;
   int lastX, lastY, lastOffX = 0, lastOffY = 0, lastShX = 0, lastShY = 0;
@@ -109,6 +109,7 @@ struct CoefCtx {
   CoefCtx(int comp_, int w_, int h_, bool sh, bool bd) : comp(comp_), w(w_), h(h_), signHiding(sh), bdpcm(bd) {
     ch = comp ? 1 : 0;
     const int lw = floorLog2(w), lh = floorLog2(h);
+    log2w = lw;
     log2CGw = kLog2Sbb[lw][lh][0];
     log2CGh = kLog2Sbb[lw][lh][1];
     log2CG = log2CGw + log2CGh;
@@ -1556,18 +1557,32 @@ struct Parser {
       if ((c.predmode == MODE_INTRA && mask) || mask == 3) t.jccr = cab.bin(JointCbCrFlag + mask - 1) ? mask : 0;
     }
     (void)isp;
-    // coefficient levels go straight into the picture's pool: a zeroed w*h block per coded component
-    // (and per chroma component of a joint Cb-Cr TU), in component order
+    // coefficient levels: decoded into the zeroed scratch block, then the bounding box of the non-zero
+    // levels goes into the picture's pool (a block per coded component, and per chroma component of a
+    // joint Cb-Cr TU, in component order); the scratch is zeroed again
+    if (pic.box.size() < 3 * (size_t)(ti + 1)) pic.box.resize(3 * (size_t)(ti + 1), 0);
     for (int comp = 0; comp < 3; comp++) {
       vvcr_tu &tt = pic.tu[ti];
       if (!tuValid(tt, comp) || !(tt.b[comp][4] || (comp > 0 && tt.jccr))) continue;
-      const size_t n = (size_t)tt.b[comp][2] * tt.b[comp][3], off = pic.coef.size();
-      tt.b[comp][6] = (int32_t)off;
-      pic.coef.resize(off + n);
+      const int w = tt.b[comp][2];
       const bool coded = comp == 0 ? cbfLuma : (!lumaOnly && tt.b[comp][4]);
-      if (coded) residual_coding(ci, ti, comp, cuCtx, pic.coef.data() + off);
+      boxR = boxC = 0;
+      if (coded) residual_coding(ci, ti, comp, cuCtx, scratch);
+      const size_t off = pic.coef.size();
+      tt.b[comp][6] = (int32_t)off;
+      pic.box[3 * (size_t)ti + comp] = (uint16_t)(boxR | boxC << 8);
+      if (boxR && boxC) {
+        pic.coef.resize(off + (size_t)boxR * boxC);
+        int32_t *dst = pic.coef.data() + off;
+        for (int y = 0; y < boxR; y++, dst += boxC) {
+          std::memcpy(dst, scratch + y * w, (size_t)boxC * sizeof(int32_t));
+          std::memset(scratch + y * w, 0, (size_t)boxC * sizeof(int32_t));
+        }
+      }
     }
   }
+  alignas(64) int32_t scratch[64 * 64] = {};   // one transform block's levels, zero between blocks
+  int boxR = 0, boxC = 0;                      // bounding box of its non-zero levels (rows, columns)
 
   int cu_qp_delta(int predQP) {   // CABACReader::cu_qp_delta (:2850)
     int dqp = 0;
@@ -1609,7 +1624,7 @@ struct Parser {
     int ts = ((c.bdpcm && comp == 0) || (c.bdpcmc && comp != 0)) ? 1 : (t.b[comp][5] == MTS_SKIP ? 1 : 0);
     if (tsAllowed(c, t, comp)) ts = cab.bin(TransformSkipFlag + (comp == 0 ? 0 : 1));
     t.b[comp][5] = ts ? MTS_SKIP : MTS_DCT2;
-    if (ts) { residual_codingTS(c, comp, w, h, coeff); return; }
+    if (ts) { residual_codingTS(c, comp, w, h, coeff); boxR = h; boxC = w; return; }
     const bool signHiding = ph.signHiding;
     CoefCtx cc(comp, w, h, signHiding, false);
     cc.scanPosLast = last_sig_coeff(cc, c, comp, w, h);
@@ -1731,6 +1746,10 @@ struct Parser {
         lastNZPos = std::max(lastNZPos, sp);
         coeff[blkPos] = tc;
       }
+    }
+    for (int k = 0; k < numNonZero; k++) {
+      boxR = std::max(boxR, (sigBlkPos[k] >> cc.log2w) + 1);
+      boxC = std::max(boxC, (sigBlkPos[k] & (cc.w - 1)) + 1);
     }
     const unsigned numSigns = (cc.signHiding && (lastNZPos - firstNZPos >= 4)) ? numNonZero - 1 : numNonZero;
     unsigned signPattern = numSigns ? cab.eps(numSigns) << (32 - numSigns) : 0;
@@ -2113,14 +2132,34 @@ void PictureSyntax::reset(int W_, int H_, int ctuLog2_) {
   hCtu = (H + ctuSize - 1) >> ctuLog2;
   w4 = (W + 3) >> 2;
   h4 = (H + 3) >> 2;
-  cu.clear(); cux.clear(); pu.clear(); pux.clear(); tu.clear(); coef.clear();
-  coef.reserve((size_t)W * H * 3 / 2 + 8192);   // dense blocks: at most every sample of the three planes
+  cu.clear(); cux.clear(); pu.clear(); pux.clear(); tu.clear(); coef.clear(); box.clear();
+  coef.reserve((size_t)W * H * 3 / 2 + 8192);   // at most every sample of the three planes
   for (int c = 0; c < 2; c++) map[c].assign((size_t)w4 * h4, -1);
   const size_t n = (size_t)wCtu * hCtu;
   sao.assign(n * 3, vvcr_sao());
   for (int c = 0; c < 3; c++) { alfEn[c].assign(n, 0); alfAlt[c].assign(n, 0); }
   for (int c = 0; c < 2; c++) ccCtl[c].assign(n, 0);
   alfFset.assign(n, 0);
+}
+
+void PictureSyntax::dense_rows(std::vector<vvcr_tu> &tus, std::vector<int32_t> &pool) const {
+  tus.assign(tu.begin(), tu.end());
+  size_t n = 0;
+  for (const vvcr_tu &t : tu)
+    for (int c = 0; c < 3; c++)
+      if (t.b[c][6] >= 0) n += (size_t)t.b[c][2] * t.b[c][3];
+  pool.assign(n, 0);
+  size_t off = 0;
+  for (size_t i = 0; i < tu.size(); i++)
+    for (int c = 0; c < 3; c++) {
+      const int32_t *b = tu[i].b[c];
+      if (b[6] < 0) continue;
+      const int rows = box[3 * i + c] & 255, cols = box[3 * i + c] >> 8;
+      for (int y = 0; y < rows; y++)
+        std::memcpy(pool.data() + off + (size_t)y * b[2], coef.data() + b[6] + (size_t)y * cols, (size_t)cols * sizeof(int32_t));
+      tus[i].b[c][6] = (int32_t)off;
+      off += (size_t)b[2] * b[3];
+    }
 }
 
 int PictureSyntax::cuAt(int ch, int x, int y) const {
@@ -2135,6 +2174,7 @@ void parse_slice_data(PictureSyntax &pic, const SliceCtx &sc, const uint8_t *rbs
 }
 
 void finish_picture_syntax(PictureSyntax &pic, int bitDepth) {
+  pic.box.resize(3 * pic.tu.size(), 0);   // TUs after the last one with levels
   // PU::getFinalIntraMode (UnitTools.cpp:627) of intra PUs, 4:2:0: DM resolves to the co-located luma
   // mode (PU::getCoLocatedIntraLumaMode :642), MIP luma neighbours count as planar
   for (vvcr_pu &u : pic.pu) {

@@ -37,7 +37,11 @@ struct PictureSyntax {
   bigbuf::vec<vvcr_pu> pu;
   bigbuf::vec<PuSyntax> pux;
   bigbuf::vec<vvcr_tu> tu;
+  // coefficient levels packed per transform block: only the bounding box of the non-zero levels (the
+  // whole block for transform skip), rows of box-width; tu[t].b[c][6] is the box's offset in coef and
+  // box[3 t + c] = rows | cols << 8. dense_rows() gives the w*h-per-block form of vvcr_picture_submit.
   bigbuf::vec<int32_t> coef;
+  bigbuf::vec<uint16_t> box;
   // maps over 4x4 luma units: CU index per channel (-1 = not decoded)
   bigbuf::vec<int32_t> map[2];
   // loop-filter syntax per CTB
@@ -45,6 +49,7 @@ struct PictureSyntax {
   std::vector<uint8_t> alfEn[3], alfAlt[3], ccCtl[2];
   std::vector<int16_t> alfFset;
   void reset(int W, int H, int ctuLog2);
+  void dense_rows(std::vector<vvcr_tu> &tus, std::vector<int32_t> &pool) const;
   int cuAt(int ch, int x, int y) const;   // x, y in samples of channel ch; -1 outside / not decoded
 };
 

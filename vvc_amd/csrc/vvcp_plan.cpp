@@ -49,11 +49,16 @@ extern "C" int vvcp_plan_picture(vvcp_stream *h, int32_t idx, const vvcr_seq_par
     D.pu.assign(S.pu.begin(), S.pu.end());
     D.tu = std::move(S.tu);
     D.coef = std::move(S.coef);
+    D.coef_box = std::move(S.box);
     D.motion = std::move(p.motion);
     D.geo.assign(p.geo.begin(), p.geo.end());
     D.cu_map[0] = std::move(S.map[0]);
     D.cu_map[1] = std::move(S.map[1]);
     vvcr_picture_adopt(pic, std::move(D));
+  } catch (const VvcrError &e) {
+    vvcp::set_api_error(std::string("vvcr_picture_submit: ") + e.msg);
+    vvcr_picture_destroy(pic);
+    return e.code;
   } catch (const std::exception &e) {
     vvcp::set_api_error(std::string("vvcr_picture_submit: ") + e.what());
     vvcr_picture_destroy(pic);

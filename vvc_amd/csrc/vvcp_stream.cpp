@@ -324,11 +324,17 @@ int64_t vvcp_picture_rows(const vvcp_stream *h, int32_t idx, int32_t what, void 
   const vvcp::PictureSyntax &s = p.syn;
   const void *src = nullptr;
   int64_t count = 0, esz = 0;
+  std::vector<vvcr_tu> dtu;     // TU rows and coefficient pool in vvcr_picture_submit's dense form
+  std::vector<int32_t> dcoef;
+  if (what == VVCP_ROWS_TU || what == VVCP_ROWS_COEF) {
+    if (p.handedOver) return VVCR_E_STATE;
+    s.dense_rows(dtu, dcoef);
+  }
   switch (what) {
     case VVCP_ROWS_CU: src = s.cu.data(); count = (int64_t)s.cu.size(); esz = sizeof(vvcr_cu); break;
     case VVCP_ROWS_PU: src = s.pu.data(); count = (int64_t)s.pu.size(); esz = sizeof(vvcr_pu); break;
-    case VVCP_ROWS_TU: src = s.tu.data(); count = (int64_t)s.tu.size(); esz = sizeof(vvcr_tu); break;
-    case VVCP_ROWS_COEF: src = s.coef.data(); count = (int64_t)s.coef.size(); esz = 4; break;
+    case VVCP_ROWS_TU: src = dtu.data(); count = (int64_t)dtu.size(); esz = sizeof(vvcr_tu); break;
+    case VVCP_ROWS_COEF: src = dcoef.data(); count = (int64_t)dcoef.size(); esz = 4; break;
     case VVCP_ROWS_SAO: src = s.sao.data(); count = (int64_t)s.sao.size(); esz = sizeof(vvcr_sao); break;
     case VVCP_ROWS_ALF_EN0: case VVCP_ROWS_ALF_EN0 + 1: case VVCP_ROWS_ALF_EN0 + 2:
       src = s.alfEn[what - VVCP_ROWS_ALF_EN0].data(); count = (int64_t)s.alfEn[0].size(); esz = 1; break;

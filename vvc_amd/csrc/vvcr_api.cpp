@@ -33,7 +33,15 @@ template <class T>
 struct DevVec {
   T *p = nullptr;
   size_t cap = 0;
+  bool view = false;   // p points into a Prepared record's upload arena (not owned)
+  void set_view(T *q) {
+    if (p && !view) VVCR_CHECK_HIP(hipFree(p));
+    p = q;
+    cap = 0;
+    view = true;
+  }
   void ensure(size_t n) {
+    if (view) { p = nullptr; view = false; }
     if (n <= cap) return;
     if (p) VVCR_CHECK_HIP(hipFree(p));
     size_t c = std::max<size_t>(n, cap * 3 / 2 + 64);
@@ -49,7 +57,54 @@ struct DevVec {
   DevVec() = default;
   DevVec(const DevVec &) = delete;
   DevVec &operator=(const DevVec &) = delete;
-  ~DevVec() { if (p) (void)hipFree(p); }
+  ~DevVec() { if (p && !view) (void)hipFree(p); }
+};
+
+// Upload staging of one prepared picture: every host array its kernels read is copied into one pinned
+// buffer, then one asynchronous copy moves it to one device arena on the context's upload stream (the
+// lanes wait for its event). A picture's upload costs one DMA instead of a dozen synchronous pageable
+// copies, and the preparing thread does not wait for it.
+struct Staging {
+  uint8_t *h = nullptr;
+  size_t cap = 0, used = 0;
+  DevVec<uint8_t> arena;
+  struct Item { void **dst; size_t off; };
+  std::vector<Item> items;
+  ~Staging() { if (h) (void)hipHostFree(h); }
+  void begin() { used = 0; items.clear(); }
+  void reserve(size_t n) {
+    if (n <= cap) return;
+    const size_t c = std::max(n, cap * 3 / 2 + (1 << 20));
+    uint8_t *q = nullptr;
+    VVCR_CHECK_HIP(hipHostMalloc((void **)&q, c, hipHostMallocDefault));
+    if (used) std::memcpy(q, h, used);
+    if (h) VVCR_CHECK_HIP(hipHostFree(h));
+    h = q;
+    cap = c;
+  }
+  // appends the parts (pointer, count) as one contiguous array for d
+  template <class T> void add(DevVec<T> &d, std::initializer_list<std::pair<const T *, size_t>> parts) {
+    size_t n = 0;
+    for (auto &pt : parts) n += pt.second;
+    const size_t off = (used + 255) & ~(size_t)255;
+    reserve(off + (n + 1) * sizeof(T));
+    size_t o = off;
+    for (auto &pt : parts) {
+      if (pt.second) std::memcpy(h + o, pt.first, pt.second * sizeof(T));
+      o += pt.second * sizeof(T);
+    }
+    used = off + (n + 1) * sizeof(T);
+    items.push_back({(void **)&d.p, off});
+    d.set_view(nullptr);
+  }
+  template <class T, class A> void add(DevVec<T> &d, const std::vector<T, A> &v) { add(d, {{v.data(), v.size()}}); }
+  template <class T> void add(DevVec<T> &d, const T *src, size_t n) { add(d, {{src, n}}); }
+  void commit(hipStream_t s, hipEvent_t done) {
+    arena.ensure(used + 256);
+    for (const Item &it : items) *it.dst = arena.p + it.off;
+    if (used) VVCR_CHECK_HIP(hipMemcpyAsync(arena.p, h, used, hipMemcpyHostToDevice, s));
+    VVCR_CHECK_HIP(hipEventRecord(done, s));
+  }
 };
 
 DPlane alloc_plane(int w, int h) {
@@ -99,6 +154,9 @@ struct Prepared {
   hipEvent_t mc_done = nullptr;                 // the DMVR deltas of the launch are in h_dmvr
   int32_t *h_dmvr = nullptr;                    // pinned host copy of the DMVR deltas
   size_t h_dmvr_cap = 0;
+  Staging up;                                   // the picture's host arrays, staged for one upload
+  hipEvent_t up_done = nullptr;                 // the upload has landed in up.arena
+  bool up_issued = false;
   bool ran[NK] = {};
   bool timed[NK] = {};              // the group's events were recorded by the last launch
   bool launched = false;
@@ -112,6 +170,7 @@ struct Prepared {
     VVCR_CHECK_HIP(hipEventCreate(&start));
     VVCR_CHECK_HIP(hipEventCreateWithFlags(&mc_done, hipEventDisableTiming));
     VVCR_CHECK_HIP(hipEventCreateWithFlags(&ev_mc, hipEventDisableTiming));
+    VVCR_CHECK_HIP(hipEventCreateWithFlags(&up_done, hipEventDisableTiming));
   }
   ~Prepared() {
     for (auto &e : ev) { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); }
@@ -119,6 +178,8 @@ struct Prepared {
     (void)hipEventDestroy(start);
     (void)hipEventDestroy(mc_done);
     (void)hipEventDestroy(ev_mc);
+    if (up_issued) (void)hipEventSynchronize(up_done);   // the DMA may still read the pinned staging buffer
+    (void)hipEventDestroy(up_done);
     if (h_dmvr) (void)hipHostFree(h_dmvr);
   }
   void wait() { if (launched) VVCR_CHECK_HIP(hipEventSynchronize(done)); }
@@ -216,6 +277,7 @@ struct Lane {
 struct vvcr_ctx {
   vvcr_seq_params sp{};
   hipStream_t stream = nullptr;      // lane 0's stream (host copies, vvcr_stream)
+  hipStream_t upload_stream = nullptr;   // prepared pictures' uploads (Staging)
   hipStream_t copy_stream = nullptr; // halo row export / import (vvcr_export_rows / vvcr_import_rows), output frames
   DevVec<uint8_t> out_stage;         // vvcr_write_output to host memory
   std::vector<std::array<DPlane, 3>> dpb;
@@ -379,6 +441,9 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
       bp.sp.bit_depth != ctx->sp.bit_depth || bp.sp.dpb_slots > ctx->sp.dpb_slots)
     throw VvcrError(VVCR_E_ARG, "picture built for other sequence parameters than the context's");
   r.wait();
+  if (r.up_issued) VVCR_CHECK_HIP(hipEventSynchronize(r.up_done));   // a prepared, never launched picture
+  Staging &st = r.up;
+  st.begin();
   r.pp = bp.pp;
   const uint32_t mask = bp.mask;
   r.mask = mask;
@@ -389,8 +454,9 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   const WorkLists &wl = bp.wl;
   const double pix = (double)sp.width * sp.height * 1.5;   // samples of the three planes
   if (mask & VVCR_STAGE_RESID) {
-    r.coef.upload(bp.wl.coef);   // the packed levels of the transform blocks
-    r.tb.upload(wl.tb);
+    // the packed levels of the transform blocks: the producer's pool when it arrived packed
+    st.add(r.coef, bp.desc.coef_box.empty() ? bp.wl.coef : bp.desc.coef);
+    st.add(r.tb, wl.tb);
     r.n_tb = (int)wl.tb.size();
     r.n_tb_small = wl.tb_small;
     double b = 0;
@@ -398,14 +464,11 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.alg_bytes[K_RESID] = b;
   }
   if (mask & VVCR_STAGE_INTER) {
-    {   // 32x32 tiles first, then the small jobs, in one buffer
-      bigbuf::vec<McJob> all(wl.mc_tile);
-      all.insert(all.end(), wl.mc_basic.begin(), wl.mc_basic.end());
-      r.mc_basic.upload(all);
-    }
-    r.mc_bidir.upload(wl.mc_bidir);
-    r.aff_pu.upload(wl.aff_pu);
-    r.aff_jobs.upload(wl.aff_jobs);
+    // 32x32 tiles first, then the small jobs, in one array
+    st.add(r.mc_basic, {{wl.mc_tile.data(), wl.mc_tile.size()}, {wl.mc_basic.data(), wl.mc_basic.size()}});
+    st.add(r.mc_bidir, wl.mc_bidir);
+    st.add(r.aff_pu, wl.aff_pu);
+    st.add(r.aff_jobs, wl.aff_jobs);
     r.n_mctile = (int)wl.mc_tile.size();
     r.n_basic = (int)wl.mc_basic.size();
     r.n_bidir = (int)wl.mc_bidir.size();
@@ -432,23 +495,21 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.alg_bytes[K_MC_AFFINE] = b;
   }
   if (pp.lmcs_enabled) {
-    std::vector<int16_t> lut(pp.lmcs_fwd, pp.lmcs_fwd + 1024);
-    lut.insert(lut.end(), pp.lmcs_inv, pp.lmcs_inv + 1024);
-    r.lmcs_lut.upload(lut);
+    st.add(r.lmcs_lut, {{pp.lmcs_fwd, 1024}, {pp.lmcs_inv, 1024}});
   }
   if (mask & VVCR_STAGE_INTRA) {
     const IntraPlan &ip = bp.intra;
-    r.tiles.upload(ip.inter_tiles);
-    r.ijobs.upload(ip.jobs);
-    r.idep_start.upload(ip.dep_start);
-    r.ideps.upload(ip.deps);
+    st.add(r.tiles, ip.inter_tiles);
+    st.add(r.ijobs, ip.jobs);
+    st.add(r.idep_start, ip.dep_start);
+    st.add(r.ideps, ip.deps);
     r.istate.ensure(16 + ip.jobs.size());
     IntraParams P[MAXLANE];   // one device copy per lane (scratch plane pointers differ)
     for (int l = 0; l < MAXLANE; l++) P[l] = make_intra_params(ctx, r, l);
-    r.iparams.upload(P, MAXLANE);
+    st.add(r.iparams, P, MAXLANE);
     r.n_ijobs = (int)ip.jobs.size();
-    r.ictu_list.upload(ip.ctu_list);
-    r.ictu_start.upload(ip.ctu_start);
+    st.add(r.ictu_list, ip.ctu_list);
+    st.add(r.ictu_start, ip.ctu_start);
     r.n_ictu = (int)ip.ctu_list.size();
     r.n_tiles = (int)ip.inter_tiles.size();
     double b = 0;
@@ -462,13 +523,10 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.alg_bytes[K_INTRA] = b;
   }
   if (mask & VVCR_STAGE_DBK) {
-    bigbuf::vec<DbkSeg> all;
     const bigbuf::vec<DbkSeg> *parts[4] = {&bp.dbk.luma[0], &bp.dbk.chroma[0], &bp.dbk.luma[1], &bp.dbk.chroma[1]};
-    for (int k = 0; k < 4; k++) {
-      r.dbk_counts[k] = (int)parts[k]->size();
-      all.insert(all.end(), parts[k]->begin(), parts[k]->end());
-    }
-    r.dbk.upload(all);
+    for (int k = 0; k < 4; k++) r.dbk_counts[k] = (int)parts[k]->size();
+    st.add(r.dbk, {{parts[0]->data(), parts[0]->size()}, {parts[1]->data(), parts[1]->size()},
+                   {parts[2]->data(), parts[2]->size()}, {parts[3]->data(), parts[3]->size()}});
     r.alg_bytes[K_DBK] = pix * 2 * 2;
   }
   const bool saoOn = pp.sao_luma || pp.sao_chroma;
@@ -476,18 +534,20 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   r.have_sao = (mask & VVCR_STAGE_SAO) && saoOn;
   r.have_alf = (mask & VVCR_STAGE_ALF) && alfOn;
   if (r.have_sao) {
-    r.sao.upload(bp.h_sao);
+    st.add(r.sao, bp.h_sao);
     r.alg_bytes[K_SAO] = pix * 2 * 2;
   }
   if (r.have_alf) {
-    r.alf_luma_coef.upload(bp.h_alf_luma_coef);
-    r.alf_luma_clip.upload(bp.h_alf_luma_clip);
-    r.alf_chroma.upload(bp.h_alf_chroma);
-    r.alf_cc.upload(bp.h_alf_cc);
-    r.alf_ctb.upload(bp.h_alf_ctb);
-    r.alf_set.upload(bp.h_alf_set);
+    st.add(r.alf_luma_coef, bp.h_alf_luma_coef);
+    st.add(r.alf_luma_clip, bp.h_alf_luma_clip);
+    st.add(r.alf_chroma, bp.h_alf_chroma);
+    st.add(r.alf_cc, bp.h_alf_cc);
+    st.add(r.alf_ctb, bp.h_alf_ctb);
+    st.add(r.alf_set, bp.h_alf_set);
     r.alg_bytes[K_ALF] = pix * 2 * 2;
   }
+  st.commit(ctx->upload_stream, r.up_done);
+  r.up_issued = true;
 }
 
 // Device phase: enqueue the kernels of a prepared picture on the context stream.
@@ -542,6 +602,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   if (ctx->slot_w_set[pp.slot] && ctx->slot_lane[pp.slot] != L) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[pp.slot], 0));
   for (int l = 0; l < ctx->nlane; l++)
     if (l != L && (ctx->slot_r_set[pp.slot] >> l & 1)) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_r[pp.slot][l], 0));
+  VVCR_CHECK_HIP(hipStreamWaitEvent(s, r.up_done, 0));   // the picture's upload
   VVCR_CHECK_HIP(hipEventRecord(r.start, s));
   if (mask & VVCR_STAGE_RESID) {
     KernelTimer t(r, K_RESID, s, ctx->timing);
@@ -709,6 +770,7 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     }
     ctx->stream = ctx->lanes[0].s;
     VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    VVCR_CHECK_HIP(hipStreamCreateWithFlags(&ctx->upload_stream, hipStreamNonBlocking));
     const int W = sp->width, H = sp->height;
     ctx->dpb.resize(sp->dpb_slots);
     for (auto &s : ctx->dpb) {
@@ -773,6 +835,7 @@ int vvcr_destroy(vvcr_ctx *ctx) {
   if (ctx->d_err) (void)hipFree(ctx->d_err);
   for (int l = 0; l < ctx->nlane; l++) (void)hipStreamDestroy(ctx->lanes[l].s);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
+  if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
   delete ctx;
   return VVCR_OK;
 }
@@ -809,6 +872,9 @@ static void pic_submit(vvcr_picture &b, const vvcr_cu *cu, int32_t ncu, const vv
   d.pu.assign(pu, pu + npu);
   d.tu.assign(tu, tu + ntu);
   d.coef.assign(coef, coef + ncoef);
+  d.coef_box.clear();   // the dense pool
+  d.cu_map[0].clear();
+  d.cu_map[1].clear();
   const size_t nm = (size_t)(b.sp.width / 4) * (b.sp.height / 4);
   if (motion) d.motion.assign(motion, motion + nm); else d.motion.clear();
   d.geo.assign(geo, geo + ngeo);

@@ -120,6 +120,8 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
       if ((p.interdir & 2) && (p.ref1 < 0 || p.ref1 >= pp.num_ref[1])) fail("PU " + std::to_string(i) + " ref1");
     }
   }
+  const bool packed = !d.coef_box.empty();
+  if (packed && d.coef_box.size() < 3 * (size_t)ntu) fail("packed coefficient boxes");
   for (int i = 0; i < ntu; i++) {
     const vvcr_tu &t = d.tu[i];
     if (t.cu < 0 || t.cu >= ncu) fail("TU " + std::to_string(i) + " CU index");
@@ -130,7 +132,11 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
       const int maxs = b[6] >= 0 ? 64 : 128;   // coded TBs are <= 64 (maxTbSize); residual-free TUs span the CU
       // every block lies inside its plane: the kernels store residual / reconstruction rows unclipped
       if (b[0] < 0 || b[1] < 0 || b[0] + b[2] > pw || b[1] + b[3] > ph || b[2] > maxs || b[3] > maxs) fail("TU " + std::to_string(i) + " area");
-      if (b[6] >= 0 && (int64_t)b[6] + (int64_t)b[2] * b[3] > (int64_t)d.coef.size()) fail("TU " + std::to_string(i) + " coefficient range");
+      if (!packed && b[6] >= 0 && (int64_t)b[6] + (int64_t)b[2] * b[3] > (int64_t)d.coef.size()) fail("TU " + std::to_string(i) + " coefficient range");
+      if (packed && b[6] >= 0) {
+        const int rows = d.coef_box[3 * (size_t)i + c] & 255, cols = d.coef_box[3 * (size_t)i + c] >> 8;
+        if (rows > b[3] || cols > b[2] || (int64_t)b[6] + (int64_t)rows * cols > (int64_t)d.coef.size()) fail("TU " + std::to_string(i) + " coefficient range");
+      }
     }
   }
   if (!d.motion.empty() && d.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4)) fail("motion field size");
@@ -489,11 +495,13 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
                    bigbuf::vec<int32_t> &packed) {
   out.clear();
   packed.clear();
+  const bool prepacked = !d.coef_box.empty();   // the producer's pool is already packed: uploaded as it is
   const int W4 = sp.width / 4, H4 = sp.height / 4;
   bigbuf::vec<int> lmap;   // luma PU per 4x4, for co-located luma modes (PU::getCoLocatedIntraLumaMode)
   bool haveMap = false;
   static const int kIct[2][4] = {{0, 3, 1, 2}, {0, -3, -1, -2}};
-  for (const vvcr_tu &t : d.tu) {
+  for (size_t ti = 0; ti < d.tu.size(); ti++) {
+    const vvcr_tu &t = d.tu[ti];
     const vvcr_cu &cu = d.cu[t.cu];
     if (!in_shard(pp, cu)) continue;
     const bool sepTree = cu.treetype != 0 || pp.dual_tree;
@@ -559,7 +567,18 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
       if (comp == 1 && t.jccr) j.ict = (int8_t)kIct[pp.joint_cbcr_sign ? 1 : 0][t.jccr];
       // bounding box of the non-zero levels: the kernel's passes skip the all-zero rows / columns
       // (dequantisation maps 0 to 0; LFNST widens it to its output area; TS / BDPCM use the whole block)
-      {
+      if (prepacked) {   // the box as parsed; LFNST widens the processed box past the stored one
+        const int SR = d.coef_box[3 * ti + src] & 255, SC = d.coef_box[3 * ti + src] >> 8;
+        int R = SR, C = SC;
+        if (ts) { R = h; C = w; }
+        else if (j.flags & TB_LFNST_APPLY) {
+          const int r = (w >= 8 && h >= 8) ? 8 : 4;
+          R = std::max(R, std::min(r, h)); C = std::max(C, std::min(r, w));
+        }
+        j.nz_rows = (uint8_t)R; j.nz_cols = (uint8_t)C;
+        j.st_rows = (uint8_t)SR; j.st_cols = (uint8_t)SC;
+        j.flags |= TB_PACKED;
+      } else {
         int R = 0, C = 0;
         if ((size_t)j.coef + (size_t)w * h > d.coef.size()) throw VvcrError(VVCR_E_ARG, "coefficient offset out of range");
         const int32_t *lv = d.coef.data() + j.coef;
@@ -581,6 +600,7 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
           }
         }
         j.nz_rows = (uint8_t)R; j.nz_cols = (uint8_t)C;
+        j.st_rows = (uint8_t)R; j.st_cols = (uint8_t)C;
         // only the box travels to the device (most of a large inter TB is zero)
         const size_t off = packed.size();
         packed.resize(off + (size_t)R * C);

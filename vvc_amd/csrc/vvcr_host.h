@@ -14,7 +14,14 @@ struct PictureDescriptors {
   // optional: CU index per 4x4 luma unit of each channel (chroma: 2x2 chroma units), -1 where none;
   // the host parser hands its maps over, other producers leave them empty and the planners build them
   bigbuf::vec<int32_t> cu_map[2];
-  void clear() { cu.clear(); pu.clear(); tu.clear(); coef.clear(); motion.clear(); geo.clear(); cu_map[0].clear(); cu_map[1].clear(); }
+  // optional: the coefficient pool packed per transform block (the host parser's form, vvcp_ctu.h
+  // PictureSyntax::coef): tu[t].b[c][6] is the offset of a rows x cols box, box[3 t + c] = rows | cols << 8.
+  // Empty: the dense w*h-per-block pool of vvcr_picture_submit.
+  bigbuf::vec<uint16_t> coef_box;
+  void clear() {
+    cu.clear(); pu.clear(); tu.clear(); coef.clear(); motion.clear(); geo.clear(); cu_map[0].clear(); cu_map[1].clear();
+    coef_box.clear();
+  }
 };
 
 // Hands a producer's descriptor arrays to a picture (vvcr_picture_submit without the copies; validates

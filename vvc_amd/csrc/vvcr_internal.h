@@ -163,7 +163,7 @@ enum : uint8_t {
   TB_LFNST_APPLY = 1 << 2,     // inverse LFNST on this component
   TB_LFNST_TRANSPOSE = 1 << 3,
   TB_BDPCM_SHIFT = 4,          // bits 4..5: 0 off, 1 horizontal, 2 vertical
-  TB_PACKED = 1 << 6,          // levels stored as the nz_rows x nz_cols box (row pitch nz_cols), not w x h
+  TB_PACKED = 1 << 6,          // levels stored as the st_rows x st_cols box (row pitch st_cols), not w x h
 };
 struct TbJob {
   int16_t x, y;                // component-plane position
@@ -175,7 +175,7 @@ struct TbJob {
   uint8_t skip_w, skip_h;      // zero-out lines of xIT (TrQuant.cpp:841-852)
   int32_t coef;                // level offset in the coefficient pool (the packed upload pool with TB_PACKED)
   uint8_t nz_rows, nz_cols;    // bounding box of the non-zero levels (host-computed; TS/BDPCM: whole block)
-  uint8_t pad8[2];
+  uint8_t st_rows, st_cols;    // TB_PACKED: the box stored at coef (rows of st_cols levels; zero outside)
   int32_t pad[2];
 };
 static_assert(sizeof(TbJob) == 32, "TbJob layout");

@@ -114,12 +114,14 @@ __device__ __forceinline__ void resid_tb(const TbParams &P, const TbJob *jp, con
 
   // 1. every global read of the block up front
   const int32_t *lv = coef + J.coef;
-  const int pitch = (J.flags & TB_PACKED) ? C : w;   // packed: only the non-zero box was uploaded
+  // packed: only the stored box was uploaded (rows of st_cols levels), zero outside it
+  const bool packed = J.flags & TB_PACKED;
+  const int SR = packed ? J.st_rows : R, SC = packed ? J.st_cols : C, pitch = packed ? SC : w;
   int lvv[PER];
 #pragma unroll
   for (int q = 0; q < PER; q++) {
     const int i = tid + q * NT;
-    lvv[q] = (i < n && (i >> lw) < R && (i & (w - 1)) < C) ? lv[(i >> lw) * pitch + (i & (w - 1))] : 0;
+    lvv[q] = (i < n && (i >> lw) < SR && (i & (w - 1)) < SC) ? lv[(i >> lw) * pitch + (i & (w - 1))] : 0;
   }
   const int ns = min(w, 32) * min(h, 32);
   uint32_t sc[16];
