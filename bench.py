@@ -260,7 +260,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--stream", default=_default_stream())
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--segments", type=int, default=8, help="DPB copies of the sequence the steps cycle through (<= 12)")
+    ap.add_argument("--segments", type=int, default=12, help="DPB copies of the sequence the steps cycle through (<= 32)")
     ap.add_argument("--resident-steps", type=int, default=20, help="timed steps of the resident (pre-planned) pass, 0 = skip")
     ap.add_argument("--sync-pictures", action="store_true",
                     help="host sync after every picture of the resident pass (profiling: kernel durations without overlap)")
@@ -288,7 +288,7 @@ def main():
     px_seq = W * H * len(infos)
     nI = sum(1 for inf in infos if inf["slice_type"] == 2)
 
-    per = min(16, 64 // a.segments)   # DPB slots per copy (64 in all)
+    per = min(16, 256 // a.segments)   # DPB slots per copy (at most 256 in all)
     # k_intra workgroups (VVCR_INTRA_WG, read at vvcr_create): the library's default sizes one intra picture at
     # a time (32 at 1080p, 60 at 4K); with several intra pictures in flight 32 each is better (4K 7.6 -> 8.6
     # Gpx/s). The 8K shard pass, one picture at a time, keeps the default.

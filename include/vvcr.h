@@ -52,7 +52,7 @@ typedef struct vvcr_seq_params {
   int32_t chroma_format;       /* 1 = 4:2:0 (only supported format) */
   int32_t bit_depth;           /* luma = chroma bit depth (8..10) */
   int32_t ctu_log2;            /* 5..7 */
-  int32_t dpb_slots;           /* number of picture buffers to allocate (1..64) */
+  int32_t dpb_slots;           /* number of picture buffers to allocate (1..256) */
   int32_t device;              /* HIP device ordinal */
 } vvcr_seq_params;
 

@@ -40,7 +40,7 @@ def _create(sp, pp):
 def test_create_rejects_unsupported_sequences():
     p, pp = _pic0()
     h = p["hdr"]
-    for kw in ({"chroma": 2}, {"width": h["width"] + 4}, {"ctu": 8}, {"slots": 0}, {"slots": 65}, {"height": 0},
+    for kw in ({"chroma": 2}, {"width": h["width"] + 4}, {"ctu": 8}, {"slots": 0}, {"slots": 257}, {"height": 0},
                {"bd": 7}, {"bd": 12}):
         r, hd = _create(_seq(h, **kw), pp)
         assert r == E_UNSUPPORTED, kw
@@ -170,3 +170,25 @@ def test_context_calls_out_of_order_and_bad_arguments():
         ctx.sync()
     finally:
         ctx.close()
+
+
+def test_inter_jobs_address_every_dpb_slot():
+    """DPB slots up to VVCR_MAX_SLOTS (256) survive into the inter work lists: a picture whose references
+    sit in slots 128..255 plans jobs that read exactly those slots (a job's slot field once held 7 bits)."""
+    L = N.lib()
+    L.vvcr_debug_mc_slots.restype = C.c_int
+    L.vvcr_debug_mc_slots.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.c_int32]
+    pics = S.load_sequence(os.path.join(GOLD, "ra416_q32"), max_pics=4)
+    for p in pics[1:]:
+        h = p["hdr"]
+        refs = sorted({int(p["ref_poc"][l][r]) for l in range(2) for r in range(h["num_ref_l%d" % l])})
+        slot_of = {poc: 255 - 3 * k for k, poc in enumerate(refs)}
+        pic = S.plan_picture(p, 130, slot_of, dpb_slots=256)
+        try:
+            n = L.vvcr_debug_mc_slots(pic.h, None, 0)
+            assert n > 0
+            out = (C.c_int32 * n)()
+            assert L.vvcr_debug_mc_slots(pic.h, out, n) == n
+            assert set(out) <= set(slot_of.values()) and max(out) == 255
+        finally:
+            pic.close()

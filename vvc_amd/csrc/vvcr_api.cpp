@@ -302,6 +302,7 @@ struct vvcr_ctx {
   bool in_picture = false;
   vvcr_picture cur;                  // the picture of vvcr_begin_picture .. vvcr_end_picture / vvcr_prepare_picture
   DevVec<uint16_t> d_scans;
+  DevVec<const int16_t *> d_ref_table;   // DPB plane pointers [slot * 3 + comp] (RefPlanes)
   ScanTables scans;
   // prepared pictures: index 0 is the scratch record of vvcr_end_picture. The table is shared by the
   // threads calling vvcr_prepare_planned and the launching thread: `prepared_mu` guards it (a record
@@ -337,8 +338,7 @@ static int n_ctb(const vvcr_seq_params &sp) {
 
 static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lane) {
   McParams P{};
-  for (size_t s = 0; s < ctx->dpb.size() && s < (size_t)VVCR_MAX_SLOTS; s++)
-    for (int c = 0; c < 3; c++) P.ref.p[s][c] = ctx->dpb[s][c].p;
+  P.ref.p = ctx->d_ref_table.p;
   for (int c = 0; c < 3; c++) {
     P.ref.stride[c] = ctx->dpb[0][c].stride; P.ref.w[c] = ctx->dpb[0][c].w; P.ref.h[c] = ctx->dpb[0][c].h;
   }
@@ -778,6 +778,12 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       s[1] = alloc_plane(W / 2, H / 2);
       s[2] = alloc_plane(W / 2, H / 2);
     }
+    {
+      std::vector<const int16_t *> t;
+      for (auto &s : ctx->dpb)
+        for (int c = 0; c < 3; c++) t.push_back(s[c].p);
+      ctx->d_ref_table.upload(t);
+    }
     ctx->slot_w.assign(sp->dpb_slots, nullptr);
     ctx->slot_w_set.assign(sp->dpb_slots, 0);
     ctx->slot_r.assign(sp->dpb_slots, {});
@@ -1110,6 +1116,24 @@ int vvcr_picture_work_counts(const vvcr_picture *pic, int64_t *counts, int32_t n
                          (int64_t)pic->dbk.total(), (int64_t)pic->wl.n_dmvr, pic->wl.ref_y0, pic->wl.ref_y1};
   for (int k = 0; k < n && k < 10; k++) counts[k] = v[k];
   return 10;
+}
+
+// Diagnostics (host only): the DPB slots the planned inter work lists read, one entry per (job, list) in
+// job order (MC tiles and blocks, bi-directional blocks, affine PUs). Returns the number of entries.
+extern "C" int vvcr_debug_mc_slots(const vvcr_picture *pic, int32_t *out, int32_t cap) {
+  if (!pic || (!out && cap)) return VVCR_E_ARG;
+  if (!pic->planned) return VVCR_E_STATE;
+  int32_t n = 0;
+  auto put = [&](int v) { if (n < cap) out[n] = v; n++; };
+  for (const auto *v : {&pic->wl.mc_tile, &pic->wl.mc_basic, &pic->wl.mc_bidir})
+    for (const McJob &j : *v) {
+      if (j.flags & MC_L0) put(j.slot[0]);
+      if (j.flags & MC_L1) put(j.slot[1]);
+    }
+  for (const AffPu &u : pic->wl.aff_pu)
+    for (int l = 0; l < 2; l++)
+      if (u.l[l].present) put(u.l[l].slot);
+  return n;
 }
 
 const char *vvcr_picture_last_error(const vvcr_picture *pic) { return pic ? pic->err.c_str() : g_create_error.c_str(); }

@@ -68,8 +68,8 @@ McJob make_job(const vvcr_pic_params &pp, int interDir, int r0, int r1, int mv0x
   McJob j{};
   j.flags = MC_LUMA | MC_CHROMA;
   if (identical_motion(pp, interDir, r0, r1, mv0x, mv0y, mv1x, mv1y)) interDir = 1;
-  if (interDir & 1) { j.flags |= MC_L0; j.slot[0] = (int8_t)pp.ref_slot[0][r0]; j.mv[0][0] = (int16_t)mv0x; j.mv[0][1] = (int16_t)mv0y; }
-  if (interDir & 2) { j.flags |= MC_L1; j.slot[1] = (int8_t)pp.ref_slot[1][r1]; j.mv[1][0] = (int16_t)mv1x; j.mv[1][1] = (int16_t)mv1y; }
+  if (interDir & 1) { j.flags |= MC_L0; j.slot[0] = (uint8_t)pp.ref_slot[0][r0]; j.mv[0][0] = (int16_t)mv0x; j.mv[0][1] = (int16_t)mv0y; }
+  if (interDir & 2) { j.flags |= MC_L1; j.slot[1] = (uint8_t)pp.ref_slot[1][r1]; j.mv[1][0] = (int16_t)mv1x; j.mv[1][1] = (int16_t)mv1y; }
   if (altHpel) j.flags |= MC_ALT_HPEL;
   j.bcw = (int8_t)bcw;
   return j;
@@ -273,7 +273,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       for (int k = 0; k < 2; k++) {
         const int l = g.cand[k][1], r = g.cand[k][2];
         if (l < 0 || l > 1 || r < 0 || r >= pp.num_ref[l]) fail("GEO candidate reference");
-        j.slot[k] = (int8_t)pp.ref_slot[l][r];
+        j.slot[k] = (uint8_t)pp.ref_slot[l][r];
         j.mv[k][0] = (int16_t)g.cand[k][3];
         j.mv[k][1] = (int16_t)g.cand[k][4];
       }

@@ -49,7 +49,7 @@ struct McJob {
   uint8_t w, h;          // luma size (4..16)
   uint16_t flags;
   int16_t mv[2][2];      // [list][hor/ver], 1/16 luma sample
-  int8_t slot[2];        // DPB slot per list
+  uint8_t slot[2];       // DPB slot per list (VVCR_MAX_SLOTS <= 256)
   int8_t bcw;            // BcwIdx (2 = default average)
   uint8_t ridx;          // MC_WP: refIdx of list 0 | refIdx of list 1 << 4 (selects the weight table rows)
   int32_t aux;           // DMVR: index of this sub-block in the delta output buffer;
@@ -93,15 +93,17 @@ struct WpTable {
   int8_t d[2][VVCR_MAX_REF][3];
 };
 
-constexpr int VVCR_MAX_SLOTS = 64;   // DPB slots of a context (vvcr_seq_params::dpb_slots)
+constexpr int VVCR_MAX_SLOTS = 256;   // DPB slots of a context (vvcr_seq_params::dpb_slots)
+static_assert(VVCR_MAX_SLOTS <= 256, "McJob::slot is a uint8_t");
 
-// DPB planes by slot: one pointer per (slot, component); every slot of a component has the same geometry.
+// DPB planes by slot: a device table of one pointer per (slot, component), [slot * 3 + comp], built at
+// vvcr_create; every slot of a component has the same geometry.
 struct RefPlanes {
-  const int16_t *p[VVCR_MAX_SLOTS][3];
+  const int16_t *const *p;
   int32_t stride[3], w[3], h[3];
   __host__ __device__ DPlane get(int slot, int comp) const {
     DPlane d;
-    d.p = const_cast<int16_t *>(p[slot][comp]);
+    d.p = const_cast<int16_t *>(p[slot * 3 + comp]);
     d.stride = stride[comp]; d.w = w[comp]; d.h = h[comp];
     return d;
   }
