@@ -78,6 +78,7 @@ struct Planner {
 
   void build_maps() {
     const size_t n = (size_t)W4 * H4;
+    cqp.assign(2 * d.tu.size(), (int8_t)-128);
     for (int k = 0; k < 2; k++) {
       tu_map[k].assign(n, -1);
       if (d.cu_map[k].size() == n) { cu_map[k] = d.cu_map[k].data(); continue; }
@@ -208,8 +209,9 @@ struct Planner {
   // inter Q block and its P neighbour, on top of the transform part tmp
   int motion_bs(int dir, int lx, int ly, int tmp) const {
     const int lpx = dir == VER ? lx - 1 : lx, lpy = dir == VER ? ly : ly - 1;
-    const vvcr_motion &mq = d.motion[(size_t)(ly >> 2) * W4 + (lx >> 2)];
-    const vvcr_motion &mp = d.motion[(size_t)(lpy >> 2) * W4 + (lpx >> 2)];
+    return motion_bs_pair(d.motion[(size_t)(lpy >> 2) * W4 + (lpx >> 2)], d.motion[(size_t)(ly >> 2) * W4 + (lx >> 2)], tmp);
+  }
+  int motion_bs_pair(const vvcr_motion &mp, const vvcr_motion &mq, int tmp) const {
     const int th = 8;
     if (pp.slice_type == 0) {
       // Picture identity: entries of the lists with equal POC are the same decoded picture.
@@ -235,6 +237,13 @@ struct Planner {
     return (std::abs(mq.mv0x - mp.mv0x) >= th || std::abs(mq.mv0y - mp.mv0y) >= th) ? tmp + 1 : tmp;
   }
 
+  // chroma_qp per (TU, Cb / Cr), computed on first use (-128: not yet)
+  mutable bigbuf::vec<int8_t> cqp;
+  int chroma_qp_cached(int t, int comp) const {
+    int8_t &c = cqp[2 * (size_t)t + comp - 1];
+    if (c == -128) c = (int8_t)chroma_qp(t, comp);
+    return c;
+  }
   // QpParam(tu, comp).Qp(0) - qpBdOffset (Quant.cpp:65-138); joint Cb-Cr mode 3 uses the JOINT_CbCr tables
   int chroma_qp(int t, int comp) const {
     const int qpy = d.cu[d.tu[t].cu].qp;
@@ -303,7 +312,7 @@ struct Planner {
         const int tq = get_tu(px >> shQ, py >> shQ, cu.chtype);
         const int p1x = px >> shP, p1y = py >> shP;
         const int tp = get_tu(dir == VER ? p1x - 1 : p1x, dir == VER ? p1y : p1y - 1, cuP.chtype);
-        const int qp = (chroma_qp(tq, comp) + chroma_qp(tp, comp) + 1) >> 1;
+        const int qp = (chroma_qp_cached(tq, comp) + chroma_qp_cached(tp, comp) + 1) >> 1;
         w |= (uint32_t)bS[k] << (2 * k) | (uint32_t)((qp + 64) & 127) << (5 + 7 * k);
         any = true;
       }
@@ -370,12 +379,42 @@ struct Planner {
       else bs[dir][r] = (uint8_t)boundary_strength(cui, dir, a[0] + x, a[1] + y);
     };
     if (cu.yvalid) {   // edge flags are only ever set on the edge lines listed: visit those, not the whole CU
+      const bool ver = dir == VER;
+      const int rstep = ver ? parts : 1, n = (ver ? a[3] : a[2]) / 4;
+      const ptrdiff_t qstep = ver ? W4 : 1, pofs = ver ? -1 : -(ptrdiff_t)W4;
+      if (fast && ver) {   // interior vertical lines row by row: the motion records of a row are adjacent
+        int lines[64], nl = 0;
+        for (int k = 0; k < ne; k++)
+          if ((!k || edges[k] != edges[k - 1]) && edges[k] > 0 && edges[k] * 4 < a[2]) lines[nl++] = edges[k];
+        const vvcr_motion *row = d.motion.data() + (size_t)(a[1] >> 2) * W4 + (a[0] >> 2);
+        int r0 = raster(a[0], a[1]);
+        for (int i = 0; i < n; i++, row += W4, r0 += parts)
+          for (int t = 0; t < nl; t++) {
+            const int u = lines[t], r = r0 + u;
+            if (!edge[dir][r]) continue;
+            if (bs[dir][r] == 0) bs[dir][r] = (uint8_t)motion_bs_pair(row[u - 1], row[u], 0);
+            else bs[dir][r] = (uint8_t)boundary_strength(cui, dir, a[0] + 4 * u, a[1] + 4 * i);
+          }
+      }
       for (int k = 0; k < ne; k++) {
         if (k && edges[k] == edges[k - 1]) continue;
         const int o = edges[k] * 4;
-        if (o < 0 || o >= (dir == VER ? a[2] : a[3])) continue;
-        if (dir == VER) for (int y = 0; y < a[3]; y += 4) bs_at(o, y);
-        else for (int x = 0; x < a[2]; x += 4) bs_at(x, o);
+        if (o < 0 || o >= (ver ? a[2] : a[3])) continue;
+        if (fast && o > 0 && ver) continue;   // done above
+        if (fast && o > 0) {   // interior line of an inter CU: the motion part unless a transform edge marks it
+          const int x0 = ver ? a[0] + o : a[0], y0 = ver ? a[1] : a[1] + o;
+          const vvcr_motion *mq = d.motion.data() + (size_t)(y0 >> 2) * W4 + (x0 >> 2);
+          int r = raster(x0, y0);
+          for (int i = 0; i < n; i++, r += rstep, mq += qstep) {
+            if (!edge[dir][r]) continue;
+            if (bs[dir][r] == 0) bs[dir][r] = (uint8_t)motion_bs_pair(mq[pofs], *mq, 0);
+            else bs[dir][r] = (uint8_t)boundary_strength(cui, dir, ver ? x0 : x0 + 4 * i, ver ? y0 + 4 * i : y0);
+          }
+        } else if (ver) {
+          for (int y = 0; y < a[3]; y += 4) bs_at(o, y);
+        } else {
+          for (int x = 0; x < a[2]; x += 4) bs_at(x, o);
+        }
       }
     } else {
       for (int y = 0; y < a[3]; y += 4)
