@@ -43,7 +43,7 @@ ENCAPP_OBJ = $(call obj,$(ENCAPP_SRC))
 WRAPS = $(shell cat $(CURDIR)/oracle/capture/wraps.txt 2>/dev/null)
 WRAPFLAGS = $(foreach s,$(WRAPS),-Wl,--wrap=$(s))
 
-all: apps capture rdo_kat
+all: apps capture rdo_kat mc_kat
 
 # syntax-trace decoder (the reference's own ENABLE_TRACING / DTRACE build, TypeDef.h) for debugging the
 # host parser element by element: make -f oracle/ref.mk trace  ->  oracle/_ref/trace/DecoderApp
@@ -81,6 +81,13 @@ $(OUT)/obj/capture/rdo_kat.o: $(CURDIR)/oracle/capture/rdo_kat.cpp
 	@mkdir -p $(@D); $(CXX) $(CXXFLAGS) -c $< -o $@
 $(OUT)/rdo_kat: $(OUT)/obj/capture/rdo_kat.o $(OUT)/libCommonLib.a
 	$(CXX) -pthread -o $@ $(OUT)/obj/capture/rdo_kat.o $(OUT)/libCommonLib.a
+
+# MC known-answer harness (InterpolationFilter::filterHor / filterVer of the reference, oracle/capture/mc_kat.cpp)
+mc_kat: $(OUT)/mc_kat
+$(OUT)/obj/capture/mc_kat.o: $(CURDIR)/oracle/capture/mc_kat.cpp
+	@mkdir -p $(@D); $(CXX) $(CXXFLAGS) -c $< -o $@
+$(OUT)/mc_kat: $(OUT)/obj/capture/mc_kat.o $(OUT)/libCommonLib.a
+	$(CXX) -pthread -o $@ $(OUT)/obj/capture/mc_kat.o $(OUT)/libCommonLib.a
 
 $(OUT)/obj/Lib/CommonLib/x86/sse41/%.o: $(SRC)/Lib/CommonLib/x86/sse41/%.cpp
 	@mkdir -p $(@D); $(CXX) $(CXXFLAGS) -msse4.1 -DUSE_SSE41 -c $< -o $@
