@@ -161,18 +161,21 @@ struct Planner {
     x1 = std::min(x1, pw - 1); y1 = std::min(y1, ph - 1);
     int m = 0;
     if (x0 > x1 || y0 > y1) return 0;
-    const int cs = ch ? 1 : 0;
+    // a unit is 4x4 luma samples in both maps: its CTU is (u >> lg); the region is looked up per CTU
+    const int lg = sp.ctu_log2 - 2;
+    int lastc = -1;
+    bool regok = false;
     for (int uy = y0 >> s; uy <= (y1 >> s); uy++)
       for (int ux = x0 >> s; ux <= (x1 >> s); ux++) {
         const size_t i = (size_t)uy * W4 + ux;
         const int32_t cu = umap[ch][i];
-        if (cu < 0) continue;
-        const bool own = written[ch][cu];
-        if ((own ? out.order[ch][i] : cu_seq[cu]) < seq && region_at((ux << s) << cs, (uy << s) << cs) == cur_reg && own) {
-          m = std::max(m, level[ch][i]);
-          const int32_t pr = prod[comp][i];
-          if (pr >= 0) add_dep(pr);
-        }
+        if (cu < 0 || !written[ch][cu] || out.order[ch][i] >= seq) continue;
+        const int c = (uy >> lg) * wc + (ux >> lg);
+        if (c != lastc) { lastc = c; regok = ctu_reg[c] == cur_reg; }
+        if (!regok) continue;
+        m = std::max(m, level[ch][i]);
+        const int32_t pr = prod[comp][i];
+        if (pr >= 0) add_dep(pr);
       }
     return m;
   }
