@@ -12,6 +12,15 @@
 //
 // Usage: VVCR_CAPTURE_DIR=<dir> vtm_capture -b stream.bin [-o out.yuv]   (DecoderApp options)
 // Output: <dir>/pic_<decodeidx>.cap  — chunk format read by vvc_amd/capfile.py
+//
+// Built with -DVVCR_DROPIN (oracle/ref.mk: oracle/_ref/vtm_vvcr) the same source is the drop-in
+// demonstration of INTEGRATION.md: DecoderApp (DecApp/DecLib unchanged, linked against libvvcr.so) whose
+// decoded pictures come from libvvcr. At DecLib::executeLoopFilters (DecLib.cpp:560) the picture's
+// descriptors go to vvcr_begin_picture / vvcr_submit / vvcr_set_loop_filter_params / vvcr_end_picture;
+// the GPU's final picture (vvcr_read_picture) overwrites the reference's reconstruction before DecApp
+// writes it (DecApp::xWriteOutput) and before later pictures predict from it, and the GPU's DMVR
+// refinements (vvcr_get_dmvr_deltas) replace the reference's before CS::setRefinedMotionField
+// (DecLib.cpp:579), so later pictures' temporal candidates come from libvvcr too.
 
 #include <cstdio>
 #include <cstdlib>
@@ -55,8 +64,10 @@ namespace vtm_mip {
 // ---------------------------------------------------------------------------------------------
 // chunk writer
 // ---------------------------------------------------------------------------------------------
+struct Chunk { char dtype; std::vector<uint64_t> dims; std::vector<uint8_t> bytes; };
 struct CapFile {
   FILE *f = nullptr;
+  std::map<std::string, Chunk> *mem = nullptr;   // in-memory chunks instead of a file (drop-in mode)
   void open(const std::string &p) {
     f = fopen(p.c_str(), "wb");
     if (!f) { perror(p.c_str()); exit(3); }
@@ -65,6 +76,15 @@ struct CapFile {
   void close() { if (f) fclose(f); f = nullptr; }
   // dtype: 'b' int8, 'B' uint8, 'h' int16, 'H' uint16, 'i' int32, 'q' int64
   void put(const char *name, char dtype, std::vector<uint64_t> dims, const void *data, size_t elsz) {
+    if (mem) {
+      uint64_t n = 1;
+      for (auto d : dims) n *= d;
+      Chunk &c = (*mem)[name];
+      c.dtype = dtype;
+      c.dims = dims;
+      c.bytes.assign((const uint8_t *)data, (const uint8_t *)data + n * elsz);
+      return;
+    }
     char nm[24] = {0};
     strncpy(nm, name, 23);
     fwrite(nm, 1, 24, f);
@@ -616,6 +636,198 @@ static void dumpTables(const char *path) {
 static DecLib *g_dec = nullptr;
 static CapFile g_file;
 
+#ifdef VVCR_DROPIN
+// ---------------------------------------------------------------------------------------------
+// drop-in: the picture through libvvcr (include/vvcr.h), its result back into the reference's buffers
+// ---------------------------------------------------------------------------------------------
+#include "vvcr.h"
+static std::map<std::string, Chunk> g_mem;
+static vvcr_ctx *g_vvcr = nullptr;
+static const int kSlots = 24;
+static std::map<int, int> g_slotOfPoc;   // POC -> DPB slot of libvvcr (slot = decode index mod kSlots)
+static int g_mismatch = 0;                // pictures whose libvvcr result differs from the reference's own
+
+template <class T> static const T *chunk(const char *name, size_t *n = nullptr) {
+  auto it = g_mem.find(name);
+  if (it == g_mem.end()) { if (n) *n = 0; return nullptr; }
+  if (n) *n = it->second.bytes.size() / sizeof(T);
+  return (const T *)it->second.bytes.data();
+}
+static int64_t hdr(const char *key) {
+  size_t nk = 0, nv = 0;
+  const char *k = chunk<char>("hdr_keys", &nk);
+  const int64_t *v = chunk<int64_t>("hdr_vals", &nv);
+  std::string keys(k, nk), want(key);
+  size_t i = 0, pos = 0;
+  while (pos <= keys.size()) {
+    size_t e = keys.find(',', pos);
+    if (e == std::string::npos) e = keys.size();
+    if (keys.compare(pos, e - pos, want) == 0 && e - pos == want.size()) return v[i];
+    pos = e + 1;
+    i++;
+  }
+  fprintf(stderr, "vtm_vvcr: header field %s missing\n", key);
+  exit(4);
+}
+static void vcheck(int rc, const char *what) {
+  if (rc < 0) { fprintf(stderr, "vtm_vvcr: %s: %s\n", what, vvcr_last_error(g_vvcr)); exit(5); }
+}
+
+// vvcr_pic_params from the descriptors (the C++ form of vvc_amd/stream.py pic_params)
+static void picParams(vvcr_pic_params &pp, int slot) {
+  std::memset(&pp, 0, sizeof pp);
+  pp.poc = (int32_t)hdr("poc"); pp.slot = slot; pp.slice_type = (int32_t)hdr("slice_type"); pp.slice_qp = (int32_t)hdr("slice_qp");
+  const int32_t *rp = chunk<int32_t>("ref_poc"), *rl = chunk<int32_t>("ref_lt");
+  for (int l = 0; l < 2; l++) {
+    pp.num_ref[l] = (int32_t)hdr(l ? "num_ref_l1" : "num_ref_l0");
+    for (int r = 0; r < pp.num_ref[l]; r++) {
+      const int poc = rp[l * MAX_NUM_REF + r];
+      auto it = g_slotOfPoc.find(poc);
+      if (it == g_slotOfPoc.end()) { fprintf(stderr, "vtm_vvcr: POC %d: reference POC %d not in libvvcr's DPB\n", pp.poc, poc); exit(6); }
+      pp.ref_poc[l][r] = poc; pp.ref_slot[l][r] = it->second; pp.ref_lt[l][r] = rl[l * MAX_NUM_REF + r];
+    }
+  }
+#define F(k) pp.k = (int32_t)hdr(#k)
+  F(dual_tree); F(dep_quant); F(sign_hiding); F(joint_cbcr); F(bdof_enabled); F(dmvr_enabled); F(prof_enabled);
+  F(lfnst_enabled); F(mts_intra); F(mts_inter); F(sbt); F(wp_p); F(wp_b); F(dbk_disable); F(dbk_beta_offset_div2);
+  F(dbk_tc_offset_div2); F(lf_across_slices); F(lf_across_tiles); F(sao_luma); F(sao_chroma); F(alf_vb_luma);
+  F(alf_vb_chroma); F(lmcs_chroma_scale); F(lmcs_min_bin); F(lmcs_max_bin); F(log2_max_ts); F(use_mts);
+  F(implicit_mts); F(joint_cbcr_sign); F(entropy_sync);
+#undef F
+  pp.lmcs_enabled = hdr("lmcs_enabled") && hdr("lmcs_slice_flag");
+  int tb = 0;
+  while ((1 << (tb + 1)) <= hdr("max_tb_size")) tb++;
+  pp.max_tb_log2 = tb;
+  pp.chroma_qp_off[0] = (int32_t)hdr("chroma_qp_off_jc");
+  pp.chroma_qp_off[1] = (int32_t)hdr("chroma_qp_off_cb");
+  pp.chroma_qp_off[2] = (int32_t)hdr("chroma_qp_off_cr");
+  std::memcpy(pp.wp, chunk<int32_t>("wp"), sizeof pp.wp);
+  std::memcpy(pp.chroma_qp_map, chunk<int32_t>("chroma_qp_map"), sizeof pp.chroma_qp_map);
+  std::memcpy(pp.chroma_qp_map[0], chunk<int32_t>("chroma_qp_map_jc"), sizeof pp.chroma_qp_map[0]);   // row 0: joint Cb-Cr
+  for (int c = 0; c < 3; c++) pp.alf_en[c] = (int32_t)hdr(c == 0 ? "alf_slice_en0" : c == 1 ? "alf_slice_en1" : "alf_slice_en2");
+  pp.ccalf_en[0] = (int32_t)hdr("ccalf_en_cb"); pp.ccalf_en[1] = (int32_t)hdr("ccalf_en_cr");
+  size_t n;
+  const int16_t *t = chunk<int16_t>("lmcs_fwd", &n);
+  std::memcpy(pp.lmcs_fwd, t, std::min<size_t>(n, 1024) * 2);
+  t = chunk<int16_t>("lmcs_inv", &n);
+  std::memcpy(pp.lmcs_inv, t, std::min<size_t>(n, 1024) * 2);
+  t = chunk<int16_t>("lmcs_pivot", &n);
+  std::memcpy(pp.lmcs_pivot, t, std::min<size_t>(n, 17) * 2);
+  const int32_t *ca = chunk<int32_t>("lmcs_cadj", &n);
+  std::memcpy(pp.lmcs_cadj, ca, std::min<size_t>(n, 16) * 4);
+  size_t nc, nr;
+  const int32_t *cb = chunk<int32_t>("tile_col_bd", &nc), *rb = chunk<int32_t>("tile_row_bd", &nr);
+  pp.num_tile_cols = (int32_t)nc - 1; pp.num_tile_rows = (int32_t)nr - 1;
+  std::memcpy(pp.tile_col_bd, cb, nc * 4);
+  std::memcpy(pp.tile_row_bd, rb, nr * 4);
+}
+
+static void dropinPicture(CodingStructure &cs) {
+  const int W = (int)hdr("width"), H = (int)hdr("height");
+  if (!g_vvcr) {
+    vvcr_seq_params sp{W, H, 1, (int32_t)hdr("bitdepth_y"), (int32_t)hdr("ctu_log2"), kSlots, 0};
+    if (vvcr_create(&sp, &g_vvcr) < 0) { fprintf(stderr, "vtm_vvcr: vvcr_create failed\n"); exit(5); }
+  }
+  const int slot = g_picCounter % kSlots, poc = (int)hdr("poc");
+  for (auto it = g_slotOfPoc.begin(); it != g_slotOfPoc.end();)
+    it = it->second == slot ? g_slotOfPoc.erase(it) : std::next(it);
+  vvcr_pic_params pp;
+  picParams(pp, slot);
+  vcheck(vvcr_begin_picture(g_vvcr, &pp), "vvcr_begin_picture");
+  size_t ncu, npu, ntu, ncoef, nmo, ngeo;
+  const vvcr_cu *cu = chunk<vvcr_cu>("cu", &ncu);
+  const vvcr_pu *pu = chunk<vvcr_pu>("pu", &npu);
+  const vvcr_tu *tu = chunk<vvcr_tu>("tu", &ntu);
+  const int32_t *coef = chunk<int32_t>("coef", &ncoef);
+  const vvcr_motion *mo = chunk<vvcr_motion>("motion", &nmo);
+  const vvcr_geo *geo = chunk<vvcr_geo>("geo", &ngeo);
+  vcheck(vvcr_submit(g_vvcr, cu, (int32_t)ncu, pu, (int32_t)npu, tu, (int32_t)ntu, coef, (int64_t)ncoef, mo, geo, (int32_t)ngeo),
+         "vvcr_submit");
+  // SAO / ALF parameters (vvc_amd/stream.py set_loop_filter_params)
+  const vvcr_sao *sao = chunk<vvcr_sao>("sao");
+  vvcr_alf alf{}, *palf = nullptr;
+  std::vector<int16_t> coefL, clipL;
+  std::vector<uint8_t> ccCtl, alt;
+  if (hdr("alf_enabled") && g_mem.count("alf_ctb_en")) {
+    size_t naps, nfx, nca, nctb;
+    chunk<int32_t>("alf_aps_ids", &naps);
+    const int16_t *fx = chunk<int16_t>("alf_fixed", &nfx), *ca2 = chunk<int16_t>("alf_coef_aps", &nca);
+    const int16_t *cl = chunk<int16_t>("alf_clip_aps"), *cdef = chunk<int16_t>("alf_clip_default");
+    const int L = MAX_NUM_ALF_CLASSES * MAX_NUM_ALF_LUMA_COEFF;
+    coefL.assign(fx, fx + nfx);
+    coefL.insert(coefL.end(), ca2, ca2 + naps * L);
+    for (size_t k = 0; k < nfx / L; k++) clipL.insert(clipL.end(), cdef, cdef + L);
+    clipL.insert(clipL.end(), cl, cl + naps * L);
+    const uint8_t *cc = chunk<uint8_t>("ccalf_ctl", &nctb);
+    nctb /= 2;
+    ccCtl.assign(cc, cc + 2 * nctb);
+    for (size_t i = 0; i < nctb; i++) {
+      if (!hdr("ccalf_en_cb")) ccCtl[i] = 0;   // control words of a disabled component are not coded
+      if (!hdr("ccalf_en_cr")) ccCtl[nctb + i] = 0;
+    }
+    const uint8_t *a = chunk<uint8_t>("alf_ctb_alt");
+    alt.assign(a, a + 3 * nctb);
+    std::fill(alt.begin(), alt.begin() + nctb, 0);
+    alf.num_luma_sets = (int32_t)(nfx / L + naps);
+    alf.luma_coef = coefL.data(); alf.luma_clip = clipL.data();
+    alf.chroma_coef = chunk<int16_t>("alf_chroma_coef"); alf.chroma_clip = chunk<int16_t>("alf_chroma_clip");
+    alf.cc_coef = chunk<int16_t>("ccalf_coef"); alf.ctb_en = chunk<uint8_t>("alf_ctb_en"); alf.ctb_alt = alt.data();
+    alf.ctb_filter_set = chunk<int16_t>("alf_ctb_fidx"); alf.cc_ctl = ccCtl.data();
+    palf = &alf;
+  }
+  vcheck(vvcr_set_loop_filter_params(g_vvcr, sao, palf), "vvcr_set_loop_filter_params");
+  vcheck(vvcr_end_picture(g_vvcr), "vvcr_end_picture");
+  g_slotOfPoc[poc] = slot;
+  // the decoded picture: libvvcr's replaces the reference's (DecApp writes and later pictures read it)
+  PelUnitBuf reco = cs.picture->getRecoBuf();
+  std::vector<uint16_t> planes[3];
+  uint16_t *ptr[3];
+  int32_t stride[3];
+  for (int c = 0; c < 3; c++) {
+    planes[c].resize((size_t)reco.bufs[c].width * reco.bufs[c].height);
+    ptr[c] = planes[c].data();
+    stride[c] = (int32_t)reco.bufs[c].width;
+  }
+  vcheck(vvcr_read_picture(g_vvcr, slot, ptr, stride), "vvcr_read_picture");
+  bool same = true;
+  for (int c = 0; c < 3; c++) {
+    PelBuf &b = reco.bufs[c];
+    for (int y = 0; y < (int)b.height; y++) {
+      Pel *row = b.buf + (size_t)y * b.stride;
+      const uint16_t *src = planes[c].data() + (size_t)y * b.width;
+      for (int x = 0; x < (int)b.width; x++) {
+        same &= row[x] == (Pel)src[x];
+        row[x] = (Pel)src[x];
+      }
+    }
+  }
+  g_mismatch += !same;
+  // DMVR: libvvcr's refinements replace the reference's before CS::setRefinedMotionField
+  size_t nd;
+  chunk<int32_t>("dmvr_delta", &nd);
+  if (nd) {
+    std::vector<int32_t> d(nd);
+    const int got = vvcr_get_dmvr_deltas(g_vvcr, d.data(), (int64_t)nd / 2);
+    vcheck(got, "vvcr_get_dmvr_deltas");
+    enum { PU_DMVR_OFF = 45, PU_DMVR = 47 };
+    const int32_t *prow = chunk<int32_t>("pu");
+    for (size_t i = 0; i < cs.pus.size(); i++) {
+      const int32_t *o = prow + i * 48;
+      if (!o[PU_DMVR]) continue;
+      PredictionUnit &u = *cs.pus[i];
+      const int dy = std::min<int>(u.lumaSize().height, DMVR_SUBCU_HEIGHT), dx = std::min<int>(u.lumaSize().width, DMVR_SUBCU_WIDTH);
+      const int n = (u.lumaSize().height / dy) * (u.lumaSize().width / dx);
+      for (int k = 0; k < n; k++) {
+        const int64_t j = (int64_t)o[PU_DMVR_OFF] + k;
+        if (j >= got) { fprintf(stderr, "vtm_vvcr: DMVR deltas short\n"); exit(7); }
+        u.mvdL0SubPu[k].hor = d[2 * j];
+        u.mvdL0SubPu[k].ver = d[2 * j + 1];
+      }
+    }
+  }
+}
+#endif
+
 static void planeOut(const char *pfx, Plane *p) {
   for (int c = 0; c < 3; c++) {
     char nm[32];
@@ -648,9 +860,15 @@ void __wrap__ZN6DecLib18executeLoopFiltersEv(DecLib *self) {
   if (!tablesDumped && getenv("VVCR_DUMP_TABLES")) { dumpTables(getenv("VVCR_DUMP_TABLES")); tablesDumped = true; }
   if (!self->m_pcPic || g_dir.empty()) { __real__ZN6DecLib18executeLoopFiltersEv(self); return; }
   CodingStructure &cs = *self->m_pcPic->cs;
+#ifdef VVCR_DROPIN
+  g_mem.clear();
+  g_file.mem = &g_mem;
+  if (!g_cap.active) initPlanes(cs);   // an intra picture without inter CUs
+#else
   char path[512];
   snprintf(path, sizeof path, "%s/pic_%03d.cap", g_dir.c_str(), g_picCounter);
   g_file.open(path);
+#endif
   snapStage(ST_PRELF);
   dumpDescriptors(g_file, *self, cs);
   __real__ZN6DecLib18executeLoopFiltersEv(self);
@@ -659,7 +877,13 @@ void __wrap__ZN6DecLib18executeLoopFiltersEv(DecLib *self) {
   snapStage(ST_ALF);
   if (cs.sps->getALFEnabledFlag()) dumpAlf(g_file, *self, cs);
   TR("alf dumped");
+#ifdef VVCR_DROPIN
+  dropinPicture(cs);
+  g_cap.active = false;
+  g_picCounter++;
+#else
   finishCapture();
+#endif
 }
 
 // LoopFilter::loopFilterPic(CodingStructure&)
@@ -802,11 +1026,21 @@ void __wrap__ZN7AreaBufIsE9rspSignalERSt6vectorIsSaIsEE(PelBuf *self, std::vecto
 
 // ---------------------------------------------------------------------------------------------
 int main(int argc, char *argv[]) {
+#ifdef VVCR_DROPIN
+  g_dir = "<libvvcr>";   // every picture goes through the capture hooks (in memory) and libvvcr
+#else
   const char *d = getenv("VVCR_CAPTURE_DIR");
   g_dir = d ? d : "";
+#endif
   DecApp *app = new DecApp;
   if (!app->parseCfg(argc, argv)) { delete app; return 1; }
   uint32_t ret = app->decode();
   delete app;
+#ifdef VVCR_DROPIN
+  fprintf(stderr, "vtm_vvcr: %d pictures decoded through libvvcr, %d differ from the reference's own reconstruction\n",
+          g_picCounter, g_mismatch);
+  if (g_vvcr) vvcr_destroy(g_vvcr);
+  if (g_mismatch) return 2;
+#endif
   return ret != 0 ? 1 : 0;
 }

@@ -43,7 +43,7 @@ ENCAPP_OBJ = $(call obj,$(ENCAPP_SRC))
 WRAPS = $(shell cat $(CURDIR)/oracle/capture/wraps.txt 2>/dev/null)
 WRAPFLAGS = $(foreach s,$(WRAPS),-Wl,--wrap=$(s))
 
-all: apps capture rdo_kat mc_kat
+all: apps capture rdo_kat mc_kat $(if $(wildcard $(CURDIR)/vvc_amd/libvvcr.so),dropin)
 
 # syntax-trace decoder (the reference's own ENABLE_TRACING / DTRACE build, TypeDef.h) for debugging the
 # host parser element by element: make -f oracle/ref.mk trace  ->  oracle/_ref/trace/DecoderApp
@@ -75,6 +75,15 @@ CAPAPP_OBJ = $(call obj,$(SRC)/App/DecoderApp/DecApp.cpp $(SRC)/App/DecoderApp/D
 $(OUT)/vtm_capture: $(OUT)/obj/capture/vtm_capture.o $(CAPAPP_OBJ) $(DEC_OBJ) $(COMMON_OBJ) $(UTIL_OBJ) $(CURDIR)/oracle/capture/wraps.txt
 	$(CXX) -pthread -o $@ $(OUT)/obj/capture/vtm_capture.o $(CAPAPP_OBJ) $(DEC_OBJ) $(UTIL_OBJ) $(COMMON_OBJ) $(WRAPFLAGS)
 
+# drop-in demonstration: the same source built with -DVVCR_DROPIN — DecApp / DecLib of
+# the reference, unchanged, linked against libvvcr.so; every decoded picture comes from libvvcr
+dropin: $(OUT)/vtm_vvcr
+$(OUT)/obj/capture/vtm_vvcr.o: $(CAP_SRC) $(CURDIR)/oracle/capture/wraps.txt $(CURDIR)/include/vvcr.h
+	@mkdir -p $(@D); $(CXX) $(CXXFLAGS) -DVVCR_DROPIN -I$(CURDIR)/include -I$(SRC)/App/DecoderApp -c $< -o $@
+$(OUT)/vtm_vvcr: $(OUT)/obj/capture/vtm_vvcr.o $(CAPAPP_OBJ) $(DEC_OBJ) $(COMMON_OBJ) $(UTIL_OBJ) $(CURDIR)/vvc_amd/libvvcr.so
+	$(CXX) -pthread -o $@ $(OUT)/obj/capture/vtm_vvcr.o $(CAPAPP_OBJ) $(DEC_OBJ) $(UTIL_OBJ) $(COMMON_OBJ) $(WRAPFLAGS) \
+	  -L$(CURDIR)/vvc_amd -lvvcr -Wl,-rpath,'$$ORIGIN/../../vvc_amd' -Wl,-rpath-link,/opt/rocm/lib
+
 # RDO known-answer harness (RdCost distortion + forward transforms of the reference, oracle/capture/rdo_kat.cpp)
 rdo_kat: $(OUT)/rdo_kat
 $(OUT)/obj/capture/rdo_kat.o: $(CURDIR)/oracle/capture/rdo_kat.cpp
@@ -103,4 +112,4 @@ $(OUT)/obj/%.o: $(SRC)/%.cpp
 clean:
 	rm -rf $(OUT)
 
-.PHONY: all apps capture clean
+.PHONY: all apps capture dropin clean

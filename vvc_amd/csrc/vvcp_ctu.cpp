@@ -52,6 +52,7 @@ struct DiagGen {   // ScanGenerator, SCAN_DIAG
 
 struct Scans {
   std::vector<ScanPos> grouped[7][7], plain[7][7];
+  std::vector<uint16_t> groupedInv[7][7];   // raster index -> first grouped scan position holding it
   Scans() {
     for (int lw = 0; lw < 7; lw++)
       for (int lh = 0; lh < 7; lh++) {
@@ -76,6 +77,9 @@ struct Scans {
           }
           gg.next();
         }
+        std::vector<uint16_t> &inv = groupedInv[lw][lh];
+        inv.assign(w * h, (uint16_t)(w * h - 1));
+        for (int sp = w * h - 2; sp >= 0; sp--) inv[s[sp].idx] = (uint16_t)sp;
       }
   }
 };
@@ -97,6 +101,7 @@ struct CoefCtx {
   int ch, comp, w, h, log2w, log2CGw, log2CGh, log2CG, wg, hg, maxNumCoeff;
   bool signHiding, bdpcm;
   const ScanPos *scan, *scanCG;
+  const uint16_t *scanInv;
   int lastX, lastY, lastOffX = 0, lastOffY = 0, lastShX = 0, lastShY = 0;
   unsigned maxLastPosX, maxLastPosY;
   int scanPosLast = -1, subSetId = -1, subSetPos = -1, subSetPosX = -1, subSetPosY = -1, minSubPos = -1, maxSubPos = -1;
@@ -117,6 +122,7 @@ struct CoefCtx {
     hg = std::min(32, h) >> log2CGh;
     maxNumCoeff = w * h;
     scan = scans().grouped[lw][lh].data();
+    scanInv = scans().groupedInv[lw][lh].data();
     scanCG = scans().plain[floorLog2(wg)][floorLog2(hg)].data();
     lastX = ch ? LastX1 : LastX0;
     lastY = ch ? LastY1 : LastY0;
@@ -1672,11 +1678,7 @@ struct Parser {
       for (int i = cnt - 1; i >= 0; i--) tmp += cab.ep() << i;
       py = kMinInGroup[py] + tmp;
     }
-    const int blkPos = px + py * w;
-    int sp = 0;
-    for (; sp < cc.maxNumCoeff - 1; sp++)
-      if (blkPos == cc.scan[sp].idx) break;
-    return sp;
+    return cc.scanInv[px + py * w];   // the scan position of (px, py): first match, else the last position
   }
   void residual_coding_subblock(CoefCtx &cc, int32_t *coeff, int stateTab, int &state) {   // :3235
     const int minSubPos = cc.minSubPos;

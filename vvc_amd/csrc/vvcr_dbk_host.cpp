@@ -213,6 +213,10 @@ struct Planner {
   }
   int motion_bs_pair(const vvcr_motion &mp, const vvcr_motion &mq, int tmp) const {
     const int th = 8;
+    // the same motion on both sides (one PU, or equal neighbours): no motion boundary
+    if (mp.ref0 == mq.ref0 && mp.ref1 == mq.ref1 && mp.mv0x == mq.mv0x && mp.mv0y == mq.mv0y && mp.mv1x == mq.mv1x &&
+        mp.mv1y == mq.mv1y && (mp.ref0 >= 0 || pp.slice_type == 0))
+      return tmp;
     if (pp.slice_type == 0) {
       // Picture identity: entries of the lists with equal POC are the same decoded picture.
       const int NONE = INT32_MIN;
