@@ -1268,10 +1268,10 @@ void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb
   motionRows.alloc(field.size(), false);
   for (size_t i = 0; i < field.size(); i++) {
     const Mi &m = field[i];
-    vvcr_motion &o = motionRows.data()[i];
-    o.is_inter = m.isInter; o.inter_dir = m.interDir; o.ref0 = m.ref[0]; o.ref1 = m.ref[1];
+    MotionRec &o = motionRows.data()[i];
+    o.ref0 = (int8_t)m.ref[0]; o.ref1 = (int8_t)m.ref[1]; o.inter_dir = (uint8_t)m.interDir;
+    o.flags = (uint8_t)((m.isInter ? 1 : 0) | (m.altHpel ? 2 : 0) | (m.bcw << 2));
     o.mv0x = m.mv[0][0]; o.mv0y = m.mv[0][1]; o.mv1x = m.mv[1][0]; o.mv1y = m.mv[1][1];
-    o.bcw = m.bcw; o.alt_hpel = m.altHpel;
   }
 }
 

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "vvcp_ctu.h"
+#include "vvcr_host.h"   // MotionRec
 
 namespace vvcp {
 
@@ -34,7 +35,7 @@ struct SliceRefs {
 // the 4x4 motion field and the motion rows handed to the reconstruction path (vvcr_picture_submit's
 // `motion`): uninitialised arrays from the large-buffer cache whose passes write every entry
 template <class T> using RawArray = bigbuf::raw<T>;
-using MotionRows = RawArray<vvcr_motion>;
+using MotionRows = RawArray<MotionRec>;   // vvcr_host.h
 using MotionField = RawArray<Mi>;   // all-zero = CodingStructure::initStructData's memset
 
 // Motion of a decoded picture as later pictures' temporal candidates see it: the 4x4 field after

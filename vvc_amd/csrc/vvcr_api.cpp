@@ -882,7 +882,12 @@ static void pic_submit(vvcr_picture &b, const vvcr_cu *cu, int32_t ncu, const vv
   d.cu_map[0].clear();
   d.cu_map[1].clear();
   const size_t nm = (size_t)(b.sp.width / 4) * (b.sp.height / 4);
-  if (motion) d.motion.assign(motion, motion + nm); else d.motion.clear();
+  if (motion) {
+    d.motion.alloc(nm, false);
+    for (size_t i = 0; i < nm; i++) d.motion[i] = to_rec(motion[i]);
+  } else {
+    d.motion.clear();
+  }
   d.geo.assign(geo, geo + ngeo);
   b.planned = false;
   validate_descriptors(b.sp, b.pp, d);

@@ -211,11 +211,11 @@ struct Planner {
     const int lpx = dir == VER ? lx - 1 : lx, lpy = dir == VER ? ly : ly - 1;
     return motion_bs_pair(d.motion[(size_t)(lpy >> 2) * W4 + (lpx >> 2)], d.motion[(size_t)(ly >> 2) * W4 + (lx >> 2)], tmp);
   }
-  int motion_bs_pair(const vvcr_motion &mp, const vvcr_motion &mq, int tmp) const {
+  int motion_bs_pair(const MotionRec &mp, const MotionRec &mq, int tmp) const {
     const int th = 8;
     // the same motion on both sides (one PU, or equal neighbours): no motion boundary
-    if (mp.ref0 == mq.ref0 && mp.ref1 == mq.ref1 && mp.mv0x == mq.mv0x && mp.mv0y == mq.mv0y && mp.mv1x == mq.mv1x &&
-        mp.mv1y == mq.mv1y && (mp.ref0 >= 0 || pp.slice_type == 0))
+    if (*(const uint16_t *)&mp.ref0 == *(const uint16_t *)&mq.ref0 && std::memcmp(&mp.mv0x, &mq.mv0x, 16) == 0 &&
+        (mp.ref0 >= 0 || pp.slice_type == 0))
       return tmp;
     if (pp.slice_type == 0) {
       // Picture identity: entries of the lists with equal POC are the same decoded picture.
@@ -390,7 +390,7 @@ struct Planner {
         int lines[64], nl = 0;
         for (int k = 0; k < ne; k++)
           if ((!k || edges[k] != edges[k - 1]) && edges[k] > 0 && edges[k] * 4 < a[2]) lines[nl++] = edges[k];
-        const vvcr_motion *row = d.motion.data() + (size_t)(a[1] >> 2) * W4 + (a[0] >> 2);
+        const MotionRec *row = d.motion.data() + (size_t)(a[1] >> 2) * W4 + (a[0] >> 2);
         int r0 = raster(a[0], a[1]);
         for (int i = 0; i < n; i++, row += W4, r0 += parts)
           for (int t = 0; t < nl; t++) {
@@ -407,7 +407,7 @@ struct Planner {
         if (fast && o > 0 && ver) continue;   // done above
         if (fast && o > 0) {   // interior line of an inter CU: the motion part unless a transform edge marks it
           const int x0 = ver ? a[0] + o : a[0], y0 = ver ? a[1] : a[1] + o;
-          const vvcr_motion *mq = d.motion.data() + (size_t)(y0 >> 2) * W4 + (x0 >> 2);
+          const MotionRec *mq = d.motion.data() + (size_t)(y0 >> 2) * W4 + (x0 >> 2);
           int r = raster(x0, y0);
           for (int i = 0; i < n; i++, r += rstep, mq += qstep) {
             if (!edge[dir][r]) continue;

@@ -300,7 +300,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
         // (SbTMVP candidates of the sub-block merge list also carry cu.affine; the merge type decides)
         for (int y = 0; y < p.h; y += 8)
           for (int x = 0; x < p.w; x += 8) {
-            const vvcr_motion &m = d.motion[(size_t)((p.y + y) >> 2) * W4 + ((p.x + x) >> 2)];
+            const MotionRec &m = d.motion[(size_t)((p.y + y) >> 2) * W4 + ((p.x + x) >> 2)];
             McJob j = make_job(pp, m.inter_dir, m.ref0, m.ref1, m.mv0x, m.mv0y, m.mv1x, m.mv1y, bcw, alt);   // BCW of the CU (xWeightedAverage reads pu.cu->BcwIdx)
             set_wp(pp, j, m.ref0, m.ref1, c.bcw);
             push_mc(wl, p.x + x, p.y + y, std::min(8, p.w - x), std::min(8, p.h - y), j);

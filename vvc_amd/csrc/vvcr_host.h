@@ -4,12 +4,29 @@
 #include <vector>
 #include "vvcr_internal.h"
 
+// The 4x4 motion field as the host planners keep it (deblocking boundary strength, SbTMVP sub-block MC):
+// the fields of vvcr_motion in 20 bytes instead of 40 (it is read per 4x4 edge of every B picture, and a
+// 4K field is 518k entries). flags: is_inter | alt_hpel << 1 | bcw << 2.
+struct MotionRec {
+  int8_t ref0, ref1;
+  uint8_t inter_dir, flags;
+  int32_t mv0x, mv0y, mv1x, mv1y;
+};
+static_assert(sizeof(MotionRec) == 20, "MotionRec layout");
+inline MotionRec to_rec(const vvcr_motion &m) {
+  return {(int8_t)m.ref0, (int8_t)m.ref1, (uint8_t)m.inter_dir, (uint8_t)((m.is_inter ? 1 : 0) | (m.alt_hpel ? 2 : 0) | (m.bcw << 2)),
+          m.mv0x, m.mv0y, m.mv1x, m.mv1y};
+}
+inline vvcr_motion from_rec(const MotionRec &r) {
+  return {r.flags & 1, r.inter_dir, r.ref0, r.ref1, r.mv0x, r.mv0y, r.mv1x, r.mv1y, r.flags >> 2, (r.flags >> 1) & 1};
+}
+
 struct PictureDescriptors {
   bigbuf::vec<vvcr_cu> cu;
   bigbuf::vec<vvcr_pu> pu;
   bigbuf::vec<vvcr_tu> tu;
   bigbuf::vec<int32_t> coef;
-  bigbuf::raw<vvcr_motion> motion;
+  bigbuf::raw<MotionRec> motion;
   bigbuf::vec<vvcr_geo> geo;
   // optional: CU index per 4x4 luma unit of each channel (chroma: 2x2 chroma units), -1 where none;
   // the host parser hands its maps over, other producers leave them empty and the planners build them
