@@ -258,9 +258,18 @@ struct CoefCtx {
 // ------------------------------------------------------------------------------------------------
 struct Area { int x = 0, y = 0, w = 0, h = 0; bool cvalid = true; };
 
+// the sub-partitions of one split (at most four): inline, no heap allocation per split
+struct Parts {
+  Area a[4];
+  int n = 0;
+  void push_back(const Area &x) { a[n++] = x; }
+  size_t size() const { return (size_t)n; }
+  const Area &operator[](int i) const { return a[i]; }
+};
+
 struct Level {
   int split = CTU_LEVEL;
-  std::vector<Area> parts;
+  Parts parts;
   int idx = 0;
   bool checked = false, isImplicit = false;
   int implicitSplit = S_DONT;
@@ -448,8 +457,8 @@ struct Parser {
     return false;
   }
   // PartitionerImpl::getCUSubPartitions (UnitPartitioner.cpp:763)
-  static std::vector<Area> subParts(const Area &a, int split) {
-    std::vector<Area> r;
+  static Parts subParts(const Area &a, int split) {
+    Parts r;
     switch (split) {
       case S_QT:
         for (int i = 0; i < 4; i++) r.push_back({a.x + (i & 1) * (a.w >> 1), a.y + (i >> 1) * (a.h >> 1), a.w >> 1, a.h >> 1, true});
@@ -2136,6 +2145,10 @@ void PictureSyntax::reset(int W_, int H_, int ctuLog2_) {
   h4 = (H + 3) >> 2;
   cu.clear(); cux.clear(); pu.clear(); pux.clear(); tu.clear(); coef.clear(); box.clear();
   coef.reserve((size_t)W * H * 3 / 2 + 8192);   // at most every sample of the three planes
+  // rows: room for a densely coded intra picture (one CU per 64 luma samples), so that the vectors do not
+  // grow by reallocation (copying every row) while the CABAC pass appends; larger counts still grow
+  const size_t rows = (size_t)W * H / 64 + 1024;
+  cu.reserve(rows); cux.reserve(rows); pu.reserve(rows); pux.reserve(rows); tu.reserve(rows + rows / 2);
   for (int c = 0; c < 2; c++) map[c].assign((size_t)w4 * h4, -1);
   const size_t n = (size_t)wCtu * hCtu;
   sao.assign(n * 3, vvcr_sao());
