@@ -35,6 +35,8 @@ int main(int argc, char **argv) {
     sigaction(SIGPROF, &sa, nullptr);
   }
   const bool skipI = getenv("HOST_PROF_SKIP_I") != nullptr;   // sample B / P pictures only
+  const bool onlyI = getenv("HOST_PROF_ONLY_I") != nullptr;   // sample intra pictures only
+  const char *phase = getenv("HOST_PROF_PHASE");               // parse | derive | plan: sample that phase only
   auto sampling = [&](bool on) {
     if (!pcs) return;
     itimerval it = {{0, on ? 200 : 0}, {0, on ? 200 : 0}};
@@ -61,12 +63,16 @@ int main(int argc, char **argv) {
     for (int i = 0; i < n; i++) {
       int32_t ii[16];
       vvcp_picture_info(s, i, ii, 16);
-      sampling(!(skipI && ii[1] == 2));
+      const bool pick = !(skipI && ii[1] == 2) && !(onlyI && ii[1] != 2);
+      auto on = [&](const char *ph) { sampling(pick && (!phase || std::string(phase) == ph)); };
+      on("parse");
       auto t0 = clk::now();
       if (vvcp_parse_picture(s, i)) { fprintf(stderr, "%s\n", vvcp_last_error()); return 1; }
       auto t1 = clk::now();
+      on("derive");
       if (vvcp_derive_motion(s, i) || vvcp_refine_motion(s, i, zeros.data(), (int64_t)zeros.size() / 2)) { fprintf(stderr, "%d: %s\n", i, vvcp_last_error()); return 1; }
       auto t2 = clk::now();
+      on("plan");
       vvcr_pic_params pp;
       vvcp_picture_params(s, i, &pp);
       int32_t rs[2 * VVCR_MAX_REF] = {0};
