@@ -6,7 +6,9 @@ NAL unit - header parsing, the CABAC pass of every picture (host threads), motio
 order with each collocated picture's DMVR deltas read back from the GPU, host planning (work lists,
 intra dependency plan, deblocking edges), upload (vvcr_prepare_planned) and the GPU (residuals, motion
 compensation with DMVR/BDOF/affine-PROF/GEO/CIIP, intra, deblocking, SAO, ALF/CC-ALF) - all inside the
-timed region, `--segments` independent decodes in flight (vvc_amd/bitstream.py).
+timed region. One step = `--segments` independent decodes of the whole stream, all in flight at once (a
+serving process decoding that many streams; vvc_amd/bitstream.py), so `steps` x `segments` decodes are timed
+and the rate is a steady state, not the latency of the first intra pictures.
 The `resident` object is the same reconstruction with every picture already planned and resident in
 HBM (launch only): the GPU-side rate. Output is checked bit-exact against DecoderApp: the YUV file MD5
 of one decode, and the plane MD5s of every segment's pictures after the timed steps.
@@ -213,9 +215,9 @@ class BitstreamE2E:
             self._decode(c)
 
     def run(self, steps):
-        """Decodes the stream `steps` times; returns when every picture is launched (not finished)."""
-        per_seg = [steps // self.segments + (1 if c < steps % self.segments else 0) for c in range(self.segments)]
-        futs = [self.seg_ex.submit(self._segment, c, n) for c, n in enumerate(per_seg) if n]
+        """`steps` steps: every segment decodes the stream `steps` times (one step = `segments` decodes of the
+        whole stream, all in flight); returns when every picture is launched (not finished)."""
+        futs = [self.seg_ex.submit(self._segment, c, steps) for c in range(self.segments)]
         for f in futs:
             f.result()
 
@@ -260,7 +262,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--stream", default=_default_stream())
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--segments", type=int, default=12, help="DPB copies of the sequence the steps cycle through (<= 32)")
+    ap.add_argument("--segments", type=int, default=12,
+                    help="independent decodes in flight; one step = each of them decodes the whole stream once (<= 32)")
     ap.add_argument("--resident-steps", type=int, default=20, help="timed steps of the resident (pre-planned) pass, 0 = skip")
     ap.add_argument("--sync-pictures", action="store_true",
                     help="host sync after every picture of the resident pass (profiling: kernel durations without overlap)")
@@ -418,7 +421,7 @@ def main():
     ms_step = elapsed / a.steps * 1e3
     kind, qp = a.stream.split("_")[0], a.stream.split("_")[-1]
     desc = "%s %s" % ("random access" if kind.startswith("ra") else "all intra", qp.replace("q", "QP"))
-    value = V.job_throughput(px_seq * a.steps, elapsed, R) / 1e6
+    value = V.job_throughput(px_seq * a.segments * a.steps, elapsed, R) / 1e6
     line = {
         "metric": "decode Mpixels/sec (CABAC on host), bit-exact YUV vs DecoderApp, 1/2/4/8 GPU",
         "value": round(value, 2),
@@ -432,14 +435,14 @@ def main():
         "vs_baseline": None,
         "dtype": "int16",
         "data": "synthetic (VTM-7.3-encoded synthetic %dx%d %s stream)" % (W, H, desc),
-        "config": {"workload": "%s: %dx%d %s, %d pictures (%d intra) per step, reconstruction + DBK/SAO/ALF" % (
-                       a.stream, W, H, desc, len(infos), nI),
+        "config": {"workload": "%s: %dx%d %s, %d pictures (%d intra) per decode, %d decodes per step, reconstruction + "
+                                   "DBK/SAO/ALF" % (a.stream, W, H, desc, len(infos), nI, a.segments),
                    "parallelism": "replicas%d" % world, "segments": a.segments, "lanes": lanes_cfg,
                    "host_threads": a.e2e_threads, "bitexact_vs_reference": bool(bitexact)},
         "value_scope": "end to end from the bitstream: NAL/header parsing, CABAC (host threads), motion derivation "
                        "with the GPU's DMVR feedback, host planning, upload, GPU reconstruction and loop filters, every "
-                       "picture of every step; %d independent decodes in flight" % a.segments,
-        "host_ms_per_picture": {k: round(v / (a.steps * len(infos)) * 1e3, 3) for k, v in e2e.times.items()},
+                       "picture of every step; a step = %d independent decodes of the stream, all in flight" % a.segments,
+        "host_ms_per_picture": {k: round(v / (a.steps * a.segments * len(infos)) * 1e3, 3) for k, v in e2e.times.items()},
         "roofline": roof,
         "cpu_baseline": None,
         "resident": resident,
