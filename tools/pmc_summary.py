@@ -1,7 +1,9 @@
 """Per-kernel HBM traffic from the rocprofv3 PMC passes of tools/pmc.sh, per launch, corrected as
 MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950
-FETCH_SIZE reports half the bytes of wide (16 B/lane) streaming reads, so it is doubled (our kernels mix
-access widths: the doubled figure is an upper estimate of the read bytes, the raw one a lower one).
+FETCH_SIZE reports half the bytes read, so it is doubled. The guide establishes the factor for 16 B/lane
+streaming reads; tools/probe/fetch_cal.hip measured it for every width the kernels use (2, 4, 8 and 16 B
+per lane, and 8-byte chunks of 2-D windows as the MC gathers read them): exactly 0.500 in each case
+(profiles/r03_fetch_calibration.txt), so the doubled figure is the read traffic, not an upper bound.
 
   python tools/pmc_summary.py gpurun_out/pmc_r01 [stream] > profiles/r01_traffic.json
 """
