@@ -51,7 +51,8 @@ def _spawn_ranks():
 
 def _default_stream():
     root = os.path.dirname(os.path.abspath(__file__))
-    for n in ("ra2160l_q27", "ra2160_q27"):   # 17-picture GOP-16 stream once captured, else the 3-picture one
+    # the longest 4K RA QP27 stream captured: 17 pictures (I + GOP 16), 9 (I + 8), else the 3-picture one
+    for n in ("ra2160l_q27", "ra2160n_q27", "ra2160_q27"):
         if os.path.isdir(os.path.join(root, "tests", "golden", n)):
             return n
     return "ra2160_q27"

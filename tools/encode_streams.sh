@@ -2,7 +2,7 @@
 # Re-creates the committed test bitstreams with the REFERENCE encoder built by oracle/ref.mk
 # (VTM 7.3 EncoderApp, CTC configs from /root/reference/cfg). Test-infrastructure only; runs in the
 # build container (needs /root/reference). Every stream carries MD5 decoded-picture-hash SEI.
-#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 ra2160n_q27 ra2160f_q27 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32
+#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 ra2160n_q27 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32
 set -e
 R=/root/reference/cfg; E=${E:-$(dirname $0)/../oracle/_ref/EncoderApp}; T=${T:-/tmp/enc}; O=${O:-$(dirname $0)/../tests/golden/streams}
 mkdir -p $T $O
@@ -48,9 +48,6 @@ for n in "$@"; do case $n in
   ra2160l_q27) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 17 27 $T/syn2160l.yuv $FAST ;;
   ra2160l_q32) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 17 32 $T/syn2160l.yuv $FAST ;;
   ra2160n_q27) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 9 27 $T/syn2160l.yuv $FAST ;;
-  # the same 9 pictures with the multi-type-tree split search off and a 16-sample search range (quad-tree
-  # CUs only; ~25 min per 4K B picture with the settings above, on this container's core)
-  ra2160f_q27) [ -f $T/syn2160l.yuv ] || $G 3840 2160 17 $T/syn2160l.yuv; enc $n encoder_randomaccess_vtm.cfg 3840 2160 9 27 $T/syn2160l.yuv $FAST --SearchRange=16 --MaxMTTHierarchyDepth=0 --MaxMTTHierarchyDepthISliceL=0 --MaxMTTHierarchyDepthISliceC=0 ;;
   # a second independently moving layer cut by polygon edges: GEO (InterPrediction.cpp:1749) and CIIP
   # (IntraPrediction.cpp:681,735) CUs in quantity
   rageo480_q32) [ -f $T/syn480g.yuv ] || $G 832 480 17 $T/syn480g.yuv 0.002 0 0 layers; enc $n encoder_randomaccess_vtm.cfg 832 480 17 32 $T/syn480g.yuv ;;
