@@ -7,6 +7,16 @@
 #include <vector>
 #include "../../include/vvcr.h"
 
+// XCD-aware work order (MI355X_MICROARCH.md, workgroup dispatch): the dispatcher deals workgroups
+// round-robin over the 8 XCDs, each with its own L2, so consecutive work items (neighbouring tiles, whose
+// reference windows and halos overlap) would be fetched into eight different L2s. xcd_swizzle maps block b
+// of a G-block grid to work item t so that the blocks one XCD receives (b, b + 8, b + 16, ...) take one
+// contiguous run of items; a bijection of [0, G) for any G.
+__device__ __forceinline__ int xcd_swizzle(int b, int G) {
+  const int per = G >> 3, rem = G & 7, x = b & 7, i = b >> 3;
+  return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
+}
+
 #define VVCR_CHECK_HIP(expr)                                                        \
   do {                                                                              \
     hipError_t _e = (expr);                                                         \
