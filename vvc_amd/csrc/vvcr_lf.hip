@@ -285,32 +285,35 @@ __device__ __forceinline__ void alf_luma(const AlfParams &P, int tx, int ty) {
 #undef T
 }
 
-// One lane per chroma sample. Every sample load (the 5x5 diamond, and the CC-ALF luma taps when the
-// picture uses CC-ALF) is issued before the CTB controls are known, so that the lane waits for one
-// memory round trip plus the coefficient lookups, not a chain of them.
-__device__ __forceinline__ void alf_chroma(const AlfParams &P, int comp, int x, int y) {
-  const DPlane &S = P.src[comp];
-  const DPlane &D = P.dst[comp];
+// One lane per chroma position, Cb and Cr together: the CC-ALF luma taps (the same for both components)
+// are loaded once. Every sample load (the two 5x5 diamonds and the luma taps) is issued before the CTB
+// controls are known, so that the lane waits for one memory round trip plus the coefficient lookups, not a
+// chain of them.
+__device__ __forceinline__ void alf_chroma(const AlfParams &P, int x, int y) {
   const DPlane &Y = P.src[0];
-  if (x >= S.w || y >= S.h || y >= (P.y1 >> 1)) return;
+  if (x >= P.src[1].w || y >= P.src[1].h || y >= (P.y1 >> 1)) return;
   const int cl2 = P.ctu_log2 - 1;
   const int ctb = (y >> cl2) * P.wc + (x >> cl2);
   const int n = P.nctb;
   const int maxv = (1 << P.bd) - 1;
-  const bool alfPic = P.en[comp] != 0, ccPic = P.en[2 + comp] != 0;
-  const int cur = S.p[(size_t)y * S.stride + x];
   const int vbH = 1 << cl2, vbPos = P.vb_chroma;
   int r1, r2, r3, r4, r5, r6;
   alf_rows(y, vbH, vbPos, false, r1, r2, r3, r4, r5, r6);
   (void)r5; (void)r6;
-  int sa[12] = {};
-  if (alfPic) {
-    sa[0] = at(S, x, r3); sa[1] = at(S, x, r4);
-    sa[2] = at(S, x + 1, r1); sa[3] = at(S, x - 1, r2);
-    sa[4] = at(S, x, r1); sa[5] = at(S, x, r2);
-    sa[6] = at(S, x - 1, r1); sa[7] = at(S, x + 1, r2);
-    sa[8] = at(S, x + 2, y); sa[9] = at(S, x - 2, y);
-    sa[10] = at(S, x + 1, y); sa[11] = at(S, x - 1, y);
+  int cur[2], sa[2][12] = {};
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    const DPlane &S = P.src[1 + k];
+    cur[k] = S.p[(size_t)y * S.stride + x];
+    if (P.en[1 + k]) {
+      int *q = sa[k];
+      q[0] = at(S, x, r3); q[1] = at(S, x, r4);
+      q[2] = at(S, x + 1, r1); q[3] = at(S, x - 1, r2);
+      q[4] = at(S, x, r1); q[5] = at(S, x, r2);
+      q[6] = at(S, x - 1, r1); q[7] = at(S, x + 1, r2);
+      q[8] = at(S, x + 2, y); q[9] = at(S, x - 2, y);
+      q[10] = at(S, x + 1, y); q[11] = at(S, x - 1, y);
+    }
   }
   const int lx = x * 2, ly = y * 2;
   const int pos = ly & ((1 << P.ctu_log2) - 1);
@@ -318,51 +321,56 @@ __device__ __forceinline__ void alf_chroma(const AlfParams &P, int comp, int x, 
   if (pos == P.vb_luma - 2 || pos == P.vb_luma + 1) o3 = o1;
   else if (pos == P.vb_luma - 1 || pos == P.vb_luma) { o1 = 0; o2 = 0; o3 = 0; }
   int sl[8] = {};
-  if (ccPic) {
+  if (P.en[3] || P.en[4]) {
     sl[0] = at(Y, lx, ly);
     sl[1] = at(Y, lx, ly + o2); sl[2] = at(Y, lx - 1, ly); sl[3] = at(Y, lx + 1, ly);
     sl[4] = at(Y, lx - 1, ly + o1); sl[5] = at(Y, lx, ly + o1); sl[6] = at(Y, lx + 1, ly + o1);
     sl[7] = at(Y, lx, ly + o3);
   }
-  const bool on = alfPic && P.ctb_en[comp * n + ctb];
-  const int alt = P.ctb_alt[comp * n + ctb];
-  const int ccf = ccPic ? P.cc_ctl[(comp - 1) * n + ctb] : 0;
-  int v = cur;
-  if (on) {
-    const int16_t *fc = P.chroma_coef + alt * 7, *fl = P.chroma_clip + alt * 7;
-    int sum = 0;
+  const int yVb = y & (vbH - 1);
+  const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
 #pragma unroll
-    for (int k = 0; k < 6; k++) sum += fc[k] * clip_alf(fl[k], cur, sa[2 * k], sa[2 * k + 1]);
-    const int yVb = y & (vbH - 1);
-    const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
-    sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
-    v = clip3(0, maxv, sum + cur);
-  }
-  if (ccf) {
-    const int16_t *f = P.cc_coef + ((comp - 1) * 4 + ccf - 1) * 8;
-    const int c0 = sl[0];
-    int sum = 0;
+  for (int k = 0; k < 2; k++) {
+    const int comp = 1 + k;
+    const bool on = P.en[comp] && P.ctb_en[comp * n + ctb];
+    const int alt = P.ctb_alt[comp * n + ctb];
+    const int ccf = P.en[2 + comp] ? P.cc_ctl[k * n + ctb] : 0;
+    int v = cur[k];
+    if (on) {
+      const int16_t *fc = P.chroma_coef + alt * 7, *fl = P.chroma_clip + alt * 7;
+      int sum = 0;
 #pragma unroll
-    for (int k = 0; k < 7; k++) sum += f[k] * (sl[1 + k] - c0);
-    sum = (sum + 64) >> 7;
-    const int off = (1 << P.bd) >> 1;
-    sum = clip3(0, maxv, sum + off) - off;
-    v = clip3(0, maxv, sum + v);
+      for (int t = 0; t < 6; t++) sum += fc[t] * clip_alf(fl[t], cur[k], sa[k][2 * t], sa[k][2 * t + 1]);
+      sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
+      v = clip3(0, maxv, sum + cur[k]);
+    }
+    if (ccf) {
+      const int16_t *f = P.cc_coef + (k * 4 + ccf - 1) * 8;
+      const int c0 = sl[0];
+      int sum = 0;
+#pragma unroll
+      for (int t = 0; t < 7; t++) sum += f[t] * (sl[1 + t] - c0);
+      sum = (sum + 64) >> 7;
+      const int off = (1 << P.bd) >> 1;
+      sum = clip3(0, maxv, sum + off) - off;
+      v = clip3(0, maxv, sum + v);
+    }
+    const DPlane &D = P.dst[comp];
+    D.p[(size_t)y * D.stride + x] = (int16_t)v;
   }
-  D.p[(size_t)y * D.stride + x] = (int16_t)v;
 }
 
 // Luma and chroma ALF in one launch: the first gx * gy workgroups are luma tiles, the others take 64
-// chroma columns x 4 rows (a wave per row) of Cb, then Cr.
+// chroma columns x 4 rows (a wave per row) of Cb and Cr together.
 __global__ __launch_bounds__(256) void k_alf(AlfParams P, int gx, int gy, int gcx, int gcy) {
   const int b = blockIdx.x;
   if (b < gx * gy) {
     alf_luma(P, b % gx, b / gx);
     return;
   }
-  const int c = b - gx * gy, per = gcx * gcy, comp = 1 + c / per, r = c % per;
+  const int r = b - gx * gy;
   const int x = (r % gcx) * 64 + (threadIdx.x & 63), y = (P.y0 >> 1) + (r / gcx) * 4 + (threadIdx.x >> 6);
-  alf_chroma(P, comp, x, y);
+  alf_chroma(P, x, y);
 }
 
 }  // namespace
@@ -397,5 +405,5 @@ void launch_alf(const AlfParams &p, hipStream_t s) {
   if (p.y1 <= p.y0) return;
   const int gx = (p.src[0].w + ALF_TW - 1) / ALF_TW, gy = (p.y1 - p.y0 + ALF_TH - 1) / ALF_TH;
   const int gcx = (p.src[1].w + 63) / 64, gcy = (((p.y1 - p.y0) >> 1) + 3) / 4;
-  hipLaunchKernelGGL(k_alf, dim3(gx * gy + 2 * gcx * gcy), dim3(256), 0, s, p, gx, gy, gcx, gcy);
+  hipLaunchKernelGGL(k_alf, dim3(gx * gy + gcx * gcy), dim3(256), 0, s, p, gx, gy, gcx, gcy);
 }
