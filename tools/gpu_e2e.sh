@@ -7,6 +7,6 @@ TAG=$1; shift
 mkdir -p gpurun_out
 for sn in "$@"; do
   s=${sn%%:*}; n=${sn##*:}
-  timeout -k 10 300 python -u bench.py --stream $s --steps ${STEPS:-48} --warmup 4 --segments $n --resident-steps 0 --no-cpu \
+  timeout -k 10 300 python -u bench.py --stream $s --steps ${STEPS:-10} --warmup ${WARMUP:-2} --segments $n --resident-steps 0 --no-cpu \
     --shard-steps 0 > gpurun_out/e2e_${TAG}_${s}_s$n.json 2> gpurun_out/e2e_${TAG}_${s}_s$n.err || exit 1
 done
