@@ -263,8 +263,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--stream", default=_default_stream())
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--segments", type=int, default=12,
-                    help="independent decodes in flight; one step = each of them decodes the whole stream once (<= 32)")
+    ap.add_argument("--segments", type=int, default=0,
+                    help="independent decodes in flight; one step = each of them decodes the whole stream once (<= 32). "
+                         "Default: 16 at 4K and above, 12 below (4K 9-picture stream, end to end: 12 / 16 / 20 in flight "
+                         "2545 / 2763 / 2572 Mpx/s; 1080p 33 pictures: 12 / 16 2372 / 2122)")
     ap.add_argument("--resident-steps", type=int, default=20, help="timed steps of the resident (pre-planned) pass, 0 = skip")
     ap.add_argument("--sync-pictures", action="store_true",
                     help="host sync after every picture of the resident pass (profiling: kernel durations without overlap)")
@@ -289,6 +291,8 @@ def main():
     infos = [ps.info(i) for i in range(len(ps))]
     ps.close()
     W, H = infos[0]["width"], infos[0]["height"]
+    if a.segments <= 0:
+        a.segments = 16 if W * H >= 3840 * 2160 else 12
     px_seq = W * H * len(infos)
     nI = sum(1 for inf in infos if inf["slice_type"] == 2)
 
