@@ -104,21 +104,23 @@ PEAK_HBM_GBS = 8000.0   # MI355X HBM3E peak (guides/MI355X_MICROARCH.md)
 
 def cpu_baseline(stream_bin, pixels_per_run, min_seconds=10.0, max_runs=40):
     """VTM DecoderApp (the reference, built here from /root/reference by oracle/ref.mk) on the same
-    bitstream, single-threaded, no output file; repeated until ~min_seconds of CPU work."""
+    bitstream, single-threaded, no output file and no decoded-picture-hash check (-dph 0, as BASELINE.md
+    §2 times it: SEIDecodedPictureHash defaults to on, DecAppCfg.cpp:91, ~11 % of VTM's time); repeated
+    until ~min_seconds of CPU work."""
     exe = os.path.join(ROOT, "oracle", "_ref", "DecoderApp")
     if not os.path.exists(exe):
         return None
     runs, total = 0, 0.0
     while total < min_seconds and runs < max_runs:
         t0 = time.perf_counter()
-        r = subprocess.run([exe, "-b", stream_bin], capture_output=True, text=True)
+        r = subprocess.run([exe, "-b", stream_bin, "-dph", "0"], capture_output=True, text=True)
         dt = time.perf_counter() - t0
         if r.returncode != 0:
             return None
         runs += 1
         total += dt
     return {"value": round(pixels_per_run * runs / total / 1e6, 3), "unit": "Mpixels/s", "cores": 1, "kind": "reference",
-            "sample": "VTM-7.3 DecoderApp (x86 SIMD, 1 thread) decoding %s.bin %d times (%.1f s), parse + reconstruction"
+            "sample": "VTM-7.3 DecoderApp -b %s.bin -dph 0 (x86 SIMD, 1 thread, no output file, no hash check), %d runs (%.1f s), parse + reconstruction"
                       % (os.path.basename(stream_bin)[:-4], runs, total)}
 
 

@@ -165,6 +165,10 @@ typedef struct vvcr_alf {
 
 int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out);
 int vvcr_destroy(vvcr_ctx *ctx);
+/* Message of the last failing call MADE BY THE CALLING THREAD (like errno): with ctx the last failing
+ * context call of this thread, whatever context it was on; with NULL the last failing vvcr_create of this
+ * thread. Several threads may prepare pictures of one context at once, so the text is never shared
+ * between threads; read it on the thread that saw the error code. */
 const char *vvcr_last_error(vvcr_ctx *ctx);
 
 int vvcr_begin_picture(vvcr_ctx *ctx, const vvcr_pic_params *pp);

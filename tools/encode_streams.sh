@@ -2,7 +2,7 @@
 # Re-creates the committed test bitstreams with the REFERENCE encoder built by oracle/ref.mk
 # (VTM 7.3 EncoderApp, CTC configs from /root/reference/cfg). Test-infrastructure only; runs in the
 # build container (needs /root/reference). Every stream carries MD5 decoded-picture-hash SEI.
-#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 ra2160n_q27 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32
+#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 ra2160n_q27 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32 ralmgeo416_q32
 set -e
 R=/root/reference/cfg; E=${E:-$(dirname $0)/../oracle/_ref/EncoderApp}; T=${T:-/tmp/enc}; O=${O:-$(dirname $0)/../tests/golden/streams}
 mkdir -p $T $O
@@ -55,6 +55,9 @@ for n in "$@"; do case $n in
   aibdpcm416_q32) [ -f $T/syn416s.yuv ] || $G 416 240 17 $T/syn416s.yuv 0 0 0 screen; enc $n encoder_intra_vtm.cfg 416 240 8 32 $T/syn416s.yuv --TemporalSubsampleRatio=1 --BDPCM=1 ;;
   # scalar dequantisation on every block (Quant.cpp:369), sign data hiding, explicit MTS for inter too
   radq0416_q32) [ -f $T/syn416g.yuv ] || $G 416 240 17 $T/syn416g.yuv 0.002 0 0 layers; enc $n encoder_randomaccess_vtm.cfg 416 240 17 32 $T/syn416g.yuv --DepQuant=0 --SignHideFlag=1 --MTS=3 ;;
+  # the layered GEO / CIIP content in video range, so LMCS stays on: CIIP CUs in LMCS inter slices (the
+  # forward-mapped inter prediction blended with the intra one, IntraPrediction.cpp:681, DecCu.cpp:719)
+  ralmgeo416_q32) [ -f $T/syn416gv.yuv ] || $G 416 240 17 $T/syn416gv.yuv 0.002 1 0 layers; enc $n encoder_randomaccess_vtm.cfg 416 240 17 32 $T/syn416gv.yuv ;;
   # explicit weighted prediction at 1080p (WeightPrediction.cpp:382,413)
   rawp1080_q32) [ -f $T/syn1080f.yuv ] || $G 1920 1080 9 $T/syn1080f.yuv 0.002 0 0.03; enc $n encoder_randomaccess_vtm.cfg 1920 1080 9 32 $T/syn1080f.yuv --SearchRange=64 --WeightedPredP=1 --WeightedPredB=1 ;;
   *) echo "unknown stream $n"; exit 1 ;;

@@ -5,13 +5,13 @@
 // (include/vvcp.h: the host parser in place of DecLib's parsing, libvvcr in place of its reconstruction
 // and loop filters), writing the output pictures (POC order per coded video sequence, xWriteOutput
 // DecApp.cpp:710) through vvcr_write_output and checking them through vvcr_read_picture against the
-// decoded-picture-hash SEI (vvcp_picture_hash; PicYuvMD5.cpp calcMD5 semantics).
+// decoded-picture-hash SEI (vvcp_picture_hash; PicYuvMD5.cpp calcMD5 / calcCRC / calcChecksum semantics).
 //
 //   vvcdec -b stream.bin [-o out.yuv] [-d bitdepth] [--ClipOutputVideoToRec709Range] [-t threads]
 //
 // Options follow DecAppCfg.cpp:74-120 (-b, -o, -d, --ClipOutputVideoToRec709Range); -t is the number of
-// parser threads. The exit status is the number of pictures whose MD5 differs from the SEI, as
-// DecoderApp's (decmain.cpp:91).
+// parser threads. The exit status is 1 when any picture's hash differs from its SEI, else 0 (DecoderApp
+// returns the mismatch count, decmain.cpp:91, which the shell truncates modulo 256).
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
@@ -104,39 +104,71 @@ struct App {
   vvcr_output_params op{};
   std::vector<uint8_t> frame;
   std::vector<std::vector<uint16_t>> planes{3};
-  int mismatches = 0, verified = 0;
+  int mismatches = 0, verified = 0, unchecked = 0;
   bool quiet = false;
 
-  // DecApp::xWriteOutput (DecApp.cpp:710) and the MD5 check of DecLib (calcMD5, PicYuvMD5.cpp)
+  // DecApp::xWriteOutput (DecApp.cpp:710) and the decoded-picture-hash check of DecLib: calcMD5, calcCRC
+  // and calcChecksum (PicYuvMD5.cpp:188, :130, :169) over the whole picture, every component
   void output(int idx, int poc, int slot) {
     int32_t v[16];
     vvcp_picture_info(s, idx, v, 16);
     const int type = v[1], w = v[2], hgt = v[3], bd = v[5], tid = v[7], qp = v[9];
-    std::string md5s;
+    std::string hs;
     uint8_t sei[48];
     const int ht = vvcp_picture_hash(s, idx, sei, 48);
-    if (ht == 0) {   // samples as 1 (8-bit) or 2 little-endian bytes each, whole picture
+    if (ht >= 0 && ht <= 2) {
       int32_t strides[3] = {w, w / 2, w / 2};
       for (int c = 0; c < 3; c++) planes[c].resize((size_t)(c ? (w / 2) * (hgt / 2) : w * hgt));
       uint16_t *pl[3] = {planes[0].data(), planes[1].data(), planes[2].data()};
       if (vvcr_read_picture(ctx, slot, pl, strides)) die(std::string("vvcr_read_picture: ") + vvcr_last_error(ctx));
+      const int per = ht == 0 ? 16 : (ht == 1 ? 2 : 4);
       bool ok = true;
       for (int c = 0; c < 3; c++) {
-        Md5 m;
-        if (bd > 8) m.update((const uint8_t *)planes[c].data(), planes[c].size() * 2);
-        else for (uint16_t x : planes[c]) { const uint8_t b = (uint8_t)x; m.update(&b, 1); }
+        const int cw = c ? w / 2 : w, ch = c ? hgt / 2 : hgt;
         uint8_t d[16];
-        m.final(d);
-        ok &= std::memcmp(d, sei + 16 * c, 16) == 0;
-        md5s += (c ? "," : "") + hex(d, 16);
+        if (ht == 0) {   // samples as 1 (8-bit) or 2 little-endian bytes each
+          Md5 m;
+          if (bd > 8) m.update((const uint8_t *)planes[c].data(), planes[c].size() * 2);
+          else for (uint16_t x : planes[c]) { const uint8_t b = (uint8_t)x; m.update(&b, 1); }
+          m.final(d);
+        } else if (ht == 1) {   // compCRC: CRC-16/CCITT over the sample bytes, MSB first, 16 zero bits
+          uint32_t crc = 0xffff;
+          auto bits = [&](uint32_t byte) {
+            for (int k = 7; k >= 0; k--) {
+              const uint32_t msb = (crc >> 15) & 1;
+              crc = (((crc << 1) + ((byte >> k) & 1)) & 0xffff) ^ (msb * 0x1021);
+            }
+          };
+          for (uint16_t x : planes[c]) {
+            bits(x & 0xff);
+            if (bd > 8) bits(x >> 8);
+          }
+          for (int k = 0; k < 16; k++) {
+            const uint32_t msb = (crc >> 15) & 1;
+            crc = ((crc << 1) & 0xffff) ^ (msb * 0x1021);
+          }
+          d[0] = (uint8_t)(crc >> 8); d[1] = (uint8_t)crc;
+        } else {   // compChecksum: sample bytes xor a position mask, summed mod 2^32, big-endian
+          uint32_t sum = 0;
+          for (int y = 0; y < ch; y++)
+            for (int x = 0; x < cw; x++) {
+              const uint32_t m = (uint8_t)((x & 0xff) ^ (y & 0xff) ^ (x >> 8) ^ (y >> 8)), p = planes[c][(size_t)y * cw + x];
+              sum += (p & 0xff) ^ m;
+              if (bd > 8) sum += (p >> 8) ^ m;
+            }
+          d[0] = (uint8_t)(sum >> 24); d[1] = (uint8_t)(sum >> 16); d[2] = (uint8_t)(sum >> 8); d[3] = (uint8_t)sum;
+        }
+        ok &= std::memcmp(d, sei + per * c, per) == 0;
+        hs += (c ? "," : "") + hex(d, per);
       }
       verified++;
       if (!ok) mismatches++;
-      md5s = " [MD5:" + md5s + (ok ? ",(OK)]" : ",(***ERROR***)]");
-    } else if (ht > 0) {
-      md5s = " [hash type " + std::to_string(ht) + " not checked]";
+      hs = std::string(" [") + (ht == 0 ? "MD5:" : ht == 1 ? "CRC:" : "Checksum:") + hs + (ok ? ",(OK)]" : ",(***ERROR***)]");
+    } else if (ht > 2) {
+      hs = " [hash type " + std::to_string(ht) + " unknown, not checked]";
+      unchecked++;
     }
-    if (!quiet) printf("POC %4d LId:  0 TId: %d ( %c-SLICE, QP %2d )%s\n", poc, tid, "BPI"[std::min(2, std::max(0, type))], qp, md5s.c_str());
+    if (!quiet) printf("POC %4d LId:  0 TId: %d ( %c-SLICE, QP %2d )%s\n", poc, tid, "BPI"[std::min(2, std::max(0, type))], qp, hs.c_str());
     if (fo) {
       if (vvcr_write_output(ctx, slot, &op, frame.data(), 0)) die(std::string("vvcr_write_output: ") + vvcr_last_error(ctx));
       fwrite(frame.data(), 1, frame.size(), fo);
@@ -195,10 +227,11 @@ int main(int argc, char **argv) {
     printf("\n %d pictures, %.3f s (%.1f fps, %.1f Mpixels/s)", n, sec, n / sec, (double)n * v[2] * v[3] / sec / 1e6);
     if (app.verified)
       printf(", %d of %d picture hashes match%s", app.verified - app.mismatches, app.verified, app.mismatches ? "" : " (OK)");
+    if (app.unchecked) printf(", %d pictures with a hash of unknown type", app.unchecked);
     printf("\n");
   }
   vvcr_destroy(app.ctx);
   vvcp_close(app.s);
-  const int mismatches = app.mismatches;
-  return mismatches;
+  // 1 when any picture's hash differs (a count would wrap modulo 256 in the shell's exit status)
+  return app.mismatches ? 1 : 0;
 }

@@ -521,6 +521,8 @@ void parse_ph(Bits &b, PicHeader &h, const ParamSets &ps) {
         if (l == 1 && !pps->rpl1IdxPresent) {
         } else if (sps->rpl[l].size() > 1) h.rplIdx[l] = (int)b.u(ceilLog2((uint32_t)sps->rpl[l].size()));
         else h.rplIdx[l] = 0;
+        // u(ceilLog2(n)) reaches past n - 1 when n is not a power of two; list 1 may inherit list 0's index
+        VVCP_CHECK(h.rplIdx[l] < 0 || h.rplIdx[l] >= (int)sps->rpl[l].size(), "picture header: reference picture list index out of range");
         h.rpl[l] = sps->rpl[l][h.rplIdx[l]];
       }
       if (h.rpl[l].numLT) {
@@ -692,7 +694,10 @@ void parse_sh(Bits &b, SliceHeader &s, PicHeader &ph, const ParamSets &ps, int p
     for (int l = 0; l < 2; l++) {
       if (l == 1 && !pps->rpl1IdxPresent) {
         s.rplIdx[1] = s.rplIdx[0];
-        if (s.rplIdx[1] != -1) s.rpl[1] = sps->rpl[1][s.rplIdx[1]];
+        if (s.rplIdx[1] != -1) {
+          VVCP_CHECK(s.rplIdx[1] >= (int)sps->rpl[1].size(), "slice header: inherited list-1 RPL index out of range");
+          s.rpl[1] = sps->rpl[1][s.rplIdx[1]];
+        }
       } else {
         uint32_t spsFlag = 0;
         if (!sps->rpl[l].empty()) spsFlag = !pps->rplSpsIdc[l] ? b.u(1) : (uint32_t)(pps->rplSpsIdc[l] - 1);
@@ -702,6 +707,7 @@ void parse_sh(Bits &b, SliceHeader &s, PicHeader &ph, const ParamSets &ps, int p
             s.rplIdx[l] = -1;
           } else {
             s.rplIdx[l] = sps->rpl[l].size() > 1 ? (int)b.u(ceilLog2((uint32_t)sps->rpl[l].size())) : 0;
+            VVCP_CHECK(s.rplIdx[l] >= (int)sps->rpl[l].size(), "slice header: reference picture list index out of range");
             s.rpl[l] = sps->rpl[l][s.rplIdx[l]];
           }
         } else {
@@ -741,6 +747,7 @@ void parse_sh(Bits &b, SliceHeader &s, PicHeader &ph, const ParamSets &ps, int p
   }
   if (s.isIntra()) s.numRef[0] = s.numRef[1] = 0;   // constructRefPicList (Slice.cpp:417)
   VVCP_CHECK(s.numRef[0] > VVCR_MAX_REF || s.numRef[1] > VVCR_MAX_REF, "too many active references");
+  VVCP_CHECK(s.numRef[0] > s.rpl[0].num || s.numRef[1] > s.rpl[1].num, "more active references than list entries");
   s.cabacInit = false;
   if (pps->cabacInitPresent && !s.isIntra()) s.cabacInit = b.flag();
   s.colFromL0 = true;
@@ -748,6 +755,8 @@ void parse_sh(Bits &b, SliceHeader &s, PicHeader &ph, const ParamSets &ps, int p
   if (ph.tmvp) {
     if (s.isInterB()) s.colFromL0 = !pps->colFromL0Idc ? b.flag() : (pps->colFromL0Idc - 1) != 0;
     if (!s.isIntra() && ((s.colFromL0 && s.numRef[0] > 1) || (!s.colFromL0 && s.numRef[1] > 1))) s.colRefIdx = (int)b.ue();
+    // indexes refPoc[colList] in the motion derivation (vvcp_mv.cpp)
+    VVCP_CHECK(!s.isIntra() && s.colRefIdx >= s.numRef[s.colFromL0 ? 0 : 1], "slice header: collocated_ref_idx out of range");
   }
   std::memset(s.wp, 0, sizeof(s.wp));
   if ((pps->useWP && s.isInterP()) || (pps->wpBi && s.isInterB())) {   // parsePredWeightTable (VLCReader.cpp:3545)

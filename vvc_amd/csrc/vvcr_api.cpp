@@ -99,9 +99,17 @@ struct Staging {
   }
   template <class T, class A> void add(DevVec<T> &d, const std::vector<T, A> &v) { add(d, {{v.data(), v.size()}}); }
   template <class T> void add(DevVec<T> &d, const T *src, size_t n) { add(d, {{src, n}}); }
-  void commit(hipStream_t s, hipEvent_t done) {
+  // offset of the last add's array in the staging buffer, and its host copy there (valid until the next
+  // add): records that hold device pointers of other staged arrays are rewritten after place(), when
+  // those pointers are final
+  size_t last_off() const { return items.back().off; }
+  template <class T> T *host_at(size_t off) { return (T *)(h + off); }
+  // the device arena is sized and every staged DevVec points into it; nothing is copied yet
+  void place() {
     arena.ensure(used + 256);
     for (const Item &it : items) *it.dst = arena.p + it.off;
+  }
+  void copy(hipStream_t s, hipEvent_t done) {
     if (used) VVCR_CHECK_HIP(hipMemcpyAsync(arena.p, h, used, hipMemcpyHostToDevice, s));
     VVCR_CHECK_HIP(hipEventRecord(done, s));
   }
@@ -145,6 +153,8 @@ struct Prepared {
   DevVec<int16_t> alf_luma_coef, alf_luma_clip, alf_chroma, alf_cc, alf_set;
   DevVec<uint8_t> alf_ctb;
   DevVec<int32_t> dmvr;
+  DevVec<WpTable> wpt;               // the slice's weighted-prediction table (k_mc reads it per lane)
+  McClassTable mc_ct;                // k_mc cell classes of mc_basic
   bool have_sao = false, have_alf = false;
   int n_tb = 0, n_tb_small = 0, n_mctile = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
   hipEvent_t ev[NK][2] = {};
@@ -176,10 +186,11 @@ struct Prepared {
     for (auto &e : ev) { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); }
     (void)hipEventDestroy(done);
     (void)hipEventDestroy(start);
-    (void)hipEventDestroy(mc_done);
     (void)hipEventDestroy(ev_mc);
     if (up_issued) (void)hipEventSynchronize(up_done);   // the DMA may still read the pinned staging buffer
     (void)hipEventDestroy(up_done);
+    (void)hipEventSynchronize(mc_done);                   // nor may a queued DMVR delta read-back land in h_dmvr
+    (void)hipEventDestroy(mc_done);
     if (h_dmvr) (void)hipHostFree(h_dmvr);
   }
   void wait() { if (launched) VVCR_CHECK_HIP(hipEventSynchronize(done)); }
@@ -336,7 +347,22 @@ static int n_ctb(const vvcr_seq_params &sp) {
   return ((sp.width + ctu - 1) / ctu) * ((sp.height + ctu - 1) / ctu);
 }
 
-static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lane) {
+// WeightPrediction::getWpScaling (WeightPrediction.cpp:125-152): offsets scaled to the bit depth
+static WpTable make_wp_table(const vvcr_pic_params &pp, int bit_depth) {
+  WpTable T{};
+  const int osc = 1 << (bit_depth - 8);
+  for (int l = 0; l < 2; l++)
+    for (int i = 0; i < VVCR_MAX_REF; i++)
+      for (int c = 0; c < 3; c++) {
+        const int32_t *e = pp.wp[l][i][c];
+        T.d[l][i][c] = (int8_t)e[1];
+        T.w[l][i][c] = (int16_t)e[2];
+        T.o[l][i][c] = (int16_t)(e[3] * osc);
+      }
+  return T;
+}
+
+static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lane, const WpTable *wpd) {
   McParams P{};
   P.ref.p = ctx->d_ref_table.p;
   for (int c = 0; c < 3; c++) {
@@ -347,16 +373,8 @@ static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lan
   P.pic_h = ctx->sp.height;
   P.bd = ctx->sp.bit_depth;
   P.ctu = 1 << ctx->sp.ctu_log2;
-  // WeightPrediction::getWpScaling (WeightPrediction.cpp:125-152): offsets scaled to the bit depth
-  const int osc = 1 << (ctx->sp.bit_depth - 8);
-  for (int l = 0; l < 2; l++)
-    for (int i = 0; i < VVCR_MAX_REF; i++)
-      for (int c = 0; c < 3; c++) {
-        const int32_t *e = pp.wp[l][i][c];
-        P.wp.d[l][i][c] = (int8_t)e[1];
-        P.wp.w[l][i][c] = (int16_t)e[2];
-        P.wp.o[l][i][c] = (int16_t)(e[3] * osc);
-      }
+  P.wp = make_wp_table(pp, ctx->sp.bit_depth);
+  P.wpd = wpd;
   return P;
 }
 
@@ -453,6 +471,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   const vvcr_pic_params &pp = bp.pp;
   const WorkLists &wl = bp.wl;
   const double pix = (double)sp.width * sp.height * 1.5;   // samples of the three planes
+  size_t iparams_off = SIZE_MAX;   // staged intra parameters, rewritten after place()
   if (mask & VVCR_STAGE_RESID) {
     // the packed levels of the transform blocks: the producer's pool when it arrived packed
     st.add(r.coef, bp.desc.coef_box.empty() ? bp.wl.coef : bp.desc.coef);
@@ -467,6 +486,11 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     // 32x32 tiles first, then the small jobs, in one array
     st.add(r.mc_basic, {{wl.mc_tile.data(), wl.mc_tile.size()}, {wl.mc_basic.data(), wl.mc_basic.size()}});
     st.add(r.mc_bidir, wl.mc_bidir);
+    {
+      const WpTable wt = make_wp_table(pp, sp.bit_depth);
+      st.add(r.wpt, &wt, 1);
+    }
+    r.mc_ct = wl.mc_ct;
     st.add(r.aff_pu, wl.aff_pu);
     st.add(r.aff_jobs, wl.aff_jobs);
     r.n_mctile = (int)wl.mc_tile.size();
@@ -474,6 +498,8 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.n_bidir = (int)wl.mc_bidir.size();
     r.n_aff = (int)wl.aff_jobs.size();
     r.n_dmvr = wl.n_dmvr;
+    // the previous launch's delta read-back (copy stream, after its inter stage) may still be queued
+    VVCR_CHECK_HIP(hipEventSynchronize(r.mc_done));
     r.dmvr.ensure(2 * (size_t)r.n_dmvr + 2);
     if (r.h_dmvr_cap < 2 * (size_t)r.n_dmvr + 2) {
       if (r.h_dmvr) VVCR_CHECK_HIP(hipHostFree(r.h_dmvr));
@@ -504,9 +530,13 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     st.add(r.idep_start, ip.dep_start);
     st.add(r.ideps, ip.deps);
     r.istate.ensure(16 + ip.jobs.size());
-    IntraParams P[MAXLANE];   // one device copy per lane (scratch plane pointers differ)
-    for (int l = 0; l < MAXLANE; l++) P[l] = make_intra_params(ctx, r, l);
-    st.add(r.iparams, P, MAXLANE);
+    // one device copy per lane (scratch plane pointers differ), written after place(): they hold the
+    // arena address of the LMCS table (staged above), which is only known then
+    {
+      static const IntraParams blank[MAXLANE] = {};
+      st.add(r.iparams, blank, MAXLANE);
+    }
+    iparams_off = st.last_off();
     r.n_ijobs = (int)ip.jobs.size();
     st.add(r.ictu_list, ip.ctu_list);
     st.add(r.ictu_start, ip.ctu_start);
@@ -546,7 +576,10 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     st.add(r.alf_set, bp.h_alf_set);
     r.alg_bytes[K_ALF] = pix * 2 * 2;
   }
-  st.commit(ctx->upload_stream, r.up_done);
+  st.place();
+  if (iparams_off != SIZE_MAX)
+    for (int l = 0; l < MAXLANE; l++) st.host_at<IntraParams>(iparams_off)[l] = make_intra_params(ctx, r, l);
+  st.copy(ctx->upload_stream, r.up_done);
   r.up_issued = true;
 }
 
@@ -620,10 +653,10 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     r.launches[K_RESID] = r.n_tb > 0 ? 1 : 0;
   }
   if (mask & VVCR_STAGE_INTER) {
-    const McParams mp = make_mc_params(ctx, r.pp, L);
+    const McParams mp = make_mc_params(ctx, r.pp, L, r.wpt.p);
     {
       KernelTimer t(r, K_MC, s, ctx->timing);
-      launch_mc(mp, r.mc_basic.p, r.n_mctile, r.n_basic, s);
+      launch_mc(mp, r.mc_basic.p, r.mc_ct, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_MC] = (r.n_mctile + r.n_basic) ? 1 : 0;
     }
@@ -994,7 +1027,10 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t mask) {
   Prepared &r = *rp;
   plan_picture(ctx->cur, mask);
   prepare(ctx, r, ctx->cur);
-  launch(ctx, r);
+  {
+    std::lock_guard<std::mutex> g(ctx->launch_mu);   // launch() updates the shared slot / lane state
+    launch(ctx, r);
+  }
   ctx->in_picture = false;
   return VVCR_OK;
   API_END
@@ -1121,6 +1157,17 @@ int vvcr_picture_work_counts(const vvcr_picture *pic, int64_t *counts, int32_t n
                          (int64_t)pic->dbk.total(), (int64_t)pic->wl.n_dmvr, pic->wl.ref_y0, pic->wl.ref_y1};
   for (int k = 0; k < n && k < 10; k++) counts[k] = v[k];
   return 10;
+}
+
+// Diagnostics (host only): the raw 32-byte McJob records of a planned picture's inter work lists, which = 0
+// 32x32 tiles, 1 small blocks, 2 DMVR / BDOF blocks (tools/mc_mix.py). Returns the number of records.
+extern "C" int vvcr_debug_mc_jobs(const vvcr_picture *pic, int32_t which, void *out, int32_t cap) {
+  if (!pic || which < 0 || which > 2 || (!out && cap)) return VVCR_E_ARG;
+  if (!pic->planned) return VVCR_E_STATE;
+  const auto &v = which == 0 ? pic->wl.mc_tile : which == 1 ? pic->wl.mc_basic : pic->wl.mc_bidir;
+  const size_t n = std::min(v.size(), (size_t)std::max(cap, 0));
+  if (n) std::memcpy(out, v.data(), n * sizeof(McJob));
+  return (int)v.size();
 }
 
 // Diagnostics (host only): the DPB slots the planned inter work lists read, one entry per (job, list) in

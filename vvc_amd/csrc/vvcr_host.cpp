@@ -63,6 +63,35 @@ void push_mc(WorkLists &wl, int x0, int y0, int w, int h, const McJob &proto) {
   push_tiles(wl.mc_basic, x0, y0, w, h, proto);
 }
 
+// The k_mc class table of the combined job array (mc_tile, then mc_basic sorted by size): one class per
+// run of equal (w, h), its cell ranges padded to whole waves.
+void build_mc_classes(WorkLists &wl) {
+  McClassTable &ct = wl.mc_ct;
+  ct = McClassTable();
+  int lc = 0, cc = 0;
+  auto run = [&](const bigbuf::vec<McJob> &v, int base) {
+    for (size_t i = 0; i < v.size();) {
+      size_t e = i + 1;
+      while (e < v.size() && v[e].w == v[i].w && v[e].h == v[i].h) e++;
+      if (ct.n == MC_MAXCLS) fail("more plain-MC block sizes than k_mc classes");
+      const int k = ct.n++, w = v[i].w, h = v[i].h, n = (int)(e - i);
+      ct.job0[k] = base + (int)i;
+      ct.w[k] = w;
+      ct.h[k] = h;
+      ct.lcell0[k] = lc;
+      ct.ccell0[k] = cc;
+      lc += (n * mc_luma_cells(w, h) + 63) & ~63;
+      cc += (n * mc_chroma_cells(w, h) + 63) & ~63;
+      i = e;
+    }
+  };
+  run(wl.mc_tile, 0);
+  run(wl.mc_basic, (int)wl.mc_tile.size());
+  ct.job0[ct.n] = (int)(wl.mc_tile.size() + wl.mc_basic.size());
+  ct.lcell0[ct.n] = lc;
+  ct.ccell0[ct.n] = cc;
+}
+
 McJob make_job(const vvcr_pic_params &pp, int interDir, int r0, int r1, int mv0x, int mv0y, int mv1x, int mv1y,
                int bcw, bool altHpel) {
   McJob j{};
@@ -367,7 +396,14 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
     std::stable_partition(v.begin(), v.end(), [](const McJob &j) { return (j.flags & (MC_L0 | MC_L1)) == (MC_L0 | MC_L1); });
   };
   bi_first(wl.mc_tile);
-  bi_first(wl.mc_basic);
+  // the small blocks by size class (k_mc cell classes), bi-predicted first within a class: a wave's lanes
+  // then share one size and mostly one prediction direction
+  std::stable_sort(wl.mc_basic.begin(), wl.mc_basic.end(), [](const McJob &a, const McJob &b) {
+    const int ka = a.w << 8 | a.h, kb = b.w << 8 | b.h;
+    if (ka != kb) return ka > kb;
+    return ((a.flags & MC_L0) && (a.flags & MC_L1)) > ((b.flags & MC_L0) && (b.flags & MC_L1));
+  });
+  build_mc_classes(wl);
   std::stable_partition(wl.aff_jobs.begin(), wl.aff_jobs.end(), [&](const AffJob &j) {
     const AffPu &U = wl.aff_pu[j.pu];
     return U.l[0].present && U.l[1].present;

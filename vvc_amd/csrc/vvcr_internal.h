@@ -126,7 +126,24 @@ struct McParams {
   int32_t bd;            // bit depth
   int32_t ctu;           // CTU size (affine MV clamp, InterPrediction.cpp:937)
   WpTable wp;
+  const WpTable *wpd;    // the same table in device memory (k_mc indexes it per lane)
 };
+
+// Plain MC work of k_mc in "cells": a lane computes one cell (luma: 4 columns x 8 rows of one job; chroma:
+// 4 columns x 4 rows of one component) for every list of its job. The job array holds the 32x32 tiles,
+// then the smaller blocks, grouped in classes of one size (w, h); a class's cells are numbered job-major
+// from lcell0 / ccell0, each range padded to a multiple of 64, so no wave straddles two classes.
+constexpr int MC_MAXCLS = 12;
+struct McClassTable {
+  int32_t n = 0;                      // classes
+  int32_t job0[MC_MAXCLS + 1] = {};   // first job of the class in the combined job array; [n] = jobs in all
+  int32_t w[MC_MAXCLS] = {}, h[MC_MAXCLS] = {};
+  int32_t lcell0[MC_MAXCLS + 1] = {}; // first luma cell of each class; [n] = luma cells in all (lanes)
+  int32_t ccell0[MC_MAXCLS + 1] = {}; // chroma cells likewise
+};
+// cells of one job of size w x h: luma (w/4) x ceil(h/8), chroma 2 components x ceil(w/8) x ceil(h/8)
+__host__ __device__ inline int mc_luma_cells(int w, int h) { return (w >> 2) * ((h + 7) >> 3); }
+__host__ __device__ inline int mc_chroma_cells(int w, int h) { return 2 * ((w + 7) >> 3) * ((h + 7) >> 3); }
 
 // A workgroup-uniform record (job descriptor) through dword loads at a uniform address, so that it lands in
 // SGPRs (s_load): a plain struct copy loads its 16-bit fields with per-lane global loads, and everything
@@ -257,4 +274,4 @@ void launch_planes3(const Planes3 &p, hipStream_t s);
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, int nsmall, const int32_t *coef, const uint16_t *scans, hipStream_t s);
 // DecoderApp output frame of a picture (vvcr_write_output)
 void launch_output(const std::array<DPlane, 3> &pic, const vvcr_output_params &op, int bd, uint8_t *dst, hipStream_t s);
-void launch_mc(const McParams &p, const McJob *jobs, int ntile, int nbasic, hipStream_t s);   // 32x32 tiles, then <= 16x16 jobs
+void launch_mc(const McParams &p, const McJob *jobs, const McClassTable &ct, hipStream_t s);   // cells of the job classes
