@@ -71,6 +71,10 @@ int vvcp_alf_filters(const vvcp_stream *s, int32_t idx, int16_t *luma_coef, int1
  * copied: afterwards vvcp_picture_rows returns them empty and the picture cannot be planned again. */
 int vvcp_plan_picture(vvcp_stream *s, int32_t idx, const vvcr_seq_params *sp, int32_t slot, const int32_t *ref_slot,
                       uint32_t stage_mask, vvcr_picture **out);
+/* vvcp_plan_picture for the spatial shard of luma rows [shard_y0, shard_y1) (vvcr_pic_params::shard_y0 /
+ * shard_y1; 0, 0 = the whole picture). */
+int vvcp_plan_picture_rows(vvcp_stream *s, int32_t idx, const vvcr_seq_params *sp, int32_t slot, const int32_t *ref_slot,
+                           uint32_t stage_mask, int32_t shard_y0, int32_t shard_y1, vvcr_picture **out);
 
 /* The whole decode loop in native code (DecApp::decode, App/DecoderApp/DecApp.cpp:76-200, with this
  * parser and libvvcr in place of DecLib): CABAC of every picture on `threads` parser threads, then per

@@ -207,6 +207,10 @@ int vvcr_end_picture_stages(vvcr_ctx *ctx, uint32_t stage_mask);
  * vvcr_get_dmvr_deltas wait for the work they depend on. */
 int vvcr_prepare_picture(vvcr_ctx *ctx, uint32_t stage_mask, int32_t *handle);
 int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle);
+/* Launches only the stages of stage_mask that the picture was prepared with, e.g. the reconstruction
+ * stages and, after a halo exchange, the loop-filter stages of one prepared spatial shard (each launch
+ * orders itself after the slot's earlier writer like any other). */
+int vvcr_launch_picture_stages(vvcr_ctx *ctx, int32_t handle, uint32_t stage_mask);
 int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle);
 
 /* Host-only picture builder: the same begin / submit / loop-filter / plan sequence on a standalone

@@ -123,3 +123,44 @@ def test_threaded_planning_is_deterministic():
     with cf.ThreadPoolExecutor(6) as ex:
         par = list(ex.map(counts, jobs))
     assert par == serial
+
+
+_DBK_LISTS = r'''
+import ctypes as C, hashlib, os, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+from vvc_amd import native as N, stream as S
+L = N.lib()
+L.vvcr_debug_dbk_segments.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
+h = hashlib.md5()
+for name in sys.argv[2:]:
+    pics = S.load_sequence(os.path.join(sys.argv[1], "tests", "golden", name))
+    alloc = S.SlotAllocator(pics, 16)
+    for i, p in enumerate(pics):
+        slot = alloc.assign(i, p["hdr"]["poc"])
+        pic = S.plan_picture(p, slot, alloc.slot_of, dpb_slots=16)
+        n = L.vvcr_debug_dbk_segments(pic.h, None, 0)
+        a = np.zeros(2 * n, np.uint32)
+        L.vvcr_debug_dbk_segments(pic.h, a.ctypes.data, n)
+        h.update(a.tobytes())
+        pic.close()
+print(h.hexdigest())
+'''
+
+
+def test_deblocking_plan_independent_of_worker_count(tmp_path):
+    """The deblocking planner splits the CTUs over VVCR_DBK_THREADS workers: the segment lists (and their
+    order) must be those of a single pass, for any worker count."""
+    import subprocess
+    import sys
+    script = tmp_path / "dbk.py"
+    script.write_text(_DBK_LISTS)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = []
+    for t in ("1", "3", "8"):
+        env = dict(os.environ, VVCR_DBK_THREADS=t)
+        r = subprocess.run([sys.executable, str(script), root, "ra1080_q32", "ralm416_q32"], env=env, capture_output=True,
+                           text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out.append(r.stdout.strip())
+    assert out[0] == out[1] == out[2]

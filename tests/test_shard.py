@@ -116,3 +116,42 @@ def test_halo_exchange_over_gloo(tmp_path):
                 assert (rp[y] == peer_val + y + 10 * c).all(), (rank, c, y)
             for y in range(y0 >> s, y1 >> s):        # own rows untouched
                 assert (rp[y] == 100 * (rank + 1) + y + 10 * c).all()
+
+
+def _gather_worker(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        comm = SH.TorchComm("cpu", host_rows=True)
+        mine = np.arange(2 * (3 * rank), dtype=np.int32).reshape(-1, 2) + 1000 * rank   # rank 0 holds none
+        parts = comm.all_gather_rows(mine)
+        np.save(out % rank, np.concatenate(parts) if parts else np.zeros((0, 2), np.int32))
+        np.save((out % rank) + ".n.npy", np.array([len(p) for p in parts]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dmvr_delta_all_gather_over_gloo(tmp_path):
+    """The bitstream-driven shard ranks all-gather their DMVR deltas (rank order = the picture's PU order):
+    variable counts, including a rank with none, arrive whole and in order on every rank."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "g%d.npy")
+    mp.start_processes(_gather_worker, args=(3, 29900 + os.getpid() % 1000, out), nprocs=3, start_method="spawn")
+    exp = np.concatenate([np.arange(2 * (3 * r), dtype=np.int32).reshape(-1, 2) + 1000 * r for r in range(3)])
+    for r in range(3):
+        assert np.array_equal(np.load(out % r), exp)
+        assert list(np.load((out % r) + ".n.npy")) == [0, 3, 6]
+
+
+def test_stream_shard_rows_follow_the_tile_rows():
+    """StreamShardRank takes its rows from the parsed tile rows of the .bin (vvcp_picture_params)."""
+    from vvc_amd import parser as PZ
+    data = open(os.path.join(GOLD, "streams", "ra4320t_q32.bin"), "rb").read()
+    ps = PZ.Stream(data)
+    inf = ps.info(0)
+    pp = ps.pic_params(0)
+    ps.close()
+    p = S.load_sequence(os.path.join(GOLD, "ra4320t_q32"), max_pics=1)[0]
+    for world in (1, 2, 4, 8):
+        assert SH.stream_shard_rows(pp, inf["height"], inf["ctu_log2"], world) == SH.shard_rows(p, world)

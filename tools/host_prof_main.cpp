@@ -84,9 +84,15 @@ int main(int argc, char **argv) {
             if (ij[0] == pp.ref_poc[l][k]) { rs[l * VVCR_MAX_REF + k] = slots[j]; break; }
           }
       vvcr_picture *pic = nullptr;
-      if (vvcp_plan_picture(s, i, &sp, slots[i], rs, VVCR_STAGE_ALL, &pic)) { fprintf(stderr, "%s\n", vvcp_last_error()); return 1; }
+      // HOST_PROF_MASK: the stages planned (hex, default all): apportions the plan phase
+      const char *mk = getenv("HOST_PROF_MASK");
+      const uint32_t mask = mk ? (uint32_t)strtoul(mk, nullptr, 16) : VVCR_STAGE_ALL;
+      if (vvcp_plan_picture(s, i, &sp, slots[i], rs, mask, &pic)) { fprintf(stderr, "%s\n", vvcp_last_error()); return 1; }
       auto t3 = clk::now();
       vvcr_picture_destroy(pic);
+      if (getenv("HOST_PROF_VERBOSE"))
+        printf("pic %2d type %d  parse %6.2f  derive %6.2f  plan %6.2f ms\n", i, ii[1], std::chrono::duration<double>(t1 - t0).count() * 1e3,
+               std::chrono::duration<double>(t2 - t1).count() * 1e3, std::chrono::duration<double>(t3 - t2).count() * 1e3);
       tp += std::chrono::duration<double>(t1 - t0).count();
       td += std::chrono::duration<double>(t2 - t1).count();
       tl += std::chrono::duration<double>(t3 - t2).count();

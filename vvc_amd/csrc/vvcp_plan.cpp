@@ -18,6 +18,12 @@ int fail(vvcr_picture *pic, int rc, const char *what) {
 
 extern "C" int vvcp_plan_picture(vvcp_stream *h, int32_t idx, const vvcr_seq_params *sp, int32_t slot,
                                  const int32_t *ref_slot, uint32_t stage_mask, vvcr_picture **out) {
+  return vvcp_plan_picture_rows(h, idx, sp, slot, ref_slot, stage_mask, 0, 0, out);
+}
+
+extern "C" int vvcp_plan_picture_rows(vvcp_stream *h, int32_t idx, const vvcr_seq_params *sp, int32_t slot,
+                                      const int32_t *ref_slot, uint32_t stage_mask, int32_t shard_y0, int32_t shard_y1,
+                                      vvcr_picture **out) {
   if (!h || !sp || !out || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
   *out = nullptr;
   vvcp::PictureUnit &p = *h->s.pics[idx];
@@ -32,6 +38,8 @@ extern "C" int vvcp_plan_picture(vvcp_stream *h, int32_t idx, const vvcr_seq_par
     return VVCR_E_UNSUPPORTED;
   }
   pp.slot = slot;
+  pp.shard_y0 = shard_y0;
+  pp.shard_y1 = shard_y1;
   for (int l = 0; l < 2; l++)
     for (int r = 0; r < pp.num_ref[l]; r++) {
       if (!ref_slot) return VVCR_E_ARG;

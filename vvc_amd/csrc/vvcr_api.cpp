@@ -584,9 +584,9 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
 }
 
 // Device phase: enqueue the kernels of a prepared picture on the context stream.
-static void launch(vvcr_ctx *ctx, Prepared &r) {
+static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL) {
   const vvcr_pic_params &pp = r.pp;
-  const uint32_t mask = r.mask;
+  const uint32_t mask = r.mask & stages;
   std::vector<int> refs;
   for (int l = 0; l < 2; l++)
     for (int i = 0; i < pp.num_ref[l]; i++)
@@ -715,7 +715,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
   const int ctu = 1 << ctx->sp.ctu_log2;
   const int wc = (ctx->sp.width + ctu - 1) / ctu, n = n_ctb(ctx->sp);
   bool inTmp = false;
-  if (r.have_sao) {
+  if (r.have_sao && (mask & VVCR_STAGE_SAO)) {
     KernelTimer t(r, K_SAO, s, ctx->timing);
     SaoParams sp{};
     for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ln.tmp[c]; }
@@ -726,7 +726,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r) {
     inTmp = true;
     r.launches[K_SAO] = 3;
   }
-  if (r.have_alf) {
+  if (r.have_alf && (mask & VVCR_STAGE_ALF)) {
     KernelTimer t(r, K_ALF, s, ctx->timing);
     AlfParams ap{};
     for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ln.tmp[c] : A[c]; ap.dst[c] = inTmp ? A[c] : ln.tmp[c]; }
@@ -772,8 +772,9 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
   if (!sp || !out) return VVCR_E_ARG;
   *out = nullptr;
   if (sp->chroma_format != 1 || sp->bit_depth < 8 || sp->bit_depth > 10 || sp->width <= 0 || sp->height <= 0 ||
-      sp->dpb_slots <= 0 || sp->dpb_slots > VVCR_MAX_SLOTS || sp->width % 8 || sp->height % 8 || sp->ctu_log2 < 5 || sp->ctu_log2 > 7) {
-    g_create_error = "unsupported sequence parameters (4:2:0, 8..10 bit, size multiple of 8, CTU 32..128, <= 64 DPB slots)";
+      sp->dpb_slots <= 0 || sp->dpb_slots > VVCR_MAX_SLOTS || sp->width % 8 || sp->height % 8 || sp->width < 16 || sp->ctu_log2 < 5 ||
+      sp->ctu_log2 > 7) {
+    g_create_error = "unsupported sequence parameters (4:2:0, 8..10 bit, size multiple of 8 and width >= 16, CTU 32..128, <= 256 DPB slots)";
     return VVCR_E_UNSUPPORTED;
   }
   auto ctx = std::make_unique<vvcr_ctx>();
@@ -1082,6 +1083,15 @@ int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle) {
   API_END
 }
 
+int vvcr_launch_picture_stages(vvcr_ctx *ctx, int32_t handle, uint32_t stage_mask) {
+  if (!ctx) return VVCR_E_ARG;
+  API_BEGIN
+  std::lock_guard<std::mutex> g(ctx->launch_mu);
+  launch(ctx, get_prepared(ctx, handle), stage_mask);
+  return VVCR_OK;
+  API_END
+}
+
 int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle) {
   if (!ctx) return VVCR_E_ARG;
   API_BEGIN
@@ -1168,6 +1178,21 @@ extern "C" int vvcr_debug_mc_jobs(const vvcr_picture *pic, int32_t which, void *
   const size_t n = std::min(v.size(), (size_t)std::max(cap, 0));
   if (n) std::memcpy(out, v.data(), n * sizeof(McJob));
   return (int)v.size();
+}
+
+// Diagnostics (host only): the planned deblocking segments, the four lists back to back (luma VER, chroma
+// VER, luma HOR, chroma HOR) as the device receives them. Returns the number of segments.
+extern "C" int vvcr_debug_dbk_segments(const vvcr_picture *pic, void *out, int32_t cap) {
+  if (!pic || (!out && cap)) return VVCR_E_ARG;
+  if (!pic->planned) return VVCR_E_STATE;
+  const bigbuf::vec<DbkSeg> *parts[4] = {&pic->dbk.luma[0], &pic->dbk.chroma[0], &pic->dbk.luma[1], &pic->dbk.chroma[1]};
+  int32_t n = 0;
+  for (const auto *v : parts)
+    for (const DbkSeg &sg : *v) {
+      if (n < cap) static_cast<DbkSeg *>(out)[n] = sg;
+      n++;
+    }
+  return n;
 }
 
 // Diagnostics (host only): the DPB slots the planned inter work lists read, one entry per (job, list) in

@@ -10,8 +10,12 @@
 // so the per-CTU state of the reference reduces to per-CU work over picture-wide maps.
 #include "vvcr_dbk.h"
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <string>
+#include <thread>
+#include <vector>
 
 namespace {
 
@@ -20,14 +24,24 @@ enum { BX = 0, BY, BW, BH, BCBF };
 constexpr int MODE_INTRA = 1;
 constexpr int MRG_TYPE_SUBPU_ATMVP = 1;
 
+// Picture-wide lookup state, built once and then only read (the CTU workers share it): CU and TU index
+// maps on the 4x4 luma / 2x2 chroma grid, and the chroma QPs of every TU.
+struct Maps {
+  bigbuf::vec<int> own_cu_map[2], tu_map[2];
+  const int32_t *cu_map[2] = {nullptr, nullptr};   // the producer's CU maps when handed over, else own_cu_map
+  bigbuf::vec<int8_t> cqp;                         // [TU][Cb, Cr] QpParam(tu, comp).Qp(0) - qpBdOffset
+};
+
 struct Planner {
   const vvcr_seq_params &sp;
   const vvcr_pic_params &pp;
   const PictureDescriptors &d;
   DbkLists &out;
+  Maps &M;
   int W4, H4, ctu, parts;
-  bigbuf::vec<int> own_cu_map[2], tu_map[2];
-  const int32_t *cu_map[2] = {nullptr, nullptr};   // the producer's CU maps when handed over, else own_cu_map
+  bigbuf::vec<int> (&own_cu_map)[2] = M.own_cu_map;
+  bigbuf::vec<int> (&tu_map)[2] = M.tu_map;
+  const int32_t *(&cu_map)[2] = M.cu_map;
   // per-CU scratch in CTU-relative coordinates (the reference's per-CTU arrays, LoopFilter.h:66-79)
   int ctu_x = 0, ctu_y = 0;
   uint8_t bs[2][32 * 32];
@@ -37,8 +51,8 @@ struct Planner {
   uint8_t lenP[3][32][32], lenQ[3][32][32], tedge[32][32];
   bool left = false, top = false, internal = false;
 
-  Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, DbkLists &o)
-      : sp(s), pp(p), d(dd), out(o) {
+  Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, DbkLists &o, Maps &m)
+      : sp(s), pp(p), d(dd), out(o), M(m) {
     W4 = sp.width / 4;
     H4 = sp.height / 4;
     ctu = 1 << sp.ctu_log2;
@@ -78,7 +92,6 @@ struct Planner {
 
   void build_maps() {
     const size_t n = (size_t)W4 * H4;
-    cqp.assign(2 * d.tu.size(), (int8_t)-128);
     for (int k = 0; k < 2; k++) {
       tu_map[k].assign(n, -1);
       if (d.cu_map[k].size() == n) { cu_map[k] = d.cu_map[k].data(); continue; }
@@ -102,6 +115,9 @@ struct Planner {
       }
       if (b1[BW] > 0 && b1[BH] > 0) fill(tu_map[1], b1[BX], b1[BY], b1[BW], b1[BH], 1, (int)t);
     }
+    M.cqp.resize(2 * d.tu.size());
+    for (size_t t = 0; t < d.tu.size(); t++)
+      for (int comp = 1; comp <= 2; comp++) M.cqp[2 * t + comp - 1] = (int8_t)chroma_qp((int)t, comp);
   }
 
   void set_edges(int dir, int x, int y, int w, int h, bool val, bool edgeIdx) {
@@ -241,13 +257,7 @@ struct Planner {
     return (std::abs(mq.mv0x - mp.mv0x) >= th || std::abs(mq.mv0y - mp.mv0y) >= th) ? tmp + 1 : tmp;
   }
 
-  // chroma_qp per (TU, Cb / Cr), computed on first use (-128: not yet)
-  mutable bigbuf::vec<int8_t> cqp;
-  int chroma_qp_cached(int t, int comp) const {
-    int8_t &c = cqp[2 * (size_t)t + comp - 1];
-    if (c == -128) c = (int8_t)chroma_qp(t, comp);
-    return c;
-  }
+  int chroma_qp_cached(int t, int comp) const { return M.cqp[2 * (size_t)t + comp - 1]; }
   // QpParam(tu, comp).Qp(0) - qpBdOffset (Quant.cpp:65-138); joint Cb-Cr mode 3 uses the JOINT_CbCr tables
   int chroma_qp(int t, int comp) const {
     const int qpy = d.cu[d.tu[t].cu].qp;
@@ -441,11 +451,13 @@ struct Planner {
     std::memset(tedge, 0, sizeof tedge);
   }
 
-  void run() {
-    build_maps();
+  // CUs grouped by CTU (raster order): start[k] .. start[k + 1] index order[] for CTU k
+  void group(std::vector<int> &start, std::vector<int> &order) const {
     const int wc = (sp.width + ctu - 1) / ctu, hc = (sp.height + ctu - 1) / ctu;
     const int ncu = (int)d.cu.size();
-    std::vector<int> start((size_t)wc * hc + 1, 0), order(ncu), ctu_of(ncu);
+    start.assign((size_t)wc * hc + 1, 0);
+    order.resize(ncu);
+    std::vector<int> ctu_of(ncu);
     for (int i = 0; i < ncu; i++) {
       int a[4];
       cu_area(d.cu[i], a);
@@ -453,38 +465,78 @@ struct Planner {
       start[ctu_of[i] + 1]++;
     }
     for (int k = 0; k < wc * hc; k++) start[k + 1] += start[k];
-    {
-      std::vector<int> pos(start);
-      for (int i = 0; i < ncu; i++) order[pos[ctu_of[i]]++] = i;
-    }
+    std::vector<int> pos(start.begin(), start.end() - 1);
+    for (int i = 0; i < ncu; i++) order[pos[ctu_of[i]]++] = i;
+  }
+
+  // the edges of CTUs [k0, k1) in one direction (every CTU's state is its own: LoopFilter::xDeblockCU
+  // works CTU by CTU)
+  void run_ctus(int dir, int k0, int k1, const std::vector<int> &start, const std::vector<int> &order) {
+    const int wc = (sp.width + ctu - 1) / ctu;
     // a shard plans the edges of the CUs within VVCR_LF_HALO rows of its own rows: its loop filters
     // rebuild the deblocked samples the SAO / ALF of its rows read (see vvcr.h)
     const bool shard = pp.shard_y1 > 0;
     const int ly0 = pp.shard_y0 - VVCR_LF_HALO, ly1 = pp.shard_y1 + VVCR_LF_HALO;
-    for (int dir = 0; dir < 2; dir++)
-      for (int k = 0; k < wc * hc; k++) {
-        ctu_x = (k % wc) * ctu;
-        ctu_y = (k / wc) * ctu;
-        if (shard && (ctu_y + ctu <= ly0 || ctu_y >= ly1)) continue;
-        for (int pass = 0; pass < (pp.dual_tree ? 2 : 1); pass++) {
-          reset(dir);
-          for (int j = start[k]; j < start[k + 1]; j++) {
-            const int i = order[j];
-            if (pp.dual_tree && d.cu[i].chtype != pass) continue;
-            if (shard && !cu_in_rows(d.cu[i], ly0, ly1)) continue;
-            deblock_cu(i, dir);
-          }
+    for (int k = k0; k < k1; k++) {
+      ctu_x = (k % wc) * ctu;
+      ctu_y = (k / wc) * ctu;
+      if (shard && (ctu_y + ctu <= ly0 || ctu_y >= ly1)) continue;
+      for (int pass = 0; pass < (pp.dual_tree ? 2 : 1); pass++) {
+        reset(dir);
+        for (int j = start[k]; j < start[k + 1]; j++) {
+          const int i = order[j];
+          if (pp.dual_tree && d.cu[i].chtype != pass) continue;
+          if (shard && !cu_in_rows(d.cu[i], ly0, ly1)) continue;
+          deblock_cu(i, dir);
         }
       }
+    }
   }
 };
 
 }  // namespace
 
+// Workers take contiguous CTU ranges and fill lists of their own, appended in CTU order afterwards: the
+// lists are those of one pass over the CTUs, whatever the number of workers (VVCR_DBK_THREADS, default 4;
+// the picture's other planners run beside them).
 void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkLists &out) {
   out.clear();
   if (pp.dbk_disable) return;
   if (sp.width % 8 || sp.height % 8) throw VvcrError(VVCR_E_UNSUPPORTED, "deblocking: picture size not a multiple of 8");
-  auto P = std::make_unique<Planner>(sp, pp, d, out);   // ~200 KB of per-CTU state: keep it off the stack
-  P->run();
+  static const int nthreads = [] {
+    const char *e = getenv("VVCR_DBK_THREADS");
+    return e ? std::max(1, std::min(32, atoi(e))) : 4;
+  }();
+  Maps M;
+  std::vector<int> start, order;
+  {
+    DbkLists scratch;
+    auto P = std::make_unique<Planner>(sp, pp, d, scratch, M);   // ~200 KB of per-CTU state: keep it off the stack
+    P->build_maps();
+    P->group(start, order);
+  }
+  const int nctu = (int)start.size() - 1;
+  const int T = std::max(1, std::min(nthreads, nctu / 8));
+  std::vector<DbkLists> part(T);
+  std::vector<std::exception_ptr> err(T);
+  auto work = [&](int t) {
+    try {
+      auto P = std::make_unique<Planner>(sp, pp, d, part[t], M);
+      const int k0 = (int)((int64_t)nctu * t / T), k1 = (int)((int64_t)nctu * (t + 1) / T);
+      for (int dir = 0; dir < 2; dir++) P->run_ctus(dir, k0, k1, start, order);
+    } catch (...) {
+      err[t] = std::current_exception();
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto &x : th) x.join();
+  for (auto &e : err)
+    if (e) std::rethrow_exception(e);
+  for (int dir = 0; dir < 2; dir++)
+    for (int t = 0; t < T; t++) {
+      out.luma[dir].insert(out.luma[dir].end(), part[t].luma[dir].begin(), part[t].luma[dir].end());
+      out.chroma[dir].insert(out.chroma[dir].end(), part[t].chroma[dir].begin(), part[t].chroma[dir].end());
+    }
 }

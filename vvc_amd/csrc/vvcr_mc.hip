@@ -153,34 +153,62 @@ constexpr CellTaps make_cell_taps() {
 }
 __constant__ CellTaps c_ctaps = make_cell_taps();
 
+#ifndef MC_ROWS_AHEAD
+#define MC_ROWS_AHEAD 4
+#endif
 // Dword-aligned loads of 2 / 4 / 6 dwords (multi-dword global loads need dword alignment only).
 typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 
-// The ND dwords of sample pairs of one reference row from the even column dc (clamped columns when the
-// span leaves the row).
+// The ND dwords of sample pairs of one reference row from the even column dc: one 16-byte (+ 8-byte) load
+// when the span lies inside the row; else the same loads at the row's first / last 2 ND samples, the
+// dwords shifted into place by selects and the columns beyond the edge filled with the edge sample
+// (dc is even, so a dword is either wholly inside or wholly outside the row). Rows are >= 2 ND samples
+// wide (vvcr_create: width >= 16).
 template <int ND>
-__device__ __forceinline__ void row_dwords(const int16_t *row, int dc, int pw, bool inside, uint32_t (&w)[ND]) {
-  if (inside) {
-    const uint32_t *q = (const uint32_t *)(row + dc);
-    const u32x4a v = *(const u32x4a *)q;
-    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
-    if (ND == 6) {
-      const u32x2a u = *(const u32x2a *)(q + 4);
-      w[4 % ND] = u.x; w[5 % ND] = u.y;
-    }
-  } else {
+__device__ __forceinline__ void load_nd(const int16_t *q, uint32_t (&w)[ND]) {
+  const u32x4a v = *(const u32x4a *)q;
+  w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  if (ND == 6) {
+    const u32x2a u = *(const u32x2a *)(q + 8);
+    w[4 % ND] = u.x; w[5 % ND] = u.y;
+  }
+}
+// Edge windows: the loads start at a column inside the row (cb), and dword k of the span is loaded dword
+// k + sh (sh < 0: the span starts left of the row, > 0: right; dc is even, so a dword is either wholly
+// inside or wholly outside the row), the others are the edge sample repeated. Branch-free per row.
+struct EdgeMap {
+  int cb, sh;
+  bool left;
+};
+template <int ND>
+__device__ __forceinline__ EdgeMap edge_map(int dc, int pw) {
+  EdgeMap e;
+  if (dc < 0) { e.cb = 0; e.sh = max(dc >> 1, -ND); e.left = true; }
+  else if (dc + 2 * ND > pw) { e.cb = pw - 2 * ND; e.sh = min((dc - e.cb) >> 1, ND); e.left = false; }
+  else { e.cb = dc; e.sh = 0; e.left = false; }
+  return e;
+}
+template <int ND>
+__device__ __forceinline__ void edge_dwords(const int16_t *row, const EdgeMap &e, uint32_t (&w)[ND]) {
+  uint32_t D[ND];
+  load_nd<ND>(row + e.cb, D);
+  const uint32_t s = e.left ? (D[0] & 0xffffu) : (D[ND - 1] >> 16), fill = s | s << 16;
 #pragma unroll
-    for (int k = 0; k < ND; k++) w[k] = pk(row[clampi(dc + 2 * k, 0, pw - 1)], row[clampi(dc + 2 * k + 1, 0, pw - 1)]);
+  for (int k = 0; k < ND; k++) {
+    uint32_t v = fill;
+#pragma unroll
+    for (int t = 0; t < ND; t++) v = (k + e.sh == t) ? D[t] : v;
+    w[k] = v;
   }
 }
 
 // One list of a cell: R x 4 outputs of the N-tap separable filter from the reference plane R, window
-// origin (ox, oy) (first tap), fractions fx / fy, tap set ts (luma); v[o][c] = ((V sum + off2) >> sh2)
-// before any clamp. (The lane's outputs are its own: no other lane is involved.)
-template <int N, int R>
+// origin (ox, oy) (first tap), fractions fx / fy, tap set ts (luma); emit(o, v) receives output row o,
+// v[c] = (V sum + off2) >> sh2 before any clamp, as soon as its last H row is filtered.
+template <int N, int R, class Emit>
 __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, int fx, int fy, int ts, int sh1, int off2, int sh2,
-                                            int (&v)[R][4]) {
+                                            Emit &&emit) {
   constexpr int ND = N / 2 + 2, NT = N / 2 + 1, NV = N / 2, ROWS = R + N - 1;
   const int par = ox & 1, dc = ox - par;
   uint32_t T0[NT], T1[NT], TV[NV];
@@ -199,7 +227,9 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
   }
   uint32_t Pv[4][ROWS - 1];   // vertical pairs (H row r, H row r + 1) per column
   int prev[4] = {0, 0, 0, 0};
-  // one H row: 2 (N/2 + 1) dot2 for the four columns, then the vertical pairs with the row before
+  // one H row: 2 (N/2 + 1) dot2 for the four columns, the vertical pairs with the row before, and the V
+  // outputs whose last pair this row completes (output o reads pairs o, o + 2, .., o + N - 2), so that a
+  // pair lives only as long as an output still needs it
   auto hrow = [&](int r, const uint32_t (&w)[ND]) {
     int a = 0, b = 0, c = 0, d = 0;
 #pragma unroll
@@ -216,6 +246,18 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) prev[q] = hs[q];
+    const int o = r - (N - 1);
+    if (o >= 0) {
+      int v[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        int acc = off2;
+#pragma unroll
+        for (int m = 0; m < NV; m++) acc = dot2(Pv[q][o + 2 * m], TV[m], acc);
+        v[q] = acc >> sh2;
+      }
+      emit(o, v);
+    }
   };
   if (dc >= 0 && dc + 2 * ND <= Rp.w && oy >= 0 && oy + ROWS <= Rp.h) {
     // the whole window inside the picture (the common case): vector loads, row pointers by increment
@@ -223,29 +265,24 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
       uint32_t w[ND];
-      row_dwords<ND>(row, 0, 0, true, w);
+      load_nd<ND>(row, w);
       hrow(r, w);
       row += Rp.stride;
+      // at most MC_ROWS_AHEAD rows of loads in flight: more would only raise the register count (and lower the
+      // occupancy that hides the load latency)
+      if (r % MC_ROWS_AHEAD == MC_ROWS_AHEAD - 1) __builtin_amdgcn_sched_barrier(0);
     }
   } else {
-    const bool hin = dc >= 0 && dc + 2 * ND <= Rp.w;
+    // a window at the picture edge (rows clamped, edge columns replicated: Picture::extendPicBorder)
+    const EdgeMap e = edge_map<ND>(dc, Rp.w);
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
       const int16_t *row = Rp.p + (size_t)clampi(oy + r, 0, Rp.h - 1) * Rp.stride;
       uint32_t w[ND];
-      row_dwords<ND>(row, dc, Rp.w, hin, w);
+      edge_dwords<ND>(row, e, w);
       hrow(r, w);
     }
   }
-#pragma unroll
-  for (int o = 0; o < R; o++)
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      int acc = off2;
-#pragma unroll
-      for (int m = 0; m < NV; m++) acc = dot2(Pv[c][o + 2 * m], TV[m], acc);
-      v[o][c] = acc >> sh2;
-    }
 }
 
 // The window of list l of job J for the cell at (x, y) of component comp (picture coordinates of that
@@ -285,57 +322,57 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
   const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
   const int off2 = (rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0) - (IF_INTERNAL_OFFS << IF_FILTER_PREC);
   const int ts = (N == 8) ? ((J.w == 4 && J.h == 4) ? 1 : 0) | ((J.flags & MC_ALT_HPEL) ? 2 : 0) : 0;
-  int a[R][4];
-  {
-    const CellWin W = cell_win(P, J, comp, l0 ? 0 : 1, x, y);
-    cell_filter<N, R>(W.R, W.ox, W.oy, W.fx, W.fy, ts, sh1, off2, sh2, a);
-  }
   const int ostride = comp ? P.out[1].stride : P.out[0].stride;
   int16_t *dst = (comp == 0 ? P.out[0].p : comp == 1 ? P.out[1].p : P.out[2].p) + (size_t)y * ostride + x;
-  if (bi) {
-    int b[R][4];
-    {
-      const CellWin W = cell_win(P, J, comp, 1, x, y);
-      cell_filter<N, R>(W.R, W.ox, W.oy, W.fx, W.fy, ts, sh1, off2, sh2, b);
+  const int cx = x - (comp ? J.x >> 1 : J.x), cy = y - (comp ? J.y >> 1 : J.y);   // cell origin in the block
+  const bool wide = nc == 4 && (x & 3) == 0;
+  // one output row of 4 samples: 8-byte store, or 2-sample aligned pieces (chroma of blocks at odd
+  // multiples of 4 luma columns, or 2 wide)
+  auto store = [&](int o, const int (&a)[4]) {
+    if (o >= nr) return;
+    int16_t *q = dst + (size_t)o * ostride;
+    if (wide) *(uint2 *)q = make_uint2(pk(a[0], a[1]), pk(a[2], a[3]));
+    else {
+      ((uint32_t *)q)[0] = pk(a[0], a[1]);
+      if (nc == 4) ((uint32_t *)q)[1] = pk(a[2], a[3]);
     }
-    if (!(J.flags & (MC_WP | MC_GEO)) && J.bcw == 2) {   // AreaBuf::addAvg (Buffer.cpp:447)
+  };
+  const CellWin W0 = cell_win(P, J, comp, l0 ? 0 : 1, x, y);
+  if (!bi) {
+    cell_filter<N, R>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
+      int a[4];
+      if (rnd) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) a[q] = clampi(v[q], 0, maxv);
+      } else {   // uni with explicit WP (14-bit intermediates, WeightPrediction::addWeightUni)
+#pragma unroll
+        for (int q = 0; q < 4; q++) a[q] = combine(P, WT, J, comp, cx + q, cy + o, v[q], v[q]);
+      }
+      store(o, a);
+    });
+    return;
+  }
+  // bi: list 0's rows kept as packed 14-bit pairs, combined with list 1's as those arrive
+  uint32_t p0[R][2];
+  cell_filter<N, R>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
+    p0[o][0] = pk(v[0], v[1]);
+    p0[o][1] = pk(v[2], v[3]);
+  });
+  const CellWin W1 = cell_win(P, J, comp, 1, x, y);
+  const bool avg = !(J.flags & (MC_WP | MC_GEO)) && J.bcw == 2;
+  cell_filter<N, R>(W1.R, W1.ox, W1.oy, W1.fx, W1.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
+    const int u[4] = {lo16(p0[o][0]), hi16(p0[o][0]), lo16(p0[o][1]), hi16(p0[o][1])};
+    int a[4];
+    if (avg) {   // AreaBuf::addAvg (Buffer.cpp:447)
       const int shiftNum = headRoom + 1, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
 #pragma unroll
-      for (int o = 0; o < R; o++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) a[o][c] = clampi((a[o][c] + b[o][c] + offset) >> shiftNum, 0, maxv);
+      for (int q = 0; q < 4; q++) a[q] = clampi((u[q] + v[q] + offset) >> shiftNum, 0, maxv);
     } else {
-      const int cx = x - (comp ? J.x >> 1 : J.x), cy = y - (comp ? J.y >> 1 : J.y);   // cell origin in the block
 #pragma unroll
-      for (int o = 0; o < R; o++)
-#pragma unroll
-        for (int c = 0; c < 4; c++) a[o][c] = combine(P, WT, J, comp, cx + c, cy + o, a[o][c], b[o][c]);
+      for (int q = 0; q < 4; q++) a[q] = combine(P, WT, J, comp, cx + q, cy + o, u[q], v[q]);
     }
-  } else if (rnd) {
-#pragma unroll
-    for (int o = 0; o < R; o++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) a[o][c] = clampi(a[o][c], 0, maxv);
-  } else {   // uni with explicit WP (14-bit intermediates, WeightPrediction::addWeightUni)
-    const int cx = x - (comp ? J.x >> 1 : J.x), cy = y - (comp ? J.y >> 1 : J.y);
-#pragma unroll
-    for (int o = 0; o < R; o++)
-#pragma unroll
-      for (int c = 0; c < 4; c++) a[o][c] = combine(P, WT, J, comp, cx + c, cy + o, a[o][c], a[o][c]);
-  }
-  if (nc == 4 && (x & 3) == 0) {
-#pragma unroll
-    for (int o = 0; o < R; o++)
-      if (o < nr) *(uint2 *)(dst + (size_t)o * ostride) = make_uint2(pk(a[o][0], a[o][1]), pk(a[o][2], a[o][3]));
-  } else {   // 2-sample aligned pieces (chroma of blocks at odd multiples of 4 luma columns, or 2 wide)
-#pragma unroll
-    for (int o = 0; o < R; o++)
-      if (o < nr) {
-        uint32_t *q = (uint32_t *)(dst + (size_t)o * ostride);
-        q[0] = pk(a[o][0], a[o][1]);
-        if (nc == 4) q[1] = pk(a[o][2], a[o][3]);
-      }
-  }
+    store(o, a);
+  });
 }
 
 // A job record through two 16-byte loads (per lane: the lanes of a wave hold different jobs).

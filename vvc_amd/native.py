@@ -92,6 +92,7 @@ def lib():
         L.vvcr_picture_dmvr_deltas.argtypes = [P, I32, P, C.c_int64]
         L.vvcr_prepare_picture.argtypes = [P, C.c_uint32, C.POINTER(I32)]
         L.vvcr_launch_picture.argtypes = [P, I32]
+        L.vvcr_launch_picture_stages.argtypes = [P, I32, C.c_uint32]
         L.vvcr_release_picture.argtypes = [P, I32]
         L.vvcr_kernel_stats.argtypes = [P, I32, C.POINTER(KernelStat), I32]
         L.vvcr_stream.argtypes = [P]
@@ -128,7 +129,7 @@ class KernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 16), ("launches", C.c_int32), ("ms", C.c_float), ("alg_bytes", C.c_double)]
 
 
-EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_release_picture", "vvcr_kernel_stats", "vvcr_create", "vvcr_destroy", "vvcr_last_error", "vvcr_begin_picture", "vvcr_submit",
+EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_launch_picture_stages", "vvcr_release_picture", "vvcr_kernel_stats", "vvcr_create", "vvcr_destroy", "vvcr_last_error", "vvcr_begin_picture", "vvcr_submit",
            "vvcr_set_loop_filter_params", "vvcr_end_picture", "vvcr_end_picture_stages", "vvcr_sync",
            "vvcr_read_plane", "vvcr_write_plane", "vvcr_read_picture", "vvcr_get_dmvr_deltas", "vvcr_picture_dmvr_deltas",
            "vvcr_last_stage_times", "vvcr_stream", "vvcr_rd_plan", "vvcr_rd_run", "vvcr_fwd_plan", "vvcr_fwd_run",
@@ -307,6 +308,10 @@ class Context:
 
     def launch(self, handle):
         self._chk(self.L.vvcr_launch_picture(self.h, handle), "vvcr_launch_picture")
+
+    def launch_stages(self, handle, stages):
+        """the stages of `stages` the picture was prepared with (vvcr_launch_picture_stages)"""
+        self._chk(self.L.vvcr_launch_picture_stages(self.h, handle, stages), "vvcr_launch_picture_stages")
 
     def release(self, handle):
         self._chk(self.L.vvcr_release_picture(self.h, handle), "vvcr_release_picture")

@@ -135,6 +135,209 @@ class ShardRank(ShardGeom):
             self.ctx.release(h)
 
 
+# ------------------------------------------------------------------------------------------------
+# the product path: shards decoded from the bitstream
+# ------------------------------------------------------------------------------------------------
+def stream_shard_rows(pp, height, ctu_log2, world):
+    """shard_rows from the parsed picture parameters (tile rows of vvcr_pic_params)"""
+    nt = int(pp.num_tile_rows)
+    bd = [int(pp.tile_row_bd[k]) for k in range(nt + 1)] if nt > 0 else None
+    p = {"hdr": {"ctu_log2": ctu_log2, "height": height}}
+    if bd:
+        p["tile_row_bd"] = bd
+    return shard_rows(p, world)
+
+
+class StreamShardRank(ShardGeom):
+    """One rank of a spatially sharded decode FROM THE BITSTREAM (BASELINE config 4 end to end): every
+    rank runs the host parser (vvcp: headers, CABAC, motion derivation) and reconstructs and filters its
+    own tile rows only (vvcp_plan_picture_rows -> vvcr_pic_params::shard_y0 / shard_y1).
+
+    Per picture, in decoding order (DecApp::decode, DecApp.cpp:118-200):
+      1. the CABAC pass (whole picture: the slice's substreams follow one another);
+      2. the refined motion of its pending references: each rank's GPU refined the DMVR sub-blocks of its
+         own rows, and since the shards are whole CTU rows in raster order the ranks' delta lists, in rank
+         order, are the picture's list (vvcr_picture_dmvr_deltas order): they are all-gathered, so every
+         rank records the exact refined motion field (CS::setRefinedMotionField, UnitTools.cpp:68) and
+         derives the exact motion of every CU, including the CUs near its rows whose boundary strengths
+         its deblocking halo needs;
+      3. motion derivation, planning of the shard, upload;
+      4. the reference halo: the motion reach of the picture's MC jobs beyond the shard (max over the
+         ranks, all-reduced per picture) in each reference picture, exchanged point to point with the
+         neighbours when that reference has not yet been exchanged as deep (VTM 7.3 has no tile MC clamp);
+      5. reconstruction stages, the loop-filter halo swap, the loop-filter stages.
+    """
+
+    def __init__(self, ctx, data, rank, world, dpb_slots, rows=None):
+        import ctypes as C
+        from . import bitstream as B
+        from . import parser as PZ
+        self.ps = PZ.Stream(data)
+        self.n = n = len(self.ps)
+        inf0 = self.ps.info(0)
+        self.W, self.H = inf0["width"], inf0["height"]
+        self.sp = N.SeqParams(self.W, self.H, 1, inf0["bit_depth"], inf0["ctu_log2"], dpb_slots, 0)
+        rows = rows or stream_shard_rows(self.ps.pic_params(0), self.H, inf0["ctu_log2"], world)
+        super().__init__(ctx, rank, rows)
+        L = B._bind(N.lib())
+        L.vvcp_plan_picture_rows.argtypes = [C.c_void_p, C.c_int32, C.POINTER(N.SeqParams), C.c_int32, C.c_void_p,
+                                             C.c_uint32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
+        self.L, self.C = L, C
+        slots = (C.c_int32 * n)()
+        if L.vvcp_decode_plan(self.ps.h, 0, dpb_slots, slots, None) < 0:
+            raise RuntimeError("vvcp_decode_plan: %s" % L.vvcp_last_error().decode())
+        self.slots = list(slots)
+        plan = B.Plan(self.ps, dpb_slots)
+        self.info = plan.info
+        # decode index of every reference (the latest earlier picture of that POC in the same CVS)
+        self.refs = []
+        for i in range(n):
+            r = []
+            for l in range(2):
+                for poc in plan.refs[i][l]:
+                    j = next(k for k in range(i - 1, -1, -1) if self.info[k]["poc"] == poc and plan.cvs[k] == plan.cvs[i])
+                    if j not in r:
+                        r.append(j)
+            self.refs.append(r)
+        later = [False] * n
+        for i in range(n):
+            for j in self.refs[i]:
+                later[j] = True
+        self.ref_later = later
+        self.handle = [None] * n
+        self.ndmvr = [0] * n
+        self.refined = [False] * n
+        self.depth = {}        # DPB slot -> reference-halo rows exchanged for its current picture
+        self.reach = 0         # largest reach seen (diagnostics)
+
+    # ---- phases of picture i (a driver runs them on every rank: decode_stream_picture)
+    def parse(self, i):
+        self.ps.parse(i)
+
+    def pending(self, i):
+        """references of i whose motion is not refined yet (their deltas must be all-gathered first)"""
+        return [j for j in self.refs[i] if not self.refined[j]]
+
+    def local_deltas(self, j):
+        return self.ctx.picture_dmvr_deltas(self.handle[j], self.ndmvr[j])
+
+    def refine(self, j, parts):
+        d = np.concatenate([np.asarray(p, np.int32).reshape(-1, 2) for p in parts]) if parts else np.zeros((0, 2), np.int32)
+        self.ps.refine(j, d)
+        self.refined[j] = True
+
+    def plan(self, i):
+        """derive and plan the shard of picture i; returns its reach (rows read beyond the shard)"""
+        C = self.C
+        self.ps.derive(i)
+        pp = self.ps.pic_params(i)
+        rs = (C.c_int32 * (2 * 16))()
+        for l in range(2):
+            for r in range(pp.num_ref[l]):
+                poc = int(pp.ref_poc[l][r])
+                j = next(k for k in self.refs[i] if self.info[k]["poc"] == poc)
+                rs[l * 16 + r] = self.slots[j]
+        h = C.c_void_p()
+        rc = self.L.vvcp_plan_picture_rows(self.ps.h, i, C.byref(self.sp), self.slots[i], rs, N.STAGE_ALL, self.y0, self.y1,
+                                           C.byref(h))
+        if rc != 0:
+            raise RuntimeError("picture %d plan: %s" % (i, self.L.vvcp_last_error().decode()))
+        pic = N.Picture.wrap(h)
+        c = pic.work_counts()
+        self.ndmvr[i] = c["dmvr"]
+        reach = max(0, self.y0 - c["ref_y0"], c["ref_y1"] - self.y1) if c["ref_y1"] > c["ref_y0"] else 0
+        if self.handle[i] is not None:
+            self.ctx.release(self.handle[i])
+        self.handle[i] = self.ctx.prepare_planned(pic)
+        pic.close()
+        self.reach = max(self.reach, reach)
+        return reach
+
+    def ref_lists(self, i, M):
+        """(slot, (sends, recvs)) reference-halo exchanges picture i needs at reach M (rows rounded to 8)"""
+        M = int(-(-M // 8) * 8)
+        out = []
+        if self.world == 1 or M <= 0:
+            return out
+        for j in self.refs[i]:
+            s = self.slots[j]
+            if self.depth.get(s, 0) >= M:
+                continue
+            self.depth[s] = M
+            self.M = M
+            out.append((s, self.ref_halo()))
+        return out
+
+    def launch_recon(self, i):
+        self.depth[self.slots[i]] = 0   # the slot's new picture: no rows exchanged yet
+        self.ctx.launch_stages(self.handle[i], STAGES_RECON)
+
+    def launch_lf(self, i):
+        self.ctx.launch_stages(self.handle[i], STAGES_LF)
+        if not self.ref_later[i]:
+            self.refined[i] = True   # nobody reads its motion
+        # handles of pictures well behind whose deltas were consumed (a release waits for the picture)
+        for k in range(i - 8):
+            if self.handle[k] is not None and self.refined[k]:
+                self.ctx.release(self.handle[k])
+                self.handle[k] = None
+
+    def release(self):
+        for k in range(self.n):
+            if self.handle[k] is not None:
+                self.ctx.release(self.handle[k])
+                self.handle[k] = None
+        self.ps.close()
+
+
+def decode_stream_picture(rk, comm, i):
+    """picture i on one rank of a torch.distributed job (the other ranks run the same calls)"""
+    rk.parse(i)
+    for j in rk.pending(i):
+        mine = rk.local_deltas(j)
+        rk.refine(j, comm.all_gather_rows(mine) if rk.world > 1 else [mine])
+    reach = rk.plan(i)
+    M = comm.max_int(reach) if rk.world > 1 else 0
+    for slot, lists in rk.ref_lists(i, M):
+        exchange(rk, comm, lists, slot)
+    rk.launch_recon(i)
+    if rk.world > 1:
+        exchange(rk, comm, rk.lf_halo(), rk.slots[i])
+    rk.launch_lf(i)
+
+
+def decode_stream_local(ranks, comm, i):
+    """picture i on every rank emulated in one process (LocalComm): the same phases, all ranks at a time"""
+    for rk in ranks:
+        rk.parse(i)
+    for j in ranks[0].pending(i):
+        parts = [rk.local_deltas(j) for rk in ranks]
+        for rk in ranks:
+            rk.refine(j, parts)
+    M = max(rk.plan(i) for rk in ranks)
+
+    def phase(lists_of, slot_of):
+        staged = []
+        for rk in ranks:
+            for slot, (sends, recvs) in lists_of(rk):
+                for peer, y0, n in sends:
+                    buf = comm.buffer(rk, rk.ctx.rows_bytes(n))
+                    rk.ctx.export_rows(slot, y0, n, buf.data_ptr())
+                    comm.box[(rk.rank, peer, slot)] = buf
+                staged.append((rk, slot, recvs))
+        for rk, slot, recvs in staged:
+            for peer, y0, n in recvs:
+                rk.ctx.import_rows(slot, y0, n, comm.box.pop((peer, rk.rank, slot)).data_ptr())
+    if len(ranks) > 1:
+        phase(lambda rk: rk.ref_lists(i, M), None)
+    for rk in ranks:
+        rk.launch_recon(i)
+    if len(ranks) > 1:
+        phase(lambda rk: [(rk.slots[i], rk.lf_halo())], None)
+    for rk in ranks:
+        rk.launch_lf(i)
+
+
 def plan_and_reach(ranks, comm=None):
     """the sequence's motion reach: max over ranks (all-reduce when the ranks are in other processes)"""
     M = max(r.reach for r in ranks)
@@ -235,6 +438,24 @@ class TorchComm:
         x = t.tensor([v], dtype=t.int64, device=self.device if self.gpu else "cpu")
         self.dist.all_reduce(x, op=self.dist.ReduceOp.MAX)
         return int(x.item())
+
+    def all_gather_rows(self, a):
+        """every rank's int32 array (rows of 2), in rank order: counts first, then one padded all-gather"""
+        t, dist = self.torch, self.dist
+        dev = self.device if self.gpu else "cpu"
+        a = np.ascontiguousarray(a, np.int32).reshape(-1)
+        world = dist.get_world_size()
+        n = t.tensor([a.size], dtype=t.int64, device=dev)
+        ns = [t.zeros(1, dtype=t.int64, device=dev) for _ in range(world)]
+        dist.all_gather(ns, n)
+        ns = [int(x.item()) for x in ns]
+        m = max(max(ns), 1)
+        x = t.zeros(m, dtype=t.int32, device=dev)
+        if a.size:
+            x[:a.size] = t.from_numpy(a).to(dev)
+        outs = [t.zeros(m, dtype=t.int32, device=dev) for _ in range(world)]
+        dist.all_gather(outs, x)
+        return [o[:k].cpu().numpy().reshape(-1, 2) for o, k in zip(outs, ns)]
 
 
 class LocalComm:
