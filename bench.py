@@ -125,60 +125,64 @@ def cpu_baseline(stream_bin, pixels_per_run, min_seconds=10.0, max_runs=40):
 
 
 def shard_bench(a, R):
-    """BASELINE config 4: one tile-row stream decoded by all ranks together, each rank reconstructing and
-    filtering its own rows (vvc_amd/shard.py) and exchanging only the loop-filter halo (24 pre-deblocking
-    rows per edge) and the motion-reach rows of reference pictures with its neighbours over RCCL.
-    Strong scaling: the whole job decodes every picture once per step. Checked bit-exact afterwards:
-    rank 0 gathers every rank's rows of each slot's last picture and compares its MD5s."""
+    """BASELINE config 4 end to end from the bitstream: one tile-row stream decoded by all ranks together
+    (vvc_amd/shard.py StreamShardRank). Every rank parses the .bin (CABAC, motion derivation with the
+    all-gathered DMVR deltas of each reference), plans and reconstructs its own tile rows, and exchanges
+    only the loop-filter halo (24 pre-deblocking rows per edge) and, per picture, the motion reach of its
+    references with its neighbours over torch.distributed (RCCL on the GPU box). Strong scaling: the whole
+    job decodes every picture once per step; parse + derive + plan + upload + GPU are all in the timed
+    region. Checked bit-exact afterwards: rank 0 gathers every rank's rows of each picture and compares
+    its MD5s."""
+    from vvc_amd import parser as PZ
     from vvc_amd import shard as SH
-    d = os.path.join(ROOT, "tests", "golden", a.shard_stream)
-    if not os.path.isdir(d):
+    path = os.path.join(ROOT, "tests", "golden", "streams", a.shard_stream + ".bin")
+    if not os.path.exists(path):
         return None
-    pics = S.load_sequence(d)
-    meta = S.load_meta(d)
-    h0 = pics[0]["hdr"]
-    W, H = h0["width"], h0["height"]
+    with open(path, "rb") as f:
+        data = f.read()
+    meta = S.load_meta(os.path.join(ROOT, "tests", "golden", a.shard_stream))
+    ps = PZ.Stream(data)
+    inf = ps.info(0)
+    npic = len(ps)
+    ps.close()
+    W, H = inf["width"], inf["height"]
     slots = 8
-    ctx = N.Context(W, H, bit_depth=h0["bitdepth_y"], ctu_log2=h0["ctu_log2"], dpb_slots=slots,
+    ctx = N.Context(W, H, bit_depth=inf["bit_depth"], ctu_log2=inf["ctu_log2"], dpb_slots=slots,
                     device=int(os.environ.get("VVCR_DEVICE", R.local)))
-    t0 = time.perf_counter()
-    rk = SH.ShardRank(ctx, pics, R.rank, R.world, slots)
-    t_plan = time.perf_counter() - t0
     comm = SH.TorchComm(R.device) if R.world > 1 else None
-    M = SH.plan_and_reach([rk], comm)
     ctx.set_timing(False)
 
-    def step():
-        for i in range(len(pics)):
-            SH.decode_picture(rk, comm, i)
+    def decode(check):
+        rk = SH.StreamShardRank(ctx, data, R.rank, R.world, slots)
+        ok = True
+        for i in range(rk.n):
+            SH.decode_stream_picture(rk, comm, i)
+            if check:
+                SH.gather_to_root(rk, comm, rk.slots[i])
+                if R.rank == 0:
+                    got = D.plane_md5s([ctx.read_plane(N.BUF_RECO, rk.slots[i], c) for c in range(3)])
+                    ok = ok and got == meta["poc_plane_md5"][str(rk.info[i]["poc"])]
         ctx.sync()
-    for _ in range(max(1, a.warmup)):
-        step()
+        rows, reach = rk.rows, rk.reach
+        rk.release()
+        return ok, rows, reach
+    ok, rows, reach = decode(True)   # warm-up and parity
     R.barrier()
     t0 = time.perf_counter()
     for _ in range(a.shard_steps):
-        step()
+        decode(False)
     t1 = time.perf_counter()
     R.barrier()
     elapsed = R.max_over_ranks(t1 - t0)
-    owner = {}
-    for i, p in enumerate(pics):
-        owner[rk.slots[i]] = p["hdr"]["poc"]
-    ok = True
-    for slot, poc in sorted(owner.items()):
-        SH.gather_to_root(rk, comm, slot)
-        if R.rank == 0:
-            got = D.plane_md5s([ctx.read_plane(N.BUF_RECO, slot, c) for c in range(3)])
-            ok = ok and got == meta["poc_plane_md5"][str(poc)]
-    rk.release()
     ctx.close()
-    px = W * H * len(pics) * a.shard_steps
-    heights = [b - y for y, b in rk.rows]
+    px = W * H * npic * a.shard_steps
     return {"value": round(px / elapsed / 1e6, 2), "unit": "Mpixels/s", "n_gpus": R.world, "scaling": "strong",
-            "stream": a.shard_stream, "picture": "%dx%d" % (W, H), "pictures_per_step": len(pics), "steps": a.shard_steps,
-            "ms_per_step": round(elapsed / a.shard_steps * 1e3, 3), "shard_rows": heights, "lf_halo_rows": SH.LF_HALO,
-            "ref_halo_rows": M, "host_plan_s": round(t_plan, 3), "bitexact_vs_reference": bool(ok) if R.rank == 0 else None,
-            "note": "tile-row shards, halo exchange over torch.distributed %s point to point" % (R.dist.get_backend() if R.dist else "-")}
+            "stream": a.shard_stream, "picture": "%dx%d" % (W, H), "pictures_per_step": npic, "steps": a.shard_steps,
+            "ms_per_step": round(elapsed / a.shard_steps * 1e3, 3), "shard_rows": [b - y for y, b in rows],
+            "lf_halo_rows": SH.LF_HALO, "max_ref_reach_rows": reach, "bitexact_vs_reference": bool(ok) if R.rank == 0 else None,
+            "scope": "from the bitstream: parse + motion derivation + shard planning + upload + GPU + halo exchanges",
+            "note": "tile-row shards, halos over torch.distributed %s point to point, DMVR deltas all-gathered" % (
+                R.dist.get_backend() if R.dist else "-")}
 
 
 class BitstreamE2E:

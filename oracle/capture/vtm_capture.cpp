@@ -13,14 +13,18 @@
 // Usage: VVCR_CAPTURE_DIR=<dir> vtm_capture -b stream.bin [-o out.yuv]   (DecoderApp options)
 // Output: <dir>/pic_<decodeidx>.cap  — chunk format read by vvc_amd/capfile.py
 //
-// Built with -DVVCR_DROPIN (oracle/ref.mk: oracle/_ref/vtm_vvcr) the same source is the drop-in
-// demonstration of INTEGRATION.md: DecoderApp (DecApp/DecLib unchanged, linked against libvvcr.so) whose
-// decoded pictures come from libvvcr. At DecLib::executeLoopFilters (DecLib.cpp:560) the picture's
-// descriptors go to vvcr_begin_picture / vvcr_submit / vvcr_set_loop_filter_params / vvcr_end_picture;
-// the GPU's final picture (vvcr_read_picture) overwrites the reference's reconstruction before DecApp
-// writes it (DecApp::xWriteOutput) and before later pictures predict from it, and the GPU's DMVR
-// refinements (vvcr_get_dmvr_deltas) replace the reference's before CS::setRefinedMotionField
-// (DecLib.cpp:579), so later pictures' temporal candidates come from libvvcr too.
+// Built with -DVVCR_DROPIN (oracle/ref.mk: oracle/_ref/vtm_vvcr) the same source is the drop-in of
+// DecoderApp (DecApp / DecLib / DecCu unchanged, linked against libvvcr.so) whose
+// reconstruction and loop filters are REPLACED by libvvcr. DecCu still parses and derives motion; its
+// calls into the reference's prediction, transforms and LMCS mapping return without running (the
+// wrappers below only record what the descriptors need: TU QPs, GEO candidates), and
+// DecLib::executeLoopFilters (DecLib.cpp:560) is replaced: the picture's descriptors go to
+// vvcr_begin_picture / vvcr_submit / vvcr_set_loop_filter_params / vvcr_end_picture, libvvcr's final
+// picture (vvcr_read_picture) fills the reference's picture buffer (which the reference never wrote)
+// before DecLib's MD5 check, DecApp::xWriteOutput and later pictures' parsing read it, and libvvcr's
+// DMVR refinements (vvcr_get_dmvr_deltas) feed CS::setRefinedMotionField (DecLib.cpp:579), so later
+// pictures' temporal candidates come from libvvcr too. The calls into the reference's reconstruction
+// that ran are counted and reported (zero).
 
 #include <cstdio>
 #include <cstdlib>
@@ -123,6 +127,18 @@ static bool g_trace = getenv("VVCR_CAPTURE_TRACE") != nullptr;
 #define TR(x) do { if (g_trace) fprintf(stderr, "[cap] %s\n", x); } while (0)
 static int g_picCounter = 0;
 static PicCapture g_cap;
+// calls into the reference's reconstruction and loop filters that actually ran (__real_*): the drop-in
+// build runs none of them (main reports the counts, tests/test_dropin_gpu.py checks they are zero)
+enum { RC_FILTER_HOR, RC_MC, RC_MC_GEO, RC_INTRA, RC_ITX, RC_DBK, RC_SAO, RC_N };
+static const char *kRcName[RC_N] = {"InterpolationFilter::filterHor", "InterPrediction::motionCompensation",
+                                    "InterPrediction::motionCompensationGeo", "IntraPrediction::predIntra*",
+                                    "TrQuant::invTransformNxN", "LoopFilter::loopFilterPic", "SampleAdaptiveOffset::SAOProcess"};
+static long g_refCalls[RC_N] = {};
+#ifdef VVCR_DROPIN
+static const bool g_replace = true;    // the reference's reconstruction is replaced, not run
+#else
+static const bool g_replace = false;
+#endif
 
 static void initPlanes(const CodingStructure &cs) {
   if (g_dir.empty()) return;   // not capturing: wrappers only forward
@@ -645,7 +661,6 @@ static std::map<std::string, Chunk> g_mem;
 static vvcr_ctx *g_vvcr = nullptr;
 static const int kSlots = 24;
 static std::map<int, int> g_slotOfPoc;   // POC -> DPB slot of libvvcr (slot = decode index mod kSlots)
-static int g_mismatch = 0;                // pictures whose libvvcr result differs from the reference's own
 
 template <class T> static const T *chunk(const char *name, size_t *n = nullptr) {
   auto it = g_mem.find(name);
@@ -789,19 +804,16 @@ static void dropinPicture(CodingStructure &cs) {
     stride[c] = (int32_t)reco.bufs[c].width;
   }
   vcheck(vvcr_read_picture(g_vvcr, slot, ptr, stride), "vvcr_read_picture");
-  bool same = true;
+  // the reference never reconstructed this picture: its buffer holds libvvcr's samples only (DecLib's MD5
+  // check of the decoded-picture-hash SEI and DecApp's output read them)
   for (int c = 0; c < 3; c++) {
     PelBuf &b = reco.bufs[c];
     for (int y = 0; y < (int)b.height; y++) {
       Pel *row = b.buf + (size_t)y * b.stride;
       const uint16_t *src = planes[c].data() + (size_t)y * b.width;
-      for (int x = 0; x < (int)b.width; x++) {
-        same &= row[x] == (Pel)src[x];
-        row[x] = (Pel)src[x];
-      }
+      for (int x = 0; x < (int)b.width; x++) row[x] = (Pel)src[x];
     }
   }
-  g_mismatch += !same;
   // DMVR: libvvcr's refinements replace the reference's before CS::setRefinedMotionField
   size_t nd;
   chunk<int32_t>("dmvr_delta", &nd);
@@ -861,14 +873,34 @@ void __wrap__ZN6DecLib18executeLoopFiltersEv(DecLib *self) {
   if (!self->m_pcPic || g_dir.empty()) { __real__ZN6DecLib18executeLoopFiltersEv(self); return; }
   CodingStructure &cs = *self->m_pcPic->cs;
 #ifdef VVCR_DROPIN
+  // DecLib::executeLoopFilters (DecLib.cpp:560-623) REPLACED: the reference's deblocking, SAO and ALF do
+  // not run. What the decoder state needs from it is kept: the reshaper's flag (:570-576), the SAO
+  // parameters with merges resolved (SAOProcess's first step, SampleAdaptiveOffset.cpp:623) and the ALF
+  // filters of the slice's APSs (ALFProcess's reconstructCoeffAPSs, AdaptiveLoopFilter.cpp:439) as
+  // libvvcr's parameters, and CS::setRefinedMotionField (:579) with libvvcr's DMVR refinements.
   g_mem.clear();
   g_file.mem = &g_mem;
   if (!g_cap.active) initPlanes(cs);   // an intra picture without inter CUs
+  dumpDescriptors(g_file, *self, cs);
+  if (cs.sps->getUseLmcs() && self->m_cReshaper.getSliceReshaperInfo().getUseSliceReshaper()) self->m_cReshaper.setRecReshaped(false);
+  if (cs.sps->getSAOEnabledFlag()) {
+    self->m_cSAO.xReconstructBlkSAOParams(cs, cs.picture->getSAO());
+    dumpSao(g_file, cs);
+  }
+  if (cs.sps->getALFEnabledFlag()) {
+    Slice &sl = *cs.slice;
+    if (sl.getTileGroupAlfEnabledFlag(COMPONENT_Y) || sl.getTileGroupAlfEnabledFlag(COMPONENT_Cb) || sl.getTileGroupAlfEnabledFlag(COMPONENT_Cr))
+      self->m_cALF.reconstructCoeffAPSs(cs, true, sl.getTileGroupAlfEnabledFlag(COMPONENT_Cb) || sl.getTileGroupAlfEnabledFlag(COMPONENT_Cr), false);
+    dumpAlf(g_file, *self, cs);
+  }
+  dropinPicture(cs);
+  CS::setRefinedMotionField(cs);
+  g_cap.active = false;
+  g_picCounter++;
 #else
   char path[512];
   snprintf(path, sizeof path, "%s/pic_%03d.cap", g_dir.c_str(), g_picCounter);
   g_file.open(path);
-#endif
   snapStage(ST_PRELF);
   dumpDescriptors(g_file, *self, cs);
   __real__ZN6DecLib18executeLoopFiltersEv(self);
@@ -877,11 +909,6 @@ void __wrap__ZN6DecLib18executeLoopFiltersEv(DecLib *self) {
   snapStage(ST_ALF);
   if (cs.sps->getALFEnabledFlag()) dumpAlf(g_file, *self, cs);
   TR("alf dumped");
-#ifdef VVCR_DROPIN
-  dropinPicture(cs);
-  g_cap.active = false;
-  g_picCounter++;
-#else
   finishCapture();
 #endif
 }
@@ -890,6 +917,7 @@ void __wrap__ZN6DecLib18executeLoopFiltersEv(DecLib *self) {
 void __real__ZN10LoopFilter13loopFilterPicER15CodingStructure(LoopFilter *self, CodingStructure &cs);
 void __wrap__ZN10LoopFilter13loopFilterPicER15CodingStructure(LoopFilter *self, CodingStructure &cs) {
   snapStage(ST_DBKIN);
+  g_refCalls[RC_DBK]++;
   __real__ZN10LoopFilter13loopFilterPicER15CodingStructure(self, cs);
   snapStage(ST_DBK);
 }
@@ -897,6 +925,7 @@ void __wrap__ZN10LoopFilter13loopFilterPicER15CodingStructure(LoopFilter *self, 
 // SampleAdaptiveOffset::SAOProcess(CodingStructure&, SAOBlkParam*)
 void __real__ZN20SampleAdaptiveOffset10SAOProcessER15CodingStructureP11SAOBlkParam(SampleAdaptiveOffset *self, CodingStructure &cs, SAOBlkParam *p);
 void __wrap__ZN20SampleAdaptiveOffset10SAOProcessER15CodingStructureP11SAOBlkParam(SampleAdaptiveOffset *self, CodingStructure &cs, SAOBlkParam *p) {
+  g_refCalls[RC_SAO]++;
   __real__ZN20SampleAdaptiveOffset10SAOProcessER15CodingStructureP11SAOBlkParam(self, cs, p);
   snapStage(ST_SAO);
   if (g_cap.active) dumpSao(g_file, cs);   // parameters are merge-resolved in place by SAOProcess
@@ -905,6 +934,8 @@ void __wrap__ZN20SampleAdaptiveOffset10SAOProcessER15CodingStructureP11SAOBlkPar
 // InterPrediction::motionCompensation(CodingUnit&, RefPicList const&, bool, bool)
 void __real__ZN15InterPrediction18motionCompensationER10CodingUnitRK10RefPicListbb(InterPrediction *self, CodingUnit &cu, const RefPicList &l, bool luma, bool chroma);
 void __wrap__ZN15InterPrediction18motionCompensationER10CodingUnitRK10RefPicListbb(InterPrediction *self, CodingUnit &cu, const RefPicList &l, bool luma, bool chroma) {
+  if (g_replace) { if (!g_cap.active) initPlanes(*cu.cs); return; }   // libvvcr predicts (k_mc, DMVR / BDOF, affine)
+  g_refCalls[RC_MC]++;
   __real__ZN15InterPrediction18motionCompensationER10CodingUnitRK10RefPicListbb(self, cu, l, luma, chroma);
   if (!g_cap.active || g_cap.cs != cu.cs) { if (!g_cap.active) initPlanes(*cu.cs); }
   setCtu(*cu.cs, cu.lumaPos().x, cu.lumaPos().y);
@@ -931,7 +962,9 @@ void __wrap__ZN15InterPrediction21motionCompensationGeoER10CodingUnitR8MergeCtx(
     const MvField &f = (o[0] == 2) ? f1 : f0;
     o[1] = (o[0] == 2) ? 1 : 0; o[2] = f.refIdx; o[3] = f.mv.hor; o[4] = f.mv.ver; o[5] = m.useAltHpelIf[i];
   }
-  g_cap.geo[&cu] = g;
+  g_cap.geo[&cu] = g;   // the candidates are descriptor rows (vvcr_geo); the blend is libvvcr's in the drop-in
+  if (g_replace) return;
+  g_refCalls[RC_MC_GEO]++;
   __real__ZN15InterPrediction21motionCompensationGeoER10CodingUnitR8MergeCtx(self, cu, m);
   setCtu(*cu.cs, cu.lumaPos().x, cu.lumaPos().y);
   PelUnitBuf pb = cu.cs->getPredBuf(cu);
@@ -945,6 +978,8 @@ void __wrap__ZN15InterPrediction21motionCompensationGeoER10CodingUnitR8MergeCtx(
 // IntraPrediction::geneWeightedPred(ComponentID, PelBuf&, PU const&, Pel*)   (CIIP blend -> final pred)
 void __real__ZN15IntraPrediction16geneWeightedPredE11ComponentIDR7AreaBufIsERK14PredictionUnitPs(IntraPrediction *self, ComponentID c, PelBuf &pred, const PredictionUnit &pu, Pel *src);
 void __wrap__ZN15IntraPrediction16geneWeightedPredE11ComponentIDR7AreaBufIsERK14PredictionUnitPs(IntraPrediction *self, ComponentID c, PelBuf &pred, const PredictionUnit &pu, Pel *src) {
+  if (g_replace) return;
+  g_refCalls[RC_INTRA]++;
   __real__ZN15IntraPrediction16geneWeightedPredE11ComponentIDR7AreaBufIsERK14PredictionUnitPs(self, c, pred, pu, src);
   if (!g_cap.active) return;
   setCtu(*pu.cs, pu.lumaPos().x, pu.lumaPos().y);
@@ -962,18 +997,24 @@ static void recordIntra(const PredictionUnit &pu, ComponentID c, const PelBuf &p
 // IntraPrediction::predIntraAng(ComponentID, PelBuf&, PU const&)
 void __real__ZN15IntraPrediction12predIntraAngE11ComponentIDR7AreaBufIsERK14PredictionUnit(IntraPrediction *self, ComponentID c, PelBuf &pred, const PredictionUnit &pu);
 void __wrap__ZN15IntraPrediction12predIntraAngE11ComponentIDR7AreaBufIsERK14PredictionUnit(IntraPrediction *self, ComponentID c, PelBuf &pred, const PredictionUnit &pu) {
+  if (g_replace) { if (!g_cap.active) initPlanes(*pu.cs); return; }
+  g_refCalls[RC_INTRA]++;
   __real__ZN15IntraPrediction12predIntraAngE11ComponentIDR7AreaBufIsERK14PredictionUnit(self, c, pred, pu);
   recordIntra(pu, c, pred);
 }
 // IntraPrediction::predIntraMip(ComponentID, PelBuf&, PU const&)
 void __real__ZN15IntraPrediction12predIntraMipE11ComponentIDR7AreaBufIsERK14PredictionUnit(IntraPrediction *self, ComponentID c, PelBuf &pred, const PredictionUnit &pu);
 void __wrap__ZN15IntraPrediction12predIntraMipE11ComponentIDR7AreaBufIsERK14PredictionUnit(IntraPrediction *self, ComponentID c, PelBuf &pred, const PredictionUnit &pu) {
+  if (g_replace) { if (!g_cap.active) initPlanes(*pu.cs); return; }
+  g_refCalls[RC_INTRA]++;
   __real__ZN15IntraPrediction12predIntraMipE11ComponentIDR7AreaBufIsERK14PredictionUnit(self, c, pred, pu);
   recordIntra(pu, c, pred);
 }
 // IntraPrediction::predIntraChromaLM(ComponentID, PelBuf&, PU const&, CompArea const&, int)
 void __real__ZN15IntraPrediction17predIntraChromaLME11ComponentIDR7AreaBufIsERK14PredictionUnitRK8CompAreai(IntraPrediction *self, ComponentID c, PelBuf &pred, const PredictionUnit &pu, const CompArea &a, int mode);
 void __wrap__ZN15IntraPrediction17predIntraChromaLME11ComponentIDR7AreaBufIsERK14PredictionUnitRK8CompAreai(IntraPrediction *self, ComponentID c, PelBuf &pred, const PredictionUnit &pu, const CompArea &a, int mode) {
+  if (g_replace) { if (!g_cap.active) initPlanes(*pu.cs); return; }
+  g_refCalls[RC_INTRA]++;
   __real__ZN15IntraPrediction17predIntraChromaLME11ComponentIDR7AreaBufIsERK14PredictionUnitRK8CompAreai(self, c, pred, pu, a, mode);
   recordIntra(pu, c, pred);
 }
@@ -981,12 +1022,15 @@ void __wrap__ZN15IntraPrediction17predIntraChromaLME11ComponentIDR7AreaBufIsERK1
 // TrQuant::invTransformNxN(TransformUnit&, ComponentID const&, PelBuf&, QpParam const&)
 void __real__ZN7TrQuant15invTransformNxNER13TransformUnitRK11ComponentIDR7AreaBufIsERK7QpParam(TrQuant *self, TransformUnit &tu, const ComponentID &c, PelBuf &resi, const QpParam &q);
 void __wrap__ZN7TrQuant15invTransformNxNER13TransformUnitRK11ComponentIDR7AreaBufIsERK7QpParam(TrQuant *self, TransformUnit &tu, const ComponentID &c, PelBuf &resi, const QpParam &q) {
-  __real__ZN7TrQuant15invTransformNxNER13TransformUnitRK11ComponentIDR7AreaBufIsERK7QpParam(self, tu, c, resi, q);
+  if (!g_replace) {
+    g_refCalls[RC_ITX]++;
+    __real__ZN7TrQuant15invTransformNxNER13TransformUnitRK11ComponentIDR7AreaBufIsERK7QpParam(self, tu, c, resi, q);
+  }
   if (!g_cap.active) initPlanes(*tu.cs);
   { const CompArea &a = tu.blocks[c]; setCtu(*tu.cs, a.x << (c ? 1 : 0), a.y << (c ? 1 : 0)); }
-  auto &e = g_cap.tuqp[&tu];
-  static bool init = false; (void)init;
+  auto &e = g_cap.tuqp[&tu];   // the block's QPs (QpParam, Quant.h:68) are descriptor fields
   e[c * 2] = q.Qps[0]; e[c * 2 + 1] = q.Qps[1];
+  if (g_replace) return;
   int x, y;
   if (locate(*tu.cs, PIC_RESIDUAL, c, resi.buf, x, y)) copyBlock(g_cap.resi[c], resi, x, y);
 }
@@ -994,6 +1038,7 @@ void __wrap__ZN7TrQuant15invTransformNxNER13TransformUnitRK11ComponentIDR7AreaBu
 // TrQuant::invTransformICT(TransformUnit const&, PelBuf&, PelBuf&)
 void __real__ZN7TrQuant15invTransformICTERK13TransformUnitR7AreaBufIsES5_(TrQuant *self, const TransformUnit &tu, PelBuf &cb, PelBuf &cr);
 void __wrap__ZN7TrQuant15invTransformICTERK13TransformUnitR7AreaBufIsES5_(TrQuant *self, const TransformUnit &tu, PelBuf &cb, PelBuf &cr) {
+  if (g_replace) return;
   __real__ZN7TrQuant15invTransformICTERK13TransformUnitR7AreaBufIsES5_(self, tu, cb, cr);
   if (!g_cap.active) return;
   { const CompArea &a = tu.blocks[1]; setCtu(*tu.cs, a.x << 1, a.y << 1); }
@@ -1005,6 +1050,7 @@ void __wrap__ZN7TrQuant15invTransformICTERK13TransformUnitR7AreaBufIsES5_(TrQuan
 // AreaBuf<Pel>::scaleSignal(int, bool, ClpRng const&)  (LMCS chroma residual scaling -> final residual)
 void __real__ZN7AreaBufIsE11scaleSignalEibRK6ClpRng(PelBuf *self, int scale, bool dir, const ClpRng &r);
 void __wrap__ZN7AreaBufIsE11scaleSignalEibRK6ClpRng(PelBuf *self, int scale, bool dir, const ClpRng &r) {
+  if (g_replace) return;
   __real__ZN7AreaBufIsE11scaleSignalEibRK6ClpRng(self, scale, dir, r);
   if (!g_cap.active) return;
   for (int c = 1; c < 3; c++) {
@@ -1016,10 +1062,19 @@ void __wrap__ZN7AreaBufIsE11scaleSignalEibRK6ClpRng(PelBuf *self, int scale, boo
 // AreaBuf<Pel>::rspSignal(std::vector<Pel>&)  (LMCS forward map of an inter prediction -> final prediction)
 void __real__ZN7AreaBufIsE9rspSignalERSt6vectorIsSaIsEE(PelBuf *self, std::vector<Pel> &lut);
 void __wrap__ZN7AreaBufIsE9rspSignalERSt6vectorIsSaIsEE(PelBuf *self, std::vector<Pel> &lut) {
+  if (g_replace) return;
   __real__ZN7AreaBufIsE9rspSignalERSt6vectorIsSaIsEE(self, lut);
   if (!g_cap.active) return;
   int x, y;
   if (locate(*g_cap.cs, PIC_PREDICTION, 0, self->buf, x, y)) copyBlock(g_cap.pfin[0], *self, x, y);
+}
+
+// InterpolationFilter::filterHor (InterpolationFilter.cpp:743): counted only, to show that nothing of the
+// reference's motion compensation runs in the drop-in
+void __real__ZN19InterpolationFilter9filterHorE11ComponentIDPKsiPsiiiib12ChromaFormatRK6ClpRngibb(InterpolationFilter *self, ComponentID c, const Pel *src, int ss, Pel *dst, int ds, int w, int h, int frac, bool last, ChromaFormat f, const ClpRng &r, int idx, bool dmvr, bool alt);
+void __wrap__ZN19InterpolationFilter9filterHorE11ComponentIDPKsiPsiiiib12ChromaFormatRK6ClpRngibb(InterpolationFilter *self, ComponentID c, const Pel *src, int ss, Pel *dst, int ds, int w, int h, int frac, bool last, ChromaFormat f, const ClpRng &r, int idx, bool dmvr, bool alt) {
+  g_refCalls[RC_FILTER_HOR]++;
+  __real__ZN19InterpolationFilter9filterHorE11ComponentIDPKsiPsiiiib12ChromaFormatRK6ClpRngibb(self, c, src, ss, dst, ds, w, h, frac, last, f, r, idx, dmvr, alt);
 }
 
 }  // extern "C"
@@ -1037,10 +1092,13 @@ int main(int argc, char *argv[]) {
   uint32_t ret = app->decode();
   delete app;
 #ifdef VVCR_DROPIN
-  fprintf(stderr, "vtm_vvcr: %d pictures decoded through libvvcr, %d differ from the reference's own reconstruction\n",
-          g_picCounter, g_mismatch);
+  long ran = 0;
+  for (int k = 0; k < RC_N; k++) ran += g_refCalls[k];
+  fprintf(stderr, "vtm_vvcr: %d pictures decoded through libvvcr, %ld calls into the reference's reconstruction and loop filters\n",
+          g_picCounter, ran);
+  for (int k = 0; k < RC_N; k++) fprintf(stderr, "vtm_vvcr:   %s %ld\n", kRcName[k], g_refCalls[k]);
   if (g_vvcr) vvcr_destroy(g_vvcr);
-  if (g_mismatch) return 2;
+  if (ran) return 2;
 #endif
   return ret != 0 ? 1 : 0;
 }

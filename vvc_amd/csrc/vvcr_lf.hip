@@ -5,9 +5,8 @@
 // reading the deblocked picture and writing the SAO picture (ping-pong, so neighbours are pre-SAO).
 //
 // ALF (AdaptiveLoopFilter::deriveClassificationBlk :873, filterBlk<7x7/5x5> :1085, filterBlkCcAlf :1328):
-// luma: one workgroup per 64x16 tile staged in LDS with its 3-sample halo (classification + filter);
-// chroma: one lane per chroma sample, 5x5 diamond and the CC-ALF luma->chroma correction fused; both in
-// one launch.
+// one workgroup per 64x16 luma region and its 32x8 chroma, all three planes staged in LDS with their
+// halos (classification + 7x7 luma filter, 5x5 chroma filter + CC-ALF from the staged luma).
 // Reads the SAO picture, writes the final picture. Coordinates are clamped to the picture
 // (equivalent to PelUnitBuf::extendBorderPel(3) on the ALF input, AdaptiveLoopFilter.cpp:411).
 #include "vvcr_internal.h"
@@ -115,37 +114,58 @@ __constant__ int8_t c_perm7[4][13] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12}
 __constant__ int8_t c_th[16] = {0, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 4};
 __constant__ int8_t c_transpose[8] = {0, 1, 0, 2, 2, 3, 1, 3};
 
-// Luma ALF, LDS-tiled: one 256-lane workgroup per 64x16 output tile. The tile plus its 3-sample halo
-// (the reach of both the 8x8 Laplacian window of a 4x4 block and the 7x7 diamond) is staged once with
-// coalesced row loads and picture-clamped coordinates; four lanes classify each 4x4 block (one
-// subsampled row pair each, reduced by shuffles), then each lane filters one column of one 4x4 block.
+// ALF of one region: 64x16 luma samples and the co-located 32x8 Cb and Cr samples, one 256-lane
+// workgroup. The luma tile with its 3-sample halo and both chroma tiles with their 2-sample halo are staged
+// in LDS once, by 16-byte loads of aligned 8-sample chunks (picture-clamped coordinates); then
+//   luma: four lanes classify each 4x4 block (one subsampled row pair each, reduced by shuffles), then
+//         each lane filters one column of one 4x4 block (7x7 diamond, packed 16-bit arithmetic);
+//   chroma: one lane per chroma position filters Cb and Cr (5x5 diamond) and adds the CC-ALF correction,
+//         whose luma taps (the same for both components) come from the staged luma tile.
+// Work is dispatched in XCD-contiguous runs of regions (xcd_swizzle), so the halo rows and columns a
+// region shares with its neighbours are fetched from HBM once per XCD, and the chroma work of a region
+// reads the luma its own workgroup staged (before r04 the chroma work was dispatched after all luma
+// tiles and re-read the luma from HBM: 3.2x the algorithmic bytes).
 constexpr int ALF_TW = 64, ALF_TH = 16, ALF_HALO = 3;
-constexpr int ALF_SW = ALF_TW + 2 * ALF_HALO + 2;   // LDS row pitch (72)
-constexpr int ALF_SH = ALF_TH + 2 * ALF_HALO;       // 22 rows
+constexpr int ALF_LX = 8;                            // staged luma columns left of the tile (one chunk)
+constexpr int ALF_SW = ALF_TW + 2 * ALF_LX;          // LDS row pitch (80): chunks [X0 - 8, X0 + 72)
+constexpr int ALF_SH = ALF_TH + 2 * ALF_HALO;        // 22 rows
+constexpr int ALF_LCH = ALF_SW / 8;                  // luma chunks per row (10)
+constexpr int ALF_CW = ALF_TW / 2, ALF_CHH = ALF_TH / 2;   // chroma region 32 x 8
+constexpr int ALF_CSW = ALF_CW + 16, ALF_CSH = ALF_CHH + 4; // chroma LDS: chunks [cx0 - 8, cx0 + 40), rows cy0 - 2 .. cy0 + 9
+constexpr int ALF_CCH = ALF_CSW / 8;                 // chroma chunks per row (6)
 
-__device__ __forceinline__ void alf_luma(const AlfParams &P, int tx, int ty) {
+// 8 samples of row y from column x0 (a multiple of 8), picture-clamped (one vector load when inside)
+__device__ __forceinline__ uint4 alf_chunk(const DPlane &S, int x0, int y) {
+  const int16_t *row = S.p + (size_t)clip3(0, S.h - 1, y) * S.stride;
+  if (x0 >= 0 && x0 + 8 <= S.w) return *(const uint4 *)(row + x0);
+  int v[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) v[e] = row[clip3(0, S.w - 1, x0 + e)];
+  return make_uint4((uint32_t)(uint16_t)v[0] | (uint32_t)v[1] << 16, (uint32_t)(uint16_t)v[2] | (uint32_t)v[3] << 16,
+                    (uint32_t)(uint16_t)v[4] | (uint32_t)v[5] << 16, (uint32_t)(uint16_t)v[6] | (uint32_t)v[7] << 16);
+}
+
+__device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
   const DPlane &S = P.src[0];
   const DPlane &D = P.dst[0];
-  __shared__ int16_t t[ALF_SH * ALF_SW];
+  __shared__ __attribute__((aligned(16))) int16_t t[ALF_SH * ALF_SW];
+  __shared__ __attribute__((aligned(16))) int16_t tc[2][ALF_CSH * ALF_CSW];
   __shared__ int32_t blk[(ALF_TW / 4) * (ALF_TH / 4)];   // class | transpose << 8 | enabled << 16
   __shared__ int16_t s_cf[25 * 13], s_cl[25 * 13];       // the CTB's filter set: coefficients / clips per class
   __shared__ int8_t s_perm[4 * 13];
   const int X0 = tx * ALF_TW, Y0 = P.y0 + ty * ALF_TH;
+  const int cx0 = X0 >> 1, cy0 = Y0 >> 1;
   const int tid = threadIdx.x;
   const int W = S.w, H = S.h;
-  // all of a lane's tile loads in flight first (one memory round trip), then the CTB's flag and filter
-  // set: a 64x16 tile lies in one CTB, so both are uniform (scalar loads, read together), and the set's 25
-  // classes of coefficients / clips are staged in LDS with the samples, so the per-lane class lookups of
-  // the filter read LDS instead of memory after the classification
-  constexpr int TWH = ALF_TW + 2 * ALF_HALO, NIT = (ALF_SH * TWH + 255) / 256;
-  int16_t v[NIT];
-#pragma unroll
-  for (int k = 0; k < NIT; k++) {
-    const int i = tid + 256 * k;
-    const int r = i / TWH, c = i - r * TWH;
-    const int sx = clip3(0, W - 1, X0 - ALF_HALO + c), sy = clip3(0, H - 1, Y0 - ALF_HALO + min(r, ALF_SH - 1));
-    v[k] = S.p[sy * S.stride + sx];
-  }
+  // every staging load in flight first (one memory round trip): a luma chunk per lane (220 of them) and a
+  // chroma chunk for 144 lanes; then the CTB's flag and filter set (a 64x16 tile lies in one CTB, so both
+  // are uniform), the set's 25 classes of coefficients / clips staged in LDS with the samples
+  uint4 lv = {}, cv = {};
+  const int lr = tid / ALF_LCH, lc = tid - lr * ALF_LCH;
+  if (tid < ALF_SH * ALF_LCH) lv = alf_chunk(S, X0 - ALF_LX + 8 * lc, Y0 - ALF_HALO + lr);
+  const int ccomp = tid / (ALF_CSH * ALF_CCH), ci = tid - ccomp * (ALF_CSH * ALF_CCH);
+  const int cr = ci / ALF_CCH, cc = ci - cr * ALF_CCH;
+  if (ccomp < 2) cv = alf_chunk(P.src[1 + ccomp], cx0 - 8 + 8 * cc, cy0 - 2 + cr);
   const int ctbT = (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2);
   const int ctbE = P.ctb_en[ctbT], set = P.ctb_set[ctbT];
   const bool ctbOn = P.en[0] && ctbE;
@@ -160,12 +180,8 @@ __device__ __forceinline__ void alf_luma(const AlfParams &P, int tx, int ty) {
       clv[q] = cl[i];
     }
   }
-#pragma unroll
-  for (int k = 0; k < NIT; k++) {
-    const int i = tid + 256 * k;
-    const int r = i / TWH, c = i - r * TWH;
-    if (i < ALF_SH * TWH) t[r * ALF_SW + c] = v[k];
-  }
+  if (tid < ALF_SH * ALF_LCH) *(uint4 *)&t[lr * ALF_SW + 8 * lc] = lv;
+  if (ccomp < 2) *(uint4 *)&tc[ccomp][cr * ALF_CSW + 8 * cc] = cv;
   if (ctbOn) {
 #pragma unroll
     for (int q = 0; q < NC; q++) {
@@ -175,8 +191,8 @@ __device__ __forceinline__ void alf_luma(const AlfParams &P, int tx, int ty) {
     if (tid < 4 * 13) s_perm[tid] = (&c_perm7[0][0])[tid];
   }
   __syncthreads();
-  // sample (x, y) in picture coordinates -> LDS (valid for |x - tile| <= 3 and |y - tile| <= 3)
-#define T(x, y) ((int)t[((y) - Y0 + ALF_HALO) * ALF_SW + (x) - X0 + ALF_HALO])
+  // sample (x, y) in picture coordinates -> LDS (valid for x in [X0 - 8, X0 + 72), y in [Y0 - 3, Y0 + 19))
+#define T(x, y) ((int)t[((y) - Y0 + ALF_HALO) * ALF_SW + (x) - X0 + ALF_LX])
   const int vbH = 1 << P.ctu_log2, vbPos = P.vb_luma;
   {
     // --- classification (deriveClassificationBlk): block b, subsampled row pair ii
@@ -228,149 +244,137 @@ __device__ __forceinline__ void alf_luma(const AlfParams &P, int tx, int ty) {
   }
   __syncthreads();
   // --- 7x7 diamond filter (filterBlk<ALF_FILTER_7>): lane = one column of one 4x4 block
-  const int x = X0 + (tid & 63), by = Y0 + (tid >> 6) * 4;
-  if (x >= W || by >= H) return;
-  const int bi = blk[((tid >> 6) << 4) + ((tid & 63) >> 2)];
-  int16_t *dst = D.p + x;
-  if (!(bi >> 16)) {
-    for (int y = by; y < by + 4 && y < H; y++) dst[(size_t)y * D.stride] = (int16_t)T(x, y);
-    return;
-  }
-  const int classIdx = bi & 255, tr = (bi >> 8) & 255;
-  const int16_t *coef = s_cf + classIdx * 13, *clip = s_cl + classIdx * 13;
-  // packed 16-bit arithmetic: the two samples of a tap pair as one int16x2 (differences to the centre
-  // fit 16 bits, clips <= 1 << bd), clipped with packed min / max, then one dot2 with the coefficient
-  // pair (c, c): exactly c * clip(a - cur) + c * clip(b - cur)
-  short2_t fcp[12], clp[12], cln[12];
+  {
+    const int x = X0 + (tid & 63), by = Y0 + (tid >> 6) * 4;
+    if (x < W && by < H) {
+      const int bi = blk[((tid >> 6) << 4) + ((tid & 63) >> 2)];
+      int16_t *dst = D.p + x;
+      if (!(bi >> 16)) {
+        for (int y = by; y < by + 4 && y < H; y++) dst[(size_t)y * D.stride] = (int16_t)T(x, y);
+      } else {
+        const int classIdx = bi & 255, tr = (bi >> 8) & 255;
+        const int16_t *coef = s_cf + classIdx * 13, *clip = s_cl + classIdx * 13;
+        // packed 16-bit arithmetic: the two samples of a tap pair as one int16x2 (differences to the centre
+        // fit 16 bits, clips <= 1 << bd), clipped with packed min / max, then one dot2 with the coefficient
+        // pair (c, c): exactly c * clip(a - cur) + c * clip(b - cur)
+        short2_t fcp[12], clp[12], cln[12];
 #pragma unroll
-  for (int k = 0; k < 12; k++) {
-    const int pk = s_perm[tr * 13 + k];
-    const int c = coef[pk], l = clip[pk];
-    fcp[k] = (short2_t){(short)c, (short)c};
-    clp[k] = (short2_t){(short)l, (short)l};
-    cln[k] = (short2_t){(short)-l, (short)-l};
-  }
-  const int maxv = (1 << P.bd) - 1;
+        for (int k = 0; k < 12; k++) {
+          const int pk = s_perm[tr * 13 + k];
+          const int c = coef[pk], l = clip[pk];
+          fcp[k] = (short2_t){(short)c, (short)c};
+          clp[k] = (short2_t){(short)l, (short)l};
+          cln[k] = (short2_t){(short)-l, (short)-l};
+        }
+        const int maxv = (1 << P.bd) - 1;
 #pragma unroll
-  for (int dy = 0; dy < 4; dy++) {
-    const int y = by + dy;
-    if (y >= H) break;
-    int r1, r2, r3, r4, r5, r6;
-    alf_rows(y, vbH, vbPos, true, r1, r2, r3, r4, r5, r6);
-    const int yVb = y & (vbH - 1);
-    const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
-    const int cur = T(x, y);
-    const short2_t cc = {(short)cur, (short)cur};
-    int sum = 0;
-    auto tap = [&](int k, int a, int b) {
-      short2_t d = (short2_t){(short)a, (short)b} - cc;
-      d = __builtin_elementwise_min(__builtin_elementwise_max(d, cln[k]), clp[k]);
-      sum = __builtin_amdgcn_sdot2(d, fcp[k], sum, false);
-    };
-    tap(0, T(x, r5), T(x, r6));
-    tap(1, T(x + 1, r3), T(x - 1, r4));
-    tap(2, T(x, r3), T(x, r4));
-    tap(3, T(x - 1, r3), T(x + 1, r4));
-    tap(4, T(x + 2, r1), T(x - 2, r2));
-    tap(5, T(x + 1, r1), T(x - 1, r2));
-    tap(6, T(x, r1), T(x, r2));
-    tap(7, T(x - 1, r1), T(x + 1, r2));
-    tap(8, T(x - 2, r1), T(x + 2, r2));
-    tap(9, T(x + 3, y), T(x - 3, y));
-    tap(10, T(x + 2, y), T(x - 2, y));
-    tap(11, T(x + 1, y), T(x - 1, y));
-    sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
-    dst[(size_t)y * D.stride] = (int16_t)clip3(0, maxv, sum + cur);
+        for (int dy = 0; dy < 4; dy++) {
+          const int y = by + dy;
+          if (y >= H) break;
+          int r1, r2, r3, r4, r5, r6;
+          alf_rows(y, vbH, vbPos, true, r1, r2, r3, r4, r5, r6);
+          const int yVb = y & (vbH - 1);
+          const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
+          const int cur = T(x, y);
+          const short2_t cc2 = {(short)cur, (short)cur};
+          int sum = 0;
+          auto tap = [&](int k, int a, int b) {
+            short2_t d = (short2_t){(short)a, (short)b} - cc2;
+            d = __builtin_elementwise_min(__builtin_elementwise_max(d, cln[k]), clp[k]);
+            sum = __builtin_amdgcn_sdot2(d, fcp[k], sum, false);
+          };
+          tap(0, T(x, r5), T(x, r6));
+          tap(1, T(x + 1, r3), T(x - 1, r4));
+          tap(2, T(x, r3), T(x, r4));
+          tap(3, T(x - 1, r3), T(x + 1, r4));
+          tap(4, T(x + 2, r1), T(x - 2, r2));
+          tap(5, T(x + 1, r1), T(x - 1, r2));
+          tap(6, T(x, r1), T(x, r2));
+          tap(7, T(x - 1, r1), T(x + 1, r2));
+          tap(8, T(x - 2, r1), T(x + 2, r2));
+          tap(9, T(x + 3, y), T(x - 3, y));
+          tap(10, T(x + 2, y), T(x - 2, y));
+          tap(11, T(x + 1, y), T(x - 1, y));
+          sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
+          dst[(size_t)y * D.stride] = (int16_t)clip3(0, maxv, sum + cur);
+        }
+      }
+    }
+  }
+  // --- chroma (filterBlk<ALF_FILTER_5> per component + filterBlkCcAlf): lane = one chroma position
+  {
+    const int x = cx0 + (tid & (ALF_CW - 1)), y = cy0 + tid / ALF_CW;
+    const DPlane &C1 = P.src[1];
+    if (x < C1.w && y < C1.h && y < (P.y1 >> 1)) {
+#define TC(k, xx, yy) ((int)tc[k][((yy) - cy0 + 2) * ALF_CSW + (xx) - cx0 + 8])
+      const int cl2 = P.ctu_log2 - 1;
+      const int ctb = (y >> cl2) * P.wc + (x >> cl2);
+      const int n = P.nctb;
+      const int maxv = (1 << P.bd) - 1;
+      const int vbHc = 1 << cl2, vbPosC = P.vb_chroma;
+      int r1, r2, r3, r4, r5, r6;
+      alf_rows(y, vbHc, vbPosC, false, r1, r2, r3, r4, r5, r6);
+      (void)r5; (void)r6;
+      const int lx = x * 2, ly = y * 2;
+      const int pos = ly & ((1 << P.ctu_log2) - 1);
+      int o1 = 1, o2 = -1, o3 = 2;
+      if (pos == P.vb_luma - 2 || pos == P.vb_luma + 1) o3 = o1;
+      else if (pos == P.vb_luma - 1 || pos == P.vb_luma) { o1 = 0; o2 = 0; o3 = 0; }
+      const int yVb = y & (vbHc - 1);
+      const bool nearVB = (yVb == vbPosC - 1) || (yVb == vbPosC);
+      // CC-ALF luma taps (clamped to the picture like the staged tile: AdaptiveLoopFilter.cpp:411)
+      auto L = [&](int xx, int yy) { return T(clip3(0, W - 1, xx), clip3(0, H - 1, yy)); };
+      int sl[8] = {};
+      if (P.en[3] || P.en[4]) {
+        sl[0] = L(lx, ly);
+        sl[1] = L(lx, ly + o2); sl[2] = L(lx - 1, ly); sl[3] = L(lx + 1, ly);
+        sl[4] = L(lx - 1, ly + o1); sl[5] = L(lx, ly + o1); sl[6] = L(lx + 1, ly + o1);
+        sl[7] = L(lx, ly + o3);
+      }
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        const int comp = 1 + k;
+        const DPlane &Sc = P.src[comp];
+        auto A = [&](int xx, int yy) { return TC(k, clip3(0, Sc.w - 1, xx), clip3(0, Sc.h - 1, yy)); };
+        const int cur = TC(k, x, y);
+        const bool on = P.en[comp] && P.ctb_en[comp * n + ctb];
+        const int alt = P.ctb_alt[comp * n + ctb];
+        const int ccf = P.en[2 + comp] ? P.cc_ctl[k * n + ctb] : 0;
+        int v = cur;
+        if (on) {
+          const int16_t *fc = P.chroma_coef + alt * 7, *fl = P.chroma_clip + alt * 7;
+          const int q[12] = {A(x, r3), A(x, r4), A(x + 1, r1), A(x - 1, r2), A(x, r1), A(x, r2),
+                             A(x - 1, r1), A(x + 1, r2), A(x + 2, y), A(x - 2, y), A(x + 1, y), A(x - 1, y)};
+          int sum = 0;
+#pragma unroll
+          for (int tt = 0; tt < 6; tt++) sum += fc[tt] * clip_alf(fl[tt], cur, q[2 * tt], q[2 * tt + 1]);
+          sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
+          v = clip3(0, maxv, sum + cur);
+        }
+        if (ccf) {
+          const int16_t *f = P.cc_coef + (k * 4 + ccf - 1) * 8;
+          const int c0 = sl[0];
+          int sum = 0;
+#pragma unroll
+          for (int tt = 0; tt < 7; tt++) sum += f[tt] * (sl[1 + tt] - c0);
+          sum = (sum + 64) >> 7;
+          const int off = (1 << P.bd) >> 1;
+          sum = clip3(0, maxv, sum + off) - off;
+          v = clip3(0, maxv, sum + v);
+        }
+        const DPlane &Dc = P.dst[comp];
+        Dc.p[(size_t)y * Dc.stride + x] = (int16_t)v;
+      }
+#undef TC
+    }
   }
 #undef T
 }
 
-// One lane per chroma position, Cb and Cr together: the CC-ALF luma taps (the same for both components)
-// are loaded once. Every sample load (the two 5x5 diamonds and the luma taps) is issued before the CTB
-// controls are known, so that the lane waits for one memory round trip plus the coefficient lookups, not a
-// chain of them.
-__device__ __forceinline__ void alf_chroma(const AlfParams &P, int x, int y) {
-  const DPlane &Y = P.src[0];
-  if (x >= P.src[1].w || y >= P.src[1].h || y >= (P.y1 >> 1)) return;
-  const int cl2 = P.ctu_log2 - 1;
-  const int ctb = (y >> cl2) * P.wc + (x >> cl2);
-  const int n = P.nctb;
-  const int maxv = (1 << P.bd) - 1;
-  const int vbH = 1 << cl2, vbPos = P.vb_chroma;
-  int r1, r2, r3, r4, r5, r6;
-  alf_rows(y, vbH, vbPos, false, r1, r2, r3, r4, r5, r6);
-  (void)r5; (void)r6;
-  int cur[2], sa[2][12] = {};
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    const DPlane &S = P.src[1 + k];
-    cur[k] = S.p[(size_t)y * S.stride + x];
-    if (P.en[1 + k]) {
-      int *q = sa[k];
-      q[0] = at(S, x, r3); q[1] = at(S, x, r4);
-      q[2] = at(S, x + 1, r1); q[3] = at(S, x - 1, r2);
-      q[4] = at(S, x, r1); q[5] = at(S, x, r2);
-      q[6] = at(S, x - 1, r1); q[7] = at(S, x + 1, r2);
-      q[8] = at(S, x + 2, y); q[9] = at(S, x - 2, y);
-      q[10] = at(S, x + 1, y); q[11] = at(S, x - 1, y);
-    }
-  }
-  const int lx = x * 2, ly = y * 2;
-  const int pos = ly & ((1 << P.ctu_log2) - 1);
-  int o1 = 1, o2 = -1, o3 = 2;
-  if (pos == P.vb_luma - 2 || pos == P.vb_luma + 1) o3 = o1;
-  else if (pos == P.vb_luma - 1 || pos == P.vb_luma) { o1 = 0; o2 = 0; o3 = 0; }
-  int sl[8] = {};
-  if (P.en[3] || P.en[4]) {
-    sl[0] = at(Y, lx, ly);
-    sl[1] = at(Y, lx, ly + o2); sl[2] = at(Y, lx - 1, ly); sl[3] = at(Y, lx + 1, ly);
-    sl[4] = at(Y, lx - 1, ly + o1); sl[5] = at(Y, lx, ly + o1); sl[6] = at(Y, lx + 1, ly + o1);
-    sl[7] = at(Y, lx, ly + o3);
-  }
-  const int yVb = y & (vbH - 1);
-  const bool nearVB = (yVb == vbPos - 1) || (yVb == vbPos);
-#pragma unroll
-  for (int k = 0; k < 2; k++) {
-    const int comp = 1 + k;
-    const bool on = P.en[comp] && P.ctb_en[comp * n + ctb];
-    const int alt = P.ctb_alt[comp * n + ctb];
-    const int ccf = P.en[2 + comp] ? P.cc_ctl[k * n + ctb] : 0;
-    int v = cur[k];
-    if (on) {
-      const int16_t *fc = P.chroma_coef + alt * 7, *fl = P.chroma_clip + alt * 7;
-      int sum = 0;
-#pragma unroll
-      for (int t = 0; t < 6; t++) sum += fc[t] * clip_alf(fl[t], cur[k], sa[k][2 * t], sa[k][2 * t + 1]);
-      sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
-      v = clip3(0, maxv, sum + cur[k]);
-    }
-    if (ccf) {
-      const int16_t *f = P.cc_coef + (k * 4 + ccf - 1) * 8;
-      const int c0 = sl[0];
-      int sum = 0;
-#pragma unroll
-      for (int t = 0; t < 7; t++) sum += f[t] * (sl[1 + t] - c0);
-      sum = (sum + 64) >> 7;
-      const int off = (1 << P.bd) >> 1;
-      sum = clip3(0, maxv, sum + off) - off;
-      v = clip3(0, maxv, sum + v);
-    }
-    const DPlane &D = P.dst[comp];
-    D.p[(size_t)y * D.stride + x] = (int16_t)v;
-  }
-}
-
-// Luma and chroma ALF in one launch: the first gx * gy workgroups are luma tiles, the others take 64
-// chroma columns x 4 rows (a wave per row) of Cb and Cr together.
-__global__ __launch_bounds__(256) void k_alf(AlfParams P, int gx, int gy, int gcx, int gcy) {
-  const int b = blockIdx.x;
-  if (b < gx * gy) {
-    alf_luma(P, b % gx, b / gx);
-    return;
-  }
-  const int r = b - gx * gy;
-  const int x = (r % gcx) * 64 + (threadIdx.x & 63), y = (P.y0 >> 1) + (r / gcx) * 4 + (threadIdx.x >> 6);
-  alf_chroma(P, x, y);
+// One launch, one workgroup per region; regions in XCD-contiguous runs (raster order within a run).
+__global__ __launch_bounds__(256) void k_alf(AlfParams P, int gx, int gy) {
+  const int b = xcd_swizzle(blockIdx.x, gridDim.x);
+  alf_region(P, b % gx, b / gx);
 }
 
 }  // namespace
@@ -404,6 +408,5 @@ void launch_planes3(const Planes3 &p, hipStream_t s) {
 void launch_alf(const AlfParams &p, hipStream_t s) {
   if (p.y1 <= p.y0) return;
   const int gx = (p.src[0].w + ALF_TW - 1) / ALF_TW, gy = (p.y1 - p.y0 + ALF_TH - 1) / ALF_TH;
-  const int gcx = (p.src[1].w + 63) / 64, gcy = (((p.y1 - p.y0) >> 1) + 3) / 4;
-  hipLaunchKernelGGL(k_alf, dim3(gx * gy + gcx * gcy), dim3(256), 0, s, p, gx, gy, gcx, gcy);
+  hipLaunchKernelGGL(k_alf, dim3(gx * gy), dim3(256), 0, s, p, gx, gy);
 }

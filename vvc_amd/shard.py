@@ -168,7 +168,7 @@ class StreamShardRank(ShardGeom):
       5. reconstruction stages, the loop-filter halo swap, the loop-filter stages.
     """
 
-    def __init__(self, ctx, data, rank, world, dpb_slots, rows=None):
+    def __init__(self, ctx, data, rank, world, dpb_slots, rows=None, parse_threads=4):
         import ctypes as C
         from . import bitstream as B
         from . import parser as PZ
@@ -209,10 +209,15 @@ class StreamShardRank(ShardGeom):
         self.refined = [False] * n
         self.depth = {}        # DPB slot -> reference-halo rows exchanged for its current picture
         self.reach = 0         # largest reach seen (diagnostics)
+        # the CABAC passes run ahead on parser threads (a picture's pass depends on no other picture;
+        # ctypes releases the GIL inside the library)
+        import concurrent.futures as cf
+        self.pool = cf.ThreadPoolExecutor(max(1, parse_threads))
+        self.parsed = [self.pool.submit(self.ps.parse, i) for i in range(n)]
 
     # ---- phases of picture i (a driver runs them on every rank: decode_stream_picture)
     def parse(self, i):
-        self.ps.parse(i)
+        self.parsed[i].result()
 
     def pending(self, i):
         """references of i whose motion is not refined yet (their deltas must be all-gathered first)"""
@@ -283,6 +288,9 @@ class StreamShardRank(ShardGeom):
                 self.handle[k] = None
 
     def release(self):
+        for f in self.parsed:
+            f.cancel()
+        self.pool.shutdown(wait=True)
         for k in range(self.n):
             if self.handle[k] is not None:
                 self.ctx.release(self.handle[k])
