@@ -274,6 +274,7 @@ def main():
                          "Default: 16 at 4K and above, 12 below (4K 9-picture stream, end to end: 12 / 16 / 20 in flight "
                          "2545 / 2763 / 2572 Mpx/s; 1080p 33 pictures: 12 / 16 2372 / 2122)")
     ap.add_argument("--resident-steps", type=int, default=20, help="timed steps of the resident (pre-planned) pass, 0 = skip")
+    ap.add_argument("--single-steps", type=int, default=5, help="timed decodes of the single-stream pass (one decode in flight), 0 = skip")
     ap.add_argument("--sync-pictures", action="store_true",
                     help="host sync after every picture of the resident pass (profiling: kernel durations without overlap)")
     ap.add_argument("--e2e-threads", type=int, default=16,
@@ -336,6 +337,30 @@ def main():
         if owner is not None:
             bitexact = bitexact and check_slots(ctx, owner, meta)
     e2e.close()
+
+    # ---- single stream: one decode at a time (latency view of the same path)
+    single = None
+    if a.single_steps > 0:
+        ss = BitstreamE2E(ctx, data, per, 1, a.e2e_threads)
+        ss.run(1)
+        ctx.sync()
+        ss.times = {}
+        R.barrier()
+        s0 = time.perf_counter()
+        ss.run(a.single_steps)
+        ctx.sync()
+        s1 = time.perf_counter()
+        R.barrier()
+        s_el = R.max_over_ranks(s1 - s0)
+        for owner in ss.final:
+            if owner is not None:
+                bitexact = bitexact and check_slots(ctx, owner, meta)
+        ss.close()
+        single = {"value": round(V.job_throughput(px_seq * a.single_steps, s_el, R) / 1e6, 2), "unit": "Mpixels/s",
+                  "decodes": a.single_steps, "ms_per_decode": round(s_el / a.single_steps * 1e3, 3),
+                  "host_ms_per_picture": {k: round(v / (a.single_steps * len(infos)) * 1e3, 3) for k, v in ss.times.items()},
+                  "note": "one decode in flight (%d worker threads: CABAC ahead, plan + upload pipelined; motion derivation "
+                          "in decoding order), end to end from the bitstream like value" % a.e2e_threads}
 
     # ---- resident: every picture planned and uploaded once, the steps only launch (GPU-side rate)
     resident = None
@@ -456,6 +481,7 @@ def main():
         "host_ms_per_picture": {k: round(v / (a.steps * a.segments * len(infos)) * 1e3, 3) for k, v in e2e.times.items()},
         "roofline": roof,
         "cpu_baseline": None,
+        "single_stream": single,
         "resident": resident,
         "mc_roofline": mc_roof,
         "kernels": {k: {"ms_per_step": round(v[1], 4), "launches_per_step": v[0],
@@ -463,6 +489,10 @@ def main():
     }
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, "tests", "golden", "streams", a.stream + ".bin"), px_seq)
+        cb = line["cpu_baseline"]
+        if cb and cb.get("value"):
+            line["vs_cpu_baseline"] = {"value": round(value / cb["value"], 1),
+                                       "single_stream": round(single["value"] / cb["value"], 1) if single else None}
     ctx.close()
     if a.shard_steps > 0:
         try:

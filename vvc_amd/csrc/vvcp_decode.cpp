@@ -14,6 +14,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <thread>
 
@@ -95,120 +96,257 @@ void check(int rc, vvcr_ctx *ctx, const char *what) {
 
 }  // namespace
 
+// The decode indices of the collocated pictures of picture i (one per slice with temporal motion
+// candidates, CABACReader / DecCu read only that picture's motion: Deriver::run, vvcp_mv.cpp).
+static std::vector<int> collocated(const vvcp::PictureUnit &p, const DecodePlan &P, int i) {
+  std::vector<int> out;
+  if (!p.ph.tmvp) return out;
+  for (const vvcp::SliceHeader &sh : p.slices) {
+    if (sh.isIntra()) continue;
+    const int cl = sh.isInterB() ? (sh.colFromL0 ? 0 : 1) : 0;
+    const int poc = sh.refPoc[cl][sh.colRefIdx];
+    for (int l = 0; l < 2; l++)
+      for (int j : P.refIdx[l][i])
+        if (P.poc[j] == poc && std::find(out.begin(), out.end(), j) == out.end()) out.push_back(j);
+  }
+  return out;
+}
+
+// DMVR sub-blocks of a derived picture (PU::checkDMVRCondition PUs, 16x16 sub-blocks): none means its
+// refined motion needs nothing from the GPU
+static int64_t dmvr_subblocks(const vvcp::PictureUnit &p) {
+  int64_t n = 0;
+  for (const vvcr_pu &u : p.syn.pu)
+    if (u.dmvr) n += (int64_t)(u.h / std::min(u.h, 16)) * (u.w / std::min(u.w, 16));
+  return n;
+}
+
+// The decode loop, pipelined over a pool of `threads` workers that run the CABAC passes ahead and plan +
+// upload derived pictures (a plan task goes before any parse task: it is on the critical path). The
+// decode thread derives motion in decoding order; it waits for the GPU only for the DMVR deltas of a
+// picture's COLLOCATED pictures (the only motion derivation reads), and only when those have DMVR
+// sub-blocks (otherwise their refined motion is recorded right after their derivation). Launches stay in
+// decoding order (the DPB slot dependencies of libvvcr assume it): whichever worker finishes the upload
+// of the next picture in order launches every picture prepared by then, then the output callbacks.
 extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_params *prm) {
   if (!h || !ctx || !prm || prm->num_slots <= 0 || prm->slot_base < 0) return VVCR_E_ARG;
   vvcp::Stream &s = h->s;
   const int n = (int)s.pics.size();
-  std::vector<std::thread> pool;
-  std::atomic<int> next{0};
-  std::atomic<bool> stop{false};
-  std::mutex mu;
-  std::condition_variable cv;
-  std::vector<int> state(n, 0);   // 0 pending, 1 parsed, 2 failed
-  std::vector<std::string> perr(n);
-  std::vector<int32_t> handle(n, -1), ndmvr(n, 0);
-  std::vector<int> live;
   using clk = std::chrono::steady_clock;
-  double T[VVCP_DECODE_PHASES] = {0};
   auto since = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
+  std::vector<std::thread> pool;
+  std::mutex mu;                  // task queue, picture states, phase times
+  std::condition_variable cv;
+  std::mutex lmu;                 // launches and output callbacks (one thread at a time, in order)
+  std::vector<int> pstate(n, 0);  // parse: 0 pending, 1 running, 2 done, 3 failed
+  std::vector<std::string> perr(n);
+  std::vector<char> derivedQ(n, 0), prepared(n, 0), launched(n, 0), refined(n, 0);
+  std::vector<int32_t> handle(n, -1), ndmvr(n, 0);
+  std::deque<int> planQ;
+  int nextParse = 0, nextLaunch = 0;
+  bool stop = false;
+  std::string failure;            // first error of a worker (the decode then stops)
+  int failCode = VVCR_OK;
+  double T[VVCP_DECODE_PHASES] = {0};
+  std::vector<int> live;
+  size_t outPos = 0;
+  DecodePlan P;
+  vvcr_seq_params sp{};
   int rc = VVCR_OK;
-  try {
-    if (n == 0) return VVCR_OK;
-    DecodePlan P;
-    P.build(s, prm->slot_base, prm->num_slots);
-    const vvcp::PictureUnit &p0 = *s.pics[0];
-    vvcr_seq_params sp{p0.pps.width, p0.pps.height, 1, p0.sps.bitDepth, p0.sps.ctuLog2, prm->ctx_slots, 0};
-    const int nthreads = std::max(1, prm->threads);
-    for (int t = 0; t < nthreads; t++)
-      pool.emplace_back([&] {
-        for (int i; !stop && (i = next++) < n;) {
-          const auto a = clk::now();
-          std::string e;
-          try {
-            s.parse_picture(i);
-          } catch (const std::exception &x) {
-            e = x.what();
-          }
-          const double dt = since(a);
-          std::lock_guard<std::mutex> g(mu);
-          state[i] = e.empty() ? 1 : 2;
-          perr[i] = e;
-          T[VVCP_PHASE_PARSE] += dt;
-          cv.notify_all();
-        }
-      });
-    std::vector<char> refined(n, 0);
-    std::vector<int32_t> deltas;
-    size_t outPos = 0;
-    for (int i = 0; i < n; i++) {
-      auto t0 = clk::now();
+
+  auto fail = [&](const std::string &m, int code) {   // under mu
+    if (failure.empty()) { failure = m; failCode = code; }
+    stop = true;
+    cv.notify_all();
+  };
+  // launch every picture prepared in order (caller holds lmu, not mu)
+  auto launch_ready = [&]() {
+    for (;;) {
+      int i;
       {
-        std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return state[i] != 0; });
-        if (state[i] == 2) throw vvcp::ParseError("picture " + std::to_string(i) + ": " + perr[i]);
+        std::lock_guard<std::mutex> g(mu);
+        if (stop || nextLaunch >= n || !prepared[nextLaunch]) return;
+        i = nextLaunch;
       }
-      T[VVCP_PHASE_PARSE_WAIT] += since(t0);
-      t0 = clk::now();
-      // the collocated picture is one of the references: refine those still pending
-      for (int l = 0; l < 2; l++)
-        for (int j : P.refIdx[l][i]) {
-          if (refined[j]) continue;
-          deltas.resize(2 * (size_t)ndmvr[j] + 2);
-          const int got = vvcr_picture_dmvr_deltas(ctx, handle[j], deltas.data(), ndmvr[j]);
-          check(got, ctx, "vvcr_picture_dmvr_deltas");
-          s.refine_motion(j, deltas.data(), got);
-          refined[j] = 1;
-        }
-      T[VVCP_PHASE_DMVR_WAIT] += since(t0);
-      t0 = clk::now();
-      s.derive_motion(i);
-      T[VVCP_PHASE_DERIVE] += since(t0);
-      t0 = clk::now();
-      int32_t rs[2 * VVCR_MAX_REF] = {0};
-      for (int l = 0; l < 2; l++)
-        for (size_t r = 0; r < P.refIdx[l][i].size(); r++) rs[l * VVCR_MAX_REF + r] = P.slot[P.refIdx[l][i][r]];
-      vvcr_picture *pic = nullptr;
-      const int prc = vvcp_plan_picture(h, i, &sp, P.slot[i], rs, prm->stage_mask, &pic);
-      if (prc) throw vvcp::ParseError("picture " + std::to_string(i) + " plan: " + vvcp_last_error());
-      int64_t counts[10];
-      vvcr_picture_work_counts(pic, counts, 10);
-      ndmvr[i] = (int32_t)counts[7];
-      T[VVCP_PHASE_PLAN] += since(t0);
-      t0 = clk::now();
-      const int urc = vvcr_prepare_planned(ctx, pic, &handle[i]);
-      vvcr_picture_destroy(pic);
-      check(urc, ctx, "vvcr_prepare_planned");
-      T[VVCP_PHASE_PREPARE] += since(t0);
-      t0 = clk::now();
-      check(vvcr_launch_picture(ctx, handle[i]), ctx, "vvcr_launch_picture");
-      T[VVCP_PHASE_LAUNCH] += since(t0);
-      live.push_back(i);
-      if (!P.referenced[i] || !(prm->stage_mask & VVCR_STAGE_INTER)) refined[i] = 1;
-      t0 = clk::now();
+      const auto t0 = clk::now();
+      const int lrc = vvcr_launch_picture(ctx, handle[i]);
+      const double tl = since(t0);
+      if (lrc < 0) {
+        std::lock_guard<std::mutex> g(mu);
+        fail(std::string("vvcr_launch_picture: ") + vvcr_last_error(ctx), VVCR_E_STATE);
+        return;
+      }
+      const auto t1 = clk::now();
       while (outPos < P.outOrder.size() && P.outReady[P.outOrder[outPos]] <= i) {
         const int k = P.outOrder[outPos++];
         if (prm->on_output) prm->on_output(prm->user, k, P.poc[k], P.slot[k]);
       }
-      T[VVCP_PHASE_OUTPUT] += since(t0);
-      if (!prm->handles_out)   // pictures far behind whose deltas are no longer needed
-        while (live.size() > 24 && refined[live.front()]) {
-          check(vvcr_release_picture(ctx, handle[live.front()]), ctx, "vvcr_release_picture");
-          live.erase(live.begin());
+      const double to = since(t1);
+      std::vector<int> drop;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        launched[i] = 1;
+        nextLaunch = i + 1;
+        T[VVCP_PHASE_LAUNCH] += tl;
+        T[VVCP_PHASE_OUTPUT] += to;
+        live.push_back(i);
+        if (!prm->handles_out)   // pictures far behind whose deltas are no longer needed
+          while (live.size() > 24 && refined[live.front()]) {
+            drop.push_back(live.front());
+            live.erase(live.begin());
+          }
+        cv.notify_all();
+      }
+      for (int k : drop) vvcr_release_picture(ctx, handle[k]);
+    }
+  };
+  auto plan_one = [&](int i) {
+    auto t0 = clk::now();
+    int32_t rs[2 * VVCR_MAX_REF] = {0};
+    for (int l = 0; l < 2; l++)
+      for (size_t r = 0; r < P.refIdx[l][i].size(); r++) rs[l * VVCR_MAX_REF + r] = P.slot[P.refIdx[l][i][r]];
+    vvcr_picture *pic = nullptr;
+    if (vvcp_plan_picture(h, i, &sp, P.slot[i], rs, prm->stage_mask, &pic))
+      throw vvcp::ParseError("picture " + std::to_string(i) + " plan: " + vvcp_last_error());
+    const double tp = since(t0);
+    t0 = clk::now();
+    int32_t hd = -1;
+    const int urc = vvcr_prepare_planned(ctx, pic, &hd);
+    vvcr_picture_destroy(pic);
+    if (urc < 0) throw VvcrFail(std::string("vvcr_prepare_planned: ") + vvcr_last_error(ctx));
+    const double tu = since(t0);
+    std::lock_guard<std::mutex> g(mu);
+    handle[i] = hd;
+    prepared[i] = 1;
+    T[VVCP_PHASE_PLAN] += tp;
+    T[VVCP_PHASE_PREPARE] += tu;
+  };
+  auto worker = [&]() {
+    for (;;) {
+      int task = -1;
+      bool isPlan = false;
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || !planQ.empty() || nextParse < n; });
+        if (stop) return;
+        if (!planQ.empty()) { task = planQ.front(); planQ.pop_front(); isPlan = true; }
+        else { task = nextParse++; pstate[task] = 1; }
+      }
+      if (isPlan) {
+        try {
+          plan_one(task);
+        } catch (const VvcrFail &e) {
+          std::lock_guard<std::mutex> g(mu);
+          fail(e.what(), VVCR_E_STATE);
+          return;
+        } catch (const std::exception &e) {
+          std::lock_guard<std::mutex> g(mu);
+          fail(e.what(), VVCR_E_UNSUPPORTED);
+          return;
         }
+        std::lock_guard<std::mutex> lg(lmu);
+        launch_ready();
+      } else {
+        const auto t0 = clk::now();
+        std::string e;
+        try {
+          s.parse_picture(task);
+        } catch (const std::exception &x) {
+          e = x.what();
+        }
+        const double dt = since(t0);
+        std::lock_guard<std::mutex> g(mu);
+        pstate[task] = e.empty() ? 2 : 3;
+        perr[task] = e;
+        T[VVCP_PHASE_PARSE] += dt;
+        cv.notify_all();
+      }
+    }
+  };
+  try {
+    if (n == 0) return VVCR_OK;
+    P.build(s, prm->slot_base, prm->num_slots);
+    const vvcp::PictureUnit &p0 = *s.pics[0];
+    sp = vvcr_seq_params{p0.pps.width, p0.pps.height, 1, p0.sps.bitDepth, p0.sps.ctuLog2, prm->ctx_slots, 0};
+    const int nthreads = std::max(1, prm->threads);
+    for (int t = 0; t < nthreads; t++) pool.emplace_back(worker);
+    std::vector<int32_t> deltas;
+    for (int i = 0; i < n; i++) {
+      auto t0 = clk::now();
+      {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return stop || pstate[i] >= 2; });
+        if (stop) break;
+        if (pstate[i] == 3) throw vvcp::ParseError("picture " + std::to_string(i) + ": " + perr[i]);
+        T[VVCP_PHASE_PARSE_WAIT] += since(t0);
+      }
+      // the collocated pictures' refined motion: their DMVR deltas from the GPU (after their launch)
+      t0 = clk::now();
+      for (int j : collocated(*s.pics[i], P, i)) {
+        if (refined[j]) continue;
+        {
+          std::unique_lock<std::mutex> g(mu);
+          cv.wait(g, [&] { return stop || launched[j]; });
+          if (stop) break;
+        }
+        deltas.resize(2 * (size_t)ndmvr[j] + 2);
+        const int got = vvcr_picture_dmvr_deltas(ctx, handle[j], deltas.data(), ndmvr[j]);
+        check(got, ctx, "vvcr_picture_dmvr_deltas");
+        s.refine_motion(j, deltas.data(), got);
+        std::lock_guard<std::mutex> g(mu);
+        refined[j] = 1;
+      }
+      T[VVCP_PHASE_DMVR_WAIT] += since(t0);
+      if (stop) break;
+      t0 = clk::now();
+      s.derive_motion(i);
+      const int64_t nd = dmvr_subblocks(*s.pics[i]);
+      T[VVCP_PHASE_DERIVE] += since(t0);
+      // a picture without DMVR sub-blocks (or not referenced, or reconstructed without its inter stage)
+      // has its final motion now
+      const bool now = nd == 0 || !P.referenced[i] || !(prm->stage_mask & VVCR_STAGE_INTER);
+      if (now && P.referenced[i]) {
+        if (nd == 0) s.refine_motion(i, nullptr, 0);
+        else {   // no inter stage on the GPU: the motion unrefined (stage tests only)
+          std::vector<int32_t> zero(2 * (size_t)nd, 0);
+          s.refine_motion(i, zero.data(), nd);
+        }
+      }
+      std::lock_guard<std::mutex> g(mu);
+      ndmvr[i] = (int32_t)nd;
+      if (now) refined[i] = 1;
+      planQ.push_back(i);
+      cv.notify_all();
+    }
+    // every picture launched (or a worker failed)
+    {
+      std::unique_lock<std::mutex> g(mu);
+      cv.wait(g, [&] { return stop || nextLaunch >= n; });
     }
     if (prm->handles_out)
       for (int i = 0; i < n; i++) prm->handles_out[i] = handle[i];
   } catch (const VvcrFail &e) {
-    vvcp::set_api_error(e.what());
-    rc = VVCR_E_STATE;
+    std::lock_guard<std::mutex> g(mu);
+    fail(e.what(), VVCR_E_STATE);
   } catch (const std::exception &e) {
-    vvcp::set_api_error(e.what());
-    rc = VVCR_E_UNSUPPORTED;
+    std::lock_guard<std::mutex> g(mu);
+    fail(e.what(), VVCR_E_UNSUPPORTED);
   }
-  stop = true;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    stop = true;
+    cv.notify_all();
+  }
   for (auto &t : pool) t.join();
-  if (rc != VVCR_OK || !prm->handles_out)
+  if (!failure.empty()) {
+    vvcp::set_api_error(failure);
+    rc = failCode;
+  }
+  if (rc != VVCR_OK || !prm->handles_out) {
     for (int i : live) vvcr_release_picture(ctx, handle[i]);
+    for (int i = 0; i < n; i++)   // prepared, never launched
+      if (prepared[i] && !launched[i]) vvcr_release_picture(ctx, handle[i]);
+  }
   if (prm->phase_seconds)
     for (int k = 0; k < VVCP_DECODE_PHASES; k++) prm->phase_seconds[k] += T[k];
   return rc;
