@@ -963,7 +963,17 @@ void __wrap__ZN15InterPrediction21motionCompensationGeoER10CodingUnitR8MergeCtx(
     o[1] = (o[0] == 2) ? 1 : 0; o[2] = f.refIdx; o[3] = f.mv.hor; o[4] = f.mv.ver; o[5] = m.useAltHpelIf[i];
   }
   g_cap.geo[&cu] = g;   // the candidates are descriptor rows (vvcr_geo); the blend is libvvcr's in the drop-in
-  if (g_replace) return;
+  if (g_replace) {
+    // the PU state motionCompensationGeo leaves behind (InterPrediction.cpp:1761-1770): each candidate's
+    // merge info set and spanned in turn, the second one last; the two MCs and the blend do not run
+    for (auto &pu : CU::traversePUs(cu)) {
+      m.setMergeInfo(pu, idx[0]);
+      PU::spanMotionInfo(pu);
+      m.setMergeInfo(pu, idx[1]);
+      PU::spanMotionInfo(pu);
+    }
+    return;
+  }
   g_refCalls[RC_MC_GEO]++;
   __real__ZN15InterPrediction21motionCompensationGeoER10CodingUnitR8MergeCtx(self, cu, m);
   setCtu(*cu.cs, cu.lumaPos().x, cu.lumaPos().y);

@@ -96,7 +96,7 @@ def _stream_rank_main(rank, world, port, name, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,world", [("ratile1080_q32", 2), ("ratile416_q32", 3)])
+@pytest.mark.parametrize("name,world", [("ratile416_q32", 2), ("ratile1080_q32", 3)])
 def test_multiprocess_sharded_decode_from_bitstream(tmp_path, name, world):
     """BASELINE config 4 from the .bin: one process per rank over torch.distributed (gloo), each parsing
     the stream itself and reconstructing its own tile rows; rank 0's assembled pictures match DecoderApp."""
