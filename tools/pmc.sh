@@ -8,7 +8,7 @@ mkdir -p $O
 timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
 run() {  # name counters...
   local n=$1; shift
-  timeout -s KILL 90 rocprofv3 --pmc "$@" -f csv -d $O/$n -o run -- python3 bench.py --steps 1 --warmup 1 --resident-steps 2 --no-cpu --segments 1 --sync-pictures --shard-steps 0 ${PMC_ARGS} > $O/$n.log 2>&1
+  timeout -s KILL 150 rocprofv3 --pmc "$@" -f csv -d $O/$n -o run -- python3 bench.py --steps 1 --warmup 1 --resident-steps 2 --no-cpu --segments 1 --sync-pictures --shard-steps 0 --single-steps 0 ${PMC_ARGS} > $O/$n.log 2>&1
 }
 run fetch FETCH_SIZE &&
 run write WRITE_SIZE &&

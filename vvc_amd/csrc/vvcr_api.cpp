@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -375,6 +376,10 @@ static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lan
   P.ctu = 1 << ctx->sp.ctu_log2;
   P.wp = make_wp_table(pp, ctx->sp.bit_depth);
   P.wpd = wpd;
+  for (int c = 0; c < 3; c++) {
+    P.reco[c] = ctx->dpb[pp.slot][c];
+    P.resi[c] = ctx->lanes[lane].resi[c];
+  }
   return P;
 }
 
@@ -419,6 +424,11 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
   b.intra.clear();
   b.dbk.clear();
   if (pp.lmcs_enabled && sp.bit_depth != 10) throw VvcrError(VVCR_E_UNSUPPORTED, "LMCS tables are captured for 10-bit luma");
+  // With the residual, inter and intra stages together, plain inter CUs are reconstructed by k_mc (the
+  // prediction plus the residual straight into the picture, fused_inter_cu); a subset of those stages
+  // (the stage tests) keeps the separate prediction planes.
+  const uint32_t recon3 = VVCR_STAGE_RESID | VVCR_STAGE_INTER | VVCR_STAGE_INTRA;
+  const bool fuse = (mask & recon3) == recon3 && getenv("VVCR_NO_FUSE") == nullptr;
   // The three planners read the descriptors only and write disjoint outputs: deblocking runs on a
   // second thread beside the work lists and the intra plan (a 4K intra picture plans in ~100 ms each).
   std::exception_ptr dbk_err;
@@ -432,10 +442,10 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
       }
     });
   try {
-    if (mask & (VVCR_STAGE_RESID | VVCR_STAGE_INTER)) build_work_lists(sp, pp, b.desc, b.wl);
+    if (mask & (VVCR_STAGE_RESID | VVCR_STAGE_INTER)) build_work_lists(sp, pp, b.desc, b.wl, fuse);
     if ((mask & VVCR_STAGE_INTER) && b.wl.n_unsupported_inter)
       throw VvcrError(VVCR_E_UNSUPPORTED, std::to_string(b.wl.n_unsupported_inter) + " inter CUs use tools not supported yet");
-    if (mask & VVCR_STAGE_INTRA) plan_intra(sp, pp, b.desc, b.intra);
+    if (mask & VVCR_STAGE_INTRA) plan_intra(sp, pp, b.desc, b.intra, fuse);
   } catch (...) {
     if (dbk_thread.joinable()) dbk_thread.join();
     throw;

@@ -42,7 +42,8 @@ void push_tiles(bigbuf::vec<McJob> &out, int x0, int y0, int w, int h, McJob pro
 double mc_alg_bytes(uint16_t flags, int w, int h) {
   const int lists = ((flags & MC_L0) ? 1 : 0) + ((flags & MC_L1) ? 1 : 0);
   const double in = (double)(w + 7) * (h + 7) + 2.0 * (w / 2 + 3) * (h / 2 + 3);
-  return 2.0 * (lists * in + 1.5 * w * h);
+  // + the residual read by a fused reconstruction (MC_RESI); the output is written once either way
+  return 2.0 * (lists * in + 1.5 * w * h + ((flags & MC_RESI) ? 1.5 * w * h : 0.0));
 }
 
 // One plain MC unit (a PU, or an SbTMVP sub-block): 32x32 tiles for k_mc_tile when the PU is at least
@@ -275,7 +276,8 @@ AffList affine_list(const vvcr_pic_params &pp, const vvcr_cu &c, const vvcr_pu &
 
 }  // namespace
 
-void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl) {
+void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl,
+                      bool fuse) {
   wl.clear();
   build_tb_jobs(sp, pp, d, wl.tb, wl.coef);
   // small blocks first (64-lane workgroups), then the large ones (256 lanes)
@@ -292,13 +294,14 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   for (size_t ci = 0; ci < d.cu.size(); ci++) {
     const vvcr_cu &c = d.cu[ci];
     if (c.predmode != MODE_INTER || !c.yvalid || !in_shard(pp, c)) continue;
+    const uint16_t recon = (fuse && fused_inter_cu(pp, d, c)) ? (uint16_t)(MC_RECON | (c.rootcbf ? MC_RESI : 0)) : 0;
     if (c.geo) {
       // motionCompensationGeo (InterPrediction.cpp:1749): two uni candidates at 14 bits, blended
       const vvcr_pu &p = d.pu[c.firstpu];
       if (geo_of[ci] < 0 || p.geodir < 0 || p.geodir >= 64) { wl.n_unsupported_inter++; continue; }
       const vvcr_geo &g = d.geo[geo_of[ci]];
       McJob j{};
-      j.flags = MC_L0 | MC_L1 | MC_LUMA | MC_CHROMA | MC_GEO;
+      j.flags = MC_L0 | MC_L1 | MC_LUMA | MC_CHROMA | MC_GEO | recon;
       for (int k = 0; k < 2; k++) {
         const int l = g.cand[k][1], r = g.cand[k][2];
         if (l < 0 || l > 1 || r < 0 || r >= pp.num_ref[l]) fail("GEO candidate reference");
@@ -332,6 +335,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
             const MotionRec &m = d.motion[(size_t)((p.y + y) >> 2) * W4 + ((p.x + x) >> 2)];
             McJob j = make_job(pp, m.inter_dir, m.ref0, m.ref1, m.mv0x, m.mv0y, m.mv1x, m.mv1y, bcw, alt);   // BCW of the CU (xWeightedAverage reads pu.cu->BcwIdx)
             set_wp(pp, j, m.ref0, m.ref1, c.bcw);
+            j.flags |= recon;
             push_mc(wl, p.x + x, p.y + y, std::min(8, p.w - x), std::min(8, p.h - y), j);
           }
         continue;
@@ -387,6 +391,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       }
       McJob j = make_job(pp, p.interdir, p.ref0, p.ref1, p.mv0x, p.mv0y, p.mv1x, p.mv1y, bcw, alt);
       set_wp(pp, j, p.ref0, p.ref1, c.bcw);   // the CU's BcwIdx, not the CIIP-cleared one (:664 reads pu.cu->BcwIdx)
+      j.flags |= recon;
       push_mc(wl, p.x, p.y, p.w, p.h, j);
     }
   }

@@ -77,7 +77,24 @@ void build_scan_tables(ScanTables &st);
 
 // Throws VvcrError on inconsistent descriptors (indices out of range, blocks outside the picture).
 void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d);
-void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl);
+// fuse: the picture's reconstruction stages run together (residual, inter, intra), so plain inter CUs are
+// reconstructed by k_mc itself (fused_inter_cu)
+void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl,
+                      bool fuse);
+
+// Inter CUs whose motion compensation writes the reconstruction directly (prediction + residual, clipped,
+// into the picture: AreaBuf::reconstruct, Buffer.cpp:590, fused into k_mc's store): no LMCS in the
+// picture (no forward-mapped prediction, no chroma residual scaling), no CIIP, and every PU plain MC (no
+// affine, DMVR or BDOF: those kernels write the prediction planes). The work-list and intra planners
+// both apply it: k_mc takes these CUs, k_recon_inter the rest.
+inline bool fused_inter_cu(const vvcr_pic_params &pp, const PictureDescriptors &d, const vvcr_cu &c) {
+  if (pp.lmcs_enabled || c.predmode != 0 || !c.yvalid || !c.cvalid || c.affine || c.npu <= 0) return false;
+  for (int k = 0; k < c.npu; k++) {
+    const vvcr_pu &p = d.pu[c.firstpu + k];
+    if (p.ciip || p.dmvr || p.bdof) return false;
+  }
+  return true;
+}
 
 // Spatial shard of a picture (vvcr_pic_params::shard_y0 / shard_y1): whether a CU is reconstructed by
 // this shard (its luma position lies in the shard rows), and the rows whose deblocking edges it plans.

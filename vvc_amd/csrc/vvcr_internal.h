@@ -52,6 +52,8 @@ enum : uint16_t {
   MC_KEEP14 = 1 << 7,    // write 14-bit intermediate instead of final samples
   MC_GEO = 1 << 8,       // two uni-predicted GEO parts blended by split weights (InterpolationFilter.cpp:997)
   MC_WP = 1 << 9,        // explicit weighted prediction epilogue (WeightPrediction::addWeightUni / addWeightBi)
+  MC_RECON = 1 << 10,    // k_mc writes the reconstruction (+ residual, clipped) into the picture (fused_inter_cu)
+  MC_RESI = 1 << 11,     // MC_RECON with a residual (the CU's root cbf)
 };
 
 struct McJob {
@@ -127,6 +129,8 @@ struct McParams {
   int32_t ctu;           // CTU size (affine MV clamp, InterPrediction.cpp:937)
   WpTable wp;
   const WpTable *wpd;    // the same table in device memory (k_mc indexes it per lane)
+  DPlane reco[3];        // the picture (MC_RECON jobs)
+  DPlane resi[3];        // the residual planes (MC_RESI jobs)
 };
 
 // Plain MC work of k_mc in "cells": a lane computes one cell (luma: 4 columns x 8 rows of one job; chroma:

@@ -123,7 +123,7 @@ struct IntraParams {
   const int16_t *lmcs_fwd;           // forward LUT, 1 << bd entries (device)
 };
 
-void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out);
+void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out, bool fuse);
 void launch_recon_inter(const IntraParams &p, const ReconTile *tiles, int n, hipStream_t s);
 // LMCS inverse luma mapping of the reconstructed picture before deblocking (DecLib.cpp:574)
 void launch_lmcs_inverse(const DPlane &luma, const int16_t *inv_lut, int y0, int y1, hipStream_t s);

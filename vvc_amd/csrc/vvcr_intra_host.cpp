@@ -137,6 +137,7 @@ struct Planner {
   }
   int seq = 0;
   bool cscale = false;                              // LMCS chroma residual scaling active in this picture
+  bool fuse = false;                                // plain inter CUs reconstructed by k_mc (fused_inter_cu)
   // Slice / tile of every CTU (getCURestricted: a neighbour is usable only inside the same slice and
   // tile, CodingStructure.cpp:1519-1537, CU::isSameSliceAndTile UnitTools.cpp:170); cur_reg is the
   // region of the CU being planned / the step being resolved.
@@ -273,10 +274,12 @@ struct Planner {
       }
       return;
     }
-    // plain inter: level 0, reconstructed before the intra waves; with LMCS chroma residual scaling the
-    // chroma scale depends on reconstructed luma next to the VPDU, so the chroma becomes a step
+    // plain inter: level 0, reconstructed before the intra waves (by k_mc itself when fused: no tiles);
+    // with LMCS chroma residual scaling the chroma scale depends on reconstructed luma next to the VPDU,
+    // so the chroma becomes a step
     const bool chromaStep = cscale && c.cvalid;
-    for (int y = 0; y < c.h; y += 16)
+    if (!(fuse && fused_inter_cu(pp, d, c)))
+      for (int y = 0; y < c.h; y += 16)
       for (int x = 0; x < c.w; x += 16) {
         ReconTile t{};
         t.x = (int16_t)(c.x + x); t.y = (int16_t)(c.y + y);
@@ -826,10 +829,11 @@ struct Planner {
 
 }  // namespace
 
-void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out) {
+void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, IntraPlan &out, bool fuse) {
   out.clear();
   auto P = std::make_unique<Planner>(sp, pp, d, out);
   P->cscale = pp.lmcs_enabled && pp.lmcs_chroma_scale;
+  P->fuse = fuse;
   P->run();
 }
 
@@ -845,7 +849,7 @@ extern "C" int vvcr_debug_plan_intra(const vvcr_seq_params *sp, const vvcr_pic_p
     d.pu.assign(pu, pu + npu);
     d.tu.assign(tu, tu + ntu);
     IntraPlan ip;
-    plan_intra(*sp, *pp, d, ip);
+    plan_intra(*sp, *pp, d, ip, false);
     const int n = (int)ip.jobs.size();
     counts[0] = n;
     counts[1] = (int)ip.deps.size();

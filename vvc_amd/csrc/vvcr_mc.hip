@@ -322,15 +322,29 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
   const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
   const int off2 = (rnd ? (1 << (sh2 - 1)) + (IF_INTERNAL_OFFS << IF_FILTER_PREC) : 0) - (IF_INTERNAL_OFFS << IF_FILTER_PREC);
   const int ts = (N == 8) ? ((J.w == 4 && J.h == 4) ? 1 : 0) | ((J.flags & MC_ALT_HPEL) ? 2 : 0) : 0;
-  const int ostride = comp ? P.out[1].stride : P.out[0].stride;
-  int16_t *dst = (comp == 0 ? P.out[0].p : comp == 1 ? P.out[1].p : P.out[2].p) + (size_t)y * ostride + x;
+  // destination: the prediction planes, or with MC_RECON the picture itself (the reconstruction
+  // clip(pred + resi) of AreaBuf::reconstruct, Buffer.cpp:590, fused: no prediction plane round trip)
+  const bool recon = (J.flags & MC_RECON) != 0, addResi = (J.flags & MC_RESI) != 0;
+  const DPlane &O0 = recon ? P.reco[0] : P.out[0], &O1 = recon ? P.reco[1] : P.out[1], &O2 = recon ? P.reco[2] : P.out[2];
+  const int ostride = comp ? O1.stride : O0.stride;
+  int16_t *dst = (comp == 0 ? O0.p : comp == 1 ? O1.p : O2.p) + (size_t)y * ostride + x;
+  const int rstride = comp ? P.resi[1].stride : P.resi[0].stride;
+  const int16_t *rsrc = (comp == 0 ? P.resi[0].p : comp == 1 ? P.resi[1].p : P.resi[2].p) + (size_t)y * rstride + x;
   const int cx = x - (comp ? J.x >> 1 : J.x), cy = y - (comp ? J.y >> 1 : J.y);   // cell origin in the block
   const bool wide = nc == 4 && (x & 3) == 0;
   // one output row of 4 samples: 8-byte store, or 2-sample aligned pieces (chroma of blocks at odd
   // multiples of 4 luma columns, or 2 wide)
-  auto store = [&](int o, const int (&a)[4]) {
+  auto store = [&](int o, int (&a)[4]) {
     if (o >= nr) return;
     int16_t *q = dst + (size_t)o * ostride;
+    if (addResi) {
+      const int16_t *rr = rsrc + (size_t)o * rstride;
+      uint32_t r0, r1 = 0;
+      if (wide) { const uint2 v = *(const uint2 *)rr; r0 = v.x; r1 = v.y; }
+      else { r0 = ((const uint32_t *)rr)[0]; if (nc == 4) r1 = ((const uint32_t *)rr)[1]; }
+      a[0] = clampi(a[0] + lo16(r0), 0, maxv); a[1] = clampi(a[1] + hi16(r0), 0, maxv);
+      a[2] = clampi(a[2] + lo16(r1), 0, maxv); a[3] = clampi(a[3] + hi16(r1), 0, maxv);
+    }
     if (wide) *(uint2 *)q = make_uint2(pk(a[0], a[1]), pk(a[2], a[3]));
     else {
       ((uint32_t *)q)[0] = pk(a[0], a[1]);
