@@ -44,13 +44,18 @@ def main():
     ctx.set_timing(True)
     out = {"stream": a.stream, "pictures": len(hs), "ms_per_picture_wall": round((t1 - t0) / a.reps / len(hs) * 1e3, 4)}
     agg = {}
+    per_pic = []
     for h in hs:
         ctx.launch(h)
         ctx.sync()
+        row = {}
         for name, n, ms, alg in ctx.kernel_stats(h):
             if n:
                 g = agg.setdefault(name, [0, 0.0, 0.0])
                 g[0] += n; g[1] += ms; g[2] += alg
+                row[name] = [round(ms * 1e3, 1), round(alg / 1e6, 1), round(alg / (ms / 1e3) / 1e9) if ms else 0]
+        per_pic.append(row)
+    out["per_picture_us_MB_GBps"] = per_pic
     out["kernels"] = {k: {"launches": v[0], "us_per_launch": round(v[1] / v[0] * 1e3, 2), "alg_MB_per_launch": round(v[2] / v[0] / 1e6, 3),
                           "alg_GBps": round(v[2] / (v[1] / 1e3) / 1e9, 1) if v[1] else 0} for k, v in agg.items()}
     for h in hs:
