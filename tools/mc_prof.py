@@ -59,16 +59,37 @@ def run(stream):
         dur = (t1 - t0) / 100.0   # us (100 MHz)
         start = (t0 - base) / 100.0
         end = (t1 - base) / 100.0
-        x = (b[:, 2] & 0xffff).astype(np.int64)
-        y = ((b[:, 2] >> 16) & 0xffff).astype(np.int64)
-        w = ((b[:, 2] >> 32) & 0xff).astype(np.int64)
-        fl = b[:, 3].astype(np.int64)
-        order = np.argsort(-dur)
-        print("POC %d: %d workgroups, span %.1f us, start spread %.1f us, duration median %.2f p90 %.2f max %.2f us" % (
-            p["hdr"]["poc"], len(b), end.max(), start.max(), np.median(dur), np.percentile(dur, 90), dur.max()))
-        print("   last end at %.1f us; workgroups ending after 80%% of the span: %d" % (end.max(), int((end > 0.8 * end.max()).sum())))
-        for k in order[:8]:
-            print("   slow: start %.1f dur %.1f  job x %d y %d w %d flags 0x%x" % (start[k], dur[k], x[k], y[k], w[k], fl[k]))
+        hw = (b[:, 2] & 0xffffffff).astype(np.int64)
+        xcc = ((b[:, 2] >> 32) & 0xf).astype(np.int64)
+        cu = ((hw >> 8) & 15) | (((hw >> 13) & 7) << 4) | (((hw >> 12) & 1) << 7)
+        cu_g = xcc * 256 + cu
+        span = end.max()
+        ncu = len(np.unique(cu_g))
+        conc = dur.sum() / (span * ncu)
+        per_cu = np.bincount(np.unique(cu_g, return_inverse=True)[1])
+        print("POC %d: %d waves on %d CUs (%.1f per CU, max %d), span %.1f us, start spread %.1f us, wave duration median %.2f p10 %.2f p90 %.2f max %.2f us, mean live waves per CU %.1f" % (
+            p["hdr"]["poc"], len(b), ncu, per_cu.mean(), per_cu.max(), span, start.max(), np.median(dur), np.percentile(dur, 10),
+            np.percentile(dur, 90), dur.max(), conc))
+        tag = b[:, 3].astype(np.uint64)
+        lum = (tag >> np.uint64(63)).astype(np.int64)
+        cw = ((tag >> np.uint64(8)) & np.uint64(255)).astype(np.int64)
+        chh = (tag & np.uint64(255)).astype(np.int64)
+        nbi = ((tag >> np.uint64(16)) & np.uint64(255)).astype(np.int64)
+        nrec = ((tag >> np.uint64(24)) & np.uint64(255)).astype(np.int64)
+        nwp = ((tag >> np.uint64(32)) & np.uint64(255)).astype(np.int64)
+        nact = ((tag >> np.uint64(40)) & np.uint64(255)).astype(np.int64)
+        for k in np.argsort(-dur)[:6]:
+            print("   slow wave: start %.1f dur %.1f  %s %dx%d active %d bi %d recon %d wp/geo %d  cu %d" % (
+                start[k], dur[k], "luma" if lum[k] else "chroma", cw[k], chh[k], nact[k], nbi[k], nrec[k], nwp[k], cu_g[k]))
+        for isl in (1, 0):
+            m = lum == isl
+            if m.any():
+                print("   %s waves %d: duration median %.2f p90 %.2f; bi-full waves median %.2f, uni-full %.2f" % (
+                    "luma" if isl else "chroma", m.sum(), np.median(dur[m]), np.percentile(dur[m], 90),
+                    np.median(dur[m & (nbi == 64)]) if (m & (nbi == 64)).any() else -1,
+                    np.median(dur[m & (nbi == 0) & (nact == 64)]) if (m & (nbi == 0) & (nact == 64)).any() else -1))
+        hist = np.histogram(start, bins=8, range=(0, span))[0]
+        print("   wave starts per eighth of the span:", list(hist))
         ctx.release(h)
     ctx.close()
 

@@ -48,48 +48,73 @@ __constant__ int8_t c_geo_angle2mirror[32] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1
 __constant__ int8_t c_geo_mask_angle[6] = {0, 2, 3, 4, 5, 8};   // the angle in 0..8 that generated each stored mask
 constexpr int GEO_WEIGHT_MASK_SIZE = 224, GEO_MASK_OFFSET = 16;
 
-// Blending weight of one sample: the g_globalGeoWeights entry (Rom.cpp:778-801) that
-// InterpolationFilter::xWeightedGeoBlk (InterpolationFilter.cpp:1014-1046) walks to, computed in place.
-__device__ __forceinline__ int geo_weight(int angle, int offX, int offY, int lx, int ly) {
-  const int mir = c_geo_angle2mirror[angle];
-  const int X = mir == 1 ? GEO_WEIGHT_MASK_SIZE - 1 - offX - lx : offX + lx;
-  const int Y = mir == 2 ? GEO_WEIGHT_MASK_SIZE - 1 - offY - ly : offY + ly;
-  const int b = c_geo_mask_angle[c_geo_angle2mask[angle]];
-  const int dX = c_geo_dis[b], dY = c_geo_dis[(b + 8) & 31];
-  const int rho = (dX << 8) + (dY << 8);
-  const int wIdx = (((X + GEO_MASK_OFFSET) << 1) + 1) * dX + (((Y + GEO_MASK_OFFSET) << 1) + 1) * dY - rho;
-  return clampi((32 + wIdx + 4) >> 3, 0, 8);
-}
-
-// Combine one sample of the two lists: uni rounding (already final when rnd), WP, GEO blend, BCW, addAvg.
-__device__ __forceinline__ int combine(const McParams &P, const WpTable &WT, const McJob &J, int comp, int x, int y, int a, int b) {
+// The weighted combinations of the two lists, reduced to one per-sample form
+//   clip(((a * w0 + b * w1 + k) >> s) + o)
+// with per-cell constants (a, b: the lists' 14-bit intermediates with IF_INTERNAL_OFFS removed; uni WP
+// has b == a, w1 == 0): WeightPrediction::addWeightUni (WeightPrediction.cpp:280-378) and addWeightBi
+// (:157-222), AreaBuf::addWeightedAvg (BCW, Buffer.cpp:350) and the GEO blend of xWeightedGeoBlk
+// (InterpolationFilter.cpp:997), whose weight w0 = w(x, y), w1 = 8 - w0 varies per sample: its mask index
+// (Rom.cpp:778-801, computed in place) is linear in the sample position, so a cell carries its value at
+// the cell origin and the steps per column / row.
+struct Comb {
+  int w0, w1, k, s, o;
+  int gb, gdx, gdy;   // GEO: mask index at the cell origin, per column, per row
+  bool geo;
+};
+__device__ __forceinline__ Comb comb_setup(const WpTable &WT, const McJob &J, int comp, int bd, int cx, int cy) {
+  Comb C;
   const int cs = comp ? 1 : 0;
   const bool l0 = J.flags & MC_L0, l1 = J.flags & MC_L1, bi = l0 && l1;
-  const int bd = P.bd, maxv = (1 << bd) - 1, headRoom = max(2, IF_INTERNAL_PREC - bd);
-  if (!bi) {
-    if (J.flags & MC_WP) return wp_uni(WT, l0 ? 0 : 1, l0 ? (J.ridx & 15) : (J.ridx >> 4), comp, a, headRoom, maxv);
-    return a;
+  const int headRoom = max(2, IF_INTERNAL_PREC - bd);
+  C.geo = false;
+  C.gb = C.gdx = C.gdy = 0;
+  C.o = 0;
+  if (J.flags & MC_WP) {
+    if (!bi) {
+      const int l = l0 ? 0 : 1, r = l0 ? (J.ridx & 15) : (J.ridx >> 4);
+      const int w = WT.w[l][r][comp], sh = WT.d[l][r][comp] + headRoom;
+      C.w0 = w; C.w1 = 0; C.k = w * IF_INTERNAL_OFFS + (1 << (sh - 1)); C.s = sh; C.o = WT.o[l][r][comp];
+    } else {
+      const int r0 = J.ridx & 15, r1 = J.ridx >> 4;
+      const int sh = WT.d[0][r0][comp] + 1 + headRoom;
+      const int off = WT.o[0][r0][comp] + WT.o[1][r1][comp];
+      C.w0 = WT.w[0][r0][comp]; C.w1 = WT.w[1][r1][comp];
+      C.k = (C.w0 + C.w1) * IF_INTERNAL_OFFS + (1 << (sh - 1)) + off * (1 << (sh - 1));
+      C.s = sh;
+    }
+    return C;
   }
-  if (J.flags & MC_WP) return wp_bi(WT, J.ridx & 15, J.ridx >> 4, comp, a, b, headRoom, maxv);
+  C.k = (1 << (headRoom + 2)) + (IF_INTERNAL_OFFS << 3);
+  C.s = headRoom + 3;
   if (J.flags & MC_GEO) {
-    // xWeightedGeoBlk: (w*p0 + (8-w)*p1 + offset) >> (headRoom + 3)
-    const int w = geo_weight(J.aux & 31, (J.aux >> 8) & 255, (J.aux >> 16) & 255, ((J.x >> cs) + x - (J.pu_x >> cs)) << cs,
-                             ((J.y >> cs) + y - (J.pu_y >> cs)) << cs);
-    const int shiftW = headRoom + 3;
-    const int offset = (1 << (shiftW - 1)) + (IF_INTERNAL_OFFS << 3);
-    return clampi((w * a + (8 - w) * b + offset) >> shiftW, 0, maxv);
+    const int angle = J.aux & 31, offX = (J.aux >> 8) & 255, offY = (J.aux >> 16) & 255;
+    const int lx = ((J.x >> cs) + cx - (J.pu_x >> cs)) << cs, ly = ((J.y >> cs) + cy - (J.pu_y >> cs)) << cs;
+    const int mir = c_geo_angle2mirror[angle];
+    const int X = mir == 1 ? GEO_WEIGHT_MASK_SIZE - 1 - offX - lx : offX + lx;
+    const int Y = mir == 2 ? GEO_WEIGHT_MASK_SIZE - 1 - offY - ly : offY + ly;
+    const int b = c_geo_mask_angle[c_geo_angle2mask[angle]];
+    const int dX = c_geo_dis[b], dY = c_geo_dis[(b + 8) & 31];
+    const int rho = (dX << 8) + (dY << 8);
+    C.geo = true;
+    C.gb = (((X + GEO_MASK_OFFSET) << 1) + 1) * dX + (((Y + GEO_MASK_OFFSET) << 1) + 1) * dY - rho;
+    C.gdx = ((mir == 1 ? -2 : 2) * dX) << cs;
+    C.gdy = ((mir == 2 ? -2 : 2) * dY) << cs;
+    C.w0 = C.w1 = 0;
+    return C;
   }
-  if (J.bcw != 2) {   // AreaBuf<Pel>::addWeightedAvg (Buffer.cpp:350)
-    const int w1 = c_bcw_w1[J.bcw], w0 = 8 - w1;
-    const int shiftNum = headRoom + 3;
-    const int offset = (1 << (shiftNum - 1)) + (IF_INTERNAL_OFFS << 3);
-    return clampi((a * w0 + b * w1 + offset) >> shiftNum, 0, maxv);
-  }
-  const int shiftNum = headRoom + 1;   // AreaBuf<Pel>::addAvg (Buffer.cpp:447)
-  const int offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
-  return clampi((a + b + offset) >> shiftNum, 0, maxv);
+  const int w1 = c_bcw_w1[J.bcw];   // BCW (bcw == 2: the equal weights, used only through addAvg)
+  C.w0 = 8 - w1; C.w1 = w1;
+  return C;
 }
-
+// one sample at column q / row o of the cell
+__device__ __forceinline__ int comb_apply(const Comb &C, int q, int o, int a, int b, int maxv) {
+  int w0 = C.w0, w1 = C.w1;
+  if (C.geo) {
+    w0 = clampi((32 + C.gb + q * C.gdx + o * C.gdy + 4) >> 3, 0, 8);
+    w1 = 8 - w0;
+  }
+  return clampi(((a * w0 + b * w1 + C.k) >> C.s) + C.o, 0, maxv);
+}
 
 // ------------------------------------------------------------------------------------------------
 // k_mc: one lane per cell, no LDS and no barriers. A luma cell is 4 columns x 8 rows of one job, a chroma
@@ -351,39 +376,34 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
       if (nc == 4) ((uint32_t *)q)[1] = pk(a[2], a[3]);
     }
   };
-  const CellWin W0 = cell_win(P, J, comp, l0 ? 0 : 1, x, y);
-  if (!bi) {
-    cell_filter<N, R>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
-      int a[4];
-      if (rnd) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) a[q] = clampi(v[q], 0, maxv);
-      } else {   // uni with explicit WP (14-bit intermediates, WeightPrediction::addWeightUni)
-#pragma unroll
-        for (int q = 0; q < 4; q++) a[q] = combine(P, WT, J, comp, cx + q, cy + o, v[q], v[q]);
-      }
-      store(o, a);
-    });
-    return;
-  }
-  // bi: list 0's rows kept as packed 14-bit pairs, combined with list 1's as those arrive
+  // bi: list 0 first, its rows kept as packed 14-bit pairs; then the last list (list 1, or the only list of
+  // a uni job) through ONE filter body whose emit combines: uni and bi share it (separate bodies per case
+  // tripled k_mc's code, and its instruction footprint, not its VALU count, stretched the waves, r04)
+  const bool avg = bi && !(J.flags & (MC_WP | MC_GEO)) && J.bcw == 2;
   uint32_t p0[R][2];
-  cell_filter<N, R>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
-    p0[o][0] = pk(v[0], v[1]);
-    p0[o][1] = pk(v[2], v[3]);
-  });
-  const CellWin W1 = cell_win(P, J, comp, 1, x, y);
-  const bool avg = !(J.flags & (MC_WP | MC_GEO)) && J.bcw == 2;
-  cell_filter<N, R>(W1.R, W1.ox, W1.oy, W1.fx, W1.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
-    const int u[4] = {lo16(p0[o][0]), hi16(p0[o][0]), lo16(p0[o][1]), hi16(p0[o][1])};
+  if (bi) {
+    const CellWin W0 = cell_win(P, J, comp, 0, x, y);
+    cell_filter<N, R>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
+      p0[o][0] = pk(v[0], v[1]);
+      p0[o][1] = pk(v[2], v[3]);
+    });
+  }
+  const Comb CB = comb_setup(WT, J, comp, bd, cx, cy);
+  const CellWin W = cell_win(P, J, comp, (bi || !l0) ? 1 : 0, x, y);
+  cell_filter<N, R>(W.R, W.ox, W.oy, W.fx, W.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
     int a[4];
-    if (avg) {   // AreaBuf::addAvg (Buffer.cpp:447)
+    if (rnd) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) a[q] = clampi(v[q], 0, maxv);
+    } else if (avg) {   // AreaBuf::addAvg (Buffer.cpp:447)
+      const int u[4] = {lo16(p0[o][0]), hi16(p0[o][0]), lo16(p0[o][1]), hi16(p0[o][1])};
       const int shiftNum = headRoom + 1, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
 #pragma unroll
       for (int q = 0; q < 4; q++) a[q] = clampi((u[q] + v[q] + offset) >> shiftNum, 0, maxv);
-    } else {
+    } else {   // uni WP, bi WP / GEO / BCW
+      const int u[4] = {bi ? lo16(p0[o][0]) : v[0], bi ? hi16(p0[o][0]) : v[1], bi ? lo16(p0[o][1]) : v[2], bi ? hi16(p0[o][1]) : v[3]};
 #pragma unroll
-      for (int q = 0; q < 4; q++) a[q] = combine(P, WT, J, comp, cx + q, cy + o, u[q], v[q]);
+      for (int q = 0; q < 4; q++) a[q] = comb_apply(CB, q, o, u[q], v[q], maxv);
     }
     store(o, a);
   });
@@ -401,11 +421,12 @@ __device__ __forceinline__ McJob load_job(const McJob *p) {
 
 // Grid: the luma cells of every class (ct.lcell0[ct.n] lanes), then the chroma cells, 256 lanes per
 // workgroup; the class of a lane is wave-uniform (class ranges are whole waves).
-__global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct) {
+__device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restrict__ jobs, const McClassTable &ct, int b
+#ifdef VVCR_MC_PROF
+                                        , unsigned long long &tag
+#endif
+) {
   const int nL = ct.lcell0[ct.n], nbL = (nL + 255) >> 8;
-  // XCD-aware order (measured on the 4K B pictures, r03): the workgroups one XCD receives take a contiguous
-  // run of cells, so neighbouring blocks' windows share that XCD's L2
-  const int b = xcd_swizzle(blockIdx.x, gridDim.x);
   const bool luma = b < nbL;
   const int g = (luma ? b : b - nbL) * 256 + (int)threadIdx.x;
   const int gw = __builtin_amdgcn_readfirstlane(g & ~63);   // the wave's first cell: selects the class
@@ -420,8 +441,17 @@ __global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict_
   const int i = g - c0;
   const int per = luma ? mc_luma_cells(w, h) : mc_chroma_cells(w, h);   // a power of two
   const int jn = i >> (__ffs(per) - 1), s = i & (per - 1);
+#ifdef VVCR_MC_PROF
+  tag = (unsigned long long)luma << 63 | (unsigned long long)(w & 255) << 8 | (h & 255);
+#endif
   if (jn >= jend - jbase) return;   // padding of the class's cell range (whole waves)
   const McJob J = load_job(jobs + jbase + jn);
+#ifdef VVCR_MC_PROF
+  tag |= (unsigned long long)__builtin_popcountll(__ballot((J.flags & (MC_L0 | MC_L1)) == (MC_L0 | MC_L1))) << 16 |
+         (unsigned long long)__builtin_popcountll(__ballot(J.flags & MC_RECON)) << 24 |
+         (unsigned long long)__builtin_popcountll(__ballot(J.flags & (MC_WP | MC_GEO))) << 32 |
+         (unsigned long long)__builtin_popcountll(__ballot(1)) << 40;
+#endif
   const WpTable &WT = *P.wpd;
   if (luma) {
     const int ncx = w >> 2, cx = s & (ncx - 1), cy = s >> (__ffs(ncx) - 1);
@@ -433,11 +463,49 @@ __global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict_
     mc_cell<4, 4>(P, WT, J, comp, (J.x >> 1) + 4 * cx, (J.y >> 1) + 4 * cy, min(4, cw - 4 * cx), min(4, chh - 4 * cy));
   }
 }
+__global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct, int V) {
+#ifdef VVCR_MC_PROF
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
+  const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // XCC_ID
+#endif
+#ifdef VVCR_MC_PROF
+  unsigned long long tag = 0;
+#define MC_BODY(b) mc_body(P, jobs, ct, b, tag)
+#else
+#define MC_BODY(b) mc_body(P, jobs, ct, b)
+#endif
+  // XCD-aware order (measured on the 4K B pictures, r03): the workgroups one XCD receives take a contiguous
+  // run of blocks (256 cells each), so neighbouring blocks' windows share that XCD's L2. A grid smaller
+  // than the V blocks is persistent: workgroup j of XCD x walks run x with stride G / 8.
+  const int G = gridDim.x;
+  if (G >= V) {
+    MC_BODY(xcd_swizzle(blockIdx.x, G));
+  } else {
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, Gx = G >> 3;   // G: a multiple of 8
+    const int per = V >> 3, rem = V & 7;
+    const int lo = x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per, n = per + (x < rem ? 1 : 0);
+    for (int k = j; k < n; k += Gx) MC_BODY(lo + k);
+  }
+#undef MC_BODY
+#ifdef VVCR_MC_PROF
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0 && wv < (1 << 16)) {
+    g_mcprof[wv][0] = t0; g_mcprof[wv][1] = t1; g_mcprof[wv][2] = (unsigned long long)hw | (unsigned long long)xcc << 32; g_mcprof[wv][3] = tag;
+  }
+#endif
+}
 
 }  // namespace
 
 void launch_mc(const McParams &p, const McJob *jobs, const McClassTable &ct, hipStream_t s) {
   if (ct.n <= 0) return;
-  const int g = ((ct.lcell0[ct.n] + 255) >> 8) + ((ct.ccell0[ct.n] + 255) >> 8);
-  if (g > 0) hipLaunchKernelGGL(k_mc, dim3(g), dim3(256), 0, s, p, jobs, ct);
+  const int V = ((ct.lcell0[ct.n] + 255) >> 8) + ((ct.ccell0[ct.n] + 255) >> 8);
+  static const int cap = [] {
+    const char *e = getenv("VVCR_MC_WGS");   // persistent grid (experiments): workgroups, a multiple of 8
+    return e ? (atoi(e) & ~7) : 0;
+  }();
+  const int g = cap >= 8 && cap < V ? cap : V;
+  if (V > 0) hipLaunchKernelGGL(k_mc, dim3(g), dim3(256), 0, s, p, jobs, ct, V);
 }
