@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stream", default="ra2160_q32")
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--all-stages", action="store_true", help="prepare and launch every stage (the fused reconstruction path of k_mc)")
     a = ap.parse_args()
     pics = S.load_sequence(os.path.join(ROOT, "tests", "golden", a.stream))
     h0 = pics[0]["hdr"]
@@ -30,7 +31,9 @@ def main():
             continue
         ctx.begin_picture(S.pic_params(p, slot, alloc.slot_of))
         S.submit(ctx, p)
-        hs.append(ctx.prepare(N.STAGE_INTER))
+        if a.all_stages:
+            S.set_loop_filter_params(ctx, p)
+        hs.append(ctx.prepare(N.STAGE_ALL if a.all_stages else N.STAGE_INTER))
     ctx.set_timing(False)
     for h in hs:
         ctx.launch(h)

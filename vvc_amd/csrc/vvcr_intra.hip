@@ -1127,7 +1127,7 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
           g_iprof[slot][5] = (unsigned long long)J.comp | (unsigned long long)J.w << 8 | (unsigned long long)J.h << 16 |
                              (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40;
           g_iprof[slot][6] = (unsigned long long)gj | (unsigned long long)blockIdx.x << 32;
-          g_iprof[slot][7] = ps[9] - ps[0];
+          g_iprof[slot][7] = (unsigned long long)(uint16_t)J.x | (unsigned long long)(uint16_t)J.y << 16 | (unsigned long long)c << 32;
         }
       }
 #endif

@@ -89,7 +89,10 @@ __device__ __forceinline__ int at(const DPlane &p, int x, int y) {
   y = y < 0 ? 0 : (y >= p.h ? p.h - 1 : y);
   return p.p[(size_t)y * p.stride + x];
 }
-__device__ __forceinline__ int clip_alf(int c, int ref, int v0, int v1) { return clip3(-c, c, v0 - ref) + clip3(-c, c, v1 - ref); }
+// min / max (one v_med3_i32 each), not clip3's compare-and-select
+__device__ __forceinline__ int clip_alf(int c, int ref, int v0, int v1) {
+  return min(max(v0 - ref, -c), c) + min(max(v1 - ref, -c), c);
+}
 
 // Rows of the diamond's taps at distance 1..3 below (r1, r3, r5) / above (r2, r4, r6) row y, padded at
 // the ALF virtual boundary (AdaptiveLoopFilter.cpp filterBlk); all selects (conditional assignments
@@ -151,7 +154,8 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
   __shared__ __attribute__((aligned(16))) int16_t t[ALF_SH * ALF_SW];
   __shared__ __attribute__((aligned(16))) int16_t tc[2][ALF_CSH * ALF_CSW];
   __shared__ int32_t blk[(ALF_TW / 4) * (ALF_TH / 4)];   // class | transpose << 8 | enabled << 16
-  __shared__ int16_t s_cf[25 * 13], s_cl[25 * 13];       // the CTB's filter set: coefficients / clips per class
+  // the CTB's filter set per class, packed for the tap arithmetic: (c, c), (l, l), (-l, -l)
+  __shared__ uint4 s_cc[25 * 13];   // .x (c, c)  .y (l, l)  .z (-l, -l): one 16-byte LDS read per tap
   __shared__ int8_t s_perm[4 * 13];
   const int X0 = tx * ALF_TW, Y0 = P.y0 + ty * ALF_TH;
   const int cx0 = X0 >> 1, cy0 = Y0 >> 1;
@@ -186,7 +190,10 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
 #pragma unroll
     for (int q = 0; q < NC; q++) {
       const int i = tid + 256 * q;
-      if (i < 25 * 13) { s_cf[i] = cfv[q]; s_cl[i] = clv[q]; }
+      if (i < 25 * 13) {
+        const uint32_t c = (uint16_t)cfv[q], l = (uint16_t)clv[q], nl = (uint16_t)(-clv[q]);
+        s_cc[i] = make_uint4(c | c << 16, l | l << 16, nl | nl << 16, 0u);
+      }
     }
     if (tid < 4 * 13) s_perm[tid] = (&c_perm7[0][0])[tid];
   }
@@ -210,11 +217,13 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
 #pragma unroll
       for (int jj = 0; jj < 4; jj++) {
         const int ax = bx - 2 + jj * 2;
-        const int a = T(ax, ay) << 1, bb = T(ax + 1, ay + 1) << 1;
-        sumV += abs(a - T(ax, rA) - T(ax, rB)) + abs(bb - T(ax + 1, ay) - T(ax + 1, rB2));
-        sumH += abs(a - T(ax + 1, ay) - T(ax - 1, ay)) + abs(bb - T(ax + 2, rB) - T(ax, rB));
-        sumD0 += abs(a - T(ax - 1, rA) - T(ax + 1, rB)) + abs(bb - T(ax, ay) - T(ax + 2, rB2));
-        sumD1 += abs(a - T(ax - 1, rB) - T(ax + 1, rA)) + abs(bb - T(ax, rB2) - T(ax + 2, ay));
+        // |2 c - n1 - n2| as one v_sad_u16 each (all terms are non-negative and below 2^16)
+        const uint32_t a = T(ax, ay) << 1, bb = T(ax + 1, ay + 1) << 1;
+        auto sad = [](uint32_t c, int n1, int n2, int acc) { return (int)__builtin_amdgcn_sad_u16(c, (uint32_t)(n1 + n2), (uint32_t)acc); };
+        sumV = sad(a, T(ax, rA), T(ax, rB), sad(bb, T(ax + 1, ay), T(ax + 1, rB2), sumV));
+        sumH = sad(a, T(ax + 1, ay), T(ax - 1, ay), sad(bb, T(ax + 2, rB), T(ax, rB), sumH));
+        sumD0 = sad(a, T(ax - 1, rA), T(ax + 1, rB), sad(bb, T(ax, ay), T(ax + 2, rB2), sumD0));
+        sumD1 = sad(a, T(ax - 1, rB), T(ax + 1, rA), sad(bb, T(ax, rB2), T(ax + 2, ay), sumD1));
       }
     }
 #pragma unroll
@@ -253,7 +262,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
         for (int y = by; y < by + 4 && y < H; y++) dst[(size_t)y * D.stride] = (int16_t)T(x, y);
       } else {
         const int classIdx = bi & 255, tr = (bi >> 8) & 255;
-        const int16_t *coef = s_cf + classIdx * 13, *clip = s_cl + classIdx * 13;
+        const uint4 *cc = s_cc + classIdx * 13;
         // packed 16-bit arithmetic: the two samples of a tap pair as one int16x2 (differences to the centre
         // fit 16 bits, clips <= 1 << bd), clipped with packed min / max, then one dot2 with the coefficient
         // pair (c, c): exactly c * clip(a - cur) + c * clip(b - cur)
@@ -261,12 +270,47 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
 #pragma unroll
         for (int k = 0; k < 12; k++) {
           const int pk = s_perm[tr * 13 + k];
-          const int c = coef[pk], l = clip[pk];
-          fcp[k] = (short2_t){(short)c, (short)c};
-          clp[k] = (short2_t){(short)l, (short)l};
-          cln[k] = (short2_t){(short)-l, (short)-l};
+          const uint4 e = cc[pk];
+          fcp[k] = __builtin_bit_cast(short2_t, e.x);
+          clp[k] = __builtin_bit_cast(short2_t, e.y);
+          cln[k] = __builtin_bit_cast(short2_t, e.z);
         }
         const int maxv = (1 << P.bd) - 1;
+        const int yb = by & (vbH - 1);
+        if (yb != vbPos - 4 && yb != vbPos) {
+          // no row of this 4x4 block (one per wave: wave-uniform) touches the virtual boundary: every tap at a
+          // constant LDS offset from the block's column (immediate ds_read offsets, no row arithmetic)
+          // based at the window's top-left sample: every tap offset non-negative (ds_read offsets are unsigned)
+          const int16_t *c0 = &t[(by - Y0) * ALF_SW + (x - X0) + ALF_LX - 3];
+#define TT(dx, dy) ((int)c0[((dy) + 3) * ALF_SW + (dx) + 3])
+#pragma unroll
+          for (int dy = 0; dy < 4; dy++) {
+            if (by + dy >= H) break;
+            const int cur = TT(0, dy);
+            const short2_t cc2 = {(short)cur, (short)cur};
+            int sum = 0;
+            auto tap = [&](int k, int a, int b) {
+              short2_t d = (short2_t){(short)a, (short)b} - cc2;
+              d = __builtin_elementwise_min(__builtin_elementwise_max(d, cln[k]), clp[k]);
+              sum = __builtin_amdgcn_sdot2(d, fcp[k], sum, false);
+            };
+            tap(0, TT(0, dy + 3), TT(0, dy - 3));
+            tap(1, TT(1, dy + 2), TT(-1, dy - 2));
+            tap(2, TT(0, dy + 2), TT(0, dy - 2));
+            tap(3, TT(-1, dy + 2), TT(1, dy - 2));
+            tap(4, TT(2, dy + 1), TT(-2, dy - 1));
+            tap(5, TT(1, dy + 1), TT(-1, dy - 1));
+            tap(6, TT(0, dy + 1), TT(0, dy - 1));
+            tap(7, TT(-1, dy + 1), TT(1, dy - 1));
+            tap(8, TT(-2, dy + 1), TT(2, dy - 1));
+            tap(9, TT(3, dy), TT(-3, dy));
+            tap(10, TT(2, dy), TT(-2, dy));
+            tap(11, TT(1, dy), TT(-1, dy));
+            sum = (sum + 64) >> 7;
+            dst[(size_t)(by + dy) * D.stride] = (int16_t)clip3(0, maxv, sum + cur);
+          }
+#undef TT
+        } else
 #pragma unroll
         for (int dy = 0; dy < 4; dy++) {
           const int y = by + dy;
@@ -307,11 +351,10 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
     const DPlane &C1 = P.src[1];
     if (x < C1.w && y < C1.h && y < (P.y1 >> 1)) {
 #define TC(k, xx, yy) ((int)tc[k][((yy) - cy0 + 2) * ALF_CSW + (xx) - cx0 + 8])
-      const int cl2 = P.ctu_log2 - 1;
-      const int ctb = (y >> cl2) * P.wc + (x >> cl2);
+      const int ctb = ctbT;   // the region lies in one CTB: uniform, so the filter's coefficients are scalars
       const int n = P.nctb;
       const int maxv = (1 << P.bd) - 1;
-      const int vbHc = 1 << cl2, vbPosC = P.vb_chroma;
+      const int vbHc = 1 << (P.ctu_log2 - 1), vbPosC = P.vb_chroma;
       int r1, r2, r3, r4, r5, r6;
       alf_rows(y, vbHc, vbPosC, false, r1, r2, r3, r4, r5, r6);
       (void)r5; (void)r6;
@@ -323,7 +366,8 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
       const int yVb = y & (vbHc - 1);
       const bool nearVB = (yVb == vbPosC - 1) || (yVb == vbPosC);
       // CC-ALF luma taps (clamped to the picture like the staged tile: AdaptiveLoopFilter.cpp:411)
-      auto L = [&](int xx, int yy) { return T(clip3(0, W - 1, xx), clip3(0, H - 1, yy)); };
+      // (the staged tile holds picture-clamped samples at every position: no clamps here)
+      auto L = [&](int xx, int yy) { return T(xx, yy); };
       int sl[8] = {};
       if (P.en[3] || P.en[4]) {
         sl[0] = L(lx, ly);
@@ -335,7 +379,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
       for (int k = 0; k < 2; k++) {
         const int comp = 1 + k;
         const DPlane &Sc = P.src[comp];
-        auto A = [&](int xx, int yy) { return TC(k, clip3(0, Sc.w - 1, xx), clip3(0, Sc.h - 1, yy)); };
+        auto A = [&](int xx, int yy) { return TC(k, xx, yy); };
         const int cur = TC(k, x, y);
         const bool on = P.en[comp] && P.ctb_en[comp * n + ctb];
         const int alt = P.ctb_alt[comp * n + ctb];
@@ -345,9 +389,16 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
           const int16_t *fc = P.chroma_coef + alt * 7, *fl = P.chroma_clip + alt * 7;
           const int q[12] = {A(x, r3), A(x, r4), A(x + 1, r1), A(x - 1, r2), A(x, r1), A(x, r2),
                              A(x - 1, r1), A(x + 1, r2), A(x + 2, y), A(x - 2, y), A(x + 1, y), A(x - 1, y)};
+          // packed like the luma taps: the pair's differences to the centre clipped as int16x2, one dot2
+          const short2_t cc2 = {(short)cur, (short)cur};
           int sum = 0;
 #pragma unroll
-          for (int tt = 0; tt < 6; tt++) sum += fc[tt] * clip_alf(fl[tt], cur, q[2 * tt], q[2 * tt + 1]);
+          for (int tt = 0; tt < 6; tt++) {
+            const short c = fc[tt], l = fl[tt];
+            short2_t d = (short2_t){(short)q[2 * tt], (short)q[2 * tt + 1]} - cc2;
+            d = __builtin_elementwise_min(__builtin_elementwise_max(d, (short2_t){(short)-l, (short)-l}), (short2_t){l, l});
+            sum = __builtin_amdgcn_sdot2(d, (short2_t){c, c}, sum, false);
+          }
           sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
           v = clip3(0, maxv, sum + cur);
         }

@@ -178,6 +178,15 @@ constexpr CellTaps make_cell_taps() {
 }
 __constant__ CellTaps c_ctaps = make_cell_taps();
 
+// Lanes per workgroup. k_mc shares nothing within a workgroup (no LDS, no barrier), and a workgroup's slot
+// is freed only when its slowest wave ends: one wave per workgroup lets every wave slot refill as soon as its
+// wave ends (with four, the luma waves' spread of lifetimes left CUs half empty, r04 per-wave trace).
+#ifndef MC_WG
+#define MC_WG 64
+#endif
+#ifndef MC_RESI_AHEAD
+#define MC_RESI_AHEAD 2
+#endif
 #ifndef MC_ROWS_AHEAD
 #define MC_ROWS_AHEAD 4
 #endif
@@ -192,6 +201,11 @@ typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 // wide (vvcr_create: width >= 16).
 template <int ND>
 __device__ __forceinline__ void load_nd(const int16_t *q, uint32_t (&w)[ND]) {
+#ifdef MC_ABL_LOADS   // diagnostics ablation: no reference loads (results wrong)
+#pragma unroll
+  for (int k = 0; k < ND; k++) w[k] = (uint32_t)(uintptr_t)q * (k + 3);
+  return;
+#endif
   const u32x4a v = *(const u32x4a *)q;
   w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
   if (ND == 6) {
@@ -231,9 +245,9 @@ __device__ __forceinline__ void edge_dwords(const int16_t *row, const EdgeMap &e
 // One list of a cell: R x 4 outputs of the N-tap separable filter from the reference plane R, window
 // origin (ox, oy) (first tap), fractions fx / fy, tap set ts (luma); emit(o, v) receives output row o,
 // v[c] = (V sum + off2) >> sh2 before any clamp, as soon as its last H row is filtered.
-template <int N, int R, class Emit>
+template <int N, int R, class Emit, class Pre>
 __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, int fx, int fy, int ts, int sh1, int off2, int sh2,
-                                            Emit &&emit) {
+                                            Emit &&emit, Pre &&pre) {
   constexpr int ND = N / 2 + 2, NT = N / 2 + 1, NV = N / 2, ROWS = R + N - 1;
   const int par = ox & 1, dc = ox - par;
   uint32_t T0[NT], T1[NT], TV[NV];
@@ -257,6 +271,9 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
   // pair lives only as long as an output still needs it
   auto hrow = [&](int r, const uint32_t (&w)[ND]) {
     int a = 0, b = 0, c = 0, d = 0;
+#ifdef MC_ABL_FILTER   // diagnostics ablation: no H filter arithmetic (results wrong)
+    a = w[0] ^ T0[0]; b = w[1] ^ T1[0]; c = w[2]; d = w[3];
+#else
 #pragma unroll
     for (int k = 0; k < NT; k++) {
       a = dot2(w[k], T0[k], a);
@@ -264,6 +281,7 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
       c = dot2(w[k + 1], T0[k], c);
       d = dot2(w[k + 1], T1[k], d);
     }
+#endif
     const int hs[4] = {a >> sh1, b >> sh1, c >> sh1, d >> sh1};
     if (r > 0) {
 #pragma unroll
@@ -277,8 +295,12 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         int acc = off2;
+#ifdef MC_ABL_FILTER
+        acc += Pv[q][o] ^ Pv[q][o + N - 2] ^ TV[0];
+#else
 #pragma unroll
         for (int m = 0; m < NV; m++) acc = dot2(Pv[q][o + 2 * m], TV[m], acc);
+#endif
         v[q] = acc >> sh2;
       }
       emit(o, v);
@@ -289,6 +311,7 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
     const int16_t *row = Rp.p + (size_t)oy * Rp.stride + dc;
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
+      pre(r);
       uint32_t w[ND];
       load_nd<ND>(row, w);
       hrow(r, w);
@@ -302,6 +325,7 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
     const EdgeMap e = edge_map<ND>(dc, Rp.w);
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
+      pre(r);
       const int16_t *row = Rp.p + (size_t)clampi(oy + r, 0, Rp.h - 1) * Rp.stride;
       uint32_t w[ND];
       edge_dwords<ND>(row, e, w);
@@ -359,14 +383,22 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
   const bool wide = nc == 4 && (x & 3) == 0;
   // one output row of 4 samples: 8-byte store, or 2-sample aligned pieces (chroma of blocks at odd
   // multiples of 4 luma columns, or 2 wide)
+  // MC_RESI: the residual row of output o is loaded MC_RESI_AHEAD H rows before the row that completes o
+  // (the last list's pre hook), so the store does not wait for a memory round trip of its own
+  uint32_t rres[R][2];
+  auto pre = [&](int r) {
+    const int o = r - (N - 1) + MC_RESI_AHEAD;
+    if (o < 0 || o >= R || !addResi || o >= nr) return;
+    const int16_t *rr = rsrc + (size_t)o * rstride;
+    rres[o][1] = 0;
+    if (wide) { const uint2 v = *(const uint2 *)rr; rres[o][0] = v.x; rres[o][1] = v.y; }
+    else { rres[o][0] = ((const uint32_t *)rr)[0]; if (nc == 4) rres[o][1] = ((const uint32_t *)rr)[1]; }
+  };
   auto store = [&](int o, int (&a)[4]) {
     if (o >= nr) return;
     int16_t *q = dst + (size_t)o * ostride;
     if (addResi) {
-      const int16_t *rr = rsrc + (size_t)o * rstride;
-      uint32_t r0, r1 = 0;
-      if (wide) { const uint2 v = *(const uint2 *)rr; r0 = v.x; r1 = v.y; }
-      else { r0 = ((const uint32_t *)rr)[0]; if (nc == 4) r1 = ((const uint32_t *)rr)[1]; }
+      const uint32_t r0 = rres[o][0], r1 = rres[o][1];
       a[0] = clampi(a[0] + lo16(r0), 0, maxv); a[1] = clampi(a[1] + hi16(r0), 0, maxv);
       a[2] = clampi(a[2] + lo16(r1), 0, maxv); a[3] = clampi(a[3] + hi16(r1), 0, maxv);
     }
@@ -386,7 +418,7 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
     cell_filter<N, R>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
       p0[o][0] = pk(v[0], v[1]);
       p0[o][1] = pk(v[2], v[3]);
-    });
+    }, [](int) {});
   }
   const Comb CB = comb_setup(WT, J, comp, bd, cx, cy);
   const CellWin W = cell_win(P, J, comp, (bi || !l0) ? 1 : 0, x, y);
@@ -406,7 +438,7 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
       for (int q = 0; q < 4; q++) a[q] = comb_apply(CB, q, o, u[q], v[q], maxv);
     }
     store(o, a);
-  });
+  }, pre);
 }
 
 // A job record through two 16-byte loads (per lane: the lanes of a wave hold different jobs).
@@ -419,16 +451,16 @@ __device__ __forceinline__ McJob load_job(const McJob *p) {
   return J;
 }
 
-// Grid: the luma cells of every class (ct.lcell0[ct.n] lanes), then the chroma cells, 256 lanes per
+// Grid: the luma cells of every class (ct.lcell0[ct.n] lanes), then the chroma cells, MC_WG lanes per
 // workgroup; the class of a lane is wave-uniform (class ranges are whole waves).
 __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restrict__ jobs, const McClassTable &ct, int b
 #ifdef VVCR_MC_PROF
                                         , unsigned long long &tag
 #endif
 ) {
-  const int nL = ct.lcell0[ct.n], nbL = (nL + 255) >> 8;
+  const int nL = ct.lcell0[ct.n], nbL = (nL + MC_WG - 1) / MC_WG;
   const bool luma = b < nbL;
-  const int g = (luma ? b : b - nbL) * 256 + (int)threadIdx.x;
+  const int g = (luma ? b : b - nbL) * MC_WG + (int)threadIdx.x;
   const int gw = __builtin_amdgcn_readfirstlane(g & ~63);   // the wave's first cell: selects the class
   // the class of the wave by a scan over static fields (wave-uniform selects; a class index used to read
   // the kernel argument would make it a per-lane indexed copy)
@@ -463,7 +495,7 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
     mc_cell<4, 4>(P, WT, J, comp, (J.x >> 1) + 4 * cx, (J.y >> 1) + 4 * cy, min(4, cw - 4 * cx), min(4, chh - 4 * cy));
   }
 }
-__global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct, int V) {
+__global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(4))) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct, int V) {
 #ifdef VVCR_MC_PROF
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
@@ -476,7 +508,7 @@ __global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict_
 #define MC_BODY(b) mc_body(P, jobs, ct, b)
 #endif
   // XCD-aware order (measured on the 4K B pictures, r03): the workgroups one XCD receives take a contiguous
-  // run of blocks (256 cells each), so neighbouring blocks' windows share that XCD's L2. A grid smaller
+  // run of blocks (MC_WG cells each), so neighbouring blocks' windows share that XCD's L2. A grid smaller
   // than the V blocks is persistent: workgroup j of XCD x walks run x with stride G / 8.
   const int G = gridDim.x;
   if (G >= V) {
@@ -490,7 +522,7 @@ __global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict_
 #undef MC_BODY
 #ifdef VVCR_MC_PROF
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int wv = blockIdx.x * (MC_WG / 64) + (threadIdx.x >> 6);
   if ((threadIdx.x & 63) == 0 && wv < (1 << 16)) {
     g_mcprof[wv][0] = t0; g_mcprof[wv][1] = t1; g_mcprof[wv][2] = (unsigned long long)hw | (unsigned long long)xcc << 32; g_mcprof[wv][3] = tag;
   }
@@ -501,11 +533,11 @@ __global__ __launch_bounds__(256) void k_mc(McParams P, const McJob *__restrict_
 
 void launch_mc(const McParams &p, const McJob *jobs, const McClassTable &ct, hipStream_t s) {
   if (ct.n <= 0) return;
-  const int V = ((ct.lcell0[ct.n] + 255) >> 8) + ((ct.ccell0[ct.n] + 255) >> 8);
+  const int V = (ct.lcell0[ct.n] + MC_WG - 1) / MC_WG + (ct.ccell0[ct.n] + MC_WG - 1) / MC_WG;
   static const int cap = [] {
     const char *e = getenv("VVCR_MC_WGS");   // persistent grid (experiments): workgroups, a multiple of 8
     return e ? (atoi(e) & ~7) : 0;
   }();
   const int g = cap >= 8 && cap < V ? cap : V;
-  if (V > 0) hipLaunchKernelGGL(k_mc, dim3(g), dim3(256), 0, s, p, jobs, ct, V);
+  if (V > 0) hipLaunchKernelGGL(k_mc, dim3(g), dim3(MC_WG), 0, s, p, jobs, ct, V);
 }

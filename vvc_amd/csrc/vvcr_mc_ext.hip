@@ -119,6 +119,7 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
   // staged reference windows: luma L0/L1 (23 x WS each), then the (component, list) chroma windows
   // (11 x CWS each); the two DMVR search windows reuse the luma part first
   __shared__ int16_t fwin[2 * LWIN + 4 * CWIN];
+  __shared__ int16_t swin[2 * LWIN + 4 * CWIN];   // DMVR: the final windows, shifted by the refinement
   __shared__ int16_t bl[2][BS * BS];
   __shared__ uint32_t sad[32];
   __shared__ int16_t hl[2][23 * 16];   // luma H outputs [list][row * 16 + col]
@@ -144,23 +145,31 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
   auto mvof = [&](int l, int c) { return l ? (int)J.mv[1][c] : (int)J.mv[0][c]; };
   auto slotof = [&](int l) { return l ? (int)J.slot[1] : (int)J.slot[0]; };
 
+  // ---- every reference window, gathered once at the unrefined MVs (one memory round trip per block):
+  // luma (w+7)x(h+7) from the integer MV - 3 per list, chroma (w/2+3)x(h/2+3) from - 1 per (component,
+  // list). These are xPrefetch's windows (InterPrediction.cpp:2050): the DMVR search window (w+5)x(h+5)
+  // at - 2 lies inside, and the final MC of the refined MV reads them with coordinates clamped to them
+  // (xPad's replication); without DMVR they are the final windows themselves.
+  {
+    constexpr int LIT = (LWIN + 127) / 128, CIT = (CWIN + 63) / 64;
+    int16_t vl[LIT] = {}, vc[CIT] = {};
+    gather_regs<LIT, WS, 128>(P.ref.get(slotof(ll), 0), J.x + (mvof(ll, 0) >> 4) - 3, J.y + (mvof(ll, 1) >> 4) - 3, w + 7, h + 7,
+                              none, li, vl);
+    gather_regs<CIT, CWS, 64>(P.ref.get(slotof(cl), 1 + ccomp), (J.x >> 1) + (mvof(cl, 0) >> 5) - 1, (J.y >> 1) + (mvof(cl, 1) >> 5) - 1,
+                              (w >> 1) + 3, (h >> 1) + 3, none, lane, vc);
+    regs_to_lds<LIT, 128>(fwin + ll * LWIN, LWIN, li, vl);
+    regs_to_lds<CIT, 64>(fwin + 2 * LWIN + wave * CWIN, CWIN, lane, vc);
+  }
+  __syncthreads();
+
   // ---- DMVR search (xinitMC, xBIPMVRefine, xDMVRSubPixelErrorSurface)
   int dx = 0, dy = 0;
   bool bdof = (J.flags & MC_BDOF) != 0;
   if (dmvr) {
     const int shB = bd - 6, offB = 1 << (shB - 1);   // IF_FILTER_PREC_BILINEAR - (IF_INTERNAL_PREC_BILINEAR - bd)
     {
-      // this list's (w+5)x(h+5) search window (21 rows of pitch WS at most)
-      constexpr int DIT = (21 * WS + 127) / 128;
-      int16_t v[DIT] = {};
-      gather_regs<DIT, WS, 128>(P.ref.get(slotof(ll), 0), J.x + (mvof(ll, 0) >> 4) - 2, J.y + (mvof(ll, 1) >> 4) - 2, w + 5, h + 5,
-                                none, li, v);
-      regs_to_lds<DIT, 128>(fwin + ll * LWIN, 21 * WS, li, v);
-    }
-    __syncthreads();
-    {
       const int fx = mvof(ll, 0) & 15, fy = mvof(ll, 1) & 15;
-      const int16_t *win = fwin + ll * LWIN;
+      const int16_t *win = fwin + ll * LWIN + WS + 1;   // the search window: one row / column in
       const int n = (w + 4) * (h + 4);
 #pragma unroll
       for (int k = 0; k < 4; k++) {
@@ -255,25 +264,40 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
     ix = bx + (mvx >> fb); iy = by + (mvy >> fb);
   };
   int lfx, lfy, lix, liy, cfx, cfy, cix, ciy;
+  const int16_t *lwin = fwin + ll * LWIN, *cwin = fwin + 2 * LWIN + wave * CWIN;
   {
     Clamp lc, cc;
     refined(ll, 0, lfx, lfy, lix, liy, lc);
     refined(cl, 1 + ccomp, cfx, cfy, cix, ciy, cc);
-    constexpr int LIT = (LWIN + 127) / 128, CIT = (CWIN + 63) / 64;
-    int16_t vl[LIT] = {}, vc[CIT] = {};
-    gather_regs<LIT, WS, 128>(P.ref.get(slotof(ll), 0), lix - 3, liy - 3, w + 7, h + 7, lc, li, vl);
-    gather_regs<CIT, CWS, 64>(P.ref.get(slotof(cl), 1 + ccomp), cix - 1, ciy - 1, (w >> 1) + 3, (h >> 1) + 3, cc, lane, vc);
-    regs_to_lds<LIT, 128>(fwin + ll * LWIN, LWIN, li, vl);
-    regs_to_lds<CIT, 64>(fwin + 2 * LWIN + wave * CWIN, CWIN, lane, vc);
+    if (dmvr) {
+      // the refined windows from the staged ones: window coordinates shifted by the refinement's integer
+      // part and clamped to the prefetched window (the clamp of sample(): xPad replication; the staged
+      // samples are already clamped to the picture)
+      const int lox = lix - 3 - lc.x0, loy = liy - 3 - lc.y0, cox = cix - 1 - cc.x0, coy = ciy - 1 - cc.y0;
+      const int lmx = lc.x1 - lc.x0, lmy = lc.y1 - lc.y0, cmx = cc.x1 - cc.x0, cmy = cc.y1 - cc.y0;
+      int16_t *ld = swin + ll * LWIN, *cd = swin + 2 * LWIN + wave * CWIN;
+#pragma unroll
+      for (int k = 0; k < (LWIN + 127) / 128; k++) {
+        const int i = li + 128 * k, r = i / WS, c = i - r * WS;
+        if (r < h + 7 && c < w + 7) ld[i] = lwin[clampi(r + loy, 0, lmy) * WS + clampi(c + lox, 0, lmx)];
+      }
+#pragma unroll
+      for (int k = 0; k < (CWIN + 63) / 64; k++) {
+        const int i = lane + 64 * k, r = i / CWS, c = i - r * CWS;
+        if (r < (h >> 1) + 3 && c < (w >> 1) + 3) cd[i] = cwin[clampi(r + coy, 0, cmy) * CWS + clampi(c + cox, 0, cmx)];
+      }
+      lwin = ld;
+      cwin = cd;
+      __syncthreads();
+    }
   }
-  __syncthreads();
 
   // ---- H pass (intermediate 14-bit values: (sum + off1) >> sh1, InterpolationFilter::filter isFirst)
   const int sh1 = IF_FILTER_PREC - headRoom, off1 = -(IF_INTERNAL_OFFS << sh1);
   {
     int th[8];
     luma_taps8(lfx, alt, th);
-    const int16_t *win = fwin + ll * LWIN;
+    const int16_t *win = lwin;
     const int n = (h + 7) * w, lw = w == 16 ? 4 : 3;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -289,7 +313,7 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
     }
     int tc[4];
     chroma_taps4(cfx, tc);
-    const int16_t *cw = fwin + 2 * LWIN + wave * CWIN;
+    const int16_t *cw = cwin;
     const int cwid = w >> 1, cn = ((h >> 1) + 3) * cwid, clw = cwid == 8 ? 3 : 2;
 #pragma unroll
     for (int k = 0; k < 2; k++) {
@@ -325,7 +349,7 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
     if (bdof) {
       // integer-sample ring (xPredInterBlk :812-846): nearest integer position, << headRoom, - offset; the
       // ring lies inside the staged 8-tap window (same clamps), 3 samples in from its top-left
-      const int16_t *win = fwin + ll * LWIN;
+      const int16_t *win = lwin;
       const int xo = lfx >= 8 ? 1 : 0, yo = lfy >= 8 ? 1 : 0;
       const int n = 2 * (w + 2) + 2 * h;
       if (li < n) {
