@@ -409,11 +409,7 @@ static IntraParams make_intra_params(vvcr_ctx *ctx, const Prepared &r, int lane)
 }
 
 // ---- algorithmic bytes: each logical input once, each output once, 2 B / sample
-static double mc_bytes(const McJob &j) {
-  const int lists = ((j.flags & MC_L0) ? 1 : 0) + ((j.flags & MC_L1) ? 1 : 0);
-  const double in = (double)(j.w + 7) * (j.h + 7) + 2.0 * (j.w / 2 + 3) * (j.h / 2 + 3);
-  return 2.0 * (lists * in + 1.5 * j.w * j.h);
-}
+static double mc_bytes(const McJob &j) { return mc_alg_bytes(j.flags, j.w, j.h); }   // + the residual when fused
 
 // Host phase, part 1 (no device): every work list of the picture.
 static void plan_picture(vvcr_picture &b, uint32_t mask) {
@@ -527,6 +523,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
       const int lists = U.l[0].present + U.l[1].present;
       const double nsb = (j.w / 4.0) * (j.h / 4.0);
       b += 2.0 * (lists * nsb * (81 + 2 * 0.25 * 49) + 1.5 * j.w * j.h);   // 6-tap (4+5)^2 luma, 4-tap chroma
+      if (U.recon & MC_RESI) b += 2.0 * 1.5 * j.w * j.h;                     // the residual of a fused reconstruction
     }
     r.alg_bytes[K_MC_AFFINE] = b;
   }

@@ -37,14 +37,6 @@ void push_tiles(bigbuf::vec<McJob> &out, int x0, int y0, int w, int h, McJob pro
     }
 }
 
-// Algorithmic bytes of one plain MC unit (SURVEY.md 8(d)): every reference window once per list (8-tap luma
-// (w+7)(h+7), 4-tap chroma 2 (w/2+3)(h/2+3)) and the 4:2:0 prediction written once, 2 B per sample.
-double mc_alg_bytes(uint16_t flags, int w, int h) {
-  const int lists = ((flags & MC_L0) ? 1 : 0) + ((flags & MC_L1) ? 1 : 0);
-  const double in = (double)(w + 7) * (h + 7) + 2.0 * (w / 2 + 3) * (h / 2 + 3);
-  // + the residual read by a fused reconstruction (MC_RESI); the output is written once either way
-  return 2.0 * (lists * in + 1.5 * w * h + ((flags & MC_RESI) ? 1.5 * w * h : 0.0));
-}
 
 // One plain MC unit (a PU, or an SbTMVP sub-block): 32x32 tiles for k_mc_tile when the PU is at least
 // 32x32 (all VVC block sizes are powers of two, so the tiles cover it exactly), else <= 16x16 jobs.
@@ -122,6 +114,15 @@ void set_wp(const vvcr_pic_params &pp, McJob &j, int r0, int r1, int cu_bcw) {
 }
 
 }  // namespace
+
+// Algorithmic bytes of one plain MC unit (SURVEY.md 8(d)): every reference window once per list (8-tap luma
+// (w+7)(h+7), 4-tap chroma 2 (w/2+3)(h/2+3)) and the 4:2:0 prediction written once, 2 B per sample.
+double mc_alg_bytes(uint16_t flags, int w, int h) {
+  const int lists = ((flags & MC_L0) ? 1 : 0) + ((flags & MC_L1) ? 1 : 0);
+  const double in = (double)(w + 7) * (h + 7) + 2.0 * (w / 2 + 3) * (h / 2 + 3);
+  // + the residual read by a fused reconstruction (MC_RESI); the output is written once either way
+  return 2.0 * (lists * in + 1.5 * w * h + ((flags & MC_RESI) ? 1.5 * w * h : 0.0));
+}
 
 void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d) {
   const int ncu = (int)d.cu.size(), npu = (int)d.pu.size(), ntu = (int)d.tu.size();
@@ -347,6 +348,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
         if (p.interdir & 1) U.l[0] = affine_list(pp, c, p, 0);
         if (p.interdir & 2) U.l[1] = affine_list(pp, c, p, 1);
         U.wp = wp_applies(pp, p.interdir == 3, c.bcw) ? 1 : 0;
+        U.recon = (int16_t)recon;
         for (int l = 0; l < 2; l++) {   // the sub-block MVs lie within the model's values at the PU corners
           if (!U.l[l].present) continue;
           const AffList &A = U.l[l];
@@ -371,6 +373,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
         if ((j.flags & (MC_L0 | MC_L1)) != (MC_L0 | MC_L1)) fail("DMVR/BDOF PU is not bi-predicted");
         if (p.w % 8 || p.h % 8) fail("DMVR/BDOF PU size is not a multiple of 8");   // k_mc_bidir: 8 or 16 per side
         if (p.bdof) j.flags |= MC_BDOF;
+        j.flags |= recon;
         if (p.dmvr) {
           // xProcessDMVR sub-blocks (InterPrediction.cpp:2162-2166), raster order = delta order
           j.flags |= MC_DMVR;

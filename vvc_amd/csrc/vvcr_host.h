@@ -75,6 +75,9 @@ struct ScanTables {
 };
 void build_scan_tables(ScanTables &st);
 
+// Algorithmic bytes of one plain / DMVR / BDOF MC unit (vvcr_host.cpp)
+double mc_alg_bytes(uint16_t flags, int w, int h);
+
 // Throws VvcrError on inconsistent descriptors (indices out of range, blocks outside the picture).
 void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d);
 // fuse: the picture's reconstruction stages run together (residual, inter, intra), so plain inter CUs are
@@ -83,16 +86,14 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
                       bool fuse);
 
 // Inter CUs whose motion compensation writes the reconstruction directly (prediction + residual, clipped,
-// into the picture: AreaBuf::reconstruct, Buffer.cpp:590, fused into k_mc's store): no LMCS in the
-// picture (no forward-mapped prediction, no chroma residual scaling), no CIIP, and every PU plain MC (no
-// affine, DMVR or BDOF: those kernels write the prediction planes). The work-list and intra planners
-// both apply it: k_mc takes these CUs, k_recon_inter the rest.
+// into the picture: AreaBuf::reconstruct, Buffer.cpp:590, fused into the final store of k_mc, k_mc_bidir
+// (DMVR / BDOF) and k_mc_affine): no LMCS in the picture (no forward-mapped prediction, no chroma
+// residual scaling) and no CIIP (its blend reads the prediction). The work-list and intra planners both
+// apply it: the MC kernels take these CUs, k_recon_inter the rest.
 inline bool fused_inter_cu(const vvcr_pic_params &pp, const PictureDescriptors &d, const vvcr_cu &c) {
-  if (pp.lmcs_enabled || c.predmode != 0 || !c.yvalid || !c.cvalid || c.affine || c.npu <= 0) return false;
-  for (int k = 0; k < c.npu; k++) {
-    const vvcr_pu &p = d.pu[c.firstpu + k];
-    if (p.ciip || p.dmvr || p.bdof) return false;
-  }
+  if (pp.lmcs_enabled || c.predmode != 0 || !c.yvalid || !c.cvalid || c.npu <= 0) return false;
+  for (int k = 0; k < c.npu; k++)
+    if (d.pu[c.firstpu + k].ciip) return false;
   return true;
 }
 

@@ -84,7 +84,8 @@ struct AffList {
 struct AffPu {
   int16_t x, y, w, h;                  // luma PU area
   int32_t bcw;                         // BcwIdx (2 = default)
-  int32_t wp;                          // explicit weighted prediction applies (uni: 14-bit kept, then addWeightUni)
+  int16_t wp;                          // explicit weighted prediction applies (uni: 14-bit kept, then addWeightUni)
+  int16_t recon;                       // MC_RECON / MC_RESI: the PU's reconstruction is written by k_mc_affine
   AffList l[2];
 };
 // Affine work item: one <= 16x16 luma tile (8x8-aligned inside the PU) and its chroma.

@@ -515,6 +515,23 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
     const int offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
     return clampi((a + b + offset) >> shiftNum, 0, maxv);
   };
+  // 4 samples of a row: to the prediction plane, or (U.recon, fused_inter_cu) clip(pred + resi) straight
+  // into the picture (AreaBuf::reconstruct, Buffer.cpp:590)
+  auto store4 = [&](int comp, int x, int y, int v0, int v1, int v2, int v3) {
+    if (U.recon & MC_RECON) {
+      if (U.recon & MC_RESI) {
+        const DPlane &r = P.resi[comp];
+        const uint2 q = *(const uint2 *)(r.p + (size_t)y * r.stride + x);
+        v0 = clampi(v0 + lo16(q.x), 0, maxv); v1 = clampi(v1 + hi16(q.x), 0, maxv);
+        v2 = clampi(v2 + lo16(q.y), 0, maxv); v3 = clampi(v3 + hi16(q.y), 0, maxv);
+      }
+      const DPlane &o = P.reco[comp];
+      *(uint2 *)(o.p + (size_t)y * o.stride + x) = make_uint2(pk(v0, v1), pk(v2, v3));
+    } else {
+      const DPlane &o = P.out[comp];
+      *(uint2 *)(o.p + (size_t)y * o.stride + x) = make_uint2(pk(v0, v1), pk(v2, v3));
+    }
+  };
   const int la = U.l[0].present ? 0 : 1;
   if (lane * 4 < w * h) {
     const int i = lane * 4, y = i / w, x = i - y * w;
@@ -522,8 +539,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
     const uint2 b = bi ? *(const uint2 *)&s_lo[1][y * 16 + x] : a;
     const int v0 = combine(0, lo16(a.x), lo16(b.x)), v1 = combine(0, hi16(a.x), hi16(b.x));
     const int v2 = combine(0, lo16(a.y), lo16(b.y)), v3 = combine(0, hi16(a.y), hi16(b.y));
-    const DPlane &o = P.out[0];
-    *(uint2 *)(o.p + (size_t)(J.y + y) * o.stride + J.x + x) = make_uint2(pk(v0, v1), pk(v2, v3));
+    store4(0, J.x + x, J.y + y, v0, v1, v2, v3);
   }
   if (lane >= 64) {
     const int comp = 1 + ((lane >> 5) & 1), i = (lane & 31) * 4;
@@ -533,8 +549,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
       const uint2 b = bi ? *(const uint2 *)&s_co[kb][y * 8 + x] : a;
       const int v0 = combine(comp, lo16(a.x), lo16(b.x)), v1 = combine(comp, hi16(a.x), hi16(b.x));
       const int v2 = combine(comp, lo16(a.y), lo16(b.y)), v3 = combine(comp, hi16(a.y), hi16(b.y));
-      const DPlane &o = P.out[comp];
-      *(uint2 *)(o.p + (size_t)((J.y >> 1) + y) * o.stride + (J.x >> 1) + x) = make_uint2(pk(v0, v1), pk(v2, v3));
+      store4(comp, (J.x >> 1) + x, (J.y >> 1) + y, v0, v1, v2, v3);
     }
   }
 }

@@ -374,6 +374,16 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
   }
   __syncthreads();
 
+  // one final sample: to the prediction plane, or (MC_RECON, fused_inter_cu) clip(pred + resi) straight
+  // into the picture (AreaBuf::reconstruct, Buffer.cpp:590)
+  auto store1 = [&](int comp, int x, int y, int v) {
+    if (J.flags & MC_RECON) {
+      if (J.flags & MC_RESI) v = clampi(v + P.resi[comp].p[(size_t)y * P.resi[comp].stride + x], 0, maxv);
+      P.reco[comp].p[(size_t)y * P.reco[comp].stride + x] = (int16_t)v;
+    } else {
+      P.out[comp].p[(size_t)y * P.out[comp].stride + x] = (int16_t)v;
+    }
+  };
   // ---- chroma: the default average of the two lists (addAvg)
   {
     const int shiftNum = headRoom + 1, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
@@ -381,18 +391,16 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
     if (tid < 2 * cn) {
       const int comp = tid >= cn ? 1 : 0, i = tid - comp * cn;
       const int y = i >> clw, x = i & (cwid - 1);
-      const DPlane &o = P.out[1 + comp];
       const int v = (co[2 * comp][y * 8 + x] + co[2 * comp + 1][y * 8 + x] + offset) >> shiftNum;
-      o.p[(size_t)((J.y >> 1) + y) * o.stride + (J.x >> 1) + x] = (int16_t)clampi(v, 0, maxv);
+      store1(1 + comp, (J.x >> 1) + x, (J.y >> 1) + y, clampi(v, 0, maxv));
     }
   }
-  const DPlane &o = P.out[0];
   const int lw = w == 16 ? 4 : 3;
   if (!bdof) {
     const int shiftNum = headRoom + 1, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
     if (tid < w * h) {
       const int y = tid >> lw, x = tid & (w - 1), idx = (y + 1) * PS + x + 1;
-      o.p[(size_t)(J.y + y) * o.stride + J.x + x] = (int16_t)clampi((pr[0][idx] + pr[1][idx] + offset) >> shiftNum, 0, maxv);
+      store1(0, J.x + x, J.y + y, clampi((pr[0][idx] + pr[1][idx] + offset) >> shiftNum, 0, maxv));
     }
     return;
   }
@@ -481,7 +489,7 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
       const int idx = (y + 1) * PS + x + 1;
       const int b = sh_v[u][0] * (gx[0][idx] - gx[1][idx]) + sh_v[u][1] * (gy[0][idx] - gy[1][idx]);
       const int v = (int16_t)((pr[0][idx] + pr[1][idx] + b + offset) >> shiftNum);
-      o.p[(size_t)(J.y + y) * o.stride + J.x + x] = (int16_t)clampi(v, 0, maxv);
+      store1(0, J.x + x, J.y + y, clampi(v, 0, maxv));
     }
   }
 }
