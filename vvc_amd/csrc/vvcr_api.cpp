@@ -157,6 +157,7 @@ struct Prepared {
   DevVec<WpTable> wpt;               // the slice's weighted-prediction table (k_mc reads it per lane)
   McClassTable mc_ct;                // k_mc cell classes of mc_basic
   bool have_sao = false, have_alf = false;
+  bool zero_filled = false;   // the residual areas read are zeroed by TB_ZERO jobs: no plane clear
   int n_tb = 0, n_tb_small = 0, n_mctile = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
   hipEvent_t ev[NK][2] = {};
   hipEvent_t start = nullptr, done = nullptr;   // whole launch (events of this picture only: an event
@@ -202,6 +203,7 @@ struct Prepared {
     for (int &c : dbk_counts) c = 0;
     have_sao = have_alf = false;
     n_tb = n_tb_small = n_mctile = n_basic = n_bidir = n_aff = n_tiles = n_dmvr = 0;
+    zero_filled = false;
     for (int k = 0; k < NK; k++) { ran[k] = timed[k] = false; alg_bytes[k] = 0; launches[k] = 0; }
     launched = false;
     lane = 0;
@@ -484,8 +486,9 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     st.add(r.tb, wl.tb);
     r.n_tb = (int)wl.tb.size();
     r.n_tb_small = wl.tb_small;
+    r.zero_filled = wl.zero_filled;
     double b = 0;
-    for (const TbJob &t : wl.tb) b += (double)t.w * t.h * (4 + 2);   // int32 levels in, int16 residual out
+    for (const TbJob &t : wl.tb) b += (double)t.w * t.h * ((t.flags & TB_ZERO) ? 2 : 4 + 2);   // int32 levels in, int16 residual out
     r.alg_bytes[K_RESID] = b;
   }
   if (mask & VVCR_STAGE_INTER) {
@@ -646,10 +649,12 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
   VVCR_CHECK_HIP(hipEventRecord(r.start, s));
   if (mask & VVCR_STAGE_RESID) {
     KernelTimer t(r, K_RESID, s, ctx->timing);
-    Planes3 clr{};
-    for (int c = 0; c < 3; c++) clr.dst[c] = ln.resi[c];
-    clr.y0 = own0; clr.y1 = own1;
-    launch_planes3(clr, s);
+    if (!r.zero_filled) {
+      Planes3 clr{};
+      for (int c = 0; c < 3; c++) clr.dst[c] = ln.resi[c];
+      clr.y0 = own0; clr.y1 = own1;
+      launch_planes3(clr, s);
+    }
     TbParams tp{};
     for (int c = 0; c < 3; c++) tp.out[c] = ln.resi[c];
     tp.bd = ctx->sp.bit_depth;

@@ -204,6 +204,7 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
 
 void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out,
                    bigbuf::vec<int32_t> &packed);
+void build_zero_jobs(const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out);
 
 namespace {
 
@@ -281,6 +282,10 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
                       bool fuse) {
   wl.clear();
   build_tb_jobs(sp, pp, d, wl.tb, wl.coef);
+  if (fuse) {   // the reconstruction stages run together: the residual reads are known, zero only those
+    build_zero_jobs(pp, d, wl.tb);
+    wl.zero_filled = true;
+  }
   // small blocks first (64-lane workgroups), then the large ones (256 lanes)
   wl.tb_small = (int)(std::stable_partition(wl.tb.begin(), wl.tb.end(), [](const TbJob &j) { return j.w * j.h <= 256; }) - wl.tb.begin());
   const int W4 = sp.width / 4;
@@ -653,6 +658,62 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
         j.flags |= TB_PACKED;
       }
       out.push_back(j);
+    }
+  }
+}
+
+// TB_ZERO jobs: every transform-block area whose residual a consumer reads but no coded block writes (the
+// residual planes are not cleared per picture when the reconstruction stages run together). Readers: intra
+// CUs (k_intra reads each step's residual rectangle), inter CUs reconstructed by k_recon_inter (LMCS / CIIP:
+// the whole CU), and fused inter CUs with a coded residual (MC_RESI: all three components of the CU).
+void build_zero_jobs(const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out) {
+  auto zero = [&](int comp, int x, int y, int w, int h) {
+    // split into blocks of at most 64 x 64 (the TbJob sides are 8-bit)
+    for (int yy = 0; yy < h; yy += 64)
+      for (int xx = 0; xx < w; xx += 64) {
+        TbJob j{};
+        j.x = (int16_t)(x + xx); j.y = (int16_t)(y + yy);
+        j.w = (uint8_t)std::min(64, w - xx); j.h = (uint8_t)std::min(64, h - yy);
+        j.comp = (uint8_t)comp;
+        j.flags = TB_ZERO;
+        out.push_back(j);
+      }
+  };
+  const int ncu = (int)d.cu.size();
+  bigbuf::vec<uint8_t> reads(ncu, 0);
+  for (int i = 0; i < ncu; i++) {
+    const vvcr_cu &c = d.cu[i];
+    if (!in_shard(pp, c)) continue;
+    if (c.predmode != MODE_INTER) { reads[i] = 1; continue; }
+    if (!fused_inter_cu(pp, d, c)) {
+      reads[i] = 1;
+      if (!c.rootcbf) {   // no transform tree: the whole CU reads zeros
+        if (c.yvalid) zero(0, c.x, c.y, c.w, c.h);
+        if (c.cvalid) { zero(1, c.cx, c.cy, c.cw, c.ch); zero(2, c.cx, c.cy, c.cw, c.ch); }
+        reads[i] = 0;
+      }
+      continue;
+    }
+    reads[i] = c.rootcbf ? 1 : 0;
+  }
+  for (size_t ti = 0; ti < d.tu.size(); ti++) {
+    const vvcr_tu &t = d.tu[ti];
+    if (t.cu < 0 || t.cu >= ncu || !reads[t.cu]) continue;
+    for (int comp = 0; comp < 3; comp++) {
+      const int32_t *b = t.b[comp];
+      if (b[2] <= 0) continue;
+      // the coded-block rule of build_tb_jobs: a JCCR Cb job writes Cr too
+      bool written;
+      if (comp == 2 && t.jccr) {
+        const int src = (t.jccr >> 1) ? 1 : 2;
+        written = t.b[src][6] >= 0;
+      } else if (comp == 1 && t.jccr) {
+        const int src = (t.jccr >> 1) ? 1 : 2;
+        written = t.b[src][6] >= 0;
+      } else {
+        written = b[4] != 0 && b[6] >= 0;
+      }
+      if (!written) zero(comp, b[0], b[1], b[2], b[3]);
     }
   }
 }

@@ -198,6 +198,7 @@ enum : uint8_t {
   TB_LFNST_TRANSPOSE = 1 << 3,
   TB_BDPCM_SHIFT = 4,          // bits 4..5: 0 off, 1 horizontal, 2 vertical
   TB_PACKED = 1 << 6,          // levels stored as the st_rows x st_cols box (row pitch st_cols), not w x h
+  TB_ZERO = 1 << 7,            // no coded levels: the block's residual is zero (written instead of a plane clear)
 };
 struct TbJob {
   int16_t x, y;                // component-plane position

@@ -97,6 +97,21 @@ __device__ __forceinline__ void resid_tb(const TbParams &P, const TbJob *jp, con
   const int lane = tid & 63;
   const TbJob J = load_uniform(jp);
   const int w = J.w, h = J.h, n = w * h;
+  if (J.flags & TB_ZERO) {   // a residual area read but not coded (TB_ZERO jobs replace the plane clear)
+    const DPlane &O = P.out[J.comp];
+    if ((w & 3) == 0 && (J.x & 3) == 0) {
+      for (int i = tid; i < (n >> 2); i += NT) {
+        const int yy = (i << 2) / w, xx = (i << 2) - yy * w;
+        *(uint2 *)&O.p[(size_t)(J.y + yy) * O.stride + J.x + xx] = make_uint2(0u, 0u);
+      }
+    } else {
+      for (int i = tid; i < n; i += NT) {
+        const int yy = i / w, xx = i - yy * w;
+        O.p[(size_t)(J.y + yy) * O.stride + J.x + xx] = 0;
+      }
+    }
+    return;
+  }
   const int lw = ilog2d(w), lh = ilog2d(h);
   const bool ts = J.flags & TB_TS;
   const bool dq = (J.flags & TB_DQ) && !ts;
