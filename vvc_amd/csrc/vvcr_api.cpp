@@ -1246,7 +1246,8 @@ int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int3
     s.launches = r->ran[k] ? r->launches[k] : 0;
     s.alg_bytes = r->ran[k] ? r->alg_bytes[k] : 0.0;
     float ms = 0;
-    if (r->ran[k] && r->timed[k]) VVCR_CHECK_HIP(hipEventElapsedTime(&ms, r->ev[k][0], r->ev[k][1]));
+    // a stage with nothing to launch has an empty event pair: no kernel time
+    if (r->ran[k] && r->timed[k] && r->launches[k] > 0) VVCR_CHECK_HIP(hipEventElapsedTime(&ms, r->ev[k][0], r->ev[k][1]));
     s.ms = ms;
   }
   return NK;
