@@ -292,7 +292,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
             auto tap = [&](int k, int a, int b) {
               short2_t d = (short2_t){(short)a, (short)b} - cc2;
               d = __builtin_elementwise_min(__builtin_elementwise_max(d, cln[k]), clp[k]);
-              sum = __builtin_amdgcn_sdot2(d, fcp[k], sum, false);
+              sum = __builtin_amdgcn_sdot2(d, fcp[k], sum, true);
             };
             tap(0, TT(0, dy + 3), TT(0, dy - 3));
             tap(1, TT(1, dy + 2), TT(-1, dy - 2));
@@ -325,7 +325,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
           auto tap = [&](int k, int a, int b) {
             short2_t d = (short2_t){(short)a, (short)b} - cc2;
             d = __builtin_elementwise_min(__builtin_elementwise_max(d, cln[k]), clp[k]);
-            sum = __builtin_amdgcn_sdot2(d, fcp[k], sum, false);
+            sum = __builtin_amdgcn_sdot2(d, fcp[k], sum, true);
           };
           tap(0, T(x, r5), T(x, r6));
           tap(1, T(x + 1, r3), T(x - 1, r4));
@@ -397,7 +397,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
             const short c = fc[tt], l = fl[tt];
             short2_t d = (short2_t){(short)q[2 * tt], (short)q[2 * tt + 1]} - cc2;
             d = __builtin_elementwise_min(__builtin_elementwise_max(d, (short2_t){(short)-l, (short)-l}), (short2_t){l, l});
-            sum = __builtin_amdgcn_sdot2(d, (short2_t){c, c}, sum, false);
+            sum = __builtin_amdgcn_sdot2(d, (short2_t){c, c}, sum, true);
           }
           sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
           v = clip3(0, maxv, sum + cur);

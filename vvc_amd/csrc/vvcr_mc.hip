@@ -270,12 +270,16 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
   // outputs whose last pair this row completes (output o reads pairs o, o + 2, .., o + N - 2), so that a
   // pair lives only as long as an output still needs it
   auto hrow = [&](int r, const uint32_t (&w)[ND]) {
-    int a = 0, b = 0, c = 0, d = 0;
+    int a, b, c, d;
 #ifdef MC_ABL_FILTER   // diagnostics ablation: no H filter arithmetic (results wrong)
     a = w[0] ^ T0[0]; b = w[1] ^ T1[0]; c = w[2]; d = w[3];
 #else
+    a = dot2(w[0], T0[0], 0);
+    b = dot2(w[0], T1[0], 0);
+    c = dot2(w[1], T0[0], 0);
+    d = dot2(w[1], T1[0], 0);
 #pragma unroll
-    for (int k = 0; k < NT; k++) {
+    for (int k = 1; k < NT; k++) {
       a = dot2(w[k], T0[k], a);
       b = dot2(w[k], T1[k], b);
       c = dot2(w[k + 1], T0[k], c);
@@ -294,12 +298,13 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
       int v[4];
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        int acc = off2;
+        int acc;
 #ifdef MC_ABL_FILTER
-        acc += Pv[q][o] ^ Pv[q][o + N - 2] ^ TV[0];
+        acc = off2 + (Pv[q][o] ^ Pv[q][o + N - 2] ^ TV[0]);
 #else
+        acc = dot2(Pv[q][o], TV[0], off2);
 #pragma unroll
-        for (int m = 0; m < NV; m++) acc = dot2(Pv[q][o + 2 * m], TV[m], acc);
+        for (int m = 1; m < NV; m++) acc = dot2(Pv[q][o + 2 * m], TV[m], acc);
 #endif
         v[q] = acc >> sh2;
       }
@@ -396,6 +401,9 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
   };
   auto store = [&](int o, int (&a)[4]) {
     if (o >= nr) return;
+#ifdef MC_ABL_STORE   // diagnostics ablation: no stores unless the value is impossible (results wrong)
+    if (a[0] != -12345) return;
+#endif
     int16_t *q = dst + (size_t)o * ostride;
     if (addResi) {
       const uint32_t r0 = rres[o][0], r1 = rres[o][1];
@@ -478,6 +486,10 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
 #endif
   if (jn >= jend - jbase) return;   // padding of the class's cell range (whole waves)
   const McJob J = load_job(jobs + jbase + jn);
+#ifdef MC_ABL_EXIT   // diagnostics ablation: the job record only (results wrong)
+  if (J.flags == 0xffff) P.out[0].p[jn] = 1;
+  return;
+#endif
 #ifdef VVCR_MC_PROF
   tag |= (unsigned long long)__builtin_popcountll(__ballot((J.flags & (MC_L0 | MC_L1)) == (MC_L0 | MC_L1))) << 16 |
          (unsigned long long)__builtin_popcountll(__ballot(J.flags & MC_RECON)) << 24 |

@@ -13,8 +13,11 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 
 typedef short short2_t __attribute__((ext_vector_type(2)));
 // a.lo * b.lo + a.hi * b.hi + c (signed 16-bit halves)
+// a * b + c over int16 pairs, always in the three-operand form: the clamp bit (an i32 saturation no sum of
+// ours reaches: filter sums stay below 2^24) keeps the compiler from the two-operand v_dot2c, whose
+// accumulator is its destination and costs a v_mov per chain start (13 % of k_mc's filter VALU, r04).
 __device__ __forceinline__ int dot2(uint32_t a, uint32_t b, int c) {
-  return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, a), __builtin_bit_cast(short2_t, b), c, false);
+  return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, a), __builtin_bit_cast(short2_t, b), c, true);
 }
 __host__ __device__ constexpr uint32_t pk(int lo, int hi) { return (uint32_t)(lo & 0xffff) | ((uint32_t)hi << 16); }
 
