@@ -67,11 +67,11 @@ struct Planner {
   }
   int get_tu(int x, int y, int ch) const {
     const int s = ch ? 1 : 2;
-    const int t = tu_map[ch][(size_t)(y >> s) * W4 + (x >> s)];
-    if (t < 0) throw VvcrError(VVCR_E_ARG, "deblocking: no TU covers a neighbouring position");
-    if (ch) return t;
-    const vvcr_cu &cu = d.cu[d.tu[t].cu];
-    if (cu.isp) {   // CodingStructure::getTU (CodingStructure.cpp:379): search the ISP sub-partitions
+    int t = tu_map[ch][(size_t)(y >> s) * W4 + (x >> s)];
+    if (t == -1) throw VvcrError(VVCR_E_ARG, "deblocking: no TU covers a neighbouring position");
+    if (t >= 0) return t;   // (chroma maps and non-ISP luma TUs: no descriptor read, the common case)
+    t = -t - 2;             // an ISP CU's area (the map holds -(first TU) - 2)
+    {       // CodingStructure::getTU (CodingStructure.cpp:379): search the ISP sub-partitions
       for (int k = 0; k < 4 && t + k < (int)d.tu.size(); k++) {
         const int32_t *b = d.tu[t + k].b[0];
         if (x >= b[BX] && x < b[BX] + b[BW] && y >= b[BY] && y < b[BY] + b[BH]) return t + k;
@@ -108,7 +108,7 @@ struct Planner {
       const int32_t *b0 = d.tu[t].b[0], *b1 = d.tu[t].b[1];
       if (b0[BW] > 0 && b0[BH] > 0) {
         if (c.isp) {   // the first ISP TU owns the CU area in the index map (CodingStructure::addTU :624)
-          if ((int)t == c.firsttu) fill(tu_map[0], c.x, c.y, c.w, c.h, 2, (int)t);
+          if ((int)t == c.firsttu) fill(tu_map[0], c.x, c.y, c.w, c.h, 2, -(int)t - 2);   // flagged: get_tu searches
         } else {
           fill(tu_map[0], b0[BX], b0[BY], b0[BW], b0[BH], 2, (int)t);
         }

@@ -297,12 +297,10 @@ __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int c
       gx[r] = min(max(ox + j, 0), D.w - 1); gy[r] = cy; need[r] = j <= nT && unitAv(unitT(j));
       gx[3 + r] = cx; gy[3 + r] = min(max(oy + j, 0), D.h - 1); need[3 + r] = j <= nL && unitAv(unitL(j));
     }
-    IPROF(7);
     gather(src, gx, gy, need, gvv);
 #pragma unroll
     for (int r = 0; r < 3; r++) { tv[r] = (int16_t)gvv[r]; lv[r] = (int16_t)gvv[3 + r]; }
   }
-  IPROF(8);
   bool missing = false;
 #pragma unroll
   for (int r = 0; r < 3; r++) {
@@ -312,7 +310,6 @@ __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int c
   }
   if (__ballot(missing) == 0) { wsync(); return; }
   wsync();
-  IPROF(9);
   // missing units: the scan-order last sample of the nearest earlier available unit, else the first
   // sample of the first available unit (both are copied samples)
   const int firstAv = lo ? __builtin_ctzll(lo) : 64;
@@ -584,8 +581,10 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       // CU-level fill of the first region (predSize per split direction), kept in refF for the others
       const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
       fill_refs(SD, D, 0, J.cx, J.cy, fTop, fLeft, 0, bd, avlo, avhi, top, left, lane, ps, J.vnb, J.nul, J.nut);
+      IPROF(7);
       if (nreg > 1)
         for (int i = lane; i < RB; i += 64) { S.refF[0][i] = top[i]; S.refF[1][i] = left[i]; }
+      IPROF(8);
     } else {
       // the shift of initIntraPatternChTypeISP (:798-897); ispPrev = last row / column of region k-1
       if (!ispVer) {   // horizontal split: left column shifted, top row from the region above
@@ -1125,7 +1124,8 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
           g_iprof[slot][3] = (ps[1] - ps[0]) | (ps[2] - ps[0]) << 16 | (ps[3] - ps[0]) << 32 | (ps[4] - ps[0]) << 48;
           g_iprof[slot][4] = (ps[5] - ps[0]) | (ps[6] - ps[0]) << 16 | (ps[7] - ps[0]) << 32 | (ps[8] - ps[0]) << 48;
           g_iprof[slot][5] = (unsigned long long)J.comp | (unsigned long long)J.w << 8 | (unsigned long long)J.h << 16 |
-                             (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40;
+                             (unsigned long long)J.flags << 24 | (unsigned long long)J.mode << 32 | (unsigned long long)(xcc & 15) << 40 |
+                             (unsigned long long)J.vnb << 48;
           g_iprof[slot][6] = (unsigned long long)gj | (unsigned long long)blockIdx.x << 32;
           g_iprof[slot][7] = (unsigned long long)(uint16_t)J.x | (unsigned long long)(uint16_t)J.y << 16 | (unsigned long long)c << 32;
         }

@@ -184,6 +184,12 @@ __constant__ CellTaps c_ctaps = make_cell_taps();
 #ifndef MC_WG
 #define MC_WG 64
 #endif
+#ifndef MC_P0_LDS
+#define MC_P0_LDS 0
+#endif
+#ifndef MC_WAVES_PER_EU
+#define MC_WAVES_PER_EU 4
+#endif
 #ifndef MC_RESI_AHEAD
 #define MC_RESI_AHEAD 2
 #endif
@@ -420,12 +426,28 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
   // a uni job) through ONE filter body whose emit combines: uni and bi share it (separate bodies per case
   // tripled k_mc's code, and its instruction footprint, not its VALU count, stretched the waves, r04)
   const bool avg = bi && !(J.flags & (MC_WP | MC_GEO)) && J.bcw == 2;
+#if MC_P0_LDS
+  // list 0's rows wait in LDS (8 B per row and lane, conflict-free), not in 2 R registers: the VGPR budget
+  // sets the waves resident per SIMD, and the launch is latency x occupancy bound
+  __shared__ uint2 s_p0[MC_WG / 64][8][64];
+  uint2 (*p0s)[64] = s_p0[threadIdx.x >> 6];
+  const int pl = threadIdx.x & 63;
+#define P0_LO(o) p0s[o][pl].x
+#define P0_HI(o) p0s[o][pl].y
+#else
   uint32_t p0[R][2];
+#define P0_LO(o) p0[o][0]
+#define P0_HI(o) p0[o][1]
+#endif
   if (bi) {
     const CellWin W0 = cell_win(P, J, comp, 0, x, y);
     cell_filter<N, R>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
+#if MC_P0_LDS
+      p0s[o][pl] = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+#else
       p0[o][0] = pk(v[0], v[1]);
       p0[o][1] = pk(v[2], v[3]);
+#endif
     }, [](int) {});
   }
   const Comb CB = comb_setup(WT, J, comp, bd, cx, cy);
@@ -436,12 +458,14 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
 #pragma unroll
       for (int q = 0; q < 4; q++) a[q] = clampi(v[q], 0, maxv);
     } else if (avg) {   // AreaBuf::addAvg (Buffer.cpp:447)
-      const int u[4] = {lo16(p0[o][0]), hi16(p0[o][0]), lo16(p0[o][1]), hi16(p0[o][1])};
+      const uint32_t q0 = P0_LO(o), q1 = P0_HI(o);
+      const int u[4] = {lo16(q0), hi16(q0), lo16(q1), hi16(q1)};
       const int shiftNum = headRoom + 1, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
 #pragma unroll
       for (int q = 0; q < 4; q++) a[q] = clampi((u[q] + v[q] + offset) >> shiftNum, 0, maxv);
     } else {   // uni WP, bi WP / GEO / BCW
-      const int u[4] = {bi ? lo16(p0[o][0]) : v[0], bi ? hi16(p0[o][0]) : v[1], bi ? lo16(p0[o][1]) : v[2], bi ? hi16(p0[o][1]) : v[3]};
+      const uint32_t q0 = bi ? P0_LO(o) : 0u, q1 = bi ? P0_HI(o) : 0u;
+      const int u[4] = {bi ? lo16(q0) : v[0], bi ? hi16(q0) : v[1], bi ? lo16(q1) : v[2], bi ? hi16(q1) : v[3]};
 #pragma unroll
       for (int q = 0; q < 4; q++) a[q] = comb_apply(CB, q, o, u[q], v[q], maxv);
     }
@@ -507,7 +531,7 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
     mc_cell<4, 4>(P, WT, J, comp, (J.x >> 1) + 4 * cx, (J.y >> 1) + 4 * cy, min(4, cw - 4 * cx), min(4, chh - 4 * cy));
   }
 }
-__global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(4))) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct, int V) {
+__global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_PER_EU))) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct, int V) {
 #ifdef VVCR_MC_PROF
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
