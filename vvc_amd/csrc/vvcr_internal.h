@@ -146,9 +146,15 @@ struct McClassTable {
   int32_t lcell0[MC_MAXCLS + 1] = {}; // first luma cell of each class; [n] = luma cells in all (lanes)
   int32_t ccell0[MC_MAXCLS + 1] = {}; // chroma cells likewise
 };
-// cells of one job of size w x h: luma (w/4) x ceil(h/8), chroma 2 components x ceil(w/8) x ceil(h/8)
+// cells of one job of size w x h: luma (w/4) x ceil(h/8), chroma 2 components x ceil(w/8) x (h/16, or ceil(h/8))
 __host__ __device__ inline int mc_luma_cells(int w, int h) { return (w >> 2) * ((h + 7) >> 3); }
-__host__ __device__ inline int mc_chroma_cells(int w, int h) { return 2 * ((w + 7) >> 3) * ((h + 7) >> 3); }
+// chroma cells: 4 columns x 8 rows for blocks of >= 16 luma rows (a third less H work than two 4-row
+// cells), else 4 x 4
+#ifndef MC_TALL_CHROMA
+#define MC_TALL_CHROMA 1
+#endif
+__host__ __device__ inline bool mc_tall_chroma(int h) { return MC_TALL_CHROMA && h >= 16; }
+__host__ __device__ inline int mc_chroma_cells(int w, int h) { return 2 * ((w + 7) >> 3) * (mc_tall_chroma(h) ? h >> 4 : (h + 7) >> 3); }
 
 // A workgroup-uniform record (job descriptor) through dword loads at a uniform address, so that it lands in
 // SGPRs (s_load): a plain struct copy loads its 16-bit fields with per-lane global loads, and everything

@@ -525,13 +525,16 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
     const int ncx = w >> 2, cx = s & (ncx - 1), cy = s >> (__ffs(ncx) - 1);
     mc_cell<8, 8>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
   } else {
-    const int cw = w >> 1, chh = h >> 1, ncx = (cw + 3) >> 2, ncy = (chh + 3) >> 2, nper = ncx * ncy;
+    const int cw = w >> 1, chh = h >> 1;
+    const bool tall = mc_tall_chroma(h);   // class-uniform: 8-row chroma cells (mc_chroma_cells)
+    const int ncx = (cw + 3) >> 2, ncy = tall ? chh >> 3 : (chh + 3) >> 2, nper = ncx * ncy;
     const int comp = 1 + (s >= nper), t = s - (comp - 1) * nper;
     const int cx = t & (ncx - 1), cy = t >> (__ffs(ncx) - 1);   // ncx is a power of two
-    mc_cell<4, 4>(P, WT, J, comp, (J.x >> 1) + 4 * cx, (J.y >> 1) + 4 * cy, min(4, cw - 4 * cx), min(4, chh - 4 * cy));
+    if (tall) mc_cell<4, 8>(P, WT, J, comp, (J.x >> 1) + 4 * cx, (J.y >> 1) + 8 * cy, min(4, cw - 4 * cx), 8);
+    else mc_cell<4, 4>(P, WT, J, comp, (J.x >> 1) + 4 * cx, (J.y >> 1) + 4 * cy, min(4, cw - 4 * cx), min(4, chh - 4 * cy));
   }
 }
-__global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_PER_EU))) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct, int V) {
+__global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_PER_EU))) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct) {
 #ifdef VVCR_MC_PROF
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
@@ -544,17 +547,9 @@ __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_
 #define MC_BODY(b) mc_body(P, jobs, ct, b)
 #endif
   // XCD-aware order (measured on the 4K B pictures, r03): the workgroups one XCD receives take a contiguous
-  // run of blocks (MC_WG cells each), so neighbouring blocks' windows share that XCD's L2. A grid smaller
-  // than the V blocks is persistent: workgroup j of XCD x walks run x with stride G / 8.
-  const int G = gridDim.x;
-  if (G >= V) {
-    MC_BODY(xcd_swizzle(blockIdx.x, G));
-  } else {
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3, Gx = G >> 3;   // G: a multiple of 8
-    const int per = V >> 3, rem = V & 7;
-    const int lo = x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per, n = per + (x < rem ? 1 : 0);
-    for (int k = j; k < n; k += Gx) MC_BODY(lo + k);
-  }
+  // run of blocks (MC_WG cells each), so neighbouring blocks' windows share that XCD's L2. (A persistent
+  // grid walking the blocks was slower, 47.3 vs 41.4 us, and doubled the kernel's code: removed, r04.)
+  MC_BODY(xcd_swizzle(blockIdx.x, gridDim.x));
 #undef MC_BODY
 #ifdef VVCR_MC_PROF
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
@@ -570,10 +565,5 @@ __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_
 void launch_mc(const McParams &p, const McJob *jobs, const McClassTable &ct, hipStream_t s) {
   if (ct.n <= 0) return;
   const int V = (ct.lcell0[ct.n] + MC_WG - 1) / MC_WG + (ct.ccell0[ct.n] + MC_WG - 1) / MC_WG;
-  static const int cap = [] {
-    const char *e = getenv("VVCR_MC_WGS");   // persistent grid (experiments): workgroups, a multiple of 8
-    return e ? (atoi(e) & ~7) : 0;
-  }();
-  const int g = cap >= 8 && cap < V ? cap : V;
-  if (V > 0) hipLaunchKernelGGL(k_mc, dim3(g), dim3(MC_WG), 0, s, p, jobs, ct, V);
+  if (V > 0) hipLaunchKernelGGL(k_mc, dim3(V), dim3(MC_WG), 0, s, p, jobs, ct);
 }

@@ -212,31 +212,41 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
       if (pos < 25 && ri == 0) sad[pos] = acc;   // (sum << 1) >> 1 in xDMVRCost
     }
     __syncthreads();
-    if (tid == 0) {
-      unsigned long long minCost = sad[12];
-      minCost -= minCost >> 2;
-      int tdx = 0, tdy = 0, pos = 12;
-      bool notZero = true;
-      if (minCost < (unsigned long long)(w * h)) {
-        notZero = false;
-      } else {
-        sad[12] = (uint32_t)minCost;
-        int bx = 0, by = 0;
-        for (int k = 0; k < 25; k++)
-          if (sad[k] < minCost) { minCost = sad[k]; bx = x_search[k][0]; by = x_search[k][1]; }
-        tdx = bx; tdy = by;
-        pos = 12 + by * 5 + bx;
+    if (tid < 64) {
+      // xDMVRCost's search order, by wave 0: the scan "minCost = sad'[12]; for k: if (sad[k] < minCost)"
+      // (sad'[12] = sad[12] - sad[12] / 4) picks the first strict minimum, the centre on a tie with it:
+      // one min-reduction over the keys (cost, 0 for the centre / 1 + k for the others)
+      const uint32_t c12 = sad[12], adj = c12 - (c12 >> 2);
+      const bool notZero = adj >= (uint32_t)(w * h);
+      const uint32_t cost = tid < 25 ? (tid == 12 ? adj : sad[tid]) : 0xffffffffu;
+      unsigned long long key = (unsigned long long)cost << 5 | (unsigned long long)(tid == 12 ? 0 : tid + 1);
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) {
+        const unsigned long long o = __shfl_xor(key, m);
+        key = o < key ? o : key;
       }
-      const bool bdofSub = minCost < (unsigned long long)(2 * w * h) ? false : ((J.flags & MC_BDOF) != 0);
-      tdx <<= 4; tdy <<= 4;
-      if (notZero && abs(tdx) != 32 && abs(tdy) != 32) {
-        unsigned long long sb[5] = {sad[pos], sad[pos - 1], sad[pos - 5], sad[pos + 1], sad[pos + 5]};
-        int d[2] = {0, 0};
-        subpel_surface(sb, d);
-        tdx += d[0]; tdy += d[1];
+      if (tid == 12 && notZero) sad[12] = adj;   // the neighbours of a minimum next to the centre read it
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("" ::: "memory");
+      if (tid == 0) {
+        unsigned long long minCost = adj;
+        int tdx = 0, tdy = 0, pos = 12;
+        if (notZero) {
+          minCost = key >> 5;
+          pos = (key & 31) ? (int)(key & 31) - 1 : 12;
+          tdx = x_search[pos][0]; tdy = x_search[pos][1];
+        }
+        const bool bdofSub = minCost < (unsigned long long)(2 * w * h) ? false : ((J.flags & MC_BDOF) != 0);
+        tdx <<= 4; tdy <<= 4;
+        if (notZero && abs(tdx) != 32 && abs(tdy) != 32) {
+          unsigned long long sb[5] = {sad[pos], sad[pos - 1], sad[pos - 5], sad[pos + 1], sad[pos + 5]};
+          int d[2] = {0, 0};
+          subpel_surface(sb, d);
+          tdx += d[0]; tdy += d[1];
+        }
+        sh_delta[0] = tdx; sh_delta[1] = tdy; sh_bdof = bdofSub;
+        if (J.aux >= 0) { dmvr_out[2 * J.aux] = tdx; dmvr_out[2 * J.aux + 1] = tdy; }
       }
-      sh_delta[0] = tdx; sh_delta[1] = tdy; sh_bdof = bdofSub;
-      if (J.aux >= 0) { dmvr_out[2 * J.aux] = tdx; dmvr_out[2 * J.aux + 1] = tdy; }
     }
     __syncthreads();
     dx = __builtin_amdgcn_readfirstlane(sh_delta[0]);
