@@ -155,7 +155,7 @@ struct Prepared {
   DevVec<uint8_t> alf_ctb;
   DevVec<int32_t> dmvr;
   DevVec<WpTable> wpt;               // the slice's weighted-prediction table (k_mc reads it per lane)
-  McClassTable mc_ct;                // k_mc cell classes of mc_basic
+  McClassTable mc_ct;                // k_mc cell classes of mc_basic (edge jobs, tiles, blocks)
   bool have_sao = false, have_alf = false;
   bool zero_filled = false;   // the residual areas read are zeroed by TB_ZERO jobs: no plane clear
   int n_tb = 0, n_tb_small = 0, n_mctile = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
@@ -493,7 +493,8 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   }
   if (mask & VVCR_STAGE_INTER) {
     // 32x32 tiles first, then the small jobs, in one array
-    st.add(r.mc_basic, {{wl.mc_tile.data(), wl.mc_tile.size()}, {wl.mc_basic.data(), wl.mc_basic.size()}});
+    st.add(r.mc_basic, {{wl.mc_edge.data(), wl.mc_edge.size()}, {wl.mc_tile.data(), wl.mc_tile.size()},
+                        {wl.mc_basic.data(), wl.mc_basic.size()}});
     st.add(r.mc_bidir, wl.mc_bidir);
     {
       const WpTable wt = make_wp_table(pp, sp.bit_depth);
@@ -503,7 +504,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     st.add(r.aff_pu, wl.aff_pu);
     st.add(r.aff_jobs, wl.aff_jobs);
     r.n_mctile = (int)wl.mc_tile.size();
-    r.n_basic = (int)wl.mc_basic.size();
+    r.n_basic = (int)(wl.mc_basic.size() + wl.mc_edge.size());
     r.n_bidir = (int)wl.mc_bidir.size();
     r.n_aff = (int)wl.aff_jobs.size();
     r.n_dmvr = wl.n_dmvr;
@@ -1174,7 +1175,7 @@ int vvcr_picture_plan(vvcr_picture *pic, uint32_t stage_mask) {
 int vvcr_picture_work_counts(const vvcr_picture *pic, int64_t *counts, int32_t n) {
   if (!pic || (!counts && n)) return VVCR_E_ARG;
   if (!pic->planned) return VVCR_E_STATE;
-  const int64_t v[10] = {(int64_t)pic->wl.tb.size(), (int64_t)(pic->wl.mc_tile.size() + pic->wl.mc_basic.size()), (int64_t)pic->wl.mc_bidir.size(),
+  const int64_t v[10] = {(int64_t)pic->wl.tb.size(), (int64_t)(pic->wl.mc_tile.size() + pic->wl.mc_basic.size() + pic->wl.mc_edge.size()), (int64_t)pic->wl.mc_bidir.size(),
                          (int64_t)pic->wl.aff_jobs.size(), (int64_t)pic->intra.inter_tiles.size(), (int64_t)pic->intra.jobs.size(),
                          (int64_t)pic->dbk.total(), (int64_t)pic->wl.n_dmvr, pic->wl.ref_y0, pic->wl.ref_y1};
   for (int k = 0; k < n && k < 10; k++) counts[k] = v[k];
@@ -1214,7 +1215,7 @@ extern "C" int vvcr_debug_mc_slots(const vvcr_picture *pic, int32_t *out, int32_
   if (!pic->planned) return VVCR_E_STATE;
   int32_t n = 0;
   auto put = [&](int v) { if (n < cap) out[n] = v; n++; };
-  for (const auto *v : {&pic->wl.mc_tile, &pic->wl.mc_basic, &pic->wl.mc_bidir})
+  for (const auto *v : {&pic->wl.mc_tile, &pic->wl.mc_basic, &pic->wl.mc_edge, &pic->wl.mc_bidir})
     for (const McJob &j : *v) {
       if (j.flags & MC_L0) put(j.slot[0]);
       if (j.flags & MC_L1) put(j.slot[1]);

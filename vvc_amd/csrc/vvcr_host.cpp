@@ -56,13 +56,13 @@ void push_mc(WorkLists &wl, int x0, int y0, int w, int h, const McJob &proto) {
   push_tiles(wl.mc_basic, x0, y0, w, h, proto);
 }
 
-// The k_mc class table of the combined job array (mc_tile, then mc_basic sorted by size): one class per
-// run of equal (w, h), its cell ranges padded to whole waves.
-void build_mc_classes(WorkLists &wl) {
-  McClassTable &ct = wl.mc_ct;
+// A k_mc class table over job arrays laid out one after another from job index base (each flagged: its
+// windows may leave the picture): one class per run of equal (w, h), its cell ranges padded to whole waves.
+void build_mc_classes(McClassTable &ct, std::initializer_list<std::pair<const bigbuf::vec<McJob> *, bool>> lists, int base) {
   ct = McClassTable();
   int lc = 0, cc = 0;
-  auto run = [&](const bigbuf::vec<McJob> &v, int base) {
+  for (const auto &lv : lists) {
+    const bigbuf::vec<McJob> &v = *lv.first;
     for (size_t i = 0; i < v.size();) {
       size_t e = i + 1;
       while (e < v.size() && v[e].w == v[i].w && v[e].h == v[i].h) e++;
@@ -71,18 +71,39 @@ void build_mc_classes(WorkLists &wl) {
       ct.job0[k] = base + (int)i;
       ct.w[k] = w;
       ct.h[k] = h;
+      ct.edge[k] = lv.second ? 1 : 0;
       ct.lcell0[k] = lc;
       ct.ccell0[k] = cc;
       lc += (n * mc_luma_cells(w, h) + 63) & ~63;
       cc += (n * mc_chroma_cells(w, h) + 63) & ~63;
       i = e;
     }
-  };
-  run(wl.mc_tile, 0);
-  run(wl.mc_basic, (int)wl.mc_tile.size());
-  ct.job0[ct.n] = (int)(wl.mc_tile.size() + wl.mc_basic.size());
+    base += (int)v.size();
+  }
+  ct.job0[ct.n] = base;
   ct.lcell0[ct.n] = lc;
   ct.ccell0[ct.n] = cc;
+}
+
+// Whether any reference window of a plain MC job, as k_mc's cells read it (aligned dword runs of 12 luma /
+// 8 chroma samples from the even column at or before the first tap, 15 / 7 or 11 rows), may leave the
+// picture (conservative): such jobs form classes of their own whose waves take the clamped path (rows
+// and columns clamped: the edge-replicated margin, Picture.cpp:737); the others assume their windows
+// inside, with no per-lane test and no edge code in their path.
+bool mc_job_edge(const McJob &j, int W, int H) {
+  for (int l = 0; l < 2; l++) {
+    if (!(j.flags & (l ? MC_L1 : MC_L0))) continue;
+    const int mvx = j.mv[l][0], mvy = j.mv[l][1];
+    // luma: columns [x + (mvx >> 4) - 4, x + w + (mvx >> 4) + 8), rows [y + (mvy >> 4) - 3, y + h + (mvy >> 4) + 4]
+    // (a block shorter than a cell still filters the cell's rows: heights rounded up to the cell)
+    if (j.x + (mvx >> 4) - 4 < 0 || j.x + j.w + (mvx >> 4) + 8 > W) return true;
+    if (j.y + (mvy >> 4) - 3 < 0 || j.y + std::max<int>(j.h, 8) + (mvy >> 4) + 6 > H) return true;
+    // chroma (4:2:0)
+    const int cx = j.x >> 1, cy = j.y >> 1, cw = std::max(2, j.w >> 1), ch = std::max(4, j.h >> 1);
+    if (cx + (mvx >> 5) - 2 < 0 || cx + cw + (mvx >> 5) + 8 > (W >> 1)) return true;
+    if (cy + (mvy >> 5) - 1 < 0 || cy + ch + (mvy >> 5) + 5 > (H >> 1)) return true;
+  }
+  return false;
 }
 
 McJob make_job(const vvcr_pic_params &pp, int interDir, int r0, int r1, int mv0x, int mv0y, int mv1x, int mv1y,
@@ -416,12 +437,26 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
     if (ka != kb) return ka > kb;
     return ((a.flags & MC_L0) && (a.flags & MC_L1)) > ((b.flags & MC_L0) && (b.flags & MC_L1));
   });
-  build_mc_classes(wl);
+  // jobs whose windows may leave the picture: to the edge list (same order rules), the rest stay
+  auto split_edge = [&](bigbuf::vec<McJob> &v) {
+    auto mid = std::stable_partition(v.begin(), v.end(), [&](const McJob &j) { return !mc_job_edge(j, sp.width, sp.height); });
+    wl.mc_edge.insert(wl.mc_edge.end(), mid, v.end());
+    v.erase(mid, v.end());
+  };
+  split_edge(wl.mc_tile);
+  split_edge(wl.mc_basic);
+  std::stable_sort(wl.mc_edge.begin(), wl.mc_edge.end(), [](const McJob &a, const McJob &b) {
+    const int ka = a.w << 8 | a.h, kb = b.w << 8 | b.h;
+    if (ka != kb) return ka > kb;
+    return ((a.flags & MC_L0) && (a.flags & MC_L1)) > ((b.flags & MC_L0) && (b.flags & MC_L1));
+  });
+  // the edge classes first: their waves (longer, per-row clamped gathers) start in the first round
+  build_mc_classes(wl.mc_ct, {{&wl.mc_edge, true}, {&wl.mc_tile, false}, {&wl.mc_basic, false}}, 0);
   std::stable_partition(wl.aff_jobs.begin(), wl.aff_jobs.end(), [&](const AffJob &j) {
     const AffPu &U = wl.aff_pu[j.pu];
     return U.l[0].present && U.l[1].present;
   });
-  for (const bigbuf::vec<McJob> *v : {&wl.mc_tile, &wl.mc_basic, &wl.mc_bidir})
+  for (const bigbuf::vec<McJob> *v : {&wl.mc_tile, &wl.mc_basic, &wl.mc_edge, &wl.mc_bidir})
     for (const McJob &j : *v)
       for (int l = 0; l < 2; l++)
         if (j.flags & (l ? MC_L1 : MC_L0)) reach(j.y, j.h, j.mv[l][1]);

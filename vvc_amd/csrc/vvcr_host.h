@@ -59,9 +59,10 @@ struct WorkLists {
   int ref_y0 = 0, ref_y1 = 0;      // luma rows of the reference pictures the MC jobs read (with margins)
   double mc_alg = 0;               // algorithmic bytes of the plain MC (per PU / sub-block)
   bool zero_filled = false;        // tb holds TB_ZERO jobs for every residual area read but not coded: no clear
-  McClassTable mc_ct;              // k_mc cell classes of mc_tile + mc_basic (in that order, one array)
+  bigbuf::vec<McJob> mc_edge;      // plain MC jobs whose windows may leave the picture (their own classes)
+  McClassTable mc_ct;              // k_mc cell classes of mc_edge + mc_tile + mc_basic (in that order, one array)
   void clear() {
-    mc_alg = 0; mc_tile.clear(); mc_ct = McClassTable();
+    mc_alg = 0; mc_tile.clear(); mc_ct = McClassTable(); mc_edge.clear();
     mc_basic.clear(); mc_bidir.clear(); aff_pu.clear(); aff_jobs.clear(); tb.clear(); coef.clear();
     n_dmvr = 0; n_unsupported_inter = 0; tb_small = 0; ref_y0 = ref_y1 = 0; zero_filled = false;
   }

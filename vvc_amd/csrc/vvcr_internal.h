@@ -138,11 +138,12 @@ struct McParams {
 // 4 columns x 4 rows of one component) for every list of its job. The job array holds the 32x32 tiles,
 // then the smaller blocks, grouped in classes of one size (w, h); a class's cells are numbered job-major
 // from lcell0 / ccell0, each range padded to a multiple of 64, so no wave straddles two classes.
-constexpr int MC_MAXCLS = 12;
+constexpr int MC_MAXCLS = 24;
 struct McClassTable {
   int32_t n = 0;                      // classes
   int32_t job0[MC_MAXCLS + 1] = {};   // first job of the class in the combined job array; [n] = jobs in all
   int32_t w[MC_MAXCLS] = {}, h[MC_MAXCLS] = {};
+  int32_t edge[MC_MAXCLS] = {};       // the class's windows may leave the picture (mc_job_edge): clamped path
   int32_t lcell0[MC_MAXCLS + 1] = {}; // first luma cell of each class; [n] = luma cells in all (lanes)
   int32_t ccell0[MC_MAXCLS + 1] = {}; // chroma cells likewise
 };

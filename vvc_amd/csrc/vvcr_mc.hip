@@ -251,7 +251,7 @@ __device__ __forceinline__ void edge_dwords(const int16_t *row, const EdgeMap &e
 // One list of a cell: R x 4 outputs of the N-tap separable filter from the reference plane R, window
 // origin (ox, oy) (first tap), fractions fx / fy, tap set ts (luma); emit(o, v) receives output row o,
 // v[c] = (V sum + off2) >> sh2 before any clamp, as soon as its last H row is filtered.
-template <int N, int R, class Emit, class Pre>
+template <int N, int R, bool EDGE, class Emit, class Pre>
 __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, int fx, int fy, int ts, int sh1, int off2, int sh2,
                                             Emit &&emit, Pre &&pre) {
   constexpr int ND = N / 2 + 2, NT = N / 2 + 1, NV = N / 2, ROWS = R + N - 1;
@@ -317,8 +317,9 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
       emit(o, v);
     }
   };
-  if (dc >= 0 && dc + 2 * ND <= Rp.w && oy >= 0 && oy + ROWS <= Rp.h) {
-    // the whole window inside the picture (the common case): vector loads, row pointers by increment
+  if constexpr (!EDGE) {
+    // k_mc: the host routed every job whose windows may leave the picture to k_mc<edge> (mc_job_edge), so
+    // the window is inside: vector loads, row pointers by increment
     const int16_t *row = Rp.p + (size_t)oy * Rp.stride + dc;
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
@@ -332,7 +333,7 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
       if (r % MC_ROWS_AHEAD == MC_ROWS_AHEAD - 1) __builtin_amdgcn_sched_barrier(0);
     }
   } else {
-    // a window at the picture edge (rows clamped, edge columns replicated: Picture::extendPicBorder)
+    // k_mc<edge>: rows clamped, edge columns replicated (Picture::extendPicBorder)
     const EdgeMap e = edge_map<ND>(dc, Rp.w);
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
@@ -372,7 +373,7 @@ __device__ __forceinline__ CellWin cell_win(const McParams &P, const McJob &J, i
 // One cell: every list of the job, combined (AreaBuf::addAvg / addWeightedAvg, WP, GEO blend, or the uni
 // rounding), stored as rows of up to 4 samples. (x, y): the cell origin in the component plane; nc / nr:
 // the valid columns / rows of the cell (blocks narrower or shorter than a cell).
-template <int N, int R>
+template <int N, int R, bool EDGE>
 __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, const McJob &J, int comp, int x, int y, int nc, int nr) {
   const bool l0 = J.flags & MC_L0, l1 = J.flags & MC_L1, bi = l0 && l1;
   const int bd = P.bd, maxv = (1 << bd) - 1, headRoom = max(2, IF_INTERNAL_PREC - bd);
@@ -441,7 +442,7 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
 #endif
   if (bi) {
     const CellWin W0 = cell_win(P, J, comp, 0, x, y);
-    cell_filter<N, R>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
+    cell_filter<N, R, EDGE>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
 #if MC_P0_LDS
       p0s[o][pl] = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
 #else
@@ -452,7 +453,7 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
   }
   const Comb CB = comb_setup(WT, J, comp, bd, cx, cy);
   const CellWin W = cell_win(P, J, comp, (bi || !l0) ? 1 : 0, x, y);
-  cell_filter<N, R>(W.R, W.ox, W.oy, W.fx, W.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
+  cell_filter<N, R, EDGE>(W.R, W.ox, W.oy, W.fx, W.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
     int a[4];
     if (rnd) {
 #pragma unroll
@@ -496,11 +497,11 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
   const int gw = __builtin_amdgcn_readfirstlane(g & ~63);   // the wave's first cell: selects the class
   // the class of the wave by a scan over static fields (wave-uniform selects; a class index used to read
   // the kernel argument would make it a per-lane indexed copy)
-  int w = ct.w[0], h = ct.h[0], c0 = luma ? ct.lcell0[0] : ct.ccell0[0], jbase = ct.job0[0], jend = ct.job0[1];
+  int w = ct.w[0], h = ct.h[0], c0 = luma ? ct.lcell0[0] : ct.ccell0[0], jbase = ct.job0[0], jend = ct.job0[1], ed = ct.edge[0];
 #pragma unroll
   for (int q = 1; q < MC_MAXCLS; q++)
     if (q < ct.n && gw >= (luma ? ct.lcell0[q] : ct.ccell0[q])) {
-      w = ct.w[q]; h = ct.h[q]; c0 = luma ? ct.lcell0[q] : ct.ccell0[q]; jbase = ct.job0[q]; jend = ct.job0[q + 1];
+      w = ct.w[q]; h = ct.h[q]; c0 = luma ? ct.lcell0[q] : ct.ccell0[q]; jbase = ct.job0[q]; jend = ct.job0[q + 1]; ed = ct.edge[q];
     }
   const int i = g - c0;
   const int per = luma ? mc_luma_cells(w, h) : mc_chroma_cells(w, h);   // a power of two
@@ -521,17 +522,25 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
          (unsigned long long)__builtin_popcountll(__ballot(1)) << 40;
 #endif
   const WpTable &WT = *P.wpd;
+  // the path is a class property (wave-uniform): edge classes take the clamped gathers, the others none
   if (luma) {
     const int ncx = w >> 2, cx = s & (ncx - 1), cy = s >> (__ffs(ncx) - 1);
-    mc_cell<8, 8>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
+    if (ed) mc_cell<8, 8, true>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
+    else mc_cell<8, 8, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
   } else {
     const int cw = w >> 1, chh = h >> 1;
     const bool tall = mc_tall_chroma(h);   // class-uniform: 8-row chroma cells (mc_chroma_cells)
     const int ncx = (cw + 3) >> 2, ncy = tall ? chh >> 3 : (chh + 3) >> 2, nper = ncx * ncy;
     const int comp = 1 + (s >= nper), t = s - (comp - 1) * nper;
     const int cx = t & (ncx - 1), cy = t >> (__ffs(ncx) - 1);   // ncx is a power of two
-    if (tall) mc_cell<4, 8>(P, WT, J, comp, (J.x >> 1) + 4 * cx, (J.y >> 1) + 8 * cy, min(4, cw - 4 * cx), 8);
-    else mc_cell<4, 4>(P, WT, J, comp, (J.x >> 1) + 4 * cx, (J.y >> 1) + 4 * cy, min(4, cw - 4 * cx), min(4, chh - 4 * cy));
+    const int ox = (J.x >> 1) + 4 * cx, nc = min(4, cw - 4 * cx);
+    if (ed) {
+      if (tall) mc_cell<4, 8, true>(P, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8);
+      else mc_cell<4, 4, true>(P, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy));
+    } else {
+      if (tall) mc_cell<4, 8, false>(P, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8);
+      else mc_cell<4, 4, false>(P, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy));
+    }
   }
 }
 __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_PER_EU))) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct) {
