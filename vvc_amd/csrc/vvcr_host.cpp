@@ -74,7 +74,7 @@ void build_mc_classes(McClassTable &ct, std::initializer_list<std::pair<const bi
       ct.edge[k] = lv.second ? 1 : 0;
       ct.lcell0[k] = lc;
       ct.ccell0[k] = cc;
-      lc += (n * mc_luma_cells(w, h) + 63) & ~63;
+      lc += (n * mc_luma_cells(w, h, lv.second) + 63) & ~63;
       cc += (n * mc_chroma_cells(w, h) + 63) & ~63;
       i = e;
     }

@@ -148,7 +148,13 @@ struct McClassTable {
   int32_t ccell0[MC_MAXCLS + 1] = {}; // chroma cells likewise
 };
 // cells of one job of size w x h: luma (w/4) x ceil(h/8), chroma 2 components x ceil(w/8) x (h/16, or ceil(h/8))
-__host__ __device__ inline int mc_luma_cells(int w, int h) { return (w >> 2) * ((h + 7) >> 3); }
+#ifndef MC_TALL_LUMA
+#define MC_TALL_LUMA 0
+#endif
+// luma cells: 4 columns x 16 rows for blocks of >= 16 rows when MC_TALL_LUMA (a quarter less H work), else 4 x 8
+// (not in edge classes: their clamped path keeps 8-row cells)
+__host__ __device__ inline bool mc_tall_luma(int h, bool edge) { return MC_TALL_LUMA && h >= 16 && !edge; }
+__host__ __device__ inline int mc_luma_cells(int w, int h, bool edge) { return (w >> 2) * (mc_tall_luma(h, edge) ? h >> 4 : (h + 7) >> 3); }
 // chroma cells: 4 columns x 8 rows for blocks of >= 16 luma rows (a third less H work than two 4-row
 // cells), else 4 x 4
 #ifndef MC_TALL_CHROMA

@@ -504,7 +504,7 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
       w = ct.w[q]; h = ct.h[q]; c0 = luma ? ct.lcell0[q] : ct.ccell0[q]; jbase = ct.job0[q]; jend = ct.job0[q + 1]; ed = ct.edge[q];
     }
   const int i = g - c0;
-  const int per = luma ? mc_luma_cells(w, h) : mc_chroma_cells(w, h);   // a power of two
+  const int per = luma ? mc_luma_cells(w, h, ed) : mc_chroma_cells(w, h);   // a power of two
   const int jn = i >> (__ffs(per) - 1), s = i & (per - 1);
 #ifdef VVCR_MC_PROF
   tag = (unsigned long long)luma << 63 | (unsigned long long)(w & 255) << 8 | (h & 255);
@@ -526,6 +526,9 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
   if (luma) {
     const int ncx = w >> 2, cx = s & (ncx - 1), cy = s >> (__ffs(ncx) - 1);
     if (ed) mc_cell<8, 8, true>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
+#if MC_TALL_LUMA
+    else if (mc_tall_luma(h, false)) mc_cell<8, 16, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 16 * cy, 4, 16);
+#endif
     else mc_cell<8, 8, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
   } else {
     const int cw = w >> 1, chh = h >> 1;
@@ -558,7 +561,11 @@ __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_
   // XCD-aware order (measured on the 4K B pictures, r03): the workgroups one XCD receives take a contiguous
   // run of blocks (MC_WG cells each), so neighbouring blocks' windows share that XCD's L2. (A persistent
   // grid walking the blocks was slower, 47.3 vs 41.4 us, and doubled the kernel's code: removed, r04.)
+#ifdef MC_NO_SWIZZLE
+  MC_BODY((int)blockIdx.x);
+#else
   MC_BODY(xcd_swizzle(blockIdx.x, gridDim.x));
+#endif
 #undef MC_BODY
 #ifdef VVCR_MC_PROF
   const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
