@@ -11,6 +11,16 @@
 // (equivalent to PelUnitBuf::extendBorderPel(3) on the ALF input, AdaptiveLoopFilter.cpp:411).
 #include "vvcr_internal.h"
 
+#ifdef VVCR_ALF_PROF
+// Diagnostics build only (tools/alf_prof.py): per-workgroup phase stamps (s_memrealtime, 100 MHz) of k_alf.
+__device__ unsigned long long g_alfprof[1 << 15][6];
+extern "C" int vvcr_alf_prof_read(unsigned long long *dst, int n) {
+  return (int)hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_alfprof), (size_t)n * 6 * 8);
+}
+#define ALF_STAMP(k) do { if (threadIdx.x == 0) stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define ALF_STAMP(k) do { } while (0)
+#endif
 namespace {
 
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -148,7 +158,7 @@ __device__ __forceinline__ uint4 alf_chunk(const DPlane &S, int x0, int y) {
                     (uint32_t)(uint16_t)v[4] | (uint32_t)v[5] << 16, (uint32_t)(uint16_t)v[6] | (uint32_t)v[7] << 16);
 }
 
-__device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
+__device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, unsigned long long *stamp) {
   const DPlane &S = P.src[0];
   const DPlane &D = P.dst[0];
   __shared__ __attribute__((aligned(16))) int16_t t[ALF_SH * ALF_SW];
@@ -198,6 +208,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
     if (tid < 4 * 13) s_perm[tid] = (&c_perm7[0][0])[tid];
   }
   __syncthreads();
+  ALF_STAMP(1);
   // sample (x, y) in picture coordinates -> LDS (valid for x in [X0 - 8, X0 + 72), y in [Y0 - 3, Y0 + 19))
 #define T(x, y) ((int)t[((y) - Y0 + ALF_HALO) * ALF_SW + (x) - X0 + ALF_LX])
   const int vbH = 1 << P.ctu_log2, vbPos = P.vb_luma;
@@ -252,6 +263,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
     }
   }
   __syncthreads();
+  ALF_STAMP(2);
   // --- 7x7 diamond filter (filterBlk<ALF_FILTER_7>): lane = one column of one 4x4 block
   {
     const int x = X0 + (tid & 63), by = Y0 + (tid >> 6) * 4;
@@ -345,6 +357,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
       }
     }
   }
+  ALF_STAMP(3);
   // --- chroma (filterBlk<ALF_FILTER_5> per component + filterBlkCcAlf): lane = one chroma position
   {
     const int x = cx0 + (tid & (ALF_CW - 1)), y = cy0 + tid / ALF_CW;
@@ -425,7 +438,16 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty) {
 // One launch, one workgroup per region; regions in XCD-contiguous runs (raster order within a run).
 __global__ __launch_bounds__(256) void k_alf(AlfParams P, int gx, int gy) {
   const int b = xcd_swizzle(blockIdx.x, gridDim.x);
-  alf_region(P, b % gx, b / gx);
+  unsigned long long stamp[6] = {0, 0, 0, 0, 0, 0};
+  ALF_STAMP(0);
+  alf_region(P, b % gx, b / gx, stamp);
+  ALF_STAMP(4);
+#ifdef VVCR_ALF_PROF
+  if (threadIdx.x == 0 && blockIdx.x < (1u << 15)) {
+    for (int k = 0; k < 5; k++) g_alfprof[blockIdx.x][k] = stamp[k];
+    g_alfprof[blockIdx.x][5] = (unsigned long long)b;
+  }
+#endif
 }
 
 }  // namespace

@@ -191,7 +191,7 @@ __constant__ CellTaps c_ctaps = make_cell_taps();
 #define MC_WAVES_PER_EU 4
 #endif
 #ifndef MC_RESI_AHEAD
-#define MC_RESI_AHEAD 2
+#define MC_RESI_AHEAD 0   // 0 / 2 / 4 measured within 1 % (fused 4K B pictures); 0 holds the fewest registers
 #endif
 #ifndef MC_ROWS_AHEAD
 #define MC_ROWS_AHEAD 4
@@ -558,13 +558,14 @@ __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_
 #else
 #define MC_BODY(b) mc_body(P, jobs, ct, b)
 #endif
-  // XCD-aware order (measured on the 4K B pictures, r03): the workgroups one XCD receives take a contiguous
-  // run of blocks (MC_WG cells each), so neighbouring blocks' windows share that XCD's L2. (A persistent
-  // grid walking the blocks was slower, 47.3 vs 41.4 us, and doubled the kernel's code: removed, r04.)
-#ifdef MC_NO_SWIZZLE
-  MC_BODY((int)blockIdx.x);
-#else
+  // (A persistent grid walking the blocks was slower, 47.3 vs 41.4 us, and doubled the kernel's code:
+  // removed, r04.)
+  // Blocks in dispatch order: with one wave per workgroup the XCD-contiguous order (r03, for 256-lane
+  // workgroups) was slower (4K B pictures: QP27 32.9 -> 31.8 us, QP32 27.4 -> 25.8 us without it, r04)
+#ifdef MC_XCD_SWIZZLE
   MC_BODY(xcd_swizzle(blockIdx.x, gridDim.x));
+#else
+  MC_BODY((int)blockIdx.x);
 #endif
 #undef MC_BODY
 #ifdef VVCR_MC_PROF
