@@ -437,7 +437,11 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
 
 // One launch, one workgroup per region; regions in XCD-contiguous runs (raster order within a run).
 __global__ __launch_bounds__(256) void k_alf(AlfParams P, int gx, int gy) {
+#ifdef ALF_NO_SWIZZLE
+  const int b = (int)blockIdx.x;
+#else
   const int b = xcd_swizzle(blockIdx.x, gridDim.x);
+#endif
   unsigned long long stamp[6] = {0, 0, 0, 0, 0, 0};
   ALF_STAMP(0);
   alf_region(P, b % gx, b / gx, stamp);
