@@ -124,8 +124,6 @@ __constant__ int8_t c_perm7[4][13] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12}
                                       {9, 4, 10, 8, 1, 5, 11, 7, 3, 0, 2, 6, 12},
                                       {0, 3, 2, 1, 8, 7, 6, 5, 4, 9, 10, 11, 12},
                                       {9, 8, 10, 4, 3, 7, 11, 5, 1, 0, 2, 6, 12}};
-__constant__ int8_t c_th[16] = {0, 1, 2, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 4};
-__constant__ int8_t c_transpose[8] = {0, 1, 0, 2, 2, 3, 1, 3};
 
 // ALF of one region: 64x16 luma samples and the co-located 32x8 Cb and Cr samples, one 256-lane
 // workgroup. The luma tile with its 3-sample halo and both chroma tiles with their 2-sample halo are staged
@@ -138,7 +136,10 @@ __constant__ int8_t c_transpose[8] = {0, 1, 0, 2, 2, 3, 1, 3};
 // region shares with its neighbours are fetched from HBM once per XCD, and the chroma work of a region
 // reads the luma its own workgroup staged (before r04 the chroma work was dispatched after all luma
 // tiles and re-read the luma from HBM: 3.2x the algorithmic bytes).
-constexpr int ALF_TW = 64, ALF_TH = 16, ALF_HALO = 3;
+#ifndef ALF_ROWS
+#define ALF_ROWS 16   // region height (16 or 32; at most the CTU size, so a region lies in one CTB)
+#endif
+constexpr int ALF_TW = 64, ALF_TH = ALF_ROWS, ALF_HALO = 3;
 constexpr int ALF_LX = 8;                            // staged luma columns left of the tile (one chunk)
 constexpr int ALF_SW = ALF_TW + 2 * ALF_LX;          // LDS row pitch (80): chunks [X0 - 8, X0 + 72)
 constexpr int ALF_SH = ALF_TH + 2 * ALF_HALO;        // 22 rows
@@ -146,6 +147,8 @@ constexpr int ALF_LCH = ALF_SW / 8;                  // luma chunks per row (10)
 constexpr int ALF_CW = ALF_TW / 2, ALF_CHH = ALF_TH / 2;   // chroma region 32 x 8
 constexpr int ALF_CSW = ALF_CW + 16, ALF_CSH = ALF_CHH + 4; // chroma LDS: chunks [cx0 - 8, cx0 + 40), rows cy0 - 2 .. cy0 + 9
 constexpr int ALF_CCH = ALF_CSW / 8;                 // chroma chunks per row (6)
+constexpr int ALF_LQ = (ALF_SH * ALF_LCH + 255) / 256;   // staged luma chunks per lane
+static_assert(2 * ALF_CSH * ALF_CCH <= 256, "one chroma chunk per lane");
 
 // 8 samples of row y from column x0 (a multiple of 8), picture-clamped (one vector load when inside)
 __device__ __forceinline__ uint4 alf_chunk(const DPlane &S, int x0, int y) {
@@ -158,34 +161,71 @@ __device__ __forceinline__ uint4 alf_chunk(const DPlane &S, int x0, int y) {
                     (uint32_t)(uint16_t)v[4] | (uint32_t)v[5] << 16, (uint32_t)(uint16_t)v[6] | (uint32_t)v[7] << 16);
 }
 
+// Uniform loads of a per-CTB control byte / short through the scalar cache (the containing aligned dword,
+// constant address space: s_load). A vector load here would share the in-order vmcnt counter with the
+// sample chunks in flight, so waiting for the control value would wait for the HBM loads too.
+typedef const __attribute__((address_space(4))) uint32_t *cdword_t;
+__device__ __forceinline__ int ldc_u8(const uint8_t *base, int i) {
+  const uintptr_t a = (uintptr_t)(base + i);
+  const uint32_t w = *(cdword_t)(a & ~(uintptr_t)3);
+  return (int)((w >> ((a & 3) * 8)) & 0xff);
+}
+__device__ __forceinline__ int ldc_i16(const int16_t *base, int i) {
+  const uintptr_t a = (uintptr_t)(base + i);
+  const uint32_t w = *(cdword_t)(a & ~(uintptr_t)3);
+  return (int)(int16_t)(w >> ((a & 2) * 8));
+}
+
 __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, unsigned long long *stamp) {
   const DPlane &S = P.src[0];
   const DPlane &D = P.dst[0];
   __shared__ __attribute__((aligned(16))) int16_t t[ALF_SH * ALF_SW];
   __shared__ __attribute__((aligned(16))) int16_t tc[2][ALF_CSH * ALF_CSW];
-  __shared__ int32_t blk[(ALF_TW / 4) * (ALF_TH / 4)];   // class | transpose << 8 | enabled << 16
   // the CTB's filter set per class, packed for the tap arithmetic: (c, c), (l, l), (-l, -l)
-  __shared__ uint4 s_cc[25 * 13];   // .x (c, c)  .y (l, l)  .z (-l, -l): one 16-byte LDS read per tap
+  __shared__ uint2 s_cc[25 * 13];   // .x (c, c)  .y (l, l): one 8-byte LDS read per tap (ds_read_b64)
   __shared__ int8_t s_perm[4 * 13];
+  // the CTB's chroma filters (per component: (c, c), (l, l) per tap pair) and CC-ALF filters
+  __shared__ uint2 s_ch[2][6];
+  __shared__ int32_t s_cc8[2][8];
   const int X0 = tx * ALF_TW, Y0 = P.y0 + ty * ALF_TH;
   const int cx0 = X0 >> 1, cy0 = Y0 >> 1;
   const int tid = threadIdx.x;
   const int W = S.w, H = S.h;
   // every staging load in flight first (one memory round trip): a luma chunk per lane (220 of them) and a
-  // chroma chunk for 144 lanes; then the CTB's flag and filter set (a 64x16 tile lies in one CTB, so both
-  // are uniform), the set's 25 classes of coefficients / clips staged in LDS with the samples
-  uint4 lv = {}, cv = {};
-  const int lr = tid / ALF_LCH, lc = tid - lr * ALF_LCH;
-  if (tid < ALF_SH * ALF_LCH) lv = alf_chunk(S, X0 - ALF_LX + 8 * lc, Y0 - ALF_HALO + lr);
+  // chroma chunk for 144 lanes; then the CTB's controls (a 64x16 tile lies in one CTB, so they are
+  // uniform: scalar loads) and the filters they select (the luma set's 25 classes of coefficients / clips,
+  // both chroma filters, both CC-ALF filters), staged in LDS with the samples
+  uint4 lv[ALF_LQ] = {}, cv = {};
+#pragma unroll
+  for (int q = 0; q < ALF_LQ; q++) {
+    const int i = tid + 256 * q, lr = i / ALF_LCH, lc = i - lr * ALF_LCH;
+    if (i < ALF_SH * ALF_LCH) lv[q] = alf_chunk(S, X0 - ALF_LX + 8 * lc, Y0 - ALF_HALO + lr);
+  }
   const int ccomp = tid / (ALF_CSH * ALF_CCH), ci = tid - ccomp * (ALF_CSH * ALF_CCH);
   const int cr = ci / ALF_CCH, cc = ci - cr * ALF_CCH;
-  if (ccomp < 2) cv = alf_chunk(P.src[1 + ccomp], cx0 - 8 + 8 * cc, cy0 - 2 + cr);
+  {
+    // Cb and Cr share stride and size: select the base pointer per lane from the two uniform descriptors
+    // (a lane-indexed P.src[1 + ccomp] is a per-lane load of the descriptor, one more memory round trip)
+    DPlane cs = P.src[1];
+    cs.p = ccomp ? P.src[2].p : P.src[1].p;
+    if (ccomp < 2) cv = alf_chunk(cs, cx0 - 8 + 8 * cc, cy0 - 2 + cr);
+  }
   const int ctbT = (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2);
-  const int ctbE = P.ctb_en[ctbT], set = P.ctb_set[ctbT];
+  const int n = P.nctb;
+  // every per-CTB control of the region in one round trip (all independent, uniform), then every filter
+  // it selects in a second one, both while the sample chunks are in flight
+  // (unconditional: a load under a condition is waited for inside it, together with the chunks)
+  const int ctbE = ldc_u8(P.ctb_en, ctbT), set0 = ldc_i16(P.ctb_set, ctbT);
+  const int eCb = ldc_u8(P.ctb_en, n + ctbT), eCr = ldc_u8(P.ctb_en, 2 * n + ctbT);
+  const int altCb = ldc_u8(P.ctb_alt, n + ctbT), altCr = ldc_u8(P.ctb_alt, 2 * n + ctbT);
+  const int fCb = ldc_u8(P.cc_ctl, ctbT), fCr = ldc_u8(P.cc_ctl, n + ctbT);
   const bool ctbOn = P.en[0] && ctbE;
+  const int onCb = P.en[1] && eCb, onCr = P.en[2] && eCr;
+  const int ccCb = P.en[3] ? fCb : 0, ccCr = P.en[4] ? fCr : 0;
+  const int set = ctbOn ? set0 : 0;
   constexpr int NC = (25 * 13 + 255) / 256;
-  int16_t cfv[NC] = {}, clv[NC] = {};
-  if (ctbOn) {
+  int16_t cfv[NC], clv[NC];
+  {
     const int16_t *cf = P.luma_coef + set * 25 * 13, *cl = P.luma_clip + set * 25 * 13;
 #pragma unroll
     for (int q = 0; q < NC; q++) {
@@ -194,27 +234,45 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
       clv[q] = cl[i];
     }
   }
-  if (tid < ALF_SH * ALF_LCH) *(uint4 *)&t[lr * ALF_SW + 8 * lc] = lv;
+  // chroma filter taps and CC-ALF taps: lane & 15 = component (bit 3) and tap (bits 0..2)
+  const int ck = (tid >> 3) & 1, ctt = tid & 7;
+  const int calt = min(ck ? altCr : altCb, 7), cf_ = ck ? ccCr : ccCb;
+  const int chc = P.chroma_coef[calt * 7 + min(ctt, 6)], chl = P.chroma_clip[calt * 7 + min(ctt, 6)];
+  const int ccv = P.cc_coef[(ck * 4 + max(cf_ - 1, 0)) * 8 + ctt];
+#pragma unroll
+  for (int q = 0; q < ALF_LQ; q++) {
+    const int i = tid + 256 * q, lr = i / ALF_LCH, lc = i - lr * ALF_LCH;
+    if (i < ALF_SH * ALF_LCH) *(uint4 *)&t[lr * ALF_SW + 8 * lc] = lv[q];
+  }
   if (ccomp < 2) *(uint4 *)&tc[ccomp][cr * ALF_CSW + 8 * cc] = cv;
   if (ctbOn) {
 #pragma unroll
     for (int q = 0; q < NC; q++) {
       const int i = tid + 256 * q;
       if (i < 25 * 13) {
-        const uint32_t c = (uint16_t)cfv[q], l = (uint16_t)clv[q], nl = (uint16_t)(-clv[q]);
-        s_cc[i] = make_uint4(c | c << 16, l | l << 16, nl | nl << 16, 0u);
+        const uint32_t c = (uint16_t)cfv[q], l = (uint16_t)clv[q];
+        s_cc[i] = make_uint2(c | c << 16, l | l << 16);
       }
     }
     if (tid < 4 * 13) s_perm[tid] = (&c_perm7[0][0])[tid];
+  }
+  if (tid < 16) {
+    const uint32_t c = (uint16_t)chc, l = (uint16_t)chl;
+    if (ctt < 6) s_ch[ck][ctt] = make_uint2(c | c << 16, l | l << 16);
+    s_cc8[ck][ctt] = ccv;
   }
   __syncthreads();
   ALF_STAMP(1);
   // sample (x, y) in picture coordinates -> LDS (valid for x in [X0 - 8, X0 + 72), y in [Y0 - 3, Y0 + 19))
 #define T(x, y) ((int)t[((y) - Y0 + ALF_HALO) * ALF_SW + (x) - X0 + ALF_LX])
   const int vbH = 1 << P.ctu_log2, vbPos = P.vb_luma;
-  {
+  // Classification and filtering of a 4x4 block run on the same four lanes: lane (block b, ii) classifies
+  // the block's subsampled row pair ii, the four partial sums are reduced across the lane quad (DPP), every
+  // lane of the quad derives the class, and then filters the block's column ii (no class table in LDS,
+  // no barrier between the two).
+  for (int b = tid >> 2; b < (ALF_TW / 4) * (ALF_TH / 4); b += 64) {
     // --- classification (deriveClassificationBlk): block b, subsampled row pair ii
-    const int b = tid >> 2, ii = tid & 3;
+    const int ii = tid & 3;
     const int bx = X0 + (b & 15) * 4, by = Y0 + (b >> 4) * 4;
     const bool on = bx < W && by < H && ctbOn;
     int sumV = 0, sumH = 0, sumD0 = 0, sumD1 = 0;
@@ -237,17 +295,25 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
         sumD1 = sad(a, T(ax - 1, rB), T(ax + 1, rA), sad(bb, T(ax, rB2), T(ax + 2, ay), sumD1));
       }
     }
-#pragma unroll
-    for (int m = 1; m < 4; m <<= 1) {
-      sumV += __shfl_xor(sumV, m);
-      sumH += __shfl_xor(sumH, m);
-      sumD0 += __shfl_xor(sumD0, m);
-      sumD1 += __shfl_xor(sumD1, m);
+    // quad sums: DPP quad_perm [1,0,3,2] then [2,3,0,1] (VALU only; a shuffle is an LDS instruction)
+    auto quad_sum = [](int v) {
+      v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);
+      return v + __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);
+    };
+    sumV = quad_sum(sumV); sumH = quad_sum(sumH); sumD0 = quad_sum(sumD0); sumD1 = quad_sum(sumD1);
+    const int x = bx + ii;
+    if (bx >= W || by >= H) continue;
+    int16_t *dst = D.p + x;
+    if (!on) {
+      for (int y = by; y < by + 4 && y < H; y++) dst[(size_t)y * D.stride] = (int16_t)T(x, y);
+      continue;
     }
-    if (ii == 0) {
+    int classIdx, tr;
+    {
       const int shift = P.bd + 4;
       const int act = clip3(0, 15, ((sumV + sumH) * ((yv == vbPos - 4 || yv == vbPos) ? 96 : 64)) >> shift);
-      int classIdx = c_th[act];
+      // c_th / c_transpose as packed immediates (a lane-indexed __constant__ table is a vector load)
+      classIdx = (int)((0x4333333332222210ull >> (4 * act)) & 15);   // th[16] = {0,1,2,2,2,2,2,3,...,3,4}
       int hv1, hv0, d1, d0, dirHV, dirD, mainDir, secDir;
       if (sumV > sumH) { hv1 = sumV; hv0 = sumH; dirHV = 1; } else { hv1 = sumH; hv0 = sumV; dirHV = 3; }
       if (sumD0 > sumD1) { d1 = sumD0; d0 = sumD1; dirD = 0; } else { d1 = sumD1; d0 = sumD0; dirD = 2; }
@@ -258,23 +324,11 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
       if (hvd1 > 2 * hvd0) strength = 1;
       if (hvd1 * 2 > 9 * hvd0) strength = 2;
       if (strength) classIdx += (((mainDir & 1) << 1) + strength) * 5;
-      const int tr = c_transpose[mainDir * 2 + (secDir >> 1)];
-      blk[b] = classIdx | (tr << 8) | ((on ? 1 : 0) << 16);
+      tr = (0xDE84 >> (2 * (mainDir * 2 + (secDir >> 1)))) & 3;        // transpose[8] = {0,1,0,2,2,3,1,3}
     }
-  }
-  __syncthreads();
-  ALF_STAMP(2);
-  // --- 7x7 diamond filter (filterBlk<ALF_FILTER_7>): lane = one column of one 4x4 block
-  {
-    const int x = X0 + (tid & 63), by = Y0 + (tid >> 6) * 4;
-    if (x < W && by < H) {
-      const int bi = blk[((tid >> 6) << 4) + ((tid & 63) >> 2)];
-      int16_t *dst = D.p + x;
-      if (!(bi >> 16)) {
-        for (int y = by; y < by + 4 && y < H; y++) dst[(size_t)y * D.stride] = (int16_t)T(x, y);
-      } else {
-        const int classIdx = bi & 255, tr = (bi >> 8) & 255;
-        const uint4 *cc = s_cc + classIdx * 13;
+    {
+      {
+        const uint2 *cc = s_cc + classIdx * 13;
         // packed 16-bit arithmetic: the two samples of a tap pair as one int16x2 (differences to the centre
         // fit 16 bits, clips <= 1 << bd), clipped with packed min / max, then one dot2 with the coefficient
         // pair (c, c): exactly c * clip(a - cur) + c * clip(b - cur)
@@ -282,10 +336,10 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
 #pragma unroll
         for (int k = 0; k < 12; k++) {
           const int pk = s_perm[tr * 13 + k];
-          const uint4 e = cc[pk];
+          const uint2 e = cc[pk];
           fcp[k] = __builtin_bit_cast(short2_t, e.x);
           clp[k] = __builtin_bit_cast(short2_t, e.y);
-          cln[k] = __builtin_bit_cast(short2_t, e.z);
+          cln[k] = (short2_t){0, 0} - clp[k];
         }
         const int maxv = (1 << P.bd) - 1;
         const int yb = by & (vbH - 1);
@@ -357,15 +411,14 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
       }
     }
   }
+  ALF_STAMP(2);
   ALF_STAMP(3);
   // --- chroma (filterBlk<ALF_FILTER_5> per component + filterBlkCcAlf): lane = one chroma position
-  {
-    const int x = cx0 + (tid & (ALF_CW - 1)), y = cy0 + tid / ALF_CW;
+  for (int ci = tid; ci < ALF_CW * ALF_CHH; ci += 256) {
+    const int x = cx0 + (ci & (ALF_CW - 1)), y = cy0 + ci / ALF_CW;
     const DPlane &C1 = P.src[1];
     if (x < C1.w && y < C1.h && y < (P.y1 >> 1)) {
 #define TC(k, xx, yy) ((int)tc[k][((yy) - cy0 + 2) * ALF_CSW + (xx) - cx0 + 8])
-      const int ctb = ctbT;   // the region lies in one CTB: uniform, so the filter's coefficients are scalars
-      const int n = P.nctb;
       const int maxv = (1 << P.bd) - 1;
       const int vbHc = 1 << (P.ctu_log2 - 1), vbPosC = P.vb_chroma;
       int r1, r2, r3, r4, r5, r6;
@@ -382,7 +435,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
       // (the staged tile holds picture-clamped samples at every position: no clamps here)
       auto L = [&](int xx, int yy) { return T(xx, yy); };
       int sl[8] = {};
-      if (P.en[3] || P.en[4]) {
+      if (ccCb || ccCr) {
         sl[0] = L(lx, ly);
         sl[1] = L(lx, ly + o2); sl[2] = L(lx - 1, ly); sl[3] = L(lx + 1, ly);
         sl[4] = L(lx - 1, ly + o1); sl[5] = L(lx, ly + o1); sl[6] = L(lx + 1, ly + o1);
@@ -394,12 +447,10 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
         const DPlane &Sc = P.src[comp];
         auto A = [&](int xx, int yy) { return TC(k, xx, yy); };
         const int cur = TC(k, x, y);
-        const bool on = P.en[comp] && P.ctb_en[comp * n + ctb];
-        const int alt = P.ctb_alt[comp * n + ctb];
-        const int ccf = P.en[2 + comp] ? P.cc_ctl[k * n + ctb] : 0;
+        const bool on = k ? onCr : onCb;
+        const int ccf = k ? ccCr : ccCb;
         int v = cur;
         if (on) {
-          const int16_t *fc = P.chroma_coef + alt * 7, *fl = P.chroma_clip + alt * 7;
           const int q[12] = {A(x, r3), A(x, r4), A(x + 1, r1), A(x - 1, r2), A(x, r1), A(x, r2),
                              A(x - 1, r1), A(x + 1, r2), A(x + 2, y), A(x - 2, y), A(x + 1, y), A(x - 1, y)};
           // packed like the luma taps: the pair's differences to the centre clipped as int16x2, one dot2
@@ -407,20 +458,20 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
           int sum = 0;
 #pragma unroll
           for (int tt = 0; tt < 6; tt++) {
-            const short c = fc[tt], l = fl[tt];
+            const uint2 e = s_ch[k][tt];
+            const short2_t l2 = __builtin_bit_cast(short2_t, e.y);
             short2_t d = (short2_t){(short)q[2 * tt], (short)q[2 * tt + 1]} - cc2;
-            d = __builtin_elementwise_min(__builtin_elementwise_max(d, (short2_t){(short)-l, (short)-l}), (short2_t){l, l});
-            sum = __builtin_amdgcn_sdot2(d, (short2_t){c, c}, sum, true);
+            d = __builtin_elementwise_min(__builtin_elementwise_max(d, (short2_t){0, 0} - l2), l2);
+            sum = __builtin_amdgcn_sdot2(d, __builtin_bit_cast(short2_t, e.x), sum, true);
           }
           sum = nearVB ? (sum + 64) >> 10 : (sum + 64) >> 7;
           v = clip3(0, maxv, sum + cur);
         }
         if (ccf) {
-          const int16_t *f = P.cc_coef + (k * 4 + ccf - 1) * 8;
           const int c0 = sl[0];
           int sum = 0;
 #pragma unroll
-          for (int tt = 0; tt < 7; tt++) sum += f[tt] * (sl[1 + tt] - c0);
+          for (int tt = 0; tt < 7; tt++) sum += s_cc8[k][tt] * (sl[1 + tt] - c0);
           sum = (sum + 64) >> 7;
           const int off = (1 << P.bd) >> 1;
           sum = clip3(0, maxv, sum + off) - off;
@@ -436,7 +487,10 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
 }
 
 // One launch, one workgroup per region; regions in XCD-contiguous runs (raster order within a run).
-__global__ __launch_bounds__(256) void k_alf(AlfParams P, int gx, int gy) {
+#ifndef ALF_WAVES_PER_EU
+#define ALF_WAVES_PER_EU 1   // no cap (72 VGPRs, seven workgroups per CU); 8 (64 VGPRs) spills one VGPR, same speed
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALF_WAVES_PER_EU))) void k_alf(AlfParams P, int gx, int gy) {
 #ifdef ALF_NO_SWIZZLE
   const int b = (int)blockIdx.x;
 #else
