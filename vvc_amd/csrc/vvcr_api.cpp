@@ -527,7 +527,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
       const int lists = U.l[0].present + U.l[1].present;
       const double nsb = (j.w / 4.0) * (j.h / 4.0);
       b += 2.0 * (lists * nsb * (81 + 2 * 0.25 * 49) + 1.5 * j.w * j.h);   // 6-tap (4+5)^2 luma, 4-tap chroma
-      if (U.recon & MC_RESI) b += 2.0 * 1.5 * j.w * j.h;                     // the residual of a fused reconstruction
+      b += resi_bytes(U.recon, j.w, j.h);                                      // the residual of a fused reconstruction
     }
     r.alg_bytes[K_MC_AFFINE] = b;
   }

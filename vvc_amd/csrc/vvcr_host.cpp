@@ -141,8 +141,34 @@ void set_wp(const vvcr_pic_params &pp, McJob &j, int r0, int r1, int cu_bcw) {
 double mc_alg_bytes(uint16_t flags, int w, int h) {
   const int lists = ((flags & MC_L0) ? 1 : 0) + ((flags & MC_L1) ? 1 : 0);
   const double in = (double)(w + 7) * (h + 7) + 2.0 * (w / 2 + 3) * (h / 2 + 3);
-  // + the residual read by a fused reconstruction (MC_RESI); the output is written once either way
-  return 2.0 * (lists * in + 1.5 * w * h + ((flags & MC_RESI) ? 1.5 * w * h : 0.0));
+  // + the residual read by a fused reconstruction (MC_RESI << comp); the output is written once either way
+  return 2.0 * (lists * in + 1.5 * w * h) + resi_bytes(flags, w, h);
+}
+
+// Residual bytes a fused reconstruction reads for a w x h luma area with recon flags f (4:2:0).
+double resi_bytes(int f, int w, int h) {
+  return 2.0 * (((f & MC_RESI) ? w * h : 0) + ((f & MC_RESI_CB) ? w * h / 4 : 0) + ((f & MC_RESI_CR) ? w * h / 4 : 0));
+}
+
+// Which components of a CU have a coded residual (the coded-block rule of build_tb_jobs: a joint Cb-Cr TB
+// writes both chroma components): MC_RESI << comp per component.
+uint16_t cu_resi_flags(const PictureDescriptors &d, const vvcr_cu &c) {
+  if (!c.rootcbf) return 0;
+  uint16_t f = 0;
+  for (int k = 0; k < c.ntu; k++) {
+    const int ti = c.firsttu + k;
+    if (ti < 0 || ti >= (int)d.tu.size()) break;
+    const vvcr_tu &t = d.tu[ti];
+    for (int comp = 0; comp < 3; comp++) {
+      const int32_t *b = t.b[comp];
+      if (b[2] <= 0) continue;
+      bool written;
+      if (comp > 0 && t.jccr) written = t.b[(t.jccr >> 1) ? 1 : 2][6] >= 0;
+      else written = b[4] != 0 && b[6] >= 0;
+      if (written) f |= (uint16_t)(MC_RESI << comp);
+    }
+  }
+  return f;
 }
 
 void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d) {
@@ -321,7 +347,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   for (size_t ci = 0; ci < d.cu.size(); ci++) {
     const vvcr_cu &c = d.cu[ci];
     if (c.predmode != MODE_INTER || !c.yvalid || !in_shard(pp, c)) continue;
-    const uint16_t recon = (fuse && fused_inter_cu(pp, d, c)) ? (uint16_t)(MC_RECON | (c.rootcbf ? MC_RESI : 0)) : 0;
+    const uint16_t recon = (fuse && fused_inter_cu(pp, d, c)) ? (uint16_t)(MC_RECON | cu_resi_flags(d, c)) : 0;
     if (c.geo) {
       // motionCompensationGeo (InterPrediction.cpp:1749): two uni candidates at 14 bits, blended
       const vvcr_pu &p = d.pu[c.firstpu];
@@ -700,7 +726,8 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
 // TB_ZERO jobs: every transform-block area whose residual a consumer reads but no coded block writes (the
 // residual planes are not cleared per picture when the reconstruction stages run together). Readers: intra
 // CUs (k_intra reads each step's residual rectangle), inter CUs reconstructed by k_recon_inter (LMCS / CIIP:
-// the whole CU), and fused inter CUs with a coded residual (MC_RESI: all three components of the CU).
+// the whole CU), and fused inter CUs per component with a coded TB of that component (MC_RESI << comp:
+// that component of the whole CU).
 void build_zero_jobs(const vvcr_pic_params &pp, const PictureDescriptors &d, bigbuf::vec<TbJob> &out) {
   auto zero = [&](int comp, int x, int y, int w, int h) {
     // split into blocks of at most 64 x 64 (the TbJob sides are 8-bit)
@@ -715,13 +742,13 @@ void build_zero_jobs(const vvcr_pic_params &pp, const PictureDescriptors &d, big
       }
   };
   const int ncu = (int)d.cu.size();
-  bigbuf::vec<uint8_t> reads(ncu, 0);
+  bigbuf::vec<uint8_t> reads(ncu, 0);   // bit comp: the CU's residual of that component is read
   for (int i = 0; i < ncu; i++) {
     const vvcr_cu &c = d.cu[i];
     if (!in_shard(pp, c)) continue;
-    if (c.predmode != MODE_INTER) { reads[i] = 1; continue; }
+    if (c.predmode != MODE_INTER) { reads[i] = 7; continue; }
     if (!fused_inter_cu(pp, d, c)) {
-      reads[i] = 1;
+      reads[i] = 7;
       if (!c.rootcbf) {   // no transform tree: the whole CU reads zeros
         if (c.yvalid) zero(0, c.x, c.y, c.w, c.h);
         if (c.cvalid) { zero(1, c.cx, c.cy, c.cw, c.ch); zero(2, c.cx, c.cy, c.cw, c.ch); }
@@ -729,14 +756,15 @@ void build_zero_jobs(const vvcr_pic_params &pp, const PictureDescriptors &d, big
       }
       continue;
     }
-    reads[i] = c.rootcbf ? 1 : 0;
+    // a fused CU reads the residual of a component only where one of its TBs is coded (MC_RESI << comp)
+    reads[i] = (uint8_t)(cu_resi_flags(d, c) / MC_RESI);
   }
   for (size_t ti = 0; ti < d.tu.size(); ti++) {
     const vvcr_tu &t = d.tu[ti];
     if (t.cu < 0 || t.cu >= ncu || !reads[t.cu]) continue;
     for (int comp = 0; comp < 3; comp++) {
       const int32_t *b = t.b[comp];
-      if (b[2] <= 0) continue;
+      if (b[2] <= 0 || !((reads[t.cu] >> comp) & 1)) continue;
       // the coded-block rule of build_tb_jobs: a JCCR Cb job writes Cr too
       bool written;
       if (comp == 2 && t.jccr) {

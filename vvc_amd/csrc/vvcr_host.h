@@ -79,6 +79,8 @@ void build_scan_tables(ScanTables &st);
 
 // Algorithmic bytes of one plain / DMVR / BDOF MC unit (vvcr_host.cpp)
 double mc_alg_bytes(uint16_t flags, int w, int h);
+double resi_bytes(int recon_flags, int w, int h);
+uint16_t cu_resi_flags(const PictureDescriptors &d, const vvcr_cu &c);
 
 // Throws VvcrError on inconsistent descriptors (indices out of range, blocks outside the picture).
 void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d);

@@ -17,6 +17,16 @@ __device__ __forceinline__ int xcd_swizzle(int b, int G) {
   return x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
 }
 
+// The same in runs of R: within each super-group of 8R consecutive blocks, the R blocks one XCD receives take
+// R consecutive items (neighbouring work shares that XCD's L2, and the XCDs still take turns every R
+// items: no XCD gets a whole region of heavy work); the tail after the last super-group keeps its order.
+__device__ __forceinline__ int xcd_run_swizzle(int b, int G, int R) {
+  const int S = 8 * R, full = (G / S) * S;
+  if (b >= full) return b;
+  const int s = b / S, j = b - s * S;
+  return s * S + (j & 7) * R + (j >> 3);
+}
+
 #define VVCR_CHECK_HIP(expr)                                                        \
   do {                                                                              \
     hipError_t _e = (expr);                                                         \
@@ -53,7 +63,9 @@ enum : uint16_t {
   MC_GEO = 1 << 8,       // two uni-predicted GEO parts blended by split weights (InterpolationFilter.cpp:997)
   MC_WP = 1 << 9,        // explicit weighted prediction epilogue (WeightPrediction::addWeightUni / addWeightBi)
   MC_RECON = 1 << 10,    // k_mc writes the reconstruction (+ residual, clipped) into the picture (fused_inter_cu)
-  MC_RESI = 1 << 11,     // MC_RECON with a residual (the CU's root cbf)
+  MC_RESI = 1 << 11,     // MC_RECON with a luma residual (a coded luma TB in the CU); MC_RESI << comp per component
+  MC_RESI_CB = 1 << 12,  // ... a Cb residual (a coded Cb TB, or a joint Cb-Cr TB)
+  MC_RESI_CR = 1 << 13,  // ... a Cr residual
 };
 
 struct McJob {

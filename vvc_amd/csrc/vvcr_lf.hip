@@ -136,6 +136,16 @@ __constant__ int8_t c_perm7[4][13] = {{0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12}
 // region shares with its neighbours are fetched from HBM once per XCD, and the chroma work of a region
 // reads the luma its own workgroup staged (before r04 the chroma work was dispatched after all luma
 // tiles and re-read the luma from HBM: 3.2x the algorithmic bytes).
+// diagnostics only (timing ablations, wrong output): skip the classification sums / the luma taps / chroma
+#ifndef ALF_ABL_CLASS
+#define ALF_ABL_CLASS 0
+#endif
+#ifndef ALF_ABL_LUMA
+#define ALF_ABL_LUMA 0
+#endif
+#ifndef ALF_ABL_CHROMA
+#define ALF_ABL_CHROMA 0
+#endif
 #ifndef ALF_ROWS
 #define ALF_ROWS 16   // region height (16 or 32; at most the CTU size, so a region lies in one CTB)
 #endif
@@ -278,7 +288,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
     int sumV = 0, sumH = 0, sumD0 = 0, sumD1 = 0;
     const int yv = by & (vbH - 1);
     const int i0 = (yv == vbPos) ? 1 : 0, i1 = (yv == vbPos - 4) ? 3 : 4;
-    if (on && ii >= i0 && ii < i1) {
+    if (!ALF_ABL_CLASS && on && ii >= i0 && ii < i1) {
       const int ay = by - 2 + ii * 2;
       int rA = ay - 1, rB = ay + 1, rB2 = ay + 2;
       if (ay > 0 && (ay & (vbH - 1)) == vbPos - 2) rB2 = ay + 1;
@@ -360,6 +370,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
               d = __builtin_elementwise_min(__builtin_elementwise_max(d, cln[k]), clp[k]);
               sum = __builtin_amdgcn_sdot2(d, fcp[k], sum, true);
             };
+#if !ALF_ABL_LUMA
             tap(0, TT(0, dy + 3), TT(0, dy - 3));
             tap(1, TT(1, dy + 2), TT(-1, dy - 2));
             tap(2, TT(0, dy + 2), TT(0, dy - 2));
@@ -372,6 +383,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
             tap(9, TT(3, dy), TT(-3, dy));
             tap(10, TT(2, dy), TT(-2, dy));
             tap(11, TT(1, dy), TT(-1, dy));
+#endif
             sum = (sum + 64) >> 7;
             dst[(size_t)(by + dy) * D.stride] = (int16_t)clip3(0, maxv, sum + cur);
           }
@@ -417,7 +429,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
   for (int ci = tid; ci < ALF_CW * ALF_CHH; ci += 256) {
     const int x = cx0 + (ci & (ALF_CW - 1)), y = cy0 + ci / ALF_CW;
     const DPlane &C1 = P.src[1];
-    if (x < C1.w && y < C1.h && y < (P.y1 >> 1)) {
+    if (!ALF_ABL_CHROMA && x < C1.w && y < C1.h && y < (P.y1 >> 1)) {
 #define TC(k, xx, yy) ((int)tc[k][((yy) - cy0 + 2) * ALF_CSW + (xx) - cx0 + 8])
       const int maxv = (1 << P.bd) - 1;
       const int vbHc = 1 << (P.ctu_log2 - 1), vbPosC = P.vb_chroma;

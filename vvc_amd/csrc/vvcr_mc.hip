@@ -190,6 +190,9 @@ __constant__ CellTaps c_ctaps = make_cell_taps();
 #ifndef MC_WAVES_PER_EU
 #define MC_WAVES_PER_EU 4
 #endif
+#ifndef MC_XCD_RUN
+#define MC_XCD_RUN 32
+#endif
 #ifndef MC_RESI_AHEAD
 #define MC_RESI_AHEAD 0   // 0 / 2 / 4 measured within 1 % (fused 4K B pictures); 0 holds the fewest registers
 #endif
@@ -385,7 +388,7 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
   const int ts = (N == 8) ? ((J.w == 4 && J.h == 4) ? 1 : 0) | ((J.flags & MC_ALT_HPEL) ? 2 : 0) : 0;
   // destination: the prediction planes, or with MC_RECON the picture itself (the reconstruction
   // clip(pred + resi) of AreaBuf::reconstruct, Buffer.cpp:590, fused: no prediction plane round trip)
-  const bool recon = (J.flags & MC_RECON) != 0, addResi = (J.flags & MC_RESI) != 0;
+  const bool recon = (J.flags & MC_RECON) != 0, addResi = (J.flags & (MC_RESI << comp)) != 0;
   const DPlane &O0 = recon ? P.reco[0] : P.out[0], &O1 = recon ? P.reco[1] : P.out[1], &O2 = recon ? P.reco[2] : P.out[2];
   const int ostride = comp ? O1.stride : O0.stride;
   int16_t *dst = (comp == 0 ? O0.p : comp == 1 ? O1.p : O2.p) + (size_t)y * ostride + x;
@@ -560,10 +563,15 @@ __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_
 #endif
   // (A persistent grid walking the blocks was slower, 47.3 vs 41.4 us, and doubled the kernel's code:
   // removed, r04.)
-  // Blocks in dispatch order: with one wave per workgroup the XCD-contiguous order (r03, for 256-lane
-  // workgroups) was slower (4K B pictures: QP27 32.9 -> 31.8 us, QP32 27.4 -> 25.8 us without it, r04)
-#ifdef MC_XCD_SWIZZLE
+  // Block order: XCD runs of MC_XCD_RUN (32) consecutive blocks, the XCDs taking turns every run. Whole-grid
+  // XCD-contiguous runs (r03, xcd_swizzle) cluster heavy regions on a few XCDs (4K B pictures, fused: QP27
+  // 34.6 us, 67 MB read); dispatch order spreads the work but fetches every shared reference window into
+  // several L2s (35.2 us, 151 MB); runs of 32: 30.0 us, 78 MB (runs of 4 / 8 / 16 / 64 / 128: 32.5 / 31.0
+  // / 30.3 / 30.7 / 30.8 us; r04, tools/gpu_r04x.sh)
+#if defined(MC_XCD_SWIZZLE)
   MC_BODY(xcd_swizzle(blockIdx.x, gridDim.x));
+#elif MC_XCD_RUN > 0
+  MC_BODY(xcd_run_swizzle((int)blockIdx.x, (int)gridDim.x, MC_XCD_RUN));
 #else
   MC_BODY((int)blockIdx.x);
 #endif

@@ -22,6 +22,10 @@
 // taps come from LDS tables indexed by each lane's fraction and the pair parity is per lane (fir4_var).
 #include "vvcr_internal.h"
 #include <cstdlib>
+
+#ifndef AFF_XCD_RUN
+#define AFF_XCD_RUN 32
+#endif
 #include "vvcr_tables.h"
 #include "vvcr_mcdev.h"
 
@@ -519,7 +523,7 @@ __device__ __forceinline__ void mc_affine(const McParams &P, const AffJob *__res
   // into the picture (AreaBuf::reconstruct, Buffer.cpp:590)
   auto store4 = [&](int comp, int x, int y, int v0, int v1, int v2, int v3) {
     if (U.recon & MC_RECON) {
-      if (U.recon & MC_RESI) {
+      if (U.recon & (MC_RESI << comp)) {
         const DPlane &r = P.resi[comp];
         const uint2 q = *(const uint2 *)(r.p + (size_t)y * r.stride + x);
         v0 = clampi(v0 + lo16(q.x), 0, maxv); v1 = clampi(v1 + hi16(q.x), 0, maxv);
@@ -558,7 +562,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   __shared__ AffLds lds[2];
   __shared__ AffTapLds taps;
   const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
-  mc_affine(P, jobs, njobs, pus, 2 * blockIdx.x + half, threadIdx.x & 127, lds[half], taps, force_glob != 0);
+  // XCD runs of 32 workgroups (xcd_run_swizzle): 4K B pictures QP27 67.6 -> 31.5 MB read per launch, same
+  // time (r04, tools/gpu_r04x.sh)
+#if AFF_XCD_RUN > 0
+  const int blk = xcd_run_swizzle((int)blockIdx.x, (int)gridDim.x, AFF_XCD_RUN);
+#else
+  const int blk = (int)blockIdx.x;
+#endif
+  mc_affine(P, jobs, njobs, pus, 2 * blk + half, threadIdx.x & 127, lds[half], taps, force_glob != 0);
 }
 
 }  // namespace

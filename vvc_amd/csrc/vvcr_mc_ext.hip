@@ -12,6 +12,10 @@
 #include "vvcr_internal.h"
 #include "vvcr_tables.h"
 
+#ifndef BIDIR_XCD_RUN
+#define BIDIR_XCD_RUN 32
+#endif
+
 namespace {
 
 __constant__ int8_t x_luma[16][8] = VVCR_LUMA_FILTER_TABLE;
@@ -129,7 +133,13 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
   __shared__ int16_t gx[2][PS * PS], gy[2][PS * PS];
   __shared__ int sh_delta[2], sh_bdof;
   __shared__ int sh_v[16][2];
+  // XCD runs of 32 jobs (xcd_run_swizzle): neighbouring jobs' reference windows share an L2; 4K B pictures
+  // QP27: 26.6 -> 10.6 MB read per launch, time within 2 % (r04, tools/gpu_r04x.sh)
+#if BIDIR_XCD_RUN > 0
+  const int j = xcd_run_swizzle((int)blockIdx.x, (int)gridDim.x, BIDIR_XCD_RUN);
+#else
   const int j = blockIdx.x;
+#endif
   if (j >= njobs) return;
   const McJob J = load_uniform(jobs + j);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -388,7 +398,7 @@ __global__ __launch_bounds__(256) void k_mc_bidir(McParams P, const McJob *__res
   // into the picture (AreaBuf::reconstruct, Buffer.cpp:590)
   auto store1 = [&](int comp, int x, int y, int v) {
     if (J.flags & MC_RECON) {
-      if (J.flags & MC_RESI) v = clampi(v + P.resi[comp].p[(size_t)y * P.resi[comp].stride + x], 0, maxv);
+      if (J.flags & (MC_RESI << comp)) v = clampi(v + P.resi[comp].p[(size_t)y * P.resi[comp].stride + x], 0, maxv);
       P.reco[comp].p[(size_t)y * P.reco[comp].stride + x] = (int16_t)v;
     } else {
       P.out[comp].p[(size_t)y * P.out[comp].stride + x] = (int16_t)v;
