@@ -408,10 +408,15 @@ def main():
             run_step()
             ctx.sync()
         s_el = (time.perf_counter() - s0) / max(1, a.resident_steps // 2)
-        # one more step with per-kernel HIP events (one segment in flight): the kernel table and roofline
+        # one more step with per-kernel HIP events: the kernel table and roofline. One segment, a host sync
+        # after every picture, so that no kernel overlaps another picture's (the lanes would otherwise run
+        # independent pictures side by side, and a kernel's event interval would include their work); the
+        # same shape as the rocprofv3 one-segment --sync-pictures trace that checks these durations
         ctx.set_timing(True)
-        run_step()
-        ctx.sync()
+        for hnd in copies[nstep[0] % a.segments][0]:
+            ctx.launch(hnd)
+            ctx.sync()
+        nstep[0] += 1
         for hnd in copies[(nstep[0] - 1) % a.segments][0]:
             for name, launches, ms, alg in ctx.kernel_stats(hnd):
                 k = kern.setdefault(name, [0, 0.0, 0.0])
@@ -448,7 +453,7 @@ def main():
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
                 "us_per_launch": round(per_launch_s * 1e6, 2)}
-    mc_roof = {"peak": PEAK_HBM_GBS, "unit": "GB/s", "note": "MC interpolation kernels, HIP events, one segment in flight"}
+    mc_roof = {"peak": PEAK_HBM_GBS, "unit": "GB/s", "note": "MC interpolation kernels, HIP events, one segment, a sync after every picture"}
     for k in ("mc", "mc_affine", "mc_bidir"):
         v = kern.get(k, [0, 0.0, 0.0])
         g = v[2] / (v[1] / 1e3) / 1e9 if v[1] > 0 else 0.0

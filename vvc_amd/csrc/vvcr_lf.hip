@@ -505,6 +505,8 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALF_WAVES_PER_EU))) void k_alf(AlfParams P, int gx, int gy) {
 #ifdef ALF_NO_SWIZZLE
   const int b = (int)blockIdx.x;
+#elif defined(ALF_XCD_RUN)
+  const int b = xcd_run_swizzle((int)blockIdx.x, (int)gridDim.x, ALF_XCD_RUN);
 #else
   const int b = xcd_swizzle(blockIdx.x, gridDim.x);
 #endif
