@@ -124,6 +124,155 @@ def cpu_baseline(stream_bin, pixels_per_run, min_seconds=10.0, max_runs=40):
                       % (os.path.basename(stream_bin)[:-4], runs, total)}
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_all_cores(stream_bin, pixels_per_run, procs, runs_each=2):
+    """The like-for-like comparator of the headline's `procs` host threads:
+    `procs` VTM DecoderApp processes (-dph 0, one thread each) decoding the same bitstream at once, each
+    `runs_each` times back to back; total pixels of every run / wall time from the first start to the last
+    end."""
+    import threading
+    exe = os.path.join(ROOT, "oracle", "_ref", "DecoderApp")
+    if not os.path.exists(exe):
+        return None
+    fails = []
+
+    def worker():
+        for _ in range(runs_each):
+            r = subprocess.run([exe, "-b", stream_bin, "-dph", "0"], capture_output=True, text=True)
+            if r.returncode != 0:
+                fails.append(r.returncode)
+    th = [threading.Thread(target=worker) for _ in range(procs)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    if fails:
+        return None
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"value": round(pixels_per_run * procs * runs_each / wall / 1e6, 3), "unit": "Mpixels/s", "cores": procs,
+            "kind": "reference", "cpu": cpu_model(), "affinity_cpus": aff,
+            "sample": "%d concurrent VTM-7.3 DecoderApp processes (x86 SIMD, 1 thread each, -dph 0, no output file), "
+                      "each decoding %s.bin %d times; %.1f s wall" % (procs, os.path.basename(stream_bin)[:-4], runs_each, wall)}
+
+
+class _Roctx:
+    """rocprofv3 --selected-regions: the trace collects only between roctxProfilerResume(0) and
+    roctxProfilerPause(0), so a profile of bench.py covers exactly the kernel-table steps. Enabled by
+    VVCR_ROCTX_REGIONS=1 (no-op otherwise)."""
+    L = None
+
+    @classmethod
+    def _lib(cls):
+        if cls.L is None and os.environ.get("VVCR_ROCTX_REGIONS") == "1":
+            import ctypes
+            cls.L = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
+        return cls.L
+
+    @classmethod
+    def resume(cls):
+        if cls._lib() is not None:
+            cls.L.roctxProfilerResume(0)
+
+    @classmethod
+    def pause(cls):
+        if cls._lib() is not None:
+            cls.L.roctxProfilerPause(0)
+
+
+def kernel_table(ctx, handles, reps):
+    """Per-kernel HIP-event durations (events on the library's lanes, vvcr_kernel_stats) of one decode's
+    resident pictures: `reps` steps, each launching every picture with a host sync after it (no kernel
+    overlaps another picture's), summed per kernel and step; the table keeps the MEDIAN step's time per
+    kernel and its min / max across the steps. These are the launches a `VVCR_ROCTX_REGIONS=1 rocprofv3
+    --selected-regions` trace of the same command records. Returns {name: [launches, ms, alg_bytes, ms_min,
+    ms_max]} (per step)."""
+    ctx.set_timing(True)
+    steps = []
+    _Roctx.resume()
+    for _ in range(max(1, reps)):
+        for hnd in handles:
+            ctx.launch(hnd)
+            ctx.sync()
+        rep = {}
+        for hnd in handles:
+            for name, launches, ms, alg in ctx.kernel_stats(hnd):
+                k = rep.setdefault(name, [0, 0.0, 0.0])
+                k[0] += launches
+                k[1] += ms
+                k[2] += alg
+        steps.append(rep)
+    _Roctx.pause()
+    ctx.set_timing(False)
+    out = {}
+    for name in sorted(set().union(*steps)):
+        v = [s[name] for s in steps if name in s and s[name][0]]
+        if not v:
+            continue
+        ms = sorted(x[1] for x in v)
+        out[name] = [v[0][0], float(np.median(ms)), v[0][2], ms[0], ms[-1]]
+    return out
+
+
+def resident_handles(ctx, data, per, base=0):
+    """One decode of the stream on slots [base, base + per), its prepared pictures kept (decoding order)."""
+    from vvc_amd import bitstream as B
+    seq = B.SequenceDecode(ctx, data, nslots=per, base=base, threads=8)
+    _, handles = seq.run(keep_handles=True)
+    ctx.sync()
+    return handles, [(inf["poc"], seq.slot[i]) for i, inf in enumerate(seq.info)]
+
+
+def mc_roofline(kern, note):
+    out = {"peak": PEAK_HBM_GBS, "unit": "GB/s", "note": note}
+    tot = [0.0, 0.0]
+    for k in ("mc", "mc_affine", "mc_bidir"):
+        v = kern.get(k, [0, 0.0, 0.0, 0.0, 0.0])
+        g = v[2] / (v[1] / 1e3) / 1e9 if v[1] > 0 else 0.0
+        out[k] = {"achieved": round(g, 2), "frac": round(g / PEAK_HBM_GBS, 4),
+                  "us_per_launch": round(v[1] / max(v[0], 1) * 1e3, 2),
+                  "us_per_launch_min_max": [round(v[3] / max(v[0], 1) * 1e3, 2), round(v[4] / max(v[0], 1) * 1e3, 2)],
+                  "alg_MB_per_launch": round(v[2] / max(v[0], 1) / 1e6, 3), "launches_per_step": v[0]}
+        tot[0] += v[2]
+        tot[1] += v[1]
+    g = tot[0] / (tot[1] / 1e3) / 1e9 if tot[1] > 0 else 0.0
+    out["mc_stage"] = {"achieved": round(g, 2), "frac": round(g / PEAK_HBM_GBS, 4), "ms_per_step": round(tot[1], 4)}
+    return out
+
+
+def north_star_mc(ctx, stream, per, reps):
+    """north_star's MC target is quoted on 4K RA QP32: the same kernel table on that stream."""
+    p = os.path.join(ROOT, "tests", "golden", "streams", stream + ".bin")
+    if not os.path.exists(p):
+        return None
+    with open(p, "rb") as f:
+        data = f.read()
+    handles, slots = resident_handles(ctx, data, per)
+    meta = S.load_meta(os.path.join(ROOT, "tests", "golden", stream))
+    kern = kernel_table(ctx, handles, reps)
+    ok = check_slots(ctx, {slot: poc for poc, slot in slots}, meta)
+    for h in handles:
+        ctx.release(h)
+    r = mc_roofline(kern, "%s, one segment, a host sync after every picture, median of %d steps (HIP events)" % (stream, reps))
+    r["stream"] = stream
+    r["bitexact_vs_reference"] = bool(ok)
+    return r
+
+
 def shard_bench(a, R):
     """BASELINE config 4 end to end from the bitstream: one tile-row stream decoded by all ranks together
     (vvc_amd/shard.py StreamShardRank). Every rank parses the .bin (CABAC, motion derivation with the
@@ -275,8 +424,14 @@ def main():
                          "2545 / 2763 / 2572 Mpx/s; 1080p 33 pictures: 12 / 16 2372 / 2122)")
     ap.add_argument("--resident-steps", type=int, default=20, help="timed steps of the resident (pre-planned) pass, 0 = skip")
     ap.add_argument("--single-steps", type=int, default=5, help="timed decodes of the single-stream pass (one decode in flight), 0 = skip")
-    ap.add_argument("--kernel-table-reps", type=int, default=3,
-                    help="timed one-segment steps of the kernel table / roofline; each kernel keeps its fastest")
+    ap.add_argument("--kernel-table-reps", type=int, default=7,
+                    help="one-segment steps of the kernel table / roofline (a sync after every picture); each kernel "
+                         "reports its median step with the min / max")
+    ap.add_argument("--kernel-table-only", action="store_true",
+                    help="profiling: only the kernel table of --stream and of --north-star-stream (with "
+                         "VVCR_ROCTX_REGIONS=1 under rocprofv3 --selected-regions the trace holds exactly those steps)")
+    ap.add_argument("--north-star-stream", default="ra2160l_q32",
+                    help="north_star's MC target stream (4K RA QP32): its MC kernel table goes into `north_star_mc`")
     ap.add_argument("--sync-pictures", action="store_true",
                     help="host sync after every picture of the resident pass (profiling: kernel durations without overlap)")
     ap.add_argument("--e2e-threads", type=int, default=16,
@@ -318,6 +473,25 @@ def main():
         os.environ["VVCR_INTRA_WG"])
     if saved is None:
         os.environ.pop("VVCR_INTRA_WG", None)
+
+    if a.kernel_table_only:
+        ctx.set_timing(False)
+        handles, slots = resident_handles(ctx, data, per)
+        kern = kernel_table(ctx, handles, a.kernel_table_reps)
+        ok = check_slots(ctx, {slot: poc for poc, slot in slots}, meta)
+        for h in handles:
+            ctx.release(h)
+        out = {"stream": a.stream, "reps": a.kernel_table_reps, "bitexact_vs_reference": bool(ok),
+               "mc_roofline": mc_roofline(kern, "median of %d synced steps" % a.kernel_table_reps),
+               "kernels": {k: {"us_per_launch": round(v[1] / max(v[0], 1) * 1e3, 2), "launches_per_step": v[0],
+                               "ms_per_step": round(v[1], 4), "ms_min_max": [round(v[3], 4), round(v[4], 4)],
+                               "alg_MB_per_launch": round(v[2] / max(v[0], 1) / 1e6, 3)} for k, v in kern.items()}}
+        if a.north_star_stream and a.north_star_stream != a.stream:
+            out["north_star_mc"] = north_star_mc(ctx, a.north_star_stream, per, a.kernel_table_reps)
+        ctx.close()
+        print(json.dumps(out))
+        R.close()
+        return
 
     # ---- headline: end to end from the bitstream (parse + derive + plan + upload + GPU in the timed region)
     ctx.set_timing(False)
@@ -410,30 +584,9 @@ def main():
             run_step()
             ctx.sync()
         s_el = (time.perf_counter() - s0) / max(1, a.resident_steps // 2)
-        # per-kernel HIP events: the kernel table and roofline. One segment, a host sync after every
-        # picture, so that no kernel overlaps another picture's (the lanes would otherwise run independent
-        # pictures side by side, and a kernel's event interval would include their work); the same shape as
-        # the rocprofv3 one-segment --sync-pictures trace that checks these durations. The step runs
-        # --kernel-table-reps times and each kernel keeps its fastest step: on some boxes the first kernels
-        # of every picture after the host sync ran 2x longer in one step and not in the next.
-        ctx.set_timing(True)
-        best = {}
-        for _ in range(max(1, a.kernel_table_reps)):
-            for hnd in copies[nstep[0] % a.segments][0]:
-                ctx.launch(hnd)
-                ctx.sync()
-            nstep[0] += 1
-            rep = {}
-            for hnd in copies[(nstep[0] - 1) % a.segments][0]:
-                for name, launches, ms, alg in ctx.kernel_stats(hnd):
-                    k = rep.setdefault(name, [0, 0.0, 0.0])
-                    k[0] += launches
-                    k[1] += ms
-                    k[2] += alg
-            for name, k in rep.items():
-                if name not in best or (k[0] and k[1] < best[name][1]):
-                    best[name] = k
-        kern.update(best)
+        # per-kernel HIP events: the kernel table and roofline (kernel_table: one segment, a host sync after
+        # every picture, the median step of --kernel-table-reps)
+        kern.update(kernel_table(ctx, copies[nstep[0] % a.segments][0], a.kernel_table_reps))
         for handles, _ in copies:
             for hnd in handles:
                 ctx.release(hnd)
@@ -450,7 +603,7 @@ def main():
     roof = None
     if kern:
         dom = max(kern, key=lambda k: kern[k][1])
-        dl, dms, dalg = kern[dom]
+        dl, dms, dalg = kern[dom][:3]
         per_launch_s = dms / 1e3 / max(dl, 1)
         achieved = dalg / max(dl, 1) / per_launch_s / 1e9 if per_launch_s > 0 else 0.0
         traffic = None
@@ -464,11 +617,12 @@ def main():
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic,
                 "us_per_launch": round(per_launch_s * 1e6, 2)}
-    mc_roof = {"peak": PEAK_HBM_GBS, "unit": "GB/s", "note": "MC interpolation kernels, HIP events, one segment, a sync after every picture"}
-    for k in ("mc", "mc_affine", "mc_bidir"):
-        v = kern.get(k, [0, 0.0, 0.0])
-        g = v[2] / (v[1] / 1e3) / 1e9 if v[1] > 0 else 0.0
-        mc_roof[k] = {"achieved": round(g, 2), "frac": round(g / PEAK_HBM_GBS, 4), "us_per_launch": round(v[1] / max(v[0], 1) * 1e3, 2)}
+    mc_roof = mc_roofline(kern, "MC interpolation kernels, HIP events, one segment, a sync after every picture, median of %d steps"
+                          % a.kernel_table_reps)
+    ns_mc = None
+    if a.resident_steps > 0 and a.north_star_stream and a.north_star_stream != a.stream:
+        ns_mc = north_star_mc(ctx, a.north_star_stream, per, a.kernel_table_reps)
+        bitexact = bitexact and (ns_mc is None or ns_mc["bitexact_vs_reference"])
 
     ms_step = elapsed / a.steps * 1e3
     kind, qp = a.stream.split("_")[0], a.stream.split("_")[-1]
@@ -500,15 +654,23 @@ def main():
         "single_stream": single,
         "resident": resident,
         "mc_roofline": mc_roof,
-        "kernels": {k: {"ms_per_step": round(v[1], 4), "launches_per_step": v[0],
+        "north_star_mc": ns_mc,
+        "kernels": {k: {"ms_per_step": round(v[1], 4), "ms_min_max": [round(v[3], 4), round(v[4], 4)], "launches_per_step": v[0],
                         "alg_GBps": round(v[2] / (v[1] / 1e3) / 1e9, 2) if v[1] > 0 else 0.0} for k, v in kern.items()},
     }
     if rank == 0 and world == 1 and not a.no_cpu:
         line["cpu_baseline"] = cpu_baseline(os.path.join(ROOT, "tests", "golden", "streams", a.stream + ".bin"), px_seq)
         cb = line["cpu_baseline"]
+        ca = line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(
+            os.path.join(ROOT, "tests", "golden", "streams", a.stream + ".bin"), px_seq, a.e2e_threads)
         if cb and cb.get("value"):
             line["vs_cpu_baseline"] = {"value": round(value / cb["value"], 1),
                                        "single_stream": round(single["value"] / cb["value"], 1) if single else None}
+        if ca and ca.get("value"):
+            line["vs_cpu_baseline_all_cores"] = {"value": round(value / ca["value"], 2),
+                                                 "single_stream": round(single["value"] / ca["value"], 2) if single else None,
+                                                 "note": "value uses %d host threads + the GPU; the comparator %d DecoderApp "
+                                                         "processes on %d cores" % (a.e2e_threads, ca["cores"], ca["cores"])}
     ctx.close()
     if a.shard_steps > 0:
         try:

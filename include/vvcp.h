@@ -115,6 +115,10 @@ int vvcp_decode(vvcp_stream *s, vvcr_ctx *ctx, const vvcp_decode_params *p);
  * decode indices in output order (out_order[number of pictures]); either may be NULL. Returns the
  * number of output pictures. */
 int vvcp_decode_plan(const vvcp_stream *s, int32_t slot_base, int32_t num_slots, int32_t *slots, int32_t *out_order);
+/* vvcp_decode's prepared-handle release policy simulated on the stream's reference structure (decoding
+ * order, every picture launched after its derivation, every picture assumed to have DMVR sub-blocks):
+ * the largest number of handles alive at once when `keep` are kept beyond the policy. Host only. */
+int vvcp_decode_live_bound(const vvcp_stream *s, int32_t slot_base, int32_t num_slots, int32_t keep);
 
 /* Parsed rows of a picture (after vvcp_parse_picture): copies min(cap, count) entries to dst (dst may be
  * NULL) and returns count. MV fields of vvcr_cu / vvcr_pu hold parsed values until vvcp_derive_motion. */

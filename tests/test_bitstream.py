@@ -83,6 +83,22 @@ def test_native_decode_plan_matches(name):
         assert L.vvcp_decode_plan(s.h, 0, 1, None, None) < 0
 
 
+def test_decode_releases_handles_of_pictures_never_collocated():
+    """vvcp_decode's handle release: a referenced picture with DMVR sub-blocks that no later
+    picture uses as its collocated picture must not pin every later handle. On the 33-picture stream, with
+    every picture assumed to have DMVR sub-blocks and no handles kept beyond the policy, the live handles
+    stay within the DPB's reference span instead of growing with the stream."""
+    s = parser.Stream(_bin("ra1080l_q32"))
+    L = B._bind(N.lib())
+    n = len(s)
+    assert n > 24
+    for keep in (0, 4, 24):
+        peak = L.vvcp_decode_live_bound(s.h, 0, 16, keep)
+        assert 0 < peak <= keep + 1 + 16, (keep, peak)
+    assert L.vvcp_decode_live_bound(s.h, 0, 16, 0) < n // 2
+    assert L.vvcp_decode_live_bound(s.h, 0, 16, -1) < 0
+
+
 STREAMS = ["ai416_q37", "ailm416_q37", "ra416_q32", "ralm416_q32", "rawp416_q32", "ratile416_q32", "ra412c_q32",
            "ra1080_q32", "ratile1080_q32", "rawp1080_q32", "ra1080l_q32", "aibdpcm416_q32", "radq0416_q32", "rageo480_q32",
            "ra2160_q27", "ra2160_q32", "ra2160n_q27", "ra2160l_q32", "ra2160l_q27", "ralmgeo416_q32"]

@@ -29,6 +29,7 @@ def _bind(L):
                                         C.POINTER(C.c_void_p)]
         L.vvcp_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.vvcp_decode_plan.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
+        L.vvcp_decode_live_bound.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
         _bound = True
     return L
 

@@ -27,7 +27,7 @@ struct DecodePlan {
   int n = 0;
   std::vector<int> poc;
   std::vector<std::vector<int>> refIdx[2];   // decode index of every reference
-  std::vector<int> cvs, slot, lastUse, outOrder, outReady;
+  std::vector<int> cvs, slot, lastUse, lastRef, outOrder, outReady;   // lastRef: last picture referencing it (-1: none)
   std::vector<char> referenced, output;
 
   int find(int j, int p) const {
@@ -63,12 +63,14 @@ struct DecodePlan {
       outReady[outOrder[k]] = (int)m;
     }
     lastUse.resize(n);
+    lastRef.assign(n, -1);
     referenced.assign(n, 0);
     for (int i = 0; i < n; i++) lastUse[i] = std::max(i, outReady[i]);
     for (int j = 0; j < n; j++)
       for (int l = 0; l < 2; l++)
         for (int src : refIdx[l][j]) {
           lastUse[src] = std::max(lastUse[src], j);
+          lastRef[src] = std::max(lastRef[src], j);
           referenced[src] = 1;
         }
     std::vector<int> freeSlots, held;
@@ -86,6 +88,28 @@ struct DecodePlan {
     }
   }
 };
+
+// Which launched pictures' prepared handles (device arenas, pinned staging) may be released. A handle is
+// kept only while a later picture may still read its DMVR deltas as a collocated picture: until its
+// refined motion has been recorded, or until every picture that references it has been derived (its last
+// referencing picture lastRef < nderived). `keep` handles stay alive beyond that (recently launched ones
+// are cheap to hold). The decode loop and vvcp_decode_live_bound (the CPU test of this policy) share it.
+struct LiveHandles {
+  std::vector<int> live;   // launched, not released, in launch order
+  template <class Drop>
+  void trim(const DecodePlan &P, const std::vector<char> &refined, int nderived, size_t keep, Drop &&drop) {
+    for (size_t k = 0; k < live.size() && live.size() > keep;) {
+      const int i = live[k];
+      if (refined[i] || P.lastRef[i] < nderived) {
+        drop(i);
+        live.erase(live.begin() + k);
+      } else {
+        k++;
+      }
+    }
+  }
+};
+constexpr size_t KEEP_HANDLES = 24;
 
 struct VvcrFail : std::runtime_error {
   using std::runtime_error::runtime_error;
@@ -148,7 +172,8 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
   std::string failure;            // first error of a worker (the decode then stops)
   int failCode = VVCR_OK;
   double T[VVCP_DECODE_PHASES] = {0};
-  std::vector<int> live;
+  LiveHandles live;
+  int nderived = 0;               // pictures whose motion is derived (decode order)
   size_t outPos = 0;
   DecodePlan P;
   vvcr_seq_params sp{};
@@ -189,12 +214,9 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
         nextLaunch = i + 1;
         T[VVCP_PHASE_LAUNCH] += tl;
         T[VVCP_PHASE_OUTPUT] += to;
-        live.push_back(i);
-        if (!prm->handles_out)   // pictures far behind whose deltas are no longer needed
-          while (live.size() > 24 && refined[live.front()]) {
-            drop.push_back(live.front());
-            live.erase(live.begin());
-          }
+        live.live.push_back(i);
+        if (!prm->handles_out)   // pictures whose deltas no later derivation can read
+          live.trim(P, refined, nderived, KEEP_HANDLES, [&](int k) { drop.push_back(k); });
         cv.notify_all();
       }
       for (int k : drop) vvcr_release_picture(ctx, handle[k]);
@@ -315,6 +337,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
       std::lock_guard<std::mutex> g(mu);
       ndmvr[i] = (int32_t)nd;
       if (now) refined[i] = 1;
+      nderived = i + 1;
       planQ.push_back(i);
       cv.notify_all();
     }
@@ -343,7 +366,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
     rc = failCode;
   }
   if (rc != VVCR_OK || !prm->handles_out) {
-    for (int i : live) vvcr_release_picture(ctx, handle[i]);
+    for (int i : live.live) vvcr_release_picture(ctx, handle[i]);
     for (int i = 0; i < n; i++)   // prepared, never launched
       if (prepared[i] && !launched[i]) vvcr_release_picture(ctx, handle[i]);
   }
@@ -363,6 +386,32 @@ extern "C" int vvcp_decode_plan(const vvcp_stream *h, int32_t slot_base, int32_t
     if (out_order)
       for (size_t k = 0; k < P.outOrder.size(); k++) out_order[k] = P.outOrder[k];
     return (int)P.outOrder.size();
+  } catch (const std::exception &e) {
+    vvcp::set_api_error(e.what());
+    return VVCR_E_UNSUPPORTED;
+  }
+}
+
+// The handle-release policy of vvcp_decode on a stream's reference structure, simulated in decoding order
+// with each picture launched right after its derivation and the worst case for refinement: every picture
+// has DMVR sub-blocks, so only a collocated read records its refined motion. Returns the largest number of
+// live handles (launched, not released) with `keep` handles kept; a CPU test bounds it.
+extern "C" int vvcp_decode_live_bound(const vvcp_stream *h, int32_t slot_base, int32_t num_slots, int32_t keep) {
+  if (!h || num_slots <= 0 || slot_base < 0 || keep < 0) return VVCR_E_ARG;
+  try {
+    DecodePlan P;
+    P.build(h->s, slot_base, num_slots);
+    std::vector<char> refined(P.n, 0);
+    LiveHandles live;
+    size_t peak = 0;
+    for (int i = 0; i < P.n; i++) {
+      for (int j : collocated(*h->s.pics[i], P, i)) refined[j] = 1;
+      if (!P.referenced[i]) refined[i] = 1;
+      live.live.push_back(i);
+      peak = std::max(peak, live.live.size());
+      live.trim(P, refined, i + 1, (size_t)keep, [](int) {});
+    }
+    return (int)peak;
   } catch (const std::exception &e) {
     vvcp::set_api_error(e.what());
     return VVCR_E_UNSUPPORTED;
