@@ -171,9 +171,11 @@ def cpu_baseline_all_cores(stream_bin, pixels_per_run, procs, runs_each=2):
 
 
 class _Roctx:
-    """rocprofv3 --selected-regions: the trace collects only between roctxProfilerResume(0) and
-    roctxProfilerPause(0), so a profile of bench.py covers exactly the kernel-table steps. Enabled by
-    VVCR_ROCTX_REGIONS=1 (no-op otherwise)."""
+    """Bracketing of the kernel-table steps for a rocprofv3 kernel trace of the same command:
+    * VVCR_ROCTX_REGIONS=1: roctxProfilerResume(0) / roctxProfilerPause(0) (rocprofv3 --selected-regions
+      collects only between them);
+    * VVCR_TRACE_MARKERS=1: a one-block torch cumsum kernel on the device right before and right after the
+      steps (host-synchronised), so tools/kt_trace.py can cut the steps' launches out of any kernel trace."""
     L = None
 
     @classmethod
@@ -183,8 +185,16 @@ class _Roctx:
             cls.L = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
         return cls.L
 
+    @staticmethod
+    def _marker():
+        if os.environ.get("VVCR_TRACE_MARKERS") == "1":
+            torch.cuda.synchronize()
+            torch.arange(8, device="cuda").cumsum(0)
+            torch.cuda.synchronize()
+
     @classmethod
     def resume(cls):
+        cls._marker()
         if cls._lib() is not None:
             cls.L.roctxProfilerResume(0)
 
@@ -192,9 +202,10 @@ class _Roctx:
     def pause(cls):
         if cls._lib() is not None:
             cls.L.roctxProfilerPause(0)
+        cls._marker()
 
 
-def kernel_table(ctx, handles, reps):
+def kernel_table(ctx, handles, reps, sync="picture"):
     """Per-kernel HIP-event durations (events on the library's lanes, vvcr_kernel_stats) of one decode's
     resident pictures: `reps` steps, each launching every picture with a host sync after it (no kernel
     overlaps another picture's), summed per kernel and step; the table keeps the MEDIAN step's time per
@@ -207,7 +218,9 @@ def kernel_table(ctx, handles, reps):
     for _ in range(max(1, reps)):
         for hnd in handles:
             ctx.launch(hnd)
-            ctx.sync()
+            if sync == "picture":
+                ctx.sync()
+        ctx.sync()
         rep = {}
         for hnd in handles:
             for name, launches, ms, alg in ctx.kernel_stats(hnd):
@@ -254,7 +267,7 @@ def mc_roofline(kern, note):
     return out
 
 
-def north_star_mc(ctx, stream, per, reps):
+def north_star_mc(ctx, stream, per, reps, sync="picture"):
     """north_star's MC target is quoted on 4K RA QP32: the same kernel table on that stream."""
     p = os.path.join(ROOT, "tests", "golden", "streams", stream + ".bin")
     if not os.path.exists(p):
@@ -263,7 +276,7 @@ def north_star_mc(ctx, stream, per, reps):
         data = f.read()
     handles, slots = resident_handles(ctx, data, per)
     meta = S.load_meta(os.path.join(ROOT, "tests", "golden", stream))
-    kern = kernel_table(ctx, handles, reps)
+    kern = kernel_table(ctx, handles, reps, sync)
     ok = check_slots(ctx, {slot: poc for poc, slot in slots}, meta)
     for h in handles:
         ctx.release(h)
@@ -430,6 +443,8 @@ def main():
     ap.add_argument("--kernel-table-only", action="store_true",
                     help="profiling: only the kernel table of --stream and of --north-star-stream (with "
                          "VVCR_ROCTX_REGIONS=1 under rocprofv3 --selected-regions the trace holds exactly those steps)")
+    ap.add_argument("--kernel-table-sync", choices=("picture", "step"), default="picture",
+                    help="host sync after every picture of a kernel-table step, or only after the step")
     ap.add_argument("--north-star-stream", default="ra2160l_q32",
                     help="north_star's MC target stream (4K RA QP32): its MC kernel table goes into `north_star_mc`")
     ap.add_argument("--sync-pictures", action="store_true",
@@ -477,17 +492,17 @@ def main():
     if a.kernel_table_only:
         ctx.set_timing(False)
         handles, slots = resident_handles(ctx, data, per)
-        kern = kernel_table(ctx, handles, a.kernel_table_reps)
+        kern = kernel_table(ctx, handles, a.kernel_table_reps, a.kernel_table_sync)
         ok = check_slots(ctx, {slot: poc for poc, slot in slots}, meta)
         for h in handles:
             ctx.release(h)
-        out = {"stream": a.stream, "reps": a.kernel_table_reps, "bitexact_vs_reference": bool(ok),
+        out = {"stream": a.stream, "reps": a.kernel_table_reps, "sync": a.kernel_table_sync, "bitexact_vs_reference": bool(ok),
                "mc_roofline": mc_roofline(kern, "median of %d synced steps" % a.kernel_table_reps),
                "kernels": {k: {"us_per_launch": round(v[1] / max(v[0], 1) * 1e3, 2), "launches_per_step": v[0],
                                "ms_per_step": round(v[1], 4), "ms_min_max": [round(v[3], 4), round(v[4], 4)],
                                "alg_MB_per_launch": round(v[2] / max(v[0], 1) / 1e6, 3)} for k, v in kern.items()}}
         if a.north_star_stream and a.north_star_stream != a.stream:
-            out["north_star_mc"] = north_star_mc(ctx, a.north_star_stream, per, a.kernel_table_reps)
+            out["north_star_mc"] = north_star_mc(ctx, a.north_star_stream, per, a.kernel_table_reps, a.kernel_table_sync)
         ctx.close()
         print(json.dumps(out))
         R.close()
@@ -586,7 +601,7 @@ def main():
         s_el = (time.perf_counter() - s0) / max(1, a.resident_steps // 2)
         # per-kernel HIP events: the kernel table and roofline (kernel_table: one segment, a host sync after
         # every picture, the median step of --kernel-table-reps)
-        kern.update(kernel_table(ctx, copies[nstep[0] % a.segments][0], a.kernel_table_reps))
+        kern.update(kernel_table(ctx, copies[nstep[0] % a.segments][0], a.kernel_table_reps, a.kernel_table_sync))
         for handles, _ in copies:
             for hnd in handles:
                 ctx.release(hnd)
@@ -621,7 +636,7 @@ def main():
                           % a.kernel_table_reps)
     ns_mc = None
     if a.resident_steps > 0 and a.north_star_stream and a.north_star_stream != a.stream:
-        ns_mc = north_star_mc(ctx, a.north_star_stream, per, a.kernel_table_reps)
+        ns_mc = north_star_mc(ctx, a.north_star_stream, per, a.kernel_table_reps, a.kernel_table_sync)
         bitexact = bitexact and (ns_mc is None or ns_mc["bitexact_vs_reference"])
 
     ms_step = elapsed / a.steps * 1e3

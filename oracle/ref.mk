@@ -43,7 +43,7 @@ ENCAPP_OBJ = $(call obj,$(ENCAPP_SRC))
 WRAPS = $(shell cat $(CURDIR)/oracle/capture/wraps.txt 2>/dev/null)
 WRAPFLAGS = $(foreach s,$(WRAPS),-Wl,--wrap=$(s))
 
-all: apps capture rdo_kat mc_kat $(if $(wildcard $(CURDIR)/vvc_amd/libvvcr.so),dropin)
+all: apps capture rdo_kat mc_kat $(if $(wildcard $(CURDIR)/vvc_amd/libvvcr.so),dropin encdropin)
 
 # syntax-trace decoder (the reference's own ENABLE_TRACING / DTRACE build, TypeDef.h) for debugging the
 # host parser element by element: make -f oracle/ref.mk trace  ->  oracle/_ref/trace/DecoderApp
@@ -84,6 +84,18 @@ $(OUT)/vtm_vvcr: $(OUT)/obj/capture/vtm_vvcr.o $(CAPAPP_OBJ) $(DEC_OBJ) $(COMMON
 	$(CXX) -pthread -o $@ $(OUT)/obj/capture/vtm_vvcr.o $(CAPAPP_OBJ) $(DEC_OBJ) $(UTIL_OBJ) $(COMMON_OBJ) $(WRAPFLAGS) \
 	  -L$(CURDIR)/vvc_amd -lvvcr -Wl,-rpath,'$$ORIGIN/../../vvc_amd' -Wl,-rpath-link,/opt/rocm/lib
 
+# EncoderApp drop-in: the reference EncoderApp / EncoderLib, unchanged, linked against
+# libvvcr.so; the merge pass's Hadamard SATD goes through vvcr_rd_dist (oracle/capture/enc_vvcr.cpp).
+# -rdynamic: the binding resolves the call site of RdCost::setDistParam with dladdr.
+ENC_WRAP = -Wl,--wrap=_ZN6RdCost12setDistParamER9DistParamRK7AreaBufIKsES6_i11ComponentIDb
+encdropin: $(OUT)/vtm_enc_vvcr
+$(OUT)/obj/capture/enc_vvcr.o: $(CURDIR)/oracle/capture/enc_vvcr.cpp $(CURDIR)/include/vvcr.h
+	@mkdir -p $(@D); $(CXX) $(CXXFLAGS) -I$(CURDIR)/include -c $< -o $@
+$(OUT)/vtm_enc_vvcr: $(OUT)/obj/capture/enc_vvcr.o $(ENCAPP_OBJ) $(OUT)/libEncoderLib.a $(OUT)/libDecoderLib.a $(OUT)/libCommonLib.a $(OUT)/libUtilities.a $(CURDIR)/vvc_amd/libvvcr.so
+	$(CXX) -pthread -rdynamic -o $@ $(OUT)/obj/capture/enc_vvcr.o $(ENCAPP_OBJ) $(OUT)/libEncoderLib.a $(OUT)/libDecoderLib.a \
+	  $(OUT)/libUtilities.a $(OUT)/libCommonLib.a $(ENC_WRAP) -ldl \
+	  -L$(CURDIR)/vvc_amd -lvvcr -Wl,-rpath,'$$ORIGIN/../../vvc_amd' -Wl,-rpath-link,/opt/rocm/lib
+
 # RDO known-answer harness (RdCost distortion + forward transforms of the reference, oracle/capture/rdo_kat.cpp)
 rdo_kat: $(OUT)/rdo_kat
 $(OUT)/obj/capture/rdo_kat.o: $(CURDIR)/oracle/capture/rdo_kat.cpp
@@ -112,4 +124,4 @@ $(OUT)/obj/%.o: $(SRC)/%.cpp
 clean:
 	rm -rf $(OUT)
 
-.PHONY: all apps capture dropin clean
+.PHONY: all apps capture dropin encdropin clean

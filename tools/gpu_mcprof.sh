@@ -1,8 +1,9 @@
 #!/bin/bash
-# k_mc / k_mc_affine / k_mc_bidir per-dispatch durations (rocprofv3 kernel trace) of tools/mc_bench.py.
-# Usage: bash tools/gpu_mcprof.sh STREAM TAG
-S=${1:-ra2160l_q27}; TAG=${2:-a}
+# Per-wave timestamps of k_mc (VVCR_MC_PROF build, tools/mc_prof.py build) on the 4K QP32 / QP27 B pictures.
+set -o pipefail
+TAG=${1:-mcprof}
 export TMPDIR=/tmp
-O=gpurun_out/mcprof_$TAG
-mkdir -p $O
-timeout -k 10 150 rocprofv3 --kernel-trace --stats -f csv -d $O -o run -- python3 -u tools/mc_bench.py --stream $S --reps 3 > $O/mcb.json 2> $O/err.log
+mkdir -p gpurun_out
+for S in ${STREAMS:-ra2160l_q32 ra2160l_q27}; do
+  timeout -k 10 240 python -u tools/mc_prof.py run $S > gpurun_out/${TAG}_$S.txt 2>&1 || exit 1
+done

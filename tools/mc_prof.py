@@ -88,6 +88,17 @@ def run(stream):
                     "luma" if isl else "chroma", m.sum(), np.median(dur[m]), np.percentile(dur[m], 90),
                     np.median(dur[m & (nbi == 64)]) if (m & (nbi == 64)).any() else -1,
                     np.median(dur[m & (nbi == 0) & (nact == 64)]) if (m & (nbi == 0) & (nact == 64)).any() else -1))
+        cls = {}
+        for k in range(len(b)):
+            key = ("L" if lum[k] else "C") + "%dx%d" % (cw[k], chh[k])
+            c = cls.setdefault(key, [0, 0.0, 0])
+            c[0] += 1
+            c[1] += dur[k]
+            c[2] += nact[k]
+        tot = dur.sum()
+        print("   wave-time by class (waves, share of wave-us, median us, active lanes/wave):",
+              ", ".join("%s %d %.0f%% %.1f %.0f" % (key, c[0], 100 * c[1] / tot, c[1] / c[0], c[2] / c[0])
+                        for key, c in sorted(cls.items(), key=lambda kv: -kv[1][1])))
         hist = np.histogram(start, bins=8, range=(0, span))[0]
         print("   wave starts per eighth of the span:", list(hist))
         ctx.release(h)
