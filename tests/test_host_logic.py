@@ -158,7 +158,7 @@ def test_deblocking_plan_independent_of_worker_count(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = []
     for t in ("1", "3", "8"):
-        env = dict(os.environ, VVCR_DBK_THREADS=t)
+        env = dict(os.environ, VVCR_DBK_THREADS=t, VVCR_DBK_GPU="0")
         r = subprocess.run([sys.executable, str(script), root, "ra1080_q32", "ralm416_q32"], env=env, capture_output=True,
                            text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-2000:]

@@ -129,10 +129,11 @@ DPlane alloc_plane(int w, int h) {
 }
 
 // kernel groups timed with HIP events (vvcr_kernel_stats)
-enum { K_RESID, K_MC, K_MC_BIDIR, K_MC_AFFINE, K_RECON, K_INTRA, K_DBK, K_SAO, K_ALF, NK };
-const char *const kKernelNames[NK] = {"resid", "mc", "mc_bidir", "mc_affine", "recon_inter", "intra", "deblock", "sao", "alf"};
+enum { K_RESID, K_MC, K_MC_BIDIR, K_MC_AFFINE, K_RECON, K_INTRA, K_DBK, K_SAO, K_ALF, K_DBKP, NK };
+const char *const kKernelNames[NK] = {"resid", "mc", "mc_bidir", "mc_affine", "recon_inter", "intra", "deblock", "sao", "alf",
+                                      "deblock_plan"};
 // stage of each kernel group (bit index in VVCR_STAGE_*)
-const int kKernelStage[NK] = {0, 1, 1, 1, 2, 2, 4, 5, 6};
+const int kKernelStage[NK] = {0, 1, 1, 1, 2, 2, 4, 5, 6, 4};
 
 struct Prepared {
   vvcr_pic_params pp{};
@@ -150,6 +151,14 @@ struct Prepared {
   int n_ijobs = 0, n_ictu = 0;
   DevVec<DbkSeg> dbk;
   int dbk_counts[4] = {0, 0, 0, 0};
+  DevVec<int32_t> dbk_cnt;           // the host plan's list lengths, device copy (k_dbk reads them there)
+  // device deblocking planning (vvcr_dbk_plan.hip): compact descriptors and the 4x4 motion field
+  bool dbk_gpu = false, dbk_chroma_pass = false;
+  DevVec<DbCu> dbcu;
+  DevVec<DbPu> dbpu;
+  DevVec<DbTu> dbtu;
+  DevVec<MotionRec> dbmot;
+  int n_dbcu = 0, n_dbtu = 0;
   DevVec<int32_t> sao;
   DevVec<int16_t> alf_luma_coef, alf_luma_clip, alf_chroma, alf_cc, alf_set;
   DevVec<uint8_t> alf_ctb;
@@ -201,6 +210,8 @@ struct Prepared {
     mask = 0;
     n_ijobs = n_ictu = 0;
     for (int &c : dbk_counts) c = 0;
+    dbk_gpu = dbk_chroma_pass = false;
+    n_dbcu = n_dbtu = 0;
     have_sao = have_alf = false;
     n_tb = n_tb_small = n_mctile = n_basic = n_bidir = n_aff = n_tiles = n_dmvr = 0;
     zero_filled = false;
@@ -260,7 +271,16 @@ struct vvcr_picture {
   WorkLists wl;
   IntraPlan intra;
   DbkLists dbk;
+  bool dbk_gpu = false;              // the edges are planned on the device from dbkg (default; VVCR_DBK_GPU=0: host)
+  DbkGpuInputs dbkg;
 };
+
+// deblocking planned on the device (vvcr_dbk_plan.hip) unless VVCR_DBK_GPU=0 (the host planner,
+// vvcr_dbk_host.cpp: same lists, kept for A/B and as the parity reference of the device planner)
+static bool dbk_on_device() {
+  const char *e = getenv("VVCR_DBK_GPU");
+  return !(e && e[0] == '0');
+}
 
 // Hadamard tile of RdCost::xGetHADs for a w x h block (RdCost.cpp:2818-2911), or -1 for odd sizes
 static int rd_kind(int w, int h, int &tw, int &th) {
@@ -284,6 +304,7 @@ constexpr int MAXLANE = 16;
 struct Lane {
   hipStream_t s = nullptr;
   DPlane pred[3], resi[3], tmp[3];
+  DevVec<uint8_t> dbkp;              // device deblocking planner's maps and lists (allocated at its first use)
   int tail_slot = -1;                // DPB slot written by the lane's last picture
   uint64_t tail_seq = 0;             // launch sequence number of that picture
 };
@@ -333,6 +354,21 @@ struct vvcr_ctx {
   std::vector<std::unique_ptr<struct RdoPlan>> rdo;   // encoder RDO plans (vvcr_rd_plan / vvcr_fwd_plan)
   int32_t *d_err = nullptr;          // device error flag of the persistent intra kernel (checked by vvcr_sync)
 };
+
+// The device error words (after the lanes are idle): [0] the persistent intra kernel's dependency-wait
+// timeout (its waits poll this word and give up when it is set), [1] the device deblocking planner
+// (bit 2: a position no CU / TU covers, bit 4: list overflow) — a word of its own, so that it never
+// cuts the intra waits of other pictures short.
+static void check_device_errors(vvcr_ctx *ctx) {
+  int32_t e[2] = {0, 0};
+  VVCR_CHECK_HIP(hipMemcpy(e, ctx->d_err, sizeof e, hipMemcpyDeviceToHost));
+  if (e[0] | e[1]) {
+    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof e));
+    if (e[0]) throw VvcrError(VVCR_E_STATE, "intra reconstruction: a step's dependency wait timed out (output invalid)");
+    if (e[1] & 2) throw VvcrError(VVCR_E_STATE, "deblocking planner: no CU / TU covers a neighbouring position (inconsistent descriptors)");
+    throw VvcrError(VVCR_E_STATE, "deblocking planner: segment list overflow");
+  }
+}
 
 // every lane idle (host reads / writes of planes, vvcr_sync)
 static void sync_lanes(vvcr_ctx *ctx) {
@@ -421,6 +457,8 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
   b.wl.clear();
   b.intra.clear();
   b.dbk.clear();
+  b.dbkg.clear();
+  b.dbk_gpu = (mask & VVCR_STAGE_DBK) && dbk_on_device();
   if (pp.lmcs_enabled && sp.bit_depth != 10) throw VvcrError(VVCR_E_UNSUPPORTED, "LMCS tables are captured for 10-bit luma");
   // With the residual, inter and intra stages together, plain inter CUs are reconstructed by k_mc (the
   // prediction plus the residual straight into the picture, fused_inter_cu); a subset of those stages
@@ -431,7 +469,11 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
   // second thread beside the work lists and the intra plan (a 4K intra picture plans in ~100 ms each).
   std::exception_ptr dbk_err;
   std::thread dbk_thread;
-  if (mask & VVCR_STAGE_DBK)
+  if ((mask & VVCR_STAGE_DBK) && b.dbk_gpu) {
+    if (b.desc.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4))
+      throw VvcrError(VVCR_E_ARG, "deblocking: the motion field does not cover the picture");
+    pack_dbk_inputs(sp, pp, b.desc, b.dbkg);
+  } else if (mask & VVCR_STAGE_DBK)
     dbk_thread = std::thread([&] {
       try {
         plan_deblocking(sp, pp, b.desc, b.dbk);
@@ -563,11 +605,27 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     }
     r.alg_bytes[K_INTRA] = b;
   }
-  if (mask & VVCR_STAGE_DBK) {
+  if ((mask & VVCR_STAGE_DBK) && bp.dbk_gpu) {
+    r.dbk_gpu = true;
+    r.dbk_chroma_pass = bp.dbkg.chroma_pass;
+    r.n_dbcu = (int)bp.dbkg.cu.size();
+    r.n_dbtu = (int)bp.dbkg.tu.size();
+    if (r.n_dbcu > 0) {
+      st.add(r.dbcu, bp.dbkg.cu);
+      st.add(r.dbpu, bp.dbkg.pu);
+      st.add(r.dbtu, bp.dbkg.tu);
+      st.add(r.dbmot, bp.desc.motion.data(), bp.desc.motion.size());
+    }
+    r.alg_bytes[K_DBK] = pix * 2 * 2;
+    // the planner reads the records and the motion field once
+    r.alg_bytes[K_DBKP] = (double)r.n_dbcu * sizeof(DbCu) + (double)bp.dbkg.pu.size() * sizeof(DbPu) +
+                          (double)r.n_dbtu * sizeof(DbTu) + (double)bp.desc.motion.size() * sizeof(MotionRec);
+  } else if (mask & VVCR_STAGE_DBK) {
     const bigbuf::vec<DbkSeg> *parts[4] = {&bp.dbk.luma[0], &bp.dbk.chroma[0], &bp.dbk.luma[1], &bp.dbk.chroma[1]};
     for (int k = 0; k < 4; k++) r.dbk_counts[k] = (int)parts[k]->size();
     st.add(r.dbk, {{parts[0]->data(), parts[0]->size()}, {parts[1]->data(), parts[1]->size()},
                    {parts[2]->data(), parts[2]->size()}, {parts[3]->data(), parts[3]->size()}});
+    st.add(r.dbk_cnt, r.dbk_counts, 4);
     r.alg_bytes[K_DBK] = pix * 2 * 2;
   }
   const bool saoOn = pp.sao_luma || pp.sao_chroma;
@@ -592,6 +650,51 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     for (int l = 0; l < MAXLANE; l++) st.host_at<IntraParams>(iparams_off)[l] = make_intra_params(ctx, r, l);
   st.copy(ctx->upload_stream, r.up_done);
   r.up_issued = true;
+}
+
+// The device deblocking planner's arguments for a prepared picture on a lane: the lane's maps and lists
+// (allocated at its first use; its pictures run one after the other, so one set serves them all).
+static DbkPlanArgs dbk_plan_args(vvcr_ctx *ctx, Lane &ln, const Prepared &r) {
+  const vvcr_seq_params &sp = ctx->sp;
+  const vvcr_pic_params &pp = r.pp;
+  const int W4 = sp.width / 4, H4 = sp.height / 4;
+  const size_t n4 = (size_t)W4 * H4, a4 = (n4 + 255) & ~(size_t)255;
+  const size_t maps = 4 * a4 * sizeof(int32_t), scratch = 18 * a4, dense = 4 * a4 * sizeof(uint32_t);
+  const size_t lists = 4 * a4 * sizeof(DbkSeg);
+  ln.dbkp.ensure(maps + scratch + dense + lists + 256);
+  uint8_t *p = ln.dbkp.p;
+  DbkPlanArgs a{};
+  a.cu = r.dbcu.p; a.pu = r.dbpu.p; a.tu = r.dbtu.p; a.motion = r.dbmot.p;
+  a.ncu = r.n_dbcu; a.ntu = r.n_dbtu; a.W4 = W4; a.H4 = H4; a.ctu_log2 = sp.ctu_log2;
+  a.slice_type = pp.slice_type; a.dual_tree = pp.dual_tree; a.dbk_disable = pp.dbk_disable;
+  std::memcpy(a.ref_poc, pp.ref_poc, sizeof a.ref_poc);
+  a.shard = pp.shard_y1 > 0;
+  a.ly0 = pp.shard_y0 - VVCR_LF_HALO; a.ly1 = pp.shard_y1 + VVCR_LF_HALO;
+  a.chroma_pass = r.dbk_chroma_pass;
+  for (int k = 0; k < 2; k++) {
+    a.cu_map[k] = (int32_t *)p + k * a4;
+    a.tu_map[k] = (int32_t *)p + (2 + k) * a4;
+  }
+  uint8_t *q = p + maps;
+  a.scratch0 = q;
+  a.scratch_bytes = scratch;
+  for (int d = 0; d < 2; d++) {
+    a.bs[d] = q + (0 + d) * a4;
+    a.edge[d] = q + (2 + d) * a4;
+    a.tedge[d] = q + (4 + d) * a4;
+    for (int c = 0; c < 3; c++) {
+      a.lenP[d][c] = q + (6 + 3 * d + c) * a4;
+      a.lenQ[d][c] = q + (12 + 3 * d + c) * a4;
+    }
+  }
+  uint32_t *w = (uint32_t *)(q + scratch);
+  a.dense_bytes = dense;
+  a.segL[0] = w; a.segC[0] = w + a4; a.segL[1] = w + 2 * a4; a.segC[1] = w + 3 * a4;
+  a.out = (DbkSeg *)(q + scratch + dense);
+  a.cap = (int32_t)a4;
+  a.counts = (int32_t *)(q + scratch + dense + lists);
+  a.err = ctx->d_err + 1;
+  return a;
 }
 
 // Device phase: enqueue the kernels of a prepared picture on the context stream.
@@ -714,15 +817,38 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
     launch_lmcs_inverse(A[0], r.lmcs_lut.p + 1024, own0, own1, s);   // back to the original domain before the loop filters
     VVCR_CHECK_HIP(hipGetLastError());
   }
-  if ((mask & VVCR_STAGE_DBK) && (r.dbk_counts[0] + r.dbk_counts[1] + r.dbk_counts[2] + r.dbk_counts[3])) {
-    KernelTimer t(r, K_DBK, s, ctx->timing);
+  if ((mask & VVCR_STAGE_DBK) && (r.dbk_gpu ? r.n_dbcu > 0 : (r.dbk_counts[0] + r.dbk_counts[1] + r.dbk_counts[2] + r.dbk_counts[3]) > 0)) {
     DbkParams dp{};
     for (int c = 0; c < 3; c++) dp.pl[c] = A[c];
     dp.bd = ctx->sp.bit_depth;
     dp.beta_offset_div2 = pp.dbk_beta_offset_div2;
     dp.tc_offset_div2 = pp.dbk_tc_offset_div2;
-    launch_dbk(dp, r.dbk.p, r.dbk_counts, s);
-    r.launches[K_DBK] = (r.dbk_counts[0] + r.dbk_counts[1] > 0) + (r.dbk_counts[2] + r.dbk_counts[3] > 0);
+    if (r.dbk_gpu) {
+      DbkPlanArgs a;
+      {
+        KernelTimer t(r, K_DBKP, s, ctx->timing);
+        a = dbk_plan_args(ctx, ln, r);
+        launch_dbk_plan(a, s);
+        r.launches[K_DBKP] = 1;
+      }
+      KernelTimer t(r, K_DBK, s, ctx->timing);
+      const DbkSeg *segs[2][2] = {{a.out, a.out + a.cap}, {a.out + 2 * (size_t)a.cap, a.out + 3 * (size_t)a.cap}};
+      // workgroups per list: at most one segment per 4x4 unit (64 per workgroup and pass), capped (they loop)
+      const int gmax = std::min(1024, (a.cap + 63) / 64), g[2][2] = {{gmax, gmax}, {gmax, gmax}};
+      launch_dbk(dp, segs, a.counts, g, s);
+      r.launches[K_DBK] = 2;
+    } else {
+      KernelTimer t(r, K_DBK, s, ctx->timing);
+      const DbkSeg *segs[2][2] = {{r.dbk.p, r.dbk.p + r.dbk_counts[0]},
+                                  {r.dbk.p + r.dbk_counts[0] + r.dbk_counts[1], r.dbk.p + r.dbk_counts[0] + r.dbk_counts[1] + r.dbk_counts[2]}};
+      int g[2][2];
+      for (int d = 0; d < 2; d++)
+        for (int k = 0; k < 2; k++) g[d][k] = (r.dbk_counts[2 * d + k] + 63) / 64;
+      for (int d = 0; d < 2; d++)
+        if (g[d][0] + g[d][1]) { g[d][0] = std::max(1, g[d][0]); g[d][1] = std::max(1, g[d][1]); }
+      launch_dbk(dp, segs, r.dbk_cnt.p, g, s);
+      r.launches[K_DBK] = (r.dbk_counts[0] + r.dbk_counts[1] > 0) + (r.dbk_counts[2] + r.dbk_counts[3] > 0);
+    }
   }
   // SAO (slot -> tmp) and ALF (ping-pong back); the final picture always ends in the slot
   const int ctu = 1 << ctx->sp.ctu_log2;
@@ -858,8 +984,8 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       const int ctu = 1 << sp->ctu_log2, wc = (sp->width + ctu - 1) / ctu, hc = (sp->height + ctu - 1) / ctu;
       ctx->intra_wg = std::min(ctx->n_cu, 4 * std::min(hc, (wc + 1) / 2));
     }
-    VVCR_CHECK_HIP(hipMalloc(&ctx->d_err, sizeof(int32_t)));
-    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof(int32_t)));
+    VVCR_CHECK_HIP(hipMalloc(&ctx->d_err, 2 * sizeof(int32_t)));
+    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, 2 * sizeof(int32_t)));
     build_scan_tables(ctx->scans);
     ctx->d_scans.upload(ctx->scans.data);
     ctx->prepared.emplace_back(new Prepared());   // scratch record of vvcr_end_picture
@@ -1208,6 +1334,60 @@ extern "C" int vvcr_debug_dbk_segments(const vvcr_picture *pic, void *out, int32
   return n;
 }
 
+// Diagnostics (host only): the lengths of the host-planned deblocking lists (luma VER, chroma VER, luma HOR,
+// chroma HOR) of vvcr_debug_dbk_segments.
+extern "C" int vvcr_debug_dbk_list_sizes(const vvcr_picture *pic, int32_t *out) {
+  if (!pic || !out) return VVCR_E_ARG;
+  if (!pic->planned) return VVCR_E_STATE;
+  out[0] = (int32_t)pic->dbk.luma[0].size(); out[1] = (int32_t)pic->dbk.chroma[0].size();
+  out[2] = (int32_t)pic->dbk.luma[1].size(); out[3] = (int32_t)pic->dbk.chroma[1].size();
+  return 4;
+}
+
+// Diagnostics (tests): the device deblocking planner run on a planned picture (planned with device
+// deblocking, the default): its four segment lists back to back (luma VER, chroma VER, luma HOR, chroma
+// HOR), each sorted by position, as vvcr_debug_dbk_segments gives the host planner's. Synchronous, on lane 0.
+// Returns the number of segments.
+extern "C" int vvcr_debug_dbk_gpu_segments(vvcr_ctx *ctx, const vvcr_picture *pic, void *out, int32_t cap) {
+  if (!ctx || !pic || (!out && cap)) return VVCR_E_ARG;
+  if (!pic->planned || !pic->dbk_gpu) return VVCR_E_STATE;
+  API_BEGIN
+  std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
+  sync_lanes(ctx);
+  Prepared r;
+  r.pp = pic->pp;
+  r.dbk_gpu = true;
+  r.dbk_chroma_pass = pic->dbkg.chroma_pass;
+  r.n_dbcu = (int)pic->dbkg.cu.size();
+  r.n_dbtu = (int)pic->dbkg.tu.size();
+  r.dbcu.upload(pic->dbkg.cu);
+  r.dbpu.upload(pic->dbkg.pu);
+  r.dbtu.upload(pic->dbkg.tu);
+  r.dbmot.upload(pic->desc.motion.data(), pic->desc.motion.size());
+  Lane &ln = ctx->lanes[0];
+  DbkPlanArgs a = dbk_plan_args(ctx, ln, r);
+  int32_t cnt[4] = {0, 0, 0, 0};
+  if (r.n_dbcu > 0) {
+    launch_dbk_plan(a, ln.s);
+    VVCR_CHECK_HIP(hipStreamSynchronize(ln.s));
+    check_device_errors(ctx);
+    VVCR_CHECK_HIP(hipMemcpy(cnt, a.counts, sizeof cnt, hipMemcpyDeviceToHost));
+  }
+  int32_t n = 0;
+  std::vector<DbkSeg> v;
+  for (int k = 0; k < 4; k++) {
+    v.resize(cnt[k]);
+    if (cnt[k]) VVCR_CHECK_HIP(hipMemcpy(v.data(), a.out + (size_t)k * a.cap, cnt[k] * sizeof(DbkSeg), hipMemcpyDeviceToHost));
+    std::sort(v.begin(), v.end(), [](const DbkSeg &x, const DbkSeg &y) { return x.y4 != y.y4 ? x.y4 < y.y4 : x.x4 < y.x4; });
+    for (const DbkSeg &sg : v) {
+      if (n < cap) static_cast<DbkSeg *>(out)[n] = sg;
+      n++;
+    }
+  }
+  return n;
+  API_END
+}
+
 // Diagnostics (host only): the DPB slots the planned inter work lists read, one entry per (job, list) in
 // job order (MC tiles and blocks, bi-directional blocks, affine PUs). Returns the number of entries.
 extern "C" int vvcr_debug_mc_slots(const vvcr_picture *pic, int32_t *out, int32_t cap) {
@@ -1266,12 +1446,7 @@ int vvcr_sync(vvcr_ctx *ctx) {
   API_BEGIN
   std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
   sync_lanes(ctx);
-  int32_t e = 0;
-  VVCR_CHECK_HIP(hipMemcpy(&e, ctx->d_err, sizeof e, hipMemcpyDeviceToHost));
-  if (e) {
-    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof e));
-    throw VvcrError(VVCR_E_STATE, "intra reconstruction: a step's dependency wait timed out (output invalid)");
-  }
+  check_device_errors(ctx);
   return VVCR_OK;
   API_END
 }
@@ -1320,12 +1495,7 @@ int vvcr_read_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, int1
   sync_lanes(ctx);
   VVCR_CHECK_HIP(hipMemcpy2DAsync(dst, dst_stride * 2, p->p, p->stride * 2, p->w * 2, p->h, hipMemcpyDeviceToHost, ctx->stream));
   VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-  int32_t e = 0;
-  VVCR_CHECK_HIP(hipMemcpy(&e, ctx->d_err, sizeof e, hipMemcpyDeviceToHost));
-  if (e) {
-    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof e));
-    throw VvcrError(VVCR_E_STATE, "intra reconstruction: a step's dependency wait timed out (output invalid)");
-  }
+  check_device_errors(ctx);
   return VVCR_OK;
   API_END
 }
@@ -1338,12 +1508,7 @@ int vvcr_write_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t comp, con
   sync_lanes(ctx);
   VVCR_CHECK_HIP(hipMemcpy2DAsync(p->p, p->stride * 2, src, src_stride * 2, p->w * 2, p->h, hipMemcpyHostToDevice, ctx->stream));
   VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-  int32_t e = 0;
-  VVCR_CHECK_HIP(hipMemcpy(&e, ctx->d_err, sizeof e, hipMemcpyDeviceToHost));
-  if (e) {
-    VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof e));
-    throw VvcrError(VVCR_E_STATE, "intra reconstruction: a step's dependency wait timed out (output invalid)");
-  }
+  check_device_errors(ctx);
   return VVCR_OK;
   API_END
 }

@@ -26,5 +26,64 @@ struct DbkParams {
 };
 
 void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkLists &out);
-// segs: device copy of the four lists back to back in the order luma VER, chroma VER, luma HOR, chroma HOR
-void launch_dbk(const DbkParams &p, const DbkSeg *segs, const int counts[4], hipStream_t s);
+
+// Device planning (vvcr_dbk_plan.hip, r05): the same edges planned on the GPU from compact copies of the
+// descriptors (pack_dbk_inputs, host) and the 4x4 motion field.
+struct DbCu {
+  int16_t x, y, w, h, cx, cy, cw, ch;   // luma area; chroma area in chroma samples
+  int32_t firstpu, firsttu;
+  int16_t npu, ntu;
+  int16_t qp;
+  uint16_t flags;                       // DBC_*
+};
+static_assert(sizeof(DbCu) == 32, "DbCu layout");
+enum : uint16_t {
+  DBC_CHTYPE = 1, DBC_INTRA = 2, DBC_BDPCM = 4, DBC_BDPCMC = 8, DBC_AFFINE = 16, DBC_ISP = 32, DBC_TREE = 64,
+  DBC_YVALID = 128, DBC_CVALID = 256, DBC_CIIP = 512   // CIIP: the CU's first PU
+};
+struct DbPu {
+  int16_t x, y, w, h, cx, cy;
+  uint16_t sub;                         // 1: merge with the SbTMVP merge type (sub-block edges)
+  uint16_t pad;
+};
+static_assert(sizeof(DbPu) == 16, "DbPu layout");
+struct DbTu {
+  int16_t b[3][4];                      // per component x, y, w, h
+  int32_t cu;
+  uint8_t cbf;                          // bit c: coded block flag of component c
+  uint8_t jccr;
+  int8_t cqp[2];                        // QpParam(tu, Cb / Cr).Qp(0) - qpBdOffset (the host planner's chroma_qp)
+};
+static_assert(sizeof(DbTu) == 32, "DbTu layout");
+struct DbkGpuInputs {
+  bigbuf::vec<DbCu> cu;
+  bigbuf::vec<DbPu> pu;
+  bigbuf::vec<DbTu> tu;
+  bool chroma_pass = false;             // CUs of the chroma tree (dual tree, or local dual-tree chroma CUs)
+  void clear() { cu.clear(); pu.clear(); tu.clear(); chroma_pass = false; }
+};
+void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkGpuInputs &out);
+
+struct DbkPlanArgs {
+  const DbCu *cu; const DbPu *pu; const DbTu *tu; const MotionRec *motion;
+  int32_t ncu, ntu, W4, H4, ctu_log2;
+  int32_t slice_type, dual_tree, dbk_disable;
+  int32_t ref_poc[2][VVCR_MAX_REF];
+  int32_t shard, ly0, ly1;
+  int32_t pass;                         // 0: luma-tree CUs (chtype 0), 1: chroma-tree CUs
+  int32_t chroma_pass;                  // pass 1 needed
+  // picture-wide scratch on the 4x4 luma grid (chroma 2x2 units: the same grid), per lane
+  int32_t *cu_map[2], *tu_map[2];
+  uint8_t *bs[2], *edge[2], *lenP[2][3], *lenQ[2][3], *tedge[2];
+  uint32_t *segL[2], *segC[2];          // dense segment words (0: none)
+  void *scratch0; size_t scratch_bytes; // bs .. tedge, cleared per pass of a dual-tree picture
+  size_t dense_bytes;                   // segL / segC, right after the scratch
+  DbkSeg *out; int32_t *counts; int32_t cap;   // the four lists at out + k * cap, their lengths
+  int32_t *err;                         // bit 2: a map hole (inconsistent descriptors), bit 4: list overflow
+};
+void launch_dbk_plan(const DbkPlanArgs &a, hipStream_t s);
+
+// Filtering. segL / segC: the luma / chroma lists of direction dir at segs[dir][0 / 1]; counts (device):
+// their lengths [luma VER, chroma VER, luma HOR, chroma HOR]; g[dir][0 / 1]: workgroups per list (64 segments
+// each per pass; the kernels loop while segments remain)
+void launch_dbk(const DbkParams &p, const DbkSeg *const segs[2][2], const int32_t *counts, const int g[2][2], hipStream_t s);

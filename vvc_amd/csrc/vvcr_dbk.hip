@@ -10,6 +10,7 @@
 // reference's sequential CU order.
 #include "vvcr_dbk.h"
 #include "vvcr_gen_tables.h"
+#include <algorithm>
 
 namespace {
 
@@ -241,26 +242,28 @@ __device__ __forceinline__ void dbk_chroma(const DbkParams &P, const DbkSeg *seg
 }
 
 // One launch per direction: the first gL workgroups take the luma segments, the others the chroma ones
-// (the planes are independent; the vertical launch precedes the horizontal one).
+// (the planes are independent; the vertical launch precedes the horizontal one). The list lengths come from
+// device memory (the device planner writes them): each workgroup takes 64 segments per pass and loops
+// while segments remain.
 template <int DIR>
-__global__ __launch_bounds__(256) void k_dbk(DbkParams P, const DbkSeg *segL, int nL, int gL, const DbkSeg *segC, int nC) {
-  if ((int)blockIdx.x < gL) dbk_luma<DIR>(P, segL, nL, blockIdx.x);
-  else dbk_chroma<DIR>(P, segC, nC, blockIdx.x - gL);
+__global__ __launch_bounds__(256) void k_dbk(DbkParams P, const DbkSeg *segL, const DbkSeg *segC, const int32_t *cnt, int gL) {
+  const int nL = cnt[0], nC = cnt[1];
+  if ((int)blockIdx.x < gL) {
+    for (int b = blockIdx.x; b * 64 < nL; b += gL) dbk_luma<DIR>(P, segL, nL, b);
+  } else {
+    const int gC = (int)gridDim.x - gL;
+    for (int b = (int)blockIdx.x - gL; b * 64 < nC; b += gC) dbk_chroma<DIR>(P, segC, nC, b);
+  }
 }
 
 }  // namespace
 
-void launch_dbk(const DbkParams &p, const DbkSeg *segs, const int counts[4], hipStream_t s) {
-  const int T = 256;   // four lanes per segment
-  int off = 0;
+void launch_dbk(const DbkParams &p, const DbkSeg *const segs[2][2], const int32_t *counts, const int g[2][2], hipStream_t s) {
   for (int dir = 0; dir < 2; dir++) {
-    const int nL = counts[2 * dir], nC = counts[2 * dir + 1];
-    const DbkSeg *sL = segs + off, *sC = segs + off + nL;
-    off += nL + nC;
-    if (nL + nC == 0) continue;
-    const int gL = (4 * nL + T - 1) / T, gC = (4 * nC + T - 1) / T;
-    if (dir == 0) hipLaunchKernelGGL(k_dbk<0>, dim3(gL + gC), dim3(T), 0, s, p, sL, nL, gL, sC, nC);
-    else hipLaunchKernelGGL(k_dbk<1>, dim3(gL + gC), dim3(T), 0, s, p, sL, nL, gL, sC, nC);
+    const int gL = std::max(1, g[dir][0]), gC = std::max(1, g[dir][1]);
+    if (g[dir][0] + g[dir][1] == 0) continue;
+    if (dir == 0) hipLaunchKernelGGL(k_dbk<0>, dim3(gL + gC), dim3(256), 0, s, p, segs[0][0], segs[0][1], counts, gL);
+    else hipLaunchKernelGGL(k_dbk<1>, dim3(gL + gC), dim3(256), 0, s, p, segs[1][0], segs[1][1], counts + 2, gL);
     VVCR_CHECK_HIP(hipGetLastError());
   }
 }

@@ -540,3 +540,65 @@ void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const
       out.chroma[dir].insert(out.chroma[dir].end(), part[t].chroma[dir].begin(), part[t].chroma[dir].end());
     }
 }
+
+// Compact copies of the descriptors for the device planner (vvcr_dbk_plan.hip): one pass over the CU / PU /
+// TU rows, with the chroma QP of every TU resolved here (the host planner's chroma_qp).
+void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkGpuInputs &out) {
+  out.clear();
+  if (pp.dbk_disable) return;
+  if (sp.width % 8 || sp.height % 8) throw VvcrError(VVCR_E_UNSUPPORTED, "deblocking: picture size not a multiple of 8");
+  const size_t ncu = d.cu.size(), npu = d.pu.size(), ntu = d.tu.size();
+  if (ncu > (size_t)INT32_MAX || ntu > (size_t)INT32_MAX) throw VvcrError(VVCR_E_ARG, "deblocking: too many coding units");
+  out.cu.resize(ncu);
+  out.pu.resize(npu);
+  out.tu.resize(ntu);
+  for (size_t i = 0; i < ncu; i++) {
+    const vvcr_cu &c = d.cu[i];
+    DbCu &o = out.cu[i];
+    o.x = (int16_t)c.x; o.y = (int16_t)c.y; o.w = (int16_t)c.w; o.h = (int16_t)c.h;
+    o.cx = (int16_t)c.cx; o.cy = (int16_t)c.cy; o.cw = (int16_t)c.cw; o.ch = (int16_t)c.ch;
+    o.firstpu = c.firstpu; o.firsttu = c.firsttu; o.npu = (int16_t)c.npu; o.ntu = (int16_t)c.ntu;
+    o.qp = (int16_t)c.qp;
+    uint16_t f = 0;
+    if (c.chtype) f |= DBC_CHTYPE;
+    if (c.predmode == MODE_INTRA) f |= DBC_INTRA;
+    if (c.bdpcm) f |= DBC_BDPCM;
+    if (c.bdpcmc) f |= DBC_BDPCMC;
+    if (c.affine) f |= DBC_AFFINE;
+    if (c.isp) f |= DBC_ISP;
+    if (c.treetype != 0) f |= DBC_TREE;
+    if (c.yvalid) f |= DBC_YVALID;
+    if (c.cvalid) f |= DBC_CVALID;
+    if (c.firstpu >= 0 && (size_t)c.firstpu < npu && d.pu[c.firstpu].ciip) f |= DBC_CIIP;
+    o.flags = f;
+    if (c.chtype) out.chroma_pass = true;
+  }
+  for (size_t i = 0; i < npu; i++) {
+    const vvcr_pu &u = d.pu[i];
+    DbPu &o = out.pu[i];
+    o.x = (int16_t)u.x; o.y = (int16_t)u.y; o.w = (int16_t)u.w; o.h = (int16_t)u.h; o.cx = (int16_t)u.cx; o.cy = (int16_t)u.cy;
+    o.sub = (u.merge && u.mrgtype == MRG_TYPE_SUBPU_ATMVP) ? 1 : 0;
+    o.pad = 0;
+  }
+  const int qbd = 6 * (sp.bit_depth - 8);
+  for (size_t t = 0; t < ntu; t++) {
+    const vvcr_tu &u = d.tu[t];
+    DbTu &o = out.tu[t];
+    for (int c = 0; c < 3; c++)
+      for (int k = 0; k < 4; k++) o.b[c][k] = (int16_t)u.b[c][k];
+    o.cu = u.cu;
+    o.cbf = (uint8_t)((u.b[0][BCBF] ? 1 : 0) | (u.b[1][BCBF] ? 2 : 0) | (u.b[2][BCBF] ? 4 : 0));
+    o.jccr = (uint8_t)u.jccr;
+    // QpParam(tu, comp).Qp(0) - qpBdOffset (Quant.cpp:65-138), as Planner::chroma_qp
+    const int qpy = d.cu[u.cu].qp;
+    for (int comp = 1; comp <= 2; comp++) {
+      const bool jqp = u.jccr == 3;
+      const int off = jqp ? pp.chroma_qp_off[0] : pp.chroma_qp_off[comp];
+      const int32_t *map = pp.chroma_qp_map[jqp ? 0 : comp];
+      int q = map[std::clamp(qpy, -qbd, 63) + 64];
+      q = std::clamp(q + off, -qbd, 63) + qbd;
+      q = std::clamp(q, 0, 63 + qbd);
+      o.cqp[comp - 1] = (int8_t)(q - qbd);
+    }
+  }
+}
