@@ -346,8 +346,9 @@ __global__ __launch_bounds__(256) void k_dbkp_maps(DbkPlanArgs A) {
   };
   if (i < A.ncu) {
     const DbCu &c = A.cu[i];
-    if (c.flags & DBC_YVALID) fill(A.cu_map[0], c.x, c.y, c.w, c.h, 2, i, false);
-    if (c.flags & DBC_CVALID) fill(A.cu_map[1], c.cx, c.cy, c.cw, c.ch, 1, i, false);
+    // (a later CU wins where two cover a unit, as the host planner's fill in CU order)
+    if (c.flags & DBC_YVALID) fill(A.cu_map[0], c.x, c.y, c.w, c.h, 2, i, true);
+    if (c.flags & DBC_CVALID) fill(A.cu_map[1], c.cx, c.cy, c.cw, c.ch, 1, i, true);
   } else if (i < A.ncu + A.ntu) {
     const int t = i - A.ncu;
     const DbTu &tu = A.tu[t];
