@@ -144,3 +144,45 @@ print("MISMATCHES", bad)
     r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "MISMATCHES 0" in r.stdout, r.stdout[-2000:]
+
+
+def test_stage_by_stage_launches_stay_on_one_lane(golden_dir, monkeypatch):
+    """vvcr_launch_picture_stages: a picture launched one stage group at a time (residual, inter, intra,
+    loop filters), two segment copies interleaved call by call so the lane choice of every call would
+    differ — the later stages must run on the lane whose residual / prediction planes the earlier ones
+    wrote, and every picture stays bit-exact."""
+    from vvc_amd import native as N
+    monkeypatch.setenv("VVCR_LANES", "5")
+    monkeypatch.setenv("VVCR_INTRA_LANES", "3")   # the least recently used intra lane changes call by call
+    d = os.path.join(golden_dir, "ra416_q32")
+    pics = S.load_sequence(d)
+    meta = S.load_meta(d)
+    per = min(len(pics), 16)
+    dec = D.Decoder(pics, dpb_slots=2 * per)
+    ctx = dec.ctx
+    groups = (N.STAGE_RESID, N.STAGE_INTER, N.STAGE_INTRA | N.STAGE_LMCS_INV, N.STAGE_DBK | N.STAGE_SAO | N.STAGE_ALF)
+    try:
+        copies = []
+        for c in range(2):
+            alloc = S.SlotAllocator(pics, per, base=per * c)
+            hs = []
+            for i, p in enumerate(pics):
+                slot = alloc.assign(i, p["hdr"]["poc"])
+                ctx.begin_picture(S.pic_params(p, slot, alloc.slot_of))
+                S.submit(ctx, p)
+                S.set_loop_filter_params(ctx, p)
+                hs.append((ctx.prepare(N.STAGE_ALL), p["hdr"]["poc"], slot))
+            copies.append(hs)
+        for i in range(len(pics)):
+            for g in groups:
+                for hs in copies:
+                    ctx.launch_stages(hs[i][0], g)
+        ctx.sync()
+        for hs in copies:
+            owner = {slot: poc for _, poc, slot in hs}
+            for slot, poc in owner.items():
+                assert D.plane_md5s(dec.read(slot)) == meta["poc_plane_md5"][str(poc)], "POC %d differs" % poc
+            for h, _, _ in hs:
+                ctx.release(h)
+    finally:
+        dec.close()

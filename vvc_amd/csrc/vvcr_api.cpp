@@ -159,6 +159,7 @@ struct Prepared {
   DevVec<DbTu> dbtu;
   DevVec<MotionRec> dbmot;
   int n_dbcu = 0, n_dbtu = 0;
+  int32_t dbk_nitems[4] = {0, 0, 0, 0};
   DevVec<int32_t> sao;
   DevVec<int16_t> alf_luma_coef, alf_luma_clip, alf_chroma, alf_cc, alf_set;
   DevVec<uint8_t> alf_ctb;
@@ -166,6 +167,9 @@ struct Prepared {
   DevVec<WpTable> wpt;               // the slice's weighted-prediction table (k_mc reads it per lane)
   McClassTable mc_ct;                // k_mc cell classes of mc_basic (edge jobs, tiles, blocks)
   bool have_sao = false, have_alf = false;
+  // exactly one of SAO / ALF and every stage in one prepared picture: the picture is reconstructed and
+  // deblocked in the lane's loop-filter planes, and that one filter writes it into its slot (no copy-back)
+  bool recon_tmp = false;
   bool zero_filled = false;   // the residual areas read are zeroed by TB_ZERO jobs: no plane clear
   int n_tb = 0, n_tb_small = 0, n_mctile = 0, n_basic = 0, n_bidir = 0, n_aff = 0, n_tiles = 0, n_dmvr = 0;
   hipEvent_t ev[NK][2] = {};
@@ -182,6 +186,7 @@ struct Prepared {
   bool timed[NK] = {};              // the group's events were recorded by the last launch
   bool launched = false;
   int lane = 0;                      // execution lane of the last launch (its stream and scratch planes)
+  uint32_t staged = 0;               // stages launched so far by vvcr_launch_picture_stages (0: none pending)
   double alg_bytes[NK] = {};
   int launches[NK] = {};
 
@@ -215,8 +220,10 @@ struct Prepared {
     have_sao = have_alf = false;
     n_tb = n_tb_small = n_mctile = n_basic = n_bidir = n_aff = n_tiles = n_dmvr = 0;
     zero_filled = false;
+    recon_tmp = false;
     for (int k = 0; k < NK; k++) { ran[k] = timed[k] = false; alg_bytes[k] = 0; launches[k] = 0; }
     launched = false;
+    staged = 0;
     lane = 0;
   }
 };
@@ -305,6 +312,7 @@ struct Lane {
   hipStream_t s = nullptr;
   DPlane pred[3], resi[3], tmp[3];
   DevVec<uint8_t> dbkp;              // device deblocking planner's maps and lists (allocated at its first use)
+  const void *held = nullptr;        // a picture launched stage by stage whose later stages are pending here
   int tail_slot = -1;                // DPB slot written by the lane's last picture
   uint64_t tail_seq = 0;             // launch sequence number of that picture
 };
@@ -401,7 +409,13 @@ static WpTable make_wp_table(const vvcr_pic_params &pp, int bit_depth) {
   return T;
 }
 
-static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lane, const WpTable *wpd) {
+// the planes a prepared picture is reconstructed (and deblocked) in on a lane
+static const DPlane *recon_planes(vvcr_ctx *ctx, const Prepared &r, int lane) {
+  return r.recon_tmp ? ctx->lanes[lane].tmp : ctx->dpb[r.pp.slot].data();
+}
+
+static McParams make_mc_params(vvcr_ctx *ctx, const Prepared &r, int lane, const WpTable *wpd) {
+  const vvcr_pic_params &pp = r.pp;
   McParams P{};
   P.ref.p = ctx->d_ref_table.p;
   for (int c = 0; c < 3; c++) {
@@ -414,8 +428,9 @@ static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lan
   P.ctu = 1 << ctx->sp.ctu_log2;
   P.wp = make_wp_table(pp, ctx->sp.bit_depth);
   P.wpd = wpd;
+  const DPlane *reco = recon_planes(ctx, r, lane);
   for (int c = 0; c < 3; c++) {
-    P.reco[c] = ctx->dpb[pp.slot][c];
+    P.reco[c] = reco[c];
     P.resi[c] = ctx->lanes[lane].resi[c];
   }
   return P;
@@ -425,8 +440,9 @@ static McParams make_mc_params(vvcr_ctx *ctx, const vvcr_pic_params &pp, int lan
 static IntraParams make_intra_params(vvcr_ctx *ctx, const Prepared &r, int lane) {
   const vvcr_pic_params &pp = r.pp;
   IntraParams P{};
+  const DPlane *reco = recon_planes(ctx, r, lane);
   for (int c = 0; c < 3; c++) {
-    P.reco[c] = ctx->dpb[pp.slot][c];
+    P.reco[c] = reco[c];
     P.pred[c] = ctx->lanes[lane].pred[c];
     P.resi[c] = ctx->lanes[lane].resi[c];
   }
@@ -516,6 +532,12 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   const uint32_t mask = bp.mask;
   r.mask = mask;
   r.launched = false;
+  r.staged = 0;
+  {
+    std::lock_guard<std::mutex> g(ctx->launch_mu);   // lane state
+    for (int l = 0; l < ctx->nlane; l++)
+      if (ctx->lanes[l].held == &r) ctx->lanes[l].held = nullptr;
+  }
   for (int k = 0; k < NK; k++) { r.alg_bytes[k] = 0; r.launches[k] = 0; r.ran[k] = false; }
   const vvcr_seq_params &sp = ctx->sp;
   const vvcr_pic_params &pp = bp.pp;
@@ -610,6 +632,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.dbk_chroma_pass = bp.dbkg.chroma_pass;
     r.n_dbcu = (int)bp.dbkg.cu.size();
     r.n_dbtu = (int)bp.dbkg.tu.size();
+    for (int k = 0; k < 4; k++) r.dbk_nitems[k] = bp.dbkg.nitems[k];
     if (r.n_dbcu > 0) {
       st.add(r.dbcu, bp.dbkg.cu);
       st.add(r.dbpu, bp.dbkg.pu);
@@ -632,6 +655,8 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   const bool alfOn = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
   r.have_sao = (mask & VVCR_STAGE_SAO) && saoOn;
   r.have_alf = (mask & VVCR_STAGE_ALF) && alfOn;
+  static const bool copy_back = getenv("VVCR_COPY_BACK") != nullptr;   // diagnostics: the r04 copy-back
+  r.recon_tmp = r.have_sao != r.have_alf && (mask & VVCR_STAGE_ALL) == VVCR_STAGE_ALL && pp.shard_y1 == 0 && !copy_back;
   if (r.have_sao) {
     st.add(r.sao, bp.h_sao);
     r.alg_bytes[K_SAO] = pix * 2 * 2;
@@ -659,9 +684,9 @@ static DbkPlanArgs dbk_plan_args(vvcr_ctx *ctx, Lane &ln, const Prepared &r) {
   const vvcr_pic_params &pp = r.pp;
   const int W4 = sp.width / 4, H4 = sp.height / 4;
   const size_t n4 = (size_t)W4 * H4, a4 = (n4 + 255) & ~(size_t)255;
-  const size_t maps = 4 * a4 * sizeof(int32_t), scratch = 18 * a4, dense = 4 * a4 * sizeof(uint32_t);
+  const size_t maps = 4 * a4 * sizeof(int32_t), state = 2 * a4, items = 4 * a4 * sizeof(uint32_t);
   const size_t lists = 4 * a4 * sizeof(DbkSeg);
-  ln.dbkp.ensure(maps + scratch + dense + lists + 256);
+  ln.dbkp.ensure(maps + state + items + lists + 256);
   uint8_t *p = ln.dbkp.p;
   DbkPlanArgs a{};
   a.cu = r.dbcu.p; a.pu = r.dbpu.p; a.tu = r.dbtu.p; a.motion = r.dbmot.p;
@@ -675,24 +700,12 @@ static DbkPlanArgs dbk_plan_args(vvcr_ctx *ctx, Lane &ln, const Prepared &r) {
     a.cu_map[k] = (int32_t *)p + k * a4;
     a.tu_map[k] = (int32_t *)p + (2 + k) * a4;
   }
-  uint8_t *q = p + maps;
-  a.scratch0 = q;
-  a.scratch_bytes = scratch;
-  for (int d = 0; d < 2; d++) {
-    a.bs[d] = q + (0 + d) * a4;
-    a.edge[d] = q + (2 + d) * a4;
-    a.tedge[d] = q + (4 + d) * a4;
-    for (int c = 0; c < 3; c++) {
-      a.lenP[d][c] = q + (6 + 3 * d + c) * a4;
-      a.lenQ[d][c] = q + (12 + 3 * d + c) * a4;
-    }
-  }
-  uint32_t *w = (uint32_t *)(q + scratch);
-  a.dense_bytes = dense;
-  a.segL[0] = w; a.segC[0] = w + a4; a.segL[1] = w + 2 * a4; a.segC[1] = w + 3 * a4;
-  a.out = (DbkSeg *)(q + scratch + dense);
+  a.state[0] = p + maps; a.state[1] = p + maps + a4; a.state_pitch = a4;
+  a.items = (uint32_t *)(p + maps + state);
+  a.out = (DbkSeg *)(p + maps + state + items);
   a.cap = (int32_t)a4;
-  a.counts = (int32_t *)(q + scratch + dense + lists);
+  a.counts = (int32_t *)(p + maps + state + items + lists);
+  for (int k = 0; k < 4; k++) a.nitems[k] = r.dbk_nitems[k];
   a.err = ctx->d_err + 1;
   return a;
 }
@@ -711,26 +724,30 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
   // costs nothing; VVCR_LANE_POLICY=0: only a lane whose last picture is a reference), else the least
   // recently used of those lanes. Dependencies on pictures of the chosen lane need no event wait.
   const int lo = refs.empty() ? 0 : ctx->nintra, hi = refs.empty() ? ctx->nintra : ctx->nlane;
-  int L = -1;
-  if (!refs.empty() && ctx->lane_policy == 1) {
+  // the later stages of a picture launched stage by stage stay on its lane: they read that lane's
+  // residual / prediction planes
+  int L = r.staged ? r.lane : -1;
+  // (lanes holding another picture's pending stages are not chosen while others are free)
+  auto held = [&](int l) { return ctx->lanes[l].held != nullptr && ctx->lanes[l].held != &r; };
+  if (L < 0 && !refs.empty() && ctx->lane_policy == 1) {
     // the B lane that wrote the newest of the references (still in its slot): the pictures of one
     // segment then stay on one lane even when other segments' pictures are interleaved on it, and their
     // dependencies are stream order instead of cross-lane event waits
     uint64_t best = 0;
     for (int rs : refs) {
       const int wl = ctx->slot_lane[rs];
-      if (wl >= lo && wl < hi && ctx->slot_seq[rs] > best) { best = ctx->slot_seq[rs]; L = wl; }
+      if (wl >= lo && wl < hi && !held(wl) && ctx->slot_seq[rs] > best) { best = ctx->slot_seq[rs]; L = wl; }
     }
   }
   if (!refs.empty() && L < 0)
     for (int l = lo; l < hi && L < 0; l++) {
       const int ts = ctx->lanes[l].tail_slot;
-      if (ts >= 0 && std::find(refs.begin(), refs.end(), ts) != refs.end() && ctx->lanes[l].tail_seq == ctx->slot_seq[ts]) L = l;
+      if (ts >= 0 && !held(l) && std::find(refs.begin(), refs.end(), ts) != refs.end() && ctx->lanes[l].tail_seq == ctx->slot_seq[ts]) L = l;
     }
-  if (L < 0) {
+  for (int pass = 0; pass < 2 && L < 0; pass++) {
     uint64_t best = ~0ull;
     for (int l = lo; l < hi; l++)
-      if (ctx->lanes[l].tail_seq < best) { best = ctx->lanes[l].tail_seq; L = l; }
+      if ((pass || !held(l)) && ctx->lanes[l].tail_seq < best) { best = ctx->lanes[l].tail_seq; L = l; }
   }
   Lane &ln = ctx->lanes[L];
   hipStream_t s = ln.s;
@@ -769,7 +786,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
     r.launches[K_RESID] = r.n_tb > 0 ? 1 : 0;
   }
   if (mask & VVCR_STAGE_INTER) {
-    const McParams mp = make_mc_params(ctx, r.pp, L, r.wpt.p);
+    const McParams mp = make_mc_params(ctx, r, L, r.wpt.p);
     {
       KernelTimer t(r, K_MC, s, ctx->timing);
       launch_mc(mp, r.mc_basic.p, r.mc_ct, s);
@@ -812,7 +829,8 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
       r.launches[K_INTRA] = r.n_ijobs ? 1 : 0;
     }
   }
-  auto &A = ctx->dpb[pp.slot];
+  const DPlane *A = recon_planes(ctx, r, L);   // the picture until the last loop filter
+  const DPlane *slot = ctx->dpb[pp.slot].data();
   if ((mask & VVCR_STAGE_LMCS_INV) && pp.lmcs_enabled) {
     launch_lmcs_inverse(A[0], r.lmcs_lut.p + 1024, own0, own1, s);   // back to the original domain before the loop filters
     VVCR_CHECK_HIP(hipGetLastError());
@@ -850,25 +868,26 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
       r.launches[K_DBK] = (r.dbk_counts[0] + r.dbk_counts[1] > 0) + (r.dbk_counts[2] + r.dbk_counts[3] > 0);
     }
   }
-  // SAO (slot -> tmp) and ALF (ping-pong back); the final picture always ends in the slot
+  // SAO and ALF ping-pong between the slot and the lane's planes; the final picture always ends in the slot
+  // (a picture with one of the two was reconstructed in the lane's planes: recon_tmp)
   const int ctu = 1 << ctx->sp.ctu_log2;
   const int wc = (ctx->sp.width + ctu - 1) / ctu, n = n_ctb(ctx->sp);
-  bool inTmp = false;
+  bool inTmp = A != slot;
   if (r.have_sao && (mask & VVCR_STAGE_SAO)) {
     KernelTimer t(r, K_SAO, s, ctx->timing);
     SaoParams sp{};
-    for (int c = 0; c < 3; c++) { sp.src[c] = A[c]; sp.dst[c] = ln.tmp[c]; }
+    for (int c = 0; c < 3; c++) { sp.src[c] = inTmp ? ln.tmp[c] : slot[c]; sp.dst[c] = inTmp ? slot[c] : ln.tmp[c]; }
     sp.sao = r.sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
     sp.y0 = sao0; sp.y1 = sao1;
     launch_sao(sp, s);
     VVCR_CHECK_HIP(hipGetLastError());
-    inTmp = true;
+    inTmp = !inTmp;
     r.launches[K_SAO] = 3;
   }
   if (r.have_alf && (mask & VVCR_STAGE_ALF)) {
     KernelTimer t(r, K_ALF, s, ctx->timing);
     AlfParams ap{};
-    for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ln.tmp[c] : A[c]; ap.dst[c] = inTmp ? A[c] : ln.tmp[c]; }
+    for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ln.tmp[c] : slot[c]; ap.dst[c] = inTmp ? slot[c] : ln.tmp[c]; }
     ap.bd = ctx->sp.bit_depth; ap.ctu_log2 = ctx->sp.ctu_log2; ap.wc = wc; ap.nctb = n;
     ap.vb_luma = pp.alf_vb_luma; ap.vb_chroma = pp.alf_vb_chroma;
     for (int c = 0; c < 3; c++) ap.en[c] = pp.alf_en[c];
@@ -885,7 +904,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
   }
   if (inTmp) {
     Planes3 cp{};
-    for (int c = 0; c < 3; c++) { cp.dst[c] = A[c]; cp.src[c] = ln.tmp[c]; }
+    for (int c = 0; c < 3; c++) { cp.dst[c] = slot[c]; cp.src[c] = ln.tmp[c]; }
     cp.copy = 1;
     cp.y0 = own0; cp.y1 = own1;
     launch_planes3(cp, s);
@@ -902,6 +921,9 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
       ctx->slot_r_set[rs] |= 1u << L;
     }
   r.launched = true;
+  r.staged |= mask;
+  if ((r.staged & r.mask) == r.mask) r.staged = 0;
+  ln.held = r.staged ? &r : nullptr;
   ctx->last = &r;
 }
 
@@ -1238,6 +1260,8 @@ int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle) {
   r.wait();
   std::lock_guard<std::mutex> lg(ctx->launch_mu);
   if (ctx->last == &r) ctx->last = nullptr;
+  for (int l = 0; l < ctx->nlane; l++)
+    if (ctx->lanes[l].held == &r) ctx->lanes[l].held = nullptr;
   std::lock_guard<std::mutex> g(ctx->prepared_mu);
   if (ctx->spare.size() < 96) ctx->spare.push_back(std::move(ctx->prepared[handle]));
   else ctx->prepared[handle].reset();
@@ -1360,6 +1384,7 @@ extern "C" int vvcr_debug_dbk_gpu_segments(vvcr_ctx *ctx, const vvcr_picture *pi
   r.dbk_chroma_pass = pic->dbkg.chroma_pass;
   r.n_dbcu = (int)pic->dbkg.cu.size();
   r.n_dbtu = (int)pic->dbkg.tu.size();
+  for (int k = 0; k < 4; k++) r.dbk_nitems[k] = pic->dbkg.nitems[k];
   r.dbcu.upload(pic->dbkg.cu);
   r.dbpu.upload(pic->dbkg.pu);
   r.dbtu.upload(pic->dbkg.tu);

@@ -35,8 +35,11 @@ struct DbCu {
   int16_t npu, ntu;
   int16_t qp;
   uint16_t flags;                       // DBC_*
+  uint32_t lines[2];                    // the edge lines inside the CU per direction (bit o: offset 4 o in the
+                                        // CU's channel; TU, PU and sub-block origins: xDeblockCU's edgeIdx)
+  int32_t item0[2];                     // the first index of its units in the item list of (its pass, dir)
 };
-static_assert(sizeof(DbCu) == 32, "DbCu layout");
+static_assert(sizeof(DbCu) == 48, "DbCu layout");
 enum : uint16_t {
   DBC_CHTYPE = 1, DBC_INTRA = 2, DBC_BDPCM = 4, DBC_BDPCMC = 8, DBC_AFFINE = 16, DBC_ISP = 32, DBC_TREE = 64,
   DBC_YVALID = 128, DBC_CVALID = 256, DBC_CIIP = 512   // CIIP: the CU's first PU
@@ -60,7 +63,8 @@ struct DbkGpuInputs {
   bigbuf::vec<DbPu> pu;
   bigbuf::vec<DbTu> tu;
   bool chroma_pass = false;             // CUs of the chroma tree (dual tree, or local dual-tree chroma CUs)
-  void clear() { cu.clear(); pu.clear(); tu.clear(); chroma_pass = false; }
+  int32_t nitems[4] = {0, 0, 0, 0};     // the item lists' lengths: (pass, dir) at 2 * pass + dir
+  void clear() { cu.clear(); pu.clear(); tu.clear(); chroma_pass = false; for (int &n : nitems) n = 0; }
 };
 void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkGpuInputs &out);
 
@@ -70,15 +74,14 @@ struct DbkPlanArgs {
   int32_t slice_type, dual_tree, dbk_disable;
   int32_t ref_poc[2][VVCR_MAX_REF];
   int32_t shard, ly0, ly1;
-  int32_t pass;                         // 0: luma-tree CUs (chtype 0), 1: chroma-tree CUs
-  int32_t chroma_pass;                  // pass 1 needed
-  // picture-wide scratch on the 4x4 luma grid (chroma 2x2 units: the same grid), per lane
+  int32_t chroma_pass;                  // the picture has chroma-tree CUs (dual tree, local dual tree)
+  // picture-wide CU / TU index maps on the 4x4 luma grid (chroma 2x2 units: the same grid), per lane
   int32_t *cu_map[2], *tu_map[2];
-  uint8_t *bs[2], *edge[2], *lenP[2][3], *lenQ[2][3], *tedge[2];
-  uint32_t *segL[2], *segC[2];          // dense segment words (0: none)
-  void *scratch0; size_t scratch_bytes; // bs .. tedge, cleared per pass of a dual-tree picture
-  size_t dense_bytes;                   // segL / segC, right after the scratch
+  uint8_t *state[2];                    // local dual tree: edge flag << 7 | boundary strength of the luma CUs,
+  size_t state_pitch;                   // per direction (state[1] = state[0] + state_pitch)
   DbkSeg *out; int32_t *counts; int32_t cap;   // the four lists at out + k * cap, their lengths
+  uint32_t *items;                      // the units on CU edge lines per pass and direction (k_dbkp_maps),
+  int32_t nitems[4];                    // at items + (2 * pass + dir) * cap, their lengths (pack_dbk_inputs)
   int32_t *err;                         // bit 2: a map hole (inconsistent descriptors), bit 4: list overflow
 };
 void launch_dbk_plan(const DbkPlanArgs &a, hipStream_t s);

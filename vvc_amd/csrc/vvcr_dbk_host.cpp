@@ -572,6 +572,37 @@ void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const
     if (c.firstpu >= 0 && (size_t)c.firstpu < npu && d.pu[c.firstpu].ciip) f |= DBC_CIIP;
     o.flags = f;
     if (c.chtype) out.chroma_pass = true;
+    // the edge lines (the host planner's deblock_cu edge list, as a mask) and the CU's units on them: its
+    // runs in the item lists of its pass (vvcr_dbk_plan.hip k_dbkp_maps writes them there)
+    const int ch = c.chtype, cpx = ch ? c.cx : c.x, cpy = ch ? c.cy : c.y;
+    const int a2 = c.yvalid ? c.w : 2 * c.cw, a3 = c.yvalid ? c.h : 2 * c.ch;
+    uint64_t m[2] = {0, 0};
+    auto add = [&](int dir, int v) { if (v >= 0 && v < 64) m[dir] |= 1ull << v; };
+    for (int t = c.firsttu; t < c.firsttu + c.ntu; t++) {
+      const int32_t *tb = d.tu[t].b[ch];
+      add(0, (tb[BX] - cpx) / 4);
+      add(1, (tb[BY] - cpy) / 4);
+    }
+    if (c.npu > 0) {
+      const vvcr_pu &u = d.pu[c.firstpu];
+      const int pux = ch ? u.cx : u.x, puy = ch ? u.cy : u.y;
+      add(0, (pux - cpx) / 4);
+      add(1, (puy - cpy) / 4);
+      if ((u.merge && u.mrgtype == MRG_TYPE_SUBPU_ATMVP) || c.affine) {
+        const int pw = c.yvalid ? u.w : a2, ph = c.yvalid ? u.h : a3;
+        for (int off = 8; off < pw; off += 8) add(0, (pux + off - cpx) / 4);
+        for (int off = 8; off < ph; off += 8) add(1, (puy + off - cpy) / 4);
+      }
+    }
+    const int wq = a2 / 4, hq = a3 / 4;
+    m[0] &= wq >= 64 ? ~0ull : (1ull << wq) - 1;   // lines inside the CU
+    m[1] &= hq >= 64 ? ~0ull : (1ull << hq) - 1;
+    for (int dir = 0; dir < 2; dir++) {
+      o.lines[dir] = (uint32_t)m[dir];
+      if (m[dir] >> 32) throw VvcrError(VVCR_E_ARG, "deblocking: CU wider than 128 samples");
+      o.item0[dir] = out.nitems[2 * ch + dir];
+      out.nitems[2 * ch + dir] += __builtin_popcountll(m[dir]) * (dir == 0 ? hq : wq);
+    }
   }
   for (size_t i = 0; i < npu; i++) {
     const vvcr_pu &u = d.pu[i];

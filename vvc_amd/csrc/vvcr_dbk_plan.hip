@@ -2,127 +2,196 @@
 // control part of LoopFilter::xDeblockCU (LoopFilter.cpp:261-408) that vvcr_dbk_host.cpp runs on the
 // host — edge flags and TU / PU / sub-block markers (xSetEdgefilterMultiple :627), filter lengths from
 // transform sizes (:454) and of SbTMVP / affine sub-blocks (:550), xGetBoundaryStrengthSingle (:674), and
-// the QP / length bookkeeping of xEdgeFilterLuma (:844-979) and xEdgeFilterChroma (:1087-1244) — as one
-// thread per (CU, direction). It is the same algorithm as the host planner (every rule cited there), over
-// picture-wide maps instead of the reference's per-CTU arrays: a CU writes and reads only the edge
-// positions of its own area (its left / top boundary and its internal edges), so the CUs of a picture
-// plan independently. Kernels, per picture, on the picture's lane before the deblocking filter:
-//   k_dbkp_maps     CU index maps (luma 4x4 / chroma 2x2 units) and TU index maps, one thread per CU / TU
-//   k_dbkp_cu<dir>  the edges of one CU in one direction, the segment words into dense maps
-//   k_dbkp_compact  the dense words of both directions into the four segment lists k_dbk reads, with
-//                   their lengths on the device (order: by workgroup reservation; every segment of one
-//                   direction is independent, so the lists' order does not change the filtered samples)
+// the QP / length bookkeeping of xEdgeFilterLuma (:844-979) and xEdgeFilterChroma (:1087-1244). It is the
+// same algorithm as the host planner (every rule cited there), restated per position: the edge state of a
+// 4x4 unit (edge flag, boundary-strength marker / value, transform-edge flag, filter lengths) is written
+// only by the CU that covers the unit, through calls whose effect on the unit follows from the CU's TU / PU
+// records alone — xSetEdgefilterMultiple marks a line of units, the length rules read the neighbouring
+// TU through the index maps, and the sub-block rule reads the transform-edge flags of units of the same
+// PU, which are a predicate of the CU's TUs. So each unit on one of its CU's edge lines replays, per
+// direction, exactly the calls of its CU that touch it, in the reference's order, with the state in
+// registers:
+//   1. the xSetEdgefilterMultiple calls of the TUs, the PU and its sub-block lines
+//   2. the transform-size filter lengths of the TU whose edge holds the unit
+//   3. the sub-block filter lengths of an SbTMVP / affine PU
+//   4. the boundary strength
+//   5. the segment words, appended to the four lists k_dbk reads (a wave-aggregated atomic a list; every
+//      segment of one direction is independent, so the lists' order does not change the samples)
+// The chroma-tree CUs of a picture (dual tree, or the chroma CUs of a local dual tree) run after the luma
+// tree's, from a clean state (dual tree: the host's per-pass reset) or on top of the luma CU's state of the
+// unit (local dual tree: the host's CU order within the CTU; the luma pass leaves it in a state map).
+// Kernels, per picture, on the picture's lane before the deblocking filter:
+//   k_dbkp_maps      CU index maps (luma 4x4 / chroma 2x2 units) and TU index maps, a wave per CU / TU
+//                    record; the CU's waves list the units on their CUs' edge lines (items)
+//   k_dbkp_units<P>  steps 1-5, a thread per item of pass P (blockIdx.y: the direction)
 // Inputs: compact CU / PU / TU records (DbCu / DbPu / DbTu, vvcr_dbk.h, built by pack_dbk_inputs) and the
 // 4x4 motion field (MotionRec) of the picture, uploaded with its work lists.
+//
+// Records are read from global memory where they are used, never copied into local structs: a run-time
+// choice between two fields of a local struct is folded by the compiler into a load through a selected
+// address, which puts the struct in scratch memory (measured: 400 bytes a lane, slower than the loads).
 #include "vvcr_dbk.h"
 
 namespace {
 
 enum { VER = 0, HOR = 1 };
+constexpr int MAXTU = 4;   // TUs of a CU (the 64-sample transform split of a 128 CU, ISP, the chroma of a 128 area)
 
 __device__ __forceinline__ int cdiv(int a, int s) { return (a + (1 << s) - 1) >> s; }
 
-struct Planner {
-  const DbkPlanArgs &A;
-  __device__ explicit Planner(const DbkPlanArgs &a) : A(a) {}
+// the edge state of one unit and direction (the reference's per-CTU m_aapucBS / m_aapbEdgeFilter /
+// m_maxFilterLength* entries; chroma lengths of Cb only: Cr's equal them and are never read)
+struct UnitState {
+  int edge, bs, tedge, lp0, lq0, lp1, lq1;
+};
 
-  __device__ int pos(int x, int y) const { return (y >> 2) * A.W4 + (x >> 2); }   // luma 4x4 unit
-  __device__ int get_cu(int x, int y, int ch) const {
-    const int s = ch ? 1 : 2;
-    const int i = A.cu_map[ch][(y >> s) * A.W4 + (x >> s)];
-    if (i < 0) { atomicOr(A.err, 2); return 0; }   // "deblocking: no CU covers a neighbouring position"
-    return i;
+// One CU, wave-uniform scalars (its TU / PU records through the pointers T / PU)
+struct Cu {
+  const DbTu *T;
+  const DbPu *PU;
+  int flags, qp, ntu, npu;
+  int x, y, w, h, cx, cy;
+  int a0, a1, a2, a3;    // luma area (a chroma-tree CU: its chroma area doubled)
+  int yv, isp, ch, cpx, cpy;
+  int left, top, internal;
+  int sub;               // SbTMVP / affine: sub-block edges
+  int pux, puy;          // the PU origin in the CU's channel
+  int pa0, pa1, pa2, pa3;   // the PU's luma area (a chroma-tree CU: the CU's)
+};
+
+__device__ __forceinline__ Cu load_cu(const DbkPlanArgs &A, int i) {
+  const DbCu *c = A.cu + i;
+  Cu R;
+  R.flags = c->flags; R.qp = c->qp; R.ntu = c->ntu; R.npu = c->npu;
+  if (R.ntu > MAXTU || R.npu > 1 || R.ntu < 0 || R.npu < 0) {   // never in VVC: inconsistent descriptors
+    atomicOr(A.err, 2);
+    R.ntu = min(max(R.ntu, 0), MAXTU); R.npu = min(max(R.npu, 0), 1);
   }
-  __device__ int get_tu(int x, int y, int ch) const {
-    const int s = ch ? 1 : 2;
-    int t = A.tu_map[ch][(y >> s) * A.W4 + (x >> s)];
+  R.T = A.tu + c->firsttu;
+  R.PU = A.pu + max(c->firstpu, 0);
+  R.x = c->x; R.y = c->y; R.w = c->w; R.h = c->h; R.cx = c->cx; R.cy = c->cy;
+  R.yv = (R.flags & DBC_YVALID) ? 1 : 0;
+  R.isp = (R.flags & DBC_ISP) ? 1 : 0;
+  R.ch = (R.flags & DBC_CHTYPE) ? 1 : 0;
+  R.a0 = R.yv ? R.x : 2 * R.cx; R.a1 = R.yv ? R.y : 2 * R.cy;
+  R.a2 = R.yv ? R.w : 2 * c->cw; R.a3 = R.yv ? R.h : 2 * c->ch;
+  R.cpx = R.ch ? R.cx : R.x; R.cpy = R.ch ? R.cy : R.y;
+  if (A.dbk_disable) { R.left = R.top = R.internal = 0; }
+  else { R.internal = 1; R.left = R.cpx > 0; R.top = R.cpy > 0; }
+  R.sub = R.npu && ((R.PU->sub & 1) || (R.flags & DBC_AFFINE));
+  R.pux = R.npu ? (R.ch ? R.PU->cx : R.PU->x) : R.cpx;
+  R.puy = R.npu ? (R.ch ? R.PU->cy : R.PU->y) : R.cpy;
+  const bool own = R.npu && R.yv;
+  R.pa0 = own ? R.PU->x : R.a0; R.pa1 = own ? R.PU->y : R.a1;
+  R.pa2 = own ? R.PU->w : R.a2; R.pa3 = own ? R.PU->h : R.a3;
+  return R;
+}
+
+// the edge lines of the CU in direction DIR (offsets from the CU origin in 4-sample units of the CU's
+// channel: TU, PU and sub-block origins)
+template <int DIR>
+__device__ __forceinline__ uint64_t cu_lines(const Cu &R) {
+  uint64_t m = 0;
+  auto add = [&](int v) { if (v >= 0 && v < 64) m |= 1ull << v; };
+#pragma unroll
+  for (int k = 0; k < MAXTU; k++)
+    if (k < R.ntu) add(DIR == VER ? ((R.ch ? R.T[k].b[1][0] : R.T[k].b[0][0]) - R.cpx) / 4 : ((R.ch ? R.T[k].b[1][1] : R.T[k].b[0][1]) - R.cpy) / 4);
+  if (R.npu) {
+    add(DIR == VER ? (R.pux - R.cpx) / 4 : (R.puy - R.cpy) / 4);
+    if (R.sub)
+      for (int off = 8; off < (DIR == VER ? R.pa2 : R.pa3); off += 8) add(DIR == VER ? (R.pux + off - R.cpx) / 4 : (R.puy + off - R.cpy) / 4);
+  }
+  return m;
+}
+
+__device__ __forceinline__ int bs_set(int v, int comp) { return v << (comp * 2); }
+
+// One unit (x4, y4) of CU R in direction DIR
+template <int DIR>
+struct Unit {
+  const DbkPlanArgs &A;
+  const int (*ref_poc)[VVCR_MAX_REF];   // A.ref_poc in LDS
+  const Cu &R;
+  const int x4, y4;
+  static constexpr bool ver = DIR == VER;
+
+  // xSetEdgefilterMultiple(dir, x, y, w, h, val, edgeIdx) (:627) applied to this unit if its line holds it
+  __device__ __forceinline__ void set_edges(UnitState &st, int x, int y, int w, int h, int val, bool edgeIdx) const {
+    const bool hit = ver ? (x4 == (x >> 2) && y4 >= (y >> 2) && y4 < (y >> 2) + (h >> 2))
+                         : (y4 == (y >> 2) && x4 >= (x >> 2) && x4 < (x >> 2) + (w >> 2));
+    if (!hit) return;
+    st.edge = val;
+    if (st.bs && val) st.bs = 3;
+    else if (!edgeIdx) st.bs = val;
+  }
+
+  // whether the length rule (:454) of TU k, component COMP (0 luma, 1 chroma), covers unit (ux, uy); then
+  // (X, Y) are its component samples
+  template <int COMP>
+  __device__ __forceinline__ bool tu_edge(int k, int ux, int uy, int &X, int &Y) const {
+    const int16_t *b = R.T[k].b[COMP];
+    const int bx = b[0], by = b[1], bw = b[2], bh = b[3];
+    if (bw <= 0 || bh <= 0) return false;
+    const int cux = COMP ? R.cx : R.x, cuy = COMP ? R.cy : R.y;
+    // (bx == cux ? left : internal), without a select of two loads: left implies internal
+    if (!(ver ? (R.internal & ((bx != cux) | R.left)) : (R.internal & ((by != cuy) | R.top)))) return false;
+    constexpr int g = COMP ? 1 : 2, step = 1 << g;   // the unit's component samples: (ux, uy) << g
+    X = ux << g; Y = uy << g;
+    if (!ver) return Y == by && X >= bx && X < bx + bw && ((X - bx) & (step - 1)) == 0;
+    return X == bx && Y >= by && Y < by + bh && ((Y - by) & (step - 1)) == 0;
+  }
+
+  // the transform-edge flag of unit (ux, uy) of this CU after step 2 (the luma rule of its TUs)
+  __device__ __forceinline__ bool tedge_at(int ux, int uy) const {
+    bool e = false;
+#pragma unroll
+    for (int k = 0; k < MAXTU; k++) {
+      int X, Y;
+      if (k < R.ntu && tu_edge<0>(k, ux, uy, X, Y)) e = true;
+    }
+    return e;
+  }
+
+  // the index (in A.tu) of the CU's TU holding sample (x, y) of channel c (CodingStructure::getTU: the index
+  // maps' last writer; an ISP CU's first sub-partition that holds it)
+  __device__ __forceinline__ int own_tu(int c, int x, int y) const {
+    int f = -1;
+#pragma unroll
+    for (int k = MAXTU - 1; k >= 0; k--) {
+      if (k >= R.ntu) continue;
+      const int16_t *b = c ? R.T[k].b[1] : R.T[k].b[0];
+      const int b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+      const int g = 2 - c;   // the index maps' unit: 4x4 luma / 2x2 chroma samples
+      const bool in = b2 > 0 && b3 > 0 && (R.isp && c == 0 ? (x >= b0 && x < b0 + b2 && y >= b1 && y < b1 + b3)
+                                                           : ((x >> g) >= (b0 >> g) && (x >> g) < ((b0 + b2 + (1 << g) - 1) >> g) &&
+                                                              (y >> g) >= (b1 >> g) && (y >> g) < ((b1 + b3 + (1 << g) - 1) >> g)));
+      if (in && (f < 0 || (R.isp && c == 0))) f = k;
+    }
+    if (f < 0) { atomicOr(A.err, 2); f = 0; }
+    return (int)(R.T - A.tu) + f;
+  }
+
+  // a TU index from an index map value t at the neighbouring unit (an ISP CU's luma area: its
+  // sub-partition holding sample (x, y))
+  __device__ __forceinline__ int map_tu(int t, int x, int y) const {
     if (t == -1) { atomicOr(A.err, 2); return 0; }
     if (t >= 0) return t;
-    t = -t - 2;   // an ISP CU's area: CodingStructure::getTU (CodingStructure.cpp:379) searches its sub-partitions
+    t = -t - 2;
     for (int k = 0; k < 4 && t + k < A.ntu; k++) {
       const int16_t *b = A.tu[t + k].b[0];
       if (x >= b[0] && x < b[0] + b[2] && y >= b[1] && y < b[1] + b[3]) return t + k;
     }
     return t;
   }
-  __device__ static void cu_area(const DbCu &c, int *a) {
-    if (c.flags & DBC_YVALID) { a[0] = c.x; a[1] = c.y; a[2] = c.w; a[3] = c.h; }
-    else { a[0] = c.cx * 2; a[1] = c.cy * 2; a[2] = c.cw * 2; a[3] = c.ch * 2; }
+  __device__ __forceinline__ int map_cu(int i) const {
+    if (i < 0) { atomicOr(A.err, 2); return 0; }   // "deblocking: no CU covers a neighbouring position"
+    return i;
   }
-
-  // xSetEdgefilterMultiple (:627)
-  __device__ void set_edges(int dir, int x, int y, int w, int h, bool val, bool edgeIdx) const {
-    const int add = dir == VER ? A.W4 : 1, n = dir == VER ? h / 4 : w / 4;
-    int idx = pos(x, y);
-    uint8_t *bs = A.bs[dir], *edge = A.edge[dir];
-    for (int i = 0; i < n; i++, idx += add) {
-      edge[idx] = val;
-      if (bs[idx] && val) bs[idx] = 3;
-      else if (!edgeIdx) bs[idx] = val;
-    }
-  }
-
-  // filter lengths from the transform sizes on both sides (:454)
-  __device__ void len_from_tu(int dir, const DbCu &cu, int t, bool left, bool top, bool internal) const {
-    const DbTu &tu = A.tu[t];
-    for (int comp = 0; comp < 3; comp++) {
-      const int ch = comp ? 1 : 0;
-      const int16_t *b = tu.b[comp], *bch = tu.b[ch];
-      if (b[2] <= 0 || b[3] <= 0) continue;
-      const int cux = comp ? cu.cx : cu.x, cuy = comp ? cu.cy : cu.y;
-      const int step = 4 >> ch;
-      const bool horz = dir == HOR;
-      if (!(horz ? (b[1] == cuy ? top : internal) : (b[0] == cux ? left : internal))) continue;
-      const int n = horz ? b[2] : b[3];
-      for (int k = 0; k < n; k += step) {
-        const int qx = horz ? bch[0] + k : bch[0], qy = horz ? bch[1] : bch[1] + k;
-        const int sizeQ = horz ? b[3] : b[2];
-        const int tp = horz ? get_tu(qx, qy - 1, ch) : get_tu(qx - 1, qy, ch);
-        const int sizeP = horz ? A.tu[tp].b[comp][3] : A.tu[tp].b[comp][2];
-        const int X = horz ? b[0] + k : b[0], Y = horz ? b[1] : b[1] + k;   // component samples
-        const int g = ch ? 1 : 2;
-        if ((X | Y) & ((1 << g) - 1)) continue;
-        const int p = (Y >> g) * A.W4 + (X >> g);   // the 4x4 luma / 2x2 chroma unit: one grid
-        if (comp == 0) {
-          A.tedge[dir][p] = 1;
-          const bool small = sizeP <= 4 || sizeQ <= 4;
-          A.lenQ[dir][0][p] = small ? 1 : (sizeQ >= 32 ? 7 : 3);
-          A.lenP[dir][0][p] = small ? 1 : (sizeP >= 32 ? 7 : 3);
-        } else {
-          A.lenQ[dir][comp][p] = A.lenP[dir][comp][p] = (sizeQ >= 8 && sizeP >= 8) ? 3 : 1;
-        }
-      }
-    }
-  }
-
-  // sub-block edge lengths of SbTMVP / affine PUs (:550)
-  __device__ void len_subblocks(int dir, const DbPu &pu, int w, int h) const {
-    uint8_t *Q = A.lenQ[dir][0], *Pp = A.lenP[dir][0];
-    const uint8_t *te = A.tedge[dir];
-    const bool horz = dir == HOR;
-    const int outer = horz ? h : w, inner = horz ? w : h;
-    for (int a = 0; a < outer; a += 8)
-      for (int b = 0; b < inner; b += 4) {
-        const int x = horz ? pu.x + b : pu.x + a, y = horz ? pu.y + a : pu.y + b;
-        const int p = pos(x, y);
-        auto T = [&](int delta) { return horz ? te[pos(x, y + delta)] : te[pos(x + delta, y)]; };
-        if (T(0)) {
-          if (Q[p] > 5) Q[p] = 5;
-          if (a > 0 && Pp[p] > 5) Pp[p] = 5;
-        } else if (a > 0 && (T(-4) || a + 4 >= outer || T(4))) {
-          Q[p] = Pp[p] = 1;
-        } else if (a > 0 && (T(-8) || a + 8 >= outer || T(8))) {
-          Q[p] = Pp[p] = 2;
-        } else {
-          Q[p] = Pp[p] = 3;
-        }
-      }
-  }
-
-  __device__ static int bs_set(int v, int comp) { return v << (comp * 2); }
 
   // the motion part of xGetBoundaryStrengthSingle (:748-812)
-  __device__ int motion_bs_pair(const MotionRec &mp, const MotionRec &mq, int tmp) const {
+  __device__ __forceinline__ int motion_bs(int tmp) const {
+    const int u = y4 * A.W4 + x4, pu = ver ? u - 1 : u - A.W4;
+    const MotionRec mp = A.motion[pu], mq = A.motion[u];
     const int th = 8;
     // the same motion on both sides (one PU, or equal neighbours): no motion boundary
     if (mp.ref0 == mq.ref0 && mp.ref1 == mq.ref1 && mp.mv0x == mq.mv0x && mp.mv0y == mq.mv0y && mp.mv1x == mq.mv1x &&
@@ -130,8 +199,8 @@ struct Planner {
       return tmp;
     if (A.slice_type == 0) {
       const int NONE = INT32_MIN;
-      const int rP0 = mp.ref0 >= 0 ? A.ref_poc[0][mp.ref0] : NONE, rP1 = mp.ref1 >= 0 ? A.ref_poc[1][mp.ref1] : NONE;
-      const int rQ0 = mq.ref0 >= 0 ? A.ref_poc[0][mq.ref0] : NONE, rQ1 = mq.ref1 >= 0 ? A.ref_poc[1][mq.ref1] : NONE;
+      const int rP0 = mp.ref0 >= 0 ? ref_poc[0][mp.ref0] : NONE, rP1 = mp.ref1 >= 0 ? ref_poc[1][mp.ref1] : NONE;
+      const int rQ0 = mq.ref0 >= 0 ? ref_poc[0][mq.ref0] : NONE, rQ1 = mq.ref1 >= 0 ? ref_poc[1][mq.ref1] : NONE;
       const int p0x = mp.ref0 >= 0 ? mp.mv0x : 0, p0y = mp.ref0 >= 0 ? mp.mv0y : 0;
       const int p1x = mp.ref1 >= 0 ? mp.mv1x : 0, p1y = mp.ref1 >= 0 ? mp.mv1y : 0;
       const int q0x = mq.ref0 >= 0 ? mq.mv0x : 0, q0y = mq.ref0 >= 0 ? mq.mv0y : 0;
@@ -147,208 +216,220 @@ struct Planner {
       return b + tmp;
     }
     if (mp.ref0 < 0 || mq.ref0 < 0) { atomicOr(A.err, 2); return tmp; }   // P-slice inter block without list 0
-    if (A.ref_poc[0][mp.ref0] != A.ref_poc[0][mq.ref0]) return tmp + 1;
+    if (ref_poc[0][mp.ref0] != ref_poc[0][mq.ref0]) return tmp + 1;
     return (abs(mq.mv0x - mp.mv0x) >= th || abs(mq.mv0y - mp.mv0y) >= th) ? tmp + 1 : tmp;
   }
-  __device__ int motion_bs(int dir, int lx, int ly, int tmp) const {
-    const int lpx = dir == VER ? lx - 1 : lx, lpy = dir == VER ? ly : ly - 1;
-    return motion_bs_pair(A.motion[(lpy >> 2) * A.W4 + (lpx >> 2)], A.motion[(ly >> 2) * A.W4 + (lx >> 2)], tmp);
-  }
 
-  // xGetBoundaryStrengthSingle (:674)
-  __device__ int boundary_strength(int cui, int dir, int lx, int ly) const {
-    const DbCu &cuQ = A.cu[cui];
-    const int ch = cuQ.flags & DBC_CHTYPE ? 1 : 0;
-    const bool yv = cuQ.flags & DBC_YVALID;
-    const int sh = yv ? 0 : 1;
-    const int qx = lx >> sh, qy = ly >> sh;
-    const int px = dir == VER ? qx - 1 : qx, py = dir == VER ? qy : qy - 1;
-    const bool same = px >= (yv ? cuQ.x : cuQ.cx) && py >= (yv ? cuQ.y : cuQ.cy);
-    const DbCu &cuP = same ? cuQ : A.cu[get_cu(px, py, ch)];
-    const bool iP = cuP.flags & DBC_INTRA, iQ = cuQ.flags & DBC_INTRA;
-    if (iP || iQ) {
-      const int bsY = (iP && (cuP.flags & DBC_BDPCM)) && (iQ && (cuQ.flags & DBC_BDPCM)) ? 0 : 2;
-      const int bsC = (iP && (cuP.flags & DBC_BDPCMC)) && (iQ && (cuQ.flags & DBC_BDPCMC)) ? 0 : 2;
-      return bs_set(bsY, 0) + bs_set(bsC, 1) + bs_set(bsC, 2);
+  // LoopFilter::xDeblockCU (the host planner's deblock_cu) restricted to this unit, which lies on line o of
+  // the CU: the state it leaves there, and the unit's luma / chroma segment words (0: none)
+  __device__ __forceinline__ void run(int o, UnitState &st, uint32_t &wl, uint32_t &wc) const {
+    const int px = x4 * 4, py = y4 * 4;
+    const int u = y4 * A.W4 + x4, pu = ver ? u - 1 : u - A.W4;
+    // P side inside the CU (else through the index maps); none across the picture edge (left / top false)
+    const bool pin = (ver ? x4 > (R.a0 >> 2) : y4 > (R.a1 >> 2)) || (ver ? x4 == 0 : y4 == 0);
+    // step 1 (TU calls, then the PU's call and its sub-block lines)
+#pragma unroll
+    for (int k = 0; k < MAXTU; k++) {
+      if (k >= R.ntu) continue;
+      if (R.yv) set_edges(st, R.T[k].b[0][0], R.T[k].b[0][1], R.T[k].b[0][2], R.T[k].b[0][3], R.internal, false);
+      else set_edges(st, R.a0, R.a1, R.a2, R.a3, R.internal, false);
     }
-    const int marker = A.bs[dir][pos(lx, ly)];
-    const bool ciip = (cuQ.flags & DBC_CIIP) || (!same && (cuP.flags & DBC_CIIP));
-    if (marker && ciip) return bs_set(2, 0) + bs_set(2, 1) + bs_set(2, 2);
-    int tmp = 0;
-    if (marker) {
-      const int tqi = get_tu(qx, qy, ch);
-      const int tpi = (same && cuQ.ntu == 1 && !(cuQ.flags & DBC_ISP)) ? tqi : get_tu(px, py, ch);
-      const DbTu &tq = A.tu[tqi], &tp = A.tu[tpi];
-      if ((tq.cbf & 1) || (tp.cbf & 1)) tmp += bs_set(1, 0);
-      if ((tq.cbf & 2) || (tp.cbf & 2) || tq.jccr || tp.jccr) tmp += bs_set(1, 1);
-      if ((tq.cbf & 4) || (tp.cbf & 4) || tq.jccr || tp.jccr) tmp += bs_set(1, 2);
+    if (R.npu) {
+      const int off = ver ? R.pux != R.cpx : R.puy != R.cpy;
+      set_edges(st, R.pa0, R.pa1, R.pa2, R.pa3, R.internal & (off | (ver ? R.left : R.top)), off);
+      if (R.sub) {
+        if (ver) { for (int d = 8; d < R.pa2; d += 8) set_edges(st, R.x + d, R.y, 4, R.h, R.internal, true); }
+        else { for (int d = 8; d < R.pa3; d += 8) set_edges(st, R.x, R.y + d, R.w, 4, R.internal, true); }
+      }
     }
-    if ((tmp & 3) == 1) return tmp;
-    if (ciip) return 1;
-    if (!yv) return tmp;
-    if (marker != 0 && marker != 3) return tmp;
-    return motion_bs(dir, lx, ly, tmp);
-  }
-
-  __device__ void emit_luma(int cui, int dir, int e) const {
-    const DbCu &cu = A.cu[cui];
-    const int n = dir == VER ? cu.h / 4 : cu.w / 4;
-    const int ctu = 1 << A.ctu_log2;
-    const int ch = cu.flags & DBC_CHTYPE ? 1 : 0;
-    for (int i = 0; i < n; i++) {
-      const int px = dir == VER ? cu.x + e * 4 : cu.x + i * 4;
-      const int py = dir == VER ? cu.y + i * 4 : cu.y + e * 4;
-      const int p = pos(px, py);
-      const int b = A.bs[dir][p] & 3;
-      if (!b) continue;
-      const DbCu &cuP = A.cu[get_cu(dir == VER ? px - 1 : px, dir == VER ? py : py - 1, ch)];
-      const int qp = (cuP.qp + cu.qp + 1) >> 1;
-      int lp = A.lenP[dir][0][p], lq = A.lenQ[dir][0][p];
+    // step 2 (the host interleaves it with step 1 per TU; the two write disjoint state)
+#pragma unroll
+    for (int k = 0; k < MAXTU; k++) {
+      if (k >= R.ntu) continue;
+      int X, Y;
+      if (tu_edge<0>(k, x4, y4, X, Y)) {
+        const int sizeQ = ver ? R.T[k].b[0][2] : R.T[k].b[0][3];
+        const int tp = pin ? own_tu(0, ver ? X - 1 : X, ver ? Y : Y - 1) : map_tu(A.tu_map[0][pu], ver ? X - 1 : X, ver ? Y : Y - 1);
+        const int sizeP = ver ? A.tu[tp].b[0][2] : A.tu[tp].b[0][3];
+        st.tedge = 1;
+        const bool small = sizeP <= 4 || sizeQ <= 4;
+        st.lq0 = small ? 1 : (sizeQ >= 32 ? 7 : 3);
+        st.lp0 = small ? 1 : (sizeP >= 32 ? 7 : 3);
+      }
+      if (tu_edge<1>(k, x4, y4, X, Y)) {
+        const int sizeQ = ver ? R.T[k].b[1][2] : R.T[k].b[1][3];
+        const int tp = pin ? own_tu(1, ver ? X - 1 : X, ver ? Y : Y - 1) : map_tu(A.tu_map[1][pu], 0, 0);
+        const int sizeP = ver ? A.tu[tp].b[1][2] : A.tu[tp].b[1][3];
+        st.lq1 = st.lp1 = (sizeQ >= 8 && sizeP >= 8) ? 3 : 1;
+      }
+    }
+    // step 3: sub-block lengths (:550), units every 8 samples across, every 4 along the PU
+    if (R.sub && R.PU->w > 0) {
+      const int outer = ver ? R.pa2 : R.pa3, inner = ver ? R.pa3 : R.pa2;
+      const int a8 = ver ? px - R.pa0 : py - R.pa1, b4 = ver ? py - R.pa1 : px - R.pa0;
+      if (a8 >= 0 && a8 < outer && !(a8 & 7) && b4 >= 0 && b4 < inner) {
+        auto T = [&](int delta) { return ver ? tedge_at(x4 + delta / 4, y4) : tedge_at(x4, y4 + delta / 4); };
+        if (st.tedge) {
+          if (st.lq0 > 5) st.lq0 = 5;
+          if (a8 > 0 && st.lp0 > 5) st.lp0 = 5;
+        } else if (a8 > 0 && (T(-4) || a8 + 4 >= outer || T(4))) {
+          st.lq0 = st.lp0 = 1;
+        } else if (a8 > 0 && (T(-8) || a8 + 8 >= outer || T(8))) {
+          st.lq0 = st.lp0 = 2;
+        } else {
+          st.lq0 = st.lp0 = 3;
+        }
+      }
+    }
+    // the P-side CU of the CU's channel
+    const int cP = pin ? -1 : map_cu(A.cu_map[R.ch][pu]);
+    const int fQ = R.flags;
+    // step 4: xGetBoundaryStrengthSingle (:674); an edge inside an inter, non-CIIP luma CU that is not a
+    // transform edge has only the motion part
+    if (st.edge && (!R.yv || o * 4 < (ver ? R.a2 : R.a3))) {
+      const bool fast = R.yv && !(fQ & DBC_INTRA) && !(fQ & DBC_CIIP);
+      if (fast && st.bs == 0 && o > 0) {
+        st.bs = motion_bs(0);
+      } else {
+        const int marker = st.bs;
+        const int fP = pin ? fQ : A.cu[cP].flags;
+        const bool iP = fP & DBC_INTRA, iQ = fQ & DBC_INTRA;
+        if (iP || iQ) {
+          const int bsY = (iP && (fP & DBC_BDPCM)) && (iQ && (fQ & DBC_BDPCM)) ? 0 : 2;
+          const int bsC = (iP && (fP & DBC_BDPCMC)) && (iQ && (fQ & DBC_BDPCMC)) ? 0 : 2;
+          st.bs = bs_set(bsY, 0) + bs_set(bsC, 1) + bs_set(bsC, 2);
+        } else {
+          const bool ciip = (fQ & DBC_CIIP) || (!pin && (fP & DBC_CIIP));
+          if (marker && ciip) {
+            st.bs = bs_set(2, 0) + bs_set(2, 1) + bs_set(2, 2);
+          } else {
+            int tmp = 0;
+            if (marker) {
+              const int sh = R.yv ? 0 : 1;
+              const int qx = px >> sh, qy = py >> sh;
+              const int tq = own_tu(R.ch, qx, qy);
+              const int tp = !pin ? map_tu(A.tu_map[R.ch][pu], ver ? qx - 1 : qx, ver ? qy : qy - 1)
+                                  : (R.ntu == 1 && !R.isp) ? tq : own_tu(R.ch, ver ? qx - 1 : qx, ver ? qy : qy - 1);
+              const int cq = A.tu[tq].cbf, cp = A.tu[tp].cbf, jq = A.tu[tq].jccr, jp = A.tu[tp].jccr;
+              if ((cq & 1) || (cp & 1)) tmp += bs_set(1, 0);
+              if ((cq & 2) || (cp & 2) || jq || jp) tmp += bs_set(1, 1);
+              if ((cq & 4) || (cp & 4) || jq || jp) tmp += bs_set(1, 2);
+            }
+            if ((tmp & 3) == 1) st.bs = tmp;
+            else if (ciip) st.bs = 1;
+            else if (!R.yv) st.bs = tmp;
+            else if (marker != 0 && marker != 3) st.bs = tmp;
+            else st.bs = motion_bs(tmp);
+          }
+        }
+      }
+    }
+    // step 5: the segment words (xEdgeFilterLuma / xEdgeFilterChroma bookkeeping)
+    if (R.yv && (st.bs & 3)) {
+      const int qpP = pin ? R.qp : A.cu[cP].qp, fP = pin ? fQ : A.cu[cP].flags;
+      const int qp = (qpP + R.qp + 1) >> 1;
+      int lp = st.lp0, lq = st.lq0;
       bool pl = false, ql = false;
       if (lp > 3) {
         pl = true;
-        if (lp > 5 && (cuP.flags & DBC_AFFINE)) lp = 5;
+        if (lp > 5 && (fP & DBC_AFFINE)) lp = 5;
       }
       if (lq > 3) ql = true;
-      if (dir == HOR && py % ctu == 0) pl = false;
-      A.segL[dir][p] = (uint32_t)b | (uint32_t)lp << 2 | (uint32_t)lq << 5 | (uint32_t)(qp & 63) << 8 | (uint32_t)pl << 14 | (uint32_t)ql << 15;
+      if (!ver && (py & ((1 << A.ctu_log2) - 1)) == 0) pl = false;
+      wl = (uint32_t)(st.bs & 3) | (uint32_t)lp << 2 | (uint32_t)lq << 5 | (uint32_t)(qp & 63) << 8 | (uint32_t)pl << 14 | (uint32_t)ql << 15;
     }
-  }
-
-  __device__ void emit_chroma(int cui, int dir, int e) const {
-    const DbCu &cu = A.cu[cui];
-    int a[4];
-    cu_area(cu, a);
-    const int ctu = 1 << A.ctu_log2, parts = ctu / 4;
-    const int r = ((a[0] & (ctu - 1)) >> 2) + ((a[1] & (ctu - 1)) >> 2) * parts;   // the CTU raster index of the host planner
-    if ((dir == VER && (r % parts + e) % 4) || (dir == HOR && (r / parts + e) % 4)) return;
-    const int n = dir == VER ? a[3] / 4 : a[2] / 4;
-    const int chQ = cu.flags & DBC_CHTYPE ? 1 : 0;
-    for (int i = 0; i < n; i++) {
-      const int px = dir == VER ? a[0] + e * 4 : a[0] + i * 4;
-      const int py = dir == VER ? a[1] + i * 4 : a[1] + e * 4;
-      const int p = pos(px, py);
-      const int v = A.bs[dir][p];
-      const int bS[2] = {(v >> 2) & 3, (v >> 4) & 3};
-      if (!bS[0] && !bS[1]) continue;
-      const int nlx = dir == VER ? px - 4 : px, nly = dir == VER ? py : py - 4;
-      int cpi = chQ ? get_cu(nlx >> 1, nly >> 1, 1) : get_cu(nlx, nly, 0);
-      if ((A.cu[cpi].flags & DBC_TREE) || A.dual_tree) cpi = get_cu(nlx >> 1, nly >> 1, 1);
-      const DbCu &cuP = A.cu[cpi];
-      const bool large = A.lenP[dir][1][p] >= 3 && A.lenQ[dir][1][p] >= 3;
-      const bool ctbh = dir == HOR && py % ctu == 0;
-      uint32_t w = (uint32_t)large << 4 | (uint32_t)ctbh << 19;
-      bool any = false;
-      for (int k = 0; k < 2; k++) {
-        if (!(bS[k] == 2 || (large && bS[k] == 1))) continue;
-        const int comp = k + 1;
-        const int shP = (cuP.flags & DBC_YVALID) ? 0 : 1, shQ = (cu.flags & DBC_YVALID) ? 0 : 1;
-        const int tq = get_tu(px >> shQ, py >> shQ, chQ);
+    if ((fQ & DBC_CVALID) && (!R.isp || o == 0)) {
+      const int ctu = 1 << A.ctu_log2, parts = ctu / 4;
+      const int r = ((R.a0 & (ctu - 1)) >> 2) + ((R.a1 & (ctu - 1)) >> 2) * parts;   // the CTU raster index of the host planner
+      const int bS0 = (st.bs >> 2) & 3, bS1 = (st.bs >> 4) & 3;
+      if (!((ver && (r % parts + o) % 4) || (!ver && (r / parts + o) % 4)) && (bS0 || bS1)) {
+        // the P-side CU: of the chroma map when the luma one is of a tree-split area or the picture is dual tree
+        int cpi = pin ? -1 : cP;
+        if (!pin && R.ch == 0 && ((A.cu[cP].flags & DBC_TREE) || A.dual_tree)) cpi = map_cu(A.cu_map[1][pu]);
+        const int fP = cpi < 0 ? fQ : A.cu[cpi].flags;
+        const bool large = st.lp1 >= 3 && st.lq1 >= 3;
+        const bool ctbh = !ver && (py & ((1 << A.ctu_log2) - 1)) == 0;
+        uint32_t w = (uint32_t)large << 4 | (uint32_t)ctbh << 19;
+        bool any = false;
+        const int shQ = R.yv ? 0 : 1;
+        const int tq = own_tu(R.ch, px >> shQ, py >> shQ);
+        const int chP = (fP & DBC_CHTYPE) ? 1 : 0, shP = (fP & DBC_YVALID) ? 0 : 1;
         const int p1x = px >> shP, p1y = py >> shP;
-        const int tp = get_tu(dir == VER ? p1x - 1 : p1x, dir == VER ? p1y : p1y - 1, (cuP.flags & DBC_CHTYPE) ? 1 : 0);
-        const int qp = (A.tu[tq].cqp[comp - 1] + A.tu[tp].cqp[comp - 1] + 1) >> 1;
-        w |= (uint32_t)bS[k] << (2 * k) | (uint32_t)((qp + 64) & 127) << (5 + 7 * k);
-        any = true;
-      }
-      if (any) A.segC[dir][p] = w;
-    }
-  }
-
-  // LoopFilter::xDeblockCU for one CU and direction (the host planner's deblock_cu; edge lines of the CU as a
-  // bit mask of 4-sample offsets instead of a sorted array)
-  __device__ void deblock_cu(int cui, int dir) const {
-    const DbCu &cu = A.cu[cui];
-    int a[4];
-    cu_area(cu, a);
-    const bool yv = cu.flags & DBC_YVALID;
-    const int ch = cu.flags & DBC_CHTYPE ? 1 : 0;
-    const int cpx = ch ? cu.cx : cu.x, cpy = ch ? cu.cy : cu.y;
-    bool left, top, internal;
-    if (A.dbk_disable) { left = top = internal = false; }
-    else { internal = true; left = cpx > 0; top = cpy > 0; }
-    uint64_t lines = 0;
-    auto add_line = [&](int v) { if (v >= 0 && v < 64) lines |= 1ull << v; };
-    for (int t = cu.firsttu; t < cu.firsttu + cu.ntu; t++) {
-      const DbTu &tu = A.tu[t];
-      int ta[4];
-      if (yv) { ta[0] = tu.b[0][0]; ta[1] = tu.b[0][1]; ta[2] = tu.b[0][2]; ta[3] = tu.b[0][3]; }
-      else { ta[0] = a[0]; ta[1] = a[1]; ta[2] = a[2]; ta[3] = a[3]; }
-      set_edges(dir, ta[0], ta[1], ta[2], ta[3], internal, false);
-      len_from_tu(dir, cu, t, left, top, internal);
-      const int16_t *tb = tu.b[ch];
-      add_line(dir == HOR ? (tb[1] - cpy) / 4 : (tb[0] - cpx) / 4);
-    }
-    for (int pi = cu.firstpu; pi < cu.firstpu + cu.npu; pi++) {
-      const DbPu &pu = A.pu[pi];
-      int pa[4];
-      if (yv) { pa[0] = pu.x; pa[1] = pu.y; pa[2] = pu.w; pa[3] = pu.h; }
-      else { pa[0] = a[0]; pa[1] = a[1]; pa[2] = a[2]; pa[3] = a[3]; }
-      const int pux = ch ? pu.cx : pu.x, puy = ch ? pu.cy : pu.y;
-      const bool xoff = pux != cpx, yoff = puy != cpy;
-      if (dir == VER) set_edges(VER, pa[0], pa[1], pa[2], pa[3], xoff ? internal : left, xoff);
-      else set_edges(HOR, pa[0], pa[1], pa[2], pa[3], yoff ? internal : top, yoff);
-      add_line(dir == HOR ? (puy - cpy) / 4 : (pux - cpx) / 4);
-      if ((pu.sub & 1) || (cu.flags & DBC_AFFINE)) {
-        if (dir == HOR) {
-          for (int off = 8; off < pa[3]; off += 8) {
-            set_edges(HOR, cu.x, cu.y + off, cu.w, 4, internal, true);
-            add_line((puy + off - cpy) / 4);
-          }
-        } else {
-          for (int off = 8; off < pa[2]; off += 8) {
-            set_edges(VER, cu.x + off, cu.y, 4, cu.h, internal, true);
-            add_line((pux + off - cpx) / 4);
-          }
+        const int tp = pin ? own_tu(chP, ver ? p1x - 1 : p1x, ver ? p1y : p1y - 1)
+                           : map_tu(A.tu_map[chP][pu], ver ? p1x - 1 : p1x, ver ? p1y : p1y - 1);
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+          const int b = k ? bS1 : bS0;
+          if (!(b == 2 || (large && b == 1))) continue;
+          const int qp = (A.tu[tq].cqp[k] + A.tu[tp].cqp[k] + 1) >> 1;
+          w |= (uint32_t)b << (2 * k) | (uint32_t)((qp + 64) & 127) << (5 + 7 * k);
+          any = true;
         }
-        if (pu.w > 0) len_subblocks(dir, pu, pa[2], pa[3]);
+        if (any) wc = w;
       }
-    }
-    // an edge inside an inter, non-CIIP luma CU that is not a transform edge has only the motion part
-    const bool fast = yv && !(cu.flags & DBC_INTRA) && !(cu.flags & DBC_CIIP);
-    uint8_t *bs = A.bs[dir];
-    const uint8_t *edge = A.edge[dir];
-    auto bs_at = [&](int x, int y) {
-      const int p = pos(a[0] + x, a[1] + y);
-      if (!edge[p]) return;
-      if (fast && bs[p] == 0 && (dir == VER ? x : y) > 0) bs[p] = (uint8_t)motion_bs(dir, a[0] + x, a[1] + y, 0);
-      else bs[p] = (uint8_t)boundary_strength(cui, dir, a[0] + x, a[1] + y);
-    };
-    if (yv) {
-      const bool ver = dir == VER;
-      for (uint64_t m = lines; m; m &= m - 1) {
-        const int o = __ffsll((unsigned long long)m) - 1;
-        const int o4 = o * 4;
-        if (o4 >= (ver ? a[2] : a[3])) continue;
-        if (ver) { for (int y = 0; y < a[3]; y += 4) bs_at(o4, y); }
-        else { for (int x = 0; x < a[2]; x += 4) bs_at(x, o4); }
-      }
-    } else {
-      for (int y = 0; y < a[3]; y += 4)
-        for (int x = 0; x < a[2]; x += 4) bs_at(x, y);
-    }
-    for (uint64_t m = lines; m; m &= m - 1) {
-      const int e = __ffsll((unsigned long long)m) - 1;
-      if (yv) emit_luma(cui, dir, e);
-      if ((cu.flags & DBC_CVALID) && (!(cu.flags & DBC_ISP) || e == 0)) emit_chroma(cui, dir, e);
     }
   }
 };
 
-// index maps: CU per 4x4 luma / 2x2 chroma unit, TU likewise (an ISP CU's luma area holds -(first TU) - 2)
+__device__ __forceinline__ bool in_shard(const DbkPlanArgs &A, const Cu &R) {
+  if (!A.shard) return true;
+  const int ctu = 1 << A.ctu_log2;
+  const int ctu_y = R.a1 & ~(ctu - 1);
+  if (ctu_y + ctu <= A.ly0 || ctu_y >= A.ly1) return false;
+  return R.a1 + R.a3 > A.ly0 && R.a1 < A.ly1;
+}
+
+// lanes of the wave with w != 0 append (x4, y4, w) to list k (one atomic a wave and list)
+__device__ __forceinline__ void append(const DbkPlanArgs &A, int k, uint32_t w, int x4, int y4) {
+  const unsigned long long m = __ballot(w != 0);
+  if (!m) return;
+  const int lane = threadIdx.x & 63, first = __ffsll(m) - 1;
+  int base = 0;
+  if (lane == first) base = atomicAdd(&A.counts[k], __popcll(m));
+  base = __shfl(base, first) + __popcll(m & ((1ull << lane) - 1));
+  if (!w) return;
+  if (base < A.cap) A.out[(size_t)k * A.cap + base] = DbkSeg{(uint16_t)x4, (uint16_t)y4, w};
+  else atomicOr(A.err, 4);
+}
+
+// index maps: CU per 4x4 luma / 2x2 chroma unit, TU likewise (an ISP CU's luma area holds -(first TU) - 2);
+// a wave per CU / TU record, a lane per unit. A CU's wave also lists the units on its edge lines: an item
+// (CU index << 10 | line << 5 | unit along the line) per unit, in the list of its pass and direction
+// (A.items + (2 * pass + dir) * cap, lengths A.nitems[2 * pass + dir]).
 __global__ __launch_bounds__(256) void k_dbkp_maps(DbkPlanArgs A) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  __shared__ uint8_t s_line[4][2][32];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + wv;
   auto fill = [&](int32_t *m, int x, int y, int w, int h, int s, int v, bool atomic) {
-    for (int j = y >> s; j < cdiv(y + h, s); j++)
-      for (int k = x >> s; k < cdiv(x + w, s); k++) {
-        if (atomic) atomicMax(&m[j * A.W4 + k], v);   // later TUs win (the host planner's order)
-        else m[j * A.W4 + k] = v;
-      }
+    const int x0 = x >> s, y0 = y >> s, nx = cdiv(x + w, s) - x0, ny = cdiv(y + h, s) - y0;
+    for (int j = lane; j < nx * ny; j += 64) {
+      int32_t *d = &m[(y0 + j / nx) * A.W4 + x0 + j % nx];
+      if (atomic) atomicMax(d, v);   // a later record wins where two cover a unit (the host planner's order)
+      else *d = v;
+    }
   };
   if (i < A.ncu) {
     const DbCu &c = A.cu[i];
-    // (a later CU wins where two cover a unit, as the host planner's fill in CU order)
     if (c.flags & DBC_YVALID) fill(A.cu_map[0], c.x, c.y, c.w, c.h, 2, i, true);
     if (c.flags & DBC_CVALID) fill(A.cu_map[1], c.cx, c.cy, c.cw, c.ch, 1, i, true);
+    // the units on its edge lines (lines and list offsets from pack_dbk_inputs)
+    const int yv = (c.flags & DBC_YVALID) ? 1 : 0, ch = (c.flags & DBC_CHTYPE) ? 1 : 0;
+    const int wq = (yv ? c.w : 2 * c.cw) >> 2, hq = (yv ? c.h : 2 * c.ch) >> 2;
+#pragma unroll
+    for (int d = 0; d < 2; d++) {
+      const uint32_t m = c.lines[d];
+      const int n = d == VER ? hq : wq;
+      const bool on = lane < 32 && (m >> lane & 1);
+      const unsigned long long b = __ballot(on);
+      if (on) s_line[wv][d][__popcll(b & ((1ull << lane) - 1))] = (uint8_t)lane;
+      // (the wave's own LDS writes: the LDS runs one wave's instructions in order; the memory clobber keeps
+      // the compiler from moving the reads above the writes)
+      asm volatile("" ::: "memory");
+      const int total = __popcll(b) * n, k = 2 * ch + d, base = c.item0[d];
+      if (base + total > A.cap || n > 32) { if (lane == 0 && total) atomicOr(A.err, 4); continue; }
+      for (int j = lane; j < total; j += 64)
+        A.items[(size_t)k * A.cap + base + j] = (uint32_t)i << 10 | (uint32_t)s_line[wv][d][j / n] << 5 | (uint32_t)(j % n);
+    }
   } else if (i < A.ncu + A.ntu) {
     const int t = i - A.ncu;
     const DbTu &tu = A.tu[t];
@@ -365,83 +446,72 @@ __global__ __launch_bounds__(256) void k_dbkp_maps(DbkPlanArgs A) {
   }
 }
 
-// one thread per (CU, direction) of the pass's channel type. The host planner runs the CUs of a CTU in
-// order, the chroma tree after the luma tree: pass 0 takes the chtype-0 CUs (they never overlap), pass 1
-// the chtype-1 ones — after a clear of the scratch maps in a dual-tree picture (the host's per-pass reset),
-// on top of the luma CUs' state for the chroma CUs of a local dual tree (the host's CU order within the CTU).
-// A shard plans the CUs within VVCR_LF_HALO rows of its own rows.
-template <int DIR>
-__global__ __launch_bounds__(64) void k_dbkp_cu(DbkPlanArgs A) {
-  const int i = blockIdx.x * 64 + threadIdx.x;
-  if (i >= A.ncu) return;
-  const DbCu &c = A.cu[i];
-  if ((c.flags & DBC_CHTYPE ? 1 : 0) != A.pass) return;
-  if (A.shard) {
-    const int ctu = 1 << A.ctu_log2;
-    int a[4];
-    Planner::cu_area(c, a);
-    const int ctu_y = a[1] & ~(ctu - 1);
-    if (ctu_y + ctu <= A.ly0 || ctu_y >= A.ly1) return;
-    if (!(a[1] + a[3] > A.ly0 && a[1] < A.ly1)) return;
+// The items of pass PASS, direction DIR (blockIdx.y), a lane each, grid-stride; local_dual: the luma pass
+// leaves each unit's edge flag and boundary strength in A.state, the chroma pass starts from it
+template <int DIR, int PASS>
+__device__ __forceinline__ void items_dir(const DbkPlanArgs &A, const int (*rp)[VVCR_MAX_REF]) {
+  const int k = 2 * PASS + DIR;
+  const int total = min(DIR == VER ? A.nitems[2 * PASS] : A.nitems[2 * PASS + 1], A.cap);
+  const bool local_dual = A.chroma_pass && !A.dual_tree;
+  for (int j0 = blockIdx.x * 256; j0 < total; j0 += gridDim.x * 256) {
+    const int j = j0 + threadIdx.x;
+    uint32_t wl = 0, wc = 0;
+    int x4 = 0, y4 = 0;
+    if (j < total) {
+      const uint32_t it = A.items[(size_t)k * A.cap + j];
+      const Cu R = load_cu(A, (int)(it >> 10));
+      const int o = (it >> 5) & 31, i = it & 31;
+      if (in_shard(A, R)) {
+      x4 = (R.a0 >> 2) + (DIR == VER ? o : i);
+      y4 = (R.a1 >> 2) + (DIR == VER ? i : o);
+      const int u = y4 * A.W4 + x4;
+      UnitState st{};
+      if (PASS == 1 && local_dual) {
+        const int v = A.state[DIR][u];
+        st.edge = v >> 7; st.bs = v & 63;
+      }
+      Unit<DIR>{A, rp, R, x4, y4}.run(o, st, wl, wc);
+      if (PASS == 0 && local_dual) A.state[DIR][u] = (uint8_t)(st.edge << 7 | (st.bs & 63));
+      }
+    }
+    append(A, 2 * DIR, wl, x4, y4);
+    append(A, 2 * DIR + 1, wc, x4, y4);
   }
-  Planner(A).deblock_cu(i, DIR);
 }
 
-// dense segment words -> the four lists (luma VER, chroma VER, luma HOR, chroma HOR), each list at
-// A.out + k * A.cap; a workgroup reserves its run of each list with one atomic
-__global__ __launch_bounds__(256) void k_dbkp_compact(DbkPlanArgs A, int n4) {
-  __shared__ int s_cnt[4][4], s_base[4];
-  const int i = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t wd[4] = {0, 0, 0, 0};
-  if (i < n4) { wd[0] = A.segL[0][i]; wd[1] = A.segC[0][i]; wd[2] = A.segL[1][i]; wd[3] = A.segC[1][i]; }
-  int rank[4];
+// the units on the edge lines of the CUs of one pass (pass 0: the luma tree, pass 1: the chroma tree), a
+// thread each; blockIdx.y: the direction
+template <int PASS>
+__global__ __launch_bounds__(256) void k_dbkp_units(DbkPlanArgs A) {
+  __shared__ int s_ref_poc[2][VVCR_MAX_REF];
+  if (threadIdx.x < 2 * VVCR_MAX_REF) {
+    int v = 0;
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const unsigned long long m = __ballot(wd[k] != 0);
-    rank[k] = __popcll(m & ((1ull << lane) - 1));
-    if (lane == 0) s_cnt[k][wv] = __popcll(m);
+    for (int k = 0; k < 2 * VVCR_MAX_REF; k++) v = threadIdx.x == k ? A.ref_poc[k / VVCR_MAX_REF][k % VVCR_MAX_REF] : v;   // constant indices
+    s_ref_poc[threadIdx.x / VVCR_MAX_REF][threadIdx.x % VVCR_MAX_REF] = v;
   }
   __syncthreads();
-  if (threadIdx.x < 4) {
-    const int k = threadIdx.x;
-    const int tot = s_cnt[k][0] + s_cnt[k][1] + s_cnt[k][2] + s_cnt[k][3];
-    s_base[k] = tot ? atomicAdd(&A.counts[k], tot) : 0;
-  }
-  __syncthreads();
-  if (i >= n4) return;
-  const int x4 = i % A.W4, y4 = i / A.W4;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    if (!wd[k]) continue;
-    int off = s_base[k] + rank[k];
-    for (int q = 0; q < wv; q++) off += s_cnt[k][q];
-    if (off < A.cap) A.out[(size_t)k * A.cap + off] = DbkSeg{(uint16_t)x4, (uint16_t)y4, wd[k]};
-    else atomicOr(A.err, 4);
-  }
+  if (blockIdx.y == 0) items_dir<VER, PASS>(A, s_ref_poc);
+  else items_dir<HOR, PASS>(A, s_ref_poc);
 }
 
 }  // namespace
 
-void launch_dbk_plan(const DbkPlanArgs &a0, hipStream_t s) {
-  DbkPlanArgs a = a0;
+void launch_dbk_plan(const DbkPlanArgs &a, hipStream_t s) {
   const size_t n4 = (size_t)a.W4 * a.H4;
-  for (int k = 0; k < 2; k++) {
-    VVCR_CHECK_HIP(hipMemsetAsync(a.cu_map[k], 0xff, n4 * sizeof(int32_t), s));
-    VVCR_CHECK_HIP(hipMemsetAsync(a.tu_map[k], 0xff, n4 * sizeof(int32_t), s));
-  }
-  VVCR_CHECK_HIP(hipMemsetAsync(a.scratch0, 0, a.scratch_bytes + a.dense_bytes, s));
+  // the four maps are one run (vvcr_api.cpp dbk_plan_args): one fill; the list lengths another
+  VVCR_CHECK_HIP(hipMemsetAsync(a.cu_map[0], 0xff, (size_t)((const char *)(a.tu_map[1] + n4) - (const char *)a.cu_map[0]), s));
   VVCR_CHECK_HIP(hipMemsetAsync(a.counts, 0, 4 * sizeof(int32_t), s));
+  const bool local_dual = a.chroma_pass && !a.dual_tree;
+  if (local_dual) VVCR_CHECK_HIP(hipMemsetAsync(a.state[0], 0, 2 * a.state_pitch, s));
   const int nm = a.ncu + a.ntu;
-  if (nm > 0) hipLaunchKernelGGL(k_dbkp_maps, dim3((nm + 255) / 256), dim3(256), 0, s, a);
-  const dim3 g((a.ncu + 63) / 64);
-  for (int pass = 0; pass < (a.chroma_pass ? 2 : 1); pass++) {
-    a.pass = pass;
-    if (pass == 1 && a.dual_tree) VVCR_CHECK_HIP(hipMemsetAsync(a.scratch0, 0, a.scratch_bytes, s));
-    if (a.ncu > 0) {
-      hipLaunchKernelGGL(k_dbkp_cu<0>, g, dim3(64), 0, s, a);
-      hipLaunchKernelGGL(k_dbkp_cu<1>, g, dim3(64), 0, s, a);
-    }
+  hipLaunchKernelGGL(k_dbkp_maps, dim3(std::max(1, (nm + 3) / 4)), dim3(256), 0, s, a);
+  for (int pass = 0; pass < 2; pass++) {
+    const int n = std::max(a.nitems[2 * pass], a.nitems[2 * pass + 1]);
+    if (n == 0) continue;
+    const dim3 g((unsigned)std::min(2048, (n + 255) / 256), 2);   // (grid-stride beyond)
+    if (pass == 0) hipLaunchKernelGGL(k_dbkp_units<0>, g, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_dbkp_units<1>, g, dim3(256), 0, s, a);
   }
-  hipLaunchKernelGGL(k_dbkp_compact, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, a, (int)n4);
   VVCR_CHECK_HIP(hipGetLastError());
 }

@@ -1,12 +1,13 @@
-// vvcr_mc.hip — motion-compensated prediction for gfx950 (k_mc_basic).
+// vvcr_mc.hip — motion-compensated prediction of plain (translational) inter CUs for gfx950: k_mc.
 //
-// k_mc_basic: two waves per McJob (<= 16x16 luma block + its 4:2:0 chroma, one or two lists); k_mc_tile:
-// four waves per 32x32 tile of a PU of at least 32x32. The reference windows are gathered in aligned
-// 4- / 8-sample chunks (every window of a wave in one phase, all loads in flight before the first LDS
-// write) into LDS, rows clamped to the picture and chunks that cross the left / right picture edge
-// loaded per sample with clamped columns (equivalent to VTM's edge-replicated 288-sample margin,
+// k_mc: one lane per cell (luma 4 columns x 8 rows, chroma 4 x 4 of one component) of a McJob, no LDS and
+// no barriers, one wave per workgroup (details at the kernel's section below). The lane reads its
+// reference windows straight from the planes as aligned dword runs of sample pairs; a job whose windows
+// may leave the picture goes to the k_mc<edge> instantiation, which clamps rows and shifts / replicates the
+// dwords of a row crossing the left / right edge (equivalent to VTM's edge-replicated 288-sample margin,
 // Picture::extendPicBorder Picture.cpp:737, plus clipMv Mv.cpp:54: every filter phase sums to 64, so a
-// clamped run of equal samples filters to the same value whatever the phase).
+// clamped run of equal samples filters to the same value whatever the phase). DMVR / BDOF jobs are
+// k_mc_bidir's (vvcr_mc_ext.hip), affine ones k_mc_affine's (vvcr_mc_affine.hip).
 //
 // Filtering is InterpolationFilter::filter<N,isVertical,isFirst,isLast> (InterpolationFilter.cpp:548-650)
 // as the H-then-V pass of xPredInterBlk (InterPrediction.cpp:784-803) for EVERY fraction: a zero fraction
@@ -15,11 +16,11 @@
 // ((16 X - 2^19) >> 6) == ((X - 2^15) >> 2); (16 X + 2^9) >> 10 == (X + 32) >> 6). One code path, no
 // divergence on fractions.
 //
-// Arithmetic is packed: samples are int16 pairs in LDS dwords and each tap pair is one v_dot2c_i32_i16.
-// An output whose first tap sits on an even sample uses the pair-aligned coefficients A = (c0,c1)(c2,c3)..,
+// Arithmetic is packed: samples are int16 pairs in dwords and each tap pair is one v_dot2c_i32_i16. An
+// output whose first tap sits on an even sample uses the pair-aligned coefficients A = (c0,c1)(c2,c3)..,
 // one starting on an odd sample the shifted set B = (0,c0)(c1,c2)..(c_{N-1},0) over the same aligned
-// pairs, so every LDS read is an aligned dword. The H pass writes its outputs transposed (column-major,
-// vertical pairs packed), so the V pass reads aligned vertical pairs the same way. Results combine like
+// pairs, so every read is an aligned dword. The H outputs of consecutive rows are packed into vertical
+// pairs as they arrive, so the V pass runs on aligned pairs the same way. Results combine like
 // AreaBuf::addAvg (Buffer.cpp:447), addWeightedAvg (BCW, Buffer.cpp:350), explicit WP
 // (WeightPrediction.cpp:157-378), the GEO blend (InterpolationFilter::xWeightedGeoBlk :997) or the
 // uni-prediction rounding, and leave as 8-byte row stores.
