@@ -1263,7 +1263,13 @@ int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle) {
   for (int l = 0; l < ctx->nlane; l++)
     if (ctx->lanes[l].held == &r) ctx->lanes[l].held = nullptr;
   std::lock_guard<std::mutex> g(ctx->prepared_mu);
-  if (ctx->spare.size() < 96) ctx->spare.push_back(std::move(ctx->prepared[handle]));
+  // released records keep their pinned staging and device arena for the next picture: pinning a 4K
+  // picture's ~15 MB staging buffer takes milliseconds, and with the previous cap of 96 records the bench's
+  // 272 pictures in flight re-allocated most of theirs every step (prepare 10.5 -> 4.1 ms per picture,
+  // 3.76 -> 4.76 Gpx/s, gpurun_out/benchab_*). The pool never exceeds the peak number of records alive at
+  // once; VVCR_SPARE caps it.
+  static const size_t keep = getenv("VVCR_SPARE") ? (size_t)atol(getenv("VVCR_SPARE")) : SIZE_MAX;
+  if (ctx->spare.size() < keep) ctx->spare.push_back(std::move(ctx->prepared[handle]));
   else ctx->prepared[handle].reset();
   return VVCR_OK;
   API_END

@@ -189,9 +189,7 @@ struct Unit {
   }
 
   // the motion part of xGetBoundaryStrengthSingle (:748-812)
-  __device__ __forceinline__ int motion_bs(int tmp) const {
-    const int u = y4 * A.W4 + x4, pu = ver ? u - 1 : u - A.W4;
-    const MotionRec mp = A.motion[pu], mq = A.motion[u];
+  __device__ __forceinline__ int motion_bs(const MotionRec &mp, const MotionRec &mq, int tmp) const {
     const int th = 8;
     // the same motion on both sides (one PU, or equal neighbours): no motion boundary
     if (mp.ref0 == mq.ref0 && mp.ref1 == mq.ref1 && mp.mv0x == mq.mv0x && mp.mv0y == mq.mv0y && mp.mv1x == mq.mv1x &&
@@ -226,7 +224,20 @@ struct Unit {
     const int px = x4 * 4, py = y4 * 4;
     const int u = y4 * A.W4 + x4, pu = ver ? u - 1 : u - A.W4;
     // P side inside the CU (else through the index maps); none across the picture edge (left / top false)
-    const bool pin = (ver ? x4 > (R.a0 >> 2) : y4 > (R.a1 >> 2)) || (ver ? x4 == 0 : y4 == 0);
+    const bool pedge = ver ? x4 == 0 : y4 == 0;
+    const bool pin = (ver ? x4 > (R.a0 >> 2) : y4 > (R.a1 >> 2)) || pedge;
+    // the P side's index-map values and CU record and the motion of both sides, loaded up front (one round
+    // of loads each; their uses below are conditional)
+    int mcu = 0, mcu1 = 0, mtu0 = 0, mtu1 = 0;
+    if (!pin) {
+      mcu = R.ch ? A.cu_map[1][pu] : A.cu_map[0][pu];
+      mcu1 = A.cu_map[1][pu];
+      mtu0 = A.tu_map[0][pu];
+      mtu1 = A.tu_map[1][pu];
+    }
+    const DbCu &cPr = A.cu[max(mcu, 0)];
+    const int fPm = pin ? 0 : (int)cPr.flags, qpPm = pin ? 0 : (int)cPr.qp;
+    const MotionRec mp = A.motion[pedge ? u : pu], mq = A.motion[u];   // (no motion edge at the picture edge)
     // step 1 (TU calls, then the PU's call and its sub-block lines)
 #pragma unroll
     for (int k = 0; k < MAXTU; k++) {
@@ -249,7 +260,7 @@ struct Unit {
       int X, Y;
       if (tu_edge<0>(k, x4, y4, X, Y)) {
         const int sizeQ = ver ? R.T[k].b[0][2] : R.T[k].b[0][3];
-        const int tp = pin ? own_tu(0, ver ? X - 1 : X, ver ? Y : Y - 1) : map_tu(A.tu_map[0][pu], ver ? X - 1 : X, ver ? Y : Y - 1);
+        const int tp = pin ? own_tu(0, ver ? X - 1 : X, ver ? Y : Y - 1) : map_tu(mtu0, ver ? X - 1 : X, ver ? Y : Y - 1);
         const int sizeP = ver ? A.tu[tp].b[0][2] : A.tu[tp].b[0][3];
         st.tedge = 1;
         const bool small = sizeP <= 4 || sizeQ <= 4;
@@ -258,7 +269,7 @@ struct Unit {
       }
       if (tu_edge<1>(k, x4, y4, X, Y)) {
         const int sizeQ = ver ? R.T[k].b[1][2] : R.T[k].b[1][3];
-        const int tp = pin ? own_tu(1, ver ? X - 1 : X, ver ? Y : Y - 1) : map_tu(A.tu_map[1][pu], 0, 0);
+        const int tp = pin ? own_tu(1, ver ? X - 1 : X, ver ? Y : Y - 1) : map_tu(mtu1, 0, 0);
         const int sizeP = ver ? A.tu[tp].b[1][2] : A.tu[tp].b[1][3];
         st.lq1 = st.lp1 = (sizeQ >= 8 && sizeP >= 8) ? 3 : 1;
       }
@@ -282,17 +293,17 @@ struct Unit {
       }
     }
     // the P-side CU of the CU's channel
-    const int cP = pin ? -1 : map_cu(A.cu_map[R.ch][pu]);
+    if (!pin) map_cu(mcu);   // (a hole: the error bit; record 0 stands in, as in the host planner's lookup)
     const int fQ = R.flags;
     // step 4: xGetBoundaryStrengthSingle (:674); an edge inside an inter, non-CIIP luma CU that is not a
     // transform edge has only the motion part
     if (st.edge && (!R.yv || o * 4 < (ver ? R.a2 : R.a3))) {
       const bool fast = R.yv && !(fQ & DBC_INTRA) && !(fQ & DBC_CIIP);
       if (fast && st.bs == 0 && o > 0) {
-        st.bs = motion_bs(0);
+        st.bs = motion_bs(mp, mq, 0);
       } else {
         const int marker = st.bs;
-        const int fP = pin ? fQ : A.cu[cP].flags;
+        const int fP = pin ? fQ : fPm;
         const bool iP = fP & DBC_INTRA, iQ = fQ & DBC_INTRA;
         if (iP || iQ) {
           const int bsY = (iP && (fP & DBC_BDPCM)) && (iQ && (fQ & DBC_BDPCM)) ? 0 : 2;
@@ -308,7 +319,7 @@ struct Unit {
               const int sh = R.yv ? 0 : 1;
               const int qx = px >> sh, qy = py >> sh;
               const int tq = own_tu(R.ch, qx, qy);
-              const int tp = !pin ? map_tu(A.tu_map[R.ch][pu], ver ? qx - 1 : qx, ver ? qy : qy - 1)
+              const int tp = !pin ? map_tu(R.ch ? mtu1 : mtu0, ver ? qx - 1 : qx, ver ? qy : qy - 1)
                                   : (R.ntu == 1 && !R.isp) ? tq : own_tu(R.ch, ver ? qx - 1 : qx, ver ? qy : qy - 1);
               const int cq = A.tu[tq].cbf, cp = A.tu[tp].cbf, jq = A.tu[tq].jccr, jp = A.tu[tp].jccr;
               if ((cq & 1) || (cp & 1)) tmp += bs_set(1, 0);
@@ -319,14 +330,14 @@ struct Unit {
             else if (ciip) st.bs = 1;
             else if (!R.yv) st.bs = tmp;
             else if (marker != 0 && marker != 3) st.bs = tmp;
-            else st.bs = motion_bs(tmp);
+            else st.bs = motion_bs(mp, mq, tmp);
           }
         }
       }
     }
     // step 5: the segment words (xEdgeFilterLuma / xEdgeFilterChroma bookkeeping)
     if (R.yv && (st.bs & 3)) {
-      const int qpP = pin ? R.qp : A.cu[cP].qp, fP = pin ? fQ : A.cu[cP].flags;
+      const int qpP = pin ? R.qp : qpPm, fP = pin ? fQ : fPm;
       const int qp = (qpP + R.qp + 1) >> 1;
       int lp = st.lp0, lq = st.lq0;
       bool pl = false, ql = false;
@@ -344,9 +355,8 @@ struct Unit {
       const int bS0 = (st.bs >> 2) & 3, bS1 = (st.bs >> 4) & 3;
       if (!((ver && (r % parts + o) % 4) || (!ver && (r / parts + o) % 4)) && (bS0 || bS1)) {
         // the P-side CU: of the chroma map when the luma one is of a tree-split area or the picture is dual tree
-        int cpi = pin ? -1 : cP;
-        if (!pin && R.ch == 0 && ((A.cu[cP].flags & DBC_TREE) || A.dual_tree)) cpi = map_cu(A.cu_map[1][pu]);
-        const int fP = cpi < 0 ? fQ : A.cu[cpi].flags;
+        int fP = pin ? fQ : fPm;
+        if (!pin && R.ch == 0 && ((fPm & DBC_TREE) || A.dual_tree)) fP = A.cu[map_cu(mcu1)].flags;
         const bool large = st.lp1 >= 3 && st.lq1 >= 3;
         const bool ctbh = !ver && (py & ((1 << A.ctu_log2) - 1)) == 0;
         uint32_t w = (uint32_t)large << 4 | (uint32_t)ctbh << 19;
@@ -356,7 +366,7 @@ struct Unit {
         const int chP = (fP & DBC_CHTYPE) ? 1 : 0, shP = (fP & DBC_YVALID) ? 0 : 1;
         const int p1x = px >> shP, p1y = py >> shP;
         const int tp = pin ? own_tu(chP, ver ? p1x - 1 : p1x, ver ? p1y : p1y - 1)
-                           : map_tu(A.tu_map[chP][pu], ver ? p1x - 1 : p1x, ver ? p1y : p1y - 1);
+                           : map_tu(chP ? mtu1 : mtu0, ver ? p1x - 1 : p1x, ver ? p1y : p1y - 1);
 #pragma unroll
         for (int k = 0; k < 2; k++) {
           const int b = k ? bS1 : bS0;
