@@ -1266,13 +1266,10 @@ void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb
   Deriver d(p, field, geoRows, dpb);
   d.run();
   motionRows.alloc(field.size(), false);
-  for (size_t i = 0; i < field.size(); i++) {
-    const Mi &m = field[i];
-    MotionRec &o = motionRows.data()[i];
-    o.ref0 = (int8_t)m.ref[0]; o.ref1 = (int8_t)m.ref[1]; o.inter_dir = (uint8_t)m.interDir;
-    o.flags = (uint8_t)((m.isInter ? 1 : 0) | (m.altHpel ? 2 : 0) | (m.bcw << 2));
-    o.mv0x = m.mv[0][0]; o.mv0y = m.mv[0][1]; o.mv1x = m.mv[1][0]; o.mv1y = m.mv[1][1];
-  }
+  // the MotionRec prefix of every Mi (vvcp_mv.h)
+  const uint8_t *src = (const uint8_t *)field.data();
+  uint8_t *dst = (uint8_t *)motionRows.data();
+  for (size_t i = 0, n = field.size(); i < n; i++) std::memcpy(dst + i * sizeof(MotionRec), src + i * sizeof(Mi), sizeof(MotionRec));
 }
 
 void refine_motion(const PictureUnit &p, MotionField &&field, const int32_t *deltas, int64_t ndeltas,

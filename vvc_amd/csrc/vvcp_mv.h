@@ -3,6 +3,7 @@
 // PU:: candidate-list tools of CommonLib/UnitTools.cpp), in decoding order, CU by CU, with the
 // history-based candidate table (CodingStructure::addMiToLut) and the collocated picture's motion.
 #pragma once
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -14,17 +15,22 @@
 
 namespace vvcp {
 
-// MotionInfo (MotionInfo.h:101) of one 4x4 luma unit
+// MotionInfo (MotionInfo.h:101) of one 4x4 luma unit. Its first 20 bytes are a MotionRec (the motion
+// rows handed to the reconstruction path: ref0, ref1, inter_dir, flags = is_inter | alt_hpel << 1 |
+// bcw << 2, the four MV components), so the rows are a prefix copy of the field, not a field-by-field
+// conversion (r04: a quarter of the derivation time).
 struct Mi {
-  bool isInter = false;
-  int8_t interDir = 0;
-  bool altHpel = false;
-  uint8_t bcw = 0;
-  uint16_t slice = 0;
-  int16_t ref[2] = {-1, -1};
-  int32_t mv[2][2] = {{0, 0}, {0, 0}};
+  int8_t ref[2];
+  int8_t interDir;
+  uint8_t isInter : 1, altHpel : 1, bcw : 6;
+  int32_t mv[2][2];
+  uint16_t slice;
+  uint16_t pad_;
+  Mi() : ref{-1, -1}, interDir(0), isInter(0), altHpel(0), bcw(0), mv{{0, 0}, {0, 0}}, slice(0), pad_(0) {}
   bool same(const Mi &o) const;   // MotionInfo::operator==
 };
+static_assert(sizeof(Mi) == 24 && offsetof(Mi, mv) == offsetof(MotionRec, mv0x) && offsetof(Mi, interDir) == offsetof(MotionRec, inter_dir),
+              "Mi starts with a MotionRec");
 
 // Reference structure of one slice of a picture (what getColocatedMVP reads of the collocated picture)
 struct SliceRefs {
