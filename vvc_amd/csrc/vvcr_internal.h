@@ -150,12 +150,20 @@ struct McParams {
 // 4 columns x 4 rows of one component) for every list of its job. The job array holds the 32x32 tiles,
 // then the smaller blocks, grouped in classes of one size (w, h); a class's cells are numbered job-major
 // from lcell0 / ccell0, each range padded to a multiple of 64, so no wave straddles two classes.
-constexpr int MC_MAXCLS = 24;
+// MC_BI_SPLIT=1: the cells of bi-predicted jobs (classes of their own) take two adjacent lanes, one list each
+// (vvcr_mc.hip mc_cell): a class's cells per job double. Measured slower (r05, mc_bench in isolation, 4K B
+// pictures: QP27 33.4 vs 30.2 us, QP32 26.1 vs 25.5 us; gpurun_out/r05q_split): the doubled bi waves cost
+// more than the halved chain of each. Kept as an A/B option, off.
+#ifndef MC_BI_SPLIT
+#define MC_BI_SPLIT 0
+#endif
+constexpr int MC_MAXCLS = 32;
 struct McClassTable {
   int32_t n = 0;                      // classes
   int32_t job0[MC_MAXCLS + 1] = {};   // first job of the class in the combined job array; [n] = jobs in all
   int32_t w[MC_MAXCLS] = {}, h[MC_MAXCLS] = {};
   int32_t edge[MC_MAXCLS] = {};       // the class's windows may leave the picture (mc_job_edge): clamped path
+  int32_t split[MC_MAXCLS] = {};      // bi-predicted jobs, two lanes per cell (MC_BI_SPLIT)
   int32_t lcell0[MC_MAXCLS + 1] = {}; // first luma cell of each class; [n] = luma cells in all (lanes)
   int32_t ccell0[MC_MAXCLS + 1] = {}; // chroma cells likewise
 };

@@ -378,7 +378,8 @@ __device__ __forceinline__ CellWin cell_win(const McParams &P, const McJob &J, i
 // rounding), stored as rows of up to 4 samples. (x, y): the cell origin in the component plane; nc / nr:
 // the valid columns / rows of the cell (blocks narrower or shorter than a cell).
 template <int N, int R, bool EDGE>
-__device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, const McJob &J, int comp, int x, int y, int nc, int nr) {
+__device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, const McJob &J, int comp, int x, int y, int nc, int nr,
+                                        int half, uint2 (*sp0)[64]) {
   const bool l0 = J.flags & MC_L0, l1 = J.flags & MC_L1, bi = l0 && l1;
   const int bd = P.bd, maxv = (1 << bd) - 1, headRoom = max(2, IF_INTERNAL_PREC - bd);
   const int sh1 = IF_FILTER_PREC - headRoom;
@@ -444,6 +445,66 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
 #define P0_LO(o) p0[o][0]
 #define P0_HI(o) p0[o][1]
 #endif
+#if MC_BI_SPLIT
+  if (bi) {
+    // The cell's two lists on two adjacent lanes (half = this lane's list): each lane filters its list's R
+    // rows, the pair swaps half of them (DPP quad_perm [1,0,3,2]), and each lane combines and stores R / 2
+    // rows: the dependent chain of one list per lane instead of two (the QP32 launches are one round of
+    // waves whose bi-predicted ones set the length, r05 per-wave trace).
+    const int o0 = half * (R / 2);   // this lane's output rows [o0, o0 + R / 2)
+    const int ln = threadIdx.x & 63;
+    const CellWin W0 = cell_win(P, J, comp, half, x, y);
+    // the rows wait in LDS (8 B per row and lane): in registers they pushed the kernel to 154 VGPRs
+    cell_filter<N, R, EDGE>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
+      sp0[o][ln] = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+    }, [](int) {});
+    // (the partner lane's rows: the LDS runs one wave's instructions in order; the clobber keeps the
+    // compiler from moving the reads above the writes)
+    asm volatile("" ::: "memory");
+    // its residual rows, all in flight at once (during the filter they would cost registers: spills)
+    uint32_t rk[R / 2][2];
+    if (addResi) {
+#pragma unroll
+      for (int k = 0; k < R / 2; k++) {
+        const int16_t *rr = rsrc + (size_t)min(o0 + k, nr - 1) * rstride;
+        rk[k][1] = 0;
+        if (wide) { const uint2 v = *(const uint2 *)rr; rk[k][0] = v.x; rk[k][1] = v.y; }
+        else { rk[k][0] = ((const uint32_t *)rr)[0]; if (nc == 4) rk[k][1] = ((const uint32_t *)rr)[1]; }
+      }
+    }
+    const Comb CB = comb_setup(WT, J, comp, bd, cx, cy);
+#pragma unroll
+    for (int k = 0; k < R / 2; k++) {
+      const int o = o0 + k;
+      const uint2 l0 = sp0[o][ln & ~1], l1 = sp0[o][ln | 1];   // list 0 (half 0's lane), list 1
+      const uint32_t a0 = l0.x, a1 = l0.y, b0 = l1.x, b1 = l1.y;
+      if (o >= nr) continue;
+      const int u[4] = {lo16(a0), hi16(a0), lo16(a1), hi16(a1)}, v[4] = {lo16(b0), hi16(b0), lo16(b1), hi16(b1)};
+      int a[4];
+      if (avg) {   // AreaBuf::addAvg (Buffer.cpp:447)
+        const int shiftNum = headRoom + 1, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
+#pragma unroll
+        for (int q = 0; q < 4; q++) a[q] = clampi((u[q] + v[q] + offset) >> shiftNum, 0, maxv);
+      } else {     // bi WP / GEO / BCW
+#pragma unroll
+        for (int q = 0; q < 4; q++) a[q] = comb_apply(CB, q, o, u[q], v[q], maxv);
+      }
+      int16_t *qd = dst + (size_t)o * ostride;
+      if (addResi) {
+        a[0] = clampi(a[0] + lo16(rk[k][0]), 0, maxv); a[1] = clampi(a[1] + hi16(rk[k][0]), 0, maxv);
+        a[2] = clampi(a[2] + lo16(rk[k][1]), 0, maxv); a[3] = clampi(a[3] + hi16(rk[k][1]), 0, maxv);
+      }
+      if (wide) *(uint2 *)qd = make_uint2(pk(a[0], a[1]), pk(a[2], a[3]));
+      else {
+        ((uint32_t *)qd)[0] = pk(a[0], a[1]);
+        if (nc == 4) ((uint32_t *)qd)[1] = pk(a[2], a[3]);
+      }
+    }
+    return;
+  }
+#else
+  (void)half;
+#endif
   if (bi) {
     const CellWin W0 = cell_win(P, J, comp, 0, x, y);
     cell_filter<N, R, EDGE>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
@@ -490,7 +551,7 @@ __device__ __forceinline__ McJob load_job(const McJob *p) {
 
 // Grid: the luma cells of every class (ct.lcell0[ct.n] lanes), then the chroma cells, MC_WG lanes per
 // workgroup; the class of a lane is wave-uniform (class ranges are whole waves).
-__device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restrict__ jobs, const McClassTable &ct, int b
+__device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restrict__ jobs, const McClassTable &ct, uint2 (*sp0)[64], int b
 #ifdef VVCR_MC_PROF
                                         , unsigned long long &tag
 #endif
@@ -502,14 +563,17 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
   // the class of the wave by a scan over static fields (wave-uniform selects; a class index used to read
   // the kernel argument would make it a per-lane indexed copy)
   int w = ct.w[0], h = ct.h[0], c0 = luma ? ct.lcell0[0] : ct.ccell0[0], jbase = ct.job0[0], jend = ct.job0[1], ed = ct.edge[0];
+  int sp = ct.split[0];
 #pragma unroll
   for (int q = 1; q < MC_MAXCLS; q++)
     if (q < ct.n && gw >= (luma ? ct.lcell0[q] : ct.ccell0[q])) {
       w = ct.w[q]; h = ct.h[q]; c0 = luma ? ct.lcell0[q] : ct.ccell0[q]; jbase = ct.job0[q]; jend = ct.job0[q + 1]; ed = ct.edge[q];
+      sp = ct.split[q];
     }
   const int i = g - c0;
-  const int per = luma ? mc_luma_cells(w, h, ed) : mc_chroma_cells(w, h);   // a power of two
-  const int jn = i >> (__ffs(per) - 1), s = i & (per - 1);
+  const int per = (luma ? mc_luma_cells(w, h, ed) : mc_chroma_cells(w, h)) << sp;   // a power of two
+  const int jn = i >> (__ffs(per) - 1), s2 = i & (per - 1);
+  const int s = s2 >> sp, half = s2 & sp;   // split classes: adjacent lanes share a cell, one list each
 #ifdef VVCR_MC_PROF
   tag = (unsigned long long)luma << 63 | (unsigned long long)(w & 255) << 8 | (h & 255);
 #endif
@@ -529,11 +593,11 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
   // the path is a class property (wave-uniform): edge classes take the clamped gathers, the others none
   if (luma) {
     const int ncx = w >> 2, cx = s & (ncx - 1), cy = s >> (__ffs(ncx) - 1);
-    if (ed) mc_cell<8, 8, true>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
+    if (ed) mc_cell<8, 8, true>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy), half, sp0);
 #if MC_TALL_LUMA
-    else if (mc_tall_luma(h, false)) mc_cell<8, 16, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 16 * cy, 4, 16);
+    else if (mc_tall_luma(h, false)) mc_cell<8, 16, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 16 * cy, 4, 16, half, sp0);
 #endif
-    else mc_cell<8, 8, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
+    else mc_cell<8, 8, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy), half, sp0);
   } else {
     const int cw = w >> 1, chh = h >> 1;
     const bool tall = mc_tall_chroma(h);   // class-uniform: 8-row chroma cells (mc_chroma_cells)
@@ -542,15 +606,17 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
     const int cx = t & (ncx - 1), cy = t >> (__ffs(ncx) - 1);   // ncx is a power of two
     const int ox = (J.x >> 1) + 4 * cx, nc = min(4, cw - 4 * cx);
     if (ed) {
-      if (tall) mc_cell<4, 8, true>(P, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8);
-      else mc_cell<4, 4, true>(P, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy));
+      if (tall) mc_cell<4, 8, true>(P, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8, half, sp0);
+      else mc_cell<4, 4, true>(P, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy), half, sp0);
     } else {
-      if (tall) mc_cell<4, 8, false>(P, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8);
-      else mc_cell<4, 4, false>(P, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy));
+      if (tall) mc_cell<4, 8, false>(P, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8, half, sp0);
+      else mc_cell<4, 4, false>(P, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy), half, sp0);
     }
   }
 }
 __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_PER_EU))) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct) {
+  // split bi cells: the rows of one list per lane, 8 B per row (MC_WG is one wave)
+  __shared__ uint2 s_rows[8][64];
 #ifdef VVCR_MC_PROF
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
@@ -558,9 +624,9 @@ __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_
 #endif
 #ifdef VVCR_MC_PROF
   unsigned long long tag = 0;
-#define MC_BODY(b) mc_body(P, jobs, ct, b, tag)
+#define MC_BODY(b) mc_body(P, jobs, ct, s_rows, b, tag)
 #else
-#define MC_BODY(b) mc_body(P, jobs, ct, b)
+#define MC_BODY(b) mc_body(P, jobs, ct, s_rows, b)
 #endif
   // (A persistent grid walking the blocks was slower, 47.3 vs 41.4 us, and doubled the kernel's code:
   // removed, r04.)
