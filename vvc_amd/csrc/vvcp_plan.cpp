@@ -2,6 +2,9 @@
 // path's host-only planner (vvcr_picture_*, include/vvcr.h) without leaving native code: the same
 // create / submit / loop-filter / plan sequence a ctypes producer makes (vvc_amd/stream.py), with the
 // rows, picture parameters and ALF filters taken straight from the parser's state.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "vvcp.h"
@@ -28,6 +31,14 @@ extern "C" int vvcp_plan_picture_rows(vvcp_stream *h, int32_t idx, const vvcr_se
   *out = nullptr;
   vvcp::PictureUnit &p = *h->s.pics[idx];
   if (!p.derived || p.handedOver) return VVCR_E_STATE;
+  static const bool prof = getenv("VVCR_PLAN_PROF") != nullptr;   // diagnostics: phase times to stderr
+  auto tp = std::chrono::steady_clock::now();
+  auto mark = [&](const char *n) {
+    if (!prof) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "  vvcp %-10s %.2f ms\n", n, std::chrono::duration<double, std::milli>(t - tp).count());
+    tp = t;
+  };
   vvcr_pic_params pp;
   vvcp::AlfFilters alf;
   try {
@@ -45,6 +56,7 @@ extern "C" int vvcp_plan_picture_rows(vvcp_stream *h, int32_t idx, const vvcr_se
       if (!ref_slot) return VVCR_E_ARG;
       pp.ref_slot[l][r] = ref_slot[l * VVCR_MAX_REF + r];
     }
+  mark("params");
   vvcr_picture *pic = nullptr;
   int rc = vvcr_picture_create(sp, &pp, &pic);
   if (rc) return fail(nullptr, rc, "vvcr_picture_create");
@@ -62,7 +74,9 @@ extern "C" int vvcp_plan_picture_rows(vvcp_stream *h, int32_t idx, const vvcr_se
     D.geo.assign(p.geo.begin(), p.geo.end());
     D.cu_map[0] = std::move(S.map[0]);
     D.cu_map[1] = std::move(S.map[1]);
+    mark("copy");
     vvcr_picture_adopt(pic, std::move(D));
+    mark("adopt");
   } catch (const VvcrError &e) {
     vvcp::set_api_error(std::string("vvcr_picture_submit: ") + e.msg);
     vvcr_picture_destroy(pic);
@@ -97,7 +111,9 @@ extern "C" int vvcp_plan_picture_rows(vvcp_stream *h, int32_t idx, const vvcr_se
   }
   rc = vvcr_picture_set_loop_filter_params(pic, S.sao.data(), p.sps.alf ? &A : nullptr);
   if (rc) return fail(pic, rc, "vvcr_picture_set_loop_filter_params");
+  mark("lf_params");
   rc = vvcr_picture_plan(pic, stage_mask);
+  mark("plan");
   if (rc) return fail(pic, rc, "vvcr_picture_plan");
   p.handedOver = true;
   *out = pic;

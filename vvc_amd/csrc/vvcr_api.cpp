@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -485,10 +486,19 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
   // second thread beside the work lists and the intra plan (a 4K intra picture plans in ~100 ms each).
   std::exception_ptr dbk_err;
   std::thread dbk_thread;
+  static const bool prof = getenv("VVCR_PLAN_PROF") != nullptr;   // diagnostics: phase times to stderr
+  auto tp = std::chrono::steady_clock::now();
+  auto mark = [&](const char *n) {
+    if (!prof) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "  plan %-10s %.2f ms\n", n, std::chrono::duration<double, std::milli>(t - tp).count());
+    tp = t;
+  };
   if ((mask & VVCR_STAGE_DBK) && b.dbk_gpu) {
     if (b.desc.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4))
       throw VvcrError(VVCR_E_ARG, "deblocking: the motion field does not cover the picture");
     pack_dbk_inputs(sp, pp, b.desc, b.dbkg);
+    mark("dbk_pack");
   } else if (mask & VVCR_STAGE_DBK)
     dbk_thread = std::thread([&] {
       try {
@@ -499,9 +509,11 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
     });
   try {
     if (mask & (VVCR_STAGE_RESID | VVCR_STAGE_INTER)) build_work_lists(sp, pp, b.desc, b.wl, fuse);
+    mark("work_lists");
     if ((mask & VVCR_STAGE_INTER) && b.wl.n_unsupported_inter)
       throw VvcrError(VVCR_E_UNSUPPORTED, std::to_string(b.wl.n_unsupported_inter) + " inter CUs use tools not supported yet");
     if (mask & VVCR_STAGE_INTRA) plan_intra(sp, pp, b.desc, b.intra, fuse);
+    mark("intra");
   } catch (...) {
     if (dbk_thread.joinable()) dbk_thread.join();
     throw;

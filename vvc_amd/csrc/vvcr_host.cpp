@@ -56,10 +56,35 @@ void push_mc(WorkLists &wl, int x0, int y0, int w, int h, const McJob &proto) {
   push_tiles(wl.mc_basic, x0, y0, w, h, proto);
 }
 
+static bool mc_bi(const McJob &j) { return (j.flags & (MC_L0 | MC_L1)) == (MC_L0 | MC_L1); }
+
+// Jobs in descending (w, h), bi-predicted first within a size, stable: a counting sort over the 2 x 8 x 8
+// power-of-two size buckets (a comparison sort of a picture's SbTMVP sub-blocks took milliseconds).
+void sort_by_size_bi(bigbuf::vec<McJob> &v) {
+  auto lg = [](int x) { return x > 0 && (x & (x - 1)) == 0 && x <= 128 ? __builtin_ctz(x) : -1; };
+  int cnt[128] = {};
+  for (const McJob &j : v) {
+    const int a = lg(j.w), b = lg(j.h);
+    if (a < 0 || b < 0) {   // (never for VVC block sizes) the comparison sort
+      std::stable_sort(v.begin(), v.end(), [](const McJob &x, const McJob &y) {
+        const int kx = x.w << 8 | x.h, ky = y.w << 8 | y.h;
+        if (kx != ky) return kx > ky;
+        return mc_bi(x) > mc_bi(y);
+      });
+      return;
+    }
+    cnt[127 - ((a * 8 + b) * 2 + (mc_bi(j) ? 1 : 0))]++;   // bucket order = the sort order
+  }
+  int pos[128], run = 0;
+  for (int k = 0; k < 128; k++) { pos[k] = run; run += cnt[k]; }
+  bigbuf::vec<McJob> out(v.size());
+  for (const McJob &j : v) out[pos[127 - ((lg(j.w) * 8 + lg(j.h)) * 2 + (mc_bi(j) ? 1 : 0))]++] = j;
+  v.swap(out);
+}
+
 // A k_mc class table over job arrays laid out one after another from job index base (each flagged: its
 // windows may leave the picture): one class per run of equal (w, h) and, with MC_BI_SPLIT, equal
 // bi-prediction (the lists sort bi-predicted jobs first within a size), its cell ranges padded to whole waves.
-static bool mc_bi(const McJob &j) { return (j.flags & (MC_L0 | MC_L1)) == (MC_L0 | MC_L1); }
 void build_mc_classes(McClassTable &ct, std::initializer_list<std::pair<const bigbuf::vec<McJob> *, bool>> lists, int base) {
   ct = McClassTable();
   int lc = 0, cc = 0;
@@ -331,12 +356,22 @@ AffList affine_list(const vvcr_pic_params &pp, const vvcr_cu &c, const vvcr_pu &
 
 void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl,
                       bool fuse) {
+  static const bool prof = getenv("VVCR_PLAN_PROF") != nullptr;   // diagnostics: phase times to stderr
+  auto tp = std::chrono::steady_clock::now();
+  auto mark = [&](const char *n) {
+    if (!prof) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "    wl %-8s %.2f ms\n", n, std::chrono::duration<double, std::milli>(t - tp).count());
+    tp = t;
+  };
   wl.clear();
   build_tb_jobs(sp, pp, d, wl.tb, wl.coef);
+  mark("tb");
   if (fuse) {   // the reconstruction stages run together: the residual reads are known, zero only those
     build_zero_jobs(pp, d, wl.tb);
     wl.zero_filled = true;
   }
+  mark("zero");
   // small blocks first (64-lane workgroups), then the large ones (256 lanes)
   wl.tb_small = (int)(std::stable_partition(wl.tb.begin(), wl.tb.end(), [](const TbJob &j) { return j.w * j.h <= 256; }) - wl.tb.begin());
   const int W4 = sp.width / 4;
@@ -385,15 +420,27 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       const bool alt = c.imv == IMV_HPEL;
       const int bcw = p.ciip ? 2 : c.bcw;   // BCW is not applied to CIIP (InterPrediction.cpp:1397)
       if (p.mrgtype == MRG_TYPE_SUBPU_ATMVP) {
-        // xSubPuMC (InterPrediction.cpp:289): 8x8 sub-blocks with their own motion, no BDOF / DMVR
-        // (SbTMVP candidates of the sub-block merge list also carry cu.affine; the merge type decides)
-        for (int y = 0; y < p.h; y += 8)
-          for (int x = 0; x < p.w; x += 8) {
-            const MotionRec &m = d.motion[(size_t)((p.y + y) >> 2) * W4 + ((p.x + x) >> 2)];
+        // xSubPuMC (InterPrediction.cpp:283-360): 8x8 sub-blocks with their own motion, no BDOF / DMVR
+        // (SbTMVP candidates of the sub-block merge list also carry cu.affine; the merge type decides).
+        // Like the reference, runs of sub-blocks with the same motion along the PU's longer side are one
+        // prediction (:307-345; the same samples, fewer and larger jobs).
+        const bool ver = p.h > p.w;
+        const int fe = ver ? p.w : p.h, se = ver ? p.h : p.w;
+        auto mot = [&](int a, int b) -> const MotionRec & {   // the sub-block at (first, second) offsets
+          const int x = ver ? a : b, y = ver ? b : a;
+          return d.motion[(size_t)((p.y + y) >> 2) * W4 + ((p.x + x) >> 2)];
+        };
+        for (int a = 0; a < fe; a += 8)
+          for (int b = 0; b < se;) {
+            const MotionRec &m = mot(a, b);
+            int len = 8;
+            while (b + len < se && std::memcmp(&mot(a, b + len), &m, sizeof(MotionRec)) == 0) len += 8;
             McJob j = make_job(pp, m.inter_dir, m.ref0, m.ref1, m.mv0x, m.mv0y, m.mv1x, m.mv1y, bcw, alt);   // BCW of the CU (xWeightedAverage reads pu.cu->BcwIdx)
             set_wp(pp, j, m.ref0, m.ref1, c.bcw);
             j.flags |= recon;
-            push_mc(wl, p.x + x, p.y + y, std::min(8, p.w - x), std::min(8, p.h - y), j);
+            const int x = ver ? a : b, y = ver ? b : a;
+            push_mc(wl, p.x + x, p.y + y, ver ? std::min(8, p.w - x) : std::min(len, p.w - x), ver ? std::min(len, p.h - y) : std::min(8, p.h - y), j);
+            b += len;
           }
         continue;
       }
@@ -454,6 +501,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       push_mc(wl, p.x, p.y, p.w, p.h, j);
     }
   }
+  mark("cus");
   // bi-predicted work first (about twice the work of a uni job): the long jobs start in the first
   // dispatch rounds instead of forming the launch's tail
   auto bi_first = [](bigbuf::vec<McJob> &v) {
@@ -462,11 +510,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   bi_first(wl.mc_tile);
   // the small blocks by size class (k_mc cell classes), bi-predicted first within a class: a wave's lanes
   // then share one size and mostly one prediction direction
-  std::stable_sort(wl.mc_basic.begin(), wl.mc_basic.end(), [](const McJob &a, const McJob &b) {
-    const int ka = a.w << 8 | a.h, kb = b.w << 8 | b.h;
-    if (ka != kb) return ka > kb;
-    return ((a.flags & MC_L0) && (a.flags & MC_L1)) > ((b.flags & MC_L0) && (b.flags & MC_L1));
-  });
+  sort_by_size_bi(wl.mc_basic);
   // jobs whose windows may leave the picture: to the edge list (same order rules), the rest stay
   auto split_edge = [&](bigbuf::vec<McJob> &v) {
     auto mid = std::stable_partition(v.begin(), v.end(), [&](const McJob &j) { return !mc_job_edge(j, sp.width, sp.height); });
@@ -475,12 +519,9 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   };
   split_edge(wl.mc_tile);
   split_edge(wl.mc_basic);
-  std::stable_sort(wl.mc_edge.begin(), wl.mc_edge.end(), [](const McJob &a, const McJob &b) {
-    const int ka = a.w << 8 | a.h, kb = b.w << 8 | b.h;
-    if (ka != kb) return ka > kb;
-    return ((a.flags & MC_L0) && (a.flags & MC_L1)) > ((b.flags & MC_L0) && (b.flags & MC_L1));
-  });
+  sort_by_size_bi(wl.mc_edge);
   // the edge classes first: their waves (longer, per-row clamped gathers) start in the first round
+  mark("sorts");
   build_mc_classes(wl.mc_ct, {{&wl.mc_edge, true}, {&wl.mc_tile, false}, {&wl.mc_basic, false}}, 0);
   std::stable_partition(wl.aff_jobs.begin(), wl.aff_jobs.end(), [&](const AffJob &j) {
     const AffPu &U = wl.aff_pu[j.pu];
