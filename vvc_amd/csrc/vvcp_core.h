@@ -135,32 +135,26 @@ struct Cabac {
 #ifdef VVCP_TRACE   // bin trace in the format of the reference's D_CABAC channel (BinDecoder.cpp:315)
   int traceCount = 0;
 #endif
-  unsigned bin(unsigned id) {   // TBinDecoder::decodeBin
+  unsigned bin(unsigned id) {   // TBinDecoder::decodeBin, with the LPS / MPS choice as masks
     CtxModel &m = ctx[id];
-    const uint8_t st = m.state();
-    unsigned b = st >> 7;
-    uint16_t q = st;
-    if (q & 0x80) q ^= 0xff;
+    const unsigned st = m.state();
+    const unsigned mps = st >> 7;
+    const unsigned q = st ^ ((0u - mps) & 0xff);   // the LPS probability state
     const uint32_t lps = (((q >> 2) * (range >> 5)) >> 1) + 4;
 #ifdef VVCP_TRACE
     fprintf(stderr, "%d %d %d  [%d:%d]  %2d(MPS=%d)    -  ", traceCount++, id, range, range - lps, lps, st, value < ((range - lps) << 7));
 #endif
     range -= lps;
     const uint32_t sr = range << 7;
-    if (value < sr) {
-      if (range < 256) {
-        range <<= 1; value <<= 1;
-        if (++bitsNeeded >= 0) { value += byte() << bitsNeeded; bitsNeeded -= 8; }
-      }
-    } else {
-      b = 1 - b;
-      static const uint8_t renorm[32] = {6, 5, 4, 4, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
-      const int n = renorm[lps >> 3];
-      value = (value - sr) << n;
-      range = lps << n;
-      bitsNeeded += n;
-      if (bitsNeeded >= 0) { value += byte() << bitsNeeded; bitsNeeded -= 8; }
-    }
+    const uint32_t lpsMask = (uint32_t)((int32_t)(sr - 1 - value) >> 31);   // all ones when value >= sr
+    value -= sr & lpsMask;
+    range ^= (range ^ lps) & lpsMask;
+    const unsigned b = mps ^ (lpsMask & 1);
+    const int n = __builtin_clz(range) - 23;   // renormalise to 9 bits (range in [256, 510])
+    range <<= n;
+    value <<= n;
+    bitsNeeded += n;
+    if (bitsNeeded >= 0) { value += byte() << bitsNeeded; bitsNeeded -= 8; }
     m.update(b);
 #ifdef VVCP_TRACE
     fprintf(stderr, "%d\n", b);
@@ -171,18 +165,46 @@ struct Cabac {
     value += value;
     if (++bitsNeeded >= 0) { value += byte(); bitsNeeded = -8; }
     const uint32_t sr = range << 7;
-    unsigned b = 0;
-    if (value >= sr) { value -= sr; b = 1; }
+    const uint32_t mask = (uint32_t)((int32_t)(sr - 1 - value) >> 31);
+    value -= sr & mask;
 #ifdef VVCP_TRACE
-    fprintf(stderr, "%d  %d  EP=%d \n", traceCount++, range, b);
+    fprintf(stderr, "%d  %d  EP=%d \n", traceCount++, range, mask & 1);
 #endif
-    return b;
+    return mask & 1;
   }
-  unsigned eps(unsigned n) {   // decodeBinsEP (bit-serial form, same result as the batched one)
+  // decodeBinsEP: n bypass bins, the most significant first; whole bytes are shifted in at once
+#ifdef VVCP_TRACE
+  unsigned eps(unsigned n) {
     unsigned v = 0;
     for (unsigned i = 0; i < n; i++) v = (v << 1) | ep();
     return v;
   }
+#else
+  unsigned eps(unsigned n) {
+    unsigned v = 0;
+    for (; n > 8; n -= 8) {   // 8 bins: a byte in, then 8 compare-subtract steps against range << 7..14
+      value = (value << 8) + (byte() << (8 + bitsNeeded));
+      uint32_t sr = range << 15;
+      for (int i = 0; i < 8; i++) {
+        sr >>= 1;
+        const uint32_t mask = (uint32_t)((int32_t)(sr - 1 - value) >> 31);
+        value -= sr & mask;
+        v = v + v + (mask & 1);
+      }
+    }
+    bitsNeeded += (int)n;
+    value <<= n;
+    if (bitsNeeded >= 0) { value += byte() << bitsNeeded; bitsNeeded -= 8; }
+    uint32_t sr = range << (n + 7);
+    for (unsigned i = 0; i < n; i++) {
+      sr >>= 1;
+      const uint32_t mask = (uint32_t)((int32_t)(sr - 1 - value) >> 31);
+      value -= sr & mask;
+      v = v + v + (mask & 1);
+    }
+    return v;
+  }
+#endif
   unsigned trm() {   // decodeBinTrm
     range -= 2;
     const uint32_t sr = range << 7;

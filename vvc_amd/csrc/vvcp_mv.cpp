@@ -3,6 +3,10 @@
 #include "vvcp_mv.h"
 
 #include <algorithm>
+#include <cstdint>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -110,6 +114,8 @@ struct Deriver {
   const SPS &sps;
   const PicHeader &ph;
   MotionField &mf;
+  MotionField *col8f = nullptr;   // the collocated view being built (MotionPicture::mf: 8x8 subsample)
+  int w8 = 0;
   std::vector<vvcr_geo> &geoRows;
   const std::vector<const MotionPicture *> &dpb;
   const SliceHeader *sh = nullptr;
@@ -128,6 +134,12 @@ struct Deriver {
       : P(p), S(p.syn), sps(p.sps), ph(p.ph), mf(f), geoRows(g), dpb(d) {}
 
   Mi &at(int x, int y) { return mf[(size_t)(y >> 2) * S.w4 + (x >> 2)]; }
+  // the units of CU ci at 8-aligned positions into the collocated view, once its span is final (each
+  // unit is written by its own CU only; DMVR refinements follow in refine_motion)
+  void col8(const vvcr_cu &c) {
+    for (int y = (c.y + 7) & ~7; y < c.y + c.h; y += 8)
+      for (int x = (c.x + 7) & ~7; x < c.x + c.w; x += 8) (*col8f)[(size_t)(y >> 3) * w8 + (x >> 3)] = at(x, y);
+  }
   bool isBipredRestriction(const vvcr_cu &c) const { return (c.w == 4 && c.h == 4) || c.w + c.h == 12; }
   bool isDiffMER(int x1, int y1, int x2, int y2) const {   // PU::isDiffMER (:1506) on the PU top-left corners
     const int l = sps.log2ParMrgLevel;
@@ -150,7 +162,7 @@ struct Deriver {
   bool colocatedMVP(int l, int px, int py, Mv &out, int refIdx, bool sbFlag) const {
     if (!col || col->intra) return false;
     const int x = px & ~7, y = py & ~7;
-    const Mi &mi = col->mf[(size_t)(y >> 2) * col->w4 + (x >> 2)];
+    const Mi &mi = col->at8(x, y);
     if (!mi.isInter) return false;
     int colList = sh->checkLDC ? l : (sh->colFromL0 ? 1 : 0);
     int colRef = mi.ref[colList];
@@ -169,9 +181,20 @@ struct Deriver {
     if (curLT != colLT) return false;
     Mv m(roundMvComp(mi.mv[colList][0]), roundMvComp(mi.mv[colList][1]));
     if (curLT) { out = clipStore(m); return true; }
-    const int s = distScale(sh->poc, refPoc(l, refIdx), col->poc, cs.refPoc[colList][colRef]);
+    const int s = distScaleCol(sh->poc - refPoc(l, refIdx), col->poc - cs.refPoc[colList][colRef]);
     out = s == 4096 ? clipStore(m) : scaleMv(m, s);
     return true;
+  }
+  // distScale of the temporal candidates, memoised on the two POC distances (an SbTMVP CU asks per
+  // 8x8 sub-block and list, with a handful of distinct pairs per picture)
+  mutable int dsB[4] = {INT32_MIN, INT32_MIN, INT32_MIN, INT32_MIN}, dsD[4] = {}, dsV[4] = {}, dsNext = 0;
+  int distScaleCol(int b, int d) const {
+    for (int k = 0; k < 4; k++)
+      if (dsB[k] == b && dsD[k] == d) return dsV[k];
+    const int v = distScale(b, 0, d, 0);
+    const int k = dsNext++ & 3;
+    dsB[k] = b; dsD[k] = d; dsV[k] = v;
+    return v;
   }
   // C0 (bottom-right) / C1 (centre) positions shared by the temporal candidates
   bool posC0(const vvcr_cu &c, int &x, int &y) const {
@@ -645,7 +668,7 @@ struct Deriver {
     clipColPos(c, cx, cy);
     cx &= ~7; cy &= ~7;
     if (!col || col->intra) return false;
-    const Mi &mi = col->mf[(size_t)(cy >> 2) * col->w4 + (cx >> 2)];
+    const Mi &mi = col->at8(cx, cy);
     bool found = false;
     outDir = 0;
     if (mi.isInter) {
@@ -671,7 +694,7 @@ struct Deriver {
         int px = x + xOff, py = y + yOff;
         clipColPos(c, px, py);
         px &= ~7; py &= ~7;
-        const Mi &cm = col->mf[(size_t)(py >> 2) * col->w4 + (px >> 2)];
+        const Mi &cm = col->at8(px, py);
         Mi m;
         m.isInter = true;
         m.slice = (uint16_t)sliceIdx;
@@ -822,6 +845,10 @@ struct Deriver {
   // PU::spanMotionInfo (:3027)
   // ----------------------------------------------------------------------------------------------
   void span(int ci) {
+    spanUnits(ci);
+    col8(S.cu[ci]);
+  }
+  void spanUnits(int ci) {
     const vvcr_cu &c = S.cu[ci];
     const int pi = c.firstpu;
     if (puMrgType[pi] == MRG_SUBPU_ATMVP) {
@@ -839,8 +866,11 @@ struct Deriver {
     for (int y = c.y; y < c.y + c.h; y += 4)
       for (int x = c.x; x < c.x + c.w; x += 4) {
         Mi &d = at(x, y);
-        if (c.affine) {
+        if (c.affine) {   // the AMVR / BCW bits stay as the memset left them (zero); the MVs are setAllAffineMv's
           d.isInter = mi.isInter;
+          d.altHpel = 0;
+          d.bcw = 0;
+          d.pad_ = 0;
           d.interDir = mi.interDir;
           d.slice = mi.slice;
           for (int l = 0; l < 2; l++) {
@@ -867,7 +897,7 @@ struct Deriver {
       for (int x = c.x; x < c.x + c.w; x += 4) {
         Mi &d = at(x, y);
         if (c.affine) {
-          d.isInter = true; d.interDir = mi.interDir; d.slice = mi.slice;
+          d.isInter = true; d.altHpel = 0; d.bcw = 0; d.pad_ = 0; d.interDir = mi.interDir; d.slice = mi.slice;
           for (int l = 0; l < 2; l++) { if (mi.ref[l] == -1) d.mv[l][0] = d.mv[l][1] = 0; d.ref[l] = mi.ref[l]; }
         } else {
           d = mi;
@@ -975,6 +1005,7 @@ struct Deriver {
         }
       }
     }
+    col8(c);
     // InterPrediction::motionCompensationGeo (InterPrediction.cpp:1761-1769) leaves the PU with
     // setMergeInfo of the second candidate
     const int pi = c.firstpu;
@@ -1000,7 +1031,9 @@ struct Deriver {
     const int pi = c.firstpu;
     vvcr_pu &u = S.pu[pi];
     const PuSyntax &s = S.pux[pi];
-    if (c.affine || c.geo) spanParse(ci);   // the later spans overwrite every field of other CUs
+    // the parse-time span survives in part only for GEO (its AMVR bit); an affine CU's span writes every
+    // byte after the derivation, which reads no unit of the CU itself (its neighbours are outside it)
+    if (c.geo) spanParse(ci);
     if (u.merge) {
       if (u.mmvd) {   // getInterMergeCandidates + getInterMMVDMergeCandidates + setMmvdMergeCandiInfo
         const int base = s.mmvdMergeIdx / 32;
@@ -1169,6 +1202,14 @@ struct Deriver {
   }
 
   void run() {
+    static const bool prof = getenv("VVCR_PLAN_PROF") != nullptr;   // diagnostics: phase times to stderr
+    auto tp = std::chrono::steady_clock::now();
+    auto mark = [&](const char *n) {
+      if (!prof) return;
+      const auto t = std::chrono::steady_clock::now();
+      fprintf(stderr, "  derive %-8s %.2f ms\n", n, std::chrono::duration<double, std::milli>(t - tp).count());
+      tp = t;
+    };
     const size_t ncu = S.cu.size(), npu = S.pu.size();
     cuImv.assign(ncu, 0); cuBcw.assign(ncu, BCW_DEFAULT); cuAffType.assign(ncu, 0);
     for (int l = 0; l < 2; l++) {
@@ -1184,7 +1225,19 @@ struct Deriver {
         puRef[0][pi] = S.pu[pi].ref0; puRef[1][pi] = S.pu[pi].ref1;
       }
     }
-    mf.alloc((size_t)S.w4 * S.h4, true);   // CodingStructure::initStructData memsets the field
+    mark("arrays");
+    // CodingStructure::initStructData memsets the field; here only the units that no span writes are
+    // zeroed, those of intra CUs (span and spanParse write every byte of an inter CU's units, the affine
+    // ones included: setAllAffineMv the MVs of the lists in use, the span the rest). The luma CUs tile
+    // the picture.
+    mf.alloc((size_t)S.w4 * S.h4, false);
+    for (size_t i = 0; i < ncu; i++) {
+      const vvcr_cu &c = S.cu[i];
+      if (!c.yvalid || c.predmode != MODE_INTRA) continue;
+      for (int y = c.y >> 2; y < (c.y + c.h) >> 2; y++) std::memset((void *)&mf[(size_t)y * S.w4 + (c.x >> 2)], 0, (size_t)(c.w >> 2) * sizeof(Mi));
+      col8(c);
+    }
+    mark("field");
     int curSlice = -1;
     for (size_t i = 0; i < ncu; i++) {
       const vvcr_cu &c = S.cu[i];
@@ -1205,6 +1258,7 @@ struct Deriver {
       if (c.predmode == MODE_INTRA || !c.yvalid) continue;
       deriveCu((int)i);
     }
+    mark("cus");
     // write the derived fields back into the rows
     for (size_t i = 0; i < ncu; i++) {
       vvcr_cu &c = S.cu[i];
@@ -1248,6 +1302,7 @@ struct Deriver {
         off += (u.h / dy) * (u.w / dx);
       } else u.dmvr_off = -1;
     }
+    mark("back");
   }
 };
 
@@ -1263,13 +1318,25 @@ void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb
     motionRows.alloc((size_t)p.syn.w4 * p.syn.h4, true);
     return;
   }
-  Deriver d(p, field, geoRows, dpb);
+  static const bool prof = getenv("VVCR_PLAN_PROF") != nullptr;   // diagnostics: phase times to stderr
+  auto tp = std::chrono::steady_clock::now();
+  auto mark = [&](const char *n) {
+    if (!prof) return;
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "  derive %-8s %.2f ms\n", n, std::chrono::duration<double, std::milli>(t - tp).count());
+    tp = t;
+  };
+  // the field itself becomes the motion rows (Mi has the layout of a MotionRec); `field` gets the
+  // collocated view, the top-left 4x4 unit of every 8x8 block (MotionPicture), as each CU's span is final
+  MotionField full;
+  Deriver d(p, full, geoRows, dpb);
+  d.w8 = (p.syn.w4 + 1) >> 1;
+  field.alloc((size_t)d.w8 * ((p.syn.h4 + 1) >> 1), false);
+  d.col8f = &field;
+  mark("init");
   d.run();
-  motionRows.alloc(field.size(), false);
-  // the MotionRec prefix of every Mi (vvcp_mv.h)
-  const uint8_t *src = (const uint8_t *)field.data();
-  uint8_t *dst = (uint8_t *)motionRows.data();
-  for (size_t i = 0, n = field.size(); i < n; i++) std::memcpy(dst + i * sizeof(MotionRec), src + i * sizeof(Mi), sizeof(MotionRec));
+  mark("run");
+  motionRows.adopt(std::move(full));
 }
 
 void refine_motion(const PictureUnit &p, MotionField &&field, const int32_t *deltas, int64_t ndeltas,
@@ -1278,6 +1345,8 @@ void refine_motion(const PictureUnit &p, MotionField &&field, const int32_t *del
   out.poc = p.poc;
   out.w4 = S.w4;
   out.h4 = S.h4;
+  out.w8 = (S.w4 + 1) >> 1;
+  out.h8 = (S.h4 + 1) >> 1;
   out.intra = field.empty();
   out.mf = std::move(field);
   out.slices.resize(p.slices.size());
@@ -1302,8 +1371,9 @@ void refine_motion(const PictureUnit &p, MotionField &&field, const int32_t *del
         mi.ref[0] = (int16_t)u.ref0; mi.ref[1] = (int16_t)u.ref1;
         mi.mv[0][0] = clipStore(u.mv0x + ddx); mi.mv[0][1] = clipStore(u.mv0y + ddy);
         mi.mv[1][0] = clipStore(u.mv1x - ddx); mi.mv[1][1] = clipStore(u.mv1y - ddy);
-        for (int yy = y; yy < y + dy; yy += 4)
-          for (int xx = x; xx < x + dx; xx += 4) out.mf[(size_t)(yy >> 2) * S.w4 + (xx >> 2)] = mi;
+        // the kept units inside the sub-block: 8-aligned positions (a CU may start at x or y = 4 mod 8)
+        for (int yy = (y + 7) & ~7; yy < y + dy; yy += 8)
+          for (int xx = (x + 7) & ~7; xx < x + dx; xx += 8) out.mf[(size_t)(yy >> 3) * out.w8 + (xx >> 3)] = mi;
       }
   }
 }

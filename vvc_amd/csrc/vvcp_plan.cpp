@@ -63,10 +63,20 @@ extern "C" int vvcp_plan_picture_rows(vvcp_stream *h, int32_t idx, const vvcr_se
   vvcp::PictureSyntax &S = p.syn;
   try {
     // the transform rows, coefficient pool, motion rows and CU maps move to the picture (nothing on the
-    // host reads them again); CU / PU rows are copied: refine_motion still reads them
+    // host reads them again); CU / PU rows move too unless refine_motion has yet to read them (a PU with
+    // DMVR whose deltas are not back: they are copied)
     PictureDescriptors D;
-    D.cu.assign(S.cu.begin(), S.cu.end());
-    D.pu.assign(S.pu.begin(), S.pu.end());
+    bool pending = false;
+    if (!p.refined)
+      for (const vvcr_pu &u : S.pu) pending |= u.dmvr != 0;
+    if (pending) {
+      D.cu.assign(S.cu.begin(), S.cu.end());
+      D.pu.assign(S.pu.begin(), S.pu.end());
+    } else {
+      D.cu = std::move(S.cu);
+      D.pu = std::move(S.pu);
+      p.rowsMoved = true;
+    }
     D.tu = std::move(S.tu);
     D.coef = std::move(S.coef);
     D.coef_box = std::move(S.box);

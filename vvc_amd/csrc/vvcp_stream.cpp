@@ -330,6 +330,7 @@ int64_t vvcp_picture_rows(const vvcp_stream *h, int32_t idx, int32_t what, void 
     if (p.handedOver) return VVCR_E_STATE;
     s.dense_rows(dtu, dcoef);
   }
+  if ((what == VVCP_ROWS_CU || what == VVCP_ROWS_PU) && p.rowsMoved) return VVCR_E_STATE;
   switch (what) {
     case VVCP_ROWS_CU: src = s.cu.data(); count = (int64_t)s.cu.size(); esz = sizeof(vvcr_cu); break;
     case VVCP_ROWS_PU: src = s.pu.data(); count = (int64_t)s.pu.size(); esz = sizeof(vvcr_pu); break;
@@ -345,7 +346,7 @@ int64_t vvcp_picture_rows(const vvcp_stream *h, int32_t idx, int32_t what, void 
       src = s.ccCtl[what - VVCP_ROWS_CCALF0].data(); count = (int64_t)s.ccCtl[0].size(); esz = 1; break;
     case VVCP_ROWS_MOTION:
       if (!p.derived) return VVCR_E_STATE;
-      count = (int64_t)p.motion.size();   // the 20-byte internal records, widened to vvcr_motion rows
+      count = (int64_t)p.motion.size();   // the 24-byte internal records, widened to vvcr_motion rows
       if (dst && cap > 0)
         for (int64_t i = 0; i < std::min(cap, count); i++) ((vvcr_motion *)dst)[i] = from_rec(p.motion[i]);
       return count;

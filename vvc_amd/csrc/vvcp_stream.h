@@ -31,7 +31,8 @@ struct PictureUnit {
   MotionRows motion;
   std::vector<vvcr_geo> geo;
   bool derived = false;
-  bool handedOver = false;   // vvcp_plan_picture moved the TU rows, coefficients and motion rows out
+  bool handedOver = false;
+  bool rowsMoved = false;    // ... and the CU / PU rows (no DMVR refinement left to read them)   // vvcp_plan_picture moved the TU rows, coefficients and motion rows out
   std::unique_ptr<MotionPicture> refined;   // set by refine_motion; read as a collocated picture
 };
 

@@ -113,6 +113,16 @@ struct raw {
     n = count;
     if (zero) std::memset((void *)p, 0, count * sizeof(T));
   }
+  // takes over the buffer of an array of a type with the same size (a layout-compatible record)
+  template <class U>
+  void adopt(raw<U> &&o) {
+    static_assert(sizeof(U) == sizeof(T), "adopt: element sizes differ");
+    reset();
+    p = reinterpret_cast<T *>(o.p);
+    n = o.n;
+    o.p = nullptr;
+    o.n = 0;
+  }
   void assign(const T *b, const T *e) {
     alloc((size_t)(e - b), false);
     if (n) std::memcpy((void *)p, b, n * sizeof(T));

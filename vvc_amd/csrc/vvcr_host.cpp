@@ -424,6 +424,9 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
         // (SbTMVP candidates of the sub-block merge list also carry cu.affine; the merge type decides).
         // Like the reference, runs of sub-blocks with the same motion along the PU's longer side are one
         // prediction (:307-345; the same samples, fewer and larger jobs).
+        // VVCR_SBT_JOIN: 0 no joining, 1 runs of any length, 2 (default) runs cut into power-of-two
+        // lengths (the k_mc classes stay the power-of-two block sizes)
+        static const int join = [] { const char *e = getenv("VVCR_SBT_JOIN"); return e ? atoi(e) : 2; }();
         const bool ver = p.h > p.w;
         const int fe = ver ? p.w : p.h, se = ver ? p.h : p.w;
         auto mot = [&](int a, int b) -> const MotionRec & {   // the sub-block at (first, second) offsets
@@ -434,7 +437,10 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
           for (int b = 0; b < se;) {
             const MotionRec &m = mot(a, b);
             int len = 8;
-            while (b + len < se && std::memcmp(&mot(a, b + len), &m, sizeof(MotionRec)) == 0) len += 8;
+            if (join) {
+              while (b + len < se && std::memcmp(&mot(a, b + len), &m, sizeof(MotionRec)) == 0) len += 8;
+              if (join == 2) len = 1 << (31 - __builtin_clz(len));   // the rest of the run starts the next job
+            }
             McJob j = make_job(pp, m.inter_dir, m.ref0, m.ref1, m.mv0x, m.mv0y, m.mv1x, m.mv1y, bcw, alt);   // BCW of the CU (xWeightedAverage reads pu.cu->BcwIdx)
             set_wp(pp, j, m.ref0, m.ref1, c.bcw);
             j.flags |= recon;

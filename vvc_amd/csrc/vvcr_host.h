@@ -5,17 +5,20 @@
 #include "vvcr_internal.h"
 
 // The 4x4 motion field as the host planners keep it (deblocking boundary strength, SbTMVP sub-block MC):
-// the fields of vvcr_motion in 20 bytes instead of 40 (it is read per 4x4 edge of every B picture, and a
-// 4K field is 518k entries). flags: is_inter | alt_hpel << 1 | bcw << 2.
+// the fields of vvcr_motion in 24 bytes instead of 40 (it is read per 4x4 edge of every B picture, and a
+// 4K field is 518k entries). flags: is_inter | alt_hpel << 1 | bcw << 2. slice (the slice index) and
+// pad make it the layout of the host parser's motion field entry (vvcp::Mi), so the derived field is
+// handed over as the rows without a conversion pass.
 struct MotionRec {
   int8_t ref0, ref1;
   uint8_t inter_dir, flags;
   int32_t mv0x, mv0y, mv1x, mv1y;
+  uint16_t slice, pad;
 };
-static_assert(sizeof(MotionRec) == 20, "MotionRec layout");
+static_assert(sizeof(MotionRec) == 24, "MotionRec layout");
 inline MotionRec to_rec(const vvcr_motion &m) {
   return {(int8_t)m.ref0, (int8_t)m.ref1, (uint8_t)m.inter_dir, (uint8_t)((m.is_inter ? 1 : 0) | (m.alt_hpel ? 2 : 0) | (m.bcw << 2)),
-          m.mv0x, m.mv0y, m.mv1x, m.mv1y};
+          m.mv0x, m.mv0y, m.mv1x, m.mv1y, 0, 0};
 }
 inline vvcr_motion from_rec(const MotionRec &r) {
   return {r.flags & 1, r.inter_dir, r.ref0, r.ref1, r.mv0x, r.mv0y, r.mv1x, r.mv1y, r.flags >> 2, (r.flags >> 1) & 1};
