@@ -711,8 +711,9 @@ struct Parser {
     const int idx = (int)pic.cu.size();
     pic.cu.push_back(c);
     pic.cux.push_back(x);
+    if (yv != cv) pic.unshareMap();
     if (yv) fill_map(0, idx, a.x, a.y, a.w, a.h);
-    if (cv) fill_map(1, idx, a.x, a.y, a.w, a.h);
+    if (cv && !pic.mapShared) fill_map(1, idx, a.x, a.y, a.w, a.h);
 
     int lumaQPinLocalDualTree = -1;
     if (cuCtx.qgStart) { cuCtx.qgStart = false; cuCtx.qp = predictQP(idx, cuCtx.qp); }
@@ -2149,7 +2150,9 @@ void PictureSyntax::reset(int W_, int H_, int ctuLog2_) {
   // grow by reallocation (copying every row) while the CABAC pass appends; larger counts still grow
   const size_t rows = (size_t)W * H / 64 + 1024;
   cu.reserve(rows); cux.reserve(rows); pu.reserve(rows); pux.reserve(rows); tu.reserve(rows + rows / 2);
-  for (int c = 0; c < 2; c++) map[c].assign((size_t)w4 * h4, -1);
+  map[0].assign((size_t)w4 * h4, -1);
+  map[1].clear();
+  mapShared = true;
   const size_t n = (size_t)wCtu * hCtu;
   sao.assign(n * 3, vvcr_sao());
   for (int c = 0; c < 3; c++) { alfEn[c].assign(n, 0); alfAlt[c].assign(n, 0); }
@@ -2180,7 +2183,7 @@ void PictureSyntax::dense_rows(std::vector<vvcr_tu> &tus, std::vector<int32_t> &
 int PictureSyntax::cuAt(int ch, int x, int y) const {
   if (ch) { x <<= 1; y <<= 1; }
   if (x < 0 || y < 0 || x >= W || y >= H) return -1;
-  return map[ch][(size_t)(y >> 2) * w4 + (x >> 2)];
+  return map[ch && !mapShared ? 1 : 0][(size_t)(y >> 2) * w4 + (x >> 2)];
 }
 
 void parse_slice_data(PictureSyntax &pic, const SliceCtx &sc, const uint8_t *rbsp, size_t n, const std::vector<uint32_t> &nal_epb) {
@@ -2189,6 +2192,7 @@ void parse_slice_data(PictureSyntax &pic, const SliceCtx &sc, const uint8_t *rbs
 }
 
 void finish_picture_syntax(PictureSyntax &pic, int bitDepth) {
+  pic.unshareMap();
   pic.box.resize(3 * pic.tu.size(), 0);   // TUs after the last one with levels
   // PU::getFinalIntraMode (UnitTools.cpp:627) of intra PUs, 4:2:0: DM resolves to the co-located luma
   // mode (PU::getCoLocatedIntraLumaMode :642), MIP luma neighbours count as planar

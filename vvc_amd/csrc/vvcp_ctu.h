@@ -42,8 +42,16 @@ struct PictureSyntax {
   // box[3 t + c] = rows | cols << 8. dense_rows() gives the w*h-per-block form of vvcr_picture_submit.
   bigbuf::vec<int32_t> coef;
   bigbuf::vec<uint16_t> box;
-  // maps over 4x4 luma units: CU index per channel (-1 = not decoded)
+  // maps over 4x4 luma units: CU index per channel (-1 = not decoded). While every CU so far codes both
+  // channels (a single tree) the chroma map is the luma map: only map[0] is filled (mapShared), and
+  // map[1] becomes its copy at the first CU of one channel, or at finish_picture_syntax.
   bigbuf::vec<int32_t> map[2];
+  bool mapShared = true;
+  void unshareMap() {
+    if (!mapShared) return;
+    map[1].assign(map[0].begin(), map[0].end());
+    mapShared = false;
+  }
   // loop-filter syntax per CTB
   std::vector<vvcr_sao> sao;        // [nCtb][3], merges resolved at finish()
   std::vector<uint8_t> alfEn[3], alfAlt[3], ccCtl[2];

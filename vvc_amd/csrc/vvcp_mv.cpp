@@ -845,15 +845,11 @@ struct Deriver {
   // PU::spanMotionInfo (:3027)
   // ----------------------------------------------------------------------------------------------
   void span(int ci) {
-    spanUnits(ci);
-    col8(S.cu[ci]);
-  }
-  void spanUnits(int ci) {
     const vvcr_cu &c = S.cu[ci];
     const int pi = c.firstpu;
     if (puMrgType[pi] == MRG_SUBPU_ATMVP) {
-      for (int y = 0; y < c.h >> 2; y++)
-        for (int x = 0; x < c.w >> 2; x++) at(c.x + 4 * x, c.y + 4 * y) = subPu[(size_t)y * subW + x];
+      for (int y = 0; y < c.h >> 2; y++) std::memcpy((void *)&at(c.x, c.y + 4 * y), &subPu[(size_t)y * subW], (size_t)(c.w >> 2) * sizeof(Mi));
+      col8(c);
       return;
     }
     Mi mi;
@@ -863,24 +859,28 @@ struct Deriver {
     mi.altHpel = cuImv[ci] == IMV_HPEL;
     for (int l = 0; l < 2; l++) { mi.mv[l][0] = puMv[l][pi].h; mi.mv[l][1] = puMv[l][pi].v; mi.ref[l] = (int16_t)puRef[l][pi]; }
     mi.bcw = 0;
-    for (int y = c.y; y < c.y + c.h; y += 4)
-      for (int x = c.x; x < c.x + c.w; x += 4) {
-        Mi &d = at(x, y);
-        if (c.affine) {   // the AMVR / BCW bits stay as the memset left them (zero); the MVs are setAllAffineMv's
-          d.isInter = mi.isInter;
-          d.altHpel = 0;
-          d.bcw = 0;
-          d.pad_ = 0;
-          d.interDir = mi.interDir;
-          d.slice = mi.slice;
-          for (int l = 0; l < 2; l++) {
-            if (mi.ref[l] == -1) d.mv[l][0] = d.mv[l][1] = 0;
-            d.ref[l] = mi.ref[l];
-          }
-        } else {
-          d = mi;
+    if (c.affine) {   // the AMVR / BCW bits stay as the memset left them (zero); the MVs are setAllAffineMv's
+      for (int y = c.y; y < c.y + c.h; y += 4) {
+        Mi *d = &at(c.x, y);
+        for (int x = 0; x < c.w >> 2; x++) {
+          Mi t = mi;
+          for (int l = 0; l < 2; l++)
+            if (mi.ref[l] != -1) { t.mv[l][0] = d[x].mv[l][0]; t.mv[l][1] = d[x].mv[l][1]; }
+            else t.mv[l][0] = t.mv[l][1] = 0;
+          t.altHpel = 0;
+          d[x] = t;
         }
       }
+      col8(c);
+      return;
+    }
+    for (int y = c.y; y < c.y + c.h; y += 4) {
+      Mi *d = &at(c.x, y);
+      for (int x = 0; x < c.w >> 2; x++) d[x] = mi;
+    }
+    // the collocated view of a CU of one motion: mi at its 8-aligned units
+    for (int y = (c.y + 7) & ~7; y < c.y + c.h; y += 8)
+      for (int x = (c.x + 7) & ~7; x < c.x + c.w; x += 8) (*col8f)[(size_t)(y >> 3) * w8 + (x >> 3)] = mi;
   }
   // the parse-time spanMotionInfo (CABACReader::prediction_unit :2072): merge PUs carry their parsed
   // (not yet derived) fields; only what later derivation does not overwrite survives (GEO / affine areas)
