@@ -1,3 +1,4 @@
+#include <algorithm>
 // Host-only driver for profiling the decode path's CPU side (gprof): open a bitstream, then per picture
 // the CABAC pass, motion derivation (no DMVR refinement: timing only) and native planning. No GPU call.
 //   tools/host_prof.sh <stream.bin> [repeats]
@@ -51,6 +52,20 @@ int main(int argc, char **argv) {
   double tp = 0, td = 0, tl = 0;
   std::vector<int32_t> zeros(1 << 21, 0);   // DMVR deltas: none (timing only)
   using clk = std::chrono::steady_clock;
+  if (getenv("HOST_PROF_PARSE0")) {   // parse picture 0 only, `reps` times: min / median ms (A/B of parser builds)
+    std::vector<double> t;
+    for (int r = 0; r < reps; r++) {
+      vvcp_stream *s = nullptr;
+      if (vvcp_open(data.data(), data.size(), &s)) return 1;
+      auto t0 = clk::now();
+      if (vvcp_parse_picture(s, 0)) { fprintf(stderr, "%s\n", vvcp_last_error()); return 1; }
+      t.push_back(std::chrono::duration<double>(clk::now() - t0).count() * 1e3);
+      vvcp_close(s);
+    }
+    std::sort(t.begin(), t.end());
+    printf("parse0 min %.2f median %.2f ms over %d\n", t[0], t[t.size() / 2], reps);
+    return 0;
+  }
   for (int r = 0; r < reps; r++) {
     vvcp_stream *s = nullptr;
     if (vvcp_open(data.data(), data.size(), &s)) { fprintf(stderr, "%s\n", vvcp_last_error()); return 1; }

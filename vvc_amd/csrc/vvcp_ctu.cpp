@@ -2145,7 +2145,9 @@ void PictureSyntax::reset(int W_, int H_, int ctuLog2_) {
   w4 = (W + 3) >> 2;
   h4 = (H + 3) >> 2;
   cu.clear(); cux.clear(); pu.clear(); pux.clear(); tu.clear(); coef.clear(); box.clear();
-  coef.reserve((size_t)W * H * 3 / 2 + 8192);   // at most every sample of the three planes
+  // room for a quarter of the samples' levels (the packed boxes of a typical picture); more grows the pool
+  // (the blocks come from the large-buffer cache, page-locked once a reconstruction context exists)
+  coef.reserve((size_t)W * H / 4 + 65536);
   // rows: room for a densely coded intra picture (one CU per 64 luma samples), so that the vectors do not
   // grow by reallocation (copying every row) while the CABAC pass appends; larger counts still grow
   const size_t rows = (size_t)W * H / 64 + 1024;

@@ -1313,9 +1313,9 @@ void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb
   geoRows.clear();
   bool intra = true;
   for (const SliceHeader &s : p.slices) intra &= s.isIntra();
-  if (intra) {   // no inter CU: the field stays empty, the rows all-zero (CodingStructure::initStructData)
+  if (intra) {   // no inter CU: no field and no rows (all-zero, CodingStructure::initStructData; nothing reads them)
     field.reset();
-    motionRows.alloc((size_t)p.syn.w4 * p.syn.h4, true);
+    motionRows.clear();
     return;
   }
   static const bool prof = getenv("VVCR_PLAN_PROF") != nullptr;   // diagnostics: phase times to stderr

@@ -346,9 +346,10 @@ int64_t vvcp_picture_rows(const vvcp_stream *h, int32_t idx, int32_t what, void 
       src = s.ccCtl[what - VVCP_ROWS_CCALF0].data(); count = (int64_t)s.ccCtl[0].size(); esz = 1; break;
     case VVCP_ROWS_MOTION:
       if (!p.derived) return VVCR_E_STATE;
-      count = (int64_t)p.motion.size();   // the 24-byte internal records, widened to vvcr_motion rows
+      // the 24-byte internal records, widened to vvcr_motion rows; an intra picture has none: all-zero rows
+      count = p.motion.empty() ? (int64_t)s.w4 * s.h4 : (int64_t)p.motion.size();
       if (dst && cap > 0)
-        for (int64_t i = 0; i < std::min(cap, count); i++) ((vvcr_motion *)dst)[i] = from_rec(p.motion[i]);
+        for (int64_t i = 0; i < std::min(cap, count); i++) ((vvcr_motion *)dst)[i] = from_rec(p.motion.empty() ? MotionRec{} : p.motion[i]);
       return count;
     case VVCP_ROWS_GEO:
       if (!p.derived) return VVCR_E_STATE;

@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <atomic>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -65,15 +66,30 @@ struct DevVec {
 // Upload staging of one prepared picture: every host array its kernels read is copied into one pinned
 // buffer, then one asynchronous copy moves it to one device arena on the context's upload stream (the
 // lanes wait for its event). A picture's upload costs one DMA instead of a dozen synchronous pageable
-// copies, and the preparing thread does not wait for it.
+// copies, and the preparing thread does not wait for it. Large arrays that already sit in page-locked
+// memory (bigbuf::is_pinned) are not copied: they get their own DMA into the arena (add_big), and the
+// picture that owns them waits for it before it changes or frees them (vvcr_picture::settle).
 struct Staging {
   uint8_t *h = nullptr;
   size_t cap = 0, used = 0;
   DevVec<uint8_t> arena;
   struct Item { void **dst; size_t off; };
   std::vector<Item> items;
+  struct Ext { void **dst; const void *src; size_t bytes, off; };
+  std::vector<Ext> ext;
+  size_t ext_used = 0, base = 0;
   ~Staging() { if (h) (void)hipHostFree(h); }
-  void begin() { used = 0; items.clear(); }
+  void begin() { used = 0; items.clear(); ext.clear(); ext_used = 0; }
+  template <class T> void add_big(DevVec<T> &d, const T *src, size_t n) {
+    static const bool off = getenv("VVCR_NO_DIRECT_UPLOAD") != nullptr;   // diagnostics: stage everything
+    const size_t bytes = n * sizeof(T);
+    if (off || bytes < bigbuf::kPinMin || !bigbuf::is_pinned(src)) { add(d, src, n); return; }
+    const size_t o = (ext_used + 255) & ~(size_t)255;
+    ext.push_back({(void **)&d.p, src, bytes, o});
+    ext_used = o + bytes + sizeof(T);   // (n + 1) elements, as add() reserves
+    d.set_view(nullptr);
+  }
+  template <class T, class A> void add_big(DevVec<T> &d, const std::vector<T, A> &v) { add_big(d, v.data(), v.size()); }
   void reserve(size_t n) {
     if (n <= cap) return;
     const size_t c = std::max(n, cap * 3 / 2 + (1 << 20));
@@ -108,11 +124,14 @@ struct Staging {
   template <class T> T *host_at(size_t off) { return (T *)(h + off); }
   // the device arena is sized and every staged DevVec points into it; nothing is copied yet
   void place() {
-    arena.ensure(used + 256);
+    base = (used + 255) & ~(size_t)255;
+    arena.ensure(base + ext_used + 256);
     for (const Item &it : items) *it.dst = arena.p + it.off;
+    for (const Ext &e : ext) *e.dst = arena.p + base + e.off;
   }
   void copy(hipStream_t s, hipEvent_t done) {
     if (used) VVCR_CHECK_HIP(hipMemcpyAsync(arena.p, h, used, hipMemcpyHostToDevice, s));
+    for (const Ext &e : ext) VVCR_CHECK_HIP(hipMemcpyAsync(arena.p + base + e.off, e.src, e.bytes, hipMemcpyHostToDevice, s));
     VVCR_CHECK_HIP(hipEventRecord(done, s));
   }
 };
@@ -160,6 +179,7 @@ struct Prepared {
   DevVec<DbTu> dbtu;
   DevVec<MotionRec> dbmot;
   int n_dbcu = 0, n_dbtu = 0;
+  size_t n_dbmot = 0;   // motion records staged (0: a picture without inter CUs)
   int32_t dbk_nitems[4] = {0, 0, 0, 0};
   DevVec<int32_t> sao;
   DevVec<int16_t> alf_luma_coef, alf_luma_clip, alf_chroma, alf_cc, alf_set;
@@ -218,6 +238,7 @@ struct Prepared {
     for (int &c : dbk_counts) c = 0;
     dbk_gpu = dbk_chroma_pass = false;
     n_dbcu = n_dbtu = 0;
+    n_dbmot = 0;
     have_sao = have_alf = false;
     n_tb = n_tb_small = n_mctile = n_basic = n_bidir = n_aff = n_tiles = n_dmvr = 0;
     zero_filled = false;
@@ -281,6 +302,20 @@ struct vvcr_picture {
   DbkLists dbk;
   bool dbk_gpu = false;              // the edges are planned on the device from dbkg (default; VVCR_DBK_GPU=0: host)
   DbkGpuInputs dbkg;
+  // an upload that DMAs straight from this picture's page-locked arrays (Staging::add_big) is in flight
+  // until up_ev: settle() before the arrays change or are freed
+  mutable hipEvent_t up_ev = nullptr;
+  mutable bool up_pending = false;
+  vvcr_picture() = default;
+  vvcr_picture(const vvcr_picture &) = delete;
+  vvcr_picture &operator=(const vvcr_picture &) = delete;
+  void settle() {
+    if (up_pending) { (void)hipEventSynchronize(up_ev); up_pending = false; }
+  }
+  ~vvcr_picture() {
+    settle();
+    if (up_ev) (void)hipEventDestroy(up_ev);
+  }
 };
 
 // deblocking planned on the device (vvcr_dbk_plan.hip) unless VVCR_DBK_GPU=0 (the host planner,
@@ -469,6 +504,7 @@ static double mc_bytes(const McJob &j) { return mc_alg_bytes(j.flags, j.w, j.h);
 // Host phase, part 1 (no device): every work list of the picture.
 static void plan_picture(vvcr_picture &b, uint32_t mask) {
   if (!b.submitted) throw VvcrError(VVCR_E_STATE, "picture planned before its descriptors were submitted");
+  b.settle();
   const vvcr_seq_params &sp = b.sp;
   const vvcr_pic_params &pp = b.pp;
   b.wl.clear();
@@ -495,7 +531,11 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
     tp = t;
   };
   if ((mask & VVCR_STAGE_DBK) && b.dbk_gpu) {
-    if (b.desc.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4))
+    // (a picture without inter CUs needs no motion field: the planner never reads it then)
+    bool inter = false;
+    if (b.desc.motion.empty())
+      for (const vvcr_cu &c : b.desc.cu) inter |= c.predmode != 1;   // vvcr_cu::predmode: 1 intra
+    if ((inter || !b.desc.motion.empty()) && b.desc.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4))
       throw VvcrError(VVCR_E_ARG, "deblocking: the motion field does not cover the picture");
     pack_dbk_inputs(sp, pp, b.desc, b.dbkg);
     mark("dbk_pack");
@@ -530,14 +570,42 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
   b.planned = true;
 }
 
+// Diagnostics (VVCR_PREP_PROF): summed wall time of prepare()'s phases over all calls, printed at exit.
+namespace prep_prof {
+constexpr int N = 5;
+const char *const names[N] = {"wait", "resid+inter", "intra+dbk+lf", "place", "copy"};
+std::atomic<uint64_t> ns[N], calls;
+const bool on = getenv("VVCR_PREP_PROF") != nullptr;
+struct Report {
+  ~Report() {
+    if (!on || !calls) return;
+    fprintf(stderr, "prepare: %llu calls, ms per call:", (unsigned long long)calls.load());
+    for (int k = 0; k < N; k++) fprintf(stderr, " %s %.3f", names[k], ns[k].load() * 1e-6 / calls.load());
+    fprintf(stderr, "\n");
+  }
+} report;
+struct Timer {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(int k) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    ns[k] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count();
+    t = n;
+  }
+};
+}  // namespace prep_prof
+
 // Host phase, part 2: upload the planned lists of b into the device buffers of r.
 static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
+  prep_prof::Timer pt;
+  if (prep_prof::on) prep_prof::calls++;
   if (!bp.planned) throw VvcrError(VVCR_E_STATE, "picture not planned");
   if (bp.sp.width != ctx->sp.width || bp.sp.height != ctx->sp.height || bp.sp.ctu_log2 != ctx->sp.ctu_log2 ||
       bp.sp.bit_depth != ctx->sp.bit_depth || bp.sp.dpb_slots > ctx->sp.dpb_slots)
     throw VvcrError(VVCR_E_ARG, "picture built for other sequence parameters than the context's");
   r.wait();
   if (r.up_issued) VVCR_CHECK_HIP(hipEventSynchronize(r.up_done));   // a prepared, never launched picture
+  pt.mark(0);
   Staging &st = r.up;
   st.begin();
   r.pp = bp.pp;
@@ -558,8 +626,8 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   size_t iparams_off = SIZE_MAX;   // staged intra parameters, rewritten after place()
   if (mask & VVCR_STAGE_RESID) {
     // the packed levels of the transform blocks: the producer's pool when it arrived packed
-    st.add(r.coef, bp.desc.coef_box.empty() ? bp.wl.coef : bp.desc.coef);
-    st.add(r.tb, wl.tb);
+    st.add_big(r.coef, bp.desc.coef_box.empty() ? bp.wl.coef : bp.desc.coef);
+    st.add_big(r.tb, wl.tb);
     r.n_tb = (int)wl.tb.size();
     r.n_tb_small = wl.tb_small;
     r.zero_filled = wl.zero_filled;
@@ -607,15 +675,16 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     }
     r.alg_bytes[K_MC_AFFINE] = b;
   }
+  pt.mark(1);
   if (pp.lmcs_enabled) {
     st.add(r.lmcs_lut, {{pp.lmcs_fwd, 1024}, {pp.lmcs_inv, 1024}});
   }
   if (mask & VVCR_STAGE_INTRA) {
     const IntraPlan &ip = bp.intra;
     st.add(r.tiles, ip.inter_tiles);
-    st.add(r.ijobs, ip.jobs);
-    st.add(r.idep_start, ip.dep_start);
-    st.add(r.ideps, ip.deps);
+    st.add_big(r.ijobs, ip.jobs);
+    st.add_big(r.idep_start, ip.dep_start);
+    st.add_big(r.ideps, ip.deps);
     r.istate.ensure(16 + ip.jobs.size());
     // one device copy per lane (scratch plane pointers differ), written after place(): they hold the
     // arena address of the LMCS table (staged above), which is only known then
@@ -646,11 +715,12 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.n_dbtu = (int)bp.dbkg.tu.size();
     for (int k = 0; k < 4; k++) r.dbk_nitems[k] = bp.dbkg.nitems[k];
     if (r.n_dbcu > 0) {
-      st.add(r.dbcu, bp.dbkg.cu);
-      st.add(r.dbpu, bp.dbkg.pu);
-      st.add(r.dbtu, bp.dbkg.tu);
-      st.add(r.dbmot, bp.desc.motion.data(), bp.desc.motion.size());
+      st.add_big(r.dbcu, bp.dbkg.cu);
+      st.add_big(r.dbpu, bp.dbkg.pu);
+      st.add_big(r.dbtu, bp.dbkg.tu);
+      st.add_big(r.dbmot, bp.desc.motion.data(), bp.desc.motion.size());
     }
+    r.n_dbmot = bp.desc.motion.size();
     r.alg_bytes[K_DBK] = pix * 2 * 2;
     // the planner reads the records and the motion field once
     r.alg_bytes[K_DBKP] = (double)r.n_dbcu * sizeof(DbCu) + (double)bp.dbkg.pu.size() * sizeof(DbPu) +
@@ -682,11 +752,19 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     st.add(r.alf_set, bp.h_alf_set);
     r.alg_bytes[K_ALF] = pix * 2 * 2;
   }
+  pt.mark(2);
   st.place();
   if (iparams_off != SIZE_MAX)
     for (int l = 0; l < MAXLANE; l++) st.host_at<IntraParams>(iparams_off)[l] = make_intra_params(ctx, r, l);
+  pt.mark(3);
   st.copy(ctx->upload_stream, r.up_done);
   r.up_issued = true;
+  if (!st.ext.empty()) {   // the picture's own arrays are read by the DMA until this event
+    if (!bp.up_ev) VVCR_CHECK_HIP(hipEventCreateWithFlags(&bp.up_ev, hipEventDisableTiming));
+    VVCR_CHECK_HIP(hipEventRecord(bp.up_ev, ctx->upload_stream));
+    bp.up_pending = true;
+  }
+  pt.mark(4);
 }
 
 // The device deblocking planner's arguments for a prepared picture on a lane: the lane's maps and lists
@@ -701,7 +779,7 @@ static DbkPlanArgs dbk_plan_args(vvcr_ctx *ctx, Lane &ln, const Prepared &r) {
   ln.dbkp.ensure(maps + state + items + lists + 256);
   uint8_t *p = ln.dbkp.p;
   DbkPlanArgs a{};
-  a.cu = r.dbcu.p; a.pu = r.dbpu.p; a.tu = r.dbtu.p; a.motion = r.dbmot.p;
+  a.cu = r.dbcu.p; a.pu = r.dbpu.p; a.tu = r.dbtu.p; a.motion = r.n_dbmot ? r.dbmot.p : nullptr;
   a.ncu = r.n_dbcu; a.ntu = r.n_dbtu; a.W4 = W4; a.H4 = H4; a.ctu_log2 = sp.ctu_log2;
   a.slice_type = pp.slice_type; a.dual_tree = pp.dual_tree; a.dbk_disable = pp.dbk_disable;
   std::memcpy(a.ref_poc, pp.ref_poc, sizeof a.ref_poc);
@@ -954,6 +1032,15 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
   ctx->sp = *sp;
   try {
     VVCR_CHECK_HIP(hipSetDevice(sp->device));
+    // the host side's large per-picture arrays in page-locked memory from now on: the upload DMAs straight
+    // from them (Staging::add_big) instead of copying them into the staging buffer (VVCR_PIN_HOST=0: off)
+    if (const char *e = getenv("VVCR_PIN_HOST"); !(e && e[0] == '0'))
+      bigbuf::set_pinned_allocator(
+          [](size_t n) -> void * {
+            void *p = nullptr;
+            return hipHostMalloc(&p, n, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+          },
+          [](void *p) { (void)hipHostFree(p); });
     if (const char *e = getenv("VVCR_LANES")) ctx->nlane = std::max(2, std::min(MAXLANE, atoi(e)));
     ctx->nintra = ctx->nlane / 2;
     if (const char *e = getenv("VVCR_INTRA_LANES")) ctx->nintra = std::max(1, std::min(ctx->nlane - 1, atoi(e)));
@@ -1031,8 +1118,10 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
   return VVCR_OK;
 }
 
+static void reap_pictures(bool all);
 int vvcr_destroy(vvcr_ctx *ctx) {
   if (!ctx) return VVCR_E_ARG;
+  reap_pictures(true);
   for (int l = 0; l < ctx->nlane; l++) (void)hipStreamSynchronize(ctx->lanes[l].s);
   ctx->prepared.clear();
   for (auto &s : ctx->dpb)
@@ -1077,6 +1166,7 @@ static void pic_begin(vvcr_picture &b, const vvcr_seq_params &sp, const vvcr_pic
 static void pic_submit(vvcr_picture &b, const vvcr_cu *cu, int32_t ncu, const vvcr_pu *pu, int32_t npu, const vvcr_tu *tu,
                        int32_t ntu, const int32_t *coef, int64_t ncoef, const vvcr_motion *motion, const vvcr_geo *geo,
                        int32_t ngeo) {
+  b.settle();
   if (ncu < 0 || npu < 0 || ntu < 0 || ncoef < 0 || ngeo < 0 || (ncu && !cu) || (npu && !pu) || (ntu && !tu) ||
       (ncoef && !coef) || (ngeo && !geo))
     throw VvcrError(VVCR_E_ARG, "bad descriptor array");
@@ -1104,6 +1194,7 @@ static void pic_submit(vvcr_picture &b, const vvcr_cu *cu, int32_t ncu, const vv
 // In-library producers (the host parser, vvcp_plan.cpp) hand their arrays over instead of copying them.
 extern "C++" void vvcr_picture_adopt(vvcr_picture *pic, PictureDescriptors &&d) {
   if (!pic) throw VvcrError(VVCR_E_ARG, "null picture");
+  pic->settle();
   pic->desc = std::move(d);
   pic->planned = false;
   validate_descriptors(pic->sp, pic->pp, pic->desc);
@@ -1111,6 +1202,7 @@ extern "C++" void vvcr_picture_adopt(vvcr_picture *pic, PictureDescriptors &&d) 
 }
 
 static void pic_set_lf(vvcr_picture &b, const vvcr_sao *sao, const vvcr_alf *alf) {
+  b.settle();
   const int n = n_ctb(b.sp);
   b.planned = false;
   b.have_sao = sao != nullptr;
@@ -1407,6 +1499,7 @@ extern "C" int vvcr_debug_dbk_gpu_segments(vvcr_ctx *ctx, const vvcr_picture *pi
   r.dbpu.upload(pic->dbkg.pu);
   r.dbtu.upload(pic->dbkg.tu);
   r.dbmot.upload(pic->desc.motion.data(), pic->desc.motion.size());
+  r.n_dbmot = pic->desc.motion.size();
   Lane &ln = ctx->lanes[0];
   DbkPlanArgs a = dbk_plan_args(ctx, ln, r);
   int32_t cnt[4] = {0, 0, 0, 0};
@@ -1451,9 +1544,36 @@ extern "C" int vvcr_debug_mc_slots(const vvcr_picture *pic, int32_t *out, int32_
 
 const char *vvcr_picture_last_error(const vvcr_picture *pic) { return pic ? pic->err.c_str() : g_create_error.c_str(); }
 
+// Pictures destroyed while an upload still DMAs from their arrays: freed once its event has completed
+// (the destroying thread does not wait for the upload queue).
+static std::mutex g_grave_mu;
+static std::vector<vvcr_picture *> g_grave;
+static void reap_pictures(bool all) {
+  std::vector<vvcr_picture *> done;
+  {
+    std::lock_guard<std::mutex> g(g_grave_mu);
+    for (size_t i = 0; i < g_grave.size();) {
+      if (all || hipEventQuery(g_grave[i]->up_ev) != hipErrorNotReady) {
+        done.push_back(g_grave[i]);
+        g_grave[i] = g_grave.back();
+        g_grave.pop_back();
+      } else {
+        i++;
+      }
+    }
+  }
+  for (vvcr_picture *p : done) delete p;   // (settle() waits if `all` took a pending one)
+}
+
 int vvcr_picture_destroy(vvcr_picture *pic) {
   if (!pic) return VVCR_E_ARG;
-  delete pic;
+  if (pic->up_pending && hipEventQuery(pic->up_ev) == hipErrorNotReady) {
+    std::lock_guard<std::mutex> g(g_grave_mu);
+    g_grave.push_back(pic);
+  } else {
+    delete pic;
+  }
+  reap_pictures(false);
   return VVCR_OK;
 }
 

@@ -237,7 +237,9 @@ struct Unit {
     }
     const DbCu &cPr = A.cu[max(mcu, 0)];
     const int fPm = pin ? 0 : (int)cPr.flags, qpPm = pin ? 0 : (int)cPr.qp;
-    const MotionRec mp = A.motion[pedge ? u : pu], mq = A.motion[u];   // (no motion edge at the picture edge)
+    // (no motion edge at the picture edge; no field: a picture without inter CUs never asks for motion)
+    MotionRec mp{}, mq{};
+    if (A.motion) { mp = A.motion[pedge ? u : pu]; mq = A.motion[u]; }
     // step 1 (TU calls, then the PU's call and its sub-block lines)
 #pragma unroll
     for (int k = 0; k < MAXTU; k++) {

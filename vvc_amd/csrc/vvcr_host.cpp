@@ -40,8 +40,8 @@ void push_tiles(bigbuf::vec<McJob> &out, int x0, int y0, int w, int h, McJob pro
 
 // One plain MC unit (a PU, or an SbTMVP sub-block): 32x32 tiles for k_mc_tile when the PU is at least
 // 32x32 (all VVC block sizes are powers of two, so the tiles cover it exactly), else <= 16x16 jobs.
-void push_mc(WorkLists &wl, int x0, int y0, int w, int h, const McJob &proto) {
-  wl.mc_alg += mc_alg_bytes(proto.flags, w, h);
+void push_mc(WorkLists &wl, int x0, int y0, int w, int h, const McJob &proto, bool count = true) {
+  if (count) wl.mc_alg += mc_alg_bytes(proto.flags, w, h);
   if (w >= 32 && h >= 32 && (x0 & 7) == 0) {
     for (int y = 0; y < h; y += 32)
       for (int x = 0; x < w; x += 32) {
@@ -422,11 +422,14 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
       if (p.mrgtype == MRG_TYPE_SUBPU_ATMVP) {
         // xSubPuMC (InterPrediction.cpp:283-360): 8x8 sub-blocks with their own motion, no BDOF / DMVR
         // (SbTMVP candidates of the sub-block merge list also carry cu.affine; the merge type decides).
-        // Like the reference, runs of sub-blocks with the same motion along the PU's longer side are one
-        // prediction (:307-345; the same samples, fewer and larger jobs).
-        // VVCR_SBT_JOIN: 0 no joining, 1 runs of any length, 2 (default) runs cut into power-of-two
-        // lengths (the k_mc classes stay the power-of-two block sizes)
-        static const int join = [] { const char *e = getenv("VVCR_SBT_JOIN"); return e ? atoi(e) : 2; }();
+        // The reference predicts each run of sub-blocks with the same motion along the PU's longer side as
+        // one block (:307-345), so the algorithmic bytes count per run. The jobs: VVCR_SBT_JOIN 3 (default)
+        // a run that is a whole line of the PU is one job, other runs 8x8 jobs (a PU's jobs then stay in
+        // one or two k_mc size classes, next to each other in the launch: runs cut into jobs of several
+        // sizes scatter over the classes and lose L2 reuse, 14 % more HBM reads and +0.7 / +1.3 us per
+        // 4K QP27 / QP32 picture, profiles/r05_sbt_join*); 0 every sub-block a job, 1 a job per run,
+        // 2 runs cut into power-of-two lengths.
+        static const int join = [] { const char *e = getenv("VVCR_SBT_JOIN"); return e ? atoi(e) : 3; }();
         const bool ver = p.h > p.w;
         const int fe = ver ? p.w : p.h, se = ver ? p.h : p.w;
         auto mot = [&](int a, int b) -> const MotionRec & {   // the sub-block at (first, second) offsets
@@ -436,17 +439,22 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
         for (int a = 0; a < fe; a += 8)
           for (int b = 0; b < se;) {
             const MotionRec &m = mot(a, b);
-            int len = 8;
-            if (join) {
-              while (b + len < se && std::memcmp(&mot(a, b + len), &m, sizeof(MotionRec)) == 0) len += 8;
-              if (join == 2) len = 1 << (31 - __builtin_clz(len));   // the rest of the run starts the next job
-            }
+            int run = 8;
+            while (b + run < se && std::memcmp(&mot(a, b + run), &m, sizeof(MotionRec)) == 0) run += 8;
             McJob j = make_job(pp, m.inter_dir, m.ref0, m.ref1, m.mv0x, m.mv0y, m.mv1x, m.mv1y, bcw, alt);   // BCW of the CU (xWeightedAverage reads pu.cu->BcwIdx)
             set_wp(pp, j, m.ref0, m.ref1, c.bcw);
             j.flags |= recon;
-            const int x = ver ? a : b, y = ver ? b : a;
-            push_mc(wl, p.x + x, p.y + y, ver ? std::min(8, p.w - x) : std::min(len, p.w - x), ver ? std::min(len, p.h - y) : std::min(8, p.h - y), j);
-            b += len;
+            const int fw = std::min(8, fe - a);   // the run's extent across the line
+            wl.mc_alg += ver ? mc_alg_bytes(j.flags, fw, run) : mc_alg_bytes(j.flags, run, fw);
+            for (int o = 0; o < run;) {
+              int len = 8;
+              if (join == 1 || (join == 3 && b == 0 && run == se)) len = run;
+              else if (join == 2) len = 1 << (31 - __builtin_clz(run - o));
+              const int x = ver ? a : b + o, y = ver ? b + o : a;
+              push_mc(wl, p.x + x, p.y + y, ver ? fw : len, ver ? len : fw, j, false);
+              o += len;
+            }
+            b += run;
           }
         continue;
       }

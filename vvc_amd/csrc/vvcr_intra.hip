@@ -29,6 +29,13 @@ extern "C" int vvcr_intra_prof_read(unsigned long long *dst, int max) {
 #else
 #define IPROF(i) do { } while (0)
 #endif
+#if defined(VVCR_INTRA_PROF) && defined(VVCR_IPROF_PRE)   // diagnostics: stamps between the wait and the fill
+#define PPROF(i) IPROF(i)
+#define IPROF_POST(i) do { } while (0)
+#else
+#define PPROF(i) do { } while (0)
+#define IPROF_POST(i) IPROF(i)
+#endif
 
 #ifdef VVCR_DIAG_DUMP
 __device__ int32_t g_dbg[1024];
@@ -217,6 +224,12 @@ __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int c
 #ifdef VVCR_ABL_FILL
   return;
 #endif
+#if defined(VVCR_INTRA_PROF) && defined(VVCR_IPROF_FILL)   // diagnostics: stamps inside the fill (ps[5], ps[6])
+#define FPROF(i) do { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); ps[i] = __builtin_readcyclecounter(); } while (0)
+#else
+#define FPROF(i) do { } while (0)
+#endif
+  FPROF(5);
   const int lu = ch ? 1 : 2;   // log2 of the unit size
   const int totalLeft = (predHSize + (1 << lu) - 1) >> lu;
   const int ox = fx - 1 - mrl, oy = fy - 1 - mrl;   // corner sample of the reference line
@@ -244,6 +257,7 @@ __device__ __forceinline__ void fill_refs(const Src &src, const DPlane &D, int c
         if (j <= nT && avT(j)) top[j] = s_tile[b + j];
         if (j <= nL && avL(j)) left[j] = s_tile[b + j * src.ts];
       }
+      FPROF(6);
     } else {
       int gx[6], gy[6], gvv[6];
       bool need[6];
@@ -530,6 +544,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
 #endif
   // LMCS chroma residual scale (uniform), after the wait: it reads reconstructed luma of other steps
   const int cscale = (comp > 0 && (J.vnb & CS_SCALE)) ? chroma_scale(P, G, J.vx, J.vy, J.vnb, lane) : 0;
+  PPROF(2);
   auto store_resid = [&]() {
     if (!rlds || rreg || rsreg) return;
     if (rvload) {
@@ -570,6 +585,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   // ISP: the regions of the CU in order; region k reads the CU-level lines and region k-1
 #pragma nounroll
   for (int kreg = 0; kreg < nreg; kreg++) {
+  if (kreg == 0) PPROF(3);
   const int x0 = J.x + (ispVer ? kreg * w : 0), y0 = J.y + (isp && !ispVer ? kreg * h : 0);
 
   // ---- reference samples
@@ -580,6 +596,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
     } else if (kreg == 0) {
       // CU-level fill of the first region (predSize per split direction), kept in refF for the others
       const int fTop = ispVer ? 2 * J.cw : J.cw + w, fLeft = ispVer ? J.ch + h : 2 * J.ch;
+      PPROF(4);
       fill_refs(SD, D, 0, J.cx, J.cy, fTop, fLeft, 0, bd, avlo, avhi, top, left, lane, ps, J.vnb, J.nul, J.nut);
       IPROF(7);
       if (nreg > 1)
@@ -606,10 +623,10 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
       }
     }
   }
-  if (kreg == 0) IPROF(2);
+  if (kreg == 0) IPROF_POST(2);
   if (kreg == 0) store_resid();   // read after the wave syncs that follow
   wsync();
-  if (kreg == 0) IPROF(3);
+  if (kreg == 0) IPROF_POST(3);
 
   if (refFilter && !direct) {
     const int pS = topLen, pH = leftLen;
@@ -629,7 +646,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
     }
     wsync();
   }
-  if (kreg == 0) IPROF(4);
+  if (kreg == 0) IPROF_POST(4);
 #ifdef VVCR_DIAG_DUMP
   if (gj == 0 && kreg == 0) {
     if (lane < 16) { g_dbg[lane] = S.refU[0][lane]; g_dbg[16 + lane] = S.refU[1][lane]; g_dbg[32 + lane] = S.refF[0][lane]; }
@@ -1017,10 +1034,14 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
 #else
   finish([&](int, int) { return 0; });
 #endif
+#ifndef VVCR_IPROF_FILL
   if (kreg == 0) IPROF(5);
+#endif
   wsync();
   }   // regions
+#ifndef VVCR_IPROF_FILL
   IPROF(6);
+#endif
 }
 
 // Persistent: each workgroup takes CTUs (that have steps) in the plan's order (wavefront) from an
