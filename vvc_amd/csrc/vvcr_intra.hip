@@ -446,11 +446,15 @@ __device__ __forceinline__ int step_kind(const IntraJob &J) {
   return K_REG;
 }
 
+// kreg: the region of an ISP step (0 for every other kind). The regions of an ISP CU are iterations of the
+// kernel's step loop, not a loop in here: a loop over them made the compiler hoist the set-up of every
+// prediction path out of it and spill it (a fixed ~5,400 cycles per ISP step before the first fill).
 template <int KIND>
 __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J, const TileGeo &G, WaveScratch &S,
                                          const int32_t *dep_start, const int32_t *deps, int gj, int32_t *done,
-                                         int32_t *err, int lane, unsigned long long &t_ready, unsigned long long *ps) {
-  IPROF(0);
+                                         int32_t *err, int lane, unsigned long long &t_ready, unsigned long long *ps,
+                                         const int kreg) {
+  if (kreg == 0) IPROF(0);
   const int comp = J.comp, ch = comp ? 1 : 0;
   const int bd = P.bd, maxv = (1 << bd) - 1;
   const DPlane &D = P.reco[comp];
@@ -486,9 +490,12 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   const bool rsreg = !isp && rn <= 512;
   const bool rreg = !isp && !rsreg && rvec && n <= 4 * 64 * 4;
   const bool rvload = rvec && !rsreg;
-  uint64_t rv[4];
-  int16_t rs[8];
-  if (rvload) {
+  uint64_t rv[4] = {0, 0, 0, 0};
+  int16_t rs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (kreg > 0) {
+    // a later ISP region: its residual is in LDS (stored by region 0) or read from HBM, its
+    // dependencies were met before region 0
+  } else if (rvload) {
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       const int k = min((lane + 64 * b) * 4, rn - 4);
@@ -524,7 +531,7 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   // runs the (uniform) loop and polls the same word — one request per poll — so that no lane-divergent
   // region precedes the step body: the step body's wave syncs do not force reconvergence, and code
   // sunk into a lane-0-only region would run after the other lanes' reads of its results.
-  {
+  if (kreg == 0) {
     const int k0 = __builtin_amdgcn_readfirstlane(dep_start[gj]), k1 = __builtin_amdgcn_readfirstlane(dep_start[gj + 1]);
     for (int k = k1 - 1; k >= k0; k--) {
       const int v = __builtin_amdgcn_readfirstlane(deps[k]);
@@ -534,17 +541,17 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   }
   wsync();
 #ifdef VVCR_INTRA_PROF
-  t_ready = __builtin_amdgcn_s_memrealtime();
+  if (kreg == 0) t_ready = __builtin_amdgcn_s_memrealtime();
 #else
   (void)t_ready; (void)ps;
 #endif
-  IPROF(1);
+  if (kreg == 0) IPROF(1);
 #ifdef VVCR_ABL_ALL
   return;
 #endif
   // LMCS chroma residual scale (uniform), after the wait: it reads reconstructed luma of other steps
   const int cscale = (comp > 0 && (J.vnb & CS_SCALE)) ? chroma_scale(P, G, J.vx, J.vy, J.vnb, lane) : 0;
-  PPROF(2);
+  if (kreg == 0) PPROF(2);
   auto store_resid = [&]() {
     if (!rlds || rreg || rsreg) return;
     if (rvload) {
@@ -582,9 +589,9 @@ __device__ __forceinline__ void run_step(const IntraParams &P, const IntraJob &J
   const int lu_ = ch ? 1 : 2;
   const bool direct = (KIND == K_REG || KIND == K_CIIP || KIND == K_BDPCM) && (J.vnb & CS_PREFIX) && (J.vnb & CS_INTILE) &&
                       (J.vnb & CS_CORNER) && J.nul > 0 && J.nut > 0 && (!refFilter || dirMode == PLANAR);
-  // ISP: the regions of the CU in order; region k reads the CU-level lines and region k-1
-#pragma nounroll
-  for (int kreg = 0; kreg < nreg; kreg++) {
+  // ISP: region kreg of the CU (the kernel runs them in order); region k reads the CU-level lines and
+  // region k-1
+  {
   if (kreg == 0) PPROF(3);
   const int x0 = J.x + (ispVer ? kreg * w : 0), y0 = J.y + (isp && !ispVer ? kreg * h : 0);
 
@@ -1105,26 +1112,40 @@ __global__ __launch_bounds__(64 * NW) void k_intra(const IntraParams *__restrict
       }
     }
     __syncthreads();
-    for (;;) {
-      // uniform control flow only (no lane-0 regions anywhere around the step body): every lane adds,
-      // lane 0 adds 1, and lane 0's result is the step
-      const int lj = __builtin_amdgcn_readfirstlane(atomicAdd(&s_next, lane == 0 ? 1 : 0));
-      if (lj >= nj) break;
-      const int gj = j0 + lj;
-      const IntraJob J = jobs[gj];
-      unsigned long long t_ready = 0, ps[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // One iteration per step, and per region of an ISP step (kreg / nk): the regions are iterations of
+    // this loop so that nothing of a region's set-up is loop-invariant (run_step).
+    IntraJob J{};
+    int lj = 0, gj = 0, kreg = 0, nk = 0;
+    unsigned long long t_ready = 0, ps[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #ifdef VVCR_INTRA_PROF
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long t0 = 0;
 #endif
-      switch (step_kind(J)) {
-        case K_REG: run_step<K_REG>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
-        case K_ISP: run_step<K_ISP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
-        case K_MIP: run_step<K_MIP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
-        case K_LM: run_step<K_LM>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
-        case K_CIIP: run_step<K_CIIP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
-        case K_BDPCM: run_step<K_BDPCM>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
-        default: run_step<K_INTERC>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps); break;
+    for (;;) {
+      if (kreg == nk) {
+        // uniform control flow only (no lane-0 regions anywhere around the step body): every lane adds,
+        // lane 0 adds 1, and lane 0's result is the step
+        lj = __builtin_amdgcn_readfirstlane(atomicAdd(&s_next, lane == 0 ? 1 : 0));
+        if (lj >= nj) break;
+        gj = j0 + lj;
+        J = jobs[gj];
+        kreg = 0;
+        nk = (J.flags & (IJ_ISP_HOR | IJ_ISP_VER)) ? J.isp_k : 1;
+        t_ready = 0;
+#ifdef VVCR_INTRA_PROF
+        for (int q = 0; q < 10; q++) ps[q] = 0;
+        t0 = __builtin_amdgcn_s_memrealtime();
+#endif
       }
+      switch (step_kind(J)) {
+        case K_REG: run_step<K_REG>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps, 0); break;
+        case K_ISP: run_step<K_ISP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps, kreg); break;
+        case K_MIP: run_step<K_MIP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps, 0); break;
+        case K_LM: run_step<K_LM>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps, 0); break;
+        case K_CIIP: run_step<K_CIIP>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps, 0); break;
+        case K_BDPCM: run_step<K_BDPCM>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps, 0); break;
+        default: run_step<K_INTERC>(P, J, G, S, dep_start, deps, gj, done, err, lane, t_ready, ps, 0); break;
+      }
+      if (++kreg < nk) continue;   // the step's next region
       // hand-off: LDS stores of this wave complete before its done byte; a step read by another CTU
       // also drains its HBM stores (sc1) before its global flag
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
