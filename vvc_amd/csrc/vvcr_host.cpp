@@ -77,9 +77,10 @@ void sort_by_size_bi(bigbuf::vec<McJob> &v) {
   }
   int pos[128], run = 0;
   for (int k = 0; k < 128; k++) { pos[k] = run; run += cnt[k]; }
-  bigbuf::vec<McJob> out(v.size());
+  static thread_local bigbuf::raw<McJob> out;   // (a value-initialised vector would zero it first)
+  if (out.size() < v.size()) out.alloc(v.size() + v.size() / 4, false);
   for (const McJob &j : v) out[pos[127 - ((lg(j.w) * 8 + lg(j.h)) * 2 + (mc_bi(j) ? 1 : 0))]++] = j;
-  v.swap(out);
+  if (!v.empty()) std::memcpy((void *)v.data(), out.data(), v.size() * sizeof(McJob));
 }
 
 // A k_mc class table over job arrays laid out one after another from job index base (each flagged: its
@@ -526,10 +527,13 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   // then share one size and mostly one prediction direction
   sort_by_size_bi(wl.mc_basic);
   // jobs whose windows may leave the picture: to the edge list (same order rules), the rest stay
-  auto split_edge = [&](bigbuf::vec<McJob> &v) {
-    auto mid = std::stable_partition(v.begin(), v.end(), [&](const McJob &j) { return !mc_job_edge(j, sp.width, sp.height); });
-    wl.mc_edge.insert(wl.mc_edge.end(), mid, v.end());
-    v.erase(mid, v.end());
+  auto split_edge = [&](bigbuf::vec<McJob> &v) {   // stable, in place (std::stable_partition allocates)
+    size_t k = 0;
+    for (size_t i = 0; i < v.size(); i++) {
+      if (mc_job_edge(v[i], sp.width, sp.height)) wl.mc_edge.push_back(v[i]);
+      else v[k++] = v[i];
+    }
+    v.resize(k);
   };
   split_edge(wl.mc_tile);
   split_edge(wl.mc_basic);
@@ -537,10 +541,19 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
   // the edge classes first: their waves (longer, per-row clamped gathers) start in the first round
   mark("sorts");
   build_mc_classes(wl.mc_ct, {{&wl.mc_edge, true}, {&wl.mc_tile, false}, {&wl.mc_basic, false}}, 0);
-  std::stable_partition(wl.aff_jobs.begin(), wl.aff_jobs.end(), [&](const AffJob &j) {
-    const AffPu &U = wl.aff_pu[j.pu];
-    return U.l[0].present && U.l[1].present;
-  });
+  mark("classes");
+  {   // bi-predicted affine tiles first, stable (in place: std::stable_partition allocates)
+    static thread_local bigbuf::raw<AffJob> uni;
+    if (uni.size() < wl.aff_jobs.size()) uni.alloc(wl.aff_jobs.size() + wl.aff_jobs.size() / 4, false);
+    size_t k = 0, u = 0;
+    for (size_t i = 0; i < wl.aff_jobs.size(); i++) {
+      const AffPu &U = wl.aff_pu[wl.aff_jobs[i].pu];
+      if (U.l[0].present && U.l[1].present) wl.aff_jobs[k++] = wl.aff_jobs[i];
+      else uni[u++] = wl.aff_jobs[i];
+    }
+    if (u) std::memcpy((void *)(wl.aff_jobs.data() + k), uni.data(), u * sizeof(AffJob));
+  }
+  mark("affine");
   for (const bigbuf::vec<McJob> *v : {&wl.mc_tile, &wl.mc_basic, &wl.mc_edge, &wl.mc_bidir})
     for (const McJob &j : *v)
       for (int l = 0; l < 2; l++)
@@ -549,6 +562,7 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
     wl.ref_y0 = std::max(0, ry0);
     wl.ref_y1 = std::min(sp.height, ry1);
   }
+  mark("reach");
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -97,8 +97,8 @@ struct Planner {
   // intra, CIIP, chroma steps) carry their own order / level / producers in out.order / level / prod,
   // initialised when the CU is planned; the units of a plain inter CU share its cu_seq, level 0 and no
   // producer, so a B picture's inter CUs cost no per-unit work.
-  bigbuf::vec<int32_t> level[2];
-  bigbuf::vec<int32_t> prod[3];     // per unit of each component: the step (index into jobs) that reconstructs it
+  bigbuf::raw<int32_t> level[2];
+  bigbuf::raw<int32_t> prod[3];     // per unit of each component: the step (index into jobs) that reconstructs it
   const int32_t *umap[2] = {nullptr, nullptr};
   bigbuf::vec<int32_t> own_map[2];
   bigbuf::vec<int32_t> cu_seq;      // per CU: the seq of a plain inter CU, kInf until planned
@@ -527,8 +527,9 @@ struct Planner {
   }
     const size_t nu = (size_t)W4 * H4;
     // per-unit arrays without initialisation: only the units of written CUs are read (touch)
-    for (int k = 0; k < 2; k++) { out.order[k].resize(nu); level[k].resize(nu); }
-    for (int k = 0; k < 3; k++) prod[k].resize(nu);
+    // (resize would zero 7 arrays of a unit each per picture, 14 MB at 4K, for the few units a B picture plans)
+    for (int k = 0; k < 2; k++) { out.order[k].alloc(nu, false); level[k].alloc(nu, false); }
+    for (int k = 0; k < 3; k++) prod[k].alloc(nu, false);
     cu_seq.assign(d.cu.size(), kInf);
     for (int k = 0; k < 2; k++) written[k].assign(d.cu.size(), 0);
     for (int k = 0; k < 2; k++) {
