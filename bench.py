@@ -668,6 +668,9 @@ def main():
         "cpu_baseline": None,
         "single_stream": single,
         "resident": resident,
+        # the GPU time the end-to-end run needs, as a fraction of its wall time: value / the GPU-only rate
+        # of the same pictures (resident); the rest of the time the GPU waits for the host
+        "gpu_busy_est": round(value / resident["value"], 3) if resident and resident["value"] > 0 else None,
         "mc_roofline": mc_roof,
         "north_star_mc": ns_mc,
         "kernels": {k: {"ms_per_step": round(v[1], 4), "ms_min_max": [round(v[3], 4), round(v[4], 4)], "launches_per_step": v[0],

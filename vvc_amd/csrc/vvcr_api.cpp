@@ -572,8 +572,8 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
 
 // Diagnostics (VVCR_PREP_PROF): summed wall time of prepare()'s phases over all calls, printed at exit.
 namespace prep_prof {
-constexpr int N = 5;
-const char *const names[N] = {"wait", "resid+inter", "intra+dbk+lf", "place", "copy"};
+constexpr int N = 9;
+const char *const names[N] = {"wait", "resid", "inter-lists", "mc_done", "dmvr-bufs", "inter-bytes", "intra+dbk+lf", "place", "copy"};
 std::atomic<uint64_t> ns[N], calls;
 const bool on = getenv("VVCR_PREP_PROF") != nullptr;
 struct Report {
@@ -635,6 +635,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     for (const TbJob &t : wl.tb) b += (double)t.w * t.h * ((t.flags & TB_ZERO) ? 2 : 4 + 2);   // int32 levels in, int16 residual out
     r.alg_bytes[K_RESID] = b;
   }
+  pt.mark(1);
   if (mask & VVCR_STAGE_INTER) {
     // 32x32 tiles first, then the small jobs, in one array
     st.add(r.mc_basic, {{wl.mc_edge.data(), wl.mc_edge.size()}, {wl.mc_tile.data(), wl.mc_tile.size()},
@@ -652,8 +653,10 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.n_bidir = (int)wl.mc_bidir.size();
     r.n_aff = (int)wl.aff_jobs.size();
     r.n_dmvr = wl.n_dmvr;
+    pt.mark(2);
     // the previous launch's delta read-back (copy stream, after its inter stage) may still be queued
     VVCR_CHECK_HIP(hipEventSynchronize(r.mc_done));
+    pt.mark(3);
     r.dmvr.ensure(2 * (size_t)r.n_dmvr + 2);
     if (r.h_dmvr_cap < 2 * (size_t)r.n_dmvr + 2) {
       if (r.h_dmvr) VVCR_CHECK_HIP(hipHostFree(r.h_dmvr));
@@ -661,6 +664,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
       r.h_dmvr_cap = 2 * (size_t)r.n_dmvr + 2;
       VVCR_CHECK_HIP(hipHostMalloc((void **)&r.h_dmvr, r.h_dmvr_cap * sizeof(int32_t), hipHostMallocDefault));
     }
+    pt.mark(4);
     r.alg_bytes[K_MC] = wl.mc_alg;
     double b = 0;
     for (const McJob &j : wl.mc_bidir) b += mc_bytes(j);
@@ -675,7 +679,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     }
     r.alg_bytes[K_MC_AFFINE] = b;
   }
-  pt.mark(1);
+  pt.mark(5);
   if (pp.lmcs_enabled) {
     st.add(r.lmcs_lut, {{pp.lmcs_fwd, 1024}, {pp.lmcs_inv, 1024}});
   }
@@ -752,11 +756,11 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     st.add(r.alf_set, bp.h_alf_set);
     r.alg_bytes[K_ALF] = pix * 2 * 2;
   }
-  pt.mark(2);
+  pt.mark(6);
   st.place();
   if (iparams_off != SIZE_MAX)
     for (int l = 0; l < MAXLANE; l++) st.host_at<IntraParams>(iparams_off)[l] = make_intra_params(ctx, r, l);
-  pt.mark(3);
+  pt.mark(7);
   st.copy(ctx->upload_stream, r.up_done);
   r.up_issued = true;
   if (!st.ext.empty()) {   // the picture's own arrays are read by the DMA until this event
@@ -764,7 +768,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     VVCR_CHECK_HIP(hipEventRecord(bp.up_ev, ctx->upload_stream));
     bp.up_pending = true;
   }
-  pt.mark(4);
+  pt.mark(8);
 }
 
 // The device deblocking planner's arguments for a prepared picture on a lane: the lane's maps and lists
