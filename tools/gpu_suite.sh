@@ -1,5 +1,5 @@
 #!/bin/bash
-# Full GPU test suite, then the default bench line.
+# Full GPU test suite, then the default bench line (tag: gpurun_out/bench_<tag>.json, gpurun_out/<tag>/pytest.log).
 set -o pipefail
 export TMPDIR=/tmp
 T=${1:-r05p}

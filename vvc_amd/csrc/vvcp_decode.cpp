@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <ctime>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -157,7 +158,18 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
   vvcp::Stream &s = h->s;
   const int n = (int)s.pics.size();
   using clk = std::chrono::steady_clock;
-  auto since = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
+  // phase times: wall clock, or with VVCP_CPU_TIMES the calling thread's CPU time (diagnostics: with more
+  // threads than cores the wall time of a phase includes the time its thread waited for a core)
+  static const bool cpu_times = getenv("VVCP_CPU_TIMES") != nullptr;
+  auto tnow = []() -> double {
+    if (cpu_times) {
+      timespec ts;
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+      return ts.tv_sec + ts.tv_nsec * 1e-9;
+    }
+    return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+  };
+  auto since = [&](double a) { return tnow() - a; };
   std::vector<std::thread> pool;
   std::mutex mu;                  // task queue, picture states, phase times
   std::condition_variable cv;
@@ -193,7 +205,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
         if (stop || nextLaunch >= n || !prepared[nextLaunch]) return;
         i = nextLaunch;
       }
-      const auto t0 = clk::now();
+      const double t0 = tnow();
       const int lrc = vvcr_launch_picture(ctx, handle[i]);
       const double tl = since(t0);
       if (lrc < 0) {
@@ -201,7 +213,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
         fail(std::string("vvcr_launch_picture: ") + vvcr_last_error(ctx), VVCR_E_STATE);
         return;
       }
-      const auto t1 = clk::now();
+      const double t1 = tnow();
       while (outPos < P.outOrder.size() && P.outReady[P.outOrder[outPos]] <= i) {
         const int k = P.outOrder[outPos++];
         if (prm->on_output) prm->on_output(prm->user, k, P.poc[k], P.slot[k]);
@@ -223,7 +235,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
     }
   };
   auto plan_one = [&](int i) {
-    auto t0 = clk::now();
+    double t0 = tnow();
     int32_t rs[2 * VVCR_MAX_REF] = {0};
     for (int l = 0; l < 2; l++)
       for (size_t r = 0; r < P.refIdx[l][i].size(); r++) rs[l * VVCR_MAX_REF + r] = P.slot[P.refIdx[l][i][r]];
@@ -231,7 +243,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
     if (vvcp_plan_picture(h, i, &sp, P.slot[i], rs, prm->stage_mask, &pic))
       throw vvcp::ParseError("picture " + std::to_string(i) + " plan: " + vvcp_last_error());
     const double tp = since(t0);
-    t0 = clk::now();
+    t0 = tnow();
     int32_t hd = -1;
     const int urc = vvcr_prepare_planned(ctx, pic, &hd);
     vvcr_picture_destroy(pic);
@@ -269,7 +281,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
         std::lock_guard<std::mutex> lg(lmu);
         launch_ready();
       } else {
-        const auto t0 = clk::now();
+        const double t0 = tnow();
         std::string e;
         try {
           s.parse_picture(task);
@@ -294,7 +306,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
     for (int t = 0; t < nthreads; t++) pool.emplace_back(worker);
     std::vector<int32_t> deltas;
     for (int i = 0; i < n; i++) {
-      auto t0 = clk::now();
+      double t0 = tnow();
       {
         std::unique_lock<std::mutex> g(mu);
         cv.wait(g, [&] { return stop || pstate[i] >= 2; });
@@ -303,7 +315,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
         T[VVCP_PHASE_PARSE_WAIT] += since(t0);
       }
       // the collocated pictures' refined motion: their DMVR deltas from the GPU (after their launch)
-      t0 = clk::now();
+      t0 = tnow();
       for (int j : collocated(*s.pics[i], P, i)) {
         if (refined[j]) continue;
         {
@@ -320,7 +332,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
       }
       T[VVCP_PHASE_DMVR_WAIT] += since(t0);
       if (stop) break;
-      t0 = clk::now();
+      t0 = tnow();
       s.derive_motion(i);
       const int64_t nd = dmvr_subblocks(*s.pics[i]);
       T[VVCP_PHASE_DERIVE] += since(t0);
