@@ -103,21 +103,23 @@ struct CtxModel {
     rate = (uint8_t)(16 * r0 + r1);
   }
   uint8_t state() const { return (uint8_t)((s0 + s1) >> 8); }
-  void update(unsigned bin) {
+  void update(unsigned bin) {   // (no branch on the bin: it is unpredictable)
     const int r0 = rate >> 4, r1 = rate & 15;
-    s0 -= (s0 >> r0) & MASK0;
-    s1 -= (s1 >> r1) & MASK1;
-    if (bin) {
-      s0 += (0x7fffu >> r0) & MASK0;
-      s1 += (0x7fffu >> r1) & MASK1;
-    }
+    const unsigned m = 0u - bin;
+    s0 = (uint16_t)(s0 - ((s0 >> r0) & MASK0) + (((0x7fffu >> r0) & MASK0) & m));
+    s1 = (uint16_t)(s1 - ((s1 >> r1) & MASK1) + (((0x7fffu >> r1) & MASK1) & m));
   }
 };
 
+// The arithmetic decoder keeps VTM's state (range; value with the stream bits aligned as
+// BinDecoderBase keeps them) in a 64-bit window: value64 = VTM's value << 32 plus the next stream bits,
+// so a refill reads 4 bytes every 32 bits consumed instead of one byte every 8. The comparisons against
+// range << 7 (here << 39) see the same bits: VTM's not-yet-read bits are zeros below its 7 guard bits.
 struct Cabac {
   const uint8_t *p = nullptr, *end = nullptr;
-  uint32_t range = 510, value = 0;
-  int bitsNeeded = -8;
+  uint32_t range = 510;
+  uint64_t value = 0;
+  int bitsNeeded = -32;   // the lowest valid bit of value is bit bitsNeeded + 32; refill when it passes 32
   CtxModel ctx[vvcp_ctx::NUM_CTX];
 
   void init_contexts(int qp, int initType) {   // CtxStore::init (Contexts.cpp:939)
@@ -125,12 +127,26 @@ struct Cabac {
     for (int k = 0; k < vvcp_ctx::NUM_CTX; k++) ctx[k].init(cq, vvcp_ctx::kInit[initType][k], vvcp_ctx::kInit[3][k]);
   }
   uint32_t byte() { return p < end ? *p++ : 0; }
+  uint64_t word32() {   // the next 4 stream bytes, big-endian (zeros past the end, as byte())
+    if (end - p >= 4) {
+      const uint32_t w = (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3];
+      p += 4;
+      return w;
+    }
+    uint32_t w = 0;
+    for (int k = 0; k < 4; k++) w = w << 8 | byte();
+    return w;
+  }
+  void refill() {
+    if (bitsNeeded >= 0) { value += word32() << bitsNeeded; bitsNeeded -= 32; }
+  }
   void start(const uint8_t *b, const uint8_t *e) {   // BinDecoderBase::start
     p = b; end = e;
     range = 510;
-    value = (byte() << 8);
-    value += byte();
-    bitsNeeded = -8;
+    value = (uint64_t)byte() << 40;
+    value += (uint64_t)byte() << 32;
+    value += word32();
+    bitsNeeded = -32;
   }
 #ifdef VVCP_TRACE   // bin trace in the format of the reference's D_CABAC channel (BinDecoder.cpp:315)
   int traceCount = 0;
@@ -142,19 +158,19 @@ struct Cabac {
     const unsigned q = st ^ ((0u - mps) & 0xff);   // the LPS probability state
     const uint32_t lps = (((q >> 2) * (range >> 5)) >> 1) + 4;
 #ifdef VVCP_TRACE
-    fprintf(stderr, "%d %d %d  [%d:%d]  %2d(MPS=%d)    -  ", traceCount++, id, range, range - lps, lps, st, value < ((range - lps) << 7));
+    fprintf(stderr, "%d %d %d  [%d:%d]  %2d(MPS=%d)    -  ", traceCount++, id, range, range - lps, lps, st, value < ((uint64_t)(range - lps) << 39));
 #endif
     range -= lps;
-    const uint32_t sr = range << 7;
-    const uint32_t lpsMask = (uint32_t)((int32_t)(sr - 1 - value) >> 31);   // all ones when value >= sr
+    const uint64_t sr = (uint64_t)range << 39;
+    const uint64_t lpsMask = 0 - (uint64_t)(value >= sr);   // all ones when the LPS was decoded
     value -= sr & lpsMask;
-    range ^= (range ^ lps) & lpsMask;
-    const unsigned b = mps ^ (lpsMask & 1);
+    range ^= (range ^ lps) & (uint32_t)lpsMask;
+    const unsigned b = mps ^ (unsigned)(lpsMask & 1);
     const int n = __builtin_clz(range) - 23;   // renormalise to 9 bits (range in [256, 510])
     range <<= n;
     value <<= n;
     bitsNeeded += n;
-    if (bitsNeeded >= 0) { value += byte() << bitsNeeded; bitsNeeded -= 8; }
+    refill();
     m.update(b);
 #ifdef VVCP_TRACE
     fprintf(stderr, "%d\n", b);
@@ -163,16 +179,18 @@ struct Cabac {
   }
   unsigned ep() {   // decodeBinEP
     value += value;
-    if (++bitsNeeded >= 0) { value += byte(); bitsNeeded = -8; }
-    const uint32_t sr = range << 7;
-    const uint32_t mask = (uint32_t)((int32_t)(sr - 1 - value) >> 31);
+    ++bitsNeeded;
+    refill();
+    const uint64_t sr = (uint64_t)range << 39;
+    const uint64_t mask = 0 - (uint64_t)(value >= sr);
     value -= sr & mask;
 #ifdef VVCP_TRACE
-    fprintf(stderr, "%d  %d  EP=%d \n", traceCount++, range, mask & 1);
+    fprintf(stderr, "%d  %d  EP=%d \n", traceCount++, range, (int)(mask & 1));
 #endif
-    return mask & 1;
+    return (unsigned)(mask & 1);
   }
-  // decodeBinsEP: n bypass bins, the most significant first; whole bytes are shifted in at once
+  // decodeBinsEP: n bypass bins, the most significant first, in chunks of up to 8 (one shift and at most
+  // one refill per chunk, then a compare-subtract per bin against range << 39..46)
 #ifdef VVCP_TRACE
   unsigned eps(unsigned n) {
     unsigned v = 0;
@@ -182,36 +200,31 @@ struct Cabac {
 #else
   unsigned eps(unsigned n) {
     unsigned v = 0;
-    for (; n > 8; n -= 8) {   // 8 bins: a byte in, then 8 compare-subtract steps against range << 7..14
-      value = (value << 8) + (byte() << (8 + bitsNeeded));
-      uint32_t sr = range << 15;
-      for (int i = 0; i < 8; i++) {
+    while (n) {
+      const unsigned k = n < 8 ? n : 8;
+      value <<= k;
+      bitsNeeded += (int)k;
+      refill();
+      uint64_t sr = (uint64_t)range << (39 + k);
+      for (unsigned i = 0; i < k; i++) {
         sr >>= 1;
-        const uint32_t mask = (uint32_t)((int32_t)(sr - 1 - value) >> 31);
+        const uint64_t mask = 0 - (uint64_t)(value >= sr);
         value -= sr & mask;
-        v = v + v + (mask & 1);
+        v = v + v + (unsigned)(mask & 1);
       }
-    }
-    bitsNeeded += (int)n;
-    value <<= n;
-    if (bitsNeeded >= 0) { value += byte() << bitsNeeded; bitsNeeded -= 8; }
-    uint32_t sr = range << (n + 7);
-    for (unsigned i = 0; i < n; i++) {
-      sr >>= 1;
-      const uint32_t mask = (uint32_t)((int32_t)(sr - 1 - value) >> 31);
-      value -= sr & mask;
-      v = v + v + (mask & 1);
+      n -= k;
     }
     return v;
   }
 #endif
   unsigned trm() {   // decodeBinTrm
     range -= 2;
-    const uint32_t sr = range << 7;
+    const uint64_t sr = (uint64_t)range << 39;
     if (value >= sr) return 1;
     if (range < 256) {
       range += range; value += value;
-      if (++bitsNeeded == 0) { value += byte(); bitsNeeded = -8; }
+      ++bitsNeeded;
+      refill();
     }
     return 0;
   }

@@ -50,9 +50,15 @@ struct DiagGen {   // ScanGenerator, SCAN_DIAG
   }
 };
 
+// The regular residual path decodes levels into a padded block: row stride kPS, and the two columns
+// right of a 64-wide block and the two rows below any block stay zero, so the context templates
+// (CoeffCodingContext::sigCtxIdAbs / templateAbsSum, ContextModelling.h:105-190) read their five
+// neighbours without bounds tests (the zeros are exactly the reference's "outside the block").
+constexpr int kPS = 66;
 struct Scans {
   std::vector<ScanPos> grouped[7][7], plain[7][7];
   std::vector<uint16_t> groupedInv[7][7];   // raster index -> first grouped scan position holding it
+  std::vector<uint16_t> groupedP[7][7];     // grouped scan position -> index in the padded block
   Scans() {
     for (int lw = 0; lw < 7; lw++)
       for (int lh = 0; lh < 7; lh++) {
@@ -80,6 +86,9 @@ struct Scans {
         std::vector<uint16_t> &inv = groupedInv[lw][lh];
         inv.assign(w * h, (uint16_t)(w * h - 1));
         for (int sp = w * h - 2; sp >= 0; sp--) inv[s[sp].idx] = (uint16_t)sp;
+        std::vector<uint16_t> &pp = groupedP[lw][lh];
+        pp.resize(w * h);
+        for (int sp = 0; sp < w * h; sp++) pp[sp] = (uint16_t)(s[sp].y * kPS + s[sp].x);
       }
   }
 };
@@ -101,7 +110,7 @@ struct CoefCtx {
   int ch, comp, w, h, log2w, log2CGw, log2CGh, log2CG, wg, hg, maxNumCoeff;
   bool signHiding, bdpcm;
   const ScanPos *scan, *scanCG;
-  const uint16_t *scanInv;
+  const uint16_t *scanInv, *pscan;
   int lastX, lastY, lastOffX = 0, lastOffY = 0, lastShX = 0, lastShY = 0;
   unsigned maxLastPosX, maxLastPosY;
   int scanPosLast = -1, subSetId = -1, subSetPos = -1, subSetPosX = -1, subSetPosY = -1, minSubPos = -1, maxSubPos = -1;
@@ -123,6 +132,7 @@ struct CoefCtx {
     maxNumCoeff = w * h;
     scan = scans().grouped[lw][lh].data();
     scanInv = scans().groupedInv[lw][lh].data();
+    pscan = scans().groupedP[lw][lh].data();
     scanCG = scans().plain[floorLog2(wg)][floorLog2(hg)].data();
     lastX = ch ? LastX1 : LastX0;
     lastY = ch ? LastY1 : LastY0;
@@ -161,21 +171,17 @@ struct CoefCtx {
   bool isSigGroup() const { return (sigCG >> subSetPos) & 1; }
   unsigned lastXCtx(unsigned p) const { return lastX + lastOffX + (p >> lastShX); }
   unsigned lastYCtx(unsigned p) const { return lastY + lastOffY + (p >> lastShY); }
+  // (padded block, kPS: the neighbours outside the block read zeros)
   unsigned sigCtxIdAbs(int sp, const int32_t *coeff, int state) {
-    const int py = scan[sp].y, px = scan[sp].x;
-    const int32_t *d = coeff + px + py * w;
-    const int diag = px + py;
+    const int diag = scan[sp].x + scan[sp].y;
+    const int32_t *d = coeff + pscan[sp];
     int numPos = 0, sumAbs = 0;
     auto upd = [&](int32_t v) { const int a = std::abs(v); sumAbs += std::min(4 + (a & 1), a); numPos += !!a; };
-    if (px < w - 1) {
-      upd(d[1]);
-      if (px < w - 2) upd(d[2]);
-      if (py < h - 1) upd(d[w + 1]);
-    }
-    if (py < h - 1) {
-      upd(d[w]);
-      if (py < h - 2) upd(d[w << 1]);
-    }
+    upd(d[1]);
+    upd(d[2]);
+    upd(d[kPS + 1]);
+    upd(d[kPS]);
+    upd(d[2 * kPS]);
     int ofs = std::min((sumAbs + 1) >> 1, 3) + (diag < 2 ? 4 : 0);
     if (ch == 0) ofs += diag < 5 ? 4 : 0;
     tmplCpDiag = diag;
@@ -190,19 +196,9 @@ struct CoefCtx {
     }
     return (uint8_t)off;
   }
-  unsigned templateAbsSum(int sp, const int32_t *coeff, int base) const {
-    const int py = scan[sp].y, px = scan[sp].x;
-    const int32_t *d = coeff + px + py * w;
-    int sum = 0;
-    if (px < w - 1) {
-      sum += std::abs(d[1]);
-      if (px < w - 2) sum += std::abs(d[2]);
-      if (py < h - 1) sum += std::abs(d[w + 1]);
-    }
-    if (py < h - 1) {
-      sum += std::abs(d[w]);
-      if (py < h - 2) sum += std::abs(d[w << 1]);
-    }
+  unsigned templateAbsSum(int sp, const int32_t *coeff, int base) const {   // (padded block)
+    const int32_t *d = coeff + pscan[sp];
+    const int sum = std::abs(d[1]) + std::abs(d[2]) + std::abs(d[kPS + 1]) + std::abs(d[kPS]) + std::abs(d[2 * kPS]);
     return (unsigned)std::max(std::min(sum - 5 * base, 31), 0);
   }
   unsigned sigCtxIdAbsTS(int sp, const int32_t *coeff) const {
@@ -1583,7 +1579,9 @@ struct Parser {
       const int w = tt.b[comp][2];
       const bool coded = comp == 0 ? cbfLuma : (!lumaOnly && tt.b[comp][4]);
       boxR = boxC = 0;
-      if (coded) residual_coding(ci, ti, comp, cuCtx, scratch);
+      lvl = scratch;
+      lvlStride = w;
+      if (coded) residual_coding(ci, ti, comp, cuCtx);
       const size_t off = pic.coef.size();
       tt.b[comp][6] = (int32_t)off;
       pic.box[3 * (size_t)ti + comp] = (uint16_t)(boxR | boxC << 8);
@@ -1591,13 +1589,16 @@ struct Parser {
         pic.coef.resize(off + (size_t)boxR * boxC);
         int32_t *dst = pic.coef.data() + off;
         for (int y = 0; y < boxR; y++, dst += boxC) {
-          std::memcpy(dst, scratch + y * w, (size_t)boxC * sizeof(int32_t));
-          std::memset(scratch + y * w, 0, (size_t)boxC * sizeof(int32_t));
+          std::memcpy(dst, lvl + y * lvlStride, (size_t)boxC * sizeof(int32_t));
+          std::memset(lvl + y * lvlStride, 0, (size_t)boxC * sizeof(int32_t));
         }
       }
     }
   }
   alignas(64) int32_t scratch[64 * 64] = {};   // one transform block's levels, zero between blocks
+  alignas(64) int32_t pscratch[kPS * kPS] = {}; // the same, padded (regular residual path: kPS)
+  int32_t *lvl = scratch;                       // the block the last residual_coding wrote, and its stride
+  int lvlStride = 0;
   int boxR = 0, boxC = 0;                      // bounding box of its non-zero levels (rows, columns)
 
   int cu_qp_delta(int predQP) {   // CABACReader::cu_qp_delta (:2850)
@@ -1631,7 +1632,7 @@ struct Parser {
   }
 
   // residual_coding (:2918)
-  void residual_coding(int ci, int ti, int comp, CuCtx &cuCtx, int32_t *coeff) {   // coeff: zeroed w*h
+  void residual_coding(int ci, int ti, int comp, CuCtx &cuCtx) {   // into lvl (zeroed), set here
     const vvcr_cu &c = pic.cu[ci];
     vvcr_tu &t = pic.tu[ti];
     const int w = t.b[comp][2], h = t.b[comp][3];
@@ -1640,7 +1641,10 @@ struct Parser {
     int ts = ((c.bdpcm && comp == 0) || (c.bdpcmc && comp != 0)) ? 1 : (t.b[comp][5] == MTS_SKIP ? 1 : 0);
     if (tsAllowed(c, t, comp)) ts = cab.bin(TransformSkipFlag + (comp == 0 ? 0 : 1));
     t.b[comp][5] = ts ? MTS_SKIP : MTS_DCT2;
-    if (ts) { residual_codingTS(c, comp, w, h, coeff); boxR = h; boxC = w; return; }
+    if (ts) { lvl = scratch; lvlStride = w; residual_codingTS(c, comp, w, h, scratch); boxR = h; boxC = w; return; }
+    lvl = pscratch;
+    lvlStride = kPS;
+    int32_t *coeff = pscratch;
     const bool signHiding = ph.signHiding;
     CoefCtx cc(comp, w, h, signHiding, false);
     cc.scanPosLast = last_sig_coeff(cc, c, comp, w, h);
@@ -1705,7 +1709,7 @@ struct Parser {
     int remRegBins = cc.regBinLimit;
     int sigBlkPos[16];
     for (; nextSigPos >= minSubPos && remRegBins >= 4; nextSigPos--) {
-      const int blkPos = cc.scan[nextSigPos].idx;
+      const int blkPos = cc.pscan[nextSigPos];   // (padded block)
       unsigned sigFlag = (!numNonZero && nextSigPos == inferSigPos);
       if (!sigFlag) {
         const unsigned ctx = cc.sigCtxIdAbs(nextSigPos, coeff, state);
@@ -1738,7 +1742,7 @@ struct Parser {
     for (int sp = firstSigPos; sp > firstPosMode2; sp--) {
       const int sumAll = (int)cc.templateAbsSum(sp, coeff, 4);
       const unsigned rice = kGoRiceParsCoeff[sumAll];
-      int32_t &tc = coeff[cc.scan[sp].idx];
+      int32_t &tc = coeff[cc.pscan[sp]];
       if (tc >= 4) {
         const int rem = (int)cab.rem_abs(rice, 5, 15);
         tc += rem << 1;
@@ -1752,7 +1756,7 @@ struct Parser {
       const int tc = rem == pos0 ? 0 : (rem < pos0 ? rem + 1 : rem);
       state = (stateTab >> ((state << 2) + ((tc & 1) << 1))) & 3;
       if (tc) {
-        const int blkPos = cc.scan[sp].idx;
+        const int blkPos = cc.pscan[sp];
         sigBlkPos[numNonZero++] = blkPos;
         firstNZPos = sp;
         lastNZPos = std::max(lastNZPos, sp);
@@ -1760,8 +1764,9 @@ struct Parser {
       }
     }
     for (int k = 0; k < numNonZero; k++) {
-      boxR = std::max(boxR, (sigBlkPos[k] >> cc.log2w) + 1);
-      boxC = std::max(boxC, (sigBlkPos[k] & (cc.w - 1)) + 1);
+      const int r = sigBlkPos[k] / kPS;
+      boxR = std::max(boxR, r + 1);
+      boxC = std::max(boxC, sigBlkPos[k] - r * kPS + 1);
     }
     const unsigned numSigns = (cc.signHiding && (lastNZPos - firstNZPos >= 4)) ? numNonZero - 1 : numNonZero;
     unsigned signPattern = numSigns ? cab.eps(numSigns) << (32 - numSigns) : 0;

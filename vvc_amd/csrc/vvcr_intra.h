@@ -104,10 +104,8 @@ struct IntraPlan {
   bigbuf::vec<int32_t> ctu_start;    // steps of ctu_list[c]: [ctu_start[c], ctu_start[c+1])
   bigbuf::vec<int32_t> dep_start;    // step i waits for deps[dep_start[i] .. dep_start[i+1]):
   bigbuf::vec<int32_t> deps;         //   v >= 0: step ctu_start[c] + v of its own CTU; v < 0: global step ~v
-  bigbuf::raw<int32_t> order[2];     // per 4x4 luma unit / 2x2 chroma unit: seq of the step that decodes it
-                                     // (uninitialised but for the units of planned CUs: Planner::touch)
   void clear() {
-    inter_tiles.clear(); jobs.clear(); ctu_list.clear(); ctu_start.clear(); dep_start.clear(); deps.clear(); order[0].clear(); order[1].clear();
+    inter_tiles.clear(); jobs.clear(); ctu_list.clear(); ctu_start.clear(); dep_start.clear(); deps.clear();
   }
 };
 

@@ -94,11 +94,15 @@ struct Planner {
   int W4, H4, ctu;
   // Per 4x4 luma unit / 2x2 chroma unit: the CU covering it per channel (umap: the producer's maps when
   // it hands them over, else own_map). Only the units of CUs whose reconstruction is a step ("written":
-  // intra, CIIP, chroma steps) carry their own order / level / producers in out.order / level / prod,
+  // intra, CIIP, chroma steps) carry their own order / level / producers in ur (one record per unit:
+  // the planner's unit visits touch one cache line, not five arrays),
   // initialised when the CU is planned; the units of a plain inter CU share its cu_seq, level 0 and no
   // producer, so a B picture's inter CUs cost no per-unit work.
-  bigbuf::raw<int32_t> level[2];
-  bigbuf::raw<int32_t> prod[3];     // per unit of each component: the step (index into jobs) that reconstructs it
+  // per unit of channel ch: decoding order (seq), level, and the steps (indices into jobs) that reconstruct
+  // it: prod[0] luma (ch 0) or Cb, prod[1] Cr (ch 1)
+  struct UnitRec { int32_t order, level, prod[2]; };
+  bigbuf::raw<UnitRec> ur[2];
+  static int pslot(int comp) { return comp == 2 ? 1 : 0; }
   const int32_t *umap[2] = {nullptr, nullptr};
   bigbuf::vec<int32_t> own_map[2];
   bigbuf::vec<int32_t> cu_seq;      // per CU: the seq of a plain inter CU, kInf until planned
@@ -107,7 +111,7 @@ struct Planner {
   int32_t order_of(int ch, size_t i) const {
     const int32_t m = umap[ch][i];
     if (m < 0) return kInf;
-    return written[ch][m] ? out.order[ch][i] : cu_seq[m];
+    return written[ch][m] ? ur[ch][i].order : cu_seq[m];
   }
   // first write of CU ci's units of channel ch: their own order / level / producers from here on
   void touch(int ch, int ci) {
@@ -119,10 +123,7 @@ struct Planner {
     for (int uy = y >> s; uy < (y + h + (1 << s) - 1) >> s; uy++)
       for (int ux = x >> s; ux < (x + w + (1 << s) - 1) >> s; ux++) {
         const size_t i = (size_t)uy * W4 + ux;
-        out.order[ch][i] = kInf;
-        level[ch][i] = 0;
-        if (ch) prod[1][i] = prod[2][i] = -1;
-        else prod[0][i] = -1;
+        ur[ch][i] = UnitRec{kInf, 0, {-1, -1}};
       }
   }
   bigbuf::vec<std::pair<int32_t, IntraJob>> jobs;   // (level, job)
@@ -170,12 +171,14 @@ struct Planner {
       for (int ux = x0 >> s; ux <= (x1 >> s); ux++) {
         const size_t i = (size_t)uy * W4 + ux;
         const int32_t cu = umap[ch][i];
-        if (cu < 0 || !written[ch][cu] || out.order[ch][i] >= seq) continue;
+        if (cu < 0 || !written[ch][cu]) continue;
+        const UnitRec &r = ur[ch][i];
+        if (r.order >= seq) continue;
         const int c = (uy >> lg) * wc + (ux >> lg);
         if (c != lastc) { lastc = c; regok = ctu_reg[c] == cur_reg; }
         if (!regok) continue;
-        m = std::max(m, level[ch][i]);
-        const int32_t pr = prod[comp][i];
+        m = std::max(m, r.level);
+        const int32_t pr = r.prod[pslot(comp)];
         if (pr >= 0) add_dep(pr);
       }
     return m;
@@ -186,9 +189,10 @@ struct Planner {
     for (int uy = y >> s; uy < (y + h + (1 << s) - 1) >> s; uy++)
       for (int ux = x >> s; ux < (x + w + (1 << s) - 1) >> s; ux++) {
         const size_t i = (size_t)uy * W4 + ux;
-        level[ch][i] = lev;
-        if (set_order) out.order[ch][i] = seq;
-        if (comp >= 0) prod[comp][i] = job;
+        UnitRec &r = ur[ch][i];
+        r.level = lev;
+        if (set_order) r.order = seq;
+        if (comp >= 0) r.prod[pslot(comp)] = job;
       }
   }
   // level of a prediction from the reference lines of region (x, y, w, h) with lengths topLen/leftLen
@@ -528,8 +532,7 @@ struct Planner {
     const size_t nu = (size_t)W4 * H4;
     // per-unit arrays without initialisation: only the units of written CUs are read (touch)
     // (resize would zero 7 arrays of a unit each per picture, 14 MB at 4K, for the few units a B picture plans)
-    for (int k = 0; k < 2; k++) { out.order[k].alloc(nu, false); level[k].alloc(nu, false); }
-    for (int k = 0; k < 3; k++) prod[k].alloc(nu, false);
+    for (int k = 0; k < 2; k++) ur[k].alloc(nu, false);
     cu_seq.assign(d.cu.size(), kInf);
     for (int k = 0; k < 2; k++) written[k].assign(d.cu.size(), 0);
     for (int k = 0; k < 2; k++) {
