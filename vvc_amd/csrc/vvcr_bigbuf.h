@@ -10,6 +10,8 @@
 #pragma once
 #include <atomic>
 #include <unordered_set>
+#include <unistd.h>
+#include <algorithm>
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
@@ -24,11 +26,17 @@ constexpr size_t kMin = 256 << 10;
 // the cache's capacity: VVCR_BIGBUF_CAP_GB (default 24: with 16 decodes in flight the freed blocks of
 // the pictures between their parse and their upload exceed 3 GB; a smaller cache then frees and
 // re-allocates page-locked blocks, whose allocation is slow and serialised in the runtime — 4K bench
-// 5.56 Gpx/s unpinned at 3 GB, 5.62 unpinned at 24 GB, 6.38 pinned at 24 GB, 3.41 pinned at 3 GB)
+// 5.56 Gpx/s unpinned at 3 GB, 6.38 pinned at 24 GB, 3.41 pinned at 3 GB), bounded by the host memory per
+// process: a node's ranks (LOCAL_WORLD_SIZE) share its RAM
 inline size_t cache_cap() {
   static const size_t cap = [] {
-    const char *e = std::getenv("VVCR_BIGBUF_CAP_GB");
-    return (e ? (size_t)std::atoll(e) : size_t(24)) << 30;
+    if (const char *e = std::getenv("VVCR_BIGBUF_CAP_GB")) return (size_t)std::atoll(e) << 30;
+    const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+    const char *lw = std::getenv("LOCAL_WORLD_SIZE");
+    if (!lw) lw = std::getenv("WORLD_SIZE");
+    const size_t ranks = lw && std::atoi(lw) > 0 ? (size_t)std::atoi(lw) : 1;
+    const size_t share = pages > 0 && psz > 0 ? (size_t)pages * (size_t)psz / (4 * ranks) : (size_t(24) << 30);
+    return std::min(size_t(24) << 30, share);
   }();
   return cap;
 }
