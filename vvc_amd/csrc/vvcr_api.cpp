@@ -530,16 +530,7 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
     fprintf(stderr, "  plan %-10s %.2f ms\n", n, std::chrono::duration<double, std::milli>(t - tp).count());
     tp = t;
   };
-  if ((mask & VVCR_STAGE_DBK) && b.dbk_gpu) {
-    // (a picture without inter CUs needs no motion field: the planner never reads it then)
-    bool inter = false;
-    if (b.desc.motion.empty())
-      for (const vvcr_cu &c : b.desc.cu) inter |= c.predmode != 1;   // vvcr_cu::predmode: 1 intra
-    if ((inter || !b.desc.motion.empty()) && b.desc.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4))
-      throw VvcrError(VVCR_E_ARG, "deblocking: the motion field does not cover the picture");
-    pack_dbk_inputs(sp, pp, b.desc, b.dbkg);
-    mark("dbk_pack");
-  } else if (mask & VVCR_STAGE_DBK)
+  if ((mask & VVCR_STAGE_DBK) && !b.dbk_gpu)
     dbk_thread = std::thread([&] {
       try {
         plan_deblocking(sp, pp, b.desc, b.dbk);
@@ -547,16 +538,48 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
         dbk_err = std::current_exception();
       }
     });
+  // the deblocking inputs and the work lists; for a large picture (an intra picture: thousands of CUs)
+  // on a second thread beside the intra plan, which is the longest of the three (its latency is on a
+  // single stream's critical path: the later pictures launch after it)
+  std::exception_ptr side_err;
+  auto side_work = [&] {
+    try {
+      if ((mask & VVCR_STAGE_DBK) && b.dbk_gpu) {
+        // (a picture without inter CUs needs no motion field: the planner never reads it then)
+        bool inter = false;
+        if (b.desc.motion.empty())
+          for (const vvcr_cu &c : b.desc.cu) inter |= c.predmode != 1;   // vvcr_cu::predmode: 1 intra
+        if ((inter || !b.desc.motion.empty()) && b.desc.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4))
+          throw VvcrError(VVCR_E_ARG, "deblocking: the motion field does not cover the picture");
+        pack_dbk_inputs(sp, pp, b.desc, b.dbkg);
+      }
+      if (mask & (VVCR_STAGE_RESID | VVCR_STAGE_INTER)) build_work_lists(sp, pp, b.desc, b.wl, fuse);
+    } catch (...) {
+      side_err = std::current_exception();
+    }
+  };
+  static const bool serial = getenv("VVCR_PLAN_SERIAL") != nullptr;
+  std::thread side;
+  if ((mask & VVCR_STAGE_INTRA) && b.desc.cu.size() >= 16384 && !serial) side = std::thread(side_work);
+  else side_work();
+  mark(side.joinable() ? "side_start" : "dbk+lists");
   try {
-    if (mask & (VVCR_STAGE_RESID | VVCR_STAGE_INTER)) build_work_lists(sp, pp, b.desc, b.wl, fuse);
-    mark("work_lists");
-    if ((mask & VVCR_STAGE_INTER) && b.wl.n_unsupported_inter)
-      throw VvcrError(VVCR_E_UNSUPPORTED, std::to_string(b.wl.n_unsupported_inter) + " inter CUs use tools not supported yet");
     if (mask & VVCR_STAGE_INTRA) plan_intra(sp, pp, b.desc, b.intra, fuse);
     mark("intra");
   } catch (...) {
+    if (side.joinable()) side.join();
     if (dbk_thread.joinable()) dbk_thread.join();
     throw;
+  }
+  if (side.joinable()) side.join();
+  mark("side_join");
+  if (side_err) {
+    if (dbk_thread.joinable()) dbk_thread.join();
+    std::rethrow_exception(side_err);
+  }
+  if ((mask & VVCR_STAGE_INTER) && b.wl.n_unsupported_inter) {
+    if (dbk_thread.joinable()) dbk_thread.join();
+    throw VvcrError(VVCR_E_UNSUPPORTED, std::to_string(b.wl.n_unsupported_inter) + " inter CUs use tools not supported yet");
   }
   if (dbk_thread.joinable()) dbk_thread.join();
   if (dbk_err) std::rethrow_exception(dbk_err);

@@ -13,6 +13,8 @@
 #include <cstring>
 #include <memory>
 #include <queue>
+#include <thread>
+#include <exception>
 #include <string>
 #include <chrono>
 #include <cstdio>
@@ -423,11 +425,11 @@ struct Planner {
 
   // ---- availability, as the reference evaluates it when the step runs (final order map: a unit is
   // decoded before step s iff order < s)
-  bool av(int ch, int x, int y, int sq) const {
+  bool av(int ch, int x, int y, int sq, int reg) const {   // reg: the region of the step being resolved
     const int pw = ch ? sp.width / 2 : sp.width, ph = ch ? sp.height / 2 : sp.height;
     if (x < 0 || y < 0 || x >= pw || y >= ph) return false;
     const int s = ch ? 1 : 2, cs = ch ? 1 : 0;
-    return order_of(ch, (size_t)(y >> s) * W4 + (x >> s)) < sq && region_at(x << cs, y << cs) == cur_reg;
+    return order_of(ch, (size_t)(y >> s) * W4 + (x >> s)) < sq && region_at(x << cs, y << cs) == reg;
   }
   // xFillReferenceSamples unit scan (IntraPrediction.cpp:913-986, isAboveAvailable etc. :1208-1310):
   // returns the 65-bit availability mask in (lo, hi)
@@ -435,18 +437,18 @@ struct Planner {
     bool prefix, corner;
     int nul, nut;
   };
-  void fill_mask(int ch, int sq, int fx, int fy, int fw, int fh, int predSize, int predHSize, uint64_t &lo, uint32_t &hi,
+  void fill_mask(int ch, int sq, int reg, int fx, int fy, int fw, int fh, int predSize, int predHSize, uint64_t &lo, uint32_t &hi,
                  FillShape *shape = nullptr) const {
     const int uw = ch ? 2 : 4, uh = uw;
     const int totalAbove = (predSize + uw - 1) / uw, totalLeft = (predHSize + uh - 1) / uh;
     const int numAbove = std::max(fw / uw, 1), numLeft = std::max(fh / uh, 1);
     const int numAR = totalAbove - numAbove, numBL = totalLeft - numLeft;
     bool F[2 * 64 + 1] = {};
-    F[totalLeft] = av(ch, fx - 1, fy - 1, sq);
-    for (int i = 0; i < numAbove && av(ch, fx + i * uw, fy - 1, sq); i++) F[totalLeft + 1 + i] = true;
-    for (int i = 0; i < numAR && av(ch, fx + fw - 1 + uw + i * uw, fy - 1, sq); i++) F[totalLeft + 1 + numAbove + i] = true;
-    for (int i = 0; i < numLeft && av(ch, fx - 1, fy + i * uh, sq); i++) F[totalLeft - 1 - i] = true;
-    for (int i = 0; i < numBL && av(ch, fx - 1, fy + fh - 1 + uh + i * uh, sq); i++) F[totalLeft - 1 - numLeft - i] = true;
+    F[totalLeft] = av(ch, fx - 1, fy - 1, sq, reg);
+    for (int i = 0; i < numAbove && av(ch, fx + i * uw, fy - 1, sq, reg); i++) F[totalLeft + 1 + i] = true;
+    for (int i = 0; i < numAR && av(ch, fx + fw - 1 + uw + i * uw, fy - 1, sq, reg); i++) F[totalLeft + 1 + numAbove + i] = true;
+    for (int i = 0; i < numLeft && av(ch, fx - 1, fy + i * uh, sq, reg); i++) F[totalLeft - 1 - i] = true;
+    for (int i = 0; i < numBL && av(ch, fx - 1, fy + fh - 1 + uh + i * uh, sq, reg); i++) F[totalLeft - 1 - numLeft - i] = true;
     lo = 0; hi = 0;
     const int total = totalAbove + totalLeft + 1;
     if (total > 65) throw VvcrError(VVCR_E_STATE, "intra plan: more than 65 reference units");
@@ -464,31 +466,32 @@ struct Planner {
     }
   }
   // CCLM neighbourhood (above / left complete, above-right / below-left unit counts): 12 bits
-  uint32_t nb_bits(int ch, int sq, int x, int y, int w, int h, int unit) const {
+  uint32_t nb_bits(int ch, int sq, int reg, int x, int y, int w, int h, int unit) const {
     const int na = w / unit, nl = h / unit;
     int l = 0, a = 0, bl = 0, ar = 0;
-    while (l < nl && av(ch, x - 1, y + l * unit, sq)) l++;
-    while (a < na && av(ch, x + a * unit, y - 1, sq)) a++;
+    while (l < nl && av(ch, x - 1, y + l * unit, sq, reg)) l++;
+    while (a < na && av(ch, x + a * unit, y - 1, sq, reg)) a++;
     const bool left = l == nl, above = a == na;
-    if (left) while (bl < nl && av(ch, x - 1, y + h - 1 + unit + bl * unit, sq)) bl++;
-    if (above) while (ar < na && av(ch, x + w - 1 + unit + ar * unit, y - 1, sq)) ar++;
+    if (left) while (bl < nl && av(ch, x - 1, y + h - 1 + unit + bl * unit, sq, reg)) bl++;
+    if (above) while (ar < na && av(ch, x + w - 1 + unit + ar * unit, y - 1, sq, reg)) ar++;
     if (ar > 31 || bl > 31) throw VvcrError(VVCR_E_STATE, "intra plan: CCLM neighbourhood too large");
     return (above ? 1u : 0u) | (left ? 2u : 0u) | (uint32_t)ar << 2 | (uint32_t)bl << 7;
   }
-  void resolve_availability(IntraJob &j) {
+  // (const: the steps resolve on several threads)
+  void resolve_availability(IntraJob &j) const {
     const int comp = j.comp, ch = comp ? 1 : 0;
-    cur_reg = region_at(j.cx << ch, j.cy << ch);
+    const int reg = region_at(j.cx << ch, j.cy << ch);
     const bool isp = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0, ver = (j.flags & IJ_ISP_VER) != 0;
     uint64_t lo;
     uint32_t hi;
     FillShape fs;
     int fx, fy, mrl = comp ? 0 : j.mrl;
     if (!isp) {
-      fill_mask(ch, j.seq, j.x, j.y, j.w, j.h, 2 * j.w, 2 * j.h, lo, hi, &fs);
+      fill_mask(ch, j.seq, reg, j.x, j.y, j.w, j.h, 2 * j.w, 2 * j.h, lo, hi, &fs);
       fx = j.x; fy = j.y;
     } else {
       const int fTop = ver ? 2 * j.cw : j.cw + j.w, fLeft = ver ? j.ch + j.h : 2 * j.ch;
-      fill_mask(0, j.seq, j.cx, j.cy, j.cw, j.ch, fTop, fLeft, lo, hi, &fs);
+      fill_mask(0, j.seq, reg, j.cx, j.cy, j.cw, j.ch, fTop, fLeft, lo, hi, &fs);
       fx = j.cx; fy = j.cy; mrl = 0;
     }
     if (fs.prefix && fs.nul < 256 && fs.nut < 256) {
@@ -508,13 +511,13 @@ struct Planner {
     j.av[3] = 0;
     if (isp)
       for (int k = 1; k < j.isp_k && k < 4; k++) {
-        const bool a = ver ? av(0, j.x + k * j.w, j.y - 1, j.seq) : av(0, j.x - 1, j.y + k * j.h, j.seq);
+        const bool a = ver ? av(0, j.x + k * j.w, j.y - 1, j.seq, reg) : av(0, j.x - 1, j.y + k * j.h, j.seq, reg);
         if (a) j.av[2] |= 1u << (8 + k);
       }
     if (comp > 0 && j.mode >= 67 && !(j.flags & IJ_BDPCM)) {
       const bool dual = (j.flags & IJ_DUAL) != 0;
-      const uint32_t lr = dual ? nb_bits(1, j.seq, j.x, j.y, j.w, j.h, 2) : nb_bits(0, j.seq, 2 * j.x, 2 * j.y, 2 * j.w, 2 * j.h, 4);
-      const uint32_t lm = nb_bits(1, j.seq, j.x, j.y, j.w, j.h, 2);
+      const uint32_t lr = dual ? nb_bits(1, j.seq, reg, j.x, j.y, j.w, j.h, 2) : nb_bits(0, j.seq, reg, 2 * j.x, 2 * j.y, 2 * j.w, 2 * j.h, 4);
+      const uint32_t lm = nb_bits(1, j.seq, reg, j.x, j.y, j.w, j.h, 2);
       j.av[2] |= lr << 16;
       j.av[3] = lm;
     }
@@ -822,11 +825,36 @@ struct Planner {
       out.dep_start[i + 1] = (int32_t)out.deps.size();
     }
     PROF_MARK("final");
-    for (IntraJob &j : out.jobs)
-      if (j.xkind != XK_INTER_CHROMA) {
-        resolve_availability(j);   // inter chroma steps read no reference samples
+    // per step, independent of the others (the final order map is read-only now): a large plan (an
+    // intra picture, ~70 k steps at 4K) splits the steps over VVCR_PLAN_THREADS (4) threads
+    auto resolve = [&](size_t a, size_t b) {
+      for (size_t k = a; k < b; k++) {
+        IntraJob &j = out.jobs[k];
+        if (j.xkind == XK_INTER_CHROMA) continue;   // inter chroma steps read no reference samples
+        resolve_availability(j);
         set_pred_params(j);
       }
+    };
+    static const int nthr = [] { const char *e = getenv("VVCR_PLAN_THREADS"); return e ? std::max(1, atoi(e)) : 4; }();
+    const size_t njobs = out.jobs.size();
+    if (njobs >= 16384 && nthr > 1) {
+      std::vector<std::exception_ptr> err(nthr);
+      auto part = [&](int t) {
+        try {
+          resolve(njobs * t / nthr, njobs * (t + 1) / nthr);
+        } catch (...) {
+          err[t] = std::current_exception();
+        }
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < nthr; t++) th.emplace_back(part, t);
+      part(0);
+      for (std::thread &t : th) t.join();
+      for (const std::exception_ptr &e : err)
+        if (e) std::rethrow_exception(e);
+    } else {
+      resolve(0, njobs);
+    }
     PROF_MARK("avail");
   }
 };
