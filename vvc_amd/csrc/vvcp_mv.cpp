@@ -88,6 +88,13 @@ int distScale(int curPoc, int curRefPoc, int colPoc, int colRefPoc) {   // xGetD
   const int x = (0x4000 + std::abs(td / 2)) / td;
   return clip3(-4096, 4095, (tb * x + 32) >> 6);
 }
+// an entry of the collocated view (MotionPicture::mf) with its MVs compressed as getColocatedMVP reads
+// them (roundMvComp, UnitTools.cpp:1472-1473): once per stored 8x8 unit instead of per read
+inline Mi colMi(Mi m) {
+  for (int l = 0; l < 2; l++)
+    for (int k = 0; k < 2; k++) m.mv[l][k] = roundMvComp(m.mv[l][k]);
+  return m;
+}
 inline Mv scaleMv(Mv m, int s) {   // Mv::scaleMv
   auto f = [&](int c) { const long long p = (long long)s * c; return clip3(-(1 << 17), (1 << 17) - 1, (int)((p + 128 - (p >= 0)) >> 8)); };
   return Mv(f(m.h), f(m.v));
@@ -138,7 +145,7 @@ struct Deriver {
   // unit is written by its own CU only; DMVR refinements follow in refine_motion)
   void col8(const vvcr_cu &c) {
     for (int y = (c.y + 7) & ~7; y < c.y + c.h; y += 8)
-      for (int x = (c.x + 7) & ~7; x < c.x + c.w; x += 8) (*col8f)[(size_t)(y >> 3) * w8 + (x >> 3)] = at(x, y);
+      for (int x = (c.x + 7) & ~7; x < c.x + c.w; x += 8) (*col8f)[(size_t)(y >> 3) * w8 + (x >> 3)] = colMi(at(x, y));
   }
   bool isBipredRestriction(const vvcr_cu &c) const { return (c.w == 4 && c.h == 4) || c.w + c.h == 12; }
   bool isDiffMER(int x1, int y1, int x2, int y2) const {   // PU::isDiffMER (:1506) on the PU top-left corners
@@ -179,7 +186,7 @@ struct Deriver {
     const SliceRefs &cs = col->slices[mi.slice];
     const bool curLT = sh->refLT[l][refIdx], colLT = cs.refLT[colList][colRef];
     if (curLT != colLT) return false;
-    Mv m(roundMvComp(mi.mv[colList][0]), roundMvComp(mi.mv[colList][1]));
+    const Mv m(mi.mv[colList][0], mi.mv[colList][1]);   // (stored compressed: colMi)
     if (curLT) { out = clipStore(m); return true; }
     const int s = distScaleCol(sh->poc - refPoc(l, refIdx), col->poc - cs.refPoc[colList][colRef]);
     out = s == 4096 ? clipStore(m) : scaleMv(m, s);
@@ -879,8 +886,9 @@ struct Deriver {
       for (int x = 0; x < c.w >> 2; x++) d[x] = mi;
     }
     // the collocated view of a CU of one motion: mi at its 8-aligned units
+    const Mi cmi = colMi(mi);
     for (int y = (c.y + 7) & ~7; y < c.y + c.h; y += 8)
-      for (int x = (c.x + 7) & ~7; x < c.x + c.w; x += 8) (*col8f)[(size_t)(y >> 3) * w8 + (x >> 3)] = mi;
+      for (int x = (c.x + 7) & ~7; x < c.x + c.w; x += 8) (*col8f)[(size_t)(y >> 3) * w8 + (x >> 3)] = cmi;
   }
   // the parse-time spanMotionInfo (CABACReader::prediction_unit :2072): merge PUs carry their parsed
   // (not yet derived) fields; only what later derivation does not overwrite survives (GEO / affine areas)
@@ -1373,7 +1381,7 @@ void refine_motion(const PictureUnit &p, MotionField &&field, const int32_t *del
         mi.mv[1][0] = clipStore(u.mv1x - ddx); mi.mv[1][1] = clipStore(u.mv1y - ddy);
         // the kept units inside the sub-block: 8-aligned positions (a CU may start at x or y = 4 mod 8)
         for (int yy = (y + 7) & ~7; yy < y + dy; yy += 8)
-          for (int xx = (x + 7) & ~7; xx < x + dx; xx += 8) out.mf[(size_t)(yy >> 3) * out.w8 + (xx >> 3)] = mi;
+          for (int xx = (x + 7) & ~7; xx < x + dx; xx += 8) out.mf[(size_t)(yy >> 3) * out.w8 + (xx >> 3)] = colMi(mi);
       }
   }
 }
