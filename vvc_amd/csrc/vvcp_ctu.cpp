@@ -1586,11 +1586,13 @@ struct Parser {
       tt.b[comp][6] = (int32_t)off;
       pic.box[3 * (size_t)ti + comp] = (uint16_t)(boxR | boxC << 8);
       if (boxR && boxC) {
-        pic.coef.resize(off + (size_t)boxR * boxC);
-        int32_t *dst = pic.coef.data() + off;
-        for (int y = 0; y < boxR; y++, dst += boxC) {
-          std::memcpy(dst, lvl + y * lvlStride, (size_t)boxC * sizeof(int32_t));
-          std::memset(lvl + y * lvlStride, 0, (size_t)boxC * sizeof(int32_t));
+        // appended row by row (no value-initialised resize that the copy overwrites)
+        const size_t need = off + (size_t)boxR * boxC;
+        if (need > pic.coef.capacity()) pic.coef.reserve(std::max(need, 2 * pic.coef.capacity()));
+        for (int y = 0; y < boxR; y++) {
+          int32_t *src = lvl + y * lvlStride;
+          pic.coef.insert(pic.coef.end(), src, src + boxC);
+          std::memset(src, 0, (size_t)boxC * sizeof(int32_t));
         }
       }
     }
@@ -2143,16 +2145,17 @@ struct Parser {
 
 }  // namespace
 
-void PictureSyntax::reset(int W_, int H_, int ctuLog2_) {
+void PictureSyntax::reset(int W_, int H_, int ctuLog2_, bool intra) {
   W = W_; H = H_; ctuLog2 = ctuLog2_; ctuSize = 1 << ctuLog2;
   wCtu = (W + ctuSize - 1) >> ctuLog2;
   hCtu = (H + ctuSize - 1) >> ctuLog2;
   w4 = (W + 3) >> 2;
   h4 = (H + 3) >> 2;
   cu.clear(); cux.clear(); pu.clear(); pux.clear(); tu.clear(); coef.clear(); box.clear();
-  // room for a quarter of the samples' levels (the packed boxes of a typical picture); more grows the pool
-  // (the blocks come from the large-buffer cache, page-locked once a reconstruction context exists)
-  coef.reserve((size_t)W * H / 4 + 65536);
+  // room for a quarter of the samples' levels (the packed boxes of a typical inter picture), three
+  // quarters for an intra picture (the 4K QP27 I picture: 4.5 M of 8.3 M); more grows the pool (the blocks come from the
+  // large-buffer cache, page-locked once a reconstruction context exists)
+  coef.reserve((size_t)W * H / 4 * (intra ? 3 : 1) + 65536);
   // rows: room for a densely coded intra picture (one CU per 64 luma samples), so that the vectors do not
   // grow by reallocation (copying every row) while the CABAC pass appends; larger counts still grow
   const size_t rows = (size_t)W * H / 64 + 1024;

@@ -56,7 +56,7 @@ struct PictureSyntax {
   std::vector<vvcr_sao> sao;        // [nCtb][3], merges resolved at finish()
   std::vector<uint8_t> alfEn[3], alfAlt[3], ccCtl[2];
   std::vector<int16_t> alfFset;
-  void reset(int W, int H, int ctuLog2);
+  void reset(int W, int H, int ctuLog2, bool intra = false);
   void dense_rows(std::vector<vvcr_tu> &tus, std::vector<int32_t> &pool) const;
   int cuAt(int ch, int x, int y) const;   // x, y in samples of channel ch; -1 outside / not decoded
 };

@@ -167,7 +167,9 @@ void Stream::parse_picture(int idx) {
     VVCP_CHECK(p.failed, "picture failed to parse");
     return;
   }
-  p.syn.reset(p.pps.width, p.pps.height, p.sps.ctuLog2);
+  bool intra = !p.slices.empty();
+  for (const auto &sh : p.slices) intra = intra && sh.isIntra();
+  p.syn.reset(p.pps.width, p.pps.height, p.sps.ctuLog2, intra);
   ParamSets ps;
   for (int i = 0; i < 8; i++) { ps.alfAps[i] = p.alfAps[i]; ps.alfValid[i] = p.alfValid[i]; }
   for (int i = 0; i < 4; i++) { ps.lmcsAps[i] = p.lmcsAps[i]; ps.lmcsValid[i] = p.lmcsValid[i]; }
