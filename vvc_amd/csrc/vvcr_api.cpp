@@ -32,6 +32,9 @@ thread_local std::string g_create_error;
 // fail on several threads at once, so the message is never a field shared between threads.
 thread_local std::string g_ctx_error;
 
+// device / page-locked allocations made while preparing pictures (VVCR_PREP_PROF reports them)
+std::atomic<uint64_t> g_prep_allocs{0}, g_prep_alloc_bytes{0};
+
 template <class T>
 struct DevVec {
   T *p = nullptr;
@@ -47,8 +50,12 @@ struct DevVec {
     if (view) { p = nullptr; view = false; }
     if (n <= cap) return;
     if (p) VVCR_CHECK_HIP(hipFree(p));
-    size_t c = std::max<size_t>(n, cap * 3 / 2 + 64);
+    // doubling: a prepared record is recycled for pictures of every size, and each regrowth is a hipFree
+    // (which waits for the device) and a hipMalloc on the preparing thread
+    size_t c = std::max<size_t>(n, cap * 2 + 64);
     VVCR_CHECK_HIP(hipMalloc(&p, c * sizeof(T)));
+    g_prep_allocs++;
+    g_prep_alloc_bytes += c * sizeof(T);
     cap = c;
   }
   // synchronous upload: the caller guarantees no kernel is reading this buffer (Prepared::wait)
@@ -92,9 +99,11 @@ struct Staging {
   template <class T, class A> void add_big(DevVec<T> &d, const std::vector<T, A> &v) { add_big(d, v.data(), v.size()); }
   void reserve(size_t n) {
     if (n <= cap) return;
-    const size_t c = std::max(n, cap * 3 / 2 + (1 << 20));
+    const size_t c = std::max(n, cap * 2 + (1 << 20));
     uint8_t *q = nullptr;
     VVCR_CHECK_HIP(hipHostMalloc((void **)&q, c, hipHostMallocDefault));
+    g_prep_allocs++;
+    g_prep_alloc_bytes += c;
     if (used) std::memcpy(q, h, used);
     if (h) VVCR_CHECK_HIP(hipHostFree(h));
     h = q;
@@ -123,9 +132,9 @@ struct Staging {
   size_t last_off() const { return items.back().off; }
   template <class T> T *host_at(size_t off) { return (T *)(h + off); }
   // the device arena is sized and every staged DevVec points into it; nothing is copied yet
-  void place() {
+  void place(size_t floor) {
     base = (used + 255) & ~(size_t)255;
-    arena.ensure(base + ext_used + 256);
+    arena.ensure(std::max(base + ext_used + 256, floor));
     for (const Item &it : items) *it.dst = arena.p + it.off;
     for (const Ext &e : ext) *e.dst = arena.p + base + e.off;
   }
@@ -599,20 +608,30 @@ constexpr int N = 9;
 const char *const names[N] = {"wait", "resid", "inter-lists", "mc_done", "dmvr-bufs", "inter-bytes", "intra+dbk+lf", "place", "copy"};
 std::atomic<uint64_t> ns[N], calls;
 const bool on = getenv("VVCR_PREP_PROF") != nullptr;
+// wall time, or with VVCP_CPU_TIMES the calling thread's CPU time (as vvcp_decode's phase times)
+const bool cpu = getenv("VVCP_CPU_TIMES") != nullptr;
 struct Report {
   ~Report() {
     if (!on || !calls) return;
-    fprintf(stderr, "prepare: %llu calls, ms per call:", (unsigned long long)calls.load());
+    fprintf(stderr, "prepare: %llu calls, %s ms per call:", (unsigned long long)calls.load(), cpu ? "thread CPU" : "wall");
     for (int k = 0; k < N; k++) fprintf(stderr, " %s %.3f", names[k], ns[k].load() * 1e-6 / calls.load());
-    fprintf(stderr, "\n");
+    fprintf(stderr, "; %llu device / pinned allocations, %.1f MB\n", (unsigned long long)g_prep_allocs.load(), g_prep_alloc_bytes.load() * 1e-6);
   }
 } report;
+inline uint64_t now_ns() {
+  if (cpu) {
+    timespec ts;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+  }
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 struct Timer {
-  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  uint64_t t = on ? now_ns() : 0;
   void mark(int k) {
     if (!on) return;
-    const auto n = std::chrono::steady_clock::now();
-    ns[k] += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(n - t).count();
+    const uint64_t n = now_ns();
+    ns[k] += n - t;
     t = n;
   }
 };
@@ -680,11 +699,14 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     // the previous launch's delta read-back (copy stream, after its inter stage) may still be queued
     VVCR_CHECK_HIP(hipEventSynchronize(r.mc_done));
     pt.mark(3);
-    r.dmvr.ensure(2 * (size_t)r.n_dmvr + 2);
-    if (r.h_dmvr_cap < 2 * (size_t)r.n_dmvr + 2) {
+    // DMVR deltas: sized once for the most a picture can have (a sub-block per 128 luma samples: DMVR
+    // needs w, h >= 8 and w * h >= 128), so that a recycled record never reallocates them
+    const size_t ndm = std::max(2 * (size_t)r.n_dmvr + 2, 2 * ((size_t)sp.width * sp.height / 128) + 2);
+    r.dmvr.ensure(ndm);
+    if (r.h_dmvr_cap < ndm) {
       if (r.h_dmvr) VVCR_CHECK_HIP(hipHostFree(r.h_dmvr));
       r.h_dmvr = nullptr;
-      r.h_dmvr_cap = 2 * (size_t)r.n_dmvr + 2;
+      r.h_dmvr_cap = ndm;
       VVCR_CHECK_HIP(hipHostMalloc((void **)&r.h_dmvr, r.h_dmvr_cap * sizeof(int32_t), hipHostMallocDefault));
     }
     pt.mark(4);
@@ -712,7 +734,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     st.add_big(r.ijobs, ip.jobs);
     st.add_big(r.idep_start, ip.dep_start);
     st.add_big(r.ideps, ip.deps);
-    r.istate.ensure(16 + ip.jobs.size());
+    r.istate.ensure(std::max<size_t>(16 + ip.jobs.size(), (size_t)sp.width * sp.height / 64));   // (an intra picture's steps)
     // one device copy per lane (scratch plane pointers differ), written after place(): they hold the
     // arena address of the LMCS table (staged above), which is only known then
     {
@@ -780,7 +802,9 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     r.alg_bytes[K_ALF] = pix * 2 * 2;
   }
   pt.mark(6);
-  st.place();
+  // the device arena: at least 4 bytes per luma sample (a 4K intra picture stages ~30 MB), so that a record
+  // recycled from inter to intra pictures does not regrow it
+  st.place((size_t)sp.width * sp.height * 4);
   if (iparams_off != SIZE_MAX)
     for (int l = 0; l < MAXLANE; l++) st.host_at<IntraParams>(iparams_off)[l] = make_intra_params(ctx, r, l);
   pt.mark(7);
