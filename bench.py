@@ -86,12 +86,27 @@ import json
 import os
 import subprocess
 import sys
+import resource
 import time
 
 import numpy as np
 import torch  # noqa: F401  (before any libvvcr context: torch's HIP runtime must load first)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _thread_cpu():
+    """{tid: (name, user + system CPU seconds)} of this process's threads (/proc, diagnostics)"""
+    out, tick = {}, os.sysconf("SC_CLK_TCK")
+    for t in os.listdir("/proc/self/task"):
+        try:
+            st = open("/proc/self/task/%s/stat" % t).read()
+        except OSError:
+            continue
+        name = st[st.index("(") + 1:st.rindex(")")]
+        f = st[st.rindex(")") + 2:].split()
+        out[int(t)] = (name, (int(f[11]) + int(f[12])) / tick)
+    return out
 sys.path.insert(0, ROOT)
 
 from vvc_amd import native as N  # noqa: E402
@@ -518,12 +533,26 @@ def main():
     e2e.times = {}
     R.barrier()
     ctx.sync()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    th0 = _thread_cpu() if os.environ.get("VVCR_BENCH_THREADS") else None
     t0 = time.perf_counter()
     e2e.run(a.steps)
     ctx.sync()
     t1 = time.perf_counter()
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    if th0 is not None:   # diagnostics: CPU of every thread of the process over the timed steps
+        th1 = _thread_cpu()
+        d = sorted(((th1[k][1] - th0.get(k, (None, 0))[1], k, th1[k][0]) for k in th1), reverse=True)
+        print("threads: %d, CPU s over the timed steps: total %.2f; top: %s" % (
+            len(d), sum(x[0] for x in d), ", ".join("%s/%d %.2f" % (n, k, v) for v, k, n in d[:24])), file=sys.stderr)
     R.barrier()
     elapsed = R.max_over_ranks(t1 - t0)
+    npic_timed = a.steps * a.segments * len(infos)
+    # the process's CPU over the timed steps (all threads, this rank): user / system ms and page faults per picture
+    host_rusage = {"user_ms_per_picture": round((ru1.ru_utime - ru0.ru_utime) / npic_timed * 1e3, 3),
+                   "sys_ms_per_picture": round((ru1.ru_stime - ru0.ru_stime) / npic_timed * 1e3, 3),
+                   "minor_faults_per_picture": round((ru1.ru_minflt - ru0.ru_minflt) / npic_timed, 1),
+                   "cores_busy": round(((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / (t1 - t0), 2)}
     for owner in e2e.final:
         if owner is not None:
             bitexact = bitexact and check_slots(ctx, owner, meta)
@@ -664,6 +693,7 @@ def main():
                        "with the GPU's DMVR feedback, host planning, upload, GPU reconstruction and loop filters, every "
                        "picture of every step; a step = %d independent decodes of the stream, all in flight" % a.segments,
         "host_ms_per_picture": {k: round(v / (a.steps * a.segments * len(infos)) * 1e3, 3) for k, v in e2e.times.items()},
+        "host_rusage": host_rusage,
         "roofline": roof,
         "cpu_baseline": None,
         "single_stream": single,

@@ -17,6 +17,7 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <pthread.h>
 #include <thread>
 
 #include "vvcp.h"
@@ -154,6 +155,7 @@ static int64_t dmvr_subblocks(const vvcp::PictureUnit &p) {
 // decoding order (the DPB slot dependencies of libvvcr assume it): whichever worker finishes the upload
 // of the next picture in order launches every picture prepared by then, then the output callbacks.
 extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_params *prm) {
+  pthread_setname_np(pthread_self(), "vvcp-decode");   // the calling thread runs derivation (diagnostics name)
   if (!h || !ctx || !prm || prm->num_slots <= 0 || prm->slot_base < 0) return VVCR_E_ARG;
   vvcp::Stream &s = h->s;
   const int n = (int)s.pics.size();
@@ -256,6 +258,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
     T[VVCP_PHASE_PREPARE] += tu;
   };
   auto worker = [&]() {
+    pthread_setname_np(pthread_self(), "vvcp-worker");   // (per-thread CPU accounting: /proc/<pid>/task)
     for (;;) {
       int task = -1;
       bool isPlan = false;

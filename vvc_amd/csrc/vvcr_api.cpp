@@ -16,6 +16,7 @@
 #include <mutex>
 #include <thread>
 #include <atomic>
+#include <pthread.h>
 #include <chrono>
 #include <string>
 #include <vector>
@@ -541,6 +542,7 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
   };
   if ((mask & VVCR_STAGE_DBK) && !b.dbk_gpu)
     dbk_thread = std::thread([&] {
+      pthread_setname_np(pthread_self(), "vvcr-plan-dbk");
       try {
         plan_deblocking(sp, pp, b.desc, b.dbk);
       } catch (...) {
