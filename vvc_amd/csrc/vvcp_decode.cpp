@@ -174,7 +174,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
   auto since = [&](double a) { return tnow() - a; };
   std::vector<std::thread> pool;
   std::mutex mu;                  // task queue, picture states, phase times
-  std::condition_variable cv;
+  std::condition_variable cvw, cvm;   // the workers' task queue; the decode thread's waits (no herd of wake-ups)
   std::mutex lmu;                 // launches and output callbacks (one thread at a time, in order)
   std::vector<int> pstate(n, 0);  // parse: 0 pending, 1 running, 2 done, 3 failed
   std::vector<std::string> perr(n);
@@ -196,7 +196,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
   auto fail = [&](const std::string &m, int code) {   // under mu
     if (failure.empty()) { failure = m; failCode = code; }
     stop = true;
-    cv.notify_all();
+    cvw.notify_all(); cvm.notify_all();
   };
   // launch every picture prepared in order (caller holds lmu, not mu)
   auto launch_ready = [&]() {
@@ -231,7 +231,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
         live.live.push_back(i);
         if (!prm->handles_out)   // pictures whose deltas no later derivation can read
           live.trim(P, refined, nderived, KEEP_HANDLES, [&](int k) { drop.push_back(k); });
-        cv.notify_all();
+        cvm.notify_all();
       }
       for (int k : drop) vvcr_release_picture(ctx, handle[k]);
     }
@@ -264,7 +264,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
       bool isPlan = false;
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || !planQ.empty() || nextParse < n; });
+        cvw.wait(g, [&] { return stop || !planQ.empty() || nextParse < n; });
         if (stop) return;
         if (!planQ.empty()) { task = planQ.front(); planQ.pop_front(); isPlan = true; }
         else { task = nextParse++; pstate[task] = 1; }
@@ -296,7 +296,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
         pstate[task] = e.empty() ? 2 : 3;
         perr[task] = e;
         T[VVCP_PHASE_PARSE] += dt;
-        cv.notify_all();
+        cvm.notify_all();
       }
     }
   };
@@ -312,7 +312,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
       double t0 = tnow();
       {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return stop || pstate[i] >= 2; });
+        cvm.wait(g, [&] { return stop || pstate[i] >= 2; });
         if (stop) break;
         if (pstate[i] == 3) throw vvcp::ParseError("picture " + std::to_string(i) + ": " + perr[i]);
         T[VVCP_PHASE_PARSE_WAIT] += since(t0);
@@ -323,7 +323,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
         if (refined[j]) continue;
         {
           std::unique_lock<std::mutex> g(mu);
-          cv.wait(g, [&] { return stop || launched[j]; });
+          cvm.wait(g, [&] { return stop || launched[j]; });
           if (stop) break;
         }
         deltas.resize(2 * (size_t)ndmvr[j] + 2);
@@ -354,12 +354,12 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
       if (now) refined[i] = 1;
       nderived = i + 1;
       planQ.push_back(i);
-      cv.notify_all();
+      cvw.notify_one();
     }
     // every picture launched (or a worker failed)
     {
       std::unique_lock<std::mutex> g(mu);
-      cv.wait(g, [&] { return stop || nextLaunch >= n; });
+      cvm.wait(g, [&] { return stop || nextLaunch >= n; });
     }
     if (prm->handles_out)
       for (int i = 0; i < n; i++) prm->handles_out[i] = handle[i];
@@ -373,7 +373,7 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
   {
     std::lock_guard<std::mutex> g(mu);
     stop = true;
-    cv.notify_all();
+    cvw.notify_all(); cvm.notify_all();
   }
   for (auto &t : pool) t.join();
   if (!failure.empty()) {

@@ -165,6 +165,14 @@ const char *const kKernelNames[NK] = {"resid", "mc", "mc_bidir", "mc_affine", "r
 // stage of each kernel group (bit index in VVCR_STAGE_*)
 const int kKernelStage[NK] = {0, 1, 1, 1, 2, 2, 4, 5, 6, 4};
 
+// Flags of the events host threads wait on (picture done, DMVR deltas read back, upload done): HIP's default
+// active wait, or with VVCR_BLOCKING_WAIT hipEventBlockingSync (the waiting thread sleeps until the device
+// signals; measured against the default in DESIGN §5)
+static unsigned wait_flags() {
+  static const unsigned f = getenv("VVCR_BLOCKING_WAIT") ? (unsigned)hipEventBlockingSync : 0u;
+  return f;
+}
+
 struct Prepared {
   vvcr_pic_params pp{};
   uint32_t mask = 0;
@@ -223,11 +231,11 @@ struct Prepared {
 
   Prepared() {
     for (auto &e : ev) { VVCR_CHECK_HIP(hipEventCreate(&e[0])); VVCR_CHECK_HIP(hipEventCreate(&e[1])); }
-    VVCR_CHECK_HIP(hipEventCreate(&done));
+    VVCR_CHECK_HIP(hipEventCreateWithFlags(&done, wait_flags()));
     VVCR_CHECK_HIP(hipEventCreate(&start));
-    VVCR_CHECK_HIP(hipEventCreateWithFlags(&mc_done, hipEventDisableTiming));
+    VVCR_CHECK_HIP(hipEventCreateWithFlags(&mc_done, hipEventDisableTiming | wait_flags()));
     VVCR_CHECK_HIP(hipEventCreateWithFlags(&ev_mc, hipEventDisableTiming));
-    VVCR_CHECK_HIP(hipEventCreateWithFlags(&up_done, hipEventDisableTiming));
+    VVCR_CHECK_HIP(hipEventCreateWithFlags(&up_done, hipEventDisableTiming | wait_flags()));
   }
   ~Prepared() {
     for (auto &e : ev) { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); }
