@@ -174,7 +174,15 @@ struct McClassTable {
 // luma cells: 4 columns x 16 rows for blocks of >= 16 rows when MC_TALL_LUMA (a quarter less H work), else 4 x 8
 // (not in edge classes: their clamped path keeps 8-row cells)
 __host__ __device__ inline bool mc_tall_luma(int h, bool edge) { return MC_TALL_LUMA && h >= 16 && !edge; }
-__host__ __device__ inline int mc_luma_cells(int w, int h, bool edge) { return (w >> 2) * (mc_tall_luma(h, edge) ? h >> 4 : (h + 7) >> 3); }
+// MC_SHORT_LUMA: 4 x 4 luma cells outside the edge classes (twice the waves, each with a shorter chain; the
+// H pass filters 11 rows per 4 outputs instead of 15 per 8)
+#ifndef MC_SHORT_LUMA
+#define MC_SHORT_LUMA 0
+#endif
+__host__ __device__ inline bool mc_short_luma(bool edge) { return MC_SHORT_LUMA && !edge; }
+__host__ __device__ inline int mc_luma_cells(int w, int h, bool edge) {
+  return (w >> 2) * (mc_short_luma(edge) ? (h + 3) >> 2 : mc_tall_luma(h, edge) ? h >> 4 : (h + 7) >> 3);
+}
 // chroma cells: 4 columns x 8 rows for blocks of >= 16 luma rows (a third less H work than two 4-row
 // cells), else 4 x 4
 #ifndef MC_TALL_CHROMA

@@ -594,7 +594,9 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
   if (luma) {
     const int ncx = w >> 2, cx = s & (ncx - 1), cy = s >> (__ffs(ncx) - 1);
     if (ed) mc_cell<8, 8, true>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy), half, sp0);
-#if MC_TALL_LUMA
+#if MC_SHORT_LUMA
+    else if (mc_short_luma(false)) mc_cell<8, 4, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 4 * cy, 4, min(4, h - 4 * cy), half, sp0);
+#elif MC_TALL_LUMA
     else if (mc_tall_luma(h, false)) mc_cell<8, 16, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 16 * cy, 4, 16, half, sp0);
 #endif
     else mc_cell<8, 8, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy), half, sp0);
