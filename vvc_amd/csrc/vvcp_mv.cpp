@@ -881,9 +881,11 @@ struct Deriver {
       col8(c);
       return;
     }
-    for (int y = c.y; y < c.y + c.h; y += 4) {
-      Mi *d = &at(c.x, y);
-      for (int x = 0; x < c.w >> 2; x++) d[x] = mi;
+    {   // the first unit row, then whole-row copies (wide stores instead of two per 24-byte record)
+      const int n = c.w >> 2;
+      Mi *d0 = &at(c.x, c.y);
+      for (int x = 0; x < n; x++) d0[x] = mi;
+      for (int y = c.y + 4; y < c.y + c.h; y += 4) std::memcpy((void *)&at(c.x, y), d0, (size_t)n * sizeof(Mi));
     }
     // the collocated view of a CU of one motion: mi at its 8-aligned units
     const Mi cmi = colMi(mi);
