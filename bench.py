@@ -220,29 +220,34 @@ class _Roctx:
         cls._marker()
 
 
-def kernel_table(ctx, handles, reps, sync="picture"):
+def kernel_table(ctx, groups, reps, sync="picture"):
     """Per-kernel HIP-event durations (events on the library's lanes, vvcr_kernel_stats) of one decode's
-    resident pictures: `reps` steps, each launching every picture with a host sync after it (no kernel
-    overlaps another picture's), summed per kernel and step; the table keeps the MEDIAN step's time per
-    kernel and its min / max across the steps. These are the launches a `VVCR_ROCTX_REGIONS=1 rocprofv3
-    --selected-regions` trace of the same command records. Returns {name: [launches, ms, alg_bytes, ms_min,
-    ms_max]} (per step)."""
+    resident pictures, launched as the decode loop launches them (`groups`: single pictures and
+    frame-batched pairs, bitstream.launch_groups): `reps` steps, each launching every group with a host sync
+    after it (no kernel overlaps another group's), summed per kernel and step; the table keeps the MEDIAN
+    step's time per kernel and its min / max across the steps. These are the launches a
+    `VVCR_ROCTX_REGIONS=1 rocprofv3 --selected-regions` trace of the same command records. Returns {name:
+    [launches, ms, alg_bytes, ms_min, ms_max, pictures]} (per step; pictures: the pictures the kernel's
+    launches carried, > launches for the frame-batched k_mc)."""
+    from vvc_amd import bitstream as B
     ctx.set_timing(True)
     steps = []
     _Roctx.resume()
     for _ in range(max(1, reps)):
-        for hnd in handles:
-            ctx.launch(hnd)
+        for g in groups:
+            B.launch_group(ctx, g)
             if sync == "picture":
                 ctx.sync()
         ctx.sync()
         rep = {}
-        for hnd in handles:
-            for name, launches, ms, alg in ctx.kernel_stats(hnd):
-                k = rep.setdefault(name, [0, 0.0, 0.0])
-                k[0] += launches
-                k[1] += ms
-                k[2] += alg
+        for g in groups:
+            for hnd in g:
+                for name, launches, ms, alg, pics in ctx.kernel_stats(hnd):
+                    k = rep.setdefault(name, [0, 0.0, 0.0, 0])
+                    k[0] += launches
+                    k[1] += ms
+                    k[2] += alg
+                    k[3] += pics if launches else 0
         steps.append(rep)
     _Roctx.pause()
     ctx.set_timing(False)
@@ -252,29 +257,31 @@ def kernel_table(ctx, handles, reps, sync="picture"):
         if not v:
             continue
         ms = sorted(x[1] for x in v)
-        out[name] = [v[0][0], float(np.median(ms)), v[0][2], ms[0], ms[-1]]
+        out[name] = [v[0][0], float(np.median(ms)), v[0][2], ms[0], ms[-1], v[0][3]]
     return out
 
 
 def resident_handles(ctx, data, per, base=0):
-    """One decode of the stream on slots [base, base + per), its prepared pictures kept (decoding order)."""
+    """One decode of the stream on slots [base, base + per), its prepared pictures kept: their launch groups
+    (decoding order, frame-batched pairs as vvcp_decode launches them), handles and (poc, slot)s."""
     from vvc_amd import bitstream as B
     seq = B.SequenceDecode(ctx, data, nslots=per, base=base, threads=8)
     _, handles = seq.run(keep_handles=True)
     ctx.sync()
-    return handles, [(inf["poc"], seq.slot[i]) for i, inf in enumerate(seq.info)]
+    return B.launch_groups(handles, seq.batch), handles, [(inf["poc"], seq.slot[i]) for i, inf in enumerate(seq.info)]
 
 
 def mc_roofline(kern, note):
     out = {"peak": PEAK_HBM_GBS, "unit": "GB/s", "note": note}
     tot = [0.0, 0.0]
     for k in ("mc", "mc_affine", "mc_bidir"):
-        v = kern.get(k, [0, 0.0, 0.0, 0.0, 0.0])
+        v = kern.get(k, [0, 0.0, 0.0, 0.0, 0.0, 0])
         g = v[2] / (v[1] / 1e3) / 1e9 if v[1] > 0 else 0.0
         out[k] = {"achieved": round(g, 2), "frac": round(g / PEAK_HBM_GBS, 4),
                   "us_per_launch": round(v[1] / max(v[0], 1) * 1e3, 2),
                   "us_per_launch_min_max": [round(v[3] / max(v[0], 1) * 1e3, 2), round(v[4] / max(v[0], 1) * 1e3, 2)],
-                  "alg_MB_per_launch": round(v[2] / max(v[0], 1) / 1e6, 3), "launches_per_step": v[0]}
+                  "alg_MB_per_launch": round(v[2] / max(v[0], 1) / 1e6, 3), "launches_per_step": v[0],
+                  "pictures_per_step": v[5], "us_per_picture": round(v[1] / max(v[5], 1) * 1e3, 2)}
         tot[0] += v[2]
         tot[1] += v[1]
     g = tot[0] / (tot[1] / 1e3) / 1e9 if tot[1] > 0 else 0.0
@@ -289,9 +296,9 @@ def north_star_mc(ctx, stream, per, reps, sync="picture"):
         return None
     with open(p, "rb") as f:
         data = f.read()
-    handles, slots = resident_handles(ctx, data, per)
+    groups, handles, slots = resident_handles(ctx, data, per)
     meta = S.load_meta(os.path.join(ROOT, "tests", "golden", stream))
-    kern = kernel_table(ctx, handles, reps, sync)
+    kern = kernel_table(ctx, groups, reps, sync)
     ok = check_slots(ctx, {slot: poc for poc, slot in slots}, meta)
     for h in handles:
         ctx.release(h)
@@ -506,8 +513,8 @@ def main():
 
     if a.kernel_table_only:
         ctx.set_timing(False)
-        handles, slots = resident_handles(ctx, data, per)
-        kern = kernel_table(ctx, handles, a.kernel_table_reps, a.kernel_table_sync)
+        groups, handles, slots = resident_handles(ctx, data, per)
+        kern = kernel_table(ctx, groups, a.kernel_table_reps, a.kernel_table_sync)
         ok = check_slots(ctx, {slot: poc for poc, slot in slots}, meta)
         for h in handles:
             ctx.release(h)
@@ -515,7 +522,8 @@ def main():
                "mc_roofline": mc_roofline(kern, "median of %d synced steps" % a.kernel_table_reps),
                "kernels": {k: {"us_per_launch": round(v[1] / max(v[0], 1) * 1e3, 2), "launches_per_step": v[0],
                                "ms_per_step": round(v[1], 4), "ms_min_max": [round(v[3], 4), round(v[4], 4)],
-                               "alg_MB_per_launch": round(v[2] / max(v[0], 1) / 1e6, 3)} for k, v in kern.items()}}
+                               "alg_MB_per_launch": round(v[2] / max(v[0], 1) / 1e6, 3), "pictures_per_step": v[5]}
+                           for k, v in kern.items()}}
         if a.north_star_stream and a.north_star_stream != a.stream:
             out["north_star_mc"] = north_star_mc(ctx, a.north_star_stream, per, a.kernel_table_reps, a.kernel_table_sync)
         ctx.close()
@@ -592,15 +600,15 @@ def main():
         for c in range(a.segments):
             seq = B.SequenceDecode(ctx, data, nslots=per, base=per * c, threads=8)
             _, handles = seq.run(keep_handles=True)
-            copies.append((handles, [(inf["poc"], seq.slot[i]) for i, inf in enumerate(seq.info)]))
+            copies.append((B.launch_groups(handles, seq.batch), [(inf["poc"], seq.slot[i]) for i, inf in enumerate(seq.info)]))
         ctx.sync()
         t_prep = (time.perf_counter() - t_prep) / a.segments
         res_ok = True
         nstep = [0]
 
         def run_step():
-            for hnd in copies[nstep[0] % a.segments][0]:
-                ctx.launch(hnd)
+            for g in copies[nstep[0] % a.segments][0]:
+                B.launch_group(ctx, g)
                 if a.sync_pictures:
                     ctx.sync()
             nstep[0] += 1
@@ -616,9 +624,9 @@ def main():
         R.barrier()
         r_el = R.max_over_ranks(r1 - r0)
         # every copy launched back to back (as timed), then each copy's slots checked
-        for handles, _ in copies:
-            for hnd in handles:
-                ctx.launch(hnd)
+        for groups, _ in copies:
+            for g in groups:
+                B.launch_group(ctx, g)
         ctx.sync()
         for _, slots in copies:
             res_ok = res_ok and check_slots(ctx, {slot: poc for poc, slot in slots}, meta)
@@ -631,9 +639,10 @@ def main():
         # per-kernel HIP events: the kernel table and roofline (kernel_table: one segment, a host sync after
         # every picture, the median step of --kernel-table-reps)
         kern.update(kernel_table(ctx, copies[nstep[0] % a.segments][0], a.kernel_table_reps, a.kernel_table_sync))
-        for handles, _ in copies:
-            for hnd in handles:
-                ctx.release(hnd)
+        for groups, _ in copies:
+            for g in groups:
+                for hnd in g:
+                    ctx.release(hnd)
         bitexact = bitexact and res_ok
         resident = {"value": round(V.job_throughput(px_seq * a.resident_steps, r_el, R) / 1e6, 2), "unit": "Mpixels/s",
                     "steps": a.resident_steps, "ms_per_step": round(r_el / a.resident_steps * 1e3, 3),

@@ -211,6 +211,14 @@ int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle);
  * stages and, after a halo exchange, the loop-filter stages of one prepared spatial shard (each launch
  * orders itself after the slot's earlier writer like any other). */
 int vvcr_launch_picture_stages(vvcr_ctx *ctx, int32_t handle, uint32_t stage_mask);
+/* Frame-batched launch of n (1..2) prepared inter pictures that do not reference each other and write
+ * different slots (e.g. the adjacent top-temporal-layer pictures POC 1 / 3 of a GOP-16 hierarchy, which
+ * DecApp decodes one after the other): one execution lane runs their residuals, ONE plain-MC launch for
+ * all of them (a single 4K picture's k_mc is one partial round of waves), then each picture's remaining
+ * stages. Equivalent to launching them one by one (VVCR_E_ARG when a picture references another of the
+ * batch, shares its slot, or was prepared without every stage). vvcr_kernel_stat.pictures of the plain-MC
+ * group tells which record holds the batched launch's time (pictures = n) and which were carried (0). */
+int vvcr_launch_pictures(vvcr_ctx *ctx, const int32_t *handles, int32_t n);
 int vvcr_release_picture(vvcr_ctx *ctx, int32_t handle);
 
 /* Host-only picture builder: the same begin / submit / loop-filter / plan sequence on a standalone
@@ -257,6 +265,8 @@ typedef struct vvcr_kernel_stat {
   int32_t launches;
   float ms;
   double alg_bytes;
+  int32_t pictures;   /* pictures the group's launches carried (a frame-batched k_mc: n on the first, 0 on the others) */
+  int32_t pad;
 } vvcr_kernel_stat;
 int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int32_t n);
 /* Per-kernel-group event timing of later launches on (default) or off; with it off, vvcr_kernel_stats

@@ -186,3 +186,58 @@ def test_stage_by_stage_launches_stay_on_one_lane(golden_dir, monkeypatch):
                 ctx.release(h)
     finally:
         dec.close()
+
+
+def test_stage_by_stage_with_every_lane_held_fails_cleanly(golden_dir, monkeypatch):
+    """Three segment copies interleaved stage by stage over two B lanes (VVCR_LANES=5, VVCR_INTRA_LANES=3):
+    the third copy's B picture finds both B lanes holding a picture whose later stages are pending. The
+    launch must fail with VVCR_E_STATE (never overwrite a held lane's planes); after the held pictures'
+    stages complete, the refused picture launches whole and every picture of the copies stays bit-exact."""
+    from vvc_amd import native as N
+    monkeypatch.setenv("VVCR_LANES", "5")
+    monkeypatch.setenv("VVCR_INTRA_LANES", "3")
+    d = os.path.join(golden_dir, "ra416_q32")
+    pics = S.load_sequence(d)
+    meta = S.load_meta(d)
+    per = min(len(pics), 16)
+    dec = D.Decoder(pics, dpb_slots=3 * per)
+    ctx = dec.ctx
+    groups = (N.STAGE_RESID, N.STAGE_INTER, N.STAGE_INTRA | N.STAGE_LMCS_INV, N.STAGE_DBK | N.STAGE_SAO | N.STAGE_ALF)
+    try:
+        copies = []
+        for c in range(3):
+            alloc = S.SlotAllocator(pics, per, base=per * c)
+            hs = []
+            for i, p in enumerate(pics):
+                slot = alloc.assign(i, p["hdr"]["poc"])
+                ctx.begin_picture(S.pic_params(p, slot, alloc.slot_of))
+                S.submit(ctx, p)
+                S.set_loop_filter_params(ctx, p)
+                hs.append((ctx.prepare(N.STAGE_ALL), p["hdr"]["poc"], slot))
+            copies.append(hs)
+        refused = 0
+        for i in range(len(pics)):
+            pending = []   # copies whose picture i was refused: launched whole once the others' stages are done
+            for g in groups:
+                for c, hs in enumerate(copies):
+                    if c in pending:
+                        continue
+                    try:
+                        ctx.launch_stages(hs[i][0], g)
+                    except N.VvcrError as e:
+                        assert "pending" in str(e), str(e)
+                        assert g == N.STAGE_RESID, "only a picture's first stage call can be refused"
+                        pending.append(c)
+            for c in pending:
+                refused += 1
+                ctx.launch(copies[c][i][0])
+        assert refused > 0, "the interleave never found every B lane held"
+        ctx.sync()
+        for hs in copies:
+            owner = {slot: poc for _, poc, slot in hs}
+            for slot, poc in owner.items():
+                assert D.plane_md5s(dec.read(slot)) == meta["poc_plane_md5"][str(poc)], "POC %d differs" % poc
+            for h, _, _ in hs:
+                ctx.release(h)
+    finally:
+        dec.close()

@@ -32,7 +32,7 @@ def main():
     for r in range(a.reps + 2):
         ctx.launch(h)
         ctx.sync()
-        for name, n, t, alg in ctx.kernel_stats(h):
+        for name, n, t, alg, _ in ctx.kernel_stats(h):
             if name == "intra" and r >= 2:
                 ms.append(t)
     ms.sort()

@@ -52,7 +52,7 @@ def main():
         ctx.launch(h)
         ctx.sync()
         row = {}
-        for name, n, ms, alg in ctx.kernel_stats(h):
+        for name, n, ms, alg, _ in ctx.kernel_stats(h):
             if n:
                 g = agg.setdefault(name, [0, 0.0, 0.0])
                 g[0] += n; g[1] += ms; g[2] += alg

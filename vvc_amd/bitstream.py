@@ -30,6 +30,7 @@ def _bind(L):
         L.vvcp_decode.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.vvcp_decode_plan.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]
         L.vvcp_decode_live_bound.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]
+        L.vvcp_decode_batches.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]
         _bound = True
     return L
 
@@ -130,6 +131,10 @@ class SequenceDecode:
             raise P.ParseError("decode plan: %s" % self.L.vvcp_last_error().decode())
         self.slot = list(slots)[:n]
         self.out_order = list(order)[:m]
+        first = (C.c_int32 * max(n, 1))()
+        if self.L.vvcp_decode_batches(self.s.h, base, nslots, first) < 0:
+            raise P.ParseError("decode batches: %s" % self.L.vvcp_last_error().decode())
+        self.batch = list(first)[:n]   # frame batching of vvcp_decode: 2 first of a pair, 0 its partner, 1 alone
         self.info = [self.s.info(i) for i in range(n)]
         # seconds per phase (include/vvcp.h VVCP_PHASE_*): parse summed over the parser threads
         self.times = dict.fromkeys(PHASES, 0.0)
@@ -160,6 +165,24 @@ class SequenceDecode:
             raise err[0]
         order = [(self.info[k]["poc"], self.slot[k]) for k in self.out_order]
         return (order, list(handles)[:n]) if keep_handles else order
+
+
+def launch_groups(handles, batch):
+    """The prepared handles of one decode (decoding order) grouped as vvcp_decode launches them: pairs of
+    frame-batched pictures (SequenceDecode.batch) and single pictures."""
+    out, i = [], 0
+    while i < len(handles):
+        k = 2 if batch[i] == 2 and i + 1 < len(handles) else 1
+        out.append(handles[i:i + k])
+        i += k
+    return out
+
+
+def launch_group(ctx, group):
+    if len(group) > 1:
+        ctx.launch_batch(group)
+    else:
+        ctx.launch(group[0])
 
 
 def decode_bitstream(data, ctx=None, threads=8, dpb_slots=16, device=0, on_output=None):

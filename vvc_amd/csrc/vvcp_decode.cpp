@@ -31,6 +31,7 @@ struct DecodePlan {
   std::vector<std::vector<int>> refIdx[2];   // decode index of every reference
   std::vector<int> cvs, slot, lastUse, lastRef, outOrder, outReady;   // lastRef: last picture referencing it (-1: none)
   std::vector<char> referenced, output;
+  std::vector<int> batch;   // frame batching: 2 = the first of a pair launched together, 0 = its partner, 1 = alone
 
   int find(int j, int p) const {
     for (int i = j - 1; i >= 0; i--)
@@ -75,6 +76,25 @@ struct DecodePlan {
           lastRef[src] = std::max(lastRef[src], j);
           referenced[src] = 1;
         }
+    // Frame-batched plain MC (vvcr_launch_pictures): adjacent pictures of decoding order that are both inter
+    // pictures of one coded video sequence and do not reference each other (the top temporal layer's
+    // POC 1 / 3, 5 / 7, 9 / 11, 13 / 15 of a GOP-16 hierarchy) launch together. The second never needs the
+    // first's DMVR deltas (it does not reference it, so it is not its collocated picture), so its derivation
+    // does not wait for the first's launch. VVCP_MC_BATCH=0: every picture alone.
+    batch.assign(n, 1);
+    static const bool batching = [] { const char *e = getenv("VVCP_MC_BATCH"); return !(e && e[0] == '0'); }();
+    for (int i = 0; batching && i + 1 < n; i++) {
+      const int j = i + 1;
+      const bool inter = !refIdx[0][i].empty() && !refIdx[0][j].empty();
+      bool indep = cvs[i] == cvs[j];
+      for (int l = 0; l < 2; l++)
+        for (int src : refIdx[l][j]) indep = indep && src != i;
+      if (inter && indep) {
+        batch[i] = 2;
+        batch[j] = 0;
+        i++;
+      }
+    }
     std::vector<int> freeSlots, held;
     for (int k = 0; k < nslots; k++) freeSlots.push_back(base + k);
     slot.resize(n);
@@ -199,24 +219,31 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
     cvw.notify_all(); cvm.notify_all();
   };
   // launch every picture prepared in order (caller holds lmu, not mu)
+  const bool batchOK = (prm->stage_mask & VVCR_STAGE_ALL) == VVCR_STAGE_ALL;
   auto launch_ready = [&]() {
     for (;;) {
-      int i;
+      int i, nb = 1;
       {
         std::lock_guard<std::mutex> g(mu);
         if (stop || nextLaunch >= n || !prepared[nextLaunch]) return;
         i = nextLaunch;
+        if (batchOK && P.batch[i] == 2) {   // a frame-batched pair launches when both are prepared
+          if (!prepared[i + 1]) return;
+          nb = 2;
+        }
       }
       const double t0 = tnow();
-      const int lrc = vvcr_launch_picture(ctx, handle[i]);
+      const int32_t hs[2] = {handle[i], nb > 1 ? handle[i + 1] : -1};
+      const int lrc = nb > 1 ? vvcr_launch_pictures(ctx, hs, nb) : vvcr_launch_picture(ctx, handle[i]);
       const double tl = since(t0);
       if (lrc < 0) {
         std::lock_guard<std::mutex> g(mu);
         fail(std::string("vvcr_launch_picture: ") + vvcr_last_error(ctx), VVCR_E_STATE);
         return;
       }
+      const int last = i + nb - 1;
       const double t1 = tnow();
-      while (outPos < P.outOrder.size() && P.outReady[P.outOrder[outPos]] <= i) {
+      while (outPos < P.outOrder.size() && P.outReady[P.outOrder[outPos]] <= last) {
         const int k = P.outOrder[outPos++];
         if (prm->on_output) prm->on_output(prm->user, k, P.poc[k], P.slot[k]);
       }
@@ -224,11 +251,13 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
       std::vector<int> drop;
       {
         std::lock_guard<std::mutex> g(mu);
-        launched[i] = 1;
-        nextLaunch = i + 1;
+        for (int k = i; k <= last; k++) {
+          launched[k] = 1;
+          live.live.push_back(k);
+        }
+        nextLaunch = last + 1;
         T[VVCP_PHASE_LAUNCH] += tl;
         T[VVCP_PHASE_OUTPUT] += to;
-        live.live.push_back(i);
         if (!prm->handles_out)   // pictures whose deltas no later derivation can read
           live.trim(P, refined, nderived, KEEP_HANDLES, [&](int k) { drop.push_back(k); });
         cvm.notify_all();
@@ -411,6 +440,25 @@ extern "C" int vvcp_decode_plan(const vvcp_stream *h, int32_t slot_base, int32_t
 // with each picture launched right after its derivation and the worst case for refinement: every picture
 // has DMVR sub-blocks, so only a collocated read records its refined motion. Returns the largest number of
 // live handles (launched, not released) with `keep` handles kept; a CPU test bounds it.
+// The frame batching vvcp_decode applies (VVCP_MC_BATCH): first[i] = 2 for the first picture of a pair
+// launched together, 0 for its partner, 1 for a picture launched alone. Returns the number of pairs.
+extern "C" int vvcp_decode_batches(const vvcp_stream *h, int32_t slot_base, int32_t num_slots, int32_t *first) {
+  if (!h || num_slots <= 0 || slot_base < 0) return VVCR_E_ARG;
+  try {
+    DecodePlan P;
+    P.build(h->s, slot_base, num_slots);
+    int pairs = 0;
+    for (int i = 0; i < P.n; i++) {
+      if (first) first[i] = P.batch[i];
+      pairs += P.batch[i] == 2;
+    }
+    return pairs;
+  } catch (const std::exception &e) {
+    vvcp::set_api_error(e.what());
+    return VVCR_E_UNSUPPORTED;
+  }
+}
+
 extern "C" int vvcp_decode_live_bound(const vvcp_stream *h, int32_t slot_base, int32_t num_slots, int32_t keep) {
   if (!h || num_slots <= 0 || slot_base < 0 || keep < 0) return VVCR_E_ARG;
   try {

@@ -14,6 +14,29 @@
 
 namespace vvcp {
 
+// Mi's flag bitfields must be laid out as MotionRec::flags (vvcp_mv.h); a compiler that orders them otherwise
+// would corrupt every consumer of the motion rows, so the library refuses to load (constexpr bit_cast of
+// bitfields is not available to a static_assert).
+namespace {
+struct MiLayoutCheck {
+  MiLayoutCheck() {
+    Mi m;
+    m.isInter = 1; m.altHpel = 0; m.bcw = 2;
+    uint8_t b[sizeof(Mi)];
+    std::memcpy(b, &m, sizeof m);
+    Mi n;
+    n.isInter = 0; n.altHpel = 1; n.bcw = 0;
+    uint8_t c[sizeof(Mi)];
+    std::memcpy(c, &n, sizeof n);
+    if (b[offsetof(MotionRec, flags)] != 0x09 || c[offsetof(MotionRec, flags)] != 0x02) {
+      std::fprintf(stderr, "libvvcr: Mi flag bitfields are not laid out as MotionRec::flags\n");
+      std::abort();
+    }
+  }
+} const g_mi_layout_check;
+}  // namespace
+
+
 bool Mi::same(const Mi &o) const {
   if (isInter != o.isInter) return false;
   if (isInter) {

@@ -29,6 +29,9 @@ struct Mi {
   Mi() : ref{-1, -1}, interDir(0), isInter(0), altHpel(0), bcw(0), mv{{0, 0}, {0, 0}}, slice(0), pad_(0) {}
   bool same(const Mi &o) const;   // MotionInfo::operator==
 };
+// The flags byte's bit order is implementation-defined for bitfields; the readers of the rows (from_rec, the
+// deblocking planners, the SbTMVP equality) take flags = is_inter | alt_hpel << 1 | bcw << 2: checked when the
+// library loads (vvcp_mv.cpp, MiLayoutCheck: {isInter 1, altHpel 0, bcw 2} must be the byte 0x09).
 static_assert(sizeof(Mi) == sizeof(MotionRec) && offsetof(Mi, mv) == offsetof(MotionRec, mv0x) &&
                   offsetof(Mi, interDir) == offsetof(MotionRec, inter_dir) && offsetof(Mi, slice) == offsetof(MotionRec, slice),
               "Mi has the layout of a MotionRec");

@@ -32,6 +32,8 @@ thread_local std::string g_create_error;
 // Error text of the last failing context call, per calling thread (like errno): vvcr_prepare_planned may
 // fail on several threads at once, so the message is never a field shared between threads.
 thread_local std::string g_ctx_error;
+// live contexts: the last vvcr_destroy frees the large-buffer cache's unused page-locked blocks
+static std::atomic<int> g_live_ctx{0};
 
 // device / page-locked allocations made while preparing pictures (VVCR_PREP_PROF reports them)
 std::atomic<uint64_t> g_prep_allocs{0}, g_prep_alloc_bytes{0};
@@ -225,6 +227,9 @@ struct Prepared {
   bool timed[NK] = {};              // the group's events were recorded by the last launch
   bool launched = false;
   int lane = 0;                      // execution lane of the last launch (its stream and scratch planes)
+  int set = 0;                       // the lane's scratch set of the last launch (k: k-th picture of a batch)
+  int mc_pics = 1;                   // pictures whose plain MC the K_MC launch of this record carried (0: batched
+                                     // into another picture's launch, whose record holds the time and bytes)
   uint32_t staged = 0;               // stages launched so far by vvcr_launch_picture_stages (0: none pending)
   double alg_bytes[NK] = {};
   int launches[NK] = {};
@@ -265,6 +270,8 @@ struct Prepared {
     launched = false;
     staged = 0;
     lane = 0;
+    set = 0;
+    mc_pics = 1;
   }
 };
 
@@ -362,9 +369,15 @@ static int rd_kind(int w, int h, int &tw, int &th) {
 // slot (WAW / WAR) — so pictures that do not reference each other (the pictures of one temporal layer of
 // an RA GOP, an intra picture and the B pictures decoded before it) reconstruct concurrently.
 constexpr int MAXLANE = 16;
+// A lane's scratch planes: set 0 serves every picture; set k (allocated at the lane's first batched launch) the
+// k-th picture of a frame-batched launch (vvcr_launch_pictures), whose residual / prediction / loop-filter
+// planes must stay intact while the batch's other pictures run.
+struct ScratchSet {
+  DPlane pred[3], resi[3], tmp[3];
+};
 struct Lane {
   hipStream_t s = nullptr;
-  DPlane pred[3], resi[3], tmp[3];
+  ScratchSet set[MC_MAXPIC];
   DevVec<uint8_t> dbkp;              // device deblocking planner's maps and lists (allocated at its first use)
   const void *held = nullptr;        // a picture launched stage by stage whose later stages are pending here
   int tail_slot = -1;                // DPB slot written by the lane's last picture
@@ -463,42 +476,60 @@ static WpTable make_wp_table(const vvcr_pic_params &pp, int bit_depth) {
   return T;
 }
 
-// the planes a prepared picture is reconstructed (and deblocked) in on a lane
-static const DPlane *recon_planes(vvcr_ctx *ctx, const Prepared &r, int lane) {
-  return r.recon_tmp ? ctx->lanes[lane].tmp : ctx->dpb[r.pp.slot].data();
+// the planes a prepared picture is reconstructed (and deblocked) in on a lane's scratch set
+static const DPlane *recon_planes(vvcr_ctx *ctx, const Prepared &r, int lane, int set) {
+  return r.recon_tmp ? ctx->lanes[lane].set[set].tmp : ctx->dpb[r.pp.slot].data();
 }
 
-static McParams make_mc_params(vvcr_ctx *ctx, const Prepared &r, int lane, const WpTable *wpd) {
+static McParams make_mc_params(vvcr_ctx *ctx, const Prepared &r, int lane, int set, const WpTable *wpd) {
   const vvcr_pic_params &pp = r.pp;
   McParams P{};
   P.ref.p = ctx->d_ref_table.p;
   for (int c = 0; c < 3; c++) {
     P.ref.stride[c] = ctx->dpb[0][c].stride; P.ref.w[c] = ctx->dpb[0][c].w; P.ref.h[c] = ctx->dpb[0][c].h;
   }
-  for (int c = 0; c < 3; c++) P.out[c] = ctx->lanes[lane].pred[c];
+  const ScratchSet &S = ctx->lanes[lane].set[set];
+  for (int c = 0; c < 3; c++) P.out[c] = S.pred[c];
   P.pic_w = ctx->sp.width;
   P.pic_h = ctx->sp.height;
   P.bd = ctx->sp.bit_depth;
   P.ctu = 1 << ctx->sp.ctu_log2;
   P.wp = make_wp_table(pp, ctx->sp.bit_depth);
   P.wpd = wpd;
-  const DPlane *reco = recon_planes(ctx, r, lane);
+  const DPlane *reco = recon_planes(ctx, r, lane, set);
   for (int c = 0; c < 3; c++) {
     P.reco[c] = reco[c];
-    P.resi[c] = ctx->lanes[lane].resi[c];
+    P.resi[c] = S.resi[c];
   }
   return P;
 }
 
+// k_mc's view of a prepared picture on a lane's scratch set (one picture of a frame-batched launch)
+static McPic make_mc_pic(vvcr_ctx *ctx, const Prepared &r, int lane, int set) {
+  McPic q{};
+  const ScratchSet &S = ctx->lanes[lane].set[set];
+  const DPlane *reco = recon_planes(ctx, r, lane, set);
+  for (int c = 0; c < 3; c++) {
+    q.out[c] = S.pred[c];
+    q.reco[c] = reco[c];
+    q.resi[c] = S.resi[c];
+  }
+  q.wpd = r.wpt.p;
+  q.jobs = r.mc_basic.p;
+  q.ct = r.mc_ct;
+  return q;
+}
+
 // parameters of the intra / inter-reconstruction kernels for a prepared picture
-static IntraParams make_intra_params(vvcr_ctx *ctx, const Prepared &r, int lane) {
+static IntraParams make_intra_params(vvcr_ctx *ctx, const Prepared &r, int lane, int set) {
   const vvcr_pic_params &pp = r.pp;
   IntraParams P{};
-  const DPlane *reco = recon_planes(ctx, r, lane);
+  const DPlane *reco = recon_planes(ctx, r, lane, set);
+  const ScratchSet &S = ctx->lanes[lane].set[set];
   for (int c = 0; c < 3; c++) {
     P.reco[c] = reco[c];
-    P.pred[c] = ctx->lanes[lane].pred[c];
-    P.resi[c] = ctx->lanes[lane].resi[c];
+    P.pred[c] = S.pred[c];
+    P.resi[c] = S.resi[c];
   }
   P.bd = ctx->sp.bit_depth;
   P.ctu = 1 << ctx->sp.ctu_log2;
@@ -745,11 +776,11 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
     st.add_big(r.idep_start, ip.dep_start);
     st.add_big(r.ideps, ip.deps);
     r.istate.ensure(std::max<size_t>(16 + ip.jobs.size(), (size_t)sp.width * sp.height / 64));   // (an intra picture's steps)
-    // one device copy per lane (scratch plane pointers differ), written after place(): they hold the
-    // arena address of the LMCS table (staged above), which is only known then
+    // one device copy per lane and scratch set (the plane pointers differ; [set * MAXLANE + lane]), written
+    // after place(): they hold the arena address of the LMCS table (staged above), which is only known then
     {
-      static const IntraParams blank[MAXLANE] = {};
-      st.add(r.iparams, blank, MAXLANE);
+      static const IntraParams blank[MAXLANE * MC_MAXPIC] = {};
+      st.add(r.iparams, blank, MAXLANE * MC_MAXPIC);
     }
     iparams_off = st.last_off();
     r.n_ijobs = (int)ip.jobs.size();
@@ -816,7 +847,8 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   // recycled from inter to intra pictures does not regrow it
   st.place((size_t)sp.width * sp.height * 4);
   if (iparams_off != SIZE_MAX)
-    for (int l = 0; l < MAXLANE; l++) st.host_at<IntraParams>(iparams_off)[l] = make_intra_params(ctx, r, l);
+    for (int k = 0; k < MC_MAXPIC; k++)
+      for (int l = 0; l < MAXLANE; l++) st.host_at<IntraParams>(iparams_off)[k * MAXLANE + l] = make_intra_params(ctx, r, l, k);
   pt.mark(7);
   st.copy(ctx->upload_stream, r.up_done);
   r.up_issued = true;
@@ -861,24 +893,28 @@ static DbkPlanArgs dbk_plan_args(vvcr_ctx *ctx, Lane &ln, const Prepared &r) {
   return a;
 }
 
-// Device phase: enqueue the kernels of a prepared picture on the context stream.
-static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL) {
-  const vvcr_pic_params &pp = r.pp;
-  const uint32_t mask = r.mask & stages;
+// ---- Device phase: the kernels of prepared pictures on a lane ----------------------------------------
+
+// the distinct DPB slots a picture references
+static std::vector<int> ref_slots(const vvcr_pic_params &pp) {
   std::vector<int> refs;
   for (int l = 0; l < 2; l++)
     for (int i = 0; i < pp.num_ref[l]; i++)
       if (std::find(refs.begin(), refs.end(), pp.ref_slot[l][i]) == refs.end()) refs.push_back(pp.ref_slot[l][i]);
-  // Lane choice: pictures without references (intra) take lanes [0, nintra), which only intra pictures
-  // use, so an intra picture never queues behind B pictures and two intra-started segments may overlap;
-  // the others take the lane of [nintra, nlane) that wrote their newest reference (stream order then
-  // costs nothing; VVCR_LANE_POLICY=0: only a lane whose last picture is a reference), else the least
-  // recently used of those lanes. Dependencies on pictures of the chosen lane need no event wait.
+  return refs;
+}
+
+// Lane choice: pictures without references (intra) take lanes [0, nintra), which only intra pictures use, so
+// an intra picture never queues behind B pictures and two intra-started segments may overlap; the others take
+// the lane of [nintra, nlane) that wrote their newest reference (stream order then costs nothing;
+// VVCR_LANE_POLICY=0: only a lane whose last picture is a reference), else the least recently used of those
+// lanes. Dependencies on pictures of the chosen lane need no event wait.
+static int choose_lane(vvcr_ctx *ctx, const Prepared &r, const std::vector<int> &refs) {
   const int lo = refs.empty() ? 0 : ctx->nintra, hi = refs.empty() ? ctx->nintra : ctx->nlane;
   // the later stages of a picture launched stage by stage stay on its lane: they read that lane's
   // residual / prediction planes
   int L = r.staged ? r.lane : -1;
-  // (lanes holding another picture's pending stages are not chosen while others are free)
+  // (lanes holding another picture's pending stages are never chosen)
   auto held = [&](int l) { return ctx->lanes[l].held != nullptr && ctx->lanes[l].held != &r; };
   if (L < 0 && !refs.empty() && ctx->lane_policy == 1) {
     // the B lane that wrote the newest of the references (still in its slot): the pictures of one
@@ -895,23 +931,48 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
       const int ts = ctx->lanes[l].tail_slot;
       if (ts >= 0 && !held(l) && std::find(refs.begin(), refs.end(), ts) != refs.end() && ctx->lanes[l].tail_seq == ctx->slot_seq[ts]) L = l;
     }
-  for (int pass = 0; pass < 2 && L < 0; pass++) {
+  if (L < 0) {
     uint64_t best = ~0ull;
     for (int l = lo; l < hi; l++)
-      if ((pass || !held(l)) && ctx->lanes[l].tail_seq < best) { best = ctx->lanes[l].tail_seq; L = l; }
+      if (!held(l) && ctx->lanes[l].tail_seq < best) { best = ctx->lanes[l].tail_seq; L = l; }
   }
+  // every lane of the picture's kind holds another picture's pending stages: its residual / prediction /
+  // loop-filter planes are still to be read by those stages, so no lane may take this picture (a held lane
+  // would have its planes overwritten and the held picture's later stages would read them: wrong output)
+  if (L < 0)
+    throw VvcrError(VVCR_E_STATE, "every " + std::string(refs.empty() ? "intra" : "inter") +
+                                      " lane holds a picture launched stage by stage whose later stages are pending; "
+                                      "launch those stages first (or raise VVCR_LANES)");
+  return L;
+}
+
+// The picture's rows: a spatial shard reconstructs and filters its own rows; its SAO also covers the 8 rows
+// around them that its ALF reads (their deblocked inputs come from the VVCR_LF_HALO rows the caller imported).
+struct Rows {
+  int own0, own1, sao0, sao1;
+};
+static Rows pic_rows(const vvcr_ctx *ctx, const vvcr_pic_params &pp) {
+  const int H = ctx->sp.height;
+  const bool shard = pp.shard_y1 > 0;
+  Rows w;
+  w.own0 = shard ? pp.shard_y0 : 0;
+  w.own1 = shard ? pp.shard_y1 : H;
+  w.sao0 = shard ? std::max(0, w.own0 - 8) : 0;
+  w.sao1 = shard ? std::min(H, w.own1 + 8) : H;
+  return w;
+}
+
+// The picture's dependencies on pictures of other lanes (same-lane work is ordered by the stream anyway),
+// its upload, and its start marker.
+static void launch_begin(vvcr_ctx *ctx, Prepared &r, int L, int set, const std::vector<int> &refs) {
+  const vvcr_pic_params &pp = r.pp;
   Lane &ln = ctx->lanes[L];
   hipStream_t s = ln.s;
   r.lane = L;
-  // rows: a spatial shard reconstructs and filters its own rows; its SAO also covers the 8 rows around
-  // them that its ALF reads (their deblocked inputs come from the VVCR_LF_HALO rows the caller imported)
-  const int H = ctx->sp.height;
-  const bool shard = pp.shard_y1 > 0;
-  const int own0 = shard ? pp.shard_y0 : 0, own1 = shard ? pp.shard_y1 : H;
-  const int sao0 = shard ? std::max(0, own0 - 8) : 0, sao1 = shard ? std::min(H, own1 + 8) : H;
+  r.set = set;
+  r.mc_pics = 1;
   ln.tail_slot = pp.slot;
   ln.tail_seq = ++ctx->seq;
-  // dependencies on pictures of other lanes (same-lane work is ordered by the stream anyway)
   for (int rs : refs)
     if (ctx->slot_w_set[rs] && ctx->slot_lane[rs] != L) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[rs], 0));
   if (ctx->slot_w_set[pp.slot] && ctx->slot_lane[pp.slot] != L) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[pp.slot], 0));
@@ -919,53 +980,100 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
     if (l != L && (ctx->slot_r_set[pp.slot] >> l & 1)) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_r[pp.slot][l], 0));
   VVCR_CHECK_HIP(hipStreamWaitEvent(s, r.up_done, 0));   // the picture's upload
   VVCR_CHECK_HIP(hipEventRecord(r.start, s));
-  if (mask & VVCR_STAGE_RESID) {
-    KernelTimer t(r, K_RESID, s, ctx->timing);
-    if (!r.zero_filled) {
-      Planes3 clr{};
-      for (int c = 0; c < 3; c++) clr.dst[c] = ln.resi[c];
-      clr.y0 = own0; clr.y1 = own1;
-      launch_planes3(clr, s);
+}
+
+static void launch_resid_stage(vvcr_ctx *ctx, Prepared &r) {
+  const ScratchSet &S = ctx->lanes[r.lane].set[r.set];
+  hipStream_t s = ctx->lanes[r.lane].s;
+  const Rows rw = pic_rows(ctx, r.pp);
+  KernelTimer t(r, K_RESID, s, ctx->timing);
+  if (!r.zero_filled) {
+    Planes3 clr{};
+    for (int c = 0; c < 3; c++) clr.dst[c] = S.resi[c];
+    clr.y0 = rw.own0; clr.y1 = rw.own1;
+    launch_planes3(clr, s);
+  }
+  TbParams tp{};
+  for (int c = 0; c < 3; c++) tp.out[c] = S.resi[c];
+  tp.bd = ctx->sp.bit_depth;
+  memcpy(tp.scan_off, ctx->scans.off, sizeof(tp.scan_off));
+  memcpy(tp.lfnst_scan_off, ctx->scans.lfnst_off, sizeof(tp.lfnst_scan_off));
+  launch_resid(tp, r.tb.p, r.n_tb, r.n_tb_small, r.coef.p, ctx->d_scans.p, s);
+  VVCR_CHECK_HIP(hipGetLastError());
+  r.launches[K_RESID] = r.n_tb > 0 ? 1 : 0;
+}
+
+// plain MC (k_mc) of n pictures of one lane in one launch; the first picture's record holds the kernel time
+// and the algorithmic bytes of all of them
+static void launch_plain_mc(vvcr_ctx *ctx, Prepared *const *rs, int n) {
+  Prepared &r0 = *rs[0];
+  hipStream_t s = ctx->lanes[r0.lane].s;
+  McBatch b{};
+  b.ref.p = ctx->d_ref_table.p;
+  for (int c = 0; c < 3; c++) {
+    b.ref.stride[c] = ctx->dpb[0][c].stride; b.ref.w[c] = ctx->dpb[0][c].w; b.ref.h[c] = ctx->dpb[0][c].h;
+  }
+  b.bd = ctx->sp.bit_depth;
+  b.npic = n;
+  double bytes = 0;
+  int jobs = 0;
+  for (int k = 0; k < n; k++) {
+    b.pic[k] = make_mc_pic(ctx, *rs[k], rs[k]->lane, rs[k]->set);
+    bytes += rs[k]->alg_bytes[K_MC];
+    jobs += rs[k]->n_mctile + rs[k]->n_basic;
+    if (k) {
+      rs[k]->ran[K_MC] = true;
+      rs[k]->timed[K_MC] = false;
+      rs[k]->launches[K_MC] = 0;
+      rs[k]->mc_pics = 0;
     }
-    TbParams tp{};
-    for (int c = 0; c < 3; c++) tp.out[c] = ln.resi[c];
-    tp.bd = ctx->sp.bit_depth;
-    memcpy(tp.scan_off, ctx->scans.off, sizeof(tp.scan_off));
-    memcpy(tp.lfnst_scan_off, ctx->scans.lfnst_off, sizeof(tp.lfnst_scan_off));
-    launch_resid(tp, r.tb.p, r.n_tb, r.n_tb_small, r.coef.p, ctx->d_scans.p, s);
+  }
+  KernelTimer t(r0, K_MC, s, ctx->timing);
+  launch_mc_batch(b, s);
+  VVCR_CHECK_HIP(hipGetLastError());
+  r0.launches[K_MC] = jobs ? 1 : 0;
+  r0.mc_pics = n;
+  if (n > 1) {
+    r0.alg_bytes[K_MC] = bytes;
+    for (int k = 1; k < n; k++) rs[k]->alg_bytes[K_MC] = 0;
+  }
+}
+
+// DMVR / BDOF and affine MC, then the DMVR deltas' read-back on the copy stream (the lane goes on)
+static void launch_mc_ext_stage(vvcr_ctx *ctx, Prepared &r) {
+  hipStream_t s = ctx->lanes[r.lane].s;
+  const McParams mp = make_mc_params(ctx, r, r.lane, r.set, r.wpt.p);
+  {
+    KernelTimer t(r, K_MC_BIDIR, s, ctx->timing);
+    launch_mc_bidir(mp, r.mc_bidir.p, r.n_bidir, r.dmvr.p, s);
     VVCR_CHECK_HIP(hipGetLastError());
-    r.launches[K_RESID] = r.n_tb > 0 ? 1 : 0;
+    r.launches[K_MC_BIDIR] = r.n_bidir ? 1 : 0;
   }
-  if (mask & VVCR_STAGE_INTER) {
-    const McParams mp = make_mc_params(ctx, r, L, r.wpt.p);
-    {
-      KernelTimer t(r, K_MC, s, ctx->timing);
-      launch_mc(mp, r.mc_basic.p, r.mc_ct, s);
-      VVCR_CHECK_HIP(hipGetLastError());
-      r.launches[K_MC] = (r.n_mctile + r.n_basic) ? 1 : 0;
-    }
-    {
-      KernelTimer t(r, K_MC_BIDIR, s, ctx->timing);
-      launch_mc_bidir(mp, r.mc_bidir.p, r.n_bidir, r.dmvr.p, s);
-      VVCR_CHECK_HIP(hipGetLastError());
-      r.launches[K_MC_BIDIR] = r.n_bidir ? 1 : 0;
-    }
-    {
-      KernelTimer t(r, K_MC_AFFINE, s, ctx->timing);
-      launch_mc_affine(mp, r.aff_jobs.p, r.n_aff, r.aff_pu.p, s);
-      VVCR_CHECK_HIP(hipGetLastError());
-      r.launches[K_MC_AFFINE] = r.n_aff ? 1 : 0;
-    }
-    // the deltas go to the host on the copy stream, so the lane goes on with intra and the loop filters
-    VVCR_CHECK_HIP(hipEventRecord(r.ev_mc, s));
-    VVCR_CHECK_HIP(hipStreamWaitEvent(ctx->copy_stream, r.ev_mc, 0));
-    if (r.n_dmvr > 0)
-      VVCR_CHECK_HIP(hipMemcpyAsync(r.h_dmvr, r.dmvr.p, (size_t)r.n_dmvr * 2 * sizeof(int32_t), hipMemcpyDeviceToHost,
-                                    ctx->copy_stream));
-    VVCR_CHECK_HIP(hipEventRecord(r.mc_done, ctx->copy_stream));
+  {
+    KernelTimer t(r, K_MC_AFFINE, s, ctx->timing);
+    launch_mc_affine(mp, r.aff_jobs.p, r.n_aff, r.aff_pu.p, s);
+    VVCR_CHECK_HIP(hipGetLastError());
+    r.launches[K_MC_AFFINE] = r.n_aff ? 1 : 0;
   }
+  VVCR_CHECK_HIP(hipEventRecord(r.ev_mc, s));
+  VVCR_CHECK_HIP(hipStreamWaitEvent(ctx->copy_stream, r.ev_mc, 0));
+  if (r.n_dmvr > 0)
+    VVCR_CHECK_HIP(hipMemcpyAsync(r.h_dmvr, r.dmvr.p, (size_t)r.n_dmvr * 2 * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                  ctx->copy_stream));
+  VVCR_CHECK_HIP(hipEventRecord(r.mc_done, ctx->copy_stream));
+}
+
+// intra / inter reconstruction, LMCS inverse, deblocking, SAO, ALF (stages of mask), the picture's final
+// copy into its slot, and the dependency markers
+static void launch_rest(vvcr_ctx *ctx, Prepared &r, uint32_t mask, const std::vector<int> &refs) {
+  const vvcr_pic_params &pp = r.pp;
+  const int L = r.lane;
+  Lane &ln = ctx->lanes[L];
+  const ScratchSet &S = ln.set[r.set];
+  hipStream_t s = ln.s;
+  const Rows rw = pic_rows(ctx, pp);
   if (mask & VVCR_STAGE_INTRA) {
-    const IntraParams P = make_intra_params(ctx, r, L);
+    const IntraParams P = make_intra_params(ctx, r, L, r.set);
     {
       KernelTimer t(r, K_RECON, s, ctx->timing);
       launch_recon_inter(P, r.tiles.p, r.n_tiles, s);
@@ -974,16 +1082,16 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
     }
     {
       KernelTimer t(r, K_INTRA, s, ctx->timing);
-      launch_intra(r.iparams.p + L, r.ijobs.p, r.n_ijobs, r.ictu_list.p, r.ictu_start.p, r.n_ictu, r.idep_start.p, r.ideps.p,
-                   r.istate.p, ctx->d_err, ctx->intra_wg, s);
+      launch_intra(r.iparams.p + r.set * MAXLANE + L, r.ijobs.p, r.n_ijobs, r.ictu_list.p, r.ictu_start.p, r.n_ictu, r.idep_start.p,
+                   r.ideps.p, r.istate.p, ctx->d_err, ctx->intra_wg, s);
       VVCR_CHECK_HIP(hipGetLastError());
       r.launches[K_INTRA] = r.n_ijobs ? 1 : 0;
     }
   }
-  const DPlane *A = recon_planes(ctx, r, L);   // the picture until the last loop filter
+  const DPlane *A = recon_planes(ctx, r, L, r.set);   // the picture until the last loop filter
   const DPlane *slot = ctx->dpb[pp.slot].data();
   if ((mask & VVCR_STAGE_LMCS_INV) && pp.lmcs_enabled) {
-    launch_lmcs_inverse(A[0], r.lmcs_lut.p + 1024, own0, own1, s);   // back to the original domain before the loop filters
+    launch_lmcs_inverse(A[0], r.lmcs_lut.p + 1024, rw.own0, rw.own1, s);   // back to the original domain before the loop filters
     VVCR_CHECK_HIP(hipGetLastError());
   }
   if ((mask & VVCR_STAGE_DBK) && (r.dbk_gpu ? r.n_dbcu > 0 : (r.dbk_counts[0] + r.dbk_counts[1] + r.dbk_counts[2] + r.dbk_counts[3]) > 0)) {
@@ -1027,9 +1135,9 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
   if (r.have_sao && (mask & VVCR_STAGE_SAO)) {
     KernelTimer t(r, K_SAO, s, ctx->timing);
     SaoParams sp{};
-    for (int c = 0; c < 3; c++) { sp.src[c] = inTmp ? ln.tmp[c] : slot[c]; sp.dst[c] = inTmp ? slot[c] : ln.tmp[c]; }
+    for (int c = 0; c < 3; c++) { sp.src[c] = inTmp ? S.tmp[c] : slot[c]; sp.dst[c] = inTmp ? slot[c] : S.tmp[c]; }
     sp.sao = r.sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
-    sp.y0 = sao0; sp.y1 = sao1;
+    sp.y0 = rw.sao0; sp.y1 = rw.sao1;
     launch_sao(sp, s);
     VVCR_CHECK_HIP(hipGetLastError());
     inTmp = !inTmp;
@@ -1038,7 +1146,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
   if (r.have_alf && (mask & VVCR_STAGE_ALF)) {
     KernelTimer t(r, K_ALF, s, ctx->timing);
     AlfParams ap{};
-    for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? ln.tmp[c] : slot[c]; ap.dst[c] = inTmp ? slot[c] : ln.tmp[c]; }
+    for (int c = 0; c < 3; c++) { ap.src[c] = inTmp ? S.tmp[c] : slot[c]; ap.dst[c] = inTmp ? slot[c] : S.tmp[c]; }
     ap.bd = ctx->sp.bit_depth; ap.ctu_log2 = ctx->sp.ctu_log2; ap.wc = wc; ap.nctb = n;
     ap.vb_luma = pp.alf_vb_luma; ap.vb_chroma = pp.alf_vb_chroma;
     for (int c = 0; c < 3; c++) ap.en[c] = pp.alf_en[c];
@@ -1047,17 +1155,19 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
     ap.chroma_coef = r.alf_chroma.p; ap.chroma_clip = r.alf_chroma.p + 56; ap.cc_coef = r.alf_cc.p;
     ap.ctb_en = r.alf_ctb.p; ap.ctb_alt = r.alf_ctb.p + 3 * n; ap.cc_ctl = r.alf_ctb.p + 6 * n;
     ap.ctb_set = r.alf_set.p;
-    ap.y0 = own0; ap.y1 = own1;
+    ap.y0 = rw.own0; ap.y1 = rw.own1;
     launch_alf(ap, s);
     VVCR_CHECK_HIP(hipGetLastError());
     inTmp = !inTmp;
     r.launches[K_ALF] = 1;
   }
-  if (inTmp) {
+  // a picture still in the lane's planes goes to its slot once, by the call that completes its stages (a
+  // stage-by-stage picture's earlier calls leave it in the lane: its held lane keeps those planes)
+  if (inTmp && ((r.staged | mask) & r.mask) == r.mask) {
     Planes3 cp{};
-    for (int c = 0; c < 3; c++) { cp.dst[c] = slot[c]; cp.src[c] = ln.tmp[c]; }
+    for (int c = 0; c < 3; c++) { cp.dst[c] = slot[c]; cp.src[c] = S.tmp[c]; }
     cp.copy = 1;
-    cp.y0 = own0; cp.y1 = own1;
+    cp.y0 = rw.own0; cp.y1 = rw.own1;
     launch_planes3(cp, s);
   }
   VVCR_CHECK_HIP(hipEventRecord(r.done, s));
@@ -1076,6 +1186,68 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
   if ((r.staged & r.mask) == r.mask) r.staged = 0;
   ln.held = r.staged ? &r : nullptr;
   ctx->last = &r;
+}
+
+// Device phase of one picture (the stages of `stages` it was prepared with).
+static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL) {
+  const uint32_t mask = r.mask & stages;
+  const std::vector<int> refs = ref_slots(r.pp);
+  const int L = choose_lane(ctx, r, refs);
+  launch_begin(ctx, r, L, 0, refs);
+  if (mask & VVCR_STAGE_RESID) launch_resid_stage(ctx, r);
+  if (mask & VVCR_STAGE_INTER) {
+    Prepared *one = &r;
+    launch_plain_mc(ctx, &one, 1);
+    launch_mc_ext_stage(ctx, r);
+  }
+  launch_rest(ctx, r, mask, refs);
+}
+
+// scratch set k >= 1 of a lane (frame-batched launches), allocated at its first use
+static void ensure_scratch_set(vvcr_ctx *ctx, Lane &ln, int k) {
+  if (ln.set[k].resi[0].p) return;
+  const int W = ctx->sp.width, H = ctx->sp.height;
+  for (int c = 0; c < 3; c++) {
+    const int w = c ? W / 2 : W, h = c ? H / 2 : H;
+    ln.set[k].pred[c] = alloc_plane(w, h);
+    ln.set[k].resi[c] = alloc_plane(w, h);
+    ln.set[k].tmp[c] = alloc_plane(w, h);
+  }
+}
+
+// Frame-batched launch of n independent pictures (every stage; none references another's slot, all write
+// different slots) on one lane: picture k on the lane's scratch set k. Their residuals, then ONE k_mc launch
+// for all of their plain MC, then picture by picture DMVR / BDOF, affine and the remaining stages. Each
+// picture's dependency markers are recorded after its own last stage.
+static void launch_batch(vvcr_ctx *ctx, Prepared *const *rs, int n) {
+  if (n < 1 || n > MC_MAXPIC) throw VvcrError(VVCR_E_ARG, "a batched launch takes 1 .. " + std::to_string(MC_MAXPIC) + " pictures");
+  std::vector<std::vector<int>> refs(n);
+  for (int k = 0; k < n; k++) {
+    const Prepared &r = *rs[k];
+    if (r.staged) throw VvcrError(VVCR_E_STATE, "a picture with pending stages cannot be launched in a batch");
+    if ((r.mask & VVCR_STAGE_ALL) != VVCR_STAGE_ALL) throw VvcrError(VVCR_E_ARG, "batched pictures are prepared with every stage");
+    refs[k] = ref_slots(r.pp);
+    if (n > 1 && refs[k].empty()) throw VvcrError(VVCR_E_ARG, "batched pictures are inter pictures");
+    for (int j = 0; j < k; j++) {
+      if (rs[j] == rs[k] || rs[j]->pp.slot == r.pp.slot) throw VvcrError(VVCR_E_ARG, "batched pictures write different slots");
+      if (std::find(refs[k].begin(), refs[k].end(), rs[j]->pp.slot) != refs[k].end() ||
+          std::find(refs[j].begin(), refs[j].end(), r.pp.slot) != refs[j].end())
+        throw VvcrError(VVCR_E_ARG, "a batched picture references another picture of its batch");
+    }
+  }
+  if (n == 1) { launch(ctx, *rs[0]); return; }
+  // the lane of the first picture (its newest reference's); a picture of the batch whose references
+  // were written on other lanes waits for them by events like any picture
+  const int L = choose_lane(ctx, *rs[0], refs[0]);
+  Lane &ln = ctx->lanes[L];
+  for (int k = 1; k < n; k++) ensure_scratch_set(ctx, ln, k);
+  for (int k = 0; k < n; k++) launch_begin(ctx, *rs[k], L, k, refs[k]);
+  for (int k = 0; k < n; k++) launch_resid_stage(ctx, *rs[k]);
+  launch_plain_mc(ctx, rs, n);
+  for (int k = 0; k < n; k++) {
+    launch_mc_ext_stage(ctx, *rs[k]);
+    launch_rest(ctx, *rs[k], rs[k]->mask, refs[k]);
+  }
 }
 
 extern "C" {
@@ -1154,9 +1326,9 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       for (int c = 0; c < 3; c++) {
         Lane &ln = ctx->lanes[l];
         int w = c ? W / 2 : W, h = c ? H / 2 : H;
-        ln.pred[c] = alloc_plane(w, h);
-        ln.resi[c] = alloc_plane(w, h);
-        ln.tmp[c] = alloc_plane(w, h);
+        ln.set[0].pred[c] = alloc_plane(w, h);
+        ln.set[0].resi[c] = alloc_plane(w, h);
+        ln.set[0].tmp[c] = alloc_plane(w, h);
       }
     if (ctx->intra_wg <= 0) {
       // k_intra takes CTUs in wavefront order: the CTUs in flight are those of a few anti-diagonals
@@ -1176,6 +1348,7 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     return e.code;
   }
   *out = ctx.release();
+  g_live_ctx.fetch_add(1);
   return VVCR_OK;
 }
 
@@ -1190,7 +1363,7 @@ int vvcr_destroy(vvcr_ctx *ctx) {
   for (int l = 0; l < ctx->nlane; l++)
     for (int c = 0; c < 3; c++) {
       Lane &ln = ctx->lanes[l];
-      (void)hipFree(ln.pred[c].p); (void)hipFree(ln.resi[c].p); (void)hipFree(ln.tmp[c].p);
+      for (ScratchSet &S : ln.set) { (void)hipFree(S.pred[c].p); (void)hipFree(S.resi[c].p); (void)hipFree(S.tmp[c].p); }
     }
   for (auto &e : ctx->slot_w) if (e) (void)hipEventDestroy(e);
   for (auto &a : ctx->slot_r)
@@ -1200,6 +1373,7 @@ int vvcr_destroy(vvcr_ctx *ctx) {
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
   delete ctx;
+  if (g_live_ctx.fetch_sub(1) == 1) bigbuf::trim_pinned();
   return VVCR_OK;
 }
 
@@ -1414,6 +1588,17 @@ int vvcr_launch_picture_stages(vvcr_ctx *ctx, int32_t handle, uint32_t stage_mas
   API_BEGIN
   std::lock_guard<std::mutex> g(ctx->launch_mu);
   launch(ctx, get_prepared(ctx, handle), stage_mask);
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_launch_pictures(vvcr_ctx *ctx, const int32_t *handles, int32_t n) {
+  if (!ctx || !handles || n < 1 || n > MC_MAXPIC) return VVCR_E_ARG;
+  API_BEGIN
+  std::lock_guard<std::mutex> g(ctx->launch_mu);
+  Prepared *rs[MC_MAXPIC];
+  for (int k = 0; k < n; k++) rs[k] = &get_prepared(ctx, handles[k]);
+  launch_batch(ctx, rs, n);
   return VVCR_OK;
   API_END
 }
@@ -1650,6 +1835,7 @@ int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int3
     strncpy(s.name, kKernelNames[k], sizeof(s.name) - 1);
     s.launches = r->ran[k] ? r->launches[k] : 0;
     s.alg_bytes = r->ran[k] ? r->alg_bytes[k] : 0.0;
+    s.pictures = k == K_MC ? r->mc_pics : 1;
     float ms = 0;
     // a stage with nothing to launch has an empty event pair: no kernel time
     if (r->ran[k] && r->timed[k] && r->launches[k] > 0) VVCR_CHECK_HIP(hipEventElapsedTime(&ms, r->ev[k][0], r->ev[k][1]));
@@ -1705,8 +1891,8 @@ static DPlane *select_plane(vvcr_ctx *ctx, int32_t buf, int32_t slot, int32_t co
     case VVCR_BUF_RECO:
       if (slot < 0 || slot >= (int)ctx->dpb.size()) throw VvcrError(VVCR_E_ARG, "bad slot");
       return &ctx->dpb[slot][comp];
-    case VVCR_BUF_PRED: return &ctx->lanes[ctx->last ? ctx->last->lane : 0].pred[comp];   // of the last launched picture
-    case VVCR_BUF_RESI: return &ctx->lanes[ctx->last ? ctx->last->lane : 0].resi[comp];
+    case VVCR_BUF_PRED: return &ctx->lanes[ctx->last ? ctx->last->lane : 0].set[ctx->last ? ctx->last->set : 0].pred[comp];   // of the last launched picture
+    case VVCR_BUF_RESI: return &ctx->lanes[ctx->last ? ctx->last->lane : 0].set[ctx->last ? ctx->last->set : 0].resi[comp];
     default: throw VvcrError(VVCR_E_ARG, "bad buffer id");
   }
 }

@@ -136,6 +136,34 @@ inline void release(void *p, size_t bytes) {
   else std::free(p);
 }
 
+// frees every cached (unused) page-locked block: the reconstruction context calls it when its last
+// instance is destroyed, so a process that stops decoding does not keep gigabytes of pinned memory that
+// co-located processes and the page cache could use. Blocks still in use are freed on their release as usual.
+inline void trim_pinned() {
+  Cache &c = Cache::get();
+  std::vector<void *> drop;
+  PinFree pf = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c.mu);
+    pf = c.pin_free;
+    for (auto &kv : c.free) {
+      auto &v = kv.second;
+      for (size_t i = 0; i < v.size();) {
+        if (c.pinned.erase(v[i])) {
+          drop.push_back(v[i]);
+          c.cached -= kv.first;
+          v[i] = v.back();
+          v.pop_back();
+        } else {
+          i++;
+        }
+      }
+    }
+  }
+  if (pf)
+    for (void *p : drop) pf(p);
+}
+
 // std::vector allocator drawing large arrays from the cache
 template <class T>
 struct Alloc {

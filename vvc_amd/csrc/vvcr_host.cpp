@@ -84,8 +84,7 @@ void sort_by_size_bi(bigbuf::vec<McJob> &v) {
 }
 
 // A k_mc class table over job arrays laid out one after another from job index base (each flagged: its
-// windows may leave the picture): one class per run of equal (w, h) and, with MC_BI_SPLIT, equal
-// bi-prediction (the lists sort bi-predicted jobs first within a size), its cell ranges padded to whole waves.
+// windows may leave the picture): one class per run of equal (w, h), its cell ranges padded to whole waves.
 void build_mc_classes(McClassTable &ct, std::initializer_list<std::pair<const bigbuf::vec<McJob> *, bool>> lists, int base) {
   ct = McClassTable();
   int lc = 0, cc = 0;
@@ -93,19 +92,17 @@ void build_mc_classes(McClassTable &ct, std::initializer_list<std::pair<const bi
     const bigbuf::vec<McJob> &v = *lv.first;
     for (size_t i = 0; i < v.size();) {
       size_t e = i + 1;
-      while (e < v.size() && v[e].w == v[i].w && v[e].h == v[i].h && (!MC_BI_SPLIT || mc_bi(v[e]) == mc_bi(v[i]))) e++;
+      while (e < v.size() && v[e].w == v[i].w && v[e].h == v[i].h) e++;
       if (ct.n == MC_MAXCLS) fail("more plain-MC block classes than k_mc classes");
       const int k = ct.n++, w = v[i].w, h = v[i].h, n = (int)(e - i);
-      const int sp = MC_BI_SPLIT && mc_bi(v[i]) ? 1 : 0;
       ct.job0[k] = base + (int)i;
       ct.w[k] = w;
       ct.h[k] = h;
       ct.edge[k] = lv.second ? 1 : 0;
-      ct.split[k] = sp;
       ct.lcell0[k] = lc;
       ct.ccell0[k] = cc;
-      lc += ((n * mc_luma_cells(w, h, lv.second)) << sp) + 63 & ~63;
-      cc += ((n * mc_chroma_cells(w, h)) << sp) + 63 & ~63;
+      lc += (n * mc_luma_cells(w, h)) + 63 & ~63;
+      cc += (n * mc_chroma_cells(w, h)) + 63 & ~63;
       i = e;
     }
     base += (int)v.size();

@@ -150,46 +150,43 @@ struct McParams {
 // 4 columns x 4 rows of one component) for every list of its job. The job array holds the 32x32 tiles,
 // then the smaller blocks, grouped in classes of one size (w, h); a class's cells are numbered job-major
 // from lcell0 / ccell0, each range padded to a multiple of 64, so no wave straddles two classes.
-// MC_BI_SPLIT=1: the cells of bi-predicted jobs (classes of their own) take two adjacent lanes, one list each
-// (vvcr_mc.hip mc_cell): a class's cells per job double. Measured slower (r05, mc_bench in isolation, 4K B
-// pictures: QP27 33.4 vs 30.2 us, QP32 26.1 vs 25.5 us; gpurun_out/r05q_split): the doubled bi waves cost
-// more than the halved chain of each. Kept as an A/B option, off.
-#ifndef MC_BI_SPLIT
-#define MC_BI_SPLIT 0
-#endif
 constexpr int MC_MAXCLS = 32;
 struct McClassTable {
   int32_t n = 0;                      // classes
   int32_t job0[MC_MAXCLS + 1] = {};   // first job of the class in the combined job array; [n] = jobs in all
   int32_t w[MC_MAXCLS] = {}, h[MC_MAXCLS] = {};
   int32_t edge[MC_MAXCLS] = {};       // the class's windows may leave the picture (mc_job_edge): clamped path
-  int32_t split[MC_MAXCLS] = {};      // bi-predicted jobs, two lanes per cell (MC_BI_SPLIT)
   int32_t lcell0[MC_MAXCLS + 1] = {}; // first luma cell of each class; [n] = luma cells in all (lanes)
   int32_t ccell0[MC_MAXCLS + 1] = {}; // chroma cells likewise
 };
 // cells of one job of size w x h: luma (w/4) x ceil(h/8), chroma 2 components x ceil(w/8) x (h/16, or ceil(h/8))
-#ifndef MC_TALL_LUMA
-#define MC_TALL_LUMA 0
-#endif
-// luma cells: 4 columns x 16 rows for blocks of >= 16 rows when MC_TALL_LUMA (a quarter less H work), else 4 x 8
-// (not in edge classes: their clamped path keeps 8-row cells)
-__host__ __device__ inline bool mc_tall_luma(int h, bool edge) { return MC_TALL_LUMA && h >= 16 && !edge; }
-// MC_SHORT_LUMA: 4 x 4 luma cells outside the edge classes (twice the waves, each with a shorter chain; the
-// H pass filters 11 rows per 4 outputs instead of 15 per 8)
-#ifndef MC_SHORT_LUMA
-#define MC_SHORT_LUMA 0
-#endif
-__host__ __device__ inline bool mc_short_luma(bool edge) { return MC_SHORT_LUMA && !edge; }
-__host__ __device__ inline int mc_luma_cells(int w, int h, bool edge) {
-  return (w >> 2) * (mc_short_luma(edge) ? (h + 3) >> 2 : mc_tall_luma(h, edge) ? h >> 4 : (h + 7) >> 3);
-}
+__host__ __device__ inline int mc_luma_cells(int w, int h) { return (w >> 2) * ((h + 7) >> 3); }
 // chroma cells: 4 columns x 8 rows for blocks of >= 16 luma rows (a third less H work than two 4-row
 // cells), else 4 x 4
-#ifndef MC_TALL_CHROMA
-#define MC_TALL_CHROMA 1
-#endif
-__host__ __device__ inline bool mc_tall_chroma(int h) { return MC_TALL_CHROMA && h >= 16; }
+__host__ __device__ inline bool mc_tall_chroma(int h) { return h >= 16; }
 __host__ __device__ inline int mc_chroma_cells(int w, int h) { return 2 * ((w + 7) >> 3) * (mc_tall_chroma(h) ? h >> 4 : (h + 7) >> 3); }
+
+// Frame batching of k_mc: one launch carries the plain MC of up to MC_MAXPIC pictures that do not reference
+// each other (BASELINE.md allows frame-batched launches). A k_mc launch of a single 4K picture is one
+// partial round of waves (3.4 per SIMD at QP32): its time is the ramp and tail of that round, which a second
+// picture's waves fill. Each picture brings its destination, residual and prediction planes (its lane's
+// scratch set), its weighted-prediction table, its jobs and its class table; the DPB is shared.
+constexpr int MC_MAXPIC = 2;
+struct McPic {
+  DPlane out[3];         // prediction planes (jobs without MC_RECON)
+  DPlane reco[3];        // the picture (MC_RECON jobs)
+  DPlane resi[3];        // the residual planes (MC_RESI jobs)
+  const WpTable *wpd;    // weighted-prediction table in device memory
+  const McJob *jobs;     // the picture's plain MC jobs (class order)
+  McClassTable ct;
+};
+struct McBatch {
+  RefPlanes ref;                      // DPB planes by slot
+  int32_t bd = 10, npic = 0;
+  int32_t lblk0[MC_MAXPIC + 1] = {};  // first luma block of each picture; [npic] = luma blocks of all (launch_mc_batch)
+  int32_t cblk0[MC_MAXPIC + 1] = {};  // chroma blocks likewise, counted after every luma block
+  McPic pic[MC_MAXPIC];
+};
 
 // A workgroup-uniform record (job descriptor) through dword loads at a uniform address, so that it lands in
 // SGPRs (s_load): a plain struct copy loads its 16-bit fields with per-lane global loads, and everything
@@ -321,4 +318,4 @@ void launch_planes3(const Planes3 &p, hipStream_t s);
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, int nsmall, const int32_t *coef, const uint16_t *scans, hipStream_t s);
 // DecoderApp output frame of a picture (vvcr_write_output)
 void launch_output(const std::array<DPlane, 3> &pic, const vvcr_output_params &op, int bd, uint8_t *dst, hipStream_t s);
-void launch_mc(const McParams &p, const McJob *jobs, const McClassTable &ct, hipStream_t s);   // cells of the job classes
+void launch_mc_batch(McBatch &b, hipStream_t s);   // k_mc over the pictures of b (fills b.lblk0 / cblk0)

@@ -185,15 +185,13 @@ __constant__ CellTaps c_ctaps = make_cell_taps();
 #ifndef MC_WG
 #define MC_WG 64
 #endif
-#ifndef MC_P0_LDS
-#define MC_P0_LDS 0
-#endif
 #ifndef MC_WAVES_PER_EU
 #define MC_WAVES_PER_EU 4
 #endif
 #ifndef MC_XCD_RUN
 #define MC_XCD_RUN 32
 #endif
+static_assert(MC_WG == 64, "k_mc: one wave per workgroup (wave64)");
 #ifndef MC_RESI_AHEAD
 #define MC_RESI_AHEAD 0   // 0 / 2 / 4 measured within 1 % (fused 4K B pictures); 0 holds the fewest registers
 #endif
@@ -356,16 +354,16 @@ struct CellWin {
   DPlane R;
   int ox, oy, fx, fy;
 };
-__device__ __forceinline__ CellWin cell_win(const McParams &P, const McJob &J, int comp, int l, int x, int y) {
+__device__ __forceinline__ CellWin cell_win(const RefPlanes &ref, const McJob &J, int comp, int l, int x, int y) {
   CellWin W;
   const int cs = comp ? 1 : 0, fb = 4 + cs, half = comp ? 1 : 3;
   const int slot = l ? J.slot[1] : J.slot[0];
   // comp is a per-lane value in the chroma cells: the plane geometry by selects between static fields
   // (Cb and Cr share it), never a lane-indexed read of the kernel argument
-  W.R.p = const_cast<int16_t *>(P.ref.p[slot * 3 + comp]);
-  W.R.stride = comp ? P.ref.stride[1] : P.ref.stride[0];
-  W.R.w = comp ? P.ref.w[1] : P.ref.w[0];
-  W.R.h = comp ? P.ref.h[1] : P.ref.h[0];
+  W.R.p = const_cast<int16_t *>(ref.p[slot * 3 + comp]);
+  W.R.stride = comp ? ref.stride[1] : ref.stride[0];
+  W.R.w = comp ? ref.w[1] : ref.w[0];
+  W.R.h = comp ? ref.h[1] : ref.h[0];
   const int mvx = l ? J.mv[1][0] : J.mv[0][0], mvy = l ? J.mv[1][1] : J.mv[0][1], mask = (1 << fb) - 1;
   W.fx = mvx & mask;
   W.fy = mvy & mask;
@@ -376,12 +374,12 @@ __device__ __forceinline__ CellWin cell_win(const McParams &P, const McJob &J, i
 
 // One cell: every list of the job, combined (AreaBuf::addAvg / addWeightedAvg, WP, GEO blend, or the uni
 // rounding), stored as rows of up to 4 samples. (x, y): the cell origin in the component plane; nc / nr:
-// the valid columns / rows of the cell (blocks narrower or shorter than a cell).
+// the valid columns / rows of the cell (blocks narrower or shorter than a cell). Q: the job's picture.
 template <int N, int R, bool EDGE>
-__device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, const McJob &J, int comp, int x, int y, int nc, int nr,
-                                        int half, uint2 (*sp0)[64]) {
+__device__ __forceinline__ void mc_cell(const McBatch &B, const McPic &Q, const WpTable &WT, const McJob &J, int comp, int x, int y,
+                                        int nc, int nr) {
   const bool l0 = J.flags & MC_L0, l1 = J.flags & MC_L1, bi = l0 && l1;
-  const int bd = P.bd, maxv = (1 << bd) - 1, headRoom = max(2, IF_INTERNAL_PREC - bd);
+  const int bd = B.bd, maxv = (1 << bd) - 1, headRoom = max(2, IF_INTERNAL_PREC - bd);
   const int sh1 = IF_FILTER_PREC - headRoom;
   const bool rnd = !bi && !(J.flags & MC_KEEP14) && !(J.flags & MC_WP);
   // V pass: (sum - 64 * IF_INTERNAL_OFFS + off2) >> sh2 with the reference's off2 / sh2 (the H offset folded in)
@@ -391,11 +389,11 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
   // destination: the prediction planes, or with MC_RECON the picture itself (the reconstruction
   // clip(pred + resi) of AreaBuf::reconstruct, Buffer.cpp:590, fused: no prediction plane round trip)
   const bool recon = (J.flags & MC_RECON) != 0, addResi = (J.flags & (MC_RESI << comp)) != 0;
-  const DPlane &O0 = recon ? P.reco[0] : P.out[0], &O1 = recon ? P.reco[1] : P.out[1], &O2 = recon ? P.reco[2] : P.out[2];
+  const DPlane &O0 = recon ? Q.reco[0] : Q.out[0], &O1 = recon ? Q.reco[1] : Q.out[1], &O2 = recon ? Q.reco[2] : Q.out[2];
   const int ostride = comp ? O1.stride : O0.stride;
   int16_t *dst = (comp == 0 ? O0.p : comp == 1 ? O1.p : O2.p) + (size_t)y * ostride + x;
-  const int rstride = comp ? P.resi[1].stride : P.resi[0].stride;
-  const int16_t *rsrc = (comp == 0 ? P.resi[0].p : comp == 1 ? P.resi[1].p : P.resi[2].p) + (size_t)y * rstride + x;
+  const int rstride = comp ? Q.resi[1].stride : Q.resi[0].stride;
+  const int16_t *rsrc = (comp == 0 ? Q.resi[0].p : comp == 1 ? Q.resi[1].p : Q.resi[2].p) + (size_t)y * rstride + x;
   const int cx = x - (comp ? J.x >> 1 : J.x), cy = y - (comp ? J.y >> 1 : J.y);   // cell origin in the block
   const bool wide = nc == 4 && (x & 3) == 0;
   // one output row of 4 samples: 8-byte store, or 2-sample aligned pieces (chroma of blocks at odd
@@ -430,107 +428,33 @@ __device__ __forceinline__ void mc_cell(const McParams &P, const WpTable &WT, co
   };
   // bi: list 0 first, its rows kept as packed 14-bit pairs; then the last list (list 1, or the only list of
   // a uni job) through ONE filter body whose emit combines: uni and bi share it (separate bodies per case
-  // tripled k_mc's code, and its instruction footprint, not its VALU count, stretched the waves, r04)
+  // tripled k_mc's code, and its instruction footprint, not its VALU count, stretched the waves, r04).
+  // (r05: list 0's rows in LDS instead of registers, bi cells split over two lanes, 4- and 16-row luma cells:
+  // each measured slower, profiles/r05_mc_*; removed.)
   const bool avg = bi && !(J.flags & (MC_WP | MC_GEO)) && J.bcw == 2;
-#if MC_P0_LDS
-  // list 0's rows wait in LDS (8 B per row and lane, conflict-free), not in 2 R registers: the VGPR budget
-  // sets the waves resident per SIMD, and the launch is latency x occupancy bound
-  __shared__ uint2 s_p0[MC_WG / 64][8][64];
-  uint2 (*p0s)[64] = s_p0[threadIdx.x >> 6];
-  const int pl = threadIdx.x & 63;
-#define P0_LO(o) p0s[o][pl].x
-#define P0_HI(o) p0s[o][pl].y
-#else
   uint32_t p0[R][2];
-#define P0_LO(o) p0[o][0]
-#define P0_HI(o) p0[o][1]
-#endif
-#if MC_BI_SPLIT
   if (bi) {
-    // The cell's two lists on two adjacent lanes (half = this lane's list): each lane filters its list's R
-    // rows, the pair swaps half of them (DPP quad_perm [1,0,3,2]), and each lane combines and stores R / 2
-    // rows: the dependent chain of one list per lane instead of two (the QP32 launches are one round of
-    // waves whose bi-predicted ones set the length, r05 per-wave trace).
-    const int o0 = half * (R / 2);   // this lane's output rows [o0, o0 + R / 2)
-    const int ln = threadIdx.x & 63;
-    const CellWin W0 = cell_win(P, J, comp, half, x, y);
-    // the rows wait in LDS (8 B per row and lane): in registers they pushed the kernel to 154 VGPRs
+    const CellWin W0 = cell_win(B.ref, J, comp, 0, x, y);
     cell_filter<N, R, EDGE>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
-      sp0[o][ln] = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
-    }, [](int) {});
-    // (the partner lane's rows: the LDS runs one wave's instructions in order; the clobber keeps the
-    // compiler from moving the reads above the writes)
-    asm volatile("" ::: "memory");
-    // its residual rows, all in flight at once (during the filter they would cost registers: spills)
-    uint32_t rk[R / 2][2];
-    if (addResi) {
-#pragma unroll
-      for (int k = 0; k < R / 2; k++) {
-        const int16_t *rr = rsrc + (size_t)min(o0 + k, nr - 1) * rstride;
-        rk[k][1] = 0;
-        if (wide) { const uint2 v = *(const uint2 *)rr; rk[k][0] = v.x; rk[k][1] = v.y; }
-        else { rk[k][0] = ((const uint32_t *)rr)[0]; if (nc == 4) rk[k][1] = ((const uint32_t *)rr)[1]; }
-      }
-    }
-    const Comb CB = comb_setup(WT, J, comp, bd, cx, cy);
-#pragma unroll
-    for (int k = 0; k < R / 2; k++) {
-      const int o = o0 + k;
-      const uint2 l0 = sp0[o][ln & ~1], l1 = sp0[o][ln | 1];   // list 0 (half 0's lane), list 1
-      const uint32_t a0 = l0.x, a1 = l0.y, b0 = l1.x, b1 = l1.y;
-      if (o >= nr) continue;
-      const int u[4] = {lo16(a0), hi16(a0), lo16(a1), hi16(a1)}, v[4] = {lo16(b0), hi16(b0), lo16(b1), hi16(b1)};
-      int a[4];
-      if (avg) {   // AreaBuf::addAvg (Buffer.cpp:447)
-        const int shiftNum = headRoom + 1, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
-#pragma unroll
-        for (int q = 0; q < 4; q++) a[q] = clampi((u[q] + v[q] + offset) >> shiftNum, 0, maxv);
-      } else {     // bi WP / GEO / BCW
-#pragma unroll
-        for (int q = 0; q < 4; q++) a[q] = comb_apply(CB, q, o, u[q], v[q], maxv);
-      }
-      int16_t *qd = dst + (size_t)o * ostride;
-      if (addResi) {
-        a[0] = clampi(a[0] + lo16(rk[k][0]), 0, maxv); a[1] = clampi(a[1] + hi16(rk[k][0]), 0, maxv);
-        a[2] = clampi(a[2] + lo16(rk[k][1]), 0, maxv); a[3] = clampi(a[3] + hi16(rk[k][1]), 0, maxv);
-      }
-      if (wide) *(uint2 *)qd = make_uint2(pk(a[0], a[1]), pk(a[2], a[3]));
-      else {
-        ((uint32_t *)qd)[0] = pk(a[0], a[1]);
-        if (nc == 4) ((uint32_t *)qd)[1] = pk(a[2], a[3]);
-      }
-    }
-    return;
-  }
-#else
-  (void)half;
-#endif
-  if (bi) {
-    const CellWin W0 = cell_win(P, J, comp, 0, x, y);
-    cell_filter<N, R, EDGE>(W0.R, W0.ox, W0.oy, W0.fx, W0.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
-#if MC_P0_LDS
-      p0s[o][pl] = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
-#else
       p0[o][0] = pk(v[0], v[1]);
       p0[o][1] = pk(v[2], v[3]);
-#endif
     }, [](int) {});
   }
   const Comb CB = comb_setup(WT, J, comp, bd, cx, cy);
-  const CellWin W = cell_win(P, J, comp, (bi || !l0) ? 1 : 0, x, y);
+  const CellWin W = cell_win(B.ref, J, comp, (bi || !l0) ? 1 : 0, x, y);
   cell_filter<N, R, EDGE>(W.R, W.ox, W.oy, W.fx, W.fy, ts, sh1, off2, sh2, [&](int o, const int (&v)[4]) {
     int a[4];
     if (rnd) {
 #pragma unroll
       for (int q = 0; q < 4; q++) a[q] = clampi(v[q], 0, maxv);
     } else if (avg) {   // AreaBuf::addAvg (Buffer.cpp:447)
-      const uint32_t q0 = P0_LO(o), q1 = P0_HI(o);
+      const uint32_t q0 = p0[o][0], q1 = p0[o][1];
       const int u[4] = {lo16(q0), hi16(q0), lo16(q1), hi16(q1)};
       const int shiftNum = headRoom + 1, offset = (1 << (shiftNum - 1)) + 2 * IF_INTERNAL_OFFS;
 #pragma unroll
       for (int q = 0; q < 4; q++) a[q] = clampi((u[q] + v[q] + offset) >> shiftNum, 0, maxv);
     } else {   // uni WP, bi WP / GEO / BCW
-      const uint32_t q0 = bi ? P0_LO(o) : 0u, q1 = bi ? P0_HI(o) : 0u;
+      const uint32_t q0 = bi ? p0[o][0] : 0u, q1 = bi ? p0[o][1] : 0u;
       const int u[4] = {bi ? lo16(q0) : v[0], bi ? hi16(q0) : v[1], bi ? lo16(q1) : v[2], bi ? hi16(q1) : v[3]};
 #pragma unroll
       for (int q = 0; q < 4; q++) a[q] = comb_apply(CB, q, o, u[q], v[q], maxv);
@@ -549,38 +473,47 @@ __device__ __forceinline__ McJob load_job(const McJob *p) {
   return J;
 }
 
-// Grid: the luma cells of every class (ct.lcell0[ct.n] lanes), then the chroma cells, MC_WG lanes per
-// workgroup; the class of a lane is wave-uniform (class ranges are whole waves).
-__device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restrict__ jobs, const McClassTable &ct, uint2 (*sp0)[64], int b
+// Grid (frame-batched: the plain MC of B.npic pictures in one launch): the luma blocks of picture 0, of
+// picture 1, ..., then the chroma blocks likewise (the longer luma waves first); within a picture, the cells
+// of its classes as in its class table, MC_WG lanes per workgroup. The picture and the class of a wave are
+// wave-uniform (a picture's class ranges are whole waves).
+__device__ __forceinline__ void mc_body(const McBatch &B, int b
 #ifdef VVCR_MC_PROF
                                         , unsigned long long &tag
 #endif
 ) {
-  const int nL = ct.lcell0[ct.n], nbL = (nL + MC_WG - 1) / MC_WG;
+  const int nbL = B.lblk0[B.npic];
   const bool luma = b < nbL;
-  const int g = (luma ? b : b - nbL) * MC_WG + (int)threadIdx.x;
+  const int bb = luma ? b : b - nbL;
+  // the block's picture by a scan over static fields (uniform compares, no indexed kernel-argument read)
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < MC_MAXPIC; q++)
+    if (q < B.npic && bb >= (luma ? B.lblk0[q] : B.cblk0[q])) p = q;
+  p = __builtin_amdgcn_readfirstlane(p);
+  static_assert(MC_MAXPIC == 2, "k_mc: the picture select below");
+  const McPic &Q = p ? B.pic[1] : B.pic[0];
+  const McClassTable &ct = Q.ct;
+  const int g = (bb - (luma ? B.lblk0[p] : B.cblk0[p])) * MC_WG + (int)threadIdx.x;
   const int gw = __builtin_amdgcn_readfirstlane(g & ~63);   // the wave's first cell: selects the class
   // the class of the wave by a scan over static fields (wave-uniform selects; a class index used to read
   // the kernel argument would make it a per-lane indexed copy)
   int w = ct.w[0], h = ct.h[0], c0 = luma ? ct.lcell0[0] : ct.ccell0[0], jbase = ct.job0[0], jend = ct.job0[1], ed = ct.edge[0];
-  int sp = ct.split[0];
 #pragma unroll
   for (int q = 1; q < MC_MAXCLS; q++)
     if (q < ct.n && gw >= (luma ? ct.lcell0[q] : ct.ccell0[q])) {
       w = ct.w[q]; h = ct.h[q]; c0 = luma ? ct.lcell0[q] : ct.ccell0[q]; jbase = ct.job0[q]; jend = ct.job0[q + 1]; ed = ct.edge[q];
-      sp = ct.split[q];
     }
   const int i = g - c0;
-  const int per = (luma ? mc_luma_cells(w, h, ed) : mc_chroma_cells(w, h)) << sp;   // a power of two
-  const int jn = i >> (__ffs(per) - 1), s2 = i & (per - 1);
-  const int s = s2 >> sp, half = s2 & sp;   // split classes: adjacent lanes share a cell, one list each
+  const int per = luma ? mc_luma_cells(w, h) : mc_chroma_cells(w, h);   // a power of two
+  const int jn = i >> (__ffs(per) - 1), s = i & (per - 1);
 #ifdef VVCR_MC_PROF
-  tag = (unsigned long long)luma << 63 | (unsigned long long)(w & 255) << 8 | (h & 255);
+  tag = (unsigned long long)luma << 63 | (unsigned long long)(w & 255) << 8 | (h & 255) | (unsigned long long)p << 48;
 #endif
   if (jn >= jend - jbase) return;   // padding of the class's cell range (whole waves)
-  const McJob J = load_job(jobs + jbase + jn);
+  const McJob J = load_job(Q.jobs + jbase + jn);
 #ifdef MC_ABL_EXIT   // diagnostics ablation: the job record only (results wrong)
-  if (J.flags == 0xffff) P.out[0].p[jn] = 1;
+  if (J.flags == 0xffff) Q.out[0].p[jn] = 1;
   return;
 #endif
 #ifdef VVCR_MC_PROF
@@ -589,17 +522,12 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
          (unsigned long long)__builtin_popcountll(__ballot(J.flags & (MC_WP | MC_GEO))) << 32 |
          (unsigned long long)__builtin_popcountll(__ballot(1)) << 40;
 #endif
-  const WpTable &WT = *P.wpd;
+  const WpTable &WT = *Q.wpd;
   // the path is a class property (wave-uniform): edge classes take the clamped gathers, the others none
   if (luma) {
     const int ncx = w >> 2, cx = s & (ncx - 1), cy = s >> (__ffs(ncx) - 1);
-    if (ed) mc_cell<8, 8, true>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy), half, sp0);
-#if MC_SHORT_LUMA
-    else if (mc_short_luma(false)) mc_cell<8, 4, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 4 * cy, 4, min(4, h - 4 * cy), half, sp0);
-#elif MC_TALL_LUMA
-    else if (mc_tall_luma(h, false)) mc_cell<8, 16, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 16 * cy, 4, 16, half, sp0);
-#endif
-    else mc_cell<8, 8, false>(P, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy), half, sp0);
+    if (ed) mc_cell<8, 8, true>(B, Q, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
+    else mc_cell<8, 8, false>(B, Q, WT, J, 0, J.x + 4 * cx, J.y + 8 * cy, 4, min(8, h - 8 * cy));
   } else {
     const int cw = w >> 1, chh = h >> 1;
     const bool tall = mc_tall_chroma(h);   // class-uniform: 8-row chroma cells (mc_chroma_cells)
@@ -608,27 +536,23 @@ __device__ __forceinline__ void mc_body(const McParams &P, const McJob *__restri
     const int cx = t & (ncx - 1), cy = t >> (__ffs(ncx) - 1);   // ncx is a power of two
     const int ox = (J.x >> 1) + 4 * cx, nc = min(4, cw - 4 * cx);
     if (ed) {
-      if (tall) mc_cell<4, 8, true>(P, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8, half, sp0);
-      else mc_cell<4, 4, true>(P, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy), half, sp0);
+      if (tall) mc_cell<4, 8, true>(B, Q, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8);
+      else mc_cell<4, 4, true>(B, Q, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy));
     } else {
-      if (tall) mc_cell<4, 8, false>(P, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8, half, sp0);
-      else mc_cell<4, 4, false>(P, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy), half, sp0);
+      if (tall) mc_cell<4, 8, false>(B, Q, WT, J, comp, ox, (J.y >> 1) + 8 * cy, nc, 8);
+      else mc_cell<4, 4, false>(B, Q, WT, J, comp, ox, (J.y >> 1) + 4 * cy, nc, min(4, chh - 4 * cy));
     }
   }
 }
-__global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_PER_EU))) void k_mc(McParams P, const McJob *__restrict__ jobs, McClassTable ct) {
-  // split bi cells: the rows of one list per lane, 8 B per row (MC_WG is one wave)
-  __shared__ uint2 s_rows[8][64];
+__global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_PER_EU))) void k_mc(McBatch B) {
 #ifdef VVCR_MC_PROF
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   const unsigned hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_ID
   const unsigned xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));   // XCC_ID
-#endif
-#ifdef VVCR_MC_PROF
   unsigned long long tag = 0;
-#define MC_BODY(b) mc_body(P, jobs, ct, s_rows, b, tag)
+#define MC_BODY(b) mc_body(B, b, tag)
 #else
-#define MC_BODY(b) mc_body(P, jobs, ct, s_rows, b)
+#define MC_BODY(b) mc_body(B, b)
 #endif
   // (A persistent grid walking the blocks was slower, 47.3 vs 41.4 us, and doubled the kernel's code:
   // removed, r04.)
@@ -636,10 +560,8 @@ __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_
   // XCD-contiguous runs (r03, xcd_swizzle) cluster heavy regions on a few XCDs (4K B pictures, fused: QP27
   // 34.6 us, 67 MB read); dispatch order spreads the work but fetches every shared reference window into
   // several L2s (35.2 us, 151 MB); runs of 32: 30.0 us, 78 MB (runs of 4 / 8 / 16 / 64 / 128: 32.5 / 31.0
-  // / 30.3 / 30.7 / 30.8 us; r04, tools/gpu_r04x.sh)
-#if defined(MC_XCD_SWIZZLE)
-  MC_BODY(xcd_swizzle(blockIdx.x, gridDim.x));
-#elif MC_XCD_RUN > 0
+  // / 30.3 / 30.7 / 30.8 us; r04)
+#if MC_XCD_RUN > 0
   MC_BODY(xcd_run_swizzle((int)blockIdx.x, (int)gridDim.x, MC_XCD_RUN));
 #else
   MC_BODY((int)blockIdx.x);
@@ -656,8 +578,17 @@ __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_
 
 }  // namespace
 
-void launch_mc(const McParams &p, const McJob *jobs, const McClassTable &ct, hipStream_t s) {
-  if (ct.n <= 0) return;
-  const int V = (ct.lcell0[ct.n] + MC_WG - 1) / MC_WG + (ct.ccell0[ct.n] + MC_WG - 1) / MC_WG;
-  if (V > 0) hipLaunchKernelGGL(k_mc, dim3(V), dim3(MC_WG), 0, s, p, jobs, ct);
+void launch_mc_batch(McBatch &b, hipStream_t s) {
+  int lb = 0, cb = 0;
+  for (int p = 0; p < b.npic; p++) {
+    const McClassTable &ct = b.pic[p].ct;
+    b.lblk0[p] = lb;
+    b.cblk0[p] = cb;
+    if (ct.n > 0) {
+      lb += (ct.lcell0[ct.n] + MC_WG - 1) / MC_WG;
+      cb += (ct.ccell0[ct.n] + MC_WG - 1) / MC_WG;
+    }
+  }
+  for (int p = b.npic; p <= MC_MAXPIC; p++) { b.lblk0[p] = lb; b.cblk0[p] = cb; }
+  if (lb + cb > 0) hipLaunchKernelGGL(k_mc, dim3(lb + cb), dim3(MC_WG), 0, s, b);
 }

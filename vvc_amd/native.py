@@ -93,6 +93,7 @@ def lib():
         L.vvcr_prepare_picture.argtypes = [P, C.c_uint32, C.POINTER(I32)]
         L.vvcr_launch_picture.argtypes = [P, I32]
         L.vvcr_launch_picture_stages.argtypes = [P, I32, C.c_uint32]
+        L.vvcr_launch_pictures.argtypes = [P, C.POINTER(I32), I32]
         L.vvcr_release_picture.argtypes = [P, I32]
         L.vvcr_kernel_stats.argtypes = [P, I32, C.POINTER(KernelStat), I32]
         L.vvcr_stream.argtypes = [P]
@@ -126,10 +127,11 @@ def lib():
 
 
 class KernelStat(C.Structure):
-    _fields_ = [("name", C.c_char * 16), ("launches", C.c_int32), ("ms", C.c_float), ("alg_bytes", C.c_double)]
+    _fields_ = [("name", C.c_char * 16), ("launches", C.c_int32), ("ms", C.c_float), ("alg_bytes", C.c_double),
+                ("pictures", C.c_int32), ("pad", C.c_int32)]
 
 
-EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_launch_picture_stages", "vvcr_release_picture", "vvcr_kernel_stats", "vvcr_create", "vvcr_destroy", "vvcr_last_error", "vvcr_begin_picture", "vvcr_submit",
+EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_launch_picture_stages", "vvcr_launch_pictures", "vvcr_release_picture", "vvcr_kernel_stats", "vvcr_create", "vvcr_destroy", "vvcr_last_error", "vvcr_begin_picture", "vvcr_submit",
            "vvcr_set_loop_filter_params", "vvcr_end_picture", "vvcr_end_picture_stages", "vvcr_sync",
            "vvcr_read_plane", "vvcr_write_plane", "vvcr_read_picture", "vvcr_get_dmvr_deltas", "vvcr_picture_dmvr_deltas",
            "vvcr_last_stage_times", "vvcr_stream", "vvcr_rd_plan", "vvcr_rd_run", "vvcr_fwd_plan", "vvcr_fwd_run",
@@ -309,6 +311,11 @@ class Context:
     def launch(self, handle):
         self._chk(self.L.vvcr_launch_picture(self.h, handle), "vvcr_launch_picture")
 
+    def launch_batch(self, handles):
+        """frame-batched launch of independent inter pictures (vvcr_launch_pictures): one plain-MC launch"""
+        arr = (C.c_int32 * len(handles))(*handles)
+        self._chk(self.L.vvcr_launch_pictures(self.h, arr, len(handles)), "vvcr_launch_pictures")
+
     def launch_stages(self, handle, stages):
         """the stages of `stages` the picture was prepared with (vvcr_launch_picture_stages)"""
         self._chk(self.L.vvcr_launch_picture_stages(self.h, handle, stages), "vvcr_launch_picture_stages")
@@ -362,12 +369,13 @@ class Context:
         self._chk(self.L.vvcr_rdo_release(self.h, plan), "vvcr_rdo_release")
 
     def kernel_stats(self, handle=0):
-        """[(name, launches, ms, alg_bytes)] of the last launch of a prepared picture (0 = last launched)."""
+        """[(name, launches, ms, alg_bytes, pictures)] of the last launch of a prepared picture (0 = last launched);
+        pictures: the pictures the group's launches carried (a frame-batched k_mc: 2 on the first, 0 on the other)."""
         arr = (KernelStat * 16)()
         n = self.L.vvcr_kernel_stats(self.h, handle, arr, 16)
         if n < 0:
             self._chk(n, "vvcr_kernel_stats")
-        return [(arr[i].name.decode(), arr[i].launches, arr[i].ms, arr[i].alg_bytes) for i in range(n)]
+        return [(arr[i].name.decode(), arr[i].launches, arr[i].ms, arr[i].alg_bytes, arr[i].pictures) for i in range(n)]
 
     def dmvr_deltas(self):
         """DMVR refinement deltas of the last picture, [n][2] (vvcr_get_dmvr_deltas)."""
