@@ -119,9 +119,9 @@ int vvcp_decode_plan(const vvcp_stream *s, int32_t slot_base, int32_t num_slots,
  * order, every picture launched after its derivation, every picture assumed to have DMVR sub-blocks):
  * the largest number of handles alive at once when `keep` are kept beyond the policy. Host only. */
 int vvcp_decode_live_bound(const vvcp_stream *s, int32_t slot_base, int32_t num_slots, int32_t keep);
-/* The frame batching vvcp_decode applies (vvcr_launch_pictures; VVCP_MC_BATCH=0 turns it off): first[i]
- * = 2 for the first picture of a pair launched together, 0 for its partner, 1 for a picture launched
- * alone (first may be NULL). Returns the number of pairs. Host only. */
+/* The frame batching vvcp_decode applies (vvcr_launch_pictures; VVCP_MC_BATCH=k caps a group at k pictures,
+ * 1 turns it off): first[i] = k for the first picture of a group of k launched together, 0 for a later
+ * member, 1 for a picture launched alone (first may be NULL). Returns the number of groups of > 1. Host only. */
 int vvcp_decode_batches(const vvcp_stream *s, int32_t slot_base, int32_t num_slots, int32_t *first);
 
 /* Parsed rows of a picture (after vvcp_parse_picture): copies min(cap, count) entries to dst (dst may be

@@ -211,9 +211,9 @@ int vvcr_launch_picture(vvcr_ctx *ctx, int32_t handle);
  * stages and, after a halo exchange, the loop-filter stages of one prepared spatial shard (each launch
  * orders itself after the slot's earlier writer like any other). */
 int vvcr_launch_picture_stages(vvcr_ctx *ctx, int32_t handle, uint32_t stage_mask);
-/* Frame-batched launch of n (1..2) prepared inter pictures that do not reference each other and write
+/* Frame-batched launch of n (1..4) prepared inter pictures that do not reference each other and write
  * different slots (e.g. the adjacent top-temporal-layer pictures POC 1 / 3 of a GOP-16 hierarchy, which
- * DecApp decodes one after the other): one execution lane runs their residuals, ONE plain-MC launch for
+ * DecApp decodes one after the other, with POC 6): one execution lane runs their residuals, ONE plain-MC launch for
  * all of them (a single 4K picture's k_mc is one partial round of waves), then each picture's remaining
  * stages. Equivalent to launching them one by one (VVCR_E_ARG when a picture references another of the
  * batch, shares its slot, or was prepared without every stage). vvcr_kernel_stat.pictures of the plain-MC

@@ -1,12 +1,12 @@
 """Frame-batched plain MC (vvcr_launch_pictures): the decode loop launches adjacent
 independent inter pictures of decoding order together, so ONE k_mc launch carries both pictures' plain MC.
 
-CPU: the pairing rule (vvcp_decode_batches) on the committed streams: a pair's second picture never
-references the first (so its derivation never waits for the first's DMVR deltas), both are inter pictures
-of one coded video sequence, and the GOP-16 hierarchy pairs its top-layer pictures POC 1/3, 5/7, 9/11, 13/15.
-GPU: resident pictures replayed in their launch groups stay MD5-exact; the batched record reports both
-pictures (pictures = 2) and its partner none; a batch whose pictures depend on each other is refused
-without touching the device (VVCR_E_ARG)."""
+CPU: the grouping rule (vvcp_decode_batches) on the committed streams: no member of a group references an
+earlier one (so its derivation never waits for the group's DMVR deltas), all are inter pictures of one
+coded video sequence in slots of their own, and the GOP-16 hierarchy groups POC 1/3/6, 5/7/12, 9/11/14, 13/15.
+GPU: resident pictures replayed in their launch groups stay MD5-exact; the batched record reports every
+picture of its group (pictures = k) and the others none; a batch whose pictures depend on each other is
+refused without touching the device (VVCR_E_ARG)."""
 import os
 
 import pytest
@@ -39,19 +39,23 @@ def _batches(name, nslots=16):
 @pytest.mark.parametrize("name", ["ra416_q32", "ra1080l_q32", "ra2160l_q32", "ralm416_q32", "ai416_q37", "ra4320t_q32"])
 def test_pairs_are_independent_inter_pictures(name):
     pairs, first, plan = _batches(name)
-    assert pairs == sum(1 for f in first if f == 2)
+    assert pairs == sum(1 for f in first if f > 1)
     pocs = [inf["poc"] for inf in plan.info]
-    for i, f in enumerate(first):
-        if f == 2:
-            j = i + 1
+    i = 0
+    while i < len(first):
+        k = first[i]
+        assert 1 <= k <= 4
+        g = list(range(i, i + k))
+        for j in g[1:]:
             assert first[j] == 0
-            assert plan.cvs[i] == plan.cvs[j]
-            assert plan.info[i]["slice_type"] != 2 and plan.info[j]["slice_type"] != 2, "intra picture in a batch"
-            assert pocs[i] not in plan.refs[j][0] + plan.refs[j][1], "partner references the first picture"
-        elif f == 0:
-            assert i > 0 and first[i - 1] == 2
-        else:
-            assert f == 1
+            assert plan.cvs[j] == plan.cvs[i]
+            assert plan.slot[j] not in [plan.slot[m] for m in g if m < j], "two members share a slot"
+            for m in g:
+                if m < j:
+                    assert pocs[m] not in plan.refs[j][0] + plan.refs[j][1], "a member references an earlier one"
+        if k > 1:
+            assert all(plan.info[m]["slice_type"] != 2 for m in g), "intra picture in a batch"
+        i += k
     if name.startswith("ai"):
         assert pairs == 0
 
@@ -59,8 +63,8 @@ def test_pairs_are_independent_inter_pictures(name):
 def test_gop16_top_layer_pairs():
     pairs, first, plan = _batches("ra2160l_q32")
     pocs = [inf["poc"] for inf in plan.info]
-    got = [(pocs[i], pocs[i + 1]) for i, f in enumerate(first) if f == 2]
-    assert got == [(1, 3), (5, 7), (9, 11), (13, 15)], got
+    got = [tuple(pocs[i:i + f]) for i, f in enumerate(first) if f > 1]
+    assert got == [(1, 3, 6), (5, 7, 12), (9, 11, 14), (13, 15)], got
 
 
 @pytest.mark.gpu
@@ -77,7 +81,7 @@ def test_batched_groups_replayed_stay_bitexact(name, golden_dir):
         _, handles = seq.run(keep_handles=True)
         ctx.sync()
         groups = B.launch_groups(handles, seq.batch)
-        assert any(len(g) == 2 for g in groups), "no frame-batched pair on %s" % name
+        assert any(len(g) > 1 for g in groups), "no frame-batched group on %s" % name
         owner = {seq.slot[i]: seq.info[i]["poc"] for i in range(len(handles))}
         for rnd in range(2):   # replayed twice: the second round overwrites every slot again
             for g in groups:
@@ -87,10 +91,10 @@ def test_batched_groups_replayed_stay_bitexact(name, golden_dir):
                 assert D.plane_md5s([ctx.read_plane(N.BUF_RECO, slot, c) for c in range(3)]) == meta["poc_plane_md5"][str(poc)], \
                     "POC %d after replay %d" % (poc, rnd)
         for g in groups:
-            if len(g) == 2:
-                a, b = (dict((st[0], st) for st in ctx.kernel_stats(h)) for h in g)
-                assert a["mc"][4] == 2 and b["mc"][4] == 0, (a["mc"], b["mc"])
-                assert b["mc"][1] == 0 and a["mc"][1] <= 1
+            if len(g) > 1:
+                st = [dict((x[0], x) for x in ctx.kernel_stats(h)) for h in g]
+                assert st[0]["mc"][4] == len(g) and st[0]["mc"][1] <= 1, st[0]["mc"]
+                assert all(x["mc"][4] == 0 and x["mc"][1] == 0 for x in st[1:]), [x["mc"] for x in st]
         for h in handles:
             ctx.release(h)
     finally:

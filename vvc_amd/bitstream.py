@@ -134,7 +134,7 @@ class SequenceDecode:
         first = (C.c_int32 * max(n, 1))()
         if self.L.vvcp_decode_batches(self.s.h, base, nslots, first) < 0:
             raise P.ParseError("decode batches: %s" % self.L.vvcp_last_error().decode())
-        self.batch = list(first)[:n]   # frame batching of vvcp_decode: 2 first of a pair, 0 its partner, 1 alone
+        self.batch = list(first)[:n]   # frame batching of vvcp_decode: k first of a group of k, 0 a later member
         self.info = [self.s.info(i) for i in range(n)]
         # seconds per phase (include/vvcp.h VVCP_PHASE_*): parse summed over the parser threads
         self.times = dict.fromkeys(PHASES, 0.0)
@@ -168,11 +168,11 @@ class SequenceDecode:
 
 
 def launch_groups(handles, batch):
-    """The prepared handles of one decode (decoding order) grouped as vvcp_decode launches them: pairs of
+    """The prepared handles of one decode (decoding order) grouped as vvcp_decode launches them: groups of
     frame-batched pictures (SequenceDecode.batch) and single pictures."""
     out, i = [], 0
     while i < len(handles):
-        k = 2 if batch[i] == 2 and i + 1 < len(handles) else 1
+        k = max(1, min(batch[i], len(handles) - i))
         out.append(handles[i:i + k])
         i += k
     return out

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <ctime>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -31,7 +32,7 @@ struct DecodePlan {
   std::vector<std::vector<int>> refIdx[2];   // decode index of every reference
   std::vector<int> cvs, slot, lastUse, lastRef, outOrder, outReady;   // lastRef: last picture referencing it (-1: none)
   std::vector<char> referenced, output;
-  std::vector<int> batch;   // frame batching: 2 = the first of a pair launched together, 0 = its partner, 1 = alone
+  std::vector<int> batch;   // frame batching: k = the first of a group of k launched together, 0 = a later member
 
   int find(int j, int p) const {
     for (int i = j - 1; i >= 0; i--)
@@ -76,25 +77,6 @@ struct DecodePlan {
           lastRef[src] = std::max(lastRef[src], j);
           referenced[src] = 1;
         }
-    // Frame-batched plain MC (vvcr_launch_pictures): adjacent pictures of decoding order that are both inter
-    // pictures of one coded video sequence and do not reference each other (the top temporal layer's
-    // POC 1 / 3, 5 / 7, 9 / 11, 13 / 15 of a GOP-16 hierarchy) launch together. The second never needs the
-    // first's DMVR deltas (it does not reference it, so it is not its collocated picture), so its derivation
-    // does not wait for the first's launch. VVCP_MC_BATCH=0: every picture alone.
-    batch.assign(n, 1);
-    static const bool batching = [] { const char *e = getenv("VVCP_MC_BATCH"); return !(e && e[0] == '0'); }();
-    for (int i = 0; batching && i + 1 < n; i++) {
-      const int j = i + 1;
-      const bool inter = !refIdx[0][i].empty() && !refIdx[0][j].empty();
-      bool indep = cvs[i] == cvs[j];
-      for (int l = 0; l < 2; l++)
-        for (int src : refIdx[l][j]) indep = indep && src != i;
-      if (inter && indep) {
-        batch[i] = 2;
-        batch[j] = 0;
-        i++;
-      }
-    }
     std::vector<int> freeSlots, held;
     for (int k = 0; k < nslots; k++) freeSlots.push_back(base + k);
     slot.resize(n);
@@ -107,6 +89,34 @@ struct DecodePlan {
       slot[i] = freeSlots.front();
       freeSlots.erase(freeSlots.begin());
       held.push_back(i);
+    }
+    // Frame-batched plain MC (vvcr_launch_pictures): runs of adjacent pictures of decoding order that are inter
+    // pictures of one coded video sequence, none referencing another of the run, each in a slot of its own,
+    // launch together (a GOP-16 hierarchy: POC 1 / 3 / 6, 5 / 7 / 12, 9 / 11 / 14, 13 / 15). A later member
+    // never needs an earlier one's DMVR deltas (it does not reference it, so it is not its collocated
+    // picture), so its derivation never waits for the group's launch. VVCP_MC_BATCH=k: groups of at most k
+    // (default 4 = MC_MAXPIC of libvvcr; 0 or 1: every picture alone).
+    batch.assign(n, 1);
+    static const int maxb = [] {
+      const char *e = getenv("VVCP_MC_BATCH");
+      return e ? std::max(1, std::min(4, atoi(e))) : 4;
+    }();
+    for (int i = 0; i < n;) {
+      int k = 1;
+      while (i + k < n && k < maxb) {
+        const int j = i + k;
+        bool ok = !refIdx[0][j].empty() && !refIdx[0][i].empty() && cvs[j] == cvs[i];
+        for (int m = i; m < j && ok; m++) {
+          ok = slot[m] != slot[j];
+          for (int l = 0; l < 2; l++)
+            for (int src : refIdx[l][j]) ok = ok && src != m;
+        }
+        if (!ok) break;
+        k++;
+      }
+      batch[i] = k;
+      for (int m = 1; m < k; m++) batch[i + m] = 0;
+      i += k;
     }
   }
 };
@@ -227,13 +237,15 @@ extern "C" int vvcp_decode(vvcp_stream *h, vvcr_ctx *ctx, const vvcp_decode_para
         std::lock_guard<std::mutex> g(mu);
         if (stop || nextLaunch >= n || !prepared[nextLaunch]) return;
         i = nextLaunch;
-        if (batchOK && P.batch[i] == 2) {   // a frame-batched pair launches when both are prepared
-          if (!prepared[i + 1]) return;
-          nb = 2;
+        if (batchOK && P.batch[i] > 1) {   // a frame-batched group launches when all of it is prepared
+          for (int k = 1; k < P.batch[i]; k++)
+            if (!prepared[i + k]) return;
+          nb = P.batch[i];
         }
       }
       const double t0 = tnow();
-      const int32_t hs[2] = {handle[i], nb > 1 ? handle[i + 1] : -1};
+      int32_t hs[4] = {-1, -1, -1, -1};
+      for (int k = 0; k < nb; k++) hs[k] = handle[i + k];
       const int lrc = nb > 1 ? vvcr_launch_pictures(ctx, hs, nb) : vvcr_launch_picture(ctx, handle[i]);
       const double tl = since(t0);
       if (lrc < 0) {
@@ -440,8 +452,8 @@ extern "C" int vvcp_decode_plan(const vvcp_stream *h, int32_t slot_base, int32_t
 // with each picture launched right after its derivation and the worst case for refinement: every picture
 // has DMVR sub-blocks, so only a collocated read records its refined motion. Returns the largest number of
 // live handles (launched, not released) with `keep` handles kept; a CPU test bounds it.
-// The frame batching vvcp_decode applies (VVCP_MC_BATCH): first[i] = 2 for the first picture of a pair
-// launched together, 0 for its partner, 1 for a picture launched alone. Returns the number of pairs.
+// The frame batching vvcp_decode applies (VVCP_MC_BATCH): first[i] = k for the first picture of a group of k
+// launched together, 0 for a later member, 1 for a picture launched alone. Returns the number of groups of > 1.
 extern "C" int vvcp_decode_batches(const vvcp_stream *h, int32_t slot_base, int32_t num_slots, int32_t *first) {
   if (!h || num_slots <= 0 || slot_base < 0) return VVCR_E_ARG;
   try {
@@ -450,7 +462,7 @@ extern "C" int vvcp_decode_batches(const vvcp_stream *h, int32_t slot_base, int3
     int pairs = 0;
     for (int i = 0; i < P.n; i++) {
       if (first) first[i] = P.batch[i];
-      pairs += P.batch[i] == 2;
+      pairs += P.batch[i] > 1;
     }
     return pairs;
   } catch (const std::exception &e) {

@@ -207,6 +207,7 @@ struct Prepared {
   DevVec<int32_t> dmvr;
   DevVec<WpTable> wpt;               // the slice's weighted-prediction table (k_mc reads it per lane)
   McClassTable mc_ct;                // k_mc cell classes of mc_basic (edge jobs, tiles, blocks)
+  DevVec<McClassTable> mc_ctd;       // the same in device memory (a batched k_mc reads each picture's)
   bool have_sao = false, have_alf = false;
   // exactly one of SAO / ALF and every stage in one prepared picture: the picture is reconstructed and
   // deblocked in the lane's loop-filter planes, and that one filter writes it into its slot (no copy-back)
@@ -516,7 +517,7 @@ static McPic make_mc_pic(vvcr_ctx *ctx, const Prepared &r, int lane, int set) {
   }
   q.wpd = r.wpt.p;
   q.jobs = r.mc_basic.p;
-  q.ct = r.mc_ct;
+  q.ct = r.mc_ctd.p;
   return q;
 }
 
@@ -729,6 +730,7 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
       st.add(r.wpt, &wt, 1);
     }
     r.mc_ct = wl.mc_ct;
+    st.add(r.mc_ctd, &wl.mc_ct, 1);
     st.add(r.aff_pu, wl.aff_pu);
     st.add(r.aff_jobs, wl.aff_jobs);
     r.n_mctile = (int)wl.mc_tile.size();
@@ -1017,8 +1019,10 @@ static void launch_plain_mc(vvcr_ctx *ctx, Prepared *const *rs, int n) {
   b.npic = n;
   double bytes = 0;
   int jobs = 0;
+  const McClassTable *hct[MC_MAXPIC];
   for (int k = 0; k < n; k++) {
     b.pic[k] = make_mc_pic(ctx, *rs[k], rs[k]->lane, rs[k]->set);
+    hct[k] = &rs[k]->mc_ct;
     bytes += rs[k]->alg_bytes[K_MC];
     jobs += rs[k]->n_mctile + rs[k]->n_basic;
     if (k) {
@@ -1029,7 +1033,7 @@ static void launch_plain_mc(vvcr_ctx *ctx, Prepared *const *rs, int n) {
     }
   }
   KernelTimer t(r0, K_MC, s, ctx->timing);
-  launch_mc_batch(b, s);
+  launch_mc_batch(b, hct, s);
   VVCR_CHECK_HIP(hipGetLastError());
   r0.launches[K_MC] = jobs ? 1 : 0;
   r0.mc_pics = n;
@@ -1203,24 +1207,13 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
   launch_rest(ctx, r, mask, refs);
 }
 
-// scratch set k >= 1 of a lane (frame-batched launches), allocated at its first use
-static void ensure_scratch_set(vvcr_ctx *ctx, Lane &ln, int k) {
-  if (ln.set[k].resi[0].p) return;
-  const int W = ctx->sp.width, H = ctx->sp.height;
-  for (int c = 0; c < 3; c++) {
-    const int w = c ? W / 2 : W, h = c ? H / 2 : H;
-    ln.set[k].pred[c] = alloc_plane(w, h);
-    ln.set[k].resi[c] = alloc_plane(w, h);
-    ln.set[k].tmp[c] = alloc_plane(w, h);
-  }
-}
-
 // Frame-batched launch of n independent pictures (every stage; none references another's slot, all write
 // different slots) on one lane: picture k on the lane's scratch set k. Their residuals, then ONE k_mc launch
 // for all of their plain MC, then picture by picture DMVR / BDOF, affine and the remaining stages. Each
 // picture's dependency markers are recorded after its own last stage.
 static void launch_batch(vvcr_ctx *ctx, Prepared *const *rs, int n) {
   if (n < 1 || n > MC_MAXPIC) throw VvcrError(VVCR_E_ARG, "a batched launch takes 1 .. " + std::to_string(MC_MAXPIC) + " pictures");
+  if (ctx->nlane - ctx->nintra < 1) throw VvcrError(VVCR_E_STATE, "no inter lane");
   std::vector<std::vector<int>> refs(n);
   for (int k = 0; k < n; k++) {
     const Prepared &r = *rs[k];
@@ -1240,7 +1233,9 @@ static void launch_batch(vvcr_ctx *ctx, Prepared *const *rs, int n) {
   // were written on other lanes waits for them by events like any picture
   const int L = choose_lane(ctx, *rs[0], refs[0]);
   Lane &ln = ctx->lanes[L];
-  for (int k = 1; k < n; k++) ensure_scratch_set(ctx, ln, k);
+  for (int k = 1; k < n; k++)
+    if (!ln.set[k].resi[0].p || !ln.set[k].pred[0].p || !ln.set[k].tmp[0].p)
+      throw VvcrError(VVCR_E_STATE, "lane without the scratch sets of a batched launch");
   for (int k = 0; k < n; k++) launch_begin(ctx, *rs[k], L, k, refs[k]);
   for (int k = 0; k < n; k++) launch_resid_stage(ctx, *rs[k]);
   launch_plain_mc(ctx, rs, n);
@@ -1326,9 +1321,14 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
       for (int c = 0; c < 3; c++) {
         Lane &ln = ctx->lanes[l];
         int w = c ? W / 2 : W, h = c ? H / 2 : H;
-        ln.set[0].pred[c] = alloc_plane(w, h);
-        ln.set[0].resi[c] = alloc_plane(w, h);
-        ln.set[0].tmp[c] = alloc_plane(w, h);
+        // set 0 on every lane; the batch sets on the B lanes (frame-batched launches take inter pictures
+        // only). Allocated here, not at the first batch: the intra parameters of every prepared picture hold
+        // every set's plane pointers (vvcr_prepare_*), so the planes must exist before any picture is prepared.
+        for (int k = 0; k < (l >= ctx->nintra ? MC_MAXPIC : 1); k++) {
+          ln.set[k].pred[c] = alloc_plane(w, h);
+          ln.set[k].resi[c] = alloc_plane(w, h);
+          ln.set[k].tmp[c] = alloc_plane(w, h);
+        }
       }
     if (ctx->intra_wg <= 0) {
       // k_intra takes CTUs in wavefront order: the CTUs in flight are those of a few anti-diagonals

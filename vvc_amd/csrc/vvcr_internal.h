@@ -171,14 +171,16 @@ __host__ __device__ inline int mc_chroma_cells(int w, int h) { return 2 * ((w + 
 // partial round of waves (3.4 per SIMD at QP32): its time is the ramp and tail of that round, which a second
 // picture's waves fill. Each picture brings its destination, residual and prediction planes (its lane's
 // scratch set), its weighted-prediction table, its jobs and its class table; the DPB is shared.
-constexpr int MC_MAXPIC = 2;
+#ifndef MC_MAXPIC
+#define MC_MAXPIC 4
+#endif
 struct McPic {
   DPlane out[3];         // prediction planes (jobs without MC_RECON)
   DPlane reco[3];        // the picture (MC_RECON jobs)
   DPlane resi[3];        // the residual planes (MC_RESI jobs)
   const WpTable *wpd;    // weighted-prediction table in device memory
   const McJob *jobs;     // the picture's plain MC jobs (class order)
-  McClassTable ct;
+  const McClassTable *ct;   // its class table in device memory (read through scalar loads)
 };
 struct McBatch {
   RefPlanes ref;                      // DPB planes by slot
@@ -318,4 +320,5 @@ void launch_planes3(const Planes3 &p, hipStream_t s);
 void launch_resid(const TbParams &p, const TbJob *jobs, int njobs, int nsmall, const int32_t *coef, const uint16_t *scans, hipStream_t s);
 // DecoderApp output frame of a picture (vvcr_write_output)
 void launch_output(const std::array<DPlane, 3> &pic, const vvcr_output_params &op, int bd, uint8_t *dst, hipStream_t s);
-void launch_mc_batch(McBatch &b, hipStream_t s);   // k_mc over the pictures of b (fills b.lblk0 / cblk0)
+// k_mc over the pictures of b (fills b.lblk0 / cblk0 from the host copies hct[p] of the device class tables)
+void launch_mc_batch(McBatch &b, const McClassTable *const *hct, hipStream_t s);

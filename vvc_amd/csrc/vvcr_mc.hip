@@ -192,8 +192,15 @@ __constant__ CellTaps c_ctaps = make_cell_taps();
 #define MC_XCD_RUN 32
 #endif
 static_assert(MC_WG == 64, "k_mc: one wave per workgroup (wave64)");
+// MC_RING: reference rows in flight per lane in a continuous ring (0: the r05 form, groups of MC_ROWS_AHEAD rows)
+#ifndef MC_RING
+#define MC_RING 2
+#endif
+// the residual row of an output is loaded this many H rows before the row that completes it: with the ring,
+// at least MC_RING, so that it is older than the row loads in flight when the store waits for it (a load
+// younger than them would make that wait drain the ring)
 #ifndef MC_RESI_AHEAD
-#define MC_RESI_AHEAD 0   // 0 / 2 / 4 measured within 1 % (fused 4K B pictures); 0 holds the fewest registers
+#define MC_RESI_AHEAD (MC_RING > 0 ? MC_RING : 0)
 #endif
 #ifndef MC_ROWS_AHEAD
 #define MC_ROWS_AHEAD 4
@@ -319,9 +326,29 @@ __device__ __forceinline__ void cell_filter(const DPlane &Rp, int ox, int oy, in
       emit(o, v);
     }
   };
-  if constexpr (!EDGE) {
+  if constexpr (!EDGE && MC_RING > 0) {
     // k_mc: the host routed every job whose windows may leave the picture to k_mc<edge> (mc_job_edge), so
-    // the window is inside: vector loads, row pointers by increment
+    // the window is inside: vector loads. The rows stream through a ring of MC_RING loads in flight: row
+    // r + MC_RING is issued right after row r's dwords are taken, before row r is filtered, so the next
+    // rows' memory round trips overlap this row's arithmetic (r05 issued four rows, filtered them, then
+    // issued the next four: a wave then lived ~9 dependent round trips, 13-15 us even on an idle chip,
+    // r06 per-wave trace profiles/r06_mcprof_*)
+    const int16_t *row = Rp.p + (size_t)oy * Rp.stride + dc;
+    constexpr int K = MC_RING < ROWS ? MC_RING : ROWS;
+    uint32_t ring[K][ND];
+#pragma unroll
+    for (int r = 0; r < K; r++) load_nd<ND>(row + (size_t)r * Rp.stride, ring[r]);
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+      pre(r);
+      uint32_t w[ND];
+#pragma unroll
+      for (int k = 0; k < ND; k++) w[k] = ring[r % K][k];
+      if (r + K < ROWS) load_nd<ND>(row + (size_t)(r + K) * Rp.stride, ring[r % K]);
+      hrow(r, w);
+      __builtin_amdgcn_sched_barrier(0);   // keeps the order: the load of row r + K before row r's arithmetic
+    }
+  } else if constexpr (!EDGE) {
     const int16_t *row = Rp.p + (size_t)oy * Rp.stride + dc;
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
@@ -401,13 +428,17 @@ __device__ __forceinline__ void mc_cell(const McBatch &B, const McPic &Q, const 
   // MC_RESI: the residual row of output o is loaded MC_RESI_AHEAD H rows before the row that completes o
   // (the last list's pre hook), so the store does not wait for a memory round trip of its own
   uint32_t rres[R][2];
+  // (at row 0 also every output row the look-ahead already passed: MC_RESI_AHEAD may exceed N - 1)
   auto pre = [&](int r) {
-    const int o = r - (N - 1) + MC_RESI_AHEAD;
-    if (o < 0 || o >= R || !addResi || o >= nr) return;
-    const int16_t *rr = rsrc + (size_t)o * rstride;
-    rres[o][1] = 0;
-    if (wide) { const uint2 v = *(const uint2 *)rr; rres[o][0] = v.x; rres[o][1] = v.y; }
-    else { rres[o][0] = ((const uint32_t *)rr)[0]; if (nc == 4) rres[o][1] = ((const uint32_t *)rr)[1]; }
+    const int hi = r - (N - 1) + MC_RESI_AHEAD, lo = r == 0 ? 0 : hi;
+#pragma unroll
+    for (int o = lo; o <= hi; o++) {
+      if (o < 0 || o >= R || !addResi || o >= nr) continue;
+      const int16_t *rr = rsrc + (size_t)o * rstride;
+      rres[o][1] = 0;
+      if (wide) { const uint2 v = *(const uint2 *)rr; rres[o][0] = v.x; rres[o][1] = v.y; }
+      else { rres[o][0] = ((const uint32_t *)rr)[0]; if (nc == 4) rres[o][1] = ((const uint32_t *)rr)[1]; }
+    }
   };
   auto store = [&](int o, int (&a)[4]) {
     if (o >= nr) return;
@@ -491,9 +522,9 @@ __device__ __forceinline__ void mc_body(const McBatch &B, int b
   for (int q = 1; q < MC_MAXPIC; q++)
     if (q < B.npic && bb >= (luma ? B.lblk0[q] : B.cblk0[q])) p = q;
   p = __builtin_amdgcn_readfirstlane(p);
-  static_assert(MC_MAXPIC == 2, "k_mc: the picture select below");
-  const McPic &Q = p ? B.pic[1] : B.pic[0];
-  const McClassTable &ct = Q.ct;
+  const McPic &Q = B.pic[p];   // (p uniform: a scalar-offset read of the kernel argument)
+  // the class table through the constant address space: scalar loads, whatever the compiler proves
+  const __attribute__((address_space(4))) McClassTable &ct = *(const __attribute__((address_space(4))) McClassTable *)(uintptr_t)Q.ct;
   const int g = (bb - (luma ? B.lblk0[p] : B.cblk0[p])) * MC_WG + (int)threadIdx.x;
   const int gw = __builtin_amdgcn_readfirstlane(g & ~63);   // the wave's first cell: selects the class
   // the class of the wave by a scan over static fields (wave-uniform selects; a class index used to read
@@ -578,10 +609,10 @@ __global__ __launch_bounds__(MC_WG) __attribute__((amdgpu_waves_per_eu(MC_WAVES_
 
 }  // namespace
 
-void launch_mc_batch(McBatch &b, hipStream_t s) {
+void launch_mc_batch(McBatch &b, const McClassTable *const *hct, hipStream_t s) {
   int lb = 0, cb = 0;
   for (int p = 0; p < b.npic; p++) {
-    const McClassTable &ct = b.pic[p].ct;
+    const McClassTable &ct = *hct[p];
     b.lblk0[p] = lb;
     b.cblk0[p] = cb;
     if (ct.n > 0) {
