@@ -417,6 +417,116 @@ class BitstreamE2E:
         self.seg_ex.shutdown()
 
 
+def e2e_legs(ctx, data, meta, per, segments, steps, warmup, single_steps, threads, R, px_seq, npic):
+    """The end-to-end legs of one stream: `segments` decodes in flight (steps x segments decodes timed) and
+    one decode in flight (single_steps decodes timed), both from the bitstream; every segment's pictures
+    checked against the reference's MD5s afterwards. Returns (value Mpx/s, ms per step, host ms per picture,
+    host rusage, single-stream object, bit-exact)."""
+    bitexact = True
+    e2e = BitstreamE2E(ctx, data, per, segments, threads)
+    if warmup > 0:
+        e2e.run(warmup)
+        ctx.sync()
+    e2e.times = {}
+    R.barrier()
+    ctx.sync()
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
+    th0 = _thread_cpu() if os.environ.get("VVCR_BENCH_THREADS") else None
+    t0 = time.perf_counter()
+    e2e.run(steps)
+    ctx.sync()
+    t1 = time.perf_counter()
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    if th0 is not None:   # diagnostics: CPU of every thread of the process over the timed steps
+        th1 = _thread_cpu()
+        d = sorted(((th1[k][1] - th0.get(k, (None, 0))[1], k, th1[k][0]) for k in th1), reverse=True)
+        print("threads: %d, CPU s over the timed steps: total %.2f; top: %s" % (
+            len(d), sum(x[0] for x in d), ", ".join("%s/%d %.2f" % (n, k, v) for v, k, n in d[:24])), file=sys.stderr)
+    R.barrier()
+    elapsed = R.max_over_ranks(t1 - t0)
+    npic_timed = steps * segments * npic
+    # the process's CPU over the timed steps (all threads, this rank): user / system ms and page faults per picture
+    host_rusage = {"user_ms_per_picture": round((ru1.ru_utime - ru0.ru_utime) / npic_timed * 1e3, 3),
+                   "sys_ms_per_picture": round((ru1.ru_stime - ru0.ru_stime) / npic_timed * 1e3, 3),
+                   "minor_faults_per_picture": round((ru1.ru_minflt - ru0.ru_minflt) / npic_timed, 1),
+                   "cores_busy": round(((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / (t1 - t0), 2)}
+    for owner in e2e.final:
+        if owner is not None:
+            bitexact = bitexact and check_slots(ctx, owner, meta)
+    e2e.close()
+    host_ms = {k: round(v / npic_timed * 1e3, 3) for k, v in e2e.times.items()}
+    value = V.job_throughput(px_seq * segments * steps, elapsed, R) / 1e6
+    # single stream: one decode at a time (latency view of the same path; VERDICT r03 item 2)
+    single = None
+    if single_steps > 0:
+        ss = BitstreamE2E(ctx, data, per, 1, threads)
+        ss.run(1)
+        ctx.sync()
+        ss.times = {}
+        R.barrier()
+        s0 = time.perf_counter()
+        ss.run(single_steps)
+        ctx.sync()
+        s1 = time.perf_counter()
+        R.barrier()
+        s_el = R.max_over_ranks(s1 - s0)
+        for owner in ss.final:
+            if owner is not None:
+                bitexact = bitexact and check_slots(ctx, owner, meta)
+        ss.close()
+        single = {"value": round(V.job_throughput(px_seq * single_steps, s_el, R) / 1e6, 2), "unit": "Mpixels/s",
+                  "decodes": single_steps, "ms_per_decode": round(s_el / single_steps * 1e3, 3),
+                  "host_ms_per_picture": {k: round(v / (single_steps * npic) * 1e3, 3) for k, v in ss.times.items()},
+                  "note": "one decode in flight (%d worker threads: CABAC ahead, plan + upload pipelined; motion derivation "
+                          "in decoding order), end to end from the bitstream like value" % threads}
+    return value, elapsed / steps * 1e3, host_ms, host_rusage, single, bitexact
+
+
+def cpu_ratios(value, single, cb, ca, threads):
+    """vs_cpu_baseline (one DecoderApp core) and vs_cpu_baseline_all_cores (`threads` DecoderApp processes)."""
+    out = {}
+    if cb and cb.get("value"):
+        out["vs_cpu_baseline"] = {"value": round(value / cb["value"], 1),
+                                  "single_stream": round(single["value"] / cb["value"], 1) if single else None}
+    if ca and ca.get("value"):
+        out["vs_cpu_baseline_all_cores"] = {"value": round(value / ca["value"], 2),
+                                            "single_stream": round(single["value"] / ca["value"], 2) if single else None,
+                                            "note": "value uses %d host threads + the GPU; the comparator %d DecoderApp "
+                                                    "processes on %d cores" % (threads, ca["cores"], ca["cores"])}
+    return out
+
+
+def north_star_e2e(ctx, a, R, per):
+    """north_star's target is quoted on 4K RA QP32 (>= 20x VTM CPU decode at 1 MI355X): the headline's legs
+    on that stream, end to end from the bitstream, with its own CPU baselines (rank 0, one GPU)."""
+    name = a.north_star_stream
+    p = os.path.join(ROOT, "tests", "golden", "streams", name + ".bin")
+    if not os.path.exists(p):
+        return None
+    with open(p, "rb") as f:
+        data = f.read()
+    meta = S.load_meta(os.path.join(ROOT, "tests", "golden", name))
+    from vvc_amd import parser as P
+    ps = P.Stream(data)
+    infos = [ps.info(i) for i in range(len(ps))]
+    ps.close()
+    W, H = infos[0]["width"], infos[0]["height"]
+    if (W, H) != (ctx.width, ctx.height):
+        return {"error": "north-star stream %dx%d differs from the headline context" % (W, H)}
+    px_seq = W * H * len(infos)
+    value, ms_step, host_ms, rus, single, ok = e2e_legs(ctx, data, meta, per, a.segments, a.north_star_steps, 1,
+                                                        a.single_steps, a.e2e_threads, R, px_seq, len(infos))
+    out = {"stream": name, "value": round(value, 2), "unit": "Mpixels/s",
+           "workload": "%s: %dx%d random access QP32, %d pictures per decode, %d decodes per step" % (name, W, H, len(infos), a.segments),
+           "steps": a.north_star_steps, "ms_per_step": round(ms_step, 3), "host_ms_per_picture": host_ms, "host_rusage": rus,
+           "single_stream": single, "bitexact_vs_reference": bool(ok)}
+    if R.rank == 0 and R.world == 1 and not a.no_cpu:
+        cb = out["cpu_baseline"] = cpu_baseline(p, px_seq)
+        ca = out["cpu_baseline_all_cores"] = cpu_baseline_all_cores(p, px_seq, a.e2e_threads)
+        out.update(cpu_ratios(value, single, cb, ca, a.e2e_threads))
+    return out
+
+
 def output_yuv_md5(ctx, data, meta):
     """One decode with DecoderApp's output: the YUV file's MD5 (vvcr_write_output, output order) and
     every output picture's plane MD5s, compared with the reference's."""
@@ -473,6 +583,8 @@ def main():
                     help="host sync after every picture of the resident pass (profiling: kernel durations without overlap)")
     ap.add_argument("--e2e-threads", type=int, default=16,
                     help="host planning threads (the GPU box's CPU share is 16)")
+    ap.add_argument("--north-star-steps", type=int, default=4,
+                    help="timed steps of the north-star stream's end-to-end leg (`north_star_e2e`, 0 = skip)")
     ap.add_argument("--shard-stream", default="ra4320t_q32",
                     help="tile-row stream of the spatially sharded pass (BASELINE config 4: 8K, one shard per rank)")
     ap.add_argument("--shard-steps", type=int, default=3, help="timed steps of the sharded pass (0 = skip it)")
@@ -534,61 +646,9 @@ def main():
     # ---- headline: end to end from the bitstream (parse + derive + plan + upload + GPU in the timed region)
     ctx.set_timing(False)
     bitexact = output_yuv_md5(ctx, data, meta)      # one decode writing DecoderApp's output file: its MD5
-    e2e = BitstreamE2E(ctx, data, per, a.segments, a.e2e_threads)
-    if a.warmup > 0:
-        e2e.run(a.warmup)
-        ctx.sync()
-    e2e.times = {}
-    R.barrier()
-    ctx.sync()
-    ru0 = resource.getrusage(resource.RUSAGE_SELF)
-    th0 = _thread_cpu() if os.environ.get("VVCR_BENCH_THREADS") else None
-    t0 = time.perf_counter()
-    e2e.run(a.steps)
-    ctx.sync()
-    t1 = time.perf_counter()
-    ru1 = resource.getrusage(resource.RUSAGE_SELF)
-    if th0 is not None:   # diagnostics: CPU of every thread of the process over the timed steps
-        th1 = _thread_cpu()
-        d = sorted(((th1[k][1] - th0.get(k, (None, 0))[1], k, th1[k][0]) for k in th1), reverse=True)
-        print("threads: %d, CPU s over the timed steps: total %.2f; top: %s" % (
-            len(d), sum(x[0] for x in d), ", ".join("%s/%d %.2f" % (n, k, v) for v, k, n in d[:24])), file=sys.stderr)
-    R.barrier()
-    elapsed = R.max_over_ranks(t1 - t0)
-    npic_timed = a.steps * a.segments * len(infos)
-    # the process's CPU over the timed steps (all threads, this rank): user / system ms and page faults per picture
-    host_rusage = {"user_ms_per_picture": round((ru1.ru_utime - ru0.ru_utime) / npic_timed * 1e3, 3),
-                   "sys_ms_per_picture": round((ru1.ru_stime - ru0.ru_stime) / npic_timed * 1e3, 3),
-                   "minor_faults_per_picture": round((ru1.ru_minflt - ru0.ru_minflt) / npic_timed, 1),
-                   "cores_busy": round(((ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)) / (t1 - t0), 2)}
-    for owner in e2e.final:
-        if owner is not None:
-            bitexact = bitexact and check_slots(ctx, owner, meta)
-    e2e.close()
-
-    # ---- single stream: one decode at a time (latency view of the same path)
-    single = None
-    if a.single_steps > 0:
-        ss = BitstreamE2E(ctx, data, per, 1, a.e2e_threads)
-        ss.run(1)
-        ctx.sync()
-        ss.times = {}
-        R.barrier()
-        s0 = time.perf_counter()
-        ss.run(a.single_steps)
-        ctx.sync()
-        s1 = time.perf_counter()
-        R.barrier()
-        s_el = R.max_over_ranks(s1 - s0)
-        for owner in ss.final:
-            if owner is not None:
-                bitexact = bitexact and check_slots(ctx, owner, meta)
-        ss.close()
-        single = {"value": round(V.job_throughput(px_seq * a.single_steps, s_el, R) / 1e6, 2), "unit": "Mpixels/s",
-                  "decodes": a.single_steps, "ms_per_decode": round(s_el / a.single_steps * 1e3, 3),
-                  "host_ms_per_picture": {k: round(v / (a.single_steps * len(infos)) * 1e3, 3) for k, v in ss.times.items()},
-                  "note": "one decode in flight (%d worker threads: CABAC ahead, plan + upload pipelined; motion derivation "
-                          "in decoding order), end to end from the bitstream like value" % a.e2e_threads}
+    value, ms_step, host_ms, host_rusage, single, ok = e2e_legs(ctx, data, meta, per, a.segments, a.steps, a.warmup,
+                                                                 a.single_steps, a.e2e_threads, R, px_seq, len(infos))
+    bitexact = bitexact and ok
 
     # ---- resident: every picture planned and uploaded once, the steps only launch (GPU-side rate)
     resident = None
@@ -677,10 +737,14 @@ def main():
         ns_mc = north_star_mc(ctx, a.north_star_stream, per, a.kernel_table_reps, a.kernel_table_sync)
         bitexact = bitexact and (ns_mc is None or ns_mc["bitexact_vs_reference"])
 
-    ms_step = elapsed / a.steps * 1e3
+    # ---- the north star's stream (4K RA QP32) end to end, with its own CPU baselines
+    ns_e2e = None
+    if a.north_star_steps > 0 and a.north_star_stream and a.north_star_stream != a.stream:
+        ns_e2e = north_star_e2e(ctx, a, R, per)
+        bitexact = bitexact and (ns_e2e is None or "error" in ns_e2e or ns_e2e["bitexact_vs_reference"])
+
     kind, qp = a.stream.split("_")[0], a.stream.split("_")[-1]
     desc = "%s %s" % ("random access" if kind.startswith("ra") else "all intra", qp.replace("q", "QP"))
-    value = V.job_throughput(px_seq * a.segments * a.steps, elapsed, R) / 1e6
     line = {
         "metric": "decode Mpixels/sec (CABAC on host), bit-exact YUV vs DecoderApp, 1/2/4/8 GPU",
         "value": round(value, 2),
@@ -701,7 +765,7 @@ def main():
         "value_scope": "end to end from the bitstream: NAL/header parsing, CABAC (host threads), motion derivation "
                        "with the GPU's DMVR feedback, host planning, upload, GPU reconstruction and loop filters, every "
                        "picture of every step; a step = %d independent decodes of the stream, all in flight" % a.segments,
-        "host_ms_per_picture": {k: round(v / (a.steps * a.segments * len(infos)) * 1e3, 3) for k, v in e2e.times.items()},
+        "host_ms_per_picture": host_ms,
         "host_rusage": host_rusage,
         "roofline": roof,
         "cpu_baseline": None,
@@ -712,6 +776,7 @@ def main():
         "gpu_busy_est": round(value / resident["value"], 3) if resident and resident["value"] > 0 else None,
         "mc_roofline": mc_roof,
         "north_star_mc": ns_mc,
+        "north_star_e2e": ns_e2e,
         "kernels": {k: {"ms_per_step": round(v[1], 4), "ms_min_max": [round(v[3], 4), round(v[4], 4)], "launches_per_step": v[0],
                         "alg_GBps": round(v[2] / (v[1] / 1e3) / 1e9, 2) if v[1] > 0 else 0.0} for k, v in kern.items()},
     }
@@ -720,14 +785,7 @@ def main():
         cb = line["cpu_baseline"]
         ca = line["cpu_baseline_all_cores"] = cpu_baseline_all_cores(
             os.path.join(ROOT, "tests", "golden", "streams", a.stream + ".bin"), px_seq, a.e2e_threads)
-        if cb and cb.get("value"):
-            line["vs_cpu_baseline"] = {"value": round(value / cb["value"], 1),
-                                       "single_stream": round(single["value"] / cb["value"], 1) if single else None}
-        if ca and ca.get("value"):
-            line["vs_cpu_baseline_all_cores"] = {"value": round(value / ca["value"], 2),
-                                                 "single_stream": round(single["value"] / ca["value"], 2) if single else None,
-                                                 "note": "value uses %d host threads + the GPU; the comparator %d DecoderApp "
-                                                         "processes on %d cores" % (a.e2e_threads, ca["cores"], ca["cores"])}
+        line.update(cpu_ratios(value, single, cb, ca, a.e2e_threads))
     ctx.close()
     if a.shard_steps > 0:
         try:
