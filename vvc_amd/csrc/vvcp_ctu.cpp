@@ -2114,6 +2114,11 @@ struct Parser {
     cab.start(data + starts[0], data + substreamEnd(0));
     int qps[2] = {sh.qp, sh.qp};
     const int nCtu = (int)sh.ctus.size();
+    const bool wpp = pps.entropySync;
+    // WPP (entropy_coding_sync): the context state after the first CTU of each CTU row of a tile, which the
+    // next row's first CTU starts from when the CTU above it is in the same slice and tile
+    // (DecSlice.cpp:160-176, stored at :214-219)
+    std::vector<CtxModel> syncCtx;
     for (int i = 0; i < nCtu; i++) {
       const int ctu = sh.ctus[i];
       const int cx = ctu % pic.wCtu, cy = ctu / pic.wCtu;
@@ -2128,14 +2133,25 @@ struct Parser {
           cab.start(data + starts[ss], data + substreamEnd(ss));
         }
         qps[0] = qps[1] = sh.qp;
+      } else if (cx == tx0 && wpp) {
+        if (i != 0) {
+          init_ctx();
+          cab.start(data + starts[ss], data + substreamEnd(ss));
+        }
+        // the CTU above in the same slice and tile (CodingStructure::getCURestricted of (x, y - 1))
+        if (!syncCtx.empty() && cuRestricted(0, cx << pic.ctuLog2, (cy << pic.ctuLog2) - 1, sc.sliceIdx, curTile) >= 0)
+          std::copy(syncCtx.begin(), syncCtx.end(), cab.ctx);
+        qps[0] = qps[1] = sh.qp;
       }
       ctuHmvpReset = !sh.isIntra() && cx == tx0;
       firstCuOfCtu = true;
       coding_tree_unit(ctu, qps);
+      if (cx == tx0 && wpp) syncCtx.assign(cab.ctx, cab.ctx + vvcp_ctx::NUM_CTX);
       if (i == nCtu - 1) {
         VVCP_CHECK(!cab.trm(), "missing end_of_slice terminating bit");
-      } else if (cx + 1 == tx0 + tw && cy + 1 == ty0 + th) {
-        VVCP_CHECK(!cab.trm(), "missing end_of_tile terminating bit");
+      } else if (cx + 1 == tx0 + tw && (cy + 1 == ty0 + th || wpp)) {
+        // end of a tile, or with WPP of a CTU row of the tile: the substream ends
+        VVCP_CHECK(!cab.trm(), "missing end_of_tile / end_of_subset terminating bit");
         ss++;
         VVCP_CHECK(ss >= starts.size(), "missing entry point");
       }

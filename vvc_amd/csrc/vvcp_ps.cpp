@@ -328,7 +328,6 @@ void parse_pps(Bits &b, PPS &p) {
     p.lfAcrossSlices = b.flag();
   }
   p.entropySync = b.flag();
-  VVCP_CHECK(p.entropySync, "wavefront parallel processing is not supported");
   p.cabacInitPresent = b.flag();
   p.numRefDefault[0] = (int)b.ue() + 1;
   p.numRefDefault[1] = (int)b.ue() + 1;
@@ -844,11 +843,12 @@ void parse_sh(Bits &b, SliceHeader &s, PicHeader &ph, const ParamSets &ps, int p
     const int n = (int)b.ue();
     for (int i = 0; i < n; i++) b.u(8);
   }
-  // entry points: one per tile start after the first CTU (Slice::setNumEntryPoints, Slice.cpp:247)
+  // entry points: one per tile start after the first CTU, and with entropy coding sync (WPP) one per CTU row
+  // start of a tile (Slice::setNumEntryPoints, Slice.cpp:247)
   int nEntry = 0;
   for (size_t i = 1; i < s.ctus.size(); i++) {
     const int cx = s.ctus[i] % pps->widthInCtus, cy = s.ctus[i] / pps->widthInCtus;
-    if (pps->colBd[pps->ctuToTileCol[cx]] == cx && pps->rowBd[pps->ctuToTileRow[cy]] == cy) nEntry++;
+    if (pps->colBd[pps->ctuToTileCol[cx]] == cx && (pps->rowBd[pps->ctuToTileRow[cy]] == cy || pps->entropySync)) nEntry++;
   }
   s.entryPoints.clear();
   if (nEntry > 0) {

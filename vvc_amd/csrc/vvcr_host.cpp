@@ -260,7 +260,7 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
   bool multiSlice = false;
   for (const vvcr_cu &c : d.cu) multiSlice |= c.slice != (ncu ? d.cu[0].slice : 0);
   if (multiSlice && !pp.lf_across_slices) throw VvcrError(VVCR_E_UNSUPPORTED, "slices without loop filtering across slice boundaries");
-  if (pp.entropy_sync) throw VvcrError(VVCR_E_UNSUPPORTED, "wavefront parallel processing (entropy coding sync)");
+  // (entropy_sync, WPP: a property of the CABAC pass only; the reconstruction is the same)
   if (pp.shard_y1 > 0) {
     // a shard is a run of whole tile rows: intra prediction and CABAC stop at its edges, so its
     // reconstruction needs nothing from the other shards (the loop filters do: VVCR_LF_HALO)
