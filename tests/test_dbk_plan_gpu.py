@@ -4,7 +4,7 @@ every 4-sample edge segment, one thread per CU and direction) against the host p
 pinned by the decode tests to DecoderApp's deblocked planes: the four segment lists must hold the same
 segments with the same words, picture by picture (the device lists' order differs; it does not change the
 filtered samples). Streams: dual-tree intra pictures (ai*), ISP / MIP / BDPCM (aibdpcm), affine, SbTMVP,
-GEO / CIIP (rageo), LMCS, weighted prediction, tiles, DQ0."""
+GEO / CIIP (rageo), LMCS, weighted prediction, tiles, DQ0, tiles and slices not deblocked across (ratilenf)."""
 import ctypes as C
 import os
 
@@ -35,7 +35,7 @@ def _lists(L, pic):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["ai416_q37", "aibdpcm416_q32", "ailm416_q37", "ra416_q32", "rageo480_q32", "ralmgeo416_q32",
-                                  "rawp416_q32", "ratile416_q32", "radq0416_q32", "ra1080_q32"])
+                                  "rawp416_q32", "ratile416_q32", "radq0416_q32", "ra1080_q32", "ratilenf416_q32"])
 def test_device_deblocking_plan_equals_host_plan(name, monkeypatch):
     L = N.lib()
     L.vvcr_debug_dbk_segments.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]

@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("name", ["ai416_q37", "ra416_q32", "ra1080_q32", "ailm416_q37", "ralm416_q32", "rawp416_q32", "ratile416_q32", "ratile1080_q32",
                                   "ra2160_q27", "ra2160_q32", "ra1080l_q32",
-                                  "rageo480_q32", "radq0416_q32", "aibdpcm416_q32", "rawp1080_q32", "ralmgeo416_q32"])
+                                  "rageo480_q32", "radq0416_q32", "aibdpcm416_q32", "rawp1080_q32", "ralmgeo416_q32",
+                                  "rawpp416_q32", "ratilenf416_q32"])
 def test_decode_matches_reference_md5(golden_dir, name):
     d = os.path.join(golden_dir, name)
     pics = S.load_sequence(d)

@@ -693,7 +693,7 @@ struct Parser {
     c.depth = p.depth;
     c.qtdepth = p.qtDepth;
     c.firstpu = -1; c.firsttu = -1;
-    c.slice = sc.sliceIdx;
+    c.slice = sh.sliceAddr;   // Slice::getSliceID (VLCReader.cpp:2737: the slice address); CuAux::slice is the index
     c.yvalid = yv; c.cvalid = cv;
     CuAux x;
     x.splitSeries = p.splitSeries();

@@ -1398,7 +1398,7 @@ void refine_motion(const PictureUnit &p, MotionField &&field, const int32_t *del
         const int ddx = deltas[2 * k], ddy = deltas[2 * k + 1];
         Mi mi;
         mi.isInter = true;
-        mi.slice = (uint16_t)c.slice;
+        mi.slice = (uint16_t)S.cux[u.cu].slice;
         mi.interDir = (int8_t)u.interdir;
         mi.altHpel = c.imv == IMV_HPEL;
         mi.ref[0] = (int16_t)u.ref0; mi.ref[1] = (int16_t)u.ref1;

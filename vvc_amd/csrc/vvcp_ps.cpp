@@ -276,11 +276,13 @@ static void init_tiles(PPS &p) {
   p.rowBd.assign(1, 0);
   std::vector<int> cw = p.tileColW, rh = p.tileRowH;
   int rem = p.widthInCtus;
-  for (int w : cw) rem -= w;
+  for (int w : cw) { VVCP_CHECK(w <= 0, "tile column width"); rem -= w; }
+  VVCP_CHECK(rem < 0, "tile columns wider than the picture");
   int uni = cw.back();
   while (rem > 0) { uni = std::min(rem, uni); cw.push_back(uni); rem -= uni; }
   rem = p.heightInCtus;
-  for (int h : rh) rem -= h;
+  for (int h : rh) { VVCP_CHECK(h <= 0, "tile row height"); rem -= h; }
+  VVCP_CHECK(rem < 0, "tile rows taller than the picture");
   uni = rh.back();
   while (rem > 0) { uni = std::min(rem, uni); rh.push_back(uni); rem -= uni; }
   for (int w : cw) p.colBd.push_back(p.colBd.back() + w);

@@ -204,6 +204,8 @@ struct Prepared {
   DevVec<int32_t> sao;
   DevVec<int16_t> alf_luma_coef, alf_luma_clip, alf_chroma, alf_cc, alf_set;
   DevVec<uint8_t> alf_ctb;
+  DevVec<uint8_t> lf_nb;             // lf_ctb_neighbours of the picture (SAO / ALF), n_lf_nb entries
+  int n_lf_nb = 0;
   DevVec<int32_t> dmvr;
   DevVec<WpTable> wpt;               // the slice's weighted-prediction table (k_mc reads it per lane)
   McClassTable mc_ct;                // k_mc cell classes of mc_basic (edge jobs, tiles, blocks)
@@ -328,6 +330,7 @@ struct vvcr_picture {
   DbkLists dbk;
   bool dbk_gpu = false;              // the edges are planned on the device from dbkg (default; VVCR_DBK_GPU=0: host)
   DbkGpuInputs dbkg;
+  std::vector<uint8_t> lf_nb;        // lf_ctb_neighbours (empty: loop filters across every tile / slice)
   // an upload that DMAs straight from this picture's page-locked arrays (Staging::add_big) is in flight
   // until up_ev: settle() before the arrays change or are freed
   mutable hipEvent_t up_ev = nullptr;
@@ -562,6 +565,9 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
   b.dbk.clear();
   b.dbkg.clear();
   b.dbk_gpu = (mask & VVCR_STAGE_DBK) && dbk_on_device();
+  // tiles / slices without loop filtering across them: the CTBs' neighbour availability (DBK, SAO, ALF)
+  if (mask & (VVCR_STAGE_DBK | VVCR_STAGE_SAO | VVCR_STAGE_ALF)) lf_ctb_neighbours(sp, pp, b.desc, b.lf_nb);
+  else b.lf_nb.clear();
   if (pp.lmcs_enabled && sp.bit_depth != 10) throw VvcrError(VVCR_E_UNSUPPORTED, "LMCS tables are captured for 10-bit luma");
   // With the residual, inter and intra stages together, plain inter CUs are reconstructed by k_mc (the
   // prediction plus the residual straight into the picture, fused_inter_cu); a subset of those stages
@@ -584,7 +590,7 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
     dbk_thread = std::thread([&] {
       pthread_setname_np(pthread_self(), "vvcr-plan-dbk");
       try {
-        plan_deblocking(sp, pp, b.desc, b.dbk);
+        plan_deblocking(sp, pp, b.desc, b.lf_nb, b.dbk);
       } catch (...) {
         dbk_err = std::current_exception();
       }
@@ -602,7 +608,7 @@ static void plan_picture(vvcr_picture &b, uint32_t mask) {
           for (const vvcr_cu &c : b.desc.cu) inter |= c.predmode != 1;   // vvcr_cu::predmode: 1 intra
         if ((inter || !b.desc.motion.empty()) && b.desc.motion.size() != (size_t)(sp.width / 4) * (sp.height / 4))
           throw VvcrError(VVCR_E_ARG, "deblocking: the motion field does not cover the picture");
-        pack_dbk_inputs(sp, pp, b.desc, b.dbkg);
+        pack_dbk_inputs(sp, pp, b.desc, b.lf_nb, b.dbkg);
       }
       if (mask & (VVCR_STAGE_RESID | VVCR_STAGE_INTER)) build_work_lists(sp, pp, b.desc, b.wl, fuse);
     } catch (...) {
@@ -831,6 +837,8 @@ static void prepare(vvcr_ctx *ctx, Prepared &r, const vvcr_picture &bp) {
   r.have_alf = (mask & VVCR_STAGE_ALF) && alfOn;
   static const bool copy_back = getenv("VVCR_COPY_BACK") != nullptr;   // diagnostics: the r04 copy-back
   r.recon_tmp = r.have_sao != r.have_alf && (mask & VVCR_STAGE_ALL) == VVCR_STAGE_ALL && pp.shard_y1 == 0 && !copy_back;
+  r.n_lf_nb = (r.have_sao || r.have_alf) ? (int)bp.lf_nb.size() : 0;
+  if (r.n_lf_nb) st.add(r.lf_nb, bp.lf_nb);
   if (r.have_sao) {
     st.add(r.sao, bp.h_sao);
     r.alg_bytes[K_SAO] = pix * 2 * 2;
@@ -1142,6 +1150,7 @@ static void launch_rest(vvcr_ctx *ctx, Prepared &r, uint32_t mask, const std::ve
     for (int c = 0; c < 3; c++) { sp.src[c] = inTmp ? S.tmp[c] : slot[c]; sp.dst[c] = inTmp ? slot[c] : S.tmp[c]; }
     sp.sao = r.sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
     sp.y0 = rw.sao0; sp.y1 = rw.sao1;
+    sp.nb = r.n_lf_nb ? r.lf_nb.p : nullptr;
     launch_sao(sp, s);
     VVCR_CHECK_HIP(hipGetLastError());
     inTmp = !inTmp;
@@ -1160,6 +1169,7 @@ static void launch_rest(vvcr_ctx *ctx, Prepared &r, uint32_t mask, const std::ve
     ap.ctb_en = r.alf_ctb.p; ap.ctb_alt = r.alf_ctb.p + 3 * n; ap.cc_ctl = r.alf_ctb.p + 6 * n;
     ap.ctb_set = r.alf_set.p;
     ap.y0 = rw.own0; ap.y1 = rw.own1;
+    ap.nb = r.n_lf_nb ? r.lf_nb.p : nullptr;
     launch_alf(ap, s);
     VVCR_CHECK_HIP(hipGetLastError());
     inTmp = !inTmp;

@@ -25,7 +25,10 @@ struct DbkParams {
   int32_t bd, beta_offset_div2, tc_offset_div2;
 };
 
-void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkLists &out);
+// lf_nb: lf_ctb_neighbours (vvcr_host.h) of the picture, or empty: a CU's left / top edge at a CTB edge is
+// filtered only when that CTB neighbour is available (tiles / slices not filtered across)
+void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, const std::vector<uint8_t> &lf_nb,
+                     DbkLists &out);
 
 // Device planning (vvcr_dbk_plan.hip, r05): the same edges planned on the GPU from compact copies of the
 // descriptors (pack_dbk_inputs, host) and the 4x4 motion field.
@@ -42,7 +45,8 @@ struct DbCu {
 static_assert(sizeof(DbCu) == 48, "DbCu layout");
 enum : uint16_t {
   DBC_CHTYPE = 1, DBC_INTRA = 2, DBC_BDPCM = 4, DBC_BDPCMC = 8, DBC_AFFINE = 16, DBC_ISP = 32, DBC_TREE = 64,
-  DBC_YVALID = 128, DBC_CVALID = 256, DBC_CIIP = 512   // CIIP: the CU's first PU
+  DBC_YVALID = 128, DBC_CVALID = 256, DBC_CIIP = 512,  // CIIP: the CU's first PU
+  DBC_NOLEFT = 1024, DBC_NOTOP = 2048                   // its left / top edge is a tile / slice edge not filtered across
 };
 struct DbPu {
   int16_t x, y, w, h, cx, cy;
@@ -66,7 +70,8 @@ struct DbkGpuInputs {
   int32_t nitems[4] = {0, 0, 0, 0};     // the item lists' lengths: (pass, dir) at 2 * pass + dir
   void clear() { cu.clear(); pu.clear(); tu.clear(); chroma_pass = false; for (int &n : nitems) n = 0; }
 };
-void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkGpuInputs &out);
+void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, const std::vector<uint8_t> &lf_nb,
+                     DbkGpuInputs &out);
 
 struct DbkPlanArgs {
   const DbCu *cu; const DbPu *pu; const DbTu *tu; const MotionRec *motion;

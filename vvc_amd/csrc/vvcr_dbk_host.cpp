@@ -50,9 +50,11 @@ struct Planner {
   // (edges off the grid, ISP sub-partitions 1 or 2 samples wide, are never filtered nor read)
   uint8_t lenP[3][32][32], lenQ[3][32][32], tedge[32][32];
   bool left = false, top = false, internal = false;
+  const std::vector<uint8_t> &lf_nb;   // lf_ctb_neighbours, or empty
 
-  Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, DbkLists &o, Maps &m)
-      : sp(s), pp(p), d(dd), out(o), M(m) {
+  Planner(const vvcr_seq_params &s, const vvcr_pic_params &p, const PictureDescriptors &dd, DbkLists &o, Maps &m,
+          const std::vector<uint8_t> &nb)
+      : sp(s), pp(p), d(dd), out(o), M(m), lf_nb(nb) {
     W4 = sp.width / 4;
     H4 = sp.height / 4;
     ctu = 1 << sp.ctu_log2;
@@ -339,6 +341,14 @@ struct Planner {
     }
   }
 
+  bool lf_edge_ok(const vvcr_cu &cu, bool leftEdge) const {
+    if (lf_nb.empty()) return true;
+    const int x = cu.yvalid ? cu.x : 2 * cu.cx, y = cu.yvalid ? cu.y : 2 * cu.cy;
+    if (leftEdge ? (x & (ctu - 1)) : (y & (ctu - 1))) return true;
+    const int wc = (sp.width + ctu - 1) / ctu;
+    return lf_nb[(size_t)(y >> sp.ctu_log2) * wc + (x >> sp.ctu_log2)] & (leftEdge ? LFNB_L : LFNB_A);
+  }
+
   void deblock_cu(int cui, int dir) {
     const vvcr_cu &cu = d.cu[cui];
     int a[4];
@@ -346,7 +356,13 @@ struct Planner {
     const int ch = cu.chtype;
     const int cpx = ch ? cu.cx : cu.x, cpy = ch ? cu.cy : cu.y;
     if (pp.dbk_disable) { left = top = internal = false; }
-    else { internal = true; left = cpx > 0; top = cpy > 0; }
+    else {
+      // xSetLoopfilterParam (LoopFilter.cpp:656-672): the left / top neighbour must be available across tiles /
+      // slices not filtered across (isAvailableLeft / Above); only at a CTB edge can it lie in another tile / slice
+      internal = true;
+      left = cpx > 0 && lf_edge_ok(cu, true);
+      top = cpy > 0 && lf_edge_ok(cu, false);
+    }
     int edges[2 * 128 + 16], ne = 0;
     for (int t = cu.firsttu; t < cu.firsttu + cu.ntu; t++) {
       int ta[4];
@@ -499,7 +515,8 @@ struct Planner {
 // Workers take contiguous CTU ranges and fill lists of their own, appended in CTU order afterwards: the
 // lists are those of one pass over the CTUs, whatever the number of workers (VVCR_DBK_THREADS, default 4;
 // the picture's other planners run beside them).
-void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkLists &out) {
+void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, const std::vector<uint8_t> &lf_nb,
+                     DbkLists &out) {
   out.clear();
   if (pp.dbk_disable) return;
   if (sp.width % 8 || sp.height % 8) throw VvcrError(VVCR_E_UNSUPPORTED, "deblocking: picture size not a multiple of 8");
@@ -511,7 +528,7 @@ void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const
   std::vector<int> start, order;
   {
     DbkLists scratch;
-    auto P = std::make_unique<Planner>(sp, pp, d, scratch, M);   // ~200 KB of per-CTU state: keep it off the stack
+    auto P = std::make_unique<Planner>(sp, pp, d, scratch, M, lf_nb);   // ~200 KB of per-CTU state: keep it off the stack
     P->build_maps();
     P->group(start, order);
   }
@@ -521,7 +538,7 @@ void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const
   std::vector<std::exception_ptr> err(T);
   auto work = [&](int t) {
     try {
-      auto P = std::make_unique<Planner>(sp, pp, d, part[t], M);
+      auto P = std::make_unique<Planner>(sp, pp, d, part[t], M, lf_nb);
       const int k0 = (int)((int64_t)nctu * t / T), k1 = (int)((int64_t)nctu * (t + 1) / T);
       for (int dir = 0; dir < 2; dir++) P->run_ctus(dir, k0, k1, start, order);
     } catch (...) {
@@ -543,7 +560,8 @@ void plan_deblocking(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const
 
 // Compact copies of the descriptors for the device planner (vvcr_dbk_plan.hip): one pass over the CU / PU /
 // TU rows, with the chroma QP of every TU resolved here (the host planner's chroma_qp).
-void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, DbkGpuInputs &out) {
+void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, const std::vector<uint8_t> &lf_nb,
+                     DbkGpuInputs &out) {
   out.clear();
   if (pp.dbk_disable) return;
   if (sp.width % 8 || sp.height % 8) throw VvcrError(VVCR_E_UNSUPPORTED, "deblocking: picture size not a multiple of 8");
@@ -570,6 +588,13 @@ void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const
     if (c.yvalid) f |= DBC_YVALID;
     if (c.cvalid) f |= DBC_CVALID;
     if (c.firstpu >= 0 && (size_t)c.firstpu < npu && d.pu[c.firstpu].ciip) f |= DBC_CIIP;
+    if (!lf_nb.empty()) {   // tile / slice edges not filtered across (the host planner's lf_edge_ok)
+      const int ctu = 1 << sp.ctu_log2, wc = (sp.width + ctu - 1) / ctu;
+      const int lx = c.yvalid ? c.x : 2 * c.cx, ly = c.yvalid ? c.y : 2 * c.cy;
+      const uint8_t m = lf_nb[(size_t)(ly >> sp.ctu_log2) * wc + (lx >> sp.ctu_log2)];
+      if ((lx & (ctu - 1)) == 0 && !(m & LFNB_L)) f |= DBC_NOLEFT;
+      if ((ly & (ctu - 1)) == 0 && !(m & LFNB_A)) f |= DBC_NOTOP;
+    }
     o.flags = f;
     if (c.chtype) out.chroma_pass = true;
     // the edge lines (the host planner's deblock_cu edge list, as a mask) and the CU's units on them: its

@@ -77,7 +77,7 @@ __device__ __forceinline__ Cu load_cu(const DbkPlanArgs &A, int i) {
   R.a2 = R.yv ? R.w : 2 * c->cw; R.a3 = R.yv ? R.h : 2 * c->ch;
   R.cpx = R.ch ? R.cx : R.x; R.cpy = R.ch ? R.cy : R.y;
   if (A.dbk_disable) { R.left = R.top = R.internal = 0; }
-  else { R.internal = 1; R.left = R.cpx > 0; R.top = R.cpy > 0; }
+  else { R.internal = 1; R.left = R.cpx > 0 && !(R.flags & DBC_NOLEFT); R.top = R.cpy > 0 && !(R.flags & DBC_NOTOP); }
   R.sub = R.npu && ((R.PU->sub & 1) || (R.flags & DBC_AFFINE));
   R.pux = R.npu ? (R.ch ? R.PU->cx : R.PU->x) : R.cpx;
   R.puy = R.npu ? (R.ch ? R.PU->cy : R.PU->y) : R.cpy;

@@ -255,11 +255,10 @@ void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, 
     if (n > 0 && (bd[0] != 0 || bd[n] != lim)) fail("tile boundaries do not span the picture");
     for (int t = 0; t < n; t++) if (bd[t + 1] <= bd[t]) fail("tile boundaries not increasing");
   }
-  if ((pp.num_tile_cols > 1 || pp.num_tile_rows > 1) && !pp.lf_across_tiles)
-    throw VvcrError(VVCR_E_UNSUPPORTED, "tiles without loop filtering across tile boundaries");
-  bool multiSlice = false;
-  for (const vvcr_cu &c : d.cu) multiSlice |= c.slice != (ncu ? d.cu[0].slice : 0);
-  if (multiSlice && !pp.lf_across_slices) throw VvcrError(VVCR_E_UNSUPPORTED, "slices without loop filtering across slice boundaries");
+  // (tiles / slices without loop filtering across their boundaries: lf_ctb_neighbours; the shard path needs
+  // the filters across its tile rows)
+  if (pp.shard_y1 > 0 && !pp.lf_across_tiles && (pp.num_tile_cols > 1 || pp.num_tile_rows > 1))
+    throw VvcrError(VVCR_E_UNSUPPORTED, "spatial shards of a picture without loop filtering across tiles");
   // (entropy_sync, WPP: a property of the CABAC pass only; the reconstruction is the same)
   if (pp.shard_y1 > 0) {
     // a shard is a run of whole tile rows: intra prediction and CABAC stop at its edges, so its
@@ -849,4 +848,52 @@ void build_zero_jobs(const vvcr_pic_params &pp, const PictureDescriptors &d, big
       if (!written) zero(comp, b[0], b[1], b[2], b[3]);
     }
   }
+}
+
+void lf_ctb_neighbours(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, std::vector<uint8_t> &nb) {
+  nb.clear();
+  const int ctu = 1 << sp.ctu_log2, wc = (sp.width + ctu - 1) / ctu, hc = (sp.height + ctu - 1) / ctu;
+  const bool tiles = (pp.num_tile_cols > 1 || pp.num_tile_rows > 1) && !pp.lf_across_tiles;
+  bool slices = false;
+  for (const vvcr_cu &c : d.cu) slices |= c.slice != d.cu[0].slice;
+  slices = slices && !pp.lf_across_slices;
+  if (!tiles && !slices) return;
+  // the slice of every CTB: of the CU at its origin (the first CU of a CTB in decoding order)
+  std::vector<int> slice((size_t)wc * hc, -1);
+  for (const vvcr_cu &c : d.cu) {
+    const int x = c.yvalid ? c.x : 2 * c.cx, y = c.yvalid ? c.y : 2 * c.cy;
+    if ((x & (ctu - 1)) == 0 && (y & (ctu - 1)) == 0) slice[(size_t)(y >> sp.ctu_log2) * wc + (x >> sp.ctu_log2)] = c.slice;
+  }
+  for (int v : slice)
+    if (v < 0) throw VvcrError(VVCR_E_ARG, "loop filter boundaries: a CTB without a CU at its origin");
+  auto tile_of = [&](int cx, int cy) {
+    int tc = 0, tr = 0;
+    for (int t = 0; t < pp.num_tile_cols; t++) if (cx >= pp.tile_col_bd[t]) tc = t;
+    for (int t = 0; t < pp.num_tile_rows; t++) if (cy >= pp.tile_row_bd[t]) tr = t;
+    return tr * 1024 + tc;
+  };
+  nb.assign((size_t)wc * hc, 0);
+  static const int dx[8] = {-1, 1, 0, 0, -1, 1, -1, 1}, dy[8] = {0, 0, -1, 1, -1, -1, 1, 1};
+  for (int cy = 0; cy < hc; cy++)
+    for (int cx = 0; cx < wc; cx++) {
+      const size_t k = (size_t)cy * wc + cx;
+      uint8_t m = 0;
+      for (int j = 0; j < 8; j++) {
+        const int nx = cx + dx[j], ny = cy + dy[j];
+        if (nx < 0 || ny < 0 || nx >= wc || ny >= hc) continue;
+        const size_t n = (size_t)ny * wc + nx;
+        if (slices && slice[n] != slice[k]) continue;
+        if (tiles && tile_of(nx, ny) != tile_of(cx, cy)) continue;
+        m |= (uint8_t)(1u << j);
+      }
+      nb[k] = m;
+      // ALF's raster-slice corner padding (AdaptiveLoopFilter.cpp:172-198): the top-left (bottom-right) CTB of
+      // another slice while the top and left (bottom and right) ones are available
+      const bool alf = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
+      if (alf && slices) {
+        const bool tl = cx > 0 && cy > 0 && (m & LFNB_L) && (m & LFNB_A) && slice[k - wc - 1] != slice[k];
+        const bool br = cx + 1 < wc && cy + 1 < hc && (m & LFNB_R) && (m & LFNB_B) && slice[k + wc + 1] != slice[k];
+        if (tl || br) throw VvcrError(VVCR_E_UNSUPPORTED, "ALF raster-slice corner padding (slices that are not rows of tiles)");
+      }
+    }
 }

@@ -87,6 +87,16 @@ uint16_t cu_resi_flags(const PictureDescriptors &d, const vvcr_cu &c);
 
 // Throws VvcrError on inconsistent descriptors (indices out of range, blocks outside the picture).
 void validate_descriptors(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d);
+
+// Loop filtering across tile / slice boundaries switched off (pps_loop_filter_across_tiles / _slices_enabled_flag
+// = 0 with more than one tile / slice): the availability of the 8 neighbouring CTBs of every CTB (raster order),
+// as SampleAdaptiveOffset::deriveLoopFilterBoundaryAvailibility (SampleAdaptiveOffset.cpp:668-718) derives it and
+// AdaptiveLoopFilter::isCrossedByVirtualBoundaries (AdaptiveLoopFilter.cpp:121-170) its clip flags; the
+// deblocking filter's CU left / top edges follow from bits L / A at CTB edges (LoopFilter.cpp:670-671; inside a
+// CTB both sides share tile and slice). Empty when nothing is restricted (the picture-edge rule alone).
+// Throws VVCR_E_UNSUPPORTED for the raster-slice corner padding of ALF (rasterSliceAlfPad, :172-198).
+enum : uint8_t { LFNB_L = 1, LFNB_R = 2, LFNB_A = 4, LFNB_B = 8, LFNB_AL = 16, LFNB_AR = 32, LFNB_BL = 64, LFNB_BR = 128 };
+void lf_ctb_neighbours(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, std::vector<uint8_t> &nb);
 // fuse: the picture's reconstruction stages run together (residual, inter, intra), so plain inter CUs are
 // reconstructed by k_mc itself (fused_inter_cu)
 void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const PictureDescriptors &d, WorkLists &wl,

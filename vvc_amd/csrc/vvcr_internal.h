@@ -267,6 +267,7 @@ struct SaoParams {
   const int32_t *sao;          // [nctb][3][35] vvcr_sao rows
   int32_t bd, ctu, wc;
   int32_t y0, y1;              // luma rows processed (chroma: halves); the picture edges stay the edges
+  const uint8_t *nb;           // per CTB the availability of its 8 neighbour CTBs (lf_ctb_neighbours), or null
 };
 
 struct AlfParams {
@@ -279,6 +280,7 @@ struct AlfParams {
   const uint8_t *ctb_en, *ctb_alt, *cc_ctl;
   const int16_t *ctb_set;
   int32_t y0, y1;              // luma rows processed (multiple of 16; chroma: halves)
+  const uint8_t *nb;           // per CTB its neighbours' availability (lf_ctb_neighbours: the clip flags), or null
 };
 
 struct Planes3 {

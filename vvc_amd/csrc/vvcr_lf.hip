@@ -48,7 +48,13 @@ __global__ __launch_bounds__(256) void k_sao(SaoParams P) {
   const uint4 vc = *(const uint4 *)(rc + x0), va = *(const uint4 *)(ra + x0), vb = *(const uint4 *)(rb + x0);
   int C[10], A[10], B[10];
   C[0] = rc[xl]; C[9] = rc[xr]; A[0] = ra[xl]; A[9] = ra[xr]; B[0] = rb[xl]; B[9] = rb[xr];
-  const int32_t *prm = P.sao + ((size_t)((y / cs) * P.wc + x0 / cs) * 3 + comp) * 35;
+  const int ctb = (y / cs) * P.wc + x0 / cs;
+  const int32_t *prm = P.sao + ((size_t)ctb * 3 + comp) * 35;
+  // tiles / slices not filtered across: the CTB's neighbour availability (deriveLoopFilterBoundaryAvailibility,
+  // SampleAdaptiveOffset.cpp:668-718); offsetBlock (:293-547) modifies a sample only when both samples its class
+  // compares it with lie in available CTBs
+  const int nbm = P.nb ? P.nb[ctb] : 0xff;
+  const int bx0 = (x0 / cs) * cs, by0 = (y / cs) * cs;
   const int on = prm[0], type = prm[1];
   const int e0 = prm[3], e1 = prm[4], e2 = prm[5], e3 = prm[6], e4 = prm[7];
   {
@@ -71,12 +77,19 @@ __global__ __launch_bounds__(256) void k_sao(SaoParams P) {
       // neighbours per EO class: 0 horizontal, 1 vertical, 2 135 degrees, 3 45 degrees
       const int dax = type == 1 ? 0 : (type == 3 ? 1 : -1), day = type == 0 ? 0 : -1;
       const bool rowsIn = day == 0 || (y - 1 >= 0 && y + 1 < H);
+      // the CTB offsets of row y + day / y - day
+      const int oya = y + day < by0 ? -1 : (y + day >= by0 + cs ? 1 : 0), oyb = y - day < by0 ? -1 : (y - day >= by0 + cs ? 1 : 0);
+      auto avail = [&](int ox, int oy) {   // bit of neighbour CTB (ox, oy): L R A B AL AR BL BR (vvcr_host.h LFNB_*)
+        const int bit = oy == 0 ? (ox < 0 ? 0 : 1) : (ox == 0 ? (oy < 0 ? 2 : 3) : (oy < 0 ? (ox < 0 ? 4 : 5) : (ox < 0 ? 6 : 7)));
+        return (ox == 0 && oy == 0) || ((nbm >> bit) & 1);
+      };
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int x = x0 + k;
         const int a = type == 0 ? C[k] : (type == 1 ? A[1 + k] : (type == 2 ? A[k] : A[2 + k]));
         const int b = type == 0 ? C[2 + k] : (type == 1 ? B[1 + k] : (type == 2 ? B[2 + k] : B[k]));
-        const bool in = rowsIn && x + dax >= 0 && x + dax < W && x - dax >= 0 && x - dax < W && x < W;
+        const int oxa = x + dax < bx0 ? -1 : (x + dax >= bx0 + cs ? 1 : 0), oxb = x - dax < bx0 ? -1 : (x - dax >= bx0 + cs ? 1 : 0);
+        const bool in = rowsIn && x + dax >= 0 && x + dax < W && x - dax >= 0 && x - dax < W && x < W && avail(oxa, oya) && avail(oxb, oyb);
         const int s0 = v[k], ei = 2 + sgn(s0 - a) + sgn(s0 - b);
         const int off = ei == 0 ? e0 : (ei == 1 ? e1 : (ei == 2 ? e2 : (ei == 3 ? e3 : e4)));
         if (in) v[k] = clip3(0, maxv, s0 + off);
@@ -160,13 +173,14 @@ constexpr int ALF_CCH = ALF_CSW / 8;                 // chroma chunks per row (6
 constexpr int ALF_LQ = (ALF_SH * ALF_LCH + 255) / 256;   // staged luma chunks per lane
 static_assert(2 * ALF_CSH * ALF_CCH <= 256, "one chroma chunk per lane");
 
-// 8 samples of row y from column x0 (a multiple of 8), picture-clamped (one vector load when inside)
-__device__ __forceinline__ uint4 alf_chunk(const DPlane &S, int x0, int y) {
-  const int16_t *row = S.p + (size_t)clip3(0, S.h - 1, y) * S.stride;
-  if (x0 >= 0 && x0 + 8 <= S.w) return *(const uint4 *)(row + x0);
+// 8 samples of row y from column x0 (a multiple of 8), clamped to columns [xl, xh) and rows [yl, yh): the
+// picture, or the CTB's sides that border tiles / slices not filtered across (one vector load when inside)
+__device__ __forceinline__ uint4 alf_chunk(const DPlane &S, int x0, int y, int xl, int xh, int yl, int yh) {
+  const int16_t *row = S.p + (size_t)clip3(yl, yh - 1, y) * S.stride;
+  if (x0 >= xl && x0 + 8 <= xh) return *(const uint4 *)(row + x0);
   int v[8];
 #pragma unroll
-  for (int e = 0; e < 8; e++) v[e] = row[clip3(0, S.w - 1, x0 + e)];
+  for (int e = 0; e < 8; e++) v[e] = row[clip3(xl, xh - 1, x0 + e)];
   return make_uint4((uint32_t)(uint16_t)v[0] | (uint32_t)v[1] << 16, (uint32_t)(uint16_t)v[2] | (uint32_t)v[3] << 16,
                     (uint32_t)(uint16_t)v[4] | (uint32_t)v[5] << 16, (uint32_t)(uint16_t)v[6] | (uint32_t)v[7] << 16);
 }
@@ -205,11 +219,23 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
   // chroma chunk for 144 lanes; then the CTB's controls (a 64x16 tile lies in one CTB, so they are
   // uniform: scalar loads) and the filters they select (the luma set's 25 classes of coefficients / clips,
   // both chroma filters, both CC-ALF filters), staged in LDS with the samples
+  // the sample bounds: the picture, or with tiles / slices not filtered across the CTB's clipped sides
+  // (AdaptiveLoopFilter::isCrossedByVirtualBoundaries :121-170: the CTB is filtered from a copy extended by
+  // edge replication there, as at the picture's edges)
+  int xl = 0, xh = W, yl = 0, yh = H;
+  if (P.nb) {
+    const int ctu = 1 << P.ctu_log2, bx = X0 & ~(ctu - 1), by = Y0 & ~(ctu - 1);
+    const int m = ldc_u8(P.nb, (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2));
+    if (!(m & 1)) xl = bx;
+    if (!(m & 2)) xh = min(W, bx + ctu);
+    if (!(m & 4)) yl = by;
+    if (!(m & 8)) yh = min(H, by + ctu);
+  }
   uint4 lv[ALF_LQ] = {}, cv = {};
 #pragma unroll
   for (int q = 0; q < ALF_LQ; q++) {
     const int i = tid + 256 * q, lr = i / ALF_LCH, lc = i - lr * ALF_LCH;
-    if (i < ALF_SH * ALF_LCH) lv[q] = alf_chunk(S, X0 - ALF_LX + 8 * lc, Y0 - ALF_HALO + lr);
+    if (i < ALF_SH * ALF_LCH) lv[q] = alf_chunk(S, X0 - ALF_LX + 8 * lc, Y0 - ALF_HALO + lr, xl, xh, yl, yh);
   }
   const int ccomp = tid / (ALF_CSH * ALF_CCH), ci = tid - ccomp * (ALF_CSH * ALF_CCH);
   const int cr = ci / ALF_CCH, cc = ci - cr * ALF_CCH;
@@ -218,7 +244,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
     // (a lane-indexed P.src[1 + ccomp] is a per-lane load of the descriptor, one more memory round trip)
     DPlane cs = P.src[1];
     cs.p = ccomp ? P.src[2].p : P.src[1].p;
-    if (ccomp < 2) cv = alf_chunk(cs, cx0 - 8 + 8 * cc, cy0 - 2 + cr);
+    if (ccomp < 2) cv = alf_chunk(cs, cx0 - 8 + 8 * cc, cy0 - 2 + cr, xl >> 1, xh >> 1, yl >> 1, yh >> 1);
   }
   const int ctbT = (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2);
   const int n = P.nctb;
