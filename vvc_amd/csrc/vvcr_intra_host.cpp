@@ -425,11 +425,19 @@ struct Planner {
 
   // ---- availability, as the reference evaluates it when the step runs (final order map: a unit is
   // decoded before step s iff order < s)
-  bool av(int ch, int x, int y, int sq, int reg) const {   // reg: the region of the step being resolved
+  // reg: the region of the step being resolved (low 32 bits) and, with WPP, its CTU column (high 32 bits:
+  // getCURestricted returns no CU at a CTU column beyond the current one, CodingStructure.cpp:1524-1528)
+  bool av(int ch, int x, int y, int sq, int64_t reg) const {
     const int pw = ch ? sp.width / 2 : sp.width, ph = ch ? sp.height / 2 : sp.height;
     if (x < 0 || y < 0 || x >= pw || y >= ph) return false;
     const int s = ch ? 1 : 2, cs = ch ? 1 : 0;
-    return order_of(ch, (size_t)(y >> s) * W4 + (x >> s)) < sq && region_at(x << cs, y << cs) == reg;
+    if (((x << cs) >> sp.ctu_log2) > (int)(reg >> 32)) return false;
+    return order_of(ch, (size_t)(y >> s) * W4 + (x >> s)) < sq && region_at(x << cs, y << cs) == (int)(uint32_t)reg;
+  }
+  // the availability key of a step at luma position (lx, ly)
+  int64_t av_key(int lx, int ly) const {
+    const int64_t col = pp.entropy_sync ? (lx >> sp.ctu_log2) : 0x7fffffff;
+    return (int64_t)(uint32_t)region_at(lx, ly) | col << 32;
   }
   // xFillReferenceSamples unit scan (IntraPrediction.cpp:913-986, isAboveAvailable etc. :1208-1310):
   // returns the 65-bit availability mask in (lo, hi)
@@ -437,7 +445,7 @@ struct Planner {
     bool prefix, corner;
     int nul, nut;
   };
-  void fill_mask(int ch, int sq, int reg, int fx, int fy, int fw, int fh, int predSize, int predHSize, uint64_t &lo, uint32_t &hi,
+  void fill_mask(int ch, int sq, int64_t reg, int fx, int fy, int fw, int fh, int predSize, int predHSize, uint64_t &lo, uint32_t &hi,
                  FillShape *shape = nullptr) const {
     const int uw = ch ? 2 : 4, uh = uw;
     const int totalAbove = (predSize + uw - 1) / uw, totalLeft = (predHSize + uh - 1) / uh;
@@ -466,7 +474,7 @@ struct Planner {
     }
   }
   // CCLM neighbourhood (above / left complete, above-right / below-left unit counts): 12 bits
-  uint32_t nb_bits(int ch, int sq, int reg, int x, int y, int w, int h, int unit) const {
+  uint32_t nb_bits(int ch, int sq, int64_t reg, int x, int y, int w, int h, int unit) const {
     const int na = w / unit, nl = h / unit;
     int l = 0, a = 0, bl = 0, ar = 0;
     while (l < nl && av(ch, x - 1, y + l * unit, sq, reg)) l++;
@@ -480,7 +488,7 @@ struct Planner {
   // (const: the steps resolve on several threads)
   void resolve_availability(IntraJob &j) const {
     const int comp = j.comp, ch = comp ? 1 : 0;
-    const int reg = region_at(j.cx << ch, j.cy << ch);
+    const int64_t reg = av_key(j.cx << ch, j.cy << ch);
     const bool isp = (j.flags & (IJ_ISP_HOR | IJ_ISP_VER)) != 0, ver = (j.flags & IJ_ISP_VER) != 0;
     uint64_t lo;
     uint32_t hi;
