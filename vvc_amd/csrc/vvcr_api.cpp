@@ -383,6 +383,7 @@ struct Lane {
   hipStream_t s = nullptr;
   ScratchSet set[MC_MAXPIC];
   DevVec<uint8_t> dbkp;              // device deblocking planner's maps and lists (allocated at its first use)
+  int dbkp_gen = 0;                  // generation of its maps' entries (0: the buffer is new, clear it)
   const void *held = nullptr;        // a picture launched stage by stage whose later stages are pending here
   int tail_slot = -1;                // DPB slot written by the lane's last picture
   uint64_t tail_seq = 0;             // launch sequence number of that picture
@@ -879,8 +880,10 @@ static DbkPlanArgs dbk_plan_args(vvcr_ctx *ctx, Lane &ln, const Prepared &r) {
   const size_t n4 = (size_t)W4 * H4, a4 = (n4 + 255) & ~(size_t)255;
   const size_t maps = 4 * a4 * sizeof(int32_t), state = 2 * a4, items = 4 * a4 * sizeof(uint32_t);
   const size_t lists = 4 * a4 * sizeof(DbkSeg);
+  const uint8_t *old = ln.dbkp.p;
   ln.dbkp.ensure(maps + state + items + lists + 256);
   uint8_t *p = ln.dbkp.p;
+  if (p != old) ln.dbkp_gen = 0;   // a new buffer: cleared with the next generation
   DbkPlanArgs a{};
   a.cu = r.dbcu.p; a.pu = r.dbpu.p; a.tu = r.dbtu.p; a.motion = r.n_dbmot ? r.dbmot.p : nullptr;
   a.ncu = r.n_dbcu; a.ntu = r.n_dbtu; a.W4 = W4; a.H4 = H4; a.ctu_log2 = sp.ctu_log2;
@@ -900,6 +903,10 @@ static DbkPlanArgs dbk_plan_args(vvcr_ctx *ctx, Lane &ln, const Prepared &r) {
   a.counts = (int32_t *)(p + maps + state + items + lists);
   for (int k = 0; k < 4; k++) a.nitems[k] = r.dbk_nitems[k];
   a.err = ctx->d_err + 1;
+  // the maps' generation: 1 .. 255, the maps cleared when it restarts
+  a.fill = ln.dbkp_gen == 0 || ln.dbkp_gen >= 255;
+  ln.dbkp_gen = a.fill ? 1 : ln.dbkp_gen + 1;
+  a.gen = ln.dbkp_gen;
   return a;
 }
 

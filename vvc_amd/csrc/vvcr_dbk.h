@@ -88,7 +88,12 @@ struct DbkPlanArgs {
   uint32_t *items;                      // the units on CU edge lines per pass and direction (k_dbkp_maps),
   int32_t nitems[4];                    // at items + (2 * pass + dir) * cap, their lengths (pack_dbk_inputs)
   int32_t *err;                         // bit 2: a map hole (inconsistent descriptors), bit 4: list overflow
+  // Map entries carry the generation of the picture that wrote them (gen << 24 | index; bit 23: an ISP CU's
+  // luma area, index = its first TU): an entry of another generation is a hole, so the maps are never
+  // cleared per picture. fill: clear them first (a new buffer, or the 8-bit generation wrapped).
+  int32_t gen, fill;
 };
+constexpr int DBKP_GEN_SHIFT = 24, DBKP_ISP = 1 << 23, DBKP_IDX_MASK = (1 << 23) - 1;
 void launch_dbk_plan(const DbkPlanArgs &a, hipStream_t s);
 
 // Filtering. segL / segC: the luma / chroma lists of direction dir at segs[dir][0 / 1]; counts (device):

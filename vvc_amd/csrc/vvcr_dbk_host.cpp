@@ -566,7 +566,7 @@ void pack_dbk_inputs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const
   if (pp.dbk_disable) return;
   if (sp.width % 8 || sp.height % 8) throw VvcrError(VVCR_E_UNSUPPORTED, "deblocking: picture size not a multiple of 8");
   const size_t ncu = d.cu.size(), npu = d.pu.size(), ntu = d.tu.size();
-  if (ncu > (size_t)INT32_MAX || ntu > (size_t)INT32_MAX) throw VvcrError(VVCR_E_ARG, "deblocking: too many coding units");
+  if (ncu > (size_t)DBKP_IDX_MASK || ntu > (size_t)DBKP_IDX_MASK) throw VvcrError(VVCR_E_ARG, "deblocking: too many coding units");
   out.cu.resize(ncu);
   out.pu.resize(npu);
   out.tu.resize(ntu);

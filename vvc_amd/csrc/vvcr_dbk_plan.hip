@@ -39,6 +39,13 @@ constexpr int MAXTU = 4;   // TUs of a CU (the 64-sample transform split of a 12
 
 __device__ __forceinline__ int cdiv(int a, int s) { return (a + (1 << s) - 1) >> s; }
 
+// a map entry of this picture's generation -> its index (an ISP CU's luma area: -(first TU) - 2), else -1
+__device__ __forceinline__ int map_val(const DbkPlanArgs &A, int32_t v) {
+  if ((int)((uint32_t)v >> DBKP_GEN_SHIFT) != A.gen) return -1;
+  const int i = v & DBKP_IDX_MASK;
+  return (v & DBKP_ISP) ? -i - 2 : i;
+}
+
 // the edge state of one unit and direction (the reference's per-CTU m_aapucBS / m_aapbEdgeFilter /
 // m_maxFilterLength* entries; chroma lengths of Cb only: Cr's equal them and are never read)
 struct UnitState {
@@ -230,10 +237,11 @@ struct Unit {
     // of loads each; their uses below are conditional)
     int mcu = 0, mcu1 = 0, mtu0 = 0, mtu1 = 0;
     if (!pin) {
-      mcu = R.ch ? A.cu_map[1][pu] : A.cu_map[0][pu];
-      mcu1 = A.cu_map[1][pu];
-      mtu0 = A.tu_map[0][pu];
-      mtu1 = A.tu_map[1][pu];
+      const int32_t v0 = A.cu_map[0][pu], v1 = A.cu_map[1][pu], t0 = A.tu_map[0][pu], t1 = A.tu_map[1][pu];
+      mcu1 = map_val(A, v1);
+      mcu = R.ch ? mcu1 : map_val(A, v0);
+      mtu0 = map_val(A, t0);
+      mtu1 = map_val(A, t1);
     }
     const DbCu &cPr = A.cu[max(mcu, 0)];
     const int fPm = pin ? 0 : (int)cPr.flags, qpPm = pin ? 0 : (int)cPr.qp;
@@ -412,16 +420,21 @@ __global__ __launch_bounds__(256) void k_dbkp_maps(DbkPlanArgs A) {
   __shared__ uint8_t s_line[4][2][32];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + wv;
+  // v: the index (bit 23: an ISP CU's luma area), tagged with the picture's generation
   auto fill = [&](int32_t *m, int x, int y, int w, int h, int s, int v, bool atomic) {
     const int x0 = x >> s, y0 = y >> s, nx = cdiv(x + w, s) - x0, ny = cdiv(y + h, s) - y0;
+    const int32_t e = (int32_t)((uint32_t)A.gen << DBKP_GEN_SHIFT | (uint32_t)v);
     for (int j = lane; j < nx * ny; j += 64) {
       int32_t *d = &m[(y0 + j / nx) * A.W4 + x0 + j % nx];
-      if (atomic) atomicMax(d, v);   // a later record wins where two cover a unit (the host planner's order)
-      else *d = v;
+      // a later record wins where two cover a unit (the host planner's order); an older generation's entry
+      // holds a smaller tag (unsigned: the generation is the top byte)
+      if (atomic) atomicMax((unsigned int *)d, (unsigned int)e);
+      else *d = e;
     }
   };
   if (i < A.ncu) {
     const DbCu &c = A.cu[i];
+    if (i > DBKP_IDX_MASK) { if (lane == 0) atomicOr(A.err, 4); return; }
     if (c.flags & DBC_YVALID) fill(A.cu_map[0], c.x, c.y, c.w, c.h, 2, i, true);
     if (c.flags & DBC_CVALID) fill(A.cu_map[1], c.cx, c.cy, c.cw, c.ch, 1, i, true);
     // the units on its edge lines (lines and list offsets from pack_dbk_inputs)
@@ -449,7 +462,7 @@ __global__ __launch_bounds__(256) void k_dbkp_maps(DbkPlanArgs A) {
     const int16_t *b0 = tu.b[0], *b1 = tu.b[1];
     if (b0[2] > 0 && b0[3] > 0) {
       if (c.flags & DBC_ISP) {
-        if (t == c.firsttu) fill(A.tu_map[0], c.x, c.y, c.w, c.h, 2, -t - 2, false);
+        if (t == c.firsttu) fill(A.tu_map[0], c.x, c.y, c.w, c.h, 2, DBKP_ISP | t, false);
       } else {
         fill(A.tu_map[0], b0[0], b0[1], b0[2], b0[3], 2, t, true);
       }
@@ -511,8 +524,9 @@ __global__ __launch_bounds__(256) void k_dbkp_units(DbkPlanArgs A) {
 
 void launch_dbk_plan(const DbkPlanArgs &a, hipStream_t s) {
   const size_t n4 = (size_t)a.W4 * a.H4;
-  // the four maps are one run (vvcr_api.cpp dbk_plan_args): one fill; the list lengths another
-  VVCR_CHECK_HIP(hipMemsetAsync(a.cu_map[0], 0xff, (size_t)((const char *)(a.tu_map[1] + n4) - (const char *)a.cu_map[0]), s));
+  // the four maps are one run (vvcr_api.cpp dbk_plan_args): cleared only when the generation restarts (a
+  // picture's entries are told from older ones by their tag); the list lengths every picture
+  if (a.fill) VVCR_CHECK_HIP(hipMemsetAsync(a.cu_map[0], 0, (size_t)((const char *)(a.tu_map[1] + n4) - (const char *)a.cu_map[0]), s));
   VVCR_CHECK_HIP(hipMemsetAsync(a.counts, 0, 4 * sizeof(int32_t), s));
   const bool local_dual = a.chroma_pass && !a.dual_tree;
   if (local_dual) VVCR_CHECK_HIP(hipMemsetAsync(a.state[0], 0, 2 * a.state_pitch, s));
