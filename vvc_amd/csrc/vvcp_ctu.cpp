@@ -4,7 +4,12 @@
 #include "vvcp_ctu.h"
 
 #include <algorithm>
+#include <atomic>
+#include <climits>
+#include <exception>
+#include <memory>
 #include <mutex>
+#include <thread>
 
 namespace vvcp {
 namespace {
@@ -321,7 +326,8 @@ struct CuCtx {   // CUCtx (ContextModelling.h:409)
 // The per-slice parser
 // ------------------------------------------------------------------------------------------------
 struct Parser {
-  PictureSyntax &pic;
+  PictureSyntax &pic;           // rows (CU / PU / TU, levels): the picture's, or a tile unit's own (parse_picture_data)
+  PictureSyntax &shp;           // the picture: maps, per-CTB loop-filter syntax, geometry
   const SliceCtx &sc;
   const SPS &sps;
   const PPS &pps;
@@ -337,8 +343,8 @@ struct Parser {
   int log2MaxTb, maxTb;
   int cuQpDeltaSubdiv, cuChromaQpOffsetSubdiv;
 
-  Parser(PictureSyntax &p, const SliceCtx &s)
-      : pic(p), sc(s), sps(*s.sps), pps(*s.pps), ph(*s.ph), sh(*s.sh) {
+  Parser(PictureSyntax &rows, PictureSyntax &shared, const SliceCtx &s)
+      : pic(rows), shp(shared), sc(s), sps(*s.sps), pps(*s.pps), ph(*s.ph), sh(*s.sh) {
     dualTree = sh.isIntra() && sps.dualTree;
     for (int k = 0; k < 3; k++) { minQT[k] = ph.minQT[k]; maxBTD[k] = ph.maxBTD[k]; maxBT[k] = ph.maxBT[k]; maxTT[k] = ph.maxTT[k]; }
     log2MaxTb = sps.log2MaxTb;
@@ -352,12 +358,15 @@ struct Parser {
   int minBtSize() const { return 1 << sps.log2MinCb; }
 
   // ---- maps ----
-  int cuAt(int ch, int x, int y) const { return pic.cuAt(ch, x, y); }
-  // CodingStructure::getCURestricted (CodingStructure.cpp:1519/1539): same slice and tile
+  int cuAt(int ch, int x, int y) const { return shp.cuAt(ch, x, y); }
+  // CodingStructure::getCURestricted (CodingStructure.cpp:1519/1539): same slice and tile. The tile is
+  // checked by position before the map is read: another tile's entries may belong to another unit's rows.
   int cuRestricted(int ch, int x, int y, int slice, int tile) const {
+    const int lx = ch ? x << 1 : x, ly = ch ? y << 1 : y;
+    if (lx < 0 || ly < 0 || lx >= shp.W || ly >= shp.H || tileOf(lx, ly) != tile) return -1;
     const int c = cuAt(ch, x, y);
     if (c < 0) return -1;
-    return (pic.cux[c].slice == slice && pic.cux[c].tile == tile) ? c : -1;
+    return pic.cux[c].slice == slice ? c : -1;
   }
   int tileOf(int lx, int ly) const {
     return pps.tileIdx(lx >> pic.ctuLog2, ly >> pic.ctuLog2);
@@ -366,7 +375,7 @@ struct Parser {
     const int x0 = lx >> 2, y0 = ly >> 2;
     const int x1 = std::min(pic.w4, (lx + lw + 3) >> 2), y1 = std::min(pic.h4, (ly + lh + 3) >> 2);
     for (int y = y0; y < y1; y++)
-      for (int x = x0; x < x1; x++) pic.map[ch][(size_t)y * pic.w4 + x] = cuIdx;
+      for (int x = x0; x < x1; x++) shp.map[ch][(size_t)y * pic.w4 + x] = cuIdx;
   }
 
   // ------------------------------------------------------------------------------------------------
@@ -707,9 +716,9 @@ struct Parser {
     const int idx = (int)pic.cu.size();
     pic.cu.push_back(c);
     pic.cux.push_back(x);
-    if (yv != cv) pic.unshareMap();
+    if (yv != cv) shp.unshareMap();
     if (yv) fill_map(0, idx, a.x, a.y, a.w, a.h);
-    if (cv && !pic.mapShared) fill_map(1, idx, a.x, a.y, a.w, a.h);
+    if (cv && !shp.mapShared) fill_map(1, idx, a.x, a.y, a.w, a.h);
 
     int lumaQPinLocalDualTree = -1;
     if (cuCtx.qgStart) { cuCtx.qgStart = false; cuCtx.qp = predictQP(idx, cuCtx.qp); }
@@ -774,9 +783,10 @@ struct Parser {
     const CuAux &x = pic.cux[idx];
     const int ctuX = x.ctu % pic.wCtu;
     const int tileX = pps.colBd[pps.ctuToTileCol[ctuX]];
-    const int above = cuAt(ch, bx, by - 1);
-    if (ctuX == tileX && !(bx & mask) && !(by & mask) && above >= 0 && pic.cux[above].slice == x.slice && pic.cux[above].tile == x.tile)
-      return pic.cu[above].qp;
+    if (ctuX == tileX && !(bx & mask) && !(by & mask)) {
+      const int above = cuRestricted(ch, bx, by - 1, x.slice, x.tile);
+      if (above >= 0) return pic.cu[above].qp;
+    }
     const int a = (by & mask) ? pic.cu[cuAt(ch, bx, by - 1)].qp : prevQP;
     const int b = (bx & mask) ? pic.cu[cuAt(ch, bx - 1, by)].qp : prevQP;
     return (a + b + 1) >> 1;
@@ -1943,7 +1953,7 @@ struct Parser {
   // CTU level: coding_tree_unit (:136), sao (:318), ALF / CC-ALF CTB flags
   // ------------------------------------------------------------------------------------------------
   void sao(int ctu) {
-    vvcr_sao *s = &pic.sao[(size_t)ctu * 3];
+    vvcr_sao *s = &shp.sao[(size_t)ctu * 3];
     for (int c = 0; c < 3; c++) s[c].mode = 0;
     if (!sps.sao) return;
     const bool lumaF = sh.sao[0], chromaF = sh.sao[1];
@@ -2002,7 +2012,7 @@ struct Parser {
       const int left = la ? ctu - 1 : -1, above = aa ? ctu - pic.wCtu : -1;
       for (int comp = 0; comp < 3; comp++) {
         if (!sh.alf[comp]) continue;
-        std::vector<uint8_t> &en = pic.alfEn[comp];
+        std::vector<uint8_t> &en = shp.alfEn[comp];
         int ctx = (left >= 0 && en[left] ? 1 : 0) + (above >= 0 && en[above] ? 1 : 0);
         en[ctu] = (uint8_t)cab.bin(ctbAlfFlag + comp * 3 + ctx);
         if (comp == 0 && en[ctu]) {   // readAlfCtuFilterIndex (:245)
@@ -2014,17 +2024,17 @@ struct Parser {
               idx += 16;
             } else idx = truncBin(16);
           } else idx = truncBin(16);
-          pic.alfFset[ctu] = (int16_t)idx;
+          shp.alfFset[ctu] = (int16_t)idx;
         }
         if (comp > 0) {
           const APS &aps = sc.ps->alfAps[sh.alfApsChroma];
           VVCP_CHECK(!sc.ps->alfValid[sh.alfApsChroma], "chroma ALF APS missing");
           const int numAlts = aps.alf.numAltChroma;
-          pic.alfAlt[comp][ctu] = 0;
+          shp.alfAlt[comp][ctu] = 0;
           if (en[ctu]) {
             uint8_t d = 0;
             while (d < numAlts - 1 && cab.bin(ctbAlfAlternative + comp - 1)) ++d;
-            pic.alfAlt[comp][ctu] = d;
+            shp.alfAlt[comp][ctu] = d;
           }
         }
       }
@@ -2036,7 +2046,7 @@ struct Parser {
         const int count = sc.ps->alfAps[sh.ccAlfApsId[comp - 1]].alf.ccCount[comp - 1];
         const bool la = cuRestricted(0, px - pic.ctuSize, py, sc.sliceIdx, curTile) >= 0;
         const bool aa = cuRestricted(0, px, py - pic.ctuSize, sc.sliceIdx, curTile) >= 0;
-        std::vector<uint8_t> &ctl = pic.ccCtl[comp - 1];
+        std::vector<uint8_t> &ctl = shp.ccCtl[comp - 1];
         int ctx = 0;
         if (la) ctx += ctl[ctu - 1] ? 1 : 0;
         if (aa) ctx += ctl[ctu - pic.wCtu] ? 1 : 0;
@@ -2086,8 +2096,9 @@ struct Parser {
     cab.init_contexts(sh.qp, t);
   }
 
-  // DecSlice::decompressSlice (DecSlice.cpp:73)
-  void run(const uint8_t *data, size_t n, const std::vector<uint32_t> &nal_epb) {
+  // DecSlice::decompressSlice (DecSlice.cpp:73) over the slice's CTUs [i0, i1) (indices into sh.ctus),
+  // the first of which starts substream ss (a tile start, or the slice's first CTU)
+  void run(const uint8_t *data, size_t n, const std::vector<uint32_t> &nal_epb, int i0, int i1, size_t ss) {
     // substream boundaries: entry points count emulation-prevention bytes (VLCReader.cpp:3316-3349)
     std::vector<size_t> starts;
     {
@@ -2108,10 +2119,10 @@ struct Parser {
       }
     }
     VVCP_CHECK(starts.back() > n, "entry point beyond the slice data");
-    size_t ss = 0;
+    VVCP_CHECK(ss >= starts.size(), "missing entry point");
     auto substreamEnd = [&](size_t k) { return k + 1 < starts.size() ? starts[k + 1] : n; };
     init_ctx();
-    cab.start(data + starts[0], data + substreamEnd(0));
+    cab.start(data + starts[ss], data + substreamEnd(ss));
     int qps[2] = {sh.qp, sh.qp};
     const int nCtu = (int)sh.ctus.size();
     const bool wpp = pps.entropySync;
@@ -2119,7 +2130,7 @@ struct Parser {
     // next row's first CTU starts from when the CTU above it is in the same slice and tile
     // (DecSlice.cpp:160-176, stored at :214-219)
     std::vector<CtxModel> syncCtx;
-    for (int i = 0; i < nCtu; i++) {
+    for (int i = i0; i < i1; i++) {
       const int ctu = sh.ctus[i];
       const int cx = ctu % pic.wCtu, cy = ctu / pic.wCtu;
       const int tc = pps.ctuToTileCol[cx], tr = pps.ctuToTileRow[cy];
@@ -2128,13 +2139,13 @@ struct Parser {
       curTile = pps.tileIdx(cx, cy);
       curCtu = ctu;
       if (cx == tx0 && cy == ty0) {
-        if (i != 0) {
+        if (i != i0) {
           init_ctx();
           cab.start(data + starts[ss], data + substreamEnd(ss));
         }
         qps[0] = qps[1] = sh.qp;
       } else if (cx == tx0 && wpp) {
-        if (i != 0) {
+        if (i != i0) {
           init_ctx();
           cab.start(data + starts[ss], data + substreamEnd(ss));
         }
@@ -2186,6 +2197,14 @@ void PictureSyntax::reset(int W_, int H_, int ctuLog2_, bool intra) {
   alfFset.assign(n, 0);
 }
 
+void PictureSyntax::reset_rows(const PictureSyntax &o, size_t samples) {
+  W = o.W; H = o.H; ctuLog2 = o.ctuLog2; ctuSize = o.ctuSize; wCtu = o.wCtu; hCtu = o.hCtu; w4 = o.w4; h4 = o.h4;
+  cu.clear(); cux.clear(); pu.clear(); pux.clear(); tu.clear(); coef.clear(); box.clear();
+  coef.reserve(samples / 4 + 4096);
+  const size_t rows = samples / 64 + 256;
+  cu.reserve(rows); cux.reserve(rows); pu.reserve(rows); pux.reserve(rows); tu.reserve(rows + rows / 2);
+}
+
 void PictureSyntax::dense_rows(std::vector<vvcr_tu> &tus, std::vector<int32_t> &pool) const {
   tus.assign(tu.begin(), tu.end());
   size_t n = 0;
@@ -2213,8 +2232,135 @@ int PictureSyntax::cuAt(int ch, int x, int y) const {
 }
 
 void parse_slice_data(PictureSyntax &pic, const SliceCtx &sc, const uint8_t *rbsp, size_t n, const std::vector<uint32_t> &nal_epb) {
-  Parser p(pic, sc);
-  p.run(rbsp, n, nal_epb);
+  Parser p(pic, pic, sc);
+  p.run(rbsp, n, nal_epb, 0, (int)sc.sh->ctus.size(), 0);
+}
+
+namespace {
+
+struct Segment { int slice, i0, i1, ss; };   // the slice's CTUs [i0, i1), starting substream ss
+
+// The slice's CTUs split at tile starts, with the substream each piece starts (the counting of Parser::run)
+void slice_segments(const PictureSyntax &pic, const SliceCtx &sc, int s, std::vector<Segment> &out) {
+  const PPS &pps = *sc.pps;
+  const SliceHeader &sh = *sc.sh;
+  const int nCtu = (int)sh.ctus.size();
+  int ss = 0;
+  for (int i = 0; i < nCtu; i++) {
+    const int ctu = sh.ctus[i], cx = ctu % pic.wCtu, cy = ctu / pic.wCtu;
+    const int tc = pps.ctuToTileCol[cx], tr = pps.ctuToTileRow[cy];
+    const int tx0 = pps.colBd[tc], ty0 = pps.rowBd[tr];
+    if (i == 0 || (cx == tx0 && cy == ty0)) {
+      if (i) out.back().i1 = i;
+      out.push_back({s, i, nCtu, ss});
+    }
+    if (cx + 1 == pps.colBd[tc + 1] && (cy + 1 == pps.rowBd[tr + 1] || pps.entropySync)) ss++;
+  }
+}
+
+// Appends a unit's rows to the picture's: CU / PU / TU indices and level offsets move by the rows before
+// them, and so do the map entries of the unit's CTUs
+void append_rows(PictureSyntax &pic, PictureSyntax &L, const std::vector<SliceData> &slices, const std::vector<Segment> &segs) {
+  const int32_t cuOff = (int32_t)pic.cu.size(), puOff = (int32_t)pic.pu.size(), tuOff = (int32_t)pic.tu.size();
+  const int32_t coefOff = (int32_t)pic.coef.size();
+  VVCP_CHECK(pic.cu.size() + L.cu.size() > (size_t)INT32_MAX / 2 || pic.coef.size() + L.coef.size() > (size_t)INT32_MAX, "picture rows overflow");
+  for (vvcr_cu &c : L.cu) {
+    if (c.firstpu >= 0) c.firstpu += puOff;
+    if (c.firsttu >= 0) c.firsttu += tuOff;
+  }
+  for (vvcr_pu &u : L.pu) u.cu += cuOff;
+  for (vvcr_tu &t : L.tu) {
+    t.cu += cuOff;
+    for (int c = 0; c < 3; c++)
+      if (t.b[c][6] >= 0) t.b[c][6] += coefOff;
+  }
+  pic.cu.insert(pic.cu.end(), L.cu.begin(), L.cu.end());
+  pic.cux.insert(pic.cux.end(), L.cux.begin(), L.cux.end());
+  pic.pu.insert(pic.pu.end(), L.pu.begin(), L.pu.end());
+  pic.pux.insert(pic.pux.end(), L.pux.begin(), L.pux.end());
+  pic.tu.insert(pic.tu.end(), L.tu.begin(), L.tu.end());
+  pic.box.resize(3 * (size_t)tuOff, 0);
+  L.box.resize(3 * L.tu.size(), 0);
+  pic.box.insert(pic.box.end(), L.box.begin(), L.box.end());
+  pic.coef.insert(pic.coef.end(), L.coef.begin(), L.coef.end());
+  const int s4 = pic.ctuSize >> 2;
+  for (const Segment &g : segs)
+    for (int i = g.i0; i < g.i1; i++) {
+      const int ctu = slices[g.slice].sc.sh->ctus[i];
+      const int x0 = (ctu % pic.wCtu) * s4, y0 = (ctu / pic.wCtu) * s4;
+      const int x1 = std::min(pic.w4, x0 + s4), y1 = std::min(pic.h4, y0 + s4);
+      for (int ch = 0; ch < 2; ch++)
+        for (int y = y0; y < y1; y++) {
+          int32_t *m = pic.map[ch].data() + (size_t)y * pic.w4;
+          for (int x = x0; x < x1; x++)
+            if (m[x] >= 0) m[x] += cuOff;
+        }
+    }
+}
+
+}  // namespace
+
+void parse_picture_data(PictureSyntax &pic, const std::vector<SliceData> &slices, int threads) {
+  // units of work whose CTUs lie in tiles no other unit touches: each tile of a multi-tile slice (whole tiles,
+  // no CABAC or availability dependence between them), or the slices inside one tile together
+  struct Unit { std::vector<Segment> segs; int tile; bool whole; size_t ctus; };
+  std::vector<Unit> units;
+  std::vector<Segment> segs;
+  for (size_t s = 0; s < slices.size(); s++) {
+    const SliceCtx &sc = slices[s].sc;
+    if (sc.sh->ctus.empty()) continue;
+    segs.clear();
+    slice_segments(pic, sc, (int)s, segs);
+    for (const Segment &g : segs) {
+      const int ctu = sc.sh->ctus[g.i0];
+      const int tile = sc.pps->tileIdx(ctu % pic.wCtu, ctu / pic.wCtu);
+      const bool whole = segs.size() > 1;
+      if (!whole && !units.empty() && !units.back().whole && units.back().tile == tile) units.back().segs.push_back(g);
+      else units.push_back({{g}, tile, whole, 0});
+      units.back().ctus += (size_t)(g.i1 - g.i0);
+    }
+  }
+  auto parse_unit = [&](PictureSyntax &rows, const Unit &u) {
+    for (const Segment &g : u.segs) {
+      const SliceData &d = slices[g.slice];
+      Parser p(rows, pic, d.sc);
+      p.run(d.rbsp, d.n, *d.epb, g.i0, g.i1, (size_t)g.ss);
+    }
+  };
+  const int nu = (int)units.size();
+  if (threads <= 1 || nu <= 1) {
+    for (const Unit &u : units) parse_unit(pic, u);
+    return;
+  }
+  pic.unshareMap();   // the channels' maps are written by every unit: no unit may copy one while others fill it
+  std::vector<std::unique_ptr<PictureSyntax>> loc(nu);
+  const size_t ctuArea = (size_t)pic.ctuSize * pic.ctuSize;
+  for (int u = 1; u < nu; u++) {
+    loc[u].reset(new PictureSyntax());
+    loc[u]->reset_rows(pic, units[u].ctus * ctuArea);
+  }
+  std::vector<std::exception_ptr> err(nu);
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    for (int u; (u = next.fetch_add(1)) < nu;) {
+      try {
+        parse_unit(u ? *loc[u] : pic, units[u]);
+      } catch (...) {
+        err[u] = std::current_exception();
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  const int nt = std::min(threads, nu);
+  for (int t = 1; t < nt; t++) pool.emplace_back(work);
+  work();
+  for (std::thread &t : pool) t.join();
+  for (int u = 0; u < nu; u++)
+    if (err[u]) std::rethrow_exception(err[u]);
+  for (int u = 1; u < nu; u++) {
+    append_rows(pic, *loc[u], slices, units[u].segs);
+    loc[u].reset();
+  }
 }
 
 void finish_picture_syntax(PictureSyntax &pic, int bitDepth) {

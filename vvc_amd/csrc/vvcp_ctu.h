@@ -57,6 +57,8 @@ struct PictureSyntax {
   std::vector<uint8_t> alfEn[3], alfAlt[3], ccCtl[2];
   std::vector<int16_t> alfFset;
   void reset(int W, int H, int ctuLog2, bool intra = false);
+  // a tile unit's rows (parse_picture_data): o's geometry, empty rows with room for `samples` luma samples
+  void reset_rows(const PictureSyntax &o, size_t samples);
   void dense_rows(std::vector<vvcr_tu> &tus, std::vector<int32_t> &pool) const;
   int cuAt(int ch, int x, int y) const;   // x, y in samples of channel ch; -1 outside / not decoded
 };
@@ -75,6 +77,17 @@ struct SliceCtx {
 // nal_epb: emulation-prevention positions of the NAL (entry points count them).
 void parse_slice_data(PictureSyntax &pic, const SliceCtx &sc, const uint8_t *rbsp, size_t n,
                       const std::vector<uint32_t> &nal_epb);
+// All slices of a picture. With threads > 1 the picture's tiles are parsed in parallel: each tile of a
+// multi-tile slice, or the slices inside one tile together, is a unit with rows of its own (the picture's
+// maps and per-CTB syntax are shared: units write disjoint CTUs, and read only their own tiles'), merged
+// in decoding order afterwards. The rows equal those of parse_slice_data over the slices in order.
+struct SliceData {
+  SliceCtx sc;
+  const uint8_t *rbsp;
+  size_t n;
+  const std::vector<uint32_t> *epb;
+};
+void parse_picture_data(PictureSyntax &pic, const std::vector<SliceData> &slices, int threads);
 // After the last slice: SAO merge resolution and de-quantisation (SampleAdaptiveOffset.cpp:148-264)
 void finish_picture_syntax(PictureSyntax &pic, int bitDepth);
 

@@ -3,6 +3,7 @@
 #include "vvcp_stream.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "vvcp.h"
@@ -161,6 +162,17 @@ void Stream::open(const uint8_t *d, size_t n) {
   }
 }
 
+// Threads of a picture's tile-parallel CABAC pass (parse_picture_data): VVCP_TILE_THREADS, default 8; 1 parses
+// the tiles in order on the calling thread
+static int tile_threads() {
+  static const int n = [] {
+    const char *e = std::getenv("VVCP_TILE_THREADS");
+    const int v = e ? std::atoi(e) : 8;
+    return std::max(1, std::min(v, 64));
+  }();
+  return n;
+}
+
 void Stream::parse_picture(int idx) {
   PictureUnit &p = *pics.at(idx);
   if (p.parsed) {
@@ -174,11 +186,12 @@ void Stream::parse_picture(int idx) {
   for (int i = 0; i < 8; i++) { ps.alfAps[i] = p.alfAps[i]; ps.alfValid[i] = p.alfValid[i]; }
   for (int i = 0; i < 4; i++) { ps.lmcsAps[i] = p.lmcsAps[i]; ps.lmcsValid[i] = p.lmcsValid[i]; }
   try {
+    std::vector<SliceData> sd;
     for (size_t s = 0; s < p.slices.size(); s++) {
       const Nal &nal = nals[p.sliceNal[s]];
-      SliceCtx sc{&p.sps, &p.pps, &p.ph, &p.slices[s], &ps, (int)s};
-      parse_slice_data(p.syn, sc, nal.rbsp.data(), nal.rbsp.size(), nal.epb);
+      sd.push_back({SliceCtx{&p.sps, &p.pps, &p.ph, &p.slices[s], &ps, (int)s}, nal.rbsp.data(), nal.rbsp.size(), &nal.epb});
     }
+    parse_picture_data(p.syn, sd, tile_threads());
   } catch (...) {
     p.parsed = true;   // the rows parsed so far stay readable (diagnostics)
     p.failed = true;

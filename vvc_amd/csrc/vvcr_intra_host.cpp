@@ -10,6 +10,7 @@
 #include "vvcr_intra.h"
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <queue>
@@ -103,12 +104,18 @@ struct Planner {
   // per unit of channel ch: decoding order (seq), level, and the steps (indices into jobs) that reconstruct
   // it: prod[0] luma (ch 0) or Cb, prod[1] Cr (ch 1)
   struct UnitRec { int32_t order, level, prod[2]; };
-  bigbuf::raw<UnitRec> ur[2];
+  // The per-unit / per-CU / per-CTU arrays are shared with the region planners of a tiled picture (run:
+  // each plans the CTUs of one tile / slice, writes only its own CUs' and units' entries and reads no
+  // other region's): the planner that owns them holds the storage (*_store), every planner the pointers.
+  bigbuf::raw<UnitRec> ur_store[2];
+  UnitRec *ur[2] = {nullptr, nullptr};
   static int pslot(int comp) { return comp == 2 ? 1 : 0; }
   const int32_t *umap[2] = {nullptr, nullptr};
   bigbuf::vec<int32_t> own_map[2];
-  bigbuf::vec<int32_t> cu_seq;      // per CU: the seq of a plain inter CU, kInf until planned
-  bigbuf::vec<uint8_t> written[2];  // per CU and channel: its units carry their own order / level / producers
+  bigbuf::vec<int32_t> cu_seq_store;
+  int32_t *cu_seq = nullptr;        // per CU: the seq of a plain inter CU, kInf until planned
+  bigbuf::vec<uint8_t> written_store[2];
+  uint8_t *written[2] = {nullptr, nullptr};   // per CU and channel: its units carry their own order / level / producers
   static constexpr int32_t kInf = 1 << 30;
   int32_t order_of(int ch, size_t i) const {
     const int32_t m = umap[ch][i];
@@ -144,7 +151,8 @@ struct Planner {
   // Slice / tile of every CTU (getCURestricted: a neighbour is usable only inside the same slice and
   // tile, CodingStructure.cpp:1519-1537, CU::isSameSliceAndTile UnitTools.cpp:170); cur_reg is the
   // region of the CU being planned / the step being resolved.
-  bigbuf::vec<int32_t> ctu_reg;
+  bigbuf::vec<int32_t> ctu_reg_store;
+  const int32_t *ctu_reg = nullptr;
   int wc = 1, cur_reg = 0;
   int region_at(int lx, int ly) const { return ctu_reg[(size_t)(ly >> sp.ctu_log2) * wc + (lx >> sp.ctu_log2)]; }
 
@@ -171,14 +179,14 @@ struct Planner {
     bool regok = false;
     for (int uy = y0 >> s; uy <= (y1 >> s); uy++)
       for (int ux = x0 >> s; ux <= (x1 >> s); ux++) {
+        const int c = (uy >> lg) * wc + (ux >> lg);   // the region first: another region's units are not read
+        if (c != lastc) { lastc = c; regok = ctu_reg[c] == cur_reg; }
+        if (!regok) continue;
         const size_t i = (size_t)uy * W4 + ux;
         const int32_t cu = umap[ch][i];
         if (cu < 0 || !written[ch][cu]) continue;
         const UnitRec &r = ur[ch][i];
         if (r.order >= seq) continue;
-        const int c = (uy >> lg) * wc + (ux >> lg);
-        if (c != lastc) { lastc = c; regok = ctu_reg[c] == cur_reg; }
-        if (!regok) continue;
         m = std::max(m, r.level);
         const int32_t pr = r.prod[pslot(comp)];
         if (pr >= 0) add_dep(pr);
@@ -531,6 +539,94 @@ struct Planner {
     }
   }
 
+  // the CUs of CTUs ks (raster order) in decoding order per CTU (start / order: CSR over the CTUs)
+  void plan_ctus(const std::vector<int> &ks, const std::vector<int> &start, const std::vector<int> &order) {
+    for (int k : ks)
+      for (int pass = 0; pass < (pp.dual_tree ? 2 : 1); pass++)
+        for (int jx = start[k]; jx < start[k + 1]; jx++) {
+          const int i = order[jx];
+          const vvcr_cu &c = d.cu[i];
+          if (pp.dual_tree && c.chtype != pass) continue;
+          if (!in_shard(pp, c)) continue;   // another shard reconstructs it (different tile: never read here)
+          cur_reg = ctu_reg[k];
+          if (c.predmode == MODE_INTER) {
+            inter_cu(i);
+          } else if (c.predmode == MODE_INTRA) {
+            if (c.yvalid) intra_luma(i);
+            if (c.cvalid) intra_chroma(i);
+          } else {
+            throw VvcrError(VVCR_E_UNSUPPORTED, "IBC / palette CUs are not supported");
+          }
+        }
+  }
+
+  // Steps of every CTU with their dependencies. Nothing crosses a region (tile and slice: every neighbour
+  // read is getCURestricted's), so with several regions each is planned by a planner of its own on
+  // VVCR_PLAN_THREADS threads, sharing the unit / CU arrays, and their steps are appended region by region
+  // (dependency indices moved by the steps before them); a CTU's steps stay contiguous, each region's are
+  // in raster order of its CTUs. The steps equal the sequential plan's up to that order and the seq
+  // numbers, which only order units inside one region.
+  void plan_regions(const std::vector<int> &start, const std::vector<int> &order) {
+    const int nctu = wc * ((sp.height + ctu - 1) / ctu);
+    std::vector<std::vector<int>> groups;
+    {
+      std::vector<std::pair<int32_t, int>> key(nctu);
+      for (int k = 0; k < nctu; k++) key[k] = {ctu_reg[k], k};
+      std::stable_sort(key.begin(), key.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+      for (int q = 0; q < nctu; q++) {
+        if (q == 0 || key[q].first != key[q - 1].first) groups.emplace_back();
+        groups.back().push_back(key[q].second);
+      }
+    }
+    const int ng = (int)groups.size();
+    if (ng <= 1 || plan_threads() <= 1) {
+      std::vector<int> all(nctu);
+      for (int k = 0; k < nctu; k++) all[k] = k;
+      plan_ctus(all, start, order);
+      return;
+    }
+    std::sort(groups.begin(), groups.end(), [](const auto &a, const auto &b) { return a[0] < b[0]; });
+    std::vector<std::unique_ptr<IntraPlan>> outs(ng);
+    std::vector<std::unique_ptr<Planner>> subs(ng);
+    for (int g = 0; g < ng; g++) {
+      outs[g].reset(new IntraPlan());
+      subs[g].reset(new Planner(sp, pp, d, *outs[g]));
+      Planner &P = *subs[g];
+      P.cscale = cscale; P.fuse = fuse; P.wc = wc; P.ctu_reg = ctu_reg; P.cu_seq = cu_seq;
+      for (int k = 0; k < 2; k++) { P.umap[k] = umap[k]; P.ur[k] = ur[k]; P.written[k] = written[k]; }
+    }
+    std::vector<std::exception_ptr> err(ng);
+    std::atomic<int> next{0};
+    auto work = [&]() {
+      for (int g; (g = next.fetch_add(1)) < ng;) {
+        try {
+          subs[g]->plan_ctus(groups[g], start, order);
+        } catch (...) {
+          err[g] = std::current_exception();
+        }
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < std::min(plan_threads(), ng); t++) th.emplace_back(work);
+    work();
+    for (std::thread &t : th) t.join();
+    for (const std::exception_ptr &e : err)
+      if (e) std::rethrow_exception(e);
+    for (int g = 0; g < ng; g++) {
+      Planner &P = *subs[g];
+      const int32_t jbase = (int32_t)jobs.size(), dbase = (int32_t)dep_flat.size();
+      jobs.insert(jobs.end(), P.jobs.begin(), P.jobs.end());
+      for (int32_t v : P.dep_flat) dep_flat.push_back(v + jbase);
+      for (size_t i = 1; i < P.dep_off.size(); i++) dep_off.push_back(dbase + P.dep_off[i]);
+      out.inter_tiles.insert(out.inter_tiles.end(), outs[g]->inter_tiles.begin(), outs[g]->inter_tiles.end());
+    }
+  }
+
+  static int plan_threads() {
+    static const int n = [] { const char *e = getenv("VVCR_PLAN_THREADS"); return e ? std::max(1, atoi(e)) : 4; }();
+    return n;
+  }
+
   void run() {
     static const bool prof = getenv("VVCR_PLAN_PROF") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
@@ -543,9 +639,10 @@ struct Planner {
     const size_t nu = (size_t)W4 * H4;
     // per-unit arrays without initialisation: only the units of written CUs are read (touch)
     // (resize would zero 7 arrays of a unit each per picture, 14 MB at 4K, for the few units a B picture plans)
-    for (int k = 0; k < 2; k++) ur[k].alloc(nu, false);
-    cu_seq.assign(d.cu.size(), kInf);
-    for (int k = 0; k < 2; k++) written[k].assign(d.cu.size(), 0);
+    for (int k = 0; k < 2; k++) { ur_store[k].alloc(nu, false); ur[k] = ur_store[k].p; }
+    cu_seq_store.assign(d.cu.size(), kInf);
+    cu_seq = cu_seq_store.data();
+    for (int k = 0; k < 2; k++) { written_store[k].assign(d.cu.size(), 0); written[k] = written_store[k].data(); }
     for (int k = 0; k < 2; k++) {
       if (d.cu_map[k].size() == nu) {   // the producer's CU maps (the host parser hands them over)
         umap[k] = d.cu_map[k].data();
@@ -576,14 +673,15 @@ struct Planner {
       if (pp.num_tile_rows > 0)
         for (int t = 0; t < ntr; t++)
           for (int y = pp.tile_row_bd[t]; y < pp.tile_row_bd[t + 1] && y < hc; y++) trow[y] = t;
-      ctu_reg.assign((size_t)wc * hc, 0);
+      ctu_reg_store.assign((size_t)wc * hc, 0);
       for (int y = 0; y < hc; y++)
-        for (int x = 0; x < wc; x++) ctu_reg[(size_t)y * wc + x] = (trow[y] * ntc + tcol[x]) << 16;
+        for (int x = 0; x < wc; x++) ctu_reg_store[(size_t)y * wc + x] = (trow[y] * ntc + tcol[x]) << 16;
       for (const vvcr_cu &c : d.cu) {
         const int x = c.yvalid ? c.x : 2 * c.cx, y = c.yvalid ? c.y : 2 * c.cy;
-        int32_t &r = ctu_reg[(size_t)(y >> sp.ctu_log2) * wc + (x >> sp.ctu_log2)];
+        int32_t &r = ctu_reg_store[(size_t)(y >> sp.ctu_log2) * wc + (x >> sp.ctu_log2)];
         r = (r & ~0xffff) | (c.slice & 0xffff);
       }
+      ctu_reg = ctu_reg_store.data();
     }
     std::vector<int> start((size_t)wc * hc + 1, 0), order(ncu), ctu_of(ncu);
     for (int i = 0; i < ncu; i++) {
@@ -597,23 +695,7 @@ struct Planner {
       std::vector<int> pos(start);
       for (int i = 0; i < ncu; i++) order[pos[ctu_of[i]]++] = i;
     }
-    for (int k = 0; k < wc * hc; k++)
-      for (int pass = 0; pass < (pp.dual_tree ? 2 : 1); pass++)
-        for (int jx = start[k]; jx < start[k + 1]; jx++) {
-          const int i = order[jx];
-          const vvcr_cu &c = d.cu[i];
-          if (pp.dual_tree && c.chtype != pass) continue;
-          if (!in_shard(pp, c)) continue;   // another shard reconstructs it (different tile: never read here)
-          cur_reg = ctu_reg[k];
-          if (c.predmode == MODE_INTER) {
-            inter_cu(i);
-          } else if (c.predmode == MODE_INTRA) {
-            if (c.yvalid) intra_luma(i);
-            if (c.cvalid) intra_chroma(i);
-          } else {
-            throw VvcrError(VVCR_E_UNSUPPORTED, "IBC / palette CUs are not supported");
-          }
-        }
+    plan_regions(start, order);
     PROF_MARK("jobs");
     // Steps grouped by CTU (raster order), inside a CTU by level: a topological order of the dependency
     // graph (every dependency is in the same CTU at a lower level, or in an earlier CTU — the left /
@@ -622,12 +704,17 @@ struct Planner {
     // the producing step is flagged IJ_PUBLISH (drains its global stores and raises a global flag).
     const int nj = (int)jobs.size();
     std::vector<int32_t> ctu_of_job(nj);
-    for (int i = 0; i < nj; i++) {
-      const IntraJob &j = jobs[i].second;
-      const int s = j.comp ? 1 : 0;
-      const int lx = j.cx << s, ly = j.cy << s;   // CU position in luma samples (a CU never crosses a CTU)
-      ctu_of_job[i] = (ly >> sp.ctu_log2) * wc + (lx >> sp.ctu_log2);
-      if (i && ctu_of_job[i] < ctu_of_job[i - 1]) throw VvcrError(VVCR_E_STATE, "intra plan: steps not created in CTU order");
+    {
+      std::vector<uint8_t> seen((size_t)wc * hc, 0);
+      for (int i = 0; i < nj; i++) {
+        const IntraJob &j = jobs[i].second;
+        const int s = j.comp ? 1 : 0;
+        const int lx = j.cx << s, ly = j.cy << s;   // CU position in luma samples (a CU never crosses a CTU)
+        ctu_of_job[i] = (ly >> sp.ctu_log2) * wc + (lx >> sp.ctu_log2);
+        if (i && ctu_of_job[i] == ctu_of_job[i - 1]) continue;
+        if (seen[ctu_of_job[i]]) throw VvcrError(VVCR_E_STATE, "intra plan: a CTU's steps are not contiguous");
+        seen[ctu_of_job[i]] = 1;
+      }
     }
     // the steps of one CTU are contiguous in creation order: blocks [cb[k], cb[k+1])
     std::vector<int32_t> cb;
@@ -843,7 +930,7 @@ struct Planner {
         set_pred_params(j);
       }
     };
-    static const int nthr = [] { const char *e = getenv("VVCR_PLAN_THREADS"); return e ? std::max(1, atoi(e)) : 4; }();
+    const int nthr = plan_threads();
     const size_t njobs = out.jobs.size();
     if (njobs >= 16384 && nthr > 1) {
       std::vector<std::exception_ptr> err(nthr);
