@@ -38,6 +38,19 @@ int vvcp_parse_picture(vvcp_stream *s, int32_t idx);
  * SEIread.cpp:420): returns its hash_type (0 MD5, 1 CRC, 2 checksum) and copies the per-component
  * hashes (16 / 2 / 4 bytes each, Y Cb Cr) to out[0..n); -1 when the picture has none. */
 int vvcp_picture_hash(const vvcp_stream *s, int32_t idx, uint8_t *out, int32_t n);
+/* Per-rank parsing of a spatially sharded decode (BASELINE config 4): the CABAC pass of every later
+ * vvcp_parse_picture covers only the tiles holding luma rows [y0, y1), each up to the CTU row holding
+ * y1 - 1 (a tile's substreams are decoded from its start, DecSlice.cpp:106-114, so a tile above is parsed
+ * whole; one below only as deep as needed). Motion derivation and planning then see the CUs of those rows
+ * (the shard, its deblocking halo and the tiles' HMVP / TMVP neighbourhood, all inside the tiles); the
+ * DMVR delta list of such a picture is the sub-list of its parsed PUs (vvcp_dmvr_split). y1 <= y0: every
+ * row (the default). */
+int vvcp_set_parse_rows(vvcp_stream *s, int32_t y0, int32_t y1);
+/* The delta rows (vvcp_refine_motion layout) of a derived picture's DMVR PUs above luma row y0, in
+ * [y0, y1) and from y1 on, among the PUs its CABAC pass covered: out[0..2]. With tile-row shards a
+ * rank's list is then its upper neighbour's last out[0] rows, its own rows and its lower neighbour's
+ * first out[2] rows. */
+int vvcp_dmvr_split(const vvcp_stream *s, int32_t idx, int32_t y0, int32_t y1, int64_t *out);
 
 /* Motion derivation of a parsed picture (DecCu::xDeriveCUMV, DecCu.cpp:878, with the merge / AMVP /
  * affine / SbTMVP / GEO / MMVD candidate tools of UnitTools.cpp and the history table): fills the MV

@@ -256,6 +256,12 @@ int vvcr_prepare_planned(vvcr_ctx *ctx, const vvcr_picture *pic, int32_t *handle
 int64_t vvcr_rows_bytes(const vvcr_ctx *ctx, int32_t n);
 int vvcr_export_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, void *dev_dst);
 int vvcr_import_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, const void *dev_src);
+/* The same copies enqueued on the caller's HIP stream (hipStream_t) without a host synchronisation: the
+ * export runs after the slot's last writer and before the slot's next writer; the import after the
+ * stream's earlier work (e.g. the collective that received the rows) and before every later launch that
+ * reads or writes the slot. A halo exchange over RCCL on that stream is then ordered on the device. */
+int vvcr_export_rows_async(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, void *dev_dst, void *stream);
+int vvcr_import_rows_async(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, const void *dev_src, void *stream);
 
 /* Per-kernel-group statistics of the last launch of a picture (handle 0 = the last launched picture):
  * HIP-event time on the library stream, number of kernel launches in the group and the algorithmic

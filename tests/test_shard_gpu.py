@@ -39,11 +39,13 @@ def test_sharded_decode_matches_reference_md5(golden_dir, name, world):
             c.close()
 
 
-@pytest.mark.parametrize("name,world", [("ratile416_q32", 2), ("ratile1080_q32", 3), ("ratile1080_q32", 9), ("ra4320t_q32", 8)])
-def test_sharded_decode_from_bitstream_matches_reference_md5(golden_dir, name, world):
-    """The product path of BASELINE config 4: every emulated rank parses the .bin itself (vvcp), all-gathers
-    the DMVR deltas of each reference, derives, plans and reconstructs its own tile rows only; the
-    assembled pictures match the reference decoder's MD5s."""
+@pytest.mark.parametrize("name,world,ordered", [("ratile416_q32", 2, False), ("ratile1080_q32", 3, False), ("ratile1080_q32", 9, False),
+                                                ("ra4320t_q32", 8, False), ("ratile1080_q32", 3, True), ("ra4320t_q32", 4, True)])
+def test_sharded_decode_from_bitstream_matches_reference_md5(golden_dir, name, world, ordered):
+    """The product path of BASELINE config 4: every emulated rank parses the tiles around its rows of the
+    .bin itself (vvcp), all-gathers the DMVR deltas of each reference, derives, plans and reconstructs its
+    own tile rows only; the assembled pictures match the reference decoder's MD5s. ordered: the halo rows
+    move through stream-ordered copies without host synchronisation (the RCCL path's exchange)."""
     meta = S.load_meta(os.path.join(golden_dir, name))
     data = open(os.path.join(golden_dir, "streams", name + ".bin"), "rb").read()
     from vvc_amd import parser as PZ
@@ -55,7 +57,7 @@ def test_sharded_decode_from_bitstream_matches_reference_md5(golden_dir, name, w
             for _ in range(world)]
     try:
         ranks = [SH.StreamShardRank(ctxs[r], data, r, world, slots) for r in range(world)]
-        comm = SH.LocalComm()
+        comm = SH.LocalComm(ordered=ordered)
         for i in range(ranks[0].n):
             SH.decode_stream_local(ranks, comm, i)
             got = D.plane_md5s(SH.assemble(ranks, i))

@@ -2300,20 +2300,40 @@ void append_rows(PictureSyntax &pic, PictureSyntax &L, const std::vector<SliceDa
 
 }  // namespace
 
-void parse_picture_data(PictureSyntax &pic, const std::vector<SliceData> &slices, int threads) {
+std::pair<int, int> parse_picture_data(PictureSyntax &pic, const std::vector<SliceData> &slices, int threads, int ry0, int ry1) {
   // units of work whose CTUs lie in tiles no other unit touches: each tile of a multi-tile slice (whole tiles,
   // no CABAC or availability dependence between them), or the slices inside one tile together
   struct Unit { std::vector<Segment> segs; int tile; bool whole; size_t ctus; };
   std::vector<Unit> units;
   std::vector<Segment> segs;
+  const bool all = ry0 <= 0 && ry1 >= pic.hCtu;
+  int r0 = pic.hCtu, r1 = 0;
   for (size_t s = 0; s < slices.size(); s++) {
     const SliceCtx &sc = slices[s].sc;
     if (sc.sh->ctus.empty()) continue;
     segs.clear();
     slice_segments(pic, sc, (int)s, segs);
-    for (const Segment &g : segs) {
+    for (Segment g : segs) {
       const int ctu = sc.sh->ctus[g.i0];
       const int tile = sc.pps->tileIdx(ctu % pic.wCtu, ctu / pic.wCtu);
+      if (!all) {
+        // the tiles whose rows reach [ry0, ry1). With one tile column, only the part of a tile before CTU
+        // row ry1 (its CTUs come in raster order): the parsed PUs are then a contiguous run of the
+        // picture's decoding order (vvcp_dmvr_split); with several, whole tile rows.
+        const int tr = sc.pps->ctuToTileRow[ctu / pic.wCtu];
+        const int t0 = sc.pps->rowBd[tr], t1 = sc.pps->rowBd[tr + 1];
+        if (t1 <= ry0 || t0 >= ry1) continue;
+        if (sc.pps->numTileCols() == 1) {
+          int e = g.i0;
+          while (e < g.i1 && sc.sh->ctus[e] / pic.wCtu < ry1) e++;
+          if (e == g.i0) continue;
+          g.i1 = e;
+          r1 = std::max(r1, std::min(t1, ry1));
+        } else {
+          r1 = std::max(r1, t1);
+        }
+        r0 = std::min(r0, t0);
+      }
       const bool whole = segs.size() > 1;
       if (!whole && !units.empty() && !units.back().whole && units.back().tile == tile) units.back().segs.push_back(g);
       else units.push_back({{g}, tile, whole, 0});
@@ -2327,10 +2347,11 @@ void parse_picture_data(PictureSyntax &pic, const std::vector<SliceData> &slices
       p.run(d.rbsp, d.n, *d.epb, g.i0, g.i1, (size_t)g.ss);
     }
   };
+  const std::pair<int, int> covered = all ? std::make_pair(0, pic.hCtu) : std::make_pair(std::min(r0, r1), r1);
   const int nu = (int)units.size();
   if (threads <= 1 || nu <= 1) {
     for (const Unit &u : units) parse_unit(pic, u);
-    return;
+    return covered;
   }
   pic.unshareMap();   // the channels' maps are written by every unit: no unit may copy one while others fill it
   std::vector<std::unique_ptr<PictureSyntax>> loc(nu);
@@ -2361,6 +2382,7 @@ void parse_picture_data(PictureSyntax &pic, const std::vector<SliceData> &slices
     append_rows(pic, *loc[u], slices, units[u].segs);
     loc[u].reset();
   }
+  return covered;
 }
 
 void finish_picture_syntax(PictureSyntax &pic, int bitDepth) {

@@ -87,7 +87,10 @@ struct SliceData {
   size_t n;
   const std::vector<uint32_t> *epb;
 };
-void parse_picture_data(PictureSyntax &pic, const std::vector<SliceData> &slices, int threads);
+// ry0 / ry1: the CTU rows wanted: only the tiles with rows in [ry0, ry1) are parsed, each up to CTU row
+// ry1 (a shard's rows and the halo around them); returns the CTU rows covered, [r0, r1).
+std::pair<int, int> parse_picture_data(PictureSyntax &pic, const std::vector<SliceData> &slices, int threads, int ry0 = 0,
+                                       int ry1 = 1 << 30);
 // After the last slice: SAO merge resolution and de-quantisation (SampleAdaptiveOffset.cpp:148-264)
 void finish_picture_syntax(PictureSyntax &pic, int bitDepth);
 

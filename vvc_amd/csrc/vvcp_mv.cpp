@@ -1369,6 +1369,18 @@ void derive_motion(PictureUnit &p, const std::vector<const MotionPicture *> &dpb
   mark("init");
   d.run();
   mark("run");
+  // a picture parsed in part (vvcp_set_parse_rows): the rows outside it hold no CU; zero them as
+  // CodingStructure::initStructData would (never read for this shard, but defined)
+  const int lg = p.sps.ctuLog2;
+  const int u0 = std::min(p.syn.h4, (p.parseR0 << lg) >> 2), u1 = std::min(p.syn.h4, (int)std::min<int64_t>((int64_t)p.parseR1 << lg, 1 << 30) >> 2);
+  if (u0 > 0 || u1 < p.syn.h4) {
+    const size_t w4 = (size_t)p.syn.w4, w8 = (size_t)d.w8, h8 = (size_t)(p.syn.h4 + 1) >> 1;
+    std::memset((void *)&full[0], 0, (size_t)u0 * w4 * sizeof(Mi));
+    if (u1 < p.syn.h4) std::memset((void *)&full[(size_t)u1 * w4], 0, (size_t)(p.syn.h4 - u1) * w4 * sizeof(Mi));
+    const size_t e0 = std::min<size_t>(h8, (size_t)u0 >> 1), e1 = std::min<size_t>(h8, ((size_t)u1 + 1) >> 1);
+    std::memset((void *)&field[0], 0, e0 * w8 * sizeof(Mi));
+    if (e1 < h8) std::memset((void *)&field[e1 * w8], 0, (h8 - e1) * w8 * sizeof(Mi));
+  }
   motionRows.adopt(std::move(full));
 }
 

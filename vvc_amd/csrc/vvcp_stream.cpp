@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <tuple>
 
 #include "vvcp.h"
 #include "vvcp_params.h"
@@ -191,7 +192,9 @@ void Stream::parse_picture(int idx) {
       const Nal &nal = nals[p.sliceNal[s]];
       sd.push_back({SliceCtx{&p.sps, &p.pps, &p.ph, &p.slices[s], &ps, (int)s}, nal.rbsp.data(), nal.rbsp.size(), &nal.epb});
     }
-    parse_picture_data(p.syn, sd, tile_threads());
+    const int lg = p.sps.ctuLog2;
+    const int ry0 = std::max(0, parseY0) >> lg, ry1 = parseY1 >= (1 << 30) ? (1 << 30) : (std::max(0, parseY1) + (1 << lg) - 1) >> lg;
+    std::tie(p.parseR0, p.parseR1) = parse_picture_data(p.syn, sd, tile_threads(), ry0, ry1);
   } catch (...) {
     p.parsed = true;   // the rows parsed so far stay readable (diagnostics)
     p.failed = true;
@@ -289,6 +292,27 @@ int vvcp_parse_picture(vvcp_stream *h, int32_t idx) {
   h->s.parse_picture(idx);
   return VVCR_OK;
   VVCP_API_END
+}
+
+int vvcp_set_parse_rows(vvcp_stream *h, int32_t y0, int32_t y1) {
+  if (!h) return VVCR_E_ARG;
+  if (y1 <= y0) { h->s.parseY0 = 0; h->s.parseY1 = 1 << 30; }
+  else { h->s.parseY0 = y0; h->s.parseY1 = y1; }
+  return VVCR_OK;
+}
+
+int vvcp_dmvr_split(const vvcp_stream *h, int32_t idx, int32_t y0, int32_t y1, int64_t *out) {
+  if (!h || !out || idx < 0 || idx >= (int)h->s.pics.size()) return VVCR_E_ARG;
+  const vvcp::PictureUnit &p = *h->s.pics[idx];
+  if (!p.derived) return VVCR_E_STATE;
+  out[0] = out[1] = out[2] = 0;
+  if (p.rowsMoved) return VVCR_OK;   // planned with no DMVR refinement to wait for: none of its PUs refines
+  for (const vvcr_pu &u : p.syn.pu) {
+    if (!u.dmvr) continue;
+    const int dy = std::min(u.h, 16), dx = std::min(u.w, 16);
+    out[u.y < y0 ? 0 : (u.y < y1 ? 1 : 2)] += (int64_t)(u.h / dy) * (u.w / dx);
+  }
+  return VVCR_OK;
 }
 
 int vvcp_derive_motion(vvcp_stream *h, int32_t idx) {

@@ -31,8 +31,10 @@ struct PictureUnit {
   MotionRows motion;
   std::vector<vvcr_geo> geo;
   bool derived = false;
-  bool handedOver = false;
-  bool rowsMoved = false;    // ... and the CU / PU rows (no DMVR refinement left to read them)   // vvcp_plan_picture moved the TU rows, coefficients and motion rows out
+  bool handedOver = false;   // vvcp_plan_picture moved the TU rows, coefficients and motion rows out
+  bool rowsMoved = false;    // ... and the CU / PU rows (no DMVR refinement left to read them)
+  // CTU rows the CABAC pass covered (vvcp_set_parse_rows): [parseR0, parseR1), every row by default
+  int parseR0 = 0, parseR1 = 1 << 30;
   std::unique_ptr<MotionPicture> refined;   // set by refine_motion; read as a collocated picture
 };
 
@@ -42,6 +44,8 @@ struct Stream {
   std::vector<std::unique_ptr<PictureUnit>> pics;
   void open(const uint8_t *d, size_t n);   // splits NALs and parses every header
   void parse_picture(int idx);             // CABAC pass (thread-safe across different idx)
+  // luma rows the CABAC pass must cover (vvcp_set_parse_rows): the tiles holding them, up to their CTU row
+  int parseY0 = 0, parseY1 = 1 << 30;
   // Motion derivation of picture idx; every picture it may use as collocated reference (any earlier
   // picture in decoding order) must have been refined already.
   void derive_motion(int idx);

@@ -412,7 +412,10 @@ struct vvcr_ctx {
   std::vector<std::array<hipEvent_t, MAXLANE>> slot_r;   // per DPB slot and lane: last reader
   std::vector<uint32_t> slot_r_set;                 // per DPB slot: lanes with a reader since the last write
   std::vector<uint64_t> slot_seq;                   // per DPB slot: launch sequence number of its last writer
-  std::vector<int> slot_lane;                       // per DPB slot: lane of its last writer (-1 none)
+  std::vector<int> slot_lane;                       // per DPB slot: lane of its last writer (-1 none, or a
+                                                    // caller's stream: vvcr_import_rows_async)
+  std::vector<hipEvent_t> slot_x;                   // per DPB slot: its last reader on a caller's stream
+  std::vector<uint8_t> slot_x_set;                  // (vvcr_export_rows_async): the slot's next writer waits
   int lane_policy = 1;                              // VVCR_LANE_POLICY: 1 lane of the newest reference, 0 tail only
   bool in_picture = false;
   vvcr_picture cur;                  // the picture of vvcr_begin_picture .. vvcr_end_picture / vvcr_prepare_picture
@@ -453,6 +456,11 @@ static void check_device_errors(vvcr_ctx *ctx) {
 // every lane idle (host reads / writes of planes, vvcr_sync)
 static void sync_lanes(vvcr_ctx *ctx) {
   for (int l = 0; l < ctx->nlane; l++) VVCR_CHECK_HIP(hipStreamSynchronize(ctx->lanes[l].s));
+  // row copies enqueued on callers' streams (vvcr_*_rows_async)
+  for (size_t k = 0; k < ctx->slot_w.size(); k++) {
+    if (ctx->slot_w_set[k] && ctx->slot_lane[k] < 0) VVCR_CHECK_HIP(hipEventSynchronize(ctx->slot_w[k]));
+    if (ctx->slot_x_set[k]) VVCR_CHECK_HIP(hipEventSynchronize(ctx->slot_x[k]));
+  }
 }
 
 #define API_BEGIN try {
@@ -995,6 +1003,7 @@ static void launch_begin(vvcr_ctx *ctx, Prepared &r, int L, int set, const std::
   if (ctx->slot_w_set[pp.slot] && ctx->slot_lane[pp.slot] != L) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_w[pp.slot], 0));
   for (int l = 0; l < ctx->nlane; l++)
     if (l != L && (ctx->slot_r_set[pp.slot] >> l & 1)) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_r[pp.slot][l], 0));
+  if (ctx->slot_x_set[pp.slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(s, ctx->slot_x[pp.slot], 0));   // rows exported on a caller's stream
   VVCR_CHECK_HIP(hipStreamWaitEvent(s, r.up_done, 0));   // the picture's upload
   VVCR_CHECK_HIP(hipEventRecord(r.start, s));
 }
@@ -1329,9 +1338,12 @@ int vvcr_create(const vvcr_seq_params *sp, vvcr_ctx **out) {
     ctx->slot_r_set.assign(sp->dpb_slots, 0);
     ctx->slot_seq.assign(sp->dpb_slots, 0);
     ctx->slot_lane.assign(sp->dpb_slots, -1);
+    ctx->slot_x.assign(sp->dpb_slots, nullptr);
+    ctx->slot_x_set.assign(sp->dpb_slots, 0);
     if (const char *e = getenv("VVCR_LANE_POLICY")) ctx->lane_policy = atoi(e);
     for (int k = 0; k < sp->dpb_slots; k++) {
       VVCR_CHECK_HIP(hipEventCreateWithFlags(&ctx->slot_w[k], hipEventDisableTiming));
+      VVCR_CHECK_HIP(hipEventCreateWithFlags(&ctx->slot_x[k], hipEventDisableTiming));
       for (int l = 0; l < MAXLANE; l++) VVCR_CHECK_HIP(hipEventCreateWithFlags(&ctx->slot_r[k][l], hipEventDisableTiming));
     }
     for (int l = 0; l < ctx->nlane; l++)
@@ -1383,6 +1395,7 @@ int vvcr_destroy(vvcr_ctx *ctx) {
       for (ScratchSet &S : ln.set) { (void)hipFree(S.pred[c].p); (void)hipFree(S.resi[c].p); (void)hipFree(S.tmp[c].p); }
     }
   for (auto &e : ctx->slot_w) if (e) (void)hipEventDestroy(e);
+  for (auto &e : ctx->slot_x) if (e) (void)hipEventDestroy(e);
   for (auto &a : ctx->slot_r)
     for (auto &e : a) if (e) (void)hipEventDestroy(e);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
@@ -1990,15 +2003,21 @@ int64_t vvcr_rows_bytes(const vvcr_ctx *ctx, int32_t n) {
   return (int64_t)n * W * 2 + 2 * (int64_t)(n / 2) * (W / 2) * 2;
 }
 
-static void rows_copy(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, char *dev, bool to_slot) {
+// On stream cs (the library's copy stream, or a caller's: the _async forms). Host-synchronous unless async:
+// then the copy is ordered by events instead (an export is the slot's reader on cs, slot_x; an import its
+// writer, slot_w with no lane, which every later launch touching the slot waits for).
+static void rows_copy(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, char *dev, bool to_slot, hipStream_t cs = nullptr,
+                      bool async = false) {
   if (slot < 0 || slot >= (int)ctx->dpb.size()) throw VvcrError(VVCR_E_ARG, "bad slot");
   if (y0 < 0 || n <= 0 || (y0 | n) & 1 || y0 + n > ctx->sp.height) throw VvcrError(VVCR_E_ARG, "rows outside the picture (y0, n even)");
   if (!dev) throw VvcrError(VVCR_E_ARG, "null buffer");
-  hipStream_t cs = ctx->copy_stream;
+  if (!async) cs = ctx->copy_stream;
   if (ctx->slot_w_set[slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(cs, ctx->slot_w[slot], 0));
-  if (to_slot)   // write after read: every lane's last reader of the slot
+  if (to_slot) {   // write after read: every lane's last reader of the slot, and an export on a caller's stream
     for (int l = 0; l < ctx->nlane; l++)
       if (ctx->slot_r_set[slot] >> l & 1) VVCR_CHECK_HIP(hipStreamWaitEvent(cs, ctx->slot_r[slot][l], 0));
+    if (ctx->slot_x_set[slot]) VVCR_CHECK_HIP(hipStreamWaitEvent(cs, ctx->slot_x[slot], 0));
+  }
   for (int c = 0; c < 3; c++) {
     const DPlane &pl = ctx->dpb[slot][c];
     const int s = c ? 1 : 0, r0 = y0 >> s, nr = n >> s;
@@ -2008,7 +2027,17 @@ static void rows_copy(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, char *
     else VVCR_CHECK_HIP(hipMemcpy2DAsync(dev, rowb, plane, pl.stride * 2, rowb, nr, hipMemcpyDeviceToDevice, cs));
     dev += rowb * nr;
   }
-  VVCR_CHECK_HIP(hipStreamSynchronize(cs));
+  if (!async) {
+    VVCR_CHECK_HIP(hipStreamSynchronize(cs));
+  } else if (to_slot) {
+    VVCR_CHECK_HIP(hipEventRecord(ctx->slot_w[slot], cs));
+    ctx->slot_w_set[slot] = 1;
+    ctx->slot_lane[slot] = -1;   // no lane: every lane's next launch on the slot waits
+    ctx->slot_r_set[slot] = 0;   // earlier readers: the import waited on them
+  } else {
+    VVCR_CHECK_HIP(hipEventRecord(ctx->slot_x[slot], cs));
+    ctx->slot_x_set[slot] = 1;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -2067,6 +2096,24 @@ int vvcr_import_rows(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, const v
   API_BEGIN
   std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
   rows_copy(ctx, slot, y0, n, (char *)dev_src, true);
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_export_rows_async(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, void *dev_dst, void *stream) {
+  if (!ctx || !stream) return VVCR_E_ARG;
+  API_BEGIN
+  std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
+  rows_copy(ctx, slot, y0, n, (char *)dev_dst, false, (hipStream_t)stream, true);
+  return VVCR_OK;
+  API_END
+}
+
+int vvcr_import_rows_async(vvcr_ctx *ctx, int32_t slot, int32_t y0, int32_t n, const void *dev_src, void *stream) {
+  if (!ctx || !stream) return VVCR_E_ARG;
+  API_BEGIN
+  std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
+  rows_copy(ctx, slot, y0, n, (char *)dev_src, true, (hipStream_t)stream, true);
   return VVCR_OK;
   API_END
 }

@@ -122,6 +122,8 @@ def lib():
         L.vvcr_rows_bytes.restype = C.c_int64
         L.vvcr_export_rows.argtypes = [P, I32, I32, I32, P]
         L.vvcr_import_rows.argtypes = [P, I32, I32, I32, P]
+        L.vvcr_export_rows_async.argtypes = [P, I32, I32, I32, P, P]
+        L.vvcr_import_rows_async.argtypes = [P, I32, I32, I32, P, P]
         _lib = L
     return _lib
 
@@ -138,7 +140,8 @@ EXPORTS = ["vvcr_prepare_picture", "vvcr_launch_picture", "vvcr_launch_picture_s
            "vvcr_rdo_release", "vvcr_rd_dist", "vvcr_fwd_transform", "vvcr_set_timing",
            "vvcr_picture_create", "vvcr_picture_submit", "vvcr_picture_set_loop_filter_params", "vvcr_picture_plan",
            "vvcr_picture_work_counts", "vvcr_picture_last_error", "vvcr_picture_destroy", "vvcr_prepare_planned",
-           "vvcr_rows_bytes", "vvcr_export_rows", "vvcr_import_rows", "vvcr_output_bytes", "vvcr_write_output"]
+           "vvcr_rows_bytes", "vvcr_export_rows", "vvcr_import_rows", "vvcr_export_rows_async", "vvcr_import_rows_async",
+           "vvcr_output_bytes", "vvcr_write_output"]
 
 # encoder RDO block descriptors (include/vvcr.h vvcr_rd_block / vvcr_fwd_block) as numpy record types
 RD_BLOCK = [("org_off", "<i8"), ("cur_off", "<i8"), ("org_stride", "<i4"), ("cur_stride", "<i4"), ("width", "<i4"),
@@ -307,6 +310,13 @@ class Context:
 
     def import_rows(self, slot, y0, n, dev_ptr):
         self._chk(self.L.vvcr_import_rows(self.h, slot, y0, n, dev_ptr), "vvcr_import_rows")
+
+    def export_rows_async(self, slot, y0, n, dev_ptr, stream):
+        """export_rows enqueued on a caller's HIP stream (a torch stream's cuda_stream), no host sync"""
+        self._chk(self.L.vvcr_export_rows_async(self.h, slot, y0, n, dev_ptr, stream), "vvcr_export_rows_async")
+
+    def import_rows_async(self, slot, y0, n, dev_ptr, stream):
+        self._chk(self.L.vvcr_import_rows_async(self.h, slot, y0, n, dev_ptr, stream), "vvcr_import_rows_async")
 
     def launch(self, handle):
         self._chk(self.L.vvcr_launch_picture(self.h, handle), "vvcr_launch_picture")

@@ -36,6 +36,8 @@ def _bind(lib):
     lib.vvcp_alf_filters.argtypes = [_P, _I32, _P, _P, _I32, _P, _P, _P]
     lib.vvcp_derive_motion.argtypes = [_P, _I32]
     lib.vvcp_refine_motion.argtypes = [_P, _I32, _P, _I64]
+    lib.vvcp_set_parse_rows.argtypes = [_P, _I32, _I32]
+    lib.vvcp_dmvr_split.argtypes = [_P, _I32, _I32, _I32, C.POINTER(_I64)]
     lib._vvcp_bound = True
     return lib
 
@@ -79,6 +81,19 @@ class Stream:
         rc = self.lib.vvcp_parse_picture(self.h, i)
         if rc != 0:
             raise ParseError("picture %d: %s" % (i, self.lib.vvcp_last_error().decode()))
+
+    def set_parse_rows(self, y0, y1):
+        """later CABAC passes cover only the tiles holding luma rows [y0, y1) (vvcp_set_parse_rows)"""
+        if self.lib.vvcp_set_parse_rows(self.h, int(y0), int(y1)) != 0:
+            raise ParseError("vvcp_set_parse_rows")
+
+    def dmvr_split(self, i, y0, y1):
+        """(above, inside, below): delta rows of picture i's parsed DMVR PUs around luma rows [y0, y1)"""
+        v = (_I64 * 3)()
+        rc = self.lib.vvcp_dmvr_split(self.h, i, int(y0), int(y1), v)
+        if rc != 0:
+            raise ParseError("picture %d dmvr_split: %d" % (i, rc))
+        return int(v[0]), int(v[1]), int(v[2])
 
     def derive(self, i):
         rc = self.lib.vvcp_derive_motion(self.h, i)

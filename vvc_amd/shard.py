@@ -27,6 +27,15 @@ from . import native as N
 from . import stream as S
 
 LF_HALO = 24
+# rows a rank's CABAC pass covers beyond its own (vvcp_set_parse_rows): the deblocking plan of the halo
+# (VVCR_LF_HALO rows) and the CUs on the far side of its outermost edges
+PARSE_MARGIN = LF_HALO + 8
+
+
+def parse_rows(y0, y1, ctu):
+    """luma rows a rank with rows [y0, y1) parses: the deblocking planner takes every edge of the CUs that
+    reach VVCR_LF_HALO rows into the halo, so above it needs the CTU row over the topmost of them too"""
+    return y0 - PARSE_MARGIN - ctu, y1 + PARSE_MARGIN
 STAGES_RECON = N.STAGE_RESID | N.STAGE_INTER | N.STAGE_INTRA | N.STAGE_LMCS_INV
 STAGES_LF = N.STAGE_DBK | N.STAGE_SAO | N.STAGE_ALF
 
@@ -154,13 +163,15 @@ class StreamShardRank(ShardGeom):
     own tile rows only (vvcp_plan_picture_rows -> vvcr_pic_params::shard_y0 / shard_y1).
 
     Per picture, in decoding order (DecApp::decode, DecApp.cpp:118-200):
-      1. the CABAC pass (whole picture: the slice's substreams follow one another);
+      1. the CABAC pass of the tiles around its rows only (vvcp_set_parse_rows: the tile rows that hold
+         its shard and PARSE_MARGIN rows around it; each tile's substreams on a thread of their own,
+         DecSlice.cpp:106-114). HMVP resets per tile row (DecSlice.cpp:186-191), spatial candidates stay
+         inside the tile and temporal ones inside the CTU row, so the motion of those rows is exact;
       2. the refined motion of its pending references: each rank's GPU refined the DMVR sub-blocks of its
-         own rows, and since the shards are whole CTU rows in raster order the ranks' delta lists, in rank
-         order, are the picture's list (vvcr_picture_dmvr_deltas order): they are all-gathered, so every
-         rank records the exact refined motion field (CS::setRefinedMotionField, UnitTools.cpp:68) and
-         derives the exact motion of every CU, including the CUs near its rows whose boundary strengths
-         its deblocking halo needs;
+         own rows; the lists are all-gathered and each rank takes its parsed PUs' run of them (the tile
+         rows are whole and in decoding order: the upper neighbour's last rows, its own, the lower
+         neighbour's first, vvcp_dmvr_split), so every rank records the exact refined motion field
+         (CS::setRefinedMotionField, UnitTools.cpp:68) of its rows and the rows around them;
       3. motion derivation, planning of the shard, upload;
       4. the reference halo: the motion reach of the picture's MC jobs beyond the shard (max over the
          ranks, all-reduced per picture) in each reference picture, exchanged point to point with the
@@ -179,6 +190,9 @@ class StreamShardRank(ShardGeom):
         self.sp = N.SeqParams(self.W, self.H, 1, inf0["bit_depth"], inf0["ctu_log2"], dpb_slots, 0)
         rows = rows or stream_shard_rows(self.ps.pic_params(0), self.H, inf0["ctu_log2"], world)
         super().__init__(ctx, rank, rows)
+        self.partial = world > 1
+        if self.partial:
+            self.ps.set_parse_rows(*parse_rows(self.y0, self.y1, 1 << inf0["ctu_log2"]))
         L = B._bind(N.lib())
         L.vvcp_plan_picture_rows.argtypes = [C.c_void_p, C.c_int32, C.POINTER(N.SeqParams), C.c_int32, C.c_void_p,
                                              C.c_uint32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
@@ -227,7 +241,19 @@ class StreamShardRank(ShardGeom):
         return self.ctx.picture_dmvr_deltas(self.handle[j], self.ndmvr[j])
 
     def refine(self, j, parts):
-        d = np.concatenate([np.asarray(p, np.int32).reshape(-1, 2) for p in parts]) if parts else np.zeros((0, 2), np.int32)
+        """parts: every rank's delta list of picture j (rows of its own shard), in rank order"""
+        parts = [np.asarray(p, np.int32).reshape(-1, 2) for p in parts]
+        if self.partial:
+            # the parsed PUs above the shard are the last `a` of the ranks above (whole tile rows, decoding
+            # order), those below the first `b` of the ranks below
+            a, o, b = self.ps.dmvr_split(j, self.y0, self.y1)
+            r = self.rank
+            up = np.concatenate(parts[:r]) if r else np.zeros((0, 2), np.int32)
+            down = np.concatenate(parts[r + 1:]) if r + 1 < len(parts) else np.zeros((0, 2), np.int32)
+            if len(parts[r]) != o or len(up) < a or len(down) < b:
+                raise RuntimeError("picture %d: DMVR delta lists do not match the parsed rows" % j)
+            parts = [up[len(up) - a:], parts[r], down[:b]]
+        d = np.concatenate(parts) if parts else np.zeros((0, 2), np.int32)
         self.ps.refine(j, d)
         self.refined[j] = True
 
@@ -326,16 +352,24 @@ def decode_stream_local(ranks, comm, i):
 
     def phase(lists_of, slot_of):
         staged = []
+        st = comm.stream_handle() if comm.ordered else None
         for rk in ranks:
             for slot, (sends, recvs) in lists_of(rk):
                 for peer, y0, n in sends:
                     buf = comm.buffer(rk, rk.ctx.rows_bytes(n))
-                    rk.ctx.export_rows(slot, y0, n, buf.data_ptr())
+                    if st is not None:
+                        rk.ctx.export_rows_async(slot, y0, n, buf.data_ptr(), st)
+                    else:
+                        rk.ctx.export_rows(slot, y0, n, buf.data_ptr())
                     comm.box[(rk.rank, peer, slot)] = buf
                 staged.append((rk, slot, recvs))
         for rk, slot, recvs in staged:
             for peer, y0, n in recvs:
-                rk.ctx.import_rows(slot, y0, n, comm.box.pop((peer, rk.rank, slot)).data_ptr())
+                buf = comm.box.pop((peer, rk.rank, slot))
+                if st is not None:
+                    rk.ctx.import_rows_async(slot, y0, n, buf.data_ptr(), st)
+                else:
+                    rk.ctx.import_rows(slot, y0, n, buf.data_ptr())
     if len(ranks) > 1:
         phase(lambda rk: rk.ref_lists(i, M), None)
     for rk in ranks:
@@ -359,6 +393,20 @@ def plan_and_reach(ranks, comm=None):
 def exchange(rk, comm, lists, slot):
     """export the sends, swap through comm, import the receives (rows of one DPB slot)"""
     sends, recvs = lists
+    if getattr(comm, "ordered", False):
+        # RCCL: exports, the point-to-point swap and the imports all on the comm's stream, ordered on the
+        # device by events against the library's lanes (vvcr_*_rows_async): no host synchronisation
+        st = comm.stream_handle()
+        out = []
+        for peer, y0, n in sends:
+            buf = comm.buffer(rk, rk.ctx.rows_bytes(n))
+            rk.ctx.export_rows_async(slot, y0, n, buf.data_ptr(), st)
+            out.append((peer, buf))
+        inc = [(peer, comm.buffer(rk, rk.ctx.rows_bytes(n), recv=True)) for peer, y0, n in recvs]
+        comm.swap(rk, out, inc)
+        for (peer, y0, n), (_, buf) in zip(recvs, inc):
+            rk.ctx.import_rows_async(slot, y0, n, buf.data_ptr(), st)
+        return
     out = []
     for peer, y0, n in sends:
         buf = comm.buffer(rk, rk.ctx.rows_bytes(n))
@@ -408,9 +456,19 @@ class TorchComm:
         self.gpu = dist.get_backend() == "nccl"
         self.host_rows = host_rows
         self._stage = {}
+        # nccl: the halo buffers, the library's row copies and the collectives share one stream of ours
+        # (exchange: stream-ordered, no host synchronisation)
+        self.ordered = self.gpu and not host_rows
+        self.stream = torch.cuda.Stream(device=device) if self.ordered else None
+
+    def stream_handle(self):
+        return self.stream.cuda_stream
 
     def buffer(self, rk, nbytes, recv=False):
         t = self.torch
+        if self.ordered:
+            with t.cuda.stream(self.stream):   # allocated for (and reused in order on) the exchange stream
+                return t.empty(nbytes, dtype=t.uint8, device=self.device)
         return t.empty(nbytes, dtype=t.uint8, device=self.device if self.gpu else "cpu")
 
     def dev_ptr(self, buf, staged=False):
@@ -434,6 +492,14 @@ class TorchComm:
             for peer, buf in sends:   # device -> host for the exported rows
                 buf.copy_(self._stage[id(buf)])
         ops = [dist.P2POp(dist.isend, buf, peer) for peer, buf in sends] + [dist.P2POp(dist.irecv, buf, peer) for peer, buf in recvs]
+        if self.ordered:
+            # the work's wait() makes the current stream (ours) wait for RCCL's: the imports that follow on
+            # it see the received rows; the host goes on
+            with t.cuda.stream(self.stream):
+                if ops:
+                    for r in dist.batch_isend_irecv(ops):
+                        r.wait()
+            return
         if ops:
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
@@ -470,13 +536,23 @@ class LocalComm:
     """Ranks emulated in one process (one context each, possibly on one GPU): decode_local drives all
     ranks through a picture phase by phase, the rows passing through a mailbox of device buffers."""
 
-    def __init__(self, device="cuda"):
+    def __init__(self, device="cuda", ordered=False):
+        """ordered: the row copies go on one stream of ours without host synchronisation, as TorchComm's
+        RCCL path does (vvcr_export_rows_async / vvcr_import_rows_async)"""
         import torch
         self.torch = torch
         self.device = device
         self.box = {}
+        self.ordered = ordered
+        self.stream = torch.cuda.Stream(device=device) if ordered else None
+
+    def stream_handle(self):
+        return self.stream.cuda_stream
 
     def buffer(self, rk, nbytes, recv=False):
+        if self.ordered:
+            with self.torch.cuda.stream(self.stream):
+                return self.torch.empty(nbytes, dtype=self.torch.uint8, device=self.device)
         return self.torch.empty(nbytes, dtype=self.torch.uint8, device=self.device)
 
     def max_int(self, v):
