@@ -2,6 +2,7 @@
 // reference function whose decisions it restates; the data model is flat (rows + 4x4 maps) instead of
 // the reference's CodingStructure objects.
 #include "vvcp_ctu.h"
+#include "vvcr_tables.h"
 
 #include <algorithm>
 #include <atomic>
@@ -33,15 +34,6 @@ constexpr int BCW_DEFAULT = 2;
 // Scan orders (Rom.cpp:252-380 initROM, ScanGenerator :91)
 // ------------------------------------------------------------------------------------------------
 struct ScanPos { uint16_t idx; uint8_t x, y; };
-const uint8_t kLog2Sbb[8][8][2] = {
-  {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {0, 4}, {0, 4}, {0, 4}, {0, 4}},
-  {{1, 0}, {1, 1}, {1, 1}, {1, 3}, {1, 3}, {1, 3}, {1, 3}, {1, 3}},
-  {{2, 0}, {1, 1}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}},
-  {{3, 0}, {3, 1}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}},
-  {{4, 0}, {3, 1}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}},
-  {{4, 0}, {3, 1}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}},
-  {{4, 0}, {3, 1}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}},
-  {{4, 0}, {3, 1}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}, {2, 2}}};
 
 struct DiagGen {   // ScanGenerator, SCAN_DIAG
   int w, h, line = 0, col = 0;
@@ -72,7 +64,7 @@ struct Scans {
         p.resize(w * h);
         DiagGen g(w, h);
         for (int i = 0; i < w * h; i++) { p[i] = {(uint16_t)(g.line * w + g.col), (uint8_t)g.col, (uint8_t)g.line}; g.next(); }
-        const int sw = kLog2Sbb[lw][lh][0], sh = kLog2Sbb[lw][lh][1];
+        const int sw = kLog2SbbSize[lw][lh][0], sh = kLog2SbbSize[lw][lh][1];
         const int gw = 1 << sw, gh = 1 << sh;
         const int wg = std::min(32, w) >> sw, hg = std::min(32, h) >> sh;
         std::vector<ScanPos> &s = grouped[lw][lh];
@@ -129,8 +121,8 @@ struct CoefCtx {
     ch = comp ? 1 : 0;
     const int lw = floorLog2(w), lh = floorLog2(h);
     log2w = lw;
-    log2CGw = kLog2Sbb[lw][lh][0];
-    log2CGh = kLog2Sbb[lw][lh][1];
+    log2CGw = kLog2SbbSize[lw][lh][0];
+    log2CGh = kLog2SbbSize[lw][lh][1];
     log2CG = log2CGw + log2CGh;
     wg = std::min(32, w) >> log2CGw;
     hg = std::min(32, h) >> log2CGh;

@@ -2,6 +2,7 @@
 // The decisions mirror the reference's dispatch in InterPrediction::motionCompensation
 // (InterPrediction.cpp:1517-1660) so that every PU reaches the kernel that reproduces its prediction.
 #include "vvcr_host.h"
+#include "vvcr_tables.h"
 #include <string>
 #include <cstring>
 #include <algorithm>
@@ -565,17 +566,6 @@ void build_work_lists(const vvcr_seq_params &sp, const vvcr_pic_params &pp, cons
 // scans
 // ------------------------------------------------------------------------------------------------
 namespace {
-// g_log2SbbSize (Rom.cpp:252)
-const uint8_t kSbb[8][8][2] = {
-  { {0,0},{0,1},{0,2},{0,3},{0,4},{0,4},{0,4},{0,4} },
-  { {1,0},{1,1},{1,1},{1,3},{1,3},{1,3},{1,3},{1,3} },
-  { {2,0},{1,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
-  { {3,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
-  { {4,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
-  { {4,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
-  { {4,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} },
-  { {4,0},{3,1},{2,2},{2,2},{2,2},{2,2},{2,2},{2,2} } };
-
 void diag(int bw, int bh, std::vector<int> &xs, std::vector<int> &ys) {
   xs.resize(bw * bh); ys.resize(bw * bh);
   int line = 0, col = 0;
@@ -596,7 +586,7 @@ void build_scan_tables(ScanTables &st) {
   for (int lw = 0; lw < 7; lw++)
     for (int lh = 0; lh < 7; lh++) {
       const int w = 1 << lw, h = 1 << lh;
-      const int gw = 1 << kSbb[lw][lh][0], gh = 1 << kSbb[lw][lh][1];
+      const int gw = 1 << kLog2SbbSize[lw][lh][0], gh = 1 << kLog2SbbSize[lw][lh][1];
       const int wg = std::min(w, 32) / gw, hg = std::min(h, 32) / gh;
       st.off[lw][lh] = (int32_t)st.data.size();
       diag(wg, hg, gx, gy);
