@@ -39,5 +39,18 @@ def test_encoderapp_with_gpu_merge_satd_is_byte_identical(tmp_path):
     routed = int(m.group(1))
     print("EncoderApp %.1f s, with GPU merge SATD %.1f s: %d calls routed, %s fell back, %d bytes" % (
         secs["cpu"], secs["gpu"], routed, m.group(2), len(out["gpu"][0])))
+    # speed record (VVCR_RECORD_DIR): the link-time binding makes one synchronous GPU round trip per SATD,
+    # because the reference's merge loop consumes each candidate's cost before it forms the next
+    # (EncCu.cpp:2421-2451); DESIGN.md §9 and bench_rdo.py give the batched entry's rate
+    rec = os.environ.get("VVCR_RECORD_DIR")
+    if rec:
+        import json
+        os.makedirs(rec, exist_ok=True)
+        with open(os.path.join(rec, "enc_dropin_speed.json"), "w") as f:
+            json.dump({"input": "416x240 synthetic, 3 pictures, lowdelay_small.cfg, QP 32", "encoderapp_s": round(secs["cpu"], 3),
+                       "encoderapp_gpu_merge_satd_s": round(secs["gpu"], 3), "routed_calls": routed,
+                       "fallback_calls": int(m.group(2)), "bytes": len(out["gpu"][0]),
+                       "us_added_per_routed_call": round((secs["gpu"] - secs["cpu"]) / max(routed, 1) * 1e6, 2),
+                       "bitstreams_identical": out["gpu"][0] == out["cpu"][0]}, f, indent=1)
     assert routed > 0
     assert out["gpu"][0] == out["cpu"][0], "bitstreams differ"
