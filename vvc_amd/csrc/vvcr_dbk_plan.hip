@@ -15,7 +15,7 @@
 //   2. the transform-size filter lengths of the TU whose edge holds the unit
 //   3. the sub-block filter lengths of an SbTMVP / affine PU
 //   4. the boundary strength
-//   5. the segment words, appended to the four lists k_dbk reads (a wave-aggregated atomic a list; every
+//   5. the segment words, appended to the four lists k_dbk reads (a workgroup-aggregated atomic a list; every
 //      segment of one direction is independent, so the lists' order does not change the samples)
 // The chroma-tree CUs of a picture (dual tree, or the chroma CUs of a local dual tree) run after the luma
 // tree's, from a clean state (dual tree: the host's per-pass reset) or on top of the luma CU's state of the
@@ -399,17 +399,34 @@ __device__ __forceinline__ bool in_shard(const DbkPlanArgs &A, const Cu &R) {
   return R.a1 + R.a3 > A.ly0 && R.a1 < A.ly1;
 }
 
-// lanes of the wave with w != 0 append (x4, y4, w) to list k (one atomic a wave and list)
-__device__ __forceinline__ void append(const DbkPlanArgs &A, int k, uint32_t w, int x4, int y4) {
-  const unsigned long long m = __ballot(w != 0);
-  if (!m) return;
-  const int lane = threadIdx.x & 63, first = __ffsll(m) - 1;
-  int base = 0;
-  if (lane == first) base = atomicAdd(&A.counts[k], __popcll(m));
-  base = __shfl(base, first) + __popcll(m & ((1ull << lane) - 1));
-  if (!w) return;
-  if (base < A.cap) A.out[(size_t)k * A.cap + base] = DbkSeg{(uint16_t)x4, (uint16_t)y4, w};
-  else atomicOr(A.err, 4);
+// The lanes of a 256-lane workgroup with wl / wc != 0 append (x4, y4, w) to the luma / chroma list of
+// direction dir (lists 2 dir, 2 dir + 1): one atomic per list and workgroup, the waves' runs placed by
+// their counts in LDS (an atomic per wave and list put 10 k atomics a 4K picture on the same four
+// counters). more: the caller loops again (the LDS counts are reused: a third barrier).
+__device__ __forceinline__ void append_wg(const DbkPlanArgs &A, int dir, uint32_t wl, uint32_t wc, int x4, int y4, bool more) {
+  __shared__ int s_cnt[4][2];
+  __shared__ int s_base[2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const unsigned long long ml = __ballot(wl != 0), mc = __ballot(wc != 0);
+  if (lane == 0) { s_cnt[wv][0] = __popcll(ml); s_cnt[wv][1] = __popcll(mc); }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int t = s_cnt[0][threadIdx.x] + s_cnt[1][threadIdx.x] + s_cnt[2][threadIdx.x] + s_cnt[3][threadIdx.x];
+    s_base[threadIdx.x] = t ? atomicAdd(&A.counts[2 * dir + threadIdx.x], t) : 0;
+  }
+  __syncthreads();
+  const unsigned long long below = (1ull << lane) - 1;
+  int bl = s_base[0] + __popcll(ml & below), bc = s_base[1] + __popcll(mc & below);
+  for (int w = 0; w < wv; w++) { bl += s_cnt[w][0]; bc += s_cnt[w][1]; }
+  if (wl) {
+    if (bl < A.cap) A.out[(size_t)(2 * dir) * A.cap + bl] = DbkSeg{(uint16_t)x4, (uint16_t)y4, wl};
+    else atomicOr(A.err, 4);
+  }
+  if (wc) {
+    if (bc < A.cap) A.out[(size_t)(2 * dir + 1) * A.cap + bc] = DbkSeg{(uint16_t)x4, (uint16_t)y4, wc};
+    else atomicOr(A.err, 4);
+  }
+  if (more) __syncthreads();
 }
 
 // index maps: CU per 4x4 luma / 2x2 chroma unit, TU likewise (an ISP CU's luma area holds -(first TU) - 2);
@@ -499,8 +516,7 @@ __device__ __forceinline__ void items_dir(const DbkPlanArgs &A, const int (*rp)[
       if (PASS == 0 && local_dual) A.state[DIR][u] = (uint8_t)(st.edge << 7 | (st.bs & 63));
       }
     }
-    append(A, 2 * DIR, wl, x4, y4);
-    append(A, 2 * DIR + 1, wc, x4, y4);
+    append_wg(A, DIR, wl, wc, x4, y4, j0 + (int)(gridDim.x * 256) < total);
   }
 }
 
