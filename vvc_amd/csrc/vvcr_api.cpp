@@ -231,8 +231,9 @@ struct Prepared {
   bool launched = false;
   int lane = 0;                      // execution lane of the last launch (its stream and scratch planes)
   int set = 0;                       // the lane's scratch set of the last launch (k: k-th picture of a batch)
-  int mc_pics = 1;                   // pictures whose plain MC the K_MC launch of this record carried (0: batched
-                                     // into another picture's launch, whose record holds the time and bytes)
+  int kpics[NK] = {};                // pictures each kernel group's launch of this record carried (MC groups of a
+                                     // frame-batched launch: the first picture's record holds the launch, its
+                                     // time and bytes and the count; the others 0)
   uint32_t staged = 0;               // stages launched so far by vvcr_launch_picture_stages (0: none pending)
   double alg_bytes[NK] = {};
   int launches[NK] = {};
@@ -274,7 +275,7 @@ struct Prepared {
     staged = 0;
     lane = 0;
     set = 0;
-    mc_pics = 1;
+    for (int &k : kpics) k = 1;
   }
 };
 
@@ -507,7 +508,6 @@ static McParams make_mc_params(vvcr_ctx *ctx, const Prepared &r, int lane, int s
   P.pic_h = ctx->sp.height;
   P.bd = ctx->sp.bit_depth;
   P.ctu = 1 << ctx->sp.ctu_log2;
-  P.wp = make_wp_table(pp, ctx->sp.bit_depth);
   P.wpd = wpd;
   const DPlane *reco = recon_planes(ctx, r, lane, set);
   for (int c = 0; c < 3; c++) {
@@ -995,7 +995,7 @@ static void launch_begin(vvcr_ctx *ctx, Prepared &r, int L, int set, const std::
   hipStream_t s = ln.s;
   r.lane = L;
   r.set = set;
-  r.mc_pics = 1;
+  for (int &k : r.kpics) k = 1;
   ln.tail_slot = pp.slot;
   ln.tail_seq = ++ctx->seq;
   for (int rs : refs)
@@ -1053,42 +1053,76 @@ static void launch_plain_mc(vvcr_ctx *ctx, Prepared *const *rs, int n) {
       rs[k]->ran[K_MC] = true;
       rs[k]->timed[K_MC] = false;
       rs[k]->launches[K_MC] = 0;
-      rs[k]->mc_pics = 0;
+      rs[k]->kpics[K_MC] = 0;
     }
   }
   KernelTimer t(r0, K_MC, s, ctx->timing);
   launch_mc_batch(b, hct, s);
   VVCR_CHECK_HIP(hipGetLastError());
   r0.launches[K_MC] = jobs ? 1 : 0;
-  r0.mc_pics = n;
+  r0.kpics[K_MC] = n;
   if (n > 1) {
     r0.alg_bytes[K_MC] = bytes;
     for (int k = 1; k < n; k++) rs[k]->alg_bytes[K_MC] = 0;
   }
 }
 
-// DMVR / BDOF and affine MC, then the DMVR deltas' read-back on the copy stream (the lane goes on)
-static void launch_mc_ext_stage(vvcr_ctx *ctx, Prepared &r) {
-  hipStream_t s = ctx->lanes[r.lane].s;
-  const McParams mp = make_mc_params(ctx, r, r.lane, r.set, r.wpt.p);
-  {
-    KernelTimer t(r, K_MC_BIDIR, s, ctx->timing);
-    launch_mc_bidir(mp, r.mc_bidir.p, r.n_bidir, r.dmvr.p, s);
-    VVCR_CHECK_HIP(hipGetLastError());
-    r.launches[K_MC_BIDIR] = r.n_bidir ? 1 : 0;
+// The accounting of one MC kernel group launched over the pictures rs[0, n) (frame batching): the first
+// record holds the launch (its events, launch count, the pictures with work and the bytes of all)
+static void batch_stats(Prepared *const *rs, int n, int k, int njobs_total, int pics_with_work) {
+  Prepared &r0 = *rs[0];
+  r0.launches[k] = njobs_total ? 1 : 0;
+  if (n == 1) return;
+  r0.kpics[k] = pics_with_work;
+  double bytes = 0;
+  for (int q = 0; q < n; q++) bytes += rs[q]->alg_bytes[k];
+  r0.alg_bytes[k] = bytes;
+  for (int q = 1; q < n; q++) {
+    rs[q]->ran[k] = true;
+    rs[q]->timed[k] = false;
+    rs[q]->launches[k] = 0;
+    rs[q]->kpics[k] = 0;
+    rs[q]->alg_bytes[k] = 0;
+  }
+}
+
+// DMVR / BDOF and affine MC of the pictures rs[0, n) on the first one's lane (one launch each over all of
+// them: frame batching), then each picture's DMVR deltas' read-back on the copy stream (the lane goes on)
+static void launch_mc_ext_stage(vvcr_ctx *ctx, Prepared *const *rs, int n) {
+  Prepared &r0 = *rs[0];
+  hipStream_t s = ctx->lanes[r0.lane].s;
+  ExtBatch bb, ab;
+  bb.npic = ab.npic = n;
+  int nb = 0, na = 0, pb = 0, pa = 0;
+  for (int q = 0; q < n; q++) {
+    Prepared &r = *rs[q];
+    bb.pic[q] = ab.pic[q] = make_mc_params(ctx, r, r.lane, r.set, r.wpt.p);
+    bb.njobs[q] = r.n_bidir; bb.jobs[q] = r.mc_bidir.p; bb.dmvr[q] = r.dmvr.p;
+    ab.njobs[q] = r.n_aff; ab.jobs[q] = r.aff_jobs.p; ab.pus[q] = r.aff_pu.p;
+    nb += r.n_bidir; na += r.n_aff;
+    pb += r.n_bidir > 0; pa += r.n_aff > 0;
   }
   {
-    KernelTimer t(r, K_MC_AFFINE, s, ctx->timing);
-    launch_mc_affine(mp, r.aff_jobs.p, r.n_aff, r.aff_pu.p, s);
+    KernelTimer t(r0, K_MC_BIDIR, s, ctx->timing);
+    launch_mc_bidir(bb, s);
     VVCR_CHECK_HIP(hipGetLastError());
-    r.launches[K_MC_AFFINE] = r.n_aff ? 1 : 0;
   }
-  VVCR_CHECK_HIP(hipEventRecord(r.ev_mc, s));
-  VVCR_CHECK_HIP(hipStreamWaitEvent(ctx->copy_stream, r.ev_mc, 0));
-  if (r.n_dmvr > 0)
-    VVCR_CHECK_HIP(hipMemcpyAsync(r.h_dmvr, r.dmvr.p, (size_t)r.n_dmvr * 2 * sizeof(int32_t), hipMemcpyDeviceToHost,
-                                  ctx->copy_stream));
-  VVCR_CHECK_HIP(hipEventRecord(r.mc_done, ctx->copy_stream));
+  batch_stats(rs, n, K_MC_BIDIR, nb, pb);
+  {
+    KernelTimer t(r0, K_MC_AFFINE, s, ctx->timing);
+    launch_mc_affine(ab, s);
+    VVCR_CHECK_HIP(hipGetLastError());
+  }
+  batch_stats(rs, n, K_MC_AFFINE, na, pa);
+  for (int q = 0; q < n; q++) {
+    Prepared &r = *rs[q];
+    VVCR_CHECK_HIP(hipEventRecord(r.ev_mc, s));
+    VVCR_CHECK_HIP(hipStreamWaitEvent(ctx->copy_stream, r.ev_mc, 0));
+    if (r.n_dmvr > 0)
+      VVCR_CHECK_HIP(hipMemcpyAsync(r.h_dmvr, r.dmvr.p, (size_t)r.n_dmvr * 2 * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                    ctx->copy_stream));
+    VVCR_CHECK_HIP(hipEventRecord(r.mc_done, ctx->copy_stream));
+  }
 }
 
 // intra / inter reconstruction, LMCS inverse, deblocking, SAO, ALF (stages of mask), the picture's final
@@ -1228,7 +1262,7 @@ static void launch(vvcr_ctx *ctx, Prepared &r, uint32_t stages = VVCR_STAGE_ALL)
   if (mask & VVCR_STAGE_INTER) {
     Prepared *one = &r;
     launch_plain_mc(ctx, &one, 1);
-    launch_mc_ext_stage(ctx, r);
+    launch_mc_ext_stage(ctx, &one, 1);
   }
   launch_rest(ctx, r, mask, refs);
 }
@@ -1265,10 +1299,8 @@ static void launch_batch(vvcr_ctx *ctx, Prepared *const *rs, int n) {
   for (int k = 0; k < n; k++) launch_begin(ctx, *rs[k], L, k, refs[k]);
   for (int k = 0; k < n; k++) launch_resid_stage(ctx, *rs[k]);
   launch_plain_mc(ctx, rs, n);
-  for (int k = 0; k < n; k++) {
-    launch_mc_ext_stage(ctx, *rs[k]);
-    launch_rest(ctx, *rs[k], rs[k]->mask, refs[k]);
-  }
+  launch_mc_ext_stage(ctx, rs, n);
+  for (int k = 0; k < n; k++) launch_rest(ctx, *rs[k], rs[k]->mask, refs[k]);
 }
 
 extern "C" {
@@ -1865,7 +1897,7 @@ int vvcr_kernel_stats(vvcr_ctx *ctx, int32_t handle, vvcr_kernel_stat *out, int3
     strncpy(s.name, kKernelNames[k], sizeof(s.name) - 1);
     s.launches = r->ran[k] ? r->launches[k] : 0;
     s.alg_bytes = r->ran[k] ? r->alg_bytes[k] : 0.0;
-    s.pictures = k == K_MC ? r->mc_pics : 1;
+    s.pictures = r->kpics[k];
     float ms = 0;
     // a stage with nothing to launch has an empty event pair: no kernel time
     if (r->ran[k] && r->timed[k] && r->launches[k] > 0) VVCR_CHECK_HIP(hipEventElapsedTime(&ms, r->ev[k][0], r->ev[k][1]));

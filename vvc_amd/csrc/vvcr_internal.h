@@ -140,8 +140,7 @@ struct McParams {
   int32_t pic_w, pic_h;  // luma picture size
   int32_t bd;            // bit depth
   int32_t ctu;           // CTU size (affine MV clamp, InterPrediction.cpp:937)
-  WpTable wp;
-  const WpTable *wpd;    // the same table in device memory (k_mc indexes it per lane)
+  const WpTable *wpd;    // the picture's weighted-prediction table in device memory
   DPlane reco[3];        // the picture (MC_RECON jobs)
   DPlane resi[3];        // the residual planes (MC_RESI jobs)
 };
@@ -313,8 +312,20 @@ void launch_fwd_tr(const int16_t *resi, int32_t *coef, const FwdBlockDev *blocks
                    int trv, int lfnst, hipStream_t s);
 
 // launchers (vvcr_mc.hip, vvcr_mc_ext.hip, vvcr_resid.hip, vvcr_lf.hip)
-void launch_mc_bidir(const McParams &p, const McJob *jobs, int njobs, int32_t *dmvr_out, hipStream_t s);
-void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const AffPu *pus, hipStream_t s);
+// DMVR / BDOF (k_mc_bidir) and affine (k_mc_affine) launches over the jobs of up to MC_MAXPIC pictures
+// (frame batching, vvcr_launch_pictures; a single picture is npic = 1): picture p's jobs are blocks
+// [job0[p], job0[p + 1]) of the launch (the launchers fill job0 from njobs)
+struct ExtBatch {
+  int32_t npic = 0, force_glob = 0;
+  int32_t njobs[MC_MAXPIC] = {};
+  int32_t job0[MC_MAXPIC + 1] = {};
+  McParams pic[MC_MAXPIC];
+  const void *jobs[MC_MAXPIC] = {};    // McJob (k_mc_bidir) / AffJob (k_mc_affine)
+  const AffPu *pus[MC_MAXPIC] = {};    // k_mc_affine
+  int32_t *dmvr[MC_MAXPIC] = {};       // k_mc_bidir: the picture's DMVR delta output
+};
+void launch_mc_bidir(ExtBatch &b, hipStream_t s);
+void launch_mc_affine(ExtBatch &b, hipStream_t s);
 void launch_sao(const SaoParams &p, hipStream_t s);
 void launch_alf(const AlfParams &p, hipStream_t s);
 void launch_planes3(const Planes3 &p, hipStream_t s);

@@ -444,9 +444,9 @@ __device__ __forceinline__ void mc_affine1(const McParams &P, const AffJob &J, c
   auto combine = [&](int comp, int a, int b) -> int {
     if (!bi) {
       const int l = pres[0] ? 0 : 1;
-      return U.wp ? wp_uni(P.wp, l, l ? U.l[1].ridx : U.l[0].ridx, comp, a, headRoom, maxv) : a;
+      return U.wp ? wp_uni(*P.wpd, l, l ? U.l[1].ridx : U.l[0].ridx, comp, a, headRoom, maxv) : a;
     }
-    if (U.wp) return wp_bi(P.wp, U.l[0].ridx, U.l[1].ridx, comp, a, b, headRoom, maxv);
+    if (U.wp) return wp_bi(*P.wpd, U.l[0].ridx, U.l[1].ridx, comp, a, b, headRoom, maxv);
     if (U.bcw != 2) {
       const int w1 = a_bcw_w1[U.bcw], w0 = 8 - w1;
       const int shiftNum = headRoom + 3;
@@ -492,7 +492,8 @@ __device__ __forceinline__ void mc_affine1(const McParams &P, const AffJob &J, c
   }
 }
 
-__global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__restrict__ jobs, int njobs, const AffPu *__restrict__ pus, int force_glob) {
+// A tile of one of the batch's pictures per workgroup (picture p: blocks [job0[p], job0[p + 1]))
+__global__ __launch_bounds__(64) void k_mc_affine(ExtBatch B) {
   __shared__ AffLds1 L;
   // XCD runs of 32 tiles (xcd_run_swizzle): neighbouring tiles' windows share an L2
 #if AFF_XCD_RUN > 0
@@ -500,18 +501,27 @@ __global__ __launch_bounds__(64) void k_mc_affine(McParams P, const AffJob *__re
 #else
   const int j = (int)blockIdx.x;
 #endif
-  if (j >= njobs) return;
-  const AffJob J = load_uniform(jobs + j);
-  const AffPu U = load_uniform(pus + J.pu);
-  mc_affine1(P, J, U, force_glob != 0, L);
+  if (j >= B.job0[B.npic]) return;
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < MC_MAXPIC; q++)
+    if (q < B.npic && j >= B.job0[q]) p = q;
+  const McParams &P = B.pic[p];   // (p uniform: scalar-offset reads of the kernel argument)
+  const AffJob J = load_uniform((const AffJob *)B.jobs[p] + (j - B.job0[p]));
+  const AffPu U = load_uniform(B.pus[p] + J.pu);
+  mc_affine1(P, J, U, B.force_glob != 0, L);
 }
 
 }  // namespace
 
-void launch_mc_affine(const McParams &p, const AffJob *jobs, int njobs, const AffPu *pus, hipStream_t s) {
-  if (njobs <= 0) return;
+void launch_mc_affine(ExtBatch &b, hipStream_t s) {
   // VVCR_AFF_FALLBACK=1 (tests): every list reads its windows from the reference picture, the path of
   // unions that do not fit the LDS buffers
   static const int force = [] { const char *e = getenv("VVCR_AFF_FALLBACK"); return e && e[0] == '1' ? 1 : 0; }();
-  hipLaunchKernelGGL(k_mc_affine, dim3(njobs), dim3(64), 0, s, p, jobs, njobs, pus, force);
+  b.force_glob = force;
+  b.job0[0] = 0;
+  for (int p = 0; p < MC_MAXPIC; p++) b.job0[p + 1] = b.job0[p] + (p < b.npic ? b.njobs[p] : 0);
+  const int n = b.job0[b.npic];
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_mc_affine, dim3(n), dim3(64), 0, s, b);
 }

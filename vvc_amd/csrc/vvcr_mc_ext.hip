@@ -672,7 +672,8 @@ __device__ __forceinline__ void bidir_block(const McParams &P, const McJob &J, i
   }
 }
 
-__global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__restrict__ jobs, int njobs, int32_t *dmvr_out) {
+// A job of one of the batch's pictures per workgroup (picture p: blocks [job0[p], job0[p + 1]))
+__global__ __launch_bounds__(64) void k_mc_bidir(ExtBatch B) {
   __shared__ BidirLds S;
   // XCD runs of 32 jobs (xcd_run_swizzle): neighbouring jobs' reference windows share an L2
 #if BIDIR_XCD_RUN > 0
@@ -680,8 +681,14 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
 #else
   const int j = blockIdx.x;
 #endif
-  if (j >= njobs) return;
-  const McJob J = load_uniform(jobs + j);
+  if (j >= B.job0[B.npic]) return;
+  int p = 0;
+#pragma unroll
+  for (int q = 1; q < MC_MAXPIC; q++)
+    if (q < B.npic && j >= B.job0[q]) p = q;
+  const McParams &P = B.pic[p];   // (p uniform: scalar-offset reads of the kernel argument)
+  int32_t *dmvr_out = B.dmvr[p];
+  const McJob J = load_uniform((const McJob *)B.jobs[p] + (j - B.job0[p]));
   // block sizes: DMVR sub-blocks and xSubPuBio tiles of PUs with w, h >= 8 and w * h >= 128 (the host checks
   // multiples of 8): 16x16, 16x8, 8x16; 8x8 is not produced by the reference's conditions but handled
   if (J.w == 16 && J.h == 16) bidir_block<16, 16>(P, J, dmvr_out, S);
@@ -692,7 +699,10 @@ __global__ __launch_bounds__(64) void k_mc_bidir(McParams P, const McJob *__rest
 
 }  // namespace
 
-void launch_mc_bidir(const McParams &p, const McJob *jobs, int njobs, int32_t *dmvr_out, hipStream_t s) {
-  if (njobs <= 0) return;
-  hipLaunchKernelGGL(k_mc_bidir, dim3(njobs), dim3(BIDIR_WG), 0, s, p, jobs, njobs, dmvr_out);
+void launch_mc_bidir(ExtBatch &b, hipStream_t s) {
+  b.job0[0] = 0;
+  for (int p = 0; p < MC_MAXPIC; p++) b.job0[p + 1] = b.job0[p] + (p < b.npic ? b.njobs[p] : 0);
+  const int n = b.job0[b.npic];
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_mc_bidir, dim3(n), dim3(BIDIR_WG), 0, s, b);
 }
