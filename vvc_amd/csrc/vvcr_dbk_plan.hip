@@ -23,7 +23,7 @@
 // Kernels, per picture, on the picture's lane before the deblocking filter:
 //   k_dbkp_maps      CU index maps (luma 4x4 / chroma 2x2 units) and TU index maps, a wave per CU / TU
 //                    record; the CU's waves list the units on their CUs' edge lines (items)
-//   k_dbkp_units<P>  steps 1-5, a thread per item of pass P (blockIdx.y: the direction)
+//   k_dbkp_units<D,P> steps 1-5, a thread per item of pass P and direction D
 // Inputs: compact CU / PU / TU records (DbCu / DbPu / DbTu, vvcr_dbk.h, built by pack_dbk_inputs) and the
 // 4x4 motion field (MotionRec) of the picture, uploaded with its work lists.
 //
@@ -52,63 +52,78 @@ struct UnitState {
   int edge, bs, tedge, lp0, lq0, lp1, lq1;
 };
 
-// One CU, wave-uniform scalars (its TU / PU records through the pointers T / PU)
+// Records come in whole, as 16-byte loads into registers, and their fields are taken by shifts (r06: a lane
+// used to read each 2-byte field where it was used: ~250 short loads of 64 scattered addresses per wave
+// instruction kept the texture address units busy and the waves waiting). Fields are picked with constant
+// indices only, so no record is ever addressed through a run-time index (that would put it in scratch).
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ int lo16s(uint32_t v) { return (int)(int16_t)(uint16_t)(v & 0xffffu); }
+__device__ __forceinline__ int hi16s(uint32_t v) { return (int)(int16_t)(uint16_t)(v >> 16); }
+// dword 7 of a DbTu: cbf | jccr << 8 | cqp[0] << 16 | cqp[1] << 24
+__device__ __forceinline__ uint32_t tu_word7(const DbkPlanArgs &A, int t) { return ((const uint32_t *)(A.tu + t))[7]; }
+__device__ __forceinline__ int w7_cqp(uint32_t w, int k) { return (int)(int8_t)(uint8_t)(w >> (16 + 8 * k)); }
+
+// One CU: its record, its PU's and the luma / chroma areas of its TUs (b[0], b[1]: tb[k][0..3] = x | y << 16,
+// w | h << 16 of luma, then of chroma)
 struct Cu {
-  const DbTu *T;
-  const DbPu *PU;
+  uint32_t tb[MAXTU][4];
+  int t0;                // its first TU's index
   int flags, qp, ntu, npu;
   int x, y, w, h, cx, cy;
   int a0, a1, a2, a3;    // luma area (a chroma-tree CU: its chroma area doubled)
   int yv, isp, ch, cpx, cpy;
   int left, top, internal;
   int sub;               // SbTMVP / affine: sub-block edges
+  int puw;               // the PU's luma width (0: none)
   int pux, puy;          // the PU origin in the CU's channel
   int pa0, pa1, pa2, pa3;   // the PU's luma area (a chroma-tree CU: the CU's)
+  // b[C][K] of TU k (C: 0 luma, 1 chroma; K: x, y, w, h)
+  template <int C, int K> __device__ __forceinline__ int tb_f(int k) const {
+    const uint32_t v = tb[k][2 * C + K / 2];
+    return (K & 1) ? hi16s(v) : lo16s(v);
+  }
 };
 
 __device__ __forceinline__ Cu load_cu(const DbkPlanArgs &A, int i) {
-  const DbCu *c = A.cu + i;
+  const u32x4a *c = (const u32x4a *)(A.cu + i);
+  const u32x4a c0 = c[0], c1 = c[1];   // x y w h cx cy cw ch | firstpu firsttu npu ntu qp flags
   Cu R;
-  R.flags = c->flags; R.qp = c->qp; R.ntu = c->ntu; R.npu = c->npu;
+  R.x = lo16s(c0.x); R.y = hi16s(c0.x); R.w = lo16s(c0.y); R.h = hi16s(c0.y); R.cx = lo16s(c0.z); R.cy = hi16s(c0.z);
+  const int cw = lo16s(c0.w), chh = hi16s(c0.w);
+  const int firstpu = (int)c1.x;
+  R.t0 = (int)c1.y;
+  R.npu = lo16s(c1.z); R.ntu = hi16s(c1.z);
+  R.qp = lo16s(c1.w); R.flags = (int)(c1.w >> 16);
   if (R.ntu > MAXTU || R.npu > 1 || R.ntu < 0 || R.npu < 0) {   // never in VVC: inconsistent descriptors
     atomicOr(A.err, 2);
     R.ntu = min(max(R.ntu, 0), MAXTU); R.npu = min(max(R.npu, 0), 1);
   }
-  R.T = A.tu + c->firsttu;
-  R.PU = A.pu + max(c->firstpu, 0);
-  R.x = c->x; R.y = c->y; R.w = c->w; R.h = c->h; R.cx = c->cx; R.cy = c->cy;
+#pragma unroll
+  for (int k = 0; k < MAXTU; k++) {
+    u32x4a v = {0u, 0u, 0u, 0u};
+    if (k < R.ntu) v = *(const u32x4a *)(A.tu + R.t0 + k);
+    R.tb[k][0] = v.x; R.tb[k][1] = v.y; R.tb[k][2] = v.z; R.tb[k][3] = v.w;
+  }
+  u32x4a pv = {0u, 0u, 0u, 0u};   // x y w h cx cy sub
+  if (R.npu) pv = *(const u32x4a *)(A.pu + max(firstpu, 0));
   R.yv = (R.flags & DBC_YVALID) ? 1 : 0;
   R.isp = (R.flags & DBC_ISP) ? 1 : 0;
   R.ch = (R.flags & DBC_CHTYPE) ? 1 : 0;
   R.a0 = R.yv ? R.x : 2 * R.cx; R.a1 = R.yv ? R.y : 2 * R.cy;
-  R.a2 = R.yv ? R.w : 2 * c->cw; R.a3 = R.yv ? R.h : 2 * c->ch;
+  R.a2 = R.yv ? R.w : 2 * cw; R.a3 = R.yv ? R.h : 2 * chh;
   R.cpx = R.ch ? R.cx : R.x; R.cpy = R.ch ? R.cy : R.y;
   if (A.dbk_disable) { R.left = R.top = R.internal = 0; }
   else { R.internal = 1; R.left = R.cpx > 0 && !(R.flags & DBC_NOLEFT); R.top = R.cpy > 0 && !(R.flags & DBC_NOTOP); }
-  R.sub = R.npu && ((R.PU->sub & 1) || (R.flags & DBC_AFFINE));
-  R.pux = R.npu ? (R.ch ? R.PU->cx : R.PU->x) : R.cpx;
-  R.puy = R.npu ? (R.ch ? R.PU->cy : R.PU->y) : R.cpy;
+  const int pX = lo16s(pv.x), pY = hi16s(pv.x), pW = lo16s(pv.y), pH = hi16s(pv.y), pCx = lo16s(pv.z), pCy = hi16s(pv.z);
+  R.sub = R.npu && ((pv.w & 1) || (R.flags & DBC_AFFINE));
+  R.puw = R.npu ? pW : 0;
+  R.pux = R.npu ? (R.ch ? pCx : pX) : R.cpx;
+  R.puy = R.npu ? (R.ch ? pCy : pY) : R.cpy;
   const bool own = R.npu && R.yv;
-  R.pa0 = own ? R.PU->x : R.a0; R.pa1 = own ? R.PU->y : R.a1;
-  R.pa2 = own ? R.PU->w : R.a2; R.pa3 = own ? R.PU->h : R.a3;
+  R.pa0 = own ? pX : R.a0; R.pa1 = own ? pY : R.a1;
+  R.pa2 = own ? pW : R.a2; R.pa3 = own ? pH : R.a3;
   return R;
-}
-
-// the edge lines of the CU in direction DIR (offsets from the CU origin in 4-sample units of the CU's
-// channel: TU, PU and sub-block origins)
-template <int DIR>
-__device__ __forceinline__ uint64_t cu_lines(const Cu &R) {
-  uint64_t m = 0;
-  auto add = [&](int v) { if (v >= 0 && v < 64) m |= 1ull << v; };
-#pragma unroll
-  for (int k = 0; k < MAXTU; k++)
-    if (k < R.ntu) add(DIR == VER ? ((R.ch ? R.T[k].b[1][0] : R.T[k].b[0][0]) - R.cpx) / 4 : ((R.ch ? R.T[k].b[1][1] : R.T[k].b[0][1]) - R.cpy) / 4);
-  if (R.npu) {
-    add(DIR == VER ? (R.pux - R.cpx) / 4 : (R.puy - R.cpy) / 4);
-    if (R.sub)
-      for (int off = 8; off < (DIR == VER ? R.pa2 : R.pa3); off += 8) add(DIR == VER ? (R.pux + off - R.cpx) / 4 : (R.puy + off - R.cpy) / 4);
-  }
-  return m;
 }
 
 __device__ __forceinline__ int bs_set(int v, int comp) { return v << (comp * 2); }
@@ -136,11 +151,10 @@ struct Unit {
   // (X, Y) are its component samples
   template <int COMP>
   __device__ __forceinline__ bool tu_edge(int k, int ux, int uy, int &X, int &Y) const {
-    const int16_t *b = R.T[k].b[COMP];
-    const int bx = b[0], by = b[1], bw = b[2], bh = b[3];
+    const int bx = R.tb_f<COMP, 0>(k), by = R.tb_f<COMP, 1>(k), bw = R.tb_f<COMP, 2>(k), bh = R.tb_f<COMP, 3>(k);
     if (bw <= 0 || bh <= 0) return false;
     const int cux = COMP ? R.cx : R.x, cuy = COMP ? R.cy : R.y;
-    // (bx == cux ? left : internal), without a select of two loads: left implies internal
+    // (bx == cux ? left : internal): left implies internal
     if (!(ver ? (R.internal & ((bx != cux) | R.left)) : (R.internal & ((by != cuy) | R.top)))) return false;
     constexpr int g = COMP ? 1 : 2, step = 1 << g;   // the unit's component samples: (ux, uy) << g
     X = ux << g; Y = uy << g;
@@ -160,35 +174,41 @@ struct Unit {
   }
 
   // the index (in A.tu) of the CU's TU holding sample (x, y) of channel c (CodingStructure::getTU: the index
-  // maps' last writer; an ISP CU's first sub-partition that holds it)
+  // maps' last writer; an ISP CU's first sub-partition that holds it), -1 for none
   __device__ __forceinline__ int own_tu(int c, int x, int y) const {
     int f = -1;
+    const int g = 2 - c;   // the index maps' unit: 4x4 luma / 2x2 chroma samples
 #pragma unroll
     for (int k = MAXTU - 1; k >= 0; k--) {
       if (k >= R.ntu) continue;
-      const int16_t *b = c ? R.T[k].b[1] : R.T[k].b[0];
-      const int b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
-      const int g = 2 - c;   // the index maps' unit: 4x4 luma / 2x2 chroma samples
+      const int b0 = c ? R.tb_f<1, 0>(k) : R.tb_f<0, 0>(k), b1 = c ? R.tb_f<1, 1>(k) : R.tb_f<0, 1>(k);
+      const int b2 = c ? R.tb_f<1, 2>(k) : R.tb_f<0, 2>(k), b3 = c ? R.tb_f<1, 3>(k) : R.tb_f<0, 3>(k);
       const bool in = b2 > 0 && b3 > 0 && (R.isp && c == 0 ? (x >= b0 && x < b0 + b2 && y >= b1 && y < b1 + b3)
                                                            : ((x >> g) >= (b0 >> g) && (x >> g) < ((b0 + b2 + (1 << g) - 1) >> g) &&
                                                               (y >> g) >= (b1 >> g) && (y >> g) < ((b1 + b3 + (1 << g) - 1) >> g)));
       if (in && (f < 0 || (R.isp && c == 0))) f = k;
     }
-    if (f < 0) { atomicOr(A.err, 2); f = 0; }
-    return (int)(R.T - A.tu) + f;
+    return f < 0 ? -1 : R.t0 + f;
+  }
+  // a TU index found by own_tu / map_tu, or the error bit and the stand-in record (fb) for none
+  __device__ __forceinline__ int use_tu(int t, int fb) const {
+    if (t < 0) { atomicOr(A.err, 2); return fb; }
+    return t;
   }
 
   // a TU index from an index map value t at the neighbouring unit (an ISP CU's luma area: its
-  // sub-partition holding sample (x, y))
+  // sub-partition holding sample (x, y)); -1 for a hole
   __device__ __forceinline__ int map_tu(int t, int x, int y) const {
-    if (t == -1) { atomicOr(A.err, 2); return 0; }
-    if (t >= 0) return t;
+    if (t >= -1) return t;
     t = -t - 2;
+    int r = t;
+#pragma unroll 1
     for (int k = 0; k < 4 && t + k < A.ntu; k++) {
-      const int16_t *b = A.tu[t + k].b[0];
-      if (x >= b[0] && x < b[0] + b[2] && y >= b[1] && y < b[1] + b[3]) return t + k;
+      const u32x2a v = *(const u32x2a *)(A.tu + t + k);   // b[0]: x | y << 16, w | h << 16
+      const int bx = lo16s(v.x), by = hi16s(v.x), bw = lo16s(v.y), bh = hi16s(v.y);
+      if (x >= bx && x < bx + bw && y >= by && y < by + bh) { r = t + k; break; }
     }
-    return t;
+    return r;
   }
   __device__ __forceinline__ int map_cu(int i) const {
     if (i < 0) { atomicOr(A.err, 2); return 0; }   // "deblocking: no CU covers a neighbouring position"
@@ -243,16 +263,26 @@ struct Unit {
       mtu0 = map_val(A, t0);
       mtu1 = map_val(A, t1);
     }
-    const DbCu &cPr = A.cu[max(mcu, 0)];
-    const int fPm = pin ? 0 : (int)cPr.flags, qpPm = pin ? 0 : (int)cPr.qp;
+    // dword 7 of the P-side CU record: qp | flags << 16
+    const uint32_t cPw = pin ? 0u : ((const uint32_t *)(A.cu + max(mcu, 0)))[7];
+    const int fPm = (int)(cPw >> 16), qpPm = lo16s(cPw);
     // (no motion edge at the picture edge; no field: a picture without inter CUs never asks for motion)
     MotionRec mp{}, mq{};
     if (A.motion) { mp = A.motion[pedge ? u : pu]; mq = A.motion[u]; }
+    // The TUs the rules read, each found once: the P side's luma / chroma TU at the sample left of / above
+    // the unit's first sample (inside the CU: the CU's own TUs, else the neighbour's index-map entry; the
+    // stand-in for none is the CU's first TU / record 0, with the error bit where a rule uses it), and the
+    // unit's own TU in the CU's channel
+    const int fbP = pin ? R.t0 : 0;
+    const int tpL = pedge ? -1 : (pin ? own_tu(0, ver ? px - 1 : px, ver ? py : py - 1) : map_tu(mtu0, ver ? px - 1 : px, ver ? py : py - 1));
+    const int cx2 = 2 * x4, cy2 = 2 * y4;   // the unit's first chroma sample
+    const int tpC = pedge ? -1 : (pin ? own_tu(1, ver ? cx2 - 1 : cx2, ver ? cy2 : cy2 - 1) : mtu1);
+    const int tqO = R.ch ? own_tu(1, cx2, cy2) : own_tu(0, px, py);
     // step 1 (TU calls, then the PU's call and its sub-block lines)
 #pragma unroll
     for (int k = 0; k < MAXTU; k++) {
       if (k >= R.ntu) continue;
-      if (R.yv) set_edges(st, R.T[k].b[0][0], R.T[k].b[0][1], R.T[k].b[0][2], R.T[k].b[0][3], R.internal, false);
+      if (R.yv) set_edges(st, R.tb_f<0, 0>(k), R.tb_f<0, 1>(k), R.tb_f<0, 2>(k), R.tb_f<0, 3>(k), R.internal, false);
       else set_edges(st, R.a0, R.a1, R.a2, R.a3, R.internal, false);
     }
     if (R.npu) {
@@ -269,8 +299,8 @@ struct Unit {
       if (k >= R.ntu) continue;
       int X, Y;
       if (tu_edge<0>(k, x4, y4, X, Y)) {
-        const int sizeQ = ver ? R.T[k].b[0][2] : R.T[k].b[0][3];
-        const int tp = pin ? own_tu(0, ver ? X - 1 : X, ver ? Y : Y - 1) : map_tu(mtu0, ver ? X - 1 : X, ver ? Y : Y - 1);
+        const int sizeQ = ver ? R.tb_f<0, 2>(k) : R.tb_f<0, 3>(k);
+        const int tp = use_tu(tpL, fbP);   // (X - 1, Y) / (X, Y - 1): X, Y are px, py
         const int sizeP = ver ? A.tu[tp].b[0][2] : A.tu[tp].b[0][3];
         st.tedge = 1;
         const bool small = sizeP <= 4 || sizeQ <= 4;
@@ -278,14 +308,14 @@ struct Unit {
         st.lp0 = small ? 1 : (sizeP >= 32 ? 7 : 3);
       }
       if (tu_edge<1>(k, x4, y4, X, Y)) {
-        const int sizeQ = ver ? R.T[k].b[1][2] : R.T[k].b[1][3];
-        const int tp = pin ? own_tu(1, ver ? X - 1 : X, ver ? Y : Y - 1) : map_tu(mtu1, 0, 0);
+        const int sizeQ = ver ? R.tb_f<1, 2>(k) : R.tb_f<1, 3>(k);
+        const int tp = use_tu(tpC, fbP);   // X, Y: the unit's first chroma sample
         const int sizeP = ver ? A.tu[tp].b[1][2] : A.tu[tp].b[1][3];
         st.lq1 = st.lp1 = (sizeQ >= 8 && sizeP >= 8) ? 3 : 1;
       }
     }
     // step 3: sub-block lengths (:550), units every 8 samples across, every 4 along the PU
-    if (R.sub && R.PU->w > 0) {
+    if (R.sub && R.puw > 0) {
       const int outer = ver ? R.pa2 : R.pa3, inner = ver ? R.pa3 : R.pa2;
       const int a8 = ver ? px - R.pa0 : py - R.pa1, b4 = ver ? py - R.pa1 : px - R.pa0;
       if (a8 >= 0 && a8 < outer && !(a8 & 7) && b4 >= 0 && b4 < inner) {
@@ -326,12 +356,10 @@ struct Unit {
           } else {
             int tmp = 0;
             if (marker) {
-              const int sh = R.yv ? 0 : 1;
-              const int qx = px >> sh, qy = py >> sh;
-              const int tq = own_tu(R.ch, qx, qy);
-              const int tp = !pin ? map_tu(R.ch ? mtu1 : mtu0, ver ? qx - 1 : qx, ver ? qy : qy - 1)
-                                  : (R.ntu == 1 && !R.isp) ? tq : own_tu(R.ch, ver ? qx - 1 : qx, ver ? qy : qy - 1);
-              const int cq = A.tu[tq].cbf, cp = A.tu[tp].cbf, jq = A.tu[tq].jccr, jp = A.tu[tp].jccr;
+              // (the CU's channel: a luma CU's samples (px, py), a chroma-tree CU's (px, py) / 2)
+              const int tq = use_tu(tqO, R.t0), tp = use_tu(R.ch ? tpC : tpL, fbP);
+              const uint32_t wq = tu_word7(A, tq), wp = tu_word7(A, tp);
+              const int cq = wq & 255, cp = wp & 255, jq = (wq >> 8) & 255, jp = (wp >> 8) & 255;
               if ((cq & 1) || (cp & 1)) tmp += bs_set(1, 0);
               if ((cq & 2) || (cp & 2) || jq || jp) tmp += bs_set(1, 1);
               if ((cq & 4) || (cp & 4) || jq || jp) tmp += bs_set(1, 2);
@@ -366,22 +394,19 @@ struct Unit {
       if (!((ver && (r % parts + o) % 4) || (!ver && (r / parts + o) % 4)) && (bS0 || bS1)) {
         // the P-side CU: of the chroma map when the luma one is of a tree-split area or the picture is dual tree
         int fP = pin ? fQ : fPm;
-        if (!pin && R.ch == 0 && ((fPm & DBC_TREE) || A.dual_tree)) fP = A.cu[map_cu(mcu1)].flags;
+        if (!pin && R.ch == 0 && ((fPm & DBC_TREE) || A.dual_tree)) fP = (int)(((const uint32_t *)(A.cu + map_cu(mcu1)))[7] >> 16);
         const bool large = st.lp1 >= 3 && st.lq1 >= 3;
         const bool ctbh = !ver && (py & ((1 << A.ctu_log2) - 1)) == 0;
         uint32_t w = (uint32_t)large << 4 | (uint32_t)ctbh << 19;
         bool any = false;
-        const int shQ = R.yv ? 0 : 1;
-        const int tq = own_tu(R.ch, px >> shQ, py >> shQ);
-        const int chP = (fP & DBC_CHTYPE) ? 1 : 0, shP = (fP & DBC_YVALID) ? 0 : 1;
-        const int p1x = px >> shP, p1y = py >> shP;
-        const int tp = pin ? own_tu(chP, ver ? p1x - 1 : p1x, ver ? p1y : p1y - 1)
-                           : map_tu(chP ? mtu1 : mtu0, ver ? p1x - 1 : p1x, ver ? p1y : p1y - 1);
+        // (the P CU's channel: a luma CU's samples (px, py), a chroma-tree CU's (px, py) / 2)
+        const int tq = use_tu(tqO, R.t0), tp = use_tu((fP & DBC_CHTYPE) ? tpC : tpL, fbP);
+        const uint32_t wq = tu_word7(A, tq), wp = tu_word7(A, tp);
 #pragma unroll
         for (int k = 0; k < 2; k++) {
           const int b = k ? bS1 : bS0;
           if (!(b == 2 || (large && b == 1))) continue;
-          const int qp = (A.tu[tq].cqp[k] + A.tu[tp].cqp[k] + 1) >> 1;
+          const int qp = (w7_cqp(wq, k) + w7_cqp(wp, k) + 1) >> 1;
           w |= (uint32_t)b << (2 * k) | (uint32_t)((qp + 64) & 127) << (5 + 7 * k);
           any = true;
         }
@@ -400,8 +425,8 @@ __device__ __forceinline__ bool in_shard(const DbkPlanArgs &A, const Cu &R) {
 }
 
 // The lanes of a 256-lane workgroup with wl / wc != 0 append (x4, y4, w) to the luma / chroma list of
-// direction dir (lists 2 dir, 2 dir + 1): one atomic per list and workgroup, the waves' runs placed by
-// their counts in LDS (an atomic per wave and list put 10 k atomics a 4K picture on the same four
+// direction dir (lists 2 dir, 2 dir + 1): one atomic per workgroup for both lists, the waves' runs placed
+// by their counts in LDS (an atomic per wave and list put 10 k atomics a 4K picture on the same four
 // counters). more: the caller loops again (the LDS counts are reused: a third barrier).
 __device__ __forceinline__ void append_wg(const DbkPlanArgs &A, int dir, uint32_t wl, uint32_t wc, int x4, int y4, bool more) {
   __shared__ int s_cnt[4][2];
@@ -410,9 +435,14 @@ __device__ __forceinline__ void append_wg(const DbkPlanArgs &A, int dir, uint32_
   const unsigned long long ml = __ballot(wl != 0), mc = __ballot(wc != 0);
   if (lane == 0) { s_cnt[wv][0] = __popcll(ml); s_cnt[wv][1] = __popcll(mc); }
   __syncthreads();
-  if (threadIdx.x < 2) {
-    const int t = s_cnt[0][threadIdx.x] + s_cnt[1][threadIdx.x] + s_cnt[2][threadIdx.x] + s_cnt[3][threadIdx.x];
-    s_base[threadIdx.x] = t ? atomicAdd(&A.counts[2 * dir + threadIdx.x], t) : 0;
+  if (threadIdx.x == 0) {
+    // both lists' counts in one 64-bit atomic (counts[2 dir] and counts[2 dir + 1] are one aligned pair:
+    // luma the low word)
+    const unsigned long long tl = (unsigned)(s_cnt[0][0] + s_cnt[1][0] + s_cnt[2][0] + s_cnt[3][0]);
+    const unsigned long long tc = (unsigned)(s_cnt[0][1] + s_cnt[1][1] + s_cnt[2][1] + s_cnt[3][1]);
+    const unsigned long long old = (tl | tc) ? atomicAdd((unsigned long long *)(A.counts + 2 * dir), tl | tc << 32) : 0ull;
+    s_base[0] = (int)(uint32_t)old;
+    s_base[1] = (int)(uint32_t)(old >> 32);
   }
   __syncthreads();
   const unsigned long long below = (1ull << lane) - 1;
@@ -429,63 +459,61 @@ __device__ __forceinline__ void append_wg(const DbkPlanArgs &A, int dir, uint32_
   if (more) __syncthreads();
 }
 
-// index maps: CU per 4x4 luma / 2x2 chroma unit, TU likewise (an ISP CU's luma area holds -(first TU) - 2);
-// a wave per CU / TU record, a lane per unit. A CU's wave also lists the units on its edge lines: an item
-// (CU index << 10 | line << 5 | unit along the line) per unit, in the list of its pass and direction
-// (A.items + (2 * pass + dir) * cap, lengths A.nitems[2 * pass + dir]).
-__global__ __launch_bounds__(256) void k_dbkp_maps(DbkPlanArgs A) {
-  __shared__ uint8_t s_line[4][2][32];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + wv;
-  // v: the index (bit 23: an ISP CU's luma area), tagged with the picture's generation
-  auto fill = [&](int32_t *m, int x, int y, int w, int h, int s, int v, bool atomic) {
-    const int x0 = x >> s, y0 = y >> s, nx = cdiv(x + w, s) - x0, ny = cdiv(y + h, s) - y0;
+// index maps: CU per 4x4 luma / 2x2 chroma unit, TU likewise (an ISP CU's luma area holds -(first TU) - 2).
+// A CU's record also lists the units on its edge lines: an item (CU index << 10 | line << 5 | unit along the
+// line) per unit, in the list of its pass and direction (A.items + (2 * pass + dir) * cap, lengths
+// A.nitems[2 * pass + dir]). Records are the CUs, then the TUs, a wave each, a lane per unit (r06, 4K
+// pictures: 8 / 16 / 32 lanes per record, several records per wave, took 36 / 24 / 17 us against 11.8).
+// a record's work with lanes s, s + st, ...: its map fills and, for a CU, its items. The records of one map
+// never share a unit (luma blocks lie on the 4-sample grid, an ISP CU's sub-partitions map as the CU's area;
+// chroma blocks on the 2-sample grid), so the fills are plain stores (r06: atomicMax "later record wins"
+// made the kernel atomic-bound, 13 us per 4K picture); the generation tag tells a stale entry from this
+// picture's.
+__device__ __forceinline__ void maps_record(const DbkPlanArgs &A, int i, int s, int st) {
+  auto fill = [&](int32_t *m, int x, int y, int w, int h, int sh, int v) {
+    const int x0 = x >> sh, y0 = y >> sh, nx = cdiv(x + w, sh) - x0, ny = cdiv(y + h, sh) - y0;
     const int32_t e = (int32_t)((uint32_t)A.gen << DBKP_GEN_SHIFT | (uint32_t)v);
-    for (int j = lane; j < nx * ny; j += 64) {
-      int32_t *d = &m[(y0 + j / nx) * A.W4 + x0 + j % nx];
-      // a later record wins where two cover a unit (the host planner's order); an older generation's entry
-      // holds a smaller tag (unsigned: the generation is the top byte)
-      if (atomic) atomicMax((unsigned int *)d, (unsigned int)e);
-      else *d = e;
-    }
+    for (int j = s; j < nx * ny; j += st) m[(y0 + j / nx) * A.W4 + x0 + j % nx] = e;
   };
   if (i < A.ncu) {
     const DbCu &c = A.cu[i];
-    if (i > DBKP_IDX_MASK) { if (lane == 0) atomicOr(A.err, 4); return; }
-    if (c.flags & DBC_YVALID) fill(A.cu_map[0], c.x, c.y, c.w, c.h, 2, i, true);
-    if (c.flags & DBC_CVALID) fill(A.cu_map[1], c.cx, c.cy, c.cw, c.ch, 1, i, true);
-    // the units on its edge lines (lines and list offsets from pack_dbk_inputs)
+    if (i > DBKP_IDX_MASK) { if (s == 0) atomicOr(A.err, 4); return; }
+    if (c.flags & DBC_YVALID) fill(A.cu_map[0], c.x, c.y, c.w, c.h, 2, i);
+    if (c.flags & DBC_CVALID) fill(A.cu_map[1], c.cx, c.cy, c.cw, c.ch, 1, i);
+    // the units on its edge lines (lines and list offsets from pack_dbk_inputs), line by line
     const int yv = (c.flags & DBC_YVALID) ? 1 : 0, ch = (c.flags & DBC_CHTYPE) ? 1 : 0;
     const int wq = (yv ? c.w : 2 * c.cw) >> 2, hq = (yv ? c.h : 2 * c.ch) >> 2;
 #pragma unroll
     for (int d = 0; d < 2; d++) {
-      const uint32_t m = c.lines[d];
+      uint32_t m = c.lines[d];
       const int n = d == VER ? hq : wq;
-      const bool on = lane < 32 && (m >> lane & 1);
-      const unsigned long long b = __ballot(on);
-      if (on) s_line[wv][d][__popcll(b & ((1ull << lane) - 1))] = (uint8_t)lane;
-      // (the wave's own LDS writes: the LDS runs one wave's instructions in order; the memory clobber keeps
-      // the compiler from moving the reads above the writes)
-      asm volatile("" ::: "memory");
-      const int total = __popcll(b) * n, k = 2 * ch + d, base = c.item0[d];
-      if (base + total > A.cap || n > 32) { if (lane == 0 && total) atomicOr(A.err, 4); continue; }
-      for (int j = lane; j < total; j += 64)
-        A.items[(size_t)k * A.cap + base + j] = (uint32_t)i << 10 | (uint32_t)s_line[wv][d][j / n] << 5 | (uint32_t)(j % n);
+      const int total = __popc(m) * n, k = 2 * ch + d;
+      int base = c.item0[d];
+      if (base + total > A.cap || n > 32) { if (s == 0 && total) atomicOr(A.err, 4); continue; }
+      uint32_t *out = A.items + (size_t)k * A.cap;
+      for (; m; m &= m - 1, base += n) {
+        const uint32_t line = (uint32_t)(__ffs(m) - 1);
+        for (int j = s; j < n; j += st) out[base + j] = (uint32_t)i << 10 | line << 5 | (uint32_t)j;
+      }
     }
   } else if (i < A.ncu + A.ntu) {
     const int t = i - A.ncu;
     const DbTu &tu = A.tu[t];
-    const DbCu &c = A.cu[tu.cu];
     const int16_t *b0 = tu.b[0], *b1 = tu.b[1];
     if (b0[2] > 0 && b0[3] > 0) {
+      const DbCu &c = A.cu[tu.cu];
       if (c.flags & DBC_ISP) {
-        if (t == c.firsttu) fill(A.tu_map[0], c.x, c.y, c.w, c.h, 2, DBKP_ISP | t, false);
+        if (t == c.firsttu) fill(A.tu_map[0], c.x, c.y, c.w, c.h, 2, DBKP_ISP | t);
       } else {
-        fill(A.tu_map[0], b0[0], b0[1], b0[2], b0[3], 2, t, true);
+        fill(A.tu_map[0], b0[0], b0[1], b0[2], b0[3], 2, t);
       }
     }
-    if (b1[2] > 0 && b1[3] > 0) fill(A.tu_map[1], b1[0], b1[1], b1[2], b1[3], 1, t, true);
+    if (b1[2] > 0 && b1[3] > 0) fill(A.tu_map[1], b1[0], b1[1], b1[2], b1[3], 1, t);
   }
+}
+
+__global__ __launch_bounds__(256) void k_dbkp_maps(DbkPlanArgs A) {
+  maps_record(A, blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, 64);
 }
 
 // The items of pass PASS, direction DIR (blockIdx.y), a lane each, grid-stride; local_dual: the luma pass
@@ -512,17 +540,26 @@ __device__ __forceinline__ void items_dir(const DbkPlanArgs &A, const int (*rp)[
         const int v = A.state[DIR][u];
         st.edge = v >> 7; st.bs = v & 63;
       }
+#ifdef DBKP_ABL_RUN   // diagnostics ablation: no replay (results wrong)
+      wl = R.flags == 0xffff ? 1u : 0u;
+#else
       Unit<DIR>{A, rp, R, x4, y4}.run(o, st, wl, wc);
+#endif
       if (PASS == 0 && local_dual) A.state[DIR][u] = (uint8_t)(st.edge << 7 | (st.bs & 63));
       }
     }
+#ifdef DBKP_ABL_APPEND   // diagnostics ablation: no list append (results wrong)
+    if ((wl | wc) == 0xffffffffu) A.out[j0 + threadIdx.x] = DbkSeg{(uint16_t)x4, (uint16_t)y4, wl};
+#else
     append_wg(A, DIR, wl, wc, x4, y4, j0 + (int)(gridDim.x * 256) < total);
+#endif
   }
 }
 
-// the units on the edge lines of the CUs of one pass (pass 0: the luma tree, pass 1: the chroma tree), a
-// thread each; blockIdx.y: the direction
-template <int PASS>
+// the units on the edge lines of the CUs of one pass (pass 0: the luma tree, pass 1: the chroma tree) in
+// direction DIR, a thread each (one kernel per direction: the two directions in one kernel behind a
+// blockIdx.y branch doubled its code, r06)
+template <int DIR, int PASS>
 __global__ __launch_bounds__(256) void k_dbkp_units(DbkPlanArgs A) {
   __shared__ int s_ref_poc[2][VVCR_MAX_REF];
   if (threadIdx.x < 2 * VVCR_MAX_REF) {
@@ -532,8 +569,7 @@ __global__ __launch_bounds__(256) void k_dbkp_units(DbkPlanArgs A) {
     s_ref_poc[threadIdx.x / VVCR_MAX_REF][threadIdx.x % VVCR_MAX_REF] = v;
   }
   __syncthreads();
-  if (blockIdx.y == 0) items_dir<VER, PASS>(A, s_ref_poc);
-  else items_dir<HOR, PASS>(A, s_ref_poc);
+  items_dir<DIR, PASS>(A, s_ref_poc);
 }
 
 }  // namespace
@@ -548,12 +584,18 @@ void launch_dbk_plan(const DbkPlanArgs &a, hipStream_t s) {
   if (local_dual) VVCR_CHECK_HIP(hipMemsetAsync(a.state[0], 0, 2 * a.state_pitch, s));
   const int nm = a.ncu + a.ntu;
   hipLaunchKernelGGL(k_dbkp_maps, dim3(std::max(1, (nm + 3) / 4)), dim3(256), 0, s, a);
-  for (int pass = 0; pass < 2; pass++) {
-    const int n = std::max(a.nitems[2 * pass], a.nitems[2 * pass + 1]);
-    if (n == 0) continue;
-    const dim3 g((unsigned)std::min(2048, (n + 255) / 256), 2);   // (grid-stride beyond)
-    if (pass == 0) hipLaunchKernelGGL(k_dbkp_units<0>, g, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_dbkp_units<1>, g, dim3(256), 0, s, a);
-  }
+  for (int pass = 0; pass < 2; pass++)
+    for (int dir = 0; dir < 2; dir++) {
+      const int n = a.nitems[2 * pass + dir];
+      if (n == 0) continue;
+      const dim3 g((unsigned)std::min(4096, (n + 255) / 256));   // (grid-stride beyond)
+      if (pass == 0) {
+        if (dir == VER) hipLaunchKernelGGL((k_dbkp_units<VER, 0>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_dbkp_units<HOR, 0>), g, dim3(256), 0, s, a);
+      } else {
+        if (dir == VER) hipLaunchKernelGGL((k_dbkp_units<VER, 1>), g, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_dbkp_units<HOR, 1>), g, dim3(256), 0, s, a);
+      }
+    }
   VVCR_CHECK_HIP(hipGetLastError());
 }
