@@ -441,7 +441,7 @@ struct vvcr_ctx {
 
 // The device error words (after the lanes are idle): [0] the persistent intra kernel's dependency-wait
 // timeout (its waits poll this word and give up when it is set), [1] the device deblocking planner
-// (bit 2: a position no CU / TU covers, bit 4: list overflow) — a word of its own, so that it never
+// (bit 2: a position no CU / TU covers, bit 4: list overflow, bit 8: not a wave64 device) — a word of its own, so that it never
 // cuts the intra waits of other pictures short.
 static void check_device_errors(vvcr_ctx *ctx) {
   int32_t e[2] = {0, 0};
@@ -450,6 +450,7 @@ static void check_device_errors(vvcr_ctx *ctx) {
     VVCR_CHECK_HIP(hipMemset(ctx->d_err, 0, sizeof e));
     if (e[0]) throw VvcrError(VVCR_E_STATE, "intra reconstruction: a step's dependency wait timed out (output invalid)");
     if (e[1] & 2) throw VvcrError(VVCR_E_STATE, "deblocking planner: no CU / TU covers a neighbouring position (inconsistent descriptors)");
+    if (e[1] & 8) throw VvcrError(VVCR_E_STATE, "deblocking planner: built for 64-lane waves, the device runs another wave size");
     throw VvcrError(VVCR_E_STATE, "deblocking planner: segment list overflow");
   }
 }
@@ -1172,8 +1173,13 @@ static void launch_rest(vvcr_ctx *ctx, Prepared &r, uint32_t mask, const std::ve
       }
       KernelTimer t(r, K_DBK, s, ctx->timing);
       const DbkSeg *segs[2][2] = {{a.out, a.out + a.cap}, {a.out + 2 * (size_t)a.cap, a.out + 3 * (size_t)a.cap}};
-      // workgroups per list: at most one segment per 4x4 unit (64 per workgroup and pass), capped (they loop)
-      const int gmax = std::min(1024, (a.cap + 63) / 64), g[2][2] = {{gmax, gmax}, {gmax, gmax}};
+      // workgroups per list: at most one segment per item of the direction (both passes), 64 per workgroup
+      // and pass, capped (they loop); a direction without items launches nothing
+      int g[2][2];
+      for (int d = 0; d < 2; d++) {
+        const int n = std::min(a.cap, a.nitems[d] + a.nitems[2 + d]);
+        g[d][0] = g[d][1] = std::min(1024, (n + 63) / 64);
+      }
       launch_dbk(dp, segs, a.counts, g, s);
       r.launches[K_DBK] = 2;
     } else {

@@ -87,7 +87,7 @@ struct DbkPlanArgs {
   DbkSeg *out; int32_t *counts; int32_t cap;   // the four lists at out + k * cap, their lengths
   uint32_t *items;                      // the units on CU edge lines per pass and direction (k_dbkp_maps),
   int32_t nitems[4];                    // at items + (2 * pass + dir) * cap, their lengths (pack_dbk_inputs)
-  int32_t *err;                         // bit 2: a map hole (inconsistent descriptors), bit 4: list overflow
+  int32_t *err;                         // bit 2: a map hole (inconsistent descriptors), bit 4: list overflow, bit 8: wave size
   // Map entries carry the generation of the picture that wrote them (gen << 24 | index; bit 23: an ISP CU's
   // luma area, index = its first TU): an entry of another generation is a hole, so the maps are never
   // cleared per picture. fill: clear them first (a new buffer, or the 8-bit generation wrapped).
