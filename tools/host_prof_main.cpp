@@ -1,7 +1,7 @@
 #include <algorithm>
 // Host-only driver for profiling the decode path's CPU side (gprof): open a bitstream, then per picture
 // the CABAC pass, motion derivation (no DMVR refinement: timing only) and native planning. No GPU call.
-//   tools/host_prof.sh <stream.bin> [repeats]
+//   tools/host_prof.sh <stream.bin> [repeats]   (HOST_PROF_PLAN0=1: picture 0's plan `repeats` times, min / median)
 #include <chrono>
 #include <csignal>
 #include <cstdio>
@@ -48,7 +48,7 @@ int main(int argc, char **argv) {
   std::vector<uint8_t> data;
   for (int c; (c = fgetc(f)) != EOF;) data.push_back((uint8_t)c);
   fclose(f);
-  const int reps = argc > 2 ? atoi(argv[2]) : 1;
+  int reps = argc > 2 ? atoi(argv[2]) : 1;
   double tp = 0, td = 0, tl = 0;
   std::vector<int32_t> zeros(1 << 21, 0);   // DMVR deltas: none (timing only)
   using clk = std::chrono::steady_clock;
@@ -66,6 +66,33 @@ int main(int argc, char **argv) {
     printf("parse0 min %.2f median %.2f ms over %d\n", t[0], t[t.size() / 2], reps);
     return 0;
   }
+  if (getenv("HOST_PROF_PLAN0")) {   // picture 0's plan, `reps` times (a fresh parse each, untimed): min / median ms
+    std::vector<double> t;
+    for (int r = 0; r < reps; r++) {
+      vvcp_stream *s = nullptr;
+      if (vvcp_open(data.data(), data.size(), &s)) { fprintf(stderr, "open: %s\n", vvcp_last_error()); return 1; }
+      const int n = vvcp_num_pictures(s);
+      std::vector<int32_t> slots(n), order(n);
+      vvcp_decode_plan(s, 0, 16, slots.data(), order.data());
+      int32_t inf[16];
+      vvcp_picture_info(s, 0, inf, 16);
+      vvcr_seq_params sp{inf[2], inf[3], 1, inf[5], inf[4], 16, 0};
+      if (vvcp_parse_picture(s, 0) || vvcp_derive_motion(s, 0)) { fprintf(stderr, "parse: %s\n", vvcp_last_error()); return 1; }
+      int32_t rs[2 * VVCR_MAX_REF] = {0};
+      vvcr_picture *pic = nullptr;
+      sampling(true);
+      auto t0 = clk::now();
+      if (int e = vvcp_plan_picture(s, 0, &sp, slots[0], rs, VVCR_STAGE_ALL, &pic)) { fprintf(stderr, "plan %d: %s\n", e, vvcp_last_error()); return 1; }
+      t.push_back(std::chrono::duration<double>(clk::now() - t0).count() * 1e3);
+      sampling(false);
+      vvcr_picture_destroy(pic);
+      vvcp_close(s);
+    }
+    std::sort(t.begin(), t.end());
+    printf("plan0 min %.2f median %.2f ms over %d\n", t[0], t[t.size() / 2], reps);
+    if (!pcs) return 0;
+    reps = 0;   // (the sampler's output below)
+  } else
   for (int r = 0; r < reps; r++) {
     vvcp_stream *s = nullptr;
     if (vvcp_open(data.data(), data.size(), &s)) { fprintf(stderr, "%s\n", vvcp_last_error()); return 1; }
@@ -127,6 +154,6 @@ int main(int argc, char **argv) {
     fclose(m);
     fclose(mo);
   }
-  printf("parse %.1f ms  derive %.1f ms  plan %.1f ms (all pictures, per repeat)\n", tp / reps * 1e3, td / reps * 1e3, tl / reps * 1e3);
+  if (reps) printf("parse %.1f ms  derive %.1f ms  plan %.1f ms (all pictures, per repeat)\n", tp / reps * 1e3, td / reps * 1e3, tl / reps * 1e3);
   return 0;
 }

@@ -115,17 +115,17 @@ struct CtxModel {
 // BinDecoderBase keeps them) in a 64-bit window: value64 = VTM's value << 32 plus the next stream bits,
 // so a refill reads 4 bytes every 32 bits consumed instead of one byte every 8. The comparisons against
 // range << 7 (here << 39) see the same bits: VTM's not-yet-read bits are zeros below its 7 guard bits.
-struct Cabac {
+// CabacEngine is the engine's registers; Cabac adds the context models. CabacLocal is a copy of the
+// registers with a pointer to the models, for a hot loop (residual coding): as locals the registers stay in
+// CPU registers across the loop's level stores, which the compiler must otherwise assume may alias them.
+struct CabacEngine {
   const uint8_t *p = nullptr, *end = nullptr;
   uint32_t range = 510;
   uint64_t value = 0;
   int bitsNeeded = -32;   // the lowest valid bit of value is bit bitsNeeded + 32; refill when it passes 32
-  CtxModel ctx[vvcp_ctx::NUM_CTX];
-
-  void init_contexts(int qp, int initType) {   // CtxStore::init (Contexts.cpp:939)
-    const int cq = qp < 0 ? 0 : (qp > 63 ? 63 : qp);
-    for (int k = 0; k < vvcp_ctx::NUM_CTX; k++) ctx[k].init(cq, vvcp_ctx::kInit[initType][k], vvcp_ctx::kInit[3][k]);
-  }
+#ifdef VVCP_TRACE   // bin trace in the format of the reference's D_CABAC channel (BinDecoder.cpp:315)
+  int traceCount = 0;
+#endif
   uint32_t byte() { return p < end ? *p++ : 0; }
   uint64_t word32() {   // the next 4 stream bytes, big-endian (zeros past the end, as byte())
     if (end - p >= 4) {
@@ -148,11 +148,8 @@ struct Cabac {
     value += word32();
     bitsNeeded = -32;
   }
-#ifdef VVCP_TRACE   // bin trace in the format of the reference's D_CABAC channel (BinDecoder.cpp:315)
-  int traceCount = 0;
-#endif
-  unsigned bin(unsigned id) {   // TBinDecoder::decodeBin, with the LPS / MPS choice as masks
-    CtxModel &m = ctx[id];
+  unsigned decode(CtxModel &m, unsigned id) {   // TBinDecoder::decodeBin, with the LPS / MPS choice as masks
+    (void)id;
     const unsigned st = m.state();
     const unsigned mps = st >> 7;
     const unsigned q = st ^ ((0u - mps) & 0xff);   // the LPS probability state
@@ -243,6 +240,20 @@ struct Cabac {
     }
     return offset + eps(length);
   }
+};
+struct Cabac : CabacEngine {
+  CtxModel ctx[vvcp_ctx::NUM_CTX];
+  void init_contexts(int qp, int initType) {   // CtxStore::init (Contexts.cpp:939)
+    const int cq = qp < 0 ? 0 : (qp > 63 ? 63 : qp);
+    for (int k = 0; k < vvcp_ctx::NUM_CTX; k++) ctx[k].init(cq, vvcp_ctx::kInit[initType][k], vvcp_ctx::kInit[3][k]);
+  }
+  unsigned bin(unsigned id) { return decode(ctx[id], id); }
+};
+struct CabacLocal : CabacEngine {
+  CtxModel *ctx;
+  explicit CabacLocal(Cabac &c) : CabacEngine(c), ctx(c.ctx) {}
+  void store(Cabac &c) const { static_cast<CabacEngine &>(c) = *this; }
+  unsigned bin(unsigned id) { return decode(ctx[id], id); }
 };
 
 // ------------------------------------------------------------------------------------------------

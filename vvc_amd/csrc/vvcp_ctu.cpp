@@ -1588,12 +1588,15 @@ struct Parser {
       tt.b[comp][6] = (int32_t)off;
       pic.box[3 * (size_t)ti + comp] = (uint16_t)(boxR | boxC << 8);
       if (boxR && boxC) {
-        // appended row by row (no value-initialised resize that the copy overwrites)
+        // one resize (its zero fill is a memset), then the box's rows copied in (a per-row vector insert runs
+        // the allocator's element-wise copy loop: 3 % of an intra picture's parse)
         const size_t need = off + (size_t)boxR * boxC;
         if (need > pic.coef.capacity()) pic.coef.reserve(std::max(need, 2 * pic.coef.capacity()));
-        for (int y = 0; y < boxR; y++) {
+        pic.coef.resize(need);
+        int32_t *dst = pic.coef.data() + off;
+        for (int y = 0; y < boxR; y++, dst += boxC) {
           int32_t *src = lvl + y * lvlStride;
-          pic.coef.insert(pic.coef.end(), src, src + boxC);
+          std::memcpy(dst, src, (size_t)boxC * sizeof(int32_t));
           std::memset(src, 0, (size_t)boxC * sizeof(int32_t));
         }
       }
@@ -1651,7 +1654,8 @@ struct Parser {
     int32_t *coeff = pscratch;
     const bool signHiding = ph.signHiding;
     CoefCtx cc(comp, w, h, signHiding, false);
-    cc.scanPosLast = last_sig_coeff(cc, c, comp, w, h);
+    CabacLocal cb(cab);   // the engine's registers as locals through the level loops (vvcp_core.h)
+    cc.scanPosLast = last_sig_coeff(cb, cc, c, comp, w, h);
     if (h >= 4 && w >= 4) {
       const int maxLfnstPos = ((h == 4 && w == 4) || (h == 8 && w == 8)) ? 7 : 15;
       cuCtx.violatesLfnst[comp ? 1 : 0] |= cc.scanPosLast > maxLfnstPos;
@@ -1669,11 +1673,12 @@ struct Parser {
       if (sps.mts && c.sbtinfo && h <= 32 && w <= 32 && comp == 0) {
         if ((h == 32 && cc.subSetPosY >= (16 >> cc.log2CGh)) || (w == 32 && cc.subSetPosX >= (16 >> cc.log2CGw))) continue;
       }
-      residual_coding_subblock(cc, coeff, stateTab, state);
+      residual_coding_subblock(cb, cc, coeff, stateTab, state);
       if (comp == 0 && cc.isSigGroup() && (cc.subSetPosY > 3 || cc.subSetPosX > 3)) cuCtx.violatesMtsCoeffConstraint = true;
     }
+    cb.store(cab);
   }
-  int last_sig_coeff(CoefCtx &cc, const vvcr_cu &c, int comp, int w, int h) {   // :3168
+  int last_sig_coeff(CabacLocal &cab, CoefCtx &cc, const vvcr_cu &c, int comp, int w, int h) {   // :3168
     unsigned px = 0, py = 0;
     unsigned mx = cc.maxLastPosX, my = cc.maxLastPosY;
     if (sps.mts && c.sbtinfo && w <= 32 && h <= 32 && comp == 0) {
@@ -1698,7 +1703,7 @@ struct Parser {
     }
     return cc.scanInv[px + py * w];   // the scan position of (px, py): first match, else the last position
   }
-  void residual_coding_subblock(CoefCtx &cc, int32_t *coeff, int stateTab, int &state) {   // :3235
+  void residual_coding_subblock(CabacLocal &cab, CoefCtx &cc, int32_t *coeff, int stateTab, int &state) {   // :3235 (cab: the local engine)
     const int minSubPos = cc.minSubPos;
     const bool isLast = cc.isLast();
     const int firstSigPos = isLast ? cc.scanPosLast : cc.maxSubPos;

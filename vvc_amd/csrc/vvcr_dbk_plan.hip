@@ -23,7 +23,7 @@
 // Kernels, per picture, on the picture's lane before the deblocking filter:
 //   k_dbkp_maps      CU index maps (luma 4x4 / chroma 2x2 units) and TU index maps, a wave per CU / TU
 //                    record; the CU's waves list the units on their CUs' edge lines (items)
-//   k_dbkp_units<D,P> steps 1-5, a thread per item of pass P and direction D
+//   k_dbkp_units<P>  steps 1-5, a thread per item of pass P (both directions, split by block)
 // Inputs: compact CU / PU / TU records (DbCu / DbPu / DbTu, vvcr_dbk.h, built by pack_dbk_inputs) and the
 // 4x4 motion field (MotionRec) of the picture, uploaded with its work lists.
 //
@@ -524,17 +524,18 @@ __device__ __forceinline__ bool wave64(const DbkPlanArgs &A) {
 
 __global__ __launch_bounds__(256) void k_dbkp_maps(DbkPlanArgs A) {
   if (!wave64(A)) return;
+  if (blockIdx.x == 0 && threadIdx.x < 4) A.counts[threadIdx.x] = 0;   // the lists' lengths (k_dbkp_units appends)
   maps_record(A, blockIdx.x * 4 + (threadIdx.x >> 6), threadIdx.x & 63, 64);
 }
 
 // The items of pass PASS, direction DIR (blockIdx.y), a lane each, grid-stride; local_dual: the luma pass
 // leaves each unit's edge flag and boundary strength in A.state, the chroma pass starts from it
 template <int DIR, int PASS>
-__device__ __forceinline__ void items_dir(const DbkPlanArgs &A, const int (*rp)[VVCR_MAX_REF]) {
+__device__ __forceinline__ void items_dir(const DbkPlanArgs &A, const int (*rp)[VVCR_MAX_REF], int blk, int nblk) {
   const int k = 2 * PASS + DIR;
   const int total = min(DIR == VER ? A.nitems[2 * PASS] : A.nitems[2 * PASS + 1], A.cap);
   const bool local_dual = A.chroma_pass && !A.dual_tree;
-  for (int j0 = blockIdx.x * 256; j0 < total; j0 += gridDim.x * 256) {
+  for (int j0 = blk * 256; j0 < total; j0 += nblk * 256) {
     const int j = j0 + threadIdx.x;
     uint32_t wl = 0, wc = 0;
     int x4 = 0, y4 = 0;
@@ -562,16 +563,16 @@ __device__ __forceinline__ void items_dir(const DbkPlanArgs &A, const int (*rp)[
 #ifdef DBKP_ABL_APPEND   // diagnostics ablation: no list append (results wrong)
     if ((wl | wc) == 0xffffffffu) A.out[j0 + threadIdx.x] = DbkSeg{(uint16_t)x4, (uint16_t)y4, wl};
 #else
-    append_wg(A, DIR, wl, wc, x4, y4, j0 + (int)(gridDim.x * 256) < total);
+    append_wg(A, DIR, wl, wc, x4, y4, j0 + nblk * 256 < total);
 #endif
   }
 }
 
-// the units on the edge lines of the CUs of one pass (pass 0: the luma tree, pass 1: the chroma tree) in
-// direction DIR, a thread each (one kernel per direction: the two directions in one kernel behind a
-// blockIdx.y branch doubled its code, r06)
-template <int DIR, int PASS>
-__global__ __launch_bounds__(256) void k_dbkp_units(DbkPlanArgs A) {
+// the units on the edge lines of the CUs of one pass (pass 0: the luma tree, pass 1: the chroma tree), a
+// thread each: blocks [0, gv) the vertical edges' items, the others the horizontal ones' (both directions in
+// one launch: a launch per direction cost a dispatch gap per picture)
+template <int PASS>
+__global__ __launch_bounds__(256) void k_dbkp_units(DbkPlanArgs A, int gv) {
   if (!wave64(A)) return;
   __shared__ int s_ref_poc[2][VVCR_MAX_REF];
   if (threadIdx.x < 2 * VVCR_MAX_REF) {
@@ -581,7 +582,8 @@ __global__ __launch_bounds__(256) void k_dbkp_units(DbkPlanArgs A) {
     s_ref_poc[threadIdx.x / VVCR_MAX_REF][threadIdx.x % VVCR_MAX_REF] = v;
   }
   __syncthreads();
-  items_dir<DIR, PASS>(A, s_ref_poc);
+  if ((int)blockIdx.x < gv) items_dir<VER, PASS>(A, s_ref_poc, blockIdx.x, gv);
+  else items_dir<HOR, PASS>(A, s_ref_poc, blockIdx.x - gv, gridDim.x - gv);
 }
 
 }  // namespace
@@ -589,25 +591,17 @@ __global__ __launch_bounds__(256) void k_dbkp_units(DbkPlanArgs A) {
 void launch_dbk_plan(const DbkPlanArgs &a, hipStream_t s) {
   const size_t n4 = (size_t)a.W4 * a.H4;
   // the four maps are one run (vvcr_api.cpp dbk_plan_args): cleared only when the generation restarts (a
-  // picture's entries are told from older ones by their tag); the list lengths every picture
+  // picture's entries are told from older ones by their tag); the list lengths every picture, by k_dbkp_maps
   if (a.fill) VVCR_CHECK_HIP(hipMemsetAsync(a.cu_map[0], 0, (size_t)((const char *)(a.tu_map[1] + n4) - (const char *)a.cu_map[0]), s));
-  VVCR_CHECK_HIP(hipMemsetAsync(a.counts, 0, 4 * sizeof(int32_t), s));
   const bool local_dual = a.chroma_pass && !a.dual_tree;
   if (local_dual) VVCR_CHECK_HIP(hipMemsetAsync(a.state[0], 0, 2 * a.state_pitch, s));
   const int nm = a.ncu + a.ntu;
-  hipLaunchKernelGGL(k_dbkp_maps, dim3(std::max(1, (nm + 3) / 4)), dim3(256), 0, s, a);
-  for (int pass = 0; pass < 2; pass++)
-    for (int dir = 0; dir < 2; dir++) {
-      const int n = a.nitems[2 * pass + dir];
-      if (n == 0) continue;
-      const dim3 g((unsigned)std::min(4096, (n + 255) / 256));   // (grid-stride beyond)
-      if (pass == 0) {
-        if (dir == VER) hipLaunchKernelGGL((k_dbkp_units<VER, 0>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_dbkp_units<HOR, 0>), g, dim3(256), 0, s, a);
-      } else {
-        if (dir == VER) hipLaunchKernelGGL((k_dbkp_units<VER, 1>), g, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_dbkp_units<HOR, 1>), g, dim3(256), 0, s, a);
-      }
-    }
+  hipLaunchKernelGGL(k_dbkp_maps, dim3(std::max(1, (nm + 3) / 4)), dim3(256), 0, s, a);   // (also zeroes the list lengths)
+  for (int pass = 0; pass < 2; pass++) {
+    const int gv = std::min(2048, (a.nitems[2 * pass] + 255) / 256), gh = std::min(2048, (a.nitems[2 * pass + 1] + 255) / 256);
+    if (gv + gh == 0) continue;   // (grid-stride beyond 2048 blocks a direction)
+    if (pass == 0) hipLaunchKernelGGL(k_dbkp_units<0>, dim3(gv + gh), dim3(256), 0, s, a, gv);
+    else hipLaunchKernelGGL(k_dbkp_units<1>, dim3(gv + gh), dim3(256), 0, s, a, gv);
+  }
   VVCR_CHECK_HIP(hipGetLastError());
 }

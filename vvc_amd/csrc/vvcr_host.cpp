@@ -706,7 +706,10 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
           const vvcr_pu &p = d.pu[cu.firstpu];
           int mode = src == 0 ? p.fidir_l : p.fidir_c;
           if (src > 0 && p.idir_c >= 67 && p.idir_c <= 69) {
-            if (!haveMap) {
+            // the luma CU map of the producer when it hands one over (an intra luma CU has one PU), else a
+            // PU map built here once per picture
+            const bool cmap = d.cu_map[0].size() == (size_t)W4 * H4;
+            if (!haveMap && !cmap) {
               lmap.assign((size_t)W4 * H4, -1);
               for (size_t i = 0; i < d.pu.size(); i++) {
                 const vvcr_pu &q = d.pu[i];
@@ -718,7 +721,13 @@ void build_tb_jobs(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const P
             }
             const int lx = cu.cx * 2, ly = cu.cy * 2, lww = cu.cw * 2, lhh = cu.ch * 2;
             const int rx = sepTree ? lx + (lww >> 1) : lx, ry = sepTree ? ly + (lhh >> 1) : ly;
-            const int li = lmap[(size_t)(ry >> 2) * W4 + (rx >> 2)];
+            int li;
+            if (cmap) {
+              const int lc = d.cu_map[0][(size_t)(ry >> 2) * W4 + (rx >> 2)];
+              li = lc >= 0 ? d.cu[lc].firstpu : -1;
+            } else {
+              li = lmap[(size_t)(ry >> 2) * W4 + (rx >> 2)];
+            }
             if (li < 0) throw VvcrError(VVCR_E_ARG, "no co-located luma PU for CCLM chroma TU");
             const vvcr_pu &lp = d.pu[li];
             mode = d.cu[lp.cu].mip ? 0 : lp.idir_l;

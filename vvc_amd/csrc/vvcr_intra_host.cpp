@@ -116,8 +116,14 @@ struct Planner {
   int32_t *cu_seq = nullptr;        // per CU: the seq of a plain inter CU, kInf until planned
   bigbuf::vec<uint8_t> written_store[2];
   uint8_t *written[2] = {nullptr, nullptr};   // per CU and channel: its units carry their own order / level / producers
+  // A picture without inter CUs (an intra picture: most of the planner's time) has every unit record
+  // preset to the "not decoded" sentinel (order kUnset > any seq): a unit's record is then read directly,
+  // without the CU map and written flag in front of it (r06: I picture plan -N %)
+  bool dense = false;
+  static constexpr int32_t kUnset = 0x7f7f7f7f;
   static constexpr int32_t kInf = 1 << 30;
   int32_t order_of(int ch, size_t i) const {
+    if (dense) return ur[ch][i].order;   // (kUnset or the unit's seq)
     const int32_t m = umap[ch][i];
     if (m < 0) return kInf;
     return written[ch][m] ? ur[ch][i].order : cu_seq[m];
@@ -183,8 +189,10 @@ struct Planner {
         if (c != lastc) { lastc = c; regok = ctu_reg[c] == cur_reg; }
         if (!regok) continue;
         const size_t i = (size_t)uy * W4 + ux;
-        const int32_t cu = umap[ch][i];
-        if (cu < 0 || !written[ch][cu]) continue;
+        if (!dense) {
+          const int32_t cu = umap[ch][i];
+          if (cu < 0 || !written[ch][cu]) continue;
+        }
         const UnitRec &r = ur[ch][i];
         if (r.order >= seq) continue;
         m = std::max(m, r.level);
@@ -592,7 +600,7 @@ struct Planner {
       outs[g].reset(new IntraPlan());
       subs[g].reset(new Planner(sp, pp, d, *outs[g]));
       Planner &P = *subs[g];
-      P.cscale = cscale; P.fuse = fuse; P.wc = wc; P.ctu_reg = ctu_reg; P.cu_seq = cu_seq;
+      P.cscale = cscale; P.fuse = fuse; P.wc = wc; P.ctu_reg = ctu_reg; P.cu_seq = cu_seq; P.dense = dense;
       for (int k = 0; k < 2; k++) { P.umap[k] = umap[k]; P.ur[k] = ur[k]; P.written[k] = written[k]; }
     }
     std::vector<std::exception_ptr> err(ng);
@@ -638,8 +646,14 @@ struct Planner {
   }
     const size_t nu = (size_t)W4 * H4;
     // per-unit arrays without initialisation: only the units of written CUs are read (touch)
-    // (resize would zero 7 arrays of a unit each per picture, 14 MB at 4K, for the few units a B picture plans)
-    for (int k = 0; k < 2; k++) { ur_store[k].alloc(nu, false); ur[k] = ur_store[k].p; }
+    // (resize would zero 7 arrays of a unit each per picture, 14 MB at 4K, for the few units a B picture plans);
+    // a dense picture presets them (order kUnset: every unit read before it is decoded counts as not decoded)
+    dense = std::none_of(d.cu.begin(), d.cu.end(), [](const vvcr_cu &c) { return c.predmode == MODE_INTER; });
+    for (int k = 0; k < 2; k++) {
+      ur_store[k].alloc(nu, false);
+      ur[k] = ur_store[k].p;
+      if (dense) std::memset((void *)ur[k], 0x7f, nu * sizeof(UnitRec));
+    }
     cu_seq_store.assign(d.cu.size(), kInf);
     cu_seq = cu_seq_store.data();
     for (int k = 0; k < 2; k++) { written_store[k].assign(d.cu.size(), 0); written[k] = written_store[k].data(); }
@@ -962,6 +976,22 @@ void plan_intra(const vvcr_seq_params &sp, const vvcr_pic_params &pp, const Pict
   P->cscale = pp.lmcs_enabled && pp.lmcs_chroma_scale;
   P->fuse = fuse;
   P->run();
+  // VVCR_PLAN_HASH (diagnostics): one FNV-1a hash of the whole plan per picture on stderr, to show that a
+  // planner change leaves its output unchanged
+  static const bool hash = getenv("VVCR_PLAN_HASH") != nullptr;
+  if (hash) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void *p, size_t n) {
+      for (size_t k = 0; k < n; k++) h = (h ^ ((const uint8_t *)p)[k]) * 1099511628211ull;
+    };
+    mix(out.jobs.data(), out.jobs.size() * sizeof(IntraJob));
+    mix(out.dep_start.data(), out.dep_start.size() * sizeof(int32_t));
+    mix(out.deps.data(), out.deps.size() * sizeof(int32_t));
+    mix(out.ctu_list.data(), out.ctu_list.size() * sizeof(int32_t));
+    mix(out.ctu_start.data(), out.ctu_start.size() * sizeof(int32_t));
+    mix(out.inter_tiles.data(), out.inter_tiles.size() * sizeof(ReconTile));
+    fprintf(stderr, "intra plan hash %016llx steps %zu\n", (unsigned long long)h, out.jobs.size());
+  }
 }
 
 // Diagnostics (host only, no device): the intra plan of one picture's descriptors. Per step

@@ -26,6 +26,9 @@
 #ifndef AFF_XCD_RUN
 #define AFF_XCD_RUN 32
 #endif
+#ifndef AFF_ABL
+#define AFF_ABL 0   // diagnostics ablations (results wrong): 1 no PROF, 2 no chroma, 4 no luma H, 8 no luma V, 16 no gather
+#endif
 #include "vvcr_tables.h"
 #include "vvcr_mcdev.h"
 
@@ -235,7 +238,7 @@ __device__ __forceinline__ void mc_affine1(const McParams &P, const AffJob &J, c
   uint2 vl[2][4], vc[4];
 #pragma unroll
   for (int l = 0; l < 2; l++) {
-    if (!PRES(l) || lmode[l] != 0) continue;
+    if (!PRES(l) || lmode[l] != 0 || (AFF_ABL & 16)) continue;
     const DPlane R = lref(l);
     const int n = lrows[l] << 3;
 #pragma unroll
@@ -246,7 +249,7 @@ __device__ __forceinline__ void mc_affine1(const McParams &P, const AffJob &J, c
   }
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    if (!PRES(k & 1) || cmode[k] != 0) continue;
+    if (!PRES(k & 1) || cmode[k] != 0 || (AFF_ABL & 16)) continue;
     const DPlane R = cref(k);
     const int r = lane >> 2, c = lane & 3;
     if ((lane >> 2) < crows[k] && c < cnch[k]) vc[k] = chunk4(R.p, R.stride, R.w, R.h, coy[k] + r, cax[k] + 4 * c);
@@ -295,7 +298,7 @@ __device__ __forceinline__ void mc_affine1(const McParams &P, const AffJob &J, c
 #pragma unroll
     for (int it = 0; it < 2; it++) {
       const int i = lane + 64 * it;
-      if (i < nsb * 5) {
+      if (i < nsb * 5 && !(AFF_ABL & 4)) {
         const int sb = i / 5, rp = i - sb * 5;
         const Place pl = lplace(sb);
         const int b = pl.ex + 1, par = b & 1;
@@ -316,7 +319,7 @@ __device__ __forceinline__ void mc_affine1(const McParams &P, const AffJob &J, c
         for (int q = 0; q < 4; q++) dst[(q * HTC + 2 * rp) >> 1] = pk((int16_t)((a[q] + off1) >> sh1), (int16_t)((c[q] + off1) >> sh1));
       }
     }
-    if (first) {   // chroma H of both lists: items (combo, sub-block, row pair)
+    if (first && !(AFF_ABL & 2)) {   // chroma H of both lists: items (combo, sub-block, row pair)
       const int k = lane >> 4, cb = (lane >> 2) & 3, rp = lane & 3, cl = k & 1;
       if (PRES(cl) && cb < ncb) {
         const Place pl = cplace(k, cb);
@@ -338,7 +341,7 @@ __device__ __forceinline__ void mc_affine1(const McParams &P, const AffJob &J, c
     }
     __syncthreads();
     // V pass: items (sub-block, column), 4 output rows each
-    if (lane < nsb * 4) {
+    if (lane < nsb * 4 && !(AFF_ABL & 8)) {
       const int sb = lane >> 2, c = lane & 3;
       const bool rnd = rndc && !(l ? prof[1] : prof[0]);
       const int sh2 = rnd ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
@@ -363,7 +366,7 @@ __device__ __forceinline__ void mc_affine1(const McParams &P, const AffJob &J, c
         s_lo[l][(y0 + q) * 16 + x] = (int16_t)v;
       }
     }
-    if (first) {   // chroma V: items (combo, sub-block, column); s_co takes the chroma windows' storage
+    if (first && !(AFF_ABL & 2)) {   // chroma V: items (combo, sub-block, column); s_co takes the chroma windows' storage
       const int k = lane >> 4, cb = (lane >> 2) & 3, c = lane & 3, cl = k & 1;
       if (PRES(cl) && cb < ncb) {
         const int sh2 = rndc ? IF_FILTER_PREC + headRoom : IF_FILTER_PREC;
@@ -386,7 +389,7 @@ __device__ __forceinline__ void mc_affine1(const McParams &P, const AffJob &J, c
         }
       }
     }
-    if (A.prof) {
+    if (A.prof && !(AFF_ABL & 1)) {
       __syncthreads();
       // PROF (:1209-1251) on the 14-bit luma prediction: a lane takes a 4-sample row chunk; its row and the
       // rows above / below come from the prediction (or the integer ring at the sub-block's top / bottom),
