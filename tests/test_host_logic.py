@@ -164,3 +164,38 @@ def test_deblocking_plan_independent_of_worker_count(tmp_path):
         assert r.returncode == 0, r.stderr[-2000:]
         out.append(r.stdout.strip())
     assert out[0] == out[1] == out[2]
+
+
+_PLAN_HASHES = r'''
+import os, sys
+sys.path.insert(0, sys.argv[1])
+from vvc_amd import stream as S
+for name in sys.argv[2:]:
+    pics = S.load_sequence(os.path.join(sys.argv[1], "tests", "golden", name))
+    alloc = S.SlotAllocator(pics, 16)
+    for i, p in enumerate(pics):
+        slot = alloc.assign(i, p["hdr"]["poc"])
+        S.plan_picture(p, slot, alloc.slot_of, dpb_slots=16).close()
+'''
+
+
+def test_intra_plan_fast_paths_keep_the_plan(tmp_path):
+    """The intra planner's dense-picture path (unit records preset, no CU-map indirection) must leave the
+    plan unchanged: the whole plan's hash per picture (VVCR_PLAN_HASH) with the dense path off
+    (VVCR_PLAN_DENSE=0) equals the default's, with one planner thread and with four (a tiled picture's
+    regions are planned on threads, which orders its steps region by region: compared at equal counts)."""
+    import subprocess
+    import sys
+    script = tmp_path / "plan.py"
+    script.write_text(_PLAN_HASHES)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = []
+    for dense, threads in (("0", "1"), ("1", "1"), ("0", "4"), ("1", "4")):
+        env = dict(os.environ, VVCR_PLAN_HASH="1", VVCR_PLAN_DENSE=dense, VVCR_PLAN_THREADS=threads)
+        r = subprocess.run([sys.executable, str(script), root, "ai416_q37", "ra416_q32", "ratilenf416_q32"], env=env,
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = [l for l in r.stderr.splitlines() if l.startswith("intra plan hash")]
+        assert lines
+        out.append(lines)
+    assert out[0] == out[1] and out[2] == out[3]

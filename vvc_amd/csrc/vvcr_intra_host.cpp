@@ -648,7 +648,8 @@ struct Planner {
     // per-unit arrays without initialisation: only the units of written CUs are read (touch)
     // (resize would zero 7 arrays of a unit each per picture, 14 MB at 4K, for the few units a B picture plans);
     // a dense picture presets them (order kUnset: every unit read before it is decoded counts as not decoded)
-    dense = std::none_of(d.cu.begin(), d.cu.end(), [](const vvcr_cu &c) { return c.predmode == MODE_INTER; });
+    static const bool allow_dense = [] { const char *e = getenv("VVCR_PLAN_DENSE"); return !e || atoi(e) != 0; }();   // 0: off (tests)
+    dense = allow_dense && std::none_of(d.cu.begin(), d.cu.end(), [](const vvcr_cu &c) { return c.predmode == MODE_INTER; });
     for (int k = 0; k < 2; k++) {
       ur_store[k].alloc(nu, false);
       ur[k] = ur_store[k].p;
