@@ -321,6 +321,10 @@ struct PPS {
   std::vector<int> ctuToTileCol, ctuToTileRow;
   bool rectSlice = true, singleSlicePerSubPic = false;
   int numSlicesInPic = 1;
+  // explicit rectangular slice layout (PPS::m_rectSlices, VLCReader.cpp:510-575): per slice its first tile,
+  // its size in tiles, and for slices inside one tile their count and height in CTUs
+  bool tileIdxDeltaPresent = false;
+  std::vector<int> rsTileIdx, rsWidthInTiles, rsHeightInTiles, rsNumSlicesInTile, rsHeightInCtu;
   std::vector<std::vector<int>> rectSliceCtus;   // CTU addresses of each rectangular slice
   bool lfAcrossTiles = true, lfAcrossSlices = false;   // PPS constructor defaults (no picture partition)
   bool entropySync = false, cabacInitPresent = false;
@@ -378,6 +382,8 @@ struct PicHeader {
   bool valid = false;
   bool nonRef = false, gdr = false, noOutputPrior = false;
   int ppsId = -1;
+  bool subPicIdSignalling = false;   // ph_subpic_id_signalling_present_flag
+  int subPicIdLen = 0;
   bool vbDisabled = false;
   bool picOutput = true;
   bool rplPresent = false;

@@ -325,7 +325,51 @@ void parse_pps(Bits &b, PPS &p) {
     for (int i = 0; i < nr; i++) p.tileRowH.push_back((int)b.ue() + 1);
     p.rectSlice = b.flag();
     if (p.rectSlice) p.singleSlicePerSubPic = b.flag();
-    VVCP_CHECK(p.rectSlice && !p.singleSlicePerSubPic, "explicit rectangular slice layouts are not supported");
+    if (p.rectSlice && !p.singleSlicePerSubPic) {
+      // explicit rectangular slices (VLCReader.cpp:510-575); the tile grid is known from the PPS alone
+      VVCP_CHECK(p.width <= 0 || p.height <= 0, "PPS picture size");
+      p.widthInCtus = (p.width + (1 << p.log2Ctu) - 1) >> p.log2Ctu;
+      p.heightInCtus = (p.height + (1 << p.log2Ctu) - 1) >> p.log2Ctu;
+      init_tiles(p);
+      const int ntc = p.numTileCols(), nt = p.numTiles();
+      p.numSlicesInPic = (int)b.ue() + 1;
+      VVCP_CHECK(p.numSlicesInPic > 600, "too many slices");   // MAX_SLICES
+      p.tileIdxDeltaPresent = b.flag();
+      const int n = p.numSlicesInPic;
+      p.rsTileIdx.assign(n, 0); p.rsWidthInTiles.assign(n, 1); p.rsHeightInTiles.assign(n, 1);
+      p.rsNumSlicesInTile.assign(n, 1); p.rsHeightInCtu.assign(n, 0);
+      int tileIdx = 0;
+      for (int i = 0; i < n - 1; i++) {
+        p.rsTileIdx[i] = tileIdx;
+        p.rsWidthInTiles[i] = (int)b.ue() + 1;
+        // JVET_Q0480: the height is inferred from the previous slice inside a row of tiles
+        if (p.tileIdxDeltaPresent || tileIdx % ntc == 0) p.rsHeightInTiles[i] = (int)b.ue() + 1;
+        else p.rsHeightInTiles[i] = i > 0 ? p.rsHeightInTiles[i - 1] : 1;
+        if (p.rsWidthInTiles[i] == 1 && p.rsHeightInTiles[i] == 1) {   // slices inside one tile
+          const int nst = (int)b.ue() + 1;
+          p.rsNumSlicesInTile[i] = nst;
+          for (int j = 0; j < nst - 1; j++) {
+            p.rsHeightInCtu[i] = (int)b.ue() + 1;
+            i++;
+            VVCP_CHECK(i >= n, "slices in a tile exceed the picture's slices");
+            p.rsWidthInTiles[i] = 1; p.rsHeightInTiles[i] = 1;
+            p.rsNumSlicesInTile[i] = nst;
+            p.rsTileIdx[i] = tileIdx;
+          }
+        }
+        if (i < n - 1) {
+          if (p.tileIdxDeltaPresent) {
+            tileIdx += b.se();
+            VVCP_CHECK(tileIdx < 0 || tileIdx >= nt, "invalid tile_idx_delta");
+          } else {
+            tileIdx += p.rsWidthInTiles[i];
+            if (tileIdx % ntc == 0) tileIdx += (p.rsHeightInTiles[i] - 1) * ntc;
+          }
+        }
+      }
+      VVCP_CHECK(tileIdx >= nt, "rectangular slice outside the tile grid");
+      p.rsTileIdx[n - 1] = tileIdx;
+    }
     p.lfAcrossTiles = b.flag();
     p.lfAcrossSlices = b.flag();
   }
@@ -389,7 +433,41 @@ void finalize_pps(PPS &p, const SPS &s) {
   }
   init_tiles(p);
   p.rectSliceCtus.clear();
-  if (p.rectSlice) {   // one rectangular slice holding every tile (initRectSliceMap, Slice.cpp:2283)
+  if (p.rectSlice && !p.singleSlicePerSubPic && !p.noPicPartition) {
+    // PPS::initRectSliceMap (Slice.cpp:2258-2335): the tiles of each slice in raster order, or the CTU
+    // rows of the slices inside one tile
+    const int ntc = p.numTileCols(), ntr = (int)p.rowBd.size() - 1, n = p.numSlicesInPic;
+    p.rectSliceCtus.assign(n, {});
+    for (int i = 0; i < n; i++) {
+      const int tx = p.rsTileIdx[i] % ntc, ty = p.rsTileIdx[i] / ntc;
+      VVCP_CHECK(ty >= ntr, "rectangular slice outside the tile grid");
+      if (i == n - 1) { p.rsWidthInTiles[i] = ntc - tx; p.rsHeightInTiles[i] = ntr - ty; p.rsNumSlicesInTile[i] = 1; }
+      if (p.rsWidthInTiles[i] > 1 || p.rsHeightInTiles[i] > 1) {
+        VVCP_CHECK(tx + p.rsWidthInTiles[i] > ntc || ty + p.rsHeightInTiles[i] > ntr, "rectangular slice outside the tile grid");
+        for (int j = 0; j < p.rsHeightInTiles[i]; j++)
+          for (int k = 0; k < p.rsWidthInTiles[i]; k++) add_tile_ctus(p, p.rectSliceCtus[i], tx + k, ty + j);
+      } else {
+        int cy = p.rowBd[ty];
+        const int nst = p.rsNumSlicesInTile[i];
+        for (int j = 0; j < nst - 1; j++) {
+          VVCP_CHECK(p.rsHeightInCtu[i] <= 0 || cy + p.rsHeightInCtu[i] >= p.rowBd[ty + 1], "invalid rectangular slice height");
+          for (int y = cy; y < cy + p.rsHeightInCtu[i]; y++)
+            for (int x = p.colBd[tx]; x < p.colBd[tx + 1]; x++) p.rectSliceCtus[i].push_back(y * p.widthInCtus + x);
+          cy += p.rsHeightInCtu[i];
+          i++;
+        }
+        VVCP_CHECK(cy >= p.rowBd[ty + 1], "invalid rectangular slice signalling");
+        for (int y = cy; y < p.rowBd[ty + 1]; y++)
+          for (int x = p.colBd[tx]; x < p.colBd[tx + 1]; x++) p.rectSliceCtus[i].push_back(y * p.widthInCtus + x);
+      }
+    }
+    // every CTU in exactly one slice (PPS::checkSliceMap)
+    std::vector<uint8_t> seen((size_t)p.widthInCtus * p.heightInCtus, 0);
+    for (const auto &c : p.rectSliceCtus)
+      for (int a : c) { VVCP_CHECK(seen[a], "a CTU in two rectangular slices"); seen[a] = 1; }
+    for (uint8_t v : seen) VVCP_CHECK(!v, "a CTU in no rectangular slice");
+  } else if (p.rectSlice) {   // one rectangular slice holding every tile (initRectSliceMap, Slice.cpp:2283)
+    VVCP_CHECK(p.singleSlicePerSubPic && s.numSubPics > 1, "one slice per subpicture with several subpictures is not supported");
     std::vector<int> c;
     for (int ty = 0; ty + 1 < (int)p.rowBd.size(); ty++)
       for (int tx = 0; tx + 1 < (int)p.colBd.size(); tx++) add_tile_ctus(p, c, tx, ty);
@@ -495,9 +573,10 @@ void parse_ph(Bits &b, PicHeader &h, const ParamSets &ps) {
   const SPS *sps = ps.sps(pps->spsId);
   VVCP_CHECK(!sps, "PPS references a missing SPS");
   if (sps->subPicIdPresent && !sps->subPicIdSignalling) {
-    if (b.flag()) {   // ph_subpic_id_signalling_present_flag
-      const int len = (int)b.ue() + 1;
-      for (int i = 0; i < sps->numSubPics; i++) b.u(len);
+    h.subPicIdSignalling = b.flag();   // ph_subpic_id_signalling_present_flag
+    if (h.subPicIdSignalling) {
+      h.subPicIdLen = (int)b.ue() + 1;
+      for (int i = 0; i < sps->numSubPics; i++) b.u(h.subPicIdLen);
     }
   }
   if (!sps->vbDisabledPresent) {
@@ -652,10 +731,11 @@ void parse_sh(Bits &b, SliceHeader &s, PicHeader &ph, const ParamSets &ps, int p
     else msb = prevMsb;
     s.poc = msb + lsb;
   }
-  VVCP_CHECK(sps->subPicPresent && sps->numSubPics > 1, "subpicture slice addressing is not supported");
-  if (sps->subPicPresent) {
-    int bits = sps->subPicIdSignalling ? sps->subPicIdLen : (pps->subPicIdSignalling ? pps->subPicIdLen : ceilLog2(sps->numSubPics));
-    b.u(bits);
+  if (sps->subPicPresent) {   // slice_subpic_id (VLCReader.cpp:2696-2716); VTM 7.3 decodes a subpicture's
+    // slices through the PPS slice map, the subpicture itself changes nothing else in the decoding
+    int bits = sps->subPicIdSignalling ? sps->subPicIdLen
+             : (ph.subPicIdSignalling ? ph.subPicIdLen : (pps->subPicIdSignalling ? pps->subPicIdLen : ceilLog2(sps->numSubPics)));
+    if (bits) b.u(bits);
   }
   s.ctus.clear();
   if (!pps->rectSlice) {   // raster-scan slices: tiles in raster order
