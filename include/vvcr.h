@@ -135,7 +135,7 @@ typedef struct vvcr_pic_params {
    * slice (vvcr_cu.slice) and tile only (CodingStructure::getCURestricted, CodingStructure.cpp:1519). */
   int32_t num_tile_cols, num_tile_rows;
   int32_t tile_col_bd[VVCR_MAX_TILE_LINES + 1], tile_row_bd[VVCR_MAX_TILE_LINES + 1];
-  int32_t entropy_sync;        /* WPP (pps entropy_coding_sync): not supported, rejected */
+  int32_t entropy_sync;        /* WPP (pps entropy_coding_sync): per-row contexts; intra reads no CU beyond the current CTU column */
   /* Spatial shard (multi-GPU): luma rows [shard_y0, shard_y1) of the picture, on tile-row
    * boundaries; shard_y1 = 0 means the whole picture. Reconstruction covers the CUs of the shard only.
    * The loop-filter stages then produce the final samples of the shard's rows and need, in the picture
@@ -144,6 +144,11 @@ typedef struct vvcr_pic_params {
    * there (they are part of the submitted picture). Motion compensation reads reference rows within
    * the picture's reach (vvcr_picture_work_counts counts[8..9]); they must be present in the slots. */
   int32_t shard_y0, shard_y1;
+  /* Virtual boundaries (ph / sps_loop_filter_across_virtual_boundaries_disabled_present_flag, luma samples,
+   * multiples of 8): no deblocking edge on them, no SAO edge-offset sample next to them, ALF filters each
+   * side as if the other were outside the picture (LoopFilter.cpp:410-452, SampleAdaptiveOffset.cpp:96-116,
+   * 731-750, AdaptiveLoopFilter.cpp:79-120, 458-483). vb_disabled = 0: none. */
+  int32_t vb_disabled, num_vb_ver, vb_ver[3], num_vb_hor, vb_hor[3];
 } vvcr_pic_params;
 
 #define VVCR_LF_HALO 24   /* luma rows (chroma: 12) of pre-deblocking samples a shard's loop filters read */

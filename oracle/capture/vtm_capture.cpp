@@ -241,6 +241,14 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
   H.add("lf_across_tiles", pps.getLoopFilterAcrossTilesEnabledFlag() ? 1 : 0);
   H.add("num_tiles", pps.getNumTiles());
   H.add("entropy_sync", pps.getEntropyCodingSyncEnabledFlag() ? 1 : 0);
+  // virtual boundaries (only when loop filtering across them is disabled do they change decoding)
+  H.add("vb_disabled", ph.getLoopFilterAcrossVirtualBoundariesDisabledFlag() ? 1 : 0);
+  H.add("num_vb_ver", ph.getNumVerVirtualBoundaries());
+  H.add("num_vb_hor", ph.getNumHorVirtualBoundaries());
+  for (int i = 0; i < 3; i++) {
+    H.add(std::string("vb_ver") + char('0' + i), i < (int)ph.getNumVerVirtualBoundaries() ? ph.getVirtualBoundariesPosX(i) : 0);
+    H.add(std::string("vb_hor") + char('0' + i), i < (int)ph.getNumHorVirtualBoundaries() ? ph.getVirtualBoundariesPosY(i) : 0);
+  }
   H.add("sao_enabled", sps.getSAOEnabledFlag() ? 1 : 0);
   H.add("sao_luma", sl.getSaoEnabledFlag(CHANNEL_TYPE_LUMA) ? 1 : 0);
   H.add("sao_chroma", sl.getSaoEnabledFlag(CHANNEL_TYPE_CHROMA) ? 1 : 0);
@@ -707,8 +715,13 @@ static void picParams(vvcr_pic_params &pp, int slot) {
   F(lfnst_enabled); F(mts_intra); F(mts_inter); F(sbt); F(wp_p); F(wp_b); F(dbk_disable); F(dbk_beta_offset_div2);
   F(dbk_tc_offset_div2); F(lf_across_slices); F(lf_across_tiles); F(sao_luma); F(sao_chroma); F(alf_vb_luma);
   F(alf_vb_chroma); F(lmcs_chroma_scale); F(lmcs_min_bin); F(lmcs_max_bin); F(log2_max_ts); F(use_mts);
-  F(implicit_mts); F(joint_cbcr_sign); F(entropy_sync);
+  F(implicit_mts); F(joint_cbcr_sign); F(entropy_sync); F(vb_disabled); F(num_vb_ver); F(num_vb_hor);
 #undef F
+  for (int i = 0; i < 3; i++) {
+    pp.vb_ver[i] = (int32_t)hdr((std::string("vb_ver") + char('0' + i)).c_str());
+    pp.vb_hor[i] = (int32_t)hdr((std::string("vb_hor") + char('0' + i)).c_str());
+  }
+  if (!pp.num_vb_ver && !pp.num_vb_hor) pp.vb_disabled = 0;
   pp.lmcs_enabled = hdr("lmcs_enabled") && hdr("lmcs_slice_flag");
   int tb = 0;
   while ((1 << (tb + 1)) <= hdr("max_tb_size")) tb++;

@@ -293,7 +293,8 @@ struct SPS {
   bool ladf = false, plt = false, act = false;
   int log2ParMrgLevel = 2;
   bool scalingList = false;
-  bool vbDisabledPresent = false;
+  bool vbDisabledPresent = false;   // sps_loop_filter_across_virtual_boundaries_disabled_present_flag
+  int numVbVer = 0, numVbHor = 0, vbPosX[3] = {0, 0, 0}, vbPosY[3] = {0, 0, 0};   // luma samples
   int bitsForPoc = 8;
   bool longTermRefs = false, interLayer = false, idrRplPresent = false, rpl1CopyFrom0 = false;
   std::vector<RPL> rpl[2];
@@ -384,7 +385,8 @@ struct PicHeader {
   int ppsId = -1;
   bool subPicIdSignalling = false;   // ph_subpic_id_signalling_present_flag
   int subPicIdLen = 0;
-  bool vbDisabled = false;
+  bool vbDisabled = false;          // the picture's virtual boundaries (the SPS's when it carries them)
+  int numVbVer = 0, numVbHor = 0, vbPosX[3] = {0, 0, 0}, vbPosY[3] = {0, 0, 0};
   bool picOutput = true;
   bool rplPresent = false;
   int rplIdx[2] = {-1, -1};

@@ -105,6 +105,10 @@ void build_pic_params(const PictureUnit &p, vvcr_pic_params &pp) {
   pp.dbk_tc_offset_div2 = sh.tcOffsetDiv2;
   pp.lf_across_slices = pps.lfAcrossSlices;
   pp.lf_across_tiles = pps.lfAcrossTiles;
+  pp.vb_disabled = ph.vbDisabled && (ph.numVbVer + ph.numVbHor) > 0;
+  pp.num_vb_ver = pp.vb_disabled ? ph.numVbVer : 0;
+  pp.num_vb_hor = pp.vb_disabled ? ph.numVbHor : 0;
+  for (int i = 0; i < 3; i++) { pp.vb_ver[i] = ph.vbPosX[i]; pp.vb_hor[i] = ph.vbPosY[i]; }
   pp.chroma_qp_off[1] = pps.cbQpOffset + sh.cbQpDelta;
   pp.chroma_qp_off[2] = pps.crQpOffset + sh.crQpDelta;
   pp.chroma_qp_off[0] = pps.jcQpOffset + sh.jcQpDelta;

@@ -266,7 +266,14 @@ void parse_sps(Bits &b, SPS &s) {
   s.scalingList = b.flag();
   VVCP_CHECK(s.scalingList, "scaling lists are not supported");
   s.vbDisabledPresent = b.flag();
-  VVCP_CHECK(s.vbDisabledPresent, "virtual boundaries are not supported");
+  if (s.vbDisabledPresent) {   // VLCReader.cpp:1636-1654
+    s.numVbVer = (int)b.u(2);
+    VVCP_CHECK(s.numVbVer > 3, "too many virtual boundaries");
+    for (int i = 0; i < s.numVbVer; i++) s.vbPosX[i] = (int)b.u(13) << 3;
+    s.numVbHor = (int)b.u(2);
+    VVCP_CHECK(s.numVbHor > 3, "too many virtual boundaries");
+    for (int i = 0; i < s.numVbHor; i++) s.vbPosY[i] = (int)b.u(13) << 3;
+  }
   // general_hrd_parameters / VUI / extensions follow; nothing after them affects decoding here
 }
 
@@ -579,9 +586,20 @@ void parse_ph(Bits &b, PicHeader &h, const ParamSets &ps) {
       for (int i = 0; i < sps->numSubPics; i++) b.u(h.subPicIdLen);
     }
   }
-  if (!sps->vbDisabledPresent) {
+  if (!sps->vbDisabledPresent) {   // VLCReader.cpp:1982-2013
     h.vbDisabled = b.flag();
-    VVCP_CHECK(h.vbDisabled, "virtual boundaries are not supported");
+    if (h.vbDisabled) {
+      h.numVbVer = (int)b.u(2);
+      VVCP_CHECK(h.numVbVer > 3, "too many virtual boundaries");
+      for (int i = 0; i < h.numVbVer; i++) h.vbPosX[i] = (int)b.u(13) << 3;
+      h.numVbHor = (int)b.u(2);
+      VVCP_CHECK(h.numVbHor > 3, "too many virtual boundaries");
+      for (int i = 0; i < h.numVbHor; i++) h.vbPosY[i] = (int)b.u(13) << 3;
+    }
+  } else {
+    h.vbDisabled = true;
+    h.numVbVer = sps->numVbVer; h.numVbHor = sps->numVbHor;
+    for (int i = 0; i < 3; i++) { h.vbPosX[i] = sps->vbPosX[i]; h.vbPosY[i] = sps->vbPosY[i]; }
   }
   h.picOutput = pps->outputFlagPresent ? b.flag() : true;
   h.rplPresent = b.flag();

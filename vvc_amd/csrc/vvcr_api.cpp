@@ -916,6 +916,9 @@ static DbkPlanArgs dbk_plan_args(vvcr_ctx *ctx, Lane &ln, const Prepared &r) {
   a.fill = ln.dbkp_gen == 0 || ln.dbkp_gen >= 255;
   ln.dbkp_gen = a.fill ? 1 : ln.dbkp_gen + 1;
   a.gen = ln.dbkp_gen;
+  a.num_vb[0] = pp.vb_disabled ? std::min(3, pp.num_vb_ver) : 0;
+  a.num_vb[1] = pp.vb_disabled ? std::min(3, pp.num_vb_hor) : 0;
+  for (int i = 0; i < 3; i++) { a.vb[0][i] = pp.vb_ver[i]; a.vb[1][i] = pp.vb_hor[i]; }
   return a;
 }
 
@@ -1207,6 +1210,9 @@ static void launch_rest(vvcr_ctx *ctx, Prepared &r, uint32_t mask, const std::ve
     sp.sao = r.sao.p; sp.bd = ctx->sp.bit_depth; sp.ctu = ctu; sp.wc = wc;
     sp.y0 = rw.sao0; sp.y1 = rw.sao1;
     sp.nb = r.n_lf_nb ? r.lf_nb.p : nullptr;
+    sp.nvb[0] = pp.vb_disabled ? std::min(3, pp.num_vb_ver) : 0;
+    sp.nvb[1] = pp.vb_disabled ? std::min(3, pp.num_vb_hor) : 0;
+    for (int i = 0; i < 3; i++) { sp.vb[0][i] = pp.vb_ver[i]; sp.vb[1][i] = pp.vb_hor[i]; }
     launch_sao(sp, s);
     VVCR_CHECK_HIP(hipGetLastError());
     inTmp = !inTmp;
@@ -1226,6 +1232,9 @@ static void launch_rest(vvcr_ctx *ctx, Prepared &r, uint32_t mask, const std::ve
     ap.ctb_set = r.alf_set.p;
     ap.y0 = rw.own0; ap.y1 = rw.own1;
     ap.nb = r.n_lf_nb ? r.lf_nb.p : nullptr;
+    ap.nvb[0] = pp.vb_disabled ? std::min(3, pp.num_vb_ver) : 0;
+    ap.nvb[1] = pp.vb_disabled ? std::min(3, pp.num_vb_hor) : 0;
+    for (int i = 0; i < 3; i++) { ap.vb[0][i] = pp.vb_ver[i]; ap.vb[1][i] = pp.vb_hor[i]; }
     launch_alf(ap, s);
     VVCR_CHECK_HIP(hipGetLastError());
     inTmp = !inTmp;

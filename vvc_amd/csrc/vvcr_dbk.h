@@ -92,6 +92,7 @@ struct DbkPlanArgs {
   // luma area, index = its first TU): an entry of another generation is a hole, so the maps are never
   // cleared per picture. fill: clear them first (a new buffer, or the 8-bit generation wrapped).
   int32_t gen, fill;
+  int32_t num_vb[2], vb[2][3];          // virtual boundaries (luma samples) per direction: no segment on them
 };
 constexpr int DBKP_GEN_SHIFT = 24, DBKP_ISP = 1 << 23, DBKP_IDX_MASK = (1 << 23) - 1;
 void launch_dbk_plan(const DbkPlanArgs &a, hipStream_t s);

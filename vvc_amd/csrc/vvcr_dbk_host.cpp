@@ -273,12 +273,25 @@ struct Planner {
     return q - qbd;
   }
 
+  // an edge on a virtual boundary is not filtered (xDeriveEdgefilterParam, LoopFilter.cpp:433-452: every TU,
+  // PU and sub-block edge of a CU the boundary crosses whose line is the boundary)
+  bool on_vb(int dir, int px, int py) const {
+    if (!pp.vb_disabled) return false;
+    if (dir == VER) {
+      for (int i = 0; i < pp.num_vb_ver && i < 3; i++) if (px == pp.vb_ver[i]) return true;
+    } else {
+      for (int i = 0; i < pp.num_vb_hor && i < 3; i++) if (py == pp.vb_hor[i]) return true;
+    }
+    return false;
+  }
+
   void emit_luma(int cui, int dir, int e) {
     const vvcr_cu &cu = d.cu[cui];
     const int n = dir == VER ? cu.h / 4 : cu.w / 4;
     for (int i = 0; i < n; i++) {
       const int px = dir == VER ? cu.x + e * 4 : cu.x + i * 4;
       const int py = dir == VER ? cu.y + i * 4 : cu.y + e * 4;
+      if (on_vb(dir, px, py)) continue;
       const int b = bs[dir][raster(px, py)] & 3;
       if (!b) continue;
       const vvcr_cu &cuP = d.cu[get_cu(dir == VER ? px - 1 : px, dir == VER ? py : py - 1, cu.chtype)];
@@ -309,6 +322,7 @@ struct Planner {
     for (int i = 0; i < n; i++) {
       const int px = dir == VER ? a[0] + e * 4 : a[0] + i * 4;
       const int py = dir == VER ? a[1] + i * 4 : a[1] + e * 4;
+      if (on_vb(dir, px, py)) continue;
       const int v = bs[dir][raster(px, py)];
       const int bS[2] = {(v >> 2) & 3, (v >> 4) & 3};
       if (!bS[0] && !bS[1]) continue;

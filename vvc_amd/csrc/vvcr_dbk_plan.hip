@@ -373,7 +373,11 @@ struct Unit {
         }
       }
     }
-    // step 5: the segment words (xEdgeFilterLuma / xEdgeFilterChroma bookkeeping)
+    // step 5: the segment words (xEdgeFilterLuma / xEdgeFilterChroma bookkeeping); none on a virtual
+    // boundary (xDeriveEdgefilterParam, LoopFilter.cpp:433: the edge's filter flag is cleared)
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+      if (i < A.num_vb[DIR] && (ver ? px : py) == A.vb[DIR][i]) return;
     if (R.yv && (st.bs & 3)) {
       const int qpP = pin ? R.qp : qpPm, fP = pin ? fQ : fPm;
       const int qp = (qpP + R.qp + 1) >> 1;

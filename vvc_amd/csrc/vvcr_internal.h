@@ -267,6 +267,7 @@ struct SaoParams {
   int32_t bd, ctu, wc;
   int32_t y0, y1;              // luma rows processed (chroma: halves); the picture edges stay the edges
   const uint8_t *nb;           // per CTB the availability of its 8 neighbour CTBs (lf_ctb_neighbours), or null
+  int32_t nvb[2], vb[2][3];    // virtual boundaries (luma samples): vertical ones, horizontal ones
 };
 
 struct AlfParams {
@@ -280,6 +281,7 @@ struct AlfParams {
   const int16_t *ctb_set;
   int32_t y0, y1;              // luma rows processed (multiple of 16; chroma: halves)
   const uint8_t *nb;           // per CTB its neighbours' availability (lf_ctb_neighbours: the clip flags), or null
+  int32_t nvb[2], vb[2][3];    // virtual boundaries (luma samples): vertical ones, horizontal ones
 };
 
 struct Planes3 {

@@ -83,16 +83,28 @@ __global__ __launch_bounds__(256) void k_sao(SaoParams P) {
         const int bit = oy == 0 ? (ox < 0 ? 0 : 1) : (ox == 0 ? (oy < 0 ? 2 : 3) : (oy < 0 ? (ox < 0 ? 4 : 5) : (ox < 0 ? 6 : 7)));
         return (ox == 0 && oy == 0) || ((nbm >> bit) & 1);
       };
+      // virtual boundaries (SampleAdaptiveOffset::isProcessDisabled, SampleAdaptiveOffset.cpp:96-116): no
+      // edge offset on the samples either side of one the class compares across (horizontal class: the
+      // vertical boundaries, vertical class: the horizontal ones, diagonal classes: both)
+      bool vbRow = false;
+      const int vsh = comp ? 1 : 0;
+#pragma unroll
+      for (int i = 0; i < 3; i++)
+        if (type != 0 && i < P.nvb[1]) { const int v = P.vb[1][i] >> vsh; vbRow |= y == v || y == v - 1; }
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int x = x0 + k;
+        bool vbCol = false;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+          if (type != 1 && i < P.nvb[0]) { const int v = P.vb[0][i] >> vsh; vbCol |= x == v || x == v - 1; }
         const int a = type == 0 ? C[k] : (type == 1 ? A[1 + k] : (type == 2 ? A[k] : A[2 + k]));
         const int b = type == 0 ? C[2 + k] : (type == 1 ? B[1 + k] : (type == 2 ? B[2 + k] : B[k]));
         const int oxa = x + dax < bx0 ? -1 : (x + dax >= bx0 + cs ? 1 : 0), oxb = x - dax < bx0 ? -1 : (x - dax >= bx0 + cs ? 1 : 0);
         const bool in = rowsIn && x + dax >= 0 && x + dax < W && x - dax >= 0 && x - dax < W && x < W && avail(oxa, oya) && avail(oxb, oyb);
         const int s0 = v[k], ei = 2 + sgn(s0 - a) + sgn(s0 - b);
         const int off = ei == 0 ? e0 : (ei == 1 ? e1 : (ei == 2 ? e2 : (ei == 3 ? e3 : e4)));
-        if (in) v[k] = clip3(0, maxv, s0 + off);
+        if (in && !vbRow && !vbCol) v[k] = clip3(0, maxv, s0 + off);
       }
     }
   }
@@ -200,6 +212,23 @@ __device__ __forceinline__ int ldc_i16(const int16_t *base, int i) {
   return (int)(int16_t)(w >> ((a & 2) * 8));
 }
 
+// The sub-rectangle between virtual boundaries that contains position p (luma samples; chroma: c = 1):
+// [lo, hi]. With loop filtering across virtual boundaries disabled, VTM filters every such sub-rectangle of a
+// CTB from a copy extended by edge replication (AdaptiveLoopFilter::ALFProcess :458-483), i.e. a tap
+// outside it reads the nearest sample inside: a coordinate clamp.
+__device__ __forceinline__ void vb_span(const AlfParams &P, int d, int c, int p, int &lo, int &hi) {
+  lo = -(1 << 20);
+  hi = 1 << 20;
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+    if (i < P.nvb[d]) {
+      const int v = P.vb[d][i] >> c;
+      if (v <= p) lo = max(lo, v);
+      else hi = min(hi, v - 1);
+    }
+}
+
+template <bool VB>
 __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, unsigned long long *stamp) {
   const DPlane &S = P.src[0];
   const DPlane &D = P.dst[0];
@@ -299,8 +328,13 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
   }
   __syncthreads();
   ALF_STAMP(1);
-  // sample (x, y) in picture coordinates -> LDS (valid for x in [X0 - 8, X0 + 72), y in [Y0 - 3, Y0 + 19))
-#define T(x, y) ((int)t[((y) - Y0 + ALF_HALO) * ALF_SW + (x) - X0 + ALF_LX])
+  // sample (x, y) in picture coordinates -> LDS (valid for x in [X0 - 8, X0 + 72), y in [Y0 - 3, Y0 + 19));
+  // with virtual boundaries (VB: the picture has some) clamped to the sub-rectangle [vxl, vxh] x [vyl, vyh]
+  // of the sample being classified / filtered
+  int vxl = 0, vxh = 0, vyl = 0, vyh = 0;
+#define VCX(x) (VB ? min(max((x), vxl), vxh) : (x))
+#define VCY(y) (VB ? min(max((y), vyl), vyh) : (y))
+#define T(x, y) ((int)t[(VCY(y) - Y0 + ALF_HALO) * ALF_SW + VCX(x) - X0 + ALF_LX])
   const int vbH = 1 << P.ctu_log2, vbPos = P.vb_luma;
   // Classification and filtering of a 4x4 block run on the same four lanes: lane (block b, ii) classifies
   // the block's subsampled row pair ii, the four partial sums are reduced across the lane quad (DPP), every
@@ -310,6 +344,10 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
     // --- classification (deriveClassificationBlk): block b, subsampled row pair ii
     const int ii = tid & 3;
     const int bx = X0 + (b & 15) * 4, by = Y0 + (b >> 4) * 4;
+    if (VB) {   // a 4x4 block lies in one sub-rectangle (virtual boundaries are multiples of 8)
+      vb_span(P, 0, 0, bx, vxl, vxh);
+      vb_span(P, 1, 0, by, vyl, vyh);
+    }
     const bool on = bx < W && by < H && ctbOn;
     int sumV = 0, sumH = 0, sumD0 = 0, sumD1 = 0;
     const int yv = by & (vbH - 1);
@@ -379,7 +417,7 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
         }
         const int maxv = (1 << P.bd) - 1;
         const int yb = by & (vbH - 1);
-        if (yb != vbPos - 4 && yb != vbPos) {
+        if (!VB && yb != vbPos - 4 && yb != vbPos) {
           // no row of this 4x4 block (one per wave: wave-uniform) touches the virtual boundary: every tap at a
           // constant LDS offset from the block's column (immediate ds_read offsets, no row arithmetic)
           // based at the window's top-left sample: every tap offset non-negative (ds_read offsets are unsigned)
@@ -456,7 +494,14 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
     const int x = cx0 + (ci & (ALF_CW - 1)), y = cy0 + ci / ALF_CW;
     const DPlane &C1 = P.src[1];
     if (!ALF_ABL_CHROMA && x < C1.w && y < C1.h && y < (P.y1 >> 1)) {
-#define TC(k, xx, yy) ((int)tc[k][((yy) - cy0 + 2) * ALF_CSW + (xx) - cx0 + 8])
+      int cxl = 0, cxh = 0, cyl = 0, cyh = 0;
+      if (VB) {   // the chroma sample's sub-rectangle, and the luma one of the CC-ALF taps
+        vb_span(P, 0, 1, x, cxl, cxh);
+        vb_span(P, 1, 1, y, cyl, cyh);
+        vb_span(P, 0, 0, 2 * x, vxl, vxh);
+        vb_span(P, 1, 0, 2 * y, vyl, vyh);
+      }
+#define TC(k, xx, yy) ((int)tc[k][((VB ? min(max((yy), cyl), cyh) : (yy)) - cy0 + 2) * ALF_CSW + (VB ? min(max((xx), cxl), cxh) : (xx)) - cx0 + 8])
       const int maxv = (1 << P.bd) - 1;
       const int vbHc = 1 << (P.ctu_log2 - 1), vbPosC = P.vb_chroma;
       int r1, r2, r3, r4, r5, r6;
@@ -522,12 +567,15 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
     }
   }
 #undef T
+#undef VCX
+#undef VCY
 }
 
 // One launch, one workgroup per region; regions in XCD-contiguous runs (raster order within a run).
 #ifndef ALF_WAVES_PER_EU
 #define ALF_WAVES_PER_EU 1   // no cap (72 VGPRs, seven workgroups per CU); 8 (64 VGPRs) spills one VGPR, same speed
 #endif
+template <bool VB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALF_WAVES_PER_EU))) void k_alf(AlfParams P, int gx, int gy) {
 #ifdef ALF_NO_SWIZZLE
   const int b = (int)blockIdx.x;
@@ -538,7 +586,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ALF_WAVES_P
 #endif
   unsigned long long stamp[6] = {0, 0, 0, 0, 0, 0};
   ALF_STAMP(0);
-  alf_region(P, b % gx, b / gx, stamp);
+  alf_region<VB>(P, b % gx, b / gx, stamp);
   ALF_STAMP(4);
 #ifdef VVCR_ALF_PROF
   if (threadIdx.x == 0 && blockIdx.x < (1u << 15)) {
@@ -579,5 +627,7 @@ void launch_planes3(const Planes3 &p, hipStream_t s) {
 void launch_alf(const AlfParams &p, hipStream_t s) {
   if (p.y1 <= p.y0) return;
   const int gx = (p.src[0].w + ALF_TW - 1) / ALF_TW, gy = (p.y1 - p.y0 + ALF_TH - 1) / ALF_TH;
-  hipLaunchKernelGGL(k_alf, dim3(gx * gy), dim3(256), 0, s, p, gx, gy);
+  // pictures with virtual boundaries (loop filters not across them) take the clamping instantiation
+  if (p.nvb[0] + p.nvb[1]) hipLaunchKernelGGL(k_alf<true>, dim3(gx * gy), dim3(256), 0, s, p, gx, gy);
+  else hipLaunchKernelGGL(k_alf<false>, dim3(gx * gy), dim3(256), 0, s, p, gx, gy);
 }

@@ -51,6 +51,7 @@ class PicParams(C.Structure):
         ("tile_col_bd", I32 * (MAX_TILE_LINES + 1)), ("tile_row_bd", I32 * (MAX_TILE_LINES + 1)),
         ("entropy_sync", I32),
         ("shard_y0", I32), ("shard_y1", I32),
+        ("vb_disabled", I32), ("num_vb_ver", I32), ("vb_ver", I32 * 3), ("num_vb_hor", I32), ("vb_hor", I32 * 3),
     ]
 
 

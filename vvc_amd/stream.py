@@ -105,6 +105,11 @@ def pic_params(p, slot, slot_of, missing_ref_slot=None):
         np.copyto(np.ctypeslib.as_array(pp.tile_col_bd)[:len(cb)], cb)
         np.copyto(np.ctypeslib.as_array(pp.tile_row_bd)[:len(rb)], rb)
     pp.entropy_sync = h.get("entropy_sync", 0)
+    if h.get("vb_disabled", 0):   # captures without these fields have no virtual boundaries
+        pp.num_vb_ver, pp.num_vb_hor = h["num_vb_ver"], h["num_vb_hor"]
+        pp.vb_disabled = int(pp.num_vb_ver + pp.num_vb_hor > 0)
+        for i in range(3):
+            pp.vb_ver[i], pp.vb_hor[i] = h["vb_ver%d" % i], h["vb_hor%d" % i]
     return pp
 
 
