@@ -11,5 +11,5 @@ VVCR_RECORD_DIR=gpurun_out/$T timeout -k 10 400 python -u -m pytest tests/test_e
 tail -3 gpurun_out/$T/pytest_enc.log
 timeout -k 10 300 python -u bench_rdo.py > gpurun_out/$T/bench_rdo.json 2> gpurun_out/$T/bench_rdo.err || { tail -20 gpurun_out/$T/bench_rdo.err; exit 1; }
 cat gpurun_out/$T/bench_rdo.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$T/rdo_prof -o run -- python3 bench_rdo.py --no-cpu > gpurun_out/$T/rdo_prof.log 2>&1 || { tail -20 gpurun_out/$T/rdo_prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/$T/rdo_prof -o run -- python3 bench_rdo.py --no-cpu > gpurun_out/$T/rdo_prof.log 2>&1 || { tail -20 gpurun_out/$T/rdo_prof.log; exit 1; }
 find gpurun_out/$T/rdo_prof -name "*kernel_stats.csv" | head -1 | xargs -I{} sh -c 'head -8 {}'
