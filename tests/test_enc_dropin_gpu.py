@@ -39,7 +39,8 @@ def test_encoderapp_with_gpu_merge_satd_is_byte_identical(tmp_path):
     routed = int(m.group(1))
     print("EncoderApp %.1f s, with GPU merge SATD %.1f s: %d calls routed, %s fell back, %d bytes" % (
         secs["cpu"], secs["gpu"], routed, m.group(2), len(out["gpu"][0])))
-    # speed record (VVCR_RECORD_DIR): the link-time binding makes one synchronous GPU round trip per SATD,
+    # speed record (VVCR_RECORD_DIR): the link-time binding makes one synchronous GPU round trip per SATD (one
+    # staged upload, the launches, one read-back),
     # because the reference's merge loop consumes each candidate's cost before it forms the next
     # (EncCu.cpp:2421-2451); DESIGN.md §9 and bench_rdo.py give the batched entry's rate
     rec = os.environ.get("VVCR_RECORD_DIR")

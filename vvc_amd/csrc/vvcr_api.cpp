@@ -436,6 +436,11 @@ struct vvcr_ctx {
   Prepared *last = nullptr;          // last launched (stage times, DMVR deltas)
   int n_cu = 256;                    // compute units (persistent intra launch width)
   std::vector<std::unique_ptr<struct RdoPlan>> rdo;   // encoder RDO plans (vvcr_rd_plan / vvcr_fwd_plan)
+  // vvcr_rd_dist's staging: one page-locked host span and its device copy (results, block records, tiles,
+  // samples), grown only, so that a call is one upload, its launches, one read-back and one synchronisation
+  std::mutex rd_mu;
+  char *rd_h = nullptr, *rd_d = nullptr;
+  size_t rd_cap = 0;
   int32_t *d_err = nullptr;          // device error flag of the persistent intra kernel (checked by vvcr_sync)
 };
 
@@ -1446,6 +1451,8 @@ int vvcr_destroy(vvcr_ctx *ctx) {
   for (auto &a : ctx->slot_r)
     for (auto &e : a) if (e) (void)hipEventDestroy(e);
   if (ctx->d_err) (void)hipFree(ctx->d_err);
+  if (ctx->rd_h) (void)hipHostFree(ctx->rd_h);
+  if (ctx->rd_d) (void)hipFree(ctx->rd_d);
   for (int l = 0; l < ctx->nlane; l++) (void)hipStreamDestroy(ctx->lanes[l].s);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   if (ctx->upload_stream) (void)hipStreamDestroy(ctx->upload_stream);
@@ -2281,28 +2288,67 @@ int vvcr_rdo_release(vvcr_ctx *ctx, int32_t plan) {
 
 int vvcr_rd_dist(vvcr_ctx *ctx, const vvcr_rd_block *blocks, int32_t n, const int16_t *org, int64_t norg,
                  const int16_t *cur, int64_t ncur, uint32_t *sad, uint32_t *satd) {
-  if (!ctx || !org || !cur || !sad || !satd || norg <= 0 || ncur <= 0) return VVCR_E_ARG;
-  int32_t plan = -1;
-  int r = vvcr_rd_plan(ctx, blocks, n, &plan);
-  if (r) return r;
+  if (!ctx || !org || !cur || !sad || !satd || norg <= 0 || ncur <= 0 || n < 0 || (n && !blocks)) return VVCR_E_ARG;
   API_BEGIN
-  for (int i = 0; i < n; i++) {   // every block must lie inside its pool
+  // the same tiling as vvcr_rd_plan, written straight into the staging span: [sad | satd] zeroed (the
+  // kernels accumulate into them), block records, tiles by kind, original and prediction samples. The
+  // per-call cost is then one upload, the launches, one read-back and one synchronisation (the plan /
+  // run / release route allocates and frees device memory per call: ~137 us per 8x8 SATD in the
+  // EncoderApp binding, profiles/r06/enc_dropin_speed_r06x.json)
+  int ntl[RD_KINDS] = {};
+  for (int i = 0; i < n; i++) {
     const vvcr_rd_block &b = blocks[i];
+    int tw, th;
+    const int k = rd_kind(b.width, b.height, tw, th);
+    if (k < 0 || b.width <= 0 || b.height <= 0 || b.width > 128 || b.height > 128)
+      throw VvcrError(VVCR_E_ARG, "RDO block size not supported by xGetHADs (even sizes up to 128)");
     const int64_t eo = b.org_off + (int64_t)(b.height - 1) * b.org_stride + b.width, ec = b.cur_off + (int64_t)(b.height - 1) * b.cur_stride + b.width;
     if (b.org_off < 0 || b.cur_off < 0 || eo > norg || ec > ncur) throw VvcrError(VVCR_E_ARG, "RDO block outside its sample pool");
+    ntl[k] += ((b.width + tw - 1) / tw) * ((b.height + th - 1) / th);
   }
-  DevVec<int16_t> o, c;
-  DevVec<uint32_t> ds, dh;
-  o.upload(org, norg);
-  c.upload(cur, ncur);
-  ds.ensure(n + 1);
-  dh.ensure(n + 1);
-  const int rr = vvcr_rd_run(ctx, plan, o.p, c.p, ds.p, dh.p);
-  if (rr) { vvcr_rdo_release(ctx, plan); return rr; }
-  VVCR_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-  VVCR_CHECK_HIP(hipMemcpy(sad, ds.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-  VVCR_CHECK_HIP(hipMemcpy(satd, dh.p, (size_t)n * 4, hipMemcpyDeviceToHost));
-  vvcr_rdo_release(ctx, plan);
+  auto al = [](size_t v) { return (v + 15) & ~(size_t)15; };
+  const size_t o_res = 0, o_blk = al(2 * (size_t)n * 4);
+  size_t o_tl[RD_KINDS], off = o_blk + al((size_t)n * sizeof(RdBlockDev));
+  for (int k = 0; k < RD_KINDS; k++) { o_tl[k] = off; off += al((size_t)ntl[k] * sizeof(RdTile)); }
+  const size_t o_org = off, o_cur = o_org + al((size_t)norg * 2), total = o_cur + al((size_t)ncur * 2);
+  std::lock_guard<std::mutex> lk(ctx->rd_mu);
+  if (total > ctx->rd_cap) {
+    if (ctx->rd_h) VVCR_CHECK_HIP(hipHostFree(ctx->rd_h));
+    if (ctx->rd_d) VVCR_CHECK_HIP(hipFree(ctx->rd_d));
+    ctx->rd_h = ctx->rd_d = nullptr;
+    ctx->rd_cap = 0;
+    const size_t c = std::max<size_t>(total, 1 << 20);
+    VVCR_CHECK_HIP(hipHostMalloc((void **)&ctx->rd_h, c, hipHostMallocDefault));
+    VVCR_CHECK_HIP(hipMalloc((void **)&ctx->rd_d, c));
+    ctx->rd_cap = c;
+  }
+  char *h = ctx->rd_h, *d = ctx->rd_d;
+  std::memset(h + o_res, 0, 2 * (size_t)n * 4);
+  RdBlockDev *bd = (RdBlockDev *)(h + o_blk);
+  RdTile *tl[RD_KINDS];
+  int fill[RD_KINDS] = {};
+  for (int k = 0; k < RD_KINDS; k++) tl[k] = (RdTile *)(h + o_tl[k]);
+  for (int i = 0; i < n; i++) {
+    const vvcr_rd_block &b = blocks[i];
+    int tw, th;
+    const int k = rd_kind(b.width, b.height, tw, th);
+    bd[i] = RdBlockDev{b.org_off, b.cur_off, b.org_stride, b.cur_stride};
+    for (int y = 0; y < b.height; y += th)
+      for (int x = 0; x < b.width; x += tw) tl[k][fill[k]++] = RdTile{i, (int16_t)x, (int16_t)y};
+  }
+  std::memcpy(h + o_org, org, (size_t)norg * 2);
+  std::memcpy(h + o_cur, cur, (size_t)ncur * 2);
+  hipStream_t st = ctx->stream;
+  VVCR_CHECK_HIP(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, st));
+  uint32_t *dsad = (uint32_t *)(d + o_res), *dsatd = dsad + n;
+  for (int k = 0; k < RD_KINDS; k++)
+    launch_rd_tiles(k, (const int16_t *)(d + o_org), (const int16_t *)(d + o_cur), (const RdTile *)(d + o_tl[k]), ntl[k],
+                    (const RdBlockDev *)(d + o_blk), dsad, dsatd, st);
+  VVCR_CHECK_HIP(hipGetLastError());
+  VVCR_CHECK_HIP(hipMemcpyAsync(h + o_res, d + o_res, 2 * (size_t)n * 4, hipMemcpyDeviceToHost, st));
+  VVCR_CHECK_HIP(hipStreamSynchronize(st));
+  std::memcpy(sad, h + o_res, (size_t)n * 4);
+  std::memcpy(satd, h + o_res + (size_t)n * 4, (size_t)n * 4);
   return VVCR_OK;
   API_END
 }
