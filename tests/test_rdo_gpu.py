@@ -74,6 +74,34 @@ def test_rd_dist_random_batch_matches_oracle():
         assert satd[i] == L.or_satd(po, W, pc, W, int(b["width"]), int(b["height"])), i
 
 
+def test_rd_dist_staging_reuse():
+    """consecutive calls on one context: the staging span is reused, grown for a larger pool and reused
+    again; every call's results equal the C oracle's"""
+    rng = np.random.default_rng(11)
+    L = oracle_lib.lib()
+    L.or_sad.restype = C.c_uint32
+    L.or_satd.restype = C.c_uint32
+    ctx = _ctx()
+    try:
+        for W, H, n in ((16, 16, 1), (1280, 720, 200), (32, 8, 3), (1920, 1088, 50), (8, 8, 1)):
+            org = rng.integers(0, 1024, (H, W)).astype(np.int16)
+            cur = np.clip(org + rng.integers(-60, 61, (H, W)), 0, 1023).astype(np.int16)
+            bl = np.zeros(n, N.RD_BLOCK)
+            for i in range(n):
+                w, h = [(8, 8), (16, 4), (4, 16), (2, 2), (32, 8)][i % 5]
+                w, h = min(w, W), min(h, H)
+                x, y = int(rng.integers(0, W - w + 1)), int(rng.integers(0, H - h + 1))
+                bl[i] = (y * W + x, y * W + x, W, W, w, h)
+            sad, satd = ctx.rd_dist(bl, org, cur)
+            for i, b in enumerate(bl):
+                o, c = org.ravel()[b["org_off"]:], cur.ravel()[b["cur_off"]:]
+                po, pc = C.c_void_p(o.ctypes.data), C.c_void_p(c.ctypes.data)
+                assert sad[i] == L.or_sad(po, W, pc, W, int(b["width"]), int(b["height"])), (W, i)
+                assert satd[i] == L.or_satd(po, W, pc, W, int(b["width"]), int(b["height"])), (W, i)
+    finally:
+        ctx.close()
+
+
 def test_fwd_transform_matches_reference():
     blocks = rdo_golden.tr_blocks()
     resi, ro = _pools([b[5] for b in blocks])
