@@ -588,6 +588,8 @@ def main():
     ap.add_argument("--shard-stream", default="ra4320t_q32",
                     help="tile-row stream of the spatially sharded pass (BASELINE config 4: 8K, one shard per rank)")
     ap.add_argument("--shard-steps", type=int, default=3, help="timed steps of the sharded pass (0 = skip it)")
+    ap.add_argument("--shard-timeout", type=int, default=300,
+                    help="N > 1: seconds the sharded pass may take before the line is printed without it (0 = no limit)")
     a = ap.parse_args()
 
     R = V.Ranks()
@@ -788,10 +790,35 @@ def main():
         line.update(cpu_ratios(value, single, cb, ca, a.e2e_threads))
     ctx.close()
     if a.shard_steps > 0:
+        # With N > 1 the shard leg is the only point-to-point traffic of the run (halo rows over RCCL): a
+        # watchdog on every rank bounds it, so that a stuck exchange costs the shard object, never the line
+        # (rank 0 prints it with the error; every rank then ends its own process)
+        dog = None
+        if world > 1 and a.shard_timeout > 0:
+            import threading
+            gate, state = threading.Lock(), {"done": False}
+
+            def expire():
+                gate.acquire()   # held until the process ends: the main thread's line can no longer print
+                if state["done"]:
+                    gate.release()
+                    return
+                if rank == 0:
+                    line["shard"] = {"error": "no result within %d s (watchdog)" % a.shard_timeout}
+                    print(json.dumps(line), flush=True)
+                sys.stderr.flush()
+                os._exit(0 if bitexact else 1)
+            dog = threading.Timer(a.shard_timeout, expire)
+            dog.daemon = True
+            dog.start()
         try:
             line["shard"] = shard_bench(a, R)
         except Exception as e:   # reported, never silently dropped: the line above stays valid
             line["shard"] = {"error": "%s: %s" % (type(e).__name__, str(e)[:300])}
+        if dog is not None:
+            with gate:
+                state["done"] = True
+            dog.cancel()
     if rank == 0:
         print(json.dumps(line))
     R.close()
