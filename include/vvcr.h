@@ -149,6 +149,10 @@ typedef struct vvcr_pic_params {
    * side as if the other were outside the picture (LoopFilter.cpp:410-452, SampleAdaptiveOffset.cpp:96-116,
    * 731-750, AdaptiveLoopFilter.cpp:79-120, 458-483). vb_disabled = 0: none. */
   int32_t vb_disabled, num_vb_ver, vb_ver[3], num_vb_hor, vb_hor[3];
+  /* Luma-adaptive deblocking (sps_ladf_*, LoopFilter::deriveLADFShift LoopFilter.cpp:815-840, applied at
+   * :938-943): a luma edge's QP gains ladf_qp_offset[k] of the last interval k whose lower bound the mean of
+   * its p0 / q0 samples on lines 0 and 3 exceeds (ladf_lower_bound[0] = 0). ladf_num = 0: off. */
+  int32_t ladf_num, ladf_qp_offset[5], ladf_lower_bound[5];
 } vvcr_pic_params;
 
 #define VVCR_LF_HALO 24   /* luma rows (chroma: 12) of pre-deblocking samples a shard's loop filters read */

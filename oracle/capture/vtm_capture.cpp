@@ -249,6 +249,13 @@ static void dumpDescriptors(CapFile &F, DecLib &dec, const CodingStructure &cs) 
     H.add(std::string("vb_ver") + char('0' + i), i < (int)ph.getNumVerVirtualBoundaries() ? ph.getVirtualBoundariesPosX(i) : 0);
     H.add(std::string("vb_hor") + char('0' + i), i < (int)ph.getNumHorVirtualBoundaries() ? ph.getVirtualBoundariesPosY(i) : 0);
   }
+  // luma-adaptive deblocking (SPS)
+  H.add("ladf_num", sps.getLadfEnabled() ? sps.getLadfNumIntervals() : 0);
+  for (int k = 0; k < 5; k++) {
+    const bool on = sps.getLadfEnabled() && k < sps.getLadfNumIntervals();
+    H.add(std::string("ladf_qp_offset") + char('0' + k), on ? sps.getLadfQpOffset(k) : 0);
+    H.add(std::string("ladf_lower_bound") + char('0' + k), on && k > 0 ? sps.getLadfIntervalLowerBound(k) : 0);
+  }
   H.add("sao_enabled", sps.getSAOEnabledFlag() ? 1 : 0);
   H.add("sao_luma", sl.getSaoEnabledFlag(CHANNEL_TYPE_LUMA) ? 1 : 0);
   H.add("sao_chroma", sl.getSaoEnabledFlag(CHANNEL_TYPE_CHROMA) ? 1 : 0);
@@ -722,6 +729,11 @@ static void picParams(vvcr_pic_params &pp, int slot) {
     pp.vb_hor[i] = (int32_t)hdr((std::string("vb_hor") + char('0' + i)).c_str());
   }
   if (!pp.num_vb_ver && !pp.num_vb_hor) pp.vb_disabled = 0;
+  pp.ladf_num = (int32_t)hdr("ladf_num");
+  for (int k = 0; k < 5; k++) {
+    pp.ladf_qp_offset[k] = (int32_t)hdr((std::string("ladf_qp_offset") + char('0' + k)).c_str());
+    pp.ladf_lower_bound[k] = (int32_t)hdr((std::string("ladf_lower_bound") + char('0' + k)).c_str());
+  }
   pp.lmcs_enabled = hdr("lmcs_enabled") && hdr("lmcs_slice_flag");
   int tb = 0;
   while ((1 << (tb + 1)) <= hdr("max_tb_size")) tb++;

@@ -36,7 +36,7 @@ def _lists(L, pic):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["ai416_q37", "aibdpcm416_q32", "ailm416_q37", "ra416_q32", "rageo480_q32", "ralmgeo416_q32",
                                   "rawp416_q32", "ratile416_q32", "radq0416_q32", "ra1080_q32", "ratilenf416_q32",
-                                  "rasub480_q32", "ravb416_q32", "ravb416b_q37"])
+                                  "rasub480_q32", "ravb416_q32", "ravb416b_q37", "raladf416_q32"])
 def test_device_deblocking_plan_equals_host_plan(name, monkeypatch):
     L = N.lib()
     L.vvcr_debug_dbk_segments.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]

@@ -2,7 +2,7 @@
 # Re-creates the committed test bitstreams with the REFERENCE encoder built by oracle/ref.mk
 # (VTM 7.3 EncoderApp, CTC configs from /root/reference/cfg). Test-infrastructure only; runs in the
 # build container (needs /root/reference). Every stream carries MD5 decoded-picture-hash SEI.
-#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 ra2160n_q27 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32 ralmgeo416_q32 rawpp416_q32 rawpp1080_q32 ratilenf416_q32 ratilenf1080_q32 rasub480_q32 ravb416_q32 ravb416b_q37
+#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 ra2160n_q27 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32 ralmgeo416_q32 rawpp416_q32 rawpp1080_q32 ratilenf416_q32 ratilenf1080_q32 rasub480_q32 ravb416_q32 ravb416b_q37 raladf416_q32
 set -e
 R=/root/reference/cfg; E=${E:-$(dirname $0)/../oracle/_ref/EncoderApp}; T=${T:-/tmp/enc}; O=${O:-$(dirname $0)/../tests/golden/streams}
 mkdir -p $T $O
@@ -76,6 +76,8 @@ for n in "$@"; do case $n in
   # two vertical boundaries (x = 128 on a CTU edge, x = 264 inside a CTU) and one horizontal on the CTU-row
   # edge (y = 128, where ALF's own CTU-row virtual boundary rows meet it), QP 37 (9 pictures)
   ravb416b_q37) [ -f $T/syn416.yuv ] || $G 416 240 17 $T/syn416.yuv; enc $n encoder_randomaccess_vtm.cfg 416 240 9 37 $T/syn416.yuv --LoopFilterAcrossVirtualBoundariesDisabledFlag=1 --NumVerVirtualBoundaries=2 --VirtualBoundariesPosX="128 264" --NumHorVirtualBoundaries=1 --VirtualBoundariesPosY=128 ;;
+  # luma-adaptive deblocking (LADF: the encoder's default 3 intervals, QP offsets by the edge's mean luma)
+  raladf416_q32) [ -f $T/syn416.yuv ] || $G 416 240 17 $T/syn416.yuv; enc $n encoder_randomaccess_vtm.cfg 416 240 9 32 $T/syn416.yuv --LADF=1 ;;
   ratilenf416_q32) [ -f $T/syn416.yuv ] || $G 416 240 17 $T/syn416.yuv; enc $n encoder_randomaccess_vtm.cfg 416 240 17 32 $T/syn416.yuv $TILESNF --TileColumnWidthArray=2 --TileRowHeightArray=1 --RasterSliceSizes=2 ;;
   # 3 x 3 tiles of 5 x 3 CTUs, a raster slice per tile row, no loop filtering across tiles or slices
   ratilenf1080_q32) [ -f $T/syn1080.yuv ] || $G 1920 1080 9 $T/syn1080.yuv; enc $n encoder_randomaccess_vtm.cfg 1920 1080 9 32 $T/syn1080.yuv $FAST $TILESNF --TileColumnWidthArray=5 --TileRowHeightArray=3 --RasterSliceSizes=3 ;;

@@ -291,6 +291,7 @@ struct SPS {
   bool affine = false, affineType = false, affineAmvr = false, prof = false, profCtrl = false;
   bool bcw = false, ibc = false, ciip = false, fpelMmvd = false, geo = false, lmcs = false, lfnst = false;
   bool ladf = false, plt = false, act = false;
+  int ladfNum = 0, ladfQpOffset[5] = {0, 0, 0, 0, 0}, ladfLowerBound[5] = {0, 0, 0, 0, 0};   // luma-adaptive deblocking
   int log2ParMrgLevel = 2;
   bool scalingList = false;
   bool vbDisabledPresent = false;   // sps_loop_filter_across_virtual_boundaries_disabled_present_flag

@@ -109,6 +109,8 @@ void build_pic_params(const PictureUnit &p, vvcr_pic_params &pp) {
   pp.num_vb_ver = pp.vb_disabled ? ph.numVbVer : 0;
   pp.num_vb_hor = pp.vb_disabled ? ph.numVbHor : 0;
   for (int i = 0; i < 3; i++) { pp.vb_ver[i] = ph.vbPosX[i]; pp.vb_hor[i] = ph.vbPosY[i]; }
+  pp.ladf_num = sps.ladf ? sps.ladfNum : 0;
+  for (int k = 0; k < 5; k++) { pp.ladf_qp_offset[k] = sps.ladfQpOffset[k]; pp.ladf_lower_bound[k] = sps.ladfLowerBound[k]; }
   pp.chroma_qp_off[1] = pps.cbQpOffset + sh.cbQpDelta;
   pp.chroma_qp_off[2] = pps.crQpOffset + sh.crQpDelta;
   pp.chroma_qp_off[0] = pps.jcQpOffset + sh.jcQpDelta;

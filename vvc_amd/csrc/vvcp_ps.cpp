@@ -261,7 +261,16 @@ void parse_sps(Bits &b, SPS &s) {
   s.lmcs = b.flag();
   s.lfnst = b.flag();
   s.ladf = b.flag();
-  VVCP_CHECK(s.ladf, "LADF is not supported");
+  if (s.ladf) {   // VLCReader.cpp:1609-1621: intervals, the lowest one's QP offset, then offset and bound per interval
+    s.ladfNum = (int)b.u(2) + 2;
+    s.ladfQpOffset[0] = b.se();
+    for (int k = 1; k < s.ladfNum; k++) {
+      s.ladfQpOffset[k] = b.se();
+      const int64_t d = (int64_t)b.ue() + 1;
+      VVCP_CHECK(d > (1 << 16), "LADF interval threshold out of range");
+      s.ladfLowerBound[k] = s.ladfLowerBound[k - 1] + (int)d;
+    }
+  }
   s.log2ParMrgLevel = (int)b.ue() + 2;
   s.scalingList = b.flag();
   VVCP_CHECK(s.scalingList, "scaling lists are not supported");

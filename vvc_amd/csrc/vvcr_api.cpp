@@ -1171,6 +1171,8 @@ static void launch_rest(vvcr_ctx *ctx, Prepared &r, uint32_t mask, const std::ve
     dp.bd = ctx->sp.bit_depth;
     dp.beta_offset_div2 = pp.dbk_beta_offset_div2;
     dp.tc_offset_div2 = pp.dbk_tc_offset_div2;
+    dp.ladf_num = std::min(5, pp.ladf_num);
+    for (int k = 0; k < 5; k++) { dp.ladf_qp_offset[k] = pp.ladf_qp_offset[k]; dp.ladf_lower_bound[k] = pp.ladf_lower_bound[k]; }
     if (r.dbk_gpu) {
       DbkPlanArgs a;
       {

@@ -23,6 +23,7 @@ struct DbkLists {
 struct DbkParams {
   DPlane pl[3];                // picture planes, filtered in place
   int32_t bd, beta_offset_div2, tc_offset_div2;
+  int32_t ladf_num, ladf_qp_offset[5], ladf_lower_bound[5];   // vvcr_pic_params' luma-adaptive QP offsets
 };
 
 // lf_nb: lf_ctb_neighbours (vvcr_host.h) of the picture, or empty: a CU's left / top edge at a CTB edge is

@@ -162,12 +162,26 @@ __device__ __forceinline__ void dbk_luma(const DbkParams &P, const DbkSeg *segs,
   const bool valid = i < n;
   const DbkSeg sg = valid ? segs[i] : DbkSeg{0, 0, 0};
   const uint32_t w = sg.w;
-  const int bs = w & 3, lenP = (w >> 2) & 7, lenQ = (w >> 5) & 7, qp = (w >> 8) & 63;
+  const int bs = w & 3, lenP = (w >> 2) & 7, lenQ = (w >> 5) & 7;
+  int qp = (w >> 8) & 63;
   const bool pl = (w >> 14) & 1, ql = (w >> 15) & 1;
   const DPlane &Y = P.pl[0];
   const int bd = P.bd, maxv = (1 << bd) - 1;
   const int o = DIR == 0 ? 1 : Y.stride;
   const int step = DIR == 0 ? Y.stride : 1;
+  if (P.ladf_num) {
+    // luma-adaptive QP offset (LoopFilter::deriveLADFShift :815-840): the mean of p0 and q0 on lines 0 and 3,
+    // taken before this segment is filtered; the lanes of lines 0 and 3 hold the terms
+    const int16_t *q0 = Y.p + (size_t)(sg.y4 * 4) * Y.stride + sg.x4 * 4 + line * step;
+    const int e = valid ? (int)q0[0] + (int)q0[-o] : 0;
+    const uint32_t level = (uint32_t)(__shfl(e, l0) + __shfl(e, l0 + 3)) >> 2;
+    // the bounds increase strictly, so the reference's loop-until-below is the last interval above
+    int sh = P.ladf_qp_offset[0];
+#pragma unroll
+    for (int k = 1; k < 5; k++)
+      if (k < P.ladf_num && level > (uint32_t)P.ladf_lower_bound[k]) sh = P.ladf_qp_offset[k];
+    qp += sh;
+  }
   const int tc = tc_of(clip3(0, 65, qp + 2 * (bs - 1) + 2 * P.tc_offset_div2), bd);
   const int beta = vvcr_tab::dbk_beta[clip3(0, 63, qp + 2 * P.beta_offset_div2)] * (1 << (bd - 8));
   const int sideThr = (beta + (beta >> 1)) >> 3;

@@ -52,6 +52,7 @@ class PicParams(C.Structure):
         ("entropy_sync", I32),
         ("shard_y0", I32), ("shard_y1", I32),
         ("vb_disabled", I32), ("num_vb_ver", I32), ("vb_ver", I32 * 3), ("num_vb_hor", I32), ("vb_hor", I32 * 3),
+        ("ladf_num", I32), ("ladf_qp_offset", I32 * 5), ("ladf_lower_bound", I32 * 5),
     ]
 
 

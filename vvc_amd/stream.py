@@ -110,6 +110,10 @@ def pic_params(p, slot, slot_of, missing_ref_slot=None):
         pp.vb_disabled = int(pp.num_vb_ver + pp.num_vb_hor > 0)
         for i in range(3):
             pp.vb_ver[i], pp.vb_hor[i] = h["vb_ver%d" % i], h["vb_hor%d" % i]
+    if h.get("ladf_num", 0):   # luma-adaptive deblocking (captures without the field: off)
+        pp.ladf_num = h["ladf_num"]
+        for k in range(5):
+            pp.ladf_qp_offset[k], pp.ladf_lower_bound[k] = h["ladf_qp_offset%d" % k], h["ladf_lower_bound%d" % k]
     return pp
 
 
