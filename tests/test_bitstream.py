@@ -104,7 +104,8 @@ STREAMS = ["ai416_q37", "ailm416_q37", "ra416_q32", "ralm416_q32", "rawp416_q32"
            "ra2160_q27", "ra2160_q32", "ra2160n_q27", "ra2160l_q32", "ra2160l_q27", "ralmgeo416_q32",
            # WPP (entropy coding sync) and tiles / slices without loop filtering across them (round 6)
            "rawpp416_q32", "ratilenf416_q32", "rawpp1080_q32", "ratilenf1080_q32", "rasub480_q32",
-           "ravb416_q32", "ravb416b_q37", "raladf416_q32"]
+           "ravb416_q32", "ravb416b_q37", "raladf416_q32",
+           "rarsc416_q32"]
 
 
 @pytest.mark.gpu

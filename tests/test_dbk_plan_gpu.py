@@ -36,7 +36,7 @@ def _lists(L, pic):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["ai416_q37", "aibdpcm416_q32", "ailm416_q37", "ra416_q32", "rageo480_q32", "ralmgeo416_q32",
                                   "rawp416_q32", "ratile416_q32", "radq0416_q32", "ra1080_q32", "ratilenf416_q32",
-                                  "rasub480_q32", "ravb416_q32", "ravb416b_q37", "raladf416_q32"])
+                                  "rasub480_q32", "ravb416_q32", "ravb416b_q37", "raladf416_q32", "rarsc416_q32"])
 def test_device_deblocking_plan_equals_host_plan(name, monkeypatch):
     L = N.lib()
     L.vvcr_debug_dbk_segments.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
@@ -44,7 +44,7 @@ def test_device_deblocking_plan_equals_host_plan(name, monkeypatch):
     L.vvcr_debug_dbk_gpu_segments.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]
     pics = S.load_sequence(os.path.join(GOLD, name))
     h0 = pics[0]["hdr"]
-    ctx = N.Context(h0["width"], h0["height"], dpb_slots=16)
+    ctx = N.Context(h0["width"], h0["height"], ctu_log2=h0["ctu_log2"], dpb_slots=16)
     alloc = S.SlotAllocator(pics, 16)
     try:
         for i, p in enumerate(pics):

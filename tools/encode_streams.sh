@@ -2,7 +2,7 @@
 # Re-creates the committed test bitstreams with the REFERENCE encoder built by oracle/ref.mk
 # (VTM 7.3 EncoderApp, CTC configs from /root/reference/cfg). Test-infrastructure only; runs in the
 # build container (needs /root/reference). Every stream carries MD5 decoded-picture-hash SEI.
-#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 ra2160n_q27 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32 ralmgeo416_q32 rawpp416_q32 rawpp1080_q32 ratilenf416_q32 ratilenf1080_q32 rasub480_q32 ravb416_q32 ravb416b_q37 raladf416_q32
+#   tools/encode_streams.sh <name> ...     names: ai416_q37 ra416_q32 ai480_q32 ra480_q32 ra1080_q32 ra1080t_q32 ra2160_q27 ra2160_q32 ralm416_q32 ailm416_q37 rawp416_q32 ratile416_q32 ratile1080_q32 ra4320t_q32 ra1080l_q32 ra412c_q32 ra2160l_q27 ra2160l_q32 ra2160n_q27 rageo480_q32 aibdpcm416_q32 radq0416_q32 rawp1080_q32 ralmgeo416_q32 rawpp416_q32 rawpp1080_q32 ratilenf416_q32 ratilenf1080_q32 rasub480_q32 ravb416_q32 ravb416b_q37 raladf416_q32 rarsc416_q32
 set -e
 R=/root/reference/cfg; E=${E:-$(dirname $0)/../oracle/_ref/EncoderApp}; T=${T:-/tmp/enc}; O=${O:-$(dirname $0)/../tests/golden/streams}
 mkdir -p $T $O
@@ -78,6 +78,10 @@ for n in "$@"; do case $n in
   ravb416b_q37) [ -f $T/syn416.yuv ] || $G 416 240 17 $T/syn416.yuv; enc $n encoder_randomaccess_vtm.cfg 416 240 9 37 $T/syn416.yuv --LoopFilterAcrossVirtualBoundariesDisabledFlag=1 --NumVerVirtualBoundaries=2 --VirtualBoundariesPosX="128 264" --NumHorVirtualBoundaries=1 --VirtualBoundariesPosY=128 ;;
   # luma-adaptive deblocking (LADF: the encoder's default 3 intervals, QP offsets by the edge's mean luma)
   raladf416_q32) [ -f $T/syn416.yuv ] || $G 416 240 17 $T/syn416.yuv; enc $n encoder_randomaccess_vtm.cfg 416 240 9 32 $T/syn416.yuv --LADF=1 ;;
+  # raster slices that start and end inside rows of 64x64 CTUs (1-CTU tiles, slices of 1 then 8 tiles), loop
+  # filters across tiles but not across slices: SAO's diagonal neighbours and ALF's raster-slice corner
+  # padding (AdaptiveLoopFilter.cpp:172-198) on the CTBs whose top-left / bottom-right neighbour is another slice
+  rarsc416_q32) [ -f $T/syn416.yuv ] || $G 416 240 17 $T/syn416.yuv; enc $n encoder_randomaccess_vtm.cfg 416 240 9 32 $T/syn416.yuv --CTUSize=64 --EnablePicPartitioning=1 --TileColumnWidthArray=1 --TileRowHeightArray=1 --RasterScanSlices=1 --RasterSliceSizes="1 8" --DisableLoopFilterAcrossTiles=0 --DisableLoopFilterAcrossSlices=1 ;;
   ratilenf416_q32) [ -f $T/syn416.yuv ] || $G 416 240 17 $T/syn416.yuv; enc $n encoder_randomaccess_vtm.cfg 416 240 17 32 $T/syn416.yuv $TILESNF --TileColumnWidthArray=2 --TileRowHeightArray=1 --RasterSliceSizes=2 ;;
   # 3 x 3 tiles of 5 x 3 CTUs, a raster slice per tile row, no loop filtering across tiles or slices
   ratilenf1080_q32) [ -f $T/syn1080.yuv ] || $G 1920 1080 9 $T/syn1080.yuv; enc $n encoder_randomaccess_vtm.cfg 1920 1080 9 32 $T/syn1080.yuv $FAST $TILESNF --TileColumnWidthArray=5 --TileRowHeightArray=3 --RasterSliceSizes=3 ;;

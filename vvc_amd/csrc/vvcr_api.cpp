@@ -1239,6 +1239,7 @@ static void launch_rest(vvcr_ctx *ctx, Prepared &r, uint32_t mask, const std::ve
     ap.ctb_set = r.alf_set.p;
     ap.y0 = rw.own0; ap.y1 = rw.own1;
     ap.nb = r.n_lf_nb ? r.lf_nb.p : nullptr;
+    ap.pad = r.n_lf_nb == 2 * n ? r.lf_nb.p + n : nullptr;   // lf_ctb_neighbours appends the corner flags
     ap.nvb[0] = pp.vb_disabled ? std::min(3, pp.num_vb_ver) : 0;
     ap.nvb[1] = pp.vb_disabled ? std::min(3, pp.num_vb_hor) : 0;
     for (int i = 0; i < 3; i++) { ap.vb[0][i] = pp.vb_ver[i]; ap.vb[1][i] = pp.vb_hor[i]; }
@@ -1818,6 +1819,9 @@ extern "C" int vvcr_debug_dbk_gpu_segments(vvcr_ctx *ctx, const vvcr_picture *pi
   if (!ctx || !pic || (!out && cap)) return VVCR_E_ARG;
   if (!pic->planned || !pic->dbk_gpu) return VVCR_E_STATE;
   API_BEGIN
+  // the device planner takes the context's geometry (CTU size: the CTU-row rule of the P-side length)
+  if (pic->sp.width != ctx->sp.width || pic->sp.height != ctx->sp.height || pic->sp.ctu_log2 != ctx->sp.ctu_log2)
+    throw VvcrError(VVCR_E_ARG, "picture planned for another sequence geometry than the context's");
   std::lock_guard<std::mutex> launch_guard(ctx->launch_mu);
   sync_lanes(ctx);
   Prepared r;

@@ -871,7 +871,9 @@ void lf_ctb_neighbours(const vvcr_seq_params &sp, const vvcr_pic_params &pp, con
     for (int t = 0; t < pp.num_tile_rows; t++) if (cy >= pp.tile_row_bd[t]) tr = t;
     return tr * 1024 + tc;
   };
-  nb.assign((size_t)wc * hc, 0);
+  const size_t n = (size_t)wc * hc;
+  nb.assign(n, 0);
+  std::vector<uint8_t> pad;   // ALF raster-slice corner padding per CTB (bit 0 top-left, bit 1 bottom-right)
   static const int dx[8] = {-1, 1, 0, 0, -1, 1, -1, 1}, dy[8] = {0, 0, -1, 1, -1, -1, 1, 1};
   for (int cy = 0; cy < hc; cy++)
     for (int cx = 0; cx < wc; cx++) {
@@ -887,12 +889,17 @@ void lf_ctb_neighbours(const vvcr_seq_params &sp, const vvcr_pic_params &pp, con
       }
       nb[k] = m;
       // ALF's raster-slice corner padding (AdaptiveLoopFilter.cpp:172-198): the top-left (bottom-right) CTB of
-      // another slice while the top and left (bottom and right) ones are available
-      const bool alf = pp.alf_en[0] || pp.alf_en[1] || pp.alf_en[2];
-      if (alf && slices) {
+      // another slice while the top and left (bottom and right) ones are available: the CTB's copy takes its
+      // corner margin from its first column (last column) of the same row (AreaBuf::padBorderPel, Buffer.h:571)
+      if (slices) {
         const bool tl = cx > 0 && cy > 0 && (m & LFNB_L) && (m & LFNB_A) && slice[k - wc - 1] != slice[k];
         const bool br = cx + 1 < wc && cy + 1 < hc && (m & LFNB_R) && (m & LFNB_B) && slice[k + wc + 1] != slice[k];
-        if (tl || br) throw VvcrError(VVCR_E_UNSUPPORTED, "ALF raster-slice corner padding (slices that are not rows of tiles)");
+        if (tl || br) {
+          if (pad.empty()) pad.assign(n, 0);
+          pad[k] = (uint8_t)((tl ? 1 : 0) | (br ? 2 : 0));
+        }
       }
     }
+  // the pad flags (if any CTB has one) follow the n neighbour masks: entries [n, 2n) (k_alf's AlfParams::pad)
+  if (!pad.empty()) nb.insert(nb.end(), pad.begin(), pad.end());
 }

@@ -281,6 +281,7 @@ struct AlfParams {
   const int16_t *ctb_set;
   int32_t y0, y1;              // luma rows processed (multiple of 16; chroma: halves)
   const uint8_t *nb;           // per CTB its neighbours' availability (lf_ctb_neighbours: the clip flags), or null
+  const uint8_t *pad;          // per CTB the raster-slice corner padding (bit 0 top-left, bit 1 bottom-right), or null
   int32_t nvb[2], vb[2][3];    // virtual boundaries (luma samples): vertical ones, horizontal ones
 };
 

@@ -252,19 +252,27 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
   // (AdaptiveLoopFilter::isCrossedByVirtualBoundaries :121-170: the CTB is filtered from a copy extended by
   // edge replication there, as at the picture's edges)
   int xl = 0, xh = W, yl = 0, yh = H;
+  const int ctu = 1 << P.ctu_log2, bx = X0 & ~(ctu - 1), by = Y0 & ~(ctu - 1);
+  // raster-slice corner padding (AdaptiveLoopFilter.cpp:172-198 with AreaBuf::padBorderPel): the rows above
+  // the CTB take their samples left of it from its first column, the rows below it those right of it from its
+  // last column
+  int pf = 0;
   if (P.nb) {
-    const int ctu = 1 << P.ctu_log2, bx = X0 & ~(ctu - 1), by = Y0 & ~(ctu - 1);
-    const int m = ldc_u8(P.nb, (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2));
+    const int k = (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2);
+    const int m = ldc_u8(P.nb, k);
+    if (P.pad) pf = ldc_u8(P.pad, k);
     if (!(m & 1)) xl = bx;
     if (!(m & 2)) xh = min(W, bx + ctu);
     if (!(m & 4)) yl = by;
     if (!(m & 8)) yh = min(H, by + ctu);
   }
+  auto row_xl = [&](int y, int sh) { return (pf & 1) && y < (by >> sh) ? max(xl >> sh, bx >> sh) : xl >> sh; };
+  auto row_xh = [&](int y, int sh) { return (pf & 2) && y >= ((by + ctu) >> sh) ? min(xh >> sh, (bx + ctu) >> sh) : xh >> sh; };
   uint4 lv[ALF_LQ] = {}, cv = {};
 #pragma unroll
   for (int q = 0; q < ALF_LQ; q++) {
-    const int i = tid + 256 * q, lr = i / ALF_LCH, lc = i - lr * ALF_LCH;
-    if (i < ALF_SH * ALF_LCH) lv[q] = alf_chunk(S, X0 - ALF_LX + 8 * lc, Y0 - ALF_HALO + lr, xl, xh, yl, yh);
+    const int i = tid + 256 * q, lr = i / ALF_LCH, lc = i - lr * ALF_LCH, y = Y0 - ALF_HALO + lr;
+    if (i < ALF_SH * ALF_LCH) lv[q] = alf_chunk(S, X0 - ALF_LX + 8 * lc, y, row_xl(y, 0), row_xh(y, 0), yl, yh);
   }
   const int ccomp = tid / (ALF_CSH * ALF_CCH), ci = tid - ccomp * (ALF_CSH * ALF_CCH);
   const int cr = ci / ALF_CCH, cc = ci - cr * ALF_CCH;
@@ -273,7 +281,8 @@ __device__ __forceinline__ void alf_region(const AlfParams &P, int tx, int ty, u
     // (a lane-indexed P.src[1 + ccomp] is a per-lane load of the descriptor, one more memory round trip)
     DPlane cs = P.src[1];
     cs.p = ccomp ? P.src[2].p : P.src[1].p;
-    if (ccomp < 2) cv = alf_chunk(cs, cx0 - 8 + 8 * cc, cy0 - 2 + cr, xl >> 1, xh >> 1, yl >> 1, yh >> 1);
+    const int y = cy0 - 2 + cr;
+    if (ccomp < 2) cv = alf_chunk(cs, cx0 - 8 + 8 * cc, y, row_xl(y, 1), row_xh(y, 1), yl >> 1, yh >> 1);
   }
   const int ctbT = (Y0 >> P.ctu_log2) * P.wc + (X0 >> P.ctu_log2);
   const int n = P.nctb;
