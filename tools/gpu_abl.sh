@@ -6,7 +6,7 @@ set -o pipefail
 TAG=${1:-dbkp_abl}
 export TMPDIR=/tmp
 mkdir -p gpurun_out/$TAG
-for L in vvc_amd/libvvcr.so tmp_abl/lib_*.so; do
+for L in vvc_amd/libvvcr.so ${ABL_DIR:-tmp_abl}/lib_*.so; do
   N=$(basename $L .so)
   P=gpurun_out/$TAG/$N
   VVCR_LIB=$PWD/$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $P -o run -- python3 -u bench.py --kernel-table-only --kernel-table-reps 3 --kernel-table-sync picture --stream ${STREAM:-ra2160l_q27} --north-star-stream "" > $P.json 2> $P.err || { tail -5 $P.err; exit 1; }
