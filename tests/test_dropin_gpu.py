@@ -25,7 +25,9 @@ GOLD = os.path.join(ROOT, "tests", "golden")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["ra416_q32", "ailm416_q37", "rageo480_q32", "rawp416_q32", "ralmgeo416_q32", "ra1080_q32"])
+@pytest.mark.parametrize("name", ["ra416_q32", "ailm416_q37", "rageo480_q32", "rawp416_q32", "ralmgeo416_q32", "ra1080_q32",
+                                  "rawpp416_q32", "ratilenf416_q32", "rasub480_q32", "ravb416_q32", "raladf416_q32",
+                                  "rarsc416_q32"])
 def test_decoderapp_linked_with_libvvcr(name, tmp_path):
     if not os.access(APP, os.X_OK):
         pytest.fail("oracle/_ref/vtm_vvcr is not built (make -f oracle/ref.mk dropin, in the build container)")
