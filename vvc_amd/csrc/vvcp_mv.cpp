@@ -719,28 +719,36 @@ struct Deriver {
     subPu.assign((size_t)(c.w >> 2) * (c.h >> 2), Mi());
     const int xOff = (pW >> 1) + t.h, yOff = (pH >> 1) + t.v;
     const bool restrictBi = isBipredRestriction(c);
+    // a sub-block's motion depends only on the collocated record it reads (getColocatedMVP with refIdx 0):
+    // neighbouring sub-blocks mostly read records of one collocated PU, so the last derivation is reused
+    // when the record is byte-identical (no scaling / compression redone)
+    const Mi *prevCm = nullptr;
+    Mi m;
     for (int y = c.y; y < c.y + c.h; y += pH)
       for (int x = c.x; x < c.x + c.w; x += pW) {
         int px = x + xOff, py = y + yOff;
         clipColPos(c, px, py);
         px &= ~7; py &= ~7;
         const Mi &cm = col->at8(px, py);
-        Mi m;
-        m.isInter = true;
-        m.slice = (uint16_t)sliceIdx;
-        bool f = false;
-        if (cm.isInter) {
-          for (int l = 0; l < (sh->isInterB() ? 2 : 1); l++) {
-            Mv v;
-            if (colocatedMVP(l, px, py, v, 0, true)) { m.ref[l] = 0; m.mv[l][0] = v.h; m.mv[l][1] = v.v; f = true; }
+        if (!prevCm || std::memcmp(prevCm, &cm, sizeof(Mi)) != 0) {
+          prevCm = &cm;
+          m = Mi();
+          m.isInter = true;
+          m.slice = (uint16_t)sliceIdx;
+          bool f = false;
+          if (cm.isInter) {
+            for (int l = 0; l < (sh->isInterB() ? 2 : 1); l++) {
+              Mv v;
+              if (colocatedMVP(l, px, py, v, 0, true)) { m.ref[l] = 0; m.mv[l][0] = v.h; m.mv[l][1] = v.v; f = true; }
+            }
           }
+          if (!f) {
+            for (int l = 0; l < 2; l++) { m.mv[l][0] = out[l].mv.h; m.mv[l][1] = out[l].mv.v; m.ref[l] = out[l].ref; }
+            if (!sh->isInterB()) { m.mv[1][0] = m.mv[1][1] = 0; m.ref[1] = -1; }
+          }
+          m.interDir = (m.ref[0] != -1 ? 1 : 0) + (m.ref[1] != -1 ? 2 : 0);
+          if (restrictBi && m.interDir == 3) { m.interDir = 1; m.mv[1][0] = m.mv[1][1] = 0; m.ref[1] = -1; }
         }
-        if (!f) {
-          for (int l = 0; l < 2; l++) { m.mv[l][0] = out[l].mv.h; m.mv[l][1] = out[l].mv.v; m.ref[l] = out[l].ref; }
-          if (!sh->isInterB()) { m.mv[1][0] = m.mv[1][1] = 0; m.ref[1] = -1; }
-        }
-        m.interDir = (m.ref[0] != -1 ? 1 : 0) + (m.ref[1] != -1 ? 2 : 0);
-        if (restrictBi && m.interDir == 3) { m.interDir = 1; m.mv[1][0] = m.mv[1][1] = 0; m.ref[1] = -1; }
         for (int yy = (y - c.y) >> 2; yy < (y - c.y + pH) >> 2; yy++)
           for (int xx = (x - c.x) >> 2; xx < (x - c.x + pW) >> 2; xx++) subPu[(size_t)yy * subW + xx] = m;
       }
