@@ -84,6 +84,28 @@ def test_builder_rejects_cu_outside_the_picture():
     pic.close()
 
 
+@pytest.mark.parametrize("field,value", [("num_vb_ver", 4), ("vb_ver", 100), ("vb_hor", 0), ("ladf_num", 1),
+                                         ("ladf_lower_bound", 0)])
+def test_builder_rejects_bad_filter_parameters(field, value):
+    """virtual boundaries (count <= 3, multiples of 8 inside the picture) and LADF intervals (2..5, bounds
+    increasing from 0) are checked when a picture is created; the streams' own parameters pass"""
+    from vvc_amd import native as N
+    for name in ("ravb416_q32", "raladf416_q32"):
+        p, slot, slot_of = _first_pic(name)
+        _picture(p, slot, slot_of).close()
+    p, slot, slot_of = _first_pic("ravb416_q32" if "vb" in field else "raladf416_q32")
+    h = p["hdr"]
+    pp = S.pic_params(p, slot, slot_of)
+    if field in ("vb_ver", "vb_hor"):
+        getattr(pp, field)[0] = value
+    elif field == "ladf_lower_bound":
+        pp.ladf_lower_bound[2] = pp.ladf_lower_bound[1]   # not increasing
+    else:
+        setattr(pp, field, value)
+    with pytest.raises(N.VvcrError):
+        N.Picture(h["width"], h["height"], pp, bit_depth=h["bitdepth_y"], ctu_log2=h["ctu_log2"], dpb_slots=16).close()
+
+
 def test_pic_params_refuses_missing_reference():
     p, slot, slot_of = _first_pic("ra416_q32", 1)
     with pytest.raises(KeyError):

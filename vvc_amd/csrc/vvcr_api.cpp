@@ -1476,6 +1476,22 @@ static void pic_begin(vvcr_picture &b, const vvcr_seq_params &sp, const vvcr_pic
     for (int i = 0; i < pp.num_ref[l]; i++)
       if (pp.ref_slot[l][i] < 0 || pp.ref_slot[l][i] >= sp.dpb_slots) throw VvcrError(VVCR_E_ARG, "ref slot out of range");
   }
+  // virtual boundaries (at most 3 per direction, multiples of 8 inside the picture) and LADF intervals
+  // (2..5, bounds increasing from 0): the filters' interval and boundary searches rely on both
+  if (pp.vb_disabled) {
+    for (int d = 0; d < 2; d++) {
+      const int n = d ? pp.num_vb_hor : pp.num_vb_ver, lim = d ? sp.height : sp.width;
+      const int32_t *v = d ? pp.vb_hor : pp.vb_ver;
+      if (n < 0 || n > 3) throw VvcrError(VVCR_E_ARG, "virtual boundary count");
+      for (int i = 0; i < n; i++)
+        if (v[i] <= 0 || v[i] >= lim || (v[i] & 7)) throw VvcrError(VVCR_E_ARG, "virtual boundary position");
+    }
+  }
+  if (pp.ladf_num) {
+    if (pp.ladf_num < 2 || pp.ladf_num > 5 || pp.ladf_lower_bound[0] != 0) throw VvcrError(VVCR_E_ARG, "LADF intervals");
+    for (int k = 1; k < pp.ladf_num; k++)
+      if (pp.ladf_lower_bound[k] <= pp.ladf_lower_bound[k - 1]) throw VvcrError(VVCR_E_ARG, "LADF bounds not increasing");
+  }
   b.sp = sp;
   b.pp = pp;
   b.desc.clear();
